@@ -1,0 +1,215 @@
+/*
+ * mgpileup.h — C-ABI of the MI355X per-barcode chrM pileup engine (libmgpileup.so).
+ *
+ * This is the drop-in boundary for mgatk2's `src/processing` hot path. The
+ * reference is pure Python; there is no FFI in it, so every entry point below
+ * names the reference interface it replaces (paths relative to the reference
+ * repo root, file:line):
+ *
+ *   mgp_open / mgp_close      replace constructing `PileupGenerator(config)` and
+ *                             `CellProcessor(config, output_dir)`
+ *                             (src/processing/pileup.py:13, processors.py:59) with a
+ *                             device context that owns all HBM state.
+ *   mgp_push_batch            replaces the per-record append into
+ *                             `reads_by_barcode[barcode]` inside
+ *                             `BAMReader.collect_reads_by_barcode`
+ *                             (src/processing/readers.py:85-165): the host hands over
+ *                             the chrM records of a coordinate-sorted BAM as SoA
+ *                             arrays + packed per-read payload records.
+ *   mgp_run                   replaces the filter+dedup block (readers.py:95-150),
+ *                             `process_cells_progressive` -> `process_barcode_worker`
+ *                             -> `generate_pileup` + `filter_strand_bias`
+ *                             (processors.py:20-55,87-144; pileup.py:18-154) and the
+ *                             per-cell statistics / reference-allele tallies of the
+ *                             writers (writers.py:187-229,340-349,437-458).
+ *   mgp_fetch                 copies the results (the arrays the writers consume)
+ *                             back into caller-owned host buffers.
+ *   mgp_last_error            replaces the exception taxonomy at the boundary
+ *                             (src/core/exceptions.py); the Python wrapper maps
+ *                             negative return codes to those exception classes.
+ *   mgp_comm_*                the one cross-GPU exchange: an RCCL all-reduce of the
+ *                             reference-allele tallies (writers.py:221-222,340-349)
+ *                             when cells are sharded over GPUs.
+ *   mgp_synth_generate        device-side synthetic workload generator (bench only;
+ *                             the host mirror is mgatk2_amd/synth.py, bit-identical).
+ *
+ * All pointers are plain host pointers; no C++ or torch types cross the ABI.
+ * A context is not thread-safe: drive it from one host thread. Contexts on
+ * different devices may run concurrently.
+ */
+#ifndef MGPILEUP_H
+#define MGPILEUP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MGP_ABI_VERSION 1
+
+/* ---- return codes (0 = success) ------------------------------------------ */
+#define MGP_OK               0
+#define MGP_E_INVALID      (-1)  /* invalid argument                           -> InvalidInputError */
+#define MGP_E_HIP          (-2)  /* HIP runtime error                          -> ProcessingError   */
+#define MGP_E_OOM          (-3)  /* device allocation failed                   -> ProcessingError   */
+#define MGP_E_UNSORTED     (-4)  /* records not in coordinate order            -> BAMFormatError    */
+#define MGP_E_BADREAD      (-5)  /* kept read without SEQ/QUAL (readers.py:157-158 raises) -> BAMReadError */
+#define MGP_E_SPAN         (-6)  /* a read's reference reach exceeds its declared span   -> InvalidInputError */
+#define MGP_E_STATE        (-7)  /* call out of order (e.g. fetch before run)  -> ProcessingError   */
+#define MGP_E_COMM         (-8)  /* RCCL failure                               -> ProcessingError   */
+
+/* ---- dedup modes (src/cli/utils.py:164-169, readers.py:118-150) ---------- */
+#define MGP_DEDUP_NONE        0  /* "none"                           */
+#define MGP_DEDUP_START       1  /* "alignment_start":  (start, strand)        */
+#define MGP_DEDUP_START_FRAG  2  /* "alignment_and_fragment_length": (start, strand, |tlen|) */
+
+/* ---- per-read flag bits carried in mgp_batch.flag ------------------------ */
+/* The low 12 bits are the raw BAM FLAG word. Bit 12 is set by the host when
+ * the record has no SEQ or no QUAL (pysam would return None and the reference
+ * raises BAMReadError when such a read is kept: readers.py:157-158,167-168). */
+#define MGP_FLAG_PAIRED        0x0001u
+#define MGP_FLAG_UNMAPPED      0x0004u
+#define MGP_FLAG_REVERSE       0x0010u
+#define MGP_FLAG_SECONDARY     0x0100u
+#define MGP_FLAG_SUPPLEMENTARY 0x0800u
+#define MGP_FLAG_NOSEQQUAL     0x1000u
+
+/* Engine configuration: the POD restatement of PipelineConfig
+ * (src/core/config.py:77-114) restricted to what the hot path reads. */
+typedef struct mgp_config {
+    int32_t min_baseq;          /* QualityThresholds.min_baseq          (config.py:11) */
+    int32_t min_mapq;           /* QualityThresholds.min_mapq           (config.py:12) */
+    int32_t min_dist_from_end;  /* QualityThresholds.min_distance_from_end; the reference
+                                   always uses 5 (pipeline.py:239-254 never passes it) */
+    int32_t dedup_mode;         /* MGP_DEDUP_*                                          */
+    double  max_strand_bias;    /* QualityThresholds.max_strand_bias    (config.py:13) */
+    int32_t min_reads;          /* PipelineConfig.min_reads_per_cell    (processors.py:22) */
+    int32_t n_cells;            /* whitelist length = HDF5 column count (writers.py:42) */
+    int32_t mito_len;           /* PipelineConfig.mito_length, 16569    (config.py:95)  */
+    int32_t flags;              /* reserved, must be 0                                  */
+    int64_t reserve_reads;      /* capacity hint for resident reads (grows on demand)   */
+    int64_t reserve_payload;    /* capacity hint for resident payload bytes             */
+} mgp_config;
+
+/* One batch of chrM records in BAM order (host pointers; pinned memory from
+ * mgp_host_alloc gives asynchronous H2D). Records of consecutive batches must
+ * continue the coordinate order.
+ *
+ * Payload record i lives at payload + rec_off[i] (8-byte aligned):
+ *   int32  start      0-based reference_start
+ *   uint32 l_seq      len(query_sequence), soft clips included
+ *   uint16 n_cigar
+ *   uint16 flag       same word as flag[i]
+ *   uint32 reserved   0
+ *   uint32 cigar[n_cigar]           BAM encoding (len << 4 | op)
+ *   uint8  qual[l_seq]              raw Phred bytes (as BAM stores them)
+ *   uint8  seq[(l_seq + 1) / 2]     BAM 4-bit codes, high nibble first
+ */
+typedef struct mgp_batch {
+    int64_t         n_reads;
+    const int32_t  *start;      /* reference_start                                  */
+    const int32_t  *bc;         /* whitelist index of the CB tag, -1 if absent or not whitelisted */
+    const int32_t  *tlen;       /* signed template_length                           */
+    const uint16_t *flag;       /* BAM flag | MGP_FLAG_NOSEQQUAL                    */
+    const uint8_t  *mapq;       /* mapping_quality                                  */
+    const uint32_t *span;       /* max(reference span of the CIGAR, l_seq)          */
+    const uint64_t *rec_off;    /* byte offset of record i inside `payload`         */
+    const uint8_t  *payload;
+    int64_t         payload_bytes;
+} mgp_batch;
+
+/* Run-level statistics (readers.py:193-199). */
+typedef struct mgp_stats {
+    int64_t total_reads;                   /* every record fed (readers.py:93)               */
+    int64_t filtered_reads;                /* reads kept after filters + dedup (readers.py:165) */
+    int64_t n_barcodes;                    /* cells with >= 1 kept read (readers.py:196)      */
+    int64_t duplicate_reads_with_length;   /* (start,strand,|tlen|) duplicates (readers.py:141-142) */
+    int64_t duplicate_reads_position_only; /* (start,strand) duplicates (readers.py:143-144) */
+    int64_t cells_passed;                  /* cells that produce a result (processors.py:22,30-31) */
+    int32_t max_span;                      /* max declared span over valid reads             */
+    int32_t error_bits;                    /* internal: nonzero => a check failed            */
+} mgp_stats;
+
+/* Results; every pointer is caller-owned host memory or NULL (= skip).
+ * Per-position arrays are cell-major: [n_cells][mito_len][k]. Counts are the
+ * strand-filtered per-position values the writers emit (pileup.py:128-154):
+ * a cell that does not pass (processors.py:22,30-31) is all zero. */
+typedef struct mgp_result {
+    uint32_t *counts;      /* [n_cells][mito_len][8]: A_fwd,A_rev,C_fwd,C_rev,G_fwd,G_rev,T_fwd,T_rev */
+    uint32_t *tn5;         /* [n_cells][mito_len][2]: tn5_cuts_fwd, tn5_cuts_rev (0 where depth==0) */
+    uint32_t *depth;       /* [n_cells][mito_len]   filtered depth (pileup.py:150)  */
+    uint32_t *n_reads;     /* [n_cells] kept reads (after dedup, before MAPQ)       */
+    uint8_t  *any_paired;  /* [n_cells] any kept read is_paired (processors.py:34)  */
+    uint8_t  *passed;      /* [n_cells] cell produced a result                      */
+    uint32_t *covered;     /* [n_cells] positions with filtered depth > 0           */
+    uint64_t *depth_sum;   /* [n_cells] sum of filtered depth                       */
+    uint32_t *depth_max;   /* [n_cells] max filtered depth                          */
+    uint32_t *median_lo;   /* [n_cells] lower middle of sorted covered depths       */
+    uint32_t *median_hi;   /* [n_cells] upper middle (equal to lo when covered is odd) */
+    uint32_t *first_read;  /* [n_cells] BAM index of the first kept read (dict order), UINT32_MAX if none */
+    uint64_t *ref_tally;   /* [mito_len][4] sum over passing cells of A,C,G,T totals (all ranks after comm) */
+    mgp_stats *stats;
+} mgp_result;
+
+/* Parameters of the device-side synthetic generator. */
+typedef struct mgp_synth_params {
+    uint64_t seed;
+    int64_t  n_reads;
+    int32_t  read_len;          /* 50 */
+    int32_t  n_cells;           /* must equal the context's n_cells */
+    const uint32_t *cell_cdf;   /* host array [n_cells]: cumulative thresholds in [0, 2^32) */
+    const uint8_t  *ref_codes;  /* host array [mito_len]: reference bases as BAM 4-bit codes */
+} mgp_synth_params;
+
+typedef struct mgp_ctx mgp_ctx;
+
+int         mgp_abi_version(void);
+const char *mgp_last_error(void);
+int         mgp_device_count(int *out);
+
+int  mgp_open(const mgp_config *cfg, int hip_device, mgp_ctx **out);
+void mgp_close(mgp_ctx *ctx);
+
+/* Pinned host memory helpers (hipHostMalloc / hipHostFree). */
+int  mgp_host_alloc(int64_t bytes, void **out);
+int  mgp_host_free(void *p);
+
+/* Append a batch to the device-resident read set (async H2D on the copy stream). */
+int  mgp_push_batch(mgp_ctx *ctx, const mgp_batch *batch);
+/* Drop resident reads (keeps allocations). */
+int  mgp_reset(mgp_ctx *ctx);
+/* Number of resident reads / payload bytes. */
+int  mgp_resident(mgp_ctx *ctx, int64_t *n_reads, int64_t *payload_bytes);
+
+/* Run the whole hot path over the resident reads (async on the compute stream). */
+int  mgp_run(mgp_ctx *ctx);
+/* Wait for the last run; returns the run's check status (MGP_E_UNSORTED, ...). */
+int  mgp_sync(mgp_ctx *ctx);
+/* D2H the results of the last run into caller buffers (implies mgp_sync). */
+int  mgp_fetch(mgp_ctx *ctx, mgp_result *out);
+/* Convenience: mgp_run + mgp_fetch. */
+int  mgp_finish(mgp_ctx *ctx, mgp_result *out);
+
+/* Per-stage device times (ms), averaged over the last `last_runs` runs (<= 64),
+ * measured with HIP events recorded on the compute stream around each stage.
+ * names: comma-separated stage names written into `names`. */
+int  mgp_kernel_times(mgp_ctx *ctx, int last_runs, float *ms, int max_n, int *n_out, char *names, int names_len);
+
+/* RCCL: rank 0 creates the unique id (128 bytes), every rank joins. After init,
+ * mgp_run all-reduces ref_tally over the communicator. */
+int  mgp_comm_unique_id(uint8_t *out128);
+int  mgp_comm_init(mgp_ctx *ctx, const uint8_t *uid128, int nranks, int rank);
+
+/* Fill the resident read set with the synthetic workload (replaces it). */
+int  mgp_synth_generate(mgp_ctx *ctx, const mgp_synth_params *p);
+/* Copy resident inputs back to host (used by tests to check the device
+ * generator against the host mirror). Any pointer may be NULL. */
+int  mgp_download_inputs(mgp_ctx *ctx, int32_t *start, int32_t *bc, int32_t *tlen,
+                         uint16_t *flag, uint8_t *mapq, uint32_t *span,
+                         uint64_t *rec_off, uint8_t *payload);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MGPILEUP_H */

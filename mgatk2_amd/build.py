@@ -1,0 +1,78 @@
+"""Build the native libraries in-tree.
+
+* ``mgatk2_amd/_lib/libmgpileup.so`` — HIP engine + C-ABI, gfx950 only
+  (``hipcc --offload-arch=gfx950``), linked against RCCL.
+* ``oracle/_build/liboracle.so`` — the CPU restatement (test infrastructure).
+* ``oracle/_ref/`` is not built: the reference is pure Python (no native path
+  to compile); its outputs are pinned through tests/golden/ instead.
+"""
+
+from __future__ import annotations
+
+import os
+import shutil
+import subprocess
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent.parent
+PKG = ROOT / "mgatk2_amd"
+CSRC = PKG / "csrc"
+LIB_DIR = PKG / "_lib"
+ENGINE_SO = LIB_DIR / "libmgpileup.so"
+ORACLE_DIR = ROOT / "oracle"
+ORACLE_SO = ORACLE_DIR / "_build" / "liboracle.so"
+
+HIP_SOURCES = ["mgp_engine.hip", "mgp_synth.hip"]
+HIP_FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared", "-Wall", "-Wno-unused-function"]
+
+
+def _hipcc() -> str:
+    for cand in (os.environ.get("HIPCC"), shutil.which("hipcc"), "/opt/rocm/bin/hipcc"):
+        if cand and Path(cand).exists():
+            return cand
+    raise RuntimeError("hipcc not found (need ROCm for gfx950)")
+
+
+def _stale(target: Path, deps: list[Path]) -> bool:
+    if not target.exists():
+        return True
+    t = target.stat().st_mtime
+    return any(d.stat().st_mtime > t for d in deps)
+
+
+def build_engine(force: bool = False, verbose: bool = False) -> Path:
+    deps = [CSRC / s for s in HIP_SOURCES] + [CSRC / "mgp_kernels.h", ROOT / "include" / "mgpileup.h"]
+    if force or _stale(ENGINE_SO, deps):
+        LIB_DIR.mkdir(parents=True, exist_ok=True)
+        tmp = ENGINE_SO.with_suffix(".so.tmp")
+        cmd = [_hipcc(), *HIP_FLAGS, *[str(CSRC / s) for s in HIP_SOURCES], "-o", str(tmp), "-lrccl"]
+        if verbose:
+            print(" ".join(cmd))
+        subprocess.run(cmd, check=True, cwd=str(CSRC))
+        os.replace(tmp, ENGINE_SO)
+    return ENGINE_SO
+
+
+def build_oracle(force: bool = False, verbose: bool = False) -> Path:
+    deps = [ORACLE_DIR / "mgp_oracle.c", ROOT / "include" / "mgpileup.h"]
+    if force or _stale(ORACLE_SO, deps):
+        ORACLE_SO.parent.mkdir(parents=True, exist_ok=True)
+        tmp = ORACLE_SO.with_suffix(".so.tmp")
+        cc = shutil.which("gcc") or "cc"
+        cmd = [cc, "-O2", "-std=c11", "-fPIC", "-shared", "-Wall", str(ORACLE_DIR / "mgp_oracle.c"), "-o", str(tmp)]
+        if verbose:
+            print(" ".join(cmd))
+        subprocess.run(cmd, check=True)
+        os.replace(tmp, ORACLE_SO)
+    return ORACLE_SO
+
+
+def build_all(force: bool = False, verbose: bool = False) -> None:
+    build_engine(force, verbose)
+    build_oracle(force, verbose)
+
+
+if __name__ == "__main__":
+    import sys
+
+    build_all(force="--force" in sys.argv, verbose=True)

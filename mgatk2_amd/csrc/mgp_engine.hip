@@ -1,0 +1,1304 @@
+// mgp_engine.hip — MI355X (gfx950) per-barcode chrM pileup engine + its C-ABI.
+//
+// Hot path (one mgp_run over the HBM-resident read set), restating the
+// reference's per-read Python loops (paths relative to the reference root):
+//
+//   k_bin_bounds    coordinate-order check + start-bin boundaries (the order that
+//                   pysam's fetch() guarantees, readers.py:87-92)
+//   k_bin_hist      flag/barcode filters (readers.py:95-111) + per (start-bin, cell)
+//                   histogram in LDS; each read gets its rank inside its group
+//   k_scan_*        exclusive scan of the histogram in (cell, start-bin) order:
+//                   the cell-major layout that `reads_by_barcode` builds
+//                   (readers.py:69,164) without moving any payload
+//   k_scatter       writes each valid read's grouping record at its cell-major slot
+//   k_dedup         per-cell duplicate marking (readers.py:118-150: first in BAM
+//                   order wins), kept-read count + paired flag (processors.py:22,34),
+//                   MAPQ gate (pileup.py:33), compaction of the reads to pile up and
+//                   the per-window read ranges
+//   k_pileup        CIGAR walk + end-distance / base-quality / base filters +
+//                   Tn5 cuts (pileup.py:32-95) into an LDS count tile per
+//                   (cell, position window); strand-bias filter, depth, Tn5 masking
+//                   (pileup.py:128-154) and per-cell depth statistics
+//                   (processors.py:36-39, writers.py:187-197) at the tile flush;
+//                   per-workgroup reference-allele partial tallies (writers.py:221-222)
+//   k_median        np.median of covered depths per cell (writers.py:190)
+//   k_tally_reduce  sum of the partial tallies (writers.py:340-349 input)
+//   RCCL allreduce  tallies over ranks when cells are sharded over GPUs
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/mgpileup.h"
+#include "mgp_kernels.h"
+
+using namespace mgp;
+
+// ---------------------------------------------------------------------------
+// error plumbing
+// ---------------------------------------------------------------------------
+static thread_local std::string g_err;
+
+static int set_err(int code, const std::string& msg) {
+    g_err = msg;
+    return code;
+}
+
+#define HIP_TRY(expr)                                                                   \
+    do {                                                                                \
+        hipError_t e__ = (expr);                                                        \
+        if (e__ != hipSuccess) {                                                        \
+            return set_err(e__ == hipErrorOutOfMemory ? MGP_E_OOM : MGP_E_HIP,          \
+                           std::string(#expr) + ": " + hipGetErrorString(e__));         \
+        }                                                                               \
+    } while (0)
+
+#define MGP_TRY(expr)             \
+    do {                          \
+        int r__ = (expr);         \
+        if (r__ != MGP_OK) return r__; \
+    } while (0)
+
+// ---------------------------------------------------------------------------
+// device buffers
+// ---------------------------------------------------------------------------
+struct DevBuf {
+    void* p = nullptr;
+    size_t cap = 0;
+    int ensure(size_t bytes, bool preserve = false, size_t used = 0, hipStream_t s = 0) {
+        if (bytes <= cap) return MGP_OK;
+        size_t ncap = std::max(bytes, cap + cap / 2);
+        ncap = (ncap + 255) & ~size_t(255);
+        void* np = nullptr;
+        hipError_t e = hipMalloc(&np, ncap);
+        if (e != hipSuccess) {
+            ncap = (bytes + 255) & ~size_t(255);
+            e = hipMalloc(&np, ncap);
+            if (e != hipSuccess)
+                return set_err(MGP_E_OOM, "hipMalloc(" + std::to_string(ncap) + ") failed: " +
+                                              hipGetErrorString(e));
+        }
+        if (preserve && p && used) {
+            HIP_TRY(hipMemcpyAsync(np, p, used, hipMemcpyDeviceToDevice, s));
+            HIP_TRY(hipStreamSynchronize(s));
+        }
+        if (p) (void)hipFree(p);
+        p = np;
+        cap = ncap;
+        return MGP_OK;
+    }
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+    }
+    template <typename T>
+    T* as() const { return reinterpret_cast<T*>(p); }
+};
+
+enum Stage { ST_BINS, ST_HIST, ST_SCAN, ST_SCATTER, ST_DEDUP, ST_PILEUP, ST_MEDIAN, ST_TALLY, ST_COMM, ST_N };
+static const char* kStageNames = "bins,hist,scan,scatter,dedup,pileup,median,tally,comm";
+
+struct mgp_ctx {
+    mgp_config cfg{};
+    int dev = 0;
+    hipStream_t s_comp = nullptr, s_copy = nullptr;
+    hipEvent_t ev_copy = nullptr;
+    static constexpr int kRing = 64;   // per-run event slots (timing over many runs without syncs)
+    hipEvent_t ev[kRing][ST_N][2];
+    bool stage_ran[kRing][ST_N]{};
+    int64_t runs = 0;                  // completed mgp_run calls
+    Geom g{};
+    int lds_hist_max_cells = 0;
+
+    // resident inputs (BAM order)
+    int64_t n = 0, pay = 0;
+    DevBuf start, bc, tlen, flag, mapq, span, roff, payload;
+
+    // run scratch
+    DevBuf bin_start, rank, H, P, cell_cnt, cell_base;
+    DevBuf g_idx, g_start, g_tlen, g_info, g_off, p_off, edges, tally_part, tally;
+    DevBuf n_reads, any_paired, passed, covered, dsum, dmax, med_lo, med_hi, first_read;
+    DevBuf counts, tn5, depth, stats;
+
+    bool ran = false;
+    int last_status = MGP_OK;
+    DevStats host_stats{};
+
+    ncclComm_t comm = nullptr;
+    int nranks = 1;
+};
+
+// ---------------------------------------------------------------------------
+// kernels
+// ---------------------------------------------------------------------------
+
+// Per read: sortedness check + start-bin boundaries by adjacent difference.
+__global__ void k_bin_bounds(const int32_t* __restrict__ start, int64_t n, Geom g,
+                             uint32_t* __restrict__ bin_start, DevStats* st) {
+    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    int s = start[i];
+    int b = bin_of(s, g);
+    int bp;
+    if (i == 0) {
+        bp = -1;
+    } else {
+        int sp = start[i - 1];
+        if (s < sp) atomicOr(&st->err, ERR_UNSORTED);
+        bp = bin_of(sp, g);
+    }
+    for (int bb = bp + 1; bb <= b; ++bb) bin_start[bb] = (uint32_t)i;
+    if (i == n - 1)
+        for (int bb = b + 1; bb <= g.nbins; ++bb) bin_start[bb] = (uint32_t)n;
+}
+
+__device__ __forceinline__ bool read_valid(int c, uint16_t f, int nc) {
+    return c >= 0 && c < nc && !(f & (MGP_FLAG_UNMAPPED | MGP_FLAG_SECONDARY | MGP_FLAG_SUPPLEMENTARY));
+}
+
+// One workgroup per start bin: histogram over cells (LDS when it fits, else the
+// global row) and each valid read's rank inside its (bin, cell) group.
+template <bool kLds>
+__global__ void __launch_bounds__(kBlock) k_bin_hist(const uint32_t* __restrict__ bin_start,
+                                                     const int32_t* __restrict__ bc,
+                                                     const uint16_t* __restrict__ flag,
+                                                     const uint32_t* __restrict__ span, int64_t n, Geom g,
+                                                     uint32_t* __restrict__ H, uint32_t* __restrict__ rank,
+                                                     DevStats* st) {
+    extern __shared__ uint32_t hist[];
+    const int b = blockIdx.x;
+    const int nc = g.nc;
+    uint32_t* row = H + (size_t)b * nc;
+    if (kLds) {
+        for (int c = threadIdx.x; c < nc; c += blockDim.x) hist[c] = 0;
+        __syncthreads();
+    }
+    int64_t lo = min((int64_t)bin_start[b], n);
+    int64_t hi = min(max((int64_t)bin_start[b + 1], lo), n);
+    uint32_t mspan = 0;
+    unsigned long long nvalid = 0;
+    bool badbc = false;
+    for (int64_t i = lo + threadIdx.x; i < hi; i += blockDim.x) {
+        int c = bc[i];
+        uint16_t f = flag[i];
+        badbc |= (c >= nc);
+        if (read_valid(c, f, nc)) {
+            rank[i] = kLds ? atomicAdd(&hist[c], 1u) : atomicAdd(&row[c], 1u);
+            uint32_t sp = span[i];
+            mspan = sp > mspan ? sp : mspan;
+            ++nvalid;
+        }
+    }
+    if (kLds) {
+        __syncthreads();
+        for (int c = threadIdx.x; c < nc; c += blockDim.x) row[c] = hist[c];
+    }
+    mspan = wave_max(mspan);
+    nvalid = wave_sum(nvalid);
+    if ((threadIdx.x & (kWave - 1)) == 0) {
+        if (mspan) atomicMax(&st->max_span, mspan);
+        if (nvalid) atomicAdd(&st->valid, nvalid);
+    }
+    if (badbc) atomicOr(&st->err, ERR_BADBC);
+}
+
+// Scan step a: column sums over blocks of RB rows. grid (ceil(nc/256), nrb)
+__global__ void k_scan_colsum(const uint32_t* __restrict__ H, int nrows, int nc, int RB,
+                              uint32_t* __restrict__ P) {
+    int c = blockIdx.x * blockDim.x + threadIdx.x;
+    int rb = blockIdx.y;
+    if (c >= nc) return;
+    int r0 = rb * RB, r1 = min(nrows, r0 + RB);
+    uint32_t acc = 0;
+    for (int r = r0; r < r1; ++r) acc += H[(size_t)r * nc + c];
+    P[(size_t)rb * nc + c] = acc;
+}
+
+// Scan step b: exclusive scan over row blocks per cell; per-cell totals.
+__global__ void k_scan_rows(uint32_t* __restrict__ P, int nrb, int nc, uint32_t* __restrict__ cnt) {
+    int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= nc) return;
+    uint32_t acc = 0;
+    for (int rb = 0; rb < nrb; ++rb) {
+        uint32_t v = P[(size_t)rb * nc + c];
+        P[(size_t)rb * nc + c] = acc;
+        acc += v;
+    }
+    cnt[c] = acc;
+}
+
+// Scan step c: exclusive scan over cells (single workgroup of 1024).
+__global__ void __launch_bounds__(1024) k_scan_cells(const uint32_t* __restrict__ cnt, int nc,
+                                                     uint32_t* __restrict__ base) {
+    __shared__ uint32_t wsum[16];
+    __shared__ uint32_t carry;
+    if (threadIdx.x == 0) carry = 0;
+    __syncthreads();
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    for (int c0 = 0; c0 < nc; c0 += 1024) {
+        int c = c0 + threadIdx.x;
+        uint32_t v = c < nc ? cnt[c] : 0;
+        uint32_t x = v;  // inclusive wave scan
+        for (int o = 1; o < 64; o <<= 1) {
+            uint32_t y = __shfl_up(x, o, 64);
+            if (lane >= o) x += y;
+        }
+        if (lane == 63) wsum[wid] = x;
+        __syncthreads();
+        if (threadIdx.x < 16) {
+            uint32_t w = wsum[threadIdx.x];
+            uint32_t xs = w;
+            for (int o = 1; o < 16; o <<= 1) {
+                uint32_t y = __shfl_up(xs, o, 64);
+                if ((int)threadIdx.x >= o) xs += y;
+            }
+            wsum[threadIdx.x] = xs - w;  // exclusive
+        }
+        __syncthreads();
+        uint32_t excl = carry + wsum[wid] + x - v;
+        if (c < nc) base[c] = excl;
+        __syncthreads();
+        if (threadIdx.x == 1023) carry = excl + v;
+        __syncthreads();
+    }
+}
+
+// Scan step d: H[r][c] <- exclusive (cell-major) offset; row nrows <- cell end.
+__global__ void k_scan_apply(uint32_t* __restrict__ H, const uint32_t* __restrict__ P,
+                             const uint32_t* __restrict__ base, const uint32_t* __restrict__ cnt, int nrows,
+                             int nc, int RB, int nrb) {
+    int c = blockIdx.x * blockDim.x + threadIdx.x;
+    int rb = blockIdx.y;
+    if (c >= nc) return;
+    uint32_t acc = base[c] + P[(size_t)rb * nc + c];
+    int r0 = rb * RB, r1 = min(nrows, r0 + RB);
+    for (int r = r0; r < r1; ++r) {
+        size_t k = (size_t)r * nc + c;
+        uint32_t h = H[k];
+        H[k] = acc;
+        acc += h;
+    }
+    if (rb == nrb - 1) H[(size_t)nrows * nc + c] = base[c] + cnt[c];
+}
+
+// g_info bits
+constexpr uint8_t GI_REV = 1, GI_PAIRED = 2, GI_MAPQ_OK = 4, GI_BAD = 8;
+
+// Per read: place the grouping record of each valid read at its cell-major slot.
+__global__ void k_scatter(int64_t n, const int32_t* __restrict__ start, const int32_t* __restrict__ bc,
+                          const int32_t* __restrict__ tlen, const uint16_t* __restrict__ flag,
+                          const uint8_t* __restrict__ mapq, const uint64_t* __restrict__ roff,
+                          const uint32_t* __restrict__ rank, const uint32_t* __restrict__ O, Geom g,
+                          int min_mapq, uint32_t* __restrict__ g_idx, int32_t* __restrict__ g_start,
+                          uint32_t* __restrict__ g_tlen, uint8_t* __restrict__ g_info,
+                          uint64_t* __restrict__ g_off, DevStats* st) {
+    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    int c = bc[i];
+    uint16_t f = flag[i];
+    if (!read_valid(c, f, g.nc)) return;
+    int s = start[i];
+    int b = bin_of(s, g);
+    uint32_t dest = O[(size_t)b * g.nc + c] + rank[i];
+    uint32_t end = O[(size_t)g.nbins * g.nc + c];
+    if (dest >= end) {
+        atomicOr(&st->err, ERR_OVERFLOW);
+        return;
+    }
+    int t = tlen[i];
+    uint32_t at = t < 0 ? (uint32_t)(-(int64_t)t) : (uint32_t)t;
+    uint8_t info = (f & MGP_FLAG_REVERSE ? GI_REV : 0) | (f & MGP_FLAG_PAIRED ? GI_PAIRED : 0) |
+                   ((int)mapq[i] >= min_mapq ? GI_MAPQ_OK : 0) | (f & MGP_FLAG_NOSEQQUAL ? GI_BAD : 0);
+    g_idx[dest] = (uint32_t)i;
+    g_start[dest] = s;
+    g_tlen[dest] = at;
+    g_info[dest] = info;
+    g_off[dest] = roff[i];
+}
+
+// One workgroup per cell: duplicate marking inside each (start-bin) group (the
+// group is contiguous in the cell's segment; duplicates share the exact start),
+// kept/paired counts, MAPQ gate, compaction of the reads to pile up and the
+// per-window [lo, hi) ranges into that compacted list.
+__global__ void __launch_bounds__(kBlock) k_dedup(
+    Geom g, int dedup_mode, const uint32_t* __restrict__ base, const uint32_t* __restrict__ cnt,
+    const uint32_t* __restrict__ g_idx, const int32_t* __restrict__ g_start,
+    const uint32_t* __restrict__ g_tlen, const uint8_t* __restrict__ g_info,
+    const uint64_t* __restrict__ g_off, uint64_t* __restrict__ p_off, uint32_t* __restrict__ edges,
+    uint32_t* __restrict__ n_reads, uint8_t* __restrict__ any_paired, uint32_t* __restrict__ first_read,
+    DevStats* st) {
+    extern __shared__ uint32_t sm[];
+    uint32_t* ledge = sm;                 // [2 * nwin]
+    int32_t* lbin = (int32_t*)(sm + 2 * g.nwin);  // [kBlock]
+    __shared__ uint32_t wtot[kBlock / kWave];
+    __shared__ uint32_t s_running;
+    __shared__ int32_t s_lastbin;
+
+    const int c = blockIdx.x;
+    const uint32_t seg_lo = base[c];
+    const uint32_t seg_hi = seg_lo + cnt[c];
+    const int R = ((int)(st->max_span + g.G - 1) / g.G) * g.G;
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+
+    for (int k = threadIdx.x; k < 2 * g.nwin; k += blockDim.x) ledge[k] = 0xFFFFFFFFu;
+    if (threadIdx.x == 0) {
+        s_running = 0;
+        s_lastbin = -1;
+    }
+    __syncthreads();
+
+    uint32_t nkeep = 0, minidx = 0xFFFFFFFFu;
+    unsigned long long d2 = 0, d3 = 0;
+    bool paired = false, bad = false;
+
+    for (uint32_t cb = seg_lo; cb < seg_hi; cb += blockDim.x) {
+        const uint32_t j = cb + threadIdx.x;
+        const bool active = j < seg_hi;
+        bool piled = false;
+        int b = 0;
+        if (active) {
+            const int s = g_start[j];
+            const uint8_t info = g_info[j];
+            const uint32_t tl = g_tlen[j];
+            const uint32_t idx = g_idx[j];
+            b = bin_of(s, g);
+            minidx = min(minidx, idx);
+            bool dup2 = false, dup3 = false;
+            if (dedup_mode != MGP_DEDUP_NONE) {
+                for (uint32_t m = j; m-- > seg_lo;) {
+                    const int sm2 = g_start[m];
+                    if (bin_of(sm2, g) != b) break;
+                    if (sm2 == s && ((g_info[m] ^ info) & GI_REV) == 0 && g_idx[m] < idx) {
+                        dup2 = true;
+                        if (g_tlen[m] == tl) dup3 = true;
+                    }
+                }
+                for (uint32_t m = j + 1; m < seg_hi; ++m) {
+                    const int sm2 = g_start[m];
+                    if (bin_of(sm2, g) != b) break;
+                    if (sm2 == s && ((g_info[m] ^ info) & GI_REV) == 0 && g_idx[m] < idx) {
+                        dup2 = true;
+                        if (g_tlen[m] == tl) dup3 = true;
+                    }
+                }
+                d2 += dup2;
+                d3 += dup3;
+            }
+            const bool keep = dedup_mode == MGP_DEDUP_NONE ? true
+                              : dedup_mode == MGP_DEDUP_START ? !dup2
+                                                              : !dup3;
+            if (keep) {
+                ++nkeep;
+                paired |= (info & GI_PAIRED) != 0;
+                bad |= (info & GI_BAD) != 0;
+                piled = (info & GI_MAPQ_OK) != 0;
+            }
+        }
+        // block compaction of piled reads (order preserved)
+        const unsigned long long bal = __ballot(piled);
+        const uint32_t wpre = __popcll(bal & lanemask_lt());
+        if (lane == 0) wtot[wid] = __popcll(bal);
+        __syncthreads();
+        uint32_t woff = 0, tot = 0;
+        for (int w = 0; w < kBlock / kWave; ++w) {
+            if (w < wid) woff += wtot[w];
+            tot += wtot[w];
+        }
+        const uint32_t pos = woff + wpre;
+        if (piled) lbin[pos] = b;
+        __syncthreads();
+        const uint32_t running = s_running;
+        if (piled) {
+            const int prevb = pos == 0 ? s_lastbin : lbin[pos - 1];
+            const uint32_t P = running + pos;
+            p_off[seg_lo + P] = g_off[j];
+            for (int k = 0; k < g.nwin; ++k) {
+                const int lo_b = win_lo_bin(k, R, g);
+                if (prevb < lo_b && lo_b <= b) ledge[2 * k] = P;
+                const int hi_b = win_hi_bin(k, g);
+                if (prevb < hi_b && hi_b <= b) ledge[2 * k + 1] = P;
+            }
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            if (tot) s_lastbin = lbin[tot - 1];
+            s_running = running + tot;
+        }
+        __syncthreads();
+    }
+
+    // reductions
+    nkeep = wave_sum(nkeep);
+    d2 = wave_sum(d2);
+    d3 = wave_sum(d3);
+    minidx = wave_min(minidx);
+    const bool anyp = __ballot(paired) != 0ull;
+    const bool anyb = __ballot(bad) != 0ull;
+    __shared__ uint32_t r_keep[4], r_min[4];
+    __shared__ unsigned long long r_d2[4], r_d3[4];
+    __shared__ int r_p[4], r_b[4];
+    if (lane == 0) {
+        r_keep[wid] = nkeep;
+        r_min[wid] = minidx;
+        r_d2[wid] = d2;
+        r_d3[wid] = d3;
+        r_p[wid] = anyp;
+        r_b[wid] = anyb;
+    }
+    __syncthreads();
+    const uint32_t npiled = s_running;
+    for (int k = threadIdx.x; k < 2 * g.nwin; k += blockDim.x) {
+        uint32_t e = ledge[k];
+        edges[(size_t)c * 2 * g.nwin + k] = e == 0xFFFFFFFFu ? npiled : e;
+    }
+    if (threadIdx.x == 0) {
+        uint32_t K = 0, M = 0xFFFFFFFFu;
+        unsigned long long D2 = 0, D3 = 0;
+        int PP = 0, BB = 0;
+        for (int w = 0; w < 4; ++w) {
+            K += r_keep[w];
+            M = min(M, r_min[w]);
+            D2 += r_d2[w];
+            D3 += r_d3[w];
+            PP |= r_p[w];
+            BB |= r_b[w];
+        }
+        n_reads[c] = K;
+        any_paired[c] = (uint8_t)PP;
+        first_read[c] = M;
+        if (D2) atomicAdd(&st->dup_pos, D2);
+        if (D3) atomicAdd(&st->dup_len, D3);
+        if (K) {
+            atomicAdd(&st->filtered, (unsigned long long)K);
+            atomicAdd(&st->n_barcodes, 1ull);
+        }
+        if (BB) atomicOr(&st->err, ERR_BADREAD);
+    }
+}
+
+struct PileCfg {
+    int min_baseq, min_dist, min_reads;
+    double max_bias;
+    bool bias_active;  // max_bias < 1 (max/total <= 1 otherwise)
+};
+
+__device__ __forceinline__ int base_index(uint32_t code) {
+    // BAM 4-bit codes: 1=A, 2=C, 4=G, 8=T; everything else is skipped (pileup.py:83-86)
+    return code == 1 ? 0 : code == 2 ? 1 : code == 4 ? 2 : code == 8 ? 3 : -1;
+}
+
+// One read: Tn5 cut + CIGAR walk restricted to window [w0, w0+wlen).
+__device__ __forceinline__ void pile_read(const uint8_t* __restrict__ rec, int w0, int wlen, const PileCfg& pc,
+                                          int Wp, uint32_t* __restrict__ tile, uint32_t* __restrict__ t5,
+                                          uint32_t max_span, bool& span_err) {
+    const int32_t start = *reinterpret_cast<const int32_t*>(rec);
+    const uint32_t lseq = *reinterpret_cast<const uint32_t*>(rec + 4);
+    const uint32_t ncig = *reinterpret_cast<const uint16_t*>(rec + 8);
+    const uint32_t flag = *reinterpret_cast<const uint16_t*>(rec + 10);
+    const uint32_t* cig = reinterpret_cast<const uint32_t*>(rec + 16);
+    const uint8_t* qual = rec + 16 + 4 * ncig;
+    const uint8_t* seq = qual + lseq;
+    const int strand = (flag & MGP_FLAG_REVERSE) ? 1 : 0;
+    const int64_t wend = (int64_t)w0 + wlen;
+
+    // Tn5 cut (pileup.py:43-50): reverse reads cut at start + len(seq) - 1
+    const int64_t cut = strand ? (int64_t)start + lseq - 1 : (int64_t)start;
+    if (cut >= w0 && cut < wend && cut >= 0) atomicAdd(&t5[strand * Wp + (int)(cut - w0)], 1u);
+
+    const int64_t vq0 = pc.min_dist > 0 ? pc.min_dist : 0;
+    const int64_t vq1 = pc.min_dist > 0 ? (int64_t)lseq - pc.min_dist : (int64_t)lseq;
+    int64_t ref = start, q = 0;
+    uint32_t* plane = tile + strand * Wp;
+    for (uint32_t o = 0; o < ncig; ++o) {
+        const uint32_t cg = cig[o];
+        const uint32_t op = cg & 15u;
+        const int64_t len = cg >> 4;
+        if (op == 0 || op == 7 || op == 8) {
+            int64_t klo = max((int64_t)0, max((int64_t)w0 - ref, vq0 - q));
+            int64_t khi = min(len, min(wend - ref, min(vq1, (int64_t)lseq) - q));
+            for (int64_t k = klo; k < khi; ++k) {
+                const int64_t qq = q + k;
+                const int qv = (int)(int8_t)qual[qq];
+                if (qv < pc.min_baseq) continue;
+                const uint8_t sb = seq[qq >> 1];
+                const uint32_t code = (qq & 1) ? (sb & 15u) : (sb >> 4);
+                const int bi = base_index(code);
+                if (bi < 0) continue;
+                atomicAdd(&plane[2 * bi * Wp + (int)(ref + k - w0)], 1u);
+            }
+            q += len;
+            ref += len;
+        } else if (op == 2 || op == 3) {
+            ref += len;
+        } else if (op == 4) {
+            q += len;
+        }
+    }
+    const int64_t reach = max(ref - (int64_t)start, (int64_t)lseq);
+    if (reach > (int64_t)max_span) span_err = true;
+}
+
+constexpr int kMaxPosPerThread = 8;  // W <= 8 * 256
+
+// grid (nchunks, nwin): workgroup = (cell chunk, position window); the LDS tile
+// holds 8 count planes + 2 Tn5 planes of Wp u32 each.
+__global__ void __launch_bounds__(kBlock) k_pileup(
+    Geom g, PileCfg pc, const uint8_t* __restrict__ payload, const uint64_t* __restrict__ p_off,
+    const uint32_t* __restrict__ base, const uint32_t* __restrict__ edges, const uint32_t* __restrict__ n_reads,
+    uint32_t* __restrict__ counts, uint32_t* __restrict__ tn5, uint32_t* __restrict__ depth,
+    uint32_t* __restrict__ covered, unsigned long long* __restrict__ dsum, uint32_t* __restrict__ dmax,
+    uint32_t* __restrict__ tally_part, DevStats* st) {
+    extern __shared__ uint32_t tile[];  // [10][Wp]
+    uint32_t* t5 = tile + 8 * g.Wp;
+    __shared__ uint32_t r_cov[4], r_max[4];
+    __shared__ unsigned long long r_sum[4];
+
+    const int k = blockIdx.y;
+    const int chunk = blockIdx.x;
+    const int w0 = k * g.W;
+    const int wlen = min(g.W, g.L - w0);
+    const int L = g.L;
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const uint32_t max_span = st->max_span;
+    const int min_reads = max(1, pc.min_reads);
+    bool span_err = false;
+
+    uint32_t tal[kMaxPosPerThread][4];
+#pragma unroll
+    for (int m = 0; m < kMaxPosPerThread; ++m)
+#pragma unroll
+        for (int b = 0; b < 4; ++b) tal[m][b] = 0;
+
+    const int c0 = chunk * g.cpb, c1 = min(g.nc, c0 + g.cpb);
+    for (int c = c0; c < c1; ++c) {
+        for (int x = threadIdx.x; x < 10 * g.Wp; x += blockDim.x) tile[x] = 0;
+        __syncthreads();
+        const bool gate = n_reads[c] >= (uint32_t)min_reads;
+        if (gate) {
+            const uint32_t sb = base[c];
+            const uint32_t lo = sb + edges[(size_t)c * 2 * g.nwin + 2 * k];
+            const uint32_t hi = sb + edges[(size_t)c * 2 * g.nwin + 2 * k + 1];
+            for (uint32_t j = lo + threadIdx.x; j < hi; j += blockDim.x)
+                pile_read(payload + p_off[j], w0, wlen, pc, g.Wp, tile, t5, max_span, span_err);
+        }
+        __syncthreads();
+        uint32_t cov = 0, mx = 0;
+        unsigned long long sum = 0;
+#pragma unroll
+        for (int m = 0; m < kMaxPosPerThread; ++m) {
+            const int p = threadIdx.x + m * kBlock;
+            if (p < wlen) {
+                uint32_t v[8];
+#pragma unroll
+                for (int x = 0; x < 8; ++x) v[x] = tile[x * g.Wp + p];
+                uint32_t d = 0;
+#pragma unroll
+                for (int b = 0; b < 4; ++b) {
+                    const uint32_t fw = v[2 * b], rv = v[2 * b + 1];
+                    const uint32_t tot = fw + rv;
+                    if (pc.bias_active && tot > 0) {
+                        const double bias = (double)(fw > rv ? fw : rv) / (double)tot;
+                        if (bias > pc.max_bias) {
+                            v[2 * b] = 0;
+                            v[2 * b + 1] = 0;
+                        }
+                    }
+                    const uint32_t t2 = v[2 * b] + v[2 * b + 1];
+                    tal[m][b] += t2;
+                    d += t2;
+                }
+                uint32_t tf = t5[p], tr = t5[g.Wp + p];
+                if (d == 0) tf = tr = 0;
+                const size_t P = (size_t)c * L + w0 + p;
+                uint4* cp = reinterpret_cast<uint4*>(counts + P * 8);
+                cp[0] = make_uint4(v[0], v[1], v[2], v[3]);
+                cp[1] = make_uint4(v[4], v[5], v[6], v[7]);
+                reinterpret_cast<uint2*>(tn5)[P] = make_uint2(tf, tr);
+                depth[P] = d;
+                cov += d > 0;
+                sum += d;
+                mx = d > mx ? d : mx;
+            }
+        }
+        if (gate) {
+            cov = wave_sum(cov);
+            sum = wave_sum(sum);
+            mx = wave_max(mx);
+            if (lane == 0) {
+                r_cov[wid] = cov;
+                r_sum[wid] = sum;
+                r_max[wid] = mx;
+            }
+        }
+        __syncthreads();
+        if (gate && threadIdx.x == 0) {
+            uint32_t C = 0, M = 0;
+            unsigned long long S = 0;
+            for (int w = 0; w < 4; ++w) {
+                C += r_cov[w];
+                S += r_sum[w];
+                M = max(M, r_max[w]);
+            }
+            if (C) {
+                atomicAdd(&covered[c], C);
+                atomicAdd(&dsum[c], S);
+                atomicMax(&dmax[c], M);
+            }
+        }
+    }
+#pragma unroll
+    for (int m = 0; m < kMaxPosPerThread; ++m) {
+        const int p = threadIdx.x + m * kBlock;
+        if (p < wlen) {
+            uint4* tp = reinterpret_cast<uint4*>(tally_part + ((size_t)chunk * L + w0 + p) * 4);
+            *tp = make_uint4(tal[m][0], tal[m][1], tal[m][2], tal[m][3]);
+        }
+    }
+    if (span_err) atomicOr(&st->err, ERR_SPAN);
+}
+
+// Radix select of the k-th smallest (0-based) among vals[0..n) in LDS.
+__device__ uint32_t lds_select(const uint32_t* vals, uint32_t n, uint32_t kth, uint32_t* hist, uint32_t* sh) {
+    uint32_t prefix = 0, mask = 0;
+    for (int shift = 24; shift >= 0; shift -= 8) {
+        for (int x = threadIdx.x; x < 256; x += blockDim.x) hist[x] = 0;
+        __syncthreads();
+        for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
+            const uint32_t v = vals[i];
+            if ((v & mask) == prefix) atomicAdd(&hist[(v >> shift) & 255u], 1u);
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            uint32_t acc = 0, bsel = 255;
+            for (uint32_t b2 = 0; b2 < 256; ++b2) {
+                if (acc + hist[b2] > kth) {
+                    bsel = b2;
+                    break;
+                }
+                acc += hist[b2];
+            }
+            sh[0] = prefix | (bsel << shift);
+            sh[1] = kth - acc;
+        }
+        __syncthreads();
+        prefix = sh[0];
+        kth = sh[1];
+        mask |= 255u << shift;
+        __syncthreads();
+    }
+    return prefix;
+}
+
+// One workgroup per cell: pass flag and the two middle order statistics of the
+// covered depths (np.median, writers.py:190).
+__global__ void __launch_bounds__(kBlock) k_median(Geom g, int min_reads, const uint32_t* __restrict__ depth,
+                                                   const uint32_t* __restrict__ n_reads,
+                                                   const uint32_t* __restrict__ covered,
+                                                   uint32_t* __restrict__ med_lo, uint32_t* __restrict__ med_hi,
+                                                   uint8_t* __restrict__ passed, DevStats* st) {
+    extern __shared__ uint32_t vals[];  // [L]
+    __shared__ uint32_t hist[256];
+    __shared__ uint32_t sh[2];
+    __shared__ uint32_t cnt;
+    const int c = blockIdx.x;
+    const uint32_t n = covered[c];
+    const bool pass = n > 0 && n_reads[c] >= (uint32_t)max(1, min_reads);
+    if (!pass) {
+        if (threadIdx.x == 0) {
+            med_lo[c] = 0;
+            med_hi[c] = 0;
+            passed[c] = 0;
+        }
+        return;
+    }
+    if (threadIdx.x == 0) cnt = 0;
+    __syncthreads();
+    const uint32_t* drow = depth + (size_t)c * g.L;
+    for (int p = threadIdx.x; p < g.L; p += blockDim.x) {
+        const uint32_t d = drow[p];
+        if (d) vals[atomicAdd(&cnt, 1u)] = d;
+    }
+    __syncthreads();
+    const uint32_t lo = lds_select(vals, n, (n - 1) / 2, hist, sh);
+    const uint32_t hi = (n & 1) ? lo : lds_select(vals, n, n / 2, hist, sh);
+    if (threadIdx.x == 0) {
+        med_lo[c] = lo;
+        med_hi[c] = hi;
+        passed[c] = 1;
+        atomicAdd(&st->cells_passed, 1ull);
+    }
+}
+
+__global__ void k_tally_reduce(const uint32_t* __restrict__ part, int nchunks, int L4,
+                               unsigned long long* __restrict__ tally) {
+    int x = blockIdx.x * blockDim.x + threadIdx.x;
+    if (x >= L4) return;
+    unsigned long long acc = 0;
+    for (int ch = 0; ch < nchunks; ++ch) acc += part[(size_t)ch * L4 + x];
+    tally[x] = acc;
+}
+
+__global__ void k_add_u64(uint64_t* __restrict__ a, int64_t n, uint64_t add) {
+    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) a[i] += add;
+}
+
+// ---------------------------------------------------------------------------
+// host side
+// ---------------------------------------------------------------------------
+static inline unsigned blocks_for(int64_t n, int bs = kBlock) { return (unsigned)((n + bs - 1) / bs); }
+
+static int configure_geometry(mgp_ctx* ctx) {
+    const mgp_config& c = ctx->cfg;
+    Geom& g = ctx->g;
+    g.L = c.mito_len;
+    g.G = 8;
+    g.nb_reg = (g.L + g.G - 1) / g.G;
+    g.nbins = g.nb_reg + 1;
+    g.nwin = (g.L + 1023) / 1024;          // ~1 Ki positions per window
+    g.W = (g.L + g.nwin - 1) / g.nwin;
+    g.W = ((g.W + g.G - 1) / g.G) * g.G;   // multiple of the bin width
+    g.nwin = (g.L + g.W - 1) / g.W;
+    if (g.W > kMaxPosPerThread * kBlock) return set_err(MGP_E_INVALID, "window too wide");
+    g.Wp = g.W | 1;                        // odd plane pitch
+    g.nc = c.n_cells;
+    // cells per pileup workgroup: ~4096 workgroups over the windows
+    int64_t target = 4096;
+    int64_t cpb = ((int64_t)g.nc * g.nwin + target - 1) / target;
+    g.cpb = (int)std::max<int64_t>(1, std::min<int64_t>(cpb, 64));
+    g.nchunks = g.nc > 0 ? (g.nc + g.cpb - 1) / g.cpb : 0;
+    return MGP_OK;
+}
+
+extern "C" {
+
+int mgp_abi_version(void) { return MGP_ABI_VERSION; }
+const char* mgp_last_error(void) { return g_err.c_str(); }
+
+int mgp_device_count(int* out) {
+    if (!out) return set_err(MGP_E_INVALID, "null out");
+    HIP_TRY(hipGetDeviceCount(out));
+    return MGP_OK;
+}
+
+int mgp_host_alloc(int64_t bytes, void** out) {
+    if (!out || bytes < 0) return set_err(MGP_E_INVALID, "bad args");
+    HIP_TRY(hipHostMalloc(out, (size_t)std::max<int64_t>(bytes, 1), hipHostMallocDefault));
+    return MGP_OK;
+}
+int mgp_host_free(void* p) {
+    if (p) HIP_TRY(hipHostFree(p));
+    return MGP_OK;
+}
+
+int mgp_open(const mgp_config* cfg, int hip_device, mgp_ctx** out) {
+    if (!cfg || !out) return set_err(MGP_E_INVALID, "null config/out");
+    if (cfg->mito_len <= 0 || cfg->mito_len > (1 << 24)) return set_err(MGP_E_INVALID, "mito_len out of range");
+    if (cfg->n_cells < 0) return set_err(MGP_E_INVALID, "n_cells < 0");
+    if (cfg->dedup_mode < 0 || cfg->dedup_mode > 2) return set_err(MGP_E_INVALID, "dedup_mode out of range");
+    if (cfg->flags != 0) return set_err(MGP_E_INVALID, "config.flags must be 0");
+    int ndev = 0;
+    HIP_TRY(hipGetDeviceCount(&ndev));
+    if (hip_device < 0 || hip_device >= ndev)
+        return set_err(MGP_E_INVALID, "hip_device " + std::to_string(hip_device) + " not present (" +
+                                          std::to_string(ndev) + " devices)");
+    HIP_TRY(hipSetDevice(hip_device));
+    mgp_ctx* ctx = new mgp_ctx();
+    ctx->cfg = *cfg;
+    ctx->dev = hip_device;
+    int r = configure_geometry(ctx);
+    if (r != MGP_OK) {
+        delete ctx;
+        return r;
+    }
+    hipDeviceProp_t prop;
+    HIP_TRY(hipGetDeviceProperties(&prop, hip_device));
+    ctx->lds_hist_max_cells = (int)std::min<size_t>(prop.sharedMemPerBlock, 96 * 1024) / 4;
+    // kernels whose dynamic LDS may exceed the 64 KiB default (gfx950 has 160 KiB per CU)
+    {
+        const int lds_max = (int)std::min<size_t>(prop.sharedMemPerBlock, 160 * 1024);
+        HIP_TRY(hipFuncSetAttribute((const void*)k_median, hipFuncAttributeMaxDynamicSharedMemorySize, lds_max));
+        HIP_TRY(hipFuncSetAttribute((const void*)k_bin_hist<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                    lds_max));
+        HIP_TRY(hipFuncSetAttribute((const void*)k_pileup, hipFuncAttributeMaxDynamicSharedMemorySize, lds_max));
+        if ((size_t)ctx->g.L * 4 + 2048 > (size_t)lds_max) {
+            delete ctx;
+            return set_err(MGP_E_INVALID, "mito_len too large for the per-cell median LDS buffer");
+        }
+    }
+    HIP_TRY(hipStreamCreateWithFlags(&ctx->s_comp, hipStreamNonBlocking));
+    HIP_TRY(hipStreamCreateWithFlags(&ctx->s_copy, hipStreamNonBlocking));
+    HIP_TRY(hipEventCreateWithFlags(&ctx->ev_copy, hipEventDisableTiming));
+    for (int r = 0; r < mgp_ctx::kRing; ++r)
+        for (int s = 0; s < ST_N; ++s) {
+            HIP_TRY(hipEventCreate(&ctx->ev[r][s][0]));
+            HIP_TRY(hipEventCreate(&ctx->ev[r][s][1]));
+        }
+    if (cfg->reserve_reads > 0) {
+        const size_t n = (size_t)cfg->reserve_reads;
+        MGP_TRY(ctx->start.ensure(n * 4));
+        MGP_TRY(ctx->bc.ensure(n * 4));
+        MGP_TRY(ctx->tlen.ensure(n * 4));
+        MGP_TRY(ctx->flag.ensure(n * 2));
+        MGP_TRY(ctx->mapq.ensure(n));
+        MGP_TRY(ctx->span.ensure(n * 4));
+        MGP_TRY(ctx->roff.ensure(n * 8));
+    }
+    if (cfg->reserve_payload > 0) MGP_TRY(ctx->payload.ensure((size_t)cfg->reserve_payload));
+    *out = ctx;
+    return MGP_OK;
+}
+
+void mgp_close(mgp_ctx* ctx) {
+    if (!ctx) return;
+    (void)hipSetDevice(ctx->dev);
+    (void)hipStreamSynchronize(ctx->s_comp);
+    (void)hipStreamSynchronize(ctx->s_copy);
+    if (ctx->comm) ncclCommDestroy(ctx->comm);
+    DevBuf* bufs[] = {&ctx->start,     &ctx->bc,        &ctx->tlen,     &ctx->flag,       &ctx->mapq,
+                      &ctx->span,      &ctx->roff,      &ctx->payload,  &ctx->bin_start,  &ctx->rank,
+                      &ctx->H,         &ctx->P,         &ctx->cell_cnt, &ctx->cell_base,  &ctx->g_idx,
+                      &ctx->g_start,   &ctx->g_tlen,    &ctx->g_info,   &ctx->g_off,      &ctx->p_off,
+                      &ctx->edges,     &ctx->tally_part, &ctx->tally,   &ctx->n_reads,    &ctx->any_paired,
+                      &ctx->passed,    &ctx->covered,   &ctx->dsum,     &ctx->dmax,       &ctx->med_lo,
+                      &ctx->med_hi,    &ctx->first_read, &ctx->counts,  &ctx->tn5,        &ctx->depth,
+                      &ctx->stats};
+    for (DevBuf* b : bufs) b->release();
+    for (int r = 0; r < mgp_ctx::kRing; ++r)
+        for (int s = 0; s < ST_N; ++s) {
+            (void)hipEventDestroy(ctx->ev[r][s][0]);
+            (void)hipEventDestroy(ctx->ev[r][s][1]);
+        }
+    (void)hipEventDestroy(ctx->ev_copy);
+    (void)hipStreamDestroy(ctx->s_comp);
+    (void)hipStreamDestroy(ctx->s_copy);
+    delete ctx;
+}
+
+static int ensure_inputs(mgp_ctx* ctx, int64_t n_total, int64_t pay_total, bool preserve) {
+    const size_t n = (size_t)n_total;
+    const size_t used = preserve ? (size_t)ctx->n : 0;
+    hipStream_t s = ctx->s_copy;
+    MGP_TRY(ctx->start.ensure(n * 4, preserve, used * 4, s));
+    MGP_TRY(ctx->bc.ensure(n * 4, preserve, used * 4, s));
+    MGP_TRY(ctx->tlen.ensure(n * 4, preserve, used * 4, s));
+    MGP_TRY(ctx->flag.ensure(n * 2, preserve, used * 2, s));
+    MGP_TRY(ctx->mapq.ensure(n, preserve, used, s));
+    MGP_TRY(ctx->span.ensure(n * 4, preserve, used * 4, s));
+    MGP_TRY(ctx->roff.ensure(n * 8, preserve, used * 8, s));
+    MGP_TRY(ctx->payload.ensure((size_t)pay_total + 16, preserve, preserve ? (size_t)ctx->pay : 0, s));
+    return MGP_OK;
+}
+
+int mgp_push_batch(mgp_ctx* ctx, const mgp_batch* b) {
+    if (!ctx || !b) return set_err(MGP_E_INVALID, "null ctx/batch");
+    if (b->n_reads < 0 || b->payload_bytes < 0) return set_err(MGP_E_INVALID, "negative sizes");
+    if (b->n_reads == 0) return MGP_OK;
+    if (!b->start || !b->bc || !b->tlen || !b->flag || !b->mapq || !b->span || !b->rec_off || !b->payload)
+        return set_err(MGP_E_INVALID, "null batch array");
+    if (ctx->n + b->n_reads > (int64_t)0xFFFFFFFEll)
+        return set_err(MGP_E_INVALID, "more than 2^32-2 resident reads per context; shard or batch the run");
+    HIP_TRY(hipSetDevice(ctx->dev));
+    const int64_t n0 = ctx->n, nb = b->n_reads;
+    const int64_t pay0 = (ctx->pay + 15) & ~int64_t(15);
+    MGP_TRY(ensure_inputs(ctx, n0 + nb, pay0 + b->payload_bytes, true));
+    hipStream_t s = ctx->s_copy;
+    HIP_TRY(hipMemcpyAsync(ctx->start.as<int32_t>() + n0, b->start, nb * 4, hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemcpyAsync(ctx->bc.as<int32_t>() + n0, b->bc, nb * 4, hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemcpyAsync(ctx->tlen.as<int32_t>() + n0, b->tlen, nb * 4, hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemcpyAsync(ctx->flag.as<uint16_t>() + n0, b->flag, nb * 2, hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemcpyAsync(ctx->mapq.as<uint8_t>() + n0, b->mapq, nb, hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemcpyAsync(ctx->span.as<uint32_t>() + n0, b->span, nb * 4, hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemcpyAsync(ctx->roff.as<uint64_t>() + n0, b->rec_off, nb * 8, hipMemcpyHostToDevice, s));
+    if (b->payload_bytes)
+        HIP_TRY(hipMemcpyAsync(ctx->payload.as<uint8_t>() + pay0, b->payload, b->payload_bytes,
+                               hipMemcpyHostToDevice, s));
+    if (pay0) {
+        k_add_u64<<<blocks_for(nb), kBlock, 0, s>>>(ctx->roff.as<uint64_t>() + n0, nb, (uint64_t)pay0);
+        HIP_TRY(hipGetLastError());
+    }
+    HIP_TRY(hipEventRecord(ctx->ev_copy, s));
+    ctx->n = n0 + nb;
+    ctx->pay = pay0 + b->payload_bytes;
+    ctx->ran = false;
+    return MGP_OK;
+}
+
+int mgp_reset(mgp_ctx* ctx) {
+    if (!ctx) return set_err(MGP_E_INVALID, "null ctx");
+    HIP_TRY(hipSetDevice(ctx->dev));
+    HIP_TRY(hipStreamSynchronize(ctx->s_copy));
+    HIP_TRY(hipStreamSynchronize(ctx->s_comp));
+    ctx->n = 0;
+    ctx->pay = 0;
+    ctx->ran = false;
+    return MGP_OK;
+}
+
+int mgp_resident(mgp_ctx* ctx, int64_t* n_reads, int64_t* payload_bytes) {
+    if (!ctx) return set_err(MGP_E_INVALID, "null ctx");
+    if (n_reads) *n_reads = ctx->n;
+    if (payload_bytes) *payload_bytes = ctx->pay;
+    return MGP_OK;
+}
+
+static int ensure_run_buffers(mgp_ctx* ctx) {
+    const Geom& g = ctx->g;
+    const size_t n = (size_t)std::max<int64_t>(ctx->n, 1);
+    const size_t nc = (size_t)std::max(g.nc, 1);
+    const size_t L = (size_t)g.L;
+    MGP_TRY(ctx->bin_start.ensure((size_t)(g.nbins + 1) * 4));
+    MGP_TRY(ctx->rank.ensure(n * 4));
+    MGP_TRY(ctx->H.ensure((size_t)(g.nbins + 1) * nc * 4));
+    MGP_TRY(ctx->P.ensure((size_t)((g.nbins + 31) / 32 + 1) * nc * 4));
+    MGP_TRY(ctx->cell_cnt.ensure(nc * 4));
+    MGP_TRY(ctx->cell_base.ensure(nc * 4));
+    MGP_TRY(ctx->g_idx.ensure(n * 4));
+    MGP_TRY(ctx->g_start.ensure(n * 4));
+    MGP_TRY(ctx->g_tlen.ensure(n * 4));
+    MGP_TRY(ctx->g_info.ensure(n));
+    MGP_TRY(ctx->g_off.ensure(n * 8));
+    MGP_TRY(ctx->p_off.ensure(n * 8));
+    MGP_TRY(ctx->edges.ensure(nc * 2 * g.nwin * 4));
+    MGP_TRY(ctx->tally_part.ensure((size_t)std::max(g.nchunks, 1) * L * 16));
+    MGP_TRY(ctx->tally.ensure(L * 4 * 8));
+    MGP_TRY(ctx->n_reads.ensure(nc * 4));
+    MGP_TRY(ctx->any_paired.ensure(nc));
+    MGP_TRY(ctx->passed.ensure(nc));
+    MGP_TRY(ctx->covered.ensure(nc * 4));
+    MGP_TRY(ctx->dsum.ensure(nc * 8));
+    MGP_TRY(ctx->dmax.ensure(nc * 4));
+    MGP_TRY(ctx->med_lo.ensure(nc * 4));
+    MGP_TRY(ctx->med_hi.ensure(nc * 4));
+    MGP_TRY(ctx->first_read.ensure(nc * 4));
+    MGP_TRY(ctx->counts.ensure(nc * L * 32));
+    MGP_TRY(ctx->tn5.ensure(nc * L * 8));
+    MGP_TRY(ctx->depth.ensure(nc * L * 4));
+    MGP_TRY(ctx->stats.ensure(sizeof(DevStats)));
+    return MGP_OK;
+}
+
+#define STAGE_BEGIN(st) HIP_TRY(hipEventRecord(ctx->ev[slot][st][0], s)); ctx->stage_ran[slot][st] = true
+#define STAGE_END(st) HIP_TRY(hipEventRecord(ctx->ev[slot][st][1], s))
+
+int mgp_run(mgp_ctx* ctx) {
+    if (!ctx) return set_err(MGP_E_INVALID, "null ctx");
+    HIP_TRY(hipSetDevice(ctx->dev));
+    MGP_TRY(ensure_run_buffers(ctx));
+    const Geom g = ctx->g;
+    const int64_t n = ctx->n;
+    const int nc = g.nc;
+    hipStream_t s = ctx->s_comp;
+    HIP_TRY(hipStreamWaitEvent(s, ctx->ev_copy, 0));
+    const int slot = (int)(ctx->runs % mgp_ctx::kRing);
+    for (int i = 0; i < ST_N; ++i) ctx->stage_ran[slot][i] = false;
+    DevStats* st = ctx->stats.as<DevStats>();
+    HIP_TRY(hipMemsetAsync(st, 0, sizeof(DevStats), s));
+
+    if (nc > 0) {
+        HIP_TRY(hipMemsetAsync(ctx->covered.p, 0, (size_t)nc * 4, s));
+        HIP_TRY(hipMemsetAsync(ctx->dsum.p, 0, (size_t)nc * 8, s));
+        HIP_TRY(hipMemsetAsync(ctx->dmax.p, 0, (size_t)nc * 4, s));
+    }
+
+    // 1. start-bin boundaries
+    STAGE_BEGIN(ST_BINS);
+    HIP_TRY(hipMemsetAsync(ctx->bin_start.p, 0, (size_t)(g.nbins + 1) * 4, s));
+    if (n > 0) {
+        k_bin_bounds<<<blocks_for(n), kBlock, 0, s>>>(ctx->start.as<int32_t>(), n, g, ctx->bin_start.as<uint32_t>(),
+                                                       st);
+        HIP_TRY(hipGetLastError());
+    }
+    STAGE_END(ST_BINS);
+
+    if (nc > 0) {
+        // 2. (bin, cell) histogram + ranks
+        STAGE_BEGIN(ST_HIST);
+        const bool lds = nc <= ctx->lds_hist_max_cells;
+        if (!lds || n == 0) HIP_TRY(hipMemsetAsync(ctx->H.p, 0, (size_t)(g.nbins + 1) * nc * 4, s));
+        if (n > 0) {
+            if (lds)
+                k_bin_hist<true><<<g.nbins, kBlock, (size_t)nc * 4, s>>>(
+                    ctx->bin_start.as<uint32_t>(), ctx->bc.as<int32_t>(), ctx->flag.as<uint16_t>(),
+                    ctx->span.as<uint32_t>(), n, g, ctx->H.as<uint32_t>(), ctx->rank.as<uint32_t>(), st);
+            else
+                k_bin_hist<false><<<g.nbins, kBlock, 0, s>>>(ctx->bin_start.as<uint32_t>(), ctx->bc.as<int32_t>(),
+                                                             ctx->flag.as<uint16_t>(), ctx->span.as<uint32_t>(), n, g,
+                                                             ctx->H.as<uint32_t>(), ctx->rank.as<uint32_t>(), st);
+            HIP_TRY(hipGetLastError());
+        }
+        STAGE_END(ST_HIST);
+
+        // 3. cell-major exclusive scan of the histogram
+        STAGE_BEGIN(ST_SCAN);
+        const int RB = 32;
+        const int nrb = (g.nbins + RB - 1) / RB;
+        dim3 g2((nc + kBlock - 1) / kBlock, nrb);
+        k_scan_colsum<<<g2, kBlock, 0, s>>>(ctx->H.as<uint32_t>(), g.nbins, nc, RB, ctx->P.as<uint32_t>());
+        k_scan_rows<<<blocks_for(nc), kBlock, 0, s>>>(ctx->P.as<uint32_t>(), nrb, nc, ctx->cell_cnt.as<uint32_t>());
+        k_scan_cells<<<1, 1024, 0, s>>>(ctx->cell_cnt.as<uint32_t>(), nc, ctx->cell_base.as<uint32_t>());
+        k_scan_apply<<<g2, kBlock, 0, s>>>(ctx->H.as<uint32_t>(), ctx->P.as<uint32_t>(), ctx->cell_base.as<uint32_t>(),
+                                           ctx->cell_cnt.as<uint32_t>(), g.nbins, nc, RB, nrb);
+        HIP_TRY(hipGetLastError());
+        STAGE_END(ST_SCAN);
+
+        // 4. scatter grouping records
+        STAGE_BEGIN(ST_SCATTER);
+        if (n > 0) {
+            k_scatter<<<blocks_for(n), kBlock, 0, s>>>(
+                n, ctx->start.as<int32_t>(), ctx->bc.as<int32_t>(), ctx->tlen.as<int32_t>(), ctx->flag.as<uint16_t>(),
+                ctx->mapq.as<uint8_t>(), ctx->roff.as<uint64_t>(), ctx->rank.as<uint32_t>(), ctx->H.as<uint32_t>(), g,
+                ctx->cfg.min_mapq, ctx->g_idx.as<uint32_t>(), ctx->g_start.as<int32_t>(), ctx->g_tlen.as<uint32_t>(),
+                ctx->g_info.as<uint8_t>(), ctx->g_off.as<uint64_t>(), st);
+            HIP_TRY(hipGetLastError());
+        }
+        STAGE_END(ST_SCATTER);
+
+        // 5. dedup + compaction + window ranges
+        STAGE_BEGIN(ST_DEDUP);
+        const size_t dsm = (size_t)(2 * g.nwin + kBlock) * 4;
+        k_dedup<<<nc, kBlock, dsm, s>>>(g, ctx->cfg.dedup_mode, ctx->cell_base.as<uint32_t>(),
+                                        ctx->cell_cnt.as<uint32_t>(), ctx->g_idx.as<uint32_t>(),
+                                        ctx->g_start.as<int32_t>(), ctx->g_tlen.as<uint32_t>(),
+                                        ctx->g_info.as<uint8_t>(), ctx->g_off.as<uint64_t>(), ctx->p_off.as<uint64_t>(),
+                                        ctx->edges.as<uint32_t>(), ctx->n_reads.as<uint32_t>(),
+                                        ctx->any_paired.as<uint8_t>(), ctx->first_read.as<uint32_t>(), st);
+        HIP_TRY(hipGetLastError());
+        STAGE_END(ST_DEDUP);
+
+        // 6. pileup
+        STAGE_BEGIN(ST_PILEUP);
+        PileCfg pc;
+        pc.min_baseq = ctx->cfg.min_baseq;
+        pc.min_dist = ctx->cfg.min_dist_from_end;
+        pc.min_reads = ctx->cfg.min_reads;
+        pc.max_bias = ctx->cfg.max_strand_bias;
+        pc.bias_active = ctx->cfg.max_strand_bias < 1.0;
+        dim3 gp(g.nchunks, g.nwin);
+        const size_t psm = (size_t)10 * g.Wp * 4;
+        k_pileup<<<gp, kBlock, psm, s>>>(g, pc, ctx->payload.as<uint8_t>(), ctx->p_off.as<uint64_t>(),
+                                         ctx->cell_base.as<uint32_t>(), ctx->edges.as<uint32_t>(),
+                                         ctx->n_reads.as<uint32_t>(), ctx->counts.as<uint32_t>(),
+                                         ctx->tn5.as<uint32_t>(), ctx->depth.as<uint32_t>(),
+                                         ctx->covered.as<uint32_t>(), ctx->dsum.as<unsigned long long>(),
+                                         ctx->dmax.as<uint32_t>(), ctx->tally_part.as<uint32_t>(), st);
+        HIP_TRY(hipGetLastError());
+        STAGE_END(ST_PILEUP);
+
+        // 7. medians + pass flags
+        STAGE_BEGIN(ST_MEDIAN);
+        k_median<<<nc, kBlock, (size_t)g.L * 4, s>>>(g, ctx->cfg.min_reads, ctx->depth.as<uint32_t>(),
+                                                     ctx->n_reads.as<uint32_t>(), ctx->covered.as<uint32_t>(),
+                                                     ctx->med_lo.as<uint32_t>(), ctx->med_hi.as<uint32_t>(),
+                                                     ctx->passed.as<uint8_t>(), st);
+        HIP_TRY(hipGetLastError());
+        STAGE_END(ST_MEDIAN);
+
+        // 8. tallies
+        STAGE_BEGIN(ST_TALLY);
+        k_tally_reduce<<<blocks_for((int64_t)g.L * 4), kBlock, 0, s>>>(
+            ctx->tally_part.as<uint32_t>(), g.nchunks, g.L * 4, ctx->tally.as<unsigned long long>());
+        HIP_TRY(hipGetLastError());
+        STAGE_END(ST_TALLY);
+    } else {
+        HIP_TRY(hipMemsetAsync(ctx->tally.p, 0, (size_t)g.L * 32, s));
+    }
+
+    // 9. tallies over ranks
+    if (ctx->comm) {
+        STAGE_BEGIN(ST_COMM);
+        ncclResult_t r = ncclAllReduce(ctx->tally.p, ctx->tally.p, (size_t)g.L * 4, ncclUint64, ncclSum, ctx->comm, s);
+        if (r != ncclSuccess) return set_err(MGP_E_COMM, std::string("ncclAllReduce: ") + ncclGetErrorString(r));
+        STAGE_END(ST_COMM);
+    }
+    HIP_TRY(hipMemcpyAsync(&ctx->host_stats, st, sizeof(DevStats), hipMemcpyDeviceToHost, s));
+    ctx->ran = true;
+    ctx->runs++;
+    ctx->last_status = MGP_OK;
+    return MGP_OK;
+}
+
+int mgp_sync(mgp_ctx* ctx) {
+    if (!ctx) return set_err(MGP_E_INVALID, "null ctx");
+    if (!ctx->ran) return set_err(MGP_E_STATE, "no run to wait for");
+    HIP_TRY(hipSetDevice(ctx->dev));
+    HIP_TRY(hipStreamSynchronize(ctx->s_comp));
+    const uint32_t e = ctx->host_stats.err;
+    if (e & ERR_UNSORTED) return set_err(MGP_E_UNSORTED, "records are not in coordinate order");
+    if (e & ERR_BADBC) return set_err(MGP_E_INVALID, "barcode index >= n_cells");
+    if (e & ERR_OVERFLOW) return set_err(MGP_E_INVALID, "inconsistent grouping (unsorted input?)");
+    if (e & ERR_BADREAD)
+        return set_err(MGP_E_BADREAD, "a kept read has no SEQ or QUAL (pysam would return None)");
+    if (e & ERR_SPAN) return set_err(MGP_E_SPAN, "a read's CIGAR reach exceeds the declared span");
+    return MGP_OK;
+}
+
+int mgp_fetch(mgp_ctx* ctx, mgp_result* out) {
+    if (!ctx || !out) return set_err(MGP_E_INVALID, "null ctx/out");
+    MGP_TRY(mgp_sync(ctx));
+    const Geom& g = ctx->g;
+    const size_t nc = (size_t)g.nc, L = (size_t)g.L;
+    auto d2h = [&](void* dst, const DevBuf& src, size_t bytes) -> int {
+        if (dst && bytes) HIP_TRY(hipMemcpy(dst, src.p, bytes, hipMemcpyDeviceToHost));
+        return MGP_OK;
+    };
+    MGP_TRY(d2h(out->counts, ctx->counts, nc * L * 32));
+    MGP_TRY(d2h(out->tn5, ctx->tn5, nc * L * 8));
+    MGP_TRY(d2h(out->depth, ctx->depth, nc * L * 4));
+    MGP_TRY(d2h(out->n_reads, ctx->n_reads, nc * 4));
+    MGP_TRY(d2h(out->any_paired, ctx->any_paired, nc));
+    MGP_TRY(d2h(out->passed, ctx->passed, nc));
+    MGP_TRY(d2h(out->covered, ctx->covered, nc * 4));
+    MGP_TRY(d2h(out->depth_sum, ctx->dsum, nc * 8));
+    MGP_TRY(d2h(out->depth_max, ctx->dmax, nc * 4));
+    MGP_TRY(d2h(out->median_lo, ctx->med_lo, nc * 4));
+    MGP_TRY(d2h(out->median_hi, ctx->med_hi, nc * 4));
+    MGP_TRY(d2h(out->first_read, ctx->first_read, nc * 4));
+    MGP_TRY(d2h(out->ref_tally, ctx->tally, L * 4 * 8));
+    if (out->stats) {
+        const DevStats& h = ctx->host_stats;
+        mgp_stats* o = out->stats;
+        o->total_reads = ctx->n;
+        o->filtered_reads = (int64_t)h.filtered;
+        o->n_barcodes = (int64_t)h.n_barcodes;
+        o->duplicate_reads_with_length = (int64_t)h.dup_len;
+        o->duplicate_reads_position_only = (int64_t)h.dup_pos;
+        o->cells_passed = (int64_t)h.cells_passed;
+        o->max_span = (int32_t)h.max_span;
+        o->error_bits = (int32_t)h.err;
+    }
+    return MGP_OK;
+}
+
+int mgp_finish(mgp_ctx* ctx, mgp_result* out) {
+    MGP_TRY(mgp_run(ctx));
+    return mgp_fetch(ctx, out);
+}
+
+int mgp_kernel_times(mgp_ctx* ctx, int last_runs, float* ms, int max_n, int* n_out, char* names, int names_len) {
+    if (!ctx) return set_err(MGP_E_INVALID, "null ctx");
+    if (!ctx->ran || ctx->runs == 0) return set_err(MGP_E_STATE, "no run");
+    if (last_runs < 1) last_runs = 1;
+    if (last_runs > mgp_ctx::kRing) return set_err(MGP_E_INVALID, "last_runs > 64");
+    if (last_runs > ctx->runs) last_runs = (int)ctx->runs;
+    HIP_TRY(hipSetDevice(ctx->dev));
+    HIP_TRY(hipStreamSynchronize(ctx->s_comp));
+    int k = 0;
+    for (int st = 0; st < ST_N && k < max_n; ++st, ++k) {
+        double acc = 0.0;
+        for (int r = 0; r < last_runs; ++r) {
+            const int slot = (int)((ctx->runs - 1 - r) % mgp_ctx::kRing);
+            float t = 0.f;
+            if (ctx->stage_ran[slot][st]) HIP_TRY(hipEventElapsedTime(&t, ctx->ev[slot][st][0], ctx->ev[slot][st][1]));
+            acc += t;
+        }
+        if (ms) ms[k] = (float)(acc / last_runs);
+    }
+    if (n_out) *n_out = k;
+    if (names && names_len > 0) {
+        std::strncpy(names, kStageNames, (size_t)names_len - 1);
+        names[names_len - 1] = 0;
+    }
+    return MGP_OK;
+}
+
+int mgp_comm_unique_id(uint8_t* out128) {
+    if (!out128) return set_err(MGP_E_INVALID, "null out");
+    static_assert(sizeof(ncclUniqueId) == 128, "ncclUniqueId size");
+    ncclUniqueId id;
+    ncclResult_t r = ncclGetUniqueId(&id);
+    if (r != ncclSuccess) return set_err(MGP_E_COMM, std::string("ncclGetUniqueId: ") + ncclGetErrorString(r));
+    std::memcpy(out128, &id, 128);
+    return MGP_OK;
+}
+
+int mgp_comm_init(mgp_ctx* ctx, const uint8_t* uid128, int nranks, int rank) {
+    if (!ctx || !uid128 || nranks < 1 || rank < 0 || rank >= nranks) return set_err(MGP_E_INVALID, "bad comm args");
+    HIP_TRY(hipSetDevice(ctx->dev));
+    ncclUniqueId id;
+    std::memcpy(&id, uid128, 128);
+    if (ctx->comm) ncclCommDestroy(ctx->comm);
+    ctx->comm = nullptr;
+    ncclResult_t r = ncclCommInitRank(&ctx->comm, nranks, id, rank);
+    if (r != ncclSuccess) {
+        ctx->comm = nullptr;
+        return set_err(MGP_E_COMM, std::string("ncclCommInitRank: ") + ncclGetErrorString(r));
+    }
+    ctx->nranks = nranks;
+    return MGP_OK;
+}
+
+int mgp_download_inputs(mgp_ctx* ctx, int32_t* start, int32_t* bc, int32_t* tlen, uint16_t* flag, uint8_t* mapq,
+                        uint32_t* span, uint64_t* rec_off, uint8_t* payload) {
+    if (!ctx) return set_err(MGP_E_INVALID, "null ctx");
+    HIP_TRY(hipSetDevice(ctx->dev));
+    HIP_TRY(hipStreamSynchronize(ctx->s_copy));
+    HIP_TRY(hipStreamSynchronize(ctx->s_comp));
+    const size_t n = (size_t)ctx->n;
+    if (!n) return MGP_OK;
+    if (start) HIP_TRY(hipMemcpy(start, ctx->start.p, n * 4, hipMemcpyDeviceToHost));
+    if (bc) HIP_TRY(hipMemcpy(bc, ctx->bc.p, n * 4, hipMemcpyDeviceToHost));
+    if (tlen) HIP_TRY(hipMemcpy(tlen, ctx->tlen.p, n * 4, hipMemcpyDeviceToHost));
+    if (flag) HIP_TRY(hipMemcpy(flag, ctx->flag.p, n * 2, hipMemcpyDeviceToHost));
+    if (mapq) HIP_TRY(hipMemcpy(mapq, ctx->mapq.p, n, hipMemcpyDeviceToHost));
+    if (span) HIP_TRY(hipMemcpy(span, ctx->span.p, n * 4, hipMemcpyDeviceToHost));
+    if (rec_off) HIP_TRY(hipMemcpy(rec_off, ctx->roff.p, n * 8, hipMemcpyDeviceToHost));
+    if (payload && ctx->pay) HIP_TRY(hipMemcpy(payload, ctx->payload.p, (size_t)ctx->pay, hipMemcpyDeviceToHost));
+    return MGP_OK;
+}
+
+// implemented in mgp_synth.hip
+int mgp_synth_fill(void* stream, uint64_t seed, int64_t n, int read_len, int n_cells, int mito_len,
+                   const uint32_t* d_cdf, const uint8_t* d_ref, int32_t* start, int32_t* bc, int32_t* tlen,
+                   uint16_t* flag, uint8_t* mapq, uint32_t* span, uint64_t* roff, uint8_t* payload,
+                   int64_t* payload_bytes, int phase);
+
+int mgp_synth_generate(mgp_ctx* ctx, const mgp_synth_params* p) {
+    if (!ctx || !p || !p->cell_cdf || !p->ref_codes) return set_err(MGP_E_INVALID, "null synth args");
+    if (p->n_cells != ctx->cfg.n_cells) return set_err(MGP_E_INVALID, "synth n_cells != context n_cells");
+    if (p->n_reads < 0 || p->n_reads > (int64_t)0xFFFFFFFEll || p->read_len < 12 || p->read_len > 4096)
+        return set_err(MGP_E_INVALID, "synth sizes out of range");
+    if (ctx->cfg.mito_len < p->read_len) return set_err(MGP_E_INVALID, "mito_len < read_len");
+    HIP_TRY(hipSetDevice(ctx->dev));
+    HIP_TRY(hipStreamSynchronize(ctx->s_comp));
+    HIP_TRY(hipStreamSynchronize(ctx->s_copy));
+    ctx->n = 0;
+    ctx->pay = 0;
+    const int64_t n = p->n_reads;
+    const int L = ctx->cfg.mito_len;
+    const int nc = p->n_cells;
+    // record size is at most 16 + 4*3 + len + (len+1)/2 rounded to 8
+    const int64_t max_rec = ((16 + 12 + p->read_len + (p->read_len + 1) / 2) + 7) & ~7;
+    MGP_TRY(ensure_inputs(ctx, std::max<int64_t>(n, 1), n * max_rec, false));
+    DevBuf cdf, ref;
+    MGP_TRY(cdf.ensure((size_t)std::max(nc, 1) * 4));
+    MGP_TRY(ref.ensure((size_t)L));
+    hipStream_t s = ctx->s_copy;
+    if (nc) HIP_TRY(hipMemcpyAsync(cdf.p, p->cell_cdf, (size_t)nc * 4, hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemcpyAsync(ref.p, p->ref_codes, (size_t)L, hipMemcpyHostToDevice, s));
+    int64_t pay = 0;
+    int r = mgp_synth_fill(s, p->seed, n, p->read_len, nc, L, cdf.as<uint32_t>(), ref.as<uint8_t>(),
+                           ctx->start.as<int32_t>(), ctx->bc.as<int32_t>(), ctx->tlen.as<int32_t>(),
+                           ctx->flag.as<uint16_t>(), ctx->mapq.as<uint8_t>(), ctx->span.as<uint32_t>(),
+                           ctx->roff.as<uint64_t>(), ctx->payload.as<uint8_t>(), &pay, 0);
+    if (r != MGP_OK) {
+        cdf.release();
+        ref.release();
+        return r;
+    }
+    HIP_TRY(hipStreamSynchronize(s));
+    cdf.release();
+    ref.release();
+    HIP_TRY(hipEventRecord(ctx->ev_copy, s));
+    ctx->n = n;
+    ctx->pay = pay;
+    ctx->ran = false;
+    return MGP_OK;
+}
+
+}  // extern "C"

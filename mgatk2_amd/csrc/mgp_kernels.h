@@ -1,0 +1,98 @@
+// mgp_kernels.h — device-side helpers shared by the engine kernels (gfx950, wave64).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace mgp {
+
+constexpr int kWave = 64;        // CDNA wavefront width (never 32)
+constexpr int kBlock = 256;      // 4 waves per workgroup
+
+// error bits accumulated in DevStats::err during a run
+constexpr uint32_t ERR_UNSORTED = 1u;   // start[i] < start[i-1]
+constexpr uint32_t ERR_BADREAD = 2u;    // kept read without SEQ/QUAL
+constexpr uint32_t ERR_SPAN = 4u;       // CIGAR reach larger than declared span
+constexpr uint32_t ERR_BADBC = 8u;      // bc >= n_cells
+constexpr uint32_t ERR_OVERFLOW = 16u;  // scatter destination outside its cell segment
+
+// Counters written by the kernels of one run (zeroed at run start).
+struct DevStats {
+    unsigned long long dup_len;        // duplicate_reads_with_length
+    unsigned long long dup_pos;        // duplicate_reads_position_only
+    unsigned long long filtered;       // kept reads (after dedup)
+    unsigned long long n_barcodes;     // cells with >= 1 kept read
+    unsigned long long cells_passed;   // cells producing a result
+    unsigned long long valid;          // reads passing flag + barcode filters
+    unsigned int max_span;             // max declared span over valid reads
+    unsigned int err;                  // ERR_* bits
+};
+
+// Geometry of the cell-major grouping and the position windows.
+struct Geom {
+    int L;        // mito_len
+    int G;        // start-bin width (positions per bin)
+    int nb_reg;   // ceil(L / G) regular bins; bin nb_reg holds starts >= L
+    int nbins;    // nb_reg + 1
+    int W;        // window width (positions), multiple of G
+    int Wp;       // LDS plane pitch (odd => conflict-free plane offsets)
+    int nwin;     // ceil(L / W)
+    int nc;       // cells
+    int cpb;      // cells per pileup workgroup
+    int nchunks;  // ceil(nc / cpb)
+};
+
+__device__ __forceinline__ int bin_of(int s, const Geom& g) {
+    if (s < 0) return 0;
+    if (s >= g.L) return g.nb_reg;
+    return s / g.G;
+}
+
+// start-bin window edges of pileup window k, given the reach R (multiple of G)
+__device__ __forceinline__ int win_lo_bin(int k, int R, const Geom& g) {
+    long long lo = (long long)k * g.W - R;
+    return lo <= 0 ? 0 : (int)(lo / g.G);
+}
+__device__ __forceinline__ int win_hi_bin(int k, const Geom& g) {
+    long long hi = (long long)(k + 1) * g.W / g.G;
+    return hi > g.nb_reg ? g.nb_reg : (int)hi;
+}
+
+__device__ __forceinline__ unsigned long long lanemask_lt() {
+    const unsigned lane = threadIdx.x & (kWave - 1);
+    return lane == 0 ? 0ull : (~0ull >> (64 - lane));
+}
+
+template <typename T>
+__device__ __forceinline__ T wave_sum(T v) {
+    for (int o = kWave / 2; o > 0; o >>= 1) v += __shfl_xor(v, o, kWave);
+    return v;
+}
+template <typename T>
+__device__ __forceinline__ T wave_max(T v) {
+    for (int o = kWave / 2; o > 0; o >>= 1) {
+        T w = __shfl_xor(v, o, kWave);
+        v = w > v ? w : v;
+    }
+    return v;
+}
+template <typename T>
+__device__ __forceinline__ T wave_min(T v) {
+    for (int o = kWave / 2; o > 0; o >>= 1) {
+        T w = __shfl_xor(v, o, kWave);
+        v = w < v ? w : v;
+    }
+    return v;
+}
+
+// splitmix64 finaliser + counter-based stream hash (synthetic generator; the
+// host mirror in mgatk2_amd/synth.py computes the same values with numpy uint64).
+__host__ __device__ __forceinline__ uint64_t mix64(uint64_t z) {
+    z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
+    z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
+    return z ^ (z >> 31);
+}
+__host__ __device__ __forceinline__ uint64_t shash(uint64_t seed, uint64_t i, uint64_t k) {
+    return mix64(seed * 0x9E3779B97F4A7C15ull + i * 0xD1B54A32D192ED03ull + k * 0x8CB92BA72F3D8DD7ull);
+}
+
+}  // namespace mgp

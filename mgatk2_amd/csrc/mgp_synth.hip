@@ -1,0 +1,297 @@
+// mgp_synth.hip — device-side synthetic chrM workload, used by
+// bench.py so that 200M-read inputs are created directly in HBM. The generator is
+// counter-based (every field is a pure function of (seed, read index, field id)),
+// so mgatk2_amd/synth.py reproduces it bit for bit on the host with numpy; the
+// tests check that equality. Nothing here is on the timed path.
+#include <hip/hip_runtime.h>
+
+#include <string>
+#include <vector>
+
+#include "../../include/mgpileup.h"
+#include "mgp_kernels.h"
+
+using namespace mgp;
+
+namespace {
+
+// Integer thresholds on a 24-bit uniform (x * 2^24, floored). Mirrored in synth.py.
+constexpr uint32_t DUP_FULL = 2516582;   // 0.15 : copy (bc, start, strand, |tlen|) of previous read
+constexpr uint32_t DUP_PART = 3019898;   // 0.18 : copy (bc, start, strand), fresh tlen
+// CAT_NONWL = 503316 (0.03, non-whitelisted barcode) and CAT_NOCB both map to bc = -1
+constexpr uint32_t CAT_NOCB = 671088;    // 0.04  (+0.01) no CB tag
+constexpr uint32_t CAT_SEC = 754974;     // 0.045 (+0.005) secondary
+constexpr uint32_t CAT_SUPP = 838860;    // 0.05  (+0.005) supplementary
+constexpr uint32_t CAT_UNMAP = 872415;   // 0.052 (+0.002) unmapped (placed)
+constexpr uint32_t MAPQ0 = 838860;       // 0.05  MAPQ 0, else 60
+constexpr uint32_t CIG_M = 15099494;     // 0.90  50M
+constexpr uint32_t CIG_S = 15938355;     // 0.95  kS(L-k)M
+constexpr uint32_t CIG_I = 16441671;     // 0.98  aM bI cM ; else aM bD cM
+constexpr uint32_t QUAL37 = 13421772;    // 0.80
+constexpr uint32_t BASE_N = 16777;       // 0.001
+constexpr uint32_t BASE_SUB = 184549;    // 0.011 (+0.01)
+
+enum { T_ORIG = 0, T_FULL = 1, T_PART = 2 };
+enum { C_M = 0, C_S = 1, C_I = 2, C_D = 3 };
+
+__device__ __forceinline__ uint32_t u24(uint64_t h) { return (uint32_t)(h >> 40); }
+
+__device__ __forceinline__ int read_type(uint64_t seed, int64_t i) {
+    if (i == 0) return T_ORIG;
+    const uint32_t t = u24(shash(seed, i, 1));
+    return t < DUP_FULL ? T_FULL : (t < DUP_PART ? T_PART : T_ORIG);
+}
+
+struct Cig {
+    int cls, a, b, n;
+};
+
+__device__ __forceinline__ Cig cig_of(uint64_t seed, int64_t i) {
+    const uint32_t x = u24(shash(seed, i, 8));
+    const uint64_t p = shash(seed, i, 9);
+    Cig c;
+    c.a = 0;
+    c.b = 0;
+    if (x < CIG_M) {
+        c.cls = C_M;
+        c.n = 1;
+    } else if (x < CIG_S) {
+        c.cls = C_S;
+        c.a = 1 + (int)(p % 10);
+        c.n = 2;
+    } else if (x < CIG_I) {
+        c.cls = C_I;
+        c.a = 10 + (int)(p % 31);
+        c.b = 1 + (int)((p >> 16) % 3);
+        c.n = 3;
+    } else {
+        c.cls = C_D;
+        c.a = 10 + (int)(p % 31);
+        c.b = 1 + (int)((p >> 16) % 3);
+        c.n = 3;
+    }
+    return c;
+}
+
+__device__ __forceinline__ uint64_t rec_size(int ncig, int rl) {
+    return (uint64_t)((16 + 4 * ncig + rl + (rl + 1) / 2 + 7) & ~7);
+}
+
+__global__ void k_synth_sizes(uint64_t seed, int64_t n, int rl, uint64_t* __restrict__ sz) {
+    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    sz[i] = rec_size(cig_of(seed, i).n, rl);
+}
+
+// ---- generic exclusive scan of u64 (3-phase, 4096 items per block) ----------
+constexpr int kItems = 16;
+
+__global__ void __launch_bounds__(kBlock) k_scan_block_sums(const uint64_t* __restrict__ a, int64_t n,
+                                                            uint64_t* __restrict__ bsum) {
+    const int64_t b0 = (int64_t)blockIdx.x * kBlock * kItems;
+    uint64_t acc = 0;
+    for (int k = 0; k < kItems; ++k) {
+        const int64_t i = b0 + (int64_t)k * kBlock + threadIdx.x;
+        if (i < n) acc += a[i];
+    }
+    acc = wave_sum(acc);
+    __shared__ uint64_t ws[kBlock / kWave];
+    if ((threadIdx.x & 63) == 0) ws[threadIdx.x >> 6] = acc;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint64_t t = 0;
+        for (int w = 0; w < kBlock / kWave; ++w) t += ws[w];
+        bsum[blockIdx.x] = t;
+    }
+}
+
+// exclusive scan of one block's items in place, adding offs[blockIdx.x]
+__global__ void __launch_bounds__(kBlock) k_scan_block_apply(uint64_t* __restrict__ a, int64_t n,
+                                                             const uint64_t* __restrict__ offs) {
+    const int64_t b0 = (int64_t)blockIdx.x * kBlock * kItems;
+    // thread t owns items b0 + t*kItems .. +kItems (contiguous)
+    uint64_t v[kItems];
+    uint64_t sum = 0;
+    const int64_t i0 = b0 + (int64_t)threadIdx.x * kItems;
+    for (int k = 0; k < kItems; ++k) {
+        const int64_t i = i0 + k;
+        v[k] = i < n ? a[i] : 0;
+        sum += v[k];
+    }
+    // block exclusive scan of per-thread sums
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    uint64_t x = sum;
+    for (int o = 1; o < 64; o <<= 1) {
+        uint64_t y = __shfl_up(x, o, 64);
+        if (lane >= o) x += y;
+    }
+    __shared__ uint64_t ws[kBlock / kWave];
+    if (lane == 63) ws[wid] = x;
+    __syncthreads();
+    uint64_t woff = 0;
+    for (int w = 0; w < wid; ++w) woff += ws[w];
+    uint64_t run = offs[blockIdx.x] + woff + x - sum;
+    for (int k = 0; k < kItems; ++k) {
+        const int64_t i = i0 + k;
+        if (i < n) a[i] = run;
+        run += v[k];
+    }
+}
+
+int scan_exclusive_u64(uint64_t* a, int64_t n, hipStream_t s, uint64_t* total) {
+    if (n <= 0) {
+        *total = 0;
+        return MGP_OK;
+    }
+    const int64_t per = (int64_t)kBlock * kItems;
+    const int64_t nb = (n + per - 1) / per;
+    uint64_t* bs = nullptr;
+    if (hipMalloc(&bs, (size_t)(nb + 1) * 8) != hipSuccess) return MGP_E_OOM;
+    k_scan_block_sums<<<(unsigned)nb, kBlock, 0, s>>>(a, n, bs);
+    uint64_t btot = 0;
+    int r = MGP_OK;
+    if (nb > 1) {
+        r = scan_exclusive_u64(bs, nb, s, &btot);
+    } else {
+        uint64_t t = 0;
+        (void)hipMemcpyAsync(&t, bs, 8, hipMemcpyDeviceToHost, s);
+        (void)hipStreamSynchronize(s);
+        btot = t;
+        (void)hipMemsetAsync(bs, 0, 8, s);
+    }
+    if (r == MGP_OK) {
+        k_scan_block_apply<<<(unsigned)nb, kBlock, 0, s>>>(a, n, bs);
+        if (hipStreamSynchronize(s) != hipSuccess) r = MGP_E_HIP;
+    }
+    (void)hipFree(bs);
+    *total = btot;
+    return r;
+}
+
+__device__ __forceinline__ int cell_of(uint64_t h, const uint32_t* cdf, int nc) {
+    const uint32_t u = (uint32_t)(h & 0xFFFFFFFFull);
+    int lo = 0, hi = nc;  // first c with u < cdf[c]
+    while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (u < cdf[mid]) hi = mid;
+        else lo = mid + 1;
+    }
+    return lo < nc ? lo : nc - 1;
+}
+
+__device__ __forceinline__ uint32_t code_idx(uint32_t c) { return c == 1 ? 0 : c == 2 ? 1 : c == 4 ? 2 : 3; }
+
+__global__ void k_synth_fill(uint64_t seed, int64_t n, int rl, int nc, int L, const uint32_t* __restrict__ cdf,
+                             const uint8_t* __restrict__ ref, int32_t* __restrict__ start, int32_t* __restrict__ bc,
+                             int32_t* __restrict__ tlen, uint16_t* __restrict__ flag, uint8_t* __restrict__ mapq,
+                             uint32_t* __restrict__ span, const uint64_t* __restrict__ roff,
+                             uint8_t* __restrict__ payload) {
+    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint64_t spanpos = (uint64_t)(L - rl + 1);
+    int64_t A = i;
+    while (read_type(seed, A) != T_ORIG) --A;
+    int64_t B = i;
+    while (read_type(seed, B) == T_FULL) --B;
+    const int s0 = (int)(((uint64_t)A * spanpos + (((uint64_t)u24(shash(seed, A, 2)) * spanpos) >> 24)) / (uint64_t)n);
+    const int cell = nc > 0 ? cell_of(shash(seed, A, 3), cdf, nc) : -1;
+    const int strand = (int)(shash(seed, A, 4) >> 63);
+    const int tabs = 60 + (int)(shash(seed, B, 5) % 541);
+
+    const uint32_t cat = u24(shash(seed, i, 6));
+    int b = cell;
+    uint16_t f = MGP_FLAG_PAIRED | (strand ? MGP_FLAG_REVERSE : 0);
+    if (cat < CAT_NOCB) b = -1;
+    else if (cat < CAT_SEC) f |= MGP_FLAG_SECONDARY;
+    else if (cat < CAT_SUPP) f |= MGP_FLAG_SUPPLEMENTARY;
+    else if (cat < CAT_UNMAP) f |= MGP_FLAG_UNMAPPED;
+    const uint8_t mq = u24(shash(seed, i, 7)) < MAPQ0 ? 0 : 60;
+    const Cig cg = cig_of(seed, i);
+
+    start[i] = s0;
+    bc[i] = b;
+    tlen[i] = strand ? -tabs : tabs;
+    flag[i] = f;
+    mapq[i] = mq;
+    span[i] = (uint32_t)(cg.cls == C_D ? rl + cg.b : rl);
+
+    uint8_t* rec = payload + roff[i];
+    *reinterpret_cast<int32_t*>(rec) = s0;
+    *reinterpret_cast<uint32_t*>(rec + 4) = (uint32_t)rl;
+    *reinterpret_cast<uint16_t*>(rec + 8) = (uint16_t)cg.n;
+    *reinterpret_cast<uint16_t*>(rec + 10) = f;
+    *reinterpret_cast<uint32_t*>(rec + 12) = 0;
+    uint32_t* cig = reinterpret_cast<uint32_t*>(rec + 16);
+    if (cg.cls == C_M) {
+        cig[0] = ((uint32_t)rl << 4) | 0;
+    } else if (cg.cls == C_S) {
+        cig[0] = ((uint32_t)cg.a << 4) | 4;
+        cig[1] = ((uint32_t)(rl - cg.a) << 4) | 0;
+    } else if (cg.cls == C_I) {
+        cig[0] = ((uint32_t)cg.a << 4) | 0;
+        cig[1] = ((uint32_t)cg.b << 4) | 1;
+        cig[2] = ((uint32_t)(rl - cg.a - cg.b) << 4) | 0;
+    } else {
+        cig[0] = ((uint32_t)cg.a << 4) | 0;
+        cig[1] = ((uint32_t)cg.b << 4) | 2;
+        cig[2] = ((uint32_t)(rl - cg.a) << 4) | 0;
+    }
+    uint8_t* qual = rec + 16 + 4 * cg.n;
+    uint8_t* seq = qual + rl;
+    const uint8_t kCodes[4] = {1, 2, 4, 8};
+    uint8_t hi_nib = 0;
+    for (int q = 0; q < rl; ++q) {
+        const uint64_t hq = shash(seed, i, 1000 + (uint64_t)q);
+        qual[q] = u24(hq) < QUAL37 ? 37 : (uint8_t)(2 + hq % 35);
+        int d;
+        bool rnd = false;
+        if (cg.cls == C_M) d = q;
+        else if (cg.cls == C_S) { rnd = q < cg.a; d = q - cg.a; }
+        else if (cg.cls == C_I) {
+            if (q < cg.a) d = q;
+            else if (q < cg.a + cg.b) { rnd = true; d = 0; }
+            else d = q - cg.b;
+        } else d = q < cg.a ? q : q + cg.b;
+        const uint64_t hs = shash(seed, i, 100000 + (uint64_t)q);
+        uint8_t code;
+        if (rnd) {
+            code = kCodes[hs & 3];
+        } else {
+            const uint8_t rc = ref[(uint32_t)(s0 + d) % (uint32_t)L];
+            const uint32_t m = u24(hs);
+            if (m < BASE_N) code = 15;
+            else if (m < BASE_SUB) code = kCodes[(code_idx(rc) + 1 + (uint32_t)((hs & 255) % 3)) & 3];
+            else code = rc;
+        }
+        if ((q & 1) == 0) hi_nib = code;
+        else seq[q >> 1] = (uint8_t)((hi_nib << 4) | code);
+    }
+    if (rl & 1) seq[rl >> 1] = (uint8_t)(hi_nib << 4);
+}
+
+}  // namespace
+
+extern "C" int mgp_synth_fill(void* stream, uint64_t seed, int64_t n, int read_len, int n_cells, int mito_len,
+                              const uint32_t* d_cdf, const uint8_t* d_ref, int32_t* start, int32_t* bc,
+                              int32_t* tlen, uint16_t* flag, uint8_t* mapq, uint32_t* span, uint64_t* roff,
+                              uint8_t* payload, int64_t* payload_bytes, int /*phase*/) {
+    hipStream_t s = (hipStream_t)stream;
+    if (read_len < 48) return MGP_E_INVALID;
+    if (n == 0) {
+        *payload_bytes = 0;
+        return MGP_OK;
+    }
+    const unsigned nb = (unsigned)((n + kBlock - 1) / kBlock);
+    k_synth_sizes<<<nb, kBlock, 0, s>>>(seed, n, read_len, roff);
+    if (hipGetLastError() != hipSuccess) return MGP_E_HIP;
+    uint64_t total = 0;
+    int r = scan_exclusive_u64(roff, n, s, &total);
+    if (r != MGP_OK) return r;
+    if (hipMemsetAsync(payload, 0, (size_t)total, s) != hipSuccess) return MGP_E_HIP;
+    k_synth_fill<<<nb, kBlock, 0, s>>>(seed, n, read_len, n_cells, mito_len, d_cdf, d_ref, start, bc, tlen, flag,
+                                       mapq, span, roff, payload);
+    if (hipGetLastError() != hipSuccess) return MGP_E_HIP;
+    if (hipStreamSynchronize(s) != hipSuccess) return MGP_E_HIP;
+    *payload_bytes = (int64_t)total;
+    return MGP_OK;
+}

@@ -1,0 +1,392 @@
+"""ctypes binding of libmgpileup.so (include/mgpileup.h).
+
+This is the only way the package reaches the GPU: there is no CPU fallback.
+If the library is missing or no HIP device is present, :class:`Engine` raises.
+"""
+
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass
+from pathlib import Path
+
+import numpy as np
+
+from .exceptions import BAMFormatError, BAMReadError, InvalidInputError, ProcessingError
+from .synth import ReadSoA
+
+LIB_PATH = Path(__file__).resolve().parent / "_lib" / "libmgpileup.so"
+
+MGP_OK = 0
+MGP_E_INVALID = -1
+MGP_E_HIP = -2
+MGP_E_OOM = -3
+MGP_E_UNSORTED = -4
+MGP_E_BADREAD = -5
+MGP_E_SPAN = -6
+MGP_E_STATE = -7
+MGP_E_COMM = -8
+
+DEDUP_MODES = {"none": 0, "alignment_start": 1, "alignment_and_fragment_length": 2}
+
+# names of every entry point declared in include/mgpileup.h
+ABI_SYMBOLS = (
+    "mgp_abi_version", "mgp_last_error", "mgp_device_count", "mgp_open", "mgp_close", "mgp_host_alloc",
+    "mgp_host_free", "mgp_push_batch", "mgp_reset", "mgp_resident", "mgp_run", "mgp_sync", "mgp_fetch",
+    "mgp_finish", "mgp_kernel_times", "mgp_comm_unique_id", "mgp_comm_init", "mgp_synth_generate",
+    "mgp_download_inputs",
+)
+
+
+class mgp_config(C.Structure):
+    _fields_ = [
+        ("min_baseq", C.c_int32),
+        ("min_mapq", C.c_int32),
+        ("min_dist_from_end", C.c_int32),
+        ("dedup_mode", C.c_int32),
+        ("max_strand_bias", C.c_double),
+        ("min_reads", C.c_int32),
+        ("n_cells", C.c_int32),
+        ("mito_len", C.c_int32),
+        ("flags", C.c_int32),
+        ("reserve_reads", C.c_int64),
+        ("reserve_payload", C.c_int64),
+    ]
+
+
+class mgp_batch(C.Structure):
+    _fields_ = [
+        ("n_reads", C.c_int64),
+        ("start", C.c_void_p),
+        ("bc", C.c_void_p),
+        ("tlen", C.c_void_p),
+        ("flag", C.c_void_p),
+        ("mapq", C.c_void_p),
+        ("span", C.c_void_p),
+        ("rec_off", C.c_void_p),
+        ("payload", C.c_void_p),
+        ("payload_bytes", C.c_int64),
+    ]
+
+
+class mgp_stats(C.Structure):
+    _fields_ = [
+        ("total_reads", C.c_int64),
+        ("filtered_reads", C.c_int64),
+        ("n_barcodes", C.c_int64),
+        ("duplicate_reads_with_length", C.c_int64),
+        ("duplicate_reads_position_only", C.c_int64),
+        ("cells_passed", C.c_int64),
+        ("max_span", C.c_int32),
+        ("error_bits", C.c_int32),
+    ]
+
+    def as_dict(self) -> dict:
+        return {k: int(getattr(self, k)) for k, _ in self._fields_}
+
+
+class mgp_result(C.Structure):
+    _fields_ = [
+        ("counts", C.c_void_p),
+        ("tn5", C.c_void_p),
+        ("depth", C.c_void_p),
+        ("n_reads", C.c_void_p),
+        ("any_paired", C.c_void_p),
+        ("passed", C.c_void_p),
+        ("covered", C.c_void_p),
+        ("depth_sum", C.c_void_p),
+        ("depth_max", C.c_void_p),
+        ("median_lo", C.c_void_p),
+        ("median_hi", C.c_void_p),
+        ("first_read", C.c_void_p),
+        ("ref_tally", C.c_void_p),
+        ("stats", C.POINTER(mgp_stats)),
+    ]
+
+
+class mgp_synth_params(C.Structure):
+    _fields_ = [
+        ("seed", C.c_uint64),
+        ("n_reads", C.c_int64),
+        ("read_len", C.c_int32),
+        ("n_cells", C.c_int32),
+        ("cell_cdf", C.c_void_p),
+        ("ref_codes", C.c_void_p),
+    ]
+
+
+_lib = None
+
+
+def load_library(path: Path | None = None) -> C.CDLL:
+    """Load libmgpileup.so; raises if it is absent (no fallback)."""
+    global _lib
+    if _lib is not None and path is None:
+        return _lib
+    p = Path(path) if path else LIB_PATH
+    if not p.exists():
+        raise ProcessingError(
+            f"HIP engine library not found at {p}; build it with `python -m mgatk2_amd.build` "
+            "(hipcc --offload-arch=gfx950)"
+        )
+    lib = C.CDLL(str(p))
+    vp, i32, i64 = C.c_void_p, C.c_int32, C.c_int64
+    sig = {
+        "mgp_abi_version": ([], C.c_int),
+        "mgp_last_error": ([], C.c_char_p),
+        "mgp_device_count": ([C.POINTER(C.c_int)], C.c_int),
+        "mgp_open": ([C.POINTER(mgp_config), C.c_int, C.POINTER(vp)], C.c_int),
+        "mgp_close": ([vp], None),
+        "mgp_host_alloc": ([i64, C.POINTER(vp)], C.c_int),
+        "mgp_host_free": ([vp], C.c_int),
+        "mgp_push_batch": ([vp, C.POINTER(mgp_batch)], C.c_int),
+        "mgp_reset": ([vp], C.c_int),
+        "mgp_resident": ([vp, C.POINTER(i64), C.POINTER(i64)], C.c_int),
+        "mgp_run": ([vp], C.c_int),
+        "mgp_sync": ([vp], C.c_int),
+        "mgp_fetch": ([vp, C.POINTER(mgp_result)], C.c_int),
+        "mgp_finish": ([vp, C.POINTER(mgp_result)], C.c_int),
+        "mgp_kernel_times": (
+            [vp, C.c_int, C.POINTER(C.c_float), C.c_int, C.POINTER(C.c_int), C.c_char_p, C.c_int], C.c_int
+        ),
+        "mgp_comm_unique_id": ([C.c_char_p], C.c_int),
+        "mgp_comm_init": ([vp, C.c_char_p, C.c_int, C.c_int], C.c_int),
+        "mgp_synth_generate": ([vp, C.POINTER(mgp_synth_params)], C.c_int),
+        "mgp_download_inputs": ([vp] + [vp] * 8, C.c_int),
+    }
+    for name, (args, res) in sig.items():
+        fn = getattr(lib, name)
+        fn.argtypes = args
+        fn.restype = res
+    if lib.mgp_abi_version() != 1:
+        raise ProcessingError("libmgpileup ABI version mismatch")
+    if path is None:
+        _lib = lib
+    return lib
+
+
+def _raise(code: int, what: str):
+    lib = load_library()
+    msg = (lib.mgp_last_error() or b"").decode(errors="replace")
+    text = f"{what}: {msg} (code {code})"
+    if code == MGP_E_INVALID or code == MGP_E_SPAN:
+        raise InvalidInputError(text)
+    if code == MGP_E_UNSORTED:
+        raise BAMFormatError("<resident reads>", text)
+    if code == MGP_E_BADREAD:
+        raise BAMReadError("<resident reads>", text)
+    raise ProcessingError(text)
+
+
+def _ck(code: int, what: str):
+    if code != MGP_OK:
+        _raise(code, what)
+
+
+def _ptr(a: np.ndarray | None):
+    return None if a is None else a.ctypes.data_as(C.c_void_p)
+
+
+@dataclass
+class EngineConfig:
+    """POD restatement of the hot-path fields of PipelineConfig (config.py:77-114)."""
+
+    n_cells: int
+    min_baseq: int = 20
+    min_mapq: int = 30
+    min_distance_from_end: int = 5
+    dedup_mode: str | int = "alignment_and_fragment_length"
+    max_strand_bias: float = 1.0
+    min_reads: int = 1
+    mito_len: int = 16569
+    reserve_reads: int = 0
+    reserve_payload: int = 0
+
+    def to_c(self) -> mgp_config:
+        dm = DEDUP_MODES[self.dedup_mode] if isinstance(self.dedup_mode, str) else int(self.dedup_mode)
+        return mgp_config(
+            int(self.min_baseq), int(self.min_mapq), int(self.min_distance_from_end), dm,
+            float(self.max_strand_bias), int(self.min_reads), int(self.n_cells), int(self.mito_len), 0,
+            int(self.reserve_reads), int(self.reserve_payload),
+        )
+
+
+@dataclass
+class EngineResult:
+    """Host copy of mgp_result (cell-major arrays)."""
+
+    counts: np.ndarray | None  # [n_cells, L, 8] u32
+    tn5: np.ndarray | None  # [n_cells, L, 2] u32
+    depth: np.ndarray | None  # [n_cells, L] u32
+    n_reads: np.ndarray
+    any_paired: np.ndarray
+    passed: np.ndarray
+    covered: np.ndarray
+    depth_sum: np.ndarray
+    depth_max: np.ndarray
+    median_lo: np.ndarray
+    median_hi: np.ndarray
+    first_read: np.ndarray
+    ref_tally: np.ndarray  # [L, 4] u64
+    stats: dict
+
+    @staticmethod
+    def alloc(n_cells: int, L: int, dense: bool = True) -> EngineResult:
+        return EngineResult(
+            counts=np.zeros((n_cells, L, 8), np.uint32) if dense else None,
+            tn5=np.zeros((n_cells, L, 2), np.uint32) if dense else None,
+            depth=np.zeros((n_cells, L), np.uint32) if dense else None,
+            n_reads=np.zeros(n_cells, np.uint32),
+            any_paired=np.zeros(n_cells, np.uint8),
+            passed=np.zeros(n_cells, np.uint8),
+            covered=np.zeros(n_cells, np.uint32),
+            depth_sum=np.zeros(n_cells, np.uint64),
+            depth_max=np.zeros(n_cells, np.uint32),
+            median_lo=np.zeros(n_cells, np.uint32),
+            median_hi=np.zeros(n_cells, np.uint32),
+            first_read=np.zeros(n_cells, np.uint32),
+            ref_tally=np.zeros((L, 4), np.uint64),
+            stats={},
+        )
+
+    def to_c(self, stats: mgp_stats) -> mgp_result:
+        return mgp_result(
+            _ptr(self.counts), _ptr(self.tn5), _ptr(self.depth), _ptr(self.n_reads), _ptr(self.any_paired),
+            _ptr(self.passed), _ptr(self.covered), _ptr(self.depth_sum), _ptr(self.depth_max),
+            _ptr(self.median_lo), _ptr(self.median_hi), _ptr(self.first_read), _ptr(self.ref_tally),
+            C.pointer(stats),
+        )
+
+    def cell_order(self) -> np.ndarray:
+        """Cells with >= 1 kept read in first-seen BAM order (dict order of reads_by_barcode)."""
+        idx = np.flatnonzero(self.n_reads > 0)
+        return idx[np.argsort(self.first_read[idx], kind="stable")]
+
+
+def batch_struct(soa: ReadSoA) -> mgp_batch:
+    for name in ("start", "bc", "tlen", "flag", "mapq", "span", "rec_off", "payload"):
+        a = getattr(soa, name)
+        if not a.flags["C_CONTIGUOUS"]:
+            raise InvalidInputError(f"batch array {name} must be C-contiguous")
+    return mgp_batch(
+        soa.n, _ptr(soa.start), _ptr(soa.bc), _ptr(soa.tlen), _ptr(soa.flag), _ptr(soa.mapq), _ptr(soa.span),
+        _ptr(soa.rec_off), _ptr(soa.payload), int(soa.payload.shape[0]),
+    )
+
+
+class Engine:
+    """One device context (one GPU). Not thread-safe."""
+
+    def __init__(self, cfg: EngineConfig, device: int = 0):
+        self.lib = load_library()
+        self.cfg = cfg
+        self._c = cfg.to_c()
+        h = C.c_void_p()
+        _ck(self.lib.mgp_open(C.byref(self._c), int(device), C.byref(h)), "mgp_open")
+        self._h = h
+        self._keep: list = []  # keep host batches alive until the next sync
+
+    # -- lifecycle ---------------------------------------------------------
+    def close(self):
+        if getattr(self, "_h", None):
+            self.lib.mgp_close(self._h)
+            self._h = None
+        self._keep = []
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # -- data --------------------------------------------------------------
+    def push(self, soa: ReadSoA):
+        b = batch_struct(soa)
+        _ck(self.lib.mgp_push_batch(self._h, C.byref(b)), "mgp_push_batch")
+        self._keep.append(soa)
+
+    def reset(self):
+        _ck(self.lib.mgp_reset(self._h), "mgp_reset")
+        self._keep = []
+
+    def resident(self) -> tuple[int, int]:
+        n, p = C.c_int64(), C.c_int64()
+        _ck(self.lib.mgp_resident(self._h, C.byref(n), C.byref(p)), "mgp_resident")
+        return int(n.value), int(p.value)
+
+    def synth(self, seed: int, n_reads: int, cdf: np.ndarray, ref: np.ndarray, read_len: int = 50):
+        cdf = np.ascontiguousarray(cdf, np.uint32)
+        ref = np.ascontiguousarray(ref, np.uint8)
+        p = mgp_synth_params(int(seed), int(n_reads), int(read_len), int(self.cfg.n_cells), _ptr(cdf), _ptr(ref))
+        _ck(self.lib.mgp_synth_generate(self._h, C.byref(p)), "mgp_synth_generate")
+
+    def download_inputs(self) -> ReadSoA:
+        n, pay = self.resident()
+        soa = ReadSoA(
+            np.zeros(n, np.int32), np.zeros(n, np.int32), np.zeros(n, np.int32), np.zeros(n, np.uint16),
+            np.zeros(n, np.uint8), np.zeros(n, np.uint32), np.zeros(n, np.uint64), np.zeros(pay, np.uint8),
+        )
+        _ck(
+            self.lib.mgp_download_inputs(
+                self._h, _ptr(soa.start), _ptr(soa.bc), _ptr(soa.tlen), _ptr(soa.flag), _ptr(soa.mapq),
+                _ptr(soa.span), _ptr(soa.rec_off), _ptr(soa.payload),
+            ),
+            "mgp_download_inputs",
+        )
+        return soa
+
+    # -- compute -----------------------------------------------------------
+    def run(self):
+        _ck(self.lib.mgp_run(self._h), "mgp_run")
+
+    def sync(self):
+        code = self.lib.mgp_sync(self._h)
+        self._keep = []
+        _ck(code, "mgp_sync")
+
+    def fetch(self, dense: bool = True) -> EngineResult:
+        res = EngineResult.alloc(self.cfg.n_cells, self.cfg.mito_len, dense)
+        st = mgp_stats()
+        cres = res.to_c(st)
+        _ck(self.lib.mgp_fetch(self._h, C.byref(cres)), "mgp_fetch")
+        res.stats = st.as_dict()
+        return res
+
+    def finish(self, dense: bool = True) -> EngineResult:
+        self.run()
+        return self.fetch(dense)
+
+    def kernel_times(self, last_runs: int = 1) -> dict[str, float]:
+        """Per-stage device ms averaged over the last `last_runs` runs (HIP events)."""
+        ms = (C.c_float * 32)()
+        n = C.c_int()
+        names = C.create_string_buffer(512)
+        _ck(self.lib.mgp_kernel_times(self._h, int(last_runs), ms, 32, C.byref(n), names, 512), "mgp_kernel_times")
+        keys = names.value.decode().split(",")
+        return {k: float(ms[i]) for i, k in enumerate(keys[: n.value])}
+
+    # -- multi-GPU ---------------------------------------------------------
+    @staticmethod
+    def comm_unique_id() -> bytes:
+        lib = load_library()
+        buf = C.create_string_buffer(128)
+        _ck(lib.mgp_comm_unique_id(buf), "mgp_comm_unique_id")
+        return buf.raw
+
+    def comm_init(self, uid: bytes, nranks: int, rank: int):
+        if len(uid) != 128:
+            raise InvalidInputError("RCCL unique id must be 128 bytes")
+        _ck(self.lib.mgp_comm_init(self._h, C.c_char_p(uid), int(nranks), int(rank)), "mgp_comm_init")
+
+
+def device_count() -> int:
+    lib = load_library()
+    n = C.c_int()
+    code = lib.mgp_device_count(C.byref(n))
+    return int(n.value) if code == MGP_OK else 0

@@ -1,0 +1,463 @@
+"""Synthetic chrM workload and the SoA/record packer.
+
+The engine's input is the chrM records of a coordinate-sorted BAM, as SoA key
+arrays plus one packed payload record per read (layout in include/mgpileup.h).
+This module builds that input two ways:
+
+* :func:`synth_reads` — the seeded synthetic workload. It is counter-based:
+  every field is a pure function of ``(seed, read index, field id)`` through
+  :func:`shash`, so the device generator in ``csrc/mgp_synth.hip`` (used by
+  bench.py to create 200M-read inputs directly in HBM) produces the same bytes;
+  ``tests/test_gpu_parity.py`` checks that equality.
+* :func:`pack_reads` — packs arbitrary read records (dicts with pysam-like
+  fields) for hand-written known-answer cases.
+
+Reads are L=50 by default; starts are stratified-uniform over
+``[0, mito_len - L]`` and therefore sorted; ~15% full duplicates and ~3%
+position-only duplicates of the previous read; lognormal reads/cell; 3%
+non-whitelisted and 1% untagged barcodes; 0.5% secondary, 0.5% supplementary,
+0.2% unmapped; 5% MAPQ 0; CIGAR 90% ``50M`` / 5% ``kS(50-k)M`` / 3% with an
+insertion / 2% with a deletion; Q37 for 80% of bases; 1% substitutions, 0.1% N.
+"""
+
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+
+import numpy as np
+
+MITO_LEN = 16569
+
+# splitmix64 constants (csrc/mgp_kernels.h)
+_M1 = np.uint64(0xBF58476D1CE4E5B9)
+_M2 = np.uint64(0x94D049BB133111EB)
+_C_SEED = 0x9E3779B97F4A7C15
+_C_I = np.uint64(0xD1B54A32D192ED03)
+_C_K = 0x8CB92BA72F3D8DD7
+_MASK64 = (1 << 64) - 1
+
+# thresholds on a 24-bit uniform (csrc/mgp_synth.hip)
+DUP_FULL = 2516582
+DUP_PART = 3019898
+CAT_NOCB = 671088
+CAT_SEC = 754974
+CAT_SUPP = 838860
+CAT_UNMAP = 872415
+MAPQ0 = 838860
+CIG_M = 15099494
+CIG_S = 15938355
+CIG_I = 16441671
+QUAL37 = 13421772
+BASE_N = 16777
+BASE_SUB = 184549
+
+FLAG_PAIRED = 0x1
+FLAG_UNMAPPED = 0x4
+FLAG_REVERSE = 0x10
+FLAG_SECONDARY = 0x100
+FLAG_SUPPLEMENTARY = 0x800
+FLAG_NOSEQQUAL = 0x1000
+
+CODES = np.array([1, 2, 4, 8], dtype=np.uint8)  # BAM 4-bit A, C, G, T
+SEQ_NT16 = "=ACMGRSVTWYHKDBN"
+_NT16_IDX = {ch: i for i, ch in enumerate(SEQ_NT16)}
+
+
+def _mix64(z: np.ndarray) -> np.ndarray:
+    z = (z ^ (z >> np.uint64(30))) * _M1
+    z = (z ^ (z >> np.uint64(27))) * _M2
+    return z ^ (z >> np.uint64(31))
+
+
+def shash(seed: int, i, k) -> np.ndarray:
+    """Counter-based hash ``mix64(seed*C1 + i*C2 + k*C3)`` (mod 2^64), vectorised."""
+    i = np.asarray(i, dtype=np.uint64)
+    k = np.asarray(k, dtype=np.uint64)
+    base = np.uint64((seed * _C_SEED) & _MASK64)
+    with np.errstate(over="ignore"):
+        z = base + i * _C_I + k * np.uint64(_C_K)
+        return _mix64(z)
+
+
+def _u24(h: np.ndarray) -> np.ndarray:
+    return (h >> np.uint64(40)).astype(np.int64)
+
+
+def ref_codes(seed: int, mito_len: int = MITO_LEN) -> np.ndarray:
+    """Synthetic chrM reference as BAM 4-bit codes (uniform ACGT)."""
+    h = shash(seed ^ 0x5EED, np.arange(mito_len, dtype=np.uint64), 0)
+    return CODES[(h & np.uint64(3)).astype(np.int64)]
+
+
+def cell_cdf(seed: int, n_cells: int, sigma: float = 0.5) -> np.ndarray:
+    """Lognormal(sigma) reads-per-cell weights as cumulative u32 thresholds."""
+    if n_cells <= 0:
+        return np.zeros(0, dtype=np.uint32)
+    c = np.arange(n_cells, dtype=np.uint64)
+    h1 = shash(seed ^ 0xCE11, c, 0)
+    h2 = shash(seed ^ 0xCE11, c, 1)
+    u1 = ((h1 >> np.uint64(11)).astype(np.float64) + 1.0) / 2.0**53
+    u2 = (h2 >> np.uint64(11)).astype(np.float64) / 2.0**53
+    z = np.sqrt(-2.0 * np.log(u1)) * np.cos(2.0 * np.pi * u2)
+    w = np.exp(sigma * z)
+    cdf = np.cumsum(w) / w.sum()
+    t = np.floor(cdf * 2.0**32).astype(np.uint64)
+    t = np.minimum(t, np.uint64(0xFFFFFFFF))
+    t[-1] = np.uint64(0xFFFFFFFF)
+    return t.astype(np.uint32)
+
+
+def barcode_names(n_cells: int, seed: int = 0) -> list[str]:
+    """Deterministic whitelisted 16-mer + '-1' barcodes."""
+    h = shash(seed ^ 0xBA5E, np.arange(n_cells, dtype=np.uint64), 0)
+    out = []
+    for v in h.tolist():
+        s = "".join("ACGT"[(v >> (2 * k)) & 3] for k in range(16))
+        out.append(s + "-1")
+    # collisions are astronomically unlikely; make them impossible
+    seen: dict[str, int] = {}
+    for i, s in enumerate(out):
+        if s in seen:
+            out[i] = s[:-2] + f"-{i + 2}"
+        seen[out[i]] = i
+    return out
+
+
+@dataclass
+class ReadSoA:
+    """Engine input: SoA key arrays + packed payload records (BAM order)."""
+
+    start: np.ndarray
+    bc: np.ndarray
+    tlen: np.ndarray
+    flag: np.ndarray
+    mapq: np.ndarray
+    span: np.ndarray
+    rec_off: np.ndarray
+    payload: np.ndarray
+    extra: dict = field(default_factory=dict)
+
+    @property
+    def n(self) -> int:
+        return int(self.start.shape[0])
+
+    def slice(self, lo: int, hi: int) -> ReadSoA:
+        """Reads [lo, hi) as a standalone batch (payload re-based)."""
+        if hi <= lo:
+            return empty_soa()
+        p0 = int(self.rec_off[lo])
+        p1 = int(self.rec_off[hi]) if hi < self.n else int(self.payload.shape[0])
+        return ReadSoA(
+            self.start[lo:hi].copy(),
+            self.bc[lo:hi].copy(),
+            self.tlen[lo:hi].copy(),
+            self.flag[lo:hi].copy(),
+            self.mapq[lo:hi].copy(),
+            self.span[lo:hi].copy(),
+            (self.rec_off[lo:hi] - np.uint64(p0)).astype(np.uint64),
+            self.payload[p0:p1].copy(),
+        )
+
+
+def empty_soa() -> ReadSoA:
+    return ReadSoA(
+        np.zeros(0, np.int32),
+        np.zeros(0, np.int32),
+        np.zeros(0, np.int32),
+        np.zeros(0, np.uint16),
+        np.zeros(0, np.uint8),
+        np.zeros(0, np.uint32),
+        np.zeros(0, np.uint64),
+        np.zeros(0, np.uint8),
+    )
+
+
+def concat_soa(parts: list[ReadSoA]) -> ReadSoA:
+    parts = [p for p in parts if p.n]
+    if not parts:
+        return empty_soa()
+    offs = []
+    pay = []
+    base = 0
+    for p in parts:
+        base = (base + 15) & ~15
+        offs.append(p.rec_off + np.uint64(base))
+        pad = base - sum(x.shape[0] for x in pay)
+        if pad:
+            pay.append(np.zeros(pad, np.uint8))
+        pay.append(p.payload)
+        base += p.payload.shape[0]
+    return ReadSoA(
+        np.concatenate([p.start for p in parts]),
+        np.concatenate([p.bc for p in parts]),
+        np.concatenate([p.tlen for p in parts]),
+        np.concatenate([p.flag for p in parts]),
+        np.concatenate([p.mapq for p in parts]),
+        np.concatenate([p.span for p in parts]),
+        np.concatenate(offs).astype(np.uint64),
+        np.concatenate(pay),
+    )
+
+
+def rec_size(ncig, lseq):
+    return (16 + 4 * np.asarray(ncig, np.int64) + np.asarray(lseq, np.int64) + (np.asarray(lseq, np.int64) + 1) // 2 + 7) & ~7
+
+
+def _synth_chunk(seed, i0, i1, n, read_len, n_cells, mito_len, cdf, ref):
+    """Fields of reads [i0, i1) (needs the ancestors, which hash from the index)."""
+    rl = read_len
+    # ancestors: walk back to the last ORIG (A) / last non-FULL (B) read
+    lo = max(0, i0 - 64)
+    while True:
+        idx = np.arange(lo, i1, dtype=np.uint64)
+        t = _u24(shash(seed, idx, 1))
+        typ = np.where(t < DUP_FULL, 1, np.where(t < DUP_PART, 2, 0))
+        if lo == 0:
+            typ[0] = 0
+        # need an ORIG at or before i0 inside the window (or lo == 0)
+        first_orig = np.flatnonzero(typ[: i0 - lo + 1] == 0)
+        first_nf = np.flatnonzero(typ[: i0 - lo + 1] != 1)
+        if lo == 0 or (first_orig.size and first_nf.size):
+            break
+        lo = max(0, lo - 4096)
+    ar = np.arange(lo, i1, dtype=np.int64)
+    A = np.maximum.accumulate(np.where(typ == 0, ar, -1))
+    B = np.maximum.accumulate(np.where(typ != 1, ar, -1))
+    A = A[i0 - lo :].astype(np.uint64)
+    B = B[i0 - lo :].astype(np.uint64)
+    i = np.arange(i0, i1, dtype=np.uint64)
+    m = i.shape[0]
+
+    spanpos = np.uint64(mito_len - rl + 1)
+    u = shash(seed, A, 2) >> np.uint64(40)
+    with np.errstate(over="ignore"):
+        s0 = ((A * spanpos + ((u * spanpos) >> np.uint64(24))) // np.uint64(n)).astype(np.int32)
+    if n_cells > 0:
+        hc = (shash(seed, A, 3) & np.uint64(0xFFFFFFFF)).astype(np.uint32)
+        cell = np.searchsorted(cdf, hc, side="right").astype(np.int32)
+        cell = np.minimum(cell, n_cells - 1)
+    else:
+        cell = np.full(m, -1, np.int32)
+    strand = (shash(seed, A, 4) >> np.uint64(63)).astype(np.int32)
+    tabs = (60 + (shash(seed, B, 5) % np.uint64(541))).astype(np.int32)
+
+    cat = _u24(shash(seed, i, 6))
+    bc = np.where(cat < CAT_NOCB, -1, cell).astype(np.int32)
+    flag = (FLAG_PAIRED | np.where(strand == 1, FLAG_REVERSE, 0)).astype(np.int64)
+    flag |= np.where((cat >= CAT_NOCB) & (cat < CAT_SEC), FLAG_SECONDARY, 0)
+    flag |= np.where((cat >= CAT_SEC) & (cat < CAT_SUPP), FLAG_SUPPLEMENTARY, 0)
+    flag |= np.where((cat >= CAT_SUPP) & (cat < CAT_UNMAP), FLAG_UNMAPPED, 0)
+    flag = flag.astype(np.uint16)
+    mapq = np.where(_u24(shash(seed, i, 7)) < MAPQ0, 0, 60).astype(np.uint8)
+
+    x = _u24(shash(seed, i, 8))
+    p = shash(seed, i, 9)
+    cls = np.where(x < CIG_M, 0, np.where(x < CIG_S, 1, np.where(x < CIG_I, 2, 3)))
+    a = np.zeros(m, np.int64)
+    b = np.zeros(m, np.int64)
+    s_mask = cls == 1
+    a[s_mask] = 1 + (p[s_mask] % np.uint64(10)).astype(np.int64)
+    id_mask = cls >= 2
+    a[id_mask] = 10 + (p[id_mask] % np.uint64(31)).astype(np.int64)
+    b[id_mask] = 1 + ((p[id_mask] >> np.uint64(16)) % np.uint64(3)).astype(np.int64)
+    ncig = np.choose(cls, [1, 2, 3, 3]).astype(np.int64)
+    span = np.where(cls == 3, rl + b, rl).astype(np.uint32)
+
+    cig = np.zeros((m, 3), np.uint32)
+    M = cls == 0
+    cig[M, 0] = (rl << 4) | 0
+    cig[s_mask, 0] = (a[s_mask] << 4) | 4
+    cig[s_mask, 1] = ((rl - a[s_mask]) << 4) | 0
+    Im = cls == 2
+    cig[Im, 0] = (a[Im] << 4) | 0
+    cig[Im, 1] = (b[Im] << 4) | 1
+    cig[Im, 2] = ((rl - a[Im] - b[Im]) << 4) | 0
+    Dm = cls == 3
+    cig[Dm, 0] = (a[Dm] << 4) | 0
+    cig[Dm, 1] = (b[Dm] << 4) | 2
+    cig[Dm, 2] = ((rl - a[Dm]) << 4) | 0
+
+    q = np.arange(rl, dtype=np.uint64)
+    hq = shash(seed, i[:, None], np.uint64(1000) + q[None, :])
+    qual = np.where(_u24(hq) < QUAL37, 37, 2 + (hq % np.uint64(35)).astype(np.int64)).astype(np.uint8)
+    del hq
+    qi = q.astype(np.int64)[None, :]
+    ac, bcol = a[:, None], b[:, None]
+    d = np.broadcast_to(qi, (m, rl)).copy()
+    rnd = np.zeros((m, rl), bool)
+    c1 = (cls == 1)[:, None]
+    rnd |= c1 & (qi < ac)
+    d = np.where(c1, qi - ac, d)
+    c2 = (cls == 2)[:, None]
+    rnd |= c2 & (qi >= ac) & (qi < ac + bcol)
+    d = np.where(c2 & (qi >= ac + bcol), qi - bcol, d)
+    c3 = (cls == 3)[:, None]
+    d = np.where(c3 & (qi >= ac), qi + bcol, d)
+    hs = shash(seed, i[:, None], np.uint64(100000) + q[None, :])
+    mm = _u24(hs)
+    rpos = (s0.astype(np.int64)[:, None] + np.where(rnd, 0, d)) % mito_len
+    rc = ref[rpos]
+    rc_idx = np.searchsorted(CODES, rc)  # 1,2,4,8 -> 0..3
+    sub = CODES[(rc_idx + 1 + ((hs & np.uint64(255)) % np.uint64(3)).astype(np.int64)) & 3]
+    code = np.where(mm < BASE_N, 15, np.where(mm < BASE_SUB, sub, rc)).astype(np.uint8)
+    code = np.where(rnd, CODES[(hs & np.uint64(3)).astype(np.int64)], code).astype(np.uint8)
+    del hs, mm, rpos, rc, sub, d, rnd
+
+    return dict(
+        start=s0, bc=bc, tlen=np.where(strand == 1, -tabs, tabs).astype(np.int32), flag=flag, mapq=mapq,
+        span=span, ncig=ncig, cig=cig, qual=qual, code=code,
+    )
+
+
+def _pack_fixed(start, flag, ncig, cig, qual, code, rl):
+    """Pack records for reads of one read length (vectorised)."""
+    m = start.shape[0]
+    sizes = rec_size(ncig, np.full(m, rl))
+    roff = np.zeros(m, np.uint64)
+    if m:
+        roff[1:] = np.cumsum(sizes[:-1]).astype(np.uint64)
+    total = int(sizes.sum())
+    pay = np.zeros(total, np.uint8)
+    hdr = np.zeros(m, dtype=[("start", "<i4"), ("lseq", "<u4"), ("ncig", "<u2"), ("flag", "<u2"), ("rsv", "<u4")])
+    hdr["start"] = start
+    hdr["lseq"] = rl
+    hdr["ncig"] = ncig
+    hdr["flag"] = flag
+    hb = hdr.view(np.uint8).reshape(m, 16)
+    ro = roff.astype(np.int64)
+    pay[ro[:, None] + np.arange(16)[None, :]] = hb
+    cb = cig.astype("<u4").view(np.uint8).reshape(m, -1)
+    for k in range(cig.shape[1]):
+        sel = ncig > k
+        pay[(ro[sel, None] + 16 + 4 * k + np.arange(4)[None, :])] = cb[sel, 4 * k : 4 * k + 4]
+    qoff = ro + 16 + 4 * ncig
+    pay[qoff[:, None] + np.arange(rl)[None, :]] = qual
+    nb = (rl + 1) // 2
+    c = code
+    if rl & 1:
+        c = np.concatenate([c, np.zeros((m, 1), np.uint8)], axis=1)
+    packed = ((c[:, 0::2] << 4) | c[:, 1::2]).astype(np.uint8)
+    pay[(qoff + rl)[:, None] + np.arange(nb)[None, :]] = packed
+    return roff, pay
+
+
+def synth_reads(
+    seed: int, n_reads: int, n_cells: int, read_len: int = 50, mito_len: int = MITO_LEN, chunk: int = 262144
+) -> ReadSoA:
+    """Host mirror of the device generator (bit-identical)."""
+    if read_len < 48:
+        raise ValueError("read_len must be >= 48")
+    cdf = cell_cdf(seed, n_cells)
+    ref = ref_codes(seed, mito_len)
+    parts = []
+    for i0 in range(0, n_reads, chunk):
+        i1 = min(n_reads, i0 + chunk)
+        f = _synth_chunk(seed, i0, i1, n_reads, read_len, n_cells, mito_len, cdf, ref)
+        roff, pay = _pack_fixed(f["start"], f["flag"], f["ncig"], f["cig"], f["qual"], f["code"], read_len)
+        parts.append(ReadSoA(f["start"], f["bc"], f["tlen"], f["flag"], f["mapq"], f["span"], roff, pay))
+    soa = _concat_dense(parts)
+    soa.extra.update(cdf=cdf, ref=ref, seed=seed, read_len=read_len)
+    return soa
+
+
+def _concat_dense(parts: list[ReadSoA]) -> ReadSoA:
+    """Concatenate without padding between parts (the device layout)."""
+    if not parts:
+        return empty_soa()
+    offs, base = [], 0
+    for p in parts:
+        offs.append(p.rec_off + np.uint64(base))
+        base += p.payload.shape[0]
+    return ReadSoA(
+        np.concatenate([p.start for p in parts]),
+        np.concatenate([p.bc for p in parts]),
+        np.concatenate([p.tlen for p in parts]),
+        np.concatenate([p.flag for p in parts]),
+        np.concatenate([p.mapq for p in parts]),
+        np.concatenate([p.span for p in parts]),
+        np.concatenate(offs).astype(np.uint64),
+        np.concatenate([p.payload for p in parts]),
+    )
+
+
+# ---------------------------------------------------------------------------
+# generic packer (pysam-like records)
+# ---------------------------------------------------------------------------
+def cigar_ref_span(cigar) -> int:
+    return sum(length for op, length in cigar if op in (0, 2, 3, 7, 8))
+
+
+def pack_reads(reads: list[dict]) -> ReadSoA:
+    """Pack pysam-like read dicts into the engine input.
+
+    Keys: ``reference_start``, ``flag`` (BAM flag), ``mapping_quality``,
+    ``cigartuples`` (list of (op, len) or None), ``query_sequence`` (str or
+    None), ``query_qualities`` (list of ints or None), ``template_length``,
+    ``bc`` (whitelist index or -1).
+    """
+    n = len(reads)
+    start = np.zeros(n, np.int32)
+    bc = np.zeros(n, np.int32)
+    tlen = np.zeros(n, np.int32)
+    flag = np.zeros(n, np.uint16)
+    mapq = np.zeros(n, np.uint8)
+    span = np.zeros(n, np.uint32)
+    roff = np.zeros(n, np.uint64)
+    chunks = []
+    off = 0
+    for i, r in enumerate(reads):
+        seq = r.get("query_sequence")
+        qual = r.get("query_qualities")
+        cig = r.get("cigartuples") or []
+        lseq = len(seq) if seq is not None else 0
+        f = int(r.get("flag", 0))
+        if seq is None or qual is None:
+            f |= FLAG_NOSEQQUAL
+        start[i] = r["reference_start"]
+        bc[i] = r.get("bc", -1)
+        tlen[i] = r.get("template_length", 0)
+        flag[i] = f
+        mapq[i] = r.get("mapping_quality", 60)
+        span[i] = max(cigar_ref_span(cig), lseq)
+        roff[i] = off
+        size = int(rec_size(len(cig), lseq))
+        rec = np.zeros(size, np.uint8)
+        hdr = np.array([(start[i], lseq, len(cig), f, 0)],
+                       dtype=[("s", "<i4"), ("l", "<u4"), ("n", "<u2"), ("f", "<u2"), ("r", "<u4")])
+        rec[:16] = hdr.view(np.uint8)
+        if cig:
+            rec[16 : 16 + 4 * len(cig)] = np.array([(ln << 4) | op for op, ln in cig], "<u4").view(np.uint8)
+        q0 = 16 + 4 * len(cig)
+        if lseq:
+            if qual is not None:
+                rec[q0 : q0 + lseq] = np.asarray(qual, dtype=np.int64) & 0xFF
+            else:
+                rec[q0 : q0 + lseq] = 0xFF
+            codes = [_NT16_IDX[ch] for ch in seq.upper()] if seq is not None else []
+            if lseq & 1:
+                codes.append(0)
+            codes = np.array(codes, np.uint8)
+            rec[q0 + lseq : q0 + lseq + (lseq + 1) // 2] = (codes[0::2] << 4) | codes[1::2]
+        chunks.append(rec)
+        off += size
+    payload = np.concatenate(chunks) if chunks else np.zeros(0, np.uint8)
+    return ReadSoA(start, bc, tlen, flag, mapq, span, roff, payload)
+
+
+def unpack_record(payload: np.ndarray, off: int) -> dict:
+    """Decode one payload record (test helper)."""
+    hdr = payload[off : off + 16].view(np.uint8)
+    start = int(hdr[:4].view("<i4")[0])
+    lseq = int(hdr[4:8].view("<u4")[0])
+    ncig = int(hdr[8:10].view("<u2")[0])
+    flag = int(hdr[10:12].view("<u2")[0])
+    cig = payload[off + 16 : off + 16 + 4 * ncig].view("<u4").tolist() if ncig else []
+    q0 = off + 16 + 4 * ncig
+    qual = payload[q0 : q0 + lseq].tolist()
+    sb = payload[q0 + lseq : q0 + lseq + (lseq + 1) // 2]
+    codes = np.stack([sb >> 4, sb & 15], axis=1).reshape(-1)[:lseq]
+    seq = "".join(SEQ_NT16[c] for c in codes.tolist())
+    return dict(
+        reference_start=start, flag=flag, cigartuples=[(c & 15, c >> 4) for c in cig],
+        query_sequence=seq, query_qualities=qual,
+    )

@@ -1,0 +1,103 @@
+"""The C-ABI library loads here (no GPU needed) and exports every symbol the
+header declares; host-side packing invariants."""
+
+import re
+from pathlib import Path
+
+import numpy as np
+
+ROOT = Path(__file__).resolve().parent.parent
+
+
+def header_symbols():
+    text = (ROOT / "include" / "mgpileup.h").read_text()
+    return sorted(set(re.findall(r"\b(mgp_[a-z_0-9]+)\s*\(", text)))
+
+
+def test_library_exports_header_symbols():
+    from mgatk2_amd.build import build_engine
+    from mgatk2_amd import engine
+
+    build_engine()
+    lib = engine.load_library()
+    syms = header_symbols()
+    assert len(syms) >= 19
+    for s in syms:
+        assert hasattr(lib, s), f"libmgpileup.so does not export {s}"
+    assert set(syms) == set(engine.ABI_SYMBOLS)
+    assert lib.mgp_abi_version() == 1
+
+
+def test_no_device_fails_loudly():
+    """Without a GPU the engine raises; there is no CPU fallback."""
+    import pytest
+
+    from mgatk2_amd import engine
+
+    if engine.device_count() > 0:
+        pytest.skip("a GPU is present")
+    with pytest.raises(Exception):
+        engine.Engine(engine.EngineConfig(n_cells=1))
+
+
+def test_struct_layouts_match_header(tmp_path):
+    """ctypes mirrors have the C compiler's sizes and field offsets."""
+    import ctypes as C
+    import subprocess
+
+    from mgatk2_amd import engine
+
+    structs = {
+        "mgp_config": engine.mgp_config, "mgp_batch": engine.mgp_batch, "mgp_stats": engine.mgp_stats,
+        "mgp_result": engine.mgp_result, "mgp_synth_params": engine.mgp_synth_params,
+    }
+    lines = ['#include <stdio.h>', '#include <stddef.h>', f'#include "{ROOT}/include/mgpileup.h"', "int main(){"]
+    for name, cls in structs.items():
+        lines.append(f'printf("%zu\\n", sizeof({name}));')
+        for fname, _ in cls._fields_:
+            lines.append(f'printf("%zu\\n", offsetof({name}, {fname}));')
+    lines.append("return 0;}")
+    src = tmp_path / "layout.c"
+    src.write_text("\n".join(lines))
+    exe = tmp_path / "layout"
+    subprocess.run(["gcc", str(src), "-o", str(exe)], check=True)
+    got = [int(x) for x in subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.split()]
+    want = []
+    for cls in structs.values():
+        want.append(C.sizeof(cls))
+        want.extend(getattr(cls, f).offset for f, _ in cls._fields_)
+    assert got == want
+
+
+def test_pack_and_unpack_roundtrip():
+    from mgatk2_amd.synth import pack_reads, unpack_record
+
+    reads = [
+        dict(reference_start=5, cigartuples=[(4, 2), (0, 7)], query_sequence="ACGTNRY", query_qualities=list(range(7)),
+             bc=0, flag=0x11, mapping_quality=7, template_length=-70),
+        dict(reference_start=9, cigartuples=[(0, 6)], query_sequence="TTTTGG", query_qualities=[200] * 6, bc=1,
+             flag=1, mapping_quality=60, template_length=70),
+    ]
+    soa = pack_reads(reads)
+    assert soa.n == 2 and np.all(soa.rec_off % 8 == 0)
+    for i, r in enumerate(reads):
+        d = unpack_record(soa.payload, int(soa.rec_off[i]))
+        assert d["reference_start"] == r["reference_start"]
+        assert d["cigartuples"] == r["cigartuples"]
+        assert d["query_sequence"] == r["query_sequence"]
+        assert d["query_qualities"] == r["query_qualities"]
+    assert soa.span.tolist() == [7, 6]
+
+
+def test_host_synth_is_deterministic_and_sorted():
+    from mgatk2_amd.synth import synth_reads
+
+    a = synth_reads(11, 30_000, 9)
+    b = synth_reads(11, 30_000, 9, chunk=7_000)
+    for k in ("start", "bc", "tlen", "flag", "mapq", "span", "rec_off", "payload"):
+        np.testing.assert_array_equal(getattr(a, k), getattr(b, k))
+    assert np.all(np.diff(a.start) >= 0)
+    assert a.start.min() >= 0 and a.start.max() <= 16569 - 50
+    # duplicate structure: ~15% full copies of the previous read's key
+    same = (a.start[1:] == a.start[:-1]) & (a.bc[1:] == a.bc[:-1]) & (a.tlen[1:] == a.tlen[:-1])
+    assert 0.12 < same.mean() < 0.2
