@@ -819,14 +819,16 @@ int mgp_open(const mgp_config* cfg, int hip_device, mgp_ctx** out) {
     hipDeviceProp_t prop;
     HIP_TRY(hipGetDeviceProperties(&prop, hip_device));
     ctx->lds_hist_max_cells = (int)std::min<size_t>(prop.sharedMemPerBlock, 96 * 1024) / 4;
-    // kernels whose dynamic LDS may exceed the 64 KiB default (gfx950 has 160 KiB per CU)
+    // kernels whose dynamic LDS may exceed 64 KiB (gfx950: up to 160 KiB per workgroup);
+    // best effort: the runtime may already allow it without the attribute
     {
-        const int lds_max = (int)std::min<size_t>(prop.sharedMemPerBlock, 160 * 1024);
-        HIP_TRY(hipFuncSetAttribute((const void*)k_median, hipFuncAttributeMaxDynamicSharedMemorySize, lds_max));
-        HIP_TRY(hipFuncSetAttribute((const void*)k_bin_hist<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                    lds_max));
-        HIP_TRY(hipFuncSetAttribute((const void*)k_pileup, hipFuncAttributeMaxDynamicSharedMemorySize, lds_max));
-        if ((size_t)ctx->g.L * 4 + 2048 > (size_t)lds_max) {
+        const int lds_max = (int)prop.sharedMemPerBlock;
+        (void)hipFuncSetAttribute((const void*)k_median, hipFuncAttributeMaxDynamicSharedMemorySize, lds_max);
+        (void)hipFuncSetAttribute((const void*)k_bin_hist<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  lds_max);
+        (void)hipFuncSetAttribute((const void*)k_pileup, hipFuncAttributeMaxDynamicSharedMemorySize, lds_max);
+        (void)hipGetLastError();
+        if ((size_t)ctx->g.L * 4 + 2048 > prop.sharedMemPerBlock) {
             delete ctx;
             return set_err(MGP_E_INVALID, "mito_len too large for the per-cell median LDS buffer");
         }

@@ -14,6 +14,7 @@ step() {  # name timeout cmd...
     tail -n 5 "gpurun_out/$name.log"
     return $rc
 }
+step probe 120 python scripts/probe_device.py
 step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" || exit $?
 step pytest_gpu 900 python -m pytest tests -m gpu -q -x -p no:cacheprovider
 rc=$?; [ $rc -eq 0 ] || [ $rc -eq 1 ] || exit $rc
