@@ -96,15 +96,19 @@ typedef struct mgp_config {
  * mgp_host_alloc gives asynchronous H2D). Records of consecutive batches must
  * continue the coordinate order.
  *
- * Payload record i lives at payload + rec_off[i] (8-byte aligned):
+ * Payload record i lives at payload + rec_off[i] (16-byte aligned):
  *   int32  start      0-based reference_start
  *   uint32 l_seq      len(query_sequence), soft clips included
  *   uint16 n_cigar
  *   uint16 flag       same word as flag[i]
- *   uint32 reserved   0
- *   uint32 cigar[n_cigar]           BAM encoding (len << 4 | op)
- *   uint8  qual[l_seq]              raw Phred bytes (as BAM stores them)
+ *   uint32 cigar_off  byte offset of cigar[] from the record start
+ *                     = round_up(16 + l_seq + (l_seq + 1) / 2, 4)
+ *   uint8  qual[l_seq]              raw Phred bytes (as BAM stores them), at +16
  *   uint8  seq[(l_seq + 1) / 2]     BAM 4-bit codes, high nibble first
+ *   uint32 cigar[n_cigar]           BAM encoding (len << 4 | op), at +cigar_off
+ * Record size = round_up(cigar_off + 4 * n_cigar, 16); 96 bytes for a 50M read.
+ * Qual sits at a fixed, 16-byte aligned offset so a kernel can load it with
+ * vector loads and index its bytes statically.
  */
 typedef struct mgp_batch {
     int64_t         n_reads;

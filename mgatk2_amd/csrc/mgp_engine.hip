@@ -6,21 +6,22 @@
 //   k_bin_bounds    coordinate-order check + start-bin boundaries (the order that
 //                   pysam's fetch() guarantees, readers.py:87-92)
 //   k_bin_hist      flag/barcode filters (readers.py:95-111) + per (start-bin, cell)
-//                   histogram in LDS; each read gets its rank inside its group
-//   k_scan_*        exclusive scan of the histogram in (cell, start-bin) order:
-//                   the cell-major layout that `reads_by_barcode` builds
-//                   (readers.py:69,164) without moving any payload
-//   k_scatter       writes each valid read's grouping record at its cell-major slot
-//   k_dedup         per-cell duplicate marking (readers.py:118-150: first in BAM
-//                   order wins), kept-read count + paired flag (processors.py:22,34),
-//                   MAPQ gate (pileup.py:33), compaction of the reads to pile up and
-//                   the per-window read ranges
-//   k_pileup        CIGAR walk + end-distance / base-quality / base filters +
-//                   Tn5 cuts (pileup.py:32-95) into an LDS count tile per
-//                   (cell, position window); strand-bias filter, depth, Tn5 masking
-//                   (pileup.py:128-154) and per-cell depth statistics
-//                   (processors.py:36-39, writers.py:187-197) at the tile flush;
-//                   per-workgroup reference-allele partial tallies (writers.py:221-222)
+//                   histogram in LDS; every valid read gets its STABLE rank (BAM
+//                   order) inside its (bin, cell) group, one wavefront per bin
+//   k_scan_*        exclusive scan of the histogram in (cell, start-bin) order: the
+//                   cell-major layout of `reads_by_barcode` (readers.py:69,164) with
+//                   BAM order kept inside each cell
+//   k_scatter       one 16-byte grouping element per valid read at its slot
+//   k_pileup        per (cell chunk, position window): duplicate marking by a short
+//                   walk back over equal starts (readers.py:118-150, first in BAM
+//                   order wins), kept-read counts (processors.py:22,34), MAPQ gate
+//                   (pileup.py:33), Tn5 cuts + CIGAR walk + end-distance / base
+//                   quality / base filters (pileup.py:32-95) into an LDS count tile,
+//                   then strand-bias filter, depth, Tn5 masking (pileup.py:128-154),
+//                   per-cell depth statistics (processors.py:36-39, writers.py:187-197)
+//                   and per-workgroup reference-allele partial tallies
+//                   (writers.py:221-222) at the tile flush
+//   k_gate_fixup    min-reads gate (processors.py:22) when min_reads > 1
 //   k_median        np.median of covered depths per cell (writers.py:190)
 //   k_tally_reduce  sum of the partial tallies (writers.py:340-349 input)
 //   RCCL allreduce  tallies over ranks when cells are sharded over GPUs
@@ -100,8 +101,8 @@ struct DevBuf {
     T* as() const { return reinterpret_cast<T*>(p); }
 };
 
-enum Stage { ST_BINS, ST_HIST, ST_SCAN, ST_SCATTER, ST_DEDUP, ST_PILEUP, ST_MEDIAN, ST_TALLY, ST_COMM, ST_N };
-static const char* kStageNames = "bins,hist,scan,scatter,dedup,pileup,median,tally,comm";
+enum Stage { ST_BINS, ST_HIST, ST_SCAN, ST_SCATTER, ST_PILEUP, ST_GATE, ST_MEDIAN, ST_TALLY, ST_COMM, ST_N };
+static const char* kStageNames = "bins,hist,scan,scatter,pileup,gate,median,tally,comm";
 
 struct mgp_ctx {
     mgp_config cfg{};
@@ -121,7 +122,7 @@ struct mgp_ctx {
 
     // run scratch
     DevBuf bin_start, rank, H, P, cell_cnt, cell_base;
-    DevBuf g_idx, g_start, g_tlen, g_info, g_off, p_off, edges, tally_part, tally;
+    DevBuf gel, tally_part, tally;
     DevBuf n_reads, any_paired, passed, covered, dsum, dmax, med_lo, med_hi, first_read;
     DevBuf counts, tn5, depth, stats;
 
@@ -161,50 +162,74 @@ __device__ __forceinline__ bool read_valid(int c, uint16_t f, int nc) {
     return c >= 0 && c < nc && !(f & (MGP_FLAG_UNMAPPED | MGP_FLAG_SECONDARY | MGP_FLAG_SUPPLEMENTARY));
 }
 
-// One workgroup per start bin: histogram over cells (LDS when it fits, else the
-// global row) and each valid read's rank inside its (bin, cell) group.
+// One wavefront per start bin, reads taken 64 at a time in BAM order: histogram
+// over cells (LDS when it fits, else the global row) and each valid read's STABLE
+// rank inside its (bin, cell) group. Lanes of one cell find each other with one
+// ballot per cell-id bit (a wave-wide match); the lowest lane of each peer group
+// advances the group's counter, so ranks follow BAM order.
 template <bool kLds>
-__global__ void __launch_bounds__(kBlock) k_bin_hist(const uint32_t* __restrict__ bin_start,
-                                                     const int32_t* __restrict__ bc,
-                                                     const uint16_t* __restrict__ flag,
-                                                     const uint32_t* __restrict__ span, int64_t n, Geom g,
-                                                     uint32_t* __restrict__ H, uint32_t* __restrict__ rank,
-                                                     DevStats* st) {
+__global__ void __launch_bounds__(kWave) k_bin_hist(const uint32_t* __restrict__ bin_start,
+                                                    const int32_t* __restrict__ bc,
+                                                    const uint16_t* __restrict__ flag,
+                                                    const uint32_t* __restrict__ span, int64_t n, Geom g, int cbits,
+                                                    uint32_t* __restrict__ H, uint32_t* __restrict__ rank,
+                                                    DevStats* st) {
     extern __shared__ uint32_t hist[];
     const int b = blockIdx.x;
     const int nc = g.nc;
+    const unsigned lane = threadIdx.x;
     uint32_t* row = H + (size_t)b * nc;
+    uint32_t* cnt = kLds ? hist : row;
     if (kLds) {
-        for (int c = threadIdx.x; c < nc; c += blockDim.x) hist[c] = 0;
+        for (int c = lane; c < nc; c += kWave) hist[c] = 0;
         __syncthreads();
     }
-    int64_t lo = min((int64_t)bin_start[b], n);
-    int64_t hi = min(max((int64_t)bin_start[b + 1], lo), n);
+    const int64_t lo = min((int64_t)bin_start[b], n);
+    const int64_t hi = min(max((int64_t)bin_start[b + 1], lo), n);
+    const unsigned long long lt = lanemask_lt();
     uint32_t mspan = 0;
     unsigned long long nvalid = 0;
     bool badbc = false;
-    for (int64_t i = lo + threadIdx.x; i < hi; i += blockDim.x) {
-        int c = bc[i];
-        uint16_t f = flag[i];
+    for (int64_t base = lo; base < hi; base += kWave) {
+        const int64_t i = base + lane;
+        int c = -1;
+        uint16_t f = 0;
+        uint32_t sp = 0;
+        if (i < hi) {
+            c = bc[i];
+            f = flag[i];
+            sp = span[i];
+        }
         badbc |= (c >= nc);
-        if (read_valid(c, f, nc)) {
-            rank[i] = kLds ? atomicAdd(&hist[c], 1u) : atomicAdd(&row[c], 1u);
-            uint32_t sp = span[i];
+        const bool valid = i < hi && read_valid(c, f, nc);
+        unsigned long long peers = __ballot(valid);
+        for (int bit = 0; bit < cbits; ++bit) {
+            const bool x = valid && ((c >> bit) & 1);
+            const unsigned long long m = __ballot(x);
+            peers &= x ? m : ~m;
+        }
+        if (valid) {
+            const uint32_t before = cnt[c];
+            rank[i] = before + (uint32_t)__popcll(peers & lt);
             mspan = sp > mspan ? sp : mspan;
             ++nvalid;
+            if ((peers & lt) == 0ull) cnt[c] = before + (uint32_t)__popcll(peers);  // group leader
         }
+        if (!kLds) __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");  // leader's store before next reads
+        __builtin_amdgcn_wave_barrier();
     }
     if (kLds) {
         __syncthreads();
-        for (int c = threadIdx.x; c < nc; c += blockDim.x) row[c] = hist[c];
+        for (int c = lane; c < nc; c += kWave) row[c] = hist[c];
     }
     mspan = wave_max(mspan);
     nvalid = wave_sum(nvalid);
-    if ((threadIdx.x & (kWave - 1)) == 0) {
+    const bool anybad = __ballot(badbc) != 0ull;
+    if (lane == 0) {
         if (mspan) atomicMax(&st->max_span, mspan);
         if (nvalid) atomicAdd(&st->valid, nvalid);
+        if (anybad) atomicOr(&st->err, ERR_BADBC);
     }
-    if (badbc) atomicOr(&st->err, ERR_BADBC);
 }
 
 // Scan step a: column sums over blocks of RB rows. grid (ceil(nc/256), nrb)
@@ -286,203 +311,49 @@ __global__ void k_scan_apply(uint32_t* __restrict__ H, const uint32_t* __restric
     if (rb == nrb - 1) H[(size_t)nrows * nc + c] = base[c] + cnt[c];
 }
 
-// g_info bits
-constexpr uint8_t GI_REV = 1, GI_PAIRED = 2, GI_MAPQ_OK = 4, GI_BAD = 8;
+// Grouping element (16 bytes, cell-major, BAM order inside a cell):
+//   w = record byte offset | meta << 56, start, |tlen|
+struct __align__(16) GElem {
+    unsigned long long w;
+    int32_t start;
+    uint32_t tlen;
+};
+constexpr unsigned long long GM_REV = 1ull << 56, GM_PAIRED = 2ull << 56, GM_MAPQ_OK = 4ull << 56,
+                             GM_BAD = 8ull << 56, GM_OFF = (1ull << 56) - 1;
 
-// Per read: place the grouping record of each valid read at its cell-major slot.
+// Per read: place the grouping element of each valid read at its cell-major slot.
 __global__ void k_scatter(int64_t n, const int32_t* __restrict__ start, const int32_t* __restrict__ bc,
                           const int32_t* __restrict__ tlen, const uint16_t* __restrict__ flag,
                           const uint8_t* __restrict__ mapq, const uint64_t* __restrict__ roff,
-                          const uint32_t* __restrict__ rank, const uint32_t* __restrict__ O, Geom g,
-                          int min_mapq, uint32_t* __restrict__ g_idx, int32_t* __restrict__ g_start,
-                          uint32_t* __restrict__ g_tlen, uint8_t* __restrict__ g_info,
-                          uint64_t* __restrict__ g_off, DevStats* st) {
+                          const uint32_t* __restrict__ rank, const uint32_t* __restrict__ O, Geom g, int min_mapq,
+                          GElem* __restrict__ gel, uint32_t* __restrict__ first_read, DevStats* st) {
     int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
-    int c = bc[i];
-    uint16_t f = flag[i];
+    const int c = bc[i];
+    const uint16_t f = flag[i];
     if (!read_valid(c, f, g.nc)) return;
-    int s = start[i];
-    int b = bin_of(s, g);
-    uint32_t dest = O[(size_t)b * g.nc + c] + rank[i];
-    uint32_t end = O[(size_t)g.nbins * g.nc + c];
+    const int s = start[i];
+    const int b = bin_of(s, g);
+    const uint32_t r = rank[i];
+    const uint32_t dest = O[(size_t)b * g.nc + c] + r;
+    const uint32_t end = O[(size_t)g.nbins * g.nc + c];
     if (dest >= end) {
         atomicOr(&st->err, ERR_OVERFLOW);
         return;
     }
-    int t = tlen[i];
-    uint32_t at = t < 0 ? (uint32_t)(-(int64_t)t) : (uint32_t)t;
-    uint8_t info = (f & MGP_FLAG_REVERSE ? GI_REV : 0) | (f & MGP_FLAG_PAIRED ? GI_PAIRED : 0) |
-                   ((int)mapq[i] >= min_mapq ? GI_MAPQ_OK : 0) | (f & MGP_FLAG_NOSEQQUAL ? GI_BAD : 0);
-    g_idx[dest] = (uint32_t)i;
-    g_start[dest] = s;
-    g_tlen[dest] = at;
-    g_info[dest] = info;
-    g_off[dest] = roff[i];
-}
-
-// One workgroup per cell: duplicate marking inside each (start-bin) group (the
-// group is contiguous in the cell's segment; duplicates share the exact start),
-// kept/paired counts, MAPQ gate, compaction of the reads to pile up and the
-// per-window [lo, hi) ranges into that compacted list.
-__global__ void __launch_bounds__(kBlock) k_dedup(
-    Geom g, int dedup_mode, const uint32_t* __restrict__ base, const uint32_t* __restrict__ cnt,
-    const uint32_t* __restrict__ g_idx, const int32_t* __restrict__ g_start,
-    const uint32_t* __restrict__ g_tlen, const uint8_t* __restrict__ g_info,
-    const uint64_t* __restrict__ g_off, uint64_t* __restrict__ p_off, uint32_t* __restrict__ edges,
-    uint32_t* __restrict__ n_reads, uint8_t* __restrict__ any_paired, uint32_t* __restrict__ first_read,
-    DevStats* st) {
-    extern __shared__ uint32_t sm[];
-    uint32_t* ledge = sm;                 // [2 * nwin]
-    int32_t* lbin = (int32_t*)(sm + 2 * g.nwin);  // [kBlock]
-    __shared__ uint32_t wtot[kBlock / kWave];
-    __shared__ uint32_t s_running;
-    __shared__ int32_t s_lastbin;
-
-    const int c = blockIdx.x;
-    const uint32_t seg_lo = base[c];
-    const uint32_t seg_hi = seg_lo + cnt[c];
-    const int R = ((int)(st->max_span + g.G - 1) / g.G) * g.G;
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-
-    for (int k = threadIdx.x; k < 2 * g.nwin; k += blockDim.x) ledge[k] = 0xFFFFFFFFu;
-    if (threadIdx.x == 0) {
-        s_running = 0;
-        s_lastbin = -1;
-    }
-    __syncthreads();
-
-    uint32_t nkeep = 0, minidx = 0xFFFFFFFFu;
-    unsigned long long d2 = 0, d3 = 0;
-    bool paired = false, bad = false;
-
-    for (uint32_t cb = seg_lo; cb < seg_hi; cb += blockDim.x) {
-        const uint32_t j = cb + threadIdx.x;
-        const bool active = j < seg_hi;
-        bool piled = false;
-        int b = 0;
-        if (active) {
-            const int s = g_start[j];
-            const uint8_t info = g_info[j];
-            const uint32_t tl = g_tlen[j];
-            const uint32_t idx = g_idx[j];
-            b = bin_of(s, g);
-            minidx = min(minidx, idx);
-            bool dup2 = false, dup3 = false;
-            if (dedup_mode != MGP_DEDUP_NONE) {
-                for (uint32_t m = j; m-- > seg_lo;) {
-                    const int sm2 = g_start[m];
-                    if (bin_of(sm2, g) != b) break;
-                    if (sm2 == s && ((g_info[m] ^ info) & GI_REV) == 0 && g_idx[m] < idx) {
-                        dup2 = true;
-                        if (g_tlen[m] == tl) dup3 = true;
-                    }
-                }
-                for (uint32_t m = j + 1; m < seg_hi; ++m) {
-                    const int sm2 = g_start[m];
-                    if (bin_of(sm2, g) != b) break;
-                    if (sm2 == s && ((g_info[m] ^ info) & GI_REV) == 0 && g_idx[m] < idx) {
-                        dup2 = true;
-                        if (g_tlen[m] == tl) dup3 = true;
-                    }
-                }
-                d2 += dup2;
-                d3 += dup3;
-            }
-            const bool keep = dedup_mode == MGP_DEDUP_NONE ? true
-                              : dedup_mode == MGP_DEDUP_START ? !dup2
-                                                              : !dup3;
-            if (keep) {
-                ++nkeep;
-                paired |= (info & GI_PAIRED) != 0;
-                bad |= (info & GI_BAD) != 0;
-                piled = (info & GI_MAPQ_OK) != 0;
-            }
-        }
-        // block compaction of piled reads (order preserved)
-        const unsigned long long bal = __ballot(piled);
-        const uint32_t wpre = __popcll(bal & lanemask_lt());
-        if (lane == 0) wtot[wid] = __popcll(bal);
-        __syncthreads();
-        uint32_t woff = 0, tot = 0;
-        for (int w = 0; w < kBlock / kWave; ++w) {
-            if (w < wid) woff += wtot[w];
-            tot += wtot[w];
-        }
-        const uint32_t pos = woff + wpre;
-        if (piled) lbin[pos] = b;
-        __syncthreads();
-        const uint32_t running = s_running;
-        if (piled) {
-            const int prevb = pos == 0 ? s_lastbin : lbin[pos - 1];
-            const uint32_t P = running + pos;
-            p_off[seg_lo + P] = g_off[j];
-            for (int k = 0; k < g.nwin; ++k) {
-                const int lo_b = win_lo_bin(k, R, g);
-                if (prevb < lo_b && lo_b <= b) ledge[2 * k] = P;
-                const int hi_b = win_hi_bin(k, g);
-                if (prevb < hi_b && hi_b <= b) ledge[2 * k + 1] = P;
-            }
-        }
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            if (tot) s_lastbin = lbin[tot - 1];
-            s_running = running + tot;
-        }
-        __syncthreads();
-    }
-
-    // reductions
-    nkeep = wave_sum(nkeep);
-    d2 = wave_sum(d2);
-    d3 = wave_sum(d3);
-    minidx = wave_min(minidx);
-    const bool anyp = __ballot(paired) != 0ull;
-    const bool anyb = __ballot(bad) != 0ull;
-    __shared__ uint32_t r_keep[4], r_min[4];
-    __shared__ unsigned long long r_d2[4], r_d3[4];
-    __shared__ int r_p[4], r_b[4];
-    if (lane == 0) {
-        r_keep[wid] = nkeep;
-        r_min[wid] = minidx;
-        r_d2[wid] = d2;
-        r_d3[wid] = d3;
-        r_p[wid] = anyp;
-        r_b[wid] = anyb;
-    }
-    __syncthreads();
-    const uint32_t npiled = s_running;
-    for (int k = threadIdx.x; k < 2 * g.nwin; k += blockDim.x) {
-        uint32_t e = ledge[k];
-        edges[(size_t)c * 2 * g.nwin + k] = e == 0xFFFFFFFFu ? npiled : e;
-    }
-    if (threadIdx.x == 0) {
-        uint32_t K = 0, M = 0xFFFFFFFFu;
-        unsigned long long D2 = 0, D3 = 0;
-        int PP = 0, BB = 0;
-        for (int w = 0; w < 4; ++w) {
-            K += r_keep[w];
-            M = min(M, r_min[w]);
-            D2 += r_d2[w];
-            D3 += r_d3[w];
-            PP |= r_p[w];
-            BB |= r_b[w];
-        }
-        n_reads[c] = K;
-        any_paired[c] = (uint8_t)PP;
-        first_read[c] = M;
-        if (D2) atomicAdd(&st->dup_pos, D2);
-        if (D3) atomicAdd(&st->dup_len, D3);
-        if (K) {
-            atomicAdd(&st->filtered, (unsigned long long)K);
-            atomicAdd(&st->n_barcodes, 1ull);
-        }
-        if (BB) atomicOr(&st->err, ERR_BADREAD);
-    }
+    const int t = tlen[i];
+    GElem e;
+    e.w = roff[i] | (f & MGP_FLAG_REVERSE ? GM_REV : 0ull) | (f & MGP_FLAG_PAIRED ? GM_PAIRED : 0ull) |
+          ((int)mapq[i] >= min_mapq ? GM_MAPQ_OK : 0ull) | (f & MGP_FLAG_NOSEQQUAL ? GM_BAD : 0ull);
+    e.start = s;
+    e.tlen = t < 0 ? (uint32_t)(-(int64_t)t) : (uint32_t)t;
+    gel[dest] = e;
+    // the cell's first element in cell-major order is its first valid read in BAM order
+    if (r == 0 && dest == O[c]) first_read[c] = (uint32_t)i;
 }
 
 struct PileCfg {
-    int min_baseq, min_dist, min_reads;
+    int min_baseq, min_dist, min_reads, dedup_mode;
     double max_bias;
     bool bias_active;  // max_bias < 1 (max/total <= 1 otherwise)
 };
@@ -492,44 +363,42 @@ __device__ __forceinline__ int base_index(uint32_t code) {
     return code == 1 ? 0 : code == 2 ? 1 : code == 4 ? 2 : code == 8 ? 3 : -1;
 }
 
-// One read: Tn5 cut + CIGAR walk restricted to window [w0, w0+wlen).
-__device__ __forceinline__ void pile_read(const uint8_t* __restrict__ rec, int w0, int wlen, const PileCfg& pc,
-                                          int Wp, uint32_t* __restrict__ tile, uint32_t* __restrict__ t5,
-                                          uint32_t max_span, bool& span_err) {
-    const int32_t start = *reinterpret_cast<const int32_t*>(rec);
-    const uint32_t lseq = *reinterpret_cast<const uint32_t*>(rec + 4);
-    const uint32_t ncig = *reinterpret_cast<const uint16_t*>(rec + 8);
-    const uint32_t flag = *reinterpret_cast<const uint16_t*>(rec + 10);
-    const uint32_t* cig = reinterpret_cast<const uint32_t*>(rec + 16);
-    const uint8_t* qual = rec + 16 + 4 * ncig;
-    const uint8_t* seq = qual + lseq;
-    const int strand = (flag & MGP_FLAG_REVERSE) ? 1 : 0;
-    const int64_t wend = (int64_t)w0 + wlen;
+struct Win {
+    int w0, wlen, Wp;
+};
 
-    // Tn5 cut (pileup.py:43-50): reverse reads cut at start + len(seq) - 1
+__device__ __forceinline__ void tn5_cut(int32_t start, uint32_t lseq, int strand, const Win& w, uint32_t* t5) {
+    // pileup.py:43-50: reverse reads cut at start + len(seq) - 1
     const int64_t cut = strand ? (int64_t)start + lseq - 1 : (int64_t)start;
-    if (cut >= w0 && cut < wend && cut >= 0) atomicAdd(&t5[strand * Wp + (int)(cut - w0)], 1u);
+    if (cut >= w.w0 && cut < (int64_t)w.w0 + w.wlen) atomicAdd(&t5[strand * w.Wp + (int)(cut - w.w0)], 1u);
+}
 
+// Generic path (any read): CIGAR walk with byte loads (pileup.py:55-95).
+__device__ void pile_slow(const uint8_t* __restrict__ rec, int32_t start, uint32_t lseq, uint32_t ncig,
+                          uint32_t coff, int strand, const Win& w, const PileCfg& pc, uint32_t* tile,
+                          uint32_t max_span, bool& span_err) {
+    const uint32_t* cig = reinterpret_cast<const uint32_t*>(rec + coff);
+    const uint8_t* qual = rec + 16;
+    const uint8_t* seq = qual + lseq;
+    const int64_t wend = (int64_t)w.w0 + w.wlen;
     const int64_t vq0 = pc.min_dist > 0 ? pc.min_dist : 0;
     const int64_t vq1 = pc.min_dist > 0 ? (int64_t)lseq - pc.min_dist : (int64_t)lseq;
     int64_t ref = start, q = 0;
-    uint32_t* plane = tile + strand * Wp;
+    uint32_t* plane = tile + strand * w.Wp;
     for (uint32_t o = 0; o < ncig; ++o) {
         const uint32_t cg = cig[o];
         const uint32_t op = cg & 15u;
         const int64_t len = cg >> 4;
         if (op == 0 || op == 7 || op == 8) {
-            int64_t klo = max((int64_t)0, max((int64_t)w0 - ref, vq0 - q));
-            int64_t khi = min(len, min(wend - ref, min(vq1, (int64_t)lseq) - q));
+            const int64_t klo = max((int64_t)0, max((int64_t)w.w0 - ref, vq0 - q));
+            const int64_t khi = min(len, min(wend - ref, min(vq1, (int64_t)lseq) - q));
             for (int64_t k = klo; k < khi; ++k) {
                 const int64_t qq = q + k;
-                const int qv = (int)(int8_t)qual[qq];
-                if (qv < pc.min_baseq) continue;
+                if ((int)(int8_t)qual[qq] < pc.min_baseq) continue;
                 const uint8_t sb = seq[qq >> 1];
-                const uint32_t code = (qq & 1) ? (sb & 15u) : (sb >> 4);
-                const int bi = base_index(code);
+                const int bi = base_index((qq & 1) ? (sb & 15u) : (sb >> 4));
                 if (bi < 0) continue;
-                atomicAdd(&plane[2 * bi * Wp + (int)(ref + k - w0)], 1u);
+                atomicAdd(&plane[2 * bi * w.Wp + (int)(ref + k - w.w0)], 1u);
             }
             q += len;
             ref += len;
@@ -539,34 +408,145 @@ __device__ __forceinline__ void pile_read(const uint8_t* __restrict__ rec, int w
             q += len;
         }
     }
-    const int64_t reach = max(ref - (int64_t)start, (int64_t)lseq);
-    if (reach > (int64_t)max_span) span_err = true;
+    if (max(ref - (int64_t)start, (int64_t)lseq) > (int64_t)max_span) span_err = true;
+}
+
+constexpr int kFastLen = 64;   // reads up to 64 bases and 4 CIGAR ops take the register path
+constexpr int kFastCig = 4;
+// 4-bit BAM code -> base index (1->A 2->C 4->G 8->T), 15 = skip
+constexpr unsigned long long kCodeLut = 0xFFFFFFF3FFF2F10Full;
+
+// Register path: qual (16-byte aligned at +16) and seq are loaded into registers
+// once; the per-base loop is fully unrolled so every byte index is static.
+__device__ __forceinline__ void pile_fast(const uint8_t* __restrict__ rec, int32_t start, uint32_t lseq,
+                                          uint32_t ncig, uint32_t coff, int strand, const Win& w,
+                                          const PileCfg& pc, uint32_t* tile, uint32_t max_span, bool& span_err) {
+    // CIGAR -> up to 4 aligned blocks [qs, qe) with r = q + dl (insertions do not move q: pileup.py Q1)
+    const uint32_t* cig = reinterpret_cast<const uint32_t*>(rec + coff);
+    int qs[kFastCig], qe[kFastCig], dl[kFastCig];
+    int ref = start, q = 0;
+#pragma unroll
+    for (int o = 0; o < kFastCig; ++o) {
+        qs[o] = 0;
+        qe[o] = 0;
+        dl[o] = 0;
+        if (o < (int)ncig) {
+            const uint32_t cg = cig[o];
+            const uint32_t op = cg & 15u;
+            const int len = (int)(cg >> 4);
+            if (op == 0 || op == 7 || op == 8) {
+                qs[o] = q;
+                qe[o] = q + len;
+                dl[o] = ref - q;
+                q += len;
+                ref += len;
+            } else if (op == 2 || op == 3) {
+                ref += len;
+            } else if (op == 4) {
+                q += len;
+            }
+        }
+    }
+    if ((int64_t)max(ref - start, (int)lseq) > (int64_t)max_span) span_err = true;
+
+    const uint4* qv = reinterpret_cast<const uint4*>(rec + 16);
+    uint32_t qw[kFastLen / 4];
+#pragma unroll
+    for (int k = 0; k < kFastLen / 16; ++k) {
+        const uint4 v = qv[k];
+        qw[4 * k] = v.x;
+        qw[4 * k + 1] = v.y;
+        qw[4 * k + 2] = v.z;
+        qw[4 * k + 3] = v.w;
+    }
+    // seq: 4-byte aligned dword loads, realigned with v_alignbyte
+    const uintptr_t sa = reinterpret_cast<uintptr_t>(rec) + 16 + lseq;
+    const uint32_t* sp = reinterpret_cast<const uint32_t*>(sa & ~uintptr_t(3));
+    const uint32_t sh = (uint32_t)(sa & 3) * 8u;
+    uint32_t raw[kFastLen / 8 + 1];
+#pragma unroll
+    for (int k = 0; k < kFastLen / 8 + 1; ++k) raw[k] = sp[k];
+    uint32_t sw[kFastLen / 8];
+#pragma unroll
+    for (int k = 0; k < kFastLen / 8; ++k)
+        sw[k] = (uint32_t)((((unsigned long long)raw[k + 1] << 32) | raw[k]) >> sh);
+
+    const int vq0 = pc.min_dist > 0 ? pc.min_dist : 0;
+    const int vq1 = min((int)lseq, pc.min_dist > 0 ? (int)lseq - pc.min_dist : (int)lseq);
+    const int wlo = w.w0, whi = w.w0 + w.wlen;
+    uint32_t* plane = tile + strand * w.Wp - w.w0;
+#pragma unroll
+    for (int qq = 0; qq < kFastLen; ++qq) {
+        int d = 0;
+        bool inb = false;
+#pragma unroll
+        for (int o = 0; o < kFastCig; ++o) {
+            const bool hit = qq >= qs[o] && qq < qe[o];
+            d = hit ? dl[o] : d;
+            inb |= hit;
+        }
+        const int r = qq + d;
+        const int qb = (int)(int8_t)((qw[qq >> 2] >> (8 * (qq & 3))) & 0xFFu);
+        const uint32_t code = (sw[qq >> 3] >> (8 * ((qq >> 1) & 3) + ((qq & 1) ? 0 : 4))) & 15u;
+        const int bi = (int)((kCodeLut >> (4 * code)) & 15ull);
+        const bool ok = inb && qq >= vq0 && qq < vq1 && r >= wlo && r < whi && qb >= pc.min_baseq && bi < 4;
+        if (ok) atomicAdd(&plane[2 * bi * w.Wp + r], 1u);
+    }
+}
+
+__device__ __forceinline__ void pile_read(const uint8_t* __restrict__ rec, const Win& w, const PileCfg& pc,
+                                          uint32_t* tile, uint32_t* t5, uint32_t max_span, bool& span_err) {
+    const uint4 h = *reinterpret_cast<const uint4*>(rec);
+    const int32_t start = (int32_t)h.x;
+    const uint32_t lseq = h.y;
+    const uint32_t ncig = h.z & 0xFFFFu;
+    const uint32_t flag = h.z >> 16;
+    const uint32_t coff = h.w;
+    const int strand = (flag & MGP_FLAG_REVERSE) ? 1 : 0;
+    tn5_cut(start, lseq, strand, w, t5);
+    // fast path only when every reference coordinate stays far from int32 overflow
+    if (lseq <= (uint32_t)kFastLen && ncig <= (uint32_t)kFastCig && start >= -(1 << 28) && start < (1 << 28) &&
+        max_span < (1u << 28))
+        pile_fast(rec, start, lseq, ncig, coff, strand, w, pc, tile, max_span, span_err);
+    else
+        pile_slow(rec, start, lseq, ncig, coff, strand, w, pc, tile, max_span, span_err);
 }
 
 constexpr int kMaxPosPerThread = 8;  // W <= 8 * 256
 
-// grid (nchunks, nwin): workgroup = (cell chunk, position window); the LDS tile
-// holds 8 count planes + 2 Tn5 planes of Wp u32 each.
+// grid (nchunks, nwin): workgroup = (cell chunk, position window). For each cell
+// of the chunk: the cell's grouping elements whose start bin lies in
+// [window start - reach, window end) are deduplicated (walk back over equal
+// starts: first in BAM order wins) and piled into the LDS tile (8 count planes +
+// 2 Tn5 planes of Wp u32), then the tile is strand-filtered and flushed.
 __global__ void __launch_bounds__(kBlock) k_pileup(
-    Geom g, PileCfg pc, const uint8_t* __restrict__ payload, const uint64_t* __restrict__ p_off,
-    const uint32_t* __restrict__ base, const uint32_t* __restrict__ edges, const uint32_t* __restrict__ n_reads,
-    uint32_t* __restrict__ counts, uint32_t* __restrict__ tn5, uint32_t* __restrict__ depth,
+    Geom g, PileCfg pc, const uint8_t* __restrict__ payload, const GElem* __restrict__ gel,
+    const uint32_t* __restrict__ O, uint32_t* __restrict__ counts, uint32_t* __restrict__ tn5,
+    uint32_t* __restrict__ depth, uint32_t* __restrict__ n_reads, uint8_t* __restrict__ any_paired,
     uint32_t* __restrict__ covered, unsigned long long* __restrict__ dsum, uint32_t* __restrict__ dmax,
     uint32_t* __restrict__ tally_part, DevStats* st) {
     extern __shared__ uint32_t tile[];  // [10][Wp]
     uint32_t* t5 = tile + 8 * g.Wp;
-    __shared__ uint32_t r_cov[4], r_max[4];
+    __shared__ uint32_t r_cov[4], r_max[4], r_keep[4];
     __shared__ unsigned long long r_sum[4];
+    __shared__ int r_pair[4];
 
     const int k = blockIdx.y;
     const int chunk = blockIdx.x;
-    const int w0 = k * g.W;
-    const int wlen = min(g.W, g.L - w0);
+    Win w;
+    w.w0 = k * g.W;
+    w.wlen = min(g.W, g.L - w.w0);
+    w.Wp = g.Wp;
     const int L = g.L;
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const uint32_t max_span = st->max_span;
-    const int min_reads = max(1, pc.min_reads);
-    bool span_err = false;
+    const int R = (int)((max_span + g.G - 1) / g.G) * g.G;
+    const int lo_bin = win_lo_bin(k, R, g);
+    const int own_bin = (int)((long long)k * g.W / g.G);
+    const int hi_bin = k == g.nwin - 1 ? g.nbins : win_hi_bin(k, g);
+    const int nc = g.nc;
+    bool span_err = false, bad = false;
+    unsigned long long d2 = 0, d3 = 0;
 
     uint32_t tal[kMaxPosPerThread][4];
 #pragma unroll
@@ -574,25 +554,55 @@ __global__ void __launch_bounds__(kBlock) k_pileup(
 #pragma unroll
         for (int b = 0; b < 4; ++b) tal[m][b] = 0;
 
-    const int c0 = chunk * g.cpb, c1 = min(g.nc, c0 + g.cpb);
+    const int c0 = chunk * g.cpb, c1 = min(nc, c0 + g.cpb);
     for (int c = c0; c < c1; ++c) {
         for (int x = threadIdx.x; x < 10 * g.Wp; x += blockDim.x) tile[x] = 0;
         __syncthreads();
-        const bool gate = n_reads[c] >= (uint32_t)min_reads;
-        if (gate) {
-            const uint32_t sb = base[c];
-            const uint32_t lo = sb + edges[(size_t)c * 2 * g.nwin + 2 * k];
-            const uint32_t hi = sb + edges[(size_t)c * 2 * g.nwin + 2 * k + 1];
-            for (uint32_t j = lo + threadIdx.x; j < hi; j += blockDim.x)
-                pile_read(payload + p_off[j], w0, wlen, pc, g.Wp, tile, t5, max_span, span_err);
+        const uint32_t lo = O[(size_t)lo_bin * nc + c];
+        const uint32_t own = O[(size_t)own_bin * nc + c];
+        const uint32_t hi = O[(size_t)hi_bin * nc + c];
+        uint32_t nkeep = 0;
+        bool paired = false;
+        for (uint32_t j = lo + threadIdx.x; j < hi; j += blockDim.x) {
+            const GElem e = gel[j];
+            bool dup2 = false, dup3 = false;
+            if (pc.dedup_mode != MGP_DEDUP_NONE) {
+                // duplicates share the exact start and sit just before j (BAM order)
+                for (uint32_t m = j; m-- > lo;) {
+                    const GElem p = gel[m];
+                    if (p.start != e.start) break;
+                    if (((p.w ^ e.w) & GM_REV) == 0ull) {
+                        dup2 = true;
+                        if (p.tlen == e.tlen) {
+                            dup3 = true;
+                            break;
+                        }
+                    }
+                }
+            }
+            const bool keep = pc.dedup_mode == MGP_DEDUP_NONE ? true
+                              : pc.dedup_mode == MGP_DEDUP_START ? !dup2
+                                                                 : !dup3;
+            if (j >= own) {  // statistics counted once, by the window that owns the start bin
+                d2 += dup2;
+                d3 += dup3;
+                if (keep) {
+                    ++nkeep;
+                    paired |= (e.w & GM_PAIRED) != 0ull;
+                    bad |= (e.w & GM_BAD) != 0ull;
+                }
+            }
+            if (keep && (e.w & GM_MAPQ_OK)) pile_read(payload + (e.w & GM_OFF), w, pc, tile, t5, max_span, span_err);
         }
+        nkeep = wave_sum(nkeep);
+        const bool anyp = __ballot(paired) != 0ull;
         __syncthreads();
         uint32_t cov = 0, mx = 0;
         unsigned long long sum = 0;
 #pragma unroll
         for (int m = 0; m < kMaxPosPerThread; ++m) {
             const int p = threadIdx.x + m * kBlock;
-            if (p < wlen) {
+            if (p < w.wlen) {
                 uint32_t v[8];
 #pragma unroll
                 for (int x = 0; x < 8; ++x) v[x] = tile[x * g.Wp + p];
@@ -614,7 +624,7 @@ __global__ void __launch_bounds__(kBlock) k_pileup(
                 }
                 uint32_t tf = t5[p], tr = t5[g.Wp + p];
                 if (d == 0) tf = tr = 0;
-                const size_t P = (size_t)c * L + w0 + p;
+                const size_t P = (size_t)c * L + w.w0 + p;
                 uint4* cp = reinterpret_cast<uint4*>(counts + P * 8);
                 cp[0] = make_uint4(v[0], v[1], v[2], v[3]);
                 cp[1] = make_uint4(v[4], v[5], v[6], v[7]);
@@ -625,41 +635,87 @@ __global__ void __launch_bounds__(kBlock) k_pileup(
                 mx = d > mx ? d : mx;
             }
         }
-        if (gate) {
-            cov = wave_sum(cov);
-            sum = wave_sum(sum);
-            mx = wave_max(mx);
-            if (lane == 0) {
-                r_cov[wid] = cov;
-                r_sum[wid] = sum;
-                r_max[wid] = mx;
-            }
+        cov = wave_sum(cov);
+        sum = wave_sum(sum);
+        mx = wave_max(mx);
+        if (lane == 0) {
+            r_cov[wid] = cov;
+            r_sum[wid] = sum;
+            r_max[wid] = mx;
+            r_keep[wid] = nkeep;
+            r_pair[wid] = anyp;
         }
         __syncthreads();
-        if (gate && threadIdx.x == 0) {
-            uint32_t C = 0, M = 0;
+        if (threadIdx.x == 0) {
+            uint32_t C = 0, M = 0, K = 0;
             unsigned long long S = 0;
-            for (int w = 0; w < 4; ++w) {
-                C += r_cov[w];
-                S += r_sum[w];
-                M = max(M, r_max[w]);
+            int PP = 0;
+            for (int q = 0; q < 4; ++q) {
+                C += r_cov[q];
+                S += r_sum[q];
+                M = max(M, r_max[q]);
+                K += r_keep[q];
+                PP |= r_pair[q];
             }
             if (C) {
                 atomicAdd(&covered[c], C);
                 atomicAdd(&dsum[c], S);
                 atomicMax(&dmax[c], M);
             }
+            if (K) atomicAdd(&n_reads[c], K);
+            if (PP) any_paired[c] = 1;  // benign race: every writer stores 1
         }
     }
 #pragma unroll
     for (int m = 0; m < kMaxPosPerThread; ++m) {
         const int p = threadIdx.x + m * kBlock;
-        if (p < wlen) {
-            uint4* tp = reinterpret_cast<uint4*>(tally_part + ((size_t)chunk * L + w0 + p) * 4);
+        if (p < w.wlen) {
+            uint4* tp = reinterpret_cast<uint4*>(tally_part + ((size_t)chunk * L + w.w0 + p) * 4);
             *tp = make_uint4(tal[m][0], tal[m][1], tal[m][2], tal[m][3]);
         }
     }
-    if (span_err) atomicOr(&st->err, ERR_SPAN);
+    d2 = wave_sum(d2);
+    d3 = wave_sum(d3);
+    const bool anyspan = __ballot(span_err) != 0ull, anybad = __ballot(bad) != 0ull;
+    if (lane == 0) {
+        if (d2) atomicAdd(&st->dup_pos, d2);
+        if (d3) atomicAdd(&st->dup_len, d3);
+        if (anyspan) atomicOr(&st->err, ERR_SPAN);
+        if (anybad) atomicOr(&st->err, ERR_BADREAD);
+    }
+}
+
+// min-reads gate (processors.py:22) for min_reads > 1: a cell with fewer kept
+// reads produces no result; remove its counts and its tally contribution.
+__global__ void __launch_bounds__(kBlock) k_gate_fixup(Geom g, int min_reads, const uint32_t* __restrict__ n_reads,
+                                                       uint32_t* __restrict__ counts, uint32_t* __restrict__ tn5,
+                                                       uint32_t* __restrict__ depth, uint32_t* __restrict__ covered,
+                                                       unsigned long long* __restrict__ dsum,
+                                                       uint32_t* __restrict__ dmax, uint32_t* __restrict__ tally_part) {
+    const int c = blockIdx.x;
+    const uint32_t nr = n_reads[c];
+    if (nr == 0 || nr >= (uint32_t)min_reads || covered[c] == 0) return;
+    const int L = g.L;
+    uint32_t* tp = tally_part + (size_t)(c / g.cpb) * L * 4;
+    for (int p = threadIdx.x; p < L; p += blockDim.x) {
+        const size_t P = (size_t)c * L + p;
+        if (depth[P] == 0) continue;
+        uint4* cp = reinterpret_cast<uint4*>(counts + P * 8);
+        const uint4 a = cp[0], b = cp[1];
+        const uint32_t t[4] = {a.x + a.y, a.z + a.w, b.x + b.y, b.z + b.w};
+        for (int q = 0; q < 4; ++q)
+            if (t[q]) atomicSub(&tp[(size_t)p * 4 + q], t[q]);
+        cp[0] = make_uint4(0, 0, 0, 0);
+        cp[1] = make_uint4(0, 0, 0, 0);
+        reinterpret_cast<uint2*>(tn5)[P] = make_uint2(0, 0);
+        depth[P] = 0;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        covered[c] = 0;
+        dsum[c] = 0;
+        dmax[c] = 0;
+    }
 }
 
 // Radix select of the k-th smallest (0-based) among vals[0..n) in LDS.
@@ -707,7 +763,12 @@ __global__ void __launch_bounds__(kBlock) k_median(Geom g, int min_reads, const 
     __shared__ uint32_t cnt;
     const int c = blockIdx.x;
     const uint32_t n = covered[c];
-    const bool pass = n > 0 && n_reads[c] >= (uint32_t)max(1, min_reads);
+    const uint32_t nr = n_reads[c];
+    const bool pass = n > 0 && nr >= (uint32_t)max(1, min_reads);
+    if (threadIdx.x == 0 && nr) {
+        atomicAdd(&st->filtered, (unsigned long long)nr);
+        atomicAdd(&st->n_barcodes, 1ull);
+    }
     if (!pass) {
         if (threadIdx.x == 0) {
             med_lo[c] = 0;
@@ -864,9 +925,8 @@ void mgp_close(mgp_ctx* ctx) {
     if (ctx->comm) ncclCommDestroy(ctx->comm);
     DevBuf* bufs[] = {&ctx->start,     &ctx->bc,        &ctx->tlen,     &ctx->flag,       &ctx->mapq,
                       &ctx->span,      &ctx->roff,      &ctx->payload,  &ctx->bin_start,  &ctx->rank,
-                      &ctx->H,         &ctx->P,         &ctx->cell_cnt, &ctx->cell_base,  &ctx->g_idx,
-                      &ctx->g_start,   &ctx->g_tlen,    &ctx->g_info,   &ctx->g_off,      &ctx->p_off,
-                      &ctx->edges,     &ctx->tally_part, &ctx->tally,   &ctx->n_reads,    &ctx->any_paired,
+                      &ctx->H,         &ctx->P,         &ctx->cell_cnt, &ctx->cell_base,  &ctx->gel,
+                      &ctx->tally_part, &ctx->tally,   &ctx->n_reads,    &ctx->any_paired,
                       &ctx->passed,    &ctx->covered,   &ctx->dsum,     &ctx->dmax,       &ctx->med_lo,
                       &ctx->med_hi,    &ctx->first_read, &ctx->counts,  &ctx->tn5,        &ctx->depth,
                       &ctx->stats};
@@ -893,7 +953,7 @@ static int ensure_inputs(mgp_ctx* ctx, int64_t n_total, int64_t pay_total, bool 
     MGP_TRY(ctx->mapq.ensure(n, preserve, used, s));
     MGP_TRY(ctx->span.ensure(n * 4, preserve, used * 4, s));
     MGP_TRY(ctx->roff.ensure(n * 8, preserve, used * 8, s));
-    MGP_TRY(ctx->payload.ensure((size_t)pay_total + 16, preserve, preserve ? (size_t)ctx->pay : 0, s));
+    MGP_TRY(ctx->payload.ensure((size_t)pay_total + 256, preserve, preserve ? (size_t)ctx->pay : 0, s));
     return MGP_OK;
 }
 
@@ -960,13 +1020,7 @@ static int ensure_run_buffers(mgp_ctx* ctx) {
     MGP_TRY(ctx->P.ensure((size_t)((g.nbins + 31) / 32 + 1) * nc * 4));
     MGP_TRY(ctx->cell_cnt.ensure(nc * 4));
     MGP_TRY(ctx->cell_base.ensure(nc * 4));
-    MGP_TRY(ctx->g_idx.ensure(n * 4));
-    MGP_TRY(ctx->g_start.ensure(n * 4));
-    MGP_TRY(ctx->g_tlen.ensure(n * 4));
-    MGP_TRY(ctx->g_info.ensure(n));
-    MGP_TRY(ctx->g_off.ensure(n * 8));
-    MGP_TRY(ctx->p_off.ensure(n * 8));
-    MGP_TRY(ctx->edges.ensure(nc * 2 * g.nwin * 4));
+    MGP_TRY(ctx->gel.ensure(n * sizeof(GElem)));
     MGP_TRY(ctx->tally_part.ensure((size_t)std::max(g.nchunks, 1) * L * 16));
     MGP_TRY(ctx->tally.ensure(L * 4 * 8));
     MGP_TRY(ctx->n_reads.ensure(nc * 4));
@@ -1006,6 +1060,9 @@ int mgp_run(mgp_ctx* ctx) {
         HIP_TRY(hipMemsetAsync(ctx->covered.p, 0, (size_t)nc * 4, s));
         HIP_TRY(hipMemsetAsync(ctx->dsum.p, 0, (size_t)nc * 8, s));
         HIP_TRY(hipMemsetAsync(ctx->dmax.p, 0, (size_t)nc * 4, s));
+        HIP_TRY(hipMemsetAsync(ctx->n_reads.p, 0, (size_t)nc * 4, s));
+        HIP_TRY(hipMemsetAsync(ctx->any_paired.p, 0, (size_t)nc, s));
+        HIP_TRY(hipMemsetAsync(ctx->first_read.p, 0xFF, (size_t)nc * 4, s));
     }
 
     // 1. start-bin boundaries
@@ -1019,19 +1076,22 @@ int mgp_run(mgp_ctx* ctx) {
     STAGE_END(ST_BINS);
 
     if (nc > 0) {
-        // 2. (bin, cell) histogram + ranks
+        // 2. (bin, cell) histogram + stable ranks
         STAGE_BEGIN(ST_HIST);
         const bool lds = nc <= ctx->lds_hist_max_cells;
+        int cbits = 1;
+        while (cbits < 31 && (1 << cbits) < nc) ++cbits;
         if (!lds || n == 0) HIP_TRY(hipMemsetAsync(ctx->H.p, 0, (size_t)(g.nbins + 1) * nc * 4, s));
         if (n > 0) {
             if (lds)
-                k_bin_hist<true><<<g.nbins, kBlock, (size_t)nc * 4, s>>>(
+                k_bin_hist<true><<<g.nbins, kWave, (size_t)nc * 4, s>>>(
                     ctx->bin_start.as<uint32_t>(), ctx->bc.as<int32_t>(), ctx->flag.as<uint16_t>(),
-                    ctx->span.as<uint32_t>(), n, g, ctx->H.as<uint32_t>(), ctx->rank.as<uint32_t>(), st);
+                    ctx->span.as<uint32_t>(), n, g, cbits, ctx->H.as<uint32_t>(), ctx->rank.as<uint32_t>(), st);
             else
-                k_bin_hist<false><<<g.nbins, kBlock, 0, s>>>(ctx->bin_start.as<uint32_t>(), ctx->bc.as<int32_t>(),
-                                                             ctx->flag.as<uint16_t>(), ctx->span.as<uint32_t>(), n, g,
-                                                             ctx->H.as<uint32_t>(), ctx->rank.as<uint32_t>(), st);
+                k_bin_hist<false><<<g.nbins, kWave, 0, s>>>(ctx->bin_start.as<uint32_t>(), ctx->bc.as<int32_t>(),
+                                                            ctx->flag.as<uint16_t>(), ctx->span.as<uint32_t>(), n, g,
+                                                            cbits, ctx->H.as<uint32_t>(), ctx->rank.as<uint32_t>(),
+                                                            st);
             HIP_TRY(hipGetLastError());
         }
         STAGE_END(ST_HIST);
@@ -1049,48 +1109,48 @@ int mgp_run(mgp_ctx* ctx) {
         HIP_TRY(hipGetLastError());
         STAGE_END(ST_SCAN);
 
-        // 4. scatter grouping records
+        // 4. scatter grouping elements
         STAGE_BEGIN(ST_SCATTER);
         if (n > 0) {
             k_scatter<<<blocks_for(n), kBlock, 0, s>>>(
                 n, ctx->start.as<int32_t>(), ctx->bc.as<int32_t>(), ctx->tlen.as<int32_t>(), ctx->flag.as<uint16_t>(),
                 ctx->mapq.as<uint8_t>(), ctx->roff.as<uint64_t>(), ctx->rank.as<uint32_t>(), ctx->H.as<uint32_t>(), g,
-                ctx->cfg.min_mapq, ctx->g_idx.as<uint32_t>(), ctx->g_start.as<int32_t>(), ctx->g_tlen.as<uint32_t>(),
-                ctx->g_info.as<uint8_t>(), ctx->g_off.as<uint64_t>(), st);
+                ctx->cfg.min_mapq, ctx->gel.as<GElem>(), ctx->first_read.as<uint32_t>(), st);
             HIP_TRY(hipGetLastError());
         }
         STAGE_END(ST_SCATTER);
 
-        // 5. dedup + compaction + window ranges
-        STAGE_BEGIN(ST_DEDUP);
-        const size_t dsm = (size_t)(2 * g.nwin + kBlock) * 4;
-        k_dedup<<<nc, kBlock, dsm, s>>>(g, ctx->cfg.dedup_mode, ctx->cell_base.as<uint32_t>(),
-                                        ctx->cell_cnt.as<uint32_t>(), ctx->g_idx.as<uint32_t>(),
-                                        ctx->g_start.as<int32_t>(), ctx->g_tlen.as<uint32_t>(),
-                                        ctx->g_info.as<uint8_t>(), ctx->g_off.as<uint64_t>(), ctx->p_off.as<uint64_t>(),
-                                        ctx->edges.as<uint32_t>(), ctx->n_reads.as<uint32_t>(),
-                                        ctx->any_paired.as<uint8_t>(), ctx->first_read.as<uint32_t>(), st);
-        HIP_TRY(hipGetLastError());
-        STAGE_END(ST_DEDUP);
-
-        // 6. pileup
+        // 5. dedup + pileup + strand filter + stats
         STAGE_BEGIN(ST_PILEUP);
         PileCfg pc;
         pc.min_baseq = ctx->cfg.min_baseq;
         pc.min_dist = ctx->cfg.min_dist_from_end;
         pc.min_reads = ctx->cfg.min_reads;
+        pc.dedup_mode = ctx->cfg.dedup_mode;
         pc.max_bias = ctx->cfg.max_strand_bias;
         pc.bias_active = ctx->cfg.max_strand_bias < 1.0;
         dim3 gp(g.nchunks, g.nwin);
         const size_t psm = (size_t)10 * g.Wp * 4;
-        k_pileup<<<gp, kBlock, psm, s>>>(g, pc, ctx->payload.as<uint8_t>(), ctx->p_off.as<uint64_t>(),
-                                         ctx->cell_base.as<uint32_t>(), ctx->edges.as<uint32_t>(),
-                                         ctx->n_reads.as<uint32_t>(), ctx->counts.as<uint32_t>(),
-                                         ctx->tn5.as<uint32_t>(), ctx->depth.as<uint32_t>(),
-                                         ctx->covered.as<uint32_t>(), ctx->dsum.as<unsigned long long>(),
-                                         ctx->dmax.as<uint32_t>(), ctx->tally_part.as<uint32_t>(), st);
+        k_pileup<<<gp, kBlock, psm, s>>>(g, pc, ctx->payload.as<uint8_t>(), ctx->gel.as<GElem>(),
+                                         ctx->H.as<uint32_t>(), ctx->counts.as<uint32_t>(), ctx->tn5.as<uint32_t>(),
+                                         ctx->depth.as<uint32_t>(), ctx->n_reads.as<uint32_t>(),
+                                         ctx->any_paired.as<uint8_t>(), ctx->covered.as<uint32_t>(),
+                                         ctx->dsum.as<unsigned long long>(), ctx->dmax.as<uint32_t>(),
+                                         ctx->tally_part.as<uint32_t>(), st);
         HIP_TRY(hipGetLastError());
         STAGE_END(ST_PILEUP);
+
+        // 6. min-reads gate
+        if (ctx->cfg.min_reads > 1) {
+            STAGE_BEGIN(ST_GATE);
+            k_gate_fixup<<<nc, kBlock, 0, s>>>(g, ctx->cfg.min_reads, ctx->n_reads.as<uint32_t>(),
+                                               ctx->counts.as<uint32_t>(), ctx->tn5.as<uint32_t>(),
+                                               ctx->depth.as<uint32_t>(), ctx->covered.as<uint32_t>(),
+                                               ctx->dsum.as<unsigned long long>(), ctx->dmax.as<uint32_t>(),
+                                               ctx->tally_part.as<uint32_t>());
+            HIP_TRY(hipGetLastError());
+            STAGE_END(ST_GATE);
+        }
 
         // 7. medians + pass flags
         STAGE_BEGIN(ST_MEDIAN);

@@ -73,8 +73,10 @@ __device__ __forceinline__ Cig cig_of(uint64_t seed, int64_t i) {
     return c;
 }
 
+__device__ __forceinline__ int cigar_offset(int rl) { return (16 + rl + (rl + 1) / 2 + 3) & ~3; }
+
 __device__ __forceinline__ uint64_t rec_size(int ncig, int rl) {
-    return (uint64_t)((16 + 4 * ncig + rl + (rl + 1) / 2 + 7) & ~7);
+    return (uint64_t)((cigar_offset(rl) + 4 * ncig + 15) & ~15);
 }
 
 __global__ void k_synth_sizes(uint64_t seed, int64_t n, int rl, uint64_t* __restrict__ sz) {
@@ -220,8 +222,8 @@ __global__ void k_synth_fill(uint64_t seed, int64_t n, int rl, int nc, int L, co
     *reinterpret_cast<uint32_t*>(rec + 4) = (uint32_t)rl;
     *reinterpret_cast<uint16_t*>(rec + 8) = (uint16_t)cg.n;
     *reinterpret_cast<uint16_t*>(rec + 10) = f;
-    *reinterpret_cast<uint32_t*>(rec + 12) = 0;
-    uint32_t* cig = reinterpret_cast<uint32_t*>(rec + 16);
+    *reinterpret_cast<uint32_t*>(rec + 12) = (uint32_t)cigar_offset(rl);
+    uint32_t* cig = reinterpret_cast<uint32_t*>(rec + cigar_offset(rl));
     if (cg.cls == C_M) {
         cig[0] = ((uint32_t)rl << 4) | 0;
     } else if (cg.cls == C_S) {
@@ -236,7 +238,7 @@ __global__ void k_synth_fill(uint64_t seed, int64_t n, int rl, int nc, int L, co
         cig[1] = ((uint32_t)cg.b << 4) | 2;
         cig[2] = ((uint32_t)(rl - cg.a) << 4) | 0;
     }
-    uint8_t* qual = rec + 16 + 4 * cg.n;
+    uint8_t* qual = rec + 16;
     uint8_t* seq = qual + rl;
     const uint8_t kCodes[4] = {1, 2, 4, 8};
     uint8_t hi_nib = 0;

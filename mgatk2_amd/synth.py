@@ -181,7 +181,7 @@ def concat_soa(parts: list[ReadSoA]) -> ReadSoA:
     base = 0
     for p in parts:
         base = (base + 15) & ~15
-        offs.append(p.rec_off + np.uint64(base))
+        offs.append(p.rec_off + np.uint64(base))  # records stay 16-byte aligned
         pad = base - sum(x.shape[0] for x in pay)
         if pad:
             pay.append(np.zeros(pad, np.uint8))
@@ -199,8 +199,14 @@ def concat_soa(parts: list[ReadSoA]) -> ReadSoA:
     )
 
 
+def cigar_offset(lseq):
+    """Byte offset of the CIGAR inside a record (include/mgpileup.h)."""
+    lseq = np.asarray(lseq, np.int64)
+    return (16 + lseq + (lseq + 1) // 2 + 3) & ~3
+
+
 def rec_size(ncig, lseq):
-    return (16 + 4 * np.asarray(ncig, np.int64) + np.asarray(lseq, np.int64) + (np.asarray(lseq, np.int64) + 1) // 2 + 7) & ~7
+    return (cigar_offset(lseq) + 4 * np.asarray(ncig, np.int64) + 15) & ~15
 
 
 def _synth_chunk(seed, i0, i1, n, read_len, n_cells, mito_len, cdf, ref):
@@ -318,26 +324,27 @@ def _pack_fixed(start, flag, ncig, cig, qual, code, rl):
         roff[1:] = np.cumsum(sizes[:-1]).astype(np.uint64)
     total = int(sizes.sum())
     pay = np.zeros(total, np.uint8)
-    hdr = np.zeros(m, dtype=[("start", "<i4"), ("lseq", "<u4"), ("ncig", "<u2"), ("flag", "<u2"), ("rsv", "<u4")])
+    coff = int(cigar_offset(rl))
+    hdr = np.zeros(m, dtype=[("start", "<i4"), ("lseq", "<u4"), ("ncig", "<u2"), ("flag", "<u2"), ("coff", "<u4")])
     hdr["start"] = start
     hdr["lseq"] = rl
     hdr["ncig"] = ncig
     hdr["flag"] = flag
+    hdr["coff"] = coff
     hb = hdr.view(np.uint8).reshape(m, 16)
     ro = roff.astype(np.int64)
     pay[ro[:, None] + np.arange(16)[None, :]] = hb
-    cb = cig.astype("<u4").view(np.uint8).reshape(m, -1)
-    for k in range(cig.shape[1]):
-        sel = ncig > k
-        pay[(ro[sel, None] + 16 + 4 * k + np.arange(4)[None, :])] = cb[sel, 4 * k : 4 * k + 4]
-    qoff = ro + 16 + 4 * ncig
-    pay[qoff[:, None] + np.arange(rl)[None, :]] = qual
+    pay[(ro + 16)[:, None] + np.arange(rl)[None, :]] = qual
     nb = (rl + 1) // 2
     c = code
     if rl & 1:
         c = np.concatenate([c, np.zeros((m, 1), np.uint8)], axis=1)
     packed = ((c[:, 0::2] << 4) | c[:, 1::2]).astype(np.uint8)
-    pay[(qoff + rl)[:, None] + np.arange(nb)[None, :]] = packed
+    pay[(ro + 16 + rl)[:, None] + np.arange(nb)[None, :]] = packed
+    cb = cig.astype("<u4").view(np.uint8).reshape(m, -1)
+    for k in range(cig.shape[1]):
+        sel = ncig > k
+        pay[(ro[sel, None] + coff + 4 * k + np.arange(4)[None, :])] = cb[sel, 4 * k : 4 * k + 4]
     return roff, pay
 
 
@@ -421,23 +428,23 @@ def pack_reads(reads: list[dict]) -> ReadSoA:
         span[i] = max(cigar_ref_span(cig), lseq)
         roff[i] = off
         size = int(rec_size(len(cig), lseq))
+        coff = int(cigar_offset(lseq))
         rec = np.zeros(size, np.uint8)
-        hdr = np.array([(start[i], lseq, len(cig), f, 0)],
-                       dtype=[("s", "<i4"), ("l", "<u4"), ("n", "<u2"), ("f", "<u2"), ("r", "<u4")])
+        hdr = np.array([(start[i], lseq, len(cig), f, coff)],
+                       dtype=[("s", "<i4"), ("l", "<u4"), ("n", "<u2"), ("f", "<u2"), ("c", "<u4")])
         rec[:16] = hdr.view(np.uint8)
-        if cig:
-            rec[16 : 16 + 4 * len(cig)] = np.array([(ln << 4) | op for op, ln in cig], "<u4").view(np.uint8)
-        q0 = 16 + 4 * len(cig)
         if lseq:
             if qual is not None:
-                rec[q0 : q0 + lseq] = np.asarray(qual, dtype=np.int64) & 0xFF
+                rec[16 : 16 + lseq] = np.asarray(qual, dtype=np.int64) & 0xFF
             else:
-                rec[q0 : q0 + lseq] = 0xFF
+                rec[16 : 16 + lseq] = 0xFF
             codes = [_NT16_IDX[ch] for ch in seq.upper()] if seq is not None else []
             if lseq & 1:
                 codes.append(0)
             codes = np.array(codes, np.uint8)
-            rec[q0 + lseq : q0 + lseq + (lseq + 1) // 2] = (codes[0::2] << 4) | codes[1::2]
+            rec[16 + lseq : 16 + lseq + (lseq + 1) // 2] = (codes[0::2] << 4) | codes[1::2]
+        if cig:
+            rec[coff : coff + 4 * len(cig)] = np.array([(ln << 4) | op for op, ln in cig], "<u4").view(np.uint8)
         chunks.append(rec)
         off += size
     payload = np.concatenate(chunks) if chunks else np.zeros(0, np.uint8)
@@ -451,10 +458,10 @@ def unpack_record(payload: np.ndarray, off: int) -> dict:
     lseq = int(hdr[4:8].view("<u4")[0])
     ncig = int(hdr[8:10].view("<u2")[0])
     flag = int(hdr[10:12].view("<u2")[0])
-    cig = payload[off + 16 : off + 16 + 4 * ncig].view("<u4").tolist() if ncig else []
-    q0 = off + 16 + 4 * ncig
-    qual = payload[q0 : q0 + lseq].tolist()
-    sb = payload[q0 + lseq : q0 + lseq + (lseq + 1) // 2]
+    coff = int(hdr[12:16].view("<u4")[0])
+    cig = payload[off + coff : off + coff + 4 * ncig].view("<u4").tolist() if ncig else []
+    qual = payload[off + 16 : off + 16 + lseq].tolist()
+    sb = payload[off + 16 + lseq : off + 16 + lseq + (lseq + 1) // 2]
     codes = np.stack([sb >> 4, sb & 15], axis=1).reshape(-1)[:lseq]
     seq = "".join(SEQ_NT16[c] for c in codes.tolist())
     return dict(

@@ -109,15 +109,16 @@ static int kset_test_add(kset_t *s, const key_t *k, int *err) {
 /* ---- one read's pileup (pileup.py:32-95) ------------------------------------ */
 static void pile_read(const uint8_t *rec, const mgp_config *cfg, uint32_t *bc8, uint32_t *tn5) {
     int32_t start;
-    uint32_t lseq;
+    uint32_t lseq, coff;
     uint16_t ncig, flag;
     memcpy(&start, rec, 4);
     memcpy(&lseq, rec + 4, 4);
     memcpy(&ncig, rec + 8, 2);
     memcpy(&flag, rec + 10, 2);
-    const uint8_t *cig = rec + 16;
-    const uint8_t *qual = rec + 16 + 4 * (size_t)ncig;
+    memcpy(&coff, rec + 12, 4);
+    const uint8_t *qual = rec + 16;
     const uint8_t *seq = qual + lseq;
+    const uint8_t *cig = rec + coff;
     const int64_t L = cfg->mito_len;
     const int is_reverse = (flag & MGP_FLAG_REVERSE) != 0;
     const int strand_idx = is_reverse ? 1 : 0;
