@@ -190,33 +190,46 @@ __global__ void __launch_bounds__(kWave) k_bin_hist(const uint32_t* __restrict__
     uint32_t mspan = 0;
     unsigned long long nvalid = 0;
     bool badbc = false;
-    for (int64_t base = lo; base < hi; base += kWave) {
-        const int64_t i = base + lane;
-        int c = -1;
-        uint16_t f = 0;
-        uint32_t sp = 0;
-        if (i < hi) {
-            c = bc[i];
-            f = flag[i];
-            sp = span[i];
+    constexpr int kAhead = 8;  // chunks of 64 reads whose loads are issued together
+    for (int64_t base = lo; base < hi; base += kAhead * kWave) {
+        int cc[kAhead];
+        uint16_t ff[kAhead];
+        uint32_t ss[kAhead];
+#pragma unroll
+        for (int u = 0; u < kAhead; ++u) {
+            const int64_t i = base + u * kWave + lane;
+            cc[u] = -1;
+            ff[u] = 0;
+            ss[u] = 0;
+            if (i < hi) {
+                cc[u] = bc[i];
+                ff[u] = flag[i];
+                ss[u] = span[i];
+            }
         }
-        badbc |= (c >= nc);
-        const bool valid = i < hi && read_valid(c, f, nc);
-        unsigned long long peers = __ballot(valid);
-        for (int bit = 0; bit < cbits; ++bit) {
-            const bool x = valid && ((c >> bit) & 1);
-            const unsigned long long m = __ballot(x);
-            peers &= x ? m : ~m;
+#pragma unroll
+        for (int u = 0; u < kAhead; ++u) {
+            const int64_t i = base + u * kWave + lane;
+            const int c = cc[u];
+            badbc |= (c >= nc);
+            const bool valid = i < hi && read_valid(c, ff[u], nc);
+            unsigned long long peers = __ballot(valid);
+            if (peers == 0ull) continue;
+            for (int bit = 0; bit < cbits; ++bit) {
+                const bool x = valid && ((c >> bit) & 1);
+                const unsigned long long m = __ballot(x);
+                peers &= x ? m : ~m;
+            }
+            if (valid) {
+                const uint32_t before = cnt[c];
+                rank[i] = before + (uint32_t)__popcll(peers & lt);
+                mspan = ss[u] > mspan ? ss[u] : mspan;
+                ++nvalid;
+                if ((peers & lt) == 0ull) cnt[c] = before + (uint32_t)__popcll(peers);  // group leader
+            }
+            if (!kLds) __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");  // leader's store before next reads
+            __builtin_amdgcn_wave_barrier();
         }
-        if (valid) {
-            const uint32_t before = cnt[c];
-            rank[i] = before + (uint32_t)__popcll(peers & lt);
-            mspan = sp > mspan ? sp : mspan;
-            ++nvalid;
-            if ((peers & lt) == 0ull) cnt[c] = before + (uint32_t)__popcll(peers);  // group leader
-        }
-        if (!kLds) __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");  // leader's store before next reads
-        __builtin_amdgcn_wave_barrier();
     }
     if (kLds) {
         __syncthreads();
@@ -750,16 +763,56 @@ __device__ uint32_t lds_select(const uint32_t* vals, uint32_t n, uint32_t kth, u
     return prefix;
 }
 
+constexpr int kMedBins = 8192;  // depth histogram bins in LDS (32 KiB)
+
+// k-th smallest (0-based) from an LDS histogram hist[0..nb): block scan over
+// per-thread bin ranges, then the owning thread walks its range.
+__device__ uint32_t hist_select(const uint32_t* hist, int nb, uint32_t kth, uint32_t* scratch) {
+    const int per = nb / kBlock;
+    const int b0 = threadIdx.x * per;
+    uint32_t mine = 0;
+    for (int b = 0; b < per; ++b) mine += hist[b0 + b];
+    // block exclusive scan of `mine`
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    uint32_t x = mine;
+    for (int o = 1; o < 64; o <<= 1) {
+        uint32_t y = __shfl_up(x, o, 64);
+        if (lane >= o) x += y;
+    }
+    if (lane == 63) scratch[wid] = x;
+    __syncthreads();
+    uint32_t woff = 0;
+    for (int w = 0; w < wid; ++w) woff += scratch[w];
+    const uint32_t excl = woff + x - mine;
+    if (kth >= excl && kth < excl + mine) {
+        uint32_t acc = excl;
+        for (int b = 0; b < per; ++b) {
+            const uint32_t h = hist[b0 + b];
+            if (kth < acc + h) {
+                scratch[4] = (uint32_t)(b0 + b);
+                break;
+            }
+            acc += h;
+        }
+    }
+    __syncthreads();
+    const uint32_t r = scratch[4];
+    __syncthreads();
+    return r;
+}
+
 // One workgroup per cell: pass flag and the two middle order statistics of the
-// covered depths (np.median, writers.py:190).
+// covered depths (np.median, writers.py:190). Depth histogram in LDS when the
+// cell's max depth fits kMedBins, radix select over the depth row otherwise.
 __global__ void __launch_bounds__(kBlock) k_median(Geom g, int min_reads, const uint32_t* __restrict__ depth,
                                                    const uint32_t* __restrict__ n_reads,
                                                    const uint32_t* __restrict__ covered,
+                                                   const uint32_t* __restrict__ dmax,
                                                    uint32_t* __restrict__ med_lo, uint32_t* __restrict__ med_hi,
                                                    uint8_t* __restrict__ passed, DevStats* st) {
-    extern __shared__ uint32_t vals[];  // [L]
+    extern __shared__ uint32_t vals[];  // [max(L, kMedBins)]
     __shared__ uint32_t hist[256];
-    __shared__ uint32_t sh[2];
+    __shared__ uint32_t sh[8];
     __shared__ uint32_t cnt;
     const int c = blockIdx.x;
     const uint32_t n = covered[c];
@@ -777,16 +830,29 @@ __global__ void __launch_bounds__(kBlock) k_median(Geom g, int min_reads, const 
         }
         return;
     }
-    if (threadIdx.x == 0) cnt = 0;
-    __syncthreads();
     const uint32_t* drow = depth + (size_t)c * g.L;
-    for (int p = threadIdx.x; p < g.L; p += blockDim.x) {
-        const uint32_t d = drow[p];
-        if (d) vals[atomicAdd(&cnt, 1u)] = d;
+    uint32_t lo, hi;
+    if (dmax[c] < (uint32_t)kMedBins) {
+        for (int b = threadIdx.x; b < kMedBins; b += blockDim.x) vals[b] = 0;
+        __syncthreads();
+        for (int p = threadIdx.x; p < g.L; p += blockDim.x) {
+            const uint32_t d = drow[p];
+            if (d) atomicAdd(&vals[d], 1u);
+        }
+        __syncthreads();
+        lo = hist_select(vals, kMedBins, (n - 1) / 2, sh);
+        hi = (n & 1) ? lo : hist_select(vals, kMedBins, n / 2, sh);
+    } else {
+        if (threadIdx.x == 0) cnt = 0;
+        __syncthreads();
+        for (int p = threadIdx.x; p < g.L; p += blockDim.x) {
+            const uint32_t d = drow[p];
+            if (d) vals[atomicAdd(&cnt, 1u)] = d;
+        }
+        __syncthreads();
+        lo = lds_select(vals, n, (n - 1) / 2, hist, sh);
+        hi = (n & 1) ? lo : lds_select(vals, n, n / 2, hist, sh);
     }
-    __syncthreads();
-    const uint32_t lo = lds_select(vals, n, (n - 1) / 2, hist, sh);
-    const uint32_t hi = (n & 1) ? lo : lds_select(vals, n, n / 2, hist, sh);
     if (threadIdx.x == 0) {
         med_lo[c] = lo;
         med_hi[c] = hi;
@@ -1154,8 +1220,10 @@ int mgp_run(mgp_ctx* ctx) {
 
         // 7. medians + pass flags
         STAGE_BEGIN(ST_MEDIAN);
-        k_median<<<nc, kBlock, (size_t)g.L * 4, s>>>(g, ctx->cfg.min_reads, ctx->depth.as<uint32_t>(),
+        k_median<<<nc, kBlock, (size_t)std::max(g.L, kMedBins) * 4, s>>>(
+                                                     g, ctx->cfg.min_reads, ctx->depth.as<uint32_t>(),
                                                      ctx->n_reads.as<uint32_t>(), ctx->covered.as<uint32_t>(),
+                                                     ctx->dmax.as<uint32_t>(),
                                                      ctx->med_lo.as<uint32_t>(), ctx->med_hi.as<uint32_t>(),
                                                      ctx->passed.as<uint8_t>(), st);
         HIP_TRY(hipGetLastError());

@@ -220,3 +220,12 @@ def test_overflow_bin_and_end_clamp(engine_lib, oracle_lib):
         _read(20000, [(0, 30)], "A" * 30, 1),
     ]
     _both(engine_lib, oracle_lib, reads, 2)
+
+
+def test_deep_cell_median_fallback(engine_lib, oracle_lib):
+    """Depth >= 8192 at some positions: the median leaves the LDS histogram path."""
+    reads = [_read(1000, [(0, 30)], "ACGT" * 7 + "AC", 0, tlen=100 + k) for k in range(9000)]
+    reads += [_read(2000 + 40 * k, [(0, 30)], "G" * 30, 0, tlen=77) for k in range(200)]
+    reads += [_read(3000, [(0, 30)], "T" * 30, 1, tlen=100 + k) for k in range(50)]
+    res = _both(engine_lib, oracle_lib, reads, 2, dedup_mode="alignment_and_fragment_length")
+    assert res.depth_max[0] >= 8192
