@@ -108,7 +108,9 @@ typedef struct mgp_config {
  *   uint32 cigar[n_cigar]           BAM encoding (len << 4 | op), at +cigar_off
  * Record size = round_up(cigar_off + 4 * n_cigar, 16); 96 bytes for a 50M read.
  * Qual sits at a fixed, 16-byte aligned offset so a kernel can load it with
- * vector loads and index its bytes statically.
+ * vector loads and index its bytes statically. Records are gathered in random
+ * order, so producers should place them at 128-byte aligned offsets (one L2
+ * line per record of <= 128 bytes); any 16-byte aligned placement is accepted.
  */
 typedef struct mgp_batch {
     int64_t         n_reads;
@@ -164,6 +166,8 @@ typedef struct mgp_synth_params {
     int32_t  n_cells;           /* must equal the context's n_cells */
     const uint32_t *cell_cdf;   /* host array [n_cells]: cumulative thresholds in [0, 2^32) */
     const uint8_t  *ref_codes;  /* host array [mito_len]: reference bases as BAM 4-bit codes */
+    int32_t  rec_align;         /* record placement: offsets are multiples of this (16..4096, pow2) */
+    int32_t  reserved;
 } mgp_synth_params;
 
 typedef struct mgp_ctx mgp_ctx;

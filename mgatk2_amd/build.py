@@ -40,17 +40,20 @@ def _stale(target: Path, deps: list[Path]) -> bool:
     return any(d.stat().st_mtime > t for d in deps)
 
 
-def build_engine(force: bool = False, verbose: bool = False) -> Path:
+def build_engine(force: bool = False, verbose: bool = False, out: Path | None = None,
+                 defines: tuple[str, ...] = ()) -> Path:
+    target = Path(out) if out else ENGINE_SO
     deps = [CSRC / s for s in HIP_SOURCES] + [CSRC / "mgp_kernels.h", ROOT / "include" / "mgpileup.h"]
-    if force or _stale(ENGINE_SO, deps):
+    if force or _stale(target, deps):
         LIB_DIR.mkdir(parents=True, exist_ok=True)
-        tmp = ENGINE_SO.with_suffix(".so.tmp")
-        cmd = [_hipcc(), *HIP_FLAGS, *[str(CSRC / s) for s in HIP_SOURCES], "-o", str(tmp), "-lrccl"]
+        tmp = target.with_suffix(".so.tmp")
+        cmd = [_hipcc(), *HIP_FLAGS, *[f"-D{d}" for d in defines], *[str(CSRC / s) for s in HIP_SOURCES],
+               "-o", str(tmp), "-lrccl"]
         if verbose:
             print(" ".join(cmd))
         subprocess.run(cmd, check=True, cwd=str(CSRC))
-        os.replace(tmp, ENGINE_SO)
-    return ENGINE_SO
+        os.replace(tmp, target)
+    return target
 
 
 def build_oracle(force: bool = False, verbose: bool = False) -> Path:

@@ -380,10 +380,15 @@ struct Win {
     int w0, wlen, Wp;
 };
 
+// LDS tile: 4 base planes + 1 Tn5 plane of Wp u32 each; every u32 packs the
+// forward count in its low 16 bits and the reverse count in its high 16 bits
+// (a window is processed in segments of < 65536 reads, so no half can carry).
+__device__ __forceinline__ uint32_t strand_inc(int strand) { return strand ? 0x10000u : 1u; }
+
 __device__ __forceinline__ void tn5_cut(int32_t start, uint32_t lseq, int strand, const Win& w, uint32_t* t5) {
     // pileup.py:43-50: reverse reads cut at start + len(seq) - 1
     const int64_t cut = strand ? (int64_t)start + lseq - 1 : (int64_t)start;
-    if (cut >= w.w0 && cut < (int64_t)w.w0 + w.wlen) atomicAdd(&t5[strand * w.Wp + (int)(cut - w.w0)], 1u);
+    if (cut >= w.w0 && cut < (int64_t)w.w0 + w.wlen) atomicAdd(&t5[(int)(cut - w.w0)], strand_inc(strand));
 }
 
 // Generic path (any read): CIGAR walk with byte loads (pileup.py:55-95).
@@ -397,7 +402,7 @@ __device__ void pile_slow(const uint8_t* __restrict__ rec, int32_t start, uint32
     const int64_t vq0 = pc.min_dist > 0 ? pc.min_dist : 0;
     const int64_t vq1 = pc.min_dist > 0 ? (int64_t)lseq - pc.min_dist : (int64_t)lseq;
     int64_t ref = start, q = 0;
-    uint32_t* plane = tile + strand * w.Wp;
+    const uint32_t inc = strand_inc(strand);
     for (uint32_t o = 0; o < ncig; ++o) {
         const uint32_t cg = cig[o];
         const uint32_t op = cg & 15u;
@@ -411,7 +416,7 @@ __device__ void pile_slow(const uint8_t* __restrict__ rec, int32_t start, uint32
                 const uint8_t sb = seq[qq >> 1];
                 const int bi = base_index((qq & 1) ? (sb & 15u) : (sb >> 4));
                 if (bi < 0) continue;
-                atomicAdd(&plane[2 * bi * w.Wp + (int)(ref + k - w.w0)], 1u);
+                atomicAdd(&tile[bi * w.Wp + (int)(ref + k - w.w0)], inc);
             }
             q += len;
             ref += len;
@@ -424,33 +429,76 @@ __device__ void pile_slow(const uint8_t* __restrict__ rec, int32_t start, uint32
     if (max(ref - (int64_t)start, (int64_t)lseq) > (int64_t)max_span) span_err = true;
 }
 
-constexpr int kFastLen = 64;   // reads up to 64 bases and 4 CIGAR ops take the register path
+constexpr int kFastLen = 64;   // reads up to 64 bases with <= 4 CIGAR ops and <= 2 aligned blocks
 constexpr int kFastCig = 4;
-// 4-bit BAM code -> base index (1->A 2->C 4->G 8->T), 15 = skip
-constexpr unsigned long long kCodeLut = 0xFFFFFFF3FFF2F10Full;
+constexpr uint32_t kLut2 = 0x30210u;   // 4-bit BAM code -> base index (1->0 A, 2->1 C, 4->2 G, 8->3 T)
+constexpr uint32_t kValid = 0x0116u;   // codes 1, 2, 4, 8 are counted (pileup.py:83-86)
 
-// Register path: qual (16-byte aligned at +16) and seq are loaded into registers
-// once; the per-base loop is fully unrolled so every byte index is static.
-__device__ __forceinline__ void pile_fast(const uint8_t* __restrict__ rec, int32_t start, uint32_t lseq,
-                                          uint32_t ncig, uint32_t coff, int strand, const Win& w,
-                                          const PileCfg& pc, uint32_t* tile, uint32_t max_span, bool& span_err) {
-    // CIGAR -> up to 4 aligned blocks [qs, qe) with r = q + dl (insertions do not move q: pileup.py Q1)
-    const uint32_t* cig = reinterpret_cast<const uint32_t*>(rec + coff);
-    int qs[kFastCig], qe[kFastCig], dl[kFastCig];
-    int ref = start, q = 0;
+// One read per lane, entered by EVERY lane of the wave (has = lane holds a read):
+// the unrolled loop bounds are wave reductions, so no lane may be absent.
+//
+// Register path (l_seq <= 64, <= 4 CIGAR ops, <= 2 aligned blocks): the CIGAR
+// becomes two blocks; for block k the counted query positions are
+// [a_k, b_k) = [qs_k, qe_k) intersected with the end-distance window [vq0, vq1)
+// and with the reference window (r = q + d_k in [w0, w0 + wlen)). Insertions do
+// not move q (pileup.py Q1: no branch for op 1). qual sits 16-byte aligned at +16
+// and is loaded together with the header; the per-base loop is unrolled so every
+// register index is static. Other reads take the generic byte-load path.
+#ifndef MGP_ABL
+#define MGP_ABL 0  // ablation switch for experiments: 0 = real kernel
+#endif
+__device__ __forceinline__ void pile_read(bool has, const uint8_t* __restrict__ rec, const Win& w,
+                                          const PileCfg& pc, uint32_t* tile, uint32_t* t5, uint32_t max_span,
+                                          bool& span_err) {
+    if (MGP_ABL == 1) return;
+    uint4 h = make_uint4(0, 0, 0, 0);
+    uint4 qv[4];
+    if (MGP_ABL == 3) {
+        // synthetic read from the record address only: no payload loads
+        const uint32_t x = (uint32_t)(reinterpret_cast<uintptr_t>(rec) >> 4);
+        h = make_uint4((uint32_t)w.w0 + (x * 7u) % (uint32_t)w.wlen, 50u, 1u | (x & 1u ? (MGP_FLAG_REVERSE << 16) : 0u), 92u);
 #pragma unroll
-    for (int o = 0; o < kFastCig; ++o) {
-        qs[o] = 0;
-        qe[o] = 0;
-        dl[o] = 0;
-        if (o < (int)ncig) {
+        for (int k = 0; k < 4; ++k) qv[k] = make_uint4(0x25252525u, 0x25252525u, 0x25252525u, 0x25252525u);
+        has = has && true;
+    } else if (has) {
+        const uint4* r4 = reinterpret_cast<const uint4*>(rec);
+        h = r4[0];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) qv[k] = r4[1 + k];
+    } else {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) qv[k] = make_uint4(0, 0, 0, 0);
+    }
+    const int32_t start = (int32_t)h.x;
+    const uint32_t lseq = h.y;
+    const uint32_t ncig = h.z & 0xFFFFu;
+    const uint32_t coff = h.w;
+    const int strand = ((h.z >> 16) & MGP_FLAG_REVERSE) ? 1 : 0;
+    if (has) tn5_cut(start, lseq, strand, w, t5);
+
+    bool fast = has && lseq <= (uint32_t)kFastLen && ncig <= (uint32_t)kFastCig && start >= -(1 << 28) &&
+                start < (1 << 28);
+    int qs1 = 1 << 30, dl0 = 0, dl1 = 0;
+    int a0 = 0, b0 = 0, a1 = 0, b1 = 0;
+    if (fast) {
+        const uint32_t fake_cig = (50u << 4);
+        const uint32_t* cig = MGP_ABL == 3 ? &fake_cig : reinterpret_cast<const uint32_t*>(rec + coff);
+        int qs[2] = {0, 1 << 30}, qe[2] = {0, 1 << 30}, dl[2] = {0, 0};
+        int nb = 0;
+        int ref = start, q = 0;
+        for (uint32_t o = 0; o < ncig; ++o) {
             const uint32_t cg = cig[o];
             const uint32_t op = cg & 15u;
-            const int len = (int)(cg >> 4);
+            const int len = (int)min(cg >> 4, (uint32_t)(1 << 26));
             if (op == 0 || op == 7 || op == 8) {
-                qs[o] = q;
-                qe[o] = q + len;
-                dl[o] = ref - q;
+                if (nb == 2) {
+                    fast = false;
+                    break;
+                }
+                qs[nb] = q;
+                qe[nb] = q + len;
+                dl[nb] = ref - q;
+                ++nb;
                 q += len;
                 ref += len;
             } else if (op == 2 || op == 3) {
@@ -459,87 +507,124 @@ __device__ __forceinline__ void pile_fast(const uint8_t* __restrict__ rec, int32
                 q += len;
             }
         }
-    }
-    if ((int64_t)max(ref - start, (int)lseq) > (int64_t)max_span) span_err = true;
-
-    const uint4* qv = reinterpret_cast<const uint4*>(rec + 16);
-    uint32_t qw[kFastLen / 4];
-#pragma unroll
-    for (int k = 0; k < kFastLen / 16; ++k) {
-        const uint4 v = qv[k];
-        qw[4 * k] = v.x;
-        qw[4 * k + 1] = v.y;
-        qw[4 * k + 2] = v.z;
-        qw[4 * k + 3] = v.w;
-    }
-    // seq: 4-byte aligned dword loads, realigned with v_alignbyte
-    const uintptr_t sa = reinterpret_cast<uintptr_t>(rec) + 16 + lseq;
-    const uint32_t* sp = reinterpret_cast<const uint32_t*>(sa & ~uintptr_t(3));
-    const uint32_t sh = (uint32_t)(sa & 3) * 8u;
-    uint32_t raw[kFastLen / 8 + 1];
-#pragma unroll
-    for (int k = 0; k < kFastLen / 8 + 1; ++k) raw[k] = sp[k];
-    uint32_t sw[kFastLen / 8];
-#pragma unroll
-    for (int k = 0; k < kFastLen / 8; ++k)
-        sw[k] = (uint32_t)((((unsigned long long)raw[k + 1] << 32) | raw[k]) >> sh);
-
-    const int vq0 = pc.min_dist > 0 ? pc.min_dist : 0;
-    const int vq1 = min((int)lseq, pc.min_dist > 0 ? (int)lseq - pc.min_dist : (int)lseq);
-    const int wlo = w.w0, whi = w.w0 + w.wlen;
-    uint32_t* plane = tile + strand * w.Wp - w.w0;
-#pragma unroll
-    for (int qq = 0; qq < kFastLen; ++qq) {
-        int d = 0;
-        bool inb = false;
-#pragma unroll
-        for (int o = 0; o < kFastCig; ++o) {
-            const bool hit = qq >= qs[o] && qq < qe[o];
-            d = hit ? dl[o] : d;
-            inb |= hit;
+        if (fast) {
+            if (max(ref - start, (int)lseq) > (int)max_span) span_err = true;
+            const int vq0 = pc.min_dist > 0 ? pc.min_dist : 0;
+            const int vq1 = min((int)lseq, pc.min_dist > 0 ? (int)lseq - pc.min_dist : (int)lseq);
+            const int wlo = w.w0, whi = w.w0 + w.wlen;
+            a0 = max(max(qs[0], vq0), wlo - dl[0]);
+            b0 = min(min(qe[0], vq1), whi - dl[0]);
+            a1 = max(max(qs[1], vq0), wlo - dl[1]);
+            b1 = min(min(qe[1], vq1), whi - dl[1]);
+            if (nb < 1) b0 = a0;
+            if (nb < 2) b1 = a1;
+            qs1 = qs[1];
+            dl0 = dl[0];
+            dl1 = dl[1];
         }
-        const int r = qq + d;
-        const int qb = (int)(int8_t)((qw[qq >> 2] >> (8 * (qq & 3))) & 0xFFu);
-        const uint32_t code = (sw[qq >> 3] >> (8 * ((qq >> 1) & 3) + ((qq & 1) ? 0 : 4))) & 15u;
-        const int bi = (int)((kCodeLut >> (4 * code)) & 15ull);
-        const bool ok = inb && qq >= vq0 && qq < vq1 && r >= wlo && r < whi && qb >= pc.min_baseq && bi < 4;
-        if (ok) atomicAdd(&plane[2 * bi * w.Wp + r], 1u);
     }
+    int qlo = 1 << 30, qhi = 0;
+    if (fast) {
+        if (a0 < b0) {
+            qlo = a0;
+            qhi = b0;
+        }
+        if (a1 < b1) {
+            qlo = min(qlo, a1);
+            qhi = max(qhi, b1);
+        }
+    }
+    // wave-uniform bounds of the unrolled loop (every lane participates)
+    const int wq_lo = __builtin_amdgcn_readfirstlane(wave_min(qlo));
+    const int wq_hi = __builtin_amdgcn_readfirstlane(wave_max(qhi));
+    if (wq_lo < wq_hi) {
+        uint32_t qw[kFastLen / 4];
+#pragma unroll
+        for (int k = 0; k < kFastLen / 16; ++k) {
+            qw[4 * k] = qv[k].x;
+            qw[4 * k + 1] = qv[k].y;
+            qw[4 * k + 2] = qv[k].z;
+            qw[4 * k + 3] = qv[k].w;
+        }
+        // seq: 4-byte aligned dword loads, realigned with a funnel shift
+        uint32_t sw[kFastLen / 8];
+        {
+            uint32_t raw[kFastLen / 8 + 1];
+            const uintptr_t sa = reinterpret_cast<uintptr_t>(rec) + 16 + lseq;
+            const uint32_t sh = (uint32_t)(sa & 3) * 8u;
+            if (fast && MGP_ABL != 3) {
+                const uint32_t* sp = reinterpret_cast<const uint32_t*>(sa & ~uintptr_t(3));
+#pragma unroll
+                for (int k = 0; k < kFastLen / 8 + 1; ++k) raw[k] = sp[k];
+            } else if (fast) {
+#pragma unroll
+                for (int k = 0; k < kFastLen / 8 + 1; ++k) raw[k] = 0x12481248u * (uint32_t)(k + 1);
+            } else {
+#pragma unroll
+                for (int k = 0; k < kFastLen / 8 + 1; ++k) raw[k] = 0;
+            }
+#pragma unroll
+            for (int k = 0; k < kFastLen / 8; ++k)
+                sw[k] = (uint32_t)((((unsigned long long)raw[k + 1] << 32) | raw[k]) >> sh);
+        }
+        uint32_t* base = tile - w.w0;
+        const uint32_t Wp = (uint32_t)w.Wp;
+        const uint32_t inc = strand_inc(strand);
+        const uint32_t fastbit = fast ? 1u : 0u;
+        const int minbq = pc.min_baseq;
+#pragma unroll
+        for (int qq = 0; qq < kFastLen; ++qq) {
+            if (qq < wq_lo) continue;
+            if (qq >= wq_hi) break;
+            // branch-free predicate: one exec mask per base, a single branch around the atomic
+            const bool second = qq >= qs1;
+            const int d = second ? dl1 : dl0;
+            const int lo = second ? a1 : a0, hi = second ? b1 : b0;
+            const int qb = (int)(int8_t)((qw[qq >> 2] >> (8 * (qq & 3))) & 0xFFu);
+            const uint32_t code = (sw[qq >> 3] >> (8 * ((qq >> 1) & 3) + ((qq & 1) ? 0 : 4))) & 15u;
+            const uint32_t ok = (uint32_t)(qq >= lo) & (uint32_t)(qq < hi) & (uint32_t)(qb >= minbq) &
+                                ((kValid >> code) & 1u) & fastbit;
+            const uint32_t bi = (kLut2 >> (2 * code)) & 3u;
+            if (MGP_ABL == 2) {
+                if (ok & (uint32_t)(qb == 1234567)) atomicAdd(&base[__umul24(bi, Wp) + qq + d], inc);
+            } else if (ok) {
+                atomicAdd(&base[__umul24(bi, Wp) + qq + d], inc);
+            }
+        }
+    }
+    if (has && !fast) pile_slow(rec, start, lseq, ncig, coff, strand, w, pc, tile, max_span, span_err);
 }
 
-__device__ __forceinline__ void pile_read(const uint8_t* __restrict__ rec, const Win& w, const PileCfg& pc,
-                                          uint32_t* tile, uint32_t* t5, uint32_t max_span, bool& span_err) {
-    const uint4 h = *reinterpret_cast<const uint4*>(rec);
-    const int32_t start = (int32_t)h.x;
-    const uint32_t lseq = h.y;
-    const uint32_t ncig = h.z & 0xFFFFu;
-    const uint32_t flag = h.z >> 16;
-    const uint32_t coff = h.w;
-    const int strand = (flag & MGP_FLAG_REVERSE) ? 1 : 0;
-    tn5_cut(start, lseq, strand, w, t5);
-    // fast path only when every reference coordinate stays far from int32 overflow
-    if (lseq <= (uint32_t)kFastLen && ncig <= (uint32_t)kFastCig && start >= -(1 << 28) && start < (1 << 28) &&
-        max_span < (1u << 28))
-        pile_fast(rec, start, lseq, ncig, coff, strand, w, pc, tile, max_span, span_err);
-    else
-        pile_slow(rec, start, lseq, ncig, coff, strand, w, pc, tile, max_span, span_err);
-}
+constexpr int kMaxPosPerThread = 4;  // W <= 4 * 256
+constexpr int kWaveQ = 2 * kWave;    // per-wave queue of reads waiting to be piled (LDS)
+constexpr uint32_t kSeg = 65535;     // elements per tile segment (16-bit halves cannot carry)
 
-constexpr int kMaxPosPerThread = 8;  // W <= 8 * 256
+__device__ __forceinline__ bool same_dup(const GElem& p, const GElem& e, bool& dup3) {
+    if (((p.w ^ e.w) & GM_REV) != 0ull) return false;
+    if (p.tlen == e.tlen) dup3 = true;
+    return true;
+}
 
 // grid (nchunks, nwin): workgroup = (cell chunk, position window). For each cell
-// of the chunk: the cell's grouping elements whose start bin lies in
-// [window start - reach, window end) are deduplicated (walk back over equal
-// starts: first in BAM order wins) and piled into the LDS tile (8 count planes +
-// 2 Tn5 planes of Wp u32), then the tile is strand-filtered and flushed.
-__global__ void __launch_bounds__(kBlock) k_pileup(
+// of the chunk, the cell's grouping elements with start bin in [window start -
+// reach, window end) are processed by the 4 waves independently, in interleaved
+// chunks of 64: duplicates are marked by a walk back over equal starts (first in
+// BAM order wins; shuffles inside the chunk, global loads across it), kept
+// MAPQ-passing reads go to the wave's LDS queue and are piled 64 at a time, one
+// read per lane. Workgroup barriers only at cell boundaries; the packed tile is
+// then strand-filtered and flushed.
+#ifndef MGP_PILEUP_WAVES
+#define MGP_PILEUP_WAVES 4
+#endif
+__global__ void __launch_bounds__(kBlock, MGP_PILEUP_WAVES) k_pileup(
     Geom g, PileCfg pc, const uint8_t* __restrict__ payload, const GElem* __restrict__ gel,
     const uint32_t* __restrict__ O, uint32_t* __restrict__ counts, uint32_t* __restrict__ tn5,
     uint32_t* __restrict__ depth, uint32_t* __restrict__ n_reads, uint8_t* __restrict__ any_paired,
     uint32_t* __restrict__ covered, unsigned long long* __restrict__ dsum, uint32_t* __restrict__ dmax,
     uint32_t* __restrict__ tally_part, DevStats* st) {
-    extern __shared__ uint32_t tile[];  // [10][Wp]
-    uint32_t* t5 = tile + 8 * g.Wp;
+    extern __shared__ uint32_t tile[];  // [5][Wp]: A, C, G, T, Tn5 (fwd | rev << 16)
+    uint32_t* t5 = tile + 4 * g.Wp;
+    __shared__ unsigned long long wq_all[kBlock / kWave][kWaveQ];
     __shared__ uint32_t r_cov[4], r_max[4], r_keep[4];
     __shared__ unsigned long long r_sum[4];
     __shared__ int r_pair[4];
@@ -552,12 +637,15 @@ __global__ void __launch_bounds__(kBlock) k_pileup(
     w.Wp = g.Wp;
     const int L = g.L;
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    unsigned long long* wq = wq_all[wid];
     const uint32_t max_span = st->max_span;
     const int R = (int)((max_span + g.G - 1) / g.G) * g.G;
     const int lo_bin = win_lo_bin(k, R, g);
     const int own_bin = (int)((long long)k * g.W / g.G);
     const int hi_bin = k == g.nwin - 1 ? g.nbins : win_hi_bin(k, g);
     const int nc = g.nc;
+    const unsigned long long lt = lanemask_lt();
+    const bool dedup = pc.dedup_mode != MGP_DEDUP_NONE;
     bool span_err = false, bad = false;
     unsigned long long d2 = 0, d3 = 0;
 
@@ -569,43 +657,107 @@ __global__ void __launch_bounds__(kBlock) k_pileup(
 
     const int c0 = chunk * g.cpb, c1 = min(nc, c0 + g.cpb);
     for (int c = c0; c < c1; ++c) {
-        for (int x = threadIdx.x; x < 10 * g.Wp; x += blockDim.x) tile[x] = 0;
-        __syncthreads();
+        for (int x = threadIdx.x; x < 5 * g.Wp; x += blockDim.x) tile[x] = 0;
         const uint32_t lo = O[(size_t)lo_bin * nc + c];
         const uint32_t own = O[(size_t)own_bin * nc + c];
         const uint32_t hi = O[(size_t)hi_bin * nc + c];
+        const bool drained = hi - lo > kSeg;  // tile drained into the output rows between segments
         uint32_t nkeep = 0;
         bool paired = false;
-        for (uint32_t j = lo + threadIdx.x; j < hi; j += blockDim.x) {
-            const GElem e = gel[j];
-            bool dup2 = false, dup3 = false;
-            if (pc.dedup_mode != MGP_DEDUP_NONE) {
-                // duplicates share the exact start and sit just before j (BAM order)
-                for (uint32_t m = j; m-- > lo;) {
-                    const GElem p = gel[m];
-                    if (p.start != e.start) break;
-                    if (((p.w ^ e.w) & GM_REV) == 0ull) {
-                        dup2 = true;
-                        if (p.tlen == e.tlen) {
-                            dup3 = true;
-                            break;
+        __syncthreads();
+        for (uint32_t seg = lo; seg < hi; seg += kSeg) {
+            const uint32_t seg_hi = min(hi, seg + kSeg);
+            uint32_t qn = 0;  // wave-uniform queue fill
+            for (uint32_t cb = seg + kWave * wid; cb < seg_hi; cb += kBlock) {
+                const uint32_t j = cb + lane;
+                const bool act = j < seg_hi;
+                GElem e;
+                e.w = 0;
+                e.start = INT_MIN;
+                e.tlen = 0;
+                if (act) e = gel[j];
+                bool dup2 = false, dup3 = false;
+                if (dedup) {
+                    // walk back over equal starts (duplicates sit just before j, BAM order)
+                    bool cont = act;
+                    for (int m = 1; m < kWave; ++m) {
+                        const int ps = __shfl_up(e.start, m, kWave);
+                        const unsigned long long pw = __shfl_up(e.w, m, kWave);
+                        const uint32_t pt = __shfl_up(e.tlen, m, kWave);
+                        if (cont && lane >= m) {
+                            if (ps != e.start) {
+                                cont = false;
+                            } else if (((pw ^ e.w) & GM_REV) == 0ull) {
+                                dup2 = true;
+                                if (pt == e.tlen) {
+                                    dup3 = true;
+                                    cont = false;
+                                }
+                            }
+                        }
+                        const bool more = cont && lane > m;
+                        if (__ballot(more) == 0ull) break;
+                    }
+                    // runs reaching the chunk start continue in the previous elements (global)
+                    if (cont && act) {
+                        for (uint32_t mm = cb; mm-- > lo;) {
+                            const GElem p = gel[mm];
+                            if (p.start != e.start) break;
+                            if (same_dup(p, e, dup3)) {
+                                dup2 = true;
+                                if (dup3) break;
+                            }
                         }
                     }
                 }
-            }
-            const bool keep = pc.dedup_mode == MGP_DEDUP_NONE ? true
-                              : pc.dedup_mode == MGP_DEDUP_START ? !dup2
-                                                                 : !dup3;
-            if (j >= own) {  // statistics counted once, by the window that owns the start bin
-                d2 += dup2;
-                d3 += dup3;
-                if (keep) {
-                    ++nkeep;
-                    paired |= (e.w & GM_PAIRED) != 0ull;
-                    bad |= (e.w & GM_BAD) != 0ull;
+                const bool keep = !dedup ? true : pc.dedup_mode == MGP_DEDUP_START ? !dup2 : !dup3;
+                if (act && j >= own) {  // statistics counted once, by the window owning the start bin
+                    d2 += dup2;
+                    d3 += dup3;
+                    if (keep) {
+                        ++nkeep;
+                        paired |= (e.w & GM_PAIRED) != 0ull;
+                        bad |= (e.w & GM_BAD) != 0ull;
+                    }
+                }
+                const bool piled = act && keep && (e.w & GM_MAPQ_OK);
+                const unsigned long long bal = __ballot(piled);
+                if (piled) wq[qn + (uint32_t)__popcll(bal & lt)] = e.w;
+                qn += (uint32_t)__popcll(bal);
+                __builtin_amdgcn_wave_barrier();
+                if (qn >= (uint32_t)kWave) {
+                    const unsigned long long qe = wq[lane];
+                    pile_read(true, payload + (qe & GM_OFF), w, pc, tile, t5, max_span, span_err);
+                    qn -= kWave;
+                    if ((uint32_t)lane < qn) wq[lane] = wq[kWave + lane];
+                    __builtin_amdgcn_wave_barrier();
                 }
             }
-            if (keep && (e.w & GM_MAPQ_OK)) pile_read(payload + (e.w & GM_OFF), w, pc, tile, t5, max_span, span_err);
+            {   // tail: every lane of the wave enters, lanes past qn hold no read
+                const bool has = (uint32_t)lane < qn;
+                const unsigned long long qe = has ? wq[lane] : 0ull;
+                pile_read(has, payload + (qe & GM_OFF), w, pc, tile, t5, max_span, span_err);
+            }
+            if (drained) {  // add this segment's packed tile into the 32-bit output rows
+                __syncthreads();
+                for (int p = threadIdx.x; p < w.wlen; p += blockDim.x) {
+                    const size_t P = (size_t)c * L + w.w0 + p;
+                    uint4* cp = reinterpret_cast<uint4*>(counts + P * 8);
+                    uint4 a = seg == lo ? make_uint4(0, 0, 0, 0) : cp[0];
+                    uint4 b = seg == lo ? make_uint4(0, 0, 0, 0) : cp[1];
+                    uint2 t = seg == lo ? make_uint2(0, 0) : reinterpret_cast<uint2*>(tn5)[P];
+                    const uint32_t x0 = tile[p], x1 = tile[g.Wp + p], x2 = tile[2 * g.Wp + p],
+                                   x3 = tile[3 * g.Wp + p], x4 = t5[p];
+                    a.x += x0 & 0xFFFFu; a.y += x0 >> 16; a.z += x1 & 0xFFFFu; a.w += x1 >> 16;
+                    b.x += x2 & 0xFFFFu; b.y += x2 >> 16; b.z += x3 & 0xFFFFu; b.w += x3 >> 16;
+                    t.x += x4 & 0xFFFFu; t.y += x4 >> 16;
+                    cp[0] = a;
+                    cp[1] = b;
+                    reinterpret_cast<uint2*>(tn5)[P] = t;
+                    tile[p] = tile[g.Wp + p] = tile[2 * g.Wp + p] = tile[3 * g.Wp + p] = t5[p] = 0;
+                }
+                __syncthreads();
+            }
         }
         nkeep = wave_sum(nkeep);
         const bool anyp = __ballot(paired) != 0ull;
@@ -616,9 +768,27 @@ __global__ void __launch_bounds__(kBlock) k_pileup(
         for (int m = 0; m < kMaxPosPerThread; ++m) {
             const int p = threadIdx.x + m * kBlock;
             if (p < w.wlen) {
-                uint32_t v[8];
+                const size_t P = (size_t)c * L + w.w0 + p;
+                uint32_t v[8], tf, tr;
+                if (drained) {
+                    const uint4 a = reinterpret_cast<const uint4*>(counts + P * 8)[0];
+                    const uint4 b = reinterpret_cast<const uint4*>(counts + P * 8)[1];
+                    const uint2 t = reinterpret_cast<const uint2*>(tn5)[P];
+                    v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
+                    v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+                    tf = t.x;
+                    tr = t.y;
+                } else {
 #pragma unroll
-                for (int x = 0; x < 8; ++x) v[x] = tile[x * g.Wp + p];
+                    for (int x = 0; x < 4; ++x) {
+                        const uint32_t pk = tile[x * g.Wp + p];
+                        v[2 * x] = pk & 0xFFFFu;
+                        v[2 * x + 1] = pk >> 16;
+                    }
+                    const uint32_t pk = t5[p];
+                    tf = pk & 0xFFFFu;
+                    tr = pk >> 16;
+                }
                 uint32_t d = 0;
 #pragma unroll
                 for (int b = 0; b < 4; ++b) {
@@ -635,9 +805,7 @@ __global__ void __launch_bounds__(kBlock) k_pileup(
                     tal[m][b] += t2;
                     d += t2;
                 }
-                uint32_t tf = t5[p], tr = t5[g.Wp + p];
                 if (d == 0) tf = tr = 0;
-                const size_t P = (size_t)c * L + w.w0 + p;
                 uint4* cp = reinterpret_cast<uint4*>(counts + P * 8);
                 cp[0] = make_uint4(v[0], v[1], v[2], v[3]);
                 cp[1] = make_uint4(v[4], v[5], v[6], v[7]);
@@ -887,7 +1055,7 @@ static int configure_geometry(mgp_ctx* ctx) {
     g.G = 8;
     g.nb_reg = (g.L + g.G - 1) / g.G;
     g.nbins = g.nb_reg + 1;
-    g.nwin = (g.L + 1023) / 1024;          // ~1 Ki positions per window
+    g.nwin = (g.L + 1023) / 1024;          // ~1 Ki positions per window (<= 4 * 256 per thread)
     g.W = (g.L + g.nwin - 1) / g.nwin;
     g.W = ((g.W + g.G - 1) / g.G) * g.G;   // multiple of the bin width
     g.nwin = (g.L + g.W - 1) / g.W;
@@ -1033,7 +1201,7 @@ int mgp_push_batch(mgp_ctx* ctx, const mgp_batch* b) {
         return set_err(MGP_E_INVALID, "more than 2^32-2 resident reads per context; shard or batch the run");
     HIP_TRY(hipSetDevice(ctx->dev));
     const int64_t n0 = ctx->n, nb = b->n_reads;
-    const int64_t pay0 = (ctx->pay + 15) & ~int64_t(15);
+    const int64_t pay0 = (ctx->pay + 255) & ~int64_t(255);  // keeps the batch's record alignment
     MGP_TRY(ensure_inputs(ctx, n0 + nb, pay0 + b->payload_bytes, true));
     hipStream_t s = ctx->s_copy;
     HIP_TRY(hipMemcpyAsync(ctx->start.as<int32_t>() + n0, b->start, nb * 4, hipMemcpyHostToDevice, s));
@@ -1196,7 +1364,7 @@ int mgp_run(mgp_ctx* ctx) {
         pc.max_bias = ctx->cfg.max_strand_bias;
         pc.bias_active = ctx->cfg.max_strand_bias < 1.0;
         dim3 gp(g.nchunks, g.nwin);
-        const size_t psm = (size_t)10 * g.Wp * 4;
+        const size_t psm = (size_t)5 * g.Wp * 4;
         k_pileup<<<gp, kBlock, psm, s>>>(g, pc, ctx->payload.as<uint8_t>(), ctx->gel.as<GElem>(),
                                          ctx->H.as<uint32_t>(), ctx->counts.as<uint32_t>(), ctx->tn5.as<uint32_t>(),
                                          ctx->depth.as<uint32_t>(), ctx->n_reads.as<uint32_t>(),
@@ -1386,7 +1554,7 @@ int mgp_download_inputs(mgp_ctx* ctx, int32_t* start, int32_t* bc, int32_t* tlen
 int mgp_synth_fill(void* stream, uint64_t seed, int64_t n, int read_len, int n_cells, int mito_len,
                    const uint32_t* d_cdf, const uint8_t* d_ref, int32_t* start, int32_t* bc, int32_t* tlen,
                    uint16_t* flag, uint8_t* mapq, uint32_t* span, uint64_t* roff, uint8_t* payload,
-                   int64_t* payload_bytes, int phase);
+                   int64_t* payload_bytes, int rec_align);
 
 int mgp_synth_generate(mgp_ctx* ctx, const mgp_synth_params* p) {
     if (!ctx || !p || !p->cell_cdf || !p->ref_codes) return set_err(MGP_E_INVALID, "null synth args");
@@ -1394,6 +1562,8 @@ int mgp_synth_generate(mgp_ctx* ctx, const mgp_synth_params* p) {
     if (p->n_reads < 0 || p->n_reads > (int64_t)0xFFFFFFFEll || p->read_len < 12 || p->read_len > 4096)
         return set_err(MGP_E_INVALID, "synth sizes out of range");
     if (ctx->cfg.mito_len < p->read_len) return set_err(MGP_E_INVALID, "mito_len < read_len");
+    const int align = p->rec_align ? p->rec_align : 16;
+    if (align < 16 || align > 4096 || (align & (align - 1))) return set_err(MGP_E_INVALID, "rec_align must be a power of two in [16, 4096]");
     HIP_TRY(hipSetDevice(ctx->dev));
     HIP_TRY(hipStreamSynchronize(ctx->s_comp));
     HIP_TRY(hipStreamSynchronize(ctx->s_copy));
@@ -1403,7 +1573,7 @@ int mgp_synth_generate(mgp_ctx* ctx, const mgp_synth_params* p) {
     const int L = ctx->cfg.mito_len;
     const int nc = p->n_cells;
     // record size is at most 16 + 4*3 + len + (len+1)/2 rounded to 8
-    const int64_t max_rec = ((16 + 12 + p->read_len + (p->read_len + 1) / 2) + 7) & ~7;
+    const int64_t max_rec = ((16 + 16 + p->read_len + (p->read_len + 1) / 2) + align - 1) & ~(int64_t)(align - 1);
     MGP_TRY(ensure_inputs(ctx, std::max<int64_t>(n, 1), n * max_rec, false));
     DevBuf cdf, ref;
     MGP_TRY(cdf.ensure((size_t)std::max(nc, 1) * 4));
@@ -1415,7 +1585,7 @@ int mgp_synth_generate(mgp_ctx* ctx, const mgp_synth_params* p) {
     int r = mgp_synth_fill(s, p->seed, n, p->read_len, nc, L, cdf.as<uint32_t>(), ref.as<uint8_t>(),
                            ctx->start.as<int32_t>(), ctx->bc.as<int32_t>(), ctx->tlen.as<int32_t>(),
                            ctx->flag.as<uint16_t>(), ctx->mapq.as<uint8_t>(), ctx->span.as<uint32_t>(),
-                           ctx->roff.as<uint64_t>(), ctx->payload.as<uint8_t>(), &pay, 0);
+                           ctx->roff.as<uint64_t>(), ctx->payload.as<uint8_t>(), &pay, align);
     if (r != MGP_OK) {
         cdf.release();
         ref.release();

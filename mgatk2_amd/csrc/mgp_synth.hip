@@ -75,14 +75,14 @@ __device__ __forceinline__ Cig cig_of(uint64_t seed, int64_t i) {
 
 __device__ __forceinline__ int cigar_offset(int rl) { return (16 + rl + (rl + 1) / 2 + 3) & ~3; }
 
-__device__ __forceinline__ uint64_t rec_size(int ncig, int rl) {
-    return (uint64_t)((cigar_offset(rl) + 4 * ncig + 15) & ~15);
+__device__ __forceinline__ uint64_t rec_size(int ncig, int rl, int align) {
+    return (uint64_t)((cigar_offset(rl) + 4 * ncig + align - 1) & ~(align - 1));
 }
 
-__global__ void k_synth_sizes(uint64_t seed, int64_t n, int rl, uint64_t* __restrict__ sz) {
+__global__ void k_synth_sizes(uint64_t seed, int64_t n, int rl, int align, uint64_t* __restrict__ sz) {
     int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
-    sz[i] = rec_size(cig_of(seed, i).n, rl);
+    sz[i] = rec_size(cig_of(seed, i).n, rl, align);
 }
 
 // ---- generic exclusive scan of u64 (3-phase, 4096 items per block) ----------
@@ -276,7 +276,7 @@ __global__ void k_synth_fill(uint64_t seed, int64_t n, int rl, int nc, int L, co
 extern "C" int mgp_synth_fill(void* stream, uint64_t seed, int64_t n, int read_len, int n_cells, int mito_len,
                               const uint32_t* d_cdf, const uint8_t* d_ref, int32_t* start, int32_t* bc,
                               int32_t* tlen, uint16_t* flag, uint8_t* mapq, uint32_t* span, uint64_t* roff,
-                              uint8_t* payload, int64_t* payload_bytes, int /*phase*/) {
+                              uint8_t* payload, int64_t* payload_bytes, int rec_align) {
     hipStream_t s = (hipStream_t)stream;
     if (read_len < 48) return MGP_E_INVALID;
     if (n == 0) {
@@ -284,7 +284,7 @@ extern "C" int mgp_synth_fill(void* stream, uint64_t seed, int64_t n, int read_l
         return MGP_OK;
     }
     const unsigned nb = (unsigned)((n + kBlock - 1) / kBlock);
-    k_synth_sizes<<<nb, kBlock, 0, s>>>(seed, n, read_len, roff);
+    k_synth_sizes<<<nb, kBlock, 0, s>>>(seed, n, read_len, rec_align, roff);
     if (hipGetLastError() != hipSuccess) return MGP_E_HIP;
     uint64_t total = 0;
     int r = scan_exclusive_u64(roff, n, s, &total);

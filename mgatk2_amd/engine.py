@@ -15,7 +15,10 @@ import numpy as np
 from .exceptions import BAMFormatError, BAMReadError, InvalidInputError, ProcessingError
 from .synth import ReadSoA
 
-LIB_PATH = Path(__file__).resolve().parent / "_lib" / "libmgpileup.so"
+import os
+
+# MGP_LIB selects an alternative build of the same engine (A/B experiments only)
+LIB_PATH = Path(os.environ.get("MGP_LIB") or Path(__file__).resolve().parent / "_lib" / "libmgpileup.so")
 
 MGP_OK = 0
 MGP_E_INVALID = -1
@@ -112,6 +115,8 @@ class mgp_synth_params(C.Structure):
         ("n_cells", C.c_int32),
         ("cell_cdf", C.c_void_p),
         ("ref_codes", C.c_void_p),
+        ("rec_align", C.c_int32),
+        ("reserved", C.c_int32),
     ]
 
 
@@ -320,10 +325,12 @@ class Engine:
         _ck(self.lib.mgp_resident(self._h, C.byref(n), C.byref(p)), "mgp_resident")
         return int(n.value), int(p.value)
 
-    def synth(self, seed: int, n_reads: int, cdf: np.ndarray, ref: np.ndarray, read_len: int = 50):
+    def synth(self, seed: int, n_reads: int, cdf: np.ndarray, ref: np.ndarray, read_len: int = 50,
+              rec_align: int = 128):
         cdf = np.ascontiguousarray(cdf, np.uint32)
         ref = np.ascontiguousarray(ref, np.uint8)
-        p = mgp_synth_params(int(seed), int(n_reads), int(read_len), int(self.cfg.n_cells), _ptr(cdf), _ptr(ref))
+        p = mgp_synth_params(int(seed), int(n_reads), int(read_len), int(self.cfg.n_cells), _ptr(cdf), _ptr(ref),
+                             int(rec_align), 0)
         _ck(self.lib.mgp_synth_generate(self._h, C.byref(p)), "mgp_synth_generate")
 
     def download_inputs(self) -> ReadSoA:

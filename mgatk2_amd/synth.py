@@ -180,8 +180,8 @@ def concat_soa(parts: list[ReadSoA]) -> ReadSoA:
     pay = []
     base = 0
     for p in parts:
-        base = (base + 15) & ~15
-        offs.append(p.rec_off + np.uint64(base))  # records stay 16-byte aligned
+        base = (base + 255) & ~255
+        offs.append(p.rec_off + np.uint64(base))  # records keep their alignment
         pad = base - sum(x.shape[0] for x in pay)
         if pad:
             pay.append(np.zeros(pad, np.uint8))
@@ -205,8 +205,12 @@ def cigar_offset(lseq):
     return (16 + lseq + (lseq + 1) // 2 + 3) & ~3
 
 
-def rec_size(ncig, lseq):
-    return (cigar_offset(lseq) + 4 * np.asarray(ncig, np.int64) + 15) & ~15
+REC_ALIGN = 128  # records are gathered at random: one L2 line per record of <= 128 bytes
+
+
+def rec_size(ncig, lseq, align: int = 16):
+    """Bytes a record occupies when records are placed at multiples of `align`."""
+    return (cigar_offset(lseq) + 4 * np.asarray(ncig, np.int64) + align - 1) & ~(align - 1)
 
 
 def _synth_chunk(seed, i0, i1, n, read_len, n_cells, mito_len, cdf, ref):
@@ -315,10 +319,10 @@ def _synth_chunk(seed, i0, i1, n, read_len, n_cells, mito_len, cdf, ref):
     )
 
 
-def _pack_fixed(start, flag, ncig, cig, qual, code, rl):
+def _pack_fixed(start, flag, ncig, cig, qual, code, rl, align=REC_ALIGN):
     """Pack records for reads of one read length (vectorised)."""
     m = start.shape[0]
-    sizes = rec_size(ncig, np.full(m, rl))
+    sizes = rec_size(ncig, np.full(m, rl), align)
     roff = np.zeros(m, np.uint64)
     if m:
         roff[1:] = np.cumsum(sizes[:-1]).astype(np.uint64)
@@ -349,7 +353,8 @@ def _pack_fixed(start, flag, ncig, cig, qual, code, rl):
 
 
 def synth_reads(
-    seed: int, n_reads: int, n_cells: int, read_len: int = 50, mito_len: int = MITO_LEN, chunk: int = 262144
+    seed: int, n_reads: int, n_cells: int, read_len: int = 50, mito_len: int = MITO_LEN, chunk: int = 262144,
+    rec_align: int = REC_ALIGN,
 ) -> ReadSoA:
     """Host mirror of the device generator (bit-identical)."""
     if read_len < 48:
@@ -360,7 +365,8 @@ def synth_reads(
     for i0 in range(0, n_reads, chunk):
         i1 = min(n_reads, i0 + chunk)
         f = _synth_chunk(seed, i0, i1, n_reads, read_len, n_cells, mito_len, cdf, ref)
-        roff, pay = _pack_fixed(f["start"], f["flag"], f["ncig"], f["cig"], f["qual"], f["code"], read_len)
+        roff, pay = _pack_fixed(f["start"], f["flag"], f["ncig"], f["cig"], f["qual"], f["code"], read_len,
+                                rec_align)
         parts.append(ReadSoA(f["start"], f["bc"], f["tlen"], f["flag"], f["mapq"], f["span"], roff, pay))
     soa = _concat_dense(parts)
     soa.extra.update(cdf=cdf, ref=ref, seed=seed, read_len=read_len)
@@ -394,7 +400,7 @@ def cigar_ref_span(cigar) -> int:
     return sum(length for op, length in cigar if op in (0, 2, 3, 7, 8))
 
 
-def pack_reads(reads: list[dict]) -> ReadSoA:
+def pack_reads(reads: list[dict], rec_align: int = REC_ALIGN) -> ReadSoA:
     """Pack pysam-like read dicts into the engine input.
 
     Keys: ``reference_start``, ``flag`` (BAM flag), ``mapping_quality``,
@@ -427,7 +433,7 @@ def pack_reads(reads: list[dict]) -> ReadSoA:
         mapq[i] = r.get("mapping_quality", 60)
         span[i] = max(cigar_ref_span(cig), lseq)
         roff[i] = off
-        size = int(rec_size(len(cig), lseq))
+        size = int(rec_size(len(cig), lseq, rec_align))
         coff = int(cigar_offset(lseq))
         rec = np.zeros(size, np.uint8)
         hdr = np.array([(start[i], lseq, len(cig), f, coff)],

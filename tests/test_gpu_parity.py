@@ -227,5 +227,6 @@ def test_deep_cell_median_fallback(engine_lib, oracle_lib):
     reads = [_read(1000, [(0, 30)], "ACGT" * 7 + "AC", 0, tlen=100 + k) for k in range(9000)]
     reads += [_read(2000 + 40 * k, [(0, 30)], "G" * 30, 0, tlen=77) for k in range(200)]
     reads += [_read(3000, [(0, 30)], "T" * 30, 1, tlen=100 + k) for k in range(50)]
+    reads.sort(key=lambda r: r["reference_start"])
     res = _both(engine_lib, oracle_lib, reads, 2, dedup_mode="alignment_and_fragment_length")
     assert res.depth_max[0] >= 8192
