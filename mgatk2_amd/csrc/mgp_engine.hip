@@ -3,15 +3,13 @@
 // Hot path (one mgp_run over the HBM-resident read set), restating the
 // reference's per-read Python loops (paths relative to the reference root):
 //
-//   k_bin_bounds    coordinate-order check + start-bin boundaries (the order that
-//                   pysam's fetch() guarantees, readers.py:87-92)
-//   k_bin_hist      flag/barcode filters (readers.py:95-111) + per (start-bin, cell)
-//                   histogram in LDS; every valid read gets its STABLE rank (BAM
-//                   order) inside its (bin, cell) group, one wavefront per bin
+//   k_bin_count     per start bin: bin bounds by binary search, coordinate-order
+//                   check (pysam's fetch() order, readers.py:87-92), flag/barcode
+//                   filters (readers.py:95-111) and the per-cell read histogram
 //   k_scan_*        exclusive scan of the histogram in (cell, start-bin) order: the
-//                   cell-major layout of `reads_by_barcode` (readers.py:69,164) with
-//                   BAM order kept inside each cell
-//   k_scatter       one 16-byte grouping element per valid read at its slot
+//                   cell-major layout of `reads_by_barcode` (readers.py:69,164)
+//   k_scatter       per start bin: one 16-byte grouping element per valid read at
+//                   its cell-major slot, BAM order kept inside each cell (stable)
 //   k_pileup        per (cell chunk, position window): duplicate marking by a short
 //                   walk back over equal starts (readers.py:118-150, first in BAM
 //                   order wins), kept-read counts (processors.py:22,34), MAPQ gate
@@ -101,8 +99,8 @@ struct DevBuf {
     T* as() const { return reinterpret_cast<T*>(p); }
 };
 
-enum Stage { ST_BINS, ST_HIST, ST_SCAN, ST_SCATTER, ST_PILEUP, ST_GATE, ST_MEDIAN, ST_TALLY, ST_COMM, ST_N };
-static const char* kStageNames = "bins,hist,scan,scatter,pileup,gate,median,tally,comm";
+enum Stage { ST_HIST, ST_SCAN, ST_SCATTER, ST_PILEUP, ST_GATE, ST_MEDIAN, ST_TALLY, ST_COMM, ST_N };
+static const char* kStageNames = "hist,scan,scatter,pileup,gate,median,tally,comm";
 
 struct mgp_ctx {
     mgp_config cfg{};
@@ -121,7 +119,7 @@ struct mgp_ctx {
     DevBuf start, bc, tlen, flag, mapq, span, roff, payload;
 
     // run scratch
-    DevBuf bin_start, rank, H, P, cell_cnt, cell_base;
+    DevBuf bin_start, H, Hcur, P, cell_cnt, cell_base;
     DevBuf gel, tally_part, tally;
     DevBuf n_reads, any_paired, passed, covered, dsum, dmax, med_lo, med_hi, first_read;
     DevBuf counts, tn5, depth, stats;
@@ -138,110 +136,82 @@ struct mgp_ctx {
 // kernels
 // ---------------------------------------------------------------------------
 
-// Per read: sortedness check + start-bin boundaries by adjacent difference.
-__global__ void k_bin_bounds(const int32_t* __restrict__ start, int64_t n, Geom g,
-                             uint32_t* __restrict__ bin_start, DevStats* st) {
-    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    int s = start[i];
-    int b = bin_of(s, g);
-    int bp;
-    if (i == 0) {
-        bp = -1;
-    } else {
-        int sp = start[i - 1];
-        if (s < sp) atomicOr(&st->err, ERR_UNSORTED);
-        bp = bin_of(sp, g);
-    }
-    for (int bb = bp + 1; bb <= b; ++bb) bin_start[bb] = (uint32_t)i;
-    if (i == n - 1)
-        for (int bb = b + 1; bb <= g.nbins; ++bb) bin_start[bb] = (uint32_t)n;
-}
-
 __device__ __forceinline__ bool read_valid(int c, uint16_t f, int nc) {
     return c >= 0 && c < nc && !(f & (MGP_FLAG_UNMAPPED | MGP_FLAG_SECONDARY | MGP_FLAG_SUPPLEMENTARY));
 }
 
-// One wavefront per start bin, reads taken 64 at a time in BAM order: histogram
-// over cells (LDS when it fits, else the global row) and each valid read's STABLE
-// rank inside its (bin, cell) group. Lanes of one cell find each other with one
-// ballot per cell-id bit (a wave-wide match); the lowest lane of each peer group
-// advances the group's counter, so ranks follow BAM order.
+// first index i in [0, n) with start[i] >= t (start[] is coordinate-sorted)
+__device__ __forceinline__ int64_t lower_bound_start(const int32_t* __restrict__ start, int64_t n, int64_t t) {
+    int64_t lo = 0, hi = n;
+    while (lo < hi) {
+        const int64_t mid = (lo + hi) >> 1;
+        if ((int64_t)start[mid] < t) lo = mid + 1;
+        else hi = mid;
+    }
+    return lo;
+}
+
+// smallest start of bin b (bin_of() inverse)
+__device__ __forceinline__ int64_t bin_threshold(int b, const Geom& g) {
+    if (b <= 0) return INT64_MIN;
+    if (b >= g.nbins) return INT64_MAX;
+    if (b == g.nb_reg) return g.L;
+    return (int64_t)b * g.G;
+}
+
+// One workgroup per start bin: bin bounds by binary search in the sorted starts,
+// coordinate-order check (pysam's fetch order, readers.py:87-92), flag/barcode
+// filters (readers.py:95-111) and the per-cell histogram of the bin (LDS atomics
+// when the row fits, else atomics on the global row).
 template <bool kLds>
-__global__ void __launch_bounds__(kWave) k_bin_hist(const uint32_t* __restrict__ bin_start,
-                                                    const int32_t* __restrict__ bc,
-                                                    const uint16_t* __restrict__ flag,
-                                                    const uint32_t* __restrict__ span, int64_t n, Geom g, int cbits,
-                                                    uint32_t* __restrict__ H, uint32_t* __restrict__ rank,
-                                                    DevStats* st) {
+__global__ void __launch_bounds__(kBlock) k_bin_count(const int32_t* __restrict__ start,
+                                                      const int32_t* __restrict__ bc,
+                                                      const uint16_t* __restrict__ flag,
+                                                      const uint32_t* __restrict__ span, int64_t n, Geom g,
+                                                      uint32_t* __restrict__ H, uint32_t* __restrict__ bin_lo,
+                                                      DevStats* st) {
     extern __shared__ uint32_t hist[];
+    __shared__ int64_t s_range[2];
     const int b = blockIdx.x;
     const int nc = g.nc;
-    const unsigned lane = threadIdx.x;
     uint32_t* row = H + (size_t)b * nc;
     uint32_t* cnt = kLds ? hist : row;
-    if (kLds) {
-        for (int c = lane; c < nc; c += kWave) hist[c] = 0;
-        __syncthreads();
+    if (threadIdx.x < 2) s_range[threadIdx.x] = lower_bound_start(start, n, bin_threshold(b + threadIdx.x, g));
+    if (kLds)
+        for (int c = threadIdx.x; c < nc; c += blockDim.x) hist[c] = 0;
+    __syncthreads();
+    const int64_t lo = s_range[0], hi = max(s_range[1], lo);
+    if (threadIdx.x == 0) {
+        bin_lo[b] = (uint32_t)lo;
+        if (b == g.nbins - 1) bin_lo[g.nbins] = (uint32_t)n;
     }
-    const int64_t lo = min((int64_t)bin_start[b], n);
-    const int64_t hi = min(max((int64_t)bin_start[b + 1], lo), n);
-    const unsigned long long lt = lanemask_lt();
     uint32_t mspan = 0;
     unsigned long long nvalid = 0;
-    bool badbc = false;
-    constexpr int kAhead = 8;  // chunks of 64 reads whose loads are issued together
-    for (int64_t base = lo; base < hi; base += kAhead * kWave) {
-        int cc[kAhead];
-        uint16_t ff[kAhead];
-        uint32_t ss[kAhead];
-#pragma unroll
-        for (int u = 0; u < kAhead; ++u) {
-            const int64_t i = base + u * kWave + lane;
-            cc[u] = -1;
-            ff[u] = 0;
-            ss[u] = 0;
-            if (i < hi) {
-                cc[u] = bc[i];
-                ff[u] = flag[i];
-                ss[u] = span[i];
-            }
-        }
-#pragma unroll
-        for (int u = 0; u < kAhead; ++u) {
-            const int64_t i = base + u * kWave + lane;
-            const int c = cc[u];
-            badbc |= (c >= nc);
-            const bool valid = i < hi && read_valid(c, ff[u], nc);
-            unsigned long long peers = __ballot(valid);
-            if (peers == 0ull) continue;
-            for (int bit = 0; bit < cbits; ++bit) {
-                const bool x = valid && ((c >> bit) & 1);
-                const unsigned long long m = __ballot(x);
-                peers &= x ? m : ~m;
-            }
-            if (valid) {
-                const uint32_t before = cnt[c];
-                rank[i] = before + (uint32_t)__popcll(peers & lt);
-                mspan = ss[u] > mspan ? ss[u] : mspan;
-                ++nvalid;
-                if ((peers & lt) == 0ull) cnt[c] = before + (uint32_t)__popcll(peers);  // group leader
-            }
-            if (!kLds) __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");  // leader's store before next reads
-            __builtin_amdgcn_wave_barrier();
+    bool badbc = false, unsorted = false;
+    for (int64_t i = lo + threadIdx.x; i < hi; i += blockDim.x) {
+        const int c = bc[i];
+        const uint16_t f = flag[i];
+        if (i > 0 && start[i] < start[i - 1]) unsorted = true;
+        badbc |= (c >= nc);
+        if (read_valid(c, f, nc)) {
+            atomicAdd(&cnt[c], 1u);
+            const uint32_t sp = span[i];
+            mspan = sp > mspan ? sp : mspan;
+            ++nvalid;
         }
     }
     if (kLds) {
         __syncthreads();
-        for (int c = lane; c < nc; c += kWave) row[c] = hist[c];
+        for (int c = threadIdx.x; c < nc; c += blockDim.x) row[c] = hist[c];
     }
     mspan = wave_max(mspan);
     nvalid = wave_sum(nvalid);
-    const bool anybad = __ballot(badbc) != 0ull;
-    if (lane == 0) {
+    const bool anybad = __ballot(badbc) != 0ull, anyuns = __ballot(unsorted) != 0ull;
+    if ((threadIdx.x & 63) == 0) {
         if (mspan) atomicMax(&st->max_span, mspan);
         if (nvalid) atomicAdd(&st->valid, nvalid);
         if (anybad) atomicOr(&st->err, ERR_BADBC);
+        if (anyuns) atomicOr(&st->err, ERR_UNSORTED);
     }
 }
 
@@ -334,35 +304,97 @@ struct __align__(16) GElem {
 constexpr unsigned long long GM_REV = 1ull << 56, GM_PAIRED = 2ull << 56, GM_MAPQ_OK = 4ull << 56,
                              GM_BAD = 8ull << 56, GM_OFF = (1ull << 56) - 1;
 
-// Per read: place the grouping element of each valid read at its cell-major slot.
-__global__ void k_scatter(int64_t n, const int32_t* __restrict__ start, const int32_t* __restrict__ bc,
-                          const int32_t* __restrict__ tlen, const uint16_t* __restrict__ flag,
-                          const uint8_t* __restrict__ mapq, const uint64_t* __restrict__ roff,
-                          const uint32_t* __restrict__ rank, const uint32_t* __restrict__ O, Geom g, int min_mapq,
-                          GElem* __restrict__ gel, uint32_t* __restrict__ first_read, DevStats* st) {
-    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    const int c = bc[i];
-    const uint16_t f = flag[i];
-    if (!read_valid(c, f, g.nc)) return;
-    const int s = start[i];
-    const int b = bin_of(s, g);
-    const uint32_t r = rank[i];
-    const uint32_t dest = O[(size_t)b * g.nc + c] + r;
-    const uint32_t end = O[(size_t)g.nbins * g.nc + c];
-    if (dest >= end) {
-        atomicOr(&st->err, ERR_OVERFLOW);
-        return;
+// One workgroup per start bin, reads taken 256 at a time in BAM order: each valid
+// read's grouping element goes to its cell-major slot. Slots inside a (bin, cell)
+// group follow BAM order (stable): lanes of one cell find each other with one
+// ballot per cell-id bit; the 4 waves then take turns (in wave order) to claim
+// their groups' slots from the per-cell counters in LDS (seeded with the scan).
+template <bool kLds>
+__global__ void __launch_bounds__(kBlock) k_scatter(int64_t n, const int32_t* __restrict__ start,
+                                                    const int32_t* __restrict__ bc, const int32_t* __restrict__ tlen,
+                                                    const uint16_t* __restrict__ flag, const uint8_t* __restrict__ mapq,
+                                                    const uint64_t* __restrict__ roff,
+                                                    const uint32_t* __restrict__ bin_lo, const uint32_t* __restrict__ O,
+                                                    uint32_t* __restrict__ cur, Geom g, int cbits, int min_mapq,
+                                                    GElem* __restrict__ gel, uint32_t* __restrict__ first_read) {
+    extern __shared__ uint32_t cnt_lds[];
+#if MGP_XCD_REMAP
+    // blocks are dealt round-robin over the 8 XCDs: give each XCD a contiguous bin
+    // range so concurrently written runs of one cell share that XCD's L2
+    const int per = (g.nbins + 7) / 8;
+    const int b = (int)(blockIdx.x % 8) * per + (int)(blockIdx.x / 8);
+    if (b >= g.nbins) return;
+#else
+    const int b = blockIdx.x;
+#endif
+    const int nc = g.nc;
+    const int wid = threadIdx.x >> 6;
+    // kLds: counters in LDS seeded from the scanned row; else `cur`, a global copy of
+    // the scanned rows (one workgroup owns row b and the waves take turns)
+    uint32_t* cnt = kLds ? cnt_lds : cur + (size_t)b * nc;
+    if (kLds) {
+        for (int c = threadIdx.x; c < nc; c += blockDim.x) cnt_lds[c] = O[(size_t)b * nc + c];
     }
-    const int t = tlen[i];
-    GElem e;
-    e.w = roff[i] | (f & MGP_FLAG_REVERSE ? GM_REV : 0ull) | (f & MGP_FLAG_PAIRED ? GM_PAIRED : 0ull) |
-          ((int)mapq[i] >= min_mapq ? GM_MAPQ_OK : 0ull) | (f & MGP_FLAG_NOSEQQUAL ? GM_BAD : 0ull);
-    e.start = s;
-    e.tlen = t < 0 ? (uint32_t)(-(int64_t)t) : (uint32_t)t;
-    gel[dest] = e;
-    // the cell's first element in cell-major order is its first valid read in BAM order
-    if (r == 0 && dest == O[c]) first_read[c] = (uint32_t)i;
+    const int64_t lo = bin_lo[b], hi = max((int64_t)bin_lo[b + 1], lo);
+    const unsigned long long lt = lanemask_lt();
+    __syncthreads();
+    constexpr int kAhead = 4;  // rounds of 256 reads whose loads are issued together
+    for (int64_t base0 = lo; base0 < hi; base0 += kAhead * kBlock) {
+        int cc[kAhead], ss[kAhead], tt[kAhead];
+        uint16_t ff[kAhead];
+        uint8_t mm[kAhead];
+        uint64_t oo[kAhead];
+#pragma unroll
+        for (int u = 0; u < kAhead; ++u) {
+            const int64_t i = base0 + u * kBlock + threadIdx.x;
+            cc[u] = -1;
+            ff[u] = 0;
+            if (i < hi) {
+                cc[u] = bc[i];
+                ff[u] = flag[i];
+                ss[u] = start[i];
+                tt[u] = tlen[i];
+                mm[u] = mapq[i];
+                oo[u] = roff[i];
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < kAhead; ++u) {
+            const int64_t i = base0 + u * kBlock + threadIdx.x;
+            if (base0 + u * kBlock >= hi) break;  // uniform
+            const int c = cc[u];
+            const uint16_t f = ff[u];
+            const bool valid = i < hi && read_valid(c, f, nc);
+            unsigned long long peers = __ballot(valid);
+            for (int bit = 0; bit < cbits && peers; ++bit) {
+                const bool x = valid && ((c >> bit) & 1);
+                const unsigned long long m = __ballot(x);
+                peers &= x ? m : ~m;
+            }
+            uint32_t dest = 0;
+#pragma unroll
+            for (int w = 0; w < kBlock / kWave; ++w) {
+                if (wid == w && valid) {
+                    const uint32_t before = cnt[c];
+                    dest = before + (uint32_t)__popcll(peers & lt);
+                    if ((peers & lt) == 0ull) cnt[c] = before + (uint32_t)__popcll(peers);  // group leader
+                }
+                if (!kLds) __threadfence_block();
+                __syncthreads();
+            }
+            if (valid) {
+                const int t = tt[u];
+                GElem e;
+                e.w = oo[u] | (f & MGP_FLAG_REVERSE ? GM_REV : 0ull) | (f & MGP_FLAG_PAIRED ? GM_PAIRED : 0ull) |
+                      ((int)mm[u] >= min_mapq ? GM_MAPQ_OK : 0ull) | (f & MGP_FLAG_NOSEQQUAL ? GM_BAD : 0ull);
+                e.start = ss[u];
+                e.tlen = t < 0 ? (uint32_t)(-(int64_t)t) : (uint32_t)t;
+                gel[dest] = e;
+                // the cell's first element in cell-major order is its first valid read in BAM order
+                if (dest == O[c]) first_read[c] = (uint32_t)i;  // row 0 of the scan = cell base
+            }
+        }
+    }
 }
 
 struct PileCfg {
@@ -595,7 +627,10 @@ __device__ __forceinline__ void pile_read(bool has, const uint8_t* __restrict__ 
     if (has && !fast) pile_slow(rec, start, lseq, ncig, coff, strand, w, pc, tile, max_span, span_err);
 }
 
-constexpr int kMaxPosPerThread = 4;  // W <= 4 * 256
+#ifndef MGP_WIN
+#define MGP_WIN 1024  // target window width (positions); W <= kMaxPosPerThread * 256
+#endif
+constexpr int kMaxPosPerThread = MGP_WIN / 256;
 constexpr int kWaveQ = 2 * kWave;    // per-wave queue of reads waiting to be piled (LDS)
 constexpr uint32_t kSeg = 65535;     // elements per tile segment (16-bit halves cannot carry)
 
@@ -613,6 +648,9 @@ __device__ __forceinline__ bool same_dup(const GElem& p, const GElem& e, bool& d
 // MAPQ-passing reads go to the wave's LDS queue and are piled 64 at a time, one
 // read per lane. Workgroup barriers only at cell boundaries; the packed tile is
 // then strand-filtered and flushed.
+#ifndef MGP_XCD_REMAP
+#define MGP_XCD_REMAP 0
+#endif
 #ifndef MGP_PILEUP_WAVES
 #define MGP_PILEUP_WAVES 4
 #endif
@@ -1055,7 +1093,7 @@ static int configure_geometry(mgp_ctx* ctx) {
     g.G = 8;
     g.nb_reg = (g.L + g.G - 1) / g.G;
     g.nbins = g.nb_reg + 1;
-    g.nwin = (g.L + 1023) / 1024;          // ~1 Ki positions per window (<= 4 * 256 per thread)
+    g.nwin = (g.L + MGP_WIN - 1) / MGP_WIN;  // ~MGP_WIN positions per window
     g.W = (g.L + g.nwin - 1) / g.nwin;
     g.W = ((g.W + g.G - 1) / g.G) * g.G;   // multiple of the bin width
     g.nwin = (g.L + g.W - 1) / g.W;
@@ -1119,7 +1157,9 @@ int mgp_open(const mgp_config* cfg, int hip_device, mgp_ctx** out) {
     {
         const int lds_max = (int)prop.sharedMemPerBlock;
         (void)hipFuncSetAttribute((const void*)k_median, hipFuncAttributeMaxDynamicSharedMemorySize, lds_max);
-        (void)hipFuncSetAttribute((const void*)k_bin_hist<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+        (void)hipFuncSetAttribute((const void*)k_bin_count<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  lds_max);
+        (void)hipFuncSetAttribute((const void*)k_scatter<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                   lds_max);
         (void)hipFuncSetAttribute((const void*)k_pileup, hipFuncAttributeMaxDynamicSharedMemorySize, lds_max);
         (void)hipGetLastError();
@@ -1158,7 +1198,7 @@ void mgp_close(mgp_ctx* ctx) {
     (void)hipStreamSynchronize(ctx->s_copy);
     if (ctx->comm) ncclCommDestroy(ctx->comm);
     DevBuf* bufs[] = {&ctx->start,     &ctx->bc,        &ctx->tlen,     &ctx->flag,       &ctx->mapq,
-                      &ctx->span,      &ctx->roff,      &ctx->payload,  &ctx->bin_start,  &ctx->rank,
+                      &ctx->span,      &ctx->roff,      &ctx->payload,  &ctx->bin_start,  &ctx->Hcur,
                       &ctx->H,         &ctx->P,         &ctx->cell_cnt, &ctx->cell_base,  &ctx->gel,
                       &ctx->tally_part, &ctx->tally,   &ctx->n_reads,    &ctx->any_paired,
                       &ctx->passed,    &ctx->covered,   &ctx->dsum,     &ctx->dmax,       &ctx->med_lo,
@@ -1249,7 +1289,6 @@ static int ensure_run_buffers(mgp_ctx* ctx) {
     const size_t nc = (size_t)std::max(g.nc, 1);
     const size_t L = (size_t)g.L;
     MGP_TRY(ctx->bin_start.ensure((size_t)(g.nbins + 1) * 4));
-    MGP_TRY(ctx->rank.ensure(n * 4));
     MGP_TRY(ctx->H.ensure((size_t)(g.nbins + 1) * nc * 4));
     MGP_TRY(ctx->P.ensure((size_t)((g.nbins + 31) / 32 + 1) * nc * 4));
     MGP_TRY(ctx->cell_cnt.ensure(nc * 4));
@@ -1299,38 +1338,29 @@ int mgp_run(mgp_ctx* ctx) {
         HIP_TRY(hipMemsetAsync(ctx->first_read.p, 0xFF, (size_t)nc * 4, s));
     }
 
-    // 1. start-bin boundaries
-    STAGE_BEGIN(ST_BINS);
-    HIP_TRY(hipMemsetAsync(ctx->bin_start.p, 0, (size_t)(g.nbins + 1) * 4, s));
-    if (n > 0) {
-        k_bin_bounds<<<blocks_for(n), kBlock, 0, s>>>(ctx->start.as<int32_t>(), n, g, ctx->bin_start.as<uint32_t>(),
-                                                       st);
-        HIP_TRY(hipGetLastError());
-    }
-    STAGE_END(ST_BINS);
-
     if (nc > 0) {
-        // 2. (bin, cell) histogram + stable ranks
-        STAGE_BEGIN(ST_HIST);
-        const bool lds = nc <= ctx->lds_hist_max_cells;
         int cbits = 1;
         while (cbits < 31 && (1 << cbits) < nc) ++cbits;
+        const bool lds = nc <= ctx->lds_hist_max_cells;
+        // 1. per (start bin, cell) histogram + bin bounds + order check
+        STAGE_BEGIN(ST_HIST);
         if (!lds || n == 0) HIP_TRY(hipMemsetAsync(ctx->H.p, 0, (size_t)(g.nbins + 1) * nc * 4, s));
+        if (n == 0) HIP_TRY(hipMemsetAsync(ctx->bin_start.p, 0, (size_t)(g.nbins + 1) * 4, s));
         if (n > 0) {
             if (lds)
-                k_bin_hist<true><<<g.nbins, kWave, (size_t)nc * 4, s>>>(
-                    ctx->bin_start.as<uint32_t>(), ctx->bc.as<int32_t>(), ctx->flag.as<uint16_t>(),
-                    ctx->span.as<uint32_t>(), n, g, cbits, ctx->H.as<uint32_t>(), ctx->rank.as<uint32_t>(), st);
+                k_bin_count<true><<<g.nbins, kBlock, (size_t)nc * 4, s>>>(
+                    ctx->start.as<int32_t>(), ctx->bc.as<int32_t>(), ctx->flag.as<uint16_t>(),
+                    ctx->span.as<uint32_t>(), n, g, ctx->H.as<uint32_t>(), ctx->bin_start.as<uint32_t>(), st);
             else
-                k_bin_hist<false><<<g.nbins, kWave, 0, s>>>(ctx->bin_start.as<uint32_t>(), ctx->bc.as<int32_t>(),
-                                                            ctx->flag.as<uint16_t>(), ctx->span.as<uint32_t>(), n, g,
-                                                            cbits, ctx->H.as<uint32_t>(), ctx->rank.as<uint32_t>(),
-                                                            st);
+                k_bin_count<false><<<g.nbins, kBlock, 0, s>>>(ctx->start.as<int32_t>(), ctx->bc.as<int32_t>(),
+                                                              ctx->flag.as<uint16_t>(), ctx->span.as<uint32_t>(), n,
+                                                              g, ctx->H.as<uint32_t>(), ctx->bin_start.as<uint32_t>(),
+                                                              st);
             HIP_TRY(hipGetLastError());
         }
         STAGE_END(ST_HIST);
 
-        // 3. cell-major exclusive scan of the histogram
+        // 2. cell-major exclusive scan of the histogram
         STAGE_BEGIN(ST_SCAN);
         const int RB = 32;
         const int nrb = (g.nbins + RB - 1) / RB;
@@ -1343,13 +1373,26 @@ int mgp_run(mgp_ctx* ctx) {
         HIP_TRY(hipGetLastError());
         STAGE_END(ST_SCAN);
 
-        // 4. scatter grouping elements
+        // 3. stable scatter of the grouping elements
         STAGE_BEGIN(ST_SCATTER);
         if (n > 0) {
-            k_scatter<<<blocks_for(n), kBlock, 0, s>>>(
-                n, ctx->start.as<int32_t>(), ctx->bc.as<int32_t>(), ctx->tlen.as<int32_t>(), ctx->flag.as<uint16_t>(),
-                ctx->mapq.as<uint8_t>(), ctx->roff.as<uint64_t>(), ctx->rank.as<uint32_t>(), ctx->H.as<uint32_t>(), g,
-                ctx->cfg.min_mapq, ctx->gel.as<GElem>(), ctx->first_read.as<uint32_t>(), st);
+            const unsigned sgrid = MGP_XCD_REMAP ? (unsigned)(((g.nbins + 7) / 8) * 8) : (unsigned)g.nbins;
+            if (lds) {
+                k_scatter<true><<<sgrid, kBlock, (size_t)nc * 4, s>>>(
+                    n, ctx->start.as<int32_t>(), ctx->bc.as<int32_t>(), ctx->tlen.as<int32_t>(),
+                    ctx->flag.as<uint16_t>(), ctx->mapq.as<uint8_t>(), ctx->roff.as<uint64_t>(),
+                    ctx->bin_start.as<uint32_t>(), ctx->H.as<uint32_t>(), nullptr, g, cbits, ctx->cfg.min_mapq,
+                    ctx->gel.as<GElem>(), ctx->first_read.as<uint32_t>());
+            } else {
+                MGP_TRY(ctx->Hcur.ensure((size_t)(g.nbins + 1) * nc * 4));
+                HIP_TRY(hipMemcpyAsync(ctx->Hcur.p, ctx->H.p, (size_t)(g.nbins + 1) * nc * 4,
+                                       hipMemcpyDeviceToDevice, s));
+                k_scatter<false><<<sgrid, kBlock, 0, s>>>(
+                    n, ctx->start.as<int32_t>(), ctx->bc.as<int32_t>(), ctx->tlen.as<int32_t>(),
+                    ctx->flag.as<uint16_t>(), ctx->mapq.as<uint8_t>(), ctx->roff.as<uint64_t>(),
+                    ctx->bin_start.as<uint32_t>(), ctx->H.as<uint32_t>(), ctx->Hcur.as<uint32_t>(), g, cbits,
+                    ctx->cfg.min_mapq, ctx->gel.as<GElem>(), ctx->first_read.as<uint32_t>());
+            }
             HIP_TRY(hipGetLastError());
         }
         STAGE_END(ST_SCATTER);

@@ -230,3 +230,14 @@ def test_deep_cell_median_fallback(engine_lib, oracle_lib):
     reads.sort(key=lambda r: r["reference_start"])
     res = _both(engine_lib, oracle_lib, reads, 2, dedup_mode="alignment_and_fragment_length")
     assert res.depth_max[0] >= 8192
+
+
+def test_many_cells_global_histogram_path(engine_lib, oracle_lib):
+    """More cells than the LDS histogram holds: global-row histogram and counters."""
+    from mgatk2_amd.engine import EngineConfig
+
+    soa = _synth(77, 150_000, 30_000)
+    cfg = EngineConfig(n_cells=30_000, min_baseq=0, min_mapq=0, dedup_mode="alignment_start", min_reads=0)
+    res = run_engine(engine_lib, cfg, soa)
+    exp, _ = oracle_lib.oracle_run(cfg, soa)
+    assert_same(res, exp, "30k cells")
