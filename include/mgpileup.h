@@ -75,6 +75,11 @@ extern "C" {
 #define MGP_FLAG_SUPPLEMENTARY 0x0800u
 #define MGP_FLAG_NOSEQQUAL     0x1000u
 
+/* mgp_config.flags */
+#define MGP_CFG_KEEP_TN5       0x1  /* keep Tn5 counts at positions of depth 0 (the unfiltered
+                                       generate_pileup() view, pileup.py:100-124); off = the
+                                       strand-filtered result the writers consume (pileup.py:151-152) */
+
 /* Engine configuration: the POD restatement of PipelineConfig
  * (src/core/config.py:77-114) restricted to what the hot path reads. */
 typedef struct mgp_config {
@@ -87,7 +92,7 @@ typedef struct mgp_config {
     int32_t min_reads;          /* PipelineConfig.min_reads_per_cell    (processors.py:22) */
     int32_t n_cells;            /* whitelist length = HDF5 column count (writers.py:42) */
     int32_t mito_len;           /* PipelineConfig.mito_length, 16569    (config.py:95)  */
-    int32_t flags;              /* reserved, must be 0                                  */
+    int32_t flags;              /* MGP_CFG_* bits                                       */
     int64_t reserve_reads;      /* capacity hint for resident reads (grows on demand)   */
     int64_t reserve_payload;    /* capacity hint for resident payload bytes             */
 } mgp_config;

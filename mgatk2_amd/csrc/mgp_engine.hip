@@ -401,6 +401,7 @@ struct PileCfg {
     int min_baseq, min_dist, min_reads, dedup_mode;
     double max_bias;
     bool bias_active;  // max_bias < 1 (max/total <= 1 otherwise)
+    bool keep_tn5;     // MGP_CFG_KEEP_TN5
 };
 
 __device__ __forceinline__ int base_index(uint32_t code) {
@@ -843,7 +844,7 @@ __global__ void __launch_bounds__(kBlock, MGP_PILEUP_WAVES) k_pileup(
                     tal[m][b] += t2;
                     d += t2;
                 }
-                if (d == 0) tf = tr = 0;
+                if (d == 0 && !pc.keep_tn5) tf = tr = 0;
                 uint4* cp = reinterpret_cast<uint4*>(counts + P * 8);
                 cp[0] = make_uint4(v[0], v[1], v[2], v[3]);
                 cp[1] = make_uint4(v[4], v[5], v[6], v[7]);
@@ -1134,7 +1135,7 @@ int mgp_open(const mgp_config* cfg, int hip_device, mgp_ctx** out) {
     if (cfg->mito_len <= 0 || cfg->mito_len > (1 << 24)) return set_err(MGP_E_INVALID, "mito_len out of range");
     if (cfg->n_cells < 0) return set_err(MGP_E_INVALID, "n_cells < 0");
     if (cfg->dedup_mode < 0 || cfg->dedup_mode > 2) return set_err(MGP_E_INVALID, "dedup_mode out of range");
-    if (cfg->flags != 0) return set_err(MGP_E_INVALID, "config.flags must be 0");
+    if (cfg->flags & ~MGP_CFG_KEEP_TN5) return set_err(MGP_E_INVALID, "unknown config.flags bits");
     int ndev = 0;
     HIP_TRY(hipGetDeviceCount(&ndev));
     if (hip_device < 0 || hip_device >= ndev)
@@ -1406,6 +1407,7 @@ int mgp_run(mgp_ctx* ctx) {
         pc.dedup_mode = ctx->cfg.dedup_mode;
         pc.max_bias = ctx->cfg.max_strand_bias;
         pc.bias_active = ctx->cfg.max_strand_bias < 1.0;
+        pc.keep_tn5 = (ctx->cfg.flags & MGP_CFG_KEEP_TN5) != 0;
         dim3 gp(g.nchunks, g.nwin);
         const size_t psm = (size_t)5 * g.Wp * 4;
         k_pileup<<<gp, kBlock, psm, s>>>(g, pc, ctx->payload.as<uint8_t>(), ctx->gel.as<GElem>(),

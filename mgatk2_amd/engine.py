@@ -206,13 +206,14 @@ class EngineConfig:
     mito_len: int = 16569
     reserve_reads: int = 0
     reserve_payload: int = 0
+    keep_tn5: bool = False  # MGP_CFG_KEEP_TN5
 
     def to_c(self) -> mgp_config:
         dm = DEDUP_MODES[self.dedup_mode] if isinstance(self.dedup_mode, str) else int(self.dedup_mode)
         return mgp_config(
             int(self.min_baseq), int(self.min_mapq), int(self.min_distance_from_end), dm,
-            float(self.max_strand_bias), int(self.min_reads), int(self.n_cells), int(self.mito_len), 0,
-            int(self.reserve_reads), int(self.reserve_payload),
+            float(self.max_strand_bias), int(self.min_reads), int(self.n_cells), int(self.mito_len),
+            1 if self.keep_tn5 else 0, int(self.reserve_reads), int(self.reserve_payload),
         )
 
 
@@ -368,6 +369,14 @@ class Engine:
     def finish(self, dense: bool = True) -> EngineResult:
         self.run()
         return self.fetch(dense)
+
+    def finish_raw(self) -> tuple[np.ndarray, np.ndarray]:
+        """Unfiltered counts/Tn5 of a single-cell context (PileupGenerator.generate_pileup view)."""
+        if self.cfg.n_cells != 1 or self.cfg.max_strand_bias < 1.0 or not self.cfg.keep_tn5:
+            raise InvalidInputError("finish_raw needs n_cells=1, max_strand_bias>=1 and keep_tn5")
+        self.run()
+        r = self.fetch(dense=True)
+        return r.counts[0], r.tn5[0]
 
     def kernel_times(self, last_runs: int = 1) -> dict[str, float]:
         """Per-stage device ms averaged over the last `last_runs` runs (HIP events)."""

@@ -1,0 +1,324 @@
+"""Output writers (mirror of src/file_io/writers.py).
+
+The reference writers consume one per-position dict per cell
+(``write_cell(result)``, writers.py:136,430). Here the engine hands over dense
+cell-major arrays (:class:`mgatk2_amd.engine.EngineResult`), and the writers
+format directly from them:
+
+* :class:`IncrementalTextWriter` — mgatk txt layout (writers.py:409-510):
+  ``output.{A,C,G,T,coverage}.txt.gz``, ``output.depthTable.txt``,
+  ``{mito_chr}_refAllele.txt``, ``qc/cell_stats.csv``.
+* :class:`IncrementalHDF5Writer` — ``counts.h5`` / ``metadata.h5``
+  (writers.py:20-406): uint16 ``[16569, n_barcodes]`` planes saturated at 65535,
+  whitelist-indexed columns, per-cell metadata, reference alleles, optional
+  ``barcode_metadata`` group. Needs an h5py-compatible module.
+
+Both keep the reference's ``write_cell(result_dict)`` / ``finalize(qc_dir)``
+API (for callers of the per-cell path) and add ``write_cells(res, cells)`` for
+the array path. Cell order = the order cells are written in (first-seen BAM
+order, the reference's sequential order).
+"""
+
+from __future__ import annotations
+
+import gzip
+import logging
+import shutil
+from pathlib import Path
+
+import numpy as np
+
+from .formats import write_cell_stats
+
+logger = logging.getLogger(__name__)
+
+BASES = ["A", "C", "G", "T"]
+STRANDS = ["fwd", "rev"]
+
+
+# ---------------------------------------------------------------------------
+# per-cell views of the engine result
+# ---------------------------------------------------------------------------
+def cell_qc(res, c: int, barcode: str, mito_length: int) -> dict:
+    """processors.py:33-51 for a passing cell."""
+    n = int(res.n_reads[c])
+    covered = int(res.covered[c])
+    mean_cov = float(res.depth_sum[c]) / covered  # == np.mean of the kept depths (exact int sum / n)
+    return {
+        "barcode": barcode,
+        "total_reads": n,
+        "total_fragments": n // 2 if res.any_paired[c] else n,
+        "mean_depth": mean_cov,
+        "coverage_breadth": covered / mito_length if mito_length > 0 else 0,
+    }
+
+
+def ref_alleles(tally: np.ndarray) -> list[str]:
+    """Reference allele per position: first max over A<C<G<T, N if all zero (writers.py:340-349)."""
+    t = np.asarray(tally)
+    m = np.argmax(t, axis=1)  # argmax returns the first maximum
+    best = t[np.arange(t.shape[0]), m]
+    return [("ACGT"[k] if v > 0 else "N") for k, v in zip(m.tolist(), best.tolist())]
+
+
+def pileup_dict_to_arrays(pileup: dict, mito_length: int):
+    """Inverse of the reference per-position dict (pileup.py:100-124) for one cell."""
+    counts = np.zeros((mito_length, 8), np.uint32)
+    tn5 = np.zeros((mito_length, 2), np.uint32)
+    depth = np.zeros(mito_length, np.uint32)
+    for pos, d in pileup.items():
+        for bi, b in enumerate(BASES):
+            counts[pos, 2 * bi] = d.get(f"{b}_fwd", 0)
+            counts[pos, 2 * bi + 1] = d.get(f"{b}_rev", 0)
+        tn5[pos, 0] = d.get("tn5_cuts_fwd", 0)
+        tn5[pos, 1] = d.get("tn5_cuts_rev", 0)
+        depth[pos] = d["depth"]
+    return counts, tn5, depth
+
+
+class _OneCell:
+    """Adapter: a single reference result dict seen through the EngineResult interface."""
+
+    def __init__(self, result: dict, mito_length: int):
+        self.counts, self.tn5, self.depth = pileup_dict_to_arrays(result["pileup"], mito_length)
+        self.counts = self.counts[None]
+        self.tn5 = self.tn5[None]
+        self.depth = self.depth[None]
+        qc = result.get("qc", {})
+        n = int(result.get("n_reads", qc.get("total_reads", 0)))
+        self.n_reads = np.array([n], np.uint32)
+        self.any_paired = np.array([qc.get("total_fragments", n) != n], np.uint8)
+        d = self.depth[0]
+        kept = d[d > 0]
+        self.covered = np.array([kept.size], np.uint32)
+        self.depth_sum = np.array([int(kept.sum())], np.uint64)
+        self.depth_max = np.array([int(kept.max()) if kept.size else 0], np.uint32)
+        s = np.sort(kept)
+        self.median_lo = np.array([s[(s.size - 1) // 2] if s.size else 0], np.uint32)
+        self.median_hi = np.array([s[s.size // 2] if s.size else 0], np.uint32)
+        self.qc = qc
+
+
+# ---------------------------------------------------------------------------
+# txt
+# ---------------------------------------------------------------------------
+class IncrementalTextWriter:
+    """mgatk txt format (writers.py:409-510)."""
+
+    def __init__(self, output_dir: Path, config, barcodes: list[str]):
+        self.output_dir = Path(output_dir) / "output"
+        self.output_dir.mkdir(exist_ok=True, parents=True)
+        self.config = config
+        self.barcodes = list(barcodes)
+        self.cell_stats: list[dict] = []
+        self.position_base_counts = np.zeros((config.mito_length, 4), np.int64)
+        self.cell_depths: dict[str, float] = {}
+        self.base_files = {b: open(self.output_dir / f"output.{b}.txt", "w") for b in BASES}
+        self.coverage_file = open(self.output_dir / "output.coverage.txt", "w")
+
+    # array path -----------------------------------------------------------
+    def write_cells(self, res, cells, barcodes: list[str] | None = None, tally: np.ndarray | None = None):
+        """Write the given cells (indices into `res`) in order."""
+        names = barcodes if barcodes is not None else self.barcodes
+        L = self.config.mito_length
+        for c in cells:
+            c = int(c)
+            bc = names[c]
+            self.cell_stats.append(cell_qc(res, c, bc, L))
+            self._emit(bc, res.counts[c], res.depth[c], float(res.depth_sum[c]) / int(res.covered[c]))
+        if tally is not None:
+            self.position_base_counts += tally.astype(np.int64)
+        else:
+            for c in cells:
+                cnt = res.counts[int(c)].astype(np.int64)
+                self.position_base_counts += cnt[:, 0::2] + cnt[:, 1::2]
+
+    def _emit(self, bc: str, counts: np.ndarray, depth: np.ndarray, mean_depth: float):
+        self.cell_depths[bc] = mean_depth
+        pos = np.flatnonzero(depth > 0)
+        p1 = (pos + 1).tolist()
+        self.coverage_file.write("".join(f"{p},{bc},{d}\n" for p, d in zip(p1, depth[pos].tolist())))
+        cp = counts[pos]
+        for bi, b in enumerate(BASES):
+            fw = cp[:, 2 * bi]
+            rv = cp[:, 2 * bi + 1]
+            sel = np.flatnonzero((fw > 0) | (rv > 0))
+            self.base_files[b].write(
+                "".join(f"{p1[i]},{bc},{f},{r}\n" for i, f, r in zip(sel.tolist(), fw[sel].tolist(), rv[sel].tolist()))
+            )
+
+    # reference per-cell API (writers.py:430-462) ----------------------------
+    def write_cell(self, result: dict):
+        one = _OneCell(result, self.config.mito_length)
+        if "qc" in result:
+            self.cell_stats.append(result["qc"])
+        kept = one.depth[0][one.depth[0] > 0]
+        mean = float(kept.sum()) / kept.size if kept.size else 0
+        self._emit(result["barcode"], one.counts[0], one.depth[0], mean)
+        cnt = one.counts[0].astype(np.int64)
+        self.position_base_counts += cnt[:, 0::2] + cnt[:, 1::2]
+
+    def finalize(self, qc_dir: Path):
+        for f in self.base_files.values():
+            f.close()
+        self.coverage_file.close()
+        logger.info("Compressing output .txt files...")
+        for name in [*BASES, "coverage"]:
+            txt_file = self.output_dir / f"output.{name}.txt"
+            gz_file = self.output_dir / f"output.{name}.txt.gz"
+            with open(txt_file, "rb") as f_in, gzip.open(gz_file, "wb", compresslevel=9) as f_out:
+                shutil.copyfileobj(f_in, f_out)
+            txt_file.unlink()
+        with open(self.output_dir / "output.depthTable.txt", "w") as f:
+            for cell, depth in sorted(self.cell_depths.items()):
+                f.write(f"{cell}\t{depth:.2f}\n")
+        refs = ref_alleles(self.position_base_counts)
+        with open(self.output_dir / f"{self.config.mito_chr}_refAllele.txt", "w") as f:
+            f.write("pos\tref\n")
+            f.write("".join(f"{p}\t{r}\n" for p, r in enumerate(refs, start=1)))
+        qc_dir = Path(qc_dir)
+        qc_dir.mkdir(exist_ok=True, parents=True)
+        if self.cell_stats:
+            write_cell_stats(self.cell_stats, qc_dir / "cell_stats.csv")
+
+
+# ---------------------------------------------------------------------------
+# HDF5
+# ---------------------------------------------------------------------------
+def _h5py():
+    try:
+        import h5py  # noqa: F401
+
+        return h5py
+    except ImportError as e:  # pragma: no cover - depends on the environment
+        raise ImportError(
+            "HDF5 output needs h5py (not installed); use --format txt or install h5py"
+        ) from e
+
+
+class IncrementalHDF5Writer:
+    """counts.h5 / metadata.h5 (writers.py:20-406)."""
+
+    def __init__(self, output_dir: Path, config, barcodes: list[str], barcode_metadata=None, h5=None):
+        self.h5 = h5 if h5 is not None else _h5py()
+        self.output_dir = Path(output_dir) / "output"
+        self.output_dir.mkdir(exist_ok=True, parents=True)
+        self.config = config
+        self.barcodes = list(barcodes)
+        self.barcode_to_idx = {bc: i for i, bc in enumerate(self.barcodes)}  # last duplicate wins
+        self.n_barcodes = len(self.barcodes)
+        self.n_positions = config.mito_length
+        self.barcode_metadata = barcode_metadata
+        self.cell_stats: list[dict] = []
+        self.position_base_counts = np.zeros((self.n_positions, 4), np.int64)
+        self.cell_depths: dict[str, float] = {}
+        L, n = self.n_positions, self.n_barcodes
+        # column buffers; flushed once per dataset (the reference writes per 250-cell batch)
+        self._planes = {f"{b}_{s}": np.zeros((L, n), np.uint16) for b in BASES for s in STRANDS}
+        self._tn5 = {s: np.zeros((L, n), np.uint16) for s in STRANDS}
+        self._coverage = np.zeros((L, n), np.uint16)
+        self._meta = {
+            "mean_depth": np.zeros(n, np.float32),
+            "median_depth": np.zeros(n, np.float32),
+            "max_depth": np.zeros(n, np.uint16),
+            "genome_coverage": np.zeros(n, np.float32),
+            "total_bases": np.zeros(n, np.float32),
+        }
+
+    def _put(self, col: int, counts: np.ndarray, tn5: np.ndarray, depth: np.ndarray, med_lo: int, med_hi: int,
+             depth_sum: int, covered: int, depth_max: int):
+        sat = np.minimum(counts, 65535).astype(np.uint16)
+        for bi, b in enumerate(BASES):
+            self._planes[f"{b}_fwd"][:, col] = sat[:, 2 * bi]
+            self._planes[f"{b}_rev"][:, col] = sat[:, 2 * bi + 1]
+        t = np.minimum(tn5, 65535).astype(np.uint16)
+        self._tn5["fwd"][:, col] = t[:, 0]
+        self._tn5["rev"][:, col] = t[:, 1]
+        self._coverage[:, col] = np.minimum(depth, 65535).astype(np.uint16)
+        mean = float(depth_sum) / covered
+        self._meta["mean_depth"][col] = mean
+        self._meta["median_depth"][col] = (float(med_lo) + float(med_hi)) / 2.0  # np.median of ints
+        self._meta["max_depth"][col] = min(int(depth_max), 65535)
+        self._meta["genome_coverage"][col] = covered / self.n_positions * 100
+        self._meta["total_bases"][col] = np.float32(np.int64(depth_sum))
+        return mean
+
+    def write_cells(self, res, cells, barcodes: list[str] | None = None, tally: np.ndarray | None = None):
+        names = barcodes if barcodes is not None else self.barcodes
+        for c in cells:
+            c = int(c)
+            bc = names[c]
+            if bc not in self.barcode_to_idx:
+                continue
+            col = self.barcode_to_idx[bc]
+            self.cell_stats.append(cell_qc(res, c, bc, self.n_positions))
+            self.cell_depths[bc] = self._put(
+                col, res.counts[c], res.tn5[c], res.depth[c], int(res.median_lo[c]), int(res.median_hi[c]),
+                int(res.depth_sum[c]), int(res.covered[c]), int(res.depth_max[c]),
+            )
+        if tally is not None:
+            self.position_base_counts += tally.astype(np.int64)
+        else:
+            for c in cells:
+                cnt = res.counts[int(c)].astype(np.int64)
+                self.position_base_counts += cnt[:, 0::2] + cnt[:, 1::2]
+
+    def write_cell(self, result: dict):
+        """Reference per-cell API (writers.py:136-152)."""
+        bc = result["barcode"]
+        if bc not in self.barcode_to_idx:
+            return
+        one = _OneCell(result, self.n_positions)
+        if "qc" in result:
+            self.cell_stats.append(result["qc"])
+        col = self.barcode_to_idx[bc]
+        self.cell_depths[bc] = self._put(
+            col, one.counts[0], one.tn5[0], one.depth[0], int(one.median_lo[0]), int(one.median_hi[0]),
+            int(one.depth_sum[0]), int(one.covered[0]), int(one.depth_max[0]),
+        )
+        cnt = one.counts[0].astype(np.int64)
+        self.position_base_counts += cnt[:, 0::2] + cnt[:, 1::2]
+
+    def finalize(self, qc_dir: Path):
+        h5 = self.h5
+        L, n = self.n_positions, self.n_barcodes
+        chunks = (min(1000, L), min(100, n)) if n else None
+        comp = dict(compression="gzip", compression_opts=4)
+        counts_file = h5.File(self.output_dir / "counts.h5", "w", libver="latest")
+        counts_file.attrs["n_cells"] = n
+        counts_file.attrs["n_positions"] = L
+        counts_file.attrs["mito_chr"] = self.config.mito_chr
+        counts_file.create_dataset("barcode", data=np.array(self.barcodes, dtype="S"))
+        for b in BASES:
+            for s in STRANDS:
+                counts_file.create_dataset(f"{b}_{s}", data=self._planes[f"{b}_{s}"], chunks=chunks, **comp)
+        for s in STRANDS:
+            counts_file.create_dataset(f"tn5_cuts_{s}", data=self._tn5[s], chunks=chunks, **comp)
+        meta = h5.File(self.output_dir / "metadata.h5", "w", libver="latest")
+        meta.attrs["mito_chr"] = self.config.mito_chr
+        meta.attrs["mito_length"] = L
+        meta.create_dataset("coverage", data=self._coverage, chunks=chunks, **comp)
+        for k, v in self._meta.items():
+            meta.create_dataset(k, data=v)
+        refs = ref_alleles(self.position_base_counts)
+        meta.create_dataset("reference", data=np.array(refs, dtype="S1"), **comp)
+        if self.barcode_metadata is not None:
+            grp = meta.create_group("barcode_metadata")
+            bl = self.barcode_metadata.get("barcode", [])
+            b2i = {bc: i for i, bc in enumerate(bl)}
+            reorder = [b2i[bc] for bc in self.barcodes if bc in b2i]
+            for col, values_list in self.barcode_metadata.items():
+                try:
+                    vals = [values_list[i] for i in reorder]
+                    arr = np.array(vals)
+                    if arr.dtype == object or (len(arr) > 0 and isinstance(arr[0], str)):
+                        arr = np.array(vals, dtype="S")
+                    grp.create_dataset(col, data=arr, **comp)
+                except Exception as e:  # writers.py:387-388
+                    logger.warning("Could not store metadata column '%s': %s", col, e)
+        counts_file.close()
+        meta.close()
+        qc_dir = Path(qc_dir)
+        qc_dir.mkdir(exist_ok=True, parents=True)
+        if self.cell_stats:
+            write_cell_stats(self.cell_stats, qc_dir / "cell_stats.csv")

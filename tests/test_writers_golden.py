@@ -1,0 +1,111 @@
+"""Writers against the reference's own outputs on the same inputs (tests/golden).
+
+The arrays fed to the writers come from the oracle (the checker), so this
+isolates the formatting/layout: txt files must match the reference byte for
+byte after gunzip; HDF5 datasets (captured through the same numpy-backed h5py
+stand-in the golden generator used) must match exactly.
+"""
+
+from __future__ import annotations
+
+import gzip
+import json
+import sys
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+from golden_io import CASES, Golden
+
+sys.path.insert(0, str(Path(__file__).resolve().parent / "golden"))
+
+TXT_CASES = [c for c in CASES if Golden(c).params["output_format"] == "txt"]
+H5_CASES = [c for c in CASES if Golden(c).params["output_format"] == "hdf5"]
+
+
+def _written(res):
+    order = res.cell_order()
+    return order[res.passed[order].astype(bool)]
+
+
+def _config(g):
+    from mgatk2_amd.config import PipelineConfig
+
+    p = g.params
+    return PipelineConfig(min_baseq=p["min_baseq"], min_mapq=p["min_mapq"], max_strand_bias=p["max_strand_bias"],
+                          skip_deduplication=p["skip_deduplication"],
+                          use_fragment_length_dedup=p["use_fragment_length_dedup"],
+                          min_reads_per_cell=p["min_reads_per_cell"])
+
+
+@pytest.mark.parametrize("case", TXT_CASES)
+def test_txt_writer_matches_reference(case, oracle_lib, tmp_path):
+    from mgatk2_amd.file_io import IncrementalTextWriter
+
+    g = Golden(case)
+    res, _ = oracle_lib.oracle_run(g.config(), g.soa)
+    w = IncrementalTextWriter(tmp_path, _config(g), g.whitelist)
+    w.write_cells(res, _written(res), tally=res.ref_tally)
+    w.finalize(tmp_path / "qc")
+    od = tmp_path / "output"
+    for name in ["A", "C", "G", "T", "coverage"]:
+        got = gzip.decompress((od / f"output.{name}.txt.gz").read_bytes()).decode()
+        assert got == str(g.exp(f"txt_{name}")), f"{case}: output.{name}.txt"
+    assert (od / "output.depthTable.txt").read_text() == str(g.exp("txt_depthTable"))
+    assert (od / "chrM_refAllele.txt").read_text() == str(g.exp("txt_refAllele"))
+    assert (tmp_path / "qc" / "cell_stats.csv").read_text() == str(g.exp("cell_stats"))
+
+
+@pytest.mark.parametrize("case", TXT_CASES[:2])
+def test_txt_writer_dict_api_matches_reference(case, oracle_lib, tmp_path):
+    """The reference per-cell API (write_cell(result_dict)) gives the same files."""
+    from mgatk2_amd.file_io import IncrementalTextWriter
+    from mgatk2_amd.processing.pileup import result_dict
+
+    g = Golden(case)
+    res, _ = oracle_lib.oracle_run(g.config(), g.soa)
+    w = IncrementalTextWriter(tmp_path, _config(g), g.whitelist)
+    for c in _written(res):
+        w.write_cell(result_dict(res, int(c), g.whitelist[int(c)], 16569))
+    w.finalize(tmp_path / "qc")
+    od = tmp_path / "output"
+    for name in ["A", "coverage"]:
+        got = gzip.decompress((od / f"output.{name}.txt.gz").read_bytes()).decode()
+        assert got == str(g.exp(f"txt_{name}"))
+    assert (tmp_path / "qc" / "cell_stats.csv").read_text() == str(g.exp("cell_stats"))
+
+
+@pytest.mark.parametrize("case", H5_CASES)
+def test_hdf5_writer_matches_reference(case, oracle_lib, tmp_path):
+    import make_golden as mg
+
+    from mgatk2_amd.file_io import IncrementalHDF5Writer
+
+    g = Golden(case)
+    res, _ = oracle_lib.oracle_run(g.config(), g.soa)
+    h5 = type("h5", (), {"File": mg.FakeH5File})
+    mg.FakeH5File.files.clear()
+    w = IncrementalHDF5Writer(tmp_path, _config(g), g.whitelist, h5=h5)
+    w.write_cells(res, _written(res), tally=res.ref_tally)
+    w.finalize(tmp_path / "qc")
+    cf, mf = mg.FakeH5File.files["counts.h5"], mg.FakeH5File.files["metadata.h5"]
+    for k, ds in cf.items.items():
+        exp = g.exp("h5c_" + k)
+        np.testing.assert_array_equal(ds.data, exp, err_msg=f"counts.h5/{k}")
+        assert ds.data.dtype == exp.dtype, k
+    for k, ds in mf.items.items():
+        if isinstance(ds, mg.FakeDataset):
+            exp = g.exp("h5m_" + k)
+            np.testing.assert_array_equal(ds.data, exp, err_msg=f"metadata.h5/{k}")
+            assert ds.data.dtype == exp.dtype, k
+    exp_keys = {f[len("exp_h5c_"):] for f in g.z.files if f.startswith("exp_h5c_") and not f.endswith("_json")}
+    assert set(cf.items) == exp_keys
+    assert json.loads(str(g.exp("h5c_attrs_json"))) == {k: (v.item() if hasattr(v, "item") else v)
+                                                         for k, v in cf.attrs.items()}
+    assert json.loads(str(g.exp("h5m_attrs_json"))) == {k: (v.item() if hasattr(v, "item") else v)
+                                                         for k, v in mf.attrs.items()}
+    kw = json.loads(str(g.exp("h5_kw_json")))
+    for k, ds in cf.items.items():
+        assert {a: (list(b) if isinstance(b, tuple) else b) for a, b in ds.kw.items()} == kw[k], k
+    assert (tmp_path / "qc" / "cell_stats.csv").read_text() == str(g.exp("cell_stats"))
