@@ -1,0 +1,81 @@
+/*
+ * mgpileup_host.h — host-side C-ABI of libmgphost.so (no GPU needed).
+ *
+ * BAM ingest for the engine: replaces what pysam does under
+ * `BAMReader.collect_reads_by_barcode` (src/processing/readers.py:85-165):
+ * BGZF inflate (multithreaded), `.bai` seek to the chrM records
+ * (`bam.fetch(mito_chr)`, readers.py:87-88), record decode, CB-tag whitelist
+ * lookup (readers.py:104-111), and packing into the engine's SoA batch +
+ * payload records (include/mgpileup.h). Also the two reader-side checks
+ * (readers.py:35-61) and the barcode auto-extraction pass
+ * (src/file_io/barcode_extraction.py:12-46).
+ *
+ * pysam semantics kept: query_sequence includes soft clips and is None when
+ * l_seq == 0; query_qualities is None when l_seq == 0 or qual[0] == 0xFF (both
+ * mapped to MGP_FLAG_NOSEQQUAL); cigartuples from the BAM CIGAR (or the CG tag
+ * for > 65535 operations); template_length is the signed TLEN.
+ */
+#ifndef MGPILEUP_HOST_H
+#define MGPILEUP_HOST_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct mgp_bam mgp_bam;
+
+/* Decoded reads of one reference, in BAM order, as an engine batch. The arrays
+ * are owned by the library until mgp_bam_free_batch. */
+typedef struct mgp_bam_batch {
+    int64_t   n_reads;
+    int32_t  *start;
+    int32_t  *bc;
+    int32_t  *tlen;
+    uint16_t *flag;
+    uint8_t  *mapq;
+    uint32_t *span;
+    uint64_t *rec_off;
+    uint8_t  *payload;
+    int64_t   payload_bytes;
+    int64_t   n_with_tag;      /* records carrying the barcode tag (any type) */
+    int64_t   first_tag_index; /* index of the first record with the tag, -1 if none */
+} mgp_bam_batch;
+
+const char *mgp_host_last_error(void);
+
+/* Open a BAM (BGZF) file and parse its header; uses `<path>.bai` when present. */
+int  mgp_bam_open(const char *path, int n_threads, mgp_bam **out);
+void mgp_bam_close(mgp_bam *bam);
+int  mgp_bam_n_refs(mgp_bam *bam);
+const char *mgp_bam_ref_name(mgp_bam *bam, int tid);
+int64_t mgp_bam_ref_len(mgp_bam *bam, int tid);
+int  mgp_bam_has_index(mgp_bam *bam);
+
+/* Barcode whitelist: CB value -> index in `barcodes` (last duplicate wins, as
+ * the reference's dict); `tag` is the 2-character tag name (e.g. "CB"). */
+int  mgp_bam_set_barcodes(mgp_bam *bam, const char *tag, const char *const *barcodes, int n);
+
+/* Bulk calling (readers.py:74,97-99): every record is assigned to `cell`
+ * whatever its tag; -1 switches back to whitelist lookup. Reset by
+ * mgp_bam_set_barcodes. */
+int  mgp_bam_set_bulk(mgp_bam *bam, int32_t cell);
+
+/* Decode every record of reference `tid` (fetch(contig) order) into `out`.
+ * Records are placed at multiples of `rec_align` bytes (16..4096, power of 2). */
+int  mgp_bam_read_ref(mgp_bam *bam, int tid, int rec_align, mgp_bam_batch *out);
+void mgp_bam_free_batch(mgp_bam_batch *b);
+
+/* Barcode auto-extraction pass (barcode_extraction.py:12-46): counts of the
+ * tag's string value over records of `tid` that are neither unmapped nor
+ * duplicates. Returns the number of distinct values; `*blob` receives
+ * "value\0count\n"-free packed entries: for each value, a NUL-terminated string
+ * followed by an int64 count (8 bytes, little endian). Free with mgp_host_buf_free. */
+int64_t mgp_bam_count_tag(mgp_bam *bam, int tid, const char *tag, uint8_t **blob, int64_t *blob_bytes);
+void mgp_host_buf_free(void *p);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MGPILEUP_HOST_H */

@@ -1,0 +1,341 @@
+"""BAM access for the host side.
+
+* :class:`BamFile` — ctypes binding of libmgphost.so (include/mgpileup_host.h):
+  the native BGZF/BAM decoder that replaces pysam under the reader
+  (src/processing/readers.py:37-92): header, `.bai` seek to chrM, chrM records
+  decoded straight into the engine's SoA batch.
+* :class:`BamWriter` / :func:`write_bai` — a small BGZF/BAM(/BAI) writer used
+  to build test fixtures and synthetic inputs (no pysam needed).
+"""
+
+from __future__ import annotations
+
+import ctypes as C
+import struct
+import zlib
+from pathlib import Path
+
+import numpy as np
+
+from .exceptions import BAMFormatError, BAMReadError, ProcessingError
+from .synth import SEQ_NT16, ReadSoA
+
+HOST_LIB = Path(__file__).resolve().parent / "_lib" / "libmgphost.so"
+_NT16 = {ch: i for i, ch in enumerate(SEQ_NT16)}
+CIGAR_OPS = "MIDNSHP=X"
+
+
+class mgp_bam_batch(C.Structure):
+    _fields_ = [
+        ("n_reads", C.c_int64),
+        ("start", C.POINTER(C.c_int32)),
+        ("bc", C.POINTER(C.c_int32)),
+        ("tlen", C.POINTER(C.c_int32)),
+        ("flag", C.POINTER(C.c_uint16)),
+        ("mapq", C.POINTER(C.c_uint8)),
+        ("span", C.POINTER(C.c_uint32)),
+        ("rec_off", C.POINTER(C.c_uint64)),
+        ("payload", C.POINTER(C.c_uint8)),
+        ("payload_bytes", C.c_int64),
+        ("n_with_tag", C.c_int64),
+        ("first_tag_index", C.c_int64),
+    ]
+
+
+_hlib = None
+
+
+def host_library() -> C.CDLL:
+    global _hlib
+    if _hlib is None:
+        if not HOST_LIB.exists():
+            from .build import build_host
+
+            build_host()
+        lib = C.CDLL(str(HOST_LIB))
+        vp = C.c_void_p
+        lib.mgp_host_last_error.restype = C.c_char_p
+        lib.mgp_bam_open.argtypes = [C.c_char_p, C.c_int, C.POINTER(vp)]
+        lib.mgp_bam_open.restype = C.c_int
+        lib.mgp_bam_close.argtypes = [vp]
+        lib.mgp_bam_close.restype = None
+        lib.mgp_bam_n_refs.argtypes = [vp]
+        lib.mgp_bam_ref_name.argtypes = [vp, C.c_int]
+        lib.mgp_bam_ref_name.restype = C.c_char_p
+        lib.mgp_bam_ref_len.argtypes = [vp, C.c_int]
+        lib.mgp_bam_ref_len.restype = C.c_int64
+        lib.mgp_bam_has_index.argtypes = [vp]
+        lib.mgp_bam_set_barcodes.argtypes = [vp, C.c_char_p, C.POINTER(C.c_char_p), C.c_int]
+        lib.mgp_bam_set_bulk.argtypes = [vp, C.c_int32]
+        lib.mgp_bam_read_ref.argtypes = [vp, C.c_int, C.c_int, C.POINTER(mgp_bam_batch)]
+        lib.mgp_bam_free_batch.argtypes = [C.POINTER(mgp_bam_batch)]
+        lib.mgp_bam_free_batch.restype = None
+        lib.mgp_bam_count_tag.argtypes = [vp, C.c_int, C.c_char_p, C.POINTER(C.POINTER(C.c_uint8)),
+                                          C.POINTER(C.c_int64)]
+        lib.mgp_bam_count_tag.restype = C.c_int64
+        lib.mgp_host_buf_free.argtypes = [vp]
+        lib.mgp_host_buf_free.restype = None
+        _hlib = lib
+    return _hlib
+
+
+def _err() -> str:
+    return (host_library().mgp_host_last_error() or b"").decode(errors="replace")
+
+
+class BamFile:
+    """Native BAM reader (header, reference list, chrM records -> engine SoA)."""
+
+    def __init__(self, path: str | Path, n_threads: int = 0):
+        self.lib = host_library()
+        self.path = str(path)
+        h = C.c_void_p()
+        if self.lib.mgp_bam_open(self.path.encode(), int(n_threads), C.byref(h)) != 0:
+            raise BAMFormatError(self.path, f"Cannot open: {_err()}")
+        self._h = h
+        n = self.lib.mgp_bam_n_refs(h)
+        self.references = tuple(self.lib.mgp_bam_ref_name(h, i).decode() for i in range(n))
+        self.lengths = tuple(int(self.lib.mgp_bam_ref_len(h, i)) for i in range(n))
+        self.has_index = bool(self.lib.mgp_bam_has_index(h))
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self.lib.mgp_bam_close(self._h)
+            self._h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def tid(self, contig: str) -> int:
+        return self.references.index(contig)
+
+    def read_soa(self, contig: str, barcodes: list[str], tag: str = "CB", rec_align: int = 128,
+                 bulk_cell: int = -1) -> ReadSoA:
+        """Every record of `contig` (fetch order) as an engine batch; bc = whitelist
+        index (last duplicate wins, like the reference's dict) or -1. With
+        ``bulk_cell >= 0`` every record goes to that cell (bulk calling)."""
+        arr = (C.c_char_p * max(1, len(barcodes)))(*[b.encode() for b in barcodes])
+        if self.lib.mgp_bam_set_barcodes(self._h, tag.encode(), arr, len(barcodes)) != 0:
+            raise ProcessingError(_err())
+        if bulk_cell >= 0 and self.lib.mgp_bam_set_bulk(self._h, int(bulk_cell)) != 0:
+            raise ProcessingError(_err())
+        b = mgp_bam_batch()
+        if self.lib.mgp_bam_read_ref(self._h, self.tid(contig), int(rec_align), C.byref(b)) != 0:
+            raise BAMReadError(self.path, f"Read error: {_err()}")
+        try:
+            n = int(b.n_reads)
+
+            def take(ptr, dtype, count):
+                if count == 0:
+                    return np.zeros(0, dtype)
+                return np.ctypeslib.as_array(ptr, shape=(count,)).astype(dtype, copy=True)
+
+            soa = ReadSoA(
+                take(b.start, np.int32, n), take(b.bc, np.int32, n), take(b.tlen, np.int32, n),
+                take(b.flag, np.uint16, n), take(b.mapq, np.uint8, n), take(b.span, np.uint32, n),
+                take(b.rec_off, np.uint64, n), take(b.payload, np.uint8, int(b.payload_bytes)),
+            )
+            soa.extra.update(n_with_tag=int(b.n_with_tag), first_tag_index=int(b.first_tag_index))
+            return soa
+        finally:
+            self.lib.mgp_bam_free_batch(C.byref(b))
+
+    def count_tag(self, contig: str, tag: str = "CB") -> dict[str, int]:
+        """Tag value counts over non-unmapped, non-duplicate records (barcode_extraction.py:22-32)."""
+        blob = C.POINTER(C.c_uint8)()
+        nbytes = C.c_int64()
+        n = self.lib.mgp_bam_count_tag(self._h, self.tid(contig), tag.encode(), C.byref(blob), C.byref(nbytes))
+        if n < 0:
+            raise BAMReadError(self.path, _err())
+        try:
+            raw = bytes(np.ctypeslib.as_array(blob, shape=(int(nbytes.value),))) if nbytes.value else b""
+        finally:
+            self.lib.mgp_host_buf_free(C.cast(blob, C.c_void_p))
+        out: dict[str, int] = {}
+        p = 0
+        for _ in range(n):
+            z = raw.index(b"\0", p)
+            key = raw[p:z].decode()
+            (cnt,) = struct.unpack_from("<q", raw, z + 1)
+            out[key] = cnt
+            p = z + 9
+        return out
+
+
+# ---------------------------------------------------------------------------
+# writer (fixtures / synthetic inputs)
+# ---------------------------------------------------------------------------
+_BGZF_EOF = bytes.fromhex("1f8b08040000000000ff0600424302001b0003000000000000000000")
+
+
+def _bgzf_block(data: bytes, level: int = 6) -> bytes:
+    co = zlib.compressobj(level, zlib.DEFLATED, -15)
+    cdata = co.compress(data) + co.flush()
+    bsize = len(cdata) + 25
+    hdr = struct.pack("<BBBBIBBHBBHH", 31, 139, 8, 4, 0, 0, 255, 6, 66, 67, 2, bsize)
+    return hdr + cdata + struct.pack("<II", zlib.crc32(data) & 0xFFFFFFFF, len(data))
+
+
+def reg2bin(beg: int, end: int) -> int:
+    end -= 1
+    if beg >> 14 == end >> 14:
+        return ((1 << 15) - 1) // 7 + (beg >> 14)
+    if beg >> 17 == end >> 17:
+        return ((1 << 12) - 1) // 7 + (beg >> 17)
+    if beg >> 20 == end >> 20:
+        return ((1 << 9) - 1) // 7 + (beg >> 20)
+    if beg >> 23 == end >> 23:
+        return ((1 << 6) - 1) // 7 + (beg >> 23)
+    if beg >> 26 == end >> 26:
+        return ((1 << 3) - 1) // 7 + (beg >> 26)
+    return 0
+
+
+class BamWriter:
+    """Write a coordinate-sorted BAM (+ optional .bai)."""
+
+    BLOCK = 0xFF00
+
+    def __init__(self, path: str | Path, refs: list[tuple[str, int]], text: str | None = None):
+        self.path = Path(path)
+        self.refs = refs
+        self.f = open(self.path, "wb")
+        self.coff = 0
+        self.buf = bytearray()
+        self.records: list[tuple[int, int, int, int, int]] = []  # (tid, beg, end, voff_beg, voff_end)
+        if text is None:
+            text = "@HD\tVN:1.6\tSO:coordinate\n" + "".join(f"@SQ\tSN:{n}\tLN:{ln}\n" for n, ln in refs)
+        tb = text.encode()
+        hdr = b"BAM\1" + struct.pack("<i", len(tb)) + tb + struct.pack("<i", len(refs))
+        for n, ln in refs:
+            nb = n.encode() + b"\0"
+            hdr += struct.pack("<i", len(nb)) + nb + struct.pack("<i", ln)
+        self._write(hdr)
+        self._flush()  # records start in a fresh block
+
+    def _voff(self) -> int:
+        return (self.coff << 16) | len(self.buf)
+
+    def _write(self, data: bytes):
+        self.buf += data
+        while len(self.buf) >= self.BLOCK:
+            blk = _bgzf_block(bytes(self.buf[: self.BLOCK]))
+            self.f.write(blk)
+            self.coff += len(blk)
+            del self.buf[: self.BLOCK]
+
+    def _flush(self):
+        if self.buf:
+            blk = _bgzf_block(bytes(self.buf))
+            self.f.write(blk)
+            self.coff += len(blk)
+            self.buf.clear()
+
+    def write(self, r: dict):
+        """r: tid, pos, flag, mapq, cigartuples, query_sequence (or None), query_qualities (or None),
+        template_length, tags (dict name -> str/int), query_name, next_tid, next_pos."""
+        name = (r.get("query_name", "r") + "\0").encode()
+        cig = r.get("cigartuples") or []
+        seq = r.get("query_sequence") or ""
+        qual = r.get("query_qualities")
+        lseq = len(seq)
+        cigb = b"".join(struct.pack("<I", (ln << 4) | op) for op, ln in cig)
+        codes = [_NT16[c] for c in seq.upper()]
+        if lseq & 1:
+            codes.append(0)
+        seqb = bytes((codes[i] << 4) | codes[i + 1] for i in range(0, len(codes), 2))
+        qualb = bytes([0xFF] * lseq) if qual is None else bytes(int(q) & 0xFF for q in qual)
+        aux = b""
+        for k, v in (r.get("tags") or {}).items():
+            if isinstance(v, str):
+                aux += k.encode() + b"Z" + v.encode() + b"\0"
+            else:
+                aux += k.encode() + b"i" + struct.pack("<i", int(v))
+        pos = int(r["pos"])
+        span = sum(ln for op, ln in cig if op in (0, 2, 3, 7, 8))
+        end = pos + max(span, 1)
+        bin_ = reg2bin(max(pos, 0), max(end, pos + 1)) if pos >= 0 else 4680
+        body = struct.pack(
+            "<iiBBHHHIiii", int(r.get("tid", 0)), pos, len(name), int(r.get("mapq", 60)), bin_, len(cig),
+            int(r.get("flag", 0)), lseq, int(r.get("next_tid", -1)), int(r.get("next_pos", -1)),
+            int(r.get("template_length", 0)),
+        ) + name + cigb + seqb + qualb + aux
+        vb = self._voff()
+        self._write(struct.pack("<I", len(body)) + body)
+        self.records.append((int(r.get("tid", 0)), pos, end, vb, self._voff()))
+
+    def close(self, index: bool = True):
+        self._flush()
+        self.f.write(_BGZF_EOF)
+        self.f.close()
+        if index:
+            write_bai(Path(str(self.path) + ".bai"), len(self.refs), self.records)
+
+
+def write_bai(path: Path, n_ref: int, records: list[tuple[int, int, int, int, int]]):
+    """Minimal BAI: per reference, bins with merged chunks + 16 kbp linear index."""
+    per_ref: list[dict] = [dict(bins={}, lin={}) for _ in range(n_ref)]
+    for tid, beg, end, vb, ve in records:
+        if tid < 0:
+            continue
+        ref = per_ref[tid]
+        b = reg2bin(max(beg, 0), max(end, beg + 1))
+        chunks = ref["bins"].setdefault(b, [])
+        if chunks and chunks[-1][1] == vb:
+            chunks[-1][1] = ve
+        else:
+            chunks.append([vb, ve])
+        for w in range(max(beg, 0) >> 14, (max(end, beg + 1) - 1 >> 14) + 1):
+            ref["lin"].setdefault(w, vb)
+    out = bytearray(b"BAI\1" + struct.pack("<i", n_ref))
+    for ref in per_ref:
+        out += struct.pack("<i", len(ref["bins"]))
+        for b, chunks in sorted(ref["bins"].items()):
+            out += struct.pack("<Ii", b, len(chunks))
+            for vb, ve in chunks:
+                out += struct.pack("<QQ", vb, ve)
+        nl = (max(ref["lin"]) + 1) if ref["lin"] else 0
+        out += struct.pack("<i", nl)
+        last = 0
+        for w in range(nl):
+            last = ref["lin"].get(w, last)
+            out += struct.pack("<Q", last)
+    Path(path).write_bytes(bytes(out))
+
+
+def soa_to_bam(path: str | Path, soa: ReadSoA, whitelist: list[str], contig: str = "chrM", mito_len: int = 16569,
+               index: bool = True, tag: str = "CB"):
+    """Write an engine batch as a BAM (chr1 placeholder + contig). Reads with bc = -1
+    alternate between no tag and a non-whitelisted barcode."""
+    from .synth import FLAG_NOSEQQUAL, unpack_record
+
+    w = BamWriter(path, [("chr1", 248956422), (contig, mito_len)])
+    for i in range(soa.n):
+        d = unpack_record(soa.payload, int(soa.rec_off[i]))
+        f = int(soa.flag[i])
+        q = d["query_qualities"]
+        seq = d["query_sequence"]
+        if f & FLAG_NOSEQQUAL:
+            if not seq:
+                seq, q = None, None
+            elif q and all(x == 0xFF for x in q):
+                q = None
+        b = int(soa.bc[i])
+        tags = {}
+        if b >= 0:
+            tags[tag] = whitelist[b]
+        elif i % 2 == 0:
+            tags[tag] = "NNNNNNNNNNNNNNNN-9"
+        w.write(dict(tid=1, pos=int(soa.start[i]), flag=f & 0xFFF, mapq=int(soa.mapq[i]),
+                     cigartuples=d["cigartuples"], query_sequence=seq, query_qualities=q,
+                     template_length=int(soa.tlen[i]), tags=tags, query_name=f"r{i}"))
+    w.close(index=index)

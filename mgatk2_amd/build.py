@@ -2,6 +2,7 @@
 
 * ``mgatk2_amd/_lib/libmgpileup.so`` — HIP engine + C-ABI, gfx950 only
   (``hipcc --offload-arch=gfx950``), linked against RCCL.
+* ``mgatk2_amd/_lib/libmgphost.so`` — host-side BAM ingest (g++, zlib).
 * ``oracle/_build/liboracle.so`` — the CPU restatement (test infrastructure).
 * ``oracle/_ref/`` is not built: the reference is pure Python (no native path
   to compile); its outputs are pinned through tests/golden/ instead.
@@ -19,6 +20,7 @@ PKG = ROOT / "mgatk2_amd"
 CSRC = PKG / "csrc"
 LIB_DIR = PKG / "_lib"
 ENGINE_SO = LIB_DIR / "libmgpileup.so"
+HOST_SO = LIB_DIR / "libmgphost.so"
 ORACLE_DIR = ROOT / "oracle"
 ORACLE_SO = ORACLE_DIR / "_build" / "liboracle.so"
 
@@ -56,6 +58,23 @@ def build_engine(force: bool = False, verbose: bool = False, out: Path | None = 
     return target
 
 
+def build_host(force: bool = False, verbose: bool = False) -> Path:
+    """libmgphost.so: native BAM ingest (include/mgpileup_host.h), plain C++ + zlib."""
+    srcs = [CSRC / "host" / "mgp_bam.cpp"]
+    deps = srcs + [ROOT / "include" / "mgpileup_host.h", ROOT / "include" / "mgpileup.h"]
+    if force or _stale(HOST_SO, deps):
+        LIB_DIR.mkdir(parents=True, exist_ok=True)
+        tmp = HOST_SO.with_suffix(".so.tmp")
+        cxx = shutil.which("g++") or "c++"
+        cmd = [cxx, "-O3", "-std=c++17", "-fPIC", "-shared", "-Wall", "-pthread", f"-I{ROOT / 'include'}",
+               *[str(s) for s in srcs], "-o", str(tmp), "-lz"]
+        if verbose:
+            print(" ".join(cmd))
+        subprocess.run(cmd, check=True)
+        os.replace(tmp, HOST_SO)
+    return HOST_SO
+
+
 def build_oracle(force: bool = False, verbose: bool = False) -> Path:
     deps = [ORACLE_DIR / "mgp_oracle.c", ROOT / "include" / "mgpileup.h"]
     if force or _stale(ORACLE_SO, deps):
@@ -72,6 +91,7 @@ def build_oracle(force: bool = False, verbose: bool = False) -> Path:
 
 def build_all(force: bool = False, verbose: bool = False) -> None:
     build_engine(force, verbose)
+    build_host(force, verbose)
     build_oracle(force, verbose)
 
 

@@ -1,0 +1,717 @@
+// mgp_bam.cpp — BAM ingest for the MI355X pileup engine (host side, libmgphost.so).
+//
+// Replaces pysam under BAMReader (src/processing/readers.py:35-165): BGZF
+// inflate on a thread pool, `.bai` seek to the first chrM record (what
+// `bam.fetch(mito_chr)` does, readers.py:87-88), record decode and packing into
+// the engine's SoA batch + payload records (include/mgpileup.h), CB-tag
+// whitelist lookup (readers.py:104-111). Also the tag count of the barcode
+// auto-extraction pass (src/file_io/barcode_extraction.py:22-32).
+#include <zlib.h>
+
+#include <algorithm>
+#include <atomic>
+#include <cerrno>
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <fcntl.h>
+#include <string>
+#include <thread>
+#include <unistd.h>
+#include <unordered_map>
+#include <vector>
+
+#include "../../../include/mgpileup.h"
+#include "../../../include/mgpileup_host.h"
+
+namespace {
+
+thread_local std::string g_err;
+int fail(const std::string& m) {
+    g_err = m;
+    return -1;
+}
+
+inline uint16_t rd16(const uint8_t* p) { uint16_t v; std::memcpy(&v, p, 2); return v; }
+inline uint32_t rd32(const uint8_t* p) { uint32_t v; std::memcpy(&v, p, 4); return v; }
+inline int32_t rdi32(const uint8_t* p) { int32_t v; std::memcpy(&v, p, 4); return v; }
+inline uint64_t rd64(const uint8_t* p) { uint64_t v; std::memcpy(&v, p, 8); return v; }
+
+uint64_t fnv1a(const char* s, size_t n) {
+    uint64_t h = 1469598103934665603ull;
+    for (size_t i = 0; i < n; ++i) {
+        h ^= (uint8_t)s[i];
+        h *= 1099511628211ull;
+    }
+    return h;
+}
+
+// open-addressing string -> index table (no allocation per lookup)
+struct StrTable {
+    std::vector<std::string> keys;
+    std::vector<int32_t> vals;
+    std::vector<int64_t> slot;  // index into keys, -1 = empty
+    std::vector<uint64_t> hash;
+    uint64_t mask = 0;
+    void build(const std::vector<std::string>& k, const std::vector<int32_t>& v) {
+        size_t cap = 16;
+        while (cap < k.size() * 2 + 1) cap <<= 1;
+        slot.assign(cap, -1);
+        hash.assign(cap, 0);
+        mask = cap - 1;
+        keys.clear();
+        vals.clear();
+        for (size_t i = 0; i < k.size(); ++i) put(k[i], v[i]);
+    }
+    void put(const std::string& key, int32_t v) {
+        const uint64_t h = fnv1a(key.data(), key.size());
+        uint64_t s = h & mask;
+        while (slot[s] >= 0) {
+            if (hash[s] == h && keys[slot[s]] == key) {
+                vals[slot[s]] = v;  // last duplicate wins (dict semantics)
+                return;
+            }
+            s = (s + 1) & mask;
+        }
+        slot[s] = (int64_t)keys.size();
+        hash[s] = h;
+        keys.push_back(key);
+        vals.push_back(v);
+    }
+    int32_t get(const char* p, size_t n) const {
+        if (slot.empty()) return -1;
+        const uint64_t h = fnv1a(p, n);
+        uint64_t s = h & mask;
+        while (slot[s] >= 0) {
+            const std::string& k = keys[slot[s]];
+            if (hash[s] == h && k.size() == n && std::memcmp(k.data(), p, n) == 0) return vals[slot[s]];
+            s = (s + 1) & mask;
+        }
+        return -1;
+    }
+};
+
+struct Block {
+    uint64_t coff;     // compressed offset of the block
+    uint32_t csize;    // whole block size
+    uint32_t isize;    // inflated size
+    size_t out_off;    // offset in the inflated buffer
+};
+
+}  // namespace
+
+struct mgp_bam {
+    int fd = -1;
+    std::string path;
+    int n_threads = 1;
+    int64_t file_size = 0;
+    std::vector<std::string> ref_names;
+    std::vector<int64_t> ref_lens;
+    uint64_t first_record_voff = 0;  // virtual offset right after the header
+    bool has_index = false;
+    std::vector<uint64_t> ref_first_voff;  // from the index; UINT64_MAX if the ref has no reads
+    StrTable wl;
+    char tag[2] = {'C', 'B'};
+    int32_t bulk_cell = -1;  // >= 0: every record goes to this cell (bulk calling)
+};
+
+namespace {
+
+// Reads [off, off+n) of the file.
+bool pread_all(int fd, uint8_t* dst, size_t n, uint64_t off) {
+    size_t done = 0;
+    while (done < n) {
+        ssize_t r = ::pread(fd, dst + done, n - done, (off_t)(off + done));
+        if (r < 0) {
+            if (errno == EINTR) continue;
+            return false;
+        }
+        if (r == 0) return false;
+        done += (size_t)r;
+    }
+    return true;
+}
+
+// Parse the BGZF block header at p (n bytes available); returns the block size or 0.
+uint32_t bgzf_block_size(const uint8_t* p, size_t n) {
+    if (n < 18 || p[0] != 31 || p[1] != 139 || p[2] != 8 || !(p[3] & 4)) return 0;
+    const uint16_t xlen = rd16(p + 10);
+    if (n < (size_t)12 + xlen) return 0;
+    const uint8_t* x = p + 12;
+    size_t i = 0;
+    while (i + 4 <= xlen) {
+        const uint16_t slen = rd16(x + i + 2);
+        if (x[i] == 66 && x[i + 1] == 67 && slen == 2) return (uint32_t)rd16(x + i + 4) + 1;
+        i += 4 + slen;
+    }
+    return 0;
+}
+
+bool inflate_block(const uint8_t* blk, uint32_t csize, uint8_t* out, uint32_t isize, z_stream* zs) {
+    const uint16_t xlen = rd16(blk + 10);
+    const uint8_t* cdata = blk + 12 + xlen;
+    const uint32_t clen = csize - 12 - xlen - 8;
+    if (inflateReset(zs) != Z_OK) return false;
+    zs->next_in = const_cast<uint8_t*>(cdata);
+    zs->avail_in = clen;
+    zs->next_out = out;
+    zs->avail_out = isize;
+    const int r = inflate(zs, Z_FINISH);
+    if (r != Z_STREAM_END || zs->avail_out != 0) return isize == 0 && r == Z_STREAM_END;
+    const uint32_t crc = rd32(blk + csize - 8);
+    return crc32(0, out, isize) == crc;
+}
+
+// A sequential reader over the inflated BGZF stream, inflating batches of
+// blocks in parallel.
+struct Stream {
+    mgp_bam* bam;
+    uint64_t coff;            // next compressed offset to read
+    std::vector<uint8_t> buf; // inflated bytes not consumed yet
+    size_t pos = 0;
+    bool eof = false;
+    size_t batch_bytes = 64u << 10;  // grows x4 per refill up to kMaxBatch
+    static constexpr size_t kMaxBatch = 64u << 20;
+
+    bool fill(size_t need) {
+        while (buf.size() - pos < need && !eof) {
+            if (!refill()) return false;
+        }
+        return buf.size() - pos >= need;
+    }
+
+    bool refill() {
+        if (coff >= (uint64_t)bam->file_size) {
+            eof = true;
+            return true;
+        }
+        const size_t want = (size_t)std::min<uint64_t>(batch_bytes, (uint64_t)bam->file_size - coff);
+        batch_bytes = std::min(kMaxBatch, batch_bytes * 4);
+        std::vector<uint8_t> raw(want);
+        if (!pread_all(bam->fd, raw.data(), want, coff)) {
+            fail("read error in " + bam->path);
+            return false;
+        }
+        std::vector<Block> blocks;
+        size_t p = 0, total = 0;
+        while (p < want) {
+            const uint32_t bs = bgzf_block_size(raw.data() + p, want - p);
+            if (bs == 0) {
+                if (blocks.empty()) {
+                    fail("not a BGZF block at offset " + std::to_string(coff + p));
+                    return false;
+                }
+                break;
+            }
+            if (p + bs > want) break;  // partial block: next batch
+            Block b;
+            b.coff = p;
+            b.csize = bs;
+            b.isize = rd32(raw.data() + p + bs - 4);
+            if (b.isize > 65536 || bs < 12u + rd16(raw.data() + p + 10) + 8u) {
+                fail("corrupt BGZF block at offset " + std::to_string(coff + p));
+                return false;
+            }
+            b.out_off = total;
+            total += b.isize;
+            blocks.push_back(b);
+            p += bs;
+        }
+        if (blocks.empty()) {
+            // a single block larger than the batch: read it alone
+            uint8_t hdr[18];
+            if (!pread_all(bam->fd, hdr, 18, coff)) return fail("truncated BGZF"), false;
+            const uint32_t bs = bgzf_block_size(hdr, 18);
+            if (!bs) return fail("bad BGZF header"), false;
+            if (coff + bs > (uint64_t)bam->file_size)
+                return fail("truncated BGZF block at offset " + std::to_string(coff) + " in " + bam->path), false;
+            batch_bytes = std::max<size_t>(batch_bytes, bs);
+            return refill();
+        }
+        // compact the consumed prefix, then inflate the batch into the tail
+        if (pos) {
+            buf.erase(buf.begin(), buf.begin() + (ptrdiff_t)pos);
+            pos = 0;
+        }
+        const size_t base = buf.size();
+        buf.resize(base + total);
+        std::atomic<size_t> next{0};
+        std::atomic<bool> ok{true};
+        const int nt = std::max(1, std::min<int>(bam->n_threads, (int)blocks.size()));
+        auto work = [&]() {
+            z_stream zs;
+            std::memset(&zs, 0, sizeof(zs));
+            if (inflateInit2(&zs, -15) != Z_OK) {
+                ok = false;
+                return;
+            }
+            for (;;) {
+                const size_t i = next.fetch_add(1);
+                if (i >= blocks.size()) break;
+                const Block& b = blocks[i];
+                if (!inflate_block(raw.data() + b.coff, b.csize, buf.data() + base + b.out_off, b.isize, &zs)) {
+                    ok = false;
+                    break;
+                }
+            }
+            inflateEnd(&zs);
+        };
+        std::vector<std::thread> th;
+        for (int t = 1; t < nt; ++t) th.emplace_back(work);
+        work();
+        for (auto& t : th) t.join();
+        if (!ok) return fail("BGZF inflate/CRC error in " + bam->path), false;
+        coff += p;
+        return true;
+    }
+
+    const uint8_t* peek() const { return buf.data() + pos; }
+    size_t avail() const { return buf.size() - pos; }
+};
+
+bool stream_at(mgp_bam* bam, uint64_t voff, Stream& st) {
+    st.bam = bam;
+    st.coff = voff >> 16;
+    st.buf.clear();
+    st.pos = 0;
+    st.eof = false;
+    const size_t uoff = voff & 0xFFFF;
+    if (uoff) {
+        if (!st.fill(uoff)) return false;
+        st.pos += uoff;
+    }
+    return true;
+}
+
+int parse_header(mgp_bam* bam) {
+    Stream st;
+    if (!stream_at(bam, 0, st)) return -1;
+    if (!st.fill(12)) return fail(g_err.empty() ? "truncated BAM header" : g_err);
+    const uint8_t* p = st.peek();
+    if (std::memcmp(p, "BAM\1", 4) != 0) return fail("not a BAM file (bad magic)");
+    const uint32_t l_text = rd32(p + 4);
+    if (!st.fill(8 + (size_t)l_text + 4)) return fail("truncated BAM header text");
+    st.pos += 8 + l_text;
+    const int32_t n_ref = rdi32(st.peek());
+    st.pos += 4;
+    if (n_ref < 0) return fail("negative n_ref");
+    // header bytes: magic + l_text + text + n_ref + sum(l_name + name + l_ref)
+    uint64_t hlen = 12 + (uint64_t)l_text;
+    for (int32_t r = 0; r < n_ref; ++r) {
+        if (!st.fill(4)) return fail("truncated reference list");
+        const uint32_t l_name = rd32(st.peek());
+        if (!st.fill(4 + (size_t)l_name + 4)) return fail("truncated reference entry");
+        const char* nm = (const char*)st.peek() + 4;
+        bam->ref_names.emplace_back(nm, strnlen(nm, l_name));
+        bam->ref_lens.push_back(rdi32(st.peek() + 4 + l_name));
+        st.pos += 4 + l_name + 4;
+        hlen += 4 + (uint64_t)l_name + 4;
+    }
+    // virtual offset of the first record: walk the blocks to the header's end
+    uint64_t coff = 0, acc = 0;
+    for (;;) {
+        uint8_t h[18];
+        if (!pread_all(bam->fd, h, 18, coff)) return fail("truncated BGZF while locating records");
+        const uint32_t bs = bgzf_block_size(h, 18);
+        if (!bs) return fail("bad BGZF block while locating records");
+        uint8_t tail[4];
+        if (!pread_all(bam->fd, tail, 4, coff + bs - 4)) return fail("truncated BGZF block");
+        const uint32_t isz = rd32(tail);
+        if (acc + isz > hlen) {
+            bam->first_record_voff = (coff << 16) | (hlen - acc);
+            break;
+        }
+        acc += isz;
+        coff += bs;
+        if (acc == hlen) {
+            bam->first_record_voff = coff << 16;
+            break;
+        }
+    }
+    return 0;
+}
+
+int load_index(mgp_bam* bam) {
+    const std::string ipath = bam->path + ".bai";
+    FILE* f = std::fopen(ipath.c_str(), "rb");
+    if (!f) return 0;
+    std::vector<uint8_t> d;
+    {
+        std::fseek(f, 0, SEEK_END);
+        const long sz = std::ftell(f);
+        std::fseek(f, 0, SEEK_SET);
+        d.resize((size_t)std::max(0L, sz));
+        if (sz > 0 && std::fread(d.data(), 1, d.size(), f) != d.size()) {
+            std::fclose(f);
+            return fail("cannot read " + ipath);
+        }
+        std::fclose(f);
+    }
+    size_t p = 0;
+    auto need = [&](size_t n) { return p + n <= d.size(); };
+    if (!need(8) || std::memcmp(d.data(), "BAI\1", 4) != 0) return fail("bad BAI magic in " + ipath);
+    const int32_t n_ref = rdi32(d.data() + 4);
+    p = 8;
+    if (n_ref != (int32_t)bam->ref_names.size()) return fail("BAI reference count does not match the BAM");
+    bam->ref_first_voff.assign((size_t)n_ref, UINT64_MAX);
+    for (int32_t r = 0; r < n_ref; ++r) {
+        if (!need(4)) return fail("truncated BAI");
+        const int32_t n_bin = rdi32(d.data() + p);
+        p += 4;
+        uint64_t first = UINT64_MAX;
+        for (int32_t b = 0; b < n_bin; ++b) {
+            if (!need(8)) return fail("truncated BAI");
+            const uint32_t bin = rd32(d.data() + p);
+            const int32_t n_chunk = rdi32(d.data() + p + 4);
+            p += 8;
+            if (!need((size_t)n_chunk * 16)) return fail("truncated BAI");
+            if (bin != 37450)
+                for (int32_t c = 0; c < n_chunk; ++c) first = std::min(first, rd64(d.data() + p + (size_t)c * 16));
+            p += (size_t)n_chunk * 16;
+        }
+        if (!need(4)) return fail("truncated BAI");
+        const int32_t n_intv = rdi32(d.data() + p);
+        p += 4 + (size_t)n_intv * 8;
+        if (p > d.size()) return fail("truncated BAI");
+        bam->ref_first_voff[(size_t)r] = first;
+    }
+    bam->has_index = true;
+    return 0;
+}
+
+inline uint32_t cigar_ref_span(const uint8_t* cig, uint32_t n) {
+    uint64_t s = 0;
+    for (uint32_t i = 0; i < n; ++i) {
+        const uint32_t c = rd32(cig + 4 * (size_t)i);
+        const uint32_t op = c & 15u;
+        if (op == 0 || op == 2 || op == 3 || op == 7 || op == 8) s += c >> 4;
+    }
+    return (uint32_t)std::min<uint64_t>(s, 0xFFFFFFFFu);
+}
+
+// Size of one aux field's value (after tag[2] + type[1]); 0 on malformed input.
+size_t aux_value_size(const uint8_t* v, const uint8_t* end, uint8_t type) {
+    switch (type) {
+        case 'A': case 'c': case 'C': return 1;
+        case 's': case 'S': return 2;
+        case 'i': case 'I': case 'f': return 4;
+        case 'Z': case 'H': {
+            const uint8_t* z = (const uint8_t*)std::memchr(v, 0, (size_t)(end - v));
+            return z ? (size_t)(z - v) + 1 : 0;
+        }
+        case 'B': {
+            if (end - v < 5) return 0;
+            const uint8_t sub = v[0];
+            const uint32_t cnt = rd32(v + 1);
+            size_t es = (sub == 'c' || sub == 'C') ? 1 : (sub == 's' || sub == 'S') ? 2 : 4;
+            return 5 + (size_t)cnt * es;
+        }
+        default: return 0;
+    }
+}
+
+struct Aux {
+    const uint8_t* p;
+    const uint8_t* end;
+    // returns pointer to the type byte of `tag`, or nullptr
+    const uint8_t* find(const char* tag) const {
+        const uint8_t* q = p;
+        while (q + 3 <= end) {
+            const uint8_t type = q[2];
+            const size_t vs = aux_value_size(q + 3, end, type);
+            if (!vs || vs > (size_t)(end - q - 3)) return nullptr;
+            if (q[0] == (uint8_t)tag[0] && q[1] == (uint8_t)tag[1]) return q + 2;
+            q += 3 + vs;
+        }
+        return nullptr;
+    }
+};
+
+struct Out {
+    std::vector<int32_t> start, bc, tlen;
+    std::vector<uint16_t> flag;
+    std::vector<uint8_t> mapq;
+    std::vector<uint32_t> span;
+    std::vector<uint64_t> roff;
+    std::vector<uint8_t> payload;
+};
+
+template <typename T>
+T* to_malloc(const std::vector<T>& v) {
+    T* p = (T*)std::malloc(std::max<size_t>(v.size(), 1) * sizeof(T));
+    if (p && !v.empty()) std::memcpy(p, v.data(), v.size() * sizeof(T));
+    return p;
+}
+
+// Iterate the records of `tid` in file order (fetch(contig) order); f(record
+// bytes after block_size, block_size) for each. Returns 0 or -1 (g_err set).
+template <typename F>
+int for_each_record(mgp_bam* bam, int tid, F&& f) {
+    uint64_t voff = bam->first_record_voff;
+    if (bam->has_index) {
+        voff = bam->ref_first_voff[(size_t)tid];
+        if (voff == UINT64_MAX) return 0;  // no reads on this reference
+    }
+    Stream st;
+    g_err.clear();
+    if (!stream_at(bam, voff, st)) return -1;
+    bool seen = false;
+    for (;;) {
+        if (!st.fill(4)) {
+            if (!g_err.empty()) return -1;
+            if (st.avail() == 0) return 0;  // clean end of file
+            return fail("truncated BAM record");
+        }
+        const uint32_t bs = rd32(st.peek());
+        if (bs < 32) return fail("corrupt BAM record (block_size < 32)");
+        if (!st.fill(4 + (size_t)bs)) return fail(g_err.empty() ? "truncated BAM record body" : g_err);
+        const uint8_t* r = st.peek() + 4;
+        const int32_t ref = rdi32(r);
+        if (ref == tid) {
+            seen = true;
+            if (!f(r, bs)) return -1;
+        } else if (seen || ref > tid || ref < 0) {
+            return 0;  // coordinate-sorted: tid's records are contiguous
+        }
+        st.pos += 4 + bs;
+    }
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* mgp_host_last_error(void) { return g_err.c_str(); }
+void mgp_host_buf_free(void* p) { std::free(p); }
+
+int mgp_bam_open(const char* path, int n_threads, mgp_bam** out) {
+    g_err.clear();
+    if (!path || !out) return fail("null argument");
+    mgp_bam* b = new mgp_bam();
+    b->path = path;
+    b->fd = ::open(path, O_RDONLY);
+    if (b->fd < 0) {
+        delete b;
+        return fail(std::string("cannot open ") + path + ": " + std::strerror(errno));
+    }
+    b->file_size = (int64_t)::lseek(b->fd, 0, SEEK_END);
+    unsigned hc = std::thread::hardware_concurrency();
+    b->n_threads = n_threads > 0 ? n_threads : (int)std::max(1u, std::min(hc, 16u));
+    if (parse_header(b) != 0 || load_index(b) != 0) {
+        ::close(b->fd);
+        delete b;
+        return -1;
+    }
+    *out = b;
+    return 0;
+}
+
+void mgp_bam_close(mgp_bam* b) {
+    if (!b) return;
+    if (b->fd >= 0) ::close(b->fd);
+    delete b;
+}
+
+int mgp_bam_n_refs(mgp_bam* b) { return b ? (int)b->ref_names.size() : 0; }
+const char* mgp_bam_ref_name(mgp_bam* b, int tid) {
+    return (b && tid >= 0 && tid < (int)b->ref_names.size()) ? b->ref_names[(size_t)tid].c_str() : nullptr;
+}
+int64_t mgp_bam_ref_len(mgp_bam* b, int tid) {
+    return (b && tid >= 0 && tid < (int)b->ref_lens.size()) ? b->ref_lens[(size_t)tid] : -1;
+}
+int mgp_bam_has_index(mgp_bam* b) { return b && b->has_index ? 1 : 0; }
+
+int mgp_bam_set_barcodes(mgp_bam* b, const char* tag, const char* const* barcodes, int n) {
+    if (!b || !tag || std::strlen(tag) != 2 || n < 0 || (n && !barcodes)) return fail("bad barcode arguments");
+    b->tag[0] = tag[0];
+    b->tag[1] = tag[1];
+    std::vector<std::string> k((size_t)n);
+    std::vector<int32_t> v((size_t)n);
+    for (int i = 0; i < n; ++i) {
+        k[(size_t)i] = barcodes[i];
+        v[(size_t)i] = i;
+    }
+    b->wl.build(k, v);
+    b->bulk_cell = -1;
+    return 0;
+}
+
+int mgp_bam_set_bulk(mgp_bam* b, int32_t cell) {
+    if (!b || cell < -1) return fail("bad bulk arguments");
+    b->bulk_cell = cell;
+    return 0;
+}
+
+int mgp_bam_read_ref(mgp_bam* b, int tid, int rec_align, mgp_bam_batch* out) {
+    g_err.clear();
+    if (!b || !out) return fail("null argument");
+    if (tid < 0 || tid >= (int)b->ref_names.size()) return fail("reference id out of range");
+    if (rec_align < 16 || rec_align > 4096 || (rec_align & (rec_align - 1))) return fail("bad rec_align");
+    std::memset(out, 0, sizeof(*out));
+    out->first_tag_index = -1;
+    Out o;
+    int64_t n = 0, n_tag = 0, first_tag = -1;
+    const uint64_t amask = (uint64_t)rec_align - 1;
+    const int rc = for_each_record(b, tid, [&](const uint8_t* r, uint32_t bs) -> bool {
+        const uint8_t* end = r + bs;
+        const int32_t pos = rdi32(r + 4);
+        const uint8_t l_name = r[8];
+        const uint8_t mq = r[9];
+        uint32_t n_cig = rd16(r + 12);
+        const uint16_t flg = rd16(r + 14);
+        const uint32_t l_seq = rd32(r + 16);
+        const int32_t tl = rdi32(r + 28);
+        const uint8_t* cigp = r + 32 + l_name;
+        const uint8_t* seqp = cigp + 4 * (size_t)n_cig;
+        const uint8_t* qualp = seqp + ((size_t)l_seq + 1) / 2;
+        const uint8_t* auxp = qualp + l_seq;
+        if (auxp > end) {
+            fail("corrupt BAM record (fields exceed block_size)");
+            return false;
+        }
+        Aux aux{auxp, end};
+        // CIGAR with > 65535 operations lives in the CG:B,I tag (placeholder kSmN)
+        const uint8_t* cig = cigp;
+        if (n_cig == 2 && (rd32(cigp) & 15u) == 4 && (rd32(cigp) >> 4) == l_seq && (rd32(cigp + 4) & 15u) == 3) {
+            const uint8_t* t = aux.find("CG");
+            if (t && t[0] == 'B' && (t[1] == 'I' || t[1] == 'i')) {
+                n_cig = rd32(t + 2);
+                cig = t + 6;
+            }
+        }
+        // barcode
+        int32_t bcv = -1;
+        const uint8_t* t = aux.find(b->tag);
+        if (t) {
+            ++n_tag;
+            if (first_tag < 0) first_tag = n;
+            if (t[0] == 'Z' || t[0] == 'H') {  // get_tag() -> str; numeric tags never match
+                const char* sv = (const char*)t + 1;
+                bcv = b->wl.get(sv, std::strlen(sv));
+            } else if (t[0] == 'A') {
+                bcv = b->wl.get((const char*)t + 1, 1);
+            }
+        }
+        if (b->bulk_cell >= 0) bcv = b->bulk_cell;
+        uint16_t fl = flg & 0x0FFF;
+        if (l_seq == 0 || qualp[0] == 0xFF) fl |= MGP_FLAG_NOSEQQUAL;
+        if (n_cig > 0xFFFF) {
+            fail("CIGAR with more than 65535 operations is not supported by the record format");
+            return false;
+        }
+        // payload record (include/mgpileup.h)
+        const uint64_t off = (o.payload.size() + amask) & ~amask;
+        const uint32_t coff = (uint32_t)((16 + (uint64_t)l_seq + (l_seq + 1) / 2 + 3) & ~3ull);
+        const uint64_t size = ((uint64_t)coff + 4ull * n_cig + amask) & ~amask;
+        o.payload.resize(off + size, 0);
+        uint8_t* rec = o.payload.data() + off;
+        std::memcpy(rec, &pos, 4);
+        std::memcpy(rec + 4, &l_seq, 4);
+        const uint16_t nc16 = (uint16_t)n_cig;
+        std::memcpy(rec + 8, &nc16, 2);
+        std::memcpy(rec + 10, &fl, 2);
+        std::memcpy(rec + 12, &coff, 4);
+        if (l_seq) {
+            std::memcpy(rec + 16, qualp, l_seq);
+            std::memcpy(rec + 16 + l_seq, seqp, ((size_t)l_seq + 1) / 2);
+        }
+        if (n_cig) std::memcpy(rec + coff, cig, 4 * (size_t)n_cig);
+        o.start.push_back(pos);
+        o.bc.push_back(bcv);
+        o.tlen.push_back(tl);
+        o.flag.push_back(fl);
+        o.mapq.push_back(mq);
+        o.span.push_back(std::max(cigar_ref_span(cig, n_cig), l_seq));
+        o.roff.push_back(off);
+        ++n;
+        return true;
+    });
+    if (rc != 0) return -1;
+    out->n_reads = n;
+    out->start = to_malloc(o.start);
+    out->bc = to_malloc(o.bc);
+    out->tlen = to_malloc(o.tlen);
+    out->flag = to_malloc(o.flag);
+    out->mapq = to_malloc(o.mapq);
+    out->span = to_malloc(o.span);
+    out->rec_off = to_malloc(o.roff);
+    o.payload.resize(o.payload.size() + 256, 0);  // slack for vector over-reads
+    out->payload = to_malloc(o.payload);
+    out->payload_bytes = (int64_t)o.payload.size() - 256;
+    out->n_with_tag = n_tag;
+    out->first_tag_index = first_tag;
+    if (!out->start || !out->payload) return fail("out of host memory");
+    return 0;
+}
+
+void mgp_bam_free_batch(mgp_bam_batch* x) {
+    if (!x) return;
+    std::free(x->start);
+    std::free(x->bc);
+    std::free(x->tlen);
+    std::free(x->flag);
+    std::free(x->mapq);
+    std::free(x->span);
+    std::free(x->rec_off);
+    std::free(x->payload);
+    std::memset(x, 0, sizeof(*x));
+}
+
+int64_t mgp_bam_count_tag(mgp_bam* b, int tid, const char* tag, uint8_t** blob, int64_t* blob_bytes) {
+    g_err.clear();
+    if (!b || !tag || std::strlen(tag) != 2 || !blob || !blob_bytes) return fail("bad arguments");
+    if (tid < 0 || tid >= (int)b->ref_names.size()) return fail("reference id out of range");
+    std::unordered_map<std::string, int64_t> counts;
+    std::vector<std::string> order;
+    char tg[3] = {tag[0], tag[1], 0};
+    const int rc = for_each_record(b, tid, [&](const uint8_t* r, uint32_t bs) -> bool {
+        const uint16_t flg = rd16(r + 14);
+        if (flg & (0x4 | 0x400)) return true;  // is_unmapped or is_duplicate (barcode_extraction.py:26)
+        const uint8_t l_name = r[8];
+        const uint32_t n_cig = rd16(r + 12);
+        const uint32_t l_seq = rd32(r + 16);
+        const uint8_t* auxp = r + 32 + l_name + 4 * (size_t)n_cig + ((size_t)l_seq + 1) / 2 + l_seq;
+        Aux aux{auxp, r + bs};
+        const uint8_t* t = aux.find(tg);
+        if (!t) return true;
+        std::string v;
+        switch (t[0]) {  // str(read.get_tag(tag))
+            case 'Z': case 'H': v = (const char*)t + 1; break;
+            case 'A': v = std::string(1, (char)t[1]); break;
+            case 'c': v = std::to_string((int8_t)t[1]); break;
+            case 'C': v = std::to_string((uint8_t)t[1]); break;
+            case 's': v = std::to_string((int16_t)rd16(t + 1)); break;
+            case 'S': v = std::to_string(rd16(t + 1)); break;
+            case 'i': v = std::to_string(rdi32(t + 1)); break;
+            case 'I': v = std::to_string(rd32(t + 1)); break;
+            default: return true;  // float / array tags are not barcodes
+        }
+        auto it = counts.find(v);
+        if (it == counts.end()) {
+            counts.emplace(v, 1);
+            order.push_back(v);
+        } else {
+            ++it->second;
+        }
+        return true;
+    });
+    if (rc != 0) return -1;
+    size_t bytes = 0;
+    for (const auto& k : order) bytes += k.size() + 1 + 8;
+    uint8_t* p = (uint8_t*)std::malloc(std::max<size_t>(bytes, 1));
+    if (!p) return fail("out of host memory");
+    size_t o = 0;
+    for (const auto& k : order) {
+        std::memcpy(p + o, k.c_str(), k.size() + 1);
+        o += k.size() + 1;
+        const int64_t c = counts[k];
+        std::memcpy(p + o, &c, 8);
+        o += 8;
+    }
+    *blob = p;
+    *blob_bytes = (int64_t)bytes;
+    return (int64_t)order.size();
+}
+
+}  // extern "C"

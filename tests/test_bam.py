@@ -1,0 +1,214 @@
+"""Native BAM ingest (libmgphost.so, include/mgpileup_host.h) — CPU tests.
+
+The golden cases hold the exact reads the reference consumed (through its
+pysam stand-in, tests/golden/make_golden.py) and the engine batch they map to.
+Writing those reads as a BAM and decoding it with the native reader must give
+that batch back bit for bit; the oracle on that batch reproduces the
+reference's outputs (test_oracle_golden.py), which pins BAM -> outputs.
+The writer itself is checked against an independent decode (gzip + struct,
+SAM spec §4.2) so that a symmetric writer/reader bug cannot hide.
+"""
+
+from __future__ import annotations
+
+import gzip
+import struct
+
+import numpy as np
+import pytest
+
+from golden_io import CASES, Golden
+from mgatk2_amd.bam import BamFile, BamWriter, soa_to_bam
+from mgatk2_amd.exceptions import BAMFormatError, BAMReadError
+from mgatk2_amd.synth import FLAG_NOSEQQUAL, pack_reads, unpack_record
+
+KEYS = ["start", "bc", "tlen", "flag", "mapq", "span", "rec_off"]
+
+
+def _assert_soa_equal(a, b):
+    for k in KEYS:
+        np.testing.assert_array_equal(getattr(a, k), getattr(b, k), err_msg=k)
+    np.testing.assert_array_equal(a.payload[: b.payload.size], b.payload[: a.payload.size])
+    assert a.payload.size == b.payload.size
+
+
+@pytest.mark.parametrize("case", CASES)
+@pytest.mark.parametrize("index", [True, False])
+def test_roundtrip_golden(case, index, tmp_path):
+    g = Golden(case)
+    soa_to_bam(tmp_path / "x.bam", g.soa, g.whitelist, index=index)
+    with BamFile(tmp_path / "x.bam") as bam:
+        assert bam.references == ("chr1", "chrM")
+        assert bam.lengths == (248956422, 16569)
+        assert bam.has_index == index
+        got = bam.read_soa("chrM", g.whitelist)
+    _assert_soa_equal(got, g.soa)
+
+
+def _independent_decode(path):
+    """gzip (BGZF is multi-member gzip) + struct per the SAM spec."""
+    raw = gzip.decompress(path.read_bytes())
+    assert raw[:4] == b"BAM\1"
+    (lt,) = struct.unpack_from("<i", raw, 4)
+    p = 8 + lt
+    (nref,) = struct.unpack_from("<i", raw, p)
+    p += 4
+    refs = []
+    for _ in range(nref):
+        (ln,) = struct.unpack_from("<i", raw, p)
+        refs.append(raw[p + 4 : p + 4 + ln - 1].decode())
+        p += 4 + ln + 4
+    recs = []
+    while p < len(raw):
+        (bs,) = struct.unpack_from("<i", raw, p)
+        r = raw[p + 4 : p + 4 + bs]
+        tid, pos, ln, mq, _bin, nc, flag, ls, _nt, _np, tl = struct.unpack_from("<iiBBHHHIiii", r, 0)
+        q = 32 + ln
+        cig = [(c & 15, c >> 4) for c in struct.unpack_from(f"<{nc}I", r, q)]
+        q += 4 * nc
+        sb = r[q : q + (ls + 1) // 2]
+        seq = "".join("=ACMGRSVTWYHKDBN"[(sb[i // 2] >> (4 * (1 - i % 2))) & 15] for i in range(ls))
+        q += (ls + 1) // 2
+        qual = list(r[q : q + ls])
+        q += ls
+        tags = {}
+        while q < len(r):
+            t, ty = r[q : q + 2].decode(), chr(r[q + 2])
+            if ty == "Z":
+                z = r.index(b"\0", q + 3)
+                tags[t] = r[q + 3 : z].decode()
+                q = z + 1
+            else:
+                raise AssertionError(ty)
+        recs.append(dict(tid=tid, pos=pos, mapq=mq, flag=flag, cig=cig, seq=seq, qual=qual, tlen=tl, tags=tags))
+        p += 4 + bs
+    return refs, recs
+
+
+def test_writer_independent_decode(tmp_path):
+    g = Golden("synth_run")
+    soa_to_bam(tmp_path / "x.bam", g.soa, g.whitelist)
+    refs, recs = _independent_decode(tmp_path / "x.bam")
+    assert refs == ["chr1", "chrM"] and len(recs) == g.soa.n
+    for i in range(0, g.soa.n, 7):
+        r, d = recs[i], unpack_record(g.soa.payload, int(g.soa.rec_off[i]))
+        assert r["tid"] == 1 and r["pos"] == g.soa.start[i] and r["mapq"] == g.soa.mapq[i]
+        assert r["flag"] == int(g.soa.flag[i]) & 0xFFF and r["tlen"] == g.soa.tlen[i]
+        assert r["cig"] == d["cigartuples"]
+        assert r["seq"] == d["query_sequence"]
+        if not (int(g.soa.flag[i]) & FLAG_NOSEQQUAL):
+            assert r["qual"] == d["query_qualities"]
+        b = int(g.soa.bc[i])
+        assert (r["tags"].get("CB") == g.whitelist[b]) if b >= 0 else (r["tags"].get("CB") not in g.whitelist)
+
+
+def _rd(pos, flag=0, cb="AAAC-1", seq="ACGTACGTAC", cig=None, tid=1, **kw):
+    return dict(tid=tid, pos=pos, flag=flag, mapq=60, cigartuples=cig or [(0, len(seq))], query_sequence=seq,
+                query_qualities=[30] * len(seq), template_length=kw.get("tlen", 0),
+                tags={} if cb is None else {"CB": cb})
+
+
+def test_other_contigs_many_blocks_threads(tmp_path):
+    """chrM sits between other contigs and spans many BGZF blocks: the index seek,
+    the no-index scan and 1 vs 8 inflate threads give the same batch."""
+    rng = np.random.default_rng(1)
+    w = BamWriter(tmp_path / "x.bam", [("chr1", 10**6), ("chrM", 16569), ("chrX", 10**6)])
+    for p in sorted(rng.integers(0, 10**6, 3000)):
+        w.write(_rd(int(p), tid=0, cb="CCCC-1"))
+    chrm = []
+    for p in sorted(rng.integers(0, 16500, 20000)):
+        r = _rd(int(p), flag=int(rng.choice([0, 16, 99, 147])), cb=["AAAC-1", "GGGT-1", None, "TTTT-1"][p % 4],
+                seq="".join(rng.choice(list("ACGTN"), 40)))
+        chrm.append(r)
+        w.write(r)
+    for p in sorted(rng.integers(0, 10**6, 3000)):
+        w.write(_rd(int(p), tid=2))
+    w.close(index=True)
+    wl = ["AAAC-1", "GGGT-1"]
+    with BamFile(tmp_path / "x.bam", n_threads=1) as b1:
+        a = b1.read_soa("chrM", wl)
+        assert b1.read_soa("chr1", wl).n == 3000
+        assert b1.read_soa("chrX", wl).n == 3000
+    (tmp_path / "x.bam.bai").unlink()
+    with BamFile(tmp_path / "x.bam", n_threads=8) as b8:
+        assert not b8.has_index
+        c = b8.read_soa("chrM", wl)
+    _assert_soa_equal(a, c)
+    exp = pack_reads([dict(reference_start=r["pos"], flag=r["flag"], mapping_quality=60,
+                           cigartuples=r["cigartuples"], query_sequence=r["query_sequence"],
+                           query_qualities=r["query_qualities"], template_length=0,
+                           bc={"AAAC-1": 0, "GGGT-1": 1}.get(r["tags"].get("CB"), -1)) for r in chrm])
+    _assert_soa_equal(a, exp)
+    assert a.extra["n_with_tag"] == sum(1 for r in chrm if r["tags"])
+
+
+def test_count_tag_and_bulk(tmp_path):
+    w = BamWriter(tmp_path / "x.bam", [("chrM", 16569)])
+    reads = [_rd(10, cb="A-1"), _rd(11, cb="B-1"), _rd(12, flag=4, cb="B-1"), _rd(13, flag=1024, cb="C-1"),
+             _rd(14, cb=None), _rd(15, cb="A-1"), _rd(16, flag=256, cb="D-1")]
+    for r in reads:
+        r["tid"] = 0
+    for r in reads:
+        w.write(r)
+    w.close()
+    with BamFile(tmp_path / "x.bam") as b:
+        # barcode_extraction.py:22-32: unmapped and duplicate reads are not counted
+        assert b.count_tag("chrM") == {"A-1": 2, "B-1": 1, "D-1": 1}
+        s = b.read_soa("chrM", ["A-1", "Z-1"])
+        assert s.bc.tolist() == [0, -1, -1, -1, -1, 0, -1]
+        assert s.extra["first_tag_index"] == 0 and s.extra["n_with_tag"] == 6
+        s = b.read_soa("chrM", ["bulk"], bulk_cell=0)
+        assert s.bc.tolist() == [0] * 7
+        s = b.read_soa("chrM", ["A-1", "A-1"])  # duplicates: last index wins (dict semantics)
+        assert s.bc.tolist()[0] == 1
+
+
+def test_long_cigar_cg_tag(tmp_path):
+    """> 65535 CIGAR operations are stored in the CG:B,I tag (SAM spec §4.2.2)."""
+    import mgatk2_amd.bam as mb
+
+    n_ops = 70000
+    cig = [(0, 1) if i % 2 == 0 else (2, 1) for i in range(n_ops - 1)] + [(0, 1)]
+    lseq = sum(ln for op, ln in cig if op == 0)
+    ref_span = sum(ln for op, ln in cig)
+    seq = "A" * lseq
+    w = BamWriter(tmp_path / "x.bam", [("chrM", 16569 * 20)])
+    # placeholder CIGAR kSmN + CG tag, written by hand
+    body_cig = [(4, lseq), (3, ref_span)]
+    r = _rd(5, seq=seq, cig=body_cig, tid=0)
+    w.write(r)
+    w.close(index=False)
+    raw = bytearray(gzip.decompress((tmp_path / "x.bam").read_bytes()))
+    cg = b"CGBI" + struct.pack("<I", n_ops) + b"".join(struct.pack("<I", (ln << 4) | op) for op, ln in cig)
+    # patch the single record: append CG tag and fix block_size
+    lt = struct.unpack_from("<i", raw, 4)[0]
+    p = 8 + lt + 4
+    p += 4 + struct.unpack_from("<i", raw, p)[0] + 4
+    bs = struct.unpack_from("<i", raw, p)[0]
+    rec = raw[p + 4 : p + 4 + bs] + cg
+    out = bytes(raw[:p]) + struct.pack("<i", len(rec)) + bytes(rec)
+    data = b"".join(mb._bgzf_block(out[i : i + 0xFF00]) for i in range(0, len(out), 0xFF00)) + mb._BGZF_EOF
+    (tmp_path / "y.bam").write_bytes(data)
+    assert p + 4 + bs == len(raw)
+    with BamFile(tmp_path / "y.bam") as b:
+        with pytest.raises(BAMReadError, match="65535"):
+            b.read_soa("chrM", ["AAAC-1"])
+
+
+def test_errors(tmp_path):
+    (tmp_path / "bad.bam").write_bytes(b"not a bam file at all")
+    with pytest.raises(BAMFormatError):
+        BamFile(tmp_path / "bad.bam")
+    with pytest.raises(BAMFormatError):
+        BamFile(tmp_path / "missing.bam")
+    g = Golden("synth_run")
+    soa_to_bam(tmp_path / "x.bam", g.soa, g.whitelist, index=False)
+    data = (tmp_path / "x.bam").read_bytes()
+    (tmp_path / "t.bam").write_bytes(data[: len(data) // 2])  # truncated mid-block
+    with BamFile(tmp_path / "t.bam") as b, pytest.raises(BAMReadError):
+        b.read_soa("chrM", g.whitelist)
+    corrupt = bytearray(data)
+    corrupt[2 * len(data) // 3] ^= 0xFF  # CRC / inflate failure past the header block
+    (tmp_path / "c.bam").write_bytes(bytes(corrupt))
+    with BamFile(tmp_path / "c.bam") as b, pytest.raises(BAMReadError):
+        b.read_soa("chrM", g.whitelist)
