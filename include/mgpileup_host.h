@@ -67,6 +67,11 @@ int  mgp_bam_set_bulk(mgp_bam *bam, int32_t cell);
 int  mgp_bam_read_ref(mgp_bam *bam, int tid, int rec_align, mgp_bam_batch *out);
 void mgp_bam_free_batch(mgp_bam_batch *b);
 
+/* Tag presence check of BAMReader._validate_bam_file (readers.py:53-59): index of
+ * the first of the first `max_records` records of `tid` that carries `tag`, -1
+ * if none does, -2 on error. `*n_checked` = records examined. */
+int64_t mgp_bam_find_tag(mgp_bam *bam, int tid, const char *tag, int64_t max_records, int64_t *n_checked);
+
 /* Barcode auto-extraction pass (barcode_extraction.py:12-46): counts of the
  * tag's string value over records of `tid` that are neither unmapped nor
  * duplicates. Returns the number of distinct values; `*blob` receives

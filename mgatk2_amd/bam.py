@@ -70,6 +70,8 @@ def host_library() -> C.CDLL:
         lib.mgp_bam_read_ref.argtypes = [vp, C.c_int, C.c_int, C.POINTER(mgp_bam_batch)]
         lib.mgp_bam_free_batch.argtypes = [C.POINTER(mgp_bam_batch)]
         lib.mgp_bam_free_batch.restype = None
+        lib.mgp_bam_find_tag.argtypes = [vp, C.c_int, C.c_char_p, C.c_int64, C.POINTER(C.c_int64)]
+        lib.mgp_bam_find_tag.restype = C.c_int64
         lib.mgp_bam_count_tag.argtypes = [vp, C.c_int, C.c_char_p, C.POINTER(C.POINTER(C.c_uint8)),
                                           C.POINTER(C.c_int64)]
         lib.mgp_bam_count_tag.restype = C.c_int64
@@ -148,6 +150,15 @@ class BamFile:
             return soa
         finally:
             self.lib.mgp_bam_free_batch(C.byref(b))
+
+    def find_tag(self, contig: str, tag: str, max_records: int) -> tuple[int, int]:
+        """(index of the first record carrying `tag` among the first `max_records`
+        of `contig` or -1, records examined)."""
+        n = C.c_int64()
+        i = self.lib.mgp_bam_find_tag(self._h, self.tid(contig), tag.encode(), int(max_records), C.byref(n))
+        if i < -1:
+            raise BAMReadError(self.path, _err())
+        return int(i), int(n.value)
 
     def count_tag(self, contig: str, tag: str = "CB") -> dict[str, int]:
         """Tag value counts over non-unmapped, non-duplicate records (barcode_extraction.py:22-32)."""

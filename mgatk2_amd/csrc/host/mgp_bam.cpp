@@ -470,7 +470,9 @@ int for_each_record(mgp_bam* bam, int tid, F&& f) {
         const int32_t ref = rdi32(r);
         if (ref == tid) {
             seen = true;
-            if (!f(r, bs)) return -1;
+            const int c = f(r, bs);  // 1: continue, 0: stop, < 0: error (message set)
+            if (c < 0) return -1;
+            if (c == 0) return 0;
         } else if (seen || ref > tid || ref < 0) {
             return 0;  // coordinate-sorted: tid's records are contiguous
         }
@@ -553,7 +555,7 @@ int mgp_bam_read_ref(mgp_bam* b, int tid, int rec_align, mgp_bam_batch* out) {
     Out o;
     int64_t n = 0, n_tag = 0, first_tag = -1;
     const uint64_t amask = (uint64_t)rec_align - 1;
-    const int rc = for_each_record(b, tid, [&](const uint8_t* r, uint32_t bs) -> bool {
+    const int rc = for_each_record(b, tid, [&](const uint8_t* r, uint32_t bs) -> int {
         const uint8_t* end = r + bs;
         const int32_t pos = rdi32(r + 4);
         const uint8_t l_name = r[8];
@@ -568,7 +570,7 @@ int mgp_bam_read_ref(mgp_bam* b, int tid, int rec_align, mgp_bam_batch* out) {
         const uint8_t* auxp = qualp + l_seq;
         if (auxp > end) {
             fail("corrupt BAM record (fields exceed block_size)");
-            return false;
+            return -1;
         }
         Aux aux{auxp, end};
         // CIGAR with > 65535 operations lives in the CG:B,I tag (placeholder kSmN)
@@ -598,7 +600,7 @@ int mgp_bam_read_ref(mgp_bam* b, int tid, int rec_align, mgp_bam_batch* out) {
         if (l_seq == 0 || qualp[0] == 0xFF) fl |= MGP_FLAG_NOSEQQUAL;
         if (n_cig > 0xFFFF) {
             fail("CIGAR with more than 65535 operations is not supported by the record format");
-            return false;
+            return -1;
         }
         // payload record (include/mgpileup.h)
         const uint64_t off = (o.payload.size() + amask) & ~amask;
@@ -625,7 +627,7 @@ int mgp_bam_read_ref(mgp_bam* b, int tid, int rec_align, mgp_bam_batch* out) {
         o.span.push_back(std::max(cigar_ref_span(cig, n_cig), l_seq));
         o.roff.push_back(off);
         ++n;
-        return true;
+        return 1;
     });
     if (rc != 0) return -1;
     out->n_reads = n;
@@ -658,6 +660,32 @@ void mgp_bam_free_batch(mgp_bam_batch* x) {
     std::memset(x, 0, sizeof(*x));
 }
 
+int64_t mgp_bam_find_tag(mgp_bam* b, int tid, const char* tag, int64_t max_records, int64_t* n_checked) {
+    g_err.clear();
+    if (!b || !tag || std::strlen(tag) != 2) return fail("bad arguments");
+    if (tid < 0 || tid >= (int)b->ref_names.size()) return fail("reference id out of range");
+    char tg[3] = {tag[0], tag[1], 0};
+    int64_t i = 0, found = -1;
+    const int rc = for_each_record(b, tid, [&](const uint8_t* r, uint32_t bs) -> int {
+        if (i >= max_records) return 0;
+        const uint8_t l_name = r[8];
+        const uint32_t n_cig = rd16(r + 12);
+        const uint32_t l_seq = rd32(r + 16);
+        const uint8_t* auxp = r + 32 + l_name + 4 * (size_t)n_cig + ((size_t)l_seq + 1) / 2 + l_seq;
+        if (auxp > r + bs) return fail("corrupt BAM record (fields exceed block_size)"), -1;
+        Aux aux{auxp, r + bs};
+        if (aux.find(tg)) {
+            found = i;
+            return 0;
+        }
+        ++i;
+        return 1;
+    });
+    if (rc != 0) return -2;
+    if (n_checked) *n_checked = found >= 0 ? found + 1 : i;
+    return found;
+}
+
 int64_t mgp_bam_count_tag(mgp_bam* b, int tid, const char* tag, uint8_t** blob, int64_t* blob_bytes) {
     g_err.clear();
     if (!b || !tag || std::strlen(tag) != 2 || !blob || !blob_bytes) return fail("bad arguments");
@@ -665,16 +693,16 @@ int64_t mgp_bam_count_tag(mgp_bam* b, int tid, const char* tag, uint8_t** blob, 
     std::unordered_map<std::string, int64_t> counts;
     std::vector<std::string> order;
     char tg[3] = {tag[0], tag[1], 0};
-    const int rc = for_each_record(b, tid, [&](const uint8_t* r, uint32_t bs) -> bool {
+    const int rc = for_each_record(b, tid, [&](const uint8_t* r, uint32_t bs) -> int {
         const uint16_t flg = rd16(r + 14);
-        if (flg & (0x4 | 0x400)) return true;  // is_unmapped or is_duplicate (barcode_extraction.py:26)
+        if (flg & (0x4 | 0x400)) return 1;  // is_unmapped or is_duplicate (barcode_extraction.py:26)
         const uint8_t l_name = r[8];
         const uint32_t n_cig = rd16(r + 12);
         const uint32_t l_seq = rd32(r + 16);
         const uint8_t* auxp = r + 32 + l_name + 4 * (size_t)n_cig + ((size_t)l_seq + 1) / 2 + l_seq;
         Aux aux{auxp, r + bs};
         const uint8_t* t = aux.find(tg);
-        if (!t) return true;
+        if (!t) return 1;
         std::string v;
         switch (t[0]) {  // str(read.get_tag(tag))
             case 'Z': case 'H': v = (const char*)t + 1; break;
@@ -685,7 +713,7 @@ int64_t mgp_bam_count_tag(mgp_bam* b, int tid, const char* tag, uint8_t** blob, 
             case 'S': v = std::to_string(rd16(t + 1)); break;
             case 'i': v = std::to_string(rdi32(t + 1)); break;
             case 'I': v = std::to_string(rd32(t + 1)); break;
-            default: return true;  // float / array tags are not barcodes
+            default: return 1;  // float / array tags are not barcodes
         }
         auto it = counts.find(v);
         if (it == counts.end()) {
@@ -694,7 +722,7 @@ int64_t mgp_bam_count_tag(mgp_bam* b, int tid, const char* tag, uint8_t** blob, 
         } else {
             ++it->second;
         }
-        return true;
+        return 1;
     });
     if (rc != 0) return -1;
     size_t bytes = 0;

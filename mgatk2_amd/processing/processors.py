@@ -70,23 +70,25 @@ class CellProcessor:
         self.last_stats: dict = {}
 
     # production path ------------------------------------------------------
-    def process_soa(self, soa_batches, barcodes: list[str], incremental_writer=None) -> list[dict]:
-        """Whole read set (one or more BAM-order batches) through the engine.
-
-        Returns the reference's slim result list ({"barcode", "n_reads"} per
-        written cell, processors.py:75) and keeps the EngineResult in
-        ``self.last_result``."""
+    def run_soa(self, soa_batches, n_cells: int) -> EngineResult:
+        """Whole read set (one or more BAM-order batches) through the engine:
+        filters, dedup, pileup, strand filter, per-cell statistics, tallies."""
         if isinstance(soa_batches, ReadSoA):
             soa_batches = [soa_batches]
         n = sum(b.n for b in soa_batches)
         pay = sum(int(b.payload.shape[0]) for b in soa_batches)
-        ec = self.config.engine_config(len(barcodes), reserve_reads=n, reserve_payload=pay + 256 * len(soa_batches))
+        ec = self.config.engine_config(n_cells, reserve_reads=n, reserve_payload=pay + 256 * len(soa_batches))
         with Engine(ec, device=self.device) as eng:
             for b in soa_batches:
                 eng.push(b)
             res = eng.finish()
             self.last_stats = eng.kernel_times()
         self.last_result = res
+        return res
+
+    def write_results(self, res: EngineResult, barcodes: list[str], incremental_writer=None) -> list[dict]:
+        """Passing cells in first-seen order to the writer; returns the reference's
+        slim result list ({"barcode", "n_reads"} per written cell, processors.py:75)."""
         order = res.cell_order()
         written = order[res.passed[order].astype(bool)]
         failed = int(order.size - written.size)
@@ -95,6 +97,10 @@ class CellProcessor:
         if incremental_writer is not None:
             incremental_writer.write_cells(res, written, barcodes=barcodes, tally=res.ref_tally)
         return [{"barcode": barcodes[int(c)], "n_reads": int(res.n_reads[c])} for c in written]
+
+    def process_soa(self, soa_batches, barcodes: list[str], incremental_writer=None) -> list[dict]:
+        res = self.run_soa(soa_batches, len(barcodes))
+        return self.write_results(res, barcodes, incremental_writer)
 
     # reference dict API (processors.py:63-144) ------------------------------
     def process_cells_direct(self, reads_by_barcode, incremental_writer=None):

@@ -1,0 +1,241 @@
+"""End to end: BAM file -> run_pipeline -> output files, against the reference's outputs.
+
+Each golden case holds the reads the reference's ``run_pipeline`` consumed and
+the files it wrote (tests/golden/make_golden.py). The reads are written as a
+BAM, our ``run_pipeline`` runs on it, and every txt output must match byte for
+byte after gunzip.
+
+* CPU tests: host logic only. The engine call is replaced by the oracle, the
+  CPU checker. This covers BAM ingest, validation, barcode sources, writers
+  and the summary.
+* GPU tests (``-m gpu``): the same runs through the HIP engine.
+"""
+
+from __future__ import annotations
+
+import gzip
+
+import numpy as np
+import pytest
+
+from golden_io import CASES, Golden
+from mgatk2_amd.bam import BamWriter, soa_to_bam
+from mgatk2_amd.exceptions import InvalidInputError, NoBarcodeTagsError, NoChrMReadsError
+
+TXT_CASES = [c for c in CASES if Golden(c).params["output_format"] == "txt"]
+
+
+@pytest.fixture
+def oracle_engine(monkeypatch, oracle_lib):
+    """Stand the oracle in for the engine (CPU tests of the host logic)."""
+    from mgatk2_amd.processing import processors
+
+    def run_soa(self, soa_batches, n_cells):
+        soa = soa_batches if not isinstance(soa_batches, list) else soa_batches[0]
+        res, _ = oracle_lib.oracle_run(self.config.engine_config(n_cells), soa)
+        self.last_result = res
+        return res
+
+    monkeypatch.setattr(processors.CellProcessor, "run_soa", run_soa)
+
+
+def _run_case(case, tmp_path, barcode_source="txt"):
+    from mgatk2_amd.pipeline import run_pipeline
+
+    g = Golden(case)
+    p = g.params
+    bam = tmp_path / "possorted_bam.bam"
+    soa_to_bam(bam, g.soa, g.whitelist)
+    if barcode_source == "txt":
+        bfile = tmp_path / "barcodes.tsv"
+        bfile.write_text("".join(b + "\n" for b in g.whitelist))
+    else:
+        bfile = tmp_path / "singlecell.csv"
+        rows = ["barcode,is__cell_barcode,passed_filters,excluded_reason"]
+        rows += [f"{b},1,{100 + i}," for i, b in enumerate(g.whitelist)]
+        rows += ["ZZZZ-1,0,5,lowq"]
+        bfile.write_text("\n".join(rows) + "\n")
+    out = tmp_path / "out"
+    ret = run_pipeline(
+        str(bam), str(bfile), str(out), min_baseq=p["min_baseq"], min_mapq=p["min_mapq"],
+        min_reads_per_cell=p["min_reads_per_cell"], max_strand_bias=p["max_strand_bias"],
+        min_distance_from_end=p["min_distance_from_end"], skip_deduplication=p["skip_deduplication"],
+        use_fragment_length_dedup=p["use_fragment_length_dedup"], output_format="txt",
+    )
+    return g, out, ret
+
+
+def _check_outputs(g, out, ret):
+    od = out / "output"
+    for name in ["A", "C", "G", "T", "coverage"]:
+        got = gzip.decompress((od / f"output.{name}.txt.gz").read_bytes()).decode()
+        assert got == str(g.exp(f"txt_{name}")), f"{g.name}: output.{name}.txt"
+    assert (od / "output.depthTable.txt").read_text() == str(g.exp("txt_depthTable"))
+    assert (od / "chrM_refAllele.txt").read_text() == str(g.exp("txt_refAllele"))
+    assert (out / "qc" / "cell_stats.csv").read_text() == str(g.exp("cell_stats"))
+    n_input = int((g.exp("n_reads") > 0).sum())
+    n_pass = int(g.exp("passed").sum())
+    assert ret["cells_processed"] == n_input and ret["cells_passed_qc"] == n_pass
+    assert ret["mean_reads"] == pytest.approx(float(g.exp("n_reads")[g.exp("passed") > 0].sum()) / n_pass)
+    summary = (out / "qc" / "summary.txt").read_text().splitlines()
+    assert summary[0] == "mgatk2 Run Summary" and summary[1] == "=" * 20
+    kv = dict(line.split(": ", 1) for line in summary[2:])
+    assert kv["cells_total"] == str(n_input) and kv["cells_passed_qc"] == str(n_pass)
+    assert kv["cells_failed_qc"] == str(n_input - n_pass) and kv["reference"] == "chrM"
+    assert kv["reference_length"] == "16569"
+
+
+@pytest.mark.parametrize("case", TXT_CASES)
+def test_pipeline_txt_host(case, tmp_path, oracle_engine):
+    g, out, ret = _run_case(case, tmp_path)
+    _check_outputs(g, out, ret)
+
+
+def test_pipeline_singlecell_csv(tmp_path, oracle_engine):
+    g, out, ret = _run_case("synth_run", tmp_path, barcode_source="csv")
+    _check_outputs(g, out, ret)
+
+
+def test_singlecell_csv_loader(tmp_path):
+    from mgatk2_amd.utils import load_singlecell_csv
+
+    f = tmp_path / "singlecell.csv"
+    f.write_text("barcode,is__cell_barcode,passed_filters,frac,excluded_reason,tag\n"
+                 "AAA-1,1,10,0.5,,x\nCCC-1,0,3,0.1,lowq,y\nGGG-1,1,,,,z\n")
+    bcs, meta = load_singlecell_csv(str(f))
+    assert bcs == ["AAA-1", "GGG-1"]
+    assert meta["passed_filters"] == [10, 0] and meta["frac"] == [0.5, 0]
+    assert meta["excluded_reason"] == ["", ""] and meta["tag"] == ["x", "z"]
+    assert meta["is__cell_barcode"] == [1, 1]
+    f.write_text("barcode,passed_filters\nAAA-1,3\n")
+    with pytest.raises(InvalidInputError):
+        load_singlecell_csv(str(f))
+    f.write_text("barcode,is__cell_barcode\nAAA-1,0\n")
+    with pytest.raises(InvalidInputError):
+        load_singlecell_csv(str(f))
+
+
+def test_pipeline_autodetect_barcodes(tmp_path, oracle_engine):
+    """barcode_file=None: barcodes come from the BAM's CB counts (barcode_extraction.py)."""
+    from mgatk2_amd.file_io.barcode_extraction import extract_barcodes_from_bam
+    from mgatk2_amd.pipeline import run_pipeline
+
+    g = Golden("synth_run")
+    bam = tmp_path / "x.bam"
+    soa_to_bam(bam, g.soa, g.whitelist)
+    # expected: str(CB) counts over non-unmapped, non-duplicate records
+    counts: dict[str, int] = {}
+    for i in range(g.soa.n):
+        f = int(g.soa.flag[i]) & 0xFFF
+        b = int(g.soa.bc[i])
+        tag = g.whitelist[b] if b >= 0 else ("NNNNNNNNNNNNNNNN-9" if i % 2 == 0 else None)
+        if tag is None or f & (0x4 | 0x400):
+            continue
+        counts[tag] = counts.get(tag, 0) + 1
+    for mr in (1, 10, 40):
+        assert extract_barcodes_from_bam(str(bam), min_reads=mr) == sorted(b for b, n in counts.items() if n >= mr)
+    ret = run_pipeline(str(bam), None, str(tmp_path / "o"), min_barcode_reads=10, output_format="txt")
+    assert ret["cells_processed"] > 0
+    with pytest.raises(InvalidInputError):
+        run_pipeline(str(bam), None, str(tmp_path / "o2"), min_barcode_reads=10**9, output_format="txt")
+
+
+def _tiny_bam(path, refs, tid, n, tag=True):
+    w = BamWriter(path, refs)
+    for i in range(n):
+        w.write(dict(tid=tid, pos=10 + i, flag=0, mapq=60, cigartuples=[(0, 20)], query_sequence="ACGT" * 5,
+                     query_qualities=[30] * 20, tags={"CB": "AAAC-1"} if tag else {}))
+    w.close()
+
+
+def test_reader_validation(tmp_path):
+    from mgatk2_amd.config import PipelineConfig
+    from mgatk2_amd.processing.readers import BAMReader
+
+    _tiny_bam(tmp_path / "a.bam", [("chr1", 1000), ("chr2", 1000)], 0, 5)
+    with pytest.raises(NoChrMReadsError):
+        BAMReader(str(tmp_path / "a.bam"), PipelineConfig(), {"AAAC-1"})
+    # 1001 untagged chrM records -> NoBarcodeTagsError; 1000 are not enough to fail
+    _tiny_bam(tmp_path / "b.bam", [("MT", 16569)], 0, 1001, tag=False)
+    with pytest.raises(NoBarcodeTagsError) as e:
+        BAMReader(str(tmp_path / "b.bam"), PipelineConfig(), {"AAAC-1"})
+    assert e.value.total_reads_checked == 1000
+    _tiny_bam(tmp_path / "c.bam", [("MT", 16569)], 0, 1000, tag=False)
+    cfg = PipelineConfig(mito_chr="chrM")
+    BAMReader(str(tmp_path / "c.bam"), cfg, {"AAAC-1"})
+    assert cfg.mito_chr == "MT"  # the first present name of chrM/MT/M/chrMT wins (readers.py:43-48)
+    # chrM present besides MT: chrM wins even when MT was asked for
+    _tiny_bam(tmp_path / "d.bam", [("MT", 16569), ("chrM", 16569)], 1, 3)
+    cfg = PipelineConfig(mito_chr="MT")
+    BAMReader(str(tmp_path / "d.bam"), cfg, {"AAAC-1"})
+    assert cfg.mito_chr == "chrM"
+
+
+def test_collect_reads_by_barcode_matches_engine_stats(tmp_path, oracle_lib):
+    """The dict API (readers.py:63-201) and the engine agree on kept reads and stats."""
+    from mgatk2_amd.config import PipelineConfig
+    from mgatk2_amd.processing.readers import BAMReader
+
+    for case in ("synth_run", "synth_tenx", "synth_nodedup"):
+        g = Golden(case)
+        p = g.params
+        bam = tmp_path / f"{case}.bam"
+        soa_to_bam(bam, g.soa, g.whitelist)
+        cfg = PipelineConfig(min_baseq=p["min_baseq"], min_mapq=p["min_mapq"],
+                             skip_deduplication=p["skip_deduplication"],
+                             use_fragment_length_dedup=p["use_fragment_length_dedup"])
+        reads, stats = BAMReader(str(bam), cfg, g.whitelist).collect_reads_by_barcode()
+        for k in ("total_reads", "filtered_reads", "n_barcodes"):
+            assert stats[k] == g.stats[k], (case, k)
+        if not p["skip_deduplication"]:
+            assert stats["duplicate_reads_with_length"] == g.stats["duplicate_reads_with_length"]
+            assert stats["duplicate_reads_position_only"] == g.stats["duplicate_reads_position_only"]
+        assert list(reads) == [g.whitelist[c] for c in g.exp("dict_order")]
+        n = np.zeros(len(g.whitelist), np.int64)
+        for bc, lst in reads.items():
+            n[g.whitelist.index(bc)] = len(lst)
+        np.testing.assert_array_equal(n, g.exp("n_reads"))
+
+
+def test_pipeline_missing_inputs(tmp_path):
+    from mgatk2_amd.pipeline import MtDNAPipeline
+
+    with pytest.raises(InvalidInputError):
+        MtDNAPipeline(str(tmp_path / "none.bam"), ["A"], tmp_path / "o")
+    _tiny_bam(tmp_path / "a.bam", [("chr1", 1000)], 0, 3)
+    with pytest.raises(InvalidInputError):
+        MtDNAPipeline(str(tmp_path / "a.bam"), ["A"], tmp_path / "o")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", TXT_CASES)
+def test_pipeline_txt_gpu(case, tmp_path, engine_lib):
+    g, out, ret = _run_case(case, tmp_path)
+    _check_outputs(g, out, ret)
+
+
+@pytest.mark.parametrize("case", ["synth_tenx", "kat_tenx"])
+def test_cli_tenx_10x_layout(case, tmp_path, oracle_engine, monkeypatch):
+    """`tenx -i <project>` with its defaults finds outs/possorted_bam.bam and
+    outs/singlecell.csv (cli/utils.py:18-70) and writes the reference's files."""
+    from click.testing import CliRunner
+
+    from mgatk2_amd.cli import cli
+
+    g = Golden(case)
+    outs = tmp_path / "proj" / "outs"
+    outs.mkdir(parents=True)
+    soa_to_bam(outs / "possorted_bam.bam", g.soa, g.whitelist)
+    rows = ["barcode,is__cell_barcode"] + [f"{b},1" for b in g.whitelist] + ["TTTT-1,0"]
+    (outs / "singlecell.csv").write_text("\n".join(rows) + "\n")
+    monkeypatch.chdir(tmp_path)
+    r = CliRunner().invoke(cli, ["tenx", "-i", str(tmp_path / "proj"), "-o", "res"])
+    assert r.exit_code == 0, r.output
+    od = tmp_path / "res" / "output"
+    for name in ["A", "C", "G", "T", "coverage"]:
+        got = gzip.decompress((od / f"output.{name}.txt.gz").read_bytes()).decode()
+        assert got == str(g.exp(f"txt_{name}")), name
+    assert (od / "output.depthTable.txt").read_text() == str(g.exp("txt_depthTable"))
+    assert (tmp_path / "res" / "output.log").exists()
+    r = CliRunner().invoke(cli, ["run", "-i", str(outs / "possorted_bam.bam"), "-o", "dry", "--dry-run"])
+    assert r.exit_code == 0 and not (tmp_path / "dry" / "output").exists()
