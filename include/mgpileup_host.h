@@ -80,6 +80,17 @@ int64_t mgp_bam_find_tag(mgp_bam *bam, int tid, const char *tag, int64_t max_rec
 int64_t mgp_bam_count_tag(mgp_bam *bam, int tid, const char *tag, uint8_t **blob, int64_t *blob_bytes);
 void mgp_host_buf_free(void *p);
 
+/* txt output at scale (IncrementalTextWriter, src/file_io/writers.py:430-510):
+ * appends (append != 0) or writes `<prefix>.{coverage,A,C,G,T}.txt.gz` for the
+ * cells `cells[0..n_write)` in that order, named `names[k]`, from the engine's
+ * cell-major `counts` [*][mito_len][8] and `depth` [*][mito_len] (mgp_result).
+ * Lines "pos,bc,depth" / "pos,bc,fwd,rev" (1-based pos) for depth > 0 (and
+ * fwd+rev > 0). Each group of cells is one gzip member at `level`, deflated on
+ * `n_threads` threads (0 = all cores). */
+int mgp_txt_write_cells(const char *prefix, const uint32_t *counts, const uint32_t *depth, int64_t mito_len,
+                        const int64_t *cells, int64_t n_write, const char *const *names, int level,
+                        int n_threads, int append);
+
 #ifdef __cplusplus
 }
 #endif

@@ -75,6 +75,8 @@ def host_library() -> C.CDLL:
         lib.mgp_bam_count_tag.argtypes = [vp, C.c_int, C.c_char_p, C.POINTER(C.POINTER(C.c_uint8)),
                                           C.POINTER(C.c_int64)]
         lib.mgp_bam_count_tag.restype = C.c_int64
+        lib.mgp_txt_write_cells.argtypes = [C.c_char_p, vp, vp, C.c_int64, vp, C.c_int64, C.POINTER(C.c_char_p),
+                                            C.c_int, C.c_int, C.c_int]
         lib.mgp_host_buf_free.argtypes = [vp]
         lib.mgp_host_buf_free.restype = None
         _hlib = lib
@@ -180,6 +182,27 @@ class BamFile:
             out[key] = cnt
             p = z + 9
         return out
+
+
+def txt_write_cells(prefix: str | Path, counts: np.ndarray, depth: np.ndarray, cells, names: list[str],
+                    level: int = 6, n_threads: int = 0, append: bool = True) -> None:
+    """Native txt formatter + parallel gzip (libmgphost.so `mgp_txt_write_cells`)."""
+    lib = host_library()
+    counts = np.ascontiguousarray(counts, dtype=np.uint32)
+    depth = np.ascontiguousarray(depth, dtype=np.uint32)
+    cells = np.ascontiguousarray(cells, dtype=np.int64)
+    L = depth.shape[-1]
+    if counts.shape[-2:] != (L, 8) or counts.reshape(-1, L, 8).shape[0] != depth.reshape(-1, L).shape[0]:
+        raise ValueError("counts/depth shapes do not match")
+    if cells.size and (cells.min() < 0 or cells.max() >= depth.reshape(-1, L).shape[0]):
+        raise ValueError("cell index out of range")
+    if len(names) != cells.size:
+        raise ValueError("one name per written cell")
+    arr = (C.c_char_p * max(1, len(names)))(*[n.encode() for n in names])
+    rc = lib.mgp_txt_write_cells(str(prefix).encode(), counts.ctypes.data, depth.ctypes.data, L, cells.ctypes.data,
+                                 cells.size, arr, int(level), int(n_threads), 1 if append else 0)
+    if rc != 0:
+        raise OSError(_err())
 
 
 # ---------------------------------------------------------------------------

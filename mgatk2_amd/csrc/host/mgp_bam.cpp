@@ -25,9 +25,15 @@
 #include "../../../include/mgpileup.h"
 #include "../../../include/mgpileup_host.h"
 
+// one thread-local error string for every entry point of libmgphost.so
+std::string& mgp_host_err() {
+    static thread_local std::string e;
+    return e;
+}
+
 namespace {
 
-thread_local std::string g_err;
+#define g_err mgp_host_err()
 int fail(const std::string& m) {
     g_err = m;
     return -1;

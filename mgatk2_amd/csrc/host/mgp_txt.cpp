@@ -1,0 +1,179 @@
+// mgp_txt.cpp — mgatk txt output at scale (host side, libmgphost.so).
+//
+// Formats the per-cell count files of IncrementalTextWriter
+// (src/file_io/writers.py:430-462, layout in SURVEY.md §3.3) straight from the
+// engine's cell-major arrays and deflates them on a thread pool:
+//   output.coverage.txt.gz : "pos,barcode,depth"       for depth > 0
+//   output.{A,C,G,T}.txt.gz: "pos,barcode,fwd,rev"     for depth > 0 and fwd+rev > 0
+// Positions are 1-based; cells are written in the order given. Each group of
+// cells becomes one gzip member, so the files are multi-member gzip streams
+// whose decompressed bytes equal the reference's text (gzip readers,
+// Python's gzip and zcat concatenate members).
+#include <zlib.h>
+
+#include <algorithm>
+#include <atomic>
+#include <cstdint>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "../../../include/mgpileup_host.h"
+
+std::string& mgp_host_err();  // mgp_bam.cpp
+
+namespace {
+
+int fail(const std::string& m) {
+    mgp_host_err() = m;
+    return -1;
+}
+
+inline char* put_u64(char* p, uint64_t v) {
+    char tmp[24];
+    int n = 0;
+    do {
+        tmp[n++] = (char)('0' + v % 10);
+        v /= 10;
+    } while (v);
+    while (n) *p++ = tmp[--n];
+    return p;
+}
+
+struct Text {
+    std::vector<char> b;
+    size_t n = 0;
+    char* reserve(size_t k) {
+        if (n + k > b.size()) b.resize(std::max(b.size() * 2, n + k + (1u << 16)));
+        return b.data() + n;
+    }
+};
+
+bool gzip_member(const char* src, size_t n, int level, std::vector<uint8_t>& out) {
+    out.clear();
+    if (n == 0) return true;
+    z_stream zs;
+    std::memset(&zs, 0, sizeof(zs));
+    if (deflateInit2(&zs, level, Z_DEFLATED, 15 + 16, 8, Z_DEFAULT_STRATEGY) != Z_OK) return false;
+    out.resize(deflateBound(&zs, (uLong)n) + 64);
+    zs.next_in = (Bytef*)src;
+    zs.avail_in = (uInt)n;  // chunks are kept well below 4 GiB
+    zs.next_out = out.data();
+    zs.avail_out = (uInt)out.size();
+    const int r = deflate(&zs, Z_FINISH);
+    out.resize(zs.total_out);
+    deflateEnd(&zs);
+    return r == Z_STREAM_END;
+}
+
+// One group of cells -> 5 texts (coverage, A, C, G, T).
+void format_group(const uint32_t* counts, const uint32_t* depth, int64_t L, const int64_t* cells, int64_t c0,
+                  int64_t c1, const char* const* names, Text* txt) {
+    for (int64_t k = c0; k < c1; ++k) {
+        const int64_t c = cells[k];
+        const char* bc = names[k];
+        const size_t bl = std::strlen(bc);
+        const uint32_t* d = depth + (size_t)c * (size_t)L;
+        const uint32_t* q = counts + (size_t)c * (size_t)L * 8;
+        for (int64_t p = 0; p < L; ++p) {
+            const uint32_t dp = d[p];
+            if (!dp) continue;
+            char* w = txt[0].reserve(bl + 40);
+            char* s = w;
+            w = put_u64(w, (uint64_t)p + 1);
+            *w++ = ',';
+            std::memcpy(w, bc, bl);
+            w += bl;
+            *w++ = ',';
+            w = put_u64(w, dp);
+            *w++ = '\n';
+            txt[0].n += (size_t)(w - s);
+            const uint32_t* e = q + (size_t)p * 8;
+            for (int b = 0; b < 4; ++b) {
+                const uint32_t fw = e[2 * b], rv = e[2 * b + 1];
+                if (!(fw | rv)) continue;
+                Text& t = txt[1 + b];
+                char* x = t.reserve(bl + 56);
+                char* x0 = x;
+                x = put_u64(x, (uint64_t)p + 1);
+                *x++ = ',';
+                std::memcpy(x, bc, bl);
+                x += bl;
+                *x++ = ',';
+                x = put_u64(x, fw);
+                *x++ = ',';
+                x = put_u64(x, rv);
+                *x++ = '\n';
+                t.n += (size_t)(x - x0);
+            }
+        }
+    }
+}
+
+}  // namespace
+
+extern "C" {
+
+int mgp_txt_write_cells(const char* prefix, const uint32_t* counts, const uint32_t* depth, int64_t mito_len,
+                        const int64_t* cells, int64_t n_write, const char* const* names, int level, int n_threads,
+                        int append) {
+    mgp_host_err().clear();
+    if (!prefix || (n_write > 0 && (!counts || !depth || !cells || !names)) || mito_len <= 0 || n_write < 0)
+        return fail("bad arguments");
+    if (level < 0 || level > 9) return fail("gzip level must be 0..9");
+    static const char* kNames[5] = {"coverage", "A", "C", "G", "T"};
+    FILE* f[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
+    for (int i = 0; i < 5; ++i) {
+        const std::string path = std::string(prefix) + "." + kNames[i] + ".txt.gz";
+        f[i] = std::fopen(path.c_str(), append ? "ab" : "wb");
+        if (!f[i]) {
+            for (int j = 0; j < i; ++j) std::fclose(f[j]);
+            return fail("cannot open " + path);
+        }
+    }
+    // groups of cells sized for ~4 MB of text each (a covered position costs ~30 B per file)
+    const int64_t per_group = std::max<int64_t>(1, (int64_t)((4u << 20) / ((size_t)mito_len * 40 + 1)));
+    const int64_t n_groups = (n_write + per_group - 1) / per_group;
+    const int nt = std::max(1, std::min<int>(n_threads > 0 ? n_threads : (int)std::thread::hardware_concurrency(),
+                                             (int)std::max<int64_t>(1, n_groups)));
+    const int64_t round = (int64_t)nt * 4;
+    std::vector<std::vector<uint8_t>> out((size_t)round * 5);
+    std::atomic<bool> ok{true};
+    int rc = 0;
+    for (int64_t g0 = 0; g0 < n_groups && rc == 0; g0 += round) {
+        const int64_t g1 = std::min(n_groups, g0 + round);
+        std::atomic<int64_t> next{g0};
+        auto work = [&]() {
+            Text txt[5];
+            for (;;) {
+                const int64_t g = next.fetch_add(1);
+                if (g >= g1) break;
+                for (auto& t : txt) t.n = 0;
+                const int64_t c0 = g * per_group, c1 = std::min(n_write, c0 + per_group);
+                format_group(counts, depth, mito_len, cells, c0, c1, names, txt);
+                for (int i = 0; i < 5; ++i)
+                    if (!gzip_member(txt[i].b.data(), txt[i].n, level, out[(size_t)(g - g0) * 5 + i])) ok = false;
+            }
+        };
+        std::vector<std::thread> th;
+        for (int t = 1; t < nt; ++t) th.emplace_back(work);
+        work();
+        for (auto& t : th) t.join();
+        if (!ok) {
+            rc = fail("deflate failed");
+            break;
+        }
+        for (int64_t g = g0; g < g1 && rc == 0; ++g)
+            for (int i = 0; i < 5; ++i) {
+                const auto& o = out[(size_t)(g - g0) * 5 + i];
+                if (!o.empty() && std::fwrite(o.data(), 1, o.size(), f[i]) != o.size()) rc = fail("write failed");
+            }
+    }
+    for (int i = 0; i < 5; ++i)
+        if (std::fclose(f[i]) != 0 && rc == 0) rc = fail("close failed");
+    return rc;
+}
+
+}  // extern "C"

@@ -21,13 +21,13 @@ order, the reference's sequential order).
 
 from __future__ import annotations
 
-import gzip
 import logging
-import shutil
+import os
 from pathlib import Path
 
 import numpy as np
 
+from ..bam import txt_write_cells
 from .formats import write_cell_stats
 
 logger = logging.getLogger(__name__)
@@ -103,9 +103,16 @@ class _OneCell:
 # txt
 # ---------------------------------------------------------------------------
 class IncrementalTextWriter:
-    """mgatk txt format (writers.py:409-510)."""
+    """mgatk txt format (writers.py:409-510).
 
-    def __init__(self, output_dir: Path, config, barcodes: list[str]):
+    The count files are formatted and deflated natively (libmgphost.so
+    `mgp_txt_write_cells`): every call appends gzip members to
+    ``output.{A,C,G,T,coverage}.txt.gz``, so no uncompressed copy is kept and
+    ``finalize`` has nothing left to compress. The decompressed text equals the
+    reference's."""
+
+    def __init__(self, output_dir: Path, config, barcodes: list[str], gzip_level: int | None = None,
+                 n_threads: int = 0):
         self.output_dir = Path(output_dir) / "output"
         self.output_dir.mkdir(exist_ok=True, parents=True)
         self.config = config
@@ -113,39 +120,30 @@ class IncrementalTextWriter:
         self.cell_stats: list[dict] = []
         self.position_base_counts = np.zeros((config.mito_length, 4), np.int64)
         self.cell_depths: dict[str, float] = {}
-        self.base_files = {b: open(self.output_dir / f"output.{b}.txt", "w") for b in BASES}
-        self.coverage_file = open(self.output_dir / "output.coverage.txt", "w")
+        self.gzip_level = int(os.environ.get("MGP_GZIP_LEVEL", 6)) if gzip_level is None else gzip_level
+        self.n_threads = n_threads
+        self.prefix = self.output_dir / "output"
+        for name in [*BASES, "coverage"]:
+            open(self.output_dir / f"output.{name}.txt.gz", "wb").close()
 
     # array path -----------------------------------------------------------
     def write_cells(self, res, cells, barcodes: list[str] | None = None, tally: np.ndarray | None = None):
         """Write the given cells (indices into `res`) in order."""
         names = barcodes if barcodes is not None else self.barcodes
         L = self.config.mito_length
-        for c in cells:
-            c = int(c)
-            bc = names[c]
-            self.cell_stats.append(cell_qc(res, c, bc, L))
-            self._emit(bc, res.counts[c], res.depth[c], float(res.depth_sum[c]) / int(res.covered[c]))
+        cells = np.asarray(cells, dtype=np.int64)
+        for c in cells.tolist():
+            q = cell_qc(res, c, names[c], L)
+            self.cell_stats.append(q)
+            self.cell_depths[names[c]] = q["mean_depth"]
+        txt_write_cells(self.prefix, res.counts, res.depth, cells, [names[c] for c in cells.tolist()],
+                        level=self.gzip_level, n_threads=self.n_threads)
         if tally is not None:
             self.position_base_counts += tally.astype(np.int64)
         else:
-            for c in cells:
-                cnt = res.counts[int(c)].astype(np.int64)
+            for c in cells.tolist():
+                cnt = res.counts[c].astype(np.int64)
                 self.position_base_counts += cnt[:, 0::2] + cnt[:, 1::2]
-
-    def _emit(self, bc: str, counts: np.ndarray, depth: np.ndarray, mean_depth: float):
-        self.cell_depths[bc] = mean_depth
-        pos = np.flatnonzero(depth > 0)
-        p1 = (pos + 1).tolist()
-        self.coverage_file.write("".join(f"{p},{bc},{d}\n" for p, d in zip(p1, depth[pos].tolist())))
-        cp = counts[pos]
-        for bi, b in enumerate(BASES):
-            fw = cp[:, 2 * bi]
-            rv = cp[:, 2 * bi + 1]
-            sel = np.flatnonzero((fw > 0) | (rv > 0))
-            self.base_files[b].write(
-                "".join(f"{p1[i]},{bc},{f},{r}\n" for i, f, r in zip(sel.tolist(), fw[sel].tolist(), rv[sel].tolist()))
-            )
 
     # reference per-cell API (writers.py:430-462) ----------------------------
     def write_cell(self, result: dict):
@@ -153,22 +151,13 @@ class IncrementalTextWriter:
         if "qc" in result:
             self.cell_stats.append(result["qc"])
         kept = one.depth[0][one.depth[0] > 0]
-        mean = float(kept.sum()) / kept.size if kept.size else 0
-        self._emit(result["barcode"], one.counts[0], one.depth[0], mean)
+        self.cell_depths[result["barcode"]] = float(kept.sum()) / kept.size if kept.size else 0
+        txt_write_cells(self.prefix, one.counts, one.depth, [0], [result["barcode"]], level=self.gzip_level,
+                        n_threads=1)
         cnt = one.counts[0].astype(np.int64)
         self.position_base_counts += cnt[:, 0::2] + cnt[:, 1::2]
 
     def finalize(self, qc_dir: Path):
-        for f in self.base_files.values():
-            f.close()
-        self.coverage_file.close()
-        logger.info("Compressing output .txt files...")
-        for name in [*BASES, "coverage"]:
-            txt_file = self.output_dir / f"output.{name}.txt"
-            gz_file = self.output_dir / f"output.{name}.txt.gz"
-            with open(txt_file, "rb") as f_in, gzip.open(gz_file, "wb", compresslevel=9) as f_out:
-                shutil.copyfileobj(f_in, f_out)
-            txt_file.unlink()
         with open(self.output_dir / "output.depthTable.txt", "w") as f:
             for cell, depth in sorted(self.cell_depths.items()):
                 f.write(f"{cell}\t{depth:.2f}\n")
