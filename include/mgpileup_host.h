@@ -91,6 +91,16 @@ int mgp_txt_write_cells(const char *prefix, const uint32_t *counts, const uint32
                         const int64_t *cells, int64_t n_write, const char *const *names, int level,
                         int n_threads, int append);
 
+/* HDF5 output at scale (IncrementalHDF5Writer, src/file_io/writers.py:60-406):
+ * deflates every (crow x ccol) chunk of a row-major `rows x cols` array of
+ * `elem_size`-byte elements, in the form of the HDF5 deflate filter (zlib
+ * stream of the full chunk, edge chunks padded with 0), on `n_threads`
+ * threads. Chunks are numbered row-major over the chunk grid; chunk t occupies
+ * blob[offsets[t], offsets[t+1]) (`offsets` has n_chunks + 1 entries).
+ * Returns the number of chunks, -1 on error. Free `*blob` with mgp_host_buf_free. */
+int64_t mgp_deflate_tiles(const void *data, int64_t rows, int64_t cols, int32_t elem_size, int64_t crow,
+                          int64_t ccol, int level, int n_threads, uint8_t **blob, int64_t *offsets);
+
 #ifdef __cplusplus
 }
 #endif

@@ -77,6 +77,9 @@ def host_library() -> C.CDLL:
         lib.mgp_bam_count_tag.restype = C.c_int64
         lib.mgp_txt_write_cells.argtypes = [C.c_char_p, vp, vp, C.c_int64, vp, C.c_int64, C.POINTER(C.c_char_p),
                                             C.c_int, C.c_int, C.c_int]
+        lib.mgp_deflate_tiles.argtypes = [vp, C.c_int64, C.c_int64, C.c_int32, C.c_int64, C.c_int64, C.c_int, C.c_int,
+                                          C.POINTER(C.POINTER(C.c_uint8)), vp]
+        lib.mgp_deflate_tiles.restype = C.c_int64
         lib.mgp_host_buf_free.argtypes = [vp]
         lib.mgp_host_buf_free.restype = None
         _hlib = lib
@@ -203,6 +206,26 @@ def txt_write_cells(prefix: str | Path, counts: np.ndarray, depth: np.ndarray, c
                                  cells.size, arr, int(level), int(n_threads), 1 if append else 0)
     if rc != 0:
         raise OSError(_err())
+
+
+def deflate_tiles(a: np.ndarray, chunks: tuple[int, int], level: int = 4, n_threads: int = 0) -> list[bytes]:
+    """Deflate every chunk of a 2-D array as the HDF5 deflate filter stores it
+    (libmgphost.so `mgp_deflate_tiles`); chunks in row-major grid order."""
+    lib = host_library()
+    a = np.ascontiguousarray(a)
+    rows, cols = a.shape
+    nr, nc = -(-rows // chunks[0]), -(-cols // chunks[1])
+    offs = np.zeros(nr * nc + 1, np.int64)
+    blob = C.POINTER(C.c_uint8)()
+    n = lib.mgp_deflate_tiles(a.ctypes.data, rows, cols, a.dtype.itemsize, chunks[0], chunks[1], int(level),
+                              int(n_threads), C.byref(blob), offs.ctypes.data)
+    if n < 0:
+        raise OSError(_err())
+    try:
+        raw = C.string_at(blob, int(offs[-1])) if offs[-1] else b""
+    finally:
+        lib.mgp_host_buf_free(C.cast(blob, C.c_void_p))
+    return [raw[offs[i]:offs[i + 1]] for i in range(n)]
 
 
 # ---------------------------------------------------------------------------

@@ -175,14 +175,18 @@ class IncrementalTextWriter:
 # HDF5
 # ---------------------------------------------------------------------------
 def _h5py():
+    """h5py when installed, else the ctypes binding of libhdf5 (mgatk2_amd.h5lite)."""
     try:
         import h5py  # noqa: F401
 
         return h5py
-    except ImportError as e:  # pragma: no cover - depends on the environment
-        raise ImportError(
-            "HDF5 output needs h5py (not installed); use --format txt or install h5py"
-        ) from e
+    except ImportError:
+        pass
+    from .. import h5lite
+
+    if not h5lite.available():  # pragma: no cover - depends on the environment
+        raise ImportError("HDF5 output needs h5py or libhdf5 (set MGP_HDF5_LIB); use --format txt")
+    return h5lite.module()
 
 
 class IncrementalHDF5Writer:
@@ -233,18 +237,36 @@ class IncrementalHDF5Writer:
         return mean
 
     def write_cells(self, res, cells, barcodes: list[str] | None = None, tally: np.ndarray | None = None):
+        """Columns of the given cells (whitelist index of their barcode), vectorised
+        over cells; values as in _put (writers.py:154-264)."""
         names = barcodes if barcodes is not None else self.barcodes
-        for c in cells:
-            c = int(c)
+        sel, cols = [], []
+        for c in np.asarray(cells, dtype=np.int64).tolist():
             bc = names[c]
             if bc not in self.barcode_to_idx:
                 continue
-            col = self.barcode_to_idx[bc]
-            self.cell_stats.append(cell_qc(res, c, bc, self.n_positions))
-            self.cell_depths[bc] = self._put(
-                col, res.counts[c], res.tn5[c], res.depth[c], int(res.median_lo[c]), int(res.median_hi[c]),
-                int(res.depth_sum[c]), int(res.covered[c]), int(res.depth_max[c]),
-            )
+            sel.append(c)
+            cols.append(self.barcode_to_idx[bc])
+            q = cell_qc(res, c, bc, self.n_positions)
+            self.cell_stats.append(q)
+            self.cell_depths[bc] = q["mean_depth"]
+        if sel:
+            sel_a = np.asarray(sel, np.int64)
+            col_a = np.asarray(cols, np.int64)
+            for bi, b in enumerate(BASES):
+                for si, s in enumerate(STRANDS):
+                    self._planes[f"{b}_{s}"][:, col_a] = np.minimum(res.counts[sel_a, :, 2 * bi + si], 65535).T
+            for si, s in enumerate(STRANDS):
+                self._tn5[s][:, col_a] = np.minimum(res.tn5[sel_a, :, si], 65535).T
+            self._coverage[:, col_a] = np.minimum(res.depth[sel_a], 65535).T
+            covered = res.covered[sel_a].astype(np.float64)
+            dsum = res.depth_sum[sel_a]
+            self._meta["mean_depth"][col_a] = (dsum.astype(np.float64) / covered).astype(np.float32)
+            self._meta["median_depth"][col_a] = ((res.median_lo[sel_a].astype(np.float64)
+                                                  + res.median_hi[sel_a].astype(np.float64)) / 2.0).astype(np.float32)
+            self._meta["max_depth"][col_a] = np.minimum(res.depth_max[sel_a], 65535).astype(np.uint16)
+            self._meta["genome_coverage"][col_a] = (res.covered[sel_a] / self.n_positions * 100).astype(np.float32)
+            self._meta["total_bases"][col_a] = dsum.astype(np.int64).astype(np.float32)
         if tally is not None:
             self.position_base_counts += tally.astype(np.int64)
         else:

@@ -239,3 +239,51 @@ def test_cli_tenx_10x_layout(case, tmp_path, oracle_engine, monkeypatch):
     assert (tmp_path / "res" / "output.log").exists()
     r = CliRunner().invoke(cli, ["run", "-i", str(outs / "possorted_bam.bam"), "-o", "dry", "--dry-run"])
     assert r.exit_code == 0 and not (tmp_path / "dry" / "output").exists()
+
+
+H5_CASES = [c for c in CASES if Golden(c).params["output_format"] == "hdf5"]
+
+
+def _run_case_h5(case, tmp_path):
+    from mgatk2_amd.pipeline import run_pipeline
+
+    g = Golden(case)
+    p = g.params
+    bam = tmp_path / "x.bam"
+    soa_to_bam(bam, g.soa, g.whitelist)
+    bfile = tmp_path / "barcodes.tsv"
+    bfile.write_text("".join(b + "\n" for b in g.whitelist))
+    out = tmp_path / "out"
+    ret = run_pipeline(
+        str(bam), str(bfile), str(out), min_baseq=p["min_baseq"], min_mapq=p["min_mapq"],
+        min_reads_per_cell=p["min_reads_per_cell"], max_strand_bias=p["max_strand_bias"],
+        skip_deduplication=p["skip_deduplication"], use_fragment_length_dedup=p["use_fragment_length_dedup"],
+        output_format="hdf5",
+    )
+    return g, out, ret
+
+
+def _check_h5(g, out):
+    from mgatk2_amd import h5lite
+
+    with h5lite.File(out / "output" / "counts.h5", "r") as f:
+        for k in f.keys():
+            np.testing.assert_array_equal(f[k][...], g.exp("h5c_" + k), err_msg=k)
+    with h5lite.File(out / "output" / "metadata.h5", "r") as f:
+        for k in ["coverage", "mean_depth", "median_depth", "max_depth", "genome_coverage", "total_bases",
+                  "reference"]:
+            np.testing.assert_array_equal(f[k][...], g.exp("h5m_" + k), err_msg=k)
+    assert (out / "qc" / "cell_stats.csv").read_text() == str(g.exp("cell_stats"))
+
+
+@pytest.mark.parametrize("case", H5_CASES)
+def test_pipeline_hdf5_host(case, tmp_path, oracle_engine):
+    g, out, _ = _run_case_h5(case, tmp_path)
+    _check_h5(g, out)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", H5_CASES)
+def test_pipeline_hdf5_gpu(case, tmp_path, engine_lib):
+    g, out, _ = _run_case_h5(case, tmp_path)
+    _check_h5(g, out)

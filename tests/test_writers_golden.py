@@ -109,3 +109,63 @@ def test_hdf5_writer_matches_reference(case, oracle_lib, tmp_path):
     for k, ds in cf.items.items():
         assert {a: (list(b) if isinstance(b, tuple) else b) for a, b in ds.kw.items()} == kw[k], k
     assert (tmp_path / "qc" / "cell_stats.csv").read_text() == str(g.exp("cell_stats"))
+
+
+@pytest.mark.parametrize("case", H5_CASES)
+def test_hdf5_files_match_reference(case, oracle_lib, tmp_path):
+    """Real counts.h5 / metadata.h5 through libhdf5 (mgatk2_amd.h5lite; chunks
+    deflated in parallel and written with H5Dwrite_chunk), read back through
+    libhdf5's own filter pipeline, equal the reference's datasets and attrs."""
+    from mgatk2_amd import h5lite
+    from mgatk2_amd.file_io import IncrementalHDF5Writer
+
+    if not h5lite.available():
+        pytest.skip("libhdf5 not present")
+    g = Golden(case)
+    res, _ = oracle_lib.oracle_run(g.config(), g.soa)
+    w = IncrementalHDF5Writer(tmp_path, _config(g), g.whitelist, h5=h5lite.module())
+    w.write_cells(res, _written(res), tally=res.ref_tally)
+    w.finalize(tmp_path / "qc")
+    kw = json.loads(str(g.exp("h5_kw_json")))
+    with h5lite.File(tmp_path / "output" / "counts.h5", "r") as f:
+        exp_keys = {k[len("exp_h5c_"):] for k in g.z.files if k.startswith("exp_h5c_") and not k.endswith("_json")}
+        assert set(f.keys()) == exp_keys
+        for k in exp_keys:
+            got, exp = f[k][...], g.exp("h5c_" + k)
+            assert got.dtype == exp.dtype, k
+            np.testing.assert_array_equal(got, exp, err_msg=k)
+            if kw[k]:
+                assert f[k].chunks == tuple(kw[k]["chunks"]) and f[k].compression == "gzip"
+        attrs = {k: (v.item() if hasattr(v, "item") else v) for k, v in f.attrs.items()}
+        assert attrs == json.loads(str(g.exp("h5c_attrs_json")))
+    with h5lite.File(tmp_path / "output" / "metadata.h5", "r") as f:
+        for k in ["coverage", "mean_depth", "median_depth", "max_depth", "genome_coverage", "total_bases",
+                  "reference"]:
+            got, exp = f[k][...], g.exp("h5m_" + k)
+            assert got.dtype == exp.dtype, k
+            np.testing.assert_array_equal(got, exp, err_msg=k)
+        attrs = {k: (v.item() if hasattr(v, "item") else v) for k, v in f.attrs.items()}
+        assert attrs == json.loads(str(g.exp("h5m_attrs_json")))
+
+
+def test_hdf5_barcode_metadata_group(tmp_path, oracle_lib):
+    """singlecell.csv columns land in metadata.h5/barcode_metadata, in whitelist order (writers.py:358-388)."""
+    from mgatk2_amd import h5lite
+    from mgatk2_amd.file_io import IncrementalHDF5Writer
+
+    if not h5lite.available():
+        pytest.skip("libhdf5 not present")
+    g = Golden("synth_run_h5")
+    res, _ = oracle_lib.oracle_run(g.config(), g.soa)
+    wl = g.whitelist
+    meta = {"barcode": list(reversed(wl)), "passed_filters": list(range(len(wl))),
+            "frac": [0.5] * len(wl), "excluded_reason": [""] * len(wl)}
+    w = IncrementalHDF5Writer(tmp_path, _config(g), wl, barcode_metadata=meta, h5=h5lite.module())
+    w.write_cells(res, _written(res), tally=res.ref_tally)
+    w.finalize(tmp_path / "qc")
+    with h5lite.File(tmp_path / "output" / "metadata.h5", "r") as f:
+        grp = f["barcode_metadata"]
+        assert set(grp.keys()) == set(meta)
+        assert [b.decode() for b in grp["barcode"][...]] == wl
+        np.testing.assert_array_equal(grp["passed_filters"][...], list(reversed(range(len(wl)))))
+        assert grp["frac"][...].dtype == np.float64
