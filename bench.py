@@ -44,8 +44,8 @@ def parse():
     ap.add_argument("--cells", type=int, default=10_000, help="cells per GPU")
     ap.add_argument("--read-len", type=int, default=50)
     ap.add_argument("--seed", type=int, default=20251015 + 4)
-    ap.add_argument("--cpu-sample-reads", type=int, default=10_000_000)
-    ap.add_argument("--cpu-sample-cells", type=int, default=500)
+    ap.add_argument("--cpu-sample-reads", type=int, default=20_000_000)
+    ap.add_argument("--cpu-sample-cells", type=int, default=1000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--check", action="store_true", help="bit-exact check of a sample against the oracle")
     return ap.parse_args()
