@@ -70,6 +70,8 @@ def _options(defaults: dict, helps: dict | None = None):
             click.option("--dry-run", is_flag=True, help="Show configuration and exit without processing"),
             click.option("--device", "device", default=0, type=int, show_default=True,
                          help="HIP device ordinal for the pileup engine"),
+            click.option("--devices", "devices", default=None,
+                         help="Comma-separated HIP devices to shard cells over (e.g. 0,1,2,3)"),
         ]
         for o in reversed(opts):
             f = o(f)
@@ -183,7 +185,7 @@ def run_pipeline_command(bam_path, output_dir, barcode_file, barcode_tag, min_ba
                          verbose, batch_size, max_memory, base_qual, min_mapq, min_reads, max_strand_bias,
                          min_distance_from_end, dedup_mode, output_format, sequential, dry_run=False,
                          original_bam_path=None, report_title=None, report_subtitle=None, working_directory=None,
-                         device=0) -> int:
+                         device=0, devices=None) -> int:
     """cli/utils.py:124-289: returns 0 on success, 1 on a handled error."""
     from .pipeline import run_pipeline
     from .utils import validate_bam_file, validate_barcode_file
@@ -236,6 +238,7 @@ def run_pipeline_command(bam_path, output_dir, barcode_file, barcode_tag, min_ba
             skip_deduplication=skip_dedup, use_fragment_length_dedup=use_fragment_length_dedup,
             sequential=sequential, report_title=report_title, report_subtitle=report_subtitle or
             "mgatk2 output analysis", working_directory=working_directory, device=device,
+            devices=[int(x) for x in devices.split(",")] if devices else None,
         )
         if max_memory is not None:
             run_args["max_memory_gb"] = max_memory
@@ -274,7 +277,7 @@ def cli():
 @_options(RUN_DEFAULTS)
 def run(bam_path, mito_genome, barcode_file, barcode_tag, min_barcode_reads, output_dir, ncores, verbose, batch_size,
         max_memory, base_qual, min_mapq, min_reads, max_strand_bias, min_distance_from_end, dedup_mode,
-        output_format, dry_run, device):
+        output_format, dry_run, device, devices):
     """Run mgatk2 with optimised defaults"""
     try:
         rc = run_pipeline_command(
@@ -282,7 +285,7 @@ def run(bam_path, mito_genome, barcode_file, barcode_tag, min_barcode_reads, out
             batch_size, max_memory, base_qual, min_mapq, min_reads, max_strand_bias, min_distance_from_end,
             dedup_mode, output_format, ncores == 1, dry_run=dry_run, original_bam_path=bam_path,
             report_title=get_10x_parent_directory_name(bam_path), report_subtitle="mgatk2 output analysis",
-            working_directory=os.getcwd(), device=device)
+            working_directory=os.getcwd(), device=device, devices=devices)
     except KeyboardInterrupt:
         raise SystemExit(130) from None
     if rc:
@@ -293,12 +296,12 @@ def run(bam_path, mito_genome, barcode_file, barcode_tag, min_barcode_reads, out
 @_options(TENX_DEFAULTS)
 def tenx(bam_path, mito_genome, barcode_file, barcode_tag, min_barcode_reads, output_dir, ncores, verbose, batch_size,
          max_memory, base_qual, min_mapq, min_reads, max_strand_bias, min_distance_from_end, dedup_mode,
-         output_format, dry_run, device):
+         output_format, dry_run, device, devices):
     """Run mgatk2 with original mgatk package behaviour"""
     rc = run_pipeline_command(
         bam_path, output_dir, barcode_file, barcode_tag, min_barcode_reads, mito_genome, ncores, verbose,
         batch_size, max_memory, base_qual, min_mapq, min_reads, max_strand_bias, min_distance_from_end, dedup_mode,
-        output_format, ncores == 1, dry_run=dry_run, device=device)
+        output_format, ncores == 1, dry_run=dry_run, device=device, devices=devices)
     if rc:
         raise SystemExit(rc)
 

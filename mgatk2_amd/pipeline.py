@@ -50,6 +50,7 @@ class MtDNAPipeline:
         report_subtitle: str | None = None,
         working_directory: str | None = None,
         device: int = 0,
+        devices: list[int] | None = None,
     ):
         self.bam_path = Path(bam_path)
         self.barcodes = set(barcodes)
@@ -63,6 +64,7 @@ class MtDNAPipeline:
         self.report_subtitle = report_subtitle or "mgatk2 output analysis"
         self.working_directory = working_directory
         self.device = device
+        self.devices = list(devices) if devices else [device]
         self.timings: dict[str, float] = {}
         self.engine_result = None
         self.read_stats: dict = {}
@@ -90,7 +92,7 @@ class MtDNAPipeline:
         soa, stats = reader.read_soa()
         t1 = time.time()
 
-        processor = CellProcessor(self.config, self.output_dir, device=self.device)
+        processor = CellProcessor(self.config, self.output_dir, device=self.device, devices=self.devices)
         res = processor.run_soa(soa, len(self.barcode_list))
         del soa
         t2 = time.time()
@@ -177,6 +179,7 @@ def run_pipeline(
     report_subtitle: str | None = None,
     working_directory: str | None = None,
     device: int = 0,
+    devices: list[int] | None = None,
 ) -> dict[str, Any]:
     """pipeline.py:183-269. ``min_distance_from_end`` is accepted and, as in the
     reference, not passed on (the engine uses 5)."""
@@ -214,6 +217,6 @@ def run_pipeline(
         bam_path=bam_path, barcodes=barcodes, output_dir=Path(output_dir), config=config,
         output_format=output_format, barcode_metadata=barcode_metadata, sample_name=sample_name,
         report_title=report_title, report_subtitle=report_subtitle, working_directory=working_directory,
-        device=device,
+        device=device, devices=devices,
     )
     return pipeline.run()

@@ -62,10 +62,11 @@ def process_barcode_worker(args):
 
 
 class CellProcessor:
-    def __init__(self, config, output_dir, device: int = 0):
+    def __init__(self, config, output_dir, device: int = 0, devices: list[int] | None = None):
         self.config = config
         self.output_dir = output_dir
         self.device = device
+        self.devices = list(devices) if devices else [device]
         self.last_result: EngineResult | None = None
         self.last_stats: dict = {}
 
@@ -75,6 +76,8 @@ class CellProcessor:
         filters, dedup, pileup, strand filter, per-cell statistics, tallies."""
         if isinstance(soa_batches, ReadSoA):
             soa_batches = [soa_batches]
+        if len(self.devices) > 1:
+            return self._run_sharded(soa_batches, n_cells)
         n = sum(b.n for b in soa_batches)
         pay = sum(int(b.payload.shape[0]) for b in soa_batches)
         ec = self.config.engine_config(n_cells, reserve_reads=n, reserve_payload=pay + 256 * len(soa_batches))
@@ -83,6 +86,33 @@ class CellProcessor:
                 eng.push(b)
             res = eng.finish()
             self.last_stats = eng.kernel_times()
+        self.last_result = res
+        return res
+
+    def _run_sharded(self, soa_batches, n_cells: int) -> EngineResult:
+        """Cells split into contiguous read-balanced ranges, one engine per device,
+        run concurrently (ctypes releases the GIL); results concatenated along
+        cells and tallies summed on the host."""
+        from concurrent.futures import ThreadPoolExecutor
+
+        from ..shard import merge_results, partition_cells, reads_per_cell, shard_soa
+        from ..synth import concat_soa
+
+        soa = soa_batches[0] if len(soa_batches) == 1 else concat_soa(soa_batches)
+        b = partition_cells(reads_per_cell(soa, n_cells), len(self.devices))
+        shards = [(int(lo), int(hi)) + shard_soa(soa, int(lo), int(hi)) for lo, hi in zip(b[:-1], b[1:])]
+
+        def one(i):
+            lo, hi, sub, idx = shards[i]
+            ec = self.config.engine_config(hi - lo, reserve_reads=sub.n, reserve_payload=sub.payload.shape[0] + 256)
+            with Engine(ec, device=self.devices[i]) as eng:
+                if sub.n:
+                    eng.push(sub)
+                return eng.finish(), lo, hi, idx
+
+        with ThreadPoolExecutor(len(self.devices)) as ex:
+            parts = list(ex.map(one, range(len(self.devices))))
+        res = merge_results(parts, n_cells, soa.n)
         self.last_result = res
         return res
 
