@@ -178,9 +178,12 @@ typedef struct mgp_synth_params {
 typedef struct mgp_ctx mgp_ctx;
 
 int         mgp_abi_version(void);
-const char *mgp_last_error(void);
+const char *mgp_last_error(void);  /* message of the last failing call on this thread; the
+                                     * wrapper raises the matching src/core/exceptions.py class */
 int         mgp_device_count(int *out);
 
+/* Replaces the per-run setup of CellProcessor(config, output_dir)
+ * (src/processing/processors.py:59-61) + PipelineConfig (src/core/config.py:77-114). */
 int  mgp_open(const mgp_config *cfg, int hip_device, mgp_ctx **out);
 void mgp_close(mgp_ctx *ctx);
 
@@ -188,18 +191,28 @@ void mgp_close(mgp_ctx *ctx);
 int  mgp_host_alloc(int64_t bytes, void **out);
 int  mgp_host_free(void *p);
 
-/* Append a batch to the device-resident read set (async H2D on the copy stream). */
+/* Append a batch to the device-resident read set (async H2D on the copy stream).
+ * Replaces the accumulation of reads_by_barcode in
+ * BAMReader.collect_reads_by_barcode (src/processing/readers.py:85-165): the
+ * batch is every fetch(mito_chr) record in BAM order, unfiltered. */
 int  mgp_push_batch(mgp_ctx *ctx, const mgp_batch *batch);
 /* Drop resident reads (keeps allocations). */
 int  mgp_reset(mgp_ctx *ctx);
 /* Number of resident reads / payload bytes. */
 int  mgp_resident(mgp_ctx *ctx, int64_t *n_reads, int64_t *payload_bytes);
 
-/* Run the whole hot path over the resident reads (async on the compute stream). */
+/* Run the whole hot path over the resident reads (async on the compute stream):
+ * the record filters and dedup of readers.py:95-150, process_barcode_worker
+ * (processors.py:20-55) = generate_pileup + filter_strand_bias
+ * (pileup.py:18-154) for every cell, the per-cell statistics of
+ * processors.py:33-51 / writers.py:187-197 and the reference-allele tallies of
+ * writers.py:221-222,340-349. */
 int  mgp_run(mgp_ctx *ctx);
 /* Wait for the last run; returns the run's check status (MGP_E_UNSORTED, ...). */
 int  mgp_sync(mgp_ctx *ctx);
-/* D2H the results of the last run into caller buffers (implies mgp_sync). */
+/* D2H the results of the last run into caller buffers (implies mgp_sync):
+ * the dense form of the per-cell result dicts (processors.py:41-51) and of the
+ * stats dict (readers.py:193-199). */
 int  mgp_fetch(mgp_ctx *ctx, mgp_result *out);
 /* Convenience: mgp_run + mgp_fetch. */
 int  mgp_finish(mgp_ctx *ctx, mgp_result *out);
@@ -210,7 +223,9 @@ int  mgp_finish(mgp_ctx *ctx, mgp_result *out);
 int  mgp_kernel_times(mgp_ctx *ctx, int last_runs, float *ms, int max_n, int *n_out, char *names, int names_len);
 
 /* RCCL: rank 0 creates the unique id (128 bytes), every rank joins. After init,
- * mgp_run all-reduces ref_tally over the communicator. */
+ * mgp_run all-reduces ref_tally over the communicator (no reference
+ * counterpart: the reference sums position_base_counts in one process,
+ * writers.py:221-222). */
 int  mgp_comm_unique_id(uint8_t *out128);
 int  mgp_comm_init(mgp_ctx *ctx, const uint8_t *uid128, int nranks, int rank);
 
