@@ -332,17 +332,26 @@ __global__ void __launch_bounds__(kBlock) k_scatter(int64_t n, const int32_t* __
     // kLds: counters in LDS seeded from the scanned row; else `cur`, a global copy of
     // the scanned rows (one workgroup owns row b and the waves take turns)
     uint32_t* cnt = kLds ? cnt_lds : cur + (size_t)b * nc;
+    // kLds: fbits[c] = no read of cell c in bins < b (its first read in BAM order, if
+    // any is in this bin, is claimed by the first group of c here: first_read)
+    uint32_t* fbits = cnt_lds + nc;
     if (kLds) {
-        for (int c = threadIdx.x; c < nc; c += blockDim.x) cnt_lds[c] = O[(size_t)b * nc + c];
+        for (int c = threadIdx.x; c < (nc + 31) / 32; c += blockDim.x) fbits[c] = 0;
+        __syncthreads();
+        for (int c = threadIdx.x; c < nc; c += blockDim.x) {
+            const uint32_t o = O[(size_t)b * nc + c];
+            cnt_lds[c] = o;
+            if (o == O[c]) atomicOr(&fbits[c >> 5], 1u << (c & 31));
+        }
     }
     const int64_t lo = bin_lo[b], hi = max((int64_t)bin_lo[b + 1], lo);
     const unsigned long long lt = lanemask_lt();
     __syncthreads();
     constexpr int kAhead = 4;  // rounds of 256 reads whose loads are issued together
     for (int64_t base0 = lo; base0 < hi; base0 += kAhead * kBlock) {
-        int cc[kAhead], ss[kAhead], tt[kAhead];
-        uint16_t ff[kAhead];
-        uint8_t mm[kAhead];
+        // 32-bit registers for the narrow fields: packing them would force a wait on
+        // each load before the next round's loads are issued
+        int cc[kAhead], ss[kAhead], tt[kAhead], ff[kAhead], mm[kAhead];
         uint64_t oo[kAhead];
 #pragma unroll
         for (int u = 0; u < kAhead; ++u) {
@@ -363,7 +372,7 @@ __global__ void __launch_bounds__(kBlock) k_scatter(int64_t n, const int32_t* __
             const int64_t i = base0 + u * kBlock + threadIdx.x;
             if (base0 + u * kBlock >= hi) break;  // uniform
             const int c = cc[u];
-            const uint16_t f = ff[u];
+            const uint16_t f = (uint16_t)ff[u];
             const bool valid = i < hi && read_valid(c, f, nc);
             unsigned long long peers = __ballot(valid);
             for (int bit = 0; bit < cbits && peers; ++bit) {
@@ -377,7 +386,16 @@ __global__ void __launch_bounds__(kBlock) k_scatter(int64_t n, const int32_t* __
                 if (wid == w && valid) {
                     const uint32_t before = cnt[c];
                     dest = before + (uint32_t)__popcll(peers & lt);
-                    if ((peers & lt) == 0ull) cnt[c] = before + (uint32_t)__popcll(peers);  // group leader
+                    if ((peers & lt) == 0ull) {  // group leader
+                        cnt[c] = before + (uint32_t)__popcll(peers);
+                        if (kLds) {
+                            const uint32_t m = 1u << (c & 31);
+                            if (fbits[c >> 5] & m) {
+                                atomicAnd(&fbits[c >> 5], ~m);
+                                first_read[c] = (uint32_t)i;
+                            }
+                        }
+                    }
                 }
                 if (!kLds) __threadfence_block();
                 __syncthreads();
@@ -391,7 +409,7 @@ __global__ void __launch_bounds__(kBlock) k_scatter(int64_t n, const int32_t* __
                 e.tlen = t < 0 ? (uint32_t)(-(int64_t)t) : (uint32_t)t;
                 gel[dest] = e;
                 // the cell's first element in cell-major order is its first valid read in BAM order
-                if (dest == O[c]) first_read[c] = (uint32_t)i;  // row 0 of the scan = cell base
+                if (!kLds && dest == O[c]) first_read[c] = (uint32_t)i;  // row 0 of the scan = cell base
             }
         }
     }
@@ -1378,8 +1396,9 @@ int mgp_run(mgp_ctx* ctx) {
         STAGE_BEGIN(ST_SCATTER);
         if (n > 0) {
             const unsigned sgrid = MGP_XCD_REMAP ? (unsigned)(((g.nbins + 7) / 8) * 8) : (unsigned)g.nbins;
-            if (lds) {
-                k_scatter<true><<<sgrid, kBlock, (size_t)nc * 4, s>>>(
+            const size_t sc_lds = (size_t)nc * 4 + (size_t)((nc + 31) / 32) * 4;
+            if (sc_lds <= (size_t)ctx->lds_hist_max_cells * 4) {
+                k_scatter<true><<<sgrid, kBlock, sc_lds, s>>>(
                     n, ctx->start.as<int32_t>(), ctx->bc.as<int32_t>(), ctx->tlen.as<int32_t>(),
                     ctx->flag.as<uint16_t>(), ctx->mapq.as<uint8_t>(), ctx->roff.as<uint64_t>(),
                     ctx->bin_start.as<uint32_t>(), ctx->H.as<uint32_t>(), nullptr, g, cbits, ctx->cfg.min_mapq,
