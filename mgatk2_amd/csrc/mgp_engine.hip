@@ -1117,7 +1117,12 @@ static int configure_geometry(mgp_ctx* ctx) {
     g.W = ((g.W + g.G - 1) / g.G) * g.G;   // multiple of the bin width
     g.nwin = (g.L + g.W - 1) / g.W;
     if (g.W > kMaxPosPerThread * kBlock) return set_err(MGP_E_INVALID, "window too wide");
-    g.Wp = g.W | 1;                        // odd plane pitch
+#ifndef MGP_WP_ALIGN
+#define MGP_WP_ALIGN 0
+#endif
+    // plane pitch: with a multiple of 32 the 4 base planes share the bank map
+    // (bank = position mod 32), so lanes at distinct positions never conflict
+    g.Wp = MGP_WP_ALIGN ? (g.W + MGP_WP_ALIGN - 1) / MGP_WP_ALIGN * MGP_WP_ALIGN : (g.W | 1);
     g.nc = c.n_cells;
     // cells per pileup workgroup: ~4096 workgroups over the windows
     int64_t target = 4096;
