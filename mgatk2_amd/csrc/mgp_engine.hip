@@ -347,71 +347,101 @@ __global__ void __launch_bounds__(kBlock) k_scatter(int64_t n, const int32_t* __
     const int64_t lo = bin_lo[b], hi = max((int64_t)bin_lo[b + 1], lo);
     const unsigned long long lt = lanemask_lt();
     __syncthreads();
-    constexpr int kAhead = 4;  // rounds of 256 reads whose loads are issued together
-    for (int64_t base0 = lo; base0 < hi; base0 += kAhead * kBlock) {
-        // 32-bit registers for the narrow fields: packing them would force a wait on
-        // each load before the next round's loads are issued
-        int cc[kAhead], ss[kAhead], tt[kAhead], ff[kAhead], mm[kAhead];
-        uint64_t oo[kAhead];
+    // Each wave owns a contiguous run of kAhead*64 reads per step (BAM order =
+    // wave order, then round order), so the waves claim slots in wave order with
+    // one barrier per wave per step. Loads of the next step are issued before the
+    // current step is processed (two register sets).
+    constexpr int kAhead = 4;
+    constexpr int kStep = kAhead * kBlock;
+    const int lane = threadIdx.x & 63;
+    struct Pre {
+        int c[kAhead], s[kAhead], t[kAhead], f[kAhead], m[kAhead];
+        uint64_t o[kAhead];
+    };
+    // loads are issued unconditionally (index clamped into the bin) so that every
+    // path has the same number in flight and the waits stay counted, not drained
+    auto load = [&](Pre& P, int64_t base0) {
 #pragma unroll
         for (int u = 0; u < kAhead; ++u) {
-            const int64_t i = base0 + u * kBlock + threadIdx.x;
-            cc[u] = -1;
-            ff[u] = 0;
-            if (i < hi) {
-                cc[u] = bc[i];
-                ff[u] = flag[i];
-                ss[u] = start[i];
-                tt[u] = tlen[i];
-                mm[u] = mapq[i];
-                oo[u] = roff[i];
-            }
+            const int64_t i = base0 + wid * (kAhead * kWave) + u * kWave + lane;
+            const int64_t j = i < hi ? i : hi - 1;
+            P.c[u] = bc[j];
+            P.f[u] = flag[j];
+            P.s[u] = start[j];
+            P.t[u] = tlen[j];
+            P.m[u] = mapq[j];
+            P.o[u] = roff[j];
         }
+    };
+    auto process = [&](const Pre& P, int64_t base0) {
+        unsigned long long peers[kAhead];
+        bool valid[kAhead];
 #pragma unroll
         for (int u = 0; u < kAhead; ++u) {
-            const int64_t i = base0 + u * kBlock + threadIdx.x;
-            if (base0 + u * kBlock >= hi) break;  // uniform
-            const int c = cc[u];
-            const uint16_t f = (uint16_t)ff[u];
-            const bool valid = i < hi && read_valid(c, f, nc);
-            unsigned long long peers = __ballot(valid);
-            for (int bit = 0; bit < cbits && peers; ++bit) {
-                const bool x = valid && ((c >> bit) & 1);
+            const int64_t i = base0 + wid * (kAhead * kWave) + u * kWave + lane;
+            const int c = P.c[u];
+            valid[u] = i < hi && read_valid(c, (uint16_t)P.f[u], nc);
+            unsigned long long pm = __ballot(valid[u]);
+            for (int bit = 0; bit < cbits && pm; ++bit) {
+                const bool x = valid[u] && ((c >> bit) & 1);
                 const unsigned long long m = __ballot(x);
-                peers &= x ? m : ~m;
+                pm &= x ? m : ~m;
             }
-            uint32_t dest = 0;
+            peers[u] = pm;
+        }
+        uint32_t dest[kAhead];
 #pragma unroll
-            for (int w = 0; w < kBlock / kWave; ++w) {
-                if (wid == w && valid) {
-                    const uint32_t before = cnt[c];
-                    dest = before + (uint32_t)__popcll(peers & lt);
-                    if ((peers & lt) == 0ull) {  // group leader
-                        cnt[c] = before + (uint32_t)__popcll(peers);
-                        if (kLds) {
-                            const uint32_t m = 1u << (c & 31);
-                            if (fbits[c >> 5] & m) {
-                                atomicAnd(&fbits[c >> 5], ~m);
-                                first_read[c] = (uint32_t)i;
+        for (int w = 0; w < kBlock / kWave; ++w) {
+            if (wid == w) {
+#pragma unroll
+                for (int u = 0; u < kAhead; ++u) {
+                    dest[u] = 0;
+                    if (valid[u]) {
+                        const int c = P.c[u];
+                        const uint32_t before = cnt[c];
+                        dest[u] = before + (uint32_t)__popcll(peers[u] & lt);
+                        if ((peers[u] & lt) == 0ull) {  // group leader
+                            cnt[c] = before + (uint32_t)__popcll(peers[u]);
+                            if (kLds) {
+                                const uint32_t m = 1u << (c & 31);
+                                if (fbits[c >> 5] & m) {
+                                    atomicAnd(&fbits[c >> 5], ~m);
+                                    first_read[c] =
+                                        (uint32_t)(base0 + wid * (kAhead * kWave) + u * kWave + lane);
+                                }
                             }
                         }
                     }
+                    if (!kLds) __threadfence_block();
                 }
-                if (!kLds) __threadfence_block();
-                __syncthreads();
             }
-            if (valid) {
-                const int t = tt[u];
-                GElem e;
-                e.w = oo[u] | (f & MGP_FLAG_REVERSE ? GM_REV : 0ull) | (f & MGP_FLAG_PAIRED ? GM_PAIRED : 0ull) |
-                      ((int)mm[u] >= min_mapq ? GM_MAPQ_OK : 0ull) | (f & MGP_FLAG_NOSEQQUAL ? GM_BAD : 0ull);
-                e.start = ss[u];
-                e.tlen = t < 0 ? (uint32_t)(-(int64_t)t) : (uint32_t)t;
-                gel[dest] = e;
-                // the cell's first element in cell-major order is its first valid read in BAM order
-                if (!kLds && dest == O[c]) first_read[c] = (uint32_t)i;  // row 0 of the scan = cell base
-            }
+            __syncthreads();
         }
+#pragma unroll
+        for (int u = 0; u < kAhead; ++u) {
+            if (!valid[u]) continue;
+            const int c = P.c[u];
+            const uint16_t f = (uint16_t)P.f[u];
+            const int t = P.t[u];
+            GElem e;
+            e.w = P.o[u] | (f & MGP_FLAG_REVERSE ? GM_REV : 0ull) | (f & MGP_FLAG_PAIRED ? GM_PAIRED : 0ull) |
+                  (P.m[u] >= min_mapq ? GM_MAPQ_OK : 0ull) | (f & MGP_FLAG_NOSEQQUAL ? GM_BAD : 0ull);
+            e.start = P.s[u];
+            e.tlen = t < 0 ? (uint32_t)(-(int64_t)t) : (uint32_t)t;
+            gel[dest[u]] = e;
+            // the cell's first element in cell-major order is its first valid read in BAM order
+            if (!kLds && dest[u] == O[c])
+                first_read[c] = (uint32_t)(base0 + wid * (kAhead * kWave) + u * kWave + lane);
+        }
+    };
+    if (lo >= hi) return;
+    Pre A, B;
+    load(A, lo);
+    for (int64_t base0 = lo; base0 < hi; base0 += 2 * kStep) {
+        load(B, base0 + kStep);
+        process(A, base0);
+        load(A, base0 + 2 * kStep);
+        if (base0 + kStep < hi) process(B, base0 + kStep);
     }
 }
 
