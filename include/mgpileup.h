@@ -46,7 +46,7 @@
 extern "C" {
 #endif
 
-#define MGP_ABI_VERSION 1
+#define MGP_ABI_VERSION 2  /* 2: fixed seq/CIGAR offsets for reads <= 64 bases */
 
 /* ---- return codes (0 = success) ------------------------------------------ */
 #define MGP_OK               0
@@ -106,17 +106,33 @@ typedef struct mgp_config {
  *   uint32 l_seq      len(query_sequence), soft clips included
  *   uint16 n_cigar
  *   uint16 flag       same word as flag[i]
- *   uint32 cigar_off  byte offset of cigar[] from the record start
- *                     = round_up(16 + l_seq + (l_seq + 1) / 2, 4)
+ *   uint32 cigar_off  byte offset of cigar[] from the record start (= mgp_cigar_offset(l_seq))
  *   uint8  qual[l_seq]              raw Phred bytes (as BAM stores them), at +16
- *   uint8  seq[(l_seq + 1) / 2]     BAM 4-bit codes, high nibble first
+ *   uint8  seq[(l_seq + 1) / 2]     BAM 4-bit codes, high nibble first, at +mgp_seq_offset(l_seq)
  *   uint32 cigar[n_cigar]           BAM encoding (len << 4 | op), at +cigar_off
- * Record size = round_up(cigar_off + 4 * n_cigar, 16); 96 bytes for a 50M read.
- * Qual sits at a fixed, 16-byte aligned offset so a kernel can load it with
- * vector loads and index its bytes statically. Records are gathered in random
- * order, so producers should place them at 128-byte aligned offsets (one L2
- * line per record of <= 128 bytes); any 16-byte aligned placement is accepted.
+ * qual gets at least 64 bytes and seq at least 32, so for reads of <= 64 bases
+ * every field has a fixed place: qual +16, seq +80, cigar +112, and a record
+ * with <= 4 CIGAR operations is exactly one 128-byte line that a kernel loads
+ * with 8 independent 16-byte loads and indexes statically. Record size =
+ * round_up(cigar_off + 4 * n_cigar, 16). Records are gathered in random order,
+ * so producers should place them at 128-byte aligned offsets; any 16-byte
+ * aligned placement is accepted. Kernels may read up to 128 bytes from a
+ * record start: keep >= 128 bytes after the last record (mgp_push_batch pads).
  */
+#if defined(__HIPCC__)
+#define MGP_HD __host__ __device__
+#else
+#define MGP_HD
+#endif
+static inline MGP_HD uint32_t mgp_seq_offset(uint32_t l_seq) {
+    const uint32_t q = (l_seq + 3u) & ~3u;
+    return 16u + (q > 64u ? q : 64u);
+}
+static inline MGP_HD uint32_t mgp_cigar_offset(uint32_t l_seq) {
+    const uint32_t b = ((l_seq + 1u) / 2u + 3u) & ~3u;
+    return mgp_seq_offset(l_seq) + (b > 32u ? b : 32u);
+}
+
 typedef struct mgp_batch {
     int64_t         n_reads;
     const int32_t  *start;      /* reference_start                                  */

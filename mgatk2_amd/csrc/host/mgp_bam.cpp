@@ -610,7 +610,8 @@ int mgp_bam_read_ref(mgp_bam* b, int tid, int rec_align, mgp_bam_batch* out) {
         }
         // payload record (include/mgpileup.h)
         const uint64_t off = (o.payload.size() + amask) & ~amask;
-        const uint32_t coff = (uint32_t)((16 + (uint64_t)l_seq + (l_seq + 1) / 2 + 3) & ~3ull);
+        const uint32_t soff = mgp_seq_offset(l_seq);
+        const uint32_t coff = mgp_cigar_offset(l_seq);
         const uint64_t size = ((uint64_t)coff + 4ull * n_cig + amask) & ~amask;
         o.payload.resize(off + size, 0);
         uint8_t* rec = o.payload.data() + off;
@@ -622,7 +623,7 @@ int mgp_bam_read_ref(mgp_bam* b, int tid, int rec_align, mgp_bam_batch* out) {
         std::memcpy(rec + 12, &coff, 4);
         if (l_seq) {
             std::memcpy(rec + 16, qualp, l_seq);
-            std::memcpy(rec + 16 + l_seq, seqp, ((size_t)l_seq + 1) / 2);
+            std::memcpy(rec + soff, seqp, ((size_t)l_seq + 1) / 2);
         }
         if (n_cig) std::memcpy(rec + coff, cig, 4 * (size_t)n_cig);
         o.start.push_back(pos);

@@ -478,7 +478,7 @@ __device__ void pile_slow(const uint8_t* __restrict__ rec, int32_t start, uint32
                           uint32_t max_span, bool& span_err) {
     const uint32_t* cig = reinterpret_cast<const uint32_t*>(rec + coff);
     const uint8_t* qual = rec + 16;
-    const uint8_t* seq = qual + lseq;
+    const uint8_t* seq = rec + mgp_seq_offset(lseq);
     const int64_t wend = (int64_t)w.w0 + w.wlen;
     const int64_t vq0 = pc.min_dist > 0 ? pc.min_dist : 0;
     const int64_t vq1 = pc.min_dist > 0 ? (int64_t)lseq - pc.min_dist : (int64_t)lseq;
@@ -532,23 +532,32 @@ __device__ __forceinline__ void pile_read(bool has, const uint8_t* __restrict__ 
                                           const PileCfg& pc, uint32_t* tile, uint32_t* t5, uint32_t max_span,
                                           bool& span_err) {
     if (MGP_ABL == 1) return;
+    // the whole first 128-byte line of the record in one go: header, qual (+16),
+    // seq (+80) and CIGAR (+112) of a read of <= 64 bases with <= 4 operations
+    // (include/mgpileup.h); no load depends on another
     uint4 h = make_uint4(0, 0, 0, 0);
-    uint4 qv[4];
+    uint4 qv[4], sv[2], cv = make_uint4(0, 0, 0, 0);
     if (MGP_ABL == 3) {
         // synthetic read from the record address only: no payload loads
         const uint32_t x = (uint32_t)(reinterpret_cast<uintptr_t>(rec) >> 4);
-        h = make_uint4((uint32_t)w.w0 + (x * 7u) % (uint32_t)w.wlen, 50u, 1u | (x & 1u ? (MGP_FLAG_REVERSE << 16) : 0u), 92u);
+        h = make_uint4((uint32_t)w.w0 + (x * 7u) % (uint32_t)w.wlen, 50u, 1u | (x & 1u ? (MGP_FLAG_REVERSE << 16) : 0u), 112u);
 #pragma unroll
         for (int k = 0; k < 4; ++k) qv[k] = make_uint4(0x25252525u, 0x25252525u, 0x25252525u, 0x25252525u);
-        has = has && true;
+#pragma unroll
+        for (int k = 0; k < 2; ++k) sv[k] = make_uint4(0x12481248u, 0x24812481u, 0x48124812u, 0x81248124u);
+        cv.x = 50u << 4;
     } else if (has) {
         const uint4* r4 = reinterpret_cast<const uint4*>(rec);
         h = r4[0];
 #pragma unroll
         for (int k = 0; k < 4; ++k) qv[k] = r4[1 + k];
+        sv[0] = r4[5];
+        sv[1] = r4[6];
+        cv = r4[7];
     } else {
 #pragma unroll
         for (int k = 0; k < 4; ++k) qv[k] = make_uint4(0, 0, 0, 0);
+        sv[0] = sv[1] = make_uint4(0, 0, 0, 0);
     }
     const int32_t start = (int32_t)h.x;
     const uint32_t lseq = h.y;
@@ -562,13 +571,14 @@ __device__ __forceinline__ void pile_read(bool has, const uint8_t* __restrict__ 
     int qs1 = 1 << 30, dl0 = 0, dl1 = 0;
     int a0 = 0, b0 = 0, a1 = 0, b1 = 0;
     if (fast) {
-        const uint32_t fake_cig = (50u << 4);
-        const uint32_t* cig = MGP_ABL == 3 ? &fake_cig : reinterpret_cast<const uint32_t*>(rec + coff);
+        const uint32_t cigw[4] = {cv.x, cv.y, cv.z, cv.w};
         int qs[2] = {0, 1 << 30}, qe[2] = {0, 1 << 30}, dl[2] = {0, 0};
         int nb = 0;
         int ref = start, q = 0;
-        for (uint32_t o = 0; o < ncig; ++o) {
-            const uint32_t cg = cig[o];
+#pragma unroll
+        for (int o = 0; o < kFastCig; ++o) {
+            if ((uint32_t)o >= ncig) break;
+            const uint32_t cg = cigw[o];
             const uint32_t op = cg & 15u;
             const int len = (int)min(cg >> 4, (uint32_t)(1 << 26));
             if (op == 0 || op == 7 || op == 8) {
@@ -627,27 +637,7 @@ __device__ __forceinline__ void pile_read(bool has, const uint8_t* __restrict__ 
             qw[4 * k + 2] = qv[k].z;
             qw[4 * k + 3] = qv[k].w;
         }
-        // seq: 4-byte aligned dword loads, realigned with a funnel shift
-        uint32_t sw[kFastLen / 8];
-        {
-            uint32_t raw[kFastLen / 8 + 1];
-            const uintptr_t sa = reinterpret_cast<uintptr_t>(rec) + 16 + lseq;
-            const uint32_t sh = (uint32_t)(sa & 3) * 8u;
-            if (fast && MGP_ABL != 3) {
-                const uint32_t* sp = reinterpret_cast<const uint32_t*>(sa & ~uintptr_t(3));
-#pragma unroll
-                for (int k = 0; k < kFastLen / 8 + 1; ++k) raw[k] = sp[k];
-            } else if (fast) {
-#pragma unroll
-                for (int k = 0; k < kFastLen / 8 + 1; ++k) raw[k] = 0x12481248u * (uint32_t)(k + 1);
-            } else {
-#pragma unroll
-                for (int k = 0; k < kFastLen / 8 + 1; ++k) raw[k] = 0;
-            }
-#pragma unroll
-            for (int k = 0; k < kFastLen / 8; ++k)
-                sw[k] = (uint32_t)((((unsigned long long)raw[k + 1] << 32) | raw[k]) >> sh);
-        }
+        const uint32_t sw[kFastLen / 8] = {sv[0].x, sv[0].y, sv[0].z, sv[0].w, sv[1].x, sv[1].y, sv[1].z, sv[1].w};
         uint32_t* base = tile - w.w0;
         const uint32_t Wp = (uint32_t)w.Wp;
         const uint32_t inc = strand_inc(strand);
@@ -1672,7 +1662,7 @@ int mgp_synth_generate(mgp_ctx* ctx, const mgp_synth_params* p) {
     const int L = ctx->cfg.mito_len;
     const int nc = p->n_cells;
     // record size is at most 16 + 4*3 + len + (len+1)/2 rounded to 8
-    const int64_t max_rec = ((16 + 16 + p->read_len + (p->read_len + 1) / 2) + align - 1) & ~(int64_t)(align - 1);
+    const int64_t max_rec = ((int64_t)mgp_cigar_offset((uint32_t)p->read_len) + 16 + align - 1) & ~(int64_t)(align - 1);
     MGP_TRY(ensure_inputs(ctx, std::max<int64_t>(n, 1), n * max_rec, false));
     DevBuf cdf, ref;
     MGP_TRY(cdf.ensure((size_t)std::max(nc, 1) * 4));

@@ -73,7 +73,7 @@ __device__ __forceinline__ Cig cig_of(uint64_t seed, int64_t i) {
     return c;
 }
 
-__device__ __forceinline__ int cigar_offset(int rl) { return (16 + rl + (rl + 1) / 2 + 3) & ~3; }
+__device__ __forceinline__ int cigar_offset(int rl) { return (int)mgp_cigar_offset((uint32_t)rl); }
 
 __device__ __forceinline__ uint64_t rec_size(int ncig, int rl, int align) {
     return (uint64_t)((cigar_offset(rl) + 4 * ncig + align - 1) & ~(align - 1));
@@ -239,7 +239,7 @@ __global__ void k_synth_fill(uint64_t seed, int64_t n, int rl, int nc, int L, co
         cig[2] = ((uint32_t)(rl - cg.a) << 4) | 0;
     }
     uint8_t* qual = rec + 16;
-    uint8_t* seq = qual + rl;
+    uint8_t* seq = rec + mgp_seq_offset((uint32_t)rl);
     const uint8_t kCodes[4] = {1, 2, 4, 8};
     uint8_t hi_nib = 0;
     for (int q = 0; q < rl; ++q) {

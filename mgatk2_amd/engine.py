@@ -163,7 +163,7 @@ def load_library(path: Path | None = None) -> C.CDLL:
         fn = getattr(lib, name)
         fn.argtypes = args
         fn.restype = res
-    if lib.mgp_abi_version() != 1:
+    if lib.mgp_abi_version() != 2:
         raise ProcessingError("libmgpileup ABI version mismatch")
     if path is None:
         _lib = lib

@@ -199,10 +199,19 @@ def concat_soa(parts: list[ReadSoA]) -> ReadSoA:
     )
 
 
-def cigar_offset(lseq):
-    """Byte offset of the CIGAR inside a record (include/mgpileup.h)."""
+def seq_offset(lseq):
+    """Byte offset of the packed sequence inside a record (include/mgpileup.h):
+    qual[] at +16 gets at least 64 bytes, so reads of <= 64 bases have seq at +80."""
     lseq = np.asarray(lseq, np.int64)
-    return (16 + lseq + (lseq + 1) // 2 + 3) & ~3
+    return 16 + np.maximum(64, (lseq + 3) & ~3)
+
+
+def cigar_offset(lseq):
+    """Byte offset of the CIGAR inside a record (include/mgpileup.h): seq[] gets at
+    least 32 bytes, so reads of <= 64 bases have their CIGAR at +112 and a record
+    with <= 4 CIGAR operations is exactly one 128-byte line."""
+    lseq = np.asarray(lseq, np.int64)
+    return seq_offset(lseq) + np.maximum(32, ((lseq + 1) // 2 + 3) & ~3)
 
 
 REC_ALIGN = 128  # records are gathered at random: one L2 line per record of <= 128 bytes
@@ -344,7 +353,7 @@ def _pack_fixed(start, flag, ncig, cig, qual, code, rl, align=REC_ALIGN):
     if rl & 1:
         c = np.concatenate([c, np.zeros((m, 1), np.uint8)], axis=1)
     packed = ((c[:, 0::2] << 4) | c[:, 1::2]).astype(np.uint8)
-    pay[(ro + 16 + rl)[:, None] + np.arange(nb)[None, :]] = packed
+    pay[(ro + int(seq_offset(rl)))[:, None] + np.arange(nb)[None, :]] = packed
     cb = cig.astype("<u4").view(np.uint8).reshape(m, -1)
     for k in range(cig.shape[1]):
         sel = ncig > k
@@ -448,7 +457,8 @@ def pack_reads(reads: list[dict], rec_align: int = REC_ALIGN) -> ReadSoA:
             if lseq & 1:
                 codes.append(0)
             codes = np.array(codes, np.uint8)
-            rec[16 + lseq : 16 + lseq + (lseq + 1) // 2] = (codes[0::2] << 4) | codes[1::2]
+            so = int(seq_offset(lseq))
+            rec[so : so + (lseq + 1) // 2] = (codes[0::2] << 4) | codes[1::2]
         if cig:
             rec[coff : coff + 4 * len(cig)] = np.array([(ln << 4) | op for op, ln in cig], "<u4").view(np.uint8)
         chunks.append(rec)
@@ -467,7 +477,8 @@ def unpack_record(payload: np.ndarray, off: int) -> dict:
     coff = int(hdr[12:16].view("<u4")[0])
     cig = payload[off + coff : off + coff + 4 * ncig].view("<u4").tolist() if ncig else []
     qual = payload[off + 16 : off + 16 + lseq].tolist()
-    sb = payload[off + 16 + lseq : off + 16 + lseq + (lseq + 1) // 2]
+    so = off + int(seq_offset(lseq))
+    sb = payload[so : so + (lseq + 1) // 2]
     codes = np.stack([sb >> 4, sb & 15], axis=1).reshape(-1)[:lseq]
     seq = "".join(SEQ_NT16[c] for c in codes.tolist())
     return dict(

@@ -117,7 +117,7 @@ static void pile_read(const uint8_t *rec, const mgp_config *cfg, uint32_t *bc8, 
     memcpy(&flag, rec + 10, 2);
     memcpy(&coff, rec + 12, 4);
     const uint8_t *qual = rec + 16;
-    const uint8_t *seq = qual + lseq;
+    const uint8_t *seq = rec + mgp_seq_offset(lseq);
     const uint8_t *cig = rec + coff;
     const int64_t L = cfg->mito_len;
     const int is_reverse = (flag & MGP_FLAG_REVERSE) != 0;

@@ -9,9 +9,43 @@ import numpy as np
 ROOT = Path(__file__).resolve().parent.parent
 
 
-def header_symbols():
-    text = (ROOT / "include" / "mgpileup.h").read_text()
+def header_symbols(name: str = "mgpileup.h"):
+    """Functions the header declares for export (static inline helpers excluded)."""
+    text = (ROOT / "include" / name).read_text()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    text = re.sub(r"static inline[^{]*\{[^}]*\}", "", text)
     return sorted(set(re.findall(r"\b(mgp_[a-z_0-9]+)\s*\(", text)))
+
+
+def test_host_library_exports_header_symbols():
+    from mgatk2_amd.bam import host_library
+
+    lib = host_library()
+    syms = header_symbols("mgpileup_host.h")
+    assert len(syms) >= 14
+    for s in syms:
+        assert hasattr(lib, s), f"libmgphost.so does not export {s}"
+
+
+def test_record_layout_helpers():
+    """mgp_seq_offset / mgp_cigar_offset (include/mgpileup.h) == the Python packer's."""
+    import subprocess
+
+    from mgatk2_amd.synth import cigar_offset, seq_offset
+
+    src = ROOT / "tests" / "_layout.c"
+    src.write_text('#include <stdio.h>\n#include "mgpileup.h"\nint main(void){for(unsigned l=0;l<300;++l)'
+                   'printf("%u %u\\n",mgp_seq_offset(l),mgp_cigar_offset(l));return 0;}\n')
+    try:
+        exe = Path("/tmp") / "mgp_layout_check"
+        subprocess.run(["gcc", "-std=c11", f"-I{ROOT / 'include'}", str(src), "-o", str(exe)], check=True)
+        out = subprocess.run([str(exe)], check=True, capture_output=True, text=True).stdout.split("\n")
+    finally:
+        src.unlink()
+    for lseq, line in enumerate(out[:300]):
+        so, co = map(int, line.split())
+        assert so == int(seq_offset(lseq)) and co == int(cigar_offset(lseq)), lseq
+    assert int(seq_offset(50)) == 80 and int(cigar_offset(64)) == 112 and int(cigar_offset(65)) > 112
 
 
 def test_library_exports_header_symbols():
@@ -25,7 +59,7 @@ def test_library_exports_header_symbols():
     for s in syms:
         assert hasattr(lib, s), f"libmgpileup.so does not export {s}"
     assert set(syms) == set(engine.ABI_SYMBOLS)
-    assert lib.mgp_abi_version() == 1
+    assert lib.mgp_abi_version() == 2
 
 
 def test_no_device_fails_loudly():
