@@ -94,7 +94,7 @@ def main():
                        dedup_mode="alignment_and_fragment_length", max_strand_bias=1.0, min_reads=1)
     eng = Engine(cfg, device=local_rank)
     t0 = time.time()
-    cdf, ref = cell_cdf(seed, n_cells), ref_codes(seed)
+    cdf, ref = cell_cdf(seed, n_cells), ref_codes(args.seed)  # one chrM reference for every rank
     eng.synth(seed, n_reads, cdf, ref, read_len=args.read_len)
     n_res, pay = eng.resident()
     t_gen = time.time() - t0
