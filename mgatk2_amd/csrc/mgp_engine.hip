@@ -389,33 +389,40 @@ __global__ void __launch_bounds__(kBlock) k_scatter(int64_t n, const int32_t* __
             }
             peers[u] = pm;
         }
-        uint32_t dest[kAhead];
+        // claims, in wave order: each group leader adds its group size to the cell's
+        // counter (LDS atomics return the old value; one wave's atomics execute in
+        // order, so its rounds chain without waiting in between) and, on the cell's
+        // first bin, takes the first-read bit; members read their base from the
+        // leader after the barrier, outside the serialised part
+        uint32_t bef[kAhead];
+        bool firstg[kAhead];
 #pragma unroll
         for (int w = 0; w < kBlock / kWave; ++w) {
             if (wid == w) {
 #pragma unroll
                 for (int u = 0; u < kAhead; ++u) {
-                    dest[u] = 0;
-                    if (valid[u]) {
+                    bef[u] = 0;
+                    firstg[u] = false;
+                    if (valid[u] && (peers[u] & lt) == 0ull) {
                         const int c = P.c[u];
-                        const uint32_t before = cnt[c];
-                        dest[u] = before + (uint32_t)__popcll(peers[u] & lt);
-                        if ((peers[u] & lt) == 0ull) {  // group leader
-                            cnt[c] = before + (uint32_t)__popcll(peers[u]);
-                            if (kLds) {
-                                const uint32_t m = 1u << (c & 31);
-                                if (fbits[c >> 5] & m) {
-                                    atomicAnd(&fbits[c >> 5], ~m);
-                                    first_read[c] =
-                                        (uint32_t)(base0 + wid * (kAhead * kWave) + u * kWave + lane);
-                                }
-                            }
+                        bef[u] = atomicAdd(&cnt[c], (uint32_t)__popcll(peers[u]));
+                        if (kLds) {
+                            const uint32_t m = 1u << (c & 31);
+                            firstg[u] = (atomicAnd(&fbits[c >> 5], ~m) & m) != 0u;
                         }
                     }
                     if (!kLds) __threadfence_block();
                 }
             }
             __syncthreads();
+        }
+        uint32_t dest[kAhead];
+#pragma unroll
+        for (int u = 0; u < kAhead; ++u) {
+            const int leader = peers[u] ? __builtin_ctzll(peers[u]) : lane;
+            dest[u] = (uint32_t)__shfl((int)bef[u], leader, kWave) + (uint32_t)__popcll(peers[u] & lt);
+            if (kLds && firstg[u])
+                first_read[P.c[u]] = (uint32_t)(base0 + wid * (kAhead * kWave) + u * kWave + lane);
         }
 #pragma unroll
         for (int u = 0; u < kAhead; ++u) {
