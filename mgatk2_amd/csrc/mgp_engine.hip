@@ -296,6 +296,9 @@ __global__ void k_scan_apply(uint32_t* __restrict__ H, const uint32_t* __restric
 
 // Grouping element (16 bytes, cell-major, BAM order inside a cell):
 //   w = record byte offset | meta << 56, start, |tlen|
+#ifndef MGP_SC_ABL
+#define MGP_SC_ABL 0  // scatter ablations for experiments: 0 = real kernel
+#endif
 struct __align__(16) GElem {
     unsigned long long w;
     int32_t start;
@@ -382,7 +385,8 @@ __global__ void __launch_bounds__(kBlock) k_scatter(int64_t n, const int32_t* __
             const int c = P.c[u];
             valid[u] = i < hi && read_valid(c, (uint16_t)P.f[u], nc);
             unsigned long long pm = __ballot(valid[u]);
-            for (int bit = 0; bit < cbits && pm; ++bit) {
+            if (MGP_SC_ABL == 3) pm = valid[u] ? (1ull << lane) : 0ull;
+            for (int bit = 0; bit < cbits && pm && MGP_SC_ABL != 3; ++bit) {
                 const bool x = valid[u] && ((c >> bit) & 1);
                 const unsigned long long m = __ballot(x);
                 pm &= x ? m : ~m;
@@ -414,7 +418,7 @@ __global__ void __launch_bounds__(kBlock) k_scatter(int64_t n, const int32_t* __
                     if (!kLds) __threadfence_block();
                 }
             }
-            __syncthreads();
+            if (MGP_SC_ABL != 2) __syncthreads();
         }
         uint32_t dest[kAhead];
 #pragma unroll
@@ -426,7 +430,7 @@ __global__ void __launch_bounds__(kBlock) k_scatter(int64_t n, const int32_t* __
         }
 #pragma unroll
         for (int u = 0; u < kAhead; ++u) {
-            if (!valid[u]) continue;
+            if (!valid[u] && MGP_SC_ABL != 1) continue;  // ablation 1 writes every slot (no holes)
             const int c = P.c[u];
             const uint16_t f = (uint16_t)P.f[u];
             const int t = P.t[u];
@@ -435,7 +439,10 @@ __global__ void __launch_bounds__(kBlock) k_scatter(int64_t n, const int32_t* __
                   (P.m[u] >= min_mapq ? GM_MAPQ_OK : 0ull) | (f & MGP_FLAG_NOSEQQUAL ? GM_BAD : 0ull);
             e.start = P.s[u];
             e.tlen = t < 0 ? (uint32_t)(-(int64_t)t) : (uint32_t)t;
-            gel[dest[u]] = e;
+            if (MGP_SC_ABL == 1)
+                gel[min((uint64_t)(base0 + wid * (kAhead * kWave) + u * kWave + lane), (uint64_t)n - 1)] = e;
+            else
+                gel[dest[u]] = e;
             // the cell's first element in cell-major order is its first valid read in BAM order
             if (!kLds && dest[u] == O[c])
                 first_read[c] = (uint32_t)(base0 + wid * (kAhead * kWave) + u * kWave + lane);

