@@ -8,7 +8,9 @@
 //                   filters (readers.py:95-111) and the per-cell read histogram
 //   k_scan_*        exclusive scan of the histogram in (cell, start-bin) order: the
 //                   cell-major layout of `reads_by_barcode` (readers.py:69,164)
-//   k_scatter       per start bin: one 16-byte grouping element per valid read at
+//   k_group_a/b     two-pass stable grouping: per start bin into (bin, 64-cell group)
+//                   buckets, then per cell group into cell-major order; one 16-byte
+//                   grouping element per valid read at
 //                   its cell-major slot, BAM order kept inside each cell (stable)
 //   k_pileup        per (cell chunk, position window): duplicate marking by a short
 //                   walk back over equal starts (readers.py:118-150, first in BAM
@@ -119,7 +121,7 @@ struct mgp_ctx {
     DevBuf start, bc, tlen, flag, mapq, span, roff, payload;
 
     // run scratch
-    DevBuf bin_start, H, Hcur, P, cell_cnt, cell_base;
+    DevBuf bin_start, H, P, cell_cnt, cell_base, bin_valid, bin_base, bucket_off, gel2;
     DevBuf gel, tally_part, tally;
     DevBuf n_reads, any_paired, passed, covered, dsum, dmax, med_lo, med_hi, first_read;
     DevBuf counts, tn5, depth, stats;
@@ -169,9 +171,10 @@ __global__ void __launch_bounds__(kBlock) k_bin_count(const int32_t* __restrict_
                                                       const uint16_t* __restrict__ flag,
                                                       const uint32_t* __restrict__ span, int64_t n, Geom g,
                                                       uint32_t* __restrict__ H, uint32_t* __restrict__ bin_lo,
-                                                      DevStats* st) {
+                                                      uint32_t* __restrict__ bin_valid, DevStats* st) {
     extern __shared__ uint32_t hist[];
     __shared__ int64_t s_range[2];
+    __shared__ uint32_t s_nvalid;
     const int b = blockIdx.x;
     const int nc = g.nc;
     uint32_t* row = H + (size_t)b * nc;
@@ -179,6 +182,7 @@ __global__ void __launch_bounds__(kBlock) k_bin_count(const int32_t* __restrict_
     if (threadIdx.x < 2) s_range[threadIdx.x] = lower_bound_start(start, n, bin_threshold(b + threadIdx.x, g));
     if (kLds)
         for (int c = threadIdx.x; c < nc; c += blockDim.x) hist[c] = 0;
+    if (threadIdx.x == 0) s_nvalid = 0;
     __syncthreads();
     const int64_t lo = s_range[0], hi = max(s_range[1], lo);
     if (threadIdx.x == 0) {
@@ -209,10 +213,15 @@ __global__ void __launch_bounds__(kBlock) k_bin_count(const int32_t* __restrict_
     const bool anybad = __ballot(badbc) != 0ull, anyuns = __ballot(unsorted) != 0ull;
     if ((threadIdx.x & 63) == 0) {
         if (mspan) atomicMax(&st->max_span, mspan);
-        if (nvalid) atomicAdd(&st->valid, nvalid);
+        if (nvalid) {
+            atomicAdd(&st->valid, nvalid);
+            atomicAdd(&s_nvalid, (uint32_t)nvalid);
+        }
         if (anybad) atomicOr(&st->err, ERR_BADBC);
         if (anyuns) atomicOr(&st->err, ERR_UNSORTED);
     }
+    __syncthreads();
+    if (threadIdx.x == 0) bin_valid[b] = s_nvalid;
 }
 
 // Scan step a: column sums over blocks of RB rows. grid (ceil(nc/256), nrb)
@@ -296,9 +305,6 @@ __global__ void k_scan_apply(uint32_t* __restrict__ H, const uint32_t* __restric
 
 // Grouping element (16 bytes, cell-major, BAM order inside a cell):
 //   w = record byte offset | meta << 56, start, |tlen|
-#ifndef MGP_SC_ABL
-#define MGP_SC_ABL 0  // scatter ablations for experiments: 0 = real kernel
-#endif
 struct __align__(16) GElem {
     unsigned long long w;
     int32_t start;
@@ -307,62 +313,81 @@ struct __align__(16) GElem {
 constexpr unsigned long long GM_REV = 1ull << 56, GM_PAIRED = 2ull << 56, GM_MAPQ_OK = 4ull << 56,
                              GM_BAD = 8ull << 56, GM_OFF = (1ull << 56) - 1;
 
-// One workgroup per start bin, reads taken 256 at a time in BAM order: each valid
-// read's grouping element goes to its cell-major slot. Slots inside a (bin, cell)
-// group follow BAM order (stable): lanes of one cell find each other with one
-// ballot per cell-id bit; the 4 waves then take turns (in wave order) to claim
-// their groups' slots from the per-cell counters in LDS (seeded with the scan).
-template <bool kLds>
-__global__ void __launch_bounds__(kBlock) k_scatter(int64_t n, const int32_t* __restrict__ start,
+// Grouping in two passes (a single pass that writes each 16-byte element straight
+// to its cell-major slot is bound by ~200M scattered partial-line stores):
+//   A, per start bin: valid reads -> buckets (bin, group of 64 cells), BAM order
+//      kept inside each bucket; a bucket receives a contiguous run per step, so
+//      its lines fill in L2 before they go to HBM;
+//   B, per (cell group, bin range), one wave: bucket elements -> cell-major
+//      slots; a cell's slots over consecutive bins are contiguous, so each
+//      wave writes 64 sequential streams.
+// The 6-bit cell id inside the group rides in bits 50..55 of GElem.w between
+// the passes (record offsets stay below 2^50).
+constexpr unsigned long long GM_LCELL_SHIFT = 50, GM_LCELL = 63ull << GM_LCELL_SHIFT;
+constexpr int kGroup = 64;
+
+__global__ void __launch_bounds__(kBlock) k_group_a(int64_t n, const int32_t* __restrict__ start,
                                                     const int32_t* __restrict__ bc, const int32_t* __restrict__ tlen,
                                                     const uint16_t* __restrict__ flag, const uint8_t* __restrict__ mapq,
                                                     const uint64_t* __restrict__ roff,
-                                                    const uint32_t* __restrict__ bin_lo, const uint32_t* __restrict__ O,
-                                                    uint32_t* __restrict__ cur, Geom g, int cbits, int min_mapq,
-                                                    GElem* __restrict__ gel, uint32_t* __restrict__ first_read) {
-    extern __shared__ uint32_t cnt_lds[];
-#if MGP_XCD_REMAP
-    // blocks are dealt round-robin over the 8 XCDs: give each XCD a contiguous bin
-    // range so concurrently written runs of one cell share that XCD's L2
-    const int per = (g.nbins + 7) / 8;
-    const int b = (int)(blockIdx.x % 8) * per + (int)(blockIdx.x / 8);
-    if (b >= g.nbins) return;
-#else
+                                                    const uint32_t* __restrict__ bin_lo,
+                                                    const uint32_t* __restrict__ O, const uint32_t* __restrict__ binbase,
+                                                    Geom g, int ngroups, int gbits, int min_mapq,
+                                                    uint32_t* __restrict__ bucket_off, GElem* __restrict__ gel2,
+                                                    uint32_t* __restrict__ first_read) {
+    extern __shared__ uint32_t sm[];
+    uint32_t* gcnt = sm;             // [ngroups] next free slot of each bucket of this bin
+    uint32_t* fbits = sm + ngroups;  // [ceil(nc/32)] cell's first read is in this bin
     const int b = blockIdx.x;
-#endif
     const int nc = g.nc;
-    const int wid = threadIdx.x >> 6;
-    // kLds: counters in LDS seeded from the scanned row; else `cur`, a global copy of
-    // the scanned rows (one workgroup owns row b and the waves take turns)
-    uint32_t* cnt = kLds ? cnt_lds : cur + (size_t)b * nc;
-    // kLds: fbits[c] = no read of cell c in bins < b (its first read in BAM order, if
-    // any is in this bin, is claimed by the first group of c here: first_read)
-    uint32_t* fbits = cnt_lds + nc;
-    if (kLds) {
-        for (int c = threadIdx.x; c < (nc + 31) / 32; c += blockDim.x) fbits[c] = 0;
-        __syncthreads();
-        for (int c = threadIdx.x; c < nc; c += blockDim.x) {
-            const uint32_t o = O[(size_t)b * nc + c];
-            cnt_lds[c] = o;
-            if (o == O[c]) atomicOr(&fbits[c >> 5], 1u << (c & 31));
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const unsigned long long lt = lanemask_lt();
+    // bucket sizes (one wave per group) and the first-read bits
+    for (int gi = wid; gi < ngroups; gi += kBlock / kWave) {
+        const int c = gi * kGroup + lane;
+        // reads of cell c in bin b = O[b+1][c] - O[b][c] (row nbins holds the cell ends)
+        uint32_t h = c < nc ? O[(size_t)(b + 1) * nc + c] - O[(size_t)b * nc + c] : 0u;
+        h = wave_sum(h);
+        if (lane == 0) gcnt[gi] = h;
+    }
+    for (int x = threadIdx.x; x < (nc + 31) / 32; x += blockDim.x) fbits[x] = 0;
+    __syncthreads();
+    // exclusive scan over groups (wave 0, 64 at a time), based at the bin's first slot
+    if (wid == 0) {
+        uint32_t carry = binbase[b];
+        for (int g0 = 0; g0 < ngroups; g0 += kWave) {
+            const int gi = g0 + lane;
+            const uint32_t v = gi < ngroups ? gcnt[gi] : 0u;
+            uint32_t x = v;
+            for (int o = 1; o < kWave; o <<= 1) {
+                const uint32_t y = __shfl_up(x, o, kWave);
+                if (lane >= o) x += y;
+            }
+            if (gi < ngroups) {
+                gcnt[gi] = carry + x - v;
+                bucket_off[(size_t)b * (ngroups + 1) + gi] = carry + x - v;
+            }
+            carry += __shfl(x, kWave - 1, kWave);
         }
+        if (lane == 0) bucket_off[(size_t)b * (ngroups + 1) + ngroups] = carry;
+    }
+    for (int c = threadIdx.x; c < nc; c += blockDim.x) {
+        const size_t k = (size_t)b * nc + c;
+        const uint32_t o = O[k];
+        if (O[k + nc] != o && o == O[c]) atomicOr(&fbits[c >> 5], 1u << (c & 31));
     }
     const int64_t lo = bin_lo[b], hi = max((int64_t)bin_lo[b + 1], lo);
-    const unsigned long long lt = lanemask_lt();
     __syncthreads();
-    // Each wave owns a contiguous run of kAhead*64 reads per step (BAM order =
-    // wave order, then round order), so the waves claim slots in wave order with
-    // one barrier per wave per step. Loads of the next step are issued before the
-    // current step is processed (two register sets).
+    // each wave owns a contiguous run of kAhead*64 reads per step (BAM order = wave
+    // order, then round order); waves claim bucket slots in wave order
     constexpr int kAhead = 4;
     constexpr int kStep = kAhead * kBlock;
-    const int lane = threadIdx.x & 63;
     struct Pre {
         int c[kAhead], s[kAhead], t[kAhead], f[kAhead], m[kAhead];
         uint64_t o[kAhead];
     };
-    // loads are issued unconditionally (index clamped into the bin) so that every
-    // path has the same number in flight and the waits stay counted, not drained
+    // loads issued unconditionally (index clamped into the bin) so every path has
+    // the same number in flight and the waits stay counted
     auto load = [&](Pre& P, int64_t base0) {
 #pragma unroll
         for (int u = 0; u < kAhead; ++u) {
@@ -384,68 +409,43 @@ __global__ void __launch_bounds__(kBlock) k_scatter(int64_t n, const int32_t* __
             const int64_t i = base0 + wid * (kAhead * kWave) + u * kWave + lane;
             const int c = P.c[u];
             valid[u] = i < hi && read_valid(c, (uint16_t)P.f[u], nc);
+            const int gi = c >> 6;
             unsigned long long pm = __ballot(valid[u]);
-            if (MGP_SC_ABL == 3) pm = valid[u] ? (1ull << lane) : 0ull;
-            for (int bit = 0; bit < cbits && pm && MGP_SC_ABL != 3; ++bit) {
-                const bool x = valid[u] && ((c >> bit) & 1);
+            for (int bit = 0; bit < gbits && pm; ++bit) {
+                const bool x = valid[u] && ((gi >> bit) & 1);
                 const unsigned long long m = __ballot(x);
                 pm &= x ? m : ~m;
             }
             peers[u] = pm;
+            if (valid[u] && (fbits[c >> 5] >> (c & 31)) & 1u) atomicMin(&first_read[c], (uint32_t)i);
         }
-        // claims, in wave order: each group leader adds its group size to the cell's
-        // counter (LDS atomics return the old value; one wave's atomics execute in
-        // order, so its rounds chain without waiting in between) and, on the cell's
-        // first bin, takes the first-read bit; members read their base from the
-        // leader after the barrier, outside the serialised part
         uint32_t bef[kAhead];
-        bool firstg[kAhead];
 #pragma unroll
         for (int w = 0; w < kBlock / kWave; ++w) {
             if (wid == w) {
 #pragma unroll
                 for (int u = 0; u < kAhead; ++u) {
                     bef[u] = 0;
-                    firstg[u] = false;
-                    if (valid[u] && (peers[u] & lt) == 0ull) {
-                        const int c = P.c[u];
-                        bef[u] = atomicAdd(&cnt[c], (uint32_t)__popcll(peers[u]));
-                        if (kLds) {
-                            const uint32_t m = 1u << (c & 31);
-                            firstg[u] = (atomicAnd(&fbits[c >> 5], ~m) & m) != 0u;
-                        }
-                    }
-                    if (!kLds) __threadfence_block();
+                    if (valid[u] && (peers[u] & lt) == 0ull)
+                        bef[u] = atomicAdd(&gcnt[P.c[u] >> 6], (uint32_t)__popcll(peers[u]));
                 }
             }
-            if (MGP_SC_ABL != 2) __syncthreads();
+            __syncthreads();
         }
-        uint32_t dest[kAhead];
 #pragma unroll
         for (int u = 0; u < kAhead; ++u) {
             const int leader = peers[u] ? __builtin_ctzll(peers[u]) : lane;
-            dest[u] = (uint32_t)__shfl((int)bef[u], leader, kWave) + (uint32_t)__popcll(peers[u] & lt);
-            if (kLds && firstg[u])
-                first_read[P.c[u]] = (uint32_t)(base0 + wid * (kAhead * kWave) + u * kWave + lane);
-        }
-#pragma unroll
-        for (int u = 0; u < kAhead; ++u) {
-            if (!valid[u] && MGP_SC_ABL != 1) continue;  // ablation 1 writes every slot (no holes)
-            const int c = P.c[u];
+            const uint32_t dest = (uint32_t)__shfl((int)bef[u], leader, kWave) + (uint32_t)__popcll(peers[u] & lt);
+            if (!valid[u]) continue;
             const uint16_t f = (uint16_t)P.f[u];
             const int t = P.t[u];
             GElem e;
             e.w = P.o[u] | (f & MGP_FLAG_REVERSE ? GM_REV : 0ull) | (f & MGP_FLAG_PAIRED ? GM_PAIRED : 0ull) |
-                  (P.m[u] >= min_mapq ? GM_MAPQ_OK : 0ull) | (f & MGP_FLAG_NOSEQQUAL ? GM_BAD : 0ull);
+                  (P.m[u] >= min_mapq ? GM_MAPQ_OK : 0ull) | (f & MGP_FLAG_NOSEQQUAL ? GM_BAD : 0ull) |
+                  ((unsigned long long)(P.c[u] & (kGroup - 1)) << GM_LCELL_SHIFT);
             e.start = P.s[u];
             e.tlen = t < 0 ? (uint32_t)(-(int64_t)t) : (uint32_t)t;
-            if (MGP_SC_ABL == 1)
-                gel[min((uint64_t)(base0 + wid * (kAhead * kWave) + u * kWave + lane), (uint64_t)n - 1)] = e;
-            else
-                gel[dest[u]] = e;
-            // the cell's first element in cell-major order is its first valid read in BAM order
-            if (!kLds && dest[u] == O[c])
-                first_read[c] = (uint32_t)(base0 + wid * (kAhead * kWave) + u * kWave + lane);
+            gel2[dest] = e;
         }
     };
     if (lo >= hi) return;
@@ -456,6 +456,51 @@ __global__ void __launch_bounds__(kBlock) k_scatter(int64_t n, const int32_t* __
         process(A, base0);
         load(A, base0 + 2 * kStep);
         if (base0 + kStep < hi) process(B, base0 + kStep);
+    }
+}
+
+__global__ void __launch_bounds__(kWave) k_group_b(const GElem* __restrict__ gel2,
+                                                   const uint32_t* __restrict__ bucket_off,
+                                                   const uint32_t* __restrict__ O, Geom g, int ngroups, int rb,
+                                                   GElem* __restrict__ gel) {
+    __shared__ uint32_t cnt[kGroup];
+    const int gi = blockIdx.x;
+    const int b0 = blockIdx.y * rb, b1 = min(g.nbins, b0 + rb);
+    const int lane = threadIdx.x;
+    const int nc = g.nc;
+    const int c = gi * kGroup + lane;
+    const unsigned long long lt = lanemask_lt();
+    for (int b = b0; b < b1; ++b) {
+        cnt[lane] = c < nc ? O[(size_t)b * nc + c] : 0u;
+        const uint32_t k0 = bucket_off[(size_t)b * (ngroups + 1) + gi];
+        const uint32_t k1 = bucket_off[(size_t)b * (ngroups + 1) + gi + 1];
+        __builtin_amdgcn_wave_barrier();
+        for (uint32_t k = k0; k < k1; k += kWave) {
+            const uint32_t j = k + lane;
+            const bool act = j < k1;
+            GElem e;
+            e.w = 0;
+            e.start = 0;
+            e.tlen = 0;
+            if (act) e = gel2[j];
+            const int lc = (int)((e.w >> GM_LCELL_SHIFT) & (kGroup - 1));
+            unsigned long long peers = __ballot(act);
+#pragma unroll
+            for (int bit = 0; bit < 6; ++bit) {
+                const bool x = act && ((lc >> bit) & 1);
+                const unsigned long long m = __ballot(x);
+                peers &= x ? m : ~m;
+            }
+            const uint32_t base = act ? cnt[lc] : 0u;
+            __builtin_amdgcn_wave_barrier();
+            if (act && (peers & lt) == 0ull) cnt[lc] = base + (uint32_t)__popcll(peers);
+            __builtin_amdgcn_wave_barrier();
+            if (act) {
+                e.w &= ~GM_LCELL;
+                gel[base + (uint32_t)__popcll(peers & lt)] = e;
+            }
+        }
+        __builtin_amdgcn_wave_barrier();
     }
 }
 
@@ -736,7 +781,7 @@ __global__ void __launch_bounds__(kBlock, MGP_PILEUP_WAVES) k_pileup(
     const int hi_bin = k == g.nwin - 1 ? g.nbins : win_hi_bin(k, g);
     const int nc = g.nc;
     const unsigned long long lt = lanemask_lt();
-    const bool dedup = pc.dedup_mode != MGP_DEDUP_NONE;
+    const bool dedup = MGP_ABL != 5 && pc.dedup_mode != MGP_DEDUP_NONE;
     bool span_err = false, bad = false;
     unsigned long long d2 = 0, d3 = 0;
 
@@ -767,36 +812,49 @@ __global__ void __launch_bounds__(kBlock, MGP_PILEUP_WAVES) k_pileup(
                 e.start = INT_MIN;
                 e.tlen = 0;
                 if (act) e = gel[j];
+                // the element just before the chunk, loaded with it (lane 0 only)
+                GElem pe;
+                pe.w = 0;
+                pe.start = INT_MIN;
+                pe.tlen = 0;
+                if (dedup && lane == 0 && cb > lo) pe = gel[cb - 1];
                 bool dup2 = false, dup3 = false;
                 if (dedup) {
-                    // walk back over equal starts (duplicates sit just before j, BAM order)
-                    bool cont = act;
-                    for (int m = 1; m < kWave; ++m) {
-                        const int ps = __shfl_up(e.start, m, kWave);
-                        const unsigned long long pw = __shfl_up(e.w, m, kWave);
+                    // duplicates sit just before j in BAM order among equal starts: runs of
+                    // equal starts are found by one shuffle; inside a run only |tlen| is
+                    // shuffled (the strand bit comes from a ballot)
+                    const int ps = __shfl_up(e.start, 1, kWave);
+                    const bool eqp = act && lane > 0 && ps == e.start;
+                    const unsigned long long heads = __ballot(!eqp);
+                    const int head = 63 - __builtin_clzll(heads & (lt | (1ull << lane)));
+                    const unsigned long long revm = __ballot(act && (e.w & GM_REV) != 0ull);
+                    const bool myrev = (e.w & GM_REV) != 0ull;
+                    const int maxd = __builtin_amdgcn_readfirstlane(wave_max(act ? lane - head : 0));
+                    for (int m = 1; m <= maxd; ++m) {
                         const uint32_t pt = __shfl_up(e.tlen, m, kWave);
-                        if (cont && lane >= m) {
-                            if (ps != e.start) {
-                                cont = false;
-                            } else if (((pw ^ e.w) & GM_REV) == 0ull) {
-                                dup2 = true;
-                                if (pt == e.tlen) {
-                                    dup3 = true;
-                                    cont = false;
-                                }
-                            }
+                        if (act && lane - m >= head && (((revm >> (lane - m)) & 1ull) != 0ull) == myrev) {
+                            dup2 = true;
+                            if (pt == e.tlen) dup3 = true;
                         }
-                        const bool more = cont && lane > m;
-                        if (__ballot(more) == 0ull) break;
                     }
-                    // runs reaching the chunk start continue in the previous elements (global)
-                    if (cont && act) {
-                        for (uint32_t mm = cb; mm-- > lo;) {
-                            const GElem p = gel[mm];
-                            if (p.start != e.start) break;
-                            if (same_dup(p, e, dup3)) {
-                                dup2 = true;
-                                if (dup3) break;
+                    // the first run of the chunk may continue before it
+                    const int ps0 = __shfl(pe.start, 0, kWave);
+                    if (act && head == 0 && cb > lo && ps0 == e.start) {
+                        const unsigned long long pw0 = __shfl(pe.w, 0, kWave);
+                        const uint32_t pt0 = __shfl(pe.tlen, 0, kWave);
+                        GElem p0;
+                        p0.w = pw0;
+                        p0.start = ps0;
+                        p0.tlen = pt0;
+                        if (same_dup(p0, e, dup3)) dup2 = true;
+                        if (!dup3) {
+                            for (uint32_t mm = cb - 1; mm-- > lo;) {
+                                const GElem p = gel[mm];
+                                if (p.start != e.start) break;
+                                if (same_dup(p, e, dup3)) {
+                                    dup2 = true;
+                                    if (dup3) break;
+                                }
                             }
                         }
                     }
@@ -897,11 +955,13 @@ __global__ void __launch_bounds__(kBlock, MGP_PILEUP_WAVES) k_pileup(
                     d += t2;
                 }
                 if (d == 0 && !pc.keep_tn5) tf = tr = 0;
-                uint4* cp = reinterpret_cast<uint4*>(counts + P * 8);
-                cp[0] = make_uint4(v[0], v[1], v[2], v[3]);
-                cp[1] = make_uint4(v[4], v[5], v[6], v[7]);
-                reinterpret_cast<uint2*>(tn5)[P] = make_uint2(tf, tr);
-                depth[P] = d;
+                if (MGP_ABL != 4 || (v[0] == 0xFFFFFFFFu && d == 7u)) {
+                    uint4* cp = reinterpret_cast<uint4*>(counts + P * 8);
+                    cp[0] = make_uint4(v[0], v[1], v[2], v[3]);
+                    cp[1] = make_uint4(v[4], v[5], v[6], v[7]);
+                    reinterpret_cast<uint2*>(tn5)[P] = make_uint2(tf, tr);
+                    depth[P] = d;
+                }
                 cov += d > 0;
                 sum += d;
                 mx = d > mx ? d : mx;
@@ -1217,8 +1277,7 @@ int mgp_open(const mgp_config* cfg, int hip_device, mgp_ctx** out) {
         (void)hipFuncSetAttribute((const void*)k_median, hipFuncAttributeMaxDynamicSharedMemorySize, lds_max);
         (void)hipFuncSetAttribute((const void*)k_bin_count<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                   lds_max);
-        (void)hipFuncSetAttribute((const void*)k_scatter<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  lds_max);
+        (void)hipFuncSetAttribute((const void*)k_group_a, hipFuncAttributeMaxDynamicSharedMemorySize, lds_max);
         (void)hipFuncSetAttribute((const void*)k_pileup, hipFuncAttributeMaxDynamicSharedMemorySize, lds_max);
         (void)hipGetLastError();
         if ((size_t)ctx->g.L * 4 + 2048 > prop.sharedMemPerBlock) {
@@ -1256,7 +1315,7 @@ void mgp_close(mgp_ctx* ctx) {
     (void)hipStreamSynchronize(ctx->s_copy);
     if (ctx->comm) ncclCommDestroy(ctx->comm);
     DevBuf* bufs[] = {&ctx->start,     &ctx->bc,        &ctx->tlen,     &ctx->flag,       &ctx->mapq,
-                      &ctx->span,      &ctx->roff,      &ctx->payload,  &ctx->bin_start,  &ctx->Hcur,
+                      &ctx->span,      &ctx->roff,      &ctx->payload,  &ctx->bin_start,  &ctx->gel2,
                       &ctx->H,         &ctx->P,         &ctx->cell_cnt, &ctx->cell_base,  &ctx->gel,
                       &ctx->tally_part, &ctx->tally,   &ctx->n_reads,    &ctx->any_paired,
                       &ctx->passed,    &ctx->covered,   &ctx->dsum,     &ctx->dmax,       &ctx->med_lo,
@@ -1352,6 +1411,10 @@ static int ensure_run_buffers(mgp_ctx* ctx) {
     MGP_TRY(ctx->cell_cnt.ensure(nc * 4));
     MGP_TRY(ctx->cell_base.ensure(nc * 4));
     MGP_TRY(ctx->gel.ensure(n * sizeof(GElem)));
+    MGP_TRY(ctx->gel2.ensure(n * sizeof(GElem)));
+    MGP_TRY(ctx->bin_valid.ensure((size_t)(g.nbins + 1) * 4));
+    MGP_TRY(ctx->bin_base.ensure((size_t)(g.nbins + 1) * 4));
+    MGP_TRY(ctx->bucket_off.ensure((size_t)g.nbins * ((nc + kGroup - 1) / kGroup + 1) * 4));
     MGP_TRY(ctx->tally_part.ensure((size_t)std::max(g.nchunks, 1) * L * 16));
     MGP_TRY(ctx->tally.ensure(L * 4 * 8));
     MGP_TRY(ctx->n_reads.ensure(nc * 4));
@@ -1397,8 +1460,6 @@ int mgp_run(mgp_ctx* ctx) {
     }
 
     if (nc > 0) {
-        int cbits = 1;
-        while (cbits < 31 && (1 << cbits) < nc) ++cbits;
         const bool lds = nc <= ctx->lds_hist_max_cells;
         // 1. per (start bin, cell) histogram + bin bounds + order check
         STAGE_BEGIN(ST_HIST);
@@ -1408,12 +1469,13 @@ int mgp_run(mgp_ctx* ctx) {
             if (lds)
                 k_bin_count<true><<<g.nbins, kBlock, (size_t)nc * 4, s>>>(
                     ctx->start.as<int32_t>(), ctx->bc.as<int32_t>(), ctx->flag.as<uint16_t>(),
-                    ctx->span.as<uint32_t>(), n, g, ctx->H.as<uint32_t>(), ctx->bin_start.as<uint32_t>(), st);
+                    ctx->span.as<uint32_t>(), n, g, ctx->H.as<uint32_t>(), ctx->bin_start.as<uint32_t>(),
+                    ctx->bin_valid.as<uint32_t>(), st);
             else
                 k_bin_count<false><<<g.nbins, kBlock, 0, s>>>(ctx->start.as<int32_t>(), ctx->bc.as<int32_t>(),
                                                               ctx->flag.as<uint16_t>(), ctx->span.as<uint32_t>(), n,
                                                               g, ctx->H.as<uint32_t>(), ctx->bin_start.as<uint32_t>(),
-                                                              st);
+                                                              ctx->bin_valid.as<uint32_t>(), st);
             HIP_TRY(hipGetLastError());
         }
         STAGE_END(ST_HIST);
@@ -1431,27 +1493,30 @@ int mgp_run(mgp_ctx* ctx) {
         HIP_TRY(hipGetLastError());
         STAGE_END(ST_SCAN);
 
-        // 3. stable scatter of the grouping elements
+        // 3. stable grouping into cell-major order (two passes)
         STAGE_BEGIN(ST_SCATTER);
         if (n > 0) {
-            const unsigned sgrid = MGP_XCD_REMAP ? (unsigned)(((g.nbins + 7) / 8) * 8) : (unsigned)g.nbins;
-            const size_t sc_lds = (size_t)nc * 4 + (size_t)((nc + 31) / 32) * 4;
-            if (sc_lds <= (size_t)ctx->lds_hist_max_cells * 4) {
-                k_scatter<true><<<sgrid, kBlock, sc_lds, s>>>(
-                    n, ctx->start.as<int32_t>(), ctx->bc.as<int32_t>(), ctx->tlen.as<int32_t>(),
-                    ctx->flag.as<uint16_t>(), ctx->mapq.as<uint8_t>(), ctx->roff.as<uint64_t>(),
-                    ctx->bin_start.as<uint32_t>(), ctx->H.as<uint32_t>(), nullptr, g, cbits, ctx->cfg.min_mapq,
-                    ctx->gel.as<GElem>(), ctx->first_read.as<uint32_t>());
-            } else {
-                MGP_TRY(ctx->Hcur.ensure((size_t)(g.nbins + 1) * nc * 4));
-                HIP_TRY(hipMemcpyAsync(ctx->Hcur.p, ctx->H.p, (size_t)(g.nbins + 1) * nc * 4,
-                                       hipMemcpyDeviceToDevice, s));
-                k_scatter<false><<<sgrid, kBlock, 0, s>>>(
-                    n, ctx->start.as<int32_t>(), ctx->bc.as<int32_t>(), ctx->tlen.as<int32_t>(),
-                    ctx->flag.as<uint16_t>(), ctx->mapq.as<uint8_t>(), ctx->roff.as<uint64_t>(),
-                    ctx->bin_start.as<uint32_t>(), ctx->H.as<uint32_t>(), ctx->Hcur.as<uint32_t>(), g, cbits,
-                    ctx->cfg.min_mapq, ctx->gel.as<GElem>(), ctx->first_read.as<uint32_t>());
-            }
+            const int ngroups = (nc + kGroup - 1) / kGroup;
+            int gbits = 0;
+            while (gbits < 31 && (1 << gbits) < ngroups) ++gbits;
+            k_scan_cells<<<1, 1024, 0, s>>>(ctx->bin_valid.as<uint32_t>(), g.nbins, ctx->bin_base.as<uint32_t>());
+            const size_t a_lds = (size_t)ngroups * 4 + (size_t)((nc + 31) / 32) * 4;
+            if (a_lds > (size_t)ctx->lds_hist_max_cells * 4)
+                return set_err(MGP_E_INVALID, "too many cells for one context (grouping LDS)");
+            if ((uint64_t)ctx->pay >= (1ull << GM_LCELL_SHIFT))
+                return set_err(MGP_E_INVALID, "payload too large (record offsets must stay below 2^50)");
+            k_group_a<<<g.nbins, kBlock, a_lds, s>>>(
+                n, ctx->start.as<int32_t>(), ctx->bc.as<int32_t>(), ctx->tlen.as<int32_t>(), ctx->flag.as<uint16_t>(),
+                ctx->mapq.as<uint8_t>(), ctx->roff.as<uint64_t>(), ctx->bin_start.as<uint32_t>(),
+                ctx->H.as<uint32_t>(), ctx->bin_base.as<uint32_t>(), g, ngroups, gbits,
+                ctx->cfg.min_mapq, ctx->bucket_off.as<uint32_t>(), ctx->gel2.as<GElem>(),
+                ctx->first_read.as<uint32_t>());
+            HIP_TRY(hipGetLastError());
+            // about 4096 one-wave workgroups: bins per workgroup from the group count
+            const int rb = std::max(1, (int)(((int64_t)ngroups * g.nbins + 4095) / 4096));
+            dim3 gb((unsigned)ngroups, (unsigned)((g.nbins + rb - 1) / rb));
+            k_group_b<<<gb, kWave, 0, s>>>(ctx->gel2.as<GElem>(), ctx->bucket_off.as<uint32_t>(), ctx->H.as<uint32_t>(),
+                                            g, ngroups, rb, ctx->gel.as<GElem>());
             HIP_TRY(hipGetLastError());
         }
         STAGE_END(ST_SCATTER);
