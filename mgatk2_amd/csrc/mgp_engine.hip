@@ -459,48 +459,121 @@ __global__ void __launch_bounds__(kBlock) k_group_a(int64_t n, const int32_t* __
     }
 }
 
-__global__ void __launch_bounds__(kWave) k_group_b(const GElem* __restrict__ gel2,
-                                                   const uint32_t* __restrict__ bucket_off,
-                                                   const uint32_t* __restrict__ O, Geom g, int ngroups, int rb,
-                                                   GElem* __restrict__ gel) {
-    __shared__ uint32_t cnt[kGroup];
+// Pass B: workgroup = (cell group, bin range). A step takes the group's buckets
+// of as many consecutive bins as fit the LDS stage; each wave ranks the elements
+// of its bins (one bin at a time, stable: ballot peers + per-cell counters) and
+// drops them at their place inside the step's per-cell runs in LDS; a cell's
+// slots over consecutive bins are contiguous in the output, so the stage is then
+// written out as a few long runs (full lines) instead of 64 scattered 16-byte
+// stores per instruction. A bucket larger than the stage goes straight out.
+constexpr int kStageB = 2048;
+
+__device__ __forceinline__ void group_b_rank(const GElem* __restrict__ gel2, uint32_t k0, uint32_t k1,
+                                             uint32_t* cnt, int lane, unsigned long long lt, GElem* stage,
+                                             const uint32_t* cbase, const uint32_t* cstart,
+                                             GElem* __restrict__ gel) {
+    for (uint32_t k = k0; k < k1; k += kWave) {
+        const uint32_t j = k + lane;
+        const bool act = j < k1;
+        GElem e;
+        e.w = 0;
+        e.start = 0;
+        e.tlen = 0;
+        if (act) e = gel2[j];
+        const int lc = (int)((e.w >> GM_LCELL_SHIFT) & (kGroup - 1));
+        unsigned long long peers = __ballot(act);
+#pragma unroll
+        for (int bit = 0; bit < 6; ++bit) {
+            const bool x = act && ((lc >> bit) & 1);
+            const unsigned long long m = __ballot(x);
+            peers &= x ? m : ~m;
+        }
+        const uint32_t base = act ? cnt[lc] : 0u;
+        __builtin_amdgcn_wave_barrier();
+        if (act && (peers & lt) == 0ull) cnt[lc] = base + (uint32_t)__popcll(peers);
+        __builtin_amdgcn_wave_barrier();
+        if (act) {
+            const uint32_t dest = base + (uint32_t)__popcll(peers & lt);
+            if (stage) {
+                stage[cstart[lc] + (dest - cbase[lc])] = e;
+            } else {
+                e.w &= ~GM_LCELL;
+                gel[dest] = e;
+            }
+        }
+    }
+}
+
+__global__ void __launch_bounds__(kBlock) k_group_b(const GElem* __restrict__ gel2,
+                                                    const uint32_t* __restrict__ bucket_off,
+                                                    const uint32_t* __restrict__ O, Geom g, int ngroups, int rb,
+                                                    GElem* __restrict__ gel) {
+    __shared__ GElem stage[kStageB];
+    __shared__ uint32_t cnt[kBlock / kWave][kGroup];
+    __shared__ uint32_t cbase[kGroup], cstart[kGroup + 1];
+    __shared__ int s_be;
     const int gi = blockIdx.x;
-    const int b0 = blockIdx.y * rb, b1 = min(g.nbins, b0 + rb);
-    const int lane = threadIdx.x;
+    const int B0 = blockIdx.y * rb, B1 = min(g.nbins, B0 + rb);
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const int nc = g.nc;
     const int c = gi * kGroup + lane;
     const unsigned long long lt = lanemask_lt();
-    for (int b = b0; b < b1; ++b) {
-        cnt[lane] = c < nc ? O[(size_t)b * nc + c] : 0u;
-        const uint32_t k0 = bucket_off[(size_t)b * (ngroups + 1) + gi];
-        const uint32_t k1 = bucket_off[(size_t)b * (ngroups + 1) + gi + 1];
-        __builtin_amdgcn_wave_barrier();
-        for (uint32_t k = k0; k < k1; k += kWave) {
-            const uint32_t j = k + lane;
-            const bool act = j < k1;
-            GElem e;
-            e.w = 0;
-            e.start = 0;
-            e.tlen = 0;
-            if (act) e = gel2[j];
-            const int lc = (int)((e.w >> GM_LCELL_SHIFT) & (kGroup - 1));
-            unsigned long long peers = __ballot(act);
-#pragma unroll
-            for (int bit = 0; bit < 6; ++bit) {
-                const bool x = act && ((lc >> bit) & 1);
-                const unsigned long long m = __ballot(x);
-                peers &= x ? m : ~m;
+    const size_t bo = (size_t)ngroups + 1;
+    for (int b = B0; b < B1;) {
+        if (threadIdx.x == 0) {  // bins of this step: as many as fit the stage
+            uint32_t tot = 0;
+            int be = b;
+            while (be < B1) {
+                const uint32_t sz = bucket_off[(size_t)be * bo + gi + 1] - bucket_off[(size_t)be * bo + gi];
+                if (tot + sz > (uint32_t)kStageB) break;
+                tot += sz;
+                ++be;
             }
-            const uint32_t base = act ? cnt[lc] : 0u;
-            __builtin_amdgcn_wave_barrier();
-            if (act && (peers & lt) == 0ull) cnt[lc] = base + (uint32_t)__popcll(peers);
-            __builtin_amdgcn_wave_barrier();
-            if (act) {
-                e.w &= ~GM_LCELL;
-                gel[base + (uint32_t)__popcll(peers & lt)] = e;
-            }
+            s_be = be;
         }
-        __builtin_amdgcn_wave_barrier();
+        __syncthreads();
+        const int be = s_be;
+        if (be == b) {  // one bucket larger than the stage: direct stores (wave 0)
+            if (wid == 0) {
+                cnt[0][lane] = c < nc ? O[(size_t)b * nc + c] : 0u;
+                __builtin_amdgcn_wave_barrier();
+                group_b_rank(gel2, bucket_off[(size_t)b * bo + gi], bucket_off[(size_t)b * bo + gi + 1], cnt[0],
+                             lane, lt, nullptr, nullptr, nullptr, gel);
+            }
+            __syncthreads();
+            ++b;
+            continue;
+        }
+        if (wid == 0) {  // per-cell runs of the step: base slot and place in the stage
+            const uint32_t o0 = c < nc ? O[(size_t)b * nc + c] : 0u;
+            const uint32_t len = c < nc ? O[(size_t)be * nc + c] - o0 : 0u;
+            uint32_t x = len;
+            for (int o = 1; o < kWave; o <<= 1) {
+                const uint32_t y = __shfl_up(x, o, kWave);
+                if (lane >= o) x += y;
+            }
+            cbase[lane] = o0;
+            cstart[lane] = x - len;
+            if (lane == kWave - 1) cstart[kGroup] = x;
+        }
+        __syncthreads();
+        for (int bb = b + wid; bb < be; bb += kBlock / kWave) {
+            cnt[wid][lane] = c < nc ? O[(size_t)bb * nc + c] : 0u;
+            __builtin_amdgcn_wave_barrier();
+            group_b_rank(gel2, bucket_off[(size_t)bb * bo + gi], bucket_off[(size_t)bb * bo + gi + 1], cnt[wid],
+                         lane, lt, stage, cbase, cstart, gel);
+            __builtin_amdgcn_wave_barrier();
+        }
+        __syncthreads();
+        const uint32_t tot = cstart[kGroup];
+        for (uint32_t t = threadIdx.x; t < tot; t += kBlock) {
+            GElem e = stage[t];
+            const int lc = (int)((e.w >> GM_LCELL_SHIFT) & (kGroup - 1));
+            e.w &= ~GM_LCELL;
+            gel[cbase[lc] + (t - cstart[lc])] = e;
+        }
+        __syncthreads();
+        b = be;
     }
 }
 
@@ -1512,10 +1585,10 @@ int mgp_run(mgp_ctx* ctx) {
                 ctx->cfg.min_mapq, ctx->bucket_off.as<uint32_t>(), ctx->gel2.as<GElem>(),
                 ctx->first_read.as<uint32_t>());
             HIP_TRY(hipGetLastError());
-            // about 4096 one-wave workgroups: bins per workgroup from the group count
-            const int rb = std::max(1, (int)(((int64_t)ngroups * g.nbins + 4095) / 4096));
+            // about 2048 workgroups: bins per workgroup from the group count
+            const int rb = std::max(1, (int)(((int64_t)ngroups * g.nbins + 2047) / 2048));
             dim3 gb((unsigned)ngroups, (unsigned)((g.nbins + rb - 1) / rb));
-            k_group_b<<<gb, kWave, 0, s>>>(ctx->gel2.as<GElem>(), ctx->bucket_off.as<uint32_t>(), ctx->H.as<uint32_t>(),
+            k_group_b<<<gb, kBlock, 0, s>>>(ctx->gel2.as<GElem>(), ctx->bucket_off.as<uint32_t>(), ctx->H.as<uint32_t>(),
                                             g, ngroups, rb, ctx->gel.as<GElem>());
             HIP_TRY(hipGetLastError());
         }
