@@ -325,6 +325,10 @@ constexpr unsigned long long GM_REV = 1ull << 56, GM_PAIRED = 2ull << 56, GM_MAP
 // the passes (record offsets stay below 2^50).
 constexpr unsigned long long GM_LCELL_SHIFT = 50, GM_LCELL = 63ull << GM_LCELL_SHIFT;
 constexpr int kGroup = 64;
+#ifndef MGP_STAGE_A
+#define MGP_STAGE_A 1  // pass A: stage each step in LDS and write group runs
+#endif
+constexpr int kStageA = 4 * kBlock;  // one step of pass A (kAhead * kBlock reads)
 
 __global__ void __launch_bounds__(kBlock) k_group_a(int64_t n, const int32_t* __restrict__ start,
                                                     const int32_t* __restrict__ bc, const int32_t* __restrict__ tlen,
@@ -338,6 +342,10 @@ __global__ void __launch_bounds__(kBlock) k_group_a(int64_t n, const int32_t* __
     extern __shared__ uint32_t sm[];
     uint32_t* gcnt = sm;             // [ngroups] next free slot of each bucket of this bin
     uint32_t* fbits = sm + ngroups;  // [ceil(nc/32)] cell's first read is in this bin
+    uint32_t* gbase = fbits + (g.nc + 31) / 32;  // [ngroups] bucket slots at the step start
+    uint32_t* lstart = gbase + ngroups;          // [ngroups] group runs inside the step stage
+    __shared__ GElem stage[kStageA];
+    __shared__ uint16_t sgrp[kStageA];
     const int b = blockIdx.x;
     const int nc = g.nc;
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -419,6 +427,10 @@ __global__ void __launch_bounds__(kBlock) k_group_a(int64_t n, const int32_t* __
             peers[u] = pm;
             if (valid[u] && (fbits[c >> 5] >> (c & 31)) & 1u) atomicMin(&first_read[c], (uint32_t)i);
         }
+        if (MGP_STAGE_A) {
+            for (int x = threadIdx.x; x < ngroups; x += blockDim.x) gbase[x] = gcnt[x];
+            __syncthreads();
+        }
         uint32_t bef[kAhead];
 #pragma unroll
         for (int w = 0; w < kBlock / kWave; ++w) {
@@ -432,6 +444,21 @@ __global__ void __launch_bounds__(kBlock) k_group_a(int64_t n, const int32_t* __
             }
             __syncthreads();
         }
+        if (MGP_STAGE_A && wid == 0) {  // runs of the step's groups inside the stage
+            uint32_t carry = 0;
+            for (int g0 = 0; g0 < ngroups; g0 += kWave) {
+                const int gi = g0 + lane;
+                const uint32_t v = gi < ngroups ? gcnt[gi] - gbase[gi] : 0u;
+                uint32_t x = v;
+                for (int o = 1; o < kWave; o <<= 1) {
+                    const uint32_t y = __shfl_up(x, o, kWave);
+                    if (lane >= o) x += y;
+                }
+                if (gi < ngroups) lstart[gi] = carry + x - v;
+                carry += __shfl(x, kWave - 1, kWave);
+            }
+        }
+        if (MGP_STAGE_A) __syncthreads();
 #pragma unroll
         for (int u = 0; u < kAhead; ++u) {
             const int leader = peers[u] ? __builtin_ctzll(peers[u]) : lane;
@@ -445,7 +472,23 @@ __global__ void __launch_bounds__(kBlock) k_group_a(int64_t n, const int32_t* __
                   ((unsigned long long)(P.c[u] & (kGroup - 1)) << GM_LCELL_SHIFT);
             e.start = P.s[u];
             e.tlen = t < 0 ? (uint32_t)(-(int64_t)t) : (uint32_t)t;
-            gel2[dest] = e;
+            if (MGP_STAGE_A) {
+                const int gi = P.c[u] >> 6;
+                const uint32_t si = lstart[gi] + (dest - gbase[gi]);
+                stage[si] = e;
+                sgrp[si] = (uint16_t)gi;
+            } else {
+                gel2[dest] = e;
+            }
+        }
+        if (MGP_STAGE_A) {  // the step's elements go out as runs, one per group
+            __syncthreads();
+            const uint32_t tot = lstart[ngroups - 1] + (gcnt[ngroups - 1] - gbase[ngroups - 1]);
+            for (uint32_t x = threadIdx.x; x < tot; x += blockDim.x) {
+                const int gi = sgrp[x];
+                gel2[gbase[gi] + (x - lstart[gi])] = stage[x];
+            }
+            __syncthreads();
         }
     };
     if (lo >= hi) return;
@@ -1573,7 +1616,7 @@ int mgp_run(mgp_ctx* ctx) {
             int gbits = 0;
             while (gbits < 31 && (1 << gbits) < ngroups) ++gbits;
             k_scan_cells<<<1, 1024, 0, s>>>(ctx->bin_valid.as<uint32_t>(), g.nbins, ctx->bin_base.as<uint32_t>());
-            const size_t a_lds = (size_t)ngroups * 4 + (size_t)((nc + 31) / 32) * 4;
+            const size_t a_lds = (size_t)ngroups * 12 + (size_t)((nc + 31) / 32) * 4;
             if (a_lds > (size_t)ctx->lds_hist_max_cells * 4)
                 return set_err(MGP_E_INVALID, "too many cells for one context (grouping LDS)");
             if ((uint64_t)ctx->pay >= (1ull << GM_LCELL_SHIFT))
