@@ -326,7 +326,7 @@ constexpr unsigned long long GM_REV = 1ull << 56, GM_PAIRED = 2ull << 56, GM_MAP
 constexpr unsigned long long GM_LCELL_SHIFT = 50, GM_LCELL = 63ull << GM_LCELL_SHIFT;
 constexpr int kGroup = 64;
 #ifndef MGP_STAGE_A
-#define MGP_STAGE_A 1  // pass A: stage each step in LDS and write group runs
+#define MGP_STAGE_A 0  // pass A: stage each step in LDS and write group runs (measured slower)
 #endif
 constexpr int kStageA = 4 * kBlock;  // one step of pass A (kAhead * kBlock reads)
 
@@ -816,25 +816,44 @@ __device__ __forceinline__ void pile_read(bool has, const uint8_t* __restrict__ 
         uint32_t* base = tile - w.w0;
         const uint32_t Wp = (uint32_t)w.Wp;
         const uint32_t inc = strand_inc(strand);
-        const uint32_t fastbit = fast ? 1u : 0u;
         const int minbq = pc.min_baseq;
+        // wave-uniform choice: no lane with a second aligned block -> one-block body
+        if (__ballot(fast && a1 < b1) == 0ull) {
+            uint32_t* lb = base + dl0;
 #pragma unroll
-        for (int qq = 0; qq < kFastLen; ++qq) {
-            if (qq < wq_lo) continue;
-            if (qq >= wq_hi) break;
-            // branch-free predicate: one exec mask per base, a single branch around the atomic
-            const bool second = qq >= qs1;
-            const int d = second ? dl1 : dl0;
-            const int lo = second ? a1 : a0, hi = second ? b1 : b0;
-            const int qb = (int)(int8_t)((qw[qq >> 2] >> (8 * (qq & 3))) & 0xFFu);
-            const uint32_t code = (sw[qq >> 3] >> (8 * ((qq >> 1) & 3) + ((qq & 1) ? 0 : 4))) & 15u;
-            const uint32_t ok = (uint32_t)(qq >= lo) & (uint32_t)(qq < hi) & (uint32_t)(qb >= minbq) &
-                                ((kValid >> code) & 1u) & fastbit;
-            const uint32_t bi = (kLut2 >> (2 * code)) & 3u;
-            if (MGP_ABL == 2) {
-                if (ok & (uint32_t)(qb == 1234567)) atomicAdd(&base[__umul24(bi, Wp) + qq + d], inc);
-            } else if (ok) {
-                atomicAdd(&base[__umul24(bi, Wp) + qq + d], inc);
+            for (int qq = 0; qq < kFastLen; ++qq) {
+                if (qq < wq_lo) continue;
+                if (qq >= wq_hi) break;
+                const int qb = (int)(int8_t)((qw[qq >> 2] >> (8 * (qq & 3))) & 0xFFu);
+                const uint32_t code = (sw[qq >> 3] >> (8 * ((qq >> 1) & 3) + ((qq & 1) ? 0 : 4))) & 15u;
+                const uint32_t ok = (uint32_t)(qq >= a0) & (uint32_t)(qq < b0) & (uint32_t)(qb >= minbq) &
+                                    ((kValid >> code) & 1u);
+                const uint32_t bi = (kLut2 >> (2 * code)) & 3u;
+                if (MGP_ABL == 2) {
+                    if (ok & (uint32_t)(qb == 1234567)) atomicAdd(&lb[__umul24(bi, Wp) + qq], inc);
+                } else if (ok) {
+                    atomicAdd(&lb[__umul24(bi, Wp) + qq], inc);
+                }
+            }
+        } else {
+#pragma unroll
+            for (int qq = 0; qq < kFastLen; ++qq) {
+                if (qq < wq_lo) continue;
+                if (qq >= wq_hi) break;
+                // branch-free predicate: one exec mask per base, a single branch around the atomic
+                const bool second = qq >= qs1;
+                const int d = second ? dl1 : dl0;
+                const int lo = second ? a1 : a0, hi = second ? b1 : b0;
+                const int qb = (int)(int8_t)((qw[qq >> 2] >> (8 * (qq & 3))) & 0xFFu);
+                const uint32_t code = (sw[qq >> 3] >> (8 * ((qq >> 1) & 3) + ((qq & 1) ? 0 : 4))) & 15u;
+                const uint32_t ok = (uint32_t)(qq >= lo) & (uint32_t)(qq < hi) & (uint32_t)(qb >= minbq) &
+                                    ((kValid >> code) & 1u);
+                const uint32_t bi = (kLut2 >> (2 * code)) & 3u;
+                if (MGP_ABL == 2) {
+                    if (ok & (uint32_t)(qb == 1234567)) atomicAdd(&base[__umul24(bi, Wp) + qq + d], inc);
+                } else if (ok) {
+                    atomicAdd(&base[__umul24(bi, Wp) + qq + d], inc);
+                }
             }
         }
     }
