@@ -860,6 +860,9 @@ __device__ __forceinline__ void pile_read(bool has, const uint8_t* __restrict__ 
     if (has && !fast) pile_slow(rec, start, lseq, ncig, coff, strand, w, pc, tile, max_span, span_err);
 }
 
+#ifndef MGP_QPERM
+#define MGP_QPERM 0
+#endif
 #ifndef MGP_WIN
 #define MGP_WIN 1024  // target window width (positions); W <= kMaxPosPerThread * 256
 #endif
@@ -909,6 +912,9 @@ __global__ void __launch_bounds__(kBlock, MGP_PILEUP_WAVES) k_pileup(
     const int L = g.L;
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     unsigned long long* wq = wq_all[wid];
+    // queue slot piled by this lane: MGP_QPERM spreads neighbouring reads (often equal
+    // starts, hence equal LDS addresses) over the two 32-lane halves of an LDS access
+    const int qslot = MGP_QPERM ? (((lane & 31) << 1) | (lane >> 5)) : lane;
     const uint32_t max_span = st->max_span;
     const int R = (int)((max_span + g.G - 1) / g.G) * g.G;
     const int lo_bin = win_lo_bin(k, R, g);
@@ -1010,7 +1016,7 @@ __global__ void __launch_bounds__(kBlock, MGP_PILEUP_WAVES) k_pileup(
                 qn += (uint32_t)__popcll(bal);
                 __builtin_amdgcn_wave_barrier();
                 if (qn >= (uint32_t)kWave) {
-                    const unsigned long long qe = wq[lane];
+                    const unsigned long long qe = wq[qslot];
                     pile_read(true, payload + (qe & GM_OFF), w, pc, tile, t5, max_span, span_err);
                     qn -= kWave;
                     if ((uint32_t)lane < qn) wq[lane] = wq[kWave + lane];
@@ -1018,8 +1024,8 @@ __global__ void __launch_bounds__(kBlock, MGP_PILEUP_WAVES) k_pileup(
                 }
             }
             {   // tail: every lane of the wave enters, lanes past qn hold no read
-                const bool has = (uint32_t)lane < qn;
-                const unsigned long long qe = has ? wq[lane] : 0ull;
+                const bool has = (uint32_t)qslot < qn;
+                const unsigned long long qe = has ? wq[qslot] : 0ull;
                 pile_read(has, payload + (qe & GM_OFF), w, pc, tile, t5, max_span, span_err);
             }
             if (drained) {  // add this segment's packed tile into the 32-bit output rows
@@ -1184,90 +1190,22 @@ __global__ void __launch_bounds__(kBlock) k_gate_fixup(Geom g, int min_reads, co
         dmax[c] = 0;
     }
 }
-
-// Radix select of the k-th smallest (0-based) among vals[0..n) in LDS.
-__device__ uint32_t lds_select(const uint32_t* vals, uint32_t n, uint32_t kth, uint32_t* hist, uint32_t* sh) {
-    uint32_t prefix = 0, mask = 0;
-    for (int shift = 24; shift >= 0; shift -= 8) {
-        for (int x = threadIdx.x; x < 256; x += blockDim.x) hist[x] = 0;
-        __syncthreads();
-        for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
-            const uint32_t v = vals[i];
-            if ((v & mask) == prefix) atomicAdd(&hist[(v >> shift) & 255u], 1u);
-        }
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            uint32_t acc = 0, bsel = 255;
-            for (uint32_t b2 = 0; b2 < 256; ++b2) {
-                if (acc + hist[b2] > kth) {
-                    bsel = b2;
-                    break;
-                }
-                acc += hist[b2];
-            }
-            sh[0] = prefix | (bsel << shift);
-            sh[1] = kth - acc;
-        }
-        __syncthreads();
-        prefix = sh[0];
-        kth = sh[1];
-        mask |= 255u << shift;
-        __syncthreads();
-    }
-    return prefix;
-}
-
-constexpr int kMedBins = 8192;  // depth histogram bins in LDS (32 KiB)
-
-// k-th smallest (0-based) from an LDS histogram hist[0..nb): block scan over
-// per-thread bin ranges, then the owning thread walks its range.
-__device__ uint32_t hist_select(const uint32_t* hist, int nb, uint32_t kth, uint32_t* scratch) {
-    const int per = nb / kBlock;
-    const int b0 = threadIdx.x * per;
-    uint32_t mine = 0;
-    for (int b = 0; b < per; ++b) mine += hist[b0 + b];
-    // block exclusive scan of `mine`
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    uint32_t x = mine;
-    for (int o = 1; o < 64; o <<= 1) {
-        uint32_t y = __shfl_up(x, o, 64);
-        if (lane >= o) x += y;
-    }
-    if (lane == 63) scratch[wid] = x;
-    __syncthreads();
-    uint32_t woff = 0;
-    for (int w = 0; w < wid; ++w) woff += scratch[w];
-    const uint32_t excl = woff + x - mine;
-    if (kth >= excl && kth < excl + mine) {
-        uint32_t acc = excl;
-        for (int b = 0; b < per; ++b) {
-            const uint32_t h = hist[b0 + b];
-            if (kth < acc + h) {
-                scratch[4] = (uint32_t)(b0 + b);
-                break;
-            }
-            acc += h;
-        }
-    }
-    __syncthreads();
-    const uint32_t r = scratch[4];
-    __syncthreads();
-    return r;
-}
-
 // One workgroup per cell: pass flag and the two middle order statistics of the
-// covered depths (np.median, writers.py:190). Depth histogram in LDS when the
-// cell's max depth fits kMedBins, radix select over the depth row otherwise.
+// covered depths (np.median, writers.py:190). The depth row sits in registers
+// (65 values per thread at L = 16569); each order statistic is found by a binary
+// search over the value range [1, max depth]: count(depth <= x) per thread, one
+// block reduction per step, both statistics searched in the same steps. No
+// atomics and no histogram, whatever the depths.
+constexpr int kMedRegs = 72;  // register-resident depths per thread (L <= 18432)
+
+template <bool kRegs>
 __global__ void __launch_bounds__(kBlock) k_median(Geom g, int min_reads, const uint32_t* __restrict__ depth,
                                                    const uint32_t* __restrict__ n_reads,
                                                    const uint32_t* __restrict__ covered,
                                                    const uint32_t* __restrict__ dmax,
                                                    uint32_t* __restrict__ med_lo, uint32_t* __restrict__ med_hi,
                                                    uint8_t* __restrict__ passed, DevStats* st) {
-    extern __shared__ uint32_t vals[];  // [max(L, kMedBins)]
-    __shared__ uint32_t hist[256];
-    __shared__ uint32_t sh[8];
-    __shared__ uint32_t cnt;
+    __shared__ uint32_t red[2][kBlock / kWave];
     const int c = blockIdx.x;
     const uint32_t n = covered[c];
     const uint32_t nr = n_reads[c];
@@ -1285,31 +1223,68 @@ __global__ void __launch_bounds__(kBlock) k_median(Geom g, int min_reads, const 
         return;
     }
     const uint32_t* drow = depth + (size_t)c * g.L;
-    uint32_t lo, hi;
-    if (dmax[c] < (uint32_t)kMedBins) {
-        for (int b = threadIdx.x; b < kMedBins; b += blockDim.x) vals[b] = 0;
-        __syncthreads();
-        for (int p = threadIdx.x; p < g.L; p += blockDim.x) {
-            const uint32_t d = drow[p];
-            if (d) atomicAdd(&vals[d], 1u);
+    const int L = g.L;
+    uint32_t v[kRegs ? kMedRegs : 1];
+    if (kRegs) {
+#pragma unroll
+        for (int k = 0; k < kMedRegs; ++k) {
+            const int p = threadIdx.x + k * kBlock;
+            v[k] = p < L ? drow[p] : 0u;
+        }
+    }
+    // zero depths sort first: the k-th covered value is the (zeros + k)-th overall
+    const uint32_t zeros = (uint32_t)L - n;
+    const uint32_t t_lo = zeros + (n - 1) / 2 + 1, t_hi = zeros + n / 2 + 1;  // counts to reach
+    uint32_t lo0 = 1, lo1 = dmax[c], hi0 = 1, hi1 = dmax[c];  // answers lie in [x0, x1]
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    while (lo0 < lo1 || hi0 < hi1) {
+        const uint32_t ml = lo0 + (lo1 - lo0) / 2, mh = hi0 + (hi1 - hi0) / 2;
+        uint32_t cl = 0, ch = 0;
+        if (kRegs) {
+#pragma unroll
+            for (int k = 0; k < kMedRegs; ++k) {
+                cl += v[k] <= ml;
+                ch += v[k] <= mh;
+            }
+            // padding lanes past L hold 0 and were counted as zeros: remove them
+            const uint32_t pad = (uint32_t)(kMedRegs * kBlock - L);
+            if (threadIdx.x == 0) {
+                cl -= pad;
+                ch -= pad;
+            }
+        } else {
+            for (int p = threadIdx.x; p < L; p += kBlock) {
+                const uint32_t d = drow[p];
+                cl += d <= ml;
+                ch += d <= mh;
+            }
+        }
+        cl = wave_sum(cl);
+        ch = wave_sum(ch);
+        if (lane == 0) {
+            red[0][wid] = cl;
+            red[1][wid] = ch;
         }
         __syncthreads();
-        lo = hist_select(vals, kMedBins, (n - 1) / 2, sh);
-        hi = (n & 1) ? lo : hist_select(vals, kMedBins, n / 2, sh);
-    } else {
-        if (threadIdx.x == 0) cnt = 0;
-        __syncthreads();
-        for (int p = threadIdx.x; p < g.L; p += blockDim.x) {
-            const uint32_t d = drow[p];
-            if (d) vals[atomicAdd(&cnt, 1u)] = d;
+        uint32_t sl = 0, shh = 0;
+#pragma unroll
+        for (int w = 0; w < kBlock / kWave; ++w) {
+            sl += red[0][w];
+            shh += red[1][w];
         }
         __syncthreads();
-        lo = lds_select(vals, n, (n - 1) / 2, hist, sh);
-        hi = (n & 1) ? lo : lds_select(vals, n, n / 2, hist, sh);
+        if (lo0 < lo1) {
+            if (sl >= t_lo) lo1 = ml;
+            else lo0 = ml + 1;
+        }
+        if (hi0 < hi1) {
+            if (shh >= t_hi) hi1 = mh;
+            else hi0 = mh + 1;
+        }
     }
     if (threadIdx.x == 0) {
-        med_lo[c] = lo;
-        med_hi[c] = hi;
+        med_lo[c] = lo0;
+        med_hi[c] = hi0;
         passed[c] = 1;
         atomicAdd(&st->cells_passed, 1ull);
     }
@@ -1409,7 +1384,6 @@ int mgp_open(const mgp_config* cfg, int hip_device, mgp_ctx** out) {
     // best effort: the runtime may already allow it without the attribute
     {
         const int lds_max = (int)prop.sharedMemPerBlock;
-        (void)hipFuncSetAttribute((const void*)k_median, hipFuncAttributeMaxDynamicSharedMemorySize, lds_max);
         (void)hipFuncSetAttribute((const void*)k_bin_count<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                   lds_max);
         (void)hipFuncSetAttribute((const void*)k_group_a, hipFuncAttributeMaxDynamicSharedMemorySize, lds_max);
@@ -1691,7 +1665,15 @@ int mgp_run(mgp_ctx* ctx) {
 
         // 7. medians + pass flags
         STAGE_BEGIN(ST_MEDIAN);
-        k_median<<<nc, kBlock, (size_t)std::max(g.L, kMedBins) * 4, s>>>(
+        if (g.L <= kMedRegs * kBlock)
+            k_median<true><<<nc, kBlock, 0, s>>>(
+                                                     g, ctx->cfg.min_reads, ctx->depth.as<uint32_t>(),
+                                                     ctx->n_reads.as<uint32_t>(), ctx->covered.as<uint32_t>(),
+                                                     ctx->dmax.as<uint32_t>(),
+                                                     ctx->med_lo.as<uint32_t>(), ctx->med_hi.as<uint32_t>(),
+                                                     ctx->passed.as<uint8_t>(), st);
+        else
+            k_median<false><<<nc, kBlock, 0, s>>>(
                                                      g, ctx->cfg.min_reads, ctx->depth.as<uint32_t>(),
                                                      ctx->n_reads.as<uint32_t>(), ctx->covered.as<uint32_t>(),
                                                      ctx->dmax.as<uint32_t>(),
