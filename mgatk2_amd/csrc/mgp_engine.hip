@@ -192,16 +192,34 @@ __global__ void __launch_bounds__(kBlock) k_bin_count(const int32_t* __restrict_
     uint32_t mspan = 0;
     unsigned long long nvalid = 0;
     bool badbc = false, unsorted = false;
-    for (int64_t i = lo + threadIdx.x; i < hi; i += blockDim.x) {
-        const int c = bc[i];
-        const uint16_t f = flag[i];
-        if (i > 0 && start[i] < start[i - 1]) unsorted = true;
-        badbc |= (c >= nc);
-        if (read_valid(c, f, nc)) {
-            atomicAdd(&cnt[c], 1u);
-            const uint32_t sp = span[i];
-            mspan = sp > mspan ? sp : mspan;
-            ++nvalid;
+    // 4 reads per thread per step, loads issued together (clamped index, no branches)
+    constexpr int kU = 4;
+    for (int64_t i0 = lo + threadIdx.x; i0 < hi; i0 += kU * kBlock) {
+        int cc[kU], ss[kU], sp0[kU];
+        uint32_t sp[kU];
+        uint32_t ff[kU];
+#pragma unroll
+        for (int u = 0; u < kU; ++u) {
+            const int64_t i = i0 + u * kBlock;
+            const int64_t j = i < hi ? i : hi - 1;
+            cc[u] = bc[j];
+            ff[u] = flag[j];
+            ss[u] = start[j];
+            sp0[u] = start[j > 0 ? j - 1 : 0];
+            sp[u] = span[j];
+        }
+#pragma unroll
+        for (int u = 0; u < kU; ++u) {
+            const int64_t i = i0 + u * kBlock;
+            if (i >= hi) break;
+            const int c = cc[u];
+            if (i > 0 && ss[u] < sp0[u]) unsorted = true;
+            badbc |= (c >= nc);
+            if (read_valid(c, (uint16_t)ff[u], nc)) {
+                atomicAdd(&cnt[c], 1u);
+                mspan = sp[u] > mspan ? sp[u] : mspan;
+                ++nvalid;
+            }
         }
     }
     if (kLds) {
