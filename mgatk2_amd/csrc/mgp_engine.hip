@@ -703,9 +703,16 @@ __device__ void pile_slow(const uint8_t* __restrict__ rec, int32_t start, uint32
     if (max(ref - (int64_t)start, (int64_t)lseq) > (int64_t)max_span) span_err = true;
 }
 
+#ifndef MGP_QPERM
+#define MGP_QPERM 0
+#endif
+#ifndef MGP_WIN
+#define MGP_WIN 1024  // target window width (positions); W <= kMaxPosPerThread * 256
+#endif
+constexpr int kMaxPosPerThread = MGP_WIN / 256;
+constexpr int kTilePitch = MGP_WIN;  // u32 per tile plane (>= the window width W)
 constexpr int kFastLen = 64;   // reads up to 64 bases with <= 4 CIGAR ops and <= 2 aligned blocks
 constexpr int kFastCig = 4;
-constexpr uint32_t kLut2 = 0x30210u;   // 4-bit BAM code -> base index (1->0 A, 2->1 C, 4->2 G, 8->3 T)
 constexpr uint32_t kValid = 0x0116u;   // codes 1, 2, 4, 8 are counted (pileup.py:83-86)
 
 // One read per lane, entered by EVERY lane of the wave (has = lane holds a read):
@@ -832,32 +839,50 @@ __device__ __forceinline__ void pile_read(bool has, const uint8_t* __restrict__ 
         }
         const uint32_t sw[kFastLen / 8] = {sv[0].x, sv[0].y, sv[0].z, sv[0].w, sv[1].x, sv[1].y, sv[1].z, sv[1].w};
         uint32_t* base = tile - w.w0;
-        const uint32_t Wp = (uint32_t)w.Wp;
         const uint32_t inc = strand_inc(strand);
         const int minbq = pc.min_baseq;
-        // wave-uniform choice: no lane with a second aligned block -> one-block body
-        if (__ballot(fast && a1 < b1) == 0ull) {
+        // base index = log2(code) for the counted codes 1, 2, 4, 8 (A, C, G, T); the
+        // plane offset is a shift of it (compile-time pitch)
+        constexpr int kPitchShift = __builtin_ctz(kTilePitch);
+        const bool one_block = __ballot(fast && a1 < b1) == 0ull;
+        // common case: every lane of the wave has the same single counted range
+        // [a0, b0) (all reads inside the window, same length): no range test
+        const int ua0 = __builtin_amdgcn_readfirstlane(a0), ub0 = __builtin_amdgcn_readfirstlane(b0);
+        const bool uniform = one_block && __ballot(!(fast && a0 == ua0 && b0 == ub0)) == 0ull;
+        // iterations run: a wave-uniform 64-bit mask (one scalar bit test per base)
+        auto range_mask = [](int lo, int hi) -> unsigned long long {
+            const unsigned long long h = hi >= 64 ? ~0ull : ((1ull << hi) - 1ull);
+            const unsigned long long l = lo >= 64 ? ~0ull : ((1ull << lo) - 1ull);
+            return lo < hi ? (h & ~l) : 0ull;
+        };
+        if (uniform) {
             uint32_t* lb = base + dl0;
+            const unsigned long long smask = range_mask(ua0, ub0);
 #pragma unroll
             for (int qq = 0; qq < kFastLen; ++qq) {
-                if (qq < wq_lo) continue;
-                if (qq >= wq_hi) break;
+                if (!((smask >> qq) & 1ull)) continue;
+                const int qb = (int)(int8_t)((qw[qq >> 2] >> (8 * (qq & 3))) & 0xFFu);
+                const uint32_t code = (sw[qq >> 3] >> (8 * ((qq >> 1) & 3) + ((qq & 1) ? 0 : 4))) & 15u;
+                const uint32_t ok = (uint32_t)(qb >= minbq) & ((kValid >> code) & 1u);
+                if (ok) atomicAdd(&lb[((uint32_t)__builtin_ctz(code) << kPitchShift) + qq], inc);
+            }
+        } else if (one_block) {
+            uint32_t* lb = base + dl0;
+            const unsigned long long smask = range_mask(wq_lo, wq_hi);
+#pragma unroll
+            for (int qq = 0; qq < kFastLen; ++qq) {
+                if (!((smask >> qq) & 1ull)) continue;
                 const int qb = (int)(int8_t)((qw[qq >> 2] >> (8 * (qq & 3))) & 0xFFu);
                 const uint32_t code = (sw[qq >> 3] >> (8 * ((qq >> 1) & 3) + ((qq & 1) ? 0 : 4))) & 15u;
                 const uint32_t ok = (uint32_t)(qq >= a0) & (uint32_t)(qq < b0) & (uint32_t)(qb >= minbq) &
                                     ((kValid >> code) & 1u);
-                const uint32_t bi = (kLut2 >> (2 * code)) & 3u;
-                if (MGP_ABL == 2) {
-                    if (ok & (uint32_t)(qb == 1234567)) atomicAdd(&lb[__umul24(bi, Wp) + qq], inc);
-                } else if (ok) {
-                    atomicAdd(&lb[__umul24(bi, Wp) + qq], inc);
-                }
+                if (ok) atomicAdd(&lb[((uint32_t)__builtin_ctz(code) << kPitchShift) + qq], inc);
             }
         } else {
+            const unsigned long long smask = range_mask(wq_lo, wq_hi);
 #pragma unroll
             for (int qq = 0; qq < kFastLen; ++qq) {
-                if (qq < wq_lo) continue;
-                if (qq >= wq_hi) break;
+                if (!((smask >> qq) & 1ull)) continue;
                 // branch-free predicate: one exec mask per base, a single branch around the atomic
                 const bool second = qq >= qs1;
                 const int d = second ? dl1 : dl0;
@@ -866,25 +891,13 @@ __device__ __forceinline__ void pile_read(bool has, const uint8_t* __restrict__ 
                 const uint32_t code = (sw[qq >> 3] >> (8 * ((qq >> 1) & 3) + ((qq & 1) ? 0 : 4))) & 15u;
                 const uint32_t ok = (uint32_t)(qq >= lo) & (uint32_t)(qq < hi) & (uint32_t)(qb >= minbq) &
                                     ((kValid >> code) & 1u);
-                const uint32_t bi = (kLut2 >> (2 * code)) & 3u;
-                if (MGP_ABL == 2) {
-                    if (ok & (uint32_t)(qb == 1234567)) atomicAdd(&base[__umul24(bi, Wp) + qq + d], inc);
-                } else if (ok) {
-                    atomicAdd(&base[__umul24(bi, Wp) + qq + d], inc);
-                }
+                if (ok) atomicAdd(&base[((uint32_t)__builtin_ctz(code) << kPitchShift) + qq + d], inc);
             }
         }
     }
     if (has && !fast) pile_slow(rec, start, lseq, ncig, coff, strand, w, pc, tile, max_span, span_err);
 }
 
-#ifndef MGP_QPERM
-#define MGP_QPERM 0
-#endif
-#ifndef MGP_WIN
-#define MGP_WIN 1024  // target window width (positions); W <= kMaxPosPerThread * 256
-#endif
-constexpr int kMaxPosPerThread = MGP_WIN / 256;
 constexpr int kWaveQ = 2 * kWave;    // per-wave queue of reads waiting to be piled (LDS)
 constexpr uint32_t kSeg = 65535;     // elements per tile segment (16-bit halves cannot carry)
 
@@ -1339,12 +1352,9 @@ static int configure_geometry(mgp_ctx* ctx) {
     g.W = ((g.W + g.G - 1) / g.G) * g.G;   // multiple of the bin width
     g.nwin = (g.L + g.W - 1) / g.W;
     if (g.W > kMaxPosPerThread * kBlock) return set_err(MGP_E_INVALID, "window too wide");
-#ifndef MGP_WP_ALIGN
-#define MGP_WP_ALIGN 0
-#endif
-    // plane pitch: with a multiple of 32 the 4 base planes share the bank map
-    // (bank = position mod 32), so lanes at distinct positions never conflict
-    g.Wp = MGP_WP_ALIGN ? (g.W + MGP_WP_ALIGN - 1) / MGP_WP_ALIGN * MGP_WP_ALIGN : (g.W | 1);
+    // plane pitch of the pileup tile: a compile-time power of two, so a base's plane
+    // offset is a shift folded into the address add (A/B: no bank-conflict cost)
+    g.Wp = kTilePitch;
     g.nc = c.n_cells;
     // cells per pileup workgroup: ~4096 workgroups over the windows
     int64_t target = 4096;
