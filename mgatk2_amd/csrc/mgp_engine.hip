@@ -933,6 +933,8 @@ __global__ void __launch_bounds__(kBlock, MGP_PILEUP_WAVES) k_pileup(
     __shared__ uint32_t r_cov[4], r_max[4], r_keep[4];
     __shared__ unsigned long long r_sum[4];
     __shared__ int r_pair[4];
+    __shared__ uint32_t r_qn[kBlock / kWave];
+    __shared__ unsigned long long cq[kBlock];  // pooled queue residues of the 4 waves
 
     const int k = blockIdx.y;
     const int chunk = blockIdx.x;
@@ -964,11 +966,18 @@ __global__ void __launch_bounds__(kBlock, MGP_PILEUP_WAVES) k_pileup(
         for (int b = 0; b < 4; ++b) tal[m][b] = 0;
 
     const int c0 = chunk * g.cpb, c1 = min(nc, c0 + g.cpb);
+    // element ranges of the next cell are loaded one cell ahead
+    uint32_t n_lo = c0 < c1 ? O[(size_t)lo_bin * nc + c0] : 0u;
+    uint32_t n_own = c0 < c1 ? O[(size_t)own_bin * nc + c0] : 0u;
+    uint32_t n_hi = c0 < c1 ? O[(size_t)hi_bin * nc + c0] : 0u;
     for (int c = c0; c < c1; ++c) {
         for (int x = threadIdx.x; x < 5 * g.Wp; x += blockDim.x) tile[x] = 0;
-        const uint32_t lo = O[(size_t)lo_bin * nc + c];
-        const uint32_t own = O[(size_t)own_bin * nc + c];
-        const uint32_t hi = O[(size_t)hi_bin * nc + c];
+        const uint32_t lo = n_lo, own = n_own, hi = n_hi;
+        if (c + 1 < c1) {
+            n_lo = O[(size_t)lo_bin * nc + c + 1];
+            n_own = O[(size_t)own_bin * nc + c + 1];
+            n_hi = O[(size_t)hi_bin * nc + c + 1];
+        }
         const bool drained = hi - lo > kSeg;  // tile drained into the output rows between segments
         uint32_t nkeep = 0;
         bool paired = false;
@@ -1054,10 +1063,24 @@ __global__ void __launch_bounds__(kBlock, MGP_PILEUP_WAVES) k_pileup(
                     __builtin_amdgcn_wave_barrier();
                 }
             }
-            {   // tail: every lane of the wave enters, lanes past qn hold no read
-                const bool has = (uint32_t)qslot < qn;
-                const unsigned long long qe = has ? wq[qslot] : 0ull;
-                pile_read(has, payload + (qe & GM_OFF), w, pc, tile, t5, max_span, span_err);
+            {   // tails: the waves' residues (< 64 each) are pooled and piled by as few
+                // waves as they fill (every lane of a piling wave enters pile_read)
+                if (lane == 0) r_qn[wid] = qn;
+                __syncthreads();
+                uint32_t off = 0, tot = 0;
+#pragma unroll
+                for (int x = 0; x < kBlock / kWave; ++x) {
+                    off += x < wid ? r_qn[x] : 0u;
+                    tot += r_qn[x];
+                }
+                if ((uint32_t)lane < qn) cq[off + lane] = wq[lane];
+                __syncthreads();
+                if ((uint32_t)(wid * kWave) < tot) {
+                    const uint32_t k = (uint32_t)(wid * kWave + qslot);
+                    const bool has = k < tot;
+                    const unsigned long long qe = has ? cq[k] : 0ull;
+                    pile_read(has, payload + (qe & GM_OFF), w, pc, tile, t5, max_span, span_err);
+                }
             }
             if (drained) {  // add this segment's packed tile into the 32-bit output rows
                 __syncthreads();
