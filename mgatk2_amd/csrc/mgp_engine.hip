@@ -933,8 +933,6 @@ __global__ void __launch_bounds__(kBlock, MGP_PILEUP_WAVES) k_pileup(
     __shared__ uint32_t r_cov[4], r_max[4], r_keep[4];
     __shared__ unsigned long long r_sum[4];
     __shared__ int r_pair[4];
-    __shared__ uint32_t r_qn[kBlock / kWave];
-    __shared__ unsigned long long cq[kBlock];  // pooled queue residues of the 4 waves
 
     const int k = blockIdx.y;
     const int chunk = blockIdx.x;
@@ -1063,24 +1061,10 @@ __global__ void __launch_bounds__(kBlock, MGP_PILEUP_WAVES) k_pileup(
                     __builtin_amdgcn_wave_barrier();
                 }
             }
-            {   // tails: the waves' residues (< 64 each) are pooled and piled by as few
-                // waves as they fill (every lane of a piling wave enters pile_read)
-                if (lane == 0) r_qn[wid] = qn;
-                __syncthreads();
-                uint32_t off = 0, tot = 0;
-#pragma unroll
-                for (int x = 0; x < kBlock / kWave; ++x) {
-                    off += x < wid ? r_qn[x] : 0u;
-                    tot += r_qn[x];
-                }
-                if ((uint32_t)lane < qn) cq[off + lane] = wq[lane];
-                __syncthreads();
-                if ((uint32_t)(wid * kWave) < tot) {
-                    const uint32_t k = (uint32_t)(wid * kWave + qslot);
-                    const bool has = k < tot;
-                    const unsigned long long qe = has ? cq[k] : 0ull;
-                    pile_read(has, payload + (qe & GM_OFF), w, pc, tile, t5, max_span, span_err);
-                }
+            {   // tail: every lane of the wave enters, lanes past qn hold no read
+                const bool has = (uint32_t)qslot < qn;
+                const unsigned long long qe = has ? wq[qslot] : 0ull;
+                pile_read(has, payload + (qe & GM_OFF), w, pc, tile, t5, max_span, span_err);
             }
             if (drained) {  // add this segment's packed tile into the 32-bit output rows
                 __syncthreads();
