@@ -703,6 +703,9 @@ __device__ void pile_slow(const uint8_t* __restrict__ rec, int32_t start, uint32
     if (max(ref - (int64_t)start, (int64_t)lseq) > (int64_t)max_span) span_err = true;
 }
 
+#ifndef MGP_PIPE
+#define MGP_PIPE 0  // pileup: load a batch's records one batch ahead (needs MGP_PILEUP_WAVES=3)
+#endif
 #ifndef MGP_QPERM
 #define MGP_QPERM 0
 #endif
@@ -728,37 +731,61 @@ constexpr uint32_t kValid = 0x0116u;   // codes 1, 2, 4, 8 are counted (pileup.p
 #ifndef MGP_ABL
 #define MGP_ABL 0  // ablation switch for experiments: 0 = real kernel
 #endif
+// The first 128-byte line of a record in registers: header, qual (+16), seq (+80)
+// and CIGAR (+112) of a read of <= 64 bases with <= 4 operations
+// (include/mgpileup.h); no load depends on another.
+struct RecLine {
+    uint4 h, qv[4], sv[2], cv;
+};
+
+__device__ __forceinline__ void load_line(bool has, const uint8_t* __restrict__ rec, const Win& w, RecLine& R) {
+    R.h = make_uint4(0, 0, 0, 0);
+    R.cv = make_uint4(0, 0, 0, 0);
+    if (MGP_ABL == 3) {
+        // synthetic read from the record address only: no payload loads
+        const uint32_t x = (uint32_t)(reinterpret_cast<uintptr_t>(rec) >> 4);
+        R.h = make_uint4((uint32_t)w.w0 + (x * 7u) % (uint32_t)w.wlen, 50u,
+                         1u | (x & 1u ? (MGP_FLAG_REVERSE << 16) : 0u), 112u);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) R.qv[k] = make_uint4(0x25252525u, 0x25252525u, 0x25252525u, 0x25252525u);
+#pragma unroll
+        for (int k = 0; k < 2; ++k) R.sv[k] = make_uint4(0x12481248u, 0x24812481u, 0x48124812u, 0x81248124u);
+        R.cv.x = 50u << 4;
+    } else if (has) {
+        const uint4* r4 = reinterpret_cast<const uint4*>(rec);
+        R.h = r4[0];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) R.qv[k] = r4[1 + k];
+        R.sv[0] = r4[5];
+        R.sv[1] = r4[6];
+        R.cv = r4[7];
+    } else {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) R.qv[k] = make_uint4(0, 0, 0, 0);
+        R.sv[0] = R.sv[1] = make_uint4(0, 0, 0, 0);
+    }
+}
+
+__device__ __forceinline__ void pile_line(bool has, const uint8_t* __restrict__ rec, const RecLine& R,
+                                          const Win& w, const PileCfg& pc, uint32_t* tile, uint32_t* t5,
+                                          uint32_t max_span, bool& span_err);
+
 __device__ __forceinline__ void pile_read(bool has, const uint8_t* __restrict__ rec, const Win& w,
                                           const PileCfg& pc, uint32_t* tile, uint32_t* t5, uint32_t max_span,
                                           bool& span_err) {
     if (MGP_ABL == 1) return;
-    // the whole first 128-byte line of the record in one go: header, qual (+16),
-    // seq (+80) and CIGAR (+112) of a read of <= 64 bases with <= 4 operations
-    // (include/mgpileup.h); no load depends on another
-    uint4 h = make_uint4(0, 0, 0, 0);
-    uint4 qv[4], sv[2], cv = make_uint4(0, 0, 0, 0);
-    if (MGP_ABL == 3) {
-        // synthetic read from the record address only: no payload loads
-        const uint32_t x = (uint32_t)(reinterpret_cast<uintptr_t>(rec) >> 4);
-        h = make_uint4((uint32_t)w.w0 + (x * 7u) % (uint32_t)w.wlen, 50u, 1u | (x & 1u ? (MGP_FLAG_REVERSE << 16) : 0u), 112u);
-#pragma unroll
-        for (int k = 0; k < 4; ++k) qv[k] = make_uint4(0x25252525u, 0x25252525u, 0x25252525u, 0x25252525u);
-#pragma unroll
-        for (int k = 0; k < 2; ++k) sv[k] = make_uint4(0x12481248u, 0x24812481u, 0x48124812u, 0x81248124u);
-        cv.x = 50u << 4;
-    } else if (has) {
-        const uint4* r4 = reinterpret_cast<const uint4*>(rec);
-        h = r4[0];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) qv[k] = r4[1 + k];
-        sv[0] = r4[5];
-        sv[1] = r4[6];
-        cv = r4[7];
-    } else {
-#pragma unroll
-        for (int k = 0; k < 4; ++k) qv[k] = make_uint4(0, 0, 0, 0);
-        sv[0] = sv[1] = make_uint4(0, 0, 0, 0);
-    }
+    RecLine R;
+    load_line(has, rec, w, R);
+    pile_line(has, rec, R, w, pc, tile, t5, max_span, span_err);
+}
+
+__device__ __forceinline__ void pile_line(bool has, const uint8_t* __restrict__ rec, const RecLine& R,
+                                          const Win& w, const PileCfg& pc, uint32_t* tile, uint32_t* t5,
+                                          uint32_t max_span, bool& span_err) {
+    if (MGP_ABL == 1) return;
+    const uint4 h = R.h, cv = R.cv;
+    const uint4* qv = R.qv;
+    const uint4* sv = R.sv;
     const int32_t start = (int32_t)h.x;
     const uint32_t lseq = h.y;
     const uint32_t ncig = h.z & 0xFFFFu;
@@ -983,6 +1010,9 @@ __global__ void __launch_bounds__(kBlock, MGP_PILEUP_WAVES) k_pileup(
         for (uint32_t seg = lo; seg < hi; seg += kSeg) {
             const uint32_t seg_hi = min(hi, seg + kSeg);
             uint32_t qn = 0;  // wave-uniform queue fill
+            bool pend = false;  // MGP_PIPE: a loaded batch waits in PR
+            RecLine PR;
+            const uint8_t* pend_rec = payload;
             for (uint32_t cb = seg + kWave * wid; cb < seg_hi; cb += kBlock) {
                 const uint32_t j = cb + lane;
                 const bool act = j < seg_hi;
@@ -1055,11 +1085,24 @@ __global__ void __launch_bounds__(kBlock, MGP_PILEUP_WAVES) k_pileup(
                 __builtin_amdgcn_wave_barrier();
                 if (qn >= (uint32_t)kWave) {
                     const unsigned long long qe = wq[qslot];
-                    pile_read(true, payload + (qe & GM_OFF), w, pc, tile, t5, max_span, span_err);
+                    if (MGP_PIPE) {
+                        // the batch's record lines are loaded now and piled at the next full
+                        // batch (or the tail): their latency overlaps the next chunks' work
+                        if (pend) pile_line(true, pend_rec, PR, w, pc, tile, t5, max_span, span_err);
+                        pend_rec = payload + (qe & GM_OFF);
+                        load_line(true, pend_rec, w, PR);
+                        pend = true;
+                    } else {
+                        pile_read(true, payload + (qe & GM_OFF), w, pc, tile, t5, max_span, span_err);
+                    }
                     qn -= kWave;
                     if ((uint32_t)lane < qn) wq[lane] = wq[kWave + lane];
                     __builtin_amdgcn_wave_barrier();
                 }
+            }
+            if (MGP_PIPE && pend) {
+                pile_line(true, pend_rec, PR, w, pc, tile, t5, max_span, span_err);
+                pend = false;
             }
             {   // tail: every lane of the wave enters, lanes past qn hold no read
                 const bool has = (uint32_t)qslot < qn;
