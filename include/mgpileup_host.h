@@ -91,6 +91,16 @@ int mgp_txt_write_cells(const char *prefix, const uint32_t *counts, const uint32
                         const int64_t *cells, int64_t n_write, const char *const *names, int level,
                         int n_threads, int append);
 
+/* Write an engine batch as a coordinate-sorted BAM (test and benchmark inputs; the
+ * inverse of mgp_bam_read_ref). References `ref_names`/`ref_lens`; every record goes
+ * to reference `tid`. Record i carries `tag`:Z:barcodes[bc[i]] when bc[i] >= 0;
+ * records with bc < 0 alternate between `unlisted` (if not NULL) and no tag.
+ * BGZF blocks are deflated at `level` on `n_threads` threads; `write_index` also
+ * writes `<path>.bai`. */
+int mgp_bam_write(const char *path, const char *const *ref_names, const int64_t *ref_lens, int n_ref, int tid,
+                  const mgp_bam_batch *batch, const char *const *barcodes, int n_barcodes, const char *tag,
+                  const char *unlisted, int level, int n_threads, int write_index);
+
 /* HDF5 output at scale (IncrementalHDF5Writer, src/file_io/writers.py:60-406):
  * deflates every (crow x ccol) chunk of a row-major `rows x cols` array of
  * `elem_size`-byte elements, in the form of the HDF5 deflate filter (zlib

@@ -45,6 +45,17 @@ class mgp_bam_batch(C.Structure):
 _hlib = None
 
 
+def host_threads() -> int:
+    """Host worker threads: MGP_HOST_THREADS, else OMP_NUM_THREADS, else min(cpus, 16)."""
+    import os
+
+    for var in ("MGP_HOST_THREADS", "OMP_NUM_THREADS"):
+        v = os.environ.get(var)
+        if v and v.isdigit() and int(v) > 0:
+            return int(v)
+    return max(1, min(os.cpu_count() or 1, 16))
+
+
 def host_library() -> C.CDLL:
     global _hlib
     if _hlib is None:
@@ -80,6 +91,9 @@ def host_library() -> C.CDLL:
         lib.mgp_deflate_tiles.argtypes = [vp, C.c_int64, C.c_int64, C.c_int32, C.c_int64, C.c_int64, C.c_int, C.c_int,
                                           C.POINTER(C.POINTER(C.c_uint8)), vp]
         lib.mgp_deflate_tiles.restype = C.c_int64
+        lib.mgp_bam_write.argtypes = [C.c_char_p, C.POINTER(C.c_char_p), C.POINTER(C.c_int64), C.c_int, C.c_int,
+                                      C.POINTER(mgp_bam_batch), C.POINTER(C.c_char_p), C.c_int, C.c_char_p,
+                                      C.c_char_p, C.c_int, C.c_int, C.c_int]
         lib.mgp_host_buf_free.argtypes = [vp]
         lib.mgp_host_buf_free.restype = None
         _hlib = lib
@@ -97,7 +111,7 @@ class BamFile:
         self.lib = host_library()
         self.path = str(path)
         h = C.c_void_p()
-        if self.lib.mgp_bam_open(self.path.encode(), int(n_threads), C.byref(h)) != 0:
+        if self.lib.mgp_bam_open(self.path.encode(), int(n_threads or host_threads()), C.byref(h)) != 0:
             raise BAMFormatError(self.path, f"Cannot open: {_err()}")
         self._h = h
         n = self.lib.mgp_bam_n_refs(h)
@@ -203,7 +217,7 @@ def txt_write_cells(prefix: str | Path, counts: np.ndarray, depth: np.ndarray, c
         raise ValueError("one name per written cell")
     arr = (C.c_char_p * max(1, len(names)))(*[n.encode() for n in names])
     rc = lib.mgp_txt_write_cells(str(prefix).encode(), counts.ctypes.data, depth.ctypes.data, L, cells.ctypes.data,
-                                 cells.size, arr, int(level), int(n_threads), 1 if append else 0)
+                                 cells.size, arr, int(level), int(n_threads or host_threads()), 1 if append else 0)
     if rc != 0:
         raise OSError(_err())
 
@@ -218,7 +232,7 @@ def deflate_tiles(a: np.ndarray, chunks: tuple[int, int], level: int = 4, n_thre
     offs = np.zeros(nr * nc + 1, np.int64)
     blob = C.POINTER(C.c_uint8)()
     n = lib.mgp_deflate_tiles(a.ctypes.data, rows, cols, a.dtype.itemsize, chunks[0], chunks[1], int(level),
-                              int(n_threads), C.byref(blob), offs.ctypes.data)
+                              int(n_threads or host_threads()), C.byref(blob), offs.ctypes.data)
     if n < 0:
         raise OSError(_err())
     try:
@@ -367,6 +381,29 @@ def write_bai(path: Path, n_ref: int, records: list[tuple[int, int, int, int, in
             last = ref["lin"].get(w, last)
             out += struct.pack("<Q", last)
     Path(path).write_bytes(bytes(out))
+
+
+def write_bam(path: str | Path, soa: ReadSoA, whitelist: list[str], contig: str = "chrM", mito_len: int = 16569,
+              index: bool = True, tag: str = "CB", level: int = 1, n_threads: int = 0,
+              unlisted: str | None = "NNNNNNNNNNNNNNNN-9") -> None:
+    """Native BAM writer (libmgphost.so `mgp_bam_write`): same records as
+    :func:`soa_to_bam`, BGZF deflated on a thread pool; for large inputs."""
+    lib = host_library()
+    refs = [("chr1", 248956422), (contig, mito_len)]
+    names = (C.c_char_p * 2)(*[n.encode() for n, _ in refs])
+    lens = (C.c_int64 * 2)(*[ln for _, ln in refs])
+    arrs = [np.ascontiguousarray(a) for a in (soa.start, soa.bc, soa.tlen, soa.flag, soa.mapq, soa.span,
+                                                  soa.rec_off, soa.payload)]
+    b = mgp_bam_batch(soa.n, *[C.cast(a.ctypes.data, t) for a, t in zip(arrs, (
+        C.POINTER(C.c_int32), C.POINTER(C.c_int32), C.POINTER(C.c_int32), C.POINTER(C.c_uint16),
+        C.POINTER(C.c_uint8), C.POINTER(C.c_uint32), C.POINTER(C.c_uint64), C.POINTER(C.c_uint8)))],
+        int(soa.payload.shape[0]), 0, -1)
+    bcs = (C.c_char_p * max(1, len(whitelist)))(*[w.encode() for w in whitelist])
+    rc = lib.mgp_bam_write(str(path).encode(), names, lens, 2, 1, C.byref(b), bcs, len(whitelist), tag.encode(),
+                           unlisted.encode() if unlisted else None, int(level), int(n_threads or host_threads()),
+                           1 if index else 0)
+    if rc != 0:
+        raise OSError(_err())
 
 
 def soa_to_bam(path: str | Path, soa: ReadSoA, whitelist: list[str], contig: str = "chrM", mito_len: int = 16569,

@@ -434,22 +434,6 @@ struct Aux {
     }
 };
 
-struct Out {
-    std::vector<int32_t> start, bc, tlen;
-    std::vector<uint16_t> flag;
-    std::vector<uint8_t> mapq;
-    std::vector<uint32_t> span;
-    std::vector<uint64_t> roff;
-    std::vector<uint8_t> payload;
-};
-
-template <typename T>
-T* to_malloc(const std::vector<T>& v) {
-    T* p = (T*)std::malloc(std::max<size_t>(v.size(), 1) * sizeof(T));
-    if (p && !v.empty()) std::memcpy(p, v.data(), v.size() * sizeof(T));
-    return p;
-}
-
 // Iterate the records of `tid` in file order (fetch(contig) order); f(record
 // bytes after block_size, block_size) for each. Returns 0 or -1 (g_err set).
 template <typename F>
@@ -485,6 +469,77 @@ int for_each_record(mgp_bam* bam, int tid, F&& f) {
         st.pos += 4 + bs;
     }
 }
+
+// Batched variant: f(recs, sizes) over every complete record of `tid` present in
+// the inflated buffer at once (pointers stay valid during the call). Same return
+// convention as for_each_record.
+template <typename F>
+int for_each_batch(mgp_bam* bam, int tid, F&& f) {
+    uint64_t voff = bam->first_record_voff;
+    if (bam->has_index) {
+        voff = bam->ref_first_voff[(size_t)tid];
+        if (voff == UINT64_MAX) return 0;
+    }
+    Stream st;
+    g_err.clear();
+    if (!stream_at(bam, voff, st)) return -1;
+    bool seen = false, done = false;
+    std::vector<const uint8_t*> recs;
+    std::vector<uint32_t> sizes;
+    while (!done) {
+        if (!st.fill(4)) {
+            if (!g_err.empty()) return -1;
+            if (st.avail() == 0) break;
+            return fail("truncated BAM record");
+        }
+        const uint32_t bs0 = rd32(st.peek());
+        if (bs0 < 32) return fail("corrupt BAM record (block_size < 32)");
+        if (!st.fill(4 + (size_t)bs0)) return fail(g_err.empty() ? "truncated BAM record body" : g_err);
+        recs.clear();
+        sizes.clear();
+        const uint8_t* base = st.buf.data();
+        size_t p = st.pos;
+        const size_t end = st.buf.size();
+        while (end - p >= 4) {
+            const uint32_t bs = rd32(base + p);
+            if (bs < 32) return fail("corrupt BAM record (block_size < 32)");
+            if (end - p < 4 + (size_t)bs) break;
+            const int32_t ref = rdi32(base + p + 4);
+            if (ref == tid) {
+                seen = true;
+                recs.push_back(base + p + 4);
+                sizes.push_back(bs);
+            } else if (seen || ref > tid || ref < 0) {
+                done = true;
+                break;
+            }
+            p += 4 + (size_t)bs;
+        }
+        if (!recs.empty()) {
+            const int c = f(recs, sizes);
+            if (c < 0) return -1;
+            if (c == 0) return 0;
+        }
+        st.pos = p;
+    }
+    return 0;
+}
+
+// Growable malloc'd array (handed to the caller as is: no final copy).
+template <typename T>
+struct Grow {
+    T* p = nullptr;
+    size_t n = 0, cap = 0;
+    bool reserve(size_t want) {
+        if (want <= cap) return true;
+        size_t nc = std::max(want, cap + cap / 2 + 1024);
+        T* q = (T*)std::realloc(p, nc * sizeof(T));
+        if (!q) return false;
+        p = q;
+        cap = nc;
+        return true;
+    }
+};
 
 }  // namespace
 
@@ -558,42 +613,36 @@ int mgp_bam_read_ref(mgp_bam* b, int tid, int rec_align, mgp_bam_batch* out) {
     if (rec_align < 16 || rec_align > 4096 || (rec_align & (rec_align - 1))) return fail("bad rec_align");
     std::memset(out, 0, sizeof(*out));
     out->first_tag_index = -1;
-    Out o;
-    int64_t n = 0, n_tag = 0, first_tag = -1;
+    Grow<int32_t> G_start, G_bc, G_tlen;
+    Grow<uint16_t> G_flag;
+    Grow<uint8_t> G_mapq, G_pay;
+    Grow<uint32_t> G_span;
+    Grow<uint64_t> G_roff;
+    int64_t n_tag = 0, first_tag = -1;
     const uint64_t amask = (uint64_t)rec_align - 1;
-    const int rc = for_each_record(b, tid, [&](const uint8_t* r, uint32_t bs) -> int {
+    const int nt = std::max(1, b->n_threads);
+    std::vector<uint64_t> rsz;  // payload bytes of each record of the batch (then its offset)
+    std::vector<uint32_t> ncg;  // CIGAR operations (CG tag resolved)
+    std::vector<const uint8_t*> cgp;
+    // one record: decode + pack at index k / payload offset off
+    auto decode = [&](const uint8_t* r, uint32_t bs, size_t k, uint64_t off, uint32_t n_cig, const uint8_t* cig,
+                      int64_t& tags, int64_t& first, int64_t gidx) {
         const uint8_t* end = r + bs;
         const int32_t pos = rdi32(r + 4);
         const uint8_t l_name = r[8];
         const uint8_t mq = r[9];
-        uint32_t n_cig = rd16(r + 12);
         const uint16_t flg = rd16(r + 14);
         const uint32_t l_seq = rd32(r + 16);
         const int32_t tl = rdi32(r + 28);
-        const uint8_t* cigp = r + 32 + l_name;
-        const uint8_t* seqp = cigp + 4 * (size_t)n_cig;
+        const uint8_t* seqp = r + 32 + l_name + 4 * (size_t)rd16(r + 12);
         const uint8_t* qualp = seqp + ((size_t)l_seq + 1) / 2;
         const uint8_t* auxp = qualp + l_seq;
-        if (auxp > end) {
-            fail("corrupt BAM record (fields exceed block_size)");
-            return -1;
-        }
         Aux aux{auxp, end};
-        // CIGAR with > 65535 operations lives in the CG:B,I tag (placeholder kSmN)
-        const uint8_t* cig = cigp;
-        if (n_cig == 2 && (rd32(cigp) & 15u) == 4 && (rd32(cigp) >> 4) == l_seq && (rd32(cigp + 4) & 15u) == 3) {
-            const uint8_t* t = aux.find("CG");
-            if (t && t[0] == 'B' && (t[1] == 'I' || t[1] == 'i')) {
-                n_cig = rd32(t + 2);
-                cig = t + 6;
-            }
-        }
-        // barcode
         int32_t bcv = -1;
         const uint8_t* t = aux.find(b->tag);
         if (t) {
-            ++n_tag;
-            if (first_tag < 0) first_tag = n;
+            ++tags;
+            if (first < 0) first = gidx;
             if (t[0] == 'Z' || t[0] == 'H') {  // get_tag() -> str; numeric tags never match
                 const char* sv = (const char*)t + 1;
                 bcv = b->wl.get(sv, std::strlen(sv));
@@ -604,17 +653,11 @@ int mgp_bam_read_ref(mgp_bam* b, int tid, int rec_align, mgp_bam_batch* out) {
         if (b->bulk_cell >= 0) bcv = b->bulk_cell;
         uint16_t fl = flg & 0x0FFF;
         if (l_seq == 0 || qualp[0] == 0xFF) fl |= MGP_FLAG_NOSEQQUAL;
-        if (n_cig > 0xFFFF) {
-            fail("CIGAR with more than 65535 operations is not supported by the record format");
-            return -1;
-        }
-        // payload record (include/mgpileup.h)
-        const uint64_t off = (o.payload.size() + amask) & ~amask;
         const uint32_t soff = mgp_seq_offset(l_seq);
         const uint32_t coff = mgp_cigar_offset(l_seq);
+        uint8_t* rec = G_pay.p + off;
         const uint64_t size = ((uint64_t)coff + 4ull * n_cig + amask) & ~amask;
-        o.payload.resize(off + size, 0);
-        uint8_t* rec = o.payload.data() + off;
+        std::memset(rec, 0, size);
         std::memcpy(rec, &pos, 4);
         std::memcpy(rec + 4, &l_seq, 4);
         const uint16_t nc16 = (uint16_t)n_cig;
@@ -626,31 +669,101 @@ int mgp_bam_read_ref(mgp_bam* b, int tid, int rec_align, mgp_bam_batch* out) {
             std::memcpy(rec + soff, seqp, ((size_t)l_seq + 1) / 2);
         }
         if (n_cig) std::memcpy(rec + coff, cig, 4 * (size_t)n_cig);
-        o.start.push_back(pos);
-        o.bc.push_back(bcv);
-        o.tlen.push_back(tl);
-        o.flag.push_back(fl);
-        o.mapq.push_back(mq);
-        o.span.push_back(std::max(cigar_ref_span(cig, n_cig), l_seq));
-        o.roff.push_back(off);
-        ++n;
+        G_start.p[k] = pos;
+        G_bc.p[k] = bcv;
+        G_tlen.p[k] = tl;
+        G_flag.p[k] = fl;
+        G_mapq.p[k] = mq;
+        G_span.p[k] = std::max(cigar_ref_span(cig, n_cig), l_seq);
+        G_roff.p[k] = off;
+    };
+    const int rc = for_each_batch(b, tid, [&](const std::vector<const uint8_t*>& recs,
+                                              const std::vector<uint32_t>& sizes) -> int {
+        const size_t m = recs.size();
+        rsz.resize(m);
+        ncg.resize(m);
+        cgp.resize(m);
+        // pass 1 (sequential, header fields only): sizes, CIGAR location, checks
+        uint64_t tot = 0;
+        for (size_t i = 0; i < m; ++i) {
+            const uint8_t* r = recs[i];
+            const uint8_t l_name = r[8];
+            uint32_t n_cig = rd16(r + 12);
+            const uint32_t l_seq = rd32(r + 16);
+            const uint8_t* cigp = r + 32 + l_name;
+            const uint8_t* auxp = cigp + 4 * (size_t)n_cig + ((size_t)l_seq + 1) / 2 + l_seq;
+            if (auxp > r + sizes[i]) return fail("corrupt BAM record (fields exceed block_size)"), -1;
+            const uint8_t* cig = cigp;
+            // CIGAR with > 65535 operations lives in the CG:B,I tag (placeholder kSmN)
+            if (n_cig == 2 && (rd32(cigp) & 15u) == 4 && (rd32(cigp) >> 4) == l_seq && (rd32(cigp + 4) & 15u) == 3) {
+                Aux aux{auxp, r + sizes[i]};
+                const uint8_t* t = aux.find("CG");
+                if (t && t[0] == 'B' && (t[1] == 'I' || t[1] == 'i')) {
+                    n_cig = rd32(t + 2);
+                    cig = t + 6;
+                }
+            }
+            if (n_cig > 0xFFFF)
+                return fail("CIGAR with more than 65535 operations is not supported by the record format"), -1;
+            ncg[i] = n_cig;
+            cgp[i] = cig;
+            const uint64_t off = (G_pay.n + tot + amask) & ~amask;  // records are rec_align-sized
+            rsz[i] = off;
+            tot = off - G_pay.n + (((uint64_t)mgp_cigar_offset(l_seq) + 4ull * n_cig + amask) & ~amask);
+        }
+        const size_t k0 = G_start.n;
+        const size_t kn = k0 + m;
+        if (!G_start.reserve(kn) || !G_bc.reserve(kn) || !G_tlen.reserve(kn) || !G_flag.reserve(kn) ||
+            !G_mapq.reserve(kn) || !G_span.reserve(kn) || !G_roff.reserve(kn) || !G_pay.reserve(G_pay.n + tot + 256))
+            return fail("out of host memory"), -1;
+        // pass 2 (parallel): decode + pack
+        const int tn = (int)std::max<size_t>(1, std::min<size_t>((size_t)nt, m / 4096 + 1));
+        std::vector<int64_t> tags((size_t)tn, 0), firsts((size_t)tn, -1);
+        auto work = [&](int t) {
+            const size_t lo = m * (size_t)t / (size_t)tn, hi = m * (size_t)(t + 1) / (size_t)tn;
+            for (size_t i = lo; i < hi; ++i)
+                decode(recs[i], sizes[i], k0 + i, rsz[i], ncg[i], cgp[i], tags[(size_t)t], firsts[(size_t)t],
+                       (int64_t)(k0 + i));
+        };
+        std::vector<std::thread> th;
+        for (int t = 1; t < tn; ++t) th.emplace_back(work, t);
+        work(0);
+        for (auto& x : th) x.join();
+        for (int t = 0; t < tn; ++t) {
+            n_tag += tags[(size_t)t];
+            if (first_tag < 0 && firsts[(size_t)t] >= 0) first_tag = firsts[(size_t)t];
+        }
+        G_start.n = G_bc.n = G_tlen.n = G_flag.n = G_mapq.n = G_span.n = G_roff.n = kn;
+        G_pay.n += tot;
         return 1;
     });
-    if (rc != 0) return -1;
-    out->n_reads = n;
-    out->start = to_malloc(o.start);
-    out->bc = to_malloc(o.bc);
-    out->tlen = to_malloc(o.tlen);
-    out->flag = to_malloc(o.flag);
-    out->mapq = to_malloc(o.mapq);
-    out->span = to_malloc(o.span);
-    out->rec_off = to_malloc(o.roff);
-    o.payload.resize(o.payload.size() + 256, 0);  // slack for vector over-reads
-    out->payload = to_malloc(o.payload);
-    out->payload_bytes = (int64_t)o.payload.size() - 256;
+    auto release = [&]() {
+        std::free(G_start.p); std::free(G_bc.p); std::free(G_tlen.p); std::free(G_flag.p);
+        std::free(G_mapq.p); std::free(G_span.p); std::free(G_roff.p); std::free(G_pay.p);
+    };
+    if (rc != 0) {
+        release();
+        return -1;
+    }
+    // at least one element everywhere; >= 256 bytes of payload slack for vector over-reads
+    if (!G_start.reserve(1) || !G_bc.reserve(1) || !G_tlen.reserve(1) || !G_flag.reserve(1) ||
+        !G_mapq.reserve(1) || !G_span.reserve(1) || !G_roff.reserve(1) || !G_pay.reserve(G_pay.n + 256)) {
+        release();
+        return fail("out of host memory");
+    }
+    std::memset(G_pay.p + G_pay.n, 0, 256);
+    out->n_reads = (int64_t)G_start.n;
+    out->start = G_start.p;
+    out->bc = G_bc.p;
+    out->tlen = G_tlen.p;
+    out->flag = G_flag.p;
+    out->mapq = G_mapq.p;
+    out->span = G_span.p;
+    out->rec_off = G_roff.p;
+    out->payload = G_pay.p;
+    out->payload_bytes = (int64_t)G_pay.n;
     out->n_with_tag = n_tag;
     out->first_tag_index = first_tag;
-    if (!out->start || !out->payload) return fail("out of host memory");
     return 0;
 }
 

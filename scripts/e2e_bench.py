@@ -1,0 +1,75 @@
+"""End-to-end timing on one GPU ("Also report end-to-end wall
+time including BAM decode and writers separately").
+
+Makes a synthetic coordinate-sorted BAM of BASELINE config C3 (50M chrM reads x
+5k cells, `run` parameters) with the device generator and the native BAM writer,
+then runs ``run_pipeline`` on it (txt and hdf5 outputs) and prints one JSON line
+with the stage times: BAM ingest (native decode into the engine batch), engine
+(H2D + run + D2H), writers, QC report.
+
+    python scripts/e2e_bench.py [--reads N] [--cells C] [--threads T] [--out DIR]
+"""
+
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent.parent
+sys.path.insert(0, str(ROOT))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--reads", type=int, default=50_000_000)
+    ap.add_argument("--cells", type=int, default=5_000)
+    ap.add_argument("--threads", type=int, default=16)
+    ap.add_argument("--out", default="gpurun_out/e2e")
+    ap.add_argument("--formats", default="txt,hdf5")
+    args = ap.parse_args()
+
+    from mgatk2_amd.bam import write_bam
+    from mgatk2_amd.engine import Engine, EngineConfig
+    from mgatk2_amd.pipeline import MtDNAPipeline
+    from mgatk2_amd.config import PipelineConfig
+    from mgatk2_amd.synth import barcode_names, cell_cdf, ref_codes
+
+    out = Path(args.out)
+    out.mkdir(parents=True, exist_ok=True)
+    seed = 20251015 + 3
+    t0 = time.time()
+    with Engine(EngineConfig(n_cells=args.cells), device=0) as eng:
+        eng.synth(seed, args.reads, cell_cdf(seed, args.cells), ref_codes(seed), read_len=50)
+        soa = eng.download_inputs()
+    whitelist = barcode_names(args.cells, seed)
+    t1 = time.time()
+    bam = out / "possorted_bam.bam"
+    write_bam(bam, soa, whitelist, level=1, n_threads=args.threads)
+    del soa
+    t2 = time.time()
+    (out / "barcodes.tsv").write_text("".join(b + "\n" for b in whitelist))
+    print(f"[e2e] generated {args.reads:,} reads in {t1 - t0:.1f}s; BAM {bam.stat().st_size / 1e9:.2f} GB "
+          f"written in {t2 - t1:.1f}s", file=sys.stderr, flush=True)
+
+    os.environ.setdefault("MGP_GZIP_LEVEL", "6")
+    res = {"config": f"C3: {args.reads:,} reads x {args.cells} cells, run params (q20 mapq30 "
+                     "dedup=alignment_and_fragment_length)", "host_threads": args.threads}
+    for fmt in args.formats.split(","):
+        cfg = PipelineConfig(min_baseq=20, min_mapq=30, max_strand_bias=1.0, skip_deduplication=False,
+                             use_fragment_length_dedup=True, min_reads_per_cell=1, n_cores=args.threads)
+        t = time.time()
+        p = MtDNAPipeline(str(bam), whitelist, out / f"run_{fmt}", config=cfg, output_format=fmt)
+        ret = p.run()
+        wall = time.time() - t
+        res[fmt] = {"wall_s": round(wall, 2), **{k: round(v, 2) for k, v in p.timings.items()},
+                    "reads_per_s_end_to_end": round(args.reads / wall), "cells_passed": ret.get("cells_passed_qc")}
+        print(f"[e2e] {fmt}: {res[fmt]}", file=sys.stderr, flush=True)
+    print(json.dumps(res), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -212,3 +212,19 @@ def test_errors(tmp_path):
     (tmp_path / "c.bam").write_bytes(bytes(corrupt))
     with BamFile(tmp_path / "c.bam") as b, pytest.raises(BAMReadError):
         b.read_soa("chrM", g.whitelist)
+
+
+@pytest.mark.parametrize("case", ["synth_run", "kat_run"])
+def test_native_writer_matches_python_writer(case, tmp_path):
+    """mgp_bam_write (threaded BGZF, .bai) decodes to the same batch as the Python writer."""
+    from mgatk2_amd.bam import write_bam
+
+    g = Golden(case)
+    write_bam(tmp_path / "n.bam", g.soa, g.whitelist, n_threads=3)
+    soa_to_bam(tmp_path / "p.bam", g.soa, g.whitelist)
+    with BamFile(tmp_path / "n.bam") as a, BamFile(tmp_path / "p.bam") as b:
+        assert a.has_index
+        _assert_soa_equal(a.read_soa("chrM", g.whitelist), b.read_soa("chrM", g.whitelist))
+        assert a.count_tag("chrM") == b.count_tag("chrM")
+    refs, recs = _independent_decode(tmp_path / "n.bam")
+    assert refs == ["chr1", "chrM"] and len(recs) == g.soa.n
