@@ -323,3 +323,27 @@ def test_insertion_context_matches_loop():
         if tn5[p] > 0 and ref[p] + ref[p + 1] in exp:
             exp[ref[p] + ref[p + 1]] += int(tn5[p])
     assert insertion_context(tn5, ref) == exp
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", ["synth_run", "synth_bias", "kat_run"])
+def test_pipeline_sharded_gpu(case, tmp_path, engine_lib):
+    """Cells sharded over several engine contexts, run concurrently
+    from threads; on a one-GPU box the contexts share device 0. Outputs must equal
+    the reference's, like the single-context run."""
+    from mgatk2_amd.pipeline import run_pipeline
+
+    g = Golden(case)
+    p = g.params
+    bam = tmp_path / "x.bam"
+    soa_to_bam(bam, g.soa, g.whitelist)
+    bfile = tmp_path / "barcodes.tsv"
+    bfile.write_text("".join(b + "\n" for b in g.whitelist))
+    out = tmp_path / "out"
+    ret = run_pipeline(
+        str(bam), str(bfile), str(out), min_baseq=p["min_baseq"], min_mapq=p["min_mapq"],
+        min_reads_per_cell=p["min_reads_per_cell"], max_strand_bias=p["max_strand_bias"],
+        skip_deduplication=p["skip_deduplication"], use_fragment_length_dedup=p["use_fragment_length_dedup"],
+        output_format="txt", devices=[0, 0, 0],
+    )
+    _check_outputs(g, out, ret)
