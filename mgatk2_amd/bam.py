@@ -104,6 +104,20 @@ def _err() -> str:
     return (host_library().mgp_host_last_error() or b"").decode(errors="replace")
 
 
+class _BatchOwner:
+    """Frees an mgp_bam_batch when garbage collected (owner of zero-copy views)."""
+
+    def __init__(self, lib, batch: mgp_bam_batch):
+        self.lib = lib
+        self.batch = batch
+
+    def __del__(self):
+        try:
+            self.lib.mgp_bam_free_batch(C.byref(self.batch))
+        except Exception:
+            pass
+
+
 class BamFile:
     """Native BAM reader (header, reference list, chrM records -> engine SoA)."""
 
@@ -152,23 +166,26 @@ class BamFile:
         b = mgp_bam_batch()
         if self.lib.mgp_bam_read_ref(self._h, self.tid(contig), int(rec_align), C.byref(b)) != 0:
             raise BAMReadError(self.path, f"Read error: {_err()}")
-        try:
-            n = int(b.n_reads)
+        # zero copy: the arrays view the library's buffers, which are freed when the
+        # last array referencing them is gone
+        owner = _BatchOwner(self.lib, b)
+        n = int(b.n_reads)
 
-            def take(ptr, dtype, count):
-                if count == 0:
-                    return np.zeros(0, dtype)
-                return np.ctypeslib.as_array(ptr, shape=(count,)).astype(dtype, copy=True)
+        def view(ptr, dtype, count):
+            if count == 0:
+                return np.zeros(0, dtype)
+            nbytes = count * np.dtype(dtype).itemsize
+            buf = (C.c_uint8 * nbytes).from_address(C.cast(ptr, C.c_void_p).value)
+            buf._owner = owner
+            return np.frombuffer(buf, dtype=dtype, count=count)
 
-            soa = ReadSoA(
-                take(b.start, np.int32, n), take(b.bc, np.int32, n), take(b.tlen, np.int32, n),
-                take(b.flag, np.uint16, n), take(b.mapq, np.uint8, n), take(b.span, np.uint32, n),
-                take(b.rec_off, np.uint64, n), take(b.payload, np.uint8, int(b.payload_bytes)),
-            )
-            soa.extra.update(n_with_tag=int(b.n_with_tag), first_tag_index=int(b.first_tag_index))
-            return soa
-        finally:
-            self.lib.mgp_bam_free_batch(C.byref(b))
+        soa = ReadSoA(
+            view(b.start, np.int32, n), view(b.bc, np.int32, n), view(b.tlen, np.int32, n),
+            view(b.flag, np.uint16, n), view(b.mapq, np.uint8, n), view(b.span, np.uint32, n),
+            view(b.rec_off, np.uint64, n), view(b.payload, np.uint8, int(b.payload_bytes)),
+        )
+        soa.extra.update(n_with_tag=int(b.n_with_tag), first_tag_index=int(b.first_tag_index))
+        return soa
 
     def find_tag(self, contig: str, tag: str, max_records: int) -> tuple[int, int]:
         """(index of the first record carrying `tag` among the first `max_records`

@@ -10,6 +10,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <cerrno>
 #include <cstdint>
 #include <cstdio>
@@ -32,6 +33,12 @@ std::string& mgp_host_err() {
 }
 
 namespace {
+
+// MGP_HOST_PROFILE=1: phase times of mgp_bam_read_ref on stderr
+double now_s() {
+    return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+thread_local double t_inflate = 0, t_pread = 0;
 
 #define g_err mgp_host_err()
 int fail(const std::string& m) {
@@ -194,8 +201,11 @@ struct Stream {
         }
         const size_t want = (size_t)std::min<uint64_t>(batch_bytes, (uint64_t)bam->file_size - coff);
         batch_bytes = std::min(kMaxBatch, batch_bytes * 4);
+        const double tr0 = now_s();
         std::vector<uint8_t> raw(want);
-        if (!pread_all(bam->fd, raw.data(), want, coff)) {
+        const bool rd_ok = pread_all(bam->fd, raw.data(), want, coff);
+        t_pread += now_s() - tr0;
+        if (!rd_ok) {
             fail("read error in " + bam->path);
             return false;
         }
@@ -263,10 +273,12 @@ struct Stream {
             }
             inflateEnd(&zs);
         };
+        const double ti0 = now_s();
         std::vector<std::thread> th;
         for (int t = 1; t < nt; ++t) th.emplace_back(work);
         work();
         for (auto& t : th) t.join();
+        t_inflate += now_s() - ti0;
         if (!ok) return fail("BGZF inflate/CRC error in " + bam->path), false;
         coff += p;
         return true;
@@ -621,6 +633,9 @@ int mgp_bam_read_ref(mgp_bam* b, int tid, int rec_align, mgp_bam_batch* out) {
     int64_t n_tag = 0, first_tag = -1;
     const uint64_t amask = (uint64_t)rec_align - 1;
     const int nt = std::max(1, b->n_threads);
+    const double t_begin = now_s();
+    double t_p1 = 0, t_p2 = 0;
+    t_inflate = t_pread = 0;
     std::vector<uint64_t> rsz;  // payload bytes of each record of the batch (then its offset)
     std::vector<uint32_t> ncg;  // CIGAR operations (CG tag resolved)
     std::vector<const uint8_t*> cgp;
@@ -679,6 +694,7 @@ int mgp_bam_read_ref(mgp_bam* b, int tid, int rec_align, mgp_bam_batch* out) {
     };
     const int rc = for_each_batch(b, tid, [&](const std::vector<const uint8_t*>& recs,
                                               const std::vector<uint32_t>& sizes) -> int {
+        const double tp1 = now_s();
         const size_t m = recs.size();
         rsz.resize(m);
         ncg.resize(m);
@@ -716,6 +732,8 @@ int mgp_bam_read_ref(mgp_bam* b, int tid, int rec_align, mgp_bam_batch* out) {
         if (!G_start.reserve(kn) || !G_bc.reserve(kn) || !G_tlen.reserve(kn) || !G_flag.reserve(kn) ||
             !G_mapq.reserve(kn) || !G_span.reserve(kn) || !G_roff.reserve(kn) || !G_pay.reserve(G_pay.n + tot + 256))
             return fail("out of host memory"), -1;
+        const double tp2 = now_s();
+        t_p1 += tp2 - tp1;
         // pass 2 (parallel): decode + pack
         const int tn = (int)std::max<size_t>(1, std::min<size_t>((size_t)nt, m / 4096 + 1));
         std::vector<int64_t> tags((size_t)tn, 0), firsts((size_t)tn, -1);
@@ -735,8 +753,13 @@ int mgp_bam_read_ref(mgp_bam* b, int tid, int rec_align, mgp_bam_batch* out) {
         }
         G_start.n = G_bc.n = G_tlen.n = G_flag.n = G_mapq.n = G_span.n = G_roff.n = kn;
         G_pay.n += tot;
+        t_p2 += now_s() - tp2;
         return 1;
     });
+    if (std::getenv("MGP_HOST_PROFILE"))
+        std::fprintf(stderr, "[mgp_bam_read_ref] %zu records, %d threads: total %.3f s = pread %.3f + inflate %.3f + "
+                     "scan/sizes %.3f + decode %.3f (+ rest)\n", G_start.n, nt, now_s() - t_begin, t_pread, t_inflate,
+                     t_p1, t_p2);
     auto release = [&]() {
         std::free(G_start.p); std::free(G_bc.p); std::free(G_tlen.p); std::free(G_flag.p);
         std::free(G_mapq.p); std::free(G_span.p); std::free(G_roff.p); std::free(G_pay.p);

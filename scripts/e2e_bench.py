@@ -28,7 +28,7 @@ def main():
     ap.add_argument("--reads", type=int, default=50_000_000)
     ap.add_argument("--cells", type=int, default=5_000)
     ap.add_argument("--threads", type=int, default=16)
-    ap.add_argument("--out", default="gpurun_out/e2e")
+    ap.add_argument("--out", default="/tmp/mgp_e2e")
     ap.add_argument("--formats", default="txt,hdf5")
     args = ap.parse_args()
 
