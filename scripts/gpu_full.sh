@@ -25,7 +25,7 @@ step rocprof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_
     python bench.py --steps 5 --warmup 1 --no-cpu-baseline || exit $?
 find gpurun_out/prof -name "*kernel_stats.csv" -exec cp {} gpurun_out/kernel_stats.csv \;
 for grp in FETCH_SIZE WRITE_SIZE; do
-    step pmc_$grp 400 rocprofv3 --pmc $grp --kernel-include-regex "k_pileup|k_scatter|k_bin_count|k_median" \
+    step pmc_$grp 400 rocprofv3 --pmc $grp --kernel-include-regex "k_pileup|k_group_a|k_group_b|k_bin_count|k_median" \
         --output-format csv -d gpurun_out/pmc_$grp -o pmc -- python bench.py --steps 2 --warmup 0 --no-cpu-baseline \
         || exit $?
 done
