@@ -101,8 +101,8 @@ struct DevBuf {
     T* as() const { return reinterpret_cast<T*>(p); }
 };
 
-enum Stage { ST_HIST, ST_SCAN, ST_SCATTER, ST_PILEUP, ST_GATE, ST_MEDIAN, ST_TALLY, ST_COMM, ST_N };
-static const char* kStageNames = "hist,scan,scatter,pileup,gate,median,tally,comm";
+enum Stage { ST_HIST, ST_SCAN, ST_GROUP_A, ST_GROUP_B, ST_PILEUP, ST_GATE, ST_MEDIAN, ST_TALLY, ST_COMM, ST_N };
+static const char* kStageNames = "hist,scan,group_a,group_b,pileup,gate,median,tally,comm";
 
 struct mgp_ctx {
     mgp_config cfg{};
@@ -121,8 +121,8 @@ struct mgp_ctx {
     DevBuf start, bc, tlen, flag, mapq, span, roff, payload;
 
     // run scratch
-    DevBuf bin_start, H, P, cell_cnt, cell_base, bin_valid, bin_base, bucket_off, gel2;
-    DevBuf gel, tally_part, tally;
+    DevBuf bin_start, H, P, cell_cnt, cell_base, bin_valid, bin_base, bucket_off, gel2, PG, F;
+    DevBuf pel, tally_part, tally;
     DevBuf n_reads, any_paired, passed, covered, dsum, dmax, med_lo, med_hi, first_read;
     DevBuf counts, tn5, depth, stats;
 
@@ -161,75 +161,117 @@ __device__ __forceinline__ int64_t bin_threshold(int b, const Geom& g) {
     return (int64_t)b * g.G;
 }
 
-// One workgroup per start bin: bin bounds by binary search in the sorted starts,
-// coordinate-order check (pysam's fetch order, readers.py:87-92), flag/barcode
-// filters (readers.py:95-111) and the per-cell histogram of the bin (LDS atomics
-// when the row fits, else atomics on the global row).
+constexpr int kGroup = 64;  // cells per grouping bucket (pass A) and per pass-B workgroup
+
+// Start bins are split into kParts parts (equal read-index ranges) so that
+// grouping pass A runs on kParts x nbins workgroups: a grid of ~2 slot-rounds
+// (4 workgroups per CU) would leave a long tail.
+constexpr int kParts = 4;
+__device__ __forceinline__ void part_range(int64_t lo, int64_t hi, int p, int64_t& plo, int64_t& phi) {
+    const int64_t len = hi - lo;
+    plo = lo + len * p / kParts;
+    phi = lo + len * (p + 1) / kParts;
+}
+
+// One workgroup (8 waves) per start bin: bin bounds by binary search in the
+// sorted starts, coordinate-order check (pysam's fetch order, readers.py:87-92),
+// flag/barcode filters (readers.py:95-111) and the per-cell histogram of the bin
+// (LDS atomics when the row fits, else atomics on the global row). The bin's
+// parts are counted one after the other; after each part the per-64-cell-group
+// totals are snapshotted, giving the per-(bin, part, group) counts of pass A.
+constexpr int kHistBlock = 512;
 template <bool kLds>
-__global__ void __launch_bounds__(kBlock) k_bin_count(const int32_t* __restrict__ start,
-                                                      const int32_t* __restrict__ bc,
-                                                      const uint16_t* __restrict__ flag,
-                                                      const uint32_t* __restrict__ span, int64_t n, Geom g,
-                                                      uint32_t* __restrict__ H, uint32_t* __restrict__ bin_lo,
-                                                      uint32_t* __restrict__ bin_valid, DevStats* st) {
-    extern __shared__ uint32_t hist[];
+__global__ void __launch_bounds__(kHistBlock) k_bin_count(const int32_t* __restrict__ start,
+                                                          const int32_t* __restrict__ bc,
+                                                          const uint16_t* __restrict__ flag,
+                                                          const uint32_t* __restrict__ span, int64_t n, Geom g,
+                                                          uint32_t* __restrict__ H, uint32_t* __restrict__ PG,
+                                                          int ngroups, uint32_t* __restrict__ bin_lo,
+                                                          uint32_t* __restrict__ bin_valid, DevStats* st) {
+    extern __shared__ uint32_t hist[];  // kLds: [nc] cell counts; else [ngroups] group counts; then cum[ngroups]
     __shared__ int64_t s_range[2];
     __shared__ uint32_t s_nvalid;
     const int b = blockIdx.x;
     const int nc = g.nc;
+    const int lane = threadIdx.x & 63;
+    uint32_t* cum = hist + (kLds ? nc : ngroups);
     uint32_t* row = H + (size_t)b * nc;
     uint32_t* cnt = kLds ? hist : row;
     if (threadIdx.x < 2) s_range[threadIdx.x] = lower_bound_start(start, n, bin_threshold(b + threadIdx.x, g));
-    if (kLds)
-        for (int c = threadIdx.x; c < nc; c += blockDim.x) hist[c] = 0;
+    for (int c = threadIdx.x; c < (kLds ? nc : ngroups); c += blockDim.x) hist[c] = 0;
     if (threadIdx.x == 0) s_nvalid = 0;
     __syncthreads();
-    const int64_t lo = s_range[0], hi = max(s_range[1], lo);
+    const int64_t blo = s_range[0], bhi = max(s_range[1], blo);
     if (threadIdx.x == 0) {
-        bin_lo[b] = (uint32_t)lo;
+        bin_lo[b] = (uint32_t)blo;
         if (b == g.nbins - 1) bin_lo[g.nbins] = (uint32_t)n;
     }
     uint32_t mspan = 0;
     unsigned long long nvalid = 0;
     bool badbc = false, unsorted = false;
-    // 4 reads per thread per step, loads issued together (clamped index, no branches)
-    constexpr int kU = 4;
-    for (int64_t i0 = lo + threadIdx.x; i0 < hi; i0 += kU * kBlock) {
-        int cc[kU], ss[kU], sp0[kU];
-        uint32_t sp[kU];
-        uint32_t ff[kU];
+    uint32_t* pg = PG + (size_t)b * kParts * ngroups;
+    for (int part = 0; part < kParts; ++part) {
+        int64_t lo, hi;
+        part_range(blo, bhi, part, lo, hi);
+        // 4 reads per thread per step, loads issued together (clamped index, no branches)
+        constexpr int kU = 4;
+        for (int64_t i0 = lo + threadIdx.x; i0 < hi; i0 += kU * kHistBlock) {
+            int cc[kU], ss[kU], sp0[kU];
+            uint32_t sp[kU];
+            uint32_t ff[kU];
 #pragma unroll
-        for (int u = 0; u < kU; ++u) {
-            const int64_t i = i0 + u * kBlock;
-            const int64_t j = i < hi ? i : hi - 1;
-            cc[u] = bc[j];
-            ff[u] = flag[j];
-            ss[u] = start[j];
-            sp0[u] = start[j > 0 ? j - 1 : 0];
-            sp[u] = span[j];
-        }
+            for (int u = 0; u < kU; ++u) {
+                const int64_t i = i0 + u * kHistBlock;
+                const int64_t j = i < hi ? i : hi - 1;
+                cc[u] = bc[j];
+                ff[u] = flag[j];
+                ss[u] = start[j];
+                sp0[u] = start[j > 0 ? j - 1 : 0];
+                sp[u] = span[j];
+            }
 #pragma unroll
-        for (int u = 0; u < kU; ++u) {
-            const int64_t i = i0 + u * kBlock;
-            if (i >= hi) break;
-            const int c = cc[u];
-            if (i > 0 && ss[u] < sp0[u]) unsorted = true;
-            badbc |= (c >= nc);
-            if (read_valid(c, (uint16_t)ff[u], nc)) {
-                atomicAdd(&cnt[c], 1u);
-                mspan = sp[u] > mspan ? sp[u] : mspan;
-                ++nvalid;
+            for (int u = 0; u < kU; ++u) {
+                const int64_t i = i0 + u * kHistBlock;
+                if (i >= hi) break;
+                const int c = cc[u];
+                if (i > 0 && ss[u] < sp0[u]) unsorted = true;
+                badbc |= (c >= nc);
+                if (read_valid(c, (uint16_t)ff[u], nc)) {
+                    atomicAdd(&cnt[c], 1u);
+                    if (!kLds) atomicAdd(&hist[c >> 6], 1u);
+                    mspan = sp[u] > mspan ? sp[u] : mspan;
+                    ++nvalid;
+                }
             }
         }
-    }
-    if (kLds) {
         __syncthreads();
-        for (int c = threadIdx.x; c < nc; c += blockDim.x) row[c] = hist[c];
+        // group totals so far; this part's counts are the growth since the last part
+        // (a group is always handled by the same thread, so `cum` needs no barrier)
+        uint32_t* pgp = pg + (size_t)part * ngroups;
+        if (kLds) {
+            for (int gi = threadIdx.x >> 6; gi < ngroups; gi += kHistBlock / kWave) {
+                const int c = gi * kGroup + lane;
+                const uint32_t h = wave_sum(c < nc ? hist[c] : 0u);
+                if (lane == 0) {
+                    pgp[gi] = h - (part ? cum[gi] : 0u);
+                    cum[gi] = h;
+                }
+            }
+        } else {
+            for (int gi = threadIdx.x; gi < ngroups; gi += blockDim.x) {
+                const uint32_t h = hist[gi];
+                pgp[gi] = h - (part ? cum[gi] : 0u);
+                cum[gi] = h;
+            }
+        }
+        __syncthreads();  // the snapshot is complete before the next part counts
     }
+    if (kLds)
+        for (int c = threadIdx.x; c < nc; c += blockDim.x) row[c] = hist[c];
     mspan = wave_max(mspan);
     nvalid = wave_sum(nvalid);
     const bool anybad = __ballot(badbc) != 0ull, anyuns = __ballot(unsorted) != 0ull;
-    if ((threadIdx.x & 63) == 0) {
+    if (lane == 0) {
         if (mspan) atomicMax(&st->max_span, mspan);
         if (nvalid) {
             atomicAdd(&st->valid, nvalid);
@@ -303,22 +345,26 @@ __global__ void __launch_bounds__(1024) k_scan_cells(const uint32_t* __restrict_
     }
 }
 
-// Scan step d: H[r][c] <- exclusive (cell-major) offset; row nrows <- cell end.
+// Scan step d: H[r][c] <- exclusive (cell-major) offset; row nrows <- cell end;
+// F[r] bit c <- r is the first bin holding reads of c.
 __global__ void k_scan_apply(uint32_t* __restrict__ H, const uint32_t* __restrict__ P,
                              const uint32_t* __restrict__ base, const uint32_t* __restrict__ cnt, int nrows,
-                             int nc, int RB, int nrb) {
+                             int nc, int RB, int nrb, uint32_t* __restrict__ F) {
     int c = blockIdx.x * blockDim.x + threadIdx.x;
     int rb = blockIdx.y;
     if (c >= nc) return;
-    uint32_t acc = base[c] + P[(size_t)rb * nc + c];
+    const uint32_t b0 = base[c];
+    uint32_t acc = b0 + P[(size_t)rb * nc + c];
     int r0 = rb * RB, r1 = min(nrows, r0 + RB);
+    const size_t fw = (size_t)(nc + 31) / 32;
     for (int r = r0; r < r1; ++r) {
         size_t k = (size_t)r * nc + c;
         uint32_t h = H[k];
+        if (h && acc == b0) atomicOr(&F[(size_t)r * fw + (c >> 5)], 1u << (c & 31));
         H[k] = acc;
         acc += h;
     }
-    if (rb == nrb - 1) H[(size_t)nrows * nc + c] = base[c] + cnt[c];
+    if (rb == nrb - 1) H[(size_t)nrows * nc + c] = b0 + cnt[c];
 }
 
 // Grouping element (16 bytes, cell-major, BAM order inside a cell):
@@ -329,7 +375,7 @@ struct __align__(16) GElem {
     uint32_t tlen;
 };
 constexpr unsigned long long GM_REV = 1ull << 56, GM_PAIRED = 2ull << 56, GM_MAPQ_OK = 4ull << 56,
-                             GM_BAD = 8ull << 56, GM_OFF = (1ull << 56) - 1;
+                             GM_BAD = 8ull << 56;
 
 // Grouping in two passes (a single pass that writes each 16-byte element straight
 // to its cell-major slot is bound by ~200M scattered partial-line stores):
@@ -342,7 +388,6 @@ constexpr unsigned long long GM_REV = 1ull << 56, GM_PAIRED = 2ull << 56, GM_MAP
 // The 6-bit cell id inside the group rides in bits 50..55 of GElem.w between
 // the passes (record offsets stay below 2^50).
 constexpr unsigned long long GM_LCELL_SHIFT = 50, GM_LCELL = 63ull << GM_LCELL_SHIFT;
-constexpr int kGroup = 64;
 #ifndef MGP_STAGE_A
 #define MGP_STAGE_A 0  // pass A: stage each step in LDS and write group runs (measured slower)
 #endif
@@ -353,10 +398,11 @@ __global__ void __launch_bounds__(kBlock) k_group_a(int64_t n, const int32_t* __
                                                     const uint16_t* __restrict__ flag, const uint8_t* __restrict__ mapq,
                                                     const uint64_t* __restrict__ roff,
                                                     const uint32_t* __restrict__ bin_lo,
-                                                    const uint32_t* __restrict__ O, const uint32_t* __restrict__ binbase,
+                                                    const uint32_t* __restrict__ PG, const uint32_t* __restrict__ F,
+                                                    const uint32_t* __restrict__ binbase,
                                                     Geom g, int ngroups, int gbits, int min_mapq,
                                                     uint32_t* __restrict__ bucket_off, GElem* __restrict__ gel2,
-                                                    uint32_t* __restrict__ first_read) {
+                                                    uint32_t* __restrict__ first_read, DevStats* st) {
     extern __shared__ uint32_t sm[];
     uint32_t* gcnt = sm;             // [ngroups] next free slot of each bucket of this bin
     uint32_t* fbits = sm + ngroups;  // [ceil(nc/32)] cell's first read is in this bin
@@ -364,45 +410,45 @@ __global__ void __launch_bounds__(kBlock) k_group_a(int64_t n, const int32_t* __
     uint32_t* lstart = gbase + ngroups;          // [ngroups] group runs inside the step stage
     __shared__ GElem stage[kStageA];
     __shared__ uint16_t sgrp[kStageA];
-    const int b = blockIdx.x;
+    const int b = blockIdx.x, part = blockIdx.y;
     const int nc = g.nc;
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const unsigned long long lt = lanemask_lt();
-    // bucket sizes (one wave per group) and the first-read bits
-    for (int gi = wid; gi < ngroups; gi += kBlock / kWave) {
-        const int c = gi * kGroup + lane;
-        // reads of cell c in bin b = O[b+1][c] - O[b][c] (row nbins holds the cell ends)
-        uint32_t h = c < nc ? O[(size_t)(b + 1) * nc + c] - O[(size_t)b * nc + c] : 0u;
-        h = wave_sum(h);
-        if (lane == 0) gcnt[gi] = h;
-    }
-    for (int x = threadIdx.x; x < (nc + 31) / 32; x += blockDim.x) fbits[x] = 0;
-    __syncthreads();
-    // exclusive scan over groups (wave 0, 64 at a time), based at the bin's first slot
+    // exclusive scan over groups (wave 0, 64 at a time) of the bin's bucket sizes
+    // (the parts' sums), based at the bin's first slot; this part's slots follow the
+    // earlier parts' in every bucket
+    const uint32_t* pg = PG + (size_t)b * kParts * ngroups;
     if (wid == 0) {
         uint32_t carry = binbase[b];
         for (int g0 = 0; g0 < ngroups; g0 += kWave) {
             const int gi = g0 + lane;
-            const uint32_t v = gi < ngroups ? gcnt[gi] : 0u;
+            uint32_t v = 0, before = 0;
+            if (gi < ngroups) {
+#pragma unroll
+                for (int p = 0; p < kParts; ++p) {
+                    const uint32_t x = pg[(size_t)p * ngroups + gi];
+                    v += x;
+                    before += p < part ? x : 0u;
+                }
+            }
             uint32_t x = v;
             for (int o = 1; o < kWave; o <<= 1) {
                 const uint32_t y = __shfl_up(x, o, kWave);
                 if (lane >= o) x += y;
             }
             if (gi < ngroups) {
-                gcnt[gi] = carry + x - v;
-                bucket_off[(size_t)b * (ngroups + 1) + gi] = carry + x - v;
+                gcnt[gi] = carry + x - v + before;
+                if (part == 0) bucket_off[(size_t)b * (ngroups + 1) + gi] = carry + x - v;
             }
             carry += __shfl(x, kWave - 1, kWave);
         }
-        if (lane == 0) bucket_off[(size_t)b * (ngroups + 1) + ngroups] = carry;
+        if (lane == 0 && part == 0) bucket_off[(size_t)b * (ngroups + 1) + ngroups] = carry;
     }
-    for (int c = threadIdx.x; c < nc; c += blockDim.x) {
-        const size_t k = (size_t)b * nc + c;
-        const uint32_t o = O[k];
-        if (O[k + nc] != o && o == O[c]) atomicOr(&fbits[c >> 5], 1u << (c & 31));
-    }
-    const int64_t lo = bin_lo[b], hi = max((int64_t)bin_lo[b + 1], lo);
+    // cells whose first read is in this bin (k_scan_apply)
+    const size_t fw = (size_t)(nc + 31) / 32;
+    for (int x = threadIdx.x; x < (int)fw; x += blockDim.x) fbits[x] = F[(size_t)b * fw + x];
+    int64_t lo, hi;
+    part_range(bin_lo[b], max((int64_t)bin_lo[b + 1], (int64_t)bin_lo[b]), part, lo, hi);
     __syncthreads();
     // each wave owns a contiguous run of kAhead*64 reads per step (BAM order = wave
     // order, then round order); waves claim bucket slots in wave order
@@ -496,7 +542,8 @@ __global__ void __launch_bounds__(kBlock) k_group_a(int64_t n, const int32_t* __
                 stage[si] = e;
                 sgrp[si] = (uint16_t)gi;
             } else {
-                gel2[dest] = e;
+                if ((int64_t)dest < n) gel2[dest] = e;  // always: counts and slots come from one histogram
+                else atomicOr(&st->err, ERR_OVERFLOW);
             }
         }
         if (MGP_STAGE_A) {  // the step's elements go out as runs, one per group
@@ -527,12 +574,56 @@ __global__ void __launch_bounds__(kBlock) k_group_a(int64_t n, const int32_t* __
 // slots over consecutive bins are contiguous in the output, so the stage is then
 // written out as a few long runs (full lines) instead of 64 scattered 16-byte
 // stores per instruction. A bucket larger than the stage goes straight out.
+//
+// Duplicate marking happens here (readers.py:118-150): every read that can be a
+// duplicate of a read shares its start, hence its start bin, hence its bucket,
+// and inside a cell's staged run equal starts are adjacent and in BAM order (the
+// input is coordinate-sorted and both passes are stable). So a read is a
+// duplicate iff a read before it in the run, among the equal starts, has the
+// same strand (and the same |tlen|): first in BAM order wins. Both duplicate
+// counters (readers.py:141-144) are taken here, each read being seen exactly
+// once. The output is one 8-byte pileup element per read: record offset |
+// GP_KEEP | GP_PAIRED | GP_BAD | GP_PILE (kept and MAPQ >= min_mapq, pileup.py:33).
 constexpr int kStageB = 2048;
+constexpr int kMaxRbB = 512;  // bins per pass-B workgroup (bucket sizes kept in LDS)
+#ifndef MGP_GB_WG
+#define MGP_GB_WG 8192  // target pass-B grid size
+#endif
+constexpr unsigned long long GP_PILE = 1ull << 63, GP_KEEP = 1ull << 62, GP_PAIRED = 1ull << 61,
+                             GP_BAD = 1ull << 60, GP_OFF = (1ull << GM_LCELL_SHIFT) - 1;
 
+struct DedupAcc {  // per-thread duplicate counters of pass B
+    unsigned long long d2 = 0, d3 = 0;
+};
+
+// The pileup element of one read given its duplicate flags.
+__device__ __forceinline__ unsigned long long group_b_emit(const GElem& e, bool dup2, bool dup3, int mode,
+                                                           DedupAcc& acc) {
+    const bool keep = mode == MGP_DEDUP_NONE ? true : mode == MGP_DEDUP_START ? !dup2 : !dup3;
+    acc.d2 += dup2;
+    acc.d3 += dup3;
+    unsigned long long x = e.w & GP_OFF;
+    if (keep) {
+        x |= GP_KEEP | (e.w & GM_PAIRED ? GP_PAIRED : 0ull) | (e.w & GM_BAD ? GP_BAD : 0ull);
+        if (e.w & GM_MAPQ_OK) x |= GP_PILE;
+    }
+    return x;
+}
+
+__device__ __forceinline__ bool same_key(const GElem& p, const GElem& e, bool& dup3) {
+    if (((p.w ^ e.w) & GM_REV) != 0ull) return false;
+    if (p.tlen == e.tlen) dup3 = true;
+    return true;
+}
+
+// kStage: rank into the LDS stage. Otherwise (a bucket larger than the stage):
+// rank, mark duplicates by walking back over the bucket's equal starts (BAM
+// order, other cells skipped) and store the pileup elements directly.
+template <bool kStage>
 __device__ __forceinline__ void group_b_rank(const GElem* __restrict__ gel2, uint32_t k0, uint32_t k1,
                                              uint32_t* cnt, int lane, unsigned long long lt, GElem* stage,
-                                             const uint32_t* cbase, const uint32_t* cstart,
-                                             GElem* __restrict__ gel) {
+                                             const uint32_t* cbase, const uint32_t* cstart, int mode,
+                                             unsigned long long* __restrict__ pel, DedupAcc& acc) {
     for (uint32_t k = k0; k < k1; k += kWave) {
         const uint32_t j = k + lane;
         const bool act = j < k1;
@@ -555,11 +646,21 @@ __device__ __forceinline__ void group_b_rank(const GElem* __restrict__ gel2, uin
         __builtin_amdgcn_wave_barrier();
         if (act) {
             const uint32_t dest = base + (uint32_t)__popcll(peers & lt);
-            if (stage) {
+            if (kStage) {
                 stage[cstart[lc] + (dest - cbase[lc])] = e;
             } else {
-                e.w &= ~GM_LCELL;
-                gel[dest] = e;
+                bool dup2 = false, dup3 = false;
+                if (mode != MGP_DEDUP_NONE) {
+                    for (uint32_t m = j; m-- > k0;) {
+                        const GElem p = gel2[m];
+                        if (p.start != e.start) break;
+                        if ((((p.w ^ e.w) & GM_LCELL) == 0ull) && same_key(p, e, dup3)) {
+                            dup2 = true;
+                            if (dup3) break;
+                        }
+                    }
+                }
+                pel[dest] = group_b_emit(e, dup2, dup3, mode, acc);
             }
         }
     }
@@ -568,10 +669,12 @@ __device__ __forceinline__ void group_b_rank(const GElem* __restrict__ gel2, uin
 __global__ void __launch_bounds__(kBlock) k_group_b(const GElem* __restrict__ gel2,
                                                     const uint32_t* __restrict__ bucket_off,
                                                     const uint32_t* __restrict__ O, Geom g, int ngroups, int rb,
-                                                    GElem* __restrict__ gel) {
+                                                    int mode, unsigned long long* __restrict__ pel,
+                                                    DevStats* st) {
     __shared__ GElem stage[kStageB];
     __shared__ uint32_t cnt[kBlock / kWave][kGroup];
     __shared__ uint32_t cbase[kGroup], cstart[kGroup + 1];
+    __shared__ uint32_t bsz[kMaxRbB];
     __shared__ int s_be;
     const int gi = blockIdx.x;
     const int B0 = blockIdx.y * rb, B1 = min(g.nbins, B0 + rb);
@@ -580,12 +683,17 @@ __global__ void __launch_bounds__(kBlock) k_group_b(const GElem* __restrict__ ge
     const int c = gi * kGroup + lane;
     const unsigned long long lt = lanemask_lt();
     const size_t bo = (size_t)ngroups + 1;
+    const bool dedup = mode != MGP_DEDUP_NONE;
+    DedupAcc acc;
+    for (int x = threadIdx.x; x < B1 - B0; x += kBlock)
+        bsz[x] = bucket_off[(size_t)(B0 + x) * bo + gi + 1] - bucket_off[(size_t)(B0 + x) * bo + gi];
+    __syncthreads();
     for (int b = B0; b < B1;) {
         if (threadIdx.x == 0) {  // bins of this step: as many as fit the stage
             uint32_t tot = 0;
             int be = b;
             while (be < B1) {
-                const uint32_t sz = bucket_off[(size_t)be * bo + gi + 1] - bucket_off[(size_t)be * bo + gi];
+                const uint32_t sz = bsz[be - B0];
                 if (tot + sz > (uint32_t)kStageB) break;
                 tot += sz;
                 ++be;
@@ -598,8 +706,8 @@ __global__ void __launch_bounds__(kBlock) k_group_b(const GElem* __restrict__ ge
             if (wid == 0) {
                 cnt[0][lane] = c < nc ? O[(size_t)b * nc + c] : 0u;
                 __builtin_amdgcn_wave_barrier();
-                group_b_rank(gel2, bucket_off[(size_t)b * bo + gi], bucket_off[(size_t)b * bo + gi + 1], cnt[0],
-                             lane, lt, nullptr, nullptr, nullptr, gel);
+                group_b_rank<false>(gel2, bucket_off[(size_t)b * bo + gi], bucket_off[(size_t)b * bo + gi + 1],
+                                    cnt[0], lane, lt, nullptr, nullptr, nullptr, mode, pel, acc);
             }
             __syncthreads();
             ++b;
@@ -621,20 +729,45 @@ __global__ void __launch_bounds__(kBlock) k_group_b(const GElem* __restrict__ ge
         for (int bb = b + wid; bb < be; bb += kBlock / kWave) {
             cnt[wid][lane] = c < nc ? O[(size_t)bb * nc + c] : 0u;
             __builtin_amdgcn_wave_barrier();
-            group_b_rank(gel2, bucket_off[(size_t)bb * bo + gi], bucket_off[(size_t)bb * bo + gi + 1], cnt[wid],
-                         lane, lt, stage, cbase, cstart, gel);
+            group_b_rank<true>(gel2, bucket_off[(size_t)bb * bo + gi], bucket_off[(size_t)bb * bo + gi + 1],
+                               cnt[wid], lane, lt, stage, cbase, cstart, mode, pel, acc);
             __builtin_amdgcn_wave_barrier();
         }
         __syncthreads();
         const uint32_t tot = cstart[kGroup];
         for (uint32_t t = threadIdx.x; t < tot; t += kBlock) {
-            GElem e = stage[t];
+            // the element and its two predecessors are loaded together; a longer walk
+            // is needed only behind three equal starts
+            const GElem e = stage[t];
+            const GElem p1 = stage[t >= 1 ? t - 1 : 0];
+            const GElem p2 = stage[t >= 2 ? t - 2 : 0];
             const int lc = (int)((e.w >> GM_LCELL_SHIFT) & (kGroup - 1));
-            e.w &= ~GM_LCELL;
-            gel[cbase[lc] + (t - cstart[lc])] = e;
+            bool dup2 = false, dup3 = false;
+            // equal starts of the cell's run sit just before t, in BAM order; a cell
+            // has one run in the stage, so an element of another cell ends the walk
+            auto same_run = [&](const GElem& p) {
+                return ((p.w ^ e.w) & GM_LCELL) == 0ull && p.start == e.start;
+            };
+            if (dedup && t >= 1 && same_run(p1)) {
+                dup2 = same_key(p1, e, dup3);
+                if (!dup3 && t >= 2 && same_run(p2)) {
+                    dup2 |= same_key(p2, e, dup3);
+                    for (uint32_t m = t - 2; !dup3 && m-- > 0;) {
+                        const GElem p = stage[m];
+                        if (!same_run(p)) break;
+                        dup2 |= same_key(p, e, dup3);
+                    }
+                }
+            }
+            pel[cbase[lc] + (t - cstart[lc])] = group_b_emit(e, dup2, dup3, mode, acc);
         }
         __syncthreads();
         b = be;
+    }
+    const unsigned long long d2 = wave_sum(acc.d2), d3 = wave_sum(acc.d3);
+    if (lane == 0) {
+        if (d2) atomicAdd(&st->dup_pos, d2);
+        if (d3) atomicAdd(&st->dup_len, d3);
     }
 }
 
@@ -703,12 +836,6 @@ __device__ void pile_slow(const uint8_t* __restrict__ rec, int32_t start, uint32
     if (max(ref - (int64_t)start, (int64_t)lseq) > (int64_t)max_span) span_err = true;
 }
 
-#ifndef MGP_PIPE
-#define MGP_PIPE 0  // pileup: load a batch's records one batch ahead (needs MGP_PILEUP_WAVES=3)
-#endif
-#ifndef MGP_QPERM
-#define MGP_QPERM 0
-#endif
 #ifndef MGP_WIN
 #define MGP_WIN 1024  // target window width (positions); W <= kMaxPosPerThread * 256
 #endif
@@ -928,28 +1055,20 @@ __device__ __forceinline__ void pile_line(bool has, const uint8_t* __restrict__ 
 constexpr int kWaveQ = 2 * kWave;    // per-wave queue of reads waiting to be piled (LDS)
 constexpr uint32_t kSeg = 65535;     // elements per tile segment (16-bit halves cannot carry)
 
-__device__ __forceinline__ bool same_dup(const GElem& p, const GElem& e, bool& dup3) {
-    if (((p.w ^ e.w) & GM_REV) != 0ull) return false;
-    if (p.tlen == e.tlen) dup3 = true;
-    return true;
-}
-
 // grid (nchunks, nwin): workgroup = (cell chunk, position window). For each cell
-// of the chunk, the cell's grouping elements with start bin in [window start -
-// reach, window end) are processed by the 4 waves independently, in interleaved
-// chunks of 64: duplicates are marked by a walk back over equal starts (first in
-// BAM order wins; shuffles inside the chunk, global loads across it), kept
-// MAPQ-passing reads go to the wave's LDS queue and are piled 64 at a time, one
-// read per lane. Workgroup barriers only at cell boundaries; the packed tile is
-// then strand-filtered and flushed.
-#ifndef MGP_XCD_REMAP
-#define MGP_XCD_REMAP 0
-#endif
+// of the chunk, the cell's pileup elements with start bin in [window start -
+// reach, window end) are taken by the 4 waves independently, in interleaved
+// chunks of 64 (the next chunk's elements loaded while the current one is
+// queued); the reads marked for piling (kept by pass B's duplicate marking, MAPQ
+// passed) go to the wave's LDS queue and are piled 64 at a time, one read per
+// lane. The window owning a read's start bin counts it for the per-cell kept-read
+// total and flags (processors.py:22,34,48). Workgroup barriers only at cell
+// boundaries; the packed tile is then strand-filtered and flushed.
 #ifndef MGP_PILEUP_WAVES
 #define MGP_PILEUP_WAVES 4
 #endif
 __global__ void __launch_bounds__(kBlock, MGP_PILEUP_WAVES) k_pileup(
-    Geom g, PileCfg pc, const uint8_t* __restrict__ payload, const GElem* __restrict__ gel,
+    Geom g, PileCfg pc, const uint8_t* __restrict__ payload, const unsigned long long* __restrict__ pel,
     const uint32_t* __restrict__ O, uint32_t* __restrict__ counts, uint32_t* __restrict__ tn5,
     uint32_t* __restrict__ depth, uint32_t* __restrict__ n_reads, uint8_t* __restrict__ any_paired,
     uint32_t* __restrict__ covered, unsigned long long* __restrict__ dsum, uint32_t* __restrict__ dmax,
@@ -958,8 +1077,7 @@ __global__ void __launch_bounds__(kBlock, MGP_PILEUP_WAVES) k_pileup(
     uint32_t* t5 = tile + 4 * g.Wp;
     __shared__ unsigned long long wq_all[kBlock / kWave][kWaveQ];
     __shared__ uint32_t r_cov[4], r_max[4], r_keep[4];
-    __shared__ unsigned long long r_sum[4];
-    __shared__ int r_pair[4];
+    __shared__ unsigned long long r_sum[4], r_flags[4];
 
     const int k = blockIdx.y;
     const int chunk = blockIdx.x;
@@ -970,9 +1088,6 @@ __global__ void __launch_bounds__(kBlock, MGP_PILEUP_WAVES) k_pileup(
     const int L = g.L;
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     unsigned long long* wq = wq_all[wid];
-    // queue slot piled by this lane: MGP_QPERM spreads neighbouring reads (often equal
-    // starts, hence equal LDS addresses) over the two 32-lane halves of an LDS access
-    const int qslot = MGP_QPERM ? (((lane & 31) << 1) | (lane >> 5)) : lane;
     const uint32_t max_span = st->max_span;
     const int R = (int)((max_span + g.G - 1) / g.G) * g.G;
     const int lo_bin = win_lo_bin(k, R, g);
@@ -980,9 +1095,7 @@ __global__ void __launch_bounds__(kBlock, MGP_PILEUP_WAVES) k_pileup(
     const int hi_bin = k == g.nwin - 1 ? g.nbins : win_hi_bin(k, g);
     const int nc = g.nc;
     const unsigned long long lt = lanemask_lt();
-    const bool dedup = MGP_ABL != 5 && pc.dedup_mode != MGP_DEDUP_NONE;
-    bool span_err = false, bad = false;
-    unsigned long long d2 = 0, d3 = 0;
+    bool span_err = false, bad_read = false;  // the latter: a kept read without SEQ/QUAL
 
     uint32_t tal[kMaxPosPerThread][4];
 #pragma unroll
@@ -1004,110 +1117,40 @@ __global__ void __launch_bounds__(kBlock, MGP_PILEUP_WAVES) k_pileup(
             n_hi = O[(size_t)hi_bin * nc + c + 1];
         }
         const bool drained = hi - lo > kSeg;  // tile drained into the output rows between segments
+        // kept reads and their flags, counted once: by the window owning the start bin
         uint32_t nkeep = 0;
-        bool paired = false;
+        unsigned long long fl = 0;
         __syncthreads();
         for (uint32_t seg = lo; seg < hi; seg += kSeg) {
             const uint32_t seg_hi = min(hi, seg + kSeg);
             uint32_t qn = 0;  // wave-uniform queue fill
-            bool pend = false;  // MGP_PIPE: a loaded batch waits in PR
-            RecLine PR;
-            const uint8_t* pend_rec = payload;
-            for (uint32_t cb = seg + kWave * wid; cb < seg_hi; cb += kBlock) {
-                const uint32_t j = cb + lane;
-                const bool act = j < seg_hi;
-                GElem e;
-                e.w = 0;
-                e.start = INT_MIN;
-                e.tlen = 0;
-                if (act) e = gel[j];
-                // the element just before the chunk, loaded with it (lane 0 only)
-                GElem pe;
-                pe.w = 0;
-                pe.start = INT_MIN;
-                pe.tlen = 0;
-                if (dedup && lane == 0 && cb > lo) pe = gel[cb - 1];
-                bool dup2 = false, dup3 = false;
-                if (dedup) {
-                    // duplicates sit just before j in BAM order among equal starts: runs of
-                    // equal starts are found by one shuffle; inside a run only |tlen| is
-                    // shuffled (the strand bit comes from a ballot)
-                    const int ps = __shfl_up(e.start, 1, kWave);
-                    const bool eqp = act && lane > 0 && ps == e.start;
-                    const unsigned long long heads = __ballot(!eqp);
-                    const int head = 63 - __builtin_clzll(heads & (lt | (1ull << lane)));
-                    const unsigned long long revm = __ballot(act && (e.w & GM_REV) != 0ull);
-                    const bool myrev = (e.w & GM_REV) != 0ull;
-                    const int maxd = __builtin_amdgcn_readfirstlane(wave_max(act ? lane - head : 0));
-                    for (int m = 1; m <= maxd; ++m) {
-                        const uint32_t pt = __shfl_up(e.tlen, m, kWave);
-                        if (act && lane - m >= head && (((revm >> (lane - m)) & 1ull) != 0ull) == myrev) {
-                            dup2 = true;
-                            if (pt == e.tlen) dup3 = true;
-                        }
-                    }
-                    // the first run of the chunk may continue before it
-                    const int ps0 = __shfl(pe.start, 0, kWave);
-                    if (act && head == 0 && cb > lo && ps0 == e.start) {
-                        const unsigned long long pw0 = __shfl(pe.w, 0, kWave);
-                        const uint32_t pt0 = __shfl(pe.tlen, 0, kWave);
-                        GElem p0;
-                        p0.w = pw0;
-                        p0.start = ps0;
-                        p0.tlen = pt0;
-                        if (same_dup(p0, e, dup3)) dup2 = true;
-                        if (!dup3) {
-                            for (uint32_t mm = cb - 1; mm-- > lo;) {
-                                const GElem p = gel[mm];
-                                if (p.start != e.start) break;
-                                if (same_dup(p, e, dup3)) {
-                                    dup2 = true;
-                                    if (dup3) break;
-                                }
-                            }
-                        }
-                    }
+            uint32_t cb = seg + kWave * wid;
+            unsigned long long pe = cb + lane < seg_hi ? pel[cb + lane] : 0ull;
+            for (; cb < seg_hi; cb += kBlock) {
+                const unsigned long long cur = pe;
+                const uint64_t nj = (uint64_t)cb + kBlock + lane;
+                pe = nj < seg_hi ? pel[nj] : 0ull;
+                if (cb + lane >= own) {  // cur is 0 past seg_hi
+                    nkeep += (cur & GP_KEEP) != 0ull;
+                    fl |= cur;
                 }
-                const bool keep = !dedup ? true : pc.dedup_mode == MGP_DEDUP_START ? !dup2 : !dup3;
-                if (act && j >= own) {  // statistics counted once, by the window owning the start bin
-                    d2 += dup2;
-                    d3 += dup3;
-                    if (keep) {
-                        ++nkeep;
-                        paired |= (e.w & GM_PAIRED) != 0ull;
-                        bad |= (e.w & GM_BAD) != 0ull;
-                    }
-                }
-                const bool piled = act && keep && (e.w & GM_MAPQ_OK);
+                const bool piled = (cur & GP_PILE) != 0ull;
                 const unsigned long long bal = __ballot(piled);
-                if (piled) wq[qn + (uint32_t)__popcll(bal & lt)] = e.w;
+                if (piled) wq[qn + (uint32_t)__popcll(bal & lt)] = cur;
                 qn += (uint32_t)__popcll(bal);
                 __builtin_amdgcn_wave_barrier();
                 if (qn >= (uint32_t)kWave) {
-                    const unsigned long long qe = wq[qslot];
-                    if (MGP_PIPE) {
-                        // the batch's record lines are loaded now and piled at the next full
-                        // batch (or the tail): their latency overlaps the next chunks' work
-                        if (pend) pile_line(true, pend_rec, PR, w, pc, tile, t5, max_span, span_err);
-                        pend_rec = payload + (qe & GM_OFF);
-                        load_line(true, pend_rec, w, PR);
-                        pend = true;
-                    } else {
-                        pile_read(true, payload + (qe & GM_OFF), w, pc, tile, t5, max_span, span_err);
-                    }
+                    const unsigned long long qe = wq[lane];
+                    pile_read(true, payload + (qe & GP_OFF), w, pc, tile, t5, max_span, span_err);
                     qn -= kWave;
                     if ((uint32_t)lane < qn) wq[lane] = wq[kWave + lane];
                     __builtin_amdgcn_wave_barrier();
                 }
             }
-            if (MGP_PIPE && pend) {
-                pile_line(true, pend_rec, PR, w, pc, tile, t5, max_span, span_err);
-                pend = false;
-            }
             {   // tail: every lane of the wave enters, lanes past qn hold no read
-                const bool has = (uint32_t)qslot < qn;
-                const unsigned long long qe = has ? wq[qslot] : 0ull;
-                pile_read(has, payload + (qe & GM_OFF), w, pc, tile, t5, max_span, span_err);
+                const bool has = (uint32_t)lane < qn;
+                const unsigned long long qe = has ? wq[lane] : 0ull;
+                pile_read(has, payload + (qe & GP_OFF), w, pc, tile, t5, max_span, span_err);
             }
             if (drained) {  // add this segment's packed tile into the 32-bit output rows
                 __syncthreads();
@@ -1131,7 +1174,7 @@ __global__ void __launch_bounds__(kBlock, MGP_PILEUP_WAVES) k_pileup(
             }
         }
         nkeep = wave_sum(nkeep);
-        const bool anyp = __ballot(paired) != 0ull;
+        fl = wave_or(fl);
         __syncthreads();
         uint32_t cov = 0, mx = 0;
         unsigned long long sum = 0;
@@ -1197,19 +1240,18 @@ __global__ void __launch_bounds__(kBlock, MGP_PILEUP_WAVES) k_pileup(
             r_sum[wid] = sum;
             r_max[wid] = mx;
             r_keep[wid] = nkeep;
-            r_pair[wid] = anyp;
+            r_flags[wid] = fl;
         }
         __syncthreads();
         if (threadIdx.x == 0) {
             uint32_t C = 0, M = 0, K = 0;
-            unsigned long long S = 0;
-            int PP = 0;
+            unsigned long long S = 0, F = 0;
             for (int q = 0; q < 4; ++q) {
                 C += r_cov[q];
                 S += r_sum[q];
                 M = max(M, r_max[q]);
                 K += r_keep[q];
-                PP |= r_pair[q];
+                F |= r_flags[q];
             }
             if (C) {
                 atomicAdd(&covered[c], C);
@@ -1217,7 +1259,8 @@ __global__ void __launch_bounds__(kBlock, MGP_PILEUP_WAVES) k_pileup(
                 atomicMax(&dmax[c], M);
             }
             if (K) atomicAdd(&n_reads[c], K);
-            if (PP) any_paired[c] = 1;  // benign race: every writer stores 1
+            if (F & GP_PAIRED) any_paired[c] = 1;  // benign race: every writer stores 1
+            if (F & GP_BAD) bad_read = true;
         }
     }
 #pragma unroll
@@ -1228,15 +1271,9 @@ __global__ void __launch_bounds__(kBlock, MGP_PILEUP_WAVES) k_pileup(
             *tp = make_uint4(tal[m][0], tal[m][1], tal[m][2], tal[m][3]);
         }
     }
-    d2 = wave_sum(d2);
-    d3 = wave_sum(d3);
-    const bool anyspan = __ballot(span_err) != 0ull, anybad = __ballot(bad) != 0ull;
-    if (lane == 0) {
-        if (d2) atomicAdd(&st->dup_pos, d2);
-        if (d3) atomicAdd(&st->dup_len, d3);
-        if (anyspan) atomicOr(&st->err, ERR_SPAN);
-        if (anybad) atomicOr(&st->err, ERR_BADREAD);
-    }
+    const bool anyspan = __ballot(span_err) != 0ull;
+    if (lane == 0 && anyspan) atomicOr(&st->err, ERR_SPAN);
+    if (threadIdx.x == 0 && bad_read) atomicOr(&st->err, ERR_BADREAD);
 }
 
 // min-reads gate (processors.py:22) for min_reads > 1: a cell with fewer kept
@@ -1371,13 +1408,15 @@ __global__ void __launch_bounds__(kBlock) k_median(Geom g, int min_reads, const 
     }
 }
 
+// grid (ceil(L4 / 256), ny): slice y sums the chunks y, y + ny, ... and adds into
+// the zeroed u64 tallies
 __global__ void k_tally_reduce(const uint32_t* __restrict__ part, int nchunks, int L4,
                                unsigned long long* __restrict__ tally) {
-    int x = blockIdx.x * blockDim.x + threadIdx.x;
+    const int x = blockIdx.x * blockDim.x + threadIdx.x;
     if (x >= L4) return;
     unsigned long long acc = 0;
-    for (int ch = 0; ch < nchunks; ++ch) acc += part[(size_t)ch * L4 + x];
-    tally[x] = acc;
+    for (int ch = blockIdx.y; ch < nchunks; ch += gridDim.y) acc += part[(size_t)ch * L4 + x];
+    if (acc) atomicAdd(&tally[x], acc);
 }
 
 __global__ void k_add_u64(uint64_t* __restrict__ a, int64_t n, uint64_t add) {
@@ -1388,6 +1427,9 @@ __global__ void k_add_u64(uint64_t* __restrict__ a, int64_t n, uint64_t add) {
 // ---------------------------------------------------------------------------
 // host side
 // ---------------------------------------------------------------------------
+#ifndef MGP_PILE_WG
+#define MGP_PILE_WG 16384
+#endif
 static inline unsigned blocks_for(int64_t n, int bs = kBlock) { return (unsigned)((n + bs - 1) / bs); }
 
 static int configure_geometry(mgp_ctx* ctx) {
@@ -1406,8 +1448,8 @@ static int configure_geometry(mgp_ctx* ctx) {
     // offset is a shift folded into the address add (A/B: no bank-conflict cost)
     g.Wp = kTilePitch;
     g.nc = c.n_cells;
-    // cells per pileup workgroup: ~4096 workgroups over the windows
-    int64_t target = 4096;
+    // cells per pileup workgroup: ~MGP_PILE_WG workgroups over the windows
+    int64_t target = MGP_PILE_WG;
     int64_t cpb = ((int64_t)g.nc * g.nwin + target - 1) / target;
     g.cpb = (int)std::max<int64_t>(1, std::min<int64_t>(cpb, 64));
     g.nchunks = g.nc > 0 ? (g.nc + g.cpb - 1) / g.cpb : 0;
@@ -1503,7 +1545,8 @@ void mgp_close(mgp_ctx* ctx) {
     if (ctx->comm) ncclCommDestroy(ctx->comm);
     DevBuf* bufs[] = {&ctx->start,     &ctx->bc,        &ctx->tlen,     &ctx->flag,       &ctx->mapq,
                       &ctx->span,      &ctx->roff,      &ctx->payload,  &ctx->bin_start,  &ctx->gel2,
-                      &ctx->H,         &ctx->P,         &ctx->cell_cnt, &ctx->cell_base,  &ctx->gel,
+                      &ctx->H,         &ctx->P,         &ctx->cell_cnt, &ctx->cell_base,  &ctx->pel,
+                      &ctx->PG,        &ctx->F,
                       &ctx->tally_part, &ctx->tally,   &ctx->n_reads,    &ctx->any_paired,
                       &ctx->passed,    &ctx->covered,   &ctx->dsum,     &ctx->dmax,       &ctx->med_lo,
                       &ctx->med_hi,    &ctx->first_read, &ctx->counts,  &ctx->tn5,        &ctx->depth,
@@ -1594,10 +1637,12 @@ static int ensure_run_buffers(mgp_ctx* ctx) {
     const size_t L = (size_t)g.L;
     MGP_TRY(ctx->bin_start.ensure((size_t)(g.nbins + 1) * 4));
     MGP_TRY(ctx->H.ensure((size_t)(g.nbins + 1) * nc * 4));
+    MGP_TRY(ctx->PG.ensure((size_t)g.nbins * kParts * ((nc + kGroup - 1) / kGroup) * 4));
+    MGP_TRY(ctx->F.ensure((size_t)g.nbins * ((nc + 31) / 32) * 4));
     MGP_TRY(ctx->P.ensure((size_t)((g.nbins + 31) / 32 + 1) * nc * 4));
     MGP_TRY(ctx->cell_cnt.ensure(nc * 4));
     MGP_TRY(ctx->cell_base.ensure(nc * 4));
-    MGP_TRY(ctx->gel.ensure(n * sizeof(GElem)));
+    MGP_TRY(ctx->pel.ensure(n * 8));
     MGP_TRY(ctx->gel2.ensure(n * sizeof(GElem)));
     MGP_TRY(ctx->bin_valid.ensure((size_t)(g.nbins + 1) * 4));
     MGP_TRY(ctx->bin_base.ensure((size_t)(g.nbins + 1) * 4));
@@ -1647,22 +1692,26 @@ int mgp_run(mgp_ctx* ctx) {
     }
 
     if (nc > 0) {
-        const bool lds = nc <= ctx->lds_hist_max_cells;
-        // 1. per (start bin, cell) histogram + bin bounds + order check
+        const bool lds = nc + (nc + kGroup - 1) / kGroup <= ctx->lds_hist_max_cells;
+        const int ngroups = (nc + kGroup - 1) / kGroup;
+        // 1. per (start bin, cell) histogram + per (bin, part, group) counts + bin bounds + order check
         STAGE_BEGIN(ST_HIST);
         if (!lds || n == 0) HIP_TRY(hipMemsetAsync(ctx->H.p, 0, (size_t)(g.nbins + 1) * nc * 4, s));
         if (n == 0) HIP_TRY(hipMemsetAsync(ctx->bin_start.p, 0, (size_t)(g.nbins + 1) * 4, s));
+        HIP_TRY(hipMemsetAsync(ctx->F.p, 0, (size_t)g.nbins * ((nc + 31) / 32) * 4, s));
         if (n > 0) {
+            if ((size_t)ngroups * 8 > (size_t)ctx->lds_hist_max_cells * 4)
+                return set_err(MGP_E_INVALID, "too many cells for one context (histogram LDS)");
             if (lds)
-                k_bin_count<true><<<g.nbins, kBlock, (size_t)nc * 4, s>>>(
+                k_bin_count<true><<<g.nbins, kHistBlock, (size_t)(nc + ngroups) * 4, s>>>(
                     ctx->start.as<int32_t>(), ctx->bc.as<int32_t>(), ctx->flag.as<uint16_t>(),
-                    ctx->span.as<uint32_t>(), n, g, ctx->H.as<uint32_t>(), ctx->bin_start.as<uint32_t>(),
-                    ctx->bin_valid.as<uint32_t>(), st);
+                    ctx->span.as<uint32_t>(), n, g, ctx->H.as<uint32_t>(), ctx->PG.as<uint32_t>(), ngroups,
+                    ctx->bin_start.as<uint32_t>(), ctx->bin_valid.as<uint32_t>(), st);
             else
-                k_bin_count<false><<<g.nbins, kBlock, 0, s>>>(ctx->start.as<int32_t>(), ctx->bc.as<int32_t>(),
-                                                              ctx->flag.as<uint16_t>(), ctx->span.as<uint32_t>(), n,
-                                                              g, ctx->H.as<uint32_t>(), ctx->bin_start.as<uint32_t>(),
-                                                              ctx->bin_valid.as<uint32_t>(), st);
+                k_bin_count<false><<<g.nbins, kHistBlock, (size_t)ngroups * 8, s>>>(
+                    ctx->start.as<int32_t>(), ctx->bc.as<int32_t>(), ctx->flag.as<uint16_t>(),
+                    ctx->span.as<uint32_t>(), n, g, ctx->H.as<uint32_t>(), ctx->PG.as<uint32_t>(), ngroups,
+                    ctx->bin_start.as<uint32_t>(), ctx->bin_valid.as<uint32_t>(), st);
             HIP_TRY(hipGetLastError());
         }
         STAGE_END(ST_HIST);
@@ -1675,15 +1724,15 @@ int mgp_run(mgp_ctx* ctx) {
         k_scan_colsum<<<g2, kBlock, 0, s>>>(ctx->H.as<uint32_t>(), g.nbins, nc, RB, ctx->P.as<uint32_t>());
         k_scan_rows<<<blocks_for(nc), kBlock, 0, s>>>(ctx->P.as<uint32_t>(), nrb, nc, ctx->cell_cnt.as<uint32_t>());
         k_scan_cells<<<1, 1024, 0, s>>>(ctx->cell_cnt.as<uint32_t>(), nc, ctx->cell_base.as<uint32_t>());
-        k_scan_apply<<<g2, kBlock, 0, s>>>(ctx->H.as<uint32_t>(), ctx->P.as<uint32_t>(), ctx->cell_base.as<uint32_t>(),
-                                           ctx->cell_cnt.as<uint32_t>(), g.nbins, nc, RB, nrb);
+        k_scan_apply<<<g2, kBlock, 0, s>>>(ctx->H.as<uint32_t>(), ctx->P.as<uint32_t>(),
+                                           ctx->cell_base.as<uint32_t>(), ctx->cell_cnt.as<uint32_t>(), g.nbins, nc,
+                                           RB, nrb, ctx->F.as<uint32_t>());
         HIP_TRY(hipGetLastError());
         STAGE_END(ST_SCAN);
 
-        // 3. stable grouping into cell-major order (two passes)
-        STAGE_BEGIN(ST_SCATTER);
+        // 3. stable grouping into cell-major order (two passes), duplicate marking in pass B
+        STAGE_BEGIN(ST_GROUP_A);
         if (n > 0) {
-            const int ngroups = (nc + kGroup - 1) / kGroup;
             int gbits = 0;
             while (gbits < 31 && (1 << gbits) < ngroups) ++gbits;
             k_scan_cells<<<1, 1024, 0, s>>>(ctx->bin_valid.as<uint32_t>(), g.nbins, ctx->bin_base.as<uint32_t>());
@@ -1692,21 +1741,30 @@ int mgp_run(mgp_ctx* ctx) {
                 return set_err(MGP_E_INVALID, "too many cells for one context (grouping LDS)");
             if ((uint64_t)ctx->pay >= (1ull << GM_LCELL_SHIFT))
                 return set_err(MGP_E_INVALID, "payload too large (record offsets must stay below 2^50)");
-            k_group_a<<<g.nbins, kBlock, a_lds, s>>>(
+            dim3 ga((unsigned)g.nbins, kParts);
+            k_group_a<<<ga, kBlock, a_lds, s>>>(
                 n, ctx->start.as<int32_t>(), ctx->bc.as<int32_t>(), ctx->tlen.as<int32_t>(), ctx->flag.as<uint16_t>(),
                 ctx->mapq.as<uint8_t>(), ctx->roff.as<uint64_t>(), ctx->bin_start.as<uint32_t>(),
-                ctx->H.as<uint32_t>(), ctx->bin_base.as<uint32_t>(), g, ngroups, gbits,
+                ctx->PG.as<uint32_t>(), ctx->F.as<uint32_t>(), ctx->bin_base.as<uint32_t>(), g, ngroups, gbits,
                 ctx->cfg.min_mapq, ctx->bucket_off.as<uint32_t>(), ctx->gel2.as<GElem>(),
-                ctx->first_read.as<uint32_t>());
-            HIP_TRY(hipGetLastError());
-            // about 2048 workgroups: bins per workgroup from the group count
-            const int rb = std::max(1, (int)(((int64_t)ngroups * g.nbins + 2047) / 2048));
-            dim3 gb((unsigned)ngroups, (unsigned)((g.nbins + rb - 1) / rb));
-            k_group_b<<<gb, kBlock, 0, s>>>(ctx->gel2.as<GElem>(), ctx->bucket_off.as<uint32_t>(), ctx->H.as<uint32_t>(),
-                                            g, ngroups, rb, ctx->gel.as<GElem>());
+                ctx->first_read.as<uint32_t>(), st);
             HIP_TRY(hipGetLastError());
         }
-        STAGE_END(ST_SCATTER);
+        STAGE_END(ST_GROUP_A);
+        STAGE_BEGIN(ST_GROUP_B);
+        if (n > 0) {
+            // about MGP_GB_WG workgroups (many per slot: 4 fit a CU, so a grid of a few
+            // slot-rounds leaves a tail); bins per workgroup at most kMaxRbB, whose
+            // bucket sizes the workgroup keeps in LDS
+            const int64_t tgt = MGP_GB_WG;
+            const int rb = std::min(kMaxRbB, std::max(1, (int)(((int64_t)ngroups * g.nbins + tgt - 1) / tgt)));
+            dim3 gb((unsigned)ngroups, (unsigned)((g.nbins + rb - 1) / rb));
+            k_group_b<<<gb, kBlock, 0, s>>>(ctx->gel2.as<GElem>(), ctx->bucket_off.as<uint32_t>(), ctx->H.as<uint32_t>(),
+                                            g, ngroups, rb, ctx->cfg.dedup_mode,
+                                            ctx->pel.as<unsigned long long>(), st);
+            HIP_TRY(hipGetLastError());
+        }
+        STAGE_END(ST_GROUP_B);
 
         // 5. dedup + pileup + strand filter + stats
         STAGE_BEGIN(ST_PILEUP);
@@ -1720,7 +1778,7 @@ int mgp_run(mgp_ctx* ctx) {
         pc.keep_tn5 = (ctx->cfg.flags & MGP_CFG_KEEP_TN5) != 0;
         dim3 gp(g.nchunks, g.nwin);
         const size_t psm = (size_t)5 * g.Wp * 4;
-        k_pileup<<<gp, kBlock, psm, s>>>(g, pc, ctx->payload.as<uint8_t>(), ctx->gel.as<GElem>(),
+        k_pileup<<<gp, kBlock, psm, s>>>(g, pc, ctx->payload.as<uint8_t>(), ctx->pel.as<unsigned long long>(),
                                          ctx->H.as<uint32_t>(), ctx->counts.as<uint32_t>(), ctx->tn5.as<uint32_t>(),
                                          ctx->depth.as<uint32_t>(), ctx->n_reads.as<uint32_t>(),
                                          ctx->any_paired.as<uint8_t>(), ctx->covered.as<uint32_t>(),
@@ -1762,8 +1820,10 @@ int mgp_run(mgp_ctx* ctx) {
 
         // 8. tallies
         STAGE_BEGIN(ST_TALLY);
-        k_tally_reduce<<<blocks_for((int64_t)g.L * 4), kBlock, 0, s>>>(
-            ctx->tally_part.as<uint32_t>(), g.nchunks, g.L * 4, ctx->tally.as<unsigned long long>());
+        HIP_TRY(hipMemsetAsync(ctx->tally.p, 0, (size_t)g.L * 32, s));
+        dim3 gt(blocks_for((int64_t)g.L * 4), (unsigned)std::max(1, std::min(g.nchunks, 32)));
+        k_tally_reduce<<<gt, kBlock, 0, s>>>(ctx->tally_part.as<uint32_t>(), g.nchunks, g.L * 4,
+                                             ctx->tally.as<unsigned long long>());
         HIP_TRY(hipGetLastError());
         STAGE_END(ST_TALLY);
     } else {

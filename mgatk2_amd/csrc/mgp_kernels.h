@@ -76,6 +76,11 @@ __device__ __forceinline__ T wave_max(T v) {
     return v;
 }
 template <typename T>
+__device__ __forceinline__ T wave_or(T v) {
+    for (int o = kWave / 2; o > 0; o >>= 1) v |= __shfl_xor(v, o, kWave);
+    return v;
+}
+template <typename T>
 __device__ __forceinline__ T wave_min(T v) {
     for (int o = kWave / 2; o > 0; o >>= 1) {
         T w = __shfl_xor(v, o, kWave);

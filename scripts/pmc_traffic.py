@@ -22,7 +22,7 @@ for f in glob.glob(f"{root}/pmc_*/**/*counter_collection.csv", recursive=True):
         for row in csv.DictReader(fh):
             name = row.get("Kernel_Name", "?").split("(")[0].split("<")[0].replace("void ", "").strip()
             acc[name][row["Counter_Name"]].append(float(row["Counter_Value"]))
-stage = {"k_pileup": "pileup", "k_group_a": "scatter", "k_group_b": "scatter", "k_bin_count": "hist",
+stage = {"k_pileup": "pileup", "k_group_a": "group_a", "k_group_b": "group_b", "k_bin_count": "hist",
          "k_median": "median"}
 res = {"reads": reads, "cells": cells, "unit": "bytes per launch",
        "method": "2*FETCH_SIZE + WRITE_SIZE (KB->B), mean over dispatches; gfx950 FETCH_SIZE correction",
@@ -35,7 +35,7 @@ for k, cs in acc.items():
     f = sum(fetch) / len(fetch) * 1024
     w = sum(write) / len(write) * 1024
     res["raw"][k] = {"fetch_size_B": f, "write_size_B": w}
-    if k in stage:  # the scatter stage is two kernels (group passes A and B): their bytes add
+    if k in stage:
         res[stage[k]] = res.get(stage[k], 0.0) + 2 * f + w
 out.parent.mkdir(parents=True, exist_ok=True)
 out.write_text(json.dumps(res, indent=1))

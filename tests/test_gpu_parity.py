@@ -241,3 +241,24 @@ def test_many_cells_global_histogram_path(engine_lib, oracle_lib):
     res = run_engine(engine_lib, cfg, soa)
     exp, _ = oracle_lib.oracle_run(cfg, soa)
     assert_same(res, exp, "30k cells")
+
+
+def test_deep_bins_parts_and_direct_buckets(engine_lib, oracle_lib):
+    """All reads start inside 8 start bins: every bin's parts hold tens of thousands
+    of reads (per-part group counts of the histogram feed pass A's slots) and every
+    (bin, 64-cell group) bucket exceeds pass B's LDS stage (direct path with the
+    bucket walk-back duplicate marking)."""
+    from mgatk2_amd.engine import EngineConfig
+    from mgatk2_amd.synth import synth_reads
+
+    soa = synth_reads(91, 300_000, 200)
+    new = (1000 + soa.start.astype(np.int64) * 64 // 16569).astype(np.int32)  # monotone: order kept
+    soa.start[:] = new
+    hdr = soa.payload.view(np.uint8)
+    for k in range(4):  # record header: int32 start at +0 (include/mgpileup.h)
+        hdr[soa.rec_off.astype(np.int64) + k] = ((new.view(np.uint32) >> (8 * k)) & 0xFF).astype(np.uint8)
+    for mode in ("alignment_and_fragment_length", "alignment_start", "none"):
+        cfg = EngineConfig(n_cells=200, min_baseq=20, min_mapq=30, dedup_mode=mode, min_reads=1)
+        res = run_engine(engine_lib, cfg, soa)
+        exp, _ = oracle_lib.oracle_run(cfg, soa)
+        assert_same(res, exp, f"deep bins {mode}")
