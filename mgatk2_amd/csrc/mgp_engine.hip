@@ -666,15 +666,24 @@ __device__ __forceinline__ void group_b_rank(const GElem* __restrict__ gel2, uin
     }
 }
 
+// A step: the group's buckets of consecutive bins [b, be) that fit the stage, taken
+// as one flat sequence (bin order, BAM order inside a bucket = start order). Each
+// wave loads its quarter of the sequence at once (8 independent 16-byte loads per
+// lane) and ranks it by cell (ballot peers, per-wave per-cell counters); the
+// waves' counts give every cell its run in the stage and every wave its place in
+// the run, so the stage fills in (cell, bin, BAM) order. A cell's run is then
+// written to its slots, which continue where the previous step's ended (cbase).
+constexpr int kBPer = kStageB / kBlock;  // elements per lane per step
+
 __global__ void __launch_bounds__(kBlock) k_group_b(const GElem* __restrict__ gel2,
                                                     const uint32_t* __restrict__ bucket_off,
                                                     const uint32_t* __restrict__ O, Geom g, int ngroups, int rb,
                                                     int mode, unsigned long long* __restrict__ pel,
                                                     DevStats* st) {
     __shared__ GElem stage[kStageB];
-    __shared__ uint32_t cnt[kBlock / kWave][kGroup];
+    __shared__ uint32_t wcnt[kBlock / kWave][kGroup];
     __shared__ uint32_t cbase[kGroup], cstart[kGroup + 1];
-    __shared__ uint32_t bsz[kMaxRbB];
+    __shared__ uint32_t bst[kMaxRbB], bsz[kMaxRbB], spre[kMaxRbB + 1];
     __shared__ int s_be;
     const int gi = blockIdx.x;
     const int B0 = blockIdx.y * rb, B1 = min(g.nbins, B0 + rb);
@@ -685,18 +694,24 @@ __global__ void __launch_bounds__(kBlock) k_group_b(const GElem* __restrict__ ge
     const size_t bo = (size_t)ngroups + 1;
     const bool dedup = mode != MGP_DEDUP_NONE;
     DedupAcc acc;
-    for (int x = threadIdx.x; x < B1 - B0; x += kBlock)
-        bsz[x] = bucket_off[(size_t)(B0 + x) * bo + gi + 1] - bucket_off[(size_t)(B0 + x) * bo + gi];
+    for (int x = threadIdx.x; x < B1 - B0; x += kBlock) {
+        const uint32_t o0 = bucket_off[(size_t)(B0 + x) * bo + gi];
+        bst[x] = o0;
+        bsz[x] = bucket_off[(size_t)(B0 + x) * bo + gi + 1] - o0;
+    }
+    if (wid == 0) cbase[lane] = c < nc ? O[(size_t)B0 * nc + c] : 0u;  // each cell's next slot
     __syncthreads();
     for (int b = B0; b < B1;) {
         if (threadIdx.x == 0) {  // bins of this step: as many as fit the stage
             uint32_t tot = 0;
             int be = b;
+            spre[0] = 0;
             while (be < B1) {
                 const uint32_t sz = bsz[be - B0];
                 if (tot + sz > (uint32_t)kStageB) break;
                 tot += sz;
                 ++be;
+                spre[be - b] = tot;
             }
             s_be = be;
         }
@@ -704,65 +719,115 @@ __global__ void __launch_bounds__(kBlock) k_group_b(const GElem* __restrict__ ge
         const int be = s_be;
         if (be == b) {  // one bucket larger than the stage: direct stores (wave 0)
             if (wid == 0) {
-                cnt[0][lane] = c < nc ? O[(size_t)b * nc + c] : 0u;
+                wcnt[0][lane] = cbase[lane];
                 __builtin_amdgcn_wave_barrier();
-                group_b_rank<false>(gel2, bucket_off[(size_t)b * bo + gi], bucket_off[(size_t)b * bo + gi + 1],
-                                    cnt[0], lane, lt, nullptr, nullptr, nullptr, mode, pel, acc);
+                group_b_rank<false>(gel2, bst[b - B0], bst[b - B0] + bsz[b - B0], wcnt[0], lane, lt, nullptr,
+                                    nullptr, nullptr, mode, pel, acc);
+                __builtin_amdgcn_wave_barrier();
+                cbase[lane] = wcnt[0][lane];
             }
             __syncthreads();
             ++b;
             continue;
         }
-        if (wid == 0) {  // per-cell runs of the step: base slot and place in the stage
-            const uint32_t o0 = c < nc ? O[(size_t)b * nc + c] : 0u;
-            const uint32_t len = c < nc ? O[(size_t)be * nc + c] - o0 : 0u;
-            uint32_t x = len;
+        const int nb = be - b;
+        const uint32_t tot = spre[nb];
+        // load this wave's quarter of the flat sequence (all loads issued together)
+        GElem e[kBPer];
+#pragma unroll
+        for (int u = 0; u < kBPer; ++u) {
+            const uint32_t t = (uint32_t)(wid * (kBPer * kWave) + u * kWave + lane);
+            e[u].w = 0;
+            e[u].start = 0;
+            e[u].tlen = 0;
+            if (t < tot) {
+                int lo = 0, hi = nb;  // bin k of t: spre[k] <= t < spre[k + 1]
+                while (hi - lo > 1) {
+                    const int mid = (lo + hi) >> 1;
+                    if (spre[mid] <= t) lo = mid;
+                    else hi = mid;
+                }
+                e[u] = gel2[bst[b - B0 + lo] + (t - spre[lo])];
+            }
+        }
+        // rank by cell inside the wave's quarter (stable)
+        wcnt[wid][lane] = 0;
+        __builtin_amdgcn_wave_barrier();
+        uint32_t rk[kBPer];
+#pragma unroll
+        for (int u = 0; u < kBPer; ++u) {
+            const uint32_t t = (uint32_t)(wid * (kBPer * kWave) + u * kWave + lane);
+            const bool act = t < tot;
+            const int lc = (int)((e[u].w >> GM_LCELL_SHIFT) & (kGroup - 1));
+            unsigned long long peers = __ballot(act);
+#pragma unroll
+            for (int bit = 0; bit < 6; ++bit) {
+                const bool x = act && ((lc >> bit) & 1);
+                const unsigned long long m = __ballot(x);
+                peers &= x ? m : ~m;
+            }
+            const uint32_t base = act ? wcnt[wid][lc] : 0u;
+            __builtin_amdgcn_wave_barrier();
+            if (act && (peers & lt) == 0ull) wcnt[wid][lc] = base + (uint32_t)__popcll(peers);
+            __builtin_amdgcn_wave_barrier();
+            rk[u] = base + (uint32_t)__popcll(peers & lt);
+        }
+        __syncthreads();
+        if (wid == 0) {  // per cell: the waves' places in its run, and the run in the stage
+            uint32_t run = 0;
+#pragma unroll
+            for (int w = 0; w < kBlock / kWave; ++w) {
+                const uint32_t x = wcnt[w][lane];
+                wcnt[w][lane] = run;
+                run += x;
+            }
+            uint32_t x = run;
             for (int o = 1; o < kWave; o <<= 1) {
                 const uint32_t y = __shfl_up(x, o, kWave);
                 if (lane >= o) x += y;
             }
-            cbase[lane] = o0;
-            cstart[lane] = x - len;
+            cstart[lane] = x - run;
             if (lane == kWave - 1) cstart[kGroup] = x;
         }
         __syncthreads();
-        for (int bb = b + wid; bb < be; bb += kBlock / kWave) {
-            cnt[wid][lane] = c < nc ? O[(size_t)bb * nc + c] : 0u;
-            __builtin_amdgcn_wave_barrier();
-            group_b_rank<true>(gel2, bucket_off[(size_t)bb * bo + gi], bucket_off[(size_t)bb * bo + gi + 1],
-                               cnt[wid], lane, lt, stage, cbase, cstart, mode, pel, acc);
-            __builtin_amdgcn_wave_barrier();
+#pragma unroll
+        for (int u = 0; u < kBPer; ++u) {
+            const uint32_t t = (uint32_t)(wid * (kBPer * kWave) + u * kWave + lane);
+            if (t < tot) {
+                const int lc = (int)((e[u].w >> GM_LCELL_SHIFT) & (kGroup - 1));
+                stage[cstart[lc] + wcnt[wid][lc] + rk[u]] = e[u];
+            }
         }
         __syncthreads();
-        const uint32_t tot = cstart[kGroup];
         for (uint32_t t = threadIdx.x; t < tot; t += kBlock) {
             // the element and its two predecessors are loaded together; a longer walk
             // is needed only behind three equal starts
-            const GElem e = stage[t];
+            const GElem x = stage[t];
             const GElem p1 = stage[t >= 1 ? t - 1 : 0];
             const GElem p2 = stage[t >= 2 ? t - 2 : 0];
-            const int lc = (int)((e.w >> GM_LCELL_SHIFT) & (kGroup - 1));
+            const int lc = (int)((x.w >> GM_LCELL_SHIFT) & (kGroup - 1));
             bool dup2 = false, dup3 = false;
             // equal starts of the cell's run sit just before t, in BAM order; a cell
             // has one run in the stage, so an element of another cell ends the walk
             auto same_run = [&](const GElem& p) {
-                return ((p.w ^ e.w) & GM_LCELL) == 0ull && p.start == e.start;
+                return ((p.w ^ x.w) & GM_LCELL) == 0ull && p.start == x.start;
             };
             if (dedup && t >= 1 && same_run(p1)) {
-                dup2 = same_key(p1, e, dup3);
+                dup2 = same_key(p1, x, dup3);
                 if (!dup3 && t >= 2 && same_run(p2)) {
-                    dup2 |= same_key(p2, e, dup3);
+                    dup2 |= same_key(p2, x, dup3);
                     for (uint32_t m = t - 2; !dup3 && m-- > 0;) {
                         const GElem p = stage[m];
                         if (!same_run(p)) break;
-                        dup2 |= same_key(p, e, dup3);
+                        dup2 |= same_key(p, x, dup3);
                     }
                 }
             }
-            pel[cbase[lc] + (t - cstart[lc])] = group_b_emit(e, dup2, dup3, mode, acc);
+            pel[cbase[lc] + (t - cstart[lc])] = group_b_emit(x, dup2, dup3, mode, acc);
         }
         __syncthreads();
-        b = be;
+        if (wid == 0) cbase[lane] += cstart[lane + 1] - cstart[lane];
+        b = be;  // the next step's first barrier orders the cbase update
     }
     const unsigned long long d2 = wave_sum(acc.d2), d3 = wave_sum(acc.d3);
     if (lane == 0) {
