@@ -379,19 +379,15 @@ constexpr unsigned long long GM_REV = 1ull << 56, GM_PAIRED = 2ull << 56, GM_MAP
 
 // Grouping in two passes (a single pass that writes each 16-byte element straight
 // to its cell-major slot is bound by ~200M scattered partial-line stores):
-//   A, per start bin: valid reads -> buckets (bin, group of 64 cells), BAM order
-//      kept inside each bucket; a bucket receives a contiguous run per step, so
-//      its lines fill in L2 before they go to HBM;
-//   B, per (cell group, bin range), one wave: bucket elements -> cell-major
-//      slots; a cell's slots over consecutive bins are contiguous, so each
-//      wave writes 64 sequential streams.
+//   A, per (start bin, part): valid reads -> buckets (bin, group of 64 cells), BAM
+//      order kept inside each bucket; a bucket receives a contiguous run per step,
+//      so its lines fill in L2 before they go to HBM;
+//   B, per (cell group, bin range): bucket elements -> cell-major slots through
+//      an LDS stage, duplicate marking, 8-byte pileup elements out; a cell's
+//      slots over consecutive bins are contiguous, so a step writes 64 runs.
 // The 6-bit cell id inside the group rides in bits 50..55 of GElem.w between
 // the passes (record offsets stay below 2^50).
 constexpr unsigned long long GM_LCELL_SHIFT = 50, GM_LCELL = 63ull << GM_LCELL_SHIFT;
-#ifndef MGP_STAGE_A
-#define MGP_STAGE_A 0  // pass A: stage each step in LDS and write group runs (measured slower)
-#endif
-constexpr int kStageA = 4 * kBlock;  // one step of pass A (kAhead * kBlock reads)
 
 __global__ void __launch_bounds__(kBlock) k_group_a(int64_t n, const int32_t* __restrict__ start,
                                                     const int32_t* __restrict__ bc, const int32_t* __restrict__ tlen,
@@ -404,12 +400,11 @@ __global__ void __launch_bounds__(kBlock) k_group_a(int64_t n, const int32_t* __
                                                     uint32_t* __restrict__ bucket_off, GElem* __restrict__ gel2,
                                                     uint32_t* __restrict__ first_read, DevStats* st) {
     extern __shared__ uint32_t sm[];
-    uint32_t* gcnt = sm;             // [ngroups] next free slot of each bucket of this bin
+    uint32_t* gcnt = sm;             // [ngroups] next free slot of each bucket (this part)
     uint32_t* fbits = sm + ngroups;  // [ceil(nc/32)] cell's first read is in this bin
-    uint32_t* gbase = fbits + (g.nc + 31) / 32;  // [ngroups] bucket slots at the step start
-    uint32_t* lstart = gbase + ngroups;          // [ngroups] group runs inside the step stage
-    __shared__ GElem stage[kStageA];
-    __shared__ uint16_t sgrp[kStageA];
+    // [2][waves][ngroups]: a step's per-wave group counts, then each wave's first slot
+    // (two sets, alternating per step, so a set is rewritten only behind a barrier)
+    uint32_t* wc = fbits + (g.nc + 31) / 32;
     const int b = blockIdx.x, part = blockIdx.y;
     const int nc = g.nc;
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -473,9 +468,17 @@ __global__ void __launch_bounds__(kBlock) k_group_a(int64_t n, const int32_t* __
             P.o[u] = roff[j];
         }
     };
+    // A step: each wave ranks its own reads by group (ballot peers, the leader of a
+    // group bumps the wave's LDS counter), then per group the waves' counts become
+    // consecutive slot ranges after the bucket's cursor, in wave order = BAM order.
+    // Two barriers per step, no wave waits for another's ranking.
+    int set = 0;
     auto process = [&](const Pre& P, int64_t base0) {
-        unsigned long long peers[kAhead];
+        uint32_t* my = wc + ((size_t)set * (kBlock / kWave) + wid) * ngroups;
+        for (int x = lane; x < ngroups; x += kWave) my[x] = 0;
+        __builtin_amdgcn_wave_barrier();
         bool valid[kAhead];
+        uint32_t rk[kAhead];
 #pragma unroll
         for (int u = 0; u < kAhead; ++u) {
             const int64_t i = base0 + wid * (kAhead * kWave) + u * kWave + lane;
@@ -488,46 +491,33 @@ __global__ void __launch_bounds__(kBlock) k_group_a(int64_t n, const int32_t* __
                 const unsigned long long m = __ballot(x);
                 pm &= x ? m : ~m;
             }
-            peers[u] = pm;
             if (valid[u] && (fbits[c >> 5] >> (c & 31)) & 1u) atomicMin(&first_read[c], (uint32_t)i);
-        }
-        if (MGP_STAGE_A) {
-            for (int x = threadIdx.x; x < ngroups; x += blockDim.x) gbase[x] = gcnt[x];
-            __syncthreads();
-        }
-        uint32_t bef[kAhead];
-#pragma unroll
-        for (int w = 0; w < kBlock / kWave; ++w) {
-            if (wid == w) {
-#pragma unroll
-                for (int u = 0; u < kAhead; ++u) {
-                    bef[u] = 0;
-                    if (valid[u] && (peers[u] & lt) == 0ull)
-                        bef[u] = atomicAdd(&gcnt[P.c[u] >> 6], (uint32_t)__popcll(peers[u]));
-                }
+            uint32_t bef = 0;
+            if (valid[u] && (pm & lt) == 0ull) {
+                bef = my[gi];
+                my[gi] = bef + (uint32_t)__popcll(pm);
             }
-            __syncthreads();
+            const int leader = pm ? __builtin_ctzll(pm) : lane;
+            rk[u] = (uint32_t)__shfl((int)bef, leader, kWave) + (uint32_t)__popcll(pm & lt);
+            __builtin_amdgcn_wave_barrier();
         }
-        if (MGP_STAGE_A && wid == 0) {  // runs of the step's groups inside the stage
-            uint32_t carry = 0;
-            for (int g0 = 0; g0 < ngroups; g0 += kWave) {
-                const int gi = g0 + lane;
-                const uint32_t v = gi < ngroups ? gcnt[gi] - gbase[gi] : 0u;
-                uint32_t x = v;
-                for (int o = 1; o < kWave; o <<= 1) {
-                    const uint32_t y = __shfl_up(x, o, kWave);
-                    if (lane >= o) x += y;
-                }
-                if (gi < ngroups) lstart[gi] = carry + x - v;
-                carry += __shfl(x, kWave - 1, kWave);
+        __syncthreads();
+        for (int gi = threadIdx.x; gi < ngroups; gi += kBlock) {
+            uint32_t run = gcnt[gi];
+#pragma unroll
+            for (int w = 0; w < kBlock / kWave; ++w) {
+                uint32_t* r = wc + ((size_t)set * (kBlock / kWave) + w) * ngroups;
+                const uint32_t x = r[gi];
+                r[gi] = run;
+                run += x;
             }
+            gcnt[gi] = run;
         }
-        if (MGP_STAGE_A) __syncthreads();
+        __syncthreads();
 #pragma unroll
         for (int u = 0; u < kAhead; ++u) {
-            const int leader = peers[u] ? __builtin_ctzll(peers[u]) : lane;
-            const uint32_t dest = (uint32_t)__shfl((int)bef[u], leader, kWave) + (uint32_t)__popcll(peers[u] & lt);
             if (!valid[u]) continue;
+            const uint32_t dest = my[P.c[u] >> 6] + rk[u];
             const uint16_t f = (uint16_t)P.f[u];
             const int t = P.t[u];
             GElem e;
@@ -536,25 +526,10 @@ __global__ void __launch_bounds__(kBlock) k_group_a(int64_t n, const int32_t* __
                   ((unsigned long long)(P.c[u] & (kGroup - 1)) << GM_LCELL_SHIFT);
             e.start = P.s[u];
             e.tlen = t < 0 ? (uint32_t)(-(int64_t)t) : (uint32_t)t;
-            if (MGP_STAGE_A) {
-                const int gi = P.c[u] >> 6;
-                const uint32_t si = lstart[gi] + (dest - gbase[gi]);
-                stage[si] = e;
-                sgrp[si] = (uint16_t)gi;
-            } else {
-                if ((int64_t)dest < n) gel2[dest] = e;  // always: counts and slots come from one histogram
-                else atomicOr(&st->err, ERR_OVERFLOW);
-            }
+            if ((int64_t)dest < n) gel2[dest] = e;  // always: counts and slots come from one histogram
+            else atomicOr(&st->err, ERR_OVERFLOW);
         }
-        if (MGP_STAGE_A) {  // the step's elements go out as runs, one per group
-            __syncthreads();
-            const uint32_t tot = lstart[ngroups - 1] + (gcnt[ngroups - 1] - gbase[ngroups - 1]);
-            for (uint32_t x = threadIdx.x; x < tot; x += blockDim.x) {
-                const int gi = sgrp[x];
-                gel2[gbase[gi] + (x - lstart[gi])] = stage[x];
-            }
-            __syncthreads();
-        }
+        set ^= 1;
     };
     if (lo >= hi) return;
     Pre A, B;
@@ -674,8 +649,11 @@ __device__ __forceinline__ void group_b_rank(const GElem* __restrict__ gel2, uin
 // the run, so the stage fills in (cell, bin, BAM) order. A cell's run is then
 // written to its slots, which continue where the previous step's ended (cbase).
 constexpr int kBPer = kStageB / kBlock;  // elements per lane per step
+#ifndef MGP_ABL_B
+#define MGP_ABL_B 0  // pass-B ablations (experiments only): 1 no dedup walk, 2 no pel stores, 3 no loads
+#endif
 
-__global__ void __launch_bounds__(kBlock) k_group_b(const GElem* __restrict__ gel2,
+__global__ void __launch_bounds__(kBlock, 4) k_group_b(const GElem* __restrict__ gel2,
                                                     const uint32_t* __restrict__ bucket_off,
                                                     const uint32_t* __restrict__ O, Geom g, int ngroups, int rb,
                                                     int mode, unsigned long long* __restrict__ pel,
@@ -701,8 +679,10 @@ __global__ void __launch_bounds__(kBlock) k_group_b(const GElem* __restrict__ ge
     }
     if (wid == 0) cbase[lane] = c < nc ? O[(size_t)B0 * nc + c] : 0u;  // each cell's next slot
     __syncthreads();
-    for (int b = B0; b < B1;) {
-        if (threadIdx.x == 0) {  // bins of this step: as many as fit the stage
+    // bins [b, s_be) of the step starting at b: as many as fit the stage (one if its
+    // bucket alone is larger: direct path); spre = prefix of their bucket sizes
+    auto plan = [&](int b) {
+        if (threadIdx.x == 0) {
             uint32_t tot = 0;
             int be = b;
             spre[0] = 0;
@@ -716,24 +696,13 @@ __global__ void __launch_bounds__(kBlock) k_group_b(const GElem* __restrict__ ge
             s_be = be;
         }
         __syncthreads();
-        const int be = s_be;
-        if (be == b) {  // one bucket larger than the stage: direct stores (wave 0)
-            if (wid == 0) {
-                wcnt[0][lane] = cbase[lane];
-                __builtin_amdgcn_wave_barrier();
-                group_b_rank<false>(gel2, bst[b - B0], bst[b - B0] + bsz[b - B0], wcnt[0], lane, lt, nullptr,
-                                    nullptr, nullptr, mode, pel, acc);
-                __builtin_amdgcn_wave_barrier();
-                cbase[lane] = wcnt[0][lane];
-            }
-            __syncthreads();
-            ++b;
-            continue;
-        }
+        return s_be;
+    };
+    // this wave's quarter of the step's flat sequence (all loads issued together)
+    GElem e[kBPer];
+    auto load = [&](int b, int be) {
         const int nb = be - b;
         const uint32_t tot = spre[nb];
-        // load this wave's quarter of the flat sequence (all loads issued together)
-        GElem e[kBPer];
 #pragma unroll
         for (int u = 0; u < kBPer; ++u) {
             const uint32_t t = (uint32_t)(wid * (kBPer * kWave) + u * kWave + lane);
@@ -747,8 +716,34 @@ __global__ void __launch_bounds__(kBlock) k_group_b(const GElem* __restrict__ ge
                     if (spre[mid] <= t) lo = mid;
                     else hi = mid;
                 }
-                e[u] = gel2[bst[b - B0 + lo] + (t - spre[lo])];
+                if (MGP_ABL_B == 3) {
+                    e[u].w = (unsigned long long)((t * 37u) & 63u) << GM_LCELL_SHIFT;
+                    e[u].start = (int)(bst[b - B0 + lo] + t);
+                } else {
+                    e[u] = gel2[bst[b - B0 + lo] + (t - spre[lo])];
+                }
             }
+        }
+        return tot;
+    };
+    int b = B0;
+    int be = b < B1 ? plan(b) : b;
+    uint32_t tot = be > b ? load(b, be) : 0u;
+    while (b < B1) {
+        if (be == b) {  // one bucket larger than the stage: direct stores (wave 0)
+            if (wid == 0) {
+                wcnt[0][lane] = cbase[lane];
+                __builtin_amdgcn_wave_barrier();
+                group_b_rank<false>(gel2, bst[b - B0], bst[b - B0] + bsz[b - B0], wcnt[0], lane, lt, nullptr,
+                                    nullptr, nullptr, mode, pel, acc);
+                __builtin_amdgcn_wave_barrier();
+                cbase[lane] = wcnt[0][lane];
+            }
+            __syncthreads();
+            ++b;
+            be = b < B1 ? plan(b) : b;
+            tot = be > b ? load(b, be) : 0u;
+            continue;
         }
         // rank by cell inside the wave's quarter (stable)
         wcnt[wid][lane] = 0;
@@ -798,36 +793,70 @@ __global__ void __launch_bounds__(kBlock) k_group_b(const GElem* __restrict__ ge
                 stage[cstart[lc] + wcnt[wid][lc] + rk[u]] = e[u];
             }
         }
-        __syncthreads();
-        for (uint32_t t = threadIdx.x; t < tot; t += kBlock) {
-            // the element and its two predecessors are loaded together; a longer walk
-            // is needed only behind three equal starts
-            const GElem x = stage[t];
-            const GElem p1 = stage[t >= 1 ? t - 1 : 0];
-            const GElem p2 = stage[t >= 2 ? t - 2 : 0];
-            const int lc = (int)((x.w >> GM_LCELL_SHIFT) & (kGroup - 1));
-            bool dup2 = false, dup3 = false;
-            // equal starts of the cell's run sit just before t, in BAM order; a cell
-            // has one run in the stage, so an element of another cell ends the walk
-            auto same_run = [&](const GElem& p) {
-                return ((p.w ^ x.w) & GM_LCELL) == 0ull && p.start == x.start;
-            };
-            if (dedup && t >= 1 && same_run(p1)) {
-                dup2 = same_key(p1, x, dup3);
-                if (!dup3 && t >= 2 && same_run(p2)) {
-                    dup2 |= same_key(p2, x, dup3);
+        // the next step's loads go out now and land while this step is written out
+        const uint32_t cur = tot;
+        const int nb0 = be;
+        const int nbe = nb0 < B1 ? plan(nb0) : nb0;  // (its barrier also completes the stage)
+        if (nb0 >= B1) __syncthreads();
+        const uint32_t ntot = nbe > nb0 ? load(nb0, nbe) : 0u;
+        // write-out with duplicate marking: equal starts of a cell's run sit just
+        // before t, in BAM order; a cell has one run in the stage, so an element of
+        // another cell ends the walk. The element and its two predecessors are
+        // loaded for 2 elements at once and compared branch-free; a walk further
+        // back is needed only behind three equal starts (rare).
+        constexpr int kWo = 2;
+#pragma unroll
+        for (int h = 0; h < kBPer; h += kWo) {
+            GElem xs[kWo];
+            bool d2[kWo], d3[kWo], wk[kWo];
+#pragma unroll
+            for (int q = 0; q < kWo; ++q) {
+                const uint32_t t = threadIdx.x + (uint32_t)(h + q) * kBlock;
+                const uint32_t tc = t < cur ? t : 0u;
+                const GElem x = stage[tc];
+                const GElem p1 = stage[tc >= 1u ? tc - 1u : 0u];
+                const GElem p2 = stage[tc >= 2u ? tc - 2u : 0u];
+                const bool r1 = (tc >= 1u) & (((p1.w ^ x.w) & GM_LCELL) == 0ull) & (p1.start == x.start);
+                const bool r2 = r1 & (tc >= 2u) & (((p2.w ^ x.w) & GM_LCELL) == 0ull) & (p2.start == x.start);
+                const bool s1 = r1 & (((p1.w ^ x.w) & GM_REV) == 0ull);
+                const bool s2 = r2 & (((p2.w ^ x.w) & GM_REV) == 0ull);
+                const bool t3 = (s1 & (p1.tlen == x.tlen)) | (s2 & (p2.tlen == x.tlen));
+                xs[q] = x;
+                d2[q] = dedup & (s1 | s2);
+                d3[q] = dedup & t3;
+                wk[q] = dedup & r2 & !t3 & (tc >= 3u) & (t < cur);
+            }
+#pragma unroll
+            for (int q = 0; q < kWo; ++q) {
+                if (MGP_ABL_B != 1 && __ballot(wk[q]) != 0ull && wk[q]) {
+                    const uint32_t t = threadIdx.x + (uint32_t)(h + q) * kBlock;
+                    const GElem x = xs[q];
+                    bool dup3 = false, dup2 = d2[q];
                     for (uint32_t m = t - 2; !dup3 && m-- > 0;) {
                         const GElem p = stage[m];
-                        if (!same_run(p)) break;
+                        if (((p.w ^ x.w) & GM_LCELL) != 0ull || p.start != x.start) break;
                         dup2 |= same_key(p, x, dup3);
                     }
+                    d2[q] = dup2;
+                    d3[q] = dup3;
                 }
             }
-            pel[cbase[lc] + (t - cstart[lc])] = group_b_emit(x, dup2, dup3, mode, acc);
+#pragma unroll
+            for (int q = 0; q < kWo; ++q) {
+                const uint32_t t = threadIdx.x + (uint32_t)(h + q) * kBlock;
+                if (t < cur) {
+                    const int lc = (int)((xs[q].w >> GM_LCELL_SHIFT) & (kGroup - 1));
+                    const unsigned long long pv = group_b_emit(xs[q], d2[q], d3[q], mode, acc);
+                    if (MGP_ABL_B < 2 || pv == 7ull) pel[cbase[lc] + (t - cstart[lc])] = pv;
+                }
+            }
         }
         __syncthreads();
         if (wid == 0) cbase[lane] += cstart[lane + 1] - cstart[lane];
-        b = be;  // the next step's first barrier orders the cbase update
+        __syncthreads();
+        b = nb0;
+        be = nbe;
+        tot = ntot;
     }
     const unsigned long long d2 = wave_sum(acc.d2), d3 = wave_sum(acc.d3);
     if (lane == 0) {
@@ -1801,7 +1830,7 @@ int mgp_run(mgp_ctx* ctx) {
             int gbits = 0;
             while (gbits < 31 && (1 << gbits) < ngroups) ++gbits;
             k_scan_cells<<<1, 1024, 0, s>>>(ctx->bin_valid.as<uint32_t>(), g.nbins, ctx->bin_base.as<uint32_t>());
-            const size_t a_lds = (size_t)ngroups * 12 + (size_t)((nc + 31) / 32) * 4;
+            const size_t a_lds = (size_t)ngroups * (1 + 2 * (kBlock / kWave)) * 4 + (size_t)((nc + 31) / 32) * 4;
             if (a_lds > (size_t)ctx->lds_hist_max_cells * 4)
                 return set_err(MGP_E_INVALID, "too many cells for one context (grouping LDS)");
             if ((uint64_t)ctx->pay >= (1ull << GM_LCELL_SHIFT))
@@ -1817,6 +1846,7 @@ int mgp_run(mgp_ctx* ctx) {
         }
         STAGE_END(ST_GROUP_A);
         STAGE_BEGIN(ST_GROUP_B);
+        if (MGP_ABL_B >= 2) HIP_TRY(hipMemsetAsync(ctx->pel.p, 0, (size_t)n * 8, s));  // ablation: nothing piles
         if (n > 0) {
             // about MGP_GB_WG workgroups (many per slot: 4 fit a CU, so a grid of a few
             // slot-rounds leaves a tail); bins per workgroup at most kMaxRbB, whose
