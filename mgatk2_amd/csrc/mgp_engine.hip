@@ -1147,6 +1147,13 @@ __device__ __forceinline__ void pile_line(bool has, const uint8_t* __restrict__ 
 }
 
 constexpr int kWaveQ = 2 * kWave;    // per-wave queue of reads waiting to be piled (LDS)
+
+// record offset of a pileup element (MGP_ABL 6, experiments only: every record
+// read from the first 256 MiB of the payload, to time the pileup with a small
+// gather footprint; the counts are then meaningless)
+__device__ __forceinline__ unsigned long long rec_at(unsigned long long qe) {
+    return MGP_ABL == 6 ? (qe & GP_OFF) & ((256ull << 20) - 128) : (qe & GP_OFF);
+}
 constexpr uint32_t kSeg = 65535;     // elements per tile segment (16-bit halves cannot carry)
 
 // grid (nchunks, nwin): workgroup = (cell chunk, position window). For each cell
@@ -1235,7 +1242,7 @@ __global__ void __launch_bounds__(kBlock, MGP_PILEUP_WAVES) k_pileup(
                 __builtin_amdgcn_wave_barrier();
                 if (qn >= (uint32_t)kWave) {
                     const unsigned long long qe = wq[lane];
-                    pile_read(true, payload + (qe & GP_OFF), w, pc, tile, t5, max_span, span_err);
+                    pile_read(true, payload + rec_at(qe), w, pc, tile, t5, max_span, span_err);
                     qn -= kWave;
                     if ((uint32_t)lane < qn) wq[lane] = wq[kWave + lane];
                     __builtin_amdgcn_wave_barrier();
@@ -1244,7 +1251,7 @@ __global__ void __launch_bounds__(kBlock, MGP_PILEUP_WAVES) k_pileup(
             {   // tail: every lane of the wave enters, lanes past qn hold no read
                 const bool has = (uint32_t)lane < qn;
                 const unsigned long long qe = has ? wq[lane] : 0ull;
-                pile_read(has, payload + (qe & GP_OFF), w, pc, tile, t5, max_span, span_err);
+                pile_read(has, payload + rec_at(qe), w, pc, tile, t5, max_span, span_err);
             }
             if (drained) {  // add this segment's packed tile into the 32-bit output rows
                 __syncthreads();
