@@ -262,3 +262,41 @@ def test_deep_bins_parts_and_direct_buckets(engine_lib, oracle_lib):
         res = run_engine(engine_lib, cfg, soa)
         exp, _ = oracle_lib.oracle_run(cfg, soa)
         assert_same(res, exp, f"deep bins {mode}")
+
+
+def test_deep_and_shallow_cells_mixed(engine_lib, oracle_lib):
+    """Cells above and below 65535 reads in one run: cell-windows of more than
+    65535 elements drain their packed 16-bit tile into the output rows between
+    segments, the others flush once."""
+    from mgatk2_amd.engine import EngineConfig
+    from mgatk2_amd.synth import synth_reads
+
+    soa = synth_reads(57, 500_000, 10)
+    per_cell = np.bincount(soa.bc[soa.bc >= 0], minlength=10)
+    assert per_cell.max() > 65535 > per_cell.min()
+    for mode, bias in (("alignment_and_fragment_length", 1.0), ("none", 0.9)):
+        cfg = EngineConfig(n_cells=10, min_baseq=20, min_mapq=30, dedup_mode=mode, max_strand_bias=bias,
+                           min_reads=1)
+        res = run_engine(engine_lib, cfg, soa)
+        exp, _ = oracle_lib.oracle_run(cfg, soa)
+        assert_same(res, exp, f"deep/shallow {mode}")
+
+
+def test_long_read_widens_halo_without_changing_other_cells(engine_lib):
+    """One read with a 440-base reference span in its own cell widens every
+    window's halo (reach R from max_span) for all cells: the other cells' results
+    must not change."""
+    from mgatk2_amd.engine import EngineConfig
+    from mgatk2_amd.synth import concat_soa, pack_reads, synth_reads
+
+    base = synth_reads(58, 300_000, 40)
+    cfg = EngineConfig(n_cells=41, min_baseq=20, min_mapq=30, dedup_mode="alignment_start", min_reads=1)
+    a = run_engine(engine_lib, cfg, base)
+    assert int(base.start.max()) <= 16560  # the added read keeps coordinate order
+    long_read = pack_reads([_read(16560, [(0, 10), (3, 400), (0, 30)], "A" * 40, 40)])
+    b = run_engine(engine_lib, cfg, concat_soa([base, long_read]))
+    assert b.stats["max_span"] > 64 >= a.stats["max_span"]
+    for k in ("counts", "tn5", "depth"):
+        np.testing.assert_array_equal(getattr(a, k)[:40], getattr(b, k)[:40], err_msg=k)
+    for k in ("n_reads", "covered", "depth_sum", "depth_max", "median_lo", "median_hi"):
+        np.testing.assert_array_equal(getattr(a, k)[:40], getattr(b, k)[:40], err_msg=k)
