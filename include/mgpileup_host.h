@@ -111,6 +111,18 @@ int mgp_bam_write(const char *path, const char *const *ref_names, const int64_t 
 int64_t mgp_deflate_tiles(const void *data, int64_t rows, int64_t cols, int32_t elem_size, int64_t crow,
                           int64_t ccol, int level, int n_threads, uint8_t **blob, int64_t *offsets);
 
+/* Cell sharding: gather the payload records idx[0..m) of a
+ * batch into a new, dense payload for one device. mgp_gather_offsets writes the
+ * new offset of each record (sizes rounded up to rec_align) and returns the
+ * total bytes (-1 on error); mgp_gather_records copies the records there on
+ * n_threads threads, zero-filling the alignment gaps. Replaces no reference
+ * code: the reference runs on one process. */
+int64_t mgp_gather_offsets(const uint64_t *rec_off, int64_t n_total, int64_t payload_bytes, const int64_t *idx,
+                           int64_t m, int32_t rec_align, uint64_t *out_off);
+int mgp_gather_records(const uint8_t *payload, const uint64_t *rec_off, int64_t n_total, int64_t payload_bytes,
+                       const int64_t *idx, int64_t m, const uint64_t *out_off, int64_t out_bytes, uint8_t *out,
+                       int n_threads);
+
 #ifdef __cplusplus
 }
 #endif

@@ -91,6 +91,10 @@ def host_library() -> C.CDLL:
         lib.mgp_deflate_tiles.argtypes = [vp, C.c_int64, C.c_int64, C.c_int32, C.c_int64, C.c_int64, C.c_int, C.c_int,
                                           C.POINTER(C.POINTER(C.c_uint8)), vp]
         lib.mgp_deflate_tiles.restype = C.c_int64
+        lib.mgp_gather_offsets.argtypes = [vp, C.c_int64, C.c_int64, vp, C.c_int64, C.c_int32, vp]
+        lib.mgp_gather_offsets.restype = C.c_int64
+        lib.mgp_gather_records.argtypes = [vp, vp, C.c_int64, C.c_int64, vp, C.c_int64, vp, C.c_int64, vp, C.c_int]
+        lib.mgp_gather_records.restype = C.c_int
         lib.mgp_bam_write.argtypes = [C.c_char_p, C.POINTER(C.c_char_p), C.POINTER(C.c_int64), C.c_int, C.c_int,
                                       C.POINTER(mgp_bam_batch), C.POINTER(C.c_char_p), C.c_int, C.c_char_p,
                                       C.c_char_p, C.c_int, C.c_int, C.c_int]

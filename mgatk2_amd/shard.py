@@ -43,26 +43,31 @@ def reads_per_cell(soa: ReadSoA, n_cells: int) -> np.ndarray:
     return np.bincount(bc, minlength=n_cells)[:n_cells]
 
 
-def shard_soa(soa: ReadSoA, lo: int, hi: int) -> tuple[ReadSoA, np.ndarray]:
+def shard_soa(soa: ReadSoA, lo: int, hi: int, rec_align: int = 128) -> tuple[ReadSoA, np.ndarray]:
     """Reads of cells [lo, hi) in BAM order, cell ids rebased to lo, payload
-    records gathered (alignment kept). Returns (batch, original read indices)."""
+    records gathered into a dense payload (native, multithreaded:
+    libmgphost.so `mgp_gather_records`). Returns (batch, original read indices)."""
+    import ctypes as C
+
+    from .bam import host_library, host_threads
+
     idx = np.flatnonzero((soa.bc >= lo) & (soa.bc < hi)).astype(np.int64)
-    n = soa.n
-    ends = np.empty(n, np.uint64)
-    if n:
-        ends[:-1] = soa.rec_off[1:]
-        ends[-1] = soa.payload.shape[0]
-    size = (ends[idx] - soa.rec_off[idx]).astype(np.int64)
-    new_off = np.zeros(idx.size, np.uint64)
-    if idx.size:
-        new_off[1:] = np.cumsum(size[:-1]).astype(np.uint64)
-    total = int(size.sum())
-    # byte gather: for each selected record, its byte range
-    src = np.repeat(soa.rec_off[idx].astype(np.int64) - new_off.astype(np.int64), size) + np.arange(total)
-    payload = soa.payload[src] if total else np.zeros(0, np.uint8)
+    lib = host_library()
+    roff = np.ascontiguousarray(soa.rec_off, dtype=np.uint64)
+    pay = np.ascontiguousarray(soa.payload)
+    new_off = np.zeros(max(idx.size, 1), np.uint64)
+    total = lib.mgp_gather_offsets(roff.ctypes.data, soa.n, pay.shape[0], idx.ctypes.data, idx.size, rec_align,
+                                   new_off.ctypes.data)
+    if total < 0:
+        raise ValueError((lib.mgp_host_last_error() or b"").decode())
+    payload = np.zeros(total, np.uint8)
+    if idx.size and lib.mgp_gather_records(pay.ctypes.data, roff.ctypes.data, soa.n, pay.shape[0], idx.ctypes.data,
+                                           idx.size, new_off.ctypes.data, total, payload.ctypes.data,
+                                           host_threads()) != 0:
+        raise ValueError((lib.mgp_host_last_error() or b"").decode())
     out = ReadSoA(
         soa.start[idx].copy(), (soa.bc[idx] - lo).astype(np.int32), soa.tlen[idx].copy(), soa.flag[idx].copy(),
-        soa.mapq[idx].copy(), soa.span[idx].copy(), new_off, np.ascontiguousarray(payload),
+        soa.mapq[idx].copy(), soa.span[idx].copy(), new_off[: idx.size].copy(), payload,
     )
     return out, idx
 
