@@ -92,7 +92,7 @@ def main():
     seed = args.seed + 1_000_003 * rank
     cfg = EngineConfig(n_cells=n_cells, min_baseq=20, min_mapq=30, min_distance_from_end=5,
                        dedup_mode="alignment_and_fragment_length", max_strand_bias=1.0, min_reads=1)
-    eng = Engine(cfg, device=local_rank)
+    eng = Engine(cfg, device=local_rank if os.environ.get("MGP_BENCH_NO_COMM") != "1" else 0)
     t0 = time.time()
     cdf, ref = cell_cdf(seed, n_cells), ref_codes(args.seed)  # one chrM reference for every rank
     eng.synth(seed, n_reads, cdf, ref, read_len=args.read_len)
@@ -102,7 +102,9 @@ def main():
         print(f"[bench] generated {n_res:,} reads ({pay / 1e9:.2f} GB payload) on device in {t_gen:.1f}s",
               file=sys.stderr, flush=True)
 
-    if world > 1:
+    # MGP_BENCH_NO_COMM=1: rehearse the multi-process path with several ranks on one
+    # GPU (RCCL refuses two ranks on one device); the tallies are then not reduced
+    if world > 1 and os.environ.get("MGP_BENCH_NO_COMM") != "1":
         uid = Engine.comm_unique_id() if rank == 0 else b"\0" * 128
         obj = [uid]
         dist.broadcast_object_list(obj, src=0)
