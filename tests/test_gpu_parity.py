@@ -300,3 +300,52 @@ def test_long_read_widens_halo_without_changing_other_cells(engine_lib):
         np.testing.assert_array_equal(getattr(a, k)[:40], getattr(b, k)[:40], err_msg=k)
     for k in ("n_reads", "covered", "depth_sum", "depth_max", "median_lo", "median_hi"):
         np.testing.assert_array_equal(getattr(a, k)[:40], getattr(b, k)[:40], err_msg=k)
+
+
+def test_full_size_invariants_and_cell_sample_c3(engine_lib, oracle_lib):
+    """BASELINE config C3 at full size (50M reads x 5k cells, `run` parameters):
+    size-independent properties over every cell, a bit-exact oracle check of a
+    sample of whole cells (cells are independent, so a cell's rows depend only on
+    its own reads), and a rerun."""
+    from mgatk2_amd.engine import Engine, EngineConfig
+    from mgatk2_amd.shard import shard_soa
+    from mgatk2_amd.synth import cell_cdf, ref_codes
+
+    n, nc, seed = 50_000_000, 5_000, 20251015 + 3
+    cfg = EngineConfig(n_cells=nc, min_baseq=20, min_mapq=30, dedup_mode="alignment_and_fragment_length",
+                       min_reads=1)
+    with Engine(cfg) as eng:
+        eng.synth(seed, n, cell_cdf(seed, nc), ref_codes(seed))
+        eng.run()
+        res = eng.fetch()
+        eng.run()
+        again = eng.fetch()
+        sample = eng.download_inputs()
+    assert res.stats["total_reads"] == n
+    # per position: depth = sum of the 8 (base, strand) counts; no Tn5 where depth is 0 (Q8)
+    np.testing.assert_array_equal(res.counts.sum(axis=2, dtype=np.uint64), res.depth.astype(np.uint64))
+    assert not np.any(res.tn5[res.depth == 0])
+    # per cell statistics
+    np.testing.assert_array_equal(res.covered, (res.depth > 0).sum(axis=1))
+    np.testing.assert_array_equal(res.depth_sum, res.depth.sum(axis=1, dtype=np.uint64))
+    np.testing.assert_array_equal(res.depth_max, res.depth.max(axis=1))
+    ok = res.passed.astype(bool)
+    assert np.all(res.median_lo[ok] <= res.median_hi[ok]) and np.all(res.median_hi[ok] <= res.depth_max[ok])
+    # run statistics and reference-allele tallies over passing cells
+    assert res.stats["filtered_reads"] == int(res.n_reads.sum())
+    assert res.stats["n_barcodes"] == int((res.n_reads > 0).sum())
+    assert res.stats["cells_passed"] == int(ok.sum())
+    assert res.stats["duplicate_reads_with_length"] <= res.stats["duplicate_reads_position_only"]
+    per_base = res.counts[ok].reshape(int(ok.sum()), -1, 4, 2).sum(axis=(0, 3), dtype=np.uint64)
+    np.testing.assert_array_equal(res.ref_tally, per_base)
+    # rerun: same arrays
+    for k in ("counts", "tn5", "depth", "n_reads", "median_lo", "median_hi", "ref_tally"):
+        np.testing.assert_array_equal(getattr(res, k), getattr(again, k), err_msg=f"rerun {k}")
+    # a sample of whole cells against the oracle on exactly their reads
+    for lo, hi in ((0, 8), (2500, 2508), (nc - 8, nc)):
+        sub, _ = shard_soa(sample, lo, hi)
+        scfg = EngineConfig(**{**cfg.__dict__, "n_cells": hi - lo})
+        exp, _ = oracle_lib.oracle_run(scfg, sub)
+        for k in ("counts", "tn5", "depth", "n_reads", "any_paired", "passed", "covered", "depth_sum",
+                  "depth_max", "median_lo", "median_hi"):
+            np.testing.assert_array_equal(getattr(res, k)[lo:hi], getattr(exp, k), err_msg=f"cells {lo}-{hi} {k}")
