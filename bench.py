@@ -47,6 +47,8 @@ def parse():
     ap.add_argument("--cpu-sample-reads", type=int, default=20_000_000)
     ap.add_argument("--cpu-sample-cells", type=int, default=1000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--record-layout", choices=["packed", "full"], default="packed",
+                    help="payload records: packed 64-byte (default; every C4 read fits) or full 128-byte")
     ap.add_argument("--check", action="store_true", help="bit-exact check of a sample against the oracle")
     return ap.parse_args()
 
@@ -95,7 +97,8 @@ def main():
     eng = Engine(cfg, device=local_rank if os.environ.get("MGP_BENCH_NO_COMM") != "1" else 0)
     t0 = time.time()
     cdf, ref = cell_cdf(seed, n_cells), ref_codes(args.seed)  # one chrM reference for every rank
-    eng.synth(seed, n_reads, cdf, ref, read_len=args.read_len)
+    packed = args.record_layout == "packed"
+    eng.synth(seed, n_reads, cdf, ref, read_len=args.read_len, rec_align=64 if packed else 128, pack=packed)
     n_res, pay = eng.resident()
     t_gen = time.time() - t0
     if rank == 0:
@@ -172,6 +175,7 @@ def main():
                 "reads_per_gpu": n_res,
                 "cells_per_gpu": n_cells,
                 "payload_bytes_per_gpu": pay,
+                "record_layout": args.record_layout,
                 "parallelism": f"cell-sharded x{world} (RCCL all-reduce of ref tallies)",
             },
             "roofline": {

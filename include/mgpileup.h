@@ -74,6 +74,7 @@ extern "C" {
 #define MGP_FLAG_SECONDARY     0x0100u
 #define MGP_FLAG_SUPPLEMENTARY 0x0800u
 #define MGP_FLAG_NOSEQQUAL     0x1000u
+#define MGP_FLAG_PACKED        0x2000u  /* payload record i uses the packed 64-byte layout (below) */
 
 /* mgp_config.flags */
 #define MGP_CFG_KEEP_TN5       0x1  /* keep Tn5 counts at positions of depth 0 (the unfiltered
@@ -118,7 +119,25 @@ typedef struct mgp_config {
  * so producers should place them at 128-byte aligned offsets; any 16-byte
  * aligned placement is accepted. Kernels may read up to 128 bytes from a
  * record start: keep >= 128 bytes after the last record (mgp_push_batch pads).
+ *
+ * Packed record (flag[i] has MGP_FLAG_PACKED): 64 bytes, everything the pileup
+ * reads of a short read in half a cache line (the pileup gathers one record per
+ * read in random order, so its bytes per read set the gather traffic):
+ *   int32  start
+ *   uint8  l_seq                    1 .. MGP_PACK_MAX_LEN
+ *   uint8  n_cigar | reverse << 7   n_cigar <= 4; reverse = flag & MGP_FLAG_REVERSE
+ *   uint16 cigar[4]                 len << 4 | op (len < 4096), unused entries 0
+ *   uint8  base[l_seq] at +14       qual << 2 | b for the codes A, C, G, T (b = 0..3);
+ *                                   0xFF for any other code (pileup.py:83-86 never counts it)
+ * A read may be packed iff it has SEQ and QUAL, l_seq <= 50, every qual <= 62,
+ * n_cigar <= 4 with every length < 4096 and at most 2 aligned (M, =, X)
+ * operations, and -2^28 <= start < 2^28 (mgp_pack_record). The layout keeps
+ * every bit the pileup uses; it drops the code and quality of non-ACGT bases,
+ * so producers that must reproduce query_sequence (the SimpleRead API) write
+ * the full layout. Packed records are placed at 64-byte aligned offsets.
  */
+#define MGP_PACK_MAX_LEN 50
+#define MGP_PACK_BYTES   64
 #if defined(__HIPCC__)
 #define MGP_HD __host__ __device__
 #else
@@ -131,6 +150,69 @@ static inline MGP_HD uint32_t mgp_seq_offset(uint32_t l_seq) {
 static inline MGP_HD uint32_t mgp_cigar_offset(uint32_t l_seq) {
     const uint32_t b = ((l_seq + 1u) / 2u + 3u) & ~3u;
     return mgp_seq_offset(l_seq) + (b > 32u ? b : 32u);
+}
+
+/* Expand a packed record into the full layout in full[0..128) (a non-ACGT base,
+ * byte >= 252, becomes code 15 = N with quality 0; the header flag word holds
+ * only MGP_FLAG_REVERSE). */
+static inline MGP_HD void mgp_unpack_record(const uint8_t *p, uint8_t *full) {
+    uint32_t k;
+    const uint32_t lseq = p[4] <= MGP_PACK_MAX_LEN ? p[4] : MGP_PACK_MAX_LEN;
+    const uint32_t nc = (p[5] & 0x7Fu) <= 4u ? (p[5] & 0x7Fu) : 4u;
+    const uint32_t coff = mgp_cigar_offset(lseq), soff = mgp_seq_offset(lseq);
+    for (k = 0; k < 128u; ++k) full[k] = 0;
+    for (k = 0; k < 4u; ++k) full[k] = p[k];
+    full[4] = (uint8_t)lseq;
+    full[8] = (uint8_t)nc;
+    full[10] = (uint8_t)((p[5] & 0x80u) ? MGP_FLAG_REVERSE : 0u);
+    full[12] = (uint8_t)coff;
+    for (k = 0; k < nc; ++k) {
+        full[coff + 4 * k] = p[6 + 2 * k];
+        full[coff + 4 * k + 1] = p[7 + 2 * k];
+    }
+    for (k = 0; k < lseq; ++k) {
+        const uint8_t v = p[14 + k];
+        const uint8_t code = v >= 252u ? (uint8_t)15 : (uint8_t)(1u << (v & 3u));
+        full[16 + k] = v >= 252u ? (uint8_t)0 : (uint8_t)(v >> 2);
+        full[soff + (k >> 1)] |= (k & 1u) ? code : (uint8_t)(code << 4);
+    }
+}
+
+/* Write the packed record of one read into out[0..64) and return 1, or return 0
+ * (out untouched) when the read does not fit the packed layout. seq holds BAM
+ * 4-bit codes, high nibble first; qual raw Phred bytes; cigar BAM words. */
+static inline MGP_HD int mgp_pack_record(int32_t start, uint32_t l_seq, uint16_t flag, uint32_t n_cigar,
+                                         const uint32_t *cigar, const uint8_t *seq, const uint8_t *qual,
+                                         uint8_t *out) {
+    uint32_t k, blocks = 0;
+    if ((flag & MGP_FLAG_NOSEQQUAL) || l_seq == 0u || l_seq > MGP_PACK_MAX_LEN || n_cigar > 4u) return 0;
+    if (start < -(1 << 28) || start >= (1 << 28)) return 0;
+    for (k = 0; k < n_cigar; ++k) {
+        const uint32_t op = cigar[k] & 15u;
+        if ((cigar[k] >> 4) >= 4096u) return 0;
+        blocks += (op == 0u || op == 7u || op == 8u);
+    }
+    if (blocks > 2u) return 0;
+    for (k = 0; k < l_seq; ++k)
+        if (qual[k] > 62u) return 0;
+    for (k = 0; k < 4u; ++k) out[k] = (uint8_t)((uint32_t)start >> (8u * k));
+    out[4] = (uint8_t)l_seq;
+    out[5] = (uint8_t)(n_cigar | ((flag & MGP_FLAG_REVERSE) ? 0x80u : 0u));
+    for (k = 0; k < 4u; ++k) {
+        const uint32_t c = k < n_cigar ? cigar[k] : 0u;
+        out[6 + 2 * k] = (uint8_t)c;
+        out[7 + 2 * k] = (uint8_t)(c >> 8);
+    }
+    for (k = 0; k < MGP_PACK_MAX_LEN; ++k) {
+        uint8_t v = 0xFF;  /* past l_seq: never counted */
+        if (k < l_seq) {
+            const uint32_t code = (k & 1u) ? (seq[k >> 1] & 15u) : (uint32_t)(seq[k >> 1] >> 4);
+            const int b = code == 1u ? 0 : code == 2u ? 1 : code == 4u ? 2 : code == 8u ? 3 : -1;
+            v = b < 0 ? (uint8_t)0xFF : (uint8_t)((qual[k] << 2) | (uint32_t)b);
+        }
+        out[14 + k] = v;
+    }
+    return 1;
 }
 
 typedef struct mgp_batch {
@@ -188,7 +270,7 @@ typedef struct mgp_synth_params {
     const uint32_t *cell_cdf;   /* host array [n_cells]: cumulative thresholds in [0, 2^32) */
     const uint8_t  *ref_codes;  /* host array [mito_len]: reference bases as BAM 4-bit codes */
     int32_t  rec_align;         /* record placement: offsets are multiples of this (16..4096, pow2) */
-    int32_t  reserved;
+    int32_t  pack;              /* 1: reads that fit get the packed 64-byte layout (MGP_FLAG_PACKED) */
 } mgp_synth_params;
 
 typedef struct mgp_ctx mgp_ctx;

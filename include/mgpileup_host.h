@@ -62,6 +62,12 @@ int  mgp_bam_set_barcodes(mgp_bam *bam, const char *tag, const char *const *barc
  * mgp_bam_set_barcodes. */
 int  mgp_bam_set_bulk(mgp_bam *bam, int32_t cell);
 
+/* pack != 0: records that fit the packed 64-byte layout (include/mgpileup.h,
+ * MGP_FLAG_PACKED) are written in it; the pileup reads half the bytes per read.
+ * Packing drops the code and quality of non-ACGT bases, so callers that rebuild
+ * query_sequence/query_qualities (the SimpleRead API) leave it off (default). */
+int  mgp_bam_set_pack(mgp_bam *bam, int pack);
+
 /* Decode every record of reference `tid` (fetch(contig) order) into `out`.
  * Records are placed at multiples of `rec_align` bytes (16..4096, power of 2). */
 int  mgp_bam_read_ref(mgp_bam *bam, int tid, int rec_align, mgp_bam_batch *out);

@@ -78,6 +78,7 @@ def host_library() -> C.CDLL:
         lib.mgp_bam_has_index.argtypes = [vp]
         lib.mgp_bam_set_barcodes.argtypes = [vp, C.c_char_p, C.POINTER(C.c_char_p), C.c_int]
         lib.mgp_bam_set_bulk.argtypes = [vp, C.c_int32]
+        lib.mgp_bam_set_pack.argtypes = [vp, C.c_int]
         lib.mgp_bam_read_ref.argtypes = [vp, C.c_int, C.c_int, C.POINTER(mgp_bam_batch)]
         lib.mgp_bam_free_batch.argtypes = [C.POINTER(mgp_bam_batch)]
         lib.mgp_bam_free_batch.restype = None
@@ -157,15 +158,19 @@ class BamFile:
     def tid(self, contig: str) -> int:
         return self.references.index(contig)
 
-    def read_soa(self, contig: str, barcodes: list[str], tag: str = "CB", rec_align: int = 128,
-                 bulk_cell: int = -1) -> ReadSoA:
+    def read_soa(self, contig: str, barcodes: list[str], tag: str = "CB", rec_align: int = 64,
+                 bulk_cell: int = -1, pack: bool = True) -> ReadSoA:
         """Every record of `contig` (fetch order) as an engine batch; bc = whitelist
         index (last duplicate wins, like the reference's dict) or -1. With
-        ``bulk_cell >= 0`` every record goes to that cell (bulk calling)."""
+        ``bulk_cell >= 0`` every record goes to that cell (bulk calling). pack:
+        reads that fit get the packed 64-byte record (include/mgpileup.h), which
+        drops the code and quality of non-ACGT bases (off to rebuild SimpleReads)."""
         arr = (C.c_char_p * max(1, len(barcodes)))(*[b.encode() for b in barcodes])
         if self.lib.mgp_bam_set_barcodes(self._h, tag.encode(), arr, len(barcodes)) != 0:
             raise ProcessingError(_err())
         if bulk_cell >= 0 and self.lib.mgp_bam_set_bulk(self._h, int(bulk_cell)) != 0:
+            raise ProcessingError(_err())
+        if self.lib.mgp_bam_set_pack(self._h, int(bool(pack))) != 0:
             raise ProcessingError(_err())
         b = mgp_bam_batch()
         if self.lib.mgp_bam_read_ref(self._h, self.tid(contig), int(rec_align), C.byref(b)) != 0:
@@ -435,7 +440,7 @@ def soa_to_bam(path: str | Path, soa: ReadSoA, whitelist: list[str], contig: str
 
     w = BamWriter(path, [("chr1", 248956422), (contig, mito_len)])
     for i in range(soa.n):
-        d = unpack_record(soa.payload, int(soa.rec_off[i]))
+        d = unpack_record(soa.payload, int(soa.rec_off[i]), int(soa.flag[i]))
         f = int(soa.flag[i])
         q = d["query_qualities"]
         seq = d["query_sequence"]

@@ -127,6 +127,7 @@ struct mgp_bam {
     StrTable wl;
     char tag[2] = {'C', 'B'};
     int32_t bulk_cell = -1;  // >= 0: every record goes to this cell (bulk calling)
+    bool pack = false;       // write the packed record layout where a read fits
 };
 
 namespace {
@@ -618,6 +619,37 @@ int mgp_bam_set_bulk(mgp_bam* b, int32_t cell) {
     return 0;
 }
 
+int mgp_bam_set_pack(mgp_bam* b, int pack) {
+    if (!b) return fail("null argument");
+    b->pack = pack != 0;
+    return 0;
+}
+
+// Header-level and quality checks of mgp_pack_record (include/mgpileup.h) on a
+// raw BAM record; the quality scan tests 8 bytes at a time.
+static bool bam_packable(int32_t pos, uint16_t flg, uint32_t l_seq, uint32_t n_cig, const uint8_t* cig,
+                         const uint8_t* qualp) {
+    if (l_seq == 0 || l_seq > MGP_PACK_MAX_LEN || n_cig > 4 || pos < -(1 << 28) || pos >= (1 << 28)) return false;
+    (void)flg;
+    uint32_t blocks = 0;
+    for (uint32_t k = 0; k < n_cig; ++k) {
+        const uint32_t c = rd32(cig + 4 * k);
+        if ((c >> 4) >= 4096u) return false;
+        const uint32_t op = c & 15u;
+        blocks += op == 0 || op == 7 || op == 8;
+    }
+    if (blocks > 2) return false;
+    uint32_t k = 0;
+    for (; k + 8 <= l_seq; k += 8) {  // a byte > 62: its bit 7, or bit 7 of byte + 65
+        uint64_t x;
+        std::memcpy(&x, qualp + k, 8);
+        if ((x | ((x & 0x7F7F7F7F7F7F7F7Full) + 0x4141414141414141ull)) & 0x8080808080808080ull) return false;
+    }
+    for (; k < l_seq; ++k)
+        if (qualp[k] > 62) return false;
+    return true;
+}
+
 int mgp_bam_read_ref(mgp_bam* b, int tid, int rec_align, mgp_bam_batch* out) {
     g_err.clear();
     if (!b || !out) return fail("null argument");
@@ -639,9 +671,10 @@ int mgp_bam_read_ref(mgp_bam* b, int tid, int rec_align, mgp_bam_batch* out) {
     std::vector<uint64_t> rsz;  // payload bytes of each record of the batch (then its offset)
     std::vector<uint32_t> ncg;  // CIGAR operations (CG tag resolved)
     std::vector<const uint8_t*> cgp;
+    std::vector<uint8_t> pkd;   // record is written in the packed layout
     // one record: decode + pack at index k / payload offset off
     auto decode = [&](const uint8_t* r, uint32_t bs, size_t k, uint64_t off, uint32_t n_cig, const uint8_t* cig,
-                      int64_t& tags, int64_t& first, int64_t gidx) {
+                      bool pk, int64_t& tags, int64_t& first, int64_t gidx) {
         const uint8_t* end = r + bs;
         const int32_t pos = rdi32(r + 4);
         const uint8_t l_name = r[8];
@@ -668,22 +701,31 @@ int mgp_bam_read_ref(mgp_bam* b, int tid, int rec_align, mgp_bam_batch* out) {
         if (b->bulk_cell >= 0) bcv = b->bulk_cell;
         uint16_t fl = flg & 0x0FFF;
         if (l_seq == 0 || qualp[0] == 0xFF) fl |= MGP_FLAG_NOSEQQUAL;
-        const uint32_t soff = mgp_seq_offset(l_seq);
-        const uint32_t coff = mgp_cigar_offset(l_seq);
         uint8_t* rec = G_pay.p + off;
-        const uint64_t size = ((uint64_t)coff + 4ull * n_cig + amask) & ~amask;
-        std::memset(rec, 0, size);
-        std::memcpy(rec, &pos, 4);
-        std::memcpy(rec + 4, &l_seq, 4);
-        const uint16_t nc16 = (uint16_t)n_cig;
-        std::memcpy(rec + 8, &nc16, 2);
-        std::memcpy(rec + 10, &fl, 2);
-        std::memcpy(rec + 12, &coff, 4);
-        if (l_seq) {
-            std::memcpy(rec + 16, qualp, l_seq);
-            std::memcpy(rec + soff, seqp, ((size_t)l_seq + 1) / 2);
+        if (pk) {
+            uint32_t cw[4] = {0, 0, 0, 0};
+            for (uint32_t q = 0; q < n_cig; ++q) cw[q] = rd32(cig + 4 * q);
+            fl |= MGP_FLAG_PACKED;
+            const uint64_t size = ((uint64_t)MGP_PACK_BYTES + amask) & ~amask;
+            std::memset(rec, 0, size);
+            mgp_pack_record(pos, l_seq, fl, n_cig, cw, seqp, qualp, rec);
+        } else {
+            const uint32_t soff = mgp_seq_offset(l_seq);
+            const uint32_t coff = mgp_cigar_offset(l_seq);
+            const uint64_t size = ((uint64_t)coff + 4ull * n_cig + amask) & ~amask;
+            std::memset(rec, 0, size);
+            std::memcpy(rec, &pos, 4);
+            std::memcpy(rec + 4, &l_seq, 4);
+            const uint16_t nc16 = (uint16_t)n_cig;
+            std::memcpy(rec + 8, &nc16, 2);
+            std::memcpy(rec + 10, &fl, 2);
+            std::memcpy(rec + 12, &coff, 4);
+            if (l_seq) {
+                std::memcpy(rec + 16, qualp, l_seq);
+                std::memcpy(rec + soff, seqp, ((size_t)l_seq + 1) / 2);
+            }
+            if (n_cig) std::memcpy(rec + coff, cig, 4 * (size_t)n_cig);
         }
-        if (n_cig) std::memcpy(rec + coff, cig, 4 * (size_t)n_cig);
         G_start.p[k] = pos;
         G_bc.p[k] = bcv;
         G_tlen.p[k] = tl;
@@ -699,6 +741,7 @@ int mgp_bam_read_ref(mgp_bam* b, int tid, int rec_align, mgp_bam_batch* out) {
         rsz.resize(m);
         ncg.resize(m);
         cgp.resize(m);
+        pkd.assign(m, 0);
         // pass 1 (sequential, header fields only): sizes, CIGAR location, checks
         uint64_t tot = 0;
         for (size_t i = 0; i < m; ++i) {
@@ -723,9 +766,12 @@ int mgp_bam_read_ref(mgp_bam* b, int tid, int rec_align, mgp_bam_batch* out) {
                 return fail("CIGAR with more than 65535 operations is not supported by the record format"), -1;
             ncg[i] = n_cig;
             cgp[i] = cig;
+            const uint8_t* qualp = cigp + 4 * (size_t)rd16(r + 12) + ((size_t)l_seq + 1) / 2;
+            pkd[i] = b->pack && bam_packable(rdi32(r + 4), rd16(r + 14), l_seq, n_cig, cig, qualp);
             const uint64_t off = (G_pay.n + tot + amask) & ~amask;  // records are rec_align-sized
             rsz[i] = off;
-            tot = off - G_pay.n + (((uint64_t)mgp_cigar_offset(l_seq) + 4ull * n_cig + amask) & ~amask);
+            const uint64_t rb = pkd[i] ? (uint64_t)MGP_PACK_BYTES : (uint64_t)mgp_cigar_offset(l_seq) + 4ull * n_cig;
+            tot = off - G_pay.n + ((rb + amask) & ~amask);
         }
         const size_t k0 = G_start.n;
         const size_t kn = k0 + m;
@@ -740,7 +786,8 @@ int mgp_bam_read_ref(mgp_bam* b, int tid, int rec_align, mgp_bam_batch* out) {
         auto work = [&](int t) {
             const size_t lo = m * (size_t)t / (size_t)tn, hi = m * (size_t)(t + 1) / (size_t)tn;
             for (size_t i = lo; i < hi; ++i)
-                decode(recs[i], sizes[i], k0 + i, rsz[i], ncg[i], cgp[i], tags[(size_t)t], firsts[(size_t)t],
+                decode(recs[i], sizes[i], k0 + i, rsz[i], ncg[i], cgp[i], pkd[i] != 0, tags[(size_t)t],
+                       firsts[(size_t)t],
                        (int64_t)(k0 + i));
         };
         std::vector<std::thread> th;

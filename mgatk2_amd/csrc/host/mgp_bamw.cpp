@@ -112,6 +112,11 @@ int mgp_bam_write(const char* path, const char* const* ref_names, const int64_t*
     const size_t tag_len_unlisted = unlisted ? std::strlen(unlisted) : 0;
     for (int64_t i = 0; i < batch->n_reads; ++i) {
         const uint8_t* rec = batch->payload + batch->rec_off[i];
+        uint8_t full[128];
+        if (batch->flag[i] & MGP_FLAG_PACKED) {  // N with quality 0 for its non-ACGT bases
+            mgp_unpack_record(rec, full);
+            rec = full;
+        }
         int32_t start;
         uint32_t lseq, coff;
         uint16_t ncig, flg;
@@ -119,6 +124,7 @@ int mgp_bam_write(const char* path, const char* const* ref_names, const int64_t*
         std::memcpy(&lseq, rec + 4, 4);
         std::memcpy(&ncig, rec + 8, 2);
         std::memcpy(&flg, rec + 10, 2);
+        if (batch->flag[i] & MGP_FLAG_PACKED) flg = batch->flag[i];
         std::memcpy(&coff, rec + 12, 4);
         const uint8_t* qual = rec + 16;
         const uint8_t* seq = rec + mgp_seq_offset(lseq);

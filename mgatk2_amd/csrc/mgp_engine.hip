@@ -375,7 +375,7 @@ struct __align__(16) GElem {
     uint32_t tlen;
 };
 constexpr unsigned long long GM_REV = 1ull << 56, GM_PAIRED = 2ull << 56, GM_MAPQ_OK = 4ull << 56,
-                             GM_BAD = 8ull << 56;
+                             GM_BAD = 8ull << 56, GM_PACKED = 16ull << 56;
 
 // Grouping in two passes (a single pass that writes each 16-byte element straight
 // to its cell-major slot is bound by ~200M scattered partial-line stores):
@@ -522,7 +522,7 @@ __global__ void __launch_bounds__(kBlock) k_group_a(int64_t n, const int32_t* __
             const int t = P.t[u];
             GElem e;
             e.w = P.o[u] | (f & MGP_FLAG_REVERSE ? GM_REV : 0ull) | (f & MGP_FLAG_PAIRED ? GM_PAIRED : 0ull) |
-                  (P.m[u] >= min_mapq ? GM_MAPQ_OK : 0ull) | (f & MGP_FLAG_NOSEQQUAL ? GM_BAD : 0ull) |
+                  (P.m[u] >= min_mapq ? GM_MAPQ_OK : 0ull) | (f & MGP_FLAG_NOSEQQUAL ? GM_BAD : 0ull) | (f & MGP_FLAG_PACKED ? GM_PACKED : 0ull) |
                   ((unsigned long long)(P.c[u] & (kGroup - 1)) << GM_LCELL_SHIFT);
             e.start = P.s[u];
             e.tlen = t < 0 ? (uint32_t)(-(int64_t)t) : (uint32_t)t;
@@ -565,7 +565,7 @@ constexpr int kMaxRbB = 512;  // bins per pass-B workgroup (bucket sizes kept in
 #define MGP_GB_WG 8192  // target pass-B grid size
 #endif
 constexpr unsigned long long GP_PILE = 1ull << 63, GP_KEEP = 1ull << 62, GP_PAIRED = 1ull << 61,
-                             GP_BAD = 1ull << 60, GP_OFF = (1ull << GM_LCELL_SHIFT) - 1;
+                             GP_BAD = 1ull << 60, GP_PACKED = 1ull << 59, GP_OFF = (1ull << GM_LCELL_SHIFT) - 1;
 
 struct DedupAcc {  // per-thread duplicate counters of pass B
     unsigned long long d2 = 0, d3 = 0;
@@ -579,7 +579,8 @@ __device__ __forceinline__ unsigned long long group_b_emit(const GElem& e, bool 
     acc.d3 += dup3;
     unsigned long long x = e.w & GP_OFF;
     if (keep) {
-        x |= GP_KEEP | (e.w & GM_PAIRED ? GP_PAIRED : 0ull) | (e.w & GM_BAD ? GP_BAD : 0ull);
+        x |= GP_KEEP | (e.w & GM_PAIRED ? GP_PAIRED : 0ull) | (e.w & GM_BAD ? GP_BAD : 0ull) |
+             (e.w & GM_PACKED ? GP_PACKED : 0ull);
         if (e.w & GM_MAPQ_OK) x |= GP_PILE;
     }
     return x;
@@ -893,9 +894,10 @@ __device__ __forceinline__ void tn5_cut(int32_t start, uint32_t lseq, int strand
 }
 
 // Generic path (any read): CIGAR walk with byte loads (pileup.py:55-95).
-__device__ void pile_slow(const uint8_t* __restrict__ rec, int32_t start, uint32_t lseq, uint32_t ncig,
+// Returns whether the read's reach exceeds max_span.
+__device__ bool pile_slow(const uint8_t* __restrict__ rec, int32_t start, uint32_t lseq, uint32_t ncig,
                           uint32_t coff, int strand, const Win& w, const PileCfg& pc, uint32_t* tile,
-                          uint32_t max_span, bool& span_err) {
+                          uint32_t max_span) {
     const uint32_t* cig = reinterpret_cast<const uint32_t*>(rec + coff);
     const uint8_t* qual = rec + 16;
     const uint8_t* seq = rec + mgp_seq_offset(lseq);
@@ -927,7 +929,7 @@ __device__ void pile_slow(const uint8_t* __restrict__ rec, int32_t start, uint32
             q += len;
         }
     }
-    if (max(ref - (int64_t)start, (int64_t)lseq) > (int64_t)max_span) span_err = true;
+    return max(ref - (int64_t)start, (int64_t)lseq) > (int64_t)max_span;
 }
 
 #ifndef MGP_WIN
@@ -954,14 +956,19 @@ constexpr uint32_t kValid = 0x0116u;   // codes 1, 2, 4, 8 are counted (pileup.p
 #endif
 // The first 128-byte line of a record in registers: header, qual (+16), seq (+80)
 // and CIGAR (+112) of a read of <= 64 bases with <= 4 operations
-// (include/mgpileup.h); no load depends on another.
+// (include/mgpileup.h); no load depends on another. A packed record is the
+// first 64 bytes only (h, qv[0..2]): header, CIGAR and base bytes from +14.
 struct RecLine {
     uint4 h, qv[4], sv[2], cv;
 };
 
-__device__ __forceinline__ void load_line(bool has, const uint8_t* __restrict__ rec, const Win& w, RecLine& R) {
+__device__ __forceinline__ void load_line(bool has, bool packed, const uint8_t* __restrict__ rec, const Win& w,
+                                          RecLine& R) {
     R.h = make_uint4(0, 0, 0, 0);
     R.cv = make_uint4(0, 0, 0, 0);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) R.qv[k] = make_uint4(0, 0, 0, 0);
+    R.sv[0] = R.sv[1] = make_uint4(0, 0, 0, 0);
     if (MGP_ABL == 3) {
         // synthetic read from the record address only: no payload loads
         const uint32_t x = (uint32_t)(reinterpret_cast<uintptr_t>(rec) >> 4);
@@ -975,51 +982,169 @@ __device__ __forceinline__ void load_line(bool has, const uint8_t* __restrict__ 
     } else if (has) {
         const uint4* r4 = reinterpret_cast<const uint4*>(rec);
         R.h = r4[0];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) R.qv[k] = r4[1 + k];
-        R.sv[0] = r4[5];
-        R.sv[1] = r4[6];
-        R.cv = r4[7];
-    } else {
-#pragma unroll
-        for (int k = 0; k < 4; ++k) R.qv[k] = make_uint4(0, 0, 0, 0);
-        R.sv[0] = R.sv[1] = make_uint4(0, 0, 0, 0);
+        R.qv[0] = r4[1];
+        R.qv[1] = r4[2];
+        R.qv[2] = r4[3];
+        if (!packed) {
+            R.qv[3] = r4[4];
+            R.sv[0] = r4[5];
+            R.sv[1] = r4[6];
+            R.cv = r4[7];
+        }
     }
 }
 
-__device__ __forceinline__ void pile_line(bool has, const uint8_t* __restrict__ rec, const RecLine& R,
+__device__ __forceinline__ void pile_line(bool has, bool packed, const uint8_t* __restrict__ rec, const RecLine& R,
                                           const Win& w, const PileCfg& pc, uint32_t* tile, uint32_t* t5,
-                                          uint32_t max_span, bool& span_err);
+                                          uint32_t max_span, bool& span_err, bool& pk_err);
 
-__device__ __forceinline__ void pile_read(bool has, const uint8_t* __restrict__ rec, const Win& w,
+__device__ __forceinline__ void pile_read(bool has, bool packed, const uint8_t* __restrict__ rec, const Win& w,
                                           const PileCfg& pc, uint32_t* tile, uint32_t* t5, uint32_t max_span,
-                                          bool& span_err) {
+                                          bool& span_err, bool& pk_err) {
     if (MGP_ABL == 1) return;
+    if (MGP_ABL == 3) packed = false;  // the synthetic reads are in the full layout
     RecLine R;
-    load_line(has, rec, w, R);
-    pile_line(has, rec, R, w, pc, tile, t5, max_span, span_err);
+    load_line(has, packed, rec, w, R);
+    pile_line(has, packed, rec, R, w, pc, tile, t5, max_span, span_err, pk_err);
 }
 
-__device__ __forceinline__ void pile_line(bool has, const uint8_t* __restrict__ rec, const RecLine& R,
+__device__ __forceinline__ uint32_t byte_at(const uint32_t* wd, int j) { return (wd[j >> 2] >> (8 * (j & 3))) & 0xFFu; }
+
+// The counted bases of the register-path reads of a wave (act: the lane takes
+// part). Block k of a read counts query positions [a_k, b_k) at reference q +
+// d_k. kPacked: base bytes qual << 2 | b at +14 of the packed layout; otherwise
+// qual bytes at +16 and 4-bit codes at +80. Every lane of the wave enters: the
+// unrolled loop bounds are wave reductions.
+template <bool kPacked>
+__device__ __forceinline__ void pile_bases(bool act, int a0, int b0, int a1, int b1, int qs1, int dl0, int dl1,
+                                           const RecLine& R, const Win& w, const PileCfg& pc, uint32_t* tile,
+                                           uint32_t inc) {
+    constexpr int kLen = kPacked ? MGP_PACK_MAX_LEN : kFastLen;
+    int qlo = 1 << 30, qhi = 0;
+    if (act) {
+        if (a0 < b0) {
+            qlo = a0;
+            qhi = b0;
+        }
+        if (a1 < b1) {
+            qlo = min(qlo, a1);
+            qhi = max(qhi, b1);
+        }
+    }
+    // wave-uniform bounds of the unrolled loop (every lane participates)
+    const int wq_lo = __builtin_amdgcn_readfirstlane(wave_min(qlo));
+    const int wq_hi = __builtin_amdgcn_readfirstlane(wave_max(qhi));
+    if (wq_lo >= wq_hi) return;
+    if (!act) a0 = b0 = a1 = b1 = 0;
+    uint32_t qw[16];  // packed: the 64 record bytes; else the qual bytes
+    if (kPacked) {
+        const uint4 v[4] = {R.h, R.qv[0], R.qv[1], R.qv[2]};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            qw[4 * k] = v[k].x;
+            qw[4 * k + 1] = v[k].y;
+            qw[4 * k + 2] = v[k].z;
+            qw[4 * k + 3] = v[k].w;
+        }
+    } else {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            qw[4 * k] = R.qv[k].x;
+            qw[4 * k + 1] = R.qv[k].y;
+            qw[4 * k + 2] = R.qv[k].z;
+            qw[4 * k + 3] = R.qv[k].w;
+        }
+    }
+    const uint32_t sw[8] = {R.sv[0].x, R.sv[0].y, R.sv[0].z, R.sv[0].w, R.sv[1].x, R.sv[1].y, R.sv[1].z, R.sv[1].w};
+    uint32_t* base = tile - w.w0;
+    const int minbq = pc.min_baseq;
+    // packed: counted iff qual << 2 | b lies in [4 * max(min_baseq, 0), 252) (0xFF and
+    // anything >= 252 are never counted; packed quals are <= 62)
+    const uint32_t lo4 = 4u * (uint32_t)min(max(minbq, 0), 63);
+    const uint32_t span4 = 252u - lo4;
+    // base index = log2(code) for the counted codes 1, 2, 4, 8 (A, C, G, T); the
+    // plane offset is a shift of it (compile-time pitch)
+    constexpr int kPitchShift = __builtin_ctz(kTilePitch);
+    // ok / plane of query position qq (static register indices)
+    auto decode = [&](int qq, uint32_t& plane) -> uint32_t {
+        if (kPacked) {
+            const uint32_t x = byte_at(qw, 14 + qq);
+            plane = x & 3u;
+            return (uint32_t)(x - lo4 < span4);
+        } else {
+            const int qb = (int)(int8_t)byte_at(qw, qq);
+            const uint32_t code = (sw[qq >> 3] >> (8 * ((qq >> 1) & 3) + ((qq & 1) ? 0 : 4))) & 15u;
+            plane = (uint32_t)__builtin_ctz(code | 16u);
+            return (uint32_t)(qb >= minbq) & ((kValid >> code) & 1u);
+        }
+    };
+    const bool one_block = __ballot(act && a1 < b1) == 0ull;
+    // common case: every lane of the wave has the same single counted range
+    // [a0, b0) (all reads inside the window, same length): no range test
+    const int ua0 = __builtin_amdgcn_readfirstlane(a0), ub0 = __builtin_amdgcn_readfirstlane(b0);
+    const bool uniform = one_block && __ballot(!(act && a0 == ua0 && b0 == ub0)) == 0ull;
+    // iterations run: a wave-uniform 64-bit mask (one scalar bit test per base)
+    auto range_mask = [](int lo, int hi) -> unsigned long long {
+        const unsigned long long h = hi >= 64 ? ~0ull : ((1ull << hi) - 1ull);
+        const unsigned long long l = lo >= 64 ? ~0ull : ((1ull << lo) - 1ull);
+        return lo < hi ? (h & ~l) : 0ull;
+    };
+    if (uniform) {
+        uint32_t* lb = base + dl0;
+        const unsigned long long smask = range_mask(ua0, ub0);
+#pragma unroll
+        for (int qq = 0; qq < kLen; ++qq) {
+            if (!((smask >> qq) & 1ull)) continue;
+            uint32_t plane;
+            const uint32_t ok = decode(qq, plane);
+            if (ok) atomicAdd(&lb[(plane << kPitchShift) + qq], inc);
+        }
+    } else if (one_block) {
+        uint32_t* lb = base + dl0;
+        const unsigned long long smask = range_mask(wq_lo, wq_hi);
+#pragma unroll
+        for (int qq = 0; qq < kLen; ++qq) {
+            if (!((smask >> qq) & 1ull)) continue;
+            uint32_t plane;
+            const uint32_t ok = decode(qq, plane) & (uint32_t)(qq >= a0) & (uint32_t)(qq < b0);
+            if (ok) atomicAdd(&lb[(plane << kPitchShift) + qq], inc);
+        }
+    } else {
+        const unsigned long long smask = range_mask(wq_lo, wq_hi);
+#pragma unroll
+        for (int qq = 0; qq < kLen; ++qq) {
+            if (!((smask >> qq) & 1ull)) continue;
+            // branch-free predicate: one exec mask per base, a single branch around the atomic
+            const bool second = qq >= qs1;
+            const int d = second ? dl1 : dl0;
+            const int lo = second ? a1 : a0, hi = second ? b1 : b0;
+            uint32_t plane;
+            const uint32_t ok = decode(qq, plane) & (uint32_t)(qq >= lo) & (uint32_t)(qq < hi);
+            if (ok) atomicAdd(&base[(plane << kPitchShift) + qq + d], inc);
+        }
+    }
+}
+
+__device__ __forceinline__ void pile_line(bool has, bool packed, const uint8_t* __restrict__ rec, const RecLine& R,
                                           const Win& w, const PileCfg& pc, uint32_t* tile, uint32_t* t5,
-                                          uint32_t max_span, bool& span_err) {
+                                          uint32_t max_span, bool& span_err, bool& pk_err) {
     if (MGP_ABL == 1) return;
     const uint4 h = R.h, cv = R.cv;
-    const uint4* qv = R.qv;
-    const uint4* sv = R.sv;
     const int32_t start = (int32_t)h.x;
-    const uint32_t lseq = h.y;
-    const uint32_t ncig = h.z & 0xFFFFu;
+    // header fields of either layout (include/mgpileup.h)
+    const uint32_t lseq = packed ? (h.y & 0xFFu) : h.y;
+    const uint32_t ncig = packed ? ((h.y >> 8) & 0x7Fu) : (h.z & 0xFFFFu);
     const uint32_t coff = h.w;
-    const int strand = ((h.z >> 16) & MGP_FLAG_REVERSE) ? 1 : 0;
+    const int strand = packed ? (int)((h.y >> 15) & 1u) : (((h.z >> 16) & MGP_FLAG_REVERSE) ? 1 : 0);
+    const uint32_t cigw[4] = {packed ? (h.y >> 16) : cv.x, packed ? (h.z & 0xFFFFu) : cv.y,
+                              packed ? (h.z >> 16) : cv.z, packed ? (h.w & 0xFFFFu) : cv.w};
     if (has) tn5_cut(start, lseq, strand, w, t5);
 
-    bool fast = has && lseq <= (uint32_t)kFastLen && ncig <= (uint32_t)kFastCig && start >= -(1 << 28) &&
-                start < (1 << 28);
+    bool fast = has && lseq <= (uint32_t)(packed ? MGP_PACK_MAX_LEN : kFastLen) && ncig <= (uint32_t)kFastCig &&
+                start >= -(1 << 28) && start < (1 << 28);
     int qs1 = 1 << 30, dl0 = 0, dl1 = 0;
     int a0 = 0, b0 = 0, a1 = 0, b1 = 0;
     if (fast) {
-        const uint32_t cigw[4] = {cv.x, cv.y, cv.z, cv.w};
         int qs[2] = {0, 1 << 30}, qe[2] = {0, 1 << 30}, dl[2] = {0, 0};
         int nb = 0;
         int ref = start, q = 0;
@@ -1062,88 +1187,18 @@ __device__ __forceinline__ void pile_line(bool has, const uint8_t* __restrict__ 
             dl1 = dl[1];
         }
     }
-    int qlo = 1 << 30, qhi = 0;
-    if (fast) {
-        if (a0 < b0) {
-            qlo = a0;
-            qhi = b0;
-        }
-        if (a1 < b1) {
-            qlo = min(qlo, a1);
-            qhi = max(qhi, b1);
-        }
-    }
-    // wave-uniform bounds of the unrolled loop (every lane participates)
-    const int wq_lo = __builtin_amdgcn_readfirstlane(wave_min(qlo));
-    const int wq_hi = __builtin_amdgcn_readfirstlane(wave_max(qhi));
-    if (wq_lo < wq_hi) {
-        uint32_t qw[kFastLen / 4];
-#pragma unroll
-        for (int k = 0; k < kFastLen / 16; ++k) {
-            qw[4 * k] = qv[k].x;
-            qw[4 * k + 1] = qv[k].y;
-            qw[4 * k + 2] = qv[k].z;
-            qw[4 * k + 3] = qv[k].w;
-        }
-        const uint32_t sw[kFastLen / 8] = {sv[0].x, sv[0].y, sv[0].z, sv[0].w, sv[1].x, sv[1].y, sv[1].z, sv[1].w};
-        uint32_t* base = tile - w.w0;
-        const uint32_t inc = strand_inc(strand);
-        const int minbq = pc.min_baseq;
-        // base index = log2(code) for the counted codes 1, 2, 4, 8 (A, C, G, T); the
-        // plane offset is a shift of it (compile-time pitch)
-        constexpr int kPitchShift = __builtin_ctz(kTilePitch);
-        const bool one_block = __ballot(fast && a1 < b1) == 0ull;
-        // common case: every lane of the wave has the same single counted range
-        // [a0, b0) (all reads inside the window, same length): no range test
-        const int ua0 = __builtin_amdgcn_readfirstlane(a0), ub0 = __builtin_amdgcn_readfirstlane(b0);
-        const bool uniform = one_block && __ballot(!(fast && a0 == ua0 && b0 == ub0)) == 0ull;
-        // iterations run: a wave-uniform 64-bit mask (one scalar bit test per base)
-        auto range_mask = [](int lo, int hi) -> unsigned long long {
-            const unsigned long long h = hi >= 64 ? ~0ull : ((1ull << hi) - 1ull);
-            const unsigned long long l = lo >= 64 ? ~0ull : ((1ull << lo) - 1ull);
-            return lo < hi ? (h & ~l) : 0ull;
-        };
-        if (uniform) {
-            uint32_t* lb = base + dl0;
-            const unsigned long long smask = range_mask(ua0, ub0);
-#pragma unroll
-            for (int qq = 0; qq < kFastLen; ++qq) {
-                if (!((smask >> qq) & 1ull)) continue;
-                const int qb = (int)(int8_t)((qw[qq >> 2] >> (8 * (qq & 3))) & 0xFFu);
-                const uint32_t code = (sw[qq >> 3] >> (8 * ((qq >> 1) & 3) + ((qq & 1) ? 0 : 4))) & 15u;
-                const uint32_t ok = (uint32_t)(qb >= minbq) & ((kValid >> code) & 1u);
-                if (ok) atomicAdd(&lb[((uint32_t)__builtin_ctz(code) << kPitchShift) + qq], inc);
-            }
-        } else if (one_block) {
-            uint32_t* lb = base + dl0;
-            const unsigned long long smask = range_mask(wq_lo, wq_hi);
-#pragma unroll
-            for (int qq = 0; qq < kFastLen; ++qq) {
-                if (!((smask >> qq) & 1ull)) continue;
-                const int qb = (int)(int8_t)((qw[qq >> 2] >> (8 * (qq & 3))) & 0xFFu);
-                const uint32_t code = (sw[qq >> 3] >> (8 * ((qq >> 1) & 3) + ((qq & 1) ? 0 : 4))) & 15u;
-                const uint32_t ok = (uint32_t)(qq >= a0) & (uint32_t)(qq < b0) & (uint32_t)(qb >= minbq) &
-                                    ((kValid >> code) & 1u);
-                if (ok) atomicAdd(&lb[((uint32_t)__builtin_ctz(code) << kPitchShift) + qq], inc);
-            }
-        } else {
-            const unsigned long long smask = range_mask(wq_lo, wq_hi);
-#pragma unroll
-            for (int qq = 0; qq < kFastLen; ++qq) {
-                if (!((smask >> qq) & 1ull)) continue;
-                // branch-free predicate: one exec mask per base, a single branch around the atomic
-                const bool second = qq >= qs1;
-                const int d = second ? dl1 : dl0;
-                const int lo = second ? a1 : a0, hi = second ? b1 : b0;
-                const int qb = (int)(int8_t)((qw[qq >> 2] >> (8 * (qq & 3))) & 0xFFu);
-                const uint32_t code = (sw[qq >> 3] >> (8 * ((qq >> 1) & 3) + ((qq & 1) ? 0 : 4))) & 15u;
-                const uint32_t ok = (uint32_t)(qq >= lo) & (uint32_t)(qq < hi) & (uint32_t)(qb >= minbq) &
-                                    ((kValid >> code) & 1u);
-                if (ok) atomicAdd(&base[((uint32_t)__builtin_ctz(code) << kPitchShift) + qq + d], inc);
-            }
-        }
-    }
-    if (has && !fast) pile_slow(rec, start, lseq, ncig, coff, strand, w, pc, tile, max_span, span_err);
+    const uint32_t inc = strand_inc(strand);
+    // one register pass per layout present in the wave (mixed waves are rare:
+    // producers pack every read that fits)
+    if (__ballot(fast && !packed) != 0ull)
+        pile_bases<false>(fast && !packed, a0, b0, a1, b1, qs1, dl0, dl1, R, w, pc, tile, inc);
+    if (__ballot(fast && packed) != 0ull)
+        pile_bases<true>(fast && packed, a0, b0, a1, b1, qs1, dl0, dl1, R, w, pc, tile, inc);
+    const bool slow = has && !fast;
+    pk_err = pk_err || (slow && packed);  // a packed record outside the layout's limits
+    bool se = false;
+    if (slow && !packed) se = pile_slow(rec, start, lseq, ncig, coff, strand, w, pc, tile, max_span);
+    span_err = span_err || se;
 }
 
 constexpr int kWaveQ = 2 * kWave;    // per-wave queue of reads waiting to be piled (LDS)
@@ -1197,6 +1252,7 @@ __global__ void __launch_bounds__(kBlock, MGP_PILEUP_WAVES) k_pileup(
     const int nc = g.nc;
     const unsigned long long lt = lanemask_lt();
     bool span_err = false, bad_read = false;  // the latter: a kept read without SEQ/QUAL
+    bool pk_err = false;                      // a packed record outside the packed layout's limits
 
     uint32_t tal[kMaxPosPerThread][4];
 #pragma unroll
@@ -1242,7 +1298,8 @@ __global__ void __launch_bounds__(kBlock, MGP_PILEUP_WAVES) k_pileup(
                 __builtin_amdgcn_wave_barrier();
                 if (qn >= (uint32_t)kWave) {
                     const unsigned long long qe = wq[lane];
-                    pile_read(true, payload + rec_at(qe), w, pc, tile, t5, max_span, span_err);
+                    pile_read(true, (qe & GP_PACKED) != 0ull, payload + rec_at(qe), w, pc, tile, t5, max_span,
+                              span_err, pk_err);
                     qn -= kWave;
                     if ((uint32_t)lane < qn) wq[lane] = wq[kWave + lane];
                     __builtin_amdgcn_wave_barrier();
@@ -1251,7 +1308,8 @@ __global__ void __launch_bounds__(kBlock, MGP_PILEUP_WAVES) k_pileup(
             {   // tail: every lane of the wave enters, lanes past qn hold no read
                 const bool has = (uint32_t)lane < qn;
                 const unsigned long long qe = has ? wq[lane] : 0ull;
-                pile_read(has, payload + rec_at(qe), w, pc, tile, t5, max_span, span_err);
+                pile_read(has, (qe & GP_PACKED) != 0ull, payload + rec_at(qe), w, pc, tile, t5, max_span, span_err,
+                          pk_err);
             }
             if (drained) {  // add this segment's packed tile into the 32-bit output rows
                 __syncthreads();
@@ -1374,6 +1432,8 @@ __global__ void __launch_bounds__(kBlock, MGP_PILEUP_WAVES) k_pileup(
     }
     const bool anyspan = __ballot(span_err) != 0ull;
     if (lane == 0 && anyspan) atomicOr(&st->err, ERR_SPAN);
+    const bool anypk = __ballot(pk_err) != 0ull;
+    if (lane == 0 && anypk) atomicOr(&st->err, ERR_PACKED);
     if (threadIdx.x == 0 && bad_read) atomicOr(&st->err, ERR_BADREAD);
 }
 
@@ -1958,6 +2018,8 @@ int mgp_sync(mgp_ctx* ctx) {
     if (e & ERR_BADREAD)
         return set_err(MGP_E_BADREAD, "a kept read has no SEQ or QUAL (pysam would return None)");
     if (e & ERR_SPAN) return set_err(MGP_E_SPAN, "a read's CIGAR reach exceeds the declared span");
+    if (e & ERR_PACKED)
+        return set_err(MGP_E_INVALID, "a record flagged MGP_FLAG_PACKED does not fit the packed layout's limits");
     return MGP_OK;
 }
 
@@ -2079,7 +2141,7 @@ int mgp_download_inputs(mgp_ctx* ctx, int32_t* start, int32_t* bc, int32_t* tlen
 int mgp_synth_fill(void* stream, uint64_t seed, int64_t n, int read_len, int n_cells, int mito_len,
                    const uint32_t* d_cdf, const uint8_t* d_ref, int32_t* start, int32_t* bc, int32_t* tlen,
                    uint16_t* flag, uint8_t* mapq, uint32_t* span, uint64_t* roff, uint8_t* payload,
-                   int64_t* payload_bytes, int rec_align);
+                   int64_t* payload_bytes, int rec_align, int pack);
 
 int mgp_synth_generate(mgp_ctx* ctx, const mgp_synth_params* p) {
     if (!ctx || !p || !p->cell_cdf || !p->ref_codes) return set_err(MGP_E_INVALID, "null synth args");
@@ -2110,7 +2172,7 @@ int mgp_synth_generate(mgp_ctx* ctx, const mgp_synth_params* p) {
     int r = mgp_synth_fill(s, p->seed, n, p->read_len, nc, L, cdf.as<uint32_t>(), ref.as<uint8_t>(),
                            ctx->start.as<int32_t>(), ctx->bc.as<int32_t>(), ctx->tlen.as<int32_t>(),
                            ctx->flag.as<uint16_t>(), ctx->mapq.as<uint8_t>(), ctx->span.as<uint32_t>(),
-                           ctx->roff.as<uint64_t>(), ctx->payload.as<uint8_t>(), &pay, align);
+                           ctx->roff.as<uint64_t>(), ctx->payload.as<uint8_t>(), &pay, align, p->pack);
     if (r != MGP_OK) {
         cdf.release();
         ref.release();

@@ -14,6 +14,7 @@ constexpr uint32_t ERR_BADREAD = 2u;    // kept read without SEQ/QUAL
 constexpr uint32_t ERR_SPAN = 4u;       // CIGAR reach larger than declared span
 constexpr uint32_t ERR_BADBC = 8u;      // bc >= n_cells
 constexpr uint32_t ERR_OVERFLOW = 16u;  // scatter destination outside its cell segment
+constexpr uint32_t ERR_PACKED = 32u;    // MGP_FLAG_PACKED record outside the packed layout's limits
 
 // Counters written by the kernels of one run (zeroed at run start).
 struct DevStats {

@@ -79,10 +79,15 @@ __device__ __forceinline__ uint64_t rec_size(int ncig, int rl, int align) {
     return (uint64_t)((cigar_offset(rl) + 4 * ncig + align - 1) & ~(align - 1));
 }
 
-__global__ void k_synth_sizes(uint64_t seed, int64_t n, int rl, int align, uint64_t* __restrict__ sz) {
+// every synthetic read fits the packed layout when rl <= MGP_PACK_MAX_LEN: quals
+// are <= 37, at most 3 CIGAR operations with 2 aligned blocks, lengths < 64
+__device__ __forceinline__ bool packs(int rl, int pack) { return pack && rl <= MGP_PACK_MAX_LEN; }
+
+__global__ void k_synth_sizes(uint64_t seed, int64_t n, int rl, int align, int pack, uint64_t* __restrict__ sz) {
     int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
-    sz[i] = rec_size(cig_of(seed, i).n, rl, align);
+    sz[i] = packs(rl, pack) ? (uint64_t)((MGP_PACK_BYTES + align - 1) & ~(align - 1))
+                            : rec_size(cig_of(seed, i).n, rl, align);
 }
 
 // ---- generic exclusive scan of u64 (3-phase, 4096 items per block) ----------
@@ -187,7 +192,7 @@ __global__ void k_synth_fill(uint64_t seed, int64_t n, int rl, int nc, int L, co
                              const uint8_t* __restrict__ ref, int32_t* __restrict__ start, int32_t* __restrict__ bc,
                              int32_t* __restrict__ tlen, uint16_t* __restrict__ flag, uint8_t* __restrict__ mapq,
                              uint32_t* __restrict__ span, const uint64_t* __restrict__ roff,
-                             uint8_t* __restrict__ payload) {
+                             uint8_t* __restrict__ payload, int pack) {
     int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const uint64_t spanpos = (uint64_t)(L - rl + 1);
@@ -210,6 +215,8 @@ __global__ void k_synth_fill(uint64_t seed, int64_t n, int rl, int nc, int L, co
     const uint8_t mq = u24(shash(seed, i, 7)) < MAPQ0 ? 0 : 60;
     const Cig cg = cig_of(seed, i);
 
+    const bool pk = packs(rl, pack);
+    if (pk) f |= MGP_FLAG_PACKED;
     start[i] = s0;
     bc[i] = b;
     tlen[i] = strand ? -tabs : tabs;
@@ -217,34 +224,48 @@ __global__ void k_synth_fill(uint64_t seed, int64_t n, int rl, int nc, int L, co
     mapq[i] = mq;
     span[i] = (uint32_t)(cg.cls == C_D ? rl + cg.b : rl);
 
-    uint8_t* rec = payload + roff[i];
-    *reinterpret_cast<int32_t*>(rec) = s0;
-    *reinterpret_cast<uint32_t*>(rec + 4) = (uint32_t)rl;
-    *reinterpret_cast<uint16_t*>(rec + 8) = (uint16_t)cg.n;
-    *reinterpret_cast<uint16_t*>(rec + 10) = f;
-    *reinterpret_cast<uint32_t*>(rec + 12) = (uint32_t)cigar_offset(rl);
-    uint32_t* cig = reinterpret_cast<uint32_t*>(rec + cigar_offset(rl));
+    uint32_t cw[3] = {0, 0, 0};
     if (cg.cls == C_M) {
-        cig[0] = ((uint32_t)rl << 4) | 0;
+        cw[0] = ((uint32_t)rl << 4) | 0;
     } else if (cg.cls == C_S) {
-        cig[0] = ((uint32_t)cg.a << 4) | 4;
-        cig[1] = ((uint32_t)(rl - cg.a) << 4) | 0;
+        cw[0] = ((uint32_t)cg.a << 4) | 4;
+        cw[1] = ((uint32_t)(rl - cg.a) << 4) | 0;
     } else if (cg.cls == C_I) {
-        cig[0] = ((uint32_t)cg.a << 4) | 0;
-        cig[1] = ((uint32_t)cg.b << 4) | 1;
-        cig[2] = ((uint32_t)(rl - cg.a - cg.b) << 4) | 0;
+        cw[0] = ((uint32_t)cg.a << 4) | 0;
+        cw[1] = ((uint32_t)cg.b << 4) | 1;
+        cw[2] = ((uint32_t)(rl - cg.a - cg.b) << 4) | 0;
     } else {
-        cig[0] = ((uint32_t)cg.a << 4) | 0;
-        cig[1] = ((uint32_t)cg.b << 4) | 2;
-        cig[2] = ((uint32_t)(rl - cg.a) << 4) | 0;
+        cw[0] = ((uint32_t)cg.a << 4) | 0;
+        cw[1] = ((uint32_t)cg.b << 4) | 2;
+        cw[2] = ((uint32_t)(rl - cg.a) << 4) | 0;
     }
+    uint8_t* rec = payload + roff[i];
     uint8_t* qual = rec + 16;
     uint8_t* seq = rec + mgp_seq_offset((uint32_t)rl);
+    if (pk) {  // packed layout (include/mgpileup.h); base bytes are written per base below
+        *reinterpret_cast<int32_t*>(rec) = s0;
+        rec[4] = (uint8_t)rl;
+        rec[5] = (uint8_t)(cg.n | (strand ? 0x80 : 0));
+        for (int k = 0; k < 4; ++k) {
+            const uint32_t c = k < 3 ? cw[k] : 0u;
+            rec[6 + 2 * k] = (uint8_t)c;
+            rec[7 + 2 * k] = (uint8_t)(c >> 8);
+        }
+        for (int k = rl; k < MGP_PACK_MAX_LEN; ++k) rec[14 + k] = 0xFF;
+    } else {
+        *reinterpret_cast<int32_t*>(rec) = s0;
+        *reinterpret_cast<uint32_t*>(rec + 4) = (uint32_t)rl;
+        *reinterpret_cast<uint16_t*>(rec + 8) = (uint16_t)cg.n;
+        *reinterpret_cast<uint16_t*>(rec + 10) = f;
+        *reinterpret_cast<uint32_t*>(rec + 12) = (uint32_t)cigar_offset(rl);
+        uint32_t* cig = reinterpret_cast<uint32_t*>(rec + cigar_offset(rl));
+        for (int k = 0; k < cg.n; ++k) cig[k] = cw[k];
+    }
     const uint8_t kCodes[4] = {1, 2, 4, 8};
     uint8_t hi_nib = 0;
     for (int q = 0; q < rl; ++q) {
         const uint64_t hq = shash(seed, i, 1000 + (uint64_t)q);
-        qual[q] = u24(hq) < QUAL37 ? 37 : (uint8_t)(2 + hq % 35);
+        const uint8_t qv = u24(hq) < QUAL37 ? 37 : (uint8_t)(2 + hq % 35);
         int d;
         bool rnd = false;
         if (cg.cls == C_M) d = q;
@@ -265,10 +286,15 @@ __global__ void k_synth_fill(uint64_t seed, int64_t n, int rl, int nc, int L, co
             else if (m < BASE_SUB) code = kCodes[(code_idx(rc) + 1 + (uint32_t)((hs & 255) % 3)) & 3];
             else code = rc;
         }
+        if (pk) {
+            rec[14 + q] = code == 15 ? (uint8_t)0xFF : (uint8_t)((qv << 2) | code_idx(code));
+            continue;
+        }
+        qual[q] = qv;
         if ((q & 1) == 0) hi_nib = code;
         else seq[q >> 1] = (uint8_t)((hi_nib << 4) | code);
     }
-    if (rl & 1) seq[rl >> 1] = (uint8_t)(hi_nib << 4);
+    if ((rl & 1) && !pk) seq[rl >> 1] = (uint8_t)(hi_nib << 4);
 }
 
 }  // namespace
@@ -276,7 +302,7 @@ __global__ void k_synth_fill(uint64_t seed, int64_t n, int rl, int nc, int L, co
 extern "C" int mgp_synth_fill(void* stream, uint64_t seed, int64_t n, int read_len, int n_cells, int mito_len,
                               const uint32_t* d_cdf, const uint8_t* d_ref, int32_t* start, int32_t* bc,
                               int32_t* tlen, uint16_t* flag, uint8_t* mapq, uint32_t* span, uint64_t* roff,
-                              uint8_t* payload, int64_t* payload_bytes, int rec_align) {
+                              uint8_t* payload, int64_t* payload_bytes, int rec_align, int pack) {
     hipStream_t s = (hipStream_t)stream;
     if (read_len < 48) return MGP_E_INVALID;
     if (n == 0) {
@@ -284,14 +310,14 @@ extern "C" int mgp_synth_fill(void* stream, uint64_t seed, int64_t n, int read_l
         return MGP_OK;
     }
     const unsigned nb = (unsigned)((n + kBlock - 1) / kBlock);
-    k_synth_sizes<<<nb, kBlock, 0, s>>>(seed, n, read_len, rec_align, roff);
+    k_synth_sizes<<<nb, kBlock, 0, s>>>(seed, n, read_len, rec_align, pack, roff);
     if (hipGetLastError() != hipSuccess) return MGP_E_HIP;
     uint64_t total = 0;
     int r = scan_exclusive_u64(roff, n, s, &total);
     if (r != MGP_OK) return r;
     if (hipMemsetAsync(payload, 0, (size_t)total, s) != hipSuccess) return MGP_E_HIP;
     k_synth_fill<<<nb, kBlock, 0, s>>>(seed, n, read_len, n_cells, mito_len, d_cdf, d_ref, start, bc, tlen, flag,
-                                       mapq, span, roff, payload);
+                                       mapq, span, roff, payload, pack);
     if (hipGetLastError() != hipSuccess) return MGP_E_HIP;
     if (hipStreamSynchronize(s) != hipSuccess) return MGP_E_HIP;
     *payload_bytes = (int64_t)total;

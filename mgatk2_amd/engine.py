@@ -116,7 +116,7 @@ class mgp_synth_params(C.Structure):
         ("cell_cdf", C.c_void_p),
         ("ref_codes", C.c_void_p),
         ("rec_align", C.c_int32),
-        ("reserved", C.c_int32),
+        ("pack", C.c_int32),
     ]
 
 
@@ -327,11 +327,11 @@ class Engine:
         return int(n.value), int(p.value)
 
     def synth(self, seed: int, n_reads: int, cdf: np.ndarray, ref: np.ndarray, read_len: int = 50,
-              rec_align: int = 128):
+              rec_align: int = 64, pack: bool = True):
         cdf = np.ascontiguousarray(cdf, np.uint32)
         ref = np.ascontiguousarray(ref, np.uint8)
         p = mgp_synth_params(int(seed), int(n_reads), int(read_len), int(self.cfg.n_cells), _ptr(cdf), _ptr(ref),
-                             int(rec_align), 0)
+                             int(rec_align), int(bool(pack)))
         _ck(self.lib.mgp_synth_generate(self._h, C.byref(p)), "mgp_synth_generate")
 
     def download_inputs(self) -> ReadSoA:

@@ -77,7 +77,7 @@ class BAMReader:
     def is_bulk_mode(self) -> bool:
         return self.barcodes == {"bulk"}  # readers.py:74
 
-    def read_soa(self, rec_align: int = 128) -> tuple[ReadSoA, dict]:
+    def read_soa(self, rec_align: int = 64, pack: bool = True) -> tuple[ReadSoA, dict]:
         """Every chrM record as one engine batch (BAM order).
 
         ``bc`` is the whitelist index (-1 = no tag or not whitelisted). In bulk
@@ -88,7 +88,7 @@ class BAMReader:
         try:
             with self._open() as bam:
                 soa = bam.read_soa(self.config.mito_chr, self.barcode_list, tag=self.config.barcode_tag,
-                                   rec_align=rec_align, bulk_cell=bulk)
+                                   rec_align=rec_align, bulk_cell=bulk, pack=pack)
         except BAMReadError:
             raise
         except Exception as e:
@@ -97,7 +97,7 @@ class BAMReader:
 
     def collect_reads_by_barcode(self) -> tuple[dict, dict]:
         """readers.py:63-201 on the host: dict[barcode -> list[SimpleRead]] + stats."""
-        soa, _ = self.read_soa(rec_align=16)
+        soa, _ = self.read_soa(rec_align=16, pack=False)  # query_sequence is rebuilt exactly
         index = {b: i for i, b in enumerate(self.barcode_list)}
         names = {i: b for b, i in index.items()}
         reads_by_barcode: dict[str, list] = defaultdict(list)
@@ -130,7 +130,7 @@ class BAMReader:
                         continue
                 if f & FLAG_NOSEQQUAL:  # .encode() / np.array(None, int8) raise (readers.py:158-159)
                     raise ValueError("read without sequence or base qualities")
-                d = unpack_record(soa.payload, int(soa.rec_off[i]))
+                d = unpack_record(soa.payload, int(soa.rec_off[i]), int(soa.flag[i]))
                 reads_by_barcode[barcode].append(SimpleRead(
                     reference_start=int(soa.start[i]),
                     is_reverse=rev,

@@ -43,7 +43,7 @@ def reads_per_cell(soa: ReadSoA, n_cells: int) -> np.ndarray:
     return np.bincount(bc, minlength=n_cells)[:n_cells]
 
 
-def shard_soa(soa: ReadSoA, lo: int, hi: int, rec_align: int = 128) -> tuple[ReadSoA, np.ndarray]:
+def shard_soa(soa: ReadSoA, lo: int, hi: int, rec_align: int = 64) -> tuple[ReadSoA, np.ndarray]:
     """Reads of cells [lo, hi) in BAM order, cell ids rebased to lo, payload
     records gathered into a dense payload (native, multithreaded:
     libmgphost.so `mgp_gather_records`). Returns (batch, original read indices)."""

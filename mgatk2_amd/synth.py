@@ -57,6 +57,9 @@ FLAG_REVERSE = 0x10
 FLAG_SECONDARY = 0x100
 FLAG_SUPPLEMENTARY = 0x800
 FLAG_NOSEQQUAL = 0x1000
+FLAG_PACKED = 0x2000  # the record uses the packed 64-byte layout (include/mgpileup.h)
+PACK_MAX_LEN = 50
+PACK_BYTES = 64
 
 CODES = np.array([1, 2, 4, 8], dtype=np.uint8)  # BAM 4-bit A, C, G, T
 SEQ_NT16 = "=ACMGRSVTWYHKDBN"
@@ -214,7 +217,47 @@ def cigar_offset(lseq):
     return seq_offset(lseq) + np.maximum(32, ((lseq + 1) // 2 + 3) & ~3)
 
 
-REC_ALIGN = 128  # records are gathered at random: one L2 line per record of <= 128 bytes
+REC_ALIGN = 64  # records are gathered at random: a packed record is one 64-byte half line
+
+
+def packable_mask(start, flag, lseq, ncig, cig, qual) -> np.ndarray:
+    """Which reads fit the packed layout (mgp_pack_record in include/mgpileup.h).
+    cig: [m, k] BAM words (entries past ncig ignored); qual: [m, lseq] bytes."""
+    start = np.asarray(start, np.int64)
+    lseq = np.asarray(lseq, np.int64)
+    ncig = np.asarray(ncig, np.int64)
+    ok = ((np.asarray(flag) & FLAG_NOSEQQUAL) == 0) & (lseq >= 1) & (lseq <= PACK_MAX_LEN) & (ncig <= 4)
+    ok &= (start >= -(1 << 28)) & (start < (1 << 28))
+    cig = np.asarray(cig, np.int64).reshape(start.shape[0], -1)
+    used = np.arange(cig.shape[1])[None, :] < ncig[:, None]
+    op = cig & 15
+    ok &= ~np.any(used & ((cig >> 4) >= 4096), axis=1)
+    ok &= np.sum(used & ((op == 0) | (op == 7) | (op == 8)), axis=1) <= 2
+    ok &= np.all(np.asarray(qual) <= 62, axis=1) if np.asarray(qual).size else True
+    return ok
+
+
+def pack_bytes(start, lseq, reverse, ncig, cig, qual, code) -> np.ndarray:
+    """Packed records [m, 64] (include/mgpileup.h): header, CIGAR as u16, one
+    byte per base (qual << 2 | b for A, C, G, T; 0xFF otherwise and past l_seq)."""
+    m = np.asarray(start).shape[0]
+    out = np.full((m, PACK_BYTES), 0xFF, np.uint8)
+    out[:, 0:4] = np.asarray(start, "<i4").reshape(m, 1).view(np.uint8)
+    out[:, 4] = np.asarray(lseq, np.uint8)
+    out[:, 5] = (np.asarray(ncig, np.uint8) | np.where(np.asarray(reverse), 0x80, 0)).astype(np.uint8)
+    c16 = np.zeros((m, 4), "<u2")
+    cig = np.asarray(cig, np.int64).reshape(m, -1)
+    for k in range(min(4, cig.shape[1])):
+        c16[:, k] = np.where(np.asarray(ncig) > k, cig[:, k], 0).astype("<u2")
+    out[:, 6:14] = c16.view(np.uint8).reshape(m, 8)
+    code = np.asarray(code, np.int64)
+    qual = np.asarray(qual, np.int64)
+    n = code.shape[1]
+    b = np.select([code == 1, code == 2, code == 4, code == 8], [0, 1, 2, 3], -1)
+    v = np.where(b >= 0, (qual << 2) | np.maximum(b, 0), 0xFF)
+    v = np.where(np.arange(n)[None, :] < np.asarray(lseq, np.int64).reshape(m, 1), v, 0xFF)
+    out[:, 14 : 14 + n] = v.astype(np.uint8)
+    return out
 
 
 def rec_size(ncig, lseq, align: int = 16):
@@ -328,44 +371,58 @@ def _synth_chunk(seed, i0, i1, n, read_len, n_cells, mito_len, cdf, ref):
     )
 
 
-def _pack_fixed(start, flag, ncig, cig, qual, code, rl, align=REC_ALIGN):
-    """Pack records for reads of one read length (vectorised)."""
+def _pack_fixed(start, flag, ncig, cig, qual, code, rl, align=REC_ALIGN, pack=True):
+    """Pack records for reads of one read length (vectorised). Returns (rec_off,
+    payload, flag): reads that fit get the packed layout and MGP_FLAG_PACKED."""
     m = start.shape[0]
-    sizes = rec_size(ncig, np.full(m, rl), align)
+    pk = packable_mask(start, flag, np.full(m, rl), ncig, cig, qual) if pack else np.zeros(m, bool)
+    flag = (flag | np.where(pk, FLAG_PACKED, 0)).astype(np.uint16)
+    sizes = np.where(pk, (PACK_BYTES + align - 1) & ~(align - 1), rec_size(ncig, np.full(m, rl), align))
     roff = np.zeros(m, np.uint64)
     if m:
         roff[1:] = np.cumsum(sizes[:-1]).astype(np.uint64)
     total = int(sizes.sum())
     pay = np.zeros(total, np.uint8)
-    coff = int(cigar_offset(rl))
-    hdr = np.zeros(m, dtype=[("start", "<i4"), ("lseq", "<u4"), ("ncig", "<u2"), ("flag", "<u2"), ("coff", "<u4")])
-    hdr["start"] = start
-    hdr["lseq"] = rl
-    hdr["ncig"] = ncig
-    hdr["flag"] = flag
-    hdr["coff"] = coff
-    hb = hdr.view(np.uint8).reshape(m, 16)
     ro = roff.astype(np.int64)
+    if pk.any():
+        pr = pack_bytes(start[pk], np.full(int(pk.sum()), rl), (flag[pk] & FLAG_REVERSE) != 0, ncig[pk], cig[pk],
+                        qual[pk], code[pk])
+        pay[ro[pk, None] + np.arange(PACK_BYTES)[None, :]] = pr
+    fu = ~pk
+    mf = int(fu.sum())
+    if mf == 0:
+        return roff, pay, flag
+    ro = ro[fu]
+    coff = int(cigar_offset(rl))
+    hdr = np.zeros(mf, dtype=[("start", "<i4"), ("lseq", "<u4"), ("ncig", "<u2"), ("flag", "<u2"), ("coff", "<u4")])
+    hdr["start"] = start[fu]
+    hdr["lseq"] = rl
+    hdr["ncig"] = ncig[fu]
+    hdr["flag"] = flag[fu]
+    hdr["coff"] = coff
+    hb = hdr.view(np.uint8).reshape(mf, 16)
     pay[ro[:, None] + np.arange(16)[None, :]] = hb
-    pay[(ro + 16)[:, None] + np.arange(rl)[None, :]] = qual
+    pay[(ro + 16)[:, None] + np.arange(rl)[None, :]] = qual[fu]
     nb = (rl + 1) // 2
-    c = code
+    c = code[fu]
     if rl & 1:
-        c = np.concatenate([c, np.zeros((m, 1), np.uint8)], axis=1)
+        c = np.concatenate([c, np.zeros((mf, 1), np.uint8)], axis=1)
     packed = ((c[:, 0::2] << 4) | c[:, 1::2]).astype(np.uint8)
     pay[(ro + int(seq_offset(rl)))[:, None] + np.arange(nb)[None, :]] = packed
-    cb = cig.astype("<u4").view(np.uint8).reshape(m, -1)
-    for k in range(cig.shape[1]):
-        sel = ncig > k
+    cf, nf = cig[fu], ncig[fu]
+    cb = cf.astype("<u4").view(np.uint8).reshape(mf, -1)
+    for k in range(cf.shape[1]):
+        sel = nf > k
         pay[(ro[sel, None] + coff + 4 * k + np.arange(4)[None, :])] = cb[sel, 4 * k : 4 * k + 4]
-    return roff, pay
+    return roff, pay, flag
 
 
 def synth_reads(
     seed: int, n_reads: int, n_cells: int, read_len: int = 50, mito_len: int = MITO_LEN, chunk: int = 262144,
-    rec_align: int = REC_ALIGN,
+    rec_align: int = REC_ALIGN, pack: bool = True,
 ) -> ReadSoA:
-    """Host mirror of the device generator (bit-identical)."""
+    """Host mirror of the device generator (bit-identical). pack: reads that fit
+    get the packed 64-byte record layout (all of them at read_len <= 50)."""
     if read_len < 48:
         raise ValueError("read_len must be >= 48")
     cdf = cell_cdf(seed, n_cells)
@@ -374,9 +431,9 @@ def synth_reads(
     for i0 in range(0, n_reads, chunk):
         i1 = min(n_reads, i0 + chunk)
         f = _synth_chunk(seed, i0, i1, n_reads, read_len, n_cells, mito_len, cdf, ref)
-        roff, pay = _pack_fixed(f["start"], f["flag"], f["ncig"], f["cig"], f["qual"], f["code"], read_len,
-                                rec_align)
-        parts.append(ReadSoA(f["start"], f["bc"], f["tlen"], f["flag"], f["mapq"], f["span"], roff, pay))
+        roff, pay, flag = _pack_fixed(f["start"], f["flag"], f["ncig"], f["cig"], f["qual"], f["code"], read_len,
+                                      rec_align, pack)
+        parts.append(ReadSoA(f["start"], f["bc"], f["tlen"], flag, f["mapq"], f["span"], roff, pay))
     soa = _concat_dense(parts)
     soa.extra.update(cdf=cdf, ref=ref, seed=seed, read_len=read_len)
     return soa
@@ -409,8 +466,10 @@ def cigar_ref_span(cigar) -> int:
     return sum(length for op, length in cigar if op in (0, 2, 3, 7, 8))
 
 
-def pack_reads(reads: list[dict], rec_align: int = REC_ALIGN) -> ReadSoA:
-    """Pack pysam-like read dicts into the engine input.
+def pack_reads(reads: list[dict], rec_align: int = REC_ALIGN, pack: bool = True) -> ReadSoA:
+    """Pack pysam-like read dicts into the engine input. pack: reads that fit get
+    the packed 64-byte layout (include/mgpileup.h), which keeps what the pileup
+    reads but not the code and quality of non-ACGT bases.
 
     Keys: ``reference_start``, ``flag`` (BAM flag), ``mapping_quality``,
     ``cigartuples`` (list of (op, len) or None), ``query_sequence`` (str or
@@ -442,6 +501,20 @@ def pack_reads(reads: list[dict], rec_align: int = REC_ALIGN) -> ReadSoA:
         mapq[i] = r.get("mapping_quality", 60)
         span[i] = max(cigar_ref_span(cig), lseq)
         roff[i] = off
+        if pack and seq is not None and qual is not None and lseq:
+            cw = np.array([[(ln << 4) | op for op, ln in cig] or [0]], np.int64)
+            qa = (np.asarray(qual, dtype=np.int64) & 0xFF).reshape(1, -1)
+            if packable_mask([start[i]], [f], [lseq], [len(cig)], cw, qa)[0]:
+                codes = np.array([[_NT16_IDX[ch] for ch in seq.upper()]], np.int64)
+                f |= FLAG_PACKED
+                flag[i] = f
+                size = (PACK_BYTES + rec_align - 1) & ~(rec_align - 1)
+                rec = np.zeros(size, np.uint8)
+                rec[:PACK_BYTES] = pack_bytes([start[i]], [lseq], [(f & FLAG_REVERSE) != 0], [len(cig)], cw, qa,
+                                              codes)[0]
+                chunks.append(rec)
+                off += size
+                continue
         size = int(rec_size(len(cig), lseq, rec_align))
         coff = int(cigar_offset(lseq))
         rec = np.zeros(size, np.uint8)
@@ -467,8 +540,24 @@ def pack_reads(reads: list[dict], rec_align: int = REC_ALIGN) -> ReadSoA:
     return ReadSoA(start, bc, tlen, flag, mapq, span, roff, payload)
 
 
-def unpack_record(payload: np.ndarray, off: int) -> dict:
-    """Decode one payload record (test helper)."""
+def unpack_record(payload: np.ndarray, off: int, flag: int = 0) -> dict:
+    """Decode one payload record (flag: the read's flag word, which tells the
+    layout). A packed record gives ``N`` with quality 0 for its non-ACGT bases
+    and no ``flag`` key beyond the reverse bit."""
+    if int(flag) & FLAG_PACKED:
+        r = payload[off : off + PACK_BYTES]
+        start = int(r[:4].view("<i4")[0])
+        lseq = int(r[4])
+        ncig = int(r[5]) & 0x7F
+        cig = r[6:14].view("<u2").astype(np.int64).tolist()[:ncig]
+        b = r[14 : 14 + lseq].astype(np.int64)
+        never = b >= 252  # 0xFF: a non-ACGT base
+        seq = "".join("N" if nv else "ACGT"[x & 3] for x, nv in zip(b.tolist(), never.tolist()))
+        qual = np.where(never, 0, b >> 2).tolist()
+        return dict(
+            reference_start=start, flag=FLAG_REVERSE if r[5] & 0x80 else 0,
+            cigartuples=[(c & 15, c >> 4) for c in cig], query_sequence=seq, query_qualities=qual,
+        )
     hdr = payload[off : off + 16].view(np.uint8)
     start = int(hdr[:4].view("<i4")[0])
     lseq = int(hdr[4:8].view("<u4")[0])

@@ -106,6 +106,36 @@ static int kset_test_add(kset_t *s, const key_t *k, int *err) {
     }
 }
 
+/* ---- packed record -> the full layout (include/mgpileup.h) -------------------
+ * A non-ACGT base (0xFF; any byte >= 252) becomes code 15 (N) with quality 0:
+ * pileup.py:83-86 never counts it, whatever its quality. */
+static void unpack_packed(const uint8_t *p, uint8_t *full) {
+    int32_t start;
+    uint32_t k;
+    memcpy(&start, p, 4);
+    const uint32_t lseq = p[4] <= MGP_PACK_MAX_LEN ? p[4] : MGP_PACK_MAX_LEN;
+    const uint16_t ncig = (uint16_t)(p[5] & 0x7Fu) <= 4 ? (uint16_t)(p[5] & 0x7Fu) : 4;
+    const uint16_t flag = (p[5] & 0x80u) ? (uint16_t)MGP_FLAG_REVERSE : 0;
+    const uint32_t coff = mgp_cigar_offset(lseq), soff = mgp_seq_offset(lseq);
+    memset(full, 0, 128);
+    memcpy(full, &start, 4);
+    memcpy(full + 4, &lseq, 4);
+    memcpy(full + 8, &ncig, 2);
+    memcpy(full + 10, &flag, 2);
+    memcpy(full + 12, &coff, 4);
+    for (k = 0; k < ncig; ++k) {
+        const uint32_t c = (uint32_t)p[6 + 2 * k] | ((uint32_t)p[7 + 2 * k] << 8);
+        memcpy(full + coff + 4 * k, &c, 4);
+    }
+    for (k = 0; k < lseq; ++k) {
+        const uint8_t v = p[14 + k];
+        const int never = v >= 252; /* 0xFF; quality 63 does not exist in the layout */
+        const uint8_t code = never ? 15 : (uint8_t)(1u << (v & 3u));
+        full[16 + k] = never ? 0 : (uint8_t)(v >> 2);
+        full[soff + (k >> 1)] |= (k & 1) ? code : (uint8_t)(code << 4);
+    }
+}
+
 /* ---- one read's pileup (pileup.py:32-95) ------------------------------------ */
 static void pile_read(const uint8_t *rec, const mgp_config *cfg, uint32_t *bc8, uint32_t *tn5) {
     int32_t start;
@@ -305,7 +335,13 @@ int oracle_run(const mgp_config *cfg, const mgp_batch *b, mgp_result *out, int32
         for (int64_t k = 0; k < nr; ++k) {
             const int64_t i = lst[off[c] + k];
             if ((int)b->mapq[i] < cfg->min_mapq) continue; /* pileup.py:33 */
-            pile_read(b->payload + b->rec_off[i], cfg, bc8, tn5);
+            if (b->flag[i] & MGP_FLAG_PACKED) {
+                uint8_t full[128];
+                unpack_packed(b->payload + b->rec_off[i], full);
+                pile_read(full, cfg, bc8, tn5);
+            } else {
+                pile_read(b->payload + b->rec_off[i], cfg, bc8, tn5);
+            }
         }
         /* dict of positions with depth > 0 or a tn5 cut (pileup.py:100-124),
          * then filter_strand_bias (pileup.py:128-154) */

@@ -2,7 +2,7 @@
 // (the pileup reads one 128-B record line per piled read, in cell-major order, so
 // from random places of the BAM-ordered payload). Experiment only, not product.
 //   build: hipcc --offload-arch=gfx950 -O3 scripts/probe_gather.hip -o scripts/probe_gather
-//   run:   scripts/probe_gather [GB] [M lines]
+//   run:   scripts/probe_gather [GB] [M lines] [alloc mode]
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
@@ -75,12 +75,44 @@ int main(int argc, char** argv) {
     const double gb = argc > 1 ? atof(argv[1]) : 25.6;
     const unsigned long long nreq = (unsigned long long)((argc > 2 ? atof(argv[2]) : 128.0) * 1e6);
     const unsigned long long nlines = (unsigned long long)(gb * 1e9 / 128);
+    // allocation: 0 hipMalloc, 1 hipExtMallocWithFlags(contiguous), 2 one VMM handle
+    // (hipMemCreate + hipMemMap) at the largest granularity the driver offers
+    const int amode = argc > 3 ? atoi(argv[3]) : 0;
     uint4* buf = nullptr;
     uint4* out = nullptr;
-    if (hipMalloc(&buf, nlines * 128) != hipSuccess || hipMalloc(&out, 64) != hipSuccess) {
-        printf("alloc failed\n");
+    size_t bytes = nlines * 128;
+    hipError_t e = hipSuccess;
+    if (amode == 1) {
+        e = hipExtMallocWithFlags((void**)&buf, bytes, hipDeviceMallocContiguous);
+    } else if (amode == 2) {
+        hipMemAllocationProp prop = {};
+        prop.type = hipMemAllocationTypePinned;
+        prop.location.type = hipMemLocationTypeDevice;
+        prop.location.id = 0;
+        size_t gmin = 0, grec = 0;
+        hipMemGetAllocationGranularity(&gmin, &prop, hipMemAllocationGranularityMinimum);
+        hipMemGetAllocationGranularity(&grec, &prop, hipMemAllocationGranularityRecommended);
+        printf("VMM granularity min %zu recommended %zu\n", gmin, grec);
+        const size_t gr = grec > gmin ? grec : gmin;
+        bytes = (bytes + gr - 1) / gr * gr;
+        hipMemGenericAllocationHandle_t h;
+        void* va = nullptr;
+        e = hipMemCreate(&h, bytes, &prop, 0);
+        if (e == hipSuccess) e = hipMemAddressReserve(&va, bytes, 1ull << 30, nullptr, 0);
+        if (e == hipSuccess) e = hipMemMap(va, bytes, 0, h, 0);
+        hipMemAccessDesc acc = {};
+        acc.location = prop.location;
+        acc.flags = hipMemAccessFlagsProtReadWrite;
+        if (e == hipSuccess) e = hipMemSetAccess(va, bytes, &acc, 1);
+        buf = (uint4*)va;
+    } else {
+        e = hipMalloc(&buf, bytes);
+    }
+    if (e != hipSuccess || hipMalloc(&out, 64) != hipSuccess) {
+        printf("alloc failed (mode %d): %s\n", amode, hipGetErrorString(e));
         return 1;
     }
+    printf("allocation mode %d at %p\n", amode, (void*)buf);
     hipMemset(buf, 1, nlines * 128);
     hipDeviceSynchronize();
     printf("buffer %.1f GB, %llu lines gathered per pass\n", nlines * 128 / 1e9, nreq);
@@ -92,7 +124,7 @@ int main(int argc, char** argv) {
         snprintf(name, sizeof name, "random 128B in sliding %5.0f MB region", mb);
         run<8, 2>(name, buf, nlines, nreq, 3, out, grid, (unsigned long long)(mb * 1048576.0 / 128));
     }
-    hipFree(buf);
+    if (amode != 2) hipFree(buf);  // (the VMM mapping is released at exit)
     hipFree(out);
     return 0;
 }

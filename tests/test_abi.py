@@ -112,15 +112,54 @@ def test_pack_and_unpack_roundtrip():
         dict(reference_start=9, cigartuples=[(0, 6)], query_sequence="TTTTGG", query_qualities=[200] * 6, bc=1,
              flag=1, mapping_quality=60, template_length=70),
     ]
-    soa = pack_reads(reads)
+    soa = pack_reads(reads, pack=False)
     assert soa.n == 2 and np.all(soa.rec_off % 8 == 0)
     for i, r in enumerate(reads):
-        d = unpack_record(soa.payload, int(soa.rec_off[i]))
+        d = unpack_record(soa.payload, int(soa.rec_off[i]), int(soa.flag[i]))
         assert d["reference_start"] == r["reference_start"]
         assert d["cigartuples"] == r["cigartuples"]
         assert d["query_sequence"] == r["query_sequence"]
         assert d["query_qualities"] == r["query_qualities"]
     assert soa.span.tolist() == [7, 6]
+
+
+def test_packed_layout_roundtrip_and_limits():
+    """Packed 64-byte records (include/mgpileup.h): what the pileup reads is
+    kept exactly; non-ACGT bases come back as N with quality 0; reads outside
+    the layout's limits keep the full layout."""
+    from mgatk2_amd.synth import FLAG_PACKED, PACK_BYTES, pack_reads, unpack_record
+
+    ok = [
+        dict(reference_start=5, cigartuples=[(4, 2), (0, 7)], query_sequence="ACGTNRY",
+             query_qualities=[0, 1, 62, 3, 4, 5, 6], flag=0x11),
+        dict(reference_start=16560, cigartuples=[(0, 10), (1, 3), (0, 27), (5, 9)], query_sequence="ACGT" * 10,
+             query_qualities=[37] * 40, flag=0x1),
+        dict(reference_start=0, cigartuples=[(0, 20), (2, 4000), (0, 30)], query_sequence="T" * 50,
+             query_qualities=[2] * 50, flag=0x0),
+    ]
+    bad = [
+        dict(reference_start=1, cigartuples=[(0, 51)], query_sequence="A" * 51, query_qualities=[30] * 51),  # long
+        dict(reference_start=1, cigartuples=[(0, 6)], query_sequence="A" * 6, query_qualities=[63] * 6),  # qual 63
+        dict(reference_start=1, cigartuples=[(0, 2), (2, 1), (0, 2), (2, 1), (0, 2)], query_sequence="A" * 6,
+             query_qualities=[30] * 6),  # 5 operations, 3 aligned blocks
+        dict(reference_start=1, cigartuples=[(0, 2), (3, 4096), (0, 4)], query_sequence="A" * 6,
+             query_qualities=[30] * 6),  # length >= 4096
+        dict(reference_start=1, cigartuples=[(0, 6)], query_sequence="A" * 6, query_qualities=None),
+    ]
+    soa = pack_reads(ok + bad)
+    assert (soa.flag[: len(ok)] & FLAG_PACKED).all() and not (soa.flag[len(ok):] & FLAG_PACKED).any()
+    assert np.all(np.diff(soa.rec_off[: len(ok) + 1].astype(np.int64)) == PACK_BYTES)
+    for i, r in enumerate(ok):
+        d = unpack_record(soa.payload, int(soa.rec_off[i]), int(soa.flag[i]))
+        assert d["reference_start"] == r["reference_start"]
+        assert d["cigartuples"] == r["cigartuples"]
+        want_seq = "".join(c if c in "ACGT" else "N" for c in r["query_sequence"])
+        assert d["query_sequence"] == want_seq
+        assert d["query_qualities"] == [q if c in "ACGT" else 0 for c, q in zip(r["query_sequence"],
+                                                                                  r["query_qualities"])]
+        assert bool(d["flag"] & 0x10) == bool(r["flag"] & 0x10)
+    full = pack_reads(ok, pack=False)
+    assert not (full.flag & FLAG_PACKED).any()
 
 
 def test_host_synth_is_deterministic_and_sorted():

@@ -41,8 +41,37 @@ def test_roundtrip_golden(case, index, tmp_path):
         assert bam.references == ("chr1", "chrM")
         assert bam.lengths == (248956422, 16569)
         assert bam.has_index == index
-        got = bam.read_soa("chrM", g.whitelist)
+        got = bam.read_soa("chrM", g.whitelist, rec_align=128, pack=False)
     _assert_soa_equal(got, g.soa)
+
+
+@pytest.mark.parametrize("case", CASES)
+def test_packed_decode_matches_full_decode(case, tmp_path):
+    """The decoder's packed records (mgp_pack_record) hold the full records'
+    pileup view: same SoA columns (plus MGP_FLAG_PACKED), same start / strand /
+    CIGAR, bases with N and quality 0 where the base is not A, C, G or T."""
+    from mgatk2_amd.synth import FLAG_PACKED
+
+    g = Golden(case)
+    soa_to_bam(tmp_path / "x.bam", g.soa, g.whitelist)
+    with BamFile(tmp_path / "x.bam") as bam:
+        pk = bam.read_soa("chrM", g.whitelist, pack=True)
+        fu = bam.read_soa("chrM", g.whitelist, pack=False)
+    for k in ("start", "bc", "tlen", "mapq", "span"):
+        np.testing.assert_array_equal(getattr(pk, k), getattr(fu, k), err_msg=k)
+    np.testing.assert_array_equal(pk.flag & np.uint16(0xFFFF ^ FLAG_PACKED), fu.flag)
+    assert (pk.flag & FLAG_PACKED).any()
+    for i in range(pk.n):
+        a = unpack_record(pk.payload, int(pk.rec_off[i]), int(pk.flag[i]))
+        b = unpack_record(fu.payload, int(fu.rec_off[i]), int(fu.flag[i]))
+        assert a["reference_start"] == b["reference_start"] and a["cigartuples"] == b["cigartuples"]
+        if pk.flag[i] & FLAG_PACKED:
+            acgt = [c in "ACGT" for c in b["query_sequence"]]
+            assert a["query_sequence"] == "".join(c if m else "N" for c, m in zip(b["query_sequence"], acgt))
+            assert a["query_qualities"] == [q if m else 0 for q, m in zip(b["query_qualities"], acgt)]
+            assert bool(a["flag"] & 0x10) == bool(b["flag"] & 0x10)
+        else:
+            assert a == b
 
 
 def _independent_decode(path):
@@ -91,7 +120,7 @@ def test_writer_independent_decode(tmp_path):
     refs, recs = _independent_decode(tmp_path / "x.bam")
     assert refs == ["chr1", "chrM"] and len(recs) == g.soa.n
     for i in range(0, g.soa.n, 7):
-        r, d = recs[i], unpack_record(g.soa.payload, int(g.soa.rec_off[i]))
+        r, d = recs[i], unpack_record(g.soa.payload, int(g.soa.rec_off[i]), int(g.soa.flag[i]))
         assert r["tid"] == 1 and r["pos"] == g.soa.start[i] and r["mapq"] == g.soa.mapq[i]
         assert r["flag"] == int(g.soa.flag[i]) & 0xFFF and r["tlen"] == g.soa.tlen[i]
         assert r["cig"] == d["cigartuples"]

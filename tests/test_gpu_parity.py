@@ -101,6 +101,81 @@ def test_device_generator_equals_host_mirror(engine_lib):
             np.testing.assert_array_equal(getattr(dev, k), getattr(host, k), err_msg=f"{k} n={n}")
 
 
+# ---------------------------------------------------------------------------
+# record layouts (include/mgpileup.h): full 128-byte and packed 64-byte records
+# ---------------------------------------------------------------------------
+@pytest.mark.parametrize("case", CASES)
+def test_engine_matches_reference_goldens_packed(case, engine_lib, tmp_path):
+    """The golden reads through the native BAM decoder with packing on."""
+    from mgatk2_amd.bam import BamFile, soa_to_bam
+    from mgatk2_amd.synth import FLAG_PACKED
+
+    g = Golden(case)
+    soa_to_bam(tmp_path / "x.bam", g.soa, g.whitelist)
+    with BamFile(tmp_path / "x.bam") as bam:
+        soa = bam.read_soa("chrM", g.whitelist, pack=True)
+    assert (soa.flag & FLAG_PACKED).any()
+    check_result(run_engine(engine_lib, g.config(), soa), g)
+
+
+def _mixed_layout_synth(seed, n, nc, frac_full):
+    """Synthetic reads where a random fraction keeps the full layout (one base
+    quality raised to 63..70, which the packed layout cannot hold): waves pile
+    packed and full records side by side."""
+    from mgatk2_amd.synth import ReadSoA, _pack_fixed, _synth_chunk, cell_cdf, ref_codes
+
+    cdf, ref = cell_cdf(seed, nc), ref_codes(seed)
+    f = _synth_chunk(seed, 0, n, n, 50, nc, 16569, cdf, ref)
+    rng = np.random.default_rng(seed)
+    sel = rng.random(n) < frac_full
+    pos = rng.integers(0, 50, n)
+    f["qual"][sel, pos[sel]] = rng.integers(63, 71, int(sel.sum()))
+    roff, pay, flag = _pack_fixed(f["start"], f["flag"], f["ncig"], f["cig"], f["qual"], f["code"], 50)
+    return ReadSoA(f["start"], f["bc"], f["tlen"], flag, f["mapq"], f["span"], roff, pay)
+
+
+@pytest.mark.parametrize("frac_full", [0.0, 0.05, 0.5, 1.0])
+@pytest.mark.parametrize("cfgname", sorted(CONFIGS))
+def test_mixed_record_layouts_match_oracle(engine_lib, oracle_lib, cfgname, frac_full):
+    from mgatk2_amd.engine import EngineConfig
+    from mgatk2_amd.synth import FLAG_PACKED
+
+    soa = _mixed_layout_synth(77, 200_000, 60, frac_full)
+    frac = float(np.mean((soa.flag & FLAG_PACKED) == 0))
+    assert abs(frac - frac_full) < 0.01
+    cfg = EngineConfig(n_cells=60, **CONFIGS[cfgname])
+    res = run_engine(engine_lib, cfg, soa)
+    exp, _ = oracle_lib.oracle_run(cfg, soa)
+    assert_same(res, exp, f"{cfgname} full={frac_full}")
+
+
+def test_packed_and_full_layouts_give_identical_results(engine_lib):
+    """Quality thresholds around the packed range: 0, 37, 62, 63 and a negative one."""
+    from mgatk2_amd.engine import EngineConfig
+    from mgatk2_amd.synth import synth_reads
+
+    pk = synth_reads(31, 300_000, 90, pack=True)
+    fu = synth_reads(31, 300_000, 90, pack=False)
+    for q in (-5, 0, 37, 62, 63):
+        cfg = EngineConfig(n_cells=90, min_baseq=q, min_mapq=30, dedup_mode="alignment_and_fragment_length")
+        assert_same(run_engine(engine_lib, cfg, pk), run_engine(engine_lib, cfg, fu), f"min_baseq {q}")
+
+
+def test_packed_record_out_of_limits_raises(engine_lib):
+    from mgatk2_amd.engine import EngineConfig
+    from mgatk2_amd.exceptions import InvalidInputError
+    from mgatk2_amd.synth import FLAG_PACKED, pack_reads
+
+    soa = pack_reads([_read(100, [(0, 30)], "A" * 30, 0)])
+    assert soa.flag[0] & FLAG_PACKED
+    soa.payload[int(soa.rec_off[0]) + 4] = 60  # l_seq past the layout's 50
+    with engine_lib.Engine(EngineConfig(n_cells=1, min_mapq=0)) as eng:
+        eng.push(soa)
+        eng.run()
+        with pytest.raises(InvalidInputError):
+            eng.sync()
+
+
 def test_rerun_is_idempotent(engine_lib):
     from mgatk2_amd.engine import EngineConfig
     from mgatk2_amd.synth import synth_reads
