@@ -143,7 +143,8 @@ def main():
     if pmc.exists():
         try:
             d = json.loads(pmc.read_text())
-            if d.get("reads") == n_res and d.get("cells") == n_cells:
+            if (d.get("reads") == n_res and d.get("cells") == n_cells
+                    and d.get("record_layout", "full") == args.record_layout):
                 traffic = d.get(dom)
         except Exception:
             traffic = None

@@ -16,6 +16,7 @@ root = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out"
 reads = int(sys.argv[2]) if len(sys.argv) > 2 else 200_000_000
 cells = int(sys.argv[3]) if len(sys.argv) > 3 else 10_000
 out = Path(sys.argv[4]) if len(sys.argv) > 4 else Path("profiles/pmc_traffic.json")
+layout = sys.argv[5] if len(sys.argv) > 5 else "packed"  # bench.py --record-layout of the profiled run
 acc = defaultdict(lambda: defaultdict(list))
 for f in glob.glob(f"{root}/pmc_*/**/*counter_collection.csv", recursive=True):
     with open(f) as fh:
@@ -24,7 +25,7 @@ for f in glob.glob(f"{root}/pmc_*/**/*counter_collection.csv", recursive=True):
             acc[name][row["Counter_Name"]].append(float(row["Counter_Value"]))
 stage = {"k_pileup": "pileup", "k_group_a": "group_a", "k_group_b": "group_b", "k_bin_count": "hist",
          "k_median": "median"}
-res = {"reads": reads, "cells": cells, "unit": "bytes per launch",
+res = {"reads": reads, "cells": cells, "record_layout": layout, "unit": "bytes per launch",
        "method": "2*FETCH_SIZE + WRITE_SIZE (KB->B), mean over dispatches; gfx950 FETCH_SIZE correction",
        "raw": {}}
 for k, cs in acc.items():
