@@ -1188,6 +1188,13 @@ __device__ __forceinline__ void pile_line(bool has, bool packed, const uint8_t* 
         }
     }
     const uint32_t inc = strand_inc(strand);
+    if (MGP_ABL == 8) {  // records loaded, no per-base work (experiments only)
+        const uint32_t x = R.h.x ^ R.h.y ^ R.h.z ^ R.h.w ^ R.qv[0].x ^ R.qv[0].y ^ R.qv[0].z ^ R.qv[0].w ^
+                           R.qv[1].x ^ R.qv[1].y ^ R.qv[1].z ^ R.qv[1].w ^ R.qv[2].x ^ R.qv[2].y ^ R.qv[2].z ^
+                           R.qv[2].w;
+        if (x == 0x9e3779b9u) atomicAdd(&tile[0], 1u);
+        return;
+    }
     // one register pass per layout present in the wave (mixed waves are rare:
     // producers pack every read that fits)
     if (__ballot(fast && !packed) != 0ull)
