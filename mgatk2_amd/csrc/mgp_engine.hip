@@ -3,9 +3,10 @@
 // Hot path (one mgp_run over the HBM-resident read set), restating the
 // reference's per-read Python loops (paths relative to the reference root):
 //
-//   k_bin_count     per start bin: bin bounds by binary search, coordinate-order
-//                   check (pysam's fetch() order, readers.py:87-92), flag/barcode
-//                   filters (readers.py:95-111) and the per-cell read histogram
+//   k_bin_count     per (start bin, cell slice): bin bounds by binary search,
+//                   coordinate-order check (pysam's fetch() order, readers.py:87-92),
+//                   flag/barcode filters (readers.py:95-111) and the per-cell read
+//                   histogram in LDS
 //   k_scan_*        exclusive scan of the histogram in (cell, start-bin) order: the
 //                   cell-major layout of `reads_by_barcode` (readers.py:69,164)
 //   k_group_a/b     two-pass stable grouping: per start bin into (bin, 64-cell group)
@@ -26,6 +27,7 @@
 //   k_tally_reduce  sum of the partial tallies (writers.py:340-349 input)
 //   RCCL allreduce  tallies over ranks when cells are sharded over GPUs
 #include <hip/hip_runtime.h>
+#include <cstdlib>
 #include <rccl/rccl.h>
 
 #include <algorithm>
@@ -115,6 +117,7 @@ struct mgp_ctx {
     int64_t runs = 0;                  // completed mgp_run calls
     Geom g{};
     int lds_hist_max_cells = 0;
+    int hist_slice_cells = 0;  // > 0: cap on the histogram's cells per slice (MGP_HIST_SLICE_CELLS)
 
     // resident inputs (BAM order)
     int64_t n = 0, pay = 0;
@@ -173,36 +176,42 @@ __device__ __forceinline__ void part_range(int64_t lo, int64_t hi, int p, int64_
     phi = lo + len * (p + 1) / kParts;
 }
 
-// One workgroup (8 waves) per start bin: bin bounds by binary search in the
-// sorted starts, coordinate-order check (pysam's fetch order, readers.py:87-92),
-// flag/barcode filters (readers.py:95-111) and the per-cell histogram of the bin
-// (LDS atomics when the row fits, else atomics on the global row). The bin's
-// parts are counted one after the other; after each part the per-64-cell-group
-// totals are snapshotted, giving the per-(bin, part, group) counts of pass A.
+// One workgroup (8 waves) per (start bin, cell slice): bin bounds by binary
+// search in the sorted starts, coordinate-order check (pysam's fetch order,
+// readers.py:87-92), flag/barcode filters (readers.py:95-111) and the LDS
+// histogram of the slice's cells over the bin's reads. A slice is as many
+// 64-cell groups as the LDS holds (one slice up to ~24k cells; more cells scan
+// the bin once per slice). The bin's parts are counted one after the other;
+// after each part the per-64-cell-group totals are snapshotted, giving the
+// per-(bin, part, group) counts of pass A. Slice 0 writes the bin's bounds,
+// valid count and run checks.
 constexpr int kHistBlock = 512;
-template <bool kLds>
 __global__ void __launch_bounds__(kHistBlock) k_bin_count(const int32_t* __restrict__ start,
                                                           const int32_t* __restrict__ bc,
                                                           const uint16_t* __restrict__ flag,
                                                           const uint32_t* __restrict__ span, int64_t n, Geom g,
-                                                          uint32_t* __restrict__ H, uint32_t* __restrict__ PG,
-                                                          int ngroups, uint32_t* __restrict__ bin_lo,
+                                                          int slice_cells, uint32_t* __restrict__ H,
+                                                          uint32_t* __restrict__ PG, int ngroups,
+                                                          uint32_t* __restrict__ bin_lo,
                                                           uint32_t* __restrict__ bin_valid, DevStats* st) {
-    extern __shared__ uint32_t hist[];  // kLds: [nc] cell counts; else [ngroups] group counts; then cum[ngroups]
+    extern __shared__ uint32_t hist[];  // [slice cells] counts, then cum[slice groups]
     __shared__ int64_t s_range[2];
     __shared__ uint32_t s_nvalid;
     const int b = blockIdx.x;
+    const bool first = blockIdx.y == 0;
     const int nc = g.nc;
+    const int c_lo = blockIdx.y * slice_cells, c_hi = min(nc, c_lo + slice_cells);
+    const int ncs = c_hi - c_lo;
+    const int g_lo = c_lo / kGroup, ngs = (ncs + kGroup - 1) / kGroup;
     const int lane = threadIdx.x & 63;
-    uint32_t* cum = hist + (kLds ? nc : ngroups);
+    uint32_t* cum = hist + ncs;
     uint32_t* row = H + (size_t)b * nc;
-    uint32_t* cnt = kLds ? hist : row;
     if (threadIdx.x < 2) s_range[threadIdx.x] = lower_bound_start(start, n, bin_threshold(b + threadIdx.x, g));
-    for (int c = threadIdx.x; c < (kLds ? nc : ngroups); c += blockDim.x) hist[c] = 0;
+    for (int c = threadIdx.x; c < ncs; c += blockDim.x) hist[c] = 0;
     if (threadIdx.x == 0) s_nvalid = 0;
     __syncthreads();
     const int64_t blo = s_range[0], bhi = max(s_range[1], blo);
-    if (threadIdx.x == 0) {
+    if (first && threadIdx.x == 0) {
         bin_lo[b] = (uint32_t)blo;
         if (b == g.nbins - 1) bin_lo[g.nbins] = (uint32_t)n;
     }
@@ -225,9 +234,13 @@ __global__ void __launch_bounds__(kHistBlock) k_bin_count(const int32_t* __restr
                 const int64_t j = i < hi ? i : hi - 1;
                 cc[u] = bc[j];
                 ff[u] = flag[j];
-                ss[u] = start[j];
-                sp0[u] = start[j > 0 ? j - 1 : 0];
-                sp[u] = span[j];
+                ss[u] = sp0[u] = 0;
+                sp[u] = 0;
+                if (first) {  // the run checks: slice 0 only (other slices read 6 B per read)
+                    ss[u] = start[j];
+                    sp0[u] = start[j > 0 ? j - 1 : 0];
+                    sp[u] = span[j];
+                }
             }
 #pragma unroll
             for (int u = 0; u < kU; ++u) {
@@ -237,8 +250,7 @@ __global__ void __launch_bounds__(kHistBlock) k_bin_count(const int32_t* __restr
                 if (i > 0 && ss[u] < sp0[u]) unsorted = true;
                 badbc |= (c >= nc);
                 if (read_valid(c, (uint16_t)ff[u], nc)) {
-                    atomicAdd(&cnt[c], 1u);
-                    if (!kLds) atomicAdd(&hist[c >> 6], 1u);
+                    if (c >= c_lo && c < c_hi) atomicAdd(&hist[c - c_lo], 1u);
                     mspan = sp[u] > mspan ? sp[u] : mspan;
                     ++nvalid;
                 }
@@ -246,28 +258,20 @@ __global__ void __launch_bounds__(kHistBlock) k_bin_count(const int32_t* __restr
         }
         __syncthreads();
         // group totals so far; this part's counts are the growth since the last part
-        // (a group is always handled by the same thread, so `cum` needs no barrier)
-        uint32_t* pgp = pg + (size_t)part * ngroups;
-        if (kLds) {
-            for (int gi = threadIdx.x >> 6; gi < ngroups; gi += kHistBlock / kWave) {
-                const int c = gi * kGroup + lane;
-                const uint32_t h = wave_sum(c < nc ? hist[c] : 0u);
-                if (lane == 0) {
-                    pgp[gi] = h - (part ? cum[gi] : 0u);
-                    cum[gi] = h;
-                }
-            }
-        } else {
-            for (int gi = threadIdx.x; gi < ngroups; gi += blockDim.x) {
-                const uint32_t h = hist[gi];
+        // (a group is always handled by the same wave, so `cum` needs no barrier)
+        uint32_t* pgp = pg + (size_t)part * ngroups + g_lo;
+        for (int gi = threadIdx.x >> 6; gi < ngs; gi += kHistBlock / kWave) {
+            const int c = gi * kGroup + lane;
+            const uint32_t h = wave_sum(c < ncs ? hist[c] : 0u);
+            if (lane == 0) {
                 pgp[gi] = h - (part ? cum[gi] : 0u);
                 cum[gi] = h;
             }
         }
         __syncthreads();  // the snapshot is complete before the next part counts
     }
-    if (kLds)
-        for (int c = threadIdx.x; c < nc; c += blockDim.x) row[c] = hist[c];
+    for (int c = threadIdx.x; c < ncs; c += blockDim.x) row[c_lo + c] = hist[c];
+    if (!first) return;
     mspan = wave_max(mspan);
     nvalid = wave_sum(nvalid);
     const bool anybad = __ballot(badbc) != 0ull, anyuns = __ballot(unsorted) != 0ull;
@@ -1668,11 +1672,15 @@ int mgp_open(const mgp_config* cfg, int hip_device, mgp_ctx** out) {
     hipDeviceProp_t prop;
     HIP_TRY(hipGetDeviceProperties(&prop, hip_device));
     ctx->lds_hist_max_cells = (int)std::min<size_t>(prop.sharedMemPerBlock, 96 * 1024) / 4;
+    if (const char* e = std::getenv("MGP_HIST_SLICE_CELLS")) {  // tests: force several histogram slices
+        const long v = std::strtol(e, nullptr, 10);
+        if (v >= kGroup) ctx->hist_slice_cells = (int)(v / kGroup * kGroup);
+    }
     // kernels whose dynamic LDS may exceed 64 KiB (gfx950: up to 160 KiB per workgroup);
     // best effort: the runtime may already allow it without the attribute
     {
         const int lds_max = (int)prop.sharedMemPerBlock;
-        (void)hipFuncSetAttribute((const void*)k_bin_count<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+        (void)hipFuncSetAttribute((const void*)k_bin_count, hipFuncAttributeMaxDynamicSharedMemorySize,
                                   lds_max);
         (void)hipFuncSetAttribute((const void*)k_group_a, hipFuncAttributeMaxDynamicSharedMemorySize, lds_max);
         (void)hipFuncSetAttribute((const void*)k_pileup, hipFuncAttributeMaxDynamicSharedMemorySize, lds_max);
@@ -1860,26 +1868,23 @@ int mgp_run(mgp_ctx* ctx) {
     }
 
     if (nc > 0) {
-        const bool lds = nc + (nc + kGroup - 1) / kGroup <= ctx->lds_hist_max_cells;
         const int ngroups = (nc + kGroup - 1) / kGroup;
         // 1. per (start bin, cell) histogram + per (bin, part, group) counts + bin bounds + order check
         STAGE_BEGIN(ST_HIST);
-        if (!lds || n == 0) HIP_TRY(hipMemsetAsync(ctx->H.p, 0, (size_t)(g.nbins + 1) * nc * 4, s));
+        if (n == 0) HIP_TRY(hipMemsetAsync(ctx->H.p, 0, (size_t)(g.nbins + 1) * nc * 4, s));
         if (n == 0) HIP_TRY(hipMemsetAsync(ctx->bin_start.p, 0, (size_t)(g.nbins + 1) * 4, s));
         HIP_TRY(hipMemsetAsync(ctx->F.p, 0, (size_t)g.nbins * ((nc + 31) / 32) * 4, s));
         if (n > 0) {
-            if ((size_t)ngroups * 8 > (size_t)ctx->lds_hist_max_cells * 4)
-                return set_err(MGP_E_INVALID, "too many cells for one context (histogram LDS)");
-            if (lds)
-                k_bin_count<true><<<g.nbins, kHistBlock, (size_t)(nc + ngroups) * 4, s>>>(
-                    ctx->start.as<int32_t>(), ctx->bc.as<int32_t>(), ctx->flag.as<uint16_t>(),
-                    ctx->span.as<uint32_t>(), n, g, ctx->H.as<uint32_t>(), ctx->PG.as<uint32_t>(), ngroups,
-                    ctx->bin_start.as<uint32_t>(), ctx->bin_valid.as<uint32_t>(), st);
-            else
-                k_bin_count<false><<<g.nbins, kHistBlock, (size_t)ngroups * 8, s>>>(
-                    ctx->start.as<int32_t>(), ctx->bc.as<int32_t>(), ctx->flag.as<uint16_t>(),
-                    ctx->span.as<uint32_t>(), n, g, ctx->H.as<uint32_t>(), ctx->PG.as<uint32_t>(), ngroups,
-                    ctx->bin_start.as<uint32_t>(), ctx->bin_valid.as<uint32_t>(), st);
+            // cells per slice: whole 64-cell groups, counts + group totals within the LDS budget
+            int lds_cells = ctx->lds_hist_max_cells / (kGroup + 1) * kGroup;
+            if (ctx->hist_slice_cells > 0) lds_cells = std::min(lds_cells, ctx->hist_slice_cells);
+            const int slice = nc <= lds_cells ? nc : lds_cells;
+            const int nslices = (nc + slice - 1) / slice;
+            const size_t lds = ((size_t)slice + (slice + kGroup - 1) / kGroup) * 4;
+            k_bin_count<<<dim3((unsigned)g.nbins, (unsigned)nslices), kHistBlock, lds, s>>>(
+                ctx->start.as<int32_t>(), ctx->bc.as<int32_t>(), ctx->flag.as<uint16_t>(), ctx->span.as<uint32_t>(),
+                n, g, slice, ctx->H.as<uint32_t>(), ctx->PG.as<uint32_t>(), ngroups, ctx->bin_start.as<uint32_t>(),
+                ctx->bin_valid.as<uint32_t>(), st);
             HIP_TRY(hipGetLastError());
         }
         STAGE_END(ST_HIST);

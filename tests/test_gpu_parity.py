@@ -307,15 +307,20 @@ def test_deep_cell_median_fallback(engine_lib, oracle_lib):
     assert res.depth_max[0] >= 8192
 
 
-def test_many_cells_global_histogram_path(engine_lib, oracle_lib):
-    """More cells than the LDS histogram holds: global-row histogram and counters."""
+@pytest.mark.parametrize("n_cells,slice_cells", [(30_000, None), (5_000, 1024), (3_001, 64)])
+def test_many_cells_sliced_histogram(engine_lib, oracle_lib, monkeypatch, n_cells, slice_cells):
+    """More cells than one LDS histogram holds: the bins are counted in cell
+    slices (30k cells: 2 slices; smaller slices forced with MGP_HIST_SLICE_CELLS:
+    5 and 47, the last one ragged), whose group totals must line up."""
     from mgatk2_amd.engine import EngineConfig
 
-    soa = _synth(77, 150_000, 30_000)
-    cfg = EngineConfig(n_cells=30_000, min_baseq=0, min_mapq=0, dedup_mode="alignment_start", min_reads=0)
+    if slice_cells:
+        monkeypatch.setenv("MGP_HIST_SLICE_CELLS", str(slice_cells))
+    soa = _synth(77, 5 * n_cells, n_cells)
+    cfg = EngineConfig(n_cells=n_cells, min_baseq=0, min_mapq=0, dedup_mode="alignment_start", min_reads=0)
     res = run_engine(engine_lib, cfg, soa)
     exp, _ = oracle_lib.oracle_run(cfg, soa)
-    assert_same(res, exp, "30k cells")
+    assert_same(res, exp, f"{n_cells} cells / {slice_cells}")
 
 
 def test_deep_bins_parts_and_direct_buckets(engine_lib, oracle_lib):
