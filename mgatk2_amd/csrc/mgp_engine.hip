@@ -393,7 +393,13 @@ constexpr unsigned long long GM_REV = 1ull << 56, GM_PAIRED = 2ull << 56, GM_MAP
 // the passes (record offsets stay below 2^50).
 constexpr unsigned long long GM_LCELL_SHIFT = 50, GM_LCELL = 63ull << GM_LCELL_SHIFT;
 
-__global__ void __launch_bounds__(kBlock) k_group_a(int64_t n, const int32_t* __restrict__ start,
+#ifndef MGP_GA_AHEAD
+#define MGP_GA_AHEAD 8  // reads per lane per pass-A step (A/B: 2, 3, 4, 6 slower)
+#endif
+#ifndef MGP_GA_WAVES
+#define MGP_GA_WAVES 1
+#endif
+__global__ void __launch_bounds__(kBlock, MGP_GA_WAVES) k_group_a(int64_t n, const int32_t* __restrict__ start,
                                                     const int32_t* __restrict__ bc, const int32_t* __restrict__ tlen,
                                                     const uint16_t* __restrict__ flag, const uint8_t* __restrict__ mapq,
                                                     const uint64_t* __restrict__ roff,
@@ -451,7 +457,7 @@ __global__ void __launch_bounds__(kBlock) k_group_a(int64_t n, const int32_t* __
     __syncthreads();
     // each wave owns a contiguous run of kAhead*64 reads per step (BAM order = wave
     // order, then round order); waves claim bucket slots in wave order
-    constexpr int kAhead = 4;
+    constexpr int kAhead = MGP_GA_AHEAD;
     constexpr int kStep = kAhead * kBlock;
     struct Pre {
         int c[kAhead], s[kAhead], t[kAhead], f[kAhead], m[kAhead];
