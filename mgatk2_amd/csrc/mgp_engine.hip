@@ -569,7 +569,10 @@ __global__ void __launch_bounds__(kBlock, MGP_GA_WAVES) k_group_a(int64_t n, con
 // counters (readers.py:141-144) are taken here, each read being seen exactly
 // once. The output is one 8-byte pileup element per read: record offset |
 // GP_KEEP | GP_PAIRED | GP_BAD | GP_PILE (kept and MAPQ >= min_mapq, pileup.py:33).
-constexpr int kStageB = 2048;
+#ifndef MGP_GB_STAGE
+#define MGP_GB_STAGE 2048
+#endif
+constexpr int kStageB = MGP_GB_STAGE;
 constexpr int kMaxRbB = 512;  // bins per pass-B workgroup (bucket sizes kept in LDS)
 #ifndef MGP_GB_WG
 #define MGP_GB_WG 8192  // target pass-B grid size
@@ -664,7 +667,10 @@ constexpr int kBPer = kStageB / kBlock;  // elements per lane per step
 #define MGP_ABL_B 0  // pass-B ablations (experiments only): 1 no dedup walk, 2 no pel stores, 3 no loads
 #endif
 
-__global__ void __launch_bounds__(kBlock, 4) k_group_b(const GElem* __restrict__ gel2,
+#ifndef MGP_GB_WAVES
+#define MGP_GB_WAVES 4
+#endif
+__global__ void __launch_bounds__(kBlock, MGP_GB_WAVES) k_group_b(const GElem* __restrict__ gel2,
                                                     const uint32_t* __restrict__ bucket_off,
                                                     const uint32_t* __restrict__ O, Geom g, int ngroups, int rb,
                                                     int mode, unsigned long long* __restrict__ pel,
