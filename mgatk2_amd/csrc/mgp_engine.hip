@@ -949,7 +949,7 @@ __device__ bool pile_slow(const uint8_t* __restrict__ rec, int32_t start, uint32
 }
 
 #ifndef MGP_WIN
-#define MGP_WIN 1024  // target window width (positions); W <= kMaxPosPerThread * 256
+#define MGP_WIN 1280  // target window width (positions); W <= kMaxPosPerThread * 256 (A/B: 768-2048)
 #endif
 constexpr int kMaxPosPerThread = MGP_WIN / 256;
 constexpr int kTilePitch = MGP_WIN;  // u32 per tile plane (>= the window width W)
@@ -1079,8 +1079,7 @@ __device__ __forceinline__ void pile_bases(bool act, int a0, int b0, int a1, int
     const uint32_t lo4 = 4u * (uint32_t)min(max(minbq, 0), 63);
     const uint32_t span4 = 252u - lo4;
     // base index = log2(code) for the counted codes 1, 2, 4, 8 (A, C, G, T); the
-    // plane offset is a shift of it (compile-time pitch)
-    constexpr int kPitchShift = __builtin_ctz(kTilePitch);
+    // plane offset is base index x the compile-time pitch
     // ok / plane of query position qq (static register indices)
     auto decode = [&](int qq, uint32_t& plane) -> uint32_t {
         if (kPacked) {
@@ -1113,7 +1112,7 @@ __device__ __forceinline__ void pile_bases(bool act, int a0, int b0, int a1, int
             if (!((smask >> qq) & 1ull)) continue;
             uint32_t plane;
             const uint32_t ok = decode(qq, plane);
-            if (ok) atomicAdd(&lb[(plane << kPitchShift) + qq], inc);
+            if (ok) atomicAdd(&lb[plane * (uint32_t)kTilePitch + qq], inc);
         }
     } else if (one_block) {
         uint32_t* lb = base + dl0;
@@ -1123,7 +1122,7 @@ __device__ __forceinline__ void pile_bases(bool act, int a0, int b0, int a1, int
             if (!((smask >> qq) & 1ull)) continue;
             uint32_t plane;
             const uint32_t ok = decode(qq, plane) & (uint32_t)(qq >= a0) & (uint32_t)(qq < b0);
-            if (ok) atomicAdd(&lb[(plane << kPitchShift) + qq], inc);
+            if (ok) atomicAdd(&lb[plane * (uint32_t)kTilePitch + qq], inc);
         }
     } else {
         const unsigned long long smask = range_mask(wq_lo, wq_hi);
@@ -1136,7 +1135,7 @@ __device__ __forceinline__ void pile_bases(bool act, int a0, int b0, int a1, int
             const int lo = second ? a1 : a0, hi = second ? b1 : b0;
             uint32_t plane;
             const uint32_t ok = decode(qq, plane) & (uint32_t)(qq >= lo) & (uint32_t)(qq < hi);
-            if (ok) atomicAdd(&base[(plane << kPitchShift) + qq + d], inc);
+            if (ok) atomicAdd(&base[plane * (uint32_t)kTilePitch + qq + d], inc);
         }
     }
 }
