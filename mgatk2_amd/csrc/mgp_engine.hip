@@ -670,6 +670,9 @@ constexpr int kBPer = kStageB / kBlock;  // elements per lane per step
 #ifndef MGP_GB_WAVES
 #define MGP_GB_WAVES 4
 #endif
+#ifndef MGP_GB_LOOK
+#define MGP_GB_LOOK 4  // predecessors compared branch-free before a walk back (A/B: 2-6)
+#endif
 __global__ void __launch_bounds__(kBlock, MGP_GB_WAVES) k_group_b(const GElem* __restrict__ gel2,
                                                     const uint32_t* __restrict__ bucket_off,
                                                     const uint32_t* __restrict__ O, Geom g, int ngroups, int rb,
@@ -818,10 +821,11 @@ __global__ void __launch_bounds__(kBlock, MGP_GB_WAVES) k_group_b(const GElem* _
         const uint32_t ntot = nbe > nb0 ? load(nb0, nbe) : 0u;
         // write-out with duplicate marking: equal starts of a cell's run sit just
         // before t, in BAM order; a cell has one run in the stage, so an element of
-        // another cell ends the walk. The element and its two predecessors are
+        // another cell ends the walk. The element and its kLook predecessors are
         // loaded for 2 elements at once and compared branch-free; a walk further
-        // back is needed only behind three equal starts (rare).
+        // back is needed only behind kLook + 1 equal starts.
         constexpr int kWo = 2;
+        constexpr int kLook = MGP_GB_LOOK;
 #pragma unroll
         for (int h = 0; h < kBPer; h += kWo) {
             GElem xs[kWo];
@@ -831,17 +835,22 @@ __global__ void __launch_bounds__(kBlock, MGP_GB_WAVES) k_group_b(const GElem* _
                 const uint32_t t = threadIdx.x + (uint32_t)(h + q) * kBlock;
                 const uint32_t tc = t < cur ? t : 0u;
                 const GElem x = stage[tc];
-                const GElem p1 = stage[tc >= 1u ? tc - 1u : 0u];
-                const GElem p2 = stage[tc >= 2u ? tc - 2u : 0u];
-                const bool r1 = (tc >= 1u) & (((p1.w ^ x.w) & GM_LCELL) == 0ull) & (p1.start == x.start);
-                const bool r2 = r1 & (tc >= 2u) & (((p2.w ^ x.w) & GM_LCELL) == 0ull) & (p2.start == x.start);
-                const bool s1 = r1 & (((p1.w ^ x.w) & GM_REV) == 0ull);
-                const bool s2 = r2 & (((p2.w ^ x.w) & GM_REV) == 0ull);
-                const bool t3 = (s1 & (p1.tlen == x.tlen)) | (s2 & (p2.tlen == x.tlen));
+                GElem pk[kLook];
+#pragma unroll
+                for (int k = 0; k < kLook; ++k) pk[k] = stage[tc >= (uint32_t)(k + 1) ? tc - (uint32_t)(k + 1) : 0u];
+                bool r = true, s2 = false, t3 = false;  // r: the k nearest predecessors are all in x's run
+#pragma unroll
+                for (int k = 0; k < kLook; ++k) {
+                    r = r & (tc >= (uint32_t)(k + 1)) & (((pk[k].w ^ x.w) & GM_LCELL) == 0ull) &
+                        (pk[k].start == x.start);
+                    const bool sk = r & (((pk[k].w ^ x.w) & GM_REV) == 0ull);
+                    s2 |= sk;
+                    t3 |= sk & (pk[k].tlen == x.tlen);
+                }
                 xs[q] = x;
-                d2[q] = dedup & (s1 | s2);
+                d2[q] = dedup & s2;
                 d3[q] = dedup & t3;
-                wk[q] = dedup & r2 & !t3 & (tc >= 3u) & (t < cur);
+                wk[q] = dedup & r & !t3 & (tc >= (uint32_t)(kLook + 1)) & (t < cur);
             }
 #pragma unroll
             for (int q = 0; q < kWo; ++q) {
@@ -849,7 +858,7 @@ __global__ void __launch_bounds__(kBlock, MGP_GB_WAVES) k_group_b(const GElem* _
                     const uint32_t t = threadIdx.x + (uint32_t)(h + q) * kBlock;
                     const GElem x = xs[q];
                     bool dup3 = false, dup2 = d2[q];
-                    for (uint32_t m = t - 2; !dup3 && m-- > 0;) {
+                    for (uint32_t m = t - (uint32_t)kLook; !dup3 && m-- > 0;) {
                         const GElem p = stage[m];
                         if (((p.w ^ x.w) & GM_LCELL) != 0ull || p.start != x.start) break;
                         dup2 |= same_key(p, x, dup3);
