@@ -122,6 +122,8 @@ struct mgp_ctx {
     // resident inputs (BAM order)
     int64_t n = 0, pay = 0;
     DevBuf start, bc, tlen, flag, mapq, span, roff, payload;
+    DevBuf roff_irregular;  // u32: 0 while rec_off[i] == kRecStride * i for every resident read
+    int dense = -1;         // host copy of !roff_irregular: -1 not read since the last push
 
     // run scratch
     DevBuf bin_start, H, P, cell_cnt, cell_base, bin_valid, bin_base, bucket_off, gel2, PG, F;
@@ -392,6 +394,7 @@ constexpr unsigned long long GM_REV = 1ull << 56, GM_PAIRED = 2ull << 56, GM_MAP
 // The 6-bit cell id inside the group rides in bits 50..55 of GElem.w between
 // the passes (record offsets stay below 2^50).
 constexpr unsigned long long GM_LCELL_SHIFT = 50, GM_LCELL = 63ull << GM_LCELL_SHIFT;
+constexpr uint64_t kRecStride = MGP_PACK_BYTES;  // record stride of a dense packed payload (k_check_stride)
 
 #ifndef MGP_GA_AHEAD
 #define MGP_GA_AHEAD 8  // reads per lane per pass-A step (A/B: 2, 3, 4, 6 slower)
@@ -399,6 +402,7 @@ constexpr unsigned long long GM_LCELL_SHIFT = 50, GM_LCELL = 63ull << GM_LCELL_S
 #ifndef MGP_GA_WAVES
 #define MGP_GA_WAVES 1
 #endif
+template <bool kDense>
 __global__ void __launch_bounds__(kBlock, MGP_GA_WAVES) k_group_a(int64_t n, const int32_t* __restrict__ start,
                                                     const int32_t* __restrict__ bc, const int32_t* __restrict__ tlen,
                                                     const uint16_t* __restrict__ flag, const uint8_t* __restrict__ mapq,
@@ -465,6 +469,7 @@ __global__ void __launch_bounds__(kBlock, MGP_GA_WAVES) k_group_a(int64_t n, con
     };
     // loads issued unconditionally (index clamped into the bin) so every path has
     // the same number in flight and the waits stay counted
+    // kDense: a dense packed payload (k_check_stride at ingest), offsets from the index
     auto load = [&](Pre& P, int64_t base0) {
 #pragma unroll
         for (int u = 0; u < kAhead; ++u) {
@@ -475,7 +480,7 @@ __global__ void __launch_bounds__(kBlock, MGP_GA_WAVES) k_group_a(int64_t n, con
             P.s[u] = start[j];
             P.t[u] = tlen[j];
             P.m[u] = mapq[j];
-            P.o[u] = roff[j];
+            P.o[u] = kDense ? (uint64_t)j * kRecStride : roff[j];
         }
     };
     // A step: each wave ranks its own reads by group (ballot peers, the leader of a
@@ -1616,6 +1621,15 @@ __global__ void k_add_u64(uint64_t* __restrict__ a, int64_t n, uint64_t add) {
     if (i < n) a[i] += add;
 }
 
+// Record placement check at ingest: *irregular stays 0 while every resident
+// record offset is kRecStride x its read index (a fully packed, dense payload);
+// grouping pass A then computes the offsets instead of reading them.
+__global__ void k_check_stride(const uint64_t* __restrict__ roff, int64_t n, int64_t i0, uint32_t* irregular) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const bool bad = i < n && roff[i] != (uint64_t)(i0 + i) * kRecStride;
+    if (__ballot(bad) != 0ull && (threadIdx.x & 63) == 0) atomicOr(irregular, 1u);
+}
+
 // ---------------------------------------------------------------------------
 // host side
 // ---------------------------------------------------------------------------
@@ -1702,7 +1716,9 @@ int mgp_open(const mgp_config* cfg, int hip_device, mgp_ctx** out) {
         const int lds_max = (int)prop.sharedMemPerBlock;
         (void)hipFuncSetAttribute((const void*)k_bin_count, hipFuncAttributeMaxDynamicSharedMemorySize,
                                   lds_max);
-        (void)hipFuncSetAttribute((const void*)k_group_a, hipFuncAttributeMaxDynamicSharedMemorySize, lds_max);
+        (void)hipFuncSetAttribute((const void*)k_group_a<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  lds_max);
+        (void)hipFuncSetAttribute((const void*)k_group_a<true>, hipFuncAttributeMaxDynamicSharedMemorySize, lds_max);
         (void)hipFuncSetAttribute((const void*)k_pileup, hipFuncAttributeMaxDynamicSharedMemorySize, lds_max);
         (void)hipGetLastError();
         if ((size_t)ctx->g.L * 4 + 2048 > prop.sharedMemPerBlock) {
@@ -1801,6 +1817,12 @@ int mgp_push_batch(mgp_ctx* ctx, const mgp_batch* b) {
         k_add_u64<<<blocks_for(nb), kBlock, 0, s>>>(ctx->roff.as<uint64_t>() + n0, nb, (uint64_t)pay0);
         HIP_TRY(hipGetLastError());
     }
+    MGP_TRY(ctx->roff_irregular.ensure(4));
+    if (n0 == 0) HIP_TRY(hipMemsetAsync(ctx->roff_irregular.p, 0, 4, s));
+    ctx->dense = -1;
+    k_check_stride<<<blocks_for(nb), kBlock, 0, s>>>(ctx->roff.as<uint64_t>() + n0, nb, n0,
+                                                     ctx->roff_irregular.as<uint32_t>());
+    HIP_TRY(hipGetLastError());
     HIP_TRY(hipEventRecord(ctx->ev_copy, s));
     ctx->n = n0 + nb;
     ctx->pay = pay0 + b->payload_bytes;
@@ -1872,6 +1894,12 @@ int mgp_run(mgp_ctx* ctx) {
     const int64_t n = ctx->n;
     const int nc = g.nc;
     hipStream_t s = ctx->s_comp;
+    if (ctx->dense < 0 && n > 0) {  // the ingest stride check, read once per resident set
+        uint32_t irr = 1;
+        HIP_TRY(hipStreamSynchronize(ctx->s_copy));
+        HIP_TRY(hipMemcpy(&irr, ctx->roff_irregular.p, 4, hipMemcpyDeviceToHost));
+        ctx->dense = irr == 0u;
+    }
     HIP_TRY(hipStreamWaitEvent(s, ctx->ev_copy, 0));
     const int slot = (int)(ctx->runs % mgp_ctx::kRing);
     for (int i = 0; i < ST_N; ++i) ctx->stage_ran[slot][i] = false;
@@ -1935,9 +1963,19 @@ int mgp_run(mgp_ctx* ctx) {
             if ((uint64_t)ctx->pay >= (1ull << GM_LCELL_SHIFT))
                 return set_err(MGP_E_INVALID, "payload too large (record offsets must stay below 2^50)");
             dim3 ga((unsigned)g.nbins, kParts);
-            k_group_a<<<ga, kBlock, a_lds, s>>>(
+            if (ctx->dense > 0)
+                k_group_a<true><<<ga, kBlock, a_lds, s>>>(
                 n, ctx->start.as<int32_t>(), ctx->bc.as<int32_t>(), ctx->tlen.as<int32_t>(), ctx->flag.as<uint16_t>(),
-                ctx->mapq.as<uint8_t>(), ctx->roff.as<uint64_t>(), ctx->bin_start.as<uint32_t>(),
+                ctx->mapq.as<uint8_t>(), ctx->roff.as<uint64_t>(),
+                ctx->bin_start.as<uint32_t>(),
+                ctx->PG.as<uint32_t>(), ctx->F.as<uint32_t>(), ctx->bin_base.as<uint32_t>(), g, ngroups, gbits,
+                ctx->cfg.min_mapq, ctx->bucket_off.as<uint32_t>(), ctx->gel2.as<GElem>(),
+                ctx->first_read.as<uint32_t>(), st);
+            else
+                k_group_a<false><<<ga, kBlock, a_lds, s>>>(
+                n, ctx->start.as<int32_t>(), ctx->bc.as<int32_t>(), ctx->tlen.as<int32_t>(), ctx->flag.as<uint16_t>(),
+                ctx->mapq.as<uint8_t>(), ctx->roff.as<uint64_t>(),
+                ctx->bin_start.as<uint32_t>(),
                 ctx->PG.as<uint32_t>(), ctx->F.as<uint32_t>(), ctx->bin_base.as<uint32_t>(), g, ngroups, gbits,
                 ctx->cfg.min_mapq, ctx->bucket_off.as<uint32_t>(), ctx->gel2.as<GElem>(),
                 ctx->first_read.as<uint32_t>(), st);
@@ -2210,6 +2248,13 @@ int mgp_synth_generate(mgp_ctx* ctx, const mgp_synth_params* p) {
         ref.release();
         return r;
     }
+    MGP_TRY(ctx->roff_irregular.ensure(4));
+    HIP_TRY(hipMemsetAsync(ctx->roff_irregular.p, 0, 4, s));
+    ctx->dense = -1;
+    if (n)
+        k_check_stride<<<blocks_for(n), kBlock, 0, s>>>(ctx->roff.as<uint64_t>(), n, 0,
+                                                        ctx->roff_irregular.as<uint32_t>());
+    HIP_TRY(hipGetLastError());
     HIP_TRY(hipStreamSynchronize(s));
     cdf.release();
     ref.release();

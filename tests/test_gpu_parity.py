@@ -161,6 +161,30 @@ def test_packed_and_full_layouts_give_identical_results(engine_lib):
         assert_same(run_engine(engine_lib, cfg, pk), run_engine(engine_lib, cfg, fu), f"min_baseq {q}")
 
 
+@pytest.mark.parametrize("cuts", [(0, 40_000, 100_000, 150_000), (0, 40_001, 100_003, 150_000)])
+def test_dense_packed_payload_batches(engine_lib, oracle_lib, cuts):
+    """A fully packed payload at a 64-byte stride lets grouping pass A compute
+    the record offsets (k_check_stride at ingest). Batches whose payload bases
+    keep the stride (first cut) stay dense; batches that break it (second cut:
+    the 256-byte batch alignment moves the offsets) fall back to reading them.
+    Both equal one push and the oracle."""
+    from mgatk2_amd.engine import EngineConfig
+    from mgatk2_amd.synth import FLAG_PACKED
+
+    soa = _synth(99, 150_000, 50)
+    assert (soa.flag & FLAG_PACKED).all() and np.array_equal(soa.rec_off, np.arange(soa.n, dtype=np.uint64) * 64)
+    cfg = EngineConfig(n_cells=50)
+    one = run_engine(engine_lib, cfg, soa)
+    with engine_lib.Engine(cfg) as eng:
+        for a, b in zip(cuts[:-1], cuts[1:]):
+            eng.push(soa.slice(a, b))
+        eng.run()
+        many = eng.fetch(True)
+    assert_same(one, many, str(cuts))
+    exp, _ = oracle_lib.oracle_run(cfg, soa)
+    assert_same(one, exp, "oracle")
+
+
 def test_packed_record_out_of_limits_raises(engine_lib):
     from mgatk2_amd.engine import EngineConfig
     from mgatk2_amd.exceptions import InvalidInputError
