@@ -178,6 +178,12 @@ __device__ __forceinline__ void part_range(int64_t lo, int64_t hi, int p, int64_
     phi = lo + len * (p + 1) / kParts;
 }
 
+#ifndef MGP_HIST_U
+#define MGP_HIST_U 4  // reads per thread per histogram step
+#endif
+#ifndef MGP_HIST_BLOCK
+#define MGP_HIST_BLOCK 512
+#endif
 // One workgroup (8 waves) per (start bin, cell slice): bin bounds by binary
 // search in the sorted starts, coordinate-order check (pysam's fetch order,
 // readers.py:87-92), flag/barcode filters (readers.py:95-111) and the LDS
@@ -187,7 +193,7 @@ __device__ __forceinline__ void part_range(int64_t lo, int64_t hi, int p, int64_
 // after each part the per-64-cell-group totals are snapshotted, giving the
 // per-(bin, part, group) counts of pass A. Slice 0 writes the bin's bounds,
 // valid count and run checks.
-constexpr int kHistBlock = 512;
+constexpr int kHistBlock = MGP_HIST_BLOCK;
 __global__ void __launch_bounds__(kHistBlock) k_bin_count(const int32_t* __restrict__ start,
                                                           const int32_t* __restrict__ bc,
                                                           const uint16_t* __restrict__ flag,
@@ -225,7 +231,7 @@ __global__ void __launch_bounds__(kHistBlock) k_bin_count(const int32_t* __restr
         int64_t lo, hi;
         part_range(blo, bhi, part, lo, hi);
         // 4 reads per thread per step, loads issued together (clamped index, no branches)
-        constexpr int kU = 4;
+        constexpr int kU = MGP_HIST_U;
         for (int64_t i0 = lo + threadIdx.x; i0 < hi; i0 += kU * kHistBlock) {
             int cc[kU], ss[kU], sp0[kU];
             uint32_t sp[kU];
