@@ -1307,8 +1307,11 @@ __global__ void __launch_bounds__(kBlock, MGP_PILEUP_WAVES) k_pileup(
     uint32_t n_lo = c0 < c1 ? O[(size_t)lo_bin * nc + c0] : 0u;
     uint32_t n_own = c0 < c1 ? O[(size_t)own_bin * nc + c0] : 0u;
     uint32_t n_hi = c0 < c1 ? O[(size_t)hi_bin * nc + c0] : 0u;
+    // the tile starts zeroed; each flush zeroes what it read, so the next cell
+    // starts from zero behind the flush's barrier
+    for (int x = threadIdx.x; x < 5 * g.Wp; x += blockDim.x) tile[x] = 0;
+    __syncthreads();
     for (int c = c0; c < c1; ++c) {
-        for (int x = threadIdx.x; x < 5 * g.Wp; x += blockDim.x) tile[x] = 0;
         const uint32_t lo = n_lo, own = n_own, hi = n_hi;
         if (c + 1 < c1) {
             n_lo = O[(size_t)lo_bin * nc + c + 1];
@@ -1319,7 +1322,6 @@ __global__ void __launch_bounds__(kBlock, MGP_PILEUP_WAVES) k_pileup(
         // kept reads and their flags, counted once: by the window owning the start bin
         uint32_t nkeep = 0;
         unsigned long long fl = 0;
-        __syncthreads();
         for (uint32_t seg = lo; seg < hi; seg += kSeg) {
             const uint32_t seg_hi = min(hi, seg + kSeg);
             uint32_t qn = 0;  // wave-uniform queue fill
@@ -1397,10 +1399,12 @@ __global__ void __launch_bounds__(kBlock, MGP_PILEUP_WAVES) k_pileup(
 #pragma unroll
                     for (int x = 0; x < 4; ++x) {
                         const uint32_t pk = tile[x * g.Wp + p];
+                        tile[x * g.Wp + p] = 0u;
                         v[2 * x] = pk & 0xFFFFu;
                         v[2 * x + 1] = pk >> 16;
                     }
                     const uint32_t pk = t5[p];
+                    t5[p] = 0u;
                     tf = pk & 0xFFFFu;
                     tr = pk >> 16;
                 }
