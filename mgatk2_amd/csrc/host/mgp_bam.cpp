@@ -16,6 +16,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <memory>
 #include <fcntl.h>
 #include <string>
 #include <thread>
@@ -179,10 +180,39 @@ bool inflate_block(const uint8_t* blk, uint32_t csize, uint8_t* out, uint32_t is
 
 // A sequential reader over the inflated BGZF stream, inflating batches of
 // blocks in parallel.
+// Byte buffer that grows without zero-filling (std::vector value-initialises:
+// a memset of every inflated batch).
+struct ByteBuf {
+    std::unique_ptr<uint8_t[]> p;
+    size_t n = 0, cap = 0;
+    size_t size() const { return n; }
+    uint8_t* data() { return p.get(); }
+    const uint8_t* data() const { return p.get(); }
+    void clear() { n = 0; }
+    void resize(size_t m) {
+        if (m > cap) {
+            const size_t c = std::max(m, cap + cap / 2);
+            std::unique_ptr<uint8_t[]> q(new uint8_t[c]);
+            if (n) std::memcpy(q.get(), p.get(), n);
+            p = std::move(q);
+            cap = c;
+        }
+        n = m;
+    }
+    void drop_front(size_t k) {  // drop the first k bytes
+        if (k >= n) {
+            n = 0;
+            return;
+        }
+        std::memmove(p.get(), p.get() + k, n - k);
+        n -= k;
+    }
+};
+
 struct Stream {
     mgp_bam* bam;
     uint64_t coff;            // next compressed offset to read
-    std::vector<uint8_t> buf; // inflated bytes not consumed yet
+    ByteBuf buf;              // inflated bytes not consumed yet
     size_t pos = 0;
     bool eof = false;
     size_t batch_bytes = 64u << 10;  // grows x4 per refill up to kMaxBatch
@@ -203,8 +233,9 @@ struct Stream {
         const size_t want = (size_t)std::min<uint64_t>(batch_bytes, (uint64_t)bam->file_size - coff);
         batch_bytes = std::min(kMaxBatch, batch_bytes * 4);
         const double tr0 = now_s();
-        std::vector<uint8_t> raw(want);
-        const bool rd_ok = pread_all(bam->fd, raw.data(), want, coff);
+        std::unique_ptr<uint8_t[]> raw_buf(new uint8_t[want]);
+        uint8_t* const raw_p = raw_buf.get();
+        const bool rd_ok = pread_all(bam->fd, raw_p, want, coff);
         t_pread += now_s() - tr0;
         if (!rd_ok) {
             fail("read error in " + bam->path);
@@ -213,7 +244,7 @@ struct Stream {
         std::vector<Block> blocks;
         size_t p = 0, total = 0;
         while (p < want) {
-            const uint32_t bs = bgzf_block_size(raw.data() + p, want - p);
+            const uint32_t bs = bgzf_block_size(raw_p + p, want - p);
             if (bs == 0) {
                 if (blocks.empty()) {
                     fail("not a BGZF block at offset " + std::to_string(coff + p));
@@ -225,8 +256,8 @@ struct Stream {
             Block b;
             b.coff = p;
             b.csize = bs;
-            b.isize = rd32(raw.data() + p + bs - 4);
-            if (b.isize > 65536 || bs < 12u + rd16(raw.data() + p + 10) + 8u) {
+            b.isize = rd32(raw_p + p + bs - 4);
+            if (b.isize > 65536 || bs < 12u + rd16(raw_p + p + 10) + 8u) {
                 fail("corrupt BGZF block at offset " + std::to_string(coff + p));
                 return false;
             }
@@ -248,7 +279,7 @@ struct Stream {
         }
         // compact the consumed prefix, then inflate the batch into the tail
         if (pos) {
-            buf.erase(buf.begin(), buf.begin() + (ptrdiff_t)pos);
+            buf.drop_front(pos);
             pos = 0;
         }
         const size_t base = buf.size();
@@ -267,7 +298,7 @@ struct Stream {
                 const size_t i = next.fetch_add(1);
                 if (i >= blocks.size()) break;
                 const Block& b = blocks[i];
-                if (!inflate_block(raw.data() + b.coff, b.csize, buf.data() + base + b.out_off, b.isize, &zs)) {
+                if (!inflate_block(raw_p + b.coff, b.csize, buf.data() + base + b.out_off, b.isize, &zs)) {
                     ok = false;
                     break;
                 }
