@@ -1134,28 +1134,31 @@ __device__ __forceinline__ void pile_bases(bool act, int a0, int b0, int a1, int
             const uint32_t ok = decode(qq, plane);
             if (ok) atomicAdd(&lb[plane * (uint32_t)kTilePitch + qq], inc);
         }
-    } else if (one_block) {
-        uint32_t* lb = base + dl0;
-        const unsigned long long smask = range_mask(wq_lo, wq_hi);
-#pragma unroll
-        for (int qq = 0; qq < kLen; ++qq) {
-            if (!((smask >> qq) & 1ull)) continue;
-            uint32_t plane;
-            const uint32_t ok = decode(qq, plane) & (uint32_t)(qq >= a0) & (uint32_t)(qq < b0);
-            if (ok) atomicAdd(&lb[plane * (uint32_t)kTilePitch + qq], inc);
-        }
     } else {
+        // the lane's counted query positions as a 64-bit mask: one bit test per base
+        const unsigned long long vm = range_mask(a0, b0) | range_mask(a1, b1);
+        const uint32_t vlo = (uint32_t)vm, vhi = (uint32_t)(vm >> 32);
+        auto counted = [&](int qq) -> uint32_t { return ((qq < 32 ? vlo : vhi) >> (qq & 31)) & 1u; };
         const unsigned long long smask = range_mask(wq_lo, wq_hi);
+        if (one_block) {
+            uint32_t* lb = base + dl0;
 #pragma unroll
-        for (int qq = 0; qq < kLen; ++qq) {
-            if (!((smask >> qq) & 1ull)) continue;
-            // branch-free predicate: one exec mask per base, a single branch around the atomic
-            const bool second = qq >= qs1;
-            const int d = second ? dl1 : dl0;
-            const int lo = second ? a1 : a0, hi = second ? b1 : b0;
-            uint32_t plane;
-            const uint32_t ok = decode(qq, plane) & (uint32_t)(qq >= lo) & (uint32_t)(qq < hi);
-            if (ok) atomicAdd(&base[plane * (uint32_t)kTilePitch + qq + d], inc);
+            for (int qq = 0; qq < kLen; ++qq) {
+                if (!((smask >> qq) & 1ull)) continue;
+                uint32_t plane;
+                const uint32_t ok = decode(qq, plane) & counted(qq);
+                if (ok) atomicAdd(&lb[plane * (uint32_t)kTilePitch + qq], inc);
+            }
+        } else {
+#pragma unroll
+            for (int qq = 0; qq < kLen; ++qq) {
+                if (!((smask >> qq) & 1ull)) continue;
+                // a block's reference offset: the second block starts at qs1
+                const int d = qq >= qs1 ? dl1 : dl0;
+                uint32_t plane;
+                const uint32_t ok = decode(qq, plane) & counted(qq);
+                if (ok) atomicAdd(&base[plane * (uint32_t)kTilePitch + qq + d], inc);
+            }
         }
     }
 }
