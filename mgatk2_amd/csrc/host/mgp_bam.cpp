@@ -17,6 +17,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <memory>
+#include <new>
 #include <fcntl.h>
 #include <string>
 #include <thread>
@@ -189,15 +190,19 @@ struct ByteBuf {
     uint8_t* data() { return p.get(); }
     const uint8_t* data() const { return p.get(); }
     void clear() { n = 0; }
-    void resize(size_t m) {
+    // false (buffer unchanged) when host memory runs out: no exception may cross
+    // the extern "C" entry points
+    bool resize(size_t m) {
         if (m > cap) {
             const size_t c = std::max(m, cap + cap / 2);
-            std::unique_ptr<uint8_t[]> q(new uint8_t[c]);
+            std::unique_ptr<uint8_t[]> q(new (std::nothrow) uint8_t[c]);
+            if (!q) return false;
             if (n) std::memcpy(q.get(), p.get(), n);
             p = std::move(q);
             cap = c;
         }
         n = m;
+        return true;
     }
     void drop_front(size_t k) {  // drop the first k bytes
         if (k >= n) {
@@ -233,7 +238,11 @@ struct Stream {
         const size_t want = (size_t)std::min<uint64_t>(batch_bytes, (uint64_t)bam->file_size - coff);
         batch_bytes = std::min(kMaxBatch, batch_bytes * 4);
         const double tr0 = now_s();
-        std::unique_ptr<uint8_t[]> raw_buf(new uint8_t[want]);
+        std::unique_ptr<uint8_t[]> raw_buf(new (std::nothrow) uint8_t[want]);
+        if (!raw_buf) {
+            fail("out of host memory");
+            return false;
+        }
         uint8_t* const raw_p = raw_buf.get();
         const bool rd_ok = pread_all(bam->fd, raw_p, want, coff);
         t_pread += now_s() - tr0;
@@ -283,7 +292,10 @@ struct Stream {
             pos = 0;
         }
         const size_t base = buf.size();
-        buf.resize(base + total);
+        if (!buf.resize(base + total)) {
+            fail("out of host memory");
+            return false;
+        }
         std::atomic<size_t> next{0};
         std::atomic<bool> ok{true};
         const int nt = std::max(1, std::min<int>(bam->n_threads, (int)blocks.size()));

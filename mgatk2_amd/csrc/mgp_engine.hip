@@ -1119,7 +1119,11 @@ __device__ __forceinline__ void pile_bases(bool act, int a0, int b0, int a1, int
     const int ua0 = __builtin_amdgcn_readfirstlane(a0), ub0 = __builtin_amdgcn_readfirstlane(b0);
     const bool uniform = one_block && __ballot(!(act && a0 == ua0 && b0 == ub0)) == 0ull;
     // iterations run: a wave-uniform 64-bit mask (one scalar bit test per base)
+    // (bounds clamped into [0, 64] before any shift: a block right of the window
+    // has a negative hi, and a shift by a negative amount is undefined)
     auto range_mask = [](int lo, int hi) -> unsigned long long {
+        lo = min(max(lo, 0), 64);
+        hi = min(max(hi, 0), 64);
         const unsigned long long h = hi >= 64 ? ~0ull : ((1ull << hi) - 1ull);
         const unsigned long long l = lo >= 64 ? ~0ull : ((1ull << lo) - 1ull);
         return lo < hi ? (h & ~l) : 0ull;
