@@ -408,6 +408,9 @@ constexpr uint64_t kRecStride = MGP_PACK_BYTES;  // record stride of a dense pac
 #ifndef MGP_GA_WAVES
 #define MGP_GA_WAVES 1
 #endif
+#ifndef MGP_ABL_A
+#define MGP_ABL_A 0  // pass-A ablations (experiments only): 1 no element stores, 2 no ranking (slot = read index)
+#endif
 template <bool kDense>
 __global__ void __launch_bounds__(kBlock, MGP_GA_WAVES) k_group_a(int64_t n, const int32_t* __restrict__ start,
                                                     const int32_t* __restrict__ bc, const int32_t* __restrict__ tlen,
@@ -522,6 +525,10 @@ __global__ void __launch_bounds__(kBlock, MGP_GA_WAVES) k_group_a(int64_t n, con
             rk[u] = (uint32_t)__shfl((int)bef, leader, kWave) + (uint32_t)__popcll(pm & lt);
             __builtin_amdgcn_wave_barrier();
         }
+        if (MGP_ABL_A == 2) {  // ablation: no ranking, every element at its read index
+#pragma unroll
+            for (int u = 0; u < kAhead; ++u) rk[u] = 0;
+        }
         __syncthreads();
         for (int gi = threadIdx.x; gi < ngroups; gi += kBlock) {
             uint32_t run = gcnt[gi];
@@ -538,7 +545,9 @@ __global__ void __launch_bounds__(kBlock, MGP_GA_WAVES) k_group_a(int64_t n, con
 #pragma unroll
         for (int u = 0; u < kAhead; ++u) {
             if (!valid[u]) continue;
-            const uint32_t dest = my[P.c[u] >> 6] + rk[u];
+            const uint32_t dest = MGP_ABL_A == 2 ? (uint32_t)(base0 + wid * (kAhead * kWave) + u * kWave + lane)
+                                                 : my[P.c[u] >> 6] + rk[u];
+            if (MGP_ABL_A == 1 && dest != 0xFFFFFFFFu) continue;  // ablation: no stores
             const uint16_t f = (uint16_t)P.f[u];
             const int t = P.t[u];
             GElem e;
@@ -2000,6 +2009,7 @@ int mgp_run(mgp_ctx* ctx) {
         }
         STAGE_END(ST_GROUP_A);
         STAGE_BEGIN(ST_GROUP_B);
+        if (MGP_ABL_A == 1) HIP_TRY(hipMemsetAsync(ctx->gel2.p, 0, (size_t)n * sizeof(GElem), s));  // ablation
         if (MGP_ABL_B >= 2) HIP_TRY(hipMemsetAsync(ctx->pel.p, 0, (size_t)n * 8, s));  // ablation: nothing piles
         if (n > 0) {
             // about MGP_GB_WG workgroups (many per slot: 4 fit a CU, so a grid of a few
