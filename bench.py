@@ -47,8 +47,10 @@ def parse():
     ap.add_argument("--cpu-sample-reads", type=int, default=20_000_000)
     ap.add_argument("--cpu-sample-cells", type=int, default=1000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--record-layout", choices=["packed", "full"], default="packed",
-                    help="payload records: packed 64-byte (default; every C4 read fits) or full 128-byte")
+    ap.add_argument("--record-layout", choices=["paired", "packed", "full"], default="paired",
+                    help="payload records: packed 64-byte records, two consecutive records of a cell per "
+                         "128-byte line (paired, default: the placement of mgp_place_records), packed in BAM "
+                         "order, or full 128-byte records")
     ap.add_argument("--check", action="store_true", help="bit-exact check of a sample against the oracle")
     return ap.parse_args()
 
@@ -97,8 +99,20 @@ def main():
     eng = Engine(cfg, device=local_rank if os.environ.get("MGP_BENCH_NO_COMM") != "1" else 0)
     t0 = time.time()
     cdf, ref = cell_cdf(seed, n_cells), ref_codes(args.seed)  # one chrM reference for every rank
-    packed = args.record_layout == "packed"
+    packed = args.record_layout in ("packed", "paired")
     eng.synth(seed, n_reads, cdf, ref, read_len=args.read_len, rec_align=64 if packed else 128, pack=packed)
+    if args.record_layout == "paired":
+        # the producer's placement (mgp_place_records, as the BAM decoder emits it):
+        # computed on the host from the generated barcode and flag columns, then the
+        # same reads are generated again at those offsets
+        from mgatk2_amd.bam import PLACE_PAIRED, place_records
+
+        soa = eng.download_inputs(columns=("bc", "flag"))
+        roff, pay_b = place_records(soa.bc, soa.flag, np.full(n_reads, 64, np.uint32), n_cells, PLACE_PAIRED)
+        del soa
+        eng.synth(seed, n_reads, cdf, ref, read_len=args.read_len, rec_align=64, pack=True, rec_off=roff,
+                  payload_bytes=pay_b)
+        del roff
     n_res, pay = eng.resident()
     t_gen = time.time() - t0
     if rank == 0:

@@ -152,6 +152,16 @@ static inline MGP_HD uint32_t mgp_cigar_offset(uint32_t l_seq) {
     return mgp_seq_offset(l_seq) + (b > 32u ? b : 32u);
 }
 
+/* Bytes of the record at rec (flag = its flag word): 64 for a packed record,
+ * cigar_off + 4 * n_cigar for a full one (before any alignment padding). */
+static inline MGP_HD uint32_t mgp_record_bytes(const uint8_t *rec, uint16_t flag) {
+    uint32_t l_seq, n_cigar;
+    if (flag & MGP_FLAG_PACKED) return MGP_PACK_BYTES;
+    l_seq = (uint32_t)rec[4] | ((uint32_t)rec[5] << 8) | ((uint32_t)rec[6] << 16) | ((uint32_t)rec[7] << 24);
+    n_cigar = (uint32_t)rec[8] | ((uint32_t)rec[9] << 8);
+    return mgp_cigar_offset(l_seq) + 4u * n_cigar;
+}
+
 /* Expand a packed record into the full layout in full[0..128) (a non-ACGT base,
  * byte >= 252, becomes code 15 = N with quality 0; the header flag word holds
  * only MGP_FLAG_REVERSE). */
@@ -271,6 +281,11 @@ typedef struct mgp_synth_params {
     const uint8_t  *ref_codes;  /* host array [mito_len]: reference bases as BAM 4-bit codes */
     int32_t  rec_align;         /* record placement: offsets are multiples of this (16..4096, pow2) */
     int32_t  pack;              /* 1: reads that fit get the packed 64-byte layout (MGP_FLAG_PACKED) */
+    /* optional placement (host arrays, NULL = dense in BAM order at rec_align):
+     * record i is written at rec_off[i] of a payload_bytes payload, e.g. the
+     * producer placement of mgp_place_records (include/mgpileup_host.h) */
+    const uint64_t *rec_off;
+    int64_t  payload_bytes;
 } mgp_synth_params;
 
 typedef struct mgp_ctx mgp_ctx;

@@ -68,6 +68,10 @@ int  mgp_bam_set_bulk(mgp_bam *bam, int32_t cell);
  * query_sequence/query_qualities (the SimpleRead API) leave it off (default). */
 int  mgp_bam_set_pack(mgp_bam *bam, int pack);
 
+/* Payload placement of mgp_bam_read_ref (MGP_PLACE_DENSE default, or
+ * MGP_PLACE_PAIRED: see mgp_place_records below). */
+int  mgp_bam_set_placement(mgp_bam *bam, int mode);
+
 /* Decode every record of reference `tid` (fetch(contig) order) into `out`.
  * Records are placed at multiples of `rec_align` bytes (16..4096, power of 2). */
 int  mgp_bam_read_ref(mgp_bam *bam, int tid, int rec_align, mgp_bam_batch *out);
@@ -117,17 +121,33 @@ int mgp_bam_write(const char *path, const char *const *ref_names, const int64_t 
 int64_t mgp_deflate_tiles(const void *data, int64_t rows, int64_t cols, int32_t elem_size, int64_t crow,
                           int64_t ccol, int level, int n_threads, uint8_t **blob, int64_t *offsets);
 
+/* Payload placement for producers: rec_off[i] for records of rec_bytes[i]
+ * bytes, in BAM order. MGP_PLACE_DENSE: consecutive, each rounded up to
+ * rec_align. MGP_PLACE_PAIRED: two consecutive packed (64-byte) records of one
+ * cell share a 128-byte line (one streaming pass, lines opened in BAM order;
+ * reads the engine's filters drop pair among themselves; full records take
+ * 128-byte aligned slots of their own), so one line request of the pileup's
+ * gather serves two reads of the cell it piles. Returns the payload bytes, -1
+ * on error. Replaces no reference code (pysam hands out Python objects). */
+#define MGP_PLACE_DENSE  0
+#define MGP_PLACE_PAIRED 1
+int64_t mgp_place_records(int64_t n, const int32_t *bc, const uint16_t *flag, const uint32_t *rec_bytes,
+                          int32_t n_cells, int32_t mode, int32_t rec_align, uint64_t *rec_off);
+
 /* Cell sharding: gather the payload records idx[0..m) of a
- * batch into a new, dense payload for one device. mgp_gather_offsets writes the
- * new offset of each record (sizes rounded up to rec_align) and returns the
- * total bytes (-1 on error); mgp_gather_records copies the records there on
- * n_threads threads, zero-filling the alignment gaps. Replaces no reference
- * code: the reference runs on one process. */
-int64_t mgp_gather_offsets(const uint64_t *rec_off, int64_t n_total, int64_t payload_bytes, const int64_t *idx,
-                           int64_t m, int32_t rec_align, uint64_t *out_off);
-int mgp_gather_records(const uint8_t *payload, const uint64_t *rec_off, int64_t n_total, int64_t payload_bytes,
-                       const int64_t *idx, int64_t m, const uint64_t *out_off, int64_t out_bytes, uint8_t *out,
-                       int n_threads);
+ * batch into a new payload for one device. mgp_gather_offsets reads each
+ * record's size from its header (mgp_record_bytes; any source placement),
+ * rebases the cell ids to [cell_lo, cell_lo + n_cells) (-1 outside), places the
+ * subset with mgp_place_records(mode, rec_align) and returns the new payload
+ * bytes (-1 on error). mgp_gather_records copies the records there on
+ * n_threads threads; `out` must be zero-filled by the caller (gaps stay as they
+ * are). Replaces no reference code: the reference runs on one process. */
+int64_t mgp_gather_offsets(const uint8_t *payload, const uint64_t *rec_off, const uint16_t *flag, const int32_t *bc,
+                           int64_t n_total, int64_t payload_bytes, const int64_t *idx, int64_t m, int32_t cell_lo,
+                           int32_t n_cells, int32_t mode, int32_t rec_align, uint64_t *out_off);
+int mgp_gather_records(const uint8_t *payload, const uint64_t *rec_off, const uint16_t *flag, int64_t n_total,
+                       int64_t payload_bytes, const int64_t *idx, int64_t m, const uint64_t *out_off,
+                       int64_t out_bytes, uint8_t *out, int n_threads);
 
 #ifdef __cplusplus
 }

@@ -79,6 +79,7 @@ def host_library() -> C.CDLL:
         lib.mgp_bam_set_barcodes.argtypes = [vp, C.c_char_p, C.POINTER(C.c_char_p), C.c_int]
         lib.mgp_bam_set_bulk.argtypes = [vp, C.c_int32]
         lib.mgp_bam_set_pack.argtypes = [vp, C.c_int]
+        lib.mgp_bam_set_placement.argtypes = [vp, C.c_int]
         lib.mgp_bam_read_ref.argtypes = [vp, C.c_int, C.c_int, C.POINTER(mgp_bam_batch)]
         lib.mgp_bam_free_batch.argtypes = [C.POINTER(mgp_bam_batch)]
         lib.mgp_bam_free_batch.restype = None
@@ -92,9 +93,13 @@ def host_library() -> C.CDLL:
         lib.mgp_deflate_tiles.argtypes = [vp, C.c_int64, C.c_int64, C.c_int32, C.c_int64, C.c_int64, C.c_int, C.c_int,
                                           C.POINTER(C.POINTER(C.c_uint8)), vp]
         lib.mgp_deflate_tiles.restype = C.c_int64
-        lib.mgp_gather_offsets.argtypes = [vp, C.c_int64, C.c_int64, vp, C.c_int64, C.c_int32, vp]
+        lib.mgp_place_records.argtypes = [C.c_int64, vp, vp, vp, C.c_int32, C.c_int32, C.c_int32, vp]
+        lib.mgp_place_records.restype = C.c_int64
+        lib.mgp_gather_offsets.argtypes = [vp, vp, vp, vp, C.c_int64, C.c_int64, vp, C.c_int64, C.c_int32, C.c_int32,
+                                           C.c_int32, C.c_int32, vp]
         lib.mgp_gather_offsets.restype = C.c_int64
-        lib.mgp_gather_records.argtypes = [vp, vp, C.c_int64, C.c_int64, vp, C.c_int64, vp, C.c_int64, vp, C.c_int]
+        lib.mgp_gather_records.argtypes = [vp, vp, vp, C.c_int64, C.c_int64, vp, C.c_int64, vp, C.c_int64, vp,
+                                           C.c_int]
         lib.mgp_gather_records.restype = C.c_int
         lib.mgp_bam_write.argtypes = [C.c_char_p, C.POINTER(C.c_char_p), C.POINTER(C.c_int64), C.c_int, C.c_int,
                                       C.POINTER(mgp_bam_batch), C.POINTER(C.c_char_p), C.c_int, C.c_char_p,
@@ -107,6 +112,29 @@ def host_library() -> C.CDLL:
 
 def _err() -> str:
     return (host_library().mgp_host_last_error() or b"").decode(errors="replace")
+
+
+PLACE_DENSE, PLACE_PAIRED = 0, 1  # include/mgpileup_host.h MGP_PLACE_*
+
+
+def place_records(bc: np.ndarray, flag: np.ndarray, rec_bytes: np.ndarray, n_cells: int,
+                  mode: int = PLACE_PAIRED, rec_align: int = 64) -> tuple[np.ndarray, int]:
+    """Producer placement of payload records (mgp_place_records): returns
+    (rec_off, payload_bytes). PLACE_PAIRED puts two consecutive packed records of
+    one cell into one 128-byte line."""
+    lib = host_library()
+    n = int(bc.shape[0])
+    bc = np.ascontiguousarray(bc, np.int32)
+    flag = np.ascontiguousarray(flag, np.uint16)
+    rb = np.ascontiguousarray(rec_bytes, np.uint32)
+    if flag.shape[0] != n or rb.shape[0] != n:
+        raise ValueError("bc, flag and rec_bytes must have the same length")
+    off = np.empty(n, np.uint64)
+    tot = lib.mgp_place_records(n, bc.ctypes.data, flag.ctypes.data, rb.ctypes.data, int(n_cells), int(mode),
+                                int(rec_align), off.ctypes.data)
+    if tot < 0:
+        raise ValueError(_err())
+    return off, int(tot)
 
 
 class _BatchOwner:
@@ -159,18 +187,24 @@ class BamFile:
         return self.references.index(contig)
 
     def read_soa(self, contig: str, barcodes: list[str], tag: str = "CB", rec_align: int = 64,
-                 bulk_cell: int = -1, pack: bool = True) -> ReadSoA:
+                 bulk_cell: int = -1, pack: bool = True, paired: bool | None = None) -> ReadSoA:
         """Every record of `contig` (fetch order) as an engine batch; bc = whitelist
         index (last duplicate wins, like the reference's dict) or -1. With
         ``bulk_cell >= 0`` every record goes to that cell (bulk calling). pack:
         reads that fit get the packed 64-byte record (include/mgpileup.h), which
-        drops the code and quality of non-ACGT bases (off to rebuild SimpleReads)."""
+        drops the code and quality of non-ACGT bases (off to rebuild SimpleReads).
+        paired (default: = pack): two consecutive packed records of a cell share a
+        128-byte line (mgp_place_records), so the pileup's gather fetches half the
+        lines; the records are then not in BAM order in the payload."""
+        paired = pack if paired is None else paired
         arr = (C.c_char_p * max(1, len(barcodes)))(*[b.encode() for b in barcodes])
         if self.lib.mgp_bam_set_barcodes(self._h, tag.encode(), arr, len(barcodes)) != 0:
             raise ProcessingError(_err())
         if bulk_cell >= 0 and self.lib.mgp_bam_set_bulk(self._h, int(bulk_cell)) != 0:
             raise ProcessingError(_err())
         if self.lib.mgp_bam_set_pack(self._h, int(bool(pack))) != 0:
+            raise ProcessingError(_err())
+        if self.lib.mgp_bam_set_placement(self._h, PLACE_PAIRED if paired else PLACE_DENSE) != 0:
             raise ProcessingError(_err())
         b = mgp_bam_batch()
         if self.lib.mgp_bam_read_ref(self._h, self.tid(contig), int(rec_align), C.byref(b)) != 0:

@@ -130,6 +130,7 @@ struct mgp_bam {
     char tag[2] = {'C', 'B'};
     int32_t bulk_cell = -1;  // >= 0: every record goes to this cell (bulk calling)
     bool pack = false;       // write the packed record layout where a read fits
+    int placement = MGP_PLACE_DENSE;  // payload placement (mgp_place_records)
 };
 
 namespace {
@@ -662,6 +663,13 @@ int mgp_bam_set_bulk(mgp_bam* b, int32_t cell) {
     return 0;
 }
 
+int mgp_bam_set_placement(mgp_bam* b, int mode) {
+    if (!b) return fail("null argument");
+    if (mode != MGP_PLACE_DENSE && mode != MGP_PLACE_PAIRED) return fail("unknown placement");
+    b->placement = mode;
+    return 0;
+}
+
 int mgp_bam_set_pack(mgp_bam* b, int pack) {
     if (!b) return fail("null argument");
     b->pack = pack != 0;
@@ -857,6 +865,56 @@ int mgp_bam_read_ref(mgp_bam* b, int tid, int rec_align, mgp_bam_batch* out) {
     if (rc != 0) {
         release();
         return -1;
+    }
+    // producer placement (mgp_place_records): the records decoded in BAM order are
+    // moved to their places, a parallel copy into a zero-filled (calloc) payload
+    if (b->placement == MGP_PLACE_PAIRED && G_start.n) {
+        const double tpl = now_s();
+        const size_t n = G_start.n;
+        std::vector<uint32_t> sz;
+        Grow<uint64_t> nro;
+        if (!nro.reserve(n)) {
+            release();
+            return fail("out of host memory");
+        }
+        int32_t maxbc = -1;
+        try {
+            sz.resize(n);
+        } catch (const std::bad_alloc&) {
+            std::free(nro.p);
+            release();
+            return fail("out of host memory");
+        }
+        for (size_t i = 0; i < n; ++i) {
+            sz[i] = mgp_record_bytes(G_pay.p + G_roff.p[i], G_flag.p[i]);
+            maxbc = std::max(maxbc, G_bc.p[i]);
+        }
+        const int64_t tot = mgp_place_records((int64_t)n, G_bc.p, G_flag.p, sz.data(), maxbc + 1, MGP_PLACE_PAIRED,
+                                              rec_align, nro.p);
+        uint8_t* np = tot >= 0 ? (uint8_t*)std::calloc((size_t)tot + 256, 1) : nullptr;
+        if (!np) {
+            std::free(nro.p);
+            release();
+            return fail(tot < 0 ? "record placement failed" : "out of host memory");
+        }
+        const int tn = (int)std::max<size_t>(1, std::min<size_t>((size_t)nt, n / 65536 + 1));
+        auto work = [&](int t) {
+            const size_t lo = n * (size_t)t / (size_t)tn, hi = n * (size_t)(t + 1) / (size_t)tn;
+            for (size_t i = lo; i < hi; ++i) std::memcpy(np + nro.p[i], G_pay.p + G_roff.p[i], sz[i]);
+        };
+        std::vector<std::thread> th;
+        for (int t = 1; t < tn; ++t) th.emplace_back(work, t);
+        work(0);
+        for (auto& x : th) x.join();
+        std::free(G_pay.p);
+        std::free(G_roff.p);
+        G_pay.p = np;
+        G_pay.n = (size_t)tot;
+        G_pay.cap = (size_t)tot + 256;
+        G_roff.p = nro.p;
+        G_roff.cap = nro.cap;
+        if (std::getenv("MGP_HOST_PROFILE"))
+            std::fprintf(stderr, "[mgp_bam_read_ref] paired placement %.3f s\n", now_s() - tpl);
     }
     // at least one element everywhere; >= 256 bytes of payload slack for vector over-reads
     if (!G_start.reserve(1) || !G_bc.reserve(1) || !G_tlen.reserve(1) || !G_flag.reserve(1) ||

@@ -3,8 +3,10 @@
 // Cells are split over devices in contiguous whitelist ranges;
 // each device's batch holds the records of its cells in BAM order. The SoA
 // columns are gathered by index in numpy; the payload records are gathered here:
-// sizes and the new offsets in one pass, then a parallel copy. (A numpy byte
-// gather needs an 8-byte index per payload byte: 205 GB for the 25.6 GB C4 payload.)
+// sizes from the record headers (any source placement), the producer placement
+// of the subset (mgp_place_records, mgp_place.cpp), then a parallel copy. (A
+// numpy byte gather needs an 8-byte index per payload byte: 205 GB for the
+// 25.6 GB C4 payload.)
 #include <algorithm>
 #include <cstdint>
 #include <cstring>
@@ -12,57 +14,77 @@
 #include <thread>
 #include <vector>
 
+#include "../../../include/mgpileup.h"
 #include "../../../include/mgpileup_host.h"
 
 std::string& mgp_host_err();  // mgp_bam.cpp
 
 extern "C" {
 
-int64_t mgp_gather_offsets(const uint64_t* rec_off, int64_t n_total, int64_t payload_bytes, const int64_t* idx,
-                           int64_t m, int32_t rec_align, uint64_t* out_off) {
+int64_t mgp_gather_offsets(const uint8_t* payload, const uint64_t* rec_off, const uint16_t* flag, const int32_t* bc,
+                           int64_t n_total, int64_t payload_bytes, const int64_t* idx, int64_t m, int32_t cell_lo,
+                           int32_t n_cells, int32_t mode, int32_t rec_align, uint64_t* out_off) {
     mgp_host_err().clear();
-    if ((n_total && !rec_off) || (m && (!idx || !out_off)) || m < 0 || n_total < 0 || rec_align < 16 ||
-        (rec_align & (rec_align - 1))) {
+    if ((n_total && (!payload || !rec_off || !flag || !bc)) || (m && (!idx || !out_off)) || m < 0 || n_total < 0 ||
+        n_cells < 0) {
         mgp_host_err() = "mgp_gather_offsets: bad arguments";
         return -1;
     }
-    const uint64_t amask = (uint64_t)rec_align - 1;
-    uint64_t off = 0;
+    // the records' sizes from their headers (any source placement), the shard's
+    // cell ids rebased to cell_lo, then the producer placement of the subset
+    std::vector<int32_t> lbc((size_t)m);
+    std::vector<uint16_t> lfl((size_t)m);
+    std::vector<uint32_t> sz((size_t)m);
     for (int64_t k = 0; k < m; ++k) {
         const int64_t i = idx[k];
         if (i < 0 || i >= n_total) {
             mgp_host_err() = "mgp_gather_offsets: index out of range";
             return -1;
         }
-        const uint64_t end = i + 1 < n_total ? rec_off[i + 1] : (uint64_t)payload_bytes;
-        if (end < rec_off[i] || end > (uint64_t)payload_bytes) {
-            mgp_host_err() = "mgp_gather_offsets: record offsets not increasing";
+        const uint64_t o = rec_off[i];
+        if (o + 16 > (uint64_t)payload_bytes) {
+            mgp_host_err() = "mgp_gather_offsets: record outside the payload";
             return -1;
         }
-        out_off[k] = off;
-        off += (end - rec_off[i] + amask) & ~amask;
+        const uint32_t b = mgp_record_bytes(payload + o, flag[i]);
+        if (o + b > (uint64_t)payload_bytes) {
+            mgp_host_err() = "mgp_gather_offsets: record outside the payload";
+            return -1;
+        }
+        sz[(size_t)k] = b;
+        lfl[(size_t)k] = flag[i];
+        const int64_t c = (int64_t)bc[i] - cell_lo;
+        lbc[(size_t)k] = (bc[i] >= 0 && c >= 0 && c < n_cells) ? (int32_t)c : -1;
     }
-    return (int64_t)off;
+    return mgp_place_records(m, lbc.data(), lfl.data(), sz.data(), n_cells, mode, rec_align, out_off);
 }
 
-int mgp_gather_records(const uint8_t* payload, const uint64_t* rec_off, int64_t n_total, int64_t payload_bytes,
-                       const int64_t* idx, int64_t m, const uint64_t* out_off, int64_t out_bytes, uint8_t* out,
-                       int n_threads) {
+int mgp_gather_records(const uint8_t* payload, const uint64_t* rec_off, const uint16_t* flag, int64_t n_total,
+                       int64_t payload_bytes, const int64_t* idx, int64_t m, const uint64_t* out_off,
+                       int64_t out_bytes, uint8_t* out, int n_threads) {
     mgp_host_err().clear();
-    if (m < 0 || (m && (!payload || !rec_off || !idx || !out_off || !out))) {
+    if (m < 0 || (m && (!payload || !rec_off || !flag || !idx || !out_off || !out))) {
         mgp_host_err() = "mgp_gather_records: bad arguments";
         return -1;
+    }
+    for (int64_t k = 0; k < m; ++k) {  // every source and destination inside its buffer
+        const int64_t i = idx[k];
+        if (i < 0 || i >= n_total || rec_off[i] + 16 > (uint64_t)payload_bytes) {
+            mgp_host_err() = "mgp_gather_records: record outside the payload";
+            return -1;
+        }
+        const uint32_t b = mgp_record_bytes(payload + rec_off[i], flag[i]);
+        if (rec_off[i] + b > (uint64_t)payload_bytes || out_off[k] + b > (uint64_t)out_bytes) {
+            mgp_host_err() = "mgp_gather_records: record outside the payload";
+            return -1;
+        }
     }
     const int nt = (int)std::max<int64_t>(1, std::min<int64_t>(std::max(n_threads, 1), m / 65536 + 1));
     auto work = [&](int t) {
         const int64_t lo = m * t / nt, hi = m * (t + 1) / nt;
         for (int64_t k = lo; k < hi; ++k) {
             const int64_t i = idx[k];
-            const uint64_t end = i + 1 < n_total ? rec_off[i + 1] : (uint64_t)payload_bytes;
-            const uint64_t next = k + 1 < m ? out_off[k + 1] : (uint64_t)out_bytes;
-            const uint64_t len = end - rec_off[i];
-            std::memcpy(out + out_off[k], payload + rec_off[i], len);
-            if (next > out_off[k] + len) std::memset(out + out_off[k] + len, 0, next - out_off[k] - len);
+            std::memcpy(out + out_off[k], payload + rec_off[i], mgp_record_bytes(payload + rec_off[i], flag[i]));
         }
     };
     std::vector<std::thread> th;

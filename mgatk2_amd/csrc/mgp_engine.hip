@@ -122,8 +122,9 @@ struct mgp_ctx {
     // resident inputs (BAM order)
     int64_t n = 0, pay = 0;
     DevBuf start, bc, tlen, flag, mapq, span, roff, payload;
-    DevBuf roff_irregular;  // u32: 0 while rec_off[i] == kRecStride * i for every resident read
-    int dense = -1;         // host copy of !roff_irregular: -1 not read since the last push
+    DevBuf roff32;          // u32 rec_off >> 6 (grouping pass A reads it when every offset fits, kOffR32)
+    DevBuf roff_irregular;  // u32 bits: 1 some rec_off[i] != kRecStride * i, 2 some offset not in roff32's range
+    int roff_mode = -1;     // pass A's offset source (kOffDense / kOffR32 / kOffR64); -1 not read since the last push
 
     // run scratch
     DevBuf bin_start, H, P, cell_cnt, cell_base, bin_valid, bin_base, bucket_off, gel2, PG, F;
@@ -171,7 +172,10 @@ constexpr int kGroup = 64;  // cells per grouping bucket (pass A) and per pass-B
 // Start bins are split into kParts parts (equal read-index ranges) so that
 // grouping pass A runs on kParts x nbins workgroups: a grid of ~2 slot-rounds
 // (4 workgroups per CU) would leave a long tail.
-constexpr int kParts = 4;
+#ifndef MGP_PARTS
+#define MGP_PARTS 4
+#endif
+constexpr int kParts = MGP_PARTS;
 __device__ __forceinline__ void part_range(int64_t lo, int64_t hi, int p, int64_t& plo, int64_t& phi) {
     const int64_t len = hi - lo;
     plo = lo + len * p / kParts;
@@ -401,6 +405,11 @@ constexpr unsigned long long GM_REV = 1ull << 56, GM_PAIRED = 2ull << 56, GM_MAP
 // the passes (record offsets stay below 2^50).
 constexpr unsigned long long GM_LCELL_SHIFT = 50, GM_LCELL = 63ull << GM_LCELL_SHIFT;
 constexpr uint64_t kRecStride = MGP_PACK_BYTES;  // record stride of a dense packed payload (k_check_stride)
+// where grouping pass A takes the record offsets from (k_check_stride at ingest):
+//   kOffDense  every offset is kRecStride x the read index: computed, nothing read
+//   kOffR32    every offset is a multiple of 64 below 2^38: the u32 column roff32 = rec_off >> 6
+//   kOffR64    otherwise: the u64 rec_off column
+enum { kOffDense = 0, kOffR32 = 1, kOffR64 = 2 };
 
 #ifndef MGP_GA_AHEAD
 #define MGP_GA_AHEAD 8  // reads per lane per pass-A step (A/B: 2, 3, 4, 6 slower)
@@ -411,11 +420,16 @@ constexpr uint64_t kRecStride = MGP_PACK_BYTES;  // record stride of a dense pac
 #ifndef MGP_ABL_A
 #define MGP_ABL_A 0  // pass-A ablations (experiments only): 1 no element stores, 2 no ranking (slot = read index)
 #endif
-template <bool kDense>
-__global__ void __launch_bounds__(kBlock, MGP_GA_WAVES) k_group_a(int64_t n, const int32_t* __restrict__ start,
+#ifndef MGP_GA_BLOCK
+#define MGP_GA_BLOCK 256  // threads per pass-A workgroup
+#endif
+constexpr int kGABlock = MGP_GA_BLOCK;
+template <int kOff>
+__global__ void __launch_bounds__(kGABlock, MGP_GA_WAVES) k_group_a(int64_t n, const int32_t* __restrict__ start,
                                                     const int32_t* __restrict__ bc, const int32_t* __restrict__ tlen,
                                                     const uint16_t* __restrict__ flag, const uint8_t* __restrict__ mapq,
                                                     const uint64_t* __restrict__ roff,
+                                                    const uint32_t* __restrict__ roff32,
                                                     const uint32_t* __restrict__ bin_lo,
                                                     const uint32_t* __restrict__ PG, const uint32_t* __restrict__ F,
                                                     const uint32_t* __restrict__ binbase,
@@ -471,14 +485,14 @@ __global__ void __launch_bounds__(kBlock, MGP_GA_WAVES) k_group_a(int64_t n, con
     // each wave owns a contiguous run of kAhead*64 reads per step (BAM order = wave
     // order, then round order); waves claim bucket slots in wave order
     constexpr int kAhead = MGP_GA_AHEAD;
-    constexpr int kStep = kAhead * kBlock;
+    constexpr int kStep = kAhead * kGABlock;
     struct Pre {
         int c[kAhead], s[kAhead], t[kAhead], f[kAhead], m[kAhead];
         uint64_t o[kAhead];
     };
     // loads issued unconditionally (index clamped into the bin) so every path has
     // the same number in flight and the waits stay counted
-    // kDense: a dense packed payload (k_check_stride at ingest), offsets from the index
+    // the record offset: from the index (dense), the u32 column or the u64 column (kOff)
     auto load = [&](Pre& P, int64_t base0) {
 #pragma unroll
         for (int u = 0; u < kAhead; ++u) {
@@ -489,7 +503,9 @@ __global__ void __launch_bounds__(kBlock, MGP_GA_WAVES) k_group_a(int64_t n, con
             P.s[u] = start[j];
             P.t[u] = tlen[j];
             P.m[u] = mapq[j];
-            P.o[u] = kDense ? (uint64_t)j * kRecStride : roff[j];
+            P.o[u] = kOff == kOffDense ? (uint64_t)j * kRecStride
+                     : kOff == kOffR32 ? (uint64_t)roff32[j] << 6
+                                       : roff[j];
         }
     };
     // A step: each wave ranks its own reads by group (ballot peers, the leader of a
@@ -498,7 +514,7 @@ __global__ void __launch_bounds__(kBlock, MGP_GA_WAVES) k_group_a(int64_t n, con
     // Two barriers per step, no wave waits for another's ranking.
     int set = 0;
     auto process = [&](const Pre& P, int64_t base0) {
-        uint32_t* my = wc + ((size_t)set * (kBlock / kWave) + wid) * ngroups;
+        uint32_t* my = wc + ((size_t)set * (kGABlock / kWave) + wid) * ngroups;
         for (int x = lane; x < ngroups; x += kWave) my[x] = 0;
         __builtin_amdgcn_wave_barrier();
         bool valid[kAhead];
@@ -530,11 +546,11 @@ __global__ void __launch_bounds__(kBlock, MGP_GA_WAVES) k_group_a(int64_t n, con
             for (int u = 0; u < kAhead; ++u) rk[u] = 0;
         }
         __syncthreads();
-        for (int gi = threadIdx.x; gi < ngroups; gi += kBlock) {
+        for (int gi = threadIdx.x; gi < ngroups; gi += kGABlock) {
             uint32_t run = gcnt[gi];
 #pragma unroll
-            for (int w = 0; w < kBlock / kWave; ++w) {
-                uint32_t* r = wc + ((size_t)set * (kBlock / kWave) + w) * ngroups;
+            for (int w = 0; w < kGABlock / kWave; ++w) {
+                uint32_t* r = wc + ((size_t)set * (kGABlock / kWave) + w) * ngroups;
                 const uint32_t x = r[gi];
                 r[gi] = run;
                 run += x;
@@ -1048,6 +1064,15 @@ __device__ __forceinline__ void pile_read(bool has, bool packed, const uint8_t* 
                                           bool& span_err, bool& pk_err) {
     if (MGP_ABL == 1) return;
     if (MGP_ABL == 3) packed = false;  // the synthetic reads are in the full layout
+    if (MGP_ABL == 9) {
+        // experiment: lane pairs read the two halves of ONE 128-B line (the even
+        // lane's record line), emulating a placement where consecutive piled reads
+        // of a cell share a line; counts meaningless
+        const unsigned long long a = (unsigned long long)reinterpret_cast<uintptr_t>(rec);
+        const unsigned long long p = __shfl(a, (int)(threadIdx.x & 62), kWave);
+        rec = reinterpret_cast<const uint8_t*>((p & ~127ull) + 64ull * (threadIdx.x & 1));
+        packed = true;
+    }
     RecLine R;
     load_line(has, packed, rec, w, R);
     pile_line(has, packed, rec, R, w, pc, tile, t5, max_span, span_err, pk_err);
@@ -1650,10 +1675,17 @@ __global__ void k_add_u64(uint64_t* __restrict__ a, int64_t n, uint64_t add) {
 // Record placement check at ingest: *irregular stays 0 while every resident
 // record offset is kRecStride x its read index (a fully packed, dense payload);
 // grouping pass A then computes the offsets instead of reading them.
-__global__ void k_check_stride(const uint64_t* __restrict__ roff, int64_t n, int64_t i0, uint32_t* irregular) {
+// Also writes the compact u32 column roff32 = rec_off >> 6 and sets bit 2 when an
+// offset does not fit it (not a multiple of 64, or >= 2^38).
+__global__ void k_check_stride(const uint64_t* __restrict__ roff, int64_t n, int64_t i0, uint32_t* irregular,
+                               uint32_t* __restrict__ roff32) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const bool bad = i < n && roff[i] != (uint64_t)(i0 + i) * kRecStride;
-    if (__ballot(bad) != 0ull && (threadIdx.x & 63) == 0) atomicOr(irregular, 1u);
+    const uint64_t r = i < n ? roff[i] : 0ull;
+    if (i < n) roff32[i] = (uint32_t)(r >> 6);
+    const bool bad = i < n && r != (uint64_t)(i0 + i) * kRecStride;
+    const bool wide = i < n && ((r & 63ull) != 0ull || (r >> 38) != 0ull);
+    const unsigned long long b1 = __ballot(bad), b2 = __ballot(wide);
+    if ((b1 | b2) != 0ull && (threadIdx.x & 63) == 0) atomicOr(irregular, (b1 ? 1u : 0u) | (b2 ? 2u : 0u));
 }
 
 // ---------------------------------------------------------------------------
@@ -1742,9 +1774,12 @@ int mgp_open(const mgp_config* cfg, int hip_device, mgp_ctx** out) {
         const int lds_max = (int)prop.sharedMemPerBlock;
         (void)hipFuncSetAttribute((const void*)k_bin_count, hipFuncAttributeMaxDynamicSharedMemorySize,
                                   lds_max);
-        (void)hipFuncSetAttribute((const void*)k_group_a<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+        (void)hipFuncSetAttribute((const void*)k_group_a<kOffDense>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                   lds_max);
-        (void)hipFuncSetAttribute((const void*)k_group_a<true>, hipFuncAttributeMaxDynamicSharedMemorySize, lds_max);
+        (void)hipFuncSetAttribute((const void*)k_group_a<kOffR32>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  lds_max);
+        (void)hipFuncSetAttribute((const void*)k_group_a<kOffR64>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  lds_max);
         (void)hipFuncSetAttribute((const void*)k_pileup, hipFuncAttributeMaxDynamicSharedMemorySize, lds_max);
         (void)hipGetLastError();
         if ((size_t)ctx->g.L * 4 + 2048 > prop.sharedMemPerBlock) {
@@ -1769,6 +1804,7 @@ int mgp_open(const mgp_config* cfg, int hip_device, mgp_ctx** out) {
         MGP_TRY(ctx->mapq.ensure(n));
         MGP_TRY(ctx->span.ensure(n * 4));
         MGP_TRY(ctx->roff.ensure(n * 8));
+        MGP_TRY(ctx->roff32.ensure(n * 4));
     }
     if (cfg->reserve_payload > 0) MGP_TRY(ctx->payload.ensure((size_t)cfg->reserve_payload));
     *out = ctx;
@@ -1783,6 +1819,7 @@ void mgp_close(mgp_ctx* ctx) {
     if (ctx->comm) ncclCommDestroy(ctx->comm);
     DevBuf* bufs[] = {&ctx->start,     &ctx->bc,        &ctx->tlen,     &ctx->flag,       &ctx->mapq,
                       &ctx->span,      &ctx->roff,      &ctx->payload,  &ctx->bin_start,  &ctx->gel2,
+                      &ctx->roff32,    &ctx->roff_irregular,
                       &ctx->H,         &ctx->P,         &ctx->cell_cnt, &ctx->cell_base,  &ctx->pel,
                       &ctx->PG,        &ctx->F,
                       &ctx->tally_part, &ctx->tally,   &ctx->n_reads,    &ctx->any_paired,
@@ -1812,6 +1849,7 @@ static int ensure_inputs(mgp_ctx* ctx, int64_t n_total, int64_t pay_total, bool 
     MGP_TRY(ctx->mapq.ensure(n, preserve, used, s));
     MGP_TRY(ctx->span.ensure(n * 4, preserve, used * 4, s));
     MGP_TRY(ctx->roff.ensure(n * 8, preserve, used * 8, s));
+    MGP_TRY(ctx->roff32.ensure(n * 4, preserve, used * 4, s));
     MGP_TRY(ctx->payload.ensure((size_t)pay_total + 256, preserve, preserve ? (size_t)ctx->pay : 0, s));
     return MGP_OK;
 }
@@ -1845,9 +1883,10 @@ int mgp_push_batch(mgp_ctx* ctx, const mgp_batch* b) {
     }
     MGP_TRY(ctx->roff_irregular.ensure(4));
     if (n0 == 0) HIP_TRY(hipMemsetAsync(ctx->roff_irregular.p, 0, 4, s));
-    ctx->dense = -1;
+    ctx->roff_mode = -1;
     k_check_stride<<<blocks_for(nb), kBlock, 0, s>>>(ctx->roff.as<uint64_t>() + n0, nb, n0,
-                                                     ctx->roff_irregular.as<uint32_t>());
+                                                     ctx->roff_irregular.as<uint32_t>(),
+                                                     ctx->roff32.as<uint32_t>() + n0);
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipEventRecord(ctx->ev_copy, s));
     ctx->n = n0 + nb;
@@ -1920,11 +1959,11 @@ int mgp_run(mgp_ctx* ctx) {
     const int64_t n = ctx->n;
     const int nc = g.nc;
     hipStream_t s = ctx->s_comp;
-    if (ctx->dense < 0 && n > 0) {  // the ingest stride check, read once per resident set
-        uint32_t irr = 1;
+    if (ctx->roff_mode < 0 && n > 0) {  // the ingest placement check, read once per resident set
+        uint32_t irr = 3;
         HIP_TRY(hipStreamSynchronize(ctx->s_copy));
         HIP_TRY(hipMemcpy(&irr, ctx->roff_irregular.p, 4, hipMemcpyDeviceToHost));
-        ctx->dense = irr == 0u;
+        ctx->roff_mode = !(irr & 1u) ? kOffDense : !(irr & 2u) ? kOffR32 : kOffR64;
     }
     HIP_TRY(hipStreamWaitEvent(s, ctx->ev_copy, 0));
     const int slot = (int)(ctx->runs % mgp_ctx::kRing);
@@ -1983,28 +2022,23 @@ int mgp_run(mgp_ctx* ctx) {
             int gbits = 0;
             while (gbits < 31 && (1 << gbits) < ngroups) ++gbits;
             k_scan_cells<<<1, 1024, 0, s>>>(ctx->bin_valid.as<uint32_t>(), g.nbins, ctx->bin_base.as<uint32_t>());
-            const size_t a_lds = (size_t)ngroups * (1 + 2 * (kBlock / kWave)) * 4 + (size_t)((nc + 31) / 32) * 4;
+            const size_t a_lds = (size_t)ngroups * (1 + 2 * (kGABlock / kWave)) * 4 + (size_t)((nc + 31) / 32) * 4;
             if (a_lds > (size_t)ctx->lds_hist_max_cells * 4)
                 return set_err(MGP_E_INVALID, "too many cells for one context (grouping LDS)");
             if ((uint64_t)ctx->pay >= (1ull << GM_LCELL_SHIFT))
                 return set_err(MGP_E_INVALID, "payload too large (record offsets must stay below 2^50)");
             dim3 ga((unsigned)g.nbins, kParts);
-            if (ctx->dense > 0)
-                k_group_a<true><<<ga, kBlock, a_lds, s>>>(
-                n, ctx->start.as<int32_t>(), ctx->bc.as<int32_t>(), ctx->tlen.as<int32_t>(), ctx->flag.as<uint16_t>(),
-                ctx->mapq.as<uint8_t>(), ctx->roff.as<uint64_t>(),
-                ctx->bin_start.as<uint32_t>(),
-                ctx->PG.as<uint32_t>(), ctx->F.as<uint32_t>(), ctx->bin_base.as<uint32_t>(), g, ngroups, gbits,
-                ctx->cfg.min_mapq, ctx->bucket_off.as<uint32_t>(), ctx->gel2.as<GElem>(),
-                ctx->first_read.as<uint32_t>(), st);
-            else
-                k_group_a<false><<<ga, kBlock, a_lds, s>>>(
-                n, ctx->start.as<int32_t>(), ctx->bc.as<int32_t>(), ctx->tlen.as<int32_t>(), ctx->flag.as<uint16_t>(),
-                ctx->mapq.as<uint8_t>(), ctx->roff.as<uint64_t>(),
-                ctx->bin_start.as<uint32_t>(),
-                ctx->PG.as<uint32_t>(), ctx->F.as<uint32_t>(), ctx->bin_base.as<uint32_t>(), g, ngroups, gbits,
-                ctx->cfg.min_mapq, ctx->bucket_off.as<uint32_t>(), ctx->gel2.as<GElem>(),
-                ctx->first_read.as<uint32_t>(), st);
+            auto launch_a = [&](auto kern) {
+                kern<<<ga, kGABlock, a_lds, s>>>(
+                    n, ctx->start.as<int32_t>(), ctx->bc.as<int32_t>(), ctx->tlen.as<int32_t>(),
+                    ctx->flag.as<uint16_t>(), ctx->mapq.as<uint8_t>(), ctx->roff.as<uint64_t>(),
+                    ctx->roff32.as<uint32_t>(), ctx->bin_start.as<uint32_t>(), ctx->PG.as<uint32_t>(),
+                    ctx->F.as<uint32_t>(), ctx->bin_base.as<uint32_t>(), g, ngroups, gbits, ctx->cfg.min_mapq,
+                    ctx->bucket_off.as<uint32_t>(), ctx->gel2.as<GElem>(), ctx->first_read.as<uint32_t>(), st);
+            };
+            if (ctx->roff_mode == kOffDense) launch_a(k_group_a<kOffDense>);
+            else if (ctx->roff_mode == kOffR32) launch_a(k_group_a<kOffR32>);
+            else launch_a(k_group_a<kOffR64>);
             HIP_TRY(hipGetLastError());
         }
         STAGE_END(ST_GROUP_A);
@@ -2238,7 +2272,7 @@ int mgp_download_inputs(mgp_ctx* ctx, int32_t* start, int32_t* bc, int32_t* tlen
 int mgp_synth_fill(void* stream, uint64_t seed, int64_t n, int read_len, int n_cells, int mito_len,
                    const uint32_t* d_cdf, const uint8_t* d_ref, int32_t* start, int32_t* bc, int32_t* tlen,
                    uint16_t* flag, uint8_t* mapq, uint32_t* span, uint64_t* roff, uint8_t* payload,
-                   int64_t* payload_bytes, int rec_align, int pack);
+                   int64_t* payload_bytes, int rec_align, int pack, int placed);
 
 int mgp_synth_generate(mgp_ctx* ctx, const mgp_synth_params* p) {
     if (!ctx || !p || !p->cell_cdf || !p->ref_codes) return set_err(MGP_E_INVALID, "null synth args");
@@ -2258,18 +2292,30 @@ int mgp_synth_generate(mgp_ctx* ctx, const mgp_synth_params* p) {
     const int nc = p->n_cells;
     // record size is at most 16 + 4*3 + len + (len+1)/2 rounded to 8
     const int64_t max_rec = ((int64_t)mgp_cigar_offset((uint32_t)p->read_len) + 16 + align - 1) & ~(int64_t)(align - 1);
-    MGP_TRY(ensure_inputs(ctx, std::max<int64_t>(n, 1), n * max_rec, false));
+    const bool placed = p->rec_off != nullptr;
+    if (placed && (p->payload_bytes < 0 || p->payload_bytes > n * std::max<int64_t>(max_rec, 128) + 128))
+        return set_err(MGP_E_INVALID, "synth payload_bytes out of range");
+    MGP_TRY(ensure_inputs(ctx, std::max<int64_t>(n, 1), placed ? p->payload_bytes : n * max_rec, false));
     DevBuf cdf, ref;
     MGP_TRY(cdf.ensure((size_t)std::max(nc, 1) * 4));
     MGP_TRY(ref.ensure((size_t)L));
     hipStream_t s = ctx->s_copy;
     if (nc) HIP_TRY(hipMemcpyAsync(cdf.p, p->cell_cdf, (size_t)nc * 4, hipMemcpyHostToDevice, s));
     HIP_TRY(hipMemcpyAsync(ref.p, p->ref_codes, (size_t)L, hipMemcpyHostToDevice, s));
-    int64_t pay = 0;
+    int64_t pay = placed ? p->payload_bytes : 0;
+    if (placed && n) {  // every record must fit the payload (the generator writes up to max_rec bytes)
+        for (int64_t i = 0; i < n; ++i)
+            if ((p->rec_off[i] & 15u) || (int64_t)p->rec_off[i] + (p->pack ? MGP_PACK_BYTES : max_rec) > pay) {
+                cdf.release();
+                ref.release();
+                return set_err(MGP_E_INVALID, "synth rec_off outside the payload or not 16-byte aligned");
+            }
+        HIP_TRY(hipMemcpyAsync(ctx->roff.p, p->rec_off, (size_t)n * 8, hipMemcpyHostToDevice, s));
+    }
     int r = mgp_synth_fill(s, p->seed, n, p->read_len, nc, L, cdf.as<uint32_t>(), ref.as<uint8_t>(),
                            ctx->start.as<int32_t>(), ctx->bc.as<int32_t>(), ctx->tlen.as<int32_t>(),
                            ctx->flag.as<uint16_t>(), ctx->mapq.as<uint8_t>(), ctx->span.as<uint32_t>(),
-                           ctx->roff.as<uint64_t>(), ctx->payload.as<uint8_t>(), &pay, align, p->pack);
+                           ctx->roff.as<uint64_t>(), ctx->payload.as<uint8_t>(), &pay, align, p->pack, placed);
     if (r != MGP_OK) {
         cdf.release();
         ref.release();
@@ -2277,10 +2323,11 @@ int mgp_synth_generate(mgp_ctx* ctx, const mgp_synth_params* p) {
     }
     MGP_TRY(ctx->roff_irregular.ensure(4));
     HIP_TRY(hipMemsetAsync(ctx->roff_irregular.p, 0, 4, s));
-    ctx->dense = -1;
+    ctx->roff_mode = -1;
     if (n)
         k_check_stride<<<blocks_for(n), kBlock, 0, s>>>(ctx->roff.as<uint64_t>(), n, 0,
-                                                        ctx->roff_irregular.as<uint32_t>());
+                                                        ctx->roff_irregular.as<uint32_t>(),
+                                                        ctx->roff32.as<uint32_t>());
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipStreamSynchronize(s));
     cdf.release();

@@ -302,7 +302,7 @@ __global__ void k_synth_fill(uint64_t seed, int64_t n, int rl, int nc, int L, co
 extern "C" int mgp_synth_fill(void* stream, uint64_t seed, int64_t n, int read_len, int n_cells, int mito_len,
                               const uint32_t* d_cdf, const uint8_t* d_ref, int32_t* start, int32_t* bc,
                               int32_t* tlen, uint16_t* flag, uint8_t* mapq, uint32_t* span, uint64_t* roff,
-                              uint8_t* payload, int64_t* payload_bytes, int rec_align, int pack) {
+                              uint8_t* payload, int64_t* payload_bytes, int rec_align, int pack, int placed) {
     hipStream_t s = (hipStream_t)stream;
     if (read_len < 48) return MGP_E_INVALID;
     if (n == 0) {
@@ -310,11 +310,13 @@ extern "C" int mgp_synth_fill(void* stream, uint64_t seed, int64_t n, int read_l
         return MGP_OK;
     }
     const unsigned nb = (unsigned)((n + kBlock - 1) / kBlock);
-    k_synth_sizes<<<nb, kBlock, 0, s>>>(seed, n, read_len, rec_align, pack, roff);
-    if (hipGetLastError() != hipSuccess) return MGP_E_HIP;
-    uint64_t total = 0;
-    int r = scan_exclusive_u64(roff, n, s, &total);
-    if (r != MGP_OK) return r;
+    uint64_t total = (uint64_t)*payload_bytes;
+    if (!placed) {  // dense: offsets = exclusive scan of the record sizes; else roff holds the placement
+        k_synth_sizes<<<nb, kBlock, 0, s>>>(seed, n, read_len, rec_align, pack, roff);
+        if (hipGetLastError() != hipSuccess) return MGP_E_HIP;
+        int r = scan_exclusive_u64(roff, n, s, &total);
+        if (r != MGP_OK) return r;
+    }
     if (hipMemsetAsync(payload, 0, (size_t)total, s) != hipSuccess) return MGP_E_HIP;
     k_synth_fill<<<nb, kBlock, 0, s>>>(seed, n, read_len, n_cells, mito_len, d_cdf, d_ref, start, bc, tlen, flag,
                                        mapq, span, roff, payload, pack);

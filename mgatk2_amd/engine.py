@@ -117,6 +117,8 @@ class mgp_synth_params(C.Structure):
         ("ref_codes", C.c_void_p),
         ("rec_align", C.c_int32),
         ("pack", C.c_int32),
+        ("rec_off", C.c_void_p),
+        ("payload_bytes", C.c_int64),
     ]
 
 
@@ -327,23 +329,38 @@ class Engine:
         return int(n.value), int(p.value)
 
     def synth(self, seed: int, n_reads: int, cdf: np.ndarray, ref: np.ndarray, read_len: int = 50,
-              rec_align: int = 64, pack: bool = True):
+              rec_align: int = 64, pack: bool = True, rec_off: np.ndarray | None = None, payload_bytes: int = 0):
+        """Device-side synthetic workload (replaces the resident set). rec_off: an
+        explicit placement of the records (e.g. host placement of
+        mgp_place_records, `synth.place_records`); None = dense in BAM order."""
         cdf = np.ascontiguousarray(cdf, np.uint32)
         ref = np.ascontiguousarray(ref, np.uint8)
+        ro = None if rec_off is None else np.ascontiguousarray(rec_off, np.uint64)
+        if ro is not None and ro.shape[0] != n_reads:
+            raise ValueError("rec_off must have n_reads entries")
         p = mgp_synth_params(int(seed), int(n_reads), int(read_len), int(self.cfg.n_cells), _ptr(cdf), _ptr(ref),
-                             int(rec_align), int(bool(pack)))
+                             int(rec_align), int(bool(pack)), None if ro is None else _ptr(ro),
+                             int(payload_bytes) if ro is not None else 0)
         _ck(self.lib.mgp_synth_generate(self._h, C.byref(p)), "mgp_synth_generate")
 
-    def download_inputs(self) -> ReadSoA:
+    def download_inputs(self, columns: tuple[str, ...] | None = None) -> ReadSoA:
+        """Resident inputs back on the host; `columns` limits the copy to those SoA
+        fields (the others are empty arrays)."""
         n, pay = self.resident()
+
+        def col(name, dt, m):
+            return np.zeros(m if columns is None or name in columns else 0, dt)
+
         soa = ReadSoA(
-            np.zeros(n, np.int32), np.zeros(n, np.int32), np.zeros(n, np.int32), np.zeros(n, np.uint16),
-            np.zeros(n, np.uint8), np.zeros(n, np.uint32), np.zeros(n, np.uint64), np.zeros(pay, np.uint8),
+            col("start", np.int32, n), col("bc", np.int32, n), col("tlen", np.int32, n), col("flag", np.uint16, n),
+            col("mapq", np.uint8, n), col("span", np.uint32, n), col("rec_off", np.uint64, n),
+            col("payload", np.uint8, pay),
         )
         _ck(
             self.lib.mgp_download_inputs(
-                self._h, _ptr(soa.start), _ptr(soa.bc), _ptr(soa.tlen), _ptr(soa.flag), _ptr(soa.mapq),
-                _ptr(soa.span), _ptr(soa.rec_off), _ptr(soa.payload),
+                self._h, *[_ptr(a) if a.shape[0] else None for a in (soa.start, soa.bc, soa.tlen, soa.flag,
+                                                                        soa.mapq, soa.span, soa.rec_off,
+                                                                        soa.payload)],
             ),
             "mgp_download_inputs",
         )

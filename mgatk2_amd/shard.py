@@ -43,30 +43,42 @@ def reads_per_cell(soa: ReadSoA, n_cells: int) -> np.ndarray:
     return np.bincount(bc, minlength=n_cells)[:n_cells]
 
 
-def shard_soa(soa: ReadSoA, lo: int, hi: int, rec_align: int = 64) -> tuple[ReadSoA, np.ndarray]:
+def shard_soa(soa: ReadSoA, lo: int, hi: int, rec_align: int = 64, paired: bool = True,
+              keep_all: bool = False) -> tuple[ReadSoA, np.ndarray]:
     """Reads of cells [lo, hi) in BAM order, cell ids rebased to lo, payload
-    records gathered into a dense payload (native, multithreaded:
-    libmgphost.so `mgp_gather_records`). Returns (batch, original read indices)."""
-    import ctypes as C
+    records gathered into a new payload (native, multithreaded: libmgphost.so
+    `mgp_gather_offsets` / `mgp_gather_records`), placed by the producer
+    placement (two consecutive packed records of a cell per 128-byte line when
+    `paired`, else dense at `rec_align`). keep_all: every read (lo must be 0;
+    reads outside the range keep their bc). Returns (batch, original read
+    indices)."""
+    from .bam import PLACE_DENSE, PLACE_PAIRED, host_library, host_threads
 
-    from .bam import host_library, host_threads
-
-    idx = np.flatnonzero((soa.bc >= lo) & (soa.bc < hi)).astype(np.int64)
+    if keep_all:
+        if lo != 0:
+            raise ValueError("keep_all needs lo == 0")
+        idx = np.arange(soa.n, dtype=np.int64)
+    else:
+        idx = np.flatnonzero((soa.bc >= lo) & (soa.bc < hi)).astype(np.int64)
     lib = host_library()
     roff = np.ascontiguousarray(soa.rec_off, dtype=np.uint64)
+    flag = np.ascontiguousarray(soa.flag, dtype=np.uint16)
+    bc = np.ascontiguousarray(soa.bc, dtype=np.int32)
     pay = np.ascontiguousarray(soa.payload)
     new_off = np.zeros(max(idx.size, 1), np.uint64)
-    total = lib.mgp_gather_offsets(roff.ctypes.data, soa.n, pay.shape[0], idx.ctypes.data, idx.size, rec_align,
-                                   new_off.ctypes.data)
+    total = lib.mgp_gather_offsets(pay.ctypes.data, roff.ctypes.data, flag.ctypes.data, bc.ctypes.data, soa.n,
+                                   pay.shape[0], idx.ctypes.data, idx.size, int(lo), int(hi - lo),
+                                   PLACE_PAIRED if paired else PLACE_DENSE, rec_align, new_off.ctypes.data)
     if total < 0:
         raise ValueError((lib.mgp_host_last_error() or b"").decode())
     payload = np.zeros(total, np.uint8)
-    if idx.size and lib.mgp_gather_records(pay.ctypes.data, roff.ctypes.data, soa.n, pay.shape[0], idx.ctypes.data,
-                                           idx.size, new_off.ctypes.data, total, payload.ctypes.data,
-                                           host_threads()) != 0:
+    if idx.size and lib.mgp_gather_records(pay.ctypes.data, roff.ctypes.data, flag.ctypes.data, soa.n, pay.shape[0],
+                                           idx.ctypes.data, idx.size, new_off.ctypes.data, total,
+                                           payload.ctypes.data, host_threads()) != 0:
         raise ValueError((lib.mgp_host_last_error() or b"").decode())
     out = ReadSoA(
-        soa.start[idx].copy(), (soa.bc[idx] - lo).astype(np.int32), soa.tlen[idx].copy(), soa.flag[idx].copy(),
+        soa.start[idx].copy(), (soa.bc[idx] - lo).astype(np.int32) if lo else soa.bc[idx].astype(np.int32),
+        soa.tlen[idx].copy(), soa.flag[idx].copy(),
         soa.mapq[idx].copy(), soa.span[idx].copy(), new_off[: idx.size].copy(), payload,
     )
     return out, idx

@@ -145,9 +145,18 @@ class ReadSoA:
         return int(self.start.shape[0])
 
     def slice(self, lo: int, hi: int) -> ReadSoA:
-        """Reads [lo, hi) as a standalone batch (payload re-based)."""
+        """Reads [lo, hi) as a standalone batch (payload re-based). A payload whose
+        records are not in BAM order (paired placement) is gathered and re-placed."""
         if hi <= lo:
             return empty_soa()
+        ro = self.rec_off.astype(np.int64)
+        if self.n > 1 and np.any(np.diff(ro) < 0):
+            from .shard import shard_soa
+
+            sub = ReadSoA(self.start[lo:hi], self.bc[lo:hi], self.tlen[lo:hi], self.flag[lo:hi], self.mapq[lo:hi],
+                          self.span[lo:hi], self.rec_off[lo:hi], self.payload)
+            nc = int(self.bc.max()) + 1
+            return shard_soa(sub, 0, nc, paired=True, keep_all=True)[0]
         p0 = int(self.rec_off[lo])
         p1 = int(self.rec_off[hi]) if hi < self.n else int(self.payload.shape[0])
         return ReadSoA(
@@ -160,6 +169,19 @@ class ReadSoA:
             (self.rec_off[lo:hi] - np.uint64(p0)).astype(np.uint64),
             self.payload[p0:p1].copy(),
         )
+
+
+def relocate(soa: ReadSoA, paired: bool = False, rec_align: int = 64, n_cells: int | None = None) -> ReadSoA:
+    """The same reads with their payload records moved to the producer placement
+    (mgp_place_records): dense in BAM order at `rec_align`, or paired (two
+    consecutive packed records of a cell per 128-byte line). Record bytes are
+    unchanged; only rec_off and the payload's arrangement differ."""
+    from .shard import shard_soa
+
+    nc = int(soa.bc.max()) + 1 if n_cells is None and soa.n else int(n_cells or 0)
+    out, idx = shard_soa(soa, 0, nc, rec_align=rec_align, paired=paired, keep_all=True)
+    out.extra.update(soa.extra)
+    return out
 
 
 def empty_soa() -> ReadSoA:

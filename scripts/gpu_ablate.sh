@@ -8,7 +8,7 @@ A="python bench.py --steps 10 --warmup 2 --no-cpu-baseline"
 timeout -k 10 300 $A > gpurun_out/abl_0warm.log 2>&1 || exit $?
 timeout -k 10 300 $A > gpurun_out/abl_1base.log 2>&1 || exit $?
 for v in "$@"; do
-  MGP_LIB=mgatk2_amd/_lib/$v timeout -k 10 300 $A > gpurun_out/abl_2_$v.log 2>&1 || exit $?
+  MGP_LIB=mgatk2_amd/_lib/$v timeout -k 10 300 $A > gpurun_out/abl_2_$(basename $v .so).log 2>&1 || exit $?
 done
 timeout -k 10 300 $A > gpurun_out/abl_3base2.log 2>&1 || exit $?
 python - <<'PY'

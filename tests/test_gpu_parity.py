@@ -453,3 +453,61 @@ def test_full_size_invariants_and_cell_sample_c3(engine_lib, oracle_lib):
         for k in ("counts", "tn5", "depth", "n_reads", "any_paired", "passed", "covered", "depth_sum",
                   "depth_max", "median_lo", "median_hi"):
             np.testing.assert_array_equal(getattr(res, k)[lo:hi], getattr(exp, k), err_msg=f"cells {lo}-{hi} {k}")
+
+
+# ---------------------------------------------------------------------------
+# payload placement (mgp_place_records): cell-paired lines; grouping pass A's
+# offset sources (dense index / u32 column / u64 column, k_check_stride)
+# ---------------------------------------------------------------------------
+@pytest.mark.parametrize("cfgname", sorted(CONFIGS))
+def test_paired_placement_matches_oracle(engine_lib, oracle_lib, cfgname):
+    from mgatk2_amd.engine import EngineConfig
+    from mgatk2_amd.synth import relocate
+
+    soa = relocate(_synth(1000 + 300_000 + 200, 300_000, 200), paired=True, n_cells=200)
+    cfg = EngineConfig(n_cells=200, **CONFIGS[cfgname])
+    res = run_engine(engine_lib, cfg, soa)
+    exp, _ = oracle_lib.oracle_run(cfg, soa)
+    assert_same(res, exp, f"paired {cfgname}")
+
+
+def _shifted(soa, by=16):
+    """The same payload moved by `by` bytes: offsets no longer multiples of 64
+    (pass A reads the u64 offset column)."""
+    from mgatk2_amd.synth import ReadSoA
+
+    pay = np.zeros(soa.payload.size + by, np.uint8)
+    pay[by:] = soa.payload
+    return ReadSoA(soa.start, soa.bc, soa.tlen, soa.flag, soa.mapq, soa.span,
+                   (soa.rec_off + np.uint64(by)).astype(np.uint64), pay)
+
+
+def test_offset_sources_give_identical_results(engine_lib):
+    from mgatk2_amd.engine import EngineConfig
+    from mgatk2_amd.synth import relocate
+
+    dense = _synth(5, 250_000, 70)
+    paired = relocate(dense, paired=True, n_cells=70)
+    cfg = EngineConfig(n_cells=70, min_baseq=20, min_mapq=30, dedup_mode="alignment_and_fragment_length")
+    base = run_engine(engine_lib, cfg, dense)
+    for name, soa, batches in [("paired", paired, 1), ("paired x4", paired, 4), ("shifted", _shifted(dense), 1),
+                               ("shifted paired x3", _shifted(paired), 3)]:
+        assert_same(run_engine(engine_lib, cfg, soa, batches=batches), base, name)
+
+
+def test_device_generator_with_placement(engine_lib):
+    from mgatk2_amd.bam import PLACE_PAIRED, place_records
+    from mgatk2_amd.engine import EngineConfig
+    from mgatk2_amd.synth import relocate, synth_reads
+
+    n, nc, seed = 90_001, 29, 8
+    host = synth_reads(seed, n, nc)
+    roff, tot = place_records(host.bc, host.flag, np.full(n, 64, np.uint32), nc, PLACE_PAIRED)
+    exp = relocate(host, paired=True, n_cells=nc)
+    np.testing.assert_array_equal(roff, exp.rec_off)
+    with engine_lib.Engine(EngineConfig(n_cells=nc)) as eng:
+        eng.synth(seed, n, host.extra["cdf"], host.extra["ref"], rec_off=roff, payload_bytes=tot)
+        dev = eng.download_inputs()
+    for k in ("start", "bc", "tlen", "flag", "mapq", "span", "rec_off"):
+        np.testing.assert_array_equal(getattr(dev, k), getattr(exp, k), err_msg=k)
+    np.testing.assert_array_equal(dev.payload[: exp.payload.size], exp.payload[: dev.payload.size])
