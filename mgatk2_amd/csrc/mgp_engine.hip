@@ -943,9 +943,13 @@ struct Win {
     int w0, wlen, Wp;
 };
 
-// LDS tile: 4 base planes + 1 Tn5 plane of Wp u32 each; every u32 packs the
-// forward count in its low 16 bits and the reverse count in its high 16 bits
-// (a window is processed in segments of < 65536 reads, so no half can carry).
+// LDS tile: position-major base counts tile[pos * 4 + base] (A, C, G, T), then a
+// Tn5 plane of Wp u32 at tile + 4 Wp; every u32 packs the forward count in its low
+// 16 bits and the reverse count in its high 16 bits (a window is processed in
+// segments of < 65536 reads, so no half can carry). Position-major makes a
+// count's LDS address one shift-add of the base index onto the read's row, with
+// the query offset in the instruction's immediate; a flush reads a position's 4
+// bases with one 16-byte load.
 __device__ __forceinline__ uint32_t strand_inc(int strand) { return strand ? 0x10000u : 1u; }
 
 __device__ __forceinline__ void tn5_cut(int32_t start, uint32_t lseq, int strand, const Win& w, uint32_t* t5) {
@@ -980,7 +984,7 @@ __device__ bool pile_slow(const uint8_t* __restrict__ rec, int32_t start, uint32
                 const uint8_t sb = seq[qq >> 1];
                 const int bi = base_index((qq & 1) ? (sb & 15u) : (sb >> 4));
                 if (bi < 0) continue;
-                atomicAdd(&tile[bi * w.Wp + (int)(ref + k - w.w0)], inc);
+                atomicAdd(&tile[(int)(ref + k - w.w0) * 4 + bi], inc);
             }
             q += len;
             ref += len;
@@ -997,7 +1001,7 @@ __device__ bool pile_slow(const uint8_t* __restrict__ rec, int32_t start, uint32
 #define MGP_WIN 1280  // target window width (positions); W <= kMaxPosPerThread * 256 (A/B: 768-2048)
 #endif
 constexpr int kMaxPosPerThread = MGP_WIN / 256;
-constexpr int kTilePitch = MGP_WIN;  // u32 per tile plane (>= the window width W)
+constexpr int kTilePitch = MGP_WIN;  // positions per tile (>= the window width W)
 constexpr int kFastLen = 64;   // reads up to 64 bases with <= 4 CIGAR ops and <= 2 aligned blocks
 constexpr int kFastCig = 4;
 constexpr uint32_t kValid = 0x0116u;   // codes 1, 2, 4, 8 are counted (pileup.py:83-86)
@@ -1014,6 +1018,9 @@ constexpr uint32_t kValid = 0x0116u;   // codes 1, 2, 4, 8 are counted (pileup.p
 // register index is static. Other reads take the generic byte-load path.
 #ifndef MGP_ABL
 #define MGP_ABL 0  // ablation switch for experiments: 0 = real kernel
+#endif
+#ifndef MGP_BL
+#define MGP_BL 1  // branch-free per-base counting (A/B: masked atomics 0.4 ms slower)
 #endif
 // The first 128-byte line of a record in registers: header, qual (+16), seq (+80)
 // and CIGAR (+112) of a read of <= 64 bases with <= 4 operations
@@ -1126,7 +1133,12 @@ __device__ __forceinline__ void pile_bases(bool act, int a0, int b0, int a1, int
         }
     }
     const uint32_t sw[8] = {R.sv[0].x, R.sv[0].y, R.sv[0].z, R.sv[0].w, R.sv[1].x, R.sv[1].y, R.sv[1].z, R.sv[1].w};
-    uint32_t* base = tile - w.w0;
+    // one count at tile[idx] when ok; MGP_BL: branch-free, a lane that does not count
+    // adds 0 to a slot of its own instead of being masked off
+    auto count = [&](uint32_t ok, int idx) {
+        if (MGP_BL) atomicAdd(&tile[ok ? (uint32_t)idx : (uint32_t)(threadIdx.x & 63)], ok ? inc : 0u);
+        else if (ok) atomicAdd(&tile[idx], inc);
+    };
     const int minbq = pc.min_baseq;
     // packed: counted iff qual << 2 | b lies in [4 * max(min_baseq, 0), 252) (0xFF and
     // anything >= 252 are never counted; packed quals are <= 62)
@@ -1163,14 +1175,33 @@ __device__ __forceinline__ void pile_bases(bool act, int a0, int b0, int a1, int
         return lo < hi ? (h & ~l) : 0ull;
     };
     if (uniform) {
-        uint32_t* lb = base + dl0;
+        const int lb0 = 4 * (dl0 - w.w0);
         const unsigned long long smask = range_mask(ua0, ub0);
-#pragma unroll
-        for (int qq = 0; qq < kLen; ++qq) {
-            if (!((smask >> qq) & 1ull)) continue;
+        auto body = [&](int qq) {
             uint32_t plane;
             const uint32_t ok = decode(qq, plane);
-            if (ok) atomicAdd(&lb[plane * (uint32_t)kTilePitch + qq], inc);
+            count(ok, lb0 + 4 * qq + (int)plane);
+        };
+        // the core [kC0, kC1) of the usual range [min_dist, l_seq - min_dist) of full
+        // length reads runs with no per-base range test when the wave's range covers it
+        constexpr int kC0 = 5, kC1 = kLen - 5;
+        if (ua0 <= kC0 && ub0 >= kC1) {
+            if (ua0 < kC0) {
+#pragma unroll
+                for (int qq = 0; qq < kC0; ++qq)
+                    if ((smask >> qq) & 1ull) body(qq);
+            }
+#pragma unroll
+            for (int qq = kC0; qq < kC1; ++qq) body(qq);
+            if (ub0 > kC1) {
+#pragma unroll
+                for (int qq = kC1; qq < kLen; ++qq)
+                    if ((smask >> qq) & 1ull) body(qq);
+            }
+        } else {
+#pragma unroll
+            for (int qq = 0; qq < kLen; ++qq)
+                if ((smask >> qq) & 1ull) body(qq);
         }
     } else {
         // the lane's counted query positions as a 64-bit mask: one bit test per base
@@ -1179,13 +1210,13 @@ __device__ __forceinline__ void pile_bases(bool act, int a0, int b0, int a1, int
         auto counted = [&](int qq) -> uint32_t { return ((qq < 32 ? vlo : vhi) >> (qq & 31)) & 1u; };
         const unsigned long long smask = range_mask(wq_lo, wq_hi);
         if (one_block) {
-            uint32_t* lb = base + dl0;
+            const int lb0 = 4 * (dl0 - w.w0);
 #pragma unroll
             for (int qq = 0; qq < kLen; ++qq) {
                 if (!((smask >> qq) & 1ull)) continue;
                 uint32_t plane;
                 const uint32_t ok = decode(qq, plane) & counted(qq);
-                if (ok) atomicAdd(&lb[plane * (uint32_t)kTilePitch + qq], inc);
+                count(ok, lb0 + 4 * qq + (int)plane);
             }
         } else {
 #pragma unroll
@@ -1195,7 +1226,7 @@ __device__ __forceinline__ void pile_bases(bool act, int a0, int b0, int a1, int
                 const int d = qq >= qs1 ? dl1 : dl0;
                 uint32_t plane;
                 const uint32_t ok = decode(qq, plane) & counted(qq);
-                if (ok) atomicAdd(&base[plane * (uint32_t)kTilePitch + qq + d], inc);
+                count(ok, 4 * (d - w.w0 + qq) + (int)plane);
             }
         }
     }
@@ -1306,13 +1337,14 @@ constexpr uint32_t kSeg = 65535;     // elements per tile segment (16-bit halves
 #ifndef MGP_PILEUP_WAVES
 #define MGP_PILEUP_WAVES 4
 #endif
+
 __global__ void __launch_bounds__(kBlock, MGP_PILEUP_WAVES) k_pileup(
     Geom g, PileCfg pc, const uint8_t* __restrict__ payload, const unsigned long long* __restrict__ pel,
     const uint32_t* __restrict__ O, uint32_t* __restrict__ counts, uint32_t* __restrict__ tn5,
     uint32_t* __restrict__ depth, uint32_t* __restrict__ n_reads, uint8_t* __restrict__ any_paired,
     uint32_t* __restrict__ covered, unsigned long long* __restrict__ dsum, uint32_t* __restrict__ dmax,
     uint32_t* __restrict__ tally_part, DevStats* st) {
-    extern __shared__ uint32_t tile[];  // [5][Wp]: A, C, G, T, Tn5 (fwd | rev << 16)
+    extern __shared__ __align__(16) uint32_t tile[];  // [Wp][4] A, C, G, T, then [Wp] Tn5 (fwd | rev << 16)
     uint32_t* t5 = tile + 4 * g.Wp;
     __shared__ unsigned long long wq_all[kBlock / kWave][kWaveQ];
     __shared__ uint32_t r_cov[4], r_max[4], r_keep[4];
@@ -1383,11 +1415,11 @@ __global__ void __launch_bounds__(kBlock, MGP_PILEUP_WAVES) k_pileup(
                 __builtin_amdgcn_wave_barrier();
                 if (qn >= (uint32_t)kWave) {
                     const unsigned long long qe = wq[lane];
-                    pile_read(true, (qe & GP_PACKED) != 0ull, payload + rec_at(qe), w, pc, tile, t5, max_span,
-                              span_err, pk_err);
                     qn -= kWave;
                     if ((uint32_t)lane < qn) wq[lane] = wq[kWave + lane];
                     __builtin_amdgcn_wave_barrier();
+                    pile_read(true, (qe & GP_PACKED) != 0ull, payload + rec_at(qe), w, pc, tile, t5, max_span,
+                              span_err, pk_err);
                 }
             }
             {   // tail: every lane of the wave enters, lanes past qn hold no read
@@ -1404,15 +1436,16 @@ __global__ void __launch_bounds__(kBlock, MGP_PILEUP_WAVES) k_pileup(
                     uint4 a = seg == lo ? make_uint4(0, 0, 0, 0) : cp[0];
                     uint4 b = seg == lo ? make_uint4(0, 0, 0, 0) : cp[1];
                     uint2 t = seg == lo ? make_uint2(0, 0) : reinterpret_cast<uint2*>(tn5)[P];
-                    const uint32_t x0 = tile[p], x1 = tile[g.Wp + p], x2 = tile[2 * g.Wp + p],
-                                   x3 = tile[3 * g.Wp + p], x4 = t5[p];
+                    const uint4 xb = reinterpret_cast<const uint4*>(tile)[p];
+                    const uint32_t x0 = xb.x, x1 = xb.y, x2 = xb.z, x3 = xb.w, x4 = t5[p];
                     a.x += x0 & 0xFFFFu; a.y += x0 >> 16; a.z += x1 & 0xFFFFu; a.w += x1 >> 16;
                     b.x += x2 & 0xFFFFu; b.y += x2 >> 16; b.z += x3 & 0xFFFFu; b.w += x3 >> 16;
                     t.x += x4 & 0xFFFFu; t.y += x4 >> 16;
                     cp[0] = a;
                     cp[1] = b;
                     reinterpret_cast<uint2*>(tn5)[P] = t;
-                    tile[p] = tile[g.Wp + p] = tile[2 * g.Wp + p] = tile[3 * g.Wp + p] = t5[p] = 0;
+                    reinterpret_cast<uint4*>(tile)[p] = make_uint4(0, 0, 0, 0);
+                    t5[p] = 0;
                 }
                 __syncthreads();
             }
@@ -1437,12 +1470,13 @@ __global__ void __launch_bounds__(kBlock, MGP_PILEUP_WAVES) k_pileup(
                     tf = t.x;
                     tr = t.y;
                 } else {
+                    const uint4 xb = reinterpret_cast<const uint4*>(tile)[p];
+                    reinterpret_cast<uint4*>(tile)[p] = make_uint4(0, 0, 0, 0);
+                    const uint32_t pk4[4] = {xb.x, xb.y, xb.z, xb.w};
 #pragma unroll
                     for (int x = 0; x < 4; ++x) {
-                        const uint32_t pk = tile[x * g.Wp + p];
-                        tile[x * g.Wp + p] = 0u;
-                        v[2 * x] = pk & 0xFFFFu;
-                        v[2 * x + 1] = pk >> 16;
+                        v[2 * x] = pk4[x] & 0xFFFFu;
+                        v[2 * x + 1] = pk4[x] >> 16;
                     }
                     const uint32_t pk = t5[p];
                     t5[p] = 0u;
