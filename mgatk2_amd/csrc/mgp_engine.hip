@@ -1174,26 +1174,21 @@ __device__ __forceinline__ void pile_bases(bool act, int a0, int b0, int a1, int
         const unsigned long long l = lo >= 64 ? ~0ull : ((1ull << lo) - 1ull);
         return lo < hi ? (h & ~l) : 0ull;
     };
-    if (uniform) {
-        const int lb0 = 4 * (dl0 - w.w0);
-        const unsigned long long smask = range_mask(ua0, ub0);
-        auto body = [&](int qq) {
-            uint32_t plane;
-            const uint32_t ok = decode(qq, plane);
-            count(ok, lb0 + 4 * qq + (int)plane);
-        };
-        // the core [kC0, kC1) of the usual range [min_dist, l_seq - min_dist) of full
-        // length reads runs with no per-base range test when the wave's range covers it
-        constexpr int kC0 = 5, kC1 = kLen - 5;
-        if (ua0 <= kC0 && ub0 >= kC1) {
-            if (ua0 < kC0) {
+    // the core [kC0, kC1) of the usual range [min_dist, l_seq - min_dist) of full
+    // length reads runs with no per-base range test when the wave's range covers
+    // it; bases outside it only behind a scalar bit test of the wave's range
+    constexpr int kC0 = 5, kC1 = kLen - 5;
+    auto run = [&](int lo, int hi, auto&& body) {
+        const unsigned long long smask = range_mask(lo, hi);
+        if (lo <= kC0 && hi >= kC1) {
+            if (lo < kC0) {
 #pragma unroll
                 for (int qq = 0; qq < kC0; ++qq)
                     if ((smask >> qq) & 1ull) body(qq);
             }
 #pragma unroll
             for (int qq = kC0; qq < kC1; ++qq) body(qq);
-            if (ub0 > kC1) {
+            if (hi > kC1) {
 #pragma unroll
                 for (int qq = kC1; qq < kLen; ++qq)
                     if ((smask >> qq) & 1ull) body(qq);
@@ -1203,31 +1198,34 @@ __device__ __forceinline__ void pile_bases(bool act, int a0, int b0, int a1, int
             for (int qq = 0; qq < kLen; ++qq)
                 if ((smask >> qq) & 1ull) body(qq);
         }
+    };
+    // LDS rows of the read's blocks (u32 index of query offset 0)
+    const int r0 = 4 * (dl0 - w.w0), r1 = 4 * (dl1 - w.w0);
+    if (uniform) {
+        run(ua0, ub0, [&](int qq) {
+            uint32_t plane;
+            const uint32_t ok = decode(qq, plane);
+            count(ok, r0 + 4 * qq + (int)plane);
+        });
     } else {
         // the lane's counted query positions as a 64-bit mask: one bit test per base
         const unsigned long long vm = range_mask(a0, b0) | range_mask(a1, b1);
         const uint32_t vlo = (uint32_t)vm, vhi = (uint32_t)(vm >> 32);
         auto counted = [&](int qq) -> uint32_t { return ((qq < 32 ? vlo : vhi) >> (qq & 31)) & 1u; };
-        const unsigned long long smask = range_mask(wq_lo, wq_hi);
         if (one_block) {
-            const int lb0 = 4 * (dl0 - w.w0);
-#pragma unroll
-            for (int qq = 0; qq < kLen; ++qq) {
-                if (!((smask >> qq) & 1ull)) continue;
+            run(wq_lo, wq_hi, [&](int qq) {
                 uint32_t plane;
                 const uint32_t ok = decode(qq, plane) & counted(qq);
-                count(ok, lb0 + 4 * qq + (int)plane);
-            }
+                count(ok, r0 + 4 * qq + (int)plane);
+            });
         } else {
-#pragma unroll
-            for (int qq = 0; qq < kLen; ++qq) {
-                if (!((smask >> qq) & 1ull)) continue;
-                // a block's reference offset: the second block starts at qs1
-                const int d = qq >= qs1 ? dl1 : dl0;
+            run(wq_lo, wq_hi, [&](int qq) {
+                // a block's row: the second block starts at query offset qs1
+                const int row = qq >= qs1 ? r1 : r0;
                 uint32_t plane;
                 const uint32_t ok = decode(qq, plane) & counted(qq);
-                count(ok, 4 * (d - w.w0 + qq) + (int)plane);
-            }
+                count(ok, row + 4 * qq + (int)plane);
+            });
         }
     }
 }
@@ -1262,6 +1260,14 @@ __device__ __forceinline__ void pile_line(bool has, bool packed, const uint8_t* 
             const uint32_t op = cg & 15u;
             const int len = (int)min(cg >> 4, (uint32_t)(1 << 26));
             if (op == 0 || op == 7 || op == 8) {
+                if (nb > 0 && q == qe[nb - 1] && ref - q == dl[nb - 1]) {
+                    // continues the previous block (after an I, which moves neither q
+                    // nor ref, pileup.py Q1): one block, the same counted positions
+                    qe[nb - 1] = q + len;
+                    q += len;
+                    ref += len;
+                    continue;
+                }
                 if (nb == 2) {
                     fast = false;
                     break;
