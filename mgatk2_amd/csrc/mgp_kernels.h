@@ -63,31 +63,46 @@ __device__ __forceinline__ unsigned long long lanemask_lt() {
     return lane == 0 ? 0ull : (~0ull >> (64 - lane));
 }
 
+// Wave reductions over all 64 lanes (every caller enters with the whole wave
+// active), result in every lane. They are the device library's DPP reductions
+// (row shifts + row broadcasts, then a lane read): ALU work only. A butterfly of
+// __shfl_xor is six ds_bpermute round trips through the LDS pipe.
+extern "C" __device__ uint32_t __ockl_wfred_add_u32(uint32_t);
+extern "C" __device__ uint32_t __ockl_wfred_min_u32(uint32_t);
+extern "C" __device__ uint32_t __ockl_wfred_max_u32(uint32_t);
+extern "C" __device__ uint32_t __ockl_wfred_or_u32(uint32_t);
+extern "C" __device__ int __ockl_wfred_min_i32(int);
+extern "C" __device__ int __ockl_wfred_max_i32(int);
+extern "C" __device__ unsigned long long __ockl_wfred_add_u64(unsigned long long);
+extern "C" __device__ unsigned long long __ockl_wfred_max_u64(unsigned long long);
+extern "C" __device__ unsigned long long __ockl_wfred_or_u64(unsigned long long);
+
 template <typename T>
 __device__ __forceinline__ T wave_sum(T v) {
-    for (int o = kWave / 2; o > 0; o >>= 1) v += __shfl_xor(v, o, kWave);
-    return v;
+    static_assert(sizeof(T) == 4 || sizeof(T) == 8, "wave_sum: 32- or 64-bit integers");
+    if constexpr (sizeof(T) == 4) return (T)__ockl_wfred_add_u32((uint32_t)v);  // two's complement: signed too
+    else return (T)__ockl_wfred_add_u64((unsigned long long)v);
 }
 template <typename T>
 __device__ __forceinline__ T wave_max(T v) {
-    for (int o = kWave / 2; o > 0; o >>= 1) {
-        T w = __shfl_xor(v, o, kWave);
-        v = w > v ? w : v;
+    if constexpr (sizeof(T) == 4 && T(-1) < T(0)) return (T)__ockl_wfred_max_i32((int)v);
+    else if constexpr (sizeof(T) == 4) return (T)__ockl_wfred_max_u32((uint32_t)v);
+    else {
+        static_assert(sizeof(T) == 8 && !(T(-1) < T(0)), "wave_max: 32-bit or unsigned 64-bit");
+        return (T)__ockl_wfred_max_u64((unsigned long long)v);
     }
-    return v;
 }
 template <typename T>
 __device__ __forceinline__ T wave_or(T v) {
-    for (int o = kWave / 2; o > 0; o >>= 1) v |= __shfl_xor(v, o, kWave);
-    return v;
+    static_assert(sizeof(T) == 4 || sizeof(T) == 8, "wave_or: 32- or 64-bit integers");
+    if constexpr (sizeof(T) == 4) return (T)__ockl_wfred_or_u32((uint32_t)v);
+    else return (T)__ockl_wfred_or_u64((unsigned long long)v);
 }
 template <typename T>
 __device__ __forceinline__ T wave_min(T v) {
-    for (int o = kWave / 2; o > 0; o >>= 1) {
-        T w = __shfl_xor(v, o, kWave);
-        v = w < v ? w : v;
-    }
-    return v;
+    static_assert(sizeof(T) == 4, "wave_min: 32-bit integers");
+    if constexpr (T(-1) < T(0)) return (T)__ockl_wfred_min_i32((int)v);
+    else return (T)__ockl_wfred_min_u32((uint32_t)v);
 }
 
 // splitmix64 finaliser + counter-based stream hash (synthetic generator; the
