@@ -532,13 +532,12 @@ __global__ void __launch_bounds__(kGABlock, MGP_GA_WAVES) k_group_a(int64_t n, c
                 pm &= x ? m : ~m;
             }
             if (valid[u] && (fbits[c >> 5] >> (c & 31)) & 1u) atomicMin(&first_read[c], (uint32_t)i);
-            uint32_t bef = 0;
-            if (valid[u] && (pm & lt) == 0ull) {
-                bef = my[gi];
-                my[gi] = bef + (uint32_t)__popcll(pm);
-            }
-            const int leader = pm ? __builtin_ctzll(pm) : lane;
-            rk[u] = (uint32_t)__shfl((int)bef, leader, kWave) + (uint32_t)__popcll(pm & lt);
+            // every peer reads the group's counter in one LDS read, before its leader
+            // (lowest peer) stores the bumped value: no cross-lane broadcast needed
+            const uint32_t bef = valid[u] ? my[gi] : 0u;
+            __builtin_amdgcn_wave_barrier();
+            if (valid[u] && (pm & lt) == 0ull) my[gi] = bef + (uint32_t)__popcll(pm);
+            rk[u] = bef + (uint32_t)__popcll(pm & lt);
             __builtin_amdgcn_wave_barrier();
         }
         if (MGP_ABL_A == 2) {  // ablation: no ranking, every element at its read index
