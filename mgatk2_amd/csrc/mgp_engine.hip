@@ -1724,7 +1724,11 @@ __global__ void k_check_stride(const uint64_t* __restrict__ roff, int64_t n, int
     const bool bad = i < n && r != (uint64_t)(i0 + i) * kRecStride;
     const bool wide = i < n && ((r & 63ull) != 0ull || (r >> 38) != 0ull);
     const unsigned long long b1 = __ballot(bad), b2 = __ballot(wide);
-    if ((b1 | b2) != 0ull && (threadIdx.x & 63) == 0) atomicOr(irregular, (b1 ? 1u : 0u) | (b2 ? 2u : 0u));
+    const uint32_t bits = (b1 ? 1u : 0u) | (b2 ? 2u : 0u);
+    // one atomic per wave at most, and none once the bits are set (every wave of a
+    // paired payload has irregular offsets: 3M atomics on one word took 18 ms)
+    if (bits && (threadIdx.x & 63) == 0 && (__atomic_load_n(irregular, __ATOMIC_RELAXED) & bits) != bits)
+        atomicOr(irregular, bits);
 }
 
 // ---------------------------------------------------------------------------

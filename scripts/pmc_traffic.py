@@ -16,7 +16,7 @@ root = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out"
 reads = int(sys.argv[2]) if len(sys.argv) > 2 else 200_000_000
 cells = int(sys.argv[3]) if len(sys.argv) > 3 else 10_000
 out = Path(sys.argv[4]) if len(sys.argv) > 4 else Path("profiles/pmc_traffic.json")
-layout = sys.argv[5] if len(sys.argv) > 5 else "packed"  # bench.py --record-layout of the profiled run
+layout = sys.argv[5] if len(sys.argv) > 5 else "paired"  # bench.py --record-layout of the profiled run
 acc = defaultdict(lambda: defaultdict(list))
 for f in glob.glob(f"{root}/pmc_*/**/*counter_collection.csv", recursive=True):
     with open(f) as fh:
