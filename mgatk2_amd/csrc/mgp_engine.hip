@@ -128,7 +128,7 @@ struct mgp_ctx {
 
     // run scratch
     DevBuf bin_start, H, P, cell_cnt, cell_base, bin_valid, bin_base, bucket_off, gel2, PG, F;
-    DevBuf pel, tally_part, tally;
+    DevBuf pel, tally_part, tally, bin_mspan, dup_part;
     DevBuf n_reads, any_paired, passed, covered, dsum, dmax, med_lo, med_hi, first_read;
     DevBuf counts, tn5, depth, stats;
 
@@ -205,10 +205,11 @@ __global__ void __launch_bounds__(kHistBlock) k_bin_count(const int32_t* __restr
                                                           int slice_cells, uint32_t* __restrict__ H,
                                                           uint32_t* __restrict__ PG, int ngroups,
                                                           uint32_t* __restrict__ bin_lo,
-                                                          uint32_t* __restrict__ bin_valid, DevStats* st) {
+                                                          uint32_t* __restrict__ bin_valid,
+                                                          uint32_t* __restrict__ bin_mspan, DevStats* st) {
     extern __shared__ uint32_t hist[];  // [slice cells] counts, then cum[slice groups]
     __shared__ int64_t s_range[2];
-    __shared__ uint32_t s_nvalid;
+    __shared__ uint32_t s_nvalid, s_mspan;
     const int b = blockIdx.x;
     const bool first = blockIdx.y == 0;
     const int nc = g.nc;
@@ -220,7 +221,7 @@ __global__ void __launch_bounds__(kHistBlock) k_bin_count(const int32_t* __restr
     uint32_t* row = H + (size_t)b * nc;
     if (threadIdx.x < 2) s_range[threadIdx.x] = lower_bound_start(start, n, bin_threshold(b + threadIdx.x, g));
     for (int c = threadIdx.x; c < ncs; c += blockDim.x) hist[c] = 0;
-    if (threadIdx.x == 0) s_nvalid = 0;
+    if (threadIdx.x == 0) s_nvalid = s_mspan = 0;
     __syncthreads();
     const int64_t blo = s_range[0], bhi = max(s_range[1], blo);
     if (first && threadIdx.x == 0) {
@@ -287,17 +288,19 @@ __global__ void __launch_bounds__(kHistBlock) k_bin_count(const int32_t* __restr
     mspan = wave_max(mspan);
     nvalid = wave_sum(nvalid);
     const bool anybad = __ballot(badbc) != 0ull, anyuns = __ballot(unsorted) != 0ull;
+    // per-bin results (k_run_stats reduces them): a global atomic per wave on one
+    // word serialises at the memory side
     if (lane == 0) {
-        if (mspan) atomicMax(&st->max_span, mspan);
-        if (nvalid) {
-            atomicAdd(&st->valid, nvalid);
-            atomicAdd(&s_nvalid, (uint32_t)nvalid);
-        }
+        if (mspan) atomicMax(&s_mspan, mspan);
+        if (nvalid) atomicAdd(&s_nvalid, (uint32_t)nvalid);
         if (anybad) atomicOr(&st->err, ERR_BADBC);
         if (anyuns) atomicOr(&st->err, ERR_UNSORTED);
     }
     __syncthreads();
-    if (threadIdx.x == 0) bin_valid[b] = s_nvalid;
+    if (threadIdx.x == 0) {
+        bin_valid[b] = s_nvalid;
+        bin_mspan[b] = s_mspan;
+    }
 }
 
 // Scan step a: column sums over blocks of RB rows. grid (ceil(nc/256), nrb)
@@ -712,7 +715,7 @@ __global__ void __launch_bounds__(kBlock, MGP_GB_WAVES) k_group_b(const GElem* _
                                                     const uint32_t* __restrict__ bucket_off,
                                                     const uint32_t* __restrict__ O, Geom g, int ngroups, int rb,
                                                     int mode, unsigned long long* __restrict__ pel,
-                                                    DevStats* st) {
+                                                    unsigned long long* __restrict__ dup_part, DevStats* st) {
     __shared__ GElem stage[kStageB];
     __shared__ uint32_t wcnt[kBlock / kWave][kGroup];
     __shared__ uint32_t cbase[kGroup], cstart[kGroup + 1];
@@ -919,10 +922,18 @@ __global__ void __launch_bounds__(kBlock, MGP_GB_WAVES) k_group_b(const GElem* _
         be = nbe;
         tot = ntot;
     }
+    // per-workgroup duplicate counts (k_run_stats sums them)
     const unsigned long long d2 = wave_sum(acc.d2), d3 = wave_sum(acc.d3);
+    __shared__ unsigned long long s_dup[2][kBlock / kWave];
     if (lane == 0) {
-        if (d2) atomicAdd(&st->dup_pos, d2);
-        if (d3) atomicAdd(&st->dup_len, d3);
+        s_dup[0][wid] = d2;
+        s_dup[1][wid] = d3;
+    }
+    __syncthreads();
+    if (threadIdx.x < 2) {
+        unsigned long long t = 0;
+        for (int w = 0; w < kBlock / kWave; ++w) t += s_dup[threadIdx.x][w];
+        dup_part[2 * ((size_t)blockIdx.y * gridDim.x + blockIdx.x) + threadIdx.x] = t;
     }
 }
 
@@ -1615,10 +1626,6 @@ __global__ void __launch_bounds__(kBlock) k_median(Geom g, int min_reads, const 
     const uint32_t n = covered[c];
     const uint32_t nr = n_reads[c];
     const bool pass = n > 0 && nr >= (uint32_t)max(1, min_reads);
-    if (threadIdx.x == 0 && nr) {
-        atomicAdd(&st->filtered, (unsigned long long)nr);
-        atomicAdd(&st->n_barcodes, 1ull);
-    }
     if (!pass) {
         if (threadIdx.x == 0) {
             med_lo[c] = 0;
@@ -1691,7 +1698,65 @@ __global__ void __launch_bounds__(kBlock) k_median(Geom g, int min_reads, const 
         med_lo[c] = lo0;
         med_hi[c] = hi0;
         passed[c] = 1;
-        atomicAdd(&st->cells_passed, 1ull);
+    }
+}
+
+// Run statistics from per-bin / per-workgroup / per-cell partials (one workgroup
+// of 1024 threads): which=0 after the histogram: max_span (the pileup's halo);
+// which=1 at the end: kept reads, barcodes with a kept read, passing cells and
+// the two duplicate counters (readers.py:141-144,193-199, processors.py:22).
+__global__ void __launch_bounds__(1024) k_run_stats(int which, const uint32_t* __restrict__ bin_mspan, int nbins,
+                                                    const uint32_t* __restrict__ n_reads,
+                                                    const uint8_t* __restrict__ passed, int nc,
+                                                    const unsigned long long* __restrict__ dup_part, int nparts,
+                                                    DevStats* st) {
+    __shared__ unsigned long long red[5][1024 / kWave];
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    unsigned long long a = 0, b = 0, c = 0, d = 0, e = 0;
+    if (which == 0) {
+        uint32_t m = 0;
+        for (int i = threadIdx.x; i < nbins; i += 1024) m = max(m, bin_mspan[i]);
+        m = wave_max(m);
+        if (lane == 0) red[0][wid] = m;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            uint32_t t = 0;
+            for (int w = 0; w < 1024 / kWave; ++w) t = max(t, (uint32_t)red[0][w]);
+            st->max_span = t;
+        }
+        return;
+    }
+    for (int i = threadIdx.x; i < nc; i += 1024) {
+        const uint32_t r = n_reads[i];
+        a += r;
+        b += r != 0u;
+        c += passed[i] != 0;
+    }
+    for (int i = threadIdx.x; i < nparts; i += 1024) {
+        d += dup_part[2 * (size_t)i];
+        e += dup_part[2 * (size_t)i + 1];
+    }
+    a = wave_sum(a);
+    b = wave_sum(b);
+    c = wave_sum(c);
+    d = wave_sum(d);
+    e = wave_sum(e);
+    if (lane == 0) {
+        red[0][wid] = a;
+        red[1][wid] = b;
+        red[2][wid] = c;
+        red[3][wid] = d;
+        red[4][wid] = e;
+    }
+    __syncthreads();
+    if (threadIdx.x < 5) {
+        unsigned long long t = 0;
+        for (int w = 0; w < 1024 / kWave; ++w) t += red[threadIdx.x][w];
+        if (threadIdx.x == 0) st->filtered = t;
+        else if (threadIdx.x == 1) st->n_barcodes = t;
+        else if (threadIdx.x == 2) st->cells_passed = t;
+        else if (threadIdx.x == 3) st->dup_pos = t;
+        else st->dup_len = t;
     }
 }
 
@@ -1862,7 +1927,7 @@ void mgp_close(mgp_ctx* ctx) {
     if (ctx->comm) ncclCommDestroy(ctx->comm);
     DevBuf* bufs[] = {&ctx->start,     &ctx->bc,        &ctx->tlen,     &ctx->flag,       &ctx->mapq,
                       &ctx->span,      &ctx->roff,      &ctx->payload,  &ctx->bin_start,  &ctx->gel2,
-                      &ctx->roff32,    &ctx->roff_irregular,
+                      &ctx->roff32,    &ctx->roff_irregular, &ctx->bin_mspan, &ctx->dup_part,
                       &ctx->H,         &ctx->P,         &ctx->cell_cnt, &ctx->cell_base,  &ctx->pel,
                       &ctx->PG,        &ctx->F,
                       &ctx->tally_part, &ctx->tally,   &ctx->n_reads,    &ctx->any_paired,
@@ -1971,6 +2036,7 @@ static int ensure_run_buffers(mgp_ctx* ctx) {
     MGP_TRY(ctx->pel.ensure(n * 8));
     MGP_TRY(ctx->gel2.ensure(n * sizeof(GElem)));
     MGP_TRY(ctx->bin_valid.ensure((size_t)(g.nbins + 1) * 4));
+    MGP_TRY(ctx->bin_mspan.ensure((size_t)(g.nbins + 1) * 4));
     MGP_TRY(ctx->bin_base.ensure((size_t)(g.nbins + 1) * 4));
     MGP_TRY(ctx->bucket_off.ensure((size_t)g.nbins * ((nc + kGroup - 1) / kGroup + 1) * 4));
     MGP_TRY(ctx->tally_part.ensure((size_t)std::max(g.nchunks, 1) * L * 16));
@@ -2040,7 +2106,10 @@ int mgp_run(mgp_ctx* ctx) {
             k_bin_count<<<dim3((unsigned)g.nbins, (unsigned)nslices), kHistBlock, lds, s>>>(
                 ctx->start.as<int32_t>(), ctx->bc.as<int32_t>(), ctx->flag.as<uint16_t>(), ctx->span.as<uint32_t>(),
                 n, g, slice, ctx->H.as<uint32_t>(), ctx->PG.as<uint32_t>(), ngroups, ctx->bin_start.as<uint32_t>(),
-                ctx->bin_valid.as<uint32_t>(), st);
+                ctx->bin_valid.as<uint32_t>(), ctx->bin_mspan.as<uint32_t>(), st);
+            HIP_TRY(hipGetLastError());
+            k_run_stats<<<1, 1024, 0, s>>>(0, ctx->bin_mspan.as<uint32_t>(), g.nbins, nullptr, nullptr, 0, nullptr, 0,
+                                           st);
             HIP_TRY(hipGetLastError());
         }
         STAGE_END(ST_HIST);
@@ -2088,6 +2157,7 @@ int mgp_run(mgp_ctx* ctx) {
         STAGE_BEGIN(ST_GROUP_B);
         if (MGP_ABL_A == 1) HIP_TRY(hipMemsetAsync(ctx->gel2.p, 0, (size_t)n * sizeof(GElem), s));  // ablation
         if (MGP_ABL_B >= 2) HIP_TRY(hipMemsetAsync(ctx->pel.p, 0, (size_t)n * 8, s));  // ablation: nothing piles
+        int dup_parts = 0;
         if (n > 0) {
             // about MGP_GB_WG workgroups (many per slot: 4 fit a CU, so a grid of a few
             // slot-rounds leaves a tail); bins per workgroup at most kMaxRbB, whose
@@ -2095,9 +2165,12 @@ int mgp_run(mgp_ctx* ctx) {
             const int64_t tgt = MGP_GB_WG;
             const int rb = std::min(kMaxRbB, std::max(1, (int)(((int64_t)ngroups * g.nbins + tgt - 1) / tgt)));
             dim3 gb((unsigned)ngroups, (unsigned)((g.nbins + rb - 1) / rb));
+            dup_parts = (int)(gb.x * gb.y);
+            MGP_TRY(ctx->dup_part.ensure((size_t)dup_parts * 16));
             k_group_b<<<gb, kBlock, 0, s>>>(ctx->gel2.as<GElem>(), ctx->bucket_off.as<uint32_t>(), ctx->H.as<uint32_t>(),
                                             g, ngroups, rb, ctx->cfg.dedup_mode,
-                                            ctx->pel.as<unsigned long long>(), st);
+                                            ctx->pel.as<unsigned long long>(),
+                                            ctx->dup_part.as<unsigned long long>(), st);
             HIP_TRY(hipGetLastError());
         }
         STAGE_END(ST_GROUP_B);
@@ -2160,6 +2233,9 @@ int mgp_run(mgp_ctx* ctx) {
         dim3 gt(blocks_for((int64_t)g.L * 4), (unsigned)std::max(1, std::min(g.nchunks, 32)));
         k_tally_reduce<<<gt, kBlock, 0, s>>>(ctx->tally_part.as<uint32_t>(), g.nchunks, g.L * 4,
                                              ctx->tally.as<unsigned long long>());
+        HIP_TRY(hipGetLastError());
+        k_run_stats<<<1, 1024, 0, s>>>(1, nullptr, 0, ctx->n_reads.as<uint32_t>(), ctx->passed.as<uint8_t>(), nc,
+                                       ctx->dup_part.as<unsigned long long>(), dup_parts, st);
         HIP_TRY(hipGetLastError());
         STAGE_END(ST_TALLY);
     } else {
