@@ -723,9 +723,21 @@ int mgp_bam_read_ref(mgp_bam* b, int tid, int rec_align, mgp_bam_batch* out) {
     std::vector<uint32_t> ncg;  // CIGAR operations (CG tag resolved)
     std::vector<const uint8_t*> cgp;
     std::vector<uint8_t> pkd;   // record is written in the packed layout
-    // one record: decode + pack at index k / payload offset off
+    // producer placement (mgp_place_records' rule, applied batch by batch as records
+    // stream in): open[key] = the line of cell `key` whose second half is free;
+    // key n_cells collects the reads the engine's filters drop
+    const bool paired = b->placement == MGP_PLACE_PAIRED;
+    int32_t n_keys = 0;
+    if (paired) {
+        for (int32_t v : b->wl.vals) n_keys = std::max(n_keys, v + 1);
+        if (b->bulk_cell >= 0) n_keys = std::max(n_keys, b->bulk_cell + 1);
+    }
+    std::vector<uint64_t> open(paired ? (size_t)n_keys + 1 : 0, ~0ull);
+    uint64_t cursor = 0;  // paired: payload bytes placed so far (128-byte lines)
+    // one record: decode (do_fields: the SoA columns, barcode lookup included) and
+    // pack (do_rec: the payload record at offset off) at index k
     auto decode = [&](const uint8_t* r, uint32_t bs, size_t k, uint64_t off, uint32_t n_cig, const uint8_t* cig,
-                      bool pk, int64_t& tags, int64_t& first, int64_t gidx) {
+                      bool pk, int64_t& tags, int64_t& first, int64_t gidx, bool do_fields, bool do_rec) {
         const uint8_t* end = r + bs;
         const int32_t pos = rdi32(r + 4);
         const uint8_t l_name = r[8];
@@ -736,34 +748,44 @@ int mgp_bam_read_ref(mgp_bam* b, int tid, int rec_align, mgp_bam_batch* out) {
         const uint8_t* seqp = r + 32 + l_name + 4 * (size_t)rd16(r + 12);
         const uint8_t* qualp = seqp + ((size_t)l_seq + 1) / 2;
         const uint8_t* auxp = qualp + l_seq;
-        Aux aux{auxp, end};
-        int32_t bcv = -1;
-        const uint8_t* t = aux.find(b->tag);
-        if (t) {
-            ++tags;
-            if (first < 0) first = gidx;
-            if (t[0] == 'Z' || t[0] == 'H') {  // get_tag() -> str; numeric tags never match
-                const char* sv = (const char*)t + 1;
-                bcv = b->wl.get(sv, std::strlen(sv));
-            } else if (t[0] == 'A') {
-                bcv = b->wl.get((const char*)t + 1, 1);
-            }
-        }
-        if (b->bulk_cell >= 0) bcv = b->bulk_cell;
         uint16_t fl = flg & 0x0FFF;
         if (l_seq == 0 || qualp[0] == 0xFF) fl |= MGP_FLAG_NOSEQQUAL;
+        if (pk) fl |= MGP_FLAG_PACKED;
+        if (do_fields) {
+            Aux aux{auxp, end};
+            int32_t bcv = -1;
+            const uint8_t* t = aux.find(b->tag);
+            if (t) {
+                ++tags;
+                if (first < 0) first = gidx;
+                if (t[0] == 'Z' || t[0] == 'H') {  // get_tag() -> str; numeric tags never match
+                    const char* sv = (const char*)t + 1;
+                    bcv = b->wl.get(sv, std::strlen(sv));
+                } else if (t[0] == 'A') {
+                    bcv = b->wl.get((const char*)t + 1, 1);
+                }
+            }
+            if (b->bulk_cell >= 0) bcv = b->bulk_cell;
+            G_start.p[k] = pos;
+            G_bc.p[k] = bcv;
+            G_tlen.p[k] = tl;
+            G_flag.p[k] = fl;
+            G_mapq.p[k] = mq;
+            G_span.p[k] = std::max(cigar_ref_span(cig, n_cig), l_seq);
+            G_roff.p[k] = off;
+        }
+        if (!do_rec) return;
         uint8_t* rec = G_pay.p + off;
         if (pk) {
             uint32_t cw[4] = {0, 0, 0, 0};
             for (uint32_t q = 0; q < n_cig; ++q) cw[q] = rd32(cig + 4 * q);
-            fl |= MGP_FLAG_PACKED;
             const uint64_t size = ((uint64_t)MGP_PACK_BYTES + amask) & ~amask;
-            std::memset(rec, 0, size);
-            mgp_pack_record(pos, l_seq, fl, n_cig, cw, seqp, qualp, rec);
+            if (size > MGP_PACK_BYTES && !paired) std::memset(rec + MGP_PACK_BYTES, 0, size - MGP_PACK_BYTES);
+            mgp_pack_record(pos, l_seq, fl, n_cig, cw, seqp, qualp, rec);  // writes all 64 bytes
         } else {
             const uint32_t soff = mgp_seq_offset(l_seq);
             const uint32_t coff = mgp_cigar_offset(l_seq);
-            const uint64_t size = ((uint64_t)coff + 4ull * n_cig + amask) & ~amask;
+            const uint64_t size = ((uint64_t)coff + 4ull * n_cig + (paired ? 127u : amask)) & ~(paired ? 127ull : amask);
             std::memset(rec, 0, size);
             std::memcpy(rec, &pos, 4);
             std::memcpy(rec + 4, &l_seq, 4);
@@ -777,13 +799,6 @@ int mgp_bam_read_ref(mgp_bam* b, int tid, int rec_align, mgp_bam_batch* out) {
             }
             if (n_cig) std::memcpy(rec + coff, cig, 4 * (size_t)n_cig);
         }
-        G_start.p[k] = pos;
-        G_bc.p[k] = bcv;
-        G_tlen.p[k] = tl;
-        G_flag.p[k] = fl;
-        G_mapq.p[k] = mq;
-        G_span.p[k] = std::max(cigar_ref_span(cig, n_cig), l_seq);
-        G_roff.p[k] = off;
     };
     const int rc = for_each_batch(b, tid, [&](const std::vector<const uint8_t*>& recs,
                                               const std::vector<uint32_t>& sizes) -> int {
@@ -819,32 +834,73 @@ int mgp_bam_read_ref(mgp_bam* b, int tid, int rec_align, mgp_bam_batch* out) {
             cgp[i] = cig;
             const uint8_t* qualp = cigp + 4 * (size_t)rd16(r + 12) + ((size_t)l_seq + 1) / 2;
             pkd[i] = b->pack && bam_packable(rdi32(r + 4), rd16(r + 14), l_seq, n_cig, cig, qualp);
+            const uint64_t rb = pkd[i] ? (uint64_t)MGP_PACK_BYTES : (uint64_t)mgp_cigar_offset(l_seq) + 4ull * n_cig;
+            if (paired) {  // record bytes; the offsets follow the barcodes (pass 1b)
+                rsz[i] = rb;
+                continue;
+            }
             const uint64_t off = (G_pay.n + tot + amask) & ~amask;  // records are rec_align-sized
             rsz[i] = off;
-            const uint64_t rb = pkd[i] ? (uint64_t)MGP_PACK_BYTES : (uint64_t)mgp_cigar_offset(l_seq) + 4ull * n_cig;
             tot = off - G_pay.n + ((rb + amask) & ~amask);
         }
         const size_t k0 = G_start.n;
         const size_t kn = k0 + m;
         if (!G_start.reserve(kn) || !G_bc.reserve(kn) || !G_tlen.reserve(kn) || !G_flag.reserve(kn) ||
-            !G_mapq.reserve(kn) || !G_span.reserve(kn) || !G_roff.reserve(kn) || !G_pay.reserve(G_pay.n + tot + 256))
+            !G_mapq.reserve(kn) || !G_span.reserve(kn) || !G_roff.reserve(kn) ||
+            (!paired && !G_pay.reserve(G_pay.n + tot + 256)))
             return fail("out of host memory"), -1;
         const double tp2 = now_s();
         t_p1 += tp2 - tp1;
-        // pass 2 (parallel): decode + pack
+        // pass 2 (parallel): decode + pack; paired: the columns first, then the
+        // placement from the barcodes (pass 1b, sequential), then the records
         const int tn = (int)std::max<size_t>(1, std::min<size_t>((size_t)nt, m / 4096 + 1));
         std::vector<int64_t> tags((size_t)tn, 0), firsts((size_t)tn, -1);
-        auto work = [&](int t) {
-            const size_t lo = m * (size_t)t / (size_t)tn, hi = m * (size_t)(t + 1) / (size_t)tn;
-            for (size_t i = lo; i < hi; ++i)
-                decode(recs[i], sizes[i], k0 + i, rsz[i], ncg[i], cgp[i], pkd[i] != 0, tags[(size_t)t],
-                       firsts[(size_t)t],
-                       (int64_t)(k0 + i));
+        auto run_pass = [&](bool do_fields, bool do_rec) {
+            auto work = [&](int t) {
+                const size_t lo = m * (size_t)t / (size_t)tn, hi = m * (size_t)(t + 1) / (size_t)tn;
+                for (size_t i = lo; i < hi; ++i)
+                    decode(recs[i], sizes[i], k0 + i, paired ? G_roff.p[k0 + i] : rsz[i], ncg[i], cgp[i],
+                           pkd[i] != 0, tags[(size_t)t], firsts[(size_t)t], (int64_t)(k0 + i), do_fields, do_rec);
+            };
+            std::vector<std::thread> th;
+            for (int t = 1; t < tn; ++t) th.emplace_back(work, t);
+            work(0);
+            for (auto& x : th) x.join();
         };
-        std::vector<std::thread> th;
-        for (int t = 1; t < tn; ++t) th.emplace_back(work, t);
-        work(0);
-        for (auto& x : th) x.join();
+        if (!paired) {
+            run_pass(true, true);
+        } else {
+            run_pass(true, false);
+            // pass 1b: which half-line each record takes (mgp_place_records' rule)
+            const uint64_t cur0 = cursor;
+            const uint16_t drop = MGP_FLAG_UNMAPPED | MGP_FLAG_SECONDARY | MGP_FLAG_SUPPLEMENTARY;
+            for (size_t i = 0; i < m; ++i) {
+                const size_t k = k0 + i;
+                if (!pkd[i]) {
+                    cursor = (cursor + 127) & ~127ull;
+                    G_roff.p[k] = cursor;
+                    cursor += (rsz[i] + 127) & ~127ull;
+                    continue;
+                }
+                const int32_t c = G_bc.p[k];
+                size_t key = (c >= 0 && c < n_keys && !(G_flag.p[k] & drop)) ? (size_t)c : (size_t)n_keys;
+                if (open[key] != ~0ull) {
+                    G_roff.p[k] = open[key] + MGP_PACK_BYTES;
+                    open[key] = ~0ull;
+                } else {
+                    cursor = (cursor + 127) & ~127ull;
+                    G_roff.p[k] = open[key] = cursor;
+                    cursor += 128;
+                }
+            }
+            if (!G_pay.reserve(cursor + 256)) return fail("out of host memory"), -1;
+            // second halves of lines opened in this batch that stay open: zero (a
+            // later batch may still fill them; lines closed here are fully written)
+            for (uint64_t o : open)
+                if (o != ~0ull && o >= cur0) std::memset(G_pay.p + o + MGP_PACK_BYTES, 0, MGP_PACK_BYTES);
+            run_pass(false, true);
+            tot = cursor - G_pay.n;
+        }
         for (int t = 0; t < tn; ++t) {
             n_tag += tags[(size_t)t];
             if (first_tag < 0 && firsts[(size_t)t] >= 0) first_tag = firsts[(size_t)t];
@@ -865,56 +921,6 @@ int mgp_bam_read_ref(mgp_bam* b, int tid, int rec_align, mgp_bam_batch* out) {
     if (rc != 0) {
         release();
         return -1;
-    }
-    // producer placement (mgp_place_records): the records decoded in BAM order are
-    // moved to their places, a parallel copy into a zero-filled (calloc) payload
-    if (b->placement == MGP_PLACE_PAIRED && G_start.n) {
-        const double tpl = now_s();
-        const size_t n = G_start.n;
-        std::vector<uint32_t> sz;
-        Grow<uint64_t> nro;
-        if (!nro.reserve(n)) {
-            release();
-            return fail("out of host memory");
-        }
-        int32_t maxbc = -1;
-        try {
-            sz.resize(n);
-        } catch (const std::bad_alloc&) {
-            std::free(nro.p);
-            release();
-            return fail("out of host memory");
-        }
-        for (size_t i = 0; i < n; ++i) {
-            sz[i] = mgp_record_bytes(G_pay.p + G_roff.p[i], G_flag.p[i]);
-            maxbc = std::max(maxbc, G_bc.p[i]);
-        }
-        const int64_t tot = mgp_place_records((int64_t)n, G_bc.p, G_flag.p, sz.data(), maxbc + 1, MGP_PLACE_PAIRED,
-                                              rec_align, nro.p);
-        uint8_t* np = tot >= 0 ? (uint8_t*)std::calloc((size_t)tot + 256, 1) : nullptr;
-        if (!np) {
-            std::free(nro.p);
-            release();
-            return fail(tot < 0 ? "record placement failed" : "out of host memory");
-        }
-        const int tn = (int)std::max<size_t>(1, std::min<size_t>((size_t)nt, n / 65536 + 1));
-        auto work = [&](int t) {
-            const size_t lo = n * (size_t)t / (size_t)tn, hi = n * (size_t)(t + 1) / (size_t)tn;
-            for (size_t i = lo; i < hi; ++i) std::memcpy(np + nro.p[i], G_pay.p + G_roff.p[i], sz[i]);
-        };
-        std::vector<std::thread> th;
-        for (int t = 1; t < tn; ++t) th.emplace_back(work, t);
-        work(0);
-        for (auto& x : th) x.join();
-        std::free(G_pay.p);
-        std::free(G_roff.p);
-        G_pay.p = np;
-        G_pay.n = (size_t)tot;
-        G_pay.cap = (size_t)tot + 256;
-        G_roff.p = nro.p;
-        G_roff.cap = nro.cap;
-        if (std::getenv("MGP_HOST_PROFILE"))
-            std::fprintf(stderr, "[mgp_bam_read_ref] paired placement %.3f s\n", now_s() - tpl);
     }
     // at least one element everywhere; >= 256 bytes of payload slack for vector over-reads
     if (!G_start.reserve(1) || !G_bc.reserve(1) || !G_tlen.reserve(1) || !G_flag.reserve(1) ||
