@@ -1149,6 +1149,14 @@ __device__ __forceinline__ void pile_bases(bool act, int a0, int b0, int a1, int
         if (MGP_BL) atomicAdd(&tile[ok ? (uint32_t)idx : (uint32_t)(threadIdx.x & 63)], ok ? inc : 0u);
         else if (ok) atomicAdd(&tile[idx], inc);
     };
+    // the same with the query offset outside the select: a lane that does not count
+    // adds 0 at its own slot + 4 qq (tile rows 0..80, inside the tile), so 16 qq bytes
+    // become the atomic's immediate offset and the row select is one pointer select
+    uint32_t* const own = tile + (threadIdx.x & 63);
+    auto count_q = [&](uint32_t ok, uint32_t* rowp, int qq) {
+        uint32_t* const p = ok ? rowp : own;
+        atomicAdd(p + 4 * qq, ok ? inc : 0u);
+    };
     const int minbq = pc.min_baseq;
     // packed: counted iff qual << 2 | b lies in [4 * max(min_baseq, 0), 252) (0xFF and
     // anything >= 252 are never counted; packed quals are <= 62)
@@ -1211,11 +1219,13 @@ __device__ __forceinline__ void pile_bases(bool act, int a0, int b0, int a1, int
     };
     // LDS rows of the read's blocks (u32 index of query offset 0)
     const int r0 = 4 * (dl0 - w.w0), r1 = 4 * (dl1 - w.w0);
+    uint32_t* const r0p = tile + r0;
+    uint32_t* const r1p = tile + r1;
     if (uniform) {
         run(ua0, ub0, [&](int qq) {
             uint32_t plane;
             const uint32_t ok = decode(qq, plane);
-            count(ok, r0 + 4 * qq + (int)plane);
+            count_q(ok, r0p + plane, qq);
         });
     } else {
         // the lane's counted query positions as a 64-bit mask: one bit test per base
@@ -1226,15 +1236,15 @@ __device__ __forceinline__ void pile_bases(bool act, int a0, int b0, int a1, int
             run(wq_lo, wq_hi, [&](int qq) {
                 uint32_t plane;
                 const uint32_t ok = decode(qq, plane) & counted(qq);
-                count(ok, r0 + 4 * qq + (int)plane);
+                count_q(ok, r0p + plane, qq);
             });
         } else {
             run(wq_lo, wq_hi, [&](int qq) {
                 // a block's row: the second block starts at query offset qs1
-                const int row = qq >= qs1 ? r1 : r0;
+                uint32_t* const rowp = qq >= qs1 ? r1p : r0p;
                 uint32_t plane;
                 const uint32_t ok = decode(qq, plane) & counted(qq);
-                count(ok, row + 4 * qq + (int)plane);
+                count_q(ok, rowp + plane, qq);
             });
         }
     }
