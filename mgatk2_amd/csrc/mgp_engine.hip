@@ -962,10 +962,13 @@ struct Win {
 // bases with one 16-byte load.
 __device__ __forceinline__ uint32_t strand_inc(int strand) { return strand ? 0x10000u : 1u; }
 
-__device__ __forceinline__ void tn5_cut(int32_t start, uint32_t lseq, int strand, const Win& w, uint32_t* t5) {
-    // pileup.py:43-50: reverse reads cut at start + len(seq) - 1
+__device__ __forceinline__ void tn5_cut(bool has, int32_t start, uint32_t lseq, int strand, const Win& w,
+                                        uint32_t* t5) {
+    // pileup.py:43-50: reverse reads cut at start + len(seq) - 1. Branch-free: a
+    // lane whose cut is elsewhere adds 0 to slot 0
     const int64_t cut = strand ? (int64_t)start + lseq - 1 : (int64_t)start;
-    if (cut >= w.w0 && cut < (int64_t)w.w0 + w.wlen) atomicAdd(&t5[(int)(cut - w.w0)], strand_inc(strand));
+    const bool in = has && cut >= w.w0 && cut < (int64_t)w.w0 + w.wlen;
+    atomicAdd(&t5[in ? (int)(cut - w.w0) : 0], in ? strand_inc(strand) : 0u);
 }
 
 // Generic path (any read): CIGAR walk with byte loads (pileup.py:55-95).
@@ -1028,9 +1031,6 @@ constexpr uint32_t kValid = 0x0116u;   // codes 1, 2, 4, 8 are counted (pileup.p
 // register index is static. Other reads take the generic byte-load path.
 #ifndef MGP_ABL
 #define MGP_ABL 0  // ablation switch for experiments: 0 = real kernel
-#endif
-#ifndef MGP_BL
-#define MGP_BL 1  // branch-free per-base counting (A/B: masked atomics 0.4 ms slower)
 #endif
 // The first 128-byte line of a record in registers: header, qual (+16), seq (+80)
 // and CIGAR (+112) of a read of <= 64 bases with <= 4 operations
@@ -1143,13 +1143,7 @@ __device__ __forceinline__ void pile_bases(bool act, int a0, int b0, int a1, int
         }
     }
     const uint32_t sw[8] = {R.sv[0].x, R.sv[0].y, R.sv[0].z, R.sv[0].w, R.sv[1].x, R.sv[1].y, R.sv[1].z, R.sv[1].w};
-    // one count at tile[idx] when ok; MGP_BL: branch-free, a lane that does not count
-    // adds 0 to a slot of its own instead of being masked off
-    auto count = [&](uint32_t ok, int idx) {
-        if (MGP_BL) atomicAdd(&tile[ok ? (uint32_t)idx : (uint32_t)(threadIdx.x & 63)], ok ? inc : 0u);
-        else if (ok) atomicAdd(&tile[idx], inc);
-    };
-    // the same with the query offset outside the select: a lane that does not count
+    // one count at rowp[4 qq] when ok, branch-free: a lane that does not count
     // adds 0 at its own slot + 4 qq (tile rows 0..80, inside the tile), so 16 qq bytes
     // become the atomic's immediate offset and the row select is one pointer select
     uint32_t* const own = tile + (threadIdx.x & 63);
@@ -1263,63 +1257,56 @@ __device__ __forceinline__ void pile_line(bool has, bool packed, const uint8_t* 
     const int strand = packed ? (int)((h.y >> 15) & 1u) : (((h.z >> 16) & MGP_FLAG_REVERSE) ? 1 : 0);
     const uint32_t cigw[4] = {packed ? (h.y >> 16) : cv.x, packed ? (h.z & 0xFFFFu) : cv.y,
                               packed ? (h.z >> 16) : cv.z, packed ? (h.w & 0xFFFFu) : cv.w};
-    if (has) tn5_cut(start, lseq, strand, w, t5);
+    tn5_cut(has, start, lseq, strand, w, t5);
 
     bool fast = has && lseq <= (uint32_t)(packed ? MGP_PACK_MAX_LEN : kFastLen) && ncig <= (uint32_t)kFastCig &&
                 start >= -(1 << 28) && start < (1 << 28);
-    int qs1 = 1 << 30, dl0 = 0, dl1 = 0;
-    int a0 = 0, b0 = 0, a1 = 0, b1 = 0;
-    if (fast) {
-        int qs[2] = {0, 1 << 30}, qe[2] = {0, 1 << 30}, dl[2] = {0, 0};
-        int nb = 0;
-        int ref = start, q = 0;
+    // The CIGAR as at most two aligned blocks, straight-line code (per-lane
+    // branches on the operation would be exec-mask branches for every op of every
+    // read). Block k covers query [qs_k, qe_k) at reference q + d_k. An aligned op
+    // that continues the last block (same q and reference offset: after an I,
+    // which moves neither, pileup.py Q1) extends it; a third block leaves the
+    // register path.
+    int qs0 = 0, qe0 = 0, d0 = 0, qs1 = 1 << 30, qe1 = 1 << 30, d1 = 0;
+    int nb = 0, ref = start, q = 0;
+    bool over = false;
 #pragma unroll
-        for (int o = 0; o < kFastCig; ++o) {
-            if ((uint32_t)o >= ncig) break;
-            const uint32_t cg = cigw[o];
-            const uint32_t op = cg & 15u;
-            const int len = (int)min(cg >> 4, (uint32_t)(1 << 26));
-            if (op == 0 || op == 7 || op == 8) {
-                if (nb > 0 && q == qe[nb - 1] && ref - q == dl[nb - 1]) {
-                    // continues the previous block (after an I, which moves neither q
-                    // nor ref, pileup.py Q1): one block, the same counted positions
-                    qe[nb - 1] = q + len;
-                    q += len;
-                    ref += len;
-                    continue;
-                }
-                if (nb == 2) {
-                    fast = false;
-                    break;
-                }
-                qs[nb] = q;
-                qe[nb] = q + len;
-                dl[nb] = ref - q;
-                ++nb;
-                q += len;
-                ref += len;
-            } else if (op == 2 || op == 3) {
-                ref += len;
-            } else if (op == 4) {
-                q += len;
-            }
-        }
-        if (fast) {
-            if (max(ref - start, (int)lseq) > (int)max_span) span_err = true;
-            const int vq0 = pc.min_dist > 0 ? pc.min_dist : 0;
-            const int vq1 = min((int)lseq, pc.min_dist > 0 ? (int)lseq - pc.min_dist : (int)lseq);
-            const int wlo = w.w0, whi = w.w0 + w.wlen;
-            a0 = max(max(qs[0], vq0), wlo - dl[0]);
-            b0 = min(min(qe[0], vq1), whi - dl[0]);
-            a1 = max(max(qs[1], vq0), wlo - dl[1]);
-            b1 = min(min(qe[1], vq1), whi - dl[1]);
-            if (nb < 1) b0 = a0;
-            if (nb < 2) b1 = a1;
-            qs1 = qs[1];
-            dl0 = dl[0];
-            dl1 = dl[1];
-        }
+    for (int o = 0; o < kFastCig; ++o) {
+        const bool live = (uint32_t)o < ncig;
+        const uint32_t cg = cigw[o];
+        const uint32_t op = cg & 15u;
+        const int len = (int)min(cg >> 4, (uint32_t)(1 << 26));
+        const bool isM = live && (op == 0 || op == 7 || op == 8);
+        const bool isD = live && (op == 2 || op == 3);
+        const bool isS = live && op == 4;
+        const int dl = ref - q;
+        const bool ext0 = isM && nb == 1 && q == qe0 && dl == d0;
+        const bool ext1 = isM && nb == 2 && q == qe1 && dl == d1;
+        const bool new0 = isM && nb == 0;
+        const bool new1 = isM && nb == 1 && !ext0;
+        over = over || (isM && nb == 2 && !ext1);
+        qs0 = new0 ? q : qs0;
+        d0 = new0 ? dl : d0;
+        qe0 = (new0 || ext0) ? q + len : qe0;
+        qs1 = new1 ? q : qs1;
+        d1 = new1 ? dl : d1;
+        qe1 = (new1 || ext1) ? q + len : qe1;
+        nb += (new0 || new1) ? 1 : 0;
+        q += (isM || isS) ? len : 0;
+        ref += (isM || isD) ? len : 0;
     }
+    fast = fast && !over;
+    span_err = span_err || (fast && max(ref - start, (int)lseq) > (int)max_span);
+    const int vq0 = pc.min_dist > 0 ? pc.min_dist : 0;
+    const int vq1 = min((int)lseq, pc.min_dist > 0 ? (int)lseq - pc.min_dist : (int)lseq);
+    const int wlo = w.w0, whi = w.w0 + w.wlen;
+    int a0 = max(max(qs0, vq0), wlo - d0);
+    int b0 = min(min(qe0, vq1), whi - d0);
+    int a1 = max(max(qs1, vq0), wlo - d1);
+    int b1 = min(min(qe1, vq1), whi - d1);
+    b0 = (fast && nb >= 1) ? b0 : a0;
+    b1 = (fast && nb >= 2) ? b1 : a1;
+    const int dl0 = d0, dl1 = d1;
     const uint32_t inc = strand_inc(strand);
     if (MGP_ABL == 8) {  // records loaded, no per-base work (experiments only)
         const uint32_t x = R.h.x ^ R.h.y ^ R.h.z ^ R.h.w ^ R.qv[0].x ^ R.qv[0].y ^ R.qv[0].z ^ R.qv[0].w ^
