@@ -130,7 +130,8 @@ struct mgp_ctx {
     DevBuf bin_start, H, P, cell_cnt, cell_base, bin_valid, bin_base, bucket_off, gel2, PG, F;
     DevBuf pel, tally_part, tally, bin_mspan, dup_part;
     DevBuf n_reads, any_paired, passed, covered, dsum, dmax, med_lo, med_hi, first_read;
-    DevBuf counts, tn5, depth, stats;
+    DevBuf counts, tn5, depth, stats;  // u32 rows: drained windows, and mgp_fetch's widened copy
+    DevBuf counts16, tn5_16, depth16, wide;  // the run's 16-bit result rows (Out16)
 
     bool ran = false;
     int last_status = MGP_OK;
@@ -1351,9 +1352,25 @@ constexpr uint32_t kSeg = 65535;     // elements per tile segment (16-bit halves
 #define MGP_PILEUP_WAVES 4
 #endif
 
+// Output (Out16): the strand-filtered counts as u16 pairs, exactly the tile's
+// packed words (fwd low, rev high), Tn5 as one u32 pair word and depth as u16.
+// A cell window with at most 65535 elements cannot hold a larger value, so these
+// are exact; a drained window (more elements) keeps its exact u32 rows in the
+// 32-bit arrays and is flagged in `wide` (the u16 copy is saturated, the HDF5
+// form writers.py:205-218). mgp_fetch expands the 16-bit form into the caller's
+// u32 arrays.
+struct Out16 {
+    uint4* counts;     // [cells][L]: 8 x u16 A_fwd, A_rev, ... T_rev
+    uint32_t* tn5;     // [cells][L]: fwd | rev << 16
+    uint16_t* depth;   // [cells][L]
+    uint8_t* wide;     // [cells][nwin]: 1 = exact values in the u32 arrays
+};
+
+__device__ __forceinline__ uint32_t sat16(uint32_t v) { return v > 0xFFFFu ? 0xFFFFu : v; }
+
 __global__ void __launch_bounds__(kBlock, MGP_PILEUP_WAVES) k_pileup(
     Geom g, PileCfg pc, const uint8_t* __restrict__ payload, const unsigned long long* __restrict__ pel,
-    const uint32_t* __restrict__ O, uint32_t* __restrict__ counts, uint32_t* __restrict__ tn5,
+    const uint32_t* __restrict__ O, Out16 o16, uint32_t* __restrict__ counts, uint32_t* __restrict__ tn5,
     uint32_t* __restrict__ depth, uint32_t* __restrict__ n_reads, uint8_t* __restrict__ any_paired,
     uint32_t* __restrict__ covered, unsigned long long* __restrict__ dsum, uint32_t* __restrict__ dmax,
     uint32_t* __restrict__ tally_part, DevStats* st) {
@@ -1474,6 +1491,7 @@ __global__ void __launch_bounds__(kBlock, MGP_PILEUP_WAVES) k_pileup(
             if (p < w.wlen) {
                 const size_t P = (size_t)c * L + w.w0 + p;
                 uint32_t v[8], tf, tr;
+                uint32_t pk4[4] = {0u, 0u, 0u, 0u}, pk5 = 0u;  // the packed words (not drained)
                 if (drained) {
                     const uint4 a = reinterpret_cast<const uint4*>(counts + P * 8)[0];
                     const uint4 b = reinterpret_cast<const uint4*>(counts + P * 8)[1];
@@ -1485,16 +1503,19 @@ __global__ void __launch_bounds__(kBlock, MGP_PILEUP_WAVES) k_pileup(
                 } else {
                     const uint4 xb = reinterpret_cast<const uint4*>(tile)[p];
                     reinterpret_cast<uint4*>(tile)[p] = make_uint4(0, 0, 0, 0);
-                    const uint32_t pk4[4] = {xb.x, xb.y, xb.z, xb.w};
+                    pk4[0] = xb.x;
+                    pk4[1] = xb.y;
+                    pk4[2] = xb.z;
+                    pk4[3] = xb.w;
 #pragma unroll
                     for (int x = 0; x < 4; ++x) {
                         v[2 * x] = pk4[x] & 0xFFFFu;
                         v[2 * x + 1] = pk4[x] >> 16;
                     }
-                    const uint32_t pk = t5[p];
+                    pk5 = t5[p];
                     t5[p] = 0u;
-                    tf = pk & 0xFFFFu;
-                    tr = pk >> 16;
+                    tf = pk5 & 0xFFFFu;
+                    tr = pk5 >> 16;
                 }
                 uint32_t d = 0;
 #pragma unroll
@@ -1506,19 +1527,31 @@ __global__ void __launch_bounds__(kBlock, MGP_PILEUP_WAVES) k_pileup(
                         if (bias > pc.max_bias) {
                             v[2 * b] = 0;
                             v[2 * b + 1] = 0;
+                            pk4[b] = 0u;
                         }
                     }
                     const uint32_t t2 = v[2 * b] + v[2 * b + 1];
                     tal[m][b] += t2;
                     d += t2;
                 }
-                if (d == 0 && !pc.keep_tn5) tf = tr = 0;
+                if (d == 0 && !pc.keep_tn5) {
+                    tf = tr = 0;
+                    pk5 = 0u;
+                }
                 if (MGP_ABL != 4 || (v[0] == 0xFFFFFFFFu && d == 7u)) {
-                    uint4* cp = reinterpret_cast<uint4*>(counts + P * 8);
-                    cp[0] = make_uint4(v[0], v[1], v[2], v[3]);
-                    cp[1] = make_uint4(v[4], v[5], v[6], v[7]);
-                    reinterpret_cast<uint2*>(tn5)[P] = make_uint2(tf, tr);
-                    depth[P] = d;
+                    if (drained) {  // exact u32 rows, saturated u16 copy
+                        uint4* cp = reinterpret_cast<uint4*>(counts + P * 8);
+                        cp[0] = make_uint4(v[0], v[1], v[2], v[3]);
+                        cp[1] = make_uint4(v[4], v[5], v[6], v[7]);
+                        reinterpret_cast<uint2*>(tn5)[P] = make_uint2(tf, tr);
+                        depth[P] = d;
+#pragma unroll
+                        for (int b = 0; b < 4; ++b) pk4[b] = sat16(v[2 * b]) | sat16(v[2 * b + 1]) << 16;
+                        pk5 = sat16(tf) | sat16(tr) << 16;
+                    }
+                    o16.counts[P] = make_uint4(pk4[0], pk4[1], pk4[2], pk4[3]);
+                    o16.tn5[P] = pk5;
+                    o16.depth[P] = (uint16_t)sat16(d);
                 }
                 cov += d > 0;
                 sum += d;
@@ -1537,6 +1570,7 @@ __global__ void __launch_bounds__(kBlock, MGP_PILEUP_WAVES) k_pileup(
         }
         __syncthreads();
         if (threadIdx.x == 0) {
+            o16.wide[(size_t)c * g.nwin + k] = drained ? 1u : 0u;
             uint32_t C = 0, M = 0, K = 0;
             unsigned long long S = 0, F = 0;
             for (int q = 0; q < 4; ++q) {
@@ -1574,8 +1608,9 @@ __global__ void __launch_bounds__(kBlock, MGP_PILEUP_WAVES) k_pileup(
 // min-reads gate (processors.py:22) for min_reads > 1: a cell with fewer kept
 // reads produces no result; remove its counts and its tally contribution.
 __global__ void __launch_bounds__(kBlock) k_gate_fixup(Geom g, int min_reads, const uint32_t* __restrict__ n_reads,
-                                                       uint32_t* __restrict__ counts, uint32_t* __restrict__ tn5,
-                                                       uint32_t* __restrict__ depth, uint32_t* __restrict__ covered,
+                                                       Out16 o16, uint32_t* __restrict__ counts,
+                                                       uint32_t* __restrict__ tn5, uint32_t* __restrict__ depth,
+                                                       uint32_t* __restrict__ covered,
                                                        unsigned long long* __restrict__ dsum,
                                                        uint32_t* __restrict__ dmax, uint32_t* __restrict__ tally_part) {
     const int c = blockIdx.x;
@@ -1585,16 +1620,31 @@ __global__ void __launch_bounds__(kBlock) k_gate_fixup(Geom g, int min_reads, co
     uint32_t* tp = tally_part + (size_t)(c / g.cpb) * L * 4;
     for (int p = threadIdx.x; p < L; p += blockDim.x) {
         const size_t P = (size_t)c * L + p;
-        if (depth[P] == 0) continue;
-        uint4* cp = reinterpret_cast<uint4*>(counts + P * 8);
-        const uint4 a = cp[0], b = cp[1];
-        const uint32_t t[4] = {a.x + a.y, a.z + a.w, b.x + b.y, b.z + b.w};
+        const bool wide = o16.wide[(size_t)c * g.nwin + p / g.W] != 0;
+        if ((wide ? depth[P] : (uint32_t)o16.depth[P]) == 0u) continue;
+        uint32_t t[4];
+        if (wide) {
+            uint4* cp = reinterpret_cast<uint4*>(counts + P * 8);
+            const uint4 a = cp[0], b = cp[1];
+            t[0] = a.x + a.y;
+            t[1] = a.z + a.w;
+            t[2] = b.x + b.y;
+            t[3] = b.z + b.w;
+            cp[0] = make_uint4(0, 0, 0, 0);
+            cp[1] = make_uint4(0, 0, 0, 0);
+            reinterpret_cast<uint2*>(tn5)[P] = make_uint2(0, 0);
+            depth[P] = 0;
+        } else {
+            const uint4 a = o16.counts[P];
+            const uint32_t w4[4] = {a.x, a.y, a.z, a.w};
+#pragma unroll
+            for (int q = 0; q < 4; ++q) t[q] = (w4[q] & 0xFFFFu) + (w4[q] >> 16);
+        }
         for (int q = 0; q < 4; ++q)
             if (t[q]) atomicSub(&tp[(size_t)p * 4 + q], t[q]);
-        cp[0] = make_uint4(0, 0, 0, 0);
-        cp[1] = make_uint4(0, 0, 0, 0);
-        reinterpret_cast<uint2*>(tn5)[P] = make_uint2(0, 0);
-        depth[P] = 0;
+        o16.counts[P] = make_uint4(0, 0, 0, 0);
+        o16.tn5[P] = 0u;
+        o16.depth[P] = 0;
     }
     __syncthreads();
     if (threadIdx.x == 0) {
@@ -1611,8 +1661,19 @@ __global__ void __launch_bounds__(kBlock) k_gate_fixup(Geom g, int min_reads, co
 // atomics and no histogram, whatever the depths.
 constexpr int kMedRegs = 72;  // register-resident depths per thread (L <= 18432)
 
+// The depth of position p of cell c: the u16 row, or the u32 row in a drained window.
+__device__ __forceinline__ uint32_t depth_at(const Geom& g, int c, int p, const uint16_t* __restrict__ d16,
+                                            const uint32_t* __restrict__ d32, const uint8_t* __restrict__ wide,
+                                            bool anyw) {
+    const size_t P = (size_t)c * g.L + p;
+    if (anyw && wide[(size_t)c * g.nwin + p / g.W]) return d32[P];
+    return d16[P];
+}
+
 template <bool kRegs>
-__global__ void __launch_bounds__(kBlock) k_median(Geom g, int min_reads, const uint32_t* __restrict__ depth,
+__global__ void __launch_bounds__(kBlock) k_median(Geom g, int min_reads, const uint16_t* __restrict__ depth16,
+                                                   const uint32_t* __restrict__ depth32,
+                                                   const uint8_t* __restrict__ wide,
                                                    const uint32_t* __restrict__ n_reads,
                                                    const uint32_t* __restrict__ covered,
                                                    const uint32_t* __restrict__ dmax,
@@ -1631,14 +1692,24 @@ __global__ void __launch_bounds__(kBlock) k_median(Geom g, int min_reads, const 
         }
         return;
     }
-    const uint32_t* drow = depth + (size_t)c * g.L;
     const int L = g.L;
+    bool anyw = false;  // a drained window: its depths are in the u32 row
+    for (int k = 0; k < g.nwin; ++k) anyw |= wide[(size_t)c * g.nwin + k] != 0;
+    const uint16_t* drow = depth16 + (size_t)c * g.L;
     uint32_t v[kRegs ? kMedRegs : 1];
     if (kRegs) {
+        if (anyw) {
 #pragma unroll
-        for (int k = 0; k < kMedRegs; ++k) {
-            const int p = threadIdx.x + k * kBlock;
-            v[k] = p < L ? drow[p] : 0u;
+            for (int k = 0; k < kMedRegs; ++k) {
+                const int p = threadIdx.x + k * kBlock;
+                v[k] = p < L ? depth_at(g, c, p, depth16, depth32, wide, true) : 0u;
+            }
+        } else {
+#pragma unroll
+            for (int k = 0; k < kMedRegs; ++k) {
+                const int p = threadIdx.x + k * kBlock;
+                v[k] = p < L ? (uint32_t)drow[p] : 0u;
+            }
         }
     }
     // zero depths sort first: the k-th covered value is the (zeros + k)-th overall
@@ -1663,7 +1734,7 @@ __global__ void __launch_bounds__(kBlock) k_median(Geom g, int min_reads, const 
             }
         } else {
             for (int p = threadIdx.x; p < L; p += kBlock) {
-                const uint32_t d = drow[p];
+                const uint32_t d = depth_at(g, c, p, depth16, depth32, wide, anyw);
                 cl += d <= ml;
                 ch += d <= mh;
             }
@@ -1766,6 +1837,28 @@ __global__ void k_tally_reduce(const uint32_t* __restrict__ part, int nchunks, i
     unsigned long long acc = 0;
     for (int ch = blockIdx.y; ch < nchunks; ch += gridDim.y) acc += part[(size_t)ch * L4 + x];
     if (acc) atomicAdd(&tally[x], acc);
+}
+
+// mgp_fetch: the 16-bit result rows widened into the u32 arrays the caller
+// receives (drained windows already hold their exact u32 rows). One thread per
+// (cell, position).
+__global__ void __launch_bounds__(kBlock) k_expand(Geom g, int64_t npos, Out16 o16, uint32_t* __restrict__ counts,
+                                                   uint32_t* __restrict__ tn5, uint32_t* __restrict__ depth) {
+    const int64_t P = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (P >= npos) return;
+    const int64_t c = P / g.L, p = P - c * g.L;
+    if (o16.wide[c * g.nwin + p / g.W]) return;
+    if (counts) {
+        const uint4 a = o16.counts[P];
+        uint4* cp = reinterpret_cast<uint4*>(counts + P * 8);
+        cp[0] = make_uint4(a.x & 0xFFFFu, a.x >> 16, a.y & 0xFFFFu, a.y >> 16);
+        cp[1] = make_uint4(a.z & 0xFFFFu, a.z >> 16, a.w & 0xFFFFu, a.w >> 16);
+    }
+    if (tn5) {
+        const uint32_t t = o16.tn5[P];
+        reinterpret_cast<uint2*>(tn5)[P] = make_uint2(t & 0xFFFFu, t >> 16);
+    }
+    if (depth) depth[P] = o16.depth[P];
 }
 
 __global__ void k_add_u64(uint64_t* __restrict__ a, int64_t n, uint64_t add) {
@@ -1930,7 +2023,7 @@ void mgp_close(mgp_ctx* ctx) {
                       &ctx->tally_part, &ctx->tally,   &ctx->n_reads,    &ctx->any_paired,
                       &ctx->passed,    &ctx->covered,   &ctx->dsum,     &ctx->dmax,       &ctx->med_lo,
                       &ctx->med_hi,    &ctx->first_read, &ctx->counts,  &ctx->tn5,        &ctx->depth,
-                      &ctx->stats};
+                      &ctx->stats,     &ctx->counts16,  &ctx->tn5_16,  &ctx->depth16,    &ctx->wide};
     for (DevBuf* b : bufs) b->release();
     for (int r = 0; r < mgp_ctx::kRing; ++r)
         for (int s = 0; s < ST_N; ++s) {
@@ -2050,8 +2143,21 @@ static int ensure_run_buffers(mgp_ctx* ctx) {
     MGP_TRY(ctx->counts.ensure(nc * L * 32));
     MGP_TRY(ctx->tn5.ensure(nc * L * 8));
     MGP_TRY(ctx->depth.ensure(nc * L * 4));
+    MGP_TRY(ctx->counts16.ensure(nc * L * 16));
+    MGP_TRY(ctx->tn5_16.ensure(nc * L * 4));
+    MGP_TRY(ctx->depth16.ensure(nc * L * 2));
+    MGP_TRY(ctx->wide.ensure(nc * (size_t)std::max(g.nwin, 1)));
     MGP_TRY(ctx->stats.ensure(sizeof(DevStats)));
     return MGP_OK;
+}
+
+static Out16 out16_of(mgp_ctx* ctx) {
+    Out16 o;
+    o.counts = ctx->counts16.as<uint4>();
+    o.tn5 = ctx->tn5_16.as<uint32_t>();
+    o.depth = ctx->depth16.as<uint16_t>();
+    o.wide = ctx->wide.as<uint8_t>();
+    return o;
 }
 
 #define STAGE_BEGIN(st) HIP_TRY(hipEventRecord(ctx->ev[slot][st][0], s)); ctx->stage_ran[slot][st] = true
@@ -2185,7 +2291,8 @@ int mgp_run(mgp_ctx* ctx) {
         dim3 gp(g.nchunks, g.nwin);
         const size_t psm = (size_t)5 * g.Wp * 4;
         k_pileup<<<gp, kBlock, psm, s>>>(g, pc, ctx->payload.as<uint8_t>(), ctx->pel.as<unsigned long long>(),
-                                         ctx->H.as<uint32_t>(), ctx->counts.as<uint32_t>(), ctx->tn5.as<uint32_t>(),
+                                         ctx->H.as<uint32_t>(), out16_of(ctx), ctx->counts.as<uint32_t>(),
+                                         ctx->tn5.as<uint32_t>(),
                                          ctx->depth.as<uint32_t>(), ctx->n_reads.as<uint32_t>(),
                                          ctx->any_paired.as<uint8_t>(), ctx->covered.as<uint32_t>(),
                                          ctx->dsum.as<unsigned long long>(), ctx->dmax.as<uint32_t>(),
@@ -2197,7 +2304,7 @@ int mgp_run(mgp_ctx* ctx) {
         if (ctx->cfg.min_reads > 1) {
             STAGE_BEGIN(ST_GATE);
             k_gate_fixup<<<nc, kBlock, 0, s>>>(g, ctx->cfg.min_reads, ctx->n_reads.as<uint32_t>(),
-                                               ctx->counts.as<uint32_t>(), ctx->tn5.as<uint32_t>(),
+                                               out16_of(ctx), ctx->counts.as<uint32_t>(), ctx->tn5.as<uint32_t>(),
                                                ctx->depth.as<uint32_t>(), ctx->covered.as<uint32_t>(),
                                                ctx->dsum.as<unsigned long long>(), ctx->dmax.as<uint32_t>(),
                                                ctx->tally_part.as<uint32_t>());
@@ -2209,14 +2316,16 @@ int mgp_run(mgp_ctx* ctx) {
         STAGE_BEGIN(ST_MEDIAN);
         if (g.L <= kMedRegs * kBlock)
             k_median<true><<<nc, kBlock, 0, s>>>(
-                                                     g, ctx->cfg.min_reads, ctx->depth.as<uint32_t>(),
+                                                     g, ctx->cfg.min_reads, ctx->depth16.as<uint16_t>(),
+                                                     ctx->depth.as<uint32_t>(), ctx->wide.as<uint8_t>(),
                                                      ctx->n_reads.as<uint32_t>(), ctx->covered.as<uint32_t>(),
                                                      ctx->dmax.as<uint32_t>(),
                                                      ctx->med_lo.as<uint32_t>(), ctx->med_hi.as<uint32_t>(),
                                                      ctx->passed.as<uint8_t>(), st);
         else
             k_median<false><<<nc, kBlock, 0, s>>>(
-                                                     g, ctx->cfg.min_reads, ctx->depth.as<uint32_t>(),
+                                                     g, ctx->cfg.min_reads, ctx->depth16.as<uint16_t>(),
+                                                     ctx->depth.as<uint32_t>(), ctx->wide.as<uint8_t>(),
                                                      ctx->n_reads.as<uint32_t>(), ctx->covered.as<uint32_t>(),
                                                      ctx->dmax.as<uint32_t>(),
                                                      ctx->med_lo.as<uint32_t>(), ctx->med_hi.as<uint32_t>(),
@@ -2279,6 +2388,14 @@ int mgp_fetch(mgp_ctx* ctx, mgp_result* out) {
         if (dst && bytes) HIP_TRY(hipMemcpy(dst, src.p, bytes, hipMemcpyDeviceToHost));
         return MGP_OK;
     };
+    if (nc && (out->counts || out->tn5 || out->depth)) {  // widen the 16-bit rows (drained windows are exact already)
+        const int64_t npos = (int64_t)nc * (int64_t)L;
+        k_expand<<<blocks_for(npos), kBlock, 0, ctx->s_comp>>>(
+            g, npos, out16_of(ctx), out->counts ? ctx->counts.as<uint32_t>() : nullptr,
+            out->tn5 ? ctx->tn5.as<uint32_t>() : nullptr, out->depth ? ctx->depth.as<uint32_t>() : nullptr);
+        HIP_TRY(hipGetLastError());
+        HIP_TRY(hipStreamSynchronize(ctx->s_comp));
+    }
     MGP_TRY(d2h(out->counts, ctx->counts, nc * L * 32));
     MGP_TRY(d2h(out->tn5, ctx->tn5, nc * L * 8));
     MGP_TRY(d2h(out->depth, ctx->depth, nc * L * 4));
