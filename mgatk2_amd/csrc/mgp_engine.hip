@@ -1245,6 +1245,111 @@ __device__ __forceinline__ void pile_bases(bool act, int a0, int b0, int a1, int
     }
 }
 
+// LDS byte addresses: the packed loop computes a count's address as integer
+// arithmetic (row | plane * 4) and adds through an LDS-qualified pointer, so the
+// query offset still folds into the atomic's immediate.
+typedef __attribute__((address_space(3))) uint32_t lds_u32;
+__device__ __forceinline__ uint32_t lds_addr(uint32_t* p) { return (uint32_t)(uintptr_t)(lds_u32*)p; }
+__device__ __forceinline__ void lds_add(uint32_t addr, uint32_t v) {
+    __hip_atomic_fetch_add((lds_u32*)(uintptr_t)addr, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+// Where a lane that does not count a base adds: a per-lane word plus the query
+// offset (16 bytes per position), never read. Shared by the waves of a workgroup.
+constexpr int kOwnWords = kWave + 4 * kWave;
+__shared__ uint32_t g_own[kOwnWords];
+
+// The counted bases of the packed register-path reads of a wave. The record's
+// base bytes (qual << 2 | b at +14) outside the lane's counted ranges [a_k, b_k)
+// are first set to 0xFF (never counted: one v_perm per word), so every wave
+// shape runs one loop whose body is a range test on the byte, the count's
+// address (the block's row | plane * 4, or the lane's own scratch word when the
+// base is not counted) and an LDS add; two-block waves also pick the block's row
+// per base. Every lane of the wave enters: the unrolled loop bounds are wave
+// reductions.
+__device__ __forceinline__ void pile_bases_packed(bool act, int a0, int b0, int a1, int b1, int qs1, int dl0,
+                                                  int dl1, const RecLine& R, const Win& w, const PileCfg& pc,
+                                                  uint32_t* tile, uint32_t inc) {
+    constexpr int kLen = MGP_PACK_MAX_LEN;
+    auto range_mask = [](int lo, int hi) -> unsigned long long {
+        lo = min(max(lo, 0), 64);
+        hi = min(max(hi, 0), 64);
+        const unsigned long long h = hi >= 64 ? ~0ull : ((1ull << hi) - 1ull);
+        const unsigned long long l = lo >= 64 ? ~0ull : ((1ull << lo) - 1ull);
+        return lo < hi ? (h & ~l) : 0ull;
+    };
+    const unsigned long long vm = act ? (range_mask(a0, b0) | range_mask(a1, b1)) : 0ull;
+    int qlo = 1 << 30, qhi = 0;
+    if (vm) {
+        qlo = __builtin_ctzll(vm);
+        qhi = 64 - __builtin_clzll(vm);
+    }
+    const int wq_lo = __builtin_amdgcn_readfirstlane(wave_min(qlo));
+    const int wq_hi = __builtin_amdgcn_readfirstlane(wave_max(qhi));
+    if (wq_lo >= wq_hi) return;
+    uint32_t qw[16];
+    {
+        const uint4 v[4] = {R.h, R.qv[0], R.qv[1], R.qv[2]};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            qw[4 * k] = v[k].x;
+            qw[4 * k + 1] = v[k].y;
+            qw[4 * k + 2] = v[k].z;
+            qw[4 * k + 3] = v[k].w;
+        }
+    }
+    // uncounted positions -> 0xFF: word j holds query positions 4j - 14 .. 4j - 11,
+    // bits 4j - 12 .. 4j - 9 of u = ~vm << 2 (its bits 0, 1 are the header bytes
+    // 12, 13, left alone); a set bit i selects byte i + 4 of {0xFFFFFFFF, word}
+    const unsigned long long u = ~vm << 2;
+    const uint32_t ulo = (uint32_t)u, uhi = (uint32_t)(u >> 32);
+#pragma unroll
+    for (int j = 3; j < 16; ++j) {
+        const int s = 4 * j - 12;
+        const uint32_t b4 = ((s < 32 ? ulo : uhi) >> (s & 31)) & 15u;
+        const uint32_t sel = 0x03020100u | ((b4 * 0x810204u) & 0x04040404u);
+        qw[j] = __builtin_amdgcn_perm(0xFFFFFFFFu, qw[j], sel);
+    }
+    // counted iff qual << 2 | b lies in [4 * max(min_baseq, 0), 252)
+    const uint32_t lo4 = 4u * (uint32_t)min(max(pc.min_baseq, 0), 63);
+    const uint32_t span4 = 252u - lo4;
+    const uint32_t own = lds_addr(g_own) + 4u * (threadIdx.x & 63);
+    const uint32_t tb = lds_addr(tile);
+    // rows: byte address of query offset 0 of each block (16 bytes per position)
+    const uint32_t r0 = tb + 16u * (uint32_t)(dl0 - w.w0), r1 = tb + 16u * (uint32_t)(dl1 - w.w0);
+    auto count = [&](int qq, uint32_t row) {
+        const uint32_t x = (qw[(14 + qq) >> 2] >> (8 * ((14 + qq) & 3))) & 0xFFu;
+        const uint32_t a = row | ((x & 3u) << 2);
+        lds_add((x - lo4 < span4 ? a : own) + 16u * (uint32_t)qq, inc);
+    };
+    const bool two = __ballot(act && a1 < b1) != 0ull;
+    // the wave's range [wq_lo, wq_hi): the core [kC0, kC1) without a test when
+    // covered, positions outside it behind a scalar bit test of the range
+    const unsigned long long smask = range_mask(wq_lo, wq_hi);
+    constexpr int kC0 = 5, kC1 = kLen - 5;
+    auto run = [&](auto&& body) {
+        if (wq_lo <= kC0 && wq_hi >= kC1) {
+            if (wq_lo < kC0) {
+#pragma unroll
+                for (int qq = 0; qq < kC0; ++qq)
+                    if ((smask >> qq) & 1ull) body(qq);
+            }
+#pragma unroll
+            for (int qq = kC0; qq < kC1; ++qq) body(qq);
+            if (wq_hi > kC1) {
+#pragma unroll
+                for (int qq = kC1; qq < kLen; ++qq)
+                    if ((smask >> qq) & 1ull) body(qq);
+            }
+        } else {
+#pragma unroll
+            for (int qq = 0; qq < kLen; ++qq)
+                if ((smask >> qq) & 1ull) body(qq);
+        }
+    };
+    if (two) run([&](int qq) { count(qq, qq >= qs1 ? r1 : r0); });
+    else run([&](int qq) { count(qq, r0); });
+}
+
 __device__ __forceinline__ void pile_line(bool has, bool packed, const uint8_t* __restrict__ rec, const RecLine& R,
                                           const Win& w, const PileCfg& pc, uint32_t* tile, uint32_t* t5,
                                           uint32_t max_span, bool& span_err, bool& pk_err) {
@@ -1321,7 +1426,7 @@ __device__ __forceinline__ void pile_line(bool has, bool packed, const uint8_t* 
     if (__ballot(fast && !packed) != 0ull)
         pile_bases<false>(fast && !packed, a0, b0, a1, b1, qs1, dl0, dl1, R, w, pc, tile, inc);
     if (__ballot(fast && packed) != 0ull)
-        pile_bases<true>(fast && packed, a0, b0, a1, b1, qs1, dl0, dl1, R, w, pc, tile, inc);
+        pile_bases_packed(fast && packed, a0, b0, a1, b1, qs1, dl0, dl1, R, w, pc, tile, inc);
     const bool slow = has && !fast;
     pk_err = pk_err || (slow && packed);  // a packed record outside the layout's limits
     bool se = false;
