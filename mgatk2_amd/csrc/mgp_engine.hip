@@ -31,6 +31,7 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <type_traits>
 #include <cstdio>
 #include <cstring>
 #include <string>
@@ -125,6 +126,7 @@ struct mgp_ctx {
     DevBuf roff32;          // u32 rec_off >> 6 (grouping pass A reads it when every offset fits, kOffR32)
     DevBuf roff_irregular;  // u32 bits: 1 some rec_off[i] != kRecStride * i, 2 some offset not in roff32's range
     int roff_mode = -1;     // pass A's offset source (kOffDense / kOffR32 / kOffR64); -1 not read since the last push
+    uint32_t read_bits = 0; // the ingest check's CHK_* bits of the resident reads
 
     // run scratch
     DevBuf bin_start, H, P, cell_cnt, cell_base, bin_valid, bin_base, bucket_off, gel2, PG, F;
@@ -424,6 +426,9 @@ enum { kOffDense = 0, kOffR32 = 1, kOffR64 = 2 };
 #ifndef MGP_ABL_A
 #define MGP_ABL_A 0  // pass-A ablations (experiments only): 1 no element stores, 2 no ranking (slot = read index)
 #endif
+#ifndef MGP_GA_DB
+#define MGP_GA_DB 1  // pass A: next step's loads in flight during this step (double buffer)
+#endif
 #ifndef MGP_GA_BLOCK
 #define MGP_GA_BLOCK 256  // threads per pass-A workgroup
 #endif
@@ -490,9 +495,13 @@ __global__ void __launch_bounds__(kGABlock, MGP_GA_WAVES) k_group_a(int64_t n, c
     // order, then round order); waves claim bucket slots in wave order
     constexpr int kAhead = MGP_GA_AHEAD;
     constexpr int kStep = kAhead * kGABlock;
+    // per read: barcode, start, tlen, flag | mapq << 16 and the record offset
+    // (its 64-byte unit or read index for the dense / u32 sources: 32 bits)
+    using OffT = typename std::conditional<kOff == kOffR64, uint64_t, uint32_t>::type;
     struct Pre {
-        int c[kAhead], s[kAhead], t[kAhead], f[kAhead], m[kAhead];
-        uint64_t o[kAhead];
+        int c[kAhead], s[kAhead], t[kAhead];
+        uint32_t fm[kAhead];
+        OffT o[kAhead];
     };
     // loads issued unconditionally (index clamped into the bin) so every path has
     // the same number in flight and the waits stay counted
@@ -503,13 +512,12 @@ __global__ void __launch_bounds__(kGABlock, MGP_GA_WAVES) k_group_a(int64_t n, c
             const int64_t i = base0 + wid * (kAhead * kWave) + u * kWave + lane;
             const int64_t j = i < hi ? i : hi - 1;
             P.c[u] = bc[j];
-            P.f[u] = flag[j];
+            P.fm[u] = (uint32_t)flag[j] | (uint32_t)mapq[j] << 16;
             P.s[u] = start[j];
             P.t[u] = tlen[j];
-            P.m[u] = mapq[j];
-            P.o[u] = kOff == kOffDense ? (uint64_t)j * kRecStride
-                     : kOff == kOffR32 ? (uint64_t)roff32[j] << 6
-                                       : roff[j];
+            if constexpr (kOff == kOffDense) P.o[u] = (OffT)j;
+            else if constexpr (kOff == kOffR32) P.o[u] = roff32[j];
+            else P.o[u] = roff[j];
         }
     };
     // A step: each wave ranks its own reads by group (ballot peers, the leader of a
@@ -527,7 +535,7 @@ __global__ void __launch_bounds__(kGABlock, MGP_GA_WAVES) k_group_a(int64_t n, c
         for (int u = 0; u < kAhead; ++u) {
             const int64_t i = base0 + wid * (kAhead * kWave) + u * kWave + lane;
             const int c = P.c[u];
-            valid[u] = i < hi && read_valid(c, (uint16_t)P.f[u], nc);
+            valid[u] = i < hi && read_valid(c, (uint16_t)P.fm[u], nc);
             const int gi = c >> 6;
             unsigned long long pm = __ballot(valid[u]);
             for (int bit = 0; bit < gbits && pm; ++bit) {
@@ -567,11 +575,14 @@ __global__ void __launch_bounds__(kGABlock, MGP_GA_WAVES) k_group_a(int64_t n, c
             const uint32_t dest = MGP_ABL_A == 2 ? (uint32_t)(base0 + wid * (kAhead * kWave) + u * kWave + lane)
                                                  : my[P.c[u] >> 6] + rk[u];
             if (MGP_ABL_A == 1 && dest != 0xFFFFFFFFu) continue;  // ablation: no stores
-            const uint16_t f = (uint16_t)P.f[u];
+            const uint16_t f = (uint16_t)P.fm[u];
             const int t = P.t[u];
+            const unsigned long long off = kOff == kOffDense ? (unsigned long long)P.o[u] * kRecStride
+                                           : kOff == kOffR32 ? (unsigned long long)P.o[u] << 6
+                                                             : (unsigned long long)P.o[u];
             GElem e;
-            e.w = P.o[u] | (f & MGP_FLAG_REVERSE ? GM_REV : 0ull) | (f & MGP_FLAG_PAIRED ? GM_PAIRED : 0ull) |
-                  (P.m[u] >= min_mapq ? GM_MAPQ_OK : 0ull) | (f & MGP_FLAG_NOSEQQUAL ? GM_BAD : 0ull) | (f & MGP_FLAG_PACKED ? GM_PACKED : 0ull) |
+            e.w = off | (f & MGP_FLAG_REVERSE ? GM_REV : 0ull) | (f & MGP_FLAG_PAIRED ? GM_PAIRED : 0ull) |
+                  ((int)(P.fm[u] >> 16) >= min_mapq ? GM_MAPQ_OK : 0ull) | (f & MGP_FLAG_NOSEQQUAL ? GM_BAD : 0ull) | (f & MGP_FLAG_PACKED ? GM_PACKED : 0ull) |
                   ((unsigned long long)(P.c[u] & (kGroup - 1)) << GM_LCELL_SHIFT);
             e.start = P.s[u];
             e.tlen = t < 0 ? (uint32_t)(-(int64_t)t) : (uint32_t)t;
@@ -581,6 +592,7 @@ __global__ void __launch_bounds__(kGABlock, MGP_GA_WAVES) k_group_a(int64_t n, c
         set ^= 1;
     };
     if (lo >= hi) return;
+#if MGP_GA_DB
     Pre A, B;
     load(A, lo);
     for (int64_t base0 = lo; base0 < hi; base0 += 2 * kStep) {
@@ -589,6 +601,13 @@ __global__ void __launch_bounds__(kGABlock, MGP_GA_WAVES) k_group_a(int64_t n, c
         load(A, base0 + 2 * kStep);
         if (base0 + kStep < hi) process(B, base0 + kStep);
     }
+#else
+    for (int64_t base0 = lo; base0 < hi; base0 += kStep) {
+        Pre A;
+        load(A, base0);
+        process(A, base0);
+    }
+#endif
 }
 
 // Pass B: workgroup = (cell group, bin range). A step takes the group's buckets
@@ -606,36 +625,57 @@ __global__ void __launch_bounds__(kGABlock, MGP_GA_WAVES) k_group_a(int64_t n, c
 // duplicate iff a read before it in the run, among the equal starts, has the
 // same strand (and the same |tlen|): first in BAM order wins. Both duplicate
 // counters (readers.py:141-144) are taken here, each read being seen exactly
-// once. The output is one 8-byte pileup element per read: record offset |
-// GP_KEEP | GP_PAIRED | GP_BAD | GP_PILE (kept and MAPQ >= min_mapq, pileup.py:33).
+// once. The output is one 4-byte pileup element per read (PE_*): the record's
+// offset when the read is piled (kept and MAPQ >= min_mapq, pileup.py:33),
+// PE_KEEP or PE_DUP otherwise.
 #ifndef MGP_GB_STAGE
 #define MGP_GB_STAGE 2048
 #endif
 constexpr int kStageB = MGP_GB_STAGE;
-constexpr int kMaxRbB = 512;  // bins per pass-B workgroup (bucket sizes kept in LDS)
+constexpr int kMaxRbB = 256;  // bins per pass-B workgroup (bucket sizes kept in LDS; 4 workgroups per CU)
 #ifndef MGP_GB_WG
 #define MGP_GB_WG 8192  // target pass-B grid size
 #endif
-constexpr unsigned long long GP_PILE = 1ull << 63, GP_KEEP = 1ull << 62, GP_PAIRED = 1ull << 61,
-                             GP_BAD = 1ull << 60, GP_PACKED = 1ull << 59, GP_OFF = (1ull << GM_LCELL_SHIFT) - 1;
+// Pileup element (4 bytes, cell-major): a read to pile (kept by the duplicate
+// marking, MAPQ >= min_mapq, pileup.py:33) is its record offset in units of
+// 2^unit bytes (unit 6, or 4 for 16-byte aligned placements) | PE_PACKED; a kept
+// read below min_mapq is PE_KEEP, a duplicate PE_DUP (the pileup counts the
+// kept reads, processors.py:22). Offsets stay below PE_KEEP's (mgp_run checks).
+constexpr uint32_t PE_DUP = 0xFFFFFFFFu, PE_KEEP = 0xFFFFFFFEu, PE_PACKED = 0x80000000u, PE_OFF = 0x7FFFFFFFu;
+constexpr unsigned long long GM_OFF = (1ull << GM_LCELL_SHIFT) - 1;
 
 struct DedupAcc {  // per-thread duplicate counters of pass B
     unsigned long long d2 = 0, d3 = 0;
 };
 
-// The pileup element of one read given its duplicate flags.
-__device__ __forceinline__ unsigned long long group_b_emit(const GElem& e, bool dup2, bool dup3, int mode,
-                                                           DedupAcc& acc) {
-    const bool keep = mode == MGP_DEDUP_NONE ? true : mode == MGP_DEDUP_START ? !dup2 : !dup3;
+// The pileup element of one read given its duplicate flags; keep = the read
+// survives the duplicate marking (counted in n_reads, processors.py:22).
+__device__ __forceinline__ uint32_t group_b_emit(const GElem& e, bool dup2, bool dup3, int mode, int unit,
+                                                 DedupAcc& acc, bool& keep) {
+    keep = mode == MGP_DEDUP_NONE ? true : mode == MGP_DEDUP_START ? !dup2 : !dup3;
     acc.d2 += dup2;
     acc.d3 += dup3;
-    unsigned long long x = e.w & GP_OFF;
-    if (keep) {
-        x |= GP_KEEP | (e.w & GM_PAIRED ? GP_PAIRED : 0ull) | (e.w & GM_BAD ? GP_BAD : 0ull) |
-             (e.w & GM_PACKED ? GP_PACKED : 0ull);
-        if (e.w & GM_MAPQ_OK) x |= GP_PILE;
+    if (!keep) return PE_DUP;
+    if (!(e.w & GM_MAPQ_OK)) return PE_KEEP;
+    return (uint32_t)((e.w & GM_OFF) >> unit) | (e.w & GM_PACKED ? PE_PACKED : 0u);
+}
+
+// Per-cell flags of pass B when the resident reads mix paired and unpaired ones,
+// or some read lacks SEQ/QUAL (kTrack; the ingest check's CHK_* bits): the cell
+// has a kept paired read (processors.py:34) iff it has more kept reads (its
+// elements in the workgroup's bin range, the cbase advance, minus its
+// duplicates) than kept unpaired ones, both counted here into the workgroup's
+// per-cell LDS counters; a kept read without SEQ/QUAL sets ERR_BADREAD.
+// Otherwise every kept read is paired (or none is), which the pileup applies
+// with its kept-read counts, and no read lacks SEQ/QUAL.
+template <bool kTrack>
+__device__ __forceinline__ void cell_tally(bool act, int lc, bool keep, const GElem& e, uint32_t* s_ndup,
+                                           uint32_t* s_nunp, DevStats* st) {
+    if (kTrack) {
+        if (act && !keep) atomicAdd(&s_ndup[lc], 1u);
+        if (act && keep && !(e.w & GM_PAIRED)) atomicAdd(&s_nunp[lc], 1u);
+        if (act && keep && (e.w & GM_BAD)) atomicOr(&st->err, ERR_BADREAD);
     }
-    return x;
 }
 
 __device__ __forceinline__ bool same_key(const GElem& p, const GElem& e, bool& dup3) {
@@ -650,8 +690,9 @@ __device__ __forceinline__ bool same_key(const GElem& p, const GElem& e, bool& d
 template <bool kStage>
 __device__ __forceinline__ void group_b_rank(const GElem* __restrict__ gel2, uint32_t k0, uint32_t k1,
                                              uint32_t* cnt, int lane, unsigned long long lt, GElem* stage,
-                                             const uint32_t* cbase, const uint32_t* cstart, int mode,
-                                             unsigned long long* __restrict__ pel, DedupAcc& acc) {
+                                             const uint32_t* cbase, const uint32_t* cstart, int mode, int unit,
+                                             uint32_t* __restrict__ pel, DedupAcc& acc, uint32_t* s_ndup,
+                                             uint32_t* s_nunp, DevStats* st) {
     for (uint32_t k = k0; k < k1; k += kWave) {
         const uint32_t j = k + lane;
         const bool act = j < k1;
@@ -688,7 +729,9 @@ __device__ __forceinline__ void group_b_rank(const GElem* __restrict__ gel2, uin
                         }
                     }
                 }
-                pel[dest] = group_b_emit(e, dup2, dup3, mode, acc);
+                bool keep;
+                pel[dest] = group_b_emit(e, dup2, dup3, mode, unit, acc, keep);
+                cell_tally<true>(true, lc, keep, e, s_ndup, s_nunp, st);
             }
         }
     }
@@ -712,16 +755,19 @@ constexpr int kBPer = kStageB / kBlock;  // elements per lane per step
 #ifndef MGP_GB_LOOK
 #define MGP_GB_LOOK 4  // predecessors compared branch-free before a walk back (A/B: 2-6)
 #endif
+template <bool kTrack>
 __global__ void __launch_bounds__(kBlock, MGP_GB_WAVES) k_group_b(const GElem* __restrict__ gel2,
                                                     const uint32_t* __restrict__ bucket_off,
                                                     const uint32_t* __restrict__ O, Geom g, int ngroups, int rb,
-                                                    int mode, unsigned long long* __restrict__ pel,
+                                                    int mode, int unit, uint32_t* __restrict__ pel,
+                                                    uint8_t* __restrict__ any_paired,
                                                     unsigned long long* __restrict__ dup_part, DevStats* st) {
     __shared__ GElem stage[kStageB];
     __shared__ uint32_t wcnt[kBlock / kWave][kGroup];
     __shared__ uint32_t cbase[kGroup], cstart[kGroup + 1];
     __shared__ uint32_t bst[kMaxRbB], bsz[kMaxRbB], spre[kMaxRbB + 1];
     __shared__ int s_be;
+    __shared__ uint32_t s_ndup[kGroup], s_nunp[kGroup];  // the group's duplicates / kept unpaired reads in this bin range
     const int gi = blockIdx.x;
     const int B0 = blockIdx.y * rb, B1 = min(g.nbins, B0 + rb);
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -736,7 +782,11 @@ __global__ void __launch_bounds__(kBlock, MGP_GB_WAVES) k_group_b(const GElem* _
         bst[x] = o0;
         bsz[x] = bucket_off[(size_t)(B0 + x) * bo + gi + 1] - o0;
     }
-    if (wid == 0) cbase[lane] = c < nc ? O[(size_t)B0 * nc + c] : 0u;  // each cell's next slot
+    if (wid == 0) {
+        cbase[lane] = c < nc ? O[(size_t)B0 * nc + c] : 0u;  // each cell's next slot
+        s_ndup[lane] = 0u;
+        s_nunp[lane] = 0u;
+    }
     __syncthreads();
     // bins [b, s_be) of the step starting at b: as many as fit the stage (one if its
     // bucket alone is larger: direct path); spre = prefix of their bucket sizes
@@ -794,7 +844,7 @@ __global__ void __launch_bounds__(kBlock, MGP_GB_WAVES) k_group_b(const GElem* _
                 wcnt[0][lane] = cbase[lane];
                 __builtin_amdgcn_wave_barrier();
                 group_b_rank<false>(gel2, bst[b - B0], bst[b - B0] + bsz[b - B0], wcnt[0], lane, lt, nullptr,
-                                    nullptr, nullptr, mode, pel, acc);
+                                    nullptr, nullptr, mode, unit, pel, acc, s_ndup, s_nunp, st);
                 __builtin_amdgcn_wave_barrier();
                 cbase[lane] = wcnt[0][lane];
             }
@@ -865,6 +915,7 @@ __global__ void __launch_bounds__(kBlock, MGP_GB_WAVES) k_group_b(const GElem* _
         // back is needed only behind kLook + 1 equal starts.
         constexpr int kWo = 2;
         constexpr int kLook = MGP_GB_LOOK;
+
 #pragma unroll
         for (int h = 0; h < kBPer; h += kWo) {
             GElem xs[kWo];
@@ -909,11 +960,14 @@ __global__ void __launch_bounds__(kBlock, MGP_GB_WAVES) k_group_b(const GElem* _
 #pragma unroll
             for (int q = 0; q < kWo; ++q) {
                 const uint32_t t = threadIdx.x + (uint32_t)(h + q) * kBlock;
-                if (t < cur) {
-                    const int lc = (int)((xs[q].w >> GM_LCELL_SHIFT) & (kGroup - 1));
-                    const unsigned long long pv = group_b_emit(xs[q], d2[q], d3[q], mode, acc);
-                    if (MGP_ABL_B < 2 || pv == 7ull) pel[cbase[lc] + (t - cstart[lc])] = pv;
+                const bool act = t < cur;
+                const int lc = (int)((xs[q].w >> GM_LCELL_SHIFT) & (kGroup - 1));
+                bool keep = false;
+                if (act) {
+                    const uint32_t pv = group_b_emit(xs[q], d2[q], d3[q], mode, unit, acc, keep);
+                    if (MGP_ABL_B < 2 || pv == 7u) pel[cbase[lc] + (t - cstart[lc])] = pv;
                 }
+                cell_tally<kTrack>(act, lc, keep, xs[q], s_ndup, s_nunp, st);
             }
         }
         __syncthreads();
@@ -922,6 +976,11 @@ __global__ void __launch_bounds__(kBlock, MGP_GB_WAVES) k_group_b(const GElem* _
         b = nb0;
         be = nbe;
         tot = ntot;
+    }
+    // the group's per-cell paired flags over this bin range (kTrack)
+    if (kTrack && wid == 0 && c < nc) {
+        const uint32_t kept = cbase[lane] - O[(size_t)B0 * nc + c] - s_ndup[lane];
+        if (kept > s_nunp[lane]) any_paired[c] = 1;  // benign race: every writer stores 1
     }
     // per-workgroup duplicate counts (k_run_stats sums them)
     const unsigned long long d2 = wave_sum(acc.d2), d3 = wave_sum(acc.d3);
@@ -1434,25 +1493,26 @@ __device__ __forceinline__ void pile_line(bool has, bool packed, const uint8_t* 
     span_err = span_err || se;
 }
 
-constexpr int kWaveQ = 2 * kWave;    // per-wave queue of reads waiting to be piled (LDS)
+constexpr int kWaveQ = 4 * kWave;    // per-wave ring of reads waiting to be piled (LDS, power of two)
+constexpr int kStreamU = 2;          // pileup elements per lane per stream step
 
-// record offset of a pileup element (MGP_ABL 6, experiments only: every record
-// read from the first 256 MiB of the payload, to time the pileup with a small
-// gather footprint; the counts are then meaningless)
-__device__ __forceinline__ unsigned long long rec_at(unsigned long long qe) {
-    return MGP_ABL == 6 ? (qe & GP_OFF) & ((256ull << 20) - 128) : (qe & GP_OFF);
+// record byte offset of a pileup element (MGP_ABL 6, experiments only: every
+// record read from the first 256 MiB of the payload, to time the pileup with a
+// small gather footprint; the counts are then meaningless)
+__device__ __forceinline__ unsigned long long rec_at(uint32_t qe, int unit) {
+    const unsigned long long off = (unsigned long long)(qe & PE_OFF) << unit;
+    return MGP_ABL == 6 ? off & ((256ull << 20) - 128) : off;
 }
 constexpr uint32_t kSeg = 65535;     // elements per tile segment (16-bit halves cannot carry)
 
 // grid (nchunks, nwin): workgroup = (cell chunk, position window). For each cell
 // of the chunk, the cell's pileup elements with start bin in [window start -
 // reach, window end) are taken by the 4 waves independently, in interleaved
-// chunks of 64 (the next chunk's elements loaded while the current one is
-// queued); the reads marked for piling (kept by pass B's duplicate marking, MAPQ
-// passed) go to the wave's LDS queue and are piled 64 at a time, one read per
-// lane. The window owning a read's start bin counts it for the per-cell kept-read
-// total and flags (processors.py:22,34,48). Workgroup barriers only at cell
-// boundaries; the packed tile is then strand-filtered and flushed.
+// blocks of 128 (the next step's elements loaded while the current one is
+// queued); the reads to pile (kept by pass B's duplicate marking, MAPQ passed)
+// go to the wave's LDS ring and are piled 64 at a time, one read per lane.
+// Workgroup barriers only at cell boundaries; the packed tile is then
+// strand-filtered and flushed.
 #ifndef MGP_PILEUP_WAVES
 #define MGP_PILEUP_WAVES 4
 #endif
@@ -1474,16 +1534,16 @@ struct Out16 {
 __device__ __forceinline__ uint32_t sat16(uint32_t v) { return v > 0xFFFFu ? 0xFFFFu : v; }
 
 __global__ void __launch_bounds__(kBlock, MGP_PILEUP_WAVES) k_pileup(
-    Geom g, PileCfg pc, const uint8_t* __restrict__ payload, const unsigned long long* __restrict__ pel,
+    Geom g, PileCfg pc, const uint8_t* __restrict__ payload, const uint32_t* __restrict__ pel, int unit,
     const uint32_t* __restrict__ O, Out16 o16, uint32_t* __restrict__ counts, uint32_t* __restrict__ tn5,
-    uint32_t* __restrict__ depth, uint32_t* __restrict__ n_reads, uint8_t* __restrict__ any_paired,
-    uint32_t* __restrict__ covered, unsigned long long* __restrict__ dsum, uint32_t* __restrict__ dmax,
-    uint32_t* __restrict__ tally_part, DevStats* st) {
+    uint32_t* __restrict__ depth, uint32_t* __restrict__ n_reads, uint8_t* __restrict__ any_paired, int pair_mode,
+    uint32_t* __restrict__ covered, unsigned long long* __restrict__ dsum,
+    uint32_t* __restrict__ dmax, uint32_t* __restrict__ tally_part, DevStats* st) {
     extern __shared__ __align__(16) uint32_t tile[];  // [Wp][4] A, C, G, T, then [Wp] Tn5 (fwd | rev << 16)
     uint32_t* t5 = tile + 4 * g.Wp;
-    __shared__ unsigned long long wq_all[kBlock / kWave][kWaveQ];
+    __shared__ uint32_t wq_all[kBlock / kWave][kWaveQ];
     __shared__ uint32_t r_cov[4], r_max[4], r_keep[4];
-    __shared__ unsigned long long r_sum[4], r_flags[4];
+    __shared__ unsigned long long r_sum[4];
 
     const int k = blockIdx.y;
     const int chunk = blockIdx.x;
@@ -1493,7 +1553,7 @@ __global__ void __launch_bounds__(kBlock, MGP_PILEUP_WAVES) k_pileup(
     w.Wp = g.Wp;
     const int L = g.L;
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    unsigned long long* wq = wq_all[wid];
+    uint32_t* wq = wq_all[wid];
     const uint32_t max_span = st->max_span;
     const int R = (int)((max_span + g.G - 1) / g.G) * g.G;
     const int lo_bin = win_lo_bin(k, R, g);
@@ -1501,8 +1561,8 @@ __global__ void __launch_bounds__(kBlock, MGP_PILEUP_WAVES) k_pileup(
     const int hi_bin = k == g.nwin - 1 ? g.nbins : win_hi_bin(k, g);
     const int nc = g.nc;
     const unsigned long long lt = lanemask_lt();
-    bool span_err = false, bad_read = false;  // the latter: a kept read without SEQ/QUAL
-    bool pk_err = false;                      // a packed record outside the packed layout's limits
+    bool span_err = false;
+    bool pk_err = false;  // a packed record outside the packed layout's limits
 
     uint32_t tal[kMaxPosPerThread][4];
 #pragma unroll
@@ -1526,42 +1586,54 @@ __global__ void __launch_bounds__(kBlock, MGP_PILEUP_WAVES) k_pileup(
             n_own = O[(size_t)own_bin * nc + c + 1];
             n_hi = O[(size_t)hi_bin * nc + c + 1];
         }
-        const bool drained = hi - lo > kSeg;  // tile drained into the output rows between segments
-        // kept reads and their flags, counted once: by the window owning the start bin
+        // kept reads, counted once: by the window owning the start bin
         uint32_t nkeep = 0;
-        unsigned long long fl = 0;
+        const bool drained = hi - lo > kSeg;  // tile drained into the output rows between segments
         for (uint32_t seg = lo; seg < hi; seg += kSeg) {
             const uint32_t seg_hi = min(hi, seg + kSeg);
-            uint32_t qn = 0;  // wave-uniform queue fill
-            uint32_t cb = seg + kWave * wid;
-            unsigned long long pe = cb + lane < seg_hi ? pel[cb + lane] : 0ull;
-            for (; cb < seg_hi; cb += kBlock) {
-                const unsigned long long cur = pe;
-                const uint64_t nj = (uint64_t)cb + kBlock + lane;
-                pe = nj < seg_hi ? pel[nj] : 0ull;
-                if (cb + lane >= own) {  // cur is 0 past seg_hi
-                    nkeep += (cur & GP_KEEP) != 0ull;
-                    fl |= cur;
+            // the wave's ring of queued reads: [qh, qh + qn), wave-uniform
+            uint32_t qh = 0, qn = 0;
+            // a stream step: each wave takes kStreamU x 64 consecutive elements (the
+            // waves' blocks interleaved), the next step's loaded while this one is
+            // queued and piled
+            constexpr uint32_t kStepW = kStreamU * kWave, kStepB = kStepW * (kBlock / kWave);
+            uint32_t cb = seg + kStepW * wid;
+            uint32_t pe[kStreamU];
+#pragma unroll
+            for (int u = 0; u < kStreamU; ++u) {
+                const uint32_t j = cb + u * kWave + lane;
+                pe[u] = j < seg_hi ? pel[j] : PE_DUP;
+            }
+            for (; cb < seg_hi; cb += kStepB) {
+                uint32_t cur[kStreamU];
+#pragma unroll
+                for (int u = 0; u < kStreamU; ++u) {
+                    cur[u] = pe[u];
+                    const uint64_t j = (uint64_t)cb + kStepB + u * kWave + lane;
+                    pe[u] = j < seg_hi ? pel[j] : PE_DUP;
                 }
-                const bool piled = (cur & GP_PILE) != 0ull;
-                const unsigned long long bal = __ballot(piled);
-                if (piled) wq[qn + (uint32_t)__popcll(bal & lt)] = cur;
-                qn += (uint32_t)__popcll(bal);
+#pragma unroll
+                for (int u = 0; u < kStreamU; ++u) {
+                    nkeep += (cb + u * kWave + lane >= own) & (cur[u] != PE_DUP);  // PE_DUP past seg_hi
+                    const bool piled = cur[u] < PE_KEEP;
+                    const unsigned long long bal = __ballot(piled);
+                    if (piled) wq[(qh + qn + (uint32_t)__popcll(bal & lt)) & (kWaveQ - 1)] = cur[u];
+                    qn += (uint32_t)__popcll(bal);
+                }
                 __builtin_amdgcn_wave_barrier();
-                if (qn >= (uint32_t)kWave) {
-                    const unsigned long long qe = wq[lane];
+                while (qn >= (uint32_t)kWave) {
+                    const uint32_t qe = wq[(qh + lane) & (kWaveQ - 1)];
+                    qh += kWave;
                     qn -= kWave;
-                    if ((uint32_t)lane < qn) wq[lane] = wq[kWave + lane];
-                    __builtin_amdgcn_wave_barrier();
-                    pile_read(true, (qe & GP_PACKED) != 0ull, payload + rec_at(qe), w, pc, tile, t5, max_span,
+                    pile_read(true, (qe & PE_PACKED) != 0u, payload + rec_at(qe, unit), w, pc, tile, t5, max_span,
                               span_err, pk_err);
                 }
             }
             {   // tail: every lane of the wave enters, lanes past qn hold no read
                 const bool has = (uint32_t)lane < qn;
-                const unsigned long long qe = has ? wq[lane] : 0ull;
-                pile_read(has, (qe & GP_PACKED) != 0ull, payload + rec_at(qe), w, pc, tile, t5, max_span, span_err,
-                          pk_err);
+                const uint32_t qe = has ? wq[(qh + lane) & (kWaveQ - 1)] : 0u;
+                pile_read(has, (qe & PE_PACKED) != 0u, payload + rec_at(qe, unit), w, pc, tile, t5, max_span,
+                          span_err, pk_err);
             }
             if (drained) {  // add this segment's packed tile into the 32-bit output rows
                 __syncthreads();
@@ -1586,7 +1658,6 @@ __global__ void __launch_bounds__(kBlock, MGP_PILEUP_WAVES) k_pileup(
             }
         }
         nkeep = wave_sum(nkeep);
-        fl = wave_or(fl);
         __syncthreads();
         uint32_t cov = 0, mx = 0;
         unsigned long long sum = 0;
@@ -1671,28 +1742,27 @@ __global__ void __launch_bounds__(kBlock, MGP_PILEUP_WAVES) k_pileup(
             r_sum[wid] = sum;
             r_max[wid] = mx;
             r_keep[wid] = nkeep;
-            r_flags[wid] = fl;
         }
         __syncthreads();
         if (threadIdx.x == 0) {
             o16.wide[(size_t)c * g.nwin + k] = drained ? 1u : 0u;
             uint32_t C = 0, M = 0, K = 0;
-            unsigned long long S = 0, F = 0;
+            unsigned long long S = 0;
             for (int q = 0; q < 4; ++q) {
                 C += r_cov[q];
                 S += r_sum[q];
                 M = max(M, r_max[q]);
                 K += r_keep[q];
-                F |= r_flags[q];
             }
             if (C) {
                 atomicAdd(&covered[c], C);
                 atomicAdd(&dsum[c], S);
                 atomicMax(&dmax[c], M);
             }
-            if (K) atomicAdd(&n_reads[c], K);
-            if (F & GP_PAIRED) any_paired[c] = 1;  // benign race: every writer stores 1
-            if (F & GP_BAD) bad_read = true;
+            if (K) {
+                atomicAdd(&n_reads[c], K);
+                if (pair_mode) any_paired[c] = 1;  // benign race: every writer stores 1
+            }
         }
     }
 #pragma unroll
@@ -1707,7 +1777,6 @@ __global__ void __launch_bounds__(kBlock, MGP_PILEUP_WAVES) k_pileup(
     if (lane == 0 && anyspan) atomicOr(&st->err, ERR_SPAN);
     const bool anypk = __ballot(pk_err) != 0ull;
     if (lane == 0 && anypk) atomicOr(&st->err, ERR_PACKED);
-    if (threadIdx.x == 0 && bad_read) atomicOr(&st->err, ERR_BADREAD);
 }
 
 // min-reads gate (processors.py:22) for min_reads > 1: a cell with fewer kept
@@ -1975,16 +2044,24 @@ __global__ void k_add_u64(uint64_t* __restrict__ a, int64_t n, uint64_t add) {
 // record offset is kRecStride x its read index (a fully packed, dense payload);
 // grouping pass A then computes the offsets instead of reading them.
 // Also writes the compact u32 column roff32 = rec_off >> 6 and sets bit 2 when an
-// offset does not fit it (not a multiple of 64, or >= 2^38).
-__global__ void k_check_stride(const uint64_t* __restrict__ roff, int64_t n, int64_t i0, uint32_t* irregular,
-                               uint32_t* __restrict__ roff32) {
+// offset does not fit it (not a multiple of 64, or >= 2^38). The flag word sets
+// CHK_PAIRED / CHK_UNPAIRED / CHK_NOSEQ when some read is paired / unpaired /
+// lacks SEQ or QUAL (k_group_b tracks pairedness and SEQ per read only when the
+// reads mix or lack them).
+constexpr uint32_t CHK_PAIRED = 4u, CHK_UNPAIRED = 8u, CHK_NOSEQ = 16u;
+__global__ void k_check_stride(const uint64_t* __restrict__ roff, const uint16_t* __restrict__ flag, int64_t n,
+                               int64_t i0, uint32_t* irregular, uint32_t* __restrict__ roff32) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const uint64_t r = i < n ? roff[i] : 0ull;
+    const uint32_t f = i < n ? flag[i] : 0u;
     if (i < n) roff32[i] = (uint32_t)(r >> 6);
     const bool bad = i < n && r != (uint64_t)(i0 + i) * kRecStride;
     const bool wide = i < n && ((r & 63ull) != 0ull || (r >> 38) != 0ull);
     const unsigned long long b1 = __ballot(bad), b2 = __ballot(wide);
-    const uint32_t bits = (b1 ? 1u : 0u) | (b2 ? 2u : 0u);
+    const unsigned long long b3 = __ballot(i < n && (f & MGP_FLAG_PAIRED)), b4 = __ballot(i < n && !(f & MGP_FLAG_PAIRED));
+    const unsigned long long b5 = __ballot(i < n && (f & MGP_FLAG_NOSEQQUAL));
+    const uint32_t bits = (b1 ? 1u : 0u) | (b2 ? 2u : 0u) | (b3 ? CHK_PAIRED : 0u) | (b4 ? CHK_UNPAIRED : 0u) |
+                          (b5 ? CHK_NOSEQ : 0u);
     // one atomic per wave at most, and none once the bits are set (every wave of a
     // paired payload has irregular offsets: 3M atomics on one word took 18 ms)
     if (bits && (threadIdx.x & 63) == 0 && (__atomic_load_n(irregular, __ATOMIC_RELAXED) & bits) != bits)
@@ -2187,8 +2264,8 @@ int mgp_push_batch(mgp_ctx* ctx, const mgp_batch* b) {
     MGP_TRY(ctx->roff_irregular.ensure(4));
     if (n0 == 0) HIP_TRY(hipMemsetAsync(ctx->roff_irregular.p, 0, 4, s));
     ctx->roff_mode = -1;
-    k_check_stride<<<blocks_for(nb), kBlock, 0, s>>>(ctx->roff.as<uint64_t>() + n0, nb, n0,
-                                                     ctx->roff_irregular.as<uint32_t>(),
+    k_check_stride<<<blocks_for(nb), kBlock, 0, s>>>(ctx->roff.as<uint64_t>() + n0, ctx->flag.as<uint16_t>() + n0,
+                                                     nb, n0, ctx->roff_irregular.as<uint32_t>(),
                                                      ctx->roff32.as<uint32_t>() + n0);
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipEventRecord(ctx->ev_copy, s));
@@ -2228,7 +2305,7 @@ static int ensure_run_buffers(mgp_ctx* ctx) {
     MGP_TRY(ctx->P.ensure((size_t)((g.nbins + 31) / 32 + 1) * nc * 4));
     MGP_TRY(ctx->cell_cnt.ensure(nc * 4));
     MGP_TRY(ctx->cell_base.ensure(nc * 4));
-    MGP_TRY(ctx->pel.ensure(n * 8));
+    MGP_TRY(ctx->pel.ensure(n * 4));
     MGP_TRY(ctx->gel2.ensure(n * sizeof(GElem)));
     MGP_TRY(ctx->bin_valid.ensure((size_t)(g.nbins + 1) * 4));
     MGP_TRY(ctx->bin_mspan.ensure((size_t)(g.nbins + 1) * 4));
@@ -2281,7 +2358,15 @@ int mgp_run(mgp_ctx* ctx) {
         HIP_TRY(hipStreamSynchronize(ctx->s_copy));
         HIP_TRY(hipMemcpy(&irr, ctx->roff_irregular.p, 4, hipMemcpyDeviceToHost));
         ctx->roff_mode = !(irr & 1u) ? kOffDense : !(irr & 2u) ? kOffR32 : kOffR64;
+        ctx->read_bits = irr;
     }
+    // the pileup element's record offset unit: 64 bytes, or 16 bytes when some
+    // record is not 64-byte aligned; either way a 31-bit count of units
+    const int unit = ctx->roff_mode == kOffR64 ? 4 : 6;
+    if (n > 0 && (uint64_t)ctx->pay >= ((uint64_t)(PE_KEEP & PE_OFF) << unit))
+        return set_err(MGP_E_INVALID, unit == 6 ? "payload larger than 128 GiB in one context; shard the cells"
+                                                : "payload with 16-byte aligned records larger than 32 GiB in one "
+                                                  "context; place records at 64-byte offsets or shard the cells");
     HIP_TRY(hipStreamWaitEvent(s, ctx->ev_copy, 0));
     const int slot = (int)(ctx->runs % mgp_ctx::kRing);
     for (int i = 0; i < ST_N; ++i) ctx->stage_ran[slot][i] = false;
@@ -2364,8 +2449,9 @@ int mgp_run(mgp_ctx* ctx) {
         STAGE_END(ST_GROUP_A);
         STAGE_BEGIN(ST_GROUP_B);
         if (MGP_ABL_A == 1) HIP_TRY(hipMemsetAsync(ctx->gel2.p, 0, (size_t)n * sizeof(GElem), s));  // ablation
-        if (MGP_ABL_B >= 2) HIP_TRY(hipMemsetAsync(ctx->pel.p, 0, (size_t)n * 8, s));  // ablation: nothing piles
+        if (MGP_ABL_B >= 2) HIP_TRY(hipMemsetAsync(ctx->pel.p, 0xFF, (size_t)n * 4, s));  // ablation: nothing piles
         int dup_parts = 0;
+        int pair_mode = 0;  // 1: every read is paired, the pileup flags every cell with a kept read
         if (n > 0) {
             // about MGP_GB_WG workgroups (many per slot: 4 fit a CU, so a grid of a few
             // slot-rounds leaves a tail); bins per workgroup at most kMaxRbB, whose
@@ -2375,10 +2461,18 @@ int mgp_run(mgp_ctx* ctx) {
             dim3 gb((unsigned)ngroups, (unsigned)((g.nbins + rb - 1) / rb));
             dup_parts = (int)(gb.x * gb.y);
             MGP_TRY(ctx->dup_part.ensure((size_t)dup_parts * 16));
-            k_group_b<<<gb, kBlock, 0, s>>>(ctx->gel2.as<GElem>(), ctx->bucket_off.as<uint32_t>(), ctx->H.as<uint32_t>(),
-                                            g, ngroups, rb, ctx->cfg.dedup_mode,
-                                            ctx->pel.as<unsigned long long>(),
-                                            ctx->dup_part.as<unsigned long long>(), st);
+            // per-read pairedness / SEQ tracking only when the reads mix paired and
+            // unpaired ones or some read lacks SEQ/QUAL
+            const uint32_t rbits = ctx->read_bits;
+            const bool track = ((rbits & CHK_PAIRED) && (rbits & CHK_UNPAIRED)) || (rbits & CHK_NOSEQ);
+            auto launch_b = [&](auto kern) {
+                kern<<<gb, kBlock, 0, s>>>(ctx->gel2.as<GElem>(), ctx->bucket_off.as<uint32_t>(), ctx->H.as<uint32_t>(),
+                                           g, ngroups, rb, ctx->cfg.dedup_mode, unit, ctx->pel.as<uint32_t>(),
+                                           ctx->any_paired.as<uint8_t>(), ctx->dup_part.as<unsigned long long>(), st);
+            };
+            if (track) launch_b(k_group_b<true>);
+            else launch_b(k_group_b<false>);
+            pair_mode = track ? 0 : (rbits & CHK_PAIRED) ? 1 : 0;
             HIP_TRY(hipGetLastError());
         }
         STAGE_END(ST_GROUP_B);
@@ -2395,11 +2489,10 @@ int mgp_run(mgp_ctx* ctx) {
         pc.keep_tn5 = (ctx->cfg.flags & MGP_CFG_KEEP_TN5) != 0;
         dim3 gp(g.nchunks, g.nwin);
         const size_t psm = (size_t)5 * g.Wp * 4;
-        k_pileup<<<gp, kBlock, psm, s>>>(g, pc, ctx->payload.as<uint8_t>(), ctx->pel.as<unsigned long long>(),
+        k_pileup<<<gp, kBlock, psm, s>>>(g, pc, ctx->payload.as<uint8_t>(), ctx->pel.as<uint32_t>(), unit,
                                          ctx->H.as<uint32_t>(), out16_of(ctx), ctx->counts.as<uint32_t>(),
-                                         ctx->tn5.as<uint32_t>(),
-                                         ctx->depth.as<uint32_t>(), ctx->n_reads.as<uint32_t>(),
-                                         ctx->any_paired.as<uint8_t>(), ctx->covered.as<uint32_t>(),
+                                         ctx->tn5.as<uint32_t>(), ctx->depth.as<uint32_t>(), ctx->n_reads.as<uint32_t>(),
+                                         ctx->any_paired.as<uint8_t>(), pair_mode, ctx->covered.as<uint32_t>(),
                                          ctx->dsum.as<unsigned long long>(), ctx->dmax.as<uint32_t>(),
                                          ctx->tally_part.as<uint32_t>(), st);
         HIP_TRY(hipGetLastError());
@@ -2663,7 +2756,7 @@ int mgp_synth_generate(mgp_ctx* ctx, const mgp_synth_params* p) {
     HIP_TRY(hipMemsetAsync(ctx->roff_irregular.p, 0, 4, s));
     ctx->roff_mode = -1;
     if (n)
-        k_check_stride<<<blocks_for(n), kBlock, 0, s>>>(ctx->roff.as<uint64_t>(), n, 0,
+        k_check_stride<<<blocks_for(n), kBlock, 0, s>>>(ctx->roff.as<uint64_t>(), ctx->flag.as<uint16_t>(), n, 0,
                                                         ctx->roff_irregular.as<uint32_t>(),
                                                         ctx->roff32.as<uint32_t>());
     HIP_TRY(hipGetLastError());
