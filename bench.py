@@ -107,8 +107,9 @@ def main():
         # same reads are generated again at those offsets
         from mgatk2_amd.bam import PLACE_PAIRED, place_records
 
-        soa = eng.download_inputs(columns=("bc", "flag"))
-        roff, pay_b = place_records(soa.bc, soa.flag, np.full(n_reads, 64, np.uint32), n_cells, PLACE_PAIRED)
+        soa = eng.download_inputs(columns=("bc", "flag", "start", "tlen"))
+        roff, pay_b = place_records(soa.bc, soa.flag, np.full(n_reads, 64, np.uint32), n_cells, PLACE_PAIRED,
+                                    start=soa.start, tlen=soa.tlen)
         del soa
         eng.synth(seed, n_reads, cdf, ref, read_len=args.read_len, rec_align=64, pack=True, rec_off=roff,
                   payload_bytes=pay_b)

@@ -127,24 +127,31 @@ int64_t mgp_deflate_tiles(const void *data, int64_t rows, int64_t cols, int32_t 
  * cell share a 128-byte line (one streaming pass, lines opened in BAM order;
  * reads the engine's filters drop pair among themselves; full records take
  * 128-byte aligned slots of their own), so one line request of the pileup's
- * gather serves two reads of the cell it piles. Returns the payload bytes, -1
- * on error. Replaces no reference code (pysam hands out Python objects). */
+ * gather serves two reads of the cell it piles. With the start and tlen columns
+ * (either may be NULL: no such rule), a read that repeats the start, strand and
+ * |tlen| of an earlier read of its cell (a duplicate whenever dedup is on,
+ * readers.py:118-150) is placed with the dropped reads. Returns the payload
+ * bytes, -1 on error. Replaces no reference code (pysam hands out Python
+ * objects). */
 #define MGP_PLACE_DENSE  0
 #define MGP_PLACE_PAIRED 1
-int64_t mgp_place_records(int64_t n, const int32_t *bc, const uint16_t *flag, const uint32_t *rec_bytes,
-                          int32_t n_cells, int32_t mode, int32_t rec_align, uint64_t *rec_off);
+int64_t mgp_place_records(int64_t n, const int32_t *bc, const uint16_t *flag, const int32_t *start,
+                          const int32_t *tlen, const uint32_t *rec_bytes, int32_t n_cells, int32_t mode,
+                          int32_t rec_align, uint64_t *rec_off);
 
 /* Cell sharding: gather the payload records idx[0..m) of a
  * batch into a new payload for one device. mgp_gather_offsets reads each
  * record's size from its header (mgp_record_bytes; any source placement),
  * rebases the cell ids to [cell_lo, cell_lo + n_cells) (-1 outside), places the
- * subset with mgp_place_records(mode, rec_align) and returns the new payload
+ * subset with mgp_place_records(mode, rec_align; start/tlen as given, may be
+ * NULL) and returns the new payload
  * bytes (-1 on error). mgp_gather_records copies the records there on
  * n_threads threads; `out` must be zero-filled by the caller (gaps stay as they
  * are). Replaces no reference code: the reference runs on one process. */
 int64_t mgp_gather_offsets(const uint8_t *payload, const uint64_t *rec_off, const uint16_t *flag, const int32_t *bc,
-                           int64_t n_total, int64_t payload_bytes, const int64_t *idx, int64_t m, int32_t cell_lo,
-                           int32_t n_cells, int32_t mode, int32_t rec_align, uint64_t *out_off);
+                           const int32_t *start, const int32_t *tlen, int64_t n_total, int64_t payload_bytes,
+                           const int64_t *idx, int64_t m, int32_t cell_lo, int32_t n_cells, int32_t mode,
+                           int32_t rec_align, uint64_t *out_off);
 int mgp_gather_records(const uint8_t *payload, const uint64_t *rec_off, const uint16_t *flag, int64_t n_total,
                        int64_t payload_bytes, const int64_t *idx, int64_t m, const uint64_t *out_off,
                        int64_t out_bytes, uint8_t *out, int n_threads);

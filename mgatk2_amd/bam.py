@@ -93,10 +93,10 @@ def host_library() -> C.CDLL:
         lib.mgp_deflate_tiles.argtypes = [vp, C.c_int64, C.c_int64, C.c_int32, C.c_int64, C.c_int64, C.c_int, C.c_int,
                                           C.POINTER(C.POINTER(C.c_uint8)), vp]
         lib.mgp_deflate_tiles.restype = C.c_int64
-        lib.mgp_place_records.argtypes = [C.c_int64, vp, vp, vp, C.c_int32, C.c_int32, C.c_int32, vp]
+        lib.mgp_place_records.argtypes = [C.c_int64, vp, vp, vp, vp, vp, C.c_int32, C.c_int32, C.c_int32, vp]
         lib.mgp_place_records.restype = C.c_int64
-        lib.mgp_gather_offsets.argtypes = [vp, vp, vp, vp, C.c_int64, C.c_int64, vp, C.c_int64, C.c_int32, C.c_int32,
-                                           C.c_int32, C.c_int32, vp]
+        lib.mgp_gather_offsets.argtypes = [vp, vp, vp, vp, vp, vp, C.c_int64, C.c_int64, vp, C.c_int64, C.c_int32,
+                                           C.c_int32, C.c_int32, C.c_int32, vp]
         lib.mgp_gather_offsets.restype = C.c_int64
         lib.mgp_gather_records.argtypes = [vp, vp, vp, C.c_int64, C.c_int64, vp, C.c_int64, vp, C.c_int64, vp,
                                            C.c_int]
@@ -118,10 +118,13 @@ PLACE_DENSE, PLACE_PAIRED = 0, 1  # include/mgpileup_host.h MGP_PLACE_*
 
 
 def place_records(bc: np.ndarray, flag: np.ndarray, rec_bytes: np.ndarray, n_cells: int,
-                  mode: int = PLACE_PAIRED, rec_align: int = 64) -> tuple[np.ndarray, int]:
+                  mode: int = PLACE_PAIRED, rec_align: int = 64, start: np.ndarray | None = None,
+                  tlen: np.ndarray | None = None) -> tuple[np.ndarray, int]:
     """Producer placement of payload records (mgp_place_records): returns
     (rec_off, payload_bytes). PLACE_PAIRED puts two consecutive packed records of
-    one cell into one 128-byte line."""
+    one cell into one 128-byte line; given start and tlen, a read repeating the
+    start, strand and |tlen| of an earlier read of its cell goes with the dropped
+    reads (a duplicate whenever dedup is on)."""
     lib = host_library()
     n = int(bc.shape[0])
     bc = np.ascontiguousarray(bc, np.int32)
@@ -129,8 +132,15 @@ def place_records(bc: np.ndarray, flag: np.ndarray, rec_bytes: np.ndarray, n_cel
     rb = np.ascontiguousarray(rec_bytes, np.uint32)
     if flag.shape[0] != n or rb.shape[0] != n:
         raise ValueError("bc, flag and rec_bytes must have the same length")
+    keyed = start is not None and tlen is not None
+    if keyed:
+        start = np.ascontiguousarray(start, np.int32)
+        tlen = np.ascontiguousarray(tlen, np.int32)
+        if start.shape[0] != n or tlen.shape[0] != n:
+            raise ValueError("start and tlen must have the reads' length")
     off = np.empty(n, np.uint64)
-    tot = lib.mgp_place_records(n, bc.ctypes.data, flag.ctypes.data, rb.ctypes.data, int(n_cells), int(mode),
+    tot = lib.mgp_place_records(n, bc.ctypes.data, flag.ctypes.data, start.ctypes.data if keyed else None,
+                                tlen.ctypes.data if keyed else None, rb.ctypes.data, int(n_cells), int(mode),
                                 int(rec_align), off.ctypes.data)
     if tot < 0:
         raise ValueError(_err())

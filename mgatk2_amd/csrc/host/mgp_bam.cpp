@@ -27,6 +27,7 @@
 
 #include "../../../include/mgpileup.h"
 #include "../../../include/mgpileup_host.h"
+#include "mgp_place.h"
 
 // one thread-local error string for every entry point of libmgphost.so
 std::string& mgp_host_err() {
@@ -733,6 +734,7 @@ int mgp_bam_read_ref(mgp_bam* b, int tid, int rec_align, mgp_bam_batch* out) {
         if (b->bulk_cell >= 0) n_keys = std::max(n_keys, b->bulk_cell + 1);
     }
     std::vector<uint64_t> open(paired ? (size_t)n_keys + 1 : 0, ~0ull);
+    mgp_host::DupTracker dups(paired ? (size_t)n_keys : 0);  // a cell's repeated keys go with the dropped reads
     uint64_t cursor = 0;  // paired: payload bytes placed so far (128-byte lines)
     // one record: decode (do_fields: the SoA columns, barcode lookup included) and
     // pack (do_rec: the payload record at offset off) at index k
@@ -884,6 +886,9 @@ int mgp_bam_read_ref(mgp_bam* b, int tid, int rec_align, mgp_bam_batch* out) {
                 }
                 const int32_t c = G_bc.p[k];
                 size_t key = (c >= 0 && c < n_keys && !(G_flag.p[k] & drop)) ? (size_t)c : (size_t)n_keys;
+                if (key < (size_t)n_keys &&
+                    dups.repeat(key, G_start.p[k], (G_flag.p[k] & MGP_FLAG_REVERSE) != 0, G_tlen.p[k]))
+                    key = (size_t)n_keys;
                 if (open[key] != ~0ull) {
                     G_roff.p[k] = open[key] + MGP_PACK_BYTES;
                     open[key] = ~0ull;

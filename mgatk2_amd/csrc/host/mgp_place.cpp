@@ -10,9 +10,11 @@
 // in BAM order, so the placement is one streaming pass with a table of one
 // offset per cell (what a decoder can do as it emits records). Reads the engine
 // drops at its filters (readers.py:95-111: no whitelisted barcode, unmapped,
-// secondary, supplementary) pair among themselves; full-layout records take
-// their own 128-byte aligned slots. Any placement gives the same results: the
-// engine reads every record at its rec_off.
+// secondary, supplementary) pair among themselves, and so do, given the start
+// and tlen columns, a cell's reads that repeat the start, strand and |tlen| of
+// an earlier read of the cell (duplicates, never piled: mgp_place.h); full-layout
+// records take their own 128-byte aligned slots. Any placement gives the same
+// results: the engine reads every record at its rec_off.
 #include <algorithm>
 #include <cstdint>
 #include <cstring>
@@ -21,6 +23,7 @@
 
 #include "../../../include/mgpileup.h"
 #include "../../../include/mgpileup_host.h"
+#include "mgp_place.h"
 
 std::string& mgp_host_err();  // mgp_bam.cpp
 
@@ -31,8 +34,9 @@ constexpr uint64_t kNone = ~0ull;
 
 extern "C" {
 
-int64_t mgp_place_records(int64_t n, const int32_t* bc, const uint16_t* flag, const uint32_t* rec_bytes,
-                          int32_t n_cells, int32_t mode, int32_t rec_align, uint64_t* rec_off) {
+int64_t mgp_place_records(int64_t n, const int32_t* bc, const uint16_t* flag, const int32_t* start,
+                          const int32_t* tlen, const uint32_t* rec_bytes, int32_t n_cells, int32_t mode,
+                          int32_t rec_align, uint64_t* rec_off) {
     mgp_host_err().clear();
     if (n < 0 || (n && (!bc || !flag || !rec_bytes || !rec_off)) || n_cells < 0 || rec_align < 16 ||
         rec_align > 4096 || (rec_align & (rec_align - 1)) || (mode != MGP_PLACE_DENSE && mode != MGP_PLACE_PAIRED)) {
@@ -51,6 +55,8 @@ int64_t mgp_place_records(int64_t n, const int32_t* bc, const uint16_t* flag, co
     // paired: open[k] = the line of key k whose second half is free
     std::vector<uint64_t> open((size_t)n_cells + 1, kNone);
     const uint16_t drop = MGP_FLAG_UNMAPPED | MGP_FLAG_SECONDARY | MGP_FLAG_SUPPLEMENTARY;
+    const bool keyed = start && tlen;
+    mgp_host::DupTracker dups(keyed ? (size_t)n_cells : 0);
     for (int64_t i = 0; i < n; ++i) {
         const uint16_t f = flag[i];
         if (!(f & MGP_FLAG_PACKED) || rec_bytes[i] != MGP_PACK_BYTES) {
@@ -60,7 +66,9 @@ int64_t mgp_place_records(int64_t n, const int32_t* bc, const uint16_t* flag, co
             continue;
         }
         const int32_t c = bc[i];
-        const size_t k = (c >= 0 && c < n_cells && !(f & drop)) ? (size_t)c : (size_t)n_cells;
+        size_t k = (c >= 0 && c < n_cells && !(f & drop)) ? (size_t)c : (size_t)n_cells;
+        if (keyed && k < (size_t)n_cells && dups.repeat(k, start[i], (f & MGP_FLAG_REVERSE) != 0, tlen[i]))
+            k = (size_t)n_cells;
         if (open[k] != kNone) {
             rec_off[i] = open[k] + MGP_PACK_BYTES;
             open[k] = kNone;

@@ -22,8 +22,9 @@ std::string& mgp_host_err();  // mgp_bam.cpp
 extern "C" {
 
 int64_t mgp_gather_offsets(const uint8_t* payload, const uint64_t* rec_off, const uint16_t* flag, const int32_t* bc,
-                           int64_t n_total, int64_t payload_bytes, const int64_t* idx, int64_t m, int32_t cell_lo,
-                           int32_t n_cells, int32_t mode, int32_t rec_align, uint64_t* out_off) {
+                           const int32_t* start, const int32_t* tlen, int64_t n_total, int64_t payload_bytes,
+                           const int64_t* idx, int64_t m, int32_t cell_lo, int32_t n_cells, int32_t mode,
+                           int32_t rec_align, uint64_t* out_off) {
     mgp_host_err().clear();
     if ((n_total && (!payload || !rec_off || !flag || !bc)) || (m && (!idx || !out_off)) || m < 0 || n_total < 0 ||
         n_cells < 0) {
@@ -35,6 +36,8 @@ int64_t mgp_gather_offsets(const uint8_t* payload, const uint64_t* rec_off, cons
     std::vector<int32_t> lbc((size_t)m);
     std::vector<uint16_t> lfl((size_t)m);
     std::vector<uint32_t> sz((size_t)m);
+    const bool keyed = start && tlen;
+    std::vector<int32_t> lst(keyed ? (size_t)m : 0), ltl(keyed ? (size_t)m : 0);
     for (int64_t k = 0; k < m; ++k) {
         const int64_t i = idx[k];
         if (i < 0 || i >= n_total) {
@@ -53,10 +56,15 @@ int64_t mgp_gather_offsets(const uint8_t* payload, const uint64_t* rec_off, cons
         }
         sz[(size_t)k] = b;
         lfl[(size_t)k] = flag[i];
+        if (keyed) {
+            lst[(size_t)k] = start[i];
+            ltl[(size_t)k] = tlen[i];
+        }
         const int64_t c = (int64_t)bc[i] - cell_lo;
         lbc[(size_t)k] = (bc[i] >= 0 && c >= 0 && c < n_cells) ? (int32_t)c : -1;
     }
-    return mgp_place_records(m, lbc.data(), lfl.data(), sz.data(), n_cells, mode, rec_align, out_off);
+    return mgp_place_records(m, lbc.data(), lfl.data(), keyed ? lst.data() : nullptr, keyed ? ltl.data() : nullptr,
+                             sz.data(), n_cells, mode, rec_align, out_off);
 }
 
 int mgp_gather_records(const uint8_t* payload, const uint64_t* rec_off, const uint16_t* flag, int64_t n_total,

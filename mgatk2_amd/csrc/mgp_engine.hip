@@ -111,7 +111,8 @@ struct mgp_ctx {
     mgp_config cfg{};
     int dev = 0;
     hipStream_t s_comp = nullptr, s_copy = nullptr;
-    hipEvent_t ev_copy = nullptr;
+    hipStream_t s_side = nullptr;  // the tally reduction, concurrent with the medians
+    hipEvent_t ev_copy = nullptr, ev_fork = nullptr, ev_join = nullptr;
     static constexpr int kRing = 64;   // per-run event slots (timing over many runs without syncs)
     hipEvent_t ev[kRing][ST_N][2];
     bool stage_ran[kRing][ST_N]{};
@@ -1493,8 +1494,14 @@ __device__ __forceinline__ void pile_line(bool has, bool packed, const uint8_t* 
     span_err = span_err || se;
 }
 
-constexpr int kWaveQ = 4 * kWave;    // per-wave ring of reads waiting to be piled (LDS, power of two)
-constexpr int kStreamU = 2;          // pileup elements per lane per stream step
+#ifndef MGP_STREAM_U
+#define MGP_STREAM_U 2
+#endif
+constexpr int kStreamU = MGP_STREAM_U;  // pileup elements per lane per stream step
+// per-wave ring of reads waiting to be piled (LDS, a power of two holding the
+// < 64 left over plus one stream step)
+constexpr int kWaveQ = kStreamU <= 1 ? 2 * kWave : kStreamU <= 3 ? 4 * kWave : 8 * kWave;
+static_assert(kWaveQ >= kWave * (kStreamU + 1) && kStreamU <= 7, "pileup ring too small");
 
 // record byte offset of a pileup element (MGP_ABL 6, experiments only: every
 // record read from the first 256 MiB of the payload, to time the pileup with a
@@ -2169,7 +2176,10 @@ int mgp_open(const mgp_config* cfg, int hip_device, mgp_ctx** out) {
     }
     HIP_TRY(hipStreamCreateWithFlags(&ctx->s_comp, hipStreamNonBlocking));
     HIP_TRY(hipStreamCreateWithFlags(&ctx->s_copy, hipStreamNonBlocking));
+    HIP_TRY(hipStreamCreateWithFlags(&ctx->s_side, hipStreamNonBlocking));
     HIP_TRY(hipEventCreateWithFlags(&ctx->ev_copy, hipEventDisableTiming));
+    HIP_TRY(hipEventCreateWithFlags(&ctx->ev_fork, hipEventDisableTiming));
+    HIP_TRY(hipEventCreateWithFlags(&ctx->ev_join, hipEventDisableTiming));
     for (int r = 0; r < mgp_ctx::kRing; ++r)
         for (int s = 0; s < ST_N; ++s) {
             HIP_TRY(hipEventCreate(&ctx->ev[r][s][0]));
@@ -2196,6 +2206,7 @@ void mgp_close(mgp_ctx* ctx) {
     (void)hipSetDevice(ctx->dev);
     (void)hipStreamSynchronize(ctx->s_comp);
     (void)hipStreamSynchronize(ctx->s_copy);
+    (void)hipStreamSynchronize(ctx->s_side);
     if (ctx->comm) ncclCommDestroy(ctx->comm);
     DevBuf* bufs[] = {&ctx->start,     &ctx->bc,        &ctx->tlen,     &ctx->flag,       &ctx->mapq,
                       &ctx->span,      &ctx->roff,      &ctx->payload,  &ctx->bin_start,  &ctx->gel2,
@@ -2213,8 +2224,11 @@ void mgp_close(mgp_ctx* ctx) {
             (void)hipEventDestroy(ctx->ev[r][s][1]);
         }
     (void)hipEventDestroy(ctx->ev_copy);
+    (void)hipEventDestroy(ctx->ev_fork);
+    (void)hipEventDestroy(ctx->ev_join);
     (void)hipStreamDestroy(ctx->s_comp);
     (void)hipStreamDestroy(ctx->s_copy);
+    (void)hipStreamDestroy(ctx->s_side);
     delete ctx;
 }
 
@@ -2510,7 +2524,24 @@ int mgp_run(mgp_ctx* ctx) {
             STAGE_END(ST_GATE);
         }
 
-        // 7. medians + pass flags
+        // 7. tallies on the side stream, concurrent with the medians (both only read
+        // the pileup's outputs); joined before the stats and the all-reduce
+        {
+            hipStream_t s2 = ctx->s_side;
+            HIP_TRY(hipEventRecord(ctx->ev_fork, s));
+            HIP_TRY(hipStreamWaitEvent(s2, ctx->ev_fork, 0));
+            HIP_TRY(hipEventRecord(ctx->ev[slot][ST_TALLY][0], s2));
+            ctx->stage_ran[slot][ST_TALLY] = true;
+            HIP_TRY(hipMemsetAsync(ctx->tally.p, 0, (size_t)g.L * 32, s2));
+            dim3 gt(blocks_for((int64_t)g.L * 4), (unsigned)std::max(1, std::min(g.nchunks, 32)));
+            k_tally_reduce<<<gt, kBlock, 0, s2>>>(ctx->tally_part.as<uint32_t>(), g.nchunks, g.L * 4,
+                                                  ctx->tally.as<unsigned long long>());
+            HIP_TRY(hipGetLastError());
+            HIP_TRY(hipEventRecord(ctx->ev[slot][ST_TALLY][1], s2));
+            HIP_TRY(hipEventRecord(ctx->ev_join, s2));
+        }
+
+        // 8. medians + pass flags, run statistics
         STAGE_BEGIN(ST_MEDIAN);
         if (g.L <= kMedRegs * kBlock)
             k_median<true><<<nc, kBlock, 0, s>>>(
@@ -2529,19 +2560,11 @@ int mgp_run(mgp_ctx* ctx) {
                                                      ctx->med_lo.as<uint32_t>(), ctx->med_hi.as<uint32_t>(),
                                                      ctx->passed.as<uint8_t>(), st);
         HIP_TRY(hipGetLastError());
-        STAGE_END(ST_MEDIAN);
-
-        // 8. tallies
-        STAGE_BEGIN(ST_TALLY);
-        HIP_TRY(hipMemsetAsync(ctx->tally.p, 0, (size_t)g.L * 32, s));
-        dim3 gt(blocks_for((int64_t)g.L * 4), (unsigned)std::max(1, std::min(g.nchunks, 32)));
-        k_tally_reduce<<<gt, kBlock, 0, s>>>(ctx->tally_part.as<uint32_t>(), g.nchunks, g.L * 4,
-                                             ctx->tally.as<unsigned long long>());
-        HIP_TRY(hipGetLastError());
         k_run_stats<<<1, 1024, 0, s>>>(1, nullptr, 0, ctx->n_reads.as<uint32_t>(), ctx->passed.as<uint8_t>(), nc,
                                        ctx->dup_part.as<unsigned long long>(), dup_parts, st);
         HIP_TRY(hipGetLastError());
-        STAGE_END(ST_TALLY);
+        STAGE_END(ST_MEDIAN);
+        HIP_TRY(hipStreamWaitEvent(s, ctx->ev_join, 0));
     } else {
         HIP_TRY(hipMemsetAsync(ctx->tally.p, 0, (size_t)g.L * 32, s));
     }

@@ -64,9 +64,12 @@ def shard_soa(soa: ReadSoA, lo: int, hi: int, rec_align: int = 64, paired: bool 
     roff = np.ascontiguousarray(soa.rec_off, dtype=np.uint64)
     flag = np.ascontiguousarray(soa.flag, dtype=np.uint16)
     bc = np.ascontiguousarray(soa.bc, dtype=np.int32)
+    start = np.ascontiguousarray(soa.start, dtype=np.int32)
+    tlen = np.ascontiguousarray(soa.tlen, dtype=np.int32)
     pay = np.ascontiguousarray(soa.payload)
     new_off = np.zeros(max(idx.size, 1), np.uint64)
-    total = lib.mgp_gather_offsets(pay.ctypes.data, roff.ctypes.data, flag.ctypes.data, bc.ctypes.data, soa.n,
+    total = lib.mgp_gather_offsets(pay.ctypes.data, roff.ctypes.data, flag.ctypes.data, bc.ctypes.data,
+                                   start.ctypes.data, tlen.ctypes.data, soa.n,
                                    pay.shape[0], idx.ctypes.data, idx.size, int(lo), int(hi - lo),
                                    PLACE_PAIRED if paired else PLACE_DENSE, rec_align, new_off.ctypes.data)
     if total < 0:

@@ -502,7 +502,8 @@ def test_device_generator_with_placement(engine_lib):
 
     n, nc, seed = 90_001, 29, 8
     host = synth_reads(seed, n, nc)
-    roff, tot = place_records(host.bc, host.flag, np.full(n, 64, np.uint32), nc, PLACE_PAIRED)
+    roff, tot = place_records(host.bc, host.flag, np.full(n, 64, np.uint32), nc, PLACE_PAIRED, start=host.start,
+                              tlen=host.tlen)
     exp = relocate(host, paired=True, n_cells=nc)
     np.testing.assert_array_equal(roff, exp.rec_off)
     with engine_lib.Engine(EngineConfig(n_cells=nc)) as eng:

@@ -1,7 +1,9 @@
 """Producer payload placement (mgp_place_records, include/mgpileup_host.h): two
-consecutive packed records of one cell per 128-byte line. The placement moves
-records, never changes them, so every consumer (oracle, decoder, shard gather,
-batch slicing) must give the same results as with the dense layout. CPU only."""
+consecutive packed records of one cell per 128-byte line, a cell's reads that
+repeat the start, strand and |tlen| of an earlier read of the cell placed with
+the dropped reads. The placement moves records, never changes them, so every
+consumer (oracle, decoder, shard gather, batch slicing) must give the same
+results as with the dense layout. CPU only."""
 
 from __future__ import annotations
 
@@ -15,7 +17,30 @@ from mgatk2_amd.synth import FLAG_PACKED, relocate, synth_reads
 DROP = 0x4 | 0x100 | 0x800  # unmapped, secondary, supplementary (readers.py:96-97)
 
 
-def _check_paired(bc, flag, rb, n_cells, off, total):
+def _place_keys(bc, flag, n_cells, start=None, tlen=None, packed=None):
+    """The line key of each read (mgp_place.h): its cell, or n_cells for reads the
+    engine drops and, given start/tlen, for a packed read repeating an earlier
+    packed read's key in the cell at the same start (up to 8 keys kept per start)."""
+    key = np.where((bc >= 0) & (bc < n_cells) & ((flag & DROP) == 0), bc, n_cells).astype(np.int64)
+    if start is None:
+        return key
+    seen = {}  # cell -> (start, [keys])
+    for i in range(key.size):
+        c = int(key[i])
+        if c == n_cells or not packed[i]:
+            continue
+        k = (abs(int(tlen[i])), bool(flag[i] & 0x10))
+        st, ks = seen.get(c, (None, []))
+        if st != int(start[i]):
+            seen[c] = (int(start[i]), [k])
+        elif k in ks:
+            key[i] = n_cells
+        elif len(ks) < 8:
+            ks.append(k)
+    return key
+
+
+def _check_paired(bc, flag, rb, n_cells, off, total, start=None, tlen=None):
     off = off.astype(np.int64)
     assert np.all(off % 16 == 0)
     assert np.all(off + rb <= total)
@@ -24,7 +49,7 @@ def _check_paired(bc, flag, rb, n_cells, off, total):
     assert np.all(off[o][1:] >= (off[o] + rb[o])[:-1])
     packed = ((flag & FLAG_PACKED) != 0) & (rb == 64)
     assert np.all(off[~packed] % 128 == 0)
-    key = np.where((bc >= 0) & (bc < n_cells) & ((flag & DROP) == 0), bc, n_cells)
+    key = _place_keys(bc, flag, n_cells, start, tlen, packed)
     # per key, the k-th packed record in BAM order sits in line k // 2, half k % 2
     for k in np.unique(key[packed]):
         sel = np.flatnonzero(packed & (key == k))
@@ -45,6 +70,15 @@ def test_place_records_rules():
     rb = np.where(full, rng.integers(100, 400, n), 64).astype(np.uint32)
     off, total = place_records(bc, flag, rb, nc, PLACE_PAIRED)
     _check_paired(bc, flag, rb.astype(np.int64), nc, off, total)
+    # keyed: repeats of (start, strand, |tlen|) inside a cell go with the dropped reads
+    start = np.sort(rng.integers(0, 400, n)).astype(np.int32)
+    tlen = (rng.integers(0, 3, n) * rng.choice([-1, 1], n)).astype(np.int32)
+    flag[rng.random(n) < 0.5] |= 0x10
+    koff, ktotal = place_records(bc, flag, rb, nc, PLACE_PAIRED, start=start, tlen=tlen)
+    packed = ((flag & FLAG_PACKED) != 0) & (rb == 64)
+    key = _place_keys(bc, flag, nc, start, tlen, packed)
+    assert (key == nc).sum() > (_place_keys(bc, flag, nc) == nc).sum() + 1000  # the rule applies
+    _check_paired(bc, flag, rb.astype(np.int64), nc, koff, ktotal, start, tlen)
     doff, dtot = place_records(bc, flag, rb, nc, PLACE_DENSE, rec_align=16)
     np.testing.assert_array_equal(doff[1:], np.cumsum((rb.astype(np.int64) + 15) // 16 * 16)[:-1])
     assert dtot == int(((rb.astype(np.int64) + 15) // 16 * 16).sum())
@@ -68,7 +102,7 @@ def test_relocate_roundtrip(synth):
     p = relocate(synth, paired=True, n_cells=40)
     assert np.any(np.diff(p.rec_off.astype(np.int64)) < 0)  # no longer in BAM order
     rb = np.full(p.n, 64, np.int64)
-    _check_paired(p.bc, p.flag, rb, 40, p.rec_off, p.payload.size)
+    _check_paired(p.bc, p.flag, rb, 40, p.rec_off, p.payload.size, p.start, p.tlen)
     d = relocate(p, paired=False, n_cells=40)
     for k in ("start", "bc", "tlen", "flag", "mapq", "span", "rec_off"):
         np.testing.assert_array_equal(getattr(d, k), getattr(synth, k), err_msg=k)
@@ -121,7 +155,7 @@ def test_decoder_paired_placement(tmp_path, synth):
         d = bam.read_soa("chrM", wl, pack=True, paired=False)
     assert np.array_equal(d.rec_off, np.arange(d.n, dtype=np.uint64) * 64)
     rb = np.full(p.n, 64, np.int64)
-    _check_paired(p.bc, p.flag, rb, 40, p.rec_off, p.payload.size)
+    _check_paired(p.bc, p.flag, rb, 40, p.rec_off, p.payload.size, p.start, p.tlen)
     r = relocate(p, n_cells=40)
     np.testing.assert_array_equal(r.rec_off, d.rec_off)
     np.testing.assert_array_equal(r.payload[: d.payload.size], d.payload[: r.payload.size])
