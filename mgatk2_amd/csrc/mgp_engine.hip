@@ -1540,6 +1540,15 @@ struct Out16 {
 
 __device__ __forceinline__ uint32_t sat16(uint32_t v) { return v > 0xFFFFu ? 0xFFFFu : v; }
 
+// kPacked: every resident record is packed (the ingest check's CHK_FULL clear):
+// no full-layout path, and the records of a wave's next 64 queued reads are
+// loaded before the current 64 are piled (one batch of gathers in flight
+// behind the per-base work; the registers the full-layout path would hold pay
+// for the second record set).
+#ifndef MGP_PILE_PREFETCH
+#define MGP_PILE_PREFETCH 1
+#endif
+template <bool kPacked>
 __global__ void __launch_bounds__(kBlock, MGP_PILEUP_WAVES) k_pileup(
     Geom g, PileCfg pc, const uint8_t* __restrict__ payload, const uint32_t* __restrict__ pel, int unit,
     const uint32_t* __restrict__ O, Out16 o16, uint32_t* __restrict__ counts, uint32_t* __restrict__ tn5,
@@ -1600,6 +1609,8 @@ __global__ void __launch_bounds__(kBlock, MGP_PILEUP_WAVES) k_pileup(
             const uint32_t seg_hi = min(hi, seg + kSeg);
             // the wave's ring of queued reads: [qh, qh + qn), wave-uniform
             uint32_t qh = 0, qn = 0;
+            RecLine Rp;         // kPacked: the loaded batch waiting to be piled
+            bool pend = false;  // (wave-uniform)
             // a stream step: each wave takes kStreamU x 64 consecutive elements (the
             // waves' blocks interleaved), the next step's loaded while this one is
             // queued and piled
@@ -1632,15 +1643,31 @@ __global__ void __launch_bounds__(kBlock, MGP_PILEUP_WAVES) k_pileup(
                     const uint32_t qe = wq[(qh + lane) & (kWaveQ - 1)];
                     qh += kWave;
                     qn -= kWave;
-                    pile_read(true, (qe & PE_PACKED) != 0u, payload + rec_at(qe, unit), w, pc, tile, t5, max_span,
-                              span_err, pk_err);
+                    if constexpr (kPacked && MGP_PILE_PREFETCH) {
+                        RecLine Rn;  // this batch's records load while the pending batch is piled
+                        load_line(true, true, payload + rec_at(qe, unit), w, Rn);
+                        if (pend) pile_line(true, true, nullptr, Rp, w, pc, tile, t5, max_span, span_err, pk_err);
+                        Rp = Rn;
+                        pend = true;
+                    } else {
+                        pile_read(true, kPacked || (qe & PE_PACKED) != 0u, payload + rec_at(qe, unit), w, pc, tile,
+                                  t5, max_span, span_err, pk_err);
+                    }
                 }
             }
             {   // tail: every lane of the wave enters, lanes past qn hold no read
                 const bool has = (uint32_t)lane < qn;
                 const uint32_t qe = has ? wq[(qh + lane) & (kWaveQ - 1)] : 0u;
-                pile_read(has, (qe & PE_PACKED) != 0u, payload + rec_at(qe, unit), w, pc, tile, t5, max_span,
-                          span_err, pk_err);
+                if constexpr (kPacked && MGP_PILE_PREFETCH) {
+                    RecLine Rn;
+                    load_line(has, true, payload + rec_at(qe, unit), w, Rn);
+                    if (pend) pile_line(true, true, nullptr, Rp, w, pc, tile, t5, max_span, span_err, pk_err);
+                    pend = false;
+                    pile_line(has, true, nullptr, Rn, w, pc, tile, t5, max_span, span_err, pk_err);
+                } else {
+                    pile_read(has, kPacked || (qe & PE_PACKED) != 0u, payload + rec_at(qe, unit), w, pc, tile, t5,
+                              max_span, span_err, pk_err);
+                }
             }
             if (drained) {  // add this segment's packed tile into the 32-bit output rows
                 __syncthreads();
@@ -2055,7 +2082,7 @@ __global__ void k_add_u64(uint64_t* __restrict__ a, int64_t n, uint64_t add) {
 // CHK_PAIRED / CHK_UNPAIRED / CHK_NOSEQ when some read is paired / unpaired /
 // lacks SEQ or QUAL (k_group_b tracks pairedness and SEQ per read only when the
 // reads mix or lack them).
-constexpr uint32_t CHK_PAIRED = 4u, CHK_UNPAIRED = 8u, CHK_NOSEQ = 16u;
+constexpr uint32_t CHK_PAIRED = 4u, CHK_UNPAIRED = 8u, CHK_NOSEQ = 16u, CHK_FULL = 32u;
 __global__ void k_check_stride(const uint64_t* __restrict__ roff, const uint16_t* __restrict__ flag, int64_t n,
                                int64_t i0, uint32_t* irregular, uint32_t* __restrict__ roff32) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -2067,8 +2094,9 @@ __global__ void k_check_stride(const uint64_t* __restrict__ roff, const uint16_t
     const unsigned long long b1 = __ballot(bad), b2 = __ballot(wide);
     const unsigned long long b3 = __ballot(i < n && (f & MGP_FLAG_PAIRED)), b4 = __ballot(i < n && !(f & MGP_FLAG_PAIRED));
     const unsigned long long b5 = __ballot(i < n && (f & MGP_FLAG_NOSEQQUAL));
+    const unsigned long long b6 = __ballot(i < n && !(f & MGP_FLAG_PACKED));
     const uint32_t bits = (b1 ? 1u : 0u) | (b2 ? 2u : 0u) | (b3 ? CHK_PAIRED : 0u) | (b4 ? CHK_UNPAIRED : 0u) |
-                          (b5 ? CHK_NOSEQ : 0u);
+                          (b5 ? CHK_NOSEQ : 0u) | (b6 ? CHK_FULL : 0u);
     // one atomic per wave at most, and none once the bits are set (every wave of a
     // paired payload has irregular offsets: 3M atomics on one word took 18 ms)
     if (bits && (threadIdx.x & 63) == 0 && (__atomic_load_n(irregular, __ATOMIC_RELAXED) & bits) != bits)
@@ -2167,7 +2195,8 @@ int mgp_open(const mgp_config* cfg, int hip_device, mgp_ctx** out) {
                                   lds_max);
         (void)hipFuncSetAttribute((const void*)k_group_a<kOffR64>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                   lds_max);
-        (void)hipFuncSetAttribute((const void*)k_pileup, hipFuncAttributeMaxDynamicSharedMemorySize, lds_max);
+        (void)hipFuncSetAttribute((const void*)k_pileup<false>, hipFuncAttributeMaxDynamicSharedMemorySize, lds_max);
+        (void)hipFuncSetAttribute((const void*)k_pileup<true>, hipFuncAttributeMaxDynamicSharedMemorySize, lds_max);
         (void)hipGetLastError();
         if ((size_t)ctx->g.L * 4 + 2048 > prop.sharedMemPerBlock) {
             delete ctx;
@@ -2503,7 +2532,8 @@ int mgp_run(mgp_ctx* ctx) {
         pc.keep_tn5 = (ctx->cfg.flags & MGP_CFG_KEEP_TN5) != 0;
         dim3 gp(g.nchunks, g.nwin);
         const size_t psm = (size_t)5 * g.Wp * 4;
-        k_pileup<<<gp, kBlock, psm, s>>>(g, pc, ctx->payload.as<uint8_t>(), ctx->pel.as<uint32_t>(), unit,
+        auto pile_kern = (ctx->read_bits & CHK_FULL) ? k_pileup<false> : k_pileup<true>;
+        pile_kern<<<gp, kBlock, psm, s>>>(g, pc, ctx->payload.as<uint8_t>(), ctx->pel.as<uint32_t>(), unit,
                                          ctx->H.as<uint32_t>(), out16_of(ctx), ctx->counts.as<uint32_t>(),
                                          ctx->tn5.as<uint32_t>(), ctx->depth.as<uint32_t>(), ctx->n_reads.as<uint32_t>(),
                                          ctx->any_paired.as<uint8_t>(), pair_mode, ctx->covered.as<uint32_t>(),
