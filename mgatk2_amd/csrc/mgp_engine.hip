@@ -120,6 +120,7 @@ struct mgp_ctx {
     Geom g{};
     int lds_hist_max_cells = 0;
     int hist_slice_cells = 0;  // > 0: cap on the histogram's cells per slice (MGP_HIST_SLICE_CELLS)
+    bool group_wide = false;   // MGP_GROUP_WIDE=1: 16-byte grouping elements always (tests, A/B)
 
     // resident inputs (BAM order)
     int64_t n = 0, pay = 0;
@@ -418,6 +419,22 @@ constexpr uint64_t kRecStride = MGP_PACK_BYTES;  // record stride of a dense pac
 //   kOffR64    otherwise: the u64 rec_off column
 enum { kOffDense = 0, kOffR32 = 1, kOffR64 = 2 };
 
+// Compact grouping element (8 bytes), used when every resident record is packed
+// at a 64-byte multiple below 2^37 (dense or u32 offsets), the reads do not mix
+// paired and unpaired ones and all have SEQ/QUAL, every start lies in
+// [0, mito_len) and every |tlen| < 2^17 (the ingest check's bits):
+//   bits 0..30 record offset / 64 (the pileup element's offset field), 31..36 cell
+//   in group, 37 reverse, 38 MAPQ >= min_mapq, 39..46 start mod 256, 47..63 |tlen|.
+// Pass B compares starts mod 256: its steps span fewer than 32 start bins (256
+// positions), and a cell's elements of one step are in start order, so equal
+// starts mod 256 inside a cell's run of a step are equal starts.
+constexpr int GC_LCELL_SHIFT = 31, GC_START_SHIFT = 39, GC_TLEN_SHIFT = 47;
+constexpr unsigned long long GC_OFF = 0x7FFFFFFFull, GC_LCELL = 63ull << GC_LCELL_SHIFT, GC_REV = 1ull << 37,
+                             GC_MAPQ_OK = 1ull << 38, GC_START = 255ull << GC_START_SHIFT,
+                             GC_TLEN = 0x1FFFFull << GC_TLEN_SHIFT;
+constexpr uint32_t kCompactTlen = 1u << 17;  // |tlen| below this fits the compact element
+constexpr int kCompactBins = 32;             // start bins per pass-B step (compact elements)
+
 #ifndef MGP_GA_AHEAD
 #define MGP_GA_AHEAD 8  // reads per lane per pass-A step (A/B: 2, 3, 4, 6 slower)
 #endif
@@ -434,7 +451,8 @@ enum { kOffDense = 0, kOffR32 = 1, kOffR64 = 2 };
 #define MGP_GA_BLOCK 256  // threads per pass-A workgroup
 #endif
 constexpr int kGABlock = MGP_GA_BLOCK;
-template <int kOff>
+// kCompact: 8-byte elements (GCompact, below; kOff is then dense or u32)
+template <int kOff, bool kCompact>
 __global__ void __launch_bounds__(kGABlock, MGP_GA_WAVES) k_group_a(int64_t n, const int32_t* __restrict__ start,
                                                     const int32_t* __restrict__ bc, const int32_t* __restrict__ tlen,
                                                     const uint16_t* __restrict__ flag, const uint8_t* __restrict__ mapq,
@@ -581,14 +599,27 @@ __global__ void __launch_bounds__(kGABlock, MGP_GA_WAVES) k_group_a(int64_t n, c
             const unsigned long long off = kOff == kOffDense ? (unsigned long long)P.o[u] * kRecStride
                                            : kOff == kOffR32 ? (unsigned long long)P.o[u] << 6
                                                              : (unsigned long long)P.o[u];
-            GElem e;
-            e.w = off | (f & MGP_FLAG_REVERSE ? GM_REV : 0ull) | (f & MGP_FLAG_PAIRED ? GM_PAIRED : 0ull) |
-                  ((int)(P.fm[u] >> 16) >= min_mapq ? GM_MAPQ_OK : 0ull) | (f & MGP_FLAG_NOSEQQUAL ? GM_BAD : 0ull) | (f & MGP_FLAG_PACKED ? GM_PACKED : 0ull) |
-                  ((unsigned long long)(P.c[u] & (kGroup - 1)) << GM_LCELL_SHIFT);
-            e.start = P.s[u];
-            e.tlen = t < 0 ? (uint32_t)(-(int64_t)t) : (uint32_t)t;
-            if ((int64_t)dest < n) gel2[dest] = e;  // always: counts and slots come from one histogram
-            else atomicOr(&st->err, ERR_OVERFLOW);
+            const uint32_t at = t < 0 ? (uint32_t)(-(int64_t)t) : (uint32_t)t;
+            const bool mq = (int)(P.fm[u] >> 16) >= min_mapq;
+            if ((int64_t)dest >= n) {  // never: counts and slots come from one histogram
+                atomicOr(&st->err, ERR_OVERFLOW);
+            } else if constexpr (kCompact) {
+                // the record's 64-byte unit (dense: the read index; u32 column: rec_off >> 6)
+                const unsigned long long e =
+                    (unsigned long long)P.o[u] | ((unsigned long long)(P.c[u] & (kGroup - 1)) << GC_LCELL_SHIFT) |
+                    (f & MGP_FLAG_REVERSE ? GC_REV : 0ull) | (mq ? GC_MAPQ_OK : 0ull) |
+                    ((unsigned long long)(P.s[u] & 255) << GC_START_SHIFT) | ((unsigned long long)at << GC_TLEN_SHIFT);
+                reinterpret_cast<unsigned long long*>(gel2)[dest] = e;
+            } else {
+                GElem e;
+                e.w = off | (f & MGP_FLAG_REVERSE ? GM_REV : 0ull) | (f & MGP_FLAG_PAIRED ? GM_PAIRED : 0ull) |
+                      (mq ? GM_MAPQ_OK : 0ull) | (f & MGP_FLAG_NOSEQQUAL ? GM_BAD : 0ull) |
+                      (f & MGP_FLAG_PACKED ? GM_PACKED : 0ull) |
+                      ((unsigned long long)(P.c[u] & (kGroup - 1)) << GM_LCELL_SHIFT);
+                e.start = P.s[u];
+                e.tlen = at;
+                gel2[dest] = e;
+            }
         }
         set ^= 1;
     };
@@ -649,16 +680,65 @@ struct DedupAcc {  // per-thread duplicate counters of pass B
     unsigned long long d2 = 0, d3 = 0;
 };
 
+
+#ifndef MGP_GB_WAVES
+#define MGP_GB_WAVES 4
+#endif
+#ifndef MGP_GB_WAVES_C
+#define MGP_GB_WAVES_C 5
+#endif
+// Element access for the two grouping element forms (pass B).
+struct GWide {
+    using T = GElem;
+    static constexpr int kWaves = MGP_GB_WAVES;  // pass-B waves per SIMD
+    static __device__ __forceinline__ T zero() {
+        T e;
+        e.w = 0;
+        e.start = 0;
+        e.tlen = 0;
+        return e;
+    }
+    static __device__ __forceinline__ int lcell(const T& e) { return (int)((e.w >> GM_LCELL_SHIFT) & (kGroup - 1)); }
+    // same cell and start (the run of equal starts), then same strand, then same |tlen|
+    static __device__ __forceinline__ bool run_eq(const T& a, const T& b) {
+        return ((a.w ^ b.w) & GM_LCELL) == 0ull && a.start == b.start;
+    }
+    static __device__ __forceinline__ bool start_eq(const T& a, const T& b) { return a.start == b.start; }
+    static __device__ __forceinline__ bool strand_eq(const T& a, const T& b) { return ((a.w ^ b.w) & GM_REV) == 0ull; }
+    static __device__ __forceinline__ bool tlen_eq(const T& a, const T& b) { return a.tlen == b.tlen; }
+    static __device__ __forceinline__ bool mapq_ok(const T& e) { return (e.w & GM_MAPQ_OK) != 0ull; }
+    static __device__ __forceinline__ uint32_t pile(const T& e, int unit) {
+        return (uint32_t)((e.w & GM_OFF) >> unit) | (e.w & GM_PACKED ? PE_PACKED : 0u);
+    }
+    static __device__ __forceinline__ bool paired(const T& e) { return (e.w & GM_PAIRED) != 0ull; }
+    static __device__ __forceinline__ bool bad(const T& e) { return (e.w & GM_BAD) != 0ull; }
+};
+struct GCompact {
+    using T = unsigned long long;
+    static constexpr int kWaves = MGP_GB_WAVES_C;  // fewer registers: 5 waves per SIMD (A/B: 4 slower)
+    static __device__ __forceinline__ T zero() { return 0ull; }
+    static __device__ __forceinline__ int lcell(const T& e) { return (int)((e >> GC_LCELL_SHIFT) & (kGroup - 1)); }
+    static __device__ __forceinline__ bool run_eq(const T& a, const T& b) { return ((a ^ b) & (GC_LCELL | GC_START)) == 0ull; }
+    static __device__ __forceinline__ bool start_eq(const T& a, const T& b) { return ((a ^ b) & GC_START) == 0ull; }
+    static __device__ __forceinline__ bool strand_eq(const T& a, const T& b) { return ((a ^ b) & GC_REV) == 0ull; }
+    static __device__ __forceinline__ bool tlen_eq(const T& a, const T& b) { return ((a ^ b) & GC_TLEN) == 0ull; }
+    static __device__ __forceinline__ bool mapq_ok(const T& e) { return (e & GC_MAPQ_OK) != 0ull; }
+    static __device__ __forceinline__ uint32_t pile(const T& e, int) { return (uint32_t)(e & GC_OFF) | PE_PACKED; }
+    static __device__ __forceinline__ bool paired(const T&) { return true; }
+    static __device__ __forceinline__ bool bad(const T&) { return false; }
+};
+
 // The pileup element of one read given its duplicate flags; keep = the read
 // survives the duplicate marking (counted in n_reads, processors.py:22).
-__device__ __forceinline__ uint32_t group_b_emit(const GElem& e, bool dup2, bool dup3, int mode, int unit,
+template <class Tr>
+__device__ __forceinline__ uint32_t group_b_emit(const typename Tr::T& e, bool dup2, bool dup3, int mode, int unit,
                                                  DedupAcc& acc, bool& keep) {
     keep = mode == MGP_DEDUP_NONE ? true : mode == MGP_DEDUP_START ? !dup2 : !dup3;
     acc.d2 += dup2;
     acc.d3 += dup3;
     if (!keep) return PE_DUP;
-    if (!(e.w & GM_MAPQ_OK)) return PE_KEEP;
-    return (uint32_t)((e.w & GM_OFF) >> unit) | (e.w & GM_PACKED ? PE_PACKED : 0u);
+    if (!Tr::mapq_ok(e)) return PE_KEEP;
+    return Tr::pile(e, unit);
 }
 
 // Per-cell flags of pass B when the resident reads mix paired and unpaired ones,
@@ -669,40 +749,39 @@ __device__ __forceinline__ uint32_t group_b_emit(const GElem& e, bool dup2, bool
 // per-cell LDS counters; a kept read without SEQ/QUAL sets ERR_BADREAD.
 // Otherwise every kept read is paired (or none is), which the pileup applies
 // with its kept-read counts, and no read lacks SEQ/QUAL.
-template <bool kTrack>
-__device__ __forceinline__ void cell_tally(bool act, int lc, bool keep, const GElem& e, uint32_t* s_ndup,
+template <bool kTrack, class Tr>
+__device__ __forceinline__ void cell_tally(bool act, int lc, bool keep, const typename Tr::T& e, uint32_t* s_ndup,
                                            uint32_t* s_nunp, DevStats* st) {
     if (kTrack) {
         if (act && !keep) atomicAdd(&s_ndup[lc], 1u);
-        if (act && keep && !(e.w & GM_PAIRED)) atomicAdd(&s_nunp[lc], 1u);
-        if (act && keep && (e.w & GM_BAD)) atomicOr(&st->err, ERR_BADREAD);
+        if (act && keep && !Tr::paired(e)) atomicAdd(&s_nunp[lc], 1u);
+        if (act && keep && Tr::bad(e)) atomicOr(&st->err, ERR_BADREAD);
     }
 }
 
-__device__ __forceinline__ bool same_key(const GElem& p, const GElem& e, bool& dup3) {
-    if (((p.w ^ e.w) & GM_REV) != 0ull) return false;
-    if (p.tlen == e.tlen) dup3 = true;
+template <class Tr>
+__device__ __forceinline__ bool same_key(const typename Tr::T& p, const typename Tr::T& e, bool& dup3) {
+    if (!Tr::strand_eq(p, e)) return false;
+    if (Tr::tlen_eq(p, e)) dup3 = true;
     return true;
 }
 
 // kStage: rank into the LDS stage. Otherwise (a bucket larger than the stage):
 // rank, mark duplicates by walking back over the bucket's equal starts (BAM
 // order, other cells skipped) and store the pileup elements directly.
-template <bool kStage>
-__device__ __forceinline__ void group_b_rank(const GElem* __restrict__ gel2, uint32_t k0, uint32_t k1,
-                                             uint32_t* cnt, int lane, unsigned long long lt, GElem* stage,
+template <bool kStage, class Tr>
+__device__ __forceinline__ void group_b_rank(const typename Tr::T* __restrict__ gel2, uint32_t k0, uint32_t k1,
+                                             uint32_t* cnt, int lane, unsigned long long lt, typename Tr::T* stage,
                                              const uint32_t* cbase, const uint32_t* cstart, int mode, int unit,
                                              uint32_t* __restrict__ pel, DedupAcc& acc, uint32_t* s_ndup,
                                              uint32_t* s_nunp, DevStats* st) {
+    using T = typename Tr::T;
     for (uint32_t k = k0; k < k1; k += kWave) {
         const uint32_t j = k + lane;
         const bool act = j < k1;
-        GElem e;
-        e.w = 0;
-        e.start = 0;
-        e.tlen = 0;
+        T e = Tr::zero();
         if (act) e = gel2[j];
-        const int lc = (int)((e.w >> GM_LCELL_SHIFT) & (kGroup - 1));
+        const int lc = Tr::lcell(e);
         unsigned long long peers = __ballot(act);
 #pragma unroll
         for (int bit = 0; bit < 6; ++bit) {
@@ -721,18 +800,20 @@ __device__ __forceinline__ void group_b_rank(const GElem* __restrict__ gel2, uin
             } else {
                 bool dup2 = false, dup3 = false;
                 if (mode != MGP_DEDUP_NONE) {
+                    // one bucket = one start bin (starts within 8 positions, so equal
+                    // starts mod 256 are equal starts); equal starts are adjacent
                     for (uint32_t m = j; m-- > k0;) {
-                        const GElem p = gel2[m];
-                        if (p.start != e.start) break;
-                        if ((((p.w ^ e.w) & GM_LCELL) == 0ull) && same_key(p, e, dup3)) {
+                        const T p = gel2[m];
+                        if (!Tr::start_eq(p, e)) break;
+                        if (Tr::lcell(p) == lc && same_key<Tr>(p, e, dup3)) {
                             dup2 = true;
                             if (dup3) break;
                         }
                     }
                 }
                 bool keep;
-                pel[dest] = group_b_emit(e, dup2, dup3, mode, unit, acc, keep);
-                cell_tally<true>(true, lc, keep, e, s_ndup, s_nunp, st);
+                pel[dest] = group_b_emit<Tr>(e, dup2, dup3, mode, unit, acc, keep);
+                cell_tally<true, Tr>(true, lc, keep, e, s_ndup, s_nunp, st);
             }
         }
     }
@@ -750,20 +831,19 @@ constexpr int kBPer = kStageB / kBlock;  // elements per lane per step
 #define MGP_ABL_B 0  // pass-B ablations (experiments only): 1 no dedup walk, 2 no pel stores, 3 no loads
 #endif
 
-#ifndef MGP_GB_WAVES
-#define MGP_GB_WAVES 4
-#endif
 #ifndef MGP_GB_LOOK
 #define MGP_GB_LOOK 4  // predecessors compared branch-free before a walk back (A/B: 2-6)
 #endif
-template <bool kTrack>
-__global__ void __launch_bounds__(kBlock, MGP_GB_WAVES) k_group_b(const GElem* __restrict__ gel2,
+template <bool kTrack, class Tr>
+__global__ void __launch_bounds__(kBlock, Tr::kWaves) k_group_b(const typename Tr::T* __restrict__ gel2,
                                                     const uint32_t* __restrict__ bucket_off,
                                                     const uint32_t* __restrict__ O, Geom g, int ngroups, int rb,
                                                     int mode, int unit, uint32_t* __restrict__ pel,
                                                     uint8_t* __restrict__ any_paired,
                                                     unsigned long long* __restrict__ dup_part, DevStats* st) {
-    __shared__ GElem stage[kStageB];
+    using T = typename Tr::T;
+    constexpr bool kCompact = sizeof(T) == 8;
+    __shared__ T stage[kStageB];
     __shared__ uint32_t wcnt[kBlock / kWave][kGroup];
     __shared__ uint32_t cbase[kGroup], cstart[kGroup + 1];
     __shared__ uint32_t bst[kMaxRbB], bsz[kMaxRbB], spre[kMaxRbB + 1];
@@ -799,6 +879,7 @@ __global__ void __launch_bounds__(kBlock, MGP_GB_WAVES) k_group_b(const GElem* _
             while (be < B1) {
                 const uint32_t sz = bsz[be - B0];
                 if (tot + sz > (uint32_t)kStageB) break;
+                if (kCompact && be - b >= kCompactBins) break;  // starts compared mod 256
                 tot += sz;
                 ++be;
                 spre[be - b] = tot;
@@ -809,16 +890,14 @@ __global__ void __launch_bounds__(kBlock, MGP_GB_WAVES) k_group_b(const GElem* _
         return s_be;
     };
     // this wave's quarter of the step's flat sequence (all loads issued together)
-    GElem e[kBPer];
+    T e[kBPer];
     auto load = [&](int b, int be) {
         const int nb = be - b;
         const uint32_t tot = spre[nb];
 #pragma unroll
         for (int u = 0; u < kBPer; ++u) {
             const uint32_t t = (uint32_t)(wid * (kBPer * kWave) + u * kWave + lane);
-            e[u].w = 0;
-            e[u].start = 0;
-            e[u].tlen = 0;
+            e[u] = Tr::zero();
             if (t < tot) {
                 int lo = 0, hi = nb;  // bin k of t: spre[k] <= t < spre[k + 1]
                 while (hi - lo > 1) {
@@ -826,7 +905,7 @@ __global__ void __launch_bounds__(kBlock, MGP_GB_WAVES) k_group_b(const GElem* _
                     if (spre[mid] <= t) lo = mid;
                     else hi = mid;
                 }
-                if (MGP_ABL_B == 3) {
+                if constexpr (MGP_ABL_B == 3 && !kCompact) {
                     e[u].w = (unsigned long long)((t * 37u) & 63u) << GM_LCELL_SHIFT;
                     e[u].start = (int)(bst[b - B0 + lo] + t);
                 } else {
@@ -844,7 +923,7 @@ __global__ void __launch_bounds__(kBlock, MGP_GB_WAVES) k_group_b(const GElem* _
             if (wid == 0) {
                 wcnt[0][lane] = cbase[lane];
                 __builtin_amdgcn_wave_barrier();
-                group_b_rank<false>(gel2, bst[b - B0], bst[b - B0] + bsz[b - B0], wcnt[0], lane, lt, nullptr,
+                group_b_rank<false, Tr>(gel2, bst[b - B0], bst[b - B0] + bsz[b - B0], wcnt[0], lane, lt, nullptr,
                                     nullptr, nullptr, mode, unit, pel, acc, s_ndup, s_nunp, st);
                 __builtin_amdgcn_wave_barrier();
                 cbase[lane] = wcnt[0][lane];
@@ -863,7 +942,7 @@ __global__ void __launch_bounds__(kBlock, MGP_GB_WAVES) k_group_b(const GElem* _
         for (int u = 0; u < kBPer; ++u) {
             const uint32_t t = (uint32_t)(wid * (kBPer * kWave) + u * kWave + lane);
             const bool act = t < tot;
-            const int lc = (int)((e[u].w >> GM_LCELL_SHIFT) & (kGroup - 1));
+            const int lc = Tr::lcell(e[u]);
             unsigned long long peers = __ballot(act);
 #pragma unroll
             for (int bit = 0; bit < 6; ++bit) {
@@ -899,7 +978,7 @@ __global__ void __launch_bounds__(kBlock, MGP_GB_WAVES) k_group_b(const GElem* _
         for (int u = 0; u < kBPer; ++u) {
             const uint32_t t = (uint32_t)(wid * (kBPer * kWave) + u * kWave + lane);
             if (t < tot) {
-                const int lc = (int)((e[u].w >> GM_LCELL_SHIFT) & (kGroup - 1));
+                const int lc = Tr::lcell(e[u]);
                 stage[cstart[lc] + wcnt[wid][lc] + rk[u]] = e[u];
             }
         }
@@ -919,24 +998,23 @@ __global__ void __launch_bounds__(kBlock, MGP_GB_WAVES) k_group_b(const GElem* _
 
 #pragma unroll
         for (int h = 0; h < kBPer; h += kWo) {
-            GElem xs[kWo];
+            T xs[kWo];
             bool d2[kWo], d3[kWo], wk[kWo];
 #pragma unroll
             for (int q = 0; q < kWo; ++q) {
                 const uint32_t t = threadIdx.x + (uint32_t)(h + q) * kBlock;
                 const uint32_t tc = t < cur ? t : 0u;
-                const GElem x = stage[tc];
-                GElem pk[kLook];
+                const T x = stage[tc];
+                T pk[kLook];
 #pragma unroll
                 for (int k = 0; k < kLook; ++k) pk[k] = stage[tc >= (uint32_t)(k + 1) ? tc - (uint32_t)(k + 1) : 0u];
                 bool r = true, s2 = false, t3 = false;  // r: the k nearest predecessors are all in x's run
 #pragma unroll
                 for (int k = 0; k < kLook; ++k) {
-                    r = r & (tc >= (uint32_t)(k + 1)) & (((pk[k].w ^ x.w) & GM_LCELL) == 0ull) &
-                        (pk[k].start == x.start);
-                    const bool sk = r & (((pk[k].w ^ x.w) & GM_REV) == 0ull);
+                    r = r & (tc >= (uint32_t)(k + 1)) & Tr::run_eq(pk[k], x);
+                    const bool sk = r & Tr::strand_eq(pk[k], x);
                     s2 |= sk;
-                    t3 |= sk & (pk[k].tlen == x.tlen);
+                    t3 |= sk & Tr::tlen_eq(pk[k], x);
                 }
                 xs[q] = x;
                 d2[q] = dedup & s2;
@@ -947,12 +1025,12 @@ __global__ void __launch_bounds__(kBlock, MGP_GB_WAVES) k_group_b(const GElem* _
             for (int q = 0; q < kWo; ++q) {
                 if (MGP_ABL_B != 1 && __ballot(wk[q]) != 0ull && wk[q]) {
                     const uint32_t t = threadIdx.x + (uint32_t)(h + q) * kBlock;
-                    const GElem x = xs[q];
+                    const T x = xs[q];
                     bool dup3 = false, dup2 = d2[q];
                     for (uint32_t m = t - (uint32_t)kLook; !dup3 && m-- > 0;) {
-                        const GElem p = stage[m];
-                        if (((p.w ^ x.w) & GM_LCELL) != 0ull || p.start != x.start) break;
-                        dup2 |= same_key(p, x, dup3);
+                        const T p = stage[m];
+                        if (!Tr::run_eq(p, x)) break;
+                        dup2 |= same_key<Tr>(p, x, dup3);
                     }
                     d2[q] = dup2;
                     d3[q] = dup3;
@@ -962,13 +1040,13 @@ __global__ void __launch_bounds__(kBlock, MGP_GB_WAVES) k_group_b(const GElem* _
             for (int q = 0; q < kWo; ++q) {
                 const uint32_t t = threadIdx.x + (uint32_t)(h + q) * kBlock;
                 const bool act = t < cur;
-                const int lc = (int)((xs[q].w >> GM_LCELL_SHIFT) & (kGroup - 1));
+                const int lc = Tr::lcell(xs[q]);
                 bool keep = false;
                 if (act) {
-                    const uint32_t pv = group_b_emit(xs[q], d2[q], d3[q], mode, unit, acc, keep);
+                    const uint32_t pv = group_b_emit<Tr>(xs[q], d2[q], d3[q], mode, unit, acc, keep);
                     if (MGP_ABL_B < 2 || pv == 7u) pel[cbase[lc] + (t - cstart[lc])] = pv;
                 }
-                cell_tally<kTrack>(act, lc, keep, xs[q], s_ndup, s_nunp, st);
+                cell_tally<kTrack, Tr>(act, lc, keep, xs[q], s_ndup, s_nunp, st);
             }
         }
         __syncthreads();
@@ -2082,12 +2160,17 @@ __global__ void k_add_u64(uint64_t* __restrict__ a, int64_t n, uint64_t add) {
 // CHK_PAIRED / CHK_UNPAIRED / CHK_NOSEQ when some read is paired / unpaired /
 // lacks SEQ or QUAL (k_group_b tracks pairedness and SEQ per read only when the
 // reads mix or lack them).
-constexpr uint32_t CHK_PAIRED = 4u, CHK_UNPAIRED = 8u, CHK_NOSEQ = 16u, CHK_FULL = 32u;
-__global__ void k_check_stride(const uint64_t* __restrict__ roff, const uint16_t* __restrict__ flag, int64_t n,
-                               int64_t i0, uint32_t* irregular, uint32_t* __restrict__ roff32) {
+// CHK_FULL: some record is in the full layout; CHK_WIDEKEY: some start lies
+// outside [0, mito_len) or some |tlen| >= kCompactTlen (no compact grouping element).
+constexpr uint32_t CHK_PAIRED = 4u, CHK_UNPAIRED = 8u, CHK_NOSEQ = 16u, CHK_FULL = 32u, CHK_WIDEKEY = 64u;
+__global__ void k_check_stride(const uint64_t* __restrict__ roff, const uint16_t* __restrict__ flag,
+                               const int32_t* __restrict__ start, const int32_t* __restrict__ tlen, int mito_len,
+                               int64_t n, int64_t i0, uint32_t* irregular, uint32_t* __restrict__ roff32) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const uint64_t r = i < n ? roff[i] : 0ull;
     const uint32_t f = i < n ? flag[i] : 0u;
+    const int32_t s0 = i < n ? start[i] : 0, t0 = i < n ? tlen[i] : 0;
+    const uint32_t at = t0 < 0 ? (uint32_t)(-(int64_t)t0) : (uint32_t)t0;
     if (i < n) roff32[i] = (uint32_t)(r >> 6);
     const bool bad = i < n && r != (uint64_t)(i0 + i) * kRecStride;
     const bool wide = i < n && ((r & 63ull) != 0ull || (r >> 38) != 0ull);
@@ -2095,8 +2178,9 @@ __global__ void k_check_stride(const uint64_t* __restrict__ roff, const uint16_t
     const unsigned long long b3 = __ballot(i < n && (f & MGP_FLAG_PAIRED)), b4 = __ballot(i < n && !(f & MGP_FLAG_PAIRED));
     const unsigned long long b5 = __ballot(i < n && (f & MGP_FLAG_NOSEQQUAL));
     const unsigned long long b6 = __ballot(i < n && !(f & MGP_FLAG_PACKED));
+    const unsigned long long b7 = __ballot(i < n && (s0 < 0 || s0 >= mito_len || at >= kCompactTlen));
     const uint32_t bits = (b1 ? 1u : 0u) | (b2 ? 2u : 0u) | (b3 ? CHK_PAIRED : 0u) | (b4 ? CHK_UNPAIRED : 0u) |
-                          (b5 ? CHK_NOSEQ : 0u) | (b6 ? CHK_FULL : 0u);
+                          (b5 ? CHK_NOSEQ : 0u) | (b6 ? CHK_FULL : 0u) | (b7 ? CHK_WIDEKEY : 0u);
     // one atomic per wave at most, and none once the bits are set (every wave of a
     // paired payload has irregular offsets: 3M atomics on one word took 18 ms)
     if (bits && (threadIdx.x & 63) == 0 && (__atomic_load_n(irregular, __ATOMIC_RELAXED) & bits) != bits)
@@ -2183,18 +2267,23 @@ int mgp_open(const mgp_config* cfg, int hip_device, mgp_ctx** out) {
         const long v = std::strtol(e, nullptr, 10);
         if (v >= kGroup) ctx->hist_slice_cells = (int)(v / kGroup * kGroup);
     }
+    if (const char* e = std::getenv("MGP_GROUP_WIDE")) ctx->group_wide = std::strtol(e, nullptr, 10) != 0;
     // kernels whose dynamic LDS may exceed 64 KiB (gfx950: up to 160 KiB per workgroup);
     // best effort: the runtime may already allow it without the attribute
     {
         const int lds_max = (int)prop.sharedMemPerBlock;
         (void)hipFuncSetAttribute((const void*)k_bin_count, hipFuncAttributeMaxDynamicSharedMemorySize,
                                   lds_max);
-        (void)hipFuncSetAttribute((const void*)k_group_a<kOffDense>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  lds_max);
-        (void)hipFuncSetAttribute((const void*)k_group_a<kOffR32>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  lds_max);
-        (void)hipFuncSetAttribute((const void*)k_group_a<kOffR64>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  lds_max);
+        (void)hipFuncSetAttribute((const void*)k_group_a<kOffDense, false>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, lds_max);
+        (void)hipFuncSetAttribute((const void*)k_group_a<kOffR32, false>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, lds_max);
+        (void)hipFuncSetAttribute((const void*)k_group_a<kOffR64, false>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, lds_max);
+        (void)hipFuncSetAttribute((const void*)k_group_a<kOffDense, true>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, lds_max);
+        (void)hipFuncSetAttribute((const void*)k_group_a<kOffR32, true>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, lds_max);
         (void)hipFuncSetAttribute((const void*)k_pileup<false>, hipFuncAttributeMaxDynamicSharedMemorySize, lds_max);
         (void)hipFuncSetAttribute((const void*)k_pileup<true>, hipFuncAttributeMaxDynamicSharedMemorySize, lds_max);
         (void)hipGetLastError();
@@ -2308,7 +2397,8 @@ int mgp_push_batch(mgp_ctx* ctx, const mgp_batch* b) {
     if (n0 == 0) HIP_TRY(hipMemsetAsync(ctx->roff_irregular.p, 0, 4, s));
     ctx->roff_mode = -1;
     k_check_stride<<<blocks_for(nb), kBlock, 0, s>>>(ctx->roff.as<uint64_t>() + n0, ctx->flag.as<uint16_t>() + n0,
-                                                     nb, n0, ctx->roff_irregular.as<uint32_t>(),
+                                                     ctx->start.as<int32_t>() + n0, ctx->tlen.as<int32_t>() + n0,
+                                                     ctx->cfg.mito_len, nb, n0, ctx->roff_irregular.as<uint32_t>(),
                                                      ctx->roff32.as<uint32_t>() + n0);
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipEventRecord(ctx->ev_copy, s));
@@ -2464,7 +2554,12 @@ int mgp_run(mgp_ctx* ctx) {
         HIP_TRY(hipGetLastError());
         STAGE_END(ST_SCAN);
 
-        // 3. stable grouping into cell-major order (two passes), duplicate marking in pass B
+        // 3. stable grouping into cell-major order (two passes), duplicate marking in pass B;
+        // 8-byte elements when the resident reads allow them (GCompact)
+        const uint32_t rbits = ctx->read_bits;
+        const bool track = ((rbits & CHK_PAIRED) && (rbits & CHK_UNPAIRED)) || (rbits & CHK_NOSEQ);
+        const bool compact = !ctx->group_wide && ctx->roff_mode != kOffR64 && unit == 6 && !track &&
+                             !(rbits & (CHK_FULL | CHK_WIDEKEY));
         STAGE_BEGIN(ST_GROUP_A);
         if (n > 0) {
             int gbits = 0;
@@ -2484,9 +2579,16 @@ int mgp_run(mgp_ctx* ctx) {
                     ctx->F.as<uint32_t>(), ctx->bin_base.as<uint32_t>(), g, ngroups, gbits, ctx->cfg.min_mapq,
                     ctx->bucket_off.as<uint32_t>(), ctx->gel2.as<GElem>(), ctx->first_read.as<uint32_t>(), st);
             };
-            if (ctx->roff_mode == kOffDense) launch_a(k_group_a<kOffDense>);
-            else if (ctx->roff_mode == kOffR32) launch_a(k_group_a<kOffR32>);
-            else launch_a(k_group_a<kOffR64>);
+            if (compact) {
+                if (ctx->roff_mode == kOffDense) launch_a(k_group_a<kOffDense, true>);
+                else launch_a(k_group_a<kOffR32, true>);
+            } else if (ctx->roff_mode == kOffDense) {
+                launch_a(k_group_a<kOffDense, false>);
+            } else if (ctx->roff_mode == kOffR32) {
+                launch_a(k_group_a<kOffR32, false>);
+            } else {
+                launch_a(k_group_a<kOffR64, false>);
+            }
             HIP_TRY(hipGetLastError());
         }
         STAGE_END(ST_GROUP_A);
@@ -2506,15 +2608,14 @@ int mgp_run(mgp_ctx* ctx) {
             MGP_TRY(ctx->dup_part.ensure((size_t)dup_parts * 16));
             // per-read pairedness / SEQ tracking only when the reads mix paired and
             // unpaired ones or some read lacks SEQ/QUAL
-            const uint32_t rbits = ctx->read_bits;
-            const bool track = ((rbits & CHK_PAIRED) && (rbits & CHK_UNPAIRED)) || (rbits & CHK_NOSEQ);
-            auto launch_b = [&](auto kern) {
-                kern<<<gb, kBlock, 0, s>>>(ctx->gel2.as<GElem>(), ctx->bucket_off.as<uint32_t>(), ctx->H.as<uint32_t>(),
+            auto launch_b = [&](auto kern, auto* gel) {
+                kern<<<gb, kBlock, 0, s>>>(gel, ctx->bucket_off.as<uint32_t>(), ctx->H.as<uint32_t>(),
                                            g, ngroups, rb, ctx->cfg.dedup_mode, unit, ctx->pel.as<uint32_t>(),
                                            ctx->any_paired.as<uint8_t>(), ctx->dup_part.as<unsigned long long>(), st);
             };
-            if (track) launch_b(k_group_b<true>);
-            else launch_b(k_group_b<false>);
+            if (compact) launch_b(k_group_b<false, GCompact>, ctx->gel2.as<unsigned long long>());
+            else if (track) launch_b(k_group_b<true, GWide>, ctx->gel2.as<GElem>());
+            else launch_b(k_group_b<false, GWide>, ctx->gel2.as<GElem>());
             pair_mode = track ? 0 : (rbits & CHK_PAIRED) ? 1 : 0;
             HIP_TRY(hipGetLastError());
         }
@@ -2809,8 +2910,9 @@ int mgp_synth_generate(mgp_ctx* ctx, const mgp_synth_params* p) {
     HIP_TRY(hipMemsetAsync(ctx->roff_irregular.p, 0, 4, s));
     ctx->roff_mode = -1;
     if (n)
-        k_check_stride<<<blocks_for(n), kBlock, 0, s>>>(ctx->roff.as<uint64_t>(), ctx->flag.as<uint16_t>(), n, 0,
-                                                        ctx->roff_irregular.as<uint32_t>(),
+        k_check_stride<<<blocks_for(n), kBlock, 0, s>>>(ctx->roff.as<uint64_t>(), ctx->flag.as<uint16_t>(),
+                                                        ctx->start.as<int32_t>(), ctx->tlen.as<int32_t>(),
+                                                        ctx->cfg.mito_len, n, 0, ctx->roff_irregular.as<uint32_t>(),
                                                         ctx->roff32.as<uint32_t>());
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipStreamSynchronize(s));

@@ -512,3 +512,59 @@ def test_device_generator_with_placement(engine_lib):
     for k in ("start", "bc", "tlen", "flag", "mapq", "span", "rec_off"):
         np.testing.assert_array_equal(getattr(dev, k), getattr(exp, k), err_msg=k)
     np.testing.assert_array_equal(dev.payload[: exp.payload.size], exp.payload[: dev.payload.size])
+
+
+# ---------------------------------------------------------------------------
+# grouping element forms (mgp_engine.hip): 8-byte compact elements whenever the
+# resident reads allow them, the 16-byte form forced with MGP_GROUP_WIDE=1
+# ---------------------------------------------------------------------------
+def _run_forms(engine_lib, cfg, soa, monkeypatch):
+    a = run_engine(engine_lib, cfg, soa)
+    monkeypatch.setenv("MGP_GROUP_WIDE", "1")
+    try:
+        b = run_engine(engine_lib, cfg, soa)
+    finally:
+        monkeypatch.delenv("MGP_GROUP_WIDE")
+    return a, b
+
+
+@pytest.mark.parametrize("cfgname", sorted(CONFIGS))
+def test_compact_and_wide_grouping_agree(engine_lib, oracle_lib, monkeypatch, cfgname):
+    """Synthetic reads qualify for the compact element (all packed and paired,
+    starts in [0, L), |tlen| < 2^17). Both element forms equal the oracle, on a
+    dense set and on a sparse one whose pass-B steps stop at the 32-bin cap."""
+    from mgatk2_amd.engine import EngineConfig
+
+    for seed, n, nc in [(5, 300_000, 150), (6, 20_000, 3)]:
+        soa = _synth(seed, n, nc)
+        cfg = EngineConfig(n_cells=nc, **CONFIGS[cfgname])
+        a, b = _run_forms(engine_lib, cfg, soa, monkeypatch)
+        exp, _ = oracle_lib.oracle_run(cfg, soa)
+        assert_same(a, exp, f"compact {cfgname} {n}x{nc}")
+        assert_same(b, exp, f"wide {cfgname} {n}x{nc}")
+
+
+def test_compact_starts_256_apart_are_not_duplicates(engine_lib, oracle_lib, monkeypatch):
+    """Compact elements keep start mod 256: reads of one cell with the same strand
+    and |tlen| every 256 positions (equal mod 256, one start bin 32 bins after
+    the other) are distinct reads; true duplicates at equal starts still drop."""
+    from mgatk2_amd.engine import EngineConfig
+    from mgatk2_amd.synth import pack_reads
+
+    reads = []
+    for k in range(40):
+        s = 100 + 256 * k
+        reads.append(_read(s, [(0, 30)], "ACGT" * 7 + "AC", 0, tlen=150))
+        if k % 3 == 0:  # a duplicate under both keys
+            reads.append(_read(s, [(0, 30)], "CAGT" * 7 + "CA", 0, tlen=-150))
+        if k % 4 == 1:  # same start, other strand
+            reads.append(_read(s, [(0, 30)], "GGGT" * 7 + "GG", 0, flag=0x11, tlen=150))
+    soa = pack_reads(reads)
+    for mode in ("alignment_and_fragment_length", "alignment_start", "none"):
+        cfg = EngineConfig(n_cells=1, min_baseq=0, min_mapq=0, min_reads=0, dedup_mode=mode)
+        a, b = _run_forms(engine_lib, cfg, soa, monkeypatch)
+        exp, _ = oracle_lib.oracle_run(cfg, soa)
+        assert_same(a, exp, f"compact {mode}")
+        assert_same(b, exp, f"wide {mode}")
+        if mode != "none":
+            assert exp.stats["duplicate_reads_with_length"] == 14
