@@ -557,7 +557,9 @@ __global__ void __launch_bounds__(kGABlock, MGP_GA_WAVES) k_group_a(int64_t n, c
             valid[u] = i < hi && read_valid(c, (uint16_t)P.fm[u], nc);
             const int gi = c >> 6;
             unsigned long long pm = __ballot(valid[u]);
-            for (int bit = 0; bit < gbits && pm; ++bit) {
+            // wave-uniform loop (gbits is a kernel argument): an early exit on the
+            // per-lane peer mask would make it divergent
+            for (int bit = 0; bit < gbits; ++bit) {
                 const bool x = valid[u] && ((gi >> bit) & 1);
                 const unsigned long long m = __ballot(x);
                 pm &= x ? m : ~m;
