@@ -419,20 +419,24 @@ constexpr uint64_t kRecStride = MGP_PACK_BYTES;  // record stride of a dense pac
 //   kOffR64    otherwise: the u64 rec_off column
 enum { kOffDense = 0, kOffR32 = 1, kOffR64 = 2 };
 
+// Pileup element values (see k_group_b)
+constexpr uint32_t PE_DUP = 0xFFFFFFFFu, PE_KEEP = 0xFFFFFFFEu, PE_PACKED = 0x80000000u, PE_OFF = 0x7FFFFFFFu;
+
 // Compact grouping element (8 bytes), used when every resident record is packed
 // at a 64-byte multiple below 2^37 (dense or u32 offsets), the reads do not mix
 // paired and unpaired ones and all have SEQ/QUAL, every start lies in
-// [0, mito_len) and every |tlen| < 2^17 (the ingest check's bits):
-//   bits 0..30 record offset / 64 (the pileup element's offset field), 31..36 cell
-//   in group, 37 reverse, 38 MAPQ >= min_mapq, 39..46 start mod 256, 47..63 |tlen|.
+// [0, mito_len) and every |tlen| < 2^16 (the ingest check's bits):
+//   low word   the pileup element of the read if it is kept: record offset / 64
+//              (bits 0..30) | PE_PACKED when MAPQ >= min_mapq; 0 in bit 31 otherwise
+//   high word  |tlen| (bits 0..15), start mod 256 (16..23), reverse (24), cell in
+//              group (25..30): every duplicate-key field, so pass B compares one word
 // Pass B compares starts mod 256: its steps span fewer than 32 start bins (256
 // positions), and a cell's elements of one step are in start order, so equal
 // starts mod 256 inside a cell's run of a step are equal starts.
-constexpr int GC_LCELL_SHIFT = 31, GC_START_SHIFT = 39, GC_TLEN_SHIFT = 47;
-constexpr unsigned long long GC_OFF = 0x7FFFFFFFull, GC_LCELL = 63ull << GC_LCELL_SHIFT, GC_REV = 1ull << 37,
-                             GC_MAPQ_OK = 1ull << 38, GC_START = 255ull << GC_START_SHIFT,
-                             GC_TLEN = 0x1FFFFull << GC_TLEN_SHIFT;
-constexpr uint32_t kCompactTlen = 1u << 17;  // |tlen| below this fits the compact element
+constexpr int GC_START_SHIFT = 16, GC_LCELL_SHIFT = 25;
+constexpr uint32_t GC_TLEN = 0xFFFFu, GC_START = 0xFFu << GC_START_SHIFT, GC_REV = 1u << 24,
+                   GC_LCELL = 63u << GC_LCELL_SHIFT;
+constexpr uint32_t kCompactTlen = 1u << 16;  // |tlen| below this fits the compact element
 constexpr int kCompactBins = 32;             // start bins per pass-B step (compact elements)
 
 #ifndef MGP_GA_AHEAD
@@ -607,10 +611,11 @@ __global__ void __launch_bounds__(kGABlock, MGP_GA_WAVES) k_group_a(int64_t n, c
                 atomicOr(&st->err, ERR_OVERFLOW);
             } else if constexpr (kCompact) {
                 // the record's 64-byte unit (dense: the read index; u32 column: rec_off >> 6)
-                const unsigned long long e =
-                    (unsigned long long)P.o[u] | ((unsigned long long)(P.c[u] & (kGroup - 1)) << GC_LCELL_SHIFT) |
-                    (f & MGP_FLAG_REVERSE ? GC_REV : 0ull) | (mq ? GC_MAPQ_OK : 0ull) |
-                    ((unsigned long long)(P.s[u] & 255) << GC_START_SHIFT) | ((unsigned long long)at << GC_TLEN_SHIFT);
+                const uint32_t lo = (uint32_t)P.o[u] | (mq ? PE_PACKED : 0u);
+                const uint32_t hi = at | ((uint32_t)(P.s[u] & 255) << GC_START_SHIFT) |
+                                    (f & MGP_FLAG_REVERSE ? GC_REV : 0u) |
+                                    ((uint32_t)(P.c[u] & (kGroup - 1)) << GC_LCELL_SHIFT);
+                const unsigned long long e = (unsigned long long)hi << 32 | lo;
                 reinterpret_cast<unsigned long long*>(gel2)[dest] = e;
             } else {
                 GElem e;
@@ -675,7 +680,6 @@ constexpr int kMaxRbB = 256;  // bins per pass-B workgroup (bucket sizes kept in
 // 2^unit bytes (unit 6, or 4 for 16-byte aligned placements) | PE_PACKED; a kept
 // read below min_mapq is PE_KEEP, a duplicate PE_DUP (the pileup counts the
 // kept reads, processors.py:22). Offsets stay below PE_KEEP's (mgp_run checks).
-constexpr uint32_t PE_DUP = 0xFFFFFFFFu, PE_KEEP = 0xFFFFFFFEu, PE_PACKED = 0x80000000u, PE_OFF = 0x7FFFFFFFu;
 constexpr unsigned long long GM_OFF = (1ull << GM_LCELL_SHIFT) - 1;
 
 struct DedupAcc {  // per-thread duplicate counters of pass B
@@ -712,20 +716,42 @@ struct GWide {
     static __device__ __forceinline__ uint32_t pile(const T& e, int unit) {
         return (uint32_t)((e.w & GM_OFF) >> unit) | (e.w & GM_PACKED ? PE_PACKED : 0u);
     }
+    // a predecessor's duplicate key, read from the LDS stage, against element x:
+    // same run (cell and start), then also strand, then also |tlen|
+    using P = GElem;
+    static __device__ __forceinline__ P pred(const T* stage, uint32_t i) { return stage[i]; }
+    static __device__ __forceinline__ void match(const P& p, const T& x, bool& run, bool& strand, bool& tl) {
+        run = run_eq(p, x);
+        strand = strand_eq(p, x);
+        tl = tlen_eq(p, x);
+    }
     static __device__ __forceinline__ bool paired(const T& e) { return (e.w & GM_PAIRED) != 0ull; }
     static __device__ __forceinline__ bool bad(const T& e) { return (e.w & GM_BAD) != 0ull; }
 };
 struct GCompact {
     using T = unsigned long long;
     static constexpr int kWaves = MGP_GB_WAVES_C;  // fewer registers: 5 waves per SIMD (A/B: 4 slower)
+    static __device__ __forceinline__ uint32_t key(const T& e) { return (uint32_t)(e >> 32); }
     static __device__ __forceinline__ T zero() { return 0ull; }
-    static __device__ __forceinline__ int lcell(const T& e) { return (int)((e >> GC_LCELL_SHIFT) & (kGroup - 1)); }
-    static __device__ __forceinline__ bool run_eq(const T& a, const T& b) { return ((a ^ b) & (GC_LCELL | GC_START)) == 0ull; }
-    static __device__ __forceinline__ bool start_eq(const T& a, const T& b) { return ((a ^ b) & GC_START) == 0ull; }
-    static __device__ __forceinline__ bool strand_eq(const T& a, const T& b) { return ((a ^ b) & GC_REV) == 0ull; }
-    static __device__ __forceinline__ bool tlen_eq(const T& a, const T& b) { return ((a ^ b) & GC_TLEN) == 0ull; }
-    static __device__ __forceinline__ bool mapq_ok(const T& e) { return (e & GC_MAPQ_OK) != 0ull; }
-    static __device__ __forceinline__ uint32_t pile(const T& e, int) { return (uint32_t)(e & GC_OFF) | PE_PACKED; }
+    static __device__ __forceinline__ int lcell(const T& e) { return (int)((key(e) >> GC_LCELL_SHIFT) & (kGroup - 1)); }
+    static __device__ __forceinline__ bool run_eq(const T& a, const T& b) {
+        return ((key(a) ^ key(b)) & (GC_LCELL | GC_START)) == 0u;
+    }
+    static __device__ __forceinline__ bool start_eq(const T& a, const T& b) { return ((key(a) ^ key(b)) & GC_START) == 0u; }
+    static __device__ __forceinline__ bool strand_eq(const T& a, const T& b) { return ((key(a) ^ key(b)) & GC_REV) == 0u; }
+    static __device__ __forceinline__ bool tlen_eq(const T& a, const T& b) { return ((key(a) ^ key(b)) & GC_TLEN) == 0u; }
+    static __device__ __forceinline__ bool mapq_ok(const T& e) { return ((uint32_t)e & PE_PACKED) != 0u; }
+    static __device__ __forceinline__ uint32_t pile(const T& e, int) { return (uint32_t)e; }
+    using P = uint32_t;  // the high word only (a 4-byte LDS read)
+    static __device__ __forceinline__ P pred(const T* stage, uint32_t i) {
+        return reinterpret_cast<const uint32_t*>(stage)[2 * i + 1];
+    }
+    static __device__ __forceinline__ void match(P p, const T& x, bool& run, bool& strand, bool& tl) {
+        const uint32_t d = p ^ key(x);
+        run = (d & (GC_LCELL | GC_START)) == 0u;
+        strand = (d & GC_REV) == 0u;
+        tl = (d & GC_TLEN) == 0u;
+    }
     static __device__ __forceinline__ bool paired(const T&) { return true; }
     static __device__ __forceinline__ bool bad(const T&) { return false; }
 };
@@ -1007,16 +1033,17 @@ __global__ void __launch_bounds__(kBlock, Tr::kWaves) k_group_b(const typename T
                 const uint32_t t = threadIdx.x + (uint32_t)(h + q) * kBlock;
                 const uint32_t tc = t < cur ? t : 0u;
                 const T x = stage[tc];
-                T pk[kLook];
+                typename Tr::P pk[kLook];
 #pragma unroll
-                for (int k = 0; k < kLook; ++k) pk[k] = stage[tc >= (uint32_t)(k + 1) ? tc - (uint32_t)(k + 1) : 0u];
+                for (int k = 0; k < kLook; ++k) pk[k] = Tr::pred(stage, tc >= (uint32_t)(k + 1) ? tc - (uint32_t)(k + 1) : 0u);
                 bool r = true, s2 = false, t3 = false;  // r: the k nearest predecessors are all in x's run
 #pragma unroll
                 for (int k = 0; k < kLook; ++k) {
-                    r = r & (tc >= (uint32_t)(k + 1)) & Tr::run_eq(pk[k], x);
-                    const bool sk = r & Tr::strand_eq(pk[k], x);
-                    s2 |= sk;
-                    t3 |= sk & Tr::tlen_eq(pk[k], x);
+                    bool rk, sk, tk;
+                    Tr::match(pk[k], x, rk, sk, tk);
+                    r = r & (tc >= (uint32_t)(k + 1)) & rk;
+                    s2 |= r & sk;
+                    t3 |= r & sk & tk;
                 }
                 xs[q] = x;
                 d2[q] = dedup & s2;
