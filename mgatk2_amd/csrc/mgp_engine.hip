@@ -132,7 +132,7 @@ struct mgp_ctx {
 
     // run scratch
     DevBuf bin_start, H, P, cell_cnt, cell_base, bin_valid, bin_base, bucket_off, gel2, PG, F;
-    DevBuf pel, tally_part, tally, bin_mspan, dup_part;
+    DevBuf pel, tally_part, tally, dup_part;
     DevBuf n_reads, any_paired, passed, covered, dsum, dmax, med_lo, med_hi, first_read;
     DevBuf counts, tn5, depth, stats;  // u32 rows: drained windows, and mgp_fetch's widened copy
     DevBuf counts16, tn5_16, depth16, wide;  // the run's 16-bit result rows (Out16)
@@ -194,9 +194,10 @@ __device__ __forceinline__ void part_range(int64_t lo, int64_t hi, int p, int64_
 #define MGP_HIST_BLOCK 512
 #endif
 // One workgroup (8 waves) per (start bin, cell slice): bin bounds by binary
-// search in the sorted starts, coordinate-order check (pysam's fetch order,
-// readers.py:87-92), flag/barcode filters (readers.py:95-111) and the LDS
-// histogram of the slice's cells over the bin's reads. A slice is as many
+// search in the sorted starts (the coordinate order and the largest span are
+// checked at ingest, k_check_stride), flag/barcode filters (readers.py:95-111)
+// and the LDS histogram of the slice's cells over the bin's reads: 6 bytes read
+// per read. A slice is as many
 // 64-cell groups as the LDS holds (one slice up to ~24k cells; more cells scan
 // the bin once per slice). The bin's parts are counted one after the other;
 // after each part the per-64-cell-group totals are snapshotted, giving the
@@ -205,16 +206,14 @@ __device__ __forceinline__ void part_range(int64_t lo, int64_t hi, int p, int64_
 constexpr int kHistBlock = MGP_HIST_BLOCK;
 __global__ void __launch_bounds__(kHistBlock) k_bin_count(const int32_t* __restrict__ start,
                                                           const int32_t* __restrict__ bc,
-                                                          const uint16_t* __restrict__ flag,
-                                                          const uint32_t* __restrict__ span, int64_t n, Geom g,
+                                                          const uint16_t* __restrict__ flag, int64_t n, Geom g,
                                                           int slice_cells, uint32_t* __restrict__ H,
                                                           uint32_t* __restrict__ PG, int ngroups,
                                                           uint32_t* __restrict__ bin_lo,
-                                                          uint32_t* __restrict__ bin_valid,
-                                                          uint32_t* __restrict__ bin_mspan, DevStats* st) {
+                                                          uint32_t* __restrict__ bin_valid, DevStats* st) {
     extern __shared__ uint32_t hist[];  // [slice cells] counts, then cum[slice groups]
     __shared__ int64_t s_range[2];
-    __shared__ uint32_t s_nvalid, s_mspan;
+    __shared__ uint32_t s_nvalid;
     const int b = blockIdx.x;
     const bool first = blockIdx.y == 0;
     const int nc = g.nc;
@@ -226,16 +225,15 @@ __global__ void __launch_bounds__(kHistBlock) k_bin_count(const int32_t* __restr
     uint32_t* row = H + (size_t)b * nc;
     if (threadIdx.x < 2) s_range[threadIdx.x] = lower_bound_start(start, n, bin_threshold(b + threadIdx.x, g));
     for (int c = threadIdx.x; c < ncs; c += blockDim.x) hist[c] = 0;
-    if (threadIdx.x == 0) s_nvalid = s_mspan = 0;
+    if (threadIdx.x == 0) s_nvalid = 0;
     __syncthreads();
     const int64_t blo = s_range[0], bhi = max(s_range[1], blo);
     if (first && threadIdx.x == 0) {
         bin_lo[b] = (uint32_t)blo;
         if (b == g.nbins - 1) bin_lo[g.nbins] = (uint32_t)n;
     }
-    uint32_t mspan = 0;
     unsigned long long nvalid = 0;
-    bool badbc = false, unsorted = false;
+    bool badbc = false;
     uint32_t* pg = PG + (size_t)b * kParts * ngroups;
     for (int part = 0; part < kParts; ++part) {
         int64_t lo, hi;
@@ -243,8 +241,7 @@ __global__ void __launch_bounds__(kHistBlock) k_bin_count(const int32_t* __restr
         // 4 reads per thread per step, loads issued together (clamped index, no branches)
         constexpr int kU = MGP_HIST_U;
         for (int64_t i0 = lo + threadIdx.x; i0 < hi; i0 += kU * kHistBlock) {
-            int cc[kU], ss[kU], sp0[kU];
-            uint32_t sp[kU];
+            int cc[kU];
             uint32_t ff[kU];
 #pragma unroll
             for (int u = 0; u < kU; ++u) {
@@ -252,24 +249,15 @@ __global__ void __launch_bounds__(kHistBlock) k_bin_count(const int32_t* __restr
                 const int64_t j = i < hi ? i : hi - 1;
                 cc[u] = bc[j];
                 ff[u] = flag[j];
-                ss[u] = sp0[u] = 0;
-                sp[u] = 0;
-                if (first) {  // the run checks: slice 0 only (other slices read 6 B per read)
-                    ss[u] = start[j];
-                    sp0[u] = start[j > 0 ? j - 1 : 0];
-                    sp[u] = span[j];
-                }
             }
 #pragma unroll
             for (int u = 0; u < kU; ++u) {
                 const int64_t i = i0 + u * kHistBlock;
-                if (i >= hi) break;
                 const int c = cc[u];
-                if (i > 0 && ss[u] < sp0[u]) unsorted = true;
-                badbc |= (c >= nc);
-                if (read_valid(c, (uint16_t)ff[u], nc)) {
+                const bool in = i < hi;
+                badbc |= in && (c >= nc);
+                if (in && read_valid(c, (uint16_t)ff[u], nc)) {
                     if (c >= c_lo && c < c_hi) atomicAdd(&hist[c - c_lo], 1u);
-                    mspan = sp[u] > mspan ? sp[u] : mspan;
                     ++nvalid;
                 }
             }
@@ -290,22 +278,16 @@ __global__ void __launch_bounds__(kHistBlock) k_bin_count(const int32_t* __restr
     }
     for (int c = threadIdx.x; c < ncs; c += blockDim.x) row[c_lo + c] = hist[c];
     if (!first) return;
-    mspan = wave_max(mspan);
     nvalid = wave_sum(nvalid);
-    const bool anybad = __ballot(badbc) != 0ull, anyuns = __ballot(unsorted) != 0ull;
-    // per-bin results (k_run_stats reduces them): a global atomic per wave on one
-    // word serialises at the memory side
+    const bool anybad = __ballot(badbc) != 0ull;
+    // the bin's valid count (a global atomic per wave on one word serialises at the
+    // memory side)
     if (lane == 0) {
-        if (mspan) atomicMax(&s_mspan, mspan);
         if (nvalid) atomicAdd(&s_nvalid, (uint32_t)nvalid);
         if (anybad) atomicOr(&st->err, ERR_BADBC);
-        if (anyuns) atomicOr(&st->err, ERR_UNSORTED);
     }
     __syncthreads();
-    if (threadIdx.x == 0) {
-        bin_valid[b] = s_nvalid;
-        bin_mspan[b] = s_mspan;
-    }
+    if (threadIdx.x == 0) bin_valid[b] = s_nvalid;
 }
 
 // Scan step a: column sums over blocks of RB rows. grid (ceil(nc/256), nrb)
@@ -2084,31 +2066,17 @@ __global__ void __launch_bounds__(kBlock) k_median(Geom g, int min_reads, const 
     }
 }
 
-// Run statistics from per-bin / per-workgroup / per-cell partials (one workgroup
-// of 1024 threads): which=0 after the histogram: max_span (the pileup's halo);
-// which=1 at the end: kept reads, barcodes with a kept read, passing cells and
-// the two duplicate counters (readers.py:141-144,193-199, processors.py:22).
-__global__ void __launch_bounds__(1024) k_run_stats(int which, const uint32_t* __restrict__ bin_mspan, int nbins,
-                                                    const uint32_t* __restrict__ n_reads,
+// Run statistics from per-workgroup / per-cell partials (one workgroup of 1024
+// threads) at the end of a run: kept reads, barcodes with a kept read, passing
+// cells and the two duplicate counters (readers.py:141-144,193-199,
+// processors.py:22).
+__global__ void __launch_bounds__(1024) k_run_stats(const uint32_t* __restrict__ n_reads,
                                                     const uint8_t* __restrict__ passed, int nc,
                                                     const unsigned long long* __restrict__ dup_part, int nparts,
                                                     DevStats* st) {
     __shared__ unsigned long long red[5][1024 / kWave];
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     unsigned long long a = 0, b = 0, c = 0, d = 0, e = 0;
-    if (which == 0) {
-        uint32_t m = 0;
-        for (int i = threadIdx.x; i < nbins; i += 1024) m = max(m, bin_mspan[i]);
-        m = wave_max(m);
-        if (lane == 0) red[0][wid] = m;
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            uint32_t t = 0;
-            for (int w = 0; w < 1024 / kWave; ++w) t = max(t, (uint32_t)red[0][w]);
-            st->max_span = t;
-        }
-        return;
-    }
     for (int i = threadIdx.x; i < nc; i += 1024) {
         const uint32_t r = n_reads[i];
         a += r;
@@ -2191,14 +2159,24 @@ __global__ void k_add_u64(uint64_t* __restrict__ a, int64_t n, uint64_t add) {
 // reads mix or lack them).
 // CHK_FULL: some record is in the full layout; CHK_WIDEKEY: some start lies
 // outside [0, mito_len) or some |tlen| >= kCompactTlen (no compact grouping element).
-constexpr uint32_t CHK_PAIRED = 4u, CHK_UNPAIRED = 8u, CHK_NOSEQ = 16u, CHK_FULL = 32u, CHK_WIDEKEY = 64u;
+// CHK_UNSORTED: a start below its predecessor's (pysam's fetch order,
+// readers.py:87-92; the previous batch's last read included). Word 1 of the
+// ingest words receives the largest declared span of the reads the run keeps at
+// its filters (the pileup's window halo).
+constexpr uint32_t CHK_PAIRED = 4u, CHK_UNPAIRED = 8u, CHK_NOSEQ = 16u, CHK_FULL = 32u, CHK_WIDEKEY = 64u,
+                   CHK_UNSORTED = 128u;
 __global__ void k_check_stride(const uint64_t* __restrict__ roff, const uint16_t* __restrict__ flag,
-                               const int32_t* __restrict__ start, const int32_t* __restrict__ tlen, int mito_len,
-                               int64_t n, int64_t i0, uint32_t* irregular, uint32_t* __restrict__ roff32) {
+                               const int32_t* __restrict__ start_all, const int32_t* __restrict__ tlen,
+                               const int32_t* __restrict__ bc, const uint32_t* __restrict__ span, int mito_len,
+                               int n_cells, int64_t n, int64_t i0, uint32_t* irregular,
+                               uint32_t* __restrict__ roff32) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int32_t* start = start_all + i0;
     const uint64_t r = i < n ? roff[i] : 0ull;
     const uint32_t f = i < n ? flag[i] : 0u;
     const int32_t s0 = i < n ? start[i] : 0, t0 = i < n ? tlen[i] : 0;
+    const bool uns = i < n && i0 + i > 0 && s0 < start_all[i0 + i - 1];
+    const uint32_t sp = i < n && read_valid(bc[i], (uint16_t)f, n_cells) ? span[i] : 0u;
     const uint32_t at = t0 < 0 ? (uint32_t)(-(int64_t)t0) : (uint32_t)t0;
     if (i < n) roff32[i] = (uint32_t)(r >> 6);
     const bool bad = i < n && r != (uint64_t)(i0 + i) * kRecStride;
@@ -2208,12 +2186,24 @@ __global__ void k_check_stride(const uint64_t* __restrict__ roff, const uint16_t
     const unsigned long long b5 = __ballot(i < n && (f & MGP_FLAG_NOSEQQUAL));
     const unsigned long long b6 = __ballot(i < n && !(f & MGP_FLAG_PACKED));
     const unsigned long long b7 = __ballot(i < n && (s0 < 0 || s0 >= mito_len || at >= kCompactTlen));
+    const unsigned long long b8 = __ballot(uns);
     const uint32_t bits = (b1 ? 1u : 0u) | (b2 ? 2u : 0u) | (b3 ? CHK_PAIRED : 0u) | (b4 ? CHK_UNPAIRED : 0u) |
-                          (b5 ? CHK_NOSEQ : 0u) | (b6 ? CHK_FULL : 0u) | (b7 ? CHK_WIDEKEY : 0u);
+                          (b5 ? CHK_NOSEQ : 0u) | (b6 ? CHK_FULL : 0u) | (b7 ? CHK_WIDEKEY : 0u) |
+                          (b8 ? CHK_UNSORTED : 0u);
+    const uint32_t msp = wave_max(sp);
+    if ((threadIdx.x & 63) == 0 && msp > __atomic_load_n(irregular + 1, __ATOMIC_RELAXED)) atomicMax(irregular + 1, msp);
     // one atomic per wave at most, and none once the bits are set (every wave of a
     // paired payload has irregular offsets: 3M atomics on one word took 18 ms)
     if (bits && (threadIdx.x & 63) == 0 && (__atomic_load_n(irregular, __ATOMIC_RELAXED) & bits) != bits)
         atomicOr(irregular, bits);
+}
+
+// The run's view of the ingest checks: the pileup's halo span and the order check.
+__global__ void k_ingest_stats(const uint32_t* __restrict__ ingest, DevStats* st) {
+    if (threadIdx.x == 0) {
+        st->max_span = ingest[1];
+        if (ingest[0] & CHK_UNSORTED) atomicOr(&st->err, ERR_UNSORTED);
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -2357,7 +2347,7 @@ void mgp_close(mgp_ctx* ctx) {
     if (ctx->comm) ncclCommDestroy(ctx->comm);
     DevBuf* bufs[] = {&ctx->start,     &ctx->bc,        &ctx->tlen,     &ctx->flag,       &ctx->mapq,
                       &ctx->span,      &ctx->roff,      &ctx->payload,  &ctx->bin_start,  &ctx->gel2,
-                      &ctx->roff32,    &ctx->roff_irregular, &ctx->bin_mspan, &ctx->dup_part,
+                      &ctx->roff32,    &ctx->roff_irregular, &ctx->dup_part,
                       &ctx->H,         &ctx->P,         &ctx->cell_cnt, &ctx->cell_base,  &ctx->pel,
                       &ctx->PG,        &ctx->F,
                       &ctx->tally_part, &ctx->tally,   &ctx->n_reads,    &ctx->any_paired,
@@ -2422,12 +2412,14 @@ int mgp_push_batch(mgp_ctx* ctx, const mgp_batch* b) {
         k_add_u64<<<blocks_for(nb), kBlock, 0, s>>>(ctx->roff.as<uint64_t>() + n0, nb, (uint64_t)pay0);
         HIP_TRY(hipGetLastError());
     }
-    MGP_TRY(ctx->roff_irregular.ensure(4));
-    if (n0 == 0) HIP_TRY(hipMemsetAsync(ctx->roff_irregular.p, 0, 4, s));
+    MGP_TRY(ctx->roff_irregular.ensure(8));
+    if (n0 == 0) HIP_TRY(hipMemsetAsync(ctx->roff_irregular.p, 0, 8, s));
     ctx->roff_mode = -1;
     k_check_stride<<<blocks_for(nb), kBlock, 0, s>>>(ctx->roff.as<uint64_t>() + n0, ctx->flag.as<uint16_t>() + n0,
-                                                     ctx->start.as<int32_t>() + n0, ctx->tlen.as<int32_t>() + n0,
-                                                     ctx->cfg.mito_len, nb, n0, ctx->roff_irregular.as<uint32_t>(),
+                                                     ctx->start.as<int32_t>(), ctx->tlen.as<int32_t>() + n0,
+                                                     ctx->bc.as<int32_t>() + n0, ctx->span.as<uint32_t>() + n0,
+                                                     ctx->cfg.mito_len, ctx->cfg.n_cells, nb, n0,
+                                                     ctx->roff_irregular.as<uint32_t>(),
                                                      ctx->roff32.as<uint32_t>() + n0);
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipEventRecord(ctx->ev_copy, s));
@@ -2470,7 +2462,6 @@ static int ensure_run_buffers(mgp_ctx* ctx) {
     MGP_TRY(ctx->pel.ensure(n * 4));
     MGP_TRY(ctx->gel2.ensure(n * sizeof(GElem)));
     MGP_TRY(ctx->bin_valid.ensure((size_t)(g.nbins + 1) * 4));
-    MGP_TRY(ctx->bin_mspan.ensure((size_t)(g.nbins + 1) * 4));
     MGP_TRY(ctx->bin_base.ensure((size_t)(g.nbins + 1) * 4));
     MGP_TRY(ctx->bucket_off.ensure((size_t)g.nbins * ((nc + kGroup - 1) / kGroup + 1) * 4));
     MGP_TRY(ctx->tally_part.ensure((size_t)std::max(g.nchunks, 1) * L * 16));
@@ -2559,12 +2550,11 @@ int mgp_run(mgp_ctx* ctx) {
             const int nslices = (nc + slice - 1) / slice;
             const size_t lds = ((size_t)slice + (slice + kGroup - 1) / kGroup) * 4;
             k_bin_count<<<dim3((unsigned)g.nbins, (unsigned)nslices), kHistBlock, lds, s>>>(
-                ctx->start.as<int32_t>(), ctx->bc.as<int32_t>(), ctx->flag.as<uint16_t>(), ctx->span.as<uint32_t>(),
-                n, g, slice, ctx->H.as<uint32_t>(), ctx->PG.as<uint32_t>(), ngroups, ctx->bin_start.as<uint32_t>(),
-                ctx->bin_valid.as<uint32_t>(), ctx->bin_mspan.as<uint32_t>(), st);
+                ctx->start.as<int32_t>(), ctx->bc.as<int32_t>(), ctx->flag.as<uint16_t>(), n, g, slice,
+                ctx->H.as<uint32_t>(), ctx->PG.as<uint32_t>(), ngroups, ctx->bin_start.as<uint32_t>(),
+                ctx->bin_valid.as<uint32_t>(), st);
             HIP_TRY(hipGetLastError());
-            k_run_stats<<<1, 1024, 0, s>>>(0, ctx->bin_mspan.as<uint32_t>(), g.nbins, nullptr, nullptr, 0, nullptr, 0,
-                                           st);
+            k_ingest_stats<<<1, 64, 0, s>>>(ctx->roff_irregular.as<uint32_t>(), st);
             HIP_TRY(hipGetLastError());
         }
         STAGE_END(ST_HIST);
@@ -2720,7 +2710,7 @@ int mgp_run(mgp_ctx* ctx) {
                                                      ctx->med_lo.as<uint32_t>(), ctx->med_hi.as<uint32_t>(),
                                                      ctx->passed.as<uint8_t>(), st);
         HIP_TRY(hipGetLastError());
-        k_run_stats<<<1, 1024, 0, s>>>(1, nullptr, 0, ctx->n_reads.as<uint32_t>(), ctx->passed.as<uint8_t>(), nc,
+        k_run_stats<<<1, 1024, 0, s>>>(ctx->n_reads.as<uint32_t>(), ctx->passed.as<uint8_t>(), nc,
                                        ctx->dup_part.as<unsigned long long>(), dup_parts, st);
         HIP_TRY(hipGetLastError());
         STAGE_END(ST_MEDIAN);
@@ -2935,13 +2925,15 @@ int mgp_synth_generate(mgp_ctx* ctx, const mgp_synth_params* p) {
         ref.release();
         return r;
     }
-    MGP_TRY(ctx->roff_irregular.ensure(4));
-    HIP_TRY(hipMemsetAsync(ctx->roff_irregular.p, 0, 4, s));
+    MGP_TRY(ctx->roff_irregular.ensure(8));
+    HIP_TRY(hipMemsetAsync(ctx->roff_irregular.p, 0, 8, s));
     ctx->roff_mode = -1;
     if (n)
         k_check_stride<<<blocks_for(n), kBlock, 0, s>>>(ctx->roff.as<uint64_t>(), ctx->flag.as<uint16_t>(),
                                                         ctx->start.as<int32_t>(), ctx->tlen.as<int32_t>(),
-                                                        ctx->cfg.mito_len, n, 0, ctx->roff_irregular.as<uint32_t>(),
+                                                        ctx->bc.as<int32_t>(), ctx->span.as<uint32_t>(),
+                                                        ctx->cfg.mito_len, ctx->cfg.n_cells, n, 0,
+                                                        ctx->roff_irregular.as<uint32_t>(),
                                                         ctx->roff32.as<uint32_t>());
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipStreamSynchronize(s));
