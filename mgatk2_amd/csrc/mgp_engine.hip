@@ -113,6 +113,8 @@ struct mgp_ctx {
     hipStream_t s_comp = nullptr, s_copy = nullptr;
     hipStream_t s_side = nullptr;  // the tally reduction, concurrent with the medians
     hipEvent_t ev_copy = nullptr, ev_fork = nullptr, ev_join = nullptr;
+    hipEvent_t ev_bits = nullptr;  // the run's input check words have reached h_bits
+    uint32_t* h_bits = nullptr;    // pinned host copy of the input check words (roff_irregular)
     static constexpr int kRing = 64;   // per-run event slots (timing over many runs without syncs)
     hipEvent_t ev[kRing][ST_N][2];
     bool stage_ran[kRing][ST_N]{};
@@ -126,9 +128,9 @@ struct mgp_ctx {
     int64_t n = 0, pay = 0;
     DevBuf start, bc, tlen, flag, mapq, span, roff, payload;
     DevBuf roff32;          // u32 rec_off >> 6 (grouping pass A reads it when every offset fits, kOffR32)
-    DevBuf roff_irregular;  // u32 bits: 1 some rec_off[i] != kRecStride * i, 2 some offset not in roff32's range
-    int roff_mode = -1;     // pass A's offset source (kOffDense / kOffR32 / kOffR64); -1 not read since the last push
-    uint32_t read_bits = 0; // the ingest check's CHK_* bits of the resident reads
+    DevBuf roff_irregular;  // u32 words of the input check (k_bin_count): CHK_* bits, largest kept span
+    int roff_mode = -1;     // pass A's offset source (kOffDense / kOffR32 / kOffR64), from the run's input check
+    uint32_t read_bits = 0; // the input check's CHK_* bits of the resident reads
 
     // run scratch
     DevBuf bin_start, H, P, cell_cnt, cell_base, bin_valid, bin_base, bucket_off, gel2, PG, F;
@@ -193,27 +195,48 @@ __device__ __forceinline__ void part_range(int64_t lo, int64_t hi, int p, int64_
 #ifndef MGP_HIST_BLOCK
 #define MGP_HIST_BLOCK 512
 #endif
+constexpr uint64_t kRecStride = MGP_PACK_BYTES;  // record stride of a dense packed payload
+constexpr uint32_t kCompactTlen = 1u << 16;       // |tlen| below this fits the compact grouping element
+// The input check's words (ck[0] bits, ck[1] the largest declared span of the reads
+// the run keeps at its filters: the pileup's window halo). Bit 1: some record offset
+// is not kRecStride x its read index (else the payload is dense and grouping pass A
+// computes the offsets); bit 2: some offset is not a multiple of 64 below 2^38 (else
+// pass A reads the u32 column roff32 = rec_off >> 6, written by the check).
+// CHK_PAIRED / CHK_UNPAIRED / CHK_NOSEQ: some read is paired / unpaired / lacks SEQ
+// or QUAL (pass B tracks pairedness and SEQ per read only when the reads mix or lack
+// them). CHK_FULL: some record is in the full layout. CHK_WIDEKEY: some start lies
+// outside [0, mito_len) or some |tlen| >= kCompactTlen (no compact grouping element).
+// CHK_UNSORTED: a start below its predecessor's (pysam's fetch order, readers.py:87-92).
+constexpr uint32_t CHK_PAIRED = 4u, CHK_UNPAIRED = 8u, CHK_NOSEQ = 16u, CHK_FULL = 32u, CHK_WIDEKEY = 64u,
+                   CHK_UNSORTED = 128u;
+
 // One workgroup (8 waves) per (start bin, cell slice): bin bounds by binary
-// search in the sorted starts (the coordinate order and the largest span are
-// checked at ingest, k_check_stride), flag/barcode filters (readers.py:95-111)
-// and the LDS histogram of the slice's cells over the bin's reads: 6 bytes read
-// per read. A slice is as many
-// 64-cell groups as the LDS holds (one slice up to ~24k cells; more cells scan
-// the bin once per slice). The bin's parts are counted one after the other;
-// after each part the per-64-cell-group totals are snapshotted, giving the
-// per-(bin, part, group) counts of pass A. Slice 0 writes the bin's bounds,
-// valid count and run checks.
+// search in the starts, flag/barcode filters (readers.py:95-111) and the LDS
+// histogram of the slice's cells over the bin's reads (6 bytes read per read). A
+// slice is as many 64-cell groups as the LDS holds (one slice up to ~24k cells;
+// more cells scan the bin once per slice). The bin's parts are counted one after
+// the other; after each part the per-64-cell-group totals are snapshotted, giving
+// the per-(bin, part, group) counts of pass A. Slice 0 writes the bin's bounds and
+// valid count, and runs the input check over the bin's reads (start, |tlen|, span
+// and record offset loaded with the same clamped indices; every read lies in
+// exactly one bin, so the bins' checks cover the resident set, the coordinate order
+// included: each read is compared with its predecessor).
 constexpr int kHistBlock = MGP_HIST_BLOCK;
 __global__ void __launch_bounds__(kHistBlock) k_bin_count(const int32_t* __restrict__ start,
                                                           const int32_t* __restrict__ bc,
-                                                          const uint16_t* __restrict__ flag, int64_t n, Geom g,
+                                                          const uint16_t* __restrict__ flag,
+                                                          const int32_t* __restrict__ tlen,
+                                                          const uint32_t* __restrict__ span,
+                                                          const uint64_t* __restrict__ roff, int64_t n, Geom g,
                                                           int slice_cells, uint32_t* __restrict__ H,
                                                           uint32_t* __restrict__ PG, int ngroups,
                                                           uint32_t* __restrict__ bin_lo,
-                                                          uint32_t* __restrict__ bin_valid, DevStats* st) {
+                                                          uint32_t* __restrict__ bin_valid,
+                                                          uint32_t* __restrict__ roff32, uint32_t* __restrict__ ck,
+                                                          DevStats* st) {
     extern __shared__ uint32_t hist[];  // [slice cells] counts, then cum[slice groups]
     __shared__ int64_t s_range[2];
-    __shared__ uint32_t s_nvalid;
+    __shared__ uint32_t s_nvalid, s_bits, s_msp;
     const int b = blockIdx.x;
     const bool first = blockIdx.y == 0;
     const int nc = g.nc;
@@ -225,7 +248,7 @@ __global__ void __launch_bounds__(kHistBlock) k_bin_count(const int32_t* __restr
     uint32_t* row = H + (size_t)b * nc;
     if (threadIdx.x < 2) s_range[threadIdx.x] = lower_bound_start(start, n, bin_threshold(b + threadIdx.x, g));
     for (int c = threadIdx.x; c < ncs; c += blockDim.x) hist[c] = 0;
-    if (threadIdx.x == 0) s_nvalid = 0;
+    if (threadIdx.x == 0) s_nvalid = 0, s_bits = 0, s_msp = 0;
     __syncthreads();
     const int64_t blo = s_range[0], bhi = max(s_range[1], blo);
     if (first && threadIdx.x == 0) {
@@ -234,6 +257,7 @@ __global__ void __launch_bounds__(kHistBlock) k_bin_count(const int32_t* __restr
     }
     unsigned long long nvalid = 0;
     bool badbc = false;
+    uint32_t bits = 0, msp = 0;  // the input check (slice 0)
     uint32_t* pg = PG + (size_t)b * kParts * ngroups;
     for (int part = 0; part < kParts; ++part) {
         int64_t lo, hi;
@@ -249,6 +273,38 @@ __global__ void __launch_bounds__(kHistBlock) k_bin_count(const int32_t* __restr
                 const int64_t j = i < hi ? i : hi - 1;
                 cc[u] = bc[j];
                 ff[u] = flag[j];
+            }
+            if (first) {
+                int ss[kU], sp[kU], tt[kU];
+                uint32_t vs[kU];
+                uint64_t rr[kU];
+#pragma unroll
+                for (int u = 0; u < kU; ++u) {
+                    const int64_t i = i0 + u * kHistBlock;
+                    const int64_t j = i < hi ? i : hi - 1;
+                    ss[u] = start[j];
+                    sp[u] = start[j > 0 ? j - 1 : 0];
+                    tt[u] = tlen[j];
+                    vs[u] = span[j];
+                    rr[u] = roff[j];
+                }
+#pragma unroll
+                for (int u = 0; u < kU; ++u) {
+                    const int64_t i = i0 + u * kHistBlock;
+                    if (i >= hi) continue;
+                    const uint64_t r = rr[u];
+                    const uint32_t f = ff[u];
+                    const int s0 = ss[u];
+                    const uint32_t at = tt[u] < 0 ? (uint32_t)(-(int64_t)tt[u]) : (uint32_t)tt[u];
+                    roff32[i] = (uint32_t)(r >> 6);
+                    bits |= (r != (uint64_t)i * kRecStride ? 1u : 0u) |
+                            ((r & 63ull) != 0ull || (r >> 38) != 0ull ? 2u : 0u) |
+                            (f & MGP_FLAG_PAIRED ? CHK_PAIRED : CHK_UNPAIRED) |
+                            (f & MGP_FLAG_NOSEQQUAL ? CHK_NOSEQ : 0u) | (f & MGP_FLAG_PACKED ? 0u : CHK_FULL) |
+                            (s0 < 0 || s0 >= g.L || at >= kCompactTlen ? CHK_WIDEKEY : 0u) |
+                            (i > 0 && s0 < sp[u] ? CHK_UNSORTED : 0u);
+                    if (read_valid(cc[u], (uint16_t)f, nc)) msp = max(msp, vs[u]);
+                }
             }
 #pragma unroll
             for (int u = 0; u < kU; ++u) {
@@ -280,14 +336,22 @@ __global__ void __launch_bounds__(kHistBlock) k_bin_count(const int32_t* __restr
     if (!first) return;
     nvalid = wave_sum(nvalid);
     const bool anybad = __ballot(badbc) != 0ull;
-    // the bin's valid count (a global atomic per wave on one word serialises at the
-    // memory side)
+    bits = wave_or(bits);
+    msp = wave_max(msp);
+    // the bin's valid count and check words (a global atomic per wave on one word
+    // serialises at the memory side: one per workgroup)
     if (lane == 0) {
         if (nvalid) atomicAdd(&s_nvalid, (uint32_t)nvalid);
+        if (bits) atomicOr(&s_bits, bits);
         if (anybad) atomicOr(&st->err, ERR_BADBC);
+        if (msp) atomicMax(&s_msp, msp);
     }
     __syncthreads();
-    if (threadIdx.x == 0) bin_valid[b] = s_nvalid;
+    if (threadIdx.x == 0) {
+        bin_valid[b] = s_nvalid;
+        if (s_bits && (__atomic_load_n(ck, __ATOMIC_RELAXED) & s_bits) != s_bits) atomicOr(ck, s_bits);
+        if (s_msp > __atomic_load_n(ck + 1, __ATOMIC_RELAXED)) atomicMax(ck + 1, s_msp);
+    }
 }
 
 // Scan step a: column sums over blocks of RB rows. grid (ceil(nc/256), nrb)
@@ -394,8 +458,7 @@ constexpr unsigned long long GM_REV = 1ull << 56, GM_PAIRED = 2ull << 56, GM_MAP
 // The 6-bit cell id inside the group rides in bits 50..55 of GElem.w between
 // the passes (record offsets stay below 2^50).
 constexpr unsigned long long GM_LCELL_SHIFT = 50, GM_LCELL = 63ull << GM_LCELL_SHIFT;
-constexpr uint64_t kRecStride = MGP_PACK_BYTES;  // record stride of a dense packed payload (k_check_stride)
-// where grouping pass A takes the record offsets from (k_check_stride at ingest):
+// where grouping pass A takes the record offsets from (the input check in k_bin_count):
 //   kOffDense  every offset is kRecStride x the read index: computed, nothing read
 //   kOffR32    every offset is a multiple of 64 below 2^38: the u32 column roff32 = rec_off >> 6
 //   kOffR64    otherwise: the u64 rec_off column
@@ -407,7 +470,7 @@ constexpr uint32_t PE_DUP = 0xFFFFFFFFu, PE_KEEP = 0xFFFFFFFEu, PE_PACKED = 0x80
 // Compact grouping element (8 bytes), used when every resident record is packed
 // at a 64-byte multiple below 2^37 (dense or u32 offsets), the reads do not mix
 // paired and unpaired ones and all have SEQ/QUAL, every start lies in
-// [0, mito_len) and every |tlen| < 2^16 (the ingest check's bits):
+// [0, mito_len) and every |tlen| < 2^16 (the input check's bits):
 //   low word   the pileup element of the read if it is kept: record offset / 64
 //              (bits 0..30) | PE_PACKED when MAPQ >= min_mapq; 0 in bit 31 otherwise
 //   high word  |tlen| (bits 0..15), start mod 256 (16..23), reverse (24), cell in
@@ -418,7 +481,6 @@ constexpr uint32_t PE_DUP = 0xFFFFFFFFu, PE_KEEP = 0xFFFFFFFEu, PE_PACKED = 0x80
 constexpr int GC_START_SHIFT = 16, GC_LCELL_SHIFT = 25;
 constexpr uint32_t GC_TLEN = 0xFFFFu, GC_START = 0xFFu << GC_START_SHIFT, GC_REV = 1u << 24,
                    GC_LCELL = 63u << GC_LCELL_SHIFT;
-constexpr uint32_t kCompactTlen = 1u << 16;  // |tlen| below this fits the compact element
 constexpr int kCompactBins = 32;             // start bins per pass-B step (compact elements)
 
 #ifndef MGP_GA_AHEAD
@@ -752,7 +814,7 @@ __device__ __forceinline__ uint32_t group_b_emit(const typename Tr::T& e, bool d
 }
 
 // Per-cell flags of pass B when the resident reads mix paired and unpaired ones,
-// or some read lacks SEQ/QUAL (kTrack; the ingest check's CHK_* bits): the cell
+// or some read lacks SEQ/QUAL (kTrack; the input check's CHK_* bits): the cell
 // has a kept paired read (processors.py:34) iff it has more kept reads (its
 // elements in the workgroup's bin range, the cbase advance, minus its
 // duplicates) than kept unpaired ones, both counted here into the workgroup's
@@ -1629,7 +1691,7 @@ struct Out16 {
 
 __device__ __forceinline__ uint32_t sat16(uint32_t v) { return v > 0xFFFFu ? 0xFFFFu : v; }
 
-// kPacked: every resident record is packed (the ingest check's CHK_FULL clear):
+// kPacked: every resident record is packed (the input check's CHK_FULL clear):
 // no full-layout path, and the records of a wave's next 64 queued reads are
 // loaded before the current 64 are piled (one batch of gathers in flight
 // behind the per-base work; the registers the full-layout path would hold pay
@@ -2149,60 +2211,11 @@ __global__ void k_add_u64(uint64_t* __restrict__ a, int64_t n, uint64_t add) {
     if (i < n) a[i] += add;
 }
 
-// Record placement check at ingest: *irregular stays 0 while every resident
-// record offset is kRecStride x its read index (a fully packed, dense payload);
-// grouping pass A then computes the offsets instead of reading them.
-// Also writes the compact u32 column roff32 = rec_off >> 6 and sets bit 2 when an
-// offset does not fit it (not a multiple of 64, or >= 2^38). The flag word sets
-// CHK_PAIRED / CHK_UNPAIRED / CHK_NOSEQ when some read is paired / unpaired /
-// lacks SEQ or QUAL (k_group_b tracks pairedness and SEQ per read only when the
-// reads mix or lack them).
-// CHK_FULL: some record is in the full layout; CHK_WIDEKEY: some start lies
-// outside [0, mito_len) or some |tlen| >= kCompactTlen (no compact grouping element).
-// CHK_UNSORTED: a start below its predecessor's (pysam's fetch order,
-// readers.py:87-92; the previous batch's last read included). Word 1 of the
-// ingest words receives the largest declared span of the reads the run keeps at
-// its filters (the pileup's window halo).
-constexpr uint32_t CHK_PAIRED = 4u, CHK_UNPAIRED = 8u, CHK_NOSEQ = 16u, CHK_FULL = 32u, CHK_WIDEKEY = 64u,
-                   CHK_UNSORTED = 128u;
-__global__ void k_check_stride(const uint64_t* __restrict__ roff, const uint16_t* __restrict__ flag,
-                               const int32_t* __restrict__ start_all, const int32_t* __restrict__ tlen,
-                               const int32_t* __restrict__ bc, const uint32_t* __restrict__ span, int mito_len,
-                               int n_cells, int64_t n, int64_t i0, uint32_t* irregular,
-                               uint32_t* __restrict__ roff32) {
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const int32_t* start = start_all + i0;
-    const uint64_t r = i < n ? roff[i] : 0ull;
-    const uint32_t f = i < n ? flag[i] : 0u;
-    const int32_t s0 = i < n ? start[i] : 0, t0 = i < n ? tlen[i] : 0;
-    const bool uns = i < n && i0 + i > 0 && s0 < start_all[i0 + i - 1];
-    const uint32_t sp = i < n && read_valid(bc[i], (uint16_t)f, n_cells) ? span[i] : 0u;
-    const uint32_t at = t0 < 0 ? (uint32_t)(-(int64_t)t0) : (uint32_t)t0;
-    if (i < n) roff32[i] = (uint32_t)(r >> 6);
-    const bool bad = i < n && r != (uint64_t)(i0 + i) * kRecStride;
-    const bool wide = i < n && ((r & 63ull) != 0ull || (r >> 38) != 0ull);
-    const unsigned long long b1 = __ballot(bad), b2 = __ballot(wide);
-    const unsigned long long b3 = __ballot(i < n && (f & MGP_FLAG_PAIRED)), b4 = __ballot(i < n && !(f & MGP_FLAG_PAIRED));
-    const unsigned long long b5 = __ballot(i < n && (f & MGP_FLAG_NOSEQQUAL));
-    const unsigned long long b6 = __ballot(i < n && !(f & MGP_FLAG_PACKED));
-    const unsigned long long b7 = __ballot(i < n && (s0 < 0 || s0 >= mito_len || at >= kCompactTlen));
-    const unsigned long long b8 = __ballot(uns);
-    const uint32_t bits = (b1 ? 1u : 0u) | (b2 ? 2u : 0u) | (b3 ? CHK_PAIRED : 0u) | (b4 ? CHK_UNPAIRED : 0u) |
-                          (b5 ? CHK_NOSEQ : 0u) | (b6 ? CHK_FULL : 0u) | (b7 ? CHK_WIDEKEY : 0u) |
-                          (b8 ? CHK_UNSORTED : 0u);
-    const uint32_t msp = wave_max(sp);
-    if ((threadIdx.x & 63) == 0 && msp > __atomic_load_n(irregular + 1, __ATOMIC_RELAXED)) atomicMax(irregular + 1, msp);
-    // one atomic per wave at most, and none once the bits are set (every wave of a
-    // paired payload has irregular offsets: 3M atomics on one word took 18 ms)
-    if (bits && (threadIdx.x & 63) == 0 && (__atomic_load_n(irregular, __ATOMIC_RELAXED) & bits) != bits)
-        atomicOr(irregular, bits);
-}
-
-// The run's view of the ingest checks: the pileup's halo span and the order check.
-__global__ void k_ingest_stats(const uint32_t* __restrict__ ingest, DevStats* st) {
+// The run's view of the input check: the pileup's halo span and the order check.
+__global__ void k_check_stats(const uint32_t* __restrict__ ck, DevStats* st) {
     if (threadIdx.x == 0) {
-        st->max_span = ingest[1];
-        if (ingest[0] & CHK_UNSORTED) atomicOr(&st->err, ERR_UNSORTED);
+        st->max_span = ck[1];
+        if (ck[0] & CHK_UNSORTED) atomicOr(&st->err, ERR_UNSORTED);
     }
 }
 
@@ -2317,6 +2330,9 @@ int mgp_open(const mgp_config* cfg, int hip_device, mgp_ctx** out) {
     HIP_TRY(hipEventCreateWithFlags(&ctx->ev_copy, hipEventDisableTiming));
     HIP_TRY(hipEventCreateWithFlags(&ctx->ev_fork, hipEventDisableTiming));
     HIP_TRY(hipEventCreateWithFlags(&ctx->ev_join, hipEventDisableTiming));
+    HIP_TRY(hipEventCreateWithFlags(&ctx->ev_bits, hipEventDisableTiming));
+    HIP_TRY(hipHostMalloc((void**)&ctx->h_bits, 8, hipHostMallocDefault));
+    MGP_TRY(ctx->roff_irregular.ensure(8));
     for (int r = 0; r < mgp_ctx::kRing; ++r)
         for (int s = 0; s < ST_N; ++s) {
             HIP_TRY(hipEventCreate(&ctx->ev[r][s][0]));
@@ -2363,6 +2379,8 @@ void mgp_close(mgp_ctx* ctx) {
     (void)hipEventDestroy(ctx->ev_copy);
     (void)hipEventDestroy(ctx->ev_fork);
     (void)hipEventDestroy(ctx->ev_join);
+    (void)hipEventDestroy(ctx->ev_bits);
+    if (ctx->h_bits) (void)hipHostFree(ctx->h_bits);
     (void)hipStreamDestroy(ctx->s_comp);
     (void)hipStreamDestroy(ctx->s_copy);
     (void)hipStreamDestroy(ctx->s_side);
@@ -2412,16 +2430,6 @@ int mgp_push_batch(mgp_ctx* ctx, const mgp_batch* b) {
         k_add_u64<<<blocks_for(nb), kBlock, 0, s>>>(ctx->roff.as<uint64_t>() + n0, nb, (uint64_t)pay0);
         HIP_TRY(hipGetLastError());
     }
-    MGP_TRY(ctx->roff_irregular.ensure(8));
-    if (n0 == 0) HIP_TRY(hipMemsetAsync(ctx->roff_irregular.p, 0, 8, s));
-    ctx->roff_mode = -1;
-    k_check_stride<<<blocks_for(nb), kBlock, 0, s>>>(ctx->roff.as<uint64_t>() + n0, ctx->flag.as<uint16_t>() + n0,
-                                                     ctx->start.as<int32_t>(), ctx->tlen.as<int32_t>() + n0,
-                                                     ctx->bc.as<int32_t>() + n0, ctx->span.as<uint32_t>() + n0,
-                                                     ctx->cfg.mito_len, ctx->cfg.n_cells, nb, n0,
-                                                     ctx->roff_irregular.as<uint32_t>(),
-                                                     ctx->roff32.as<uint32_t>() + n0);
-    HIP_TRY(hipGetLastError());
     HIP_TRY(hipEventRecord(ctx->ev_copy, s));
     ctx->n = n0 + nb;
     ctx->pay = pay0 + b->payload_bytes;
@@ -2506,20 +2514,6 @@ int mgp_run(mgp_ctx* ctx) {
     const int64_t n = ctx->n;
     const int nc = g.nc;
     hipStream_t s = ctx->s_comp;
-    if (ctx->roff_mode < 0 && n > 0) {  // the ingest placement check, read once per resident set
-        uint32_t irr = 3;
-        HIP_TRY(hipStreamSynchronize(ctx->s_copy));
-        HIP_TRY(hipMemcpy(&irr, ctx->roff_irregular.p, 4, hipMemcpyDeviceToHost));
-        ctx->roff_mode = !(irr & 1u) ? kOffDense : !(irr & 2u) ? kOffR32 : kOffR64;
-        ctx->read_bits = irr;
-    }
-    // the pileup element's record offset unit: 64 bytes, or 16 bytes when some
-    // record is not 64-byte aligned; either way a 31-bit count of units
-    const int unit = ctx->roff_mode == kOffR64 ? 4 : 6;
-    if (n > 0 && (uint64_t)ctx->pay >= ((uint64_t)(PE_KEEP & PE_OFF) << unit))
-        return set_err(MGP_E_INVALID, unit == 6 ? "payload larger than 128 GiB in one context; shard the cells"
-                                                : "payload with 16-byte aligned records larger than 32 GiB in one "
-                                                  "context; place records at 64-byte offsets or shard the cells");
     HIP_TRY(hipStreamWaitEvent(s, ctx->ev_copy, 0));
     const int slot = (int)(ctx->runs % mgp_ctx::kRing);
     for (int i = 0; i < ST_N; ++i) ctx->stage_ran[slot][i] = false;
@@ -2537,8 +2531,13 @@ int mgp_run(mgp_ctx* ctx) {
 
     if (nc > 0) {
         const int ngroups = (nc + kGroup - 1) / kGroup;
-        // 1. per (start bin, cell) histogram + per (bin, part, group) counts + bin bounds + order check
+        // 1. per (start bin, cell) histogram + per (bin, part, group) counts + bin bounds, and
+        // the input check over every resident read (k_bin_count): record placement, pairedness /
+        // SEQ mix, layout, key widths, coordinate order, largest kept span. The check's words
+        // travel to pinned host memory while the scan runs; the host picks the grouping and
+        // pileup variants from them below.
         STAGE_BEGIN(ST_HIST);
+        if (n > 0) HIP_TRY(hipMemsetAsync(ctx->roff_irregular.p, 0, 8, s));
         if (n == 0) HIP_TRY(hipMemsetAsync(ctx->H.p, 0, (size_t)(g.nbins + 1) * nc * 4, s));
         if (n == 0) HIP_TRY(hipMemsetAsync(ctx->bin_start.p, 0, (size_t)(g.nbins + 1) * 4, s));
         HIP_TRY(hipMemsetAsync(ctx->F.p, 0, (size_t)g.nbins * ((nc + 31) / 32) * 4, s));
@@ -2550,12 +2549,15 @@ int mgp_run(mgp_ctx* ctx) {
             const int nslices = (nc + slice - 1) / slice;
             const size_t lds = ((size_t)slice + (slice + kGroup - 1) / kGroup) * 4;
             k_bin_count<<<dim3((unsigned)g.nbins, (unsigned)nslices), kHistBlock, lds, s>>>(
-                ctx->start.as<int32_t>(), ctx->bc.as<int32_t>(), ctx->flag.as<uint16_t>(), n, g, slice,
-                ctx->H.as<uint32_t>(), ctx->PG.as<uint32_t>(), ngroups, ctx->bin_start.as<uint32_t>(),
-                ctx->bin_valid.as<uint32_t>(), st);
+                ctx->start.as<int32_t>(), ctx->bc.as<int32_t>(), ctx->flag.as<uint16_t>(), ctx->tlen.as<int32_t>(),
+                ctx->span.as<uint32_t>(), ctx->roff.as<uint64_t>(), n, g, slice, ctx->H.as<uint32_t>(),
+                ctx->PG.as<uint32_t>(), ngroups, ctx->bin_start.as<uint32_t>(), ctx->bin_valid.as<uint32_t>(),
+                ctx->roff32.as<uint32_t>(), ctx->roff_irregular.as<uint32_t>(), st);
             HIP_TRY(hipGetLastError());
-            k_ingest_stats<<<1, 64, 0, s>>>(ctx->roff_irregular.as<uint32_t>(), st);
+            k_check_stats<<<1, 64, 0, s>>>(ctx->roff_irregular.as<uint32_t>(), st);
             HIP_TRY(hipGetLastError());
+            HIP_TRY(hipMemcpyAsync(ctx->h_bits, ctx->roff_irregular.p, 8, hipMemcpyDeviceToHost, s));
+            HIP_TRY(hipEventRecord(ctx->ev_bits, s));
         }
         STAGE_END(ST_HIST);
 
@@ -2572,6 +2574,24 @@ int mgp_run(mgp_ctx* ctx) {
                                            RB, nrb, ctx->F.as<uint32_t>());
         HIP_TRY(hipGetLastError());
         STAGE_END(ST_SCAN);
+
+        // the input check's words (the GPU runs the scan meanwhile)
+        if (n > 0) {
+            HIP_TRY(hipEventSynchronize(ctx->ev_bits));
+            const uint32_t irr = ctx->h_bits[0];
+            ctx->roff_mode = !(irr & 1u) ? kOffDense : !(irr & 2u) ? kOffR32 : kOffR64;
+            ctx->read_bits = irr;
+        } else {
+            ctx->roff_mode = kOffR64;
+            ctx->read_bits = 0;
+        }
+        // the pileup element's record offset unit: 64 bytes, or 16 bytes when some
+        // record is not 64-byte aligned; either way a 31-bit count of units
+        const int unit = ctx->roff_mode == kOffR64 ? 4 : 6;
+        if (n > 0 && (uint64_t)ctx->pay >= ((uint64_t)(PE_KEEP & PE_OFF) << unit))
+            return set_err(MGP_E_INVALID, unit == 6 ? "payload larger than 128 GiB in one context; shard the cells"
+                                                    : "payload with 16-byte aligned records larger than 32 GiB in "
+                                                      "one context; place records at 64-byte offsets or shard the cells");
 
         // 3. stable grouping into cell-major order (two passes), duplicate marking in pass B;
         // 8-byte elements when the resident reads allow them (GCompact)
@@ -2925,17 +2945,6 @@ int mgp_synth_generate(mgp_ctx* ctx, const mgp_synth_params* p) {
         ref.release();
         return r;
     }
-    MGP_TRY(ctx->roff_irregular.ensure(8));
-    HIP_TRY(hipMemsetAsync(ctx->roff_irregular.p, 0, 8, s));
-    ctx->roff_mode = -1;
-    if (n)
-        k_check_stride<<<blocks_for(n), kBlock, 0, s>>>(ctx->roff.as<uint64_t>(), ctx->flag.as<uint16_t>(),
-                                                        ctx->start.as<int32_t>(), ctx->tlen.as<int32_t>(),
-                                                        ctx->bc.as<int32_t>(), ctx->span.as<uint32_t>(),
-                                                        ctx->cfg.mito_len, ctx->cfg.n_cells, n, 0,
-                                                        ctx->roff_irregular.as<uint32_t>(),
-                                                        ctx->roff32.as<uint32_t>());
-    HIP_TRY(hipGetLastError());
     HIP_TRY(hipStreamSynchronize(s));
     cdf.release();
     ref.release();

@@ -164,7 +164,7 @@ def test_packed_and_full_layouts_give_identical_results(engine_lib):
 @pytest.mark.parametrize("cuts", [(0, 40_000, 100_000, 150_000), (0, 40_001, 100_003, 150_000)])
 def test_dense_packed_payload_batches(engine_lib, oracle_lib, cuts):
     """A fully packed payload at a 64-byte stride lets grouping pass A compute
-    the record offsets (k_check_stride at ingest). Batches whose payload bases
+    the record offsets (the input check in k_bin_count). Batches whose payload bases
     keep the stride (first cut) stay dense; batches that break it (second cut:
     the 256-byte batch alignment moves the offsets) fall back to reading them.
     Both equal one push and the oracle."""
@@ -457,7 +457,7 @@ def test_full_size_invariants_and_cell_sample_c3(engine_lib, oracle_lib):
 
 # ---------------------------------------------------------------------------
 # payload placement (mgp_place_records): cell-paired lines; grouping pass A's
-# offset sources (dense index / u32 column / u64 column, k_check_stride)
+# offset sources (dense index / u32 column / u64 column, the input check in k_bin_count)
 # ---------------------------------------------------------------------------
 @pytest.mark.parametrize("cfgname", sorted(CONFIGS))
 def test_paired_placement_matches_oracle(engine_lib, oracle_lib, cfgname):
