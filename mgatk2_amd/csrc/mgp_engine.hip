@@ -131,6 +131,7 @@ struct mgp_ctx {
     DevBuf roff_irregular;  // u32 words of the input check (k_bin_count): CHK_* bits, largest kept span
     int roff_mode = -1;     // pass A's offset source (kOffDense / kOffR32 / kOffR64), from the run's input check
     uint32_t read_bits = 0; // the input check's CHK_* bits of the resident reads
+    bool no_spec = false;   // the speculative compact grouping failed on the resident reads (ERR_RESPEC)
 
     // run scratch
     DevBuf bin_start, H, P, cell_cnt, cell_base, bin_valid, bin_base, bucket_off, gel2, PG, F;
@@ -202,6 +203,12 @@ constexpr uint32_t kCompactTlen = 1u << 16;       // |tlen| below this fits the 
 // is not kRecStride x its read index (else the payload is dense and grouping pass A
 // computes the offsets); bit 2: some offset is not a multiple of 64 below 2^38 (else
 // pass A reads the u32 column roff32 = rec_off >> 6, written by the check).
+// Where the bits come from (mgp_run): the start-bin histogram takes the flag bits
+// (CHK_PAIRED, CHK_UNPAIRED, CHK_NOSEQ, CHK_FULL) from the flags it reads anyway.
+// When they allow compact grouping elements, grouping pass A checks the rest on the
+// reads it loads anyway (coordinate order, span, key widths, 64-byte offsets) and
+// raises ERR_RESPEC if an element does not fit: mgp_sync then runs the run again on
+// the fallback path, whose standalone check (k_check_inputs) takes every bit first.
 // CHK_PAIRED / CHK_UNPAIRED / CHK_NOSEQ: some read is paired / unpaired / lacks SEQ
 // or QUAL (pass B tracks pairedness and SEQ per read only when the reads mix or lack
 // them). CHK_FULL: some record is in the full layout. CHK_WIDEKEY: some start lies
@@ -217,26 +224,19 @@ constexpr uint32_t CHK_PAIRED = 4u, CHK_UNPAIRED = 8u, CHK_NOSEQ = 16u, CHK_FULL
 // more cells scan the bin once per slice). The bin's parts are counted one after
 // the other; after each part the per-64-cell-group totals are snapshotted, giving
 // the per-(bin, part, group) counts of pass A. Slice 0 writes the bin's bounds and
-// valid count, and runs the input check over the bin's reads (start, |tlen|, span
-// and record offset loaded with the same clamped indices; every read lies in
-// exactly one bin, so the bins' checks cover the resident set, the coordinate order
-// included: each read is compared with its predecessor).
+// valid count, and ORs the flag bits of the input check into ck[0].
 constexpr int kHistBlock = MGP_HIST_BLOCK;
 __global__ void __launch_bounds__(kHistBlock) k_bin_count(const int32_t* __restrict__ start,
                                                           const int32_t* __restrict__ bc,
-                                                          const uint16_t* __restrict__ flag,
-                                                          const int32_t* __restrict__ tlen,
-                                                          const uint32_t* __restrict__ span,
-                                                          const uint64_t* __restrict__ roff, int64_t n, Geom g,
+                                                          const uint16_t* __restrict__ flag, int64_t n, Geom g,
                                                           int slice_cells, uint32_t* __restrict__ H,
                                                           uint32_t* __restrict__ PG, int ngroups,
                                                           uint32_t* __restrict__ bin_lo,
-                                                          uint32_t* __restrict__ bin_valid,
-                                                          uint32_t* __restrict__ roff32, uint32_t* __restrict__ ck,
+                                                          uint32_t* __restrict__ bin_valid, uint32_t* __restrict__ ck,
                                                           DevStats* st) {
     extern __shared__ uint32_t hist[];  // [slice cells] counts, then cum[slice groups]
     __shared__ int64_t s_range[2];
-    __shared__ uint32_t s_nvalid, s_bits, s_msp;
+    __shared__ uint32_t s_nvalid, s_bits;
     const int b = blockIdx.x;
     const bool first = blockIdx.y == 0;
     const int nc = g.nc;
@@ -248,7 +248,7 @@ __global__ void __launch_bounds__(kHistBlock) k_bin_count(const int32_t* __restr
     uint32_t* row = H + (size_t)b * nc;
     if (threadIdx.x < 2) s_range[threadIdx.x] = lower_bound_start(start, n, bin_threshold(b + threadIdx.x, g));
     for (int c = threadIdx.x; c < ncs; c += blockDim.x) hist[c] = 0;
-    if (threadIdx.x == 0) s_nvalid = 0, s_bits = 0, s_msp = 0;
+    if (threadIdx.x == 0) s_nvalid = 0, s_bits = 0;
     __syncthreads();
     const int64_t blo = s_range[0], bhi = max(s_range[1], blo);
     if (first && threadIdx.x == 0) {
@@ -257,7 +257,7 @@ __global__ void __launch_bounds__(kHistBlock) k_bin_count(const int32_t* __restr
     }
     unsigned long long nvalid = 0;
     bool badbc = false;
-    uint32_t bits = 0, msp = 0;  // the input check (slice 0)
+    uint32_t bits = 0;  // the input check's flag bits (slice 0)
     uint32_t* pg = PG + (size_t)b * kParts * ngroups;
     for (int part = 0; part < kParts; ++part) {
         int64_t lo, hi;
@@ -274,37 +274,12 @@ __global__ void __launch_bounds__(kHistBlock) k_bin_count(const int32_t* __restr
                 cc[u] = bc[j];
                 ff[u] = flag[j];
             }
-            if (first) {
-                int ss[kU], sp[kU], tt[kU];
-                uint32_t vs[kU];
-                uint64_t rr[kU];
 #pragma unroll
-                for (int u = 0; u < kU; ++u) {
-                    const int64_t i = i0 + u * kHistBlock;
-                    const int64_t j = i < hi ? i : hi - 1;
-                    ss[u] = start[j];
-                    sp[u] = start[j > 0 ? j - 1 : 0];
-                    tt[u] = tlen[j];
-                    vs[u] = span[j];
-                    rr[u] = roff[j];
-                }
-#pragma unroll
-                for (int u = 0; u < kU; ++u) {
-                    const int64_t i = i0 + u * kHistBlock;
-                    if (i >= hi) continue;
-                    const uint64_t r = rr[u];
-                    const uint32_t f = ff[u];
-                    const int s0 = ss[u];
-                    const uint32_t at = tt[u] < 0 ? (uint32_t)(-(int64_t)tt[u]) : (uint32_t)tt[u];
-                    roff32[i] = (uint32_t)(r >> 6);
-                    bits |= (r != (uint64_t)i * kRecStride ? 1u : 0u) |
-                            ((r & 63ull) != 0ull || (r >> 38) != 0ull ? 2u : 0u) |
-                            (f & MGP_FLAG_PAIRED ? CHK_PAIRED : CHK_UNPAIRED) |
-                            (f & MGP_FLAG_NOSEQQUAL ? CHK_NOSEQ : 0u) | (f & MGP_FLAG_PACKED ? 0u : CHK_FULL) |
-                            (s0 < 0 || s0 >= g.L || at >= kCompactTlen ? CHK_WIDEKEY : 0u) |
-                            (i > 0 && s0 < sp[u] ? CHK_UNSORTED : 0u);
-                    if (read_valid(cc[u], (uint16_t)f, nc)) msp = max(msp, vs[u]);
-                }
+            for (int u = 0; u < kU; ++u) {
+                const uint32_t f = ff[u];
+                if (i0 + u * kHistBlock < hi)
+                    bits |= (f & MGP_FLAG_PAIRED ? CHK_PAIRED : CHK_UNPAIRED) |
+                            (f & MGP_FLAG_NOSEQQUAL ? CHK_NOSEQ : 0u) | (f & MGP_FLAG_PACKED ? 0u : CHK_FULL);
             }
 #pragma unroll
             for (int u = 0; u < kU; ++u) {
@@ -337,20 +312,17 @@ __global__ void __launch_bounds__(kHistBlock) k_bin_count(const int32_t* __restr
     nvalid = wave_sum(nvalid);
     const bool anybad = __ballot(badbc) != 0ull;
     bits = wave_or(bits);
-    msp = wave_max(msp);
     // the bin's valid count and check words (a global atomic per wave on one word
     // serialises at the memory side: one per workgroup)
     if (lane == 0) {
         if (nvalid) atomicAdd(&s_nvalid, (uint32_t)nvalid);
         if (bits) atomicOr(&s_bits, bits);
         if (anybad) atomicOr(&st->err, ERR_BADBC);
-        if (msp) atomicMax(&s_msp, msp);
     }
     __syncthreads();
     if (threadIdx.x == 0) {
         bin_valid[b] = s_nvalid;
         if (s_bits && (__atomic_load_n(ck, __ATOMIC_RELAXED) & s_bits) != s_bits) atomicOr(ck, s_bits);
-        if (s_msp > __atomic_load_n(ck + 1, __ATOMIC_RELAXED)) atomicMax(ck + 1, s_msp);
     }
 }
 
@@ -462,7 +434,9 @@ constexpr unsigned long long GM_LCELL_SHIFT = 50, GM_LCELL = 63ull << GM_LCELL_S
 //   kOffDense  every offset is kRecStride x the read index: computed, nothing read
 //   kOffR32    every offset is a multiple of 64 below 2^38: the u32 column roff32 = rec_off >> 6
 //   kOffR64    otherwise: the u64 rec_off column
-enum { kOffDense = 0, kOffR32 = 1, kOffR64 = 2 };
+//   kOffSpec   the u64 column, with the input check's remaining tests on the loaded
+//              reads (compact elements only; a read that does not fit raises ERR_RESPEC)
+enum { kOffDense = 0, kOffR32 = 1, kOffR64 = 2, kOffSpec = 3 };
 
 // Pileup element values (see k_group_b)
 constexpr uint32_t PE_DUP = 0xFFFFFFFFu, PE_KEEP = 0xFFFFFFFEu, PE_PACKED = 0x80000000u, PE_OFF = 0x7FFFFFFFu;
@@ -506,12 +480,16 @@ __global__ void __launch_bounds__(kGABlock, MGP_GA_WAVES) k_group_a(int64_t n, c
                                                     const uint16_t* __restrict__ flag, const uint8_t* __restrict__ mapq,
                                                     const uint64_t* __restrict__ roff,
                                                     const uint32_t* __restrict__ roff32,
+                                                    const uint32_t* __restrict__ span,
                                                     const uint32_t* __restrict__ bin_lo,
                                                     const uint32_t* __restrict__ PG, const uint32_t* __restrict__ F,
                                                     const uint32_t* __restrict__ binbase,
                                                     Geom g, int ngroups, int gbits, int min_mapq,
                                                     uint32_t* __restrict__ bucket_off, GElem* __restrict__ gel2,
-                                                    uint32_t* __restrict__ first_read, DevStats* st) {
+                                                    uint32_t* __restrict__ first_read, uint32_t* __restrict__ ck,
+                                                    DevStats* st) {
+    static_assert(kOff != kOffSpec || kCompact, "the speculative check writes compact elements");
+    constexpr bool kSpec = kOff == kOffSpec;
     extern __shared__ uint32_t sm[];
     uint32_t* gcnt = sm;             // [ngroups] next free slot of each bucket (this part)
     uint32_t* fbits = sm + ngroups;  // [ceil(nc/32)] cell's first read is in this bin
@@ -564,7 +542,7 @@ __global__ void __launch_bounds__(kGABlock, MGP_GA_WAVES) k_group_a(int64_t n, c
     constexpr int kStep = kAhead * kGABlock;
     // per read: barcode, start, tlen, flag | mapq << 16 and the record offset
     // (its 64-byte unit or read index for the dense / u32 sources: 32 bits)
-    using OffT = typename std::conditional<kOff == kOffR64, uint64_t, uint32_t>::type;
+    using OffT = typename std::conditional<kOff == kOffR64 || kSpec, uint64_t, uint32_t>::type;
     struct Pre {
         int c[kAhead], s[kAhead], t[kAhead];
         uint32_t fm[kAhead];
@@ -592,7 +570,25 @@ __global__ void __launch_bounds__(kGABlock, MGP_GA_WAVES) k_group_a(int64_t n, c
     // consecutive slot ranges after the bucket's cursor, in wave order = BAM order.
     // Two barriers per step, no wave waits for another's ranking.
     int set = 0;
+    // the speculative check (kSpec): coordinate order over every read; span, key
+    // widths and 64-byte offsets over the valid reads (the ones pass A stores)
+    bool ck_uns = false, ck_bad = false;
+    uint32_t ck_span = 0;
     auto process = [&](const Pre& P, int64_t base0) {
+        // the check's extra loads go out first and land behind the ranking: the span,
+        // and the start before the wave's run (a read's predecessor is the lane below,
+        // or lane 63 of the previous slot)
+        uint32_t spn[kSpec ? kAhead : 1];
+        int prev0 = 0;
+        if constexpr (kSpec) {
+#pragma unroll
+            for (int u = 0; u < kAhead; ++u) {
+                const int64_t i = base0 + wid * (kAhead * kWave) + u * kWave + lane;
+                spn[u] = span[i < hi ? i : hi - 1];
+            }
+            const int64_t i0 = base0 + wid * (kAhead * kWave);
+            prev0 = start[i0 > 0 ? (i0 <= hi ? i0 - 1 : hi - 1) : 0];
+        }
         uint32_t* my = wc + ((size_t)set * (kGABlock / kWave) + wid) * ngroups;
         for (int x = lane; x < ngroups; x += kWave) my[x] = 0;
         __builtin_amdgcn_wave_barrier();
@@ -625,6 +621,26 @@ __global__ void __launch_bounds__(kGABlock, MGP_GA_WAVES) k_group_a(int64_t n, c
 #pragma unroll
             for (int u = 0; u < kAhead; ++u) rk[u] = 0;
         }
+        bool fit[kAhead];
+#pragma unroll
+        for (int u = 0; u < kAhead; ++u) {
+            fit[u] = true;
+            if constexpr (kSpec) {
+                const int64_t i = base0 + wid * (kAhead * kWave) + u * kWave + lane;
+                const int t = P.t[u];
+                const uint32_t at = t < 0 ? (uint32_t)(-(int64_t)t) : (uint32_t)t;
+                // the previous read's start: DPP wave_shr:1 (lane - 1), lane 0 from the slot before
+                const int below = __builtin_amdgcn_update_dpp(0, P.s[u], 0x138, 0xf, 0xf, false);
+                const int first = u ? __builtin_amdgcn_readlane(P.s[u > 0 ? u - 1 : 0], kWave - 1) : prev0;
+                const int pv = lane ? below : first;
+                ck_uns |= i < hi && i > 0 && P.s[u] < pv;
+                fit[u] = (P.o[u] & 63ull) == 0ull && P.s[u] >= 0 && P.s[u] < g.L && at < kCompactTlen;
+                if (valid[u]) {
+                    ck_span = max(ck_span, spn[u]);
+                    ck_bad |= !fit[u];
+                }
+            }
+        }
         __syncthreads();
         for (int gi = threadIdx.x; gi < ngroups; gi += kGABlock) {
             uint32_t run = gcnt[gi];
@@ -654,8 +670,10 @@ __global__ void __launch_bounds__(kGABlock, MGP_GA_WAVES) k_group_a(int64_t n, c
             if ((int64_t)dest >= n) {  // never: counts and slots come from one histogram
                 atomicOr(&st->err, ERR_OVERFLOW);
             } else if constexpr (kCompact) {
-                // the record's 64-byte unit (dense: the read index; u32 column: rec_off >> 6)
-                const uint32_t lo = (uint32_t)P.o[u] | (mq ? PE_PACKED : 0u);
+                // the record's 64-byte unit (dense: the read index; u32 column: rec_off >> 6);
+                // a read that does not fit (kSpec) piles nothing: the run is redone
+                const uint32_t unit64 = kSpec ? (uint32_t)(P.o[u] >> 6) : (uint32_t)P.o[u];
+                const uint32_t lo = fit[u] ? unit64 | (mq ? PE_PACKED : 0u) : 0u;
                 const uint32_t hi = at | ((uint32_t)(P.s[u] & 255) << GC_START_SHIFT) |
                                     (f & MGP_FLAG_REVERSE ? GC_REV : 0u) |
                                     ((uint32_t)(P.c[u] & (kGroup - 1)) << GC_LCELL_SHIFT);
@@ -691,6 +709,15 @@ __global__ void __launch_bounds__(kGABlock, MGP_GA_WAVES) k_group_a(int64_t n, c
         process(A, base0);
     }
 #endif
+    if constexpr (kSpec) {
+        const bool uns = __ballot(ck_uns) != 0ull, bad = __ballot(ck_bad) != 0ull;
+        const uint32_t sp = wave_max(ck_span);
+        if (lane == 0) {
+            if (uns) atomicOr(ck, CHK_UNSORTED);
+            if (bad) atomicOr(&st->err, ERR_RESPEC);
+            if (sp > __atomic_load_n(ck + 1, __ATOMIC_RELAXED)) atomicMax(ck + 1, sp);
+        }
+    }
 }
 
 // Pass B: workgroup = (cell group, bin range). A step takes the group's buckets
@@ -2212,6 +2239,36 @@ __global__ void k_add_u64(uint64_t* __restrict__ a, int64_t n, uint64_t add) {
 }
 
 // The run's view of the input check: the pileup's halo span and the order check.
+// The standalone input check (the fallback path of mgp_run): every bit and the span
+// over all resident reads, and the u32 offset column roff32 = rec_off >> 6.
+__global__ void k_check_inputs(const uint64_t* __restrict__ roff, const uint16_t* __restrict__ flag,
+                               const int32_t* __restrict__ start, const int32_t* __restrict__ tlen,
+                               const int32_t* __restrict__ bc, const uint32_t* __restrict__ span, int mito_len,
+                               int n_cells, int64_t n, uint32_t* __restrict__ ck, uint32_t* __restrict__ roff32) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const bool in = i < n;
+    const uint64_t r = in ? roff[i] : 0ull;
+    const uint32_t f = in ? flag[i] : 0u;
+    const int32_t s0 = in ? start[i] : 0, t0 = in ? tlen[i] : 0;
+    const bool uns = in && i > 0 && s0 < start[i - 1];
+    const uint32_t sp = in && read_valid(bc[i], (uint16_t)f, n_cells) ? span[i] : 0u;
+    const uint32_t at = t0 < 0 ? (uint32_t)(-(int64_t)t0) : (uint32_t)t0;
+    if (in) roff32[i] = (uint32_t)(r >> 6);
+    uint32_t bits = 0;
+    if (in)
+        bits = (r != (uint64_t)i * kRecStride ? 1u : 0u) | ((r & 63ull) != 0ull || (r >> 38) != 0ull ? 2u : 0u) |
+               (f & MGP_FLAG_PAIRED ? CHK_PAIRED : CHK_UNPAIRED) | (f & MGP_FLAG_NOSEQQUAL ? CHK_NOSEQ : 0u) |
+               (f & MGP_FLAG_PACKED ? 0u : CHK_FULL) |
+               (s0 < 0 || s0 >= mito_len || at >= kCompactTlen ? CHK_WIDEKEY : 0u) | (uns ? CHK_UNSORTED : 0u);
+    bits = wave_or(bits);
+    const uint32_t msp = wave_max(sp);
+    // one atomic per wave at most, and none once the bits are set
+    if ((threadIdx.x & 63) == 0) {
+        if (msp > __atomic_load_n(ck + 1, __ATOMIC_RELAXED)) atomicMax(ck + 1, msp);
+        if (bits && (__atomic_load_n(ck, __ATOMIC_RELAXED) & bits) != bits) atomicOr(ck, bits);
+    }
+}
+
 __global__ void k_check_stats(const uint32_t* __restrict__ ck, DevStats* st) {
     if (threadIdx.x == 0) {
         st->max_span = ck[1];
@@ -2315,6 +2372,8 @@ int mgp_open(const mgp_config* cfg, int hip_device, mgp_ctx** out) {
         (void)hipFuncSetAttribute((const void*)k_group_a<kOffDense, true>,
                                   hipFuncAttributeMaxDynamicSharedMemorySize, lds_max);
         (void)hipFuncSetAttribute((const void*)k_group_a<kOffR32, true>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, lds_max);
+        (void)hipFuncSetAttribute((const void*)k_group_a<kOffSpec, true>,
                                   hipFuncAttributeMaxDynamicSharedMemorySize, lds_max);
         (void)hipFuncSetAttribute((const void*)k_pileup<false>, hipFuncAttributeMaxDynamicSharedMemorySize, lds_max);
         (void)hipFuncSetAttribute((const void*)k_pileup<true>, hipFuncAttributeMaxDynamicSharedMemorySize, lds_max);
@@ -2434,6 +2493,7 @@ int mgp_push_batch(mgp_ctx* ctx, const mgp_batch* b) {
     ctx->n = n0 + nb;
     ctx->pay = pay0 + b->payload_bytes;
     ctx->ran = false;
+    ctx->no_spec = false;
     return MGP_OK;
 }
 
@@ -2445,6 +2505,7 @@ int mgp_reset(mgp_ctx* ctx) {
     ctx->n = 0;
     ctx->pay = 0;
     ctx->ran = false;
+    ctx->no_spec = false;
     return MGP_OK;
 }
 
@@ -2532,10 +2593,9 @@ int mgp_run(mgp_ctx* ctx) {
     if (nc > 0) {
         const int ngroups = (nc + kGroup - 1) / kGroup;
         // 1. per (start bin, cell) histogram + per (bin, part, group) counts + bin bounds, and
-        // the input check over every resident read (k_bin_count): record placement, pairedness /
-        // SEQ mix, layout, key widths, coordinate order, largest kept span. The check's words
-        // travel to pinned host memory while the scan runs; the host picks the grouping and
-        // pileup variants from them below.
+        // the flag bits of the input check (pairedness / SEQ mix, record layout). They travel
+        // to pinned host memory while the scan runs; the host picks the grouping and pileup
+        // variants from them below.
         STAGE_BEGIN(ST_HIST);
         if (n > 0) HIP_TRY(hipMemsetAsync(ctx->roff_irregular.p, 0, 8, s));
         if (n == 0) HIP_TRY(hipMemsetAsync(ctx->H.p, 0, (size_t)(g.nbins + 1) * nc * 4, s));
@@ -2549,12 +2609,9 @@ int mgp_run(mgp_ctx* ctx) {
             const int nslices = (nc + slice - 1) / slice;
             const size_t lds = ((size_t)slice + (slice + kGroup - 1) / kGroup) * 4;
             k_bin_count<<<dim3((unsigned)g.nbins, (unsigned)nslices), kHistBlock, lds, s>>>(
-                ctx->start.as<int32_t>(), ctx->bc.as<int32_t>(), ctx->flag.as<uint16_t>(), ctx->tlen.as<int32_t>(),
-                ctx->span.as<uint32_t>(), ctx->roff.as<uint64_t>(), n, g, slice, ctx->H.as<uint32_t>(),
-                ctx->PG.as<uint32_t>(), ngroups, ctx->bin_start.as<uint32_t>(), ctx->bin_valid.as<uint32_t>(),
-                ctx->roff32.as<uint32_t>(), ctx->roff_irregular.as<uint32_t>(), st);
-            HIP_TRY(hipGetLastError());
-            k_check_stats<<<1, 64, 0, s>>>(ctx->roff_irregular.as<uint32_t>(), st);
+                ctx->start.as<int32_t>(), ctx->bc.as<int32_t>(), ctx->flag.as<uint16_t>(), n, g, slice,
+                ctx->H.as<uint32_t>(), ctx->PG.as<uint32_t>(), ngroups, ctx->bin_start.as<uint32_t>(),
+                ctx->bin_valid.as<uint32_t>(), ctx->roff_irregular.as<uint32_t>(), st);
             HIP_TRY(hipGetLastError());
             HIP_TRY(hipMemcpyAsync(ctx->h_bits, ctx->roff_irregular.p, 8, hipMemcpyDeviceToHost, s));
             HIP_TRY(hipEventRecord(ctx->ev_bits, s));
@@ -2575,19 +2632,40 @@ int mgp_run(mgp_ctx* ctx) {
         HIP_TRY(hipGetLastError());
         STAGE_END(ST_SCAN);
 
-        // the input check's words (the GPU runs the scan meanwhile)
+        // The input check's flag bits (the GPU runs the scan meanwhile). When they allow
+        // compact grouping elements, pass A checks the rest on the reads it loads (kOffSpec);
+        // otherwise, or once that failed on the resident reads (no_spec, ERR_RESPEC), the
+        // standalone check takes every bit first (k_check_inputs, then a host wait).
+        STAGE_BEGIN(ST_GROUP_A);
+        int unit = 6;  // the pileup element's record offset unit: 64 bytes, or 16 bytes when
+                       // some record is not 64-byte aligned; either way a 31-bit count of units
+        bool spec = false, track = false;
+        ctx->roff_mode = kOffR64;
+        ctx->read_bits = 0;
         if (n > 0) {
             HIP_TRY(hipEventSynchronize(ctx->ev_bits));
-            const uint32_t irr = ctx->h_bits[0];
-            ctx->roff_mode = !(irr & 1u) ? kOffDense : !(irr & 2u) ? kOffR32 : kOffR64;
-            ctx->read_bits = irr;
-        } else {
-            ctx->roff_mode = kOffR64;
-            ctx->read_bits = 0;
+            const uint32_t fb = ctx->h_bits[0];
+            track = ((fb & CHK_PAIRED) && (fb & CHK_UNPAIRED)) || (fb & CHK_NOSEQ);
+            spec = !ctx->no_spec && !ctx->group_wide && !track && !(fb & CHK_FULL) &&
+                   (uint64_t)ctx->pay < ((uint64_t)(PE_KEEP & PE_OFF) << 6);
+            if (spec) {
+                ctx->roff_mode = kOffSpec;
+                ctx->read_bits = fb;
+            } else {
+                k_check_inputs<<<blocks_for(n), kBlock, 0, s>>>(
+                    ctx->roff.as<uint64_t>(), ctx->flag.as<uint16_t>(), ctx->start.as<int32_t>(),
+                    ctx->tlen.as<int32_t>(), ctx->bc.as<int32_t>(), ctx->span.as<uint32_t>(), ctx->cfg.mito_len,
+                    ctx->cfg.n_cells, n, ctx->roff_irregular.as<uint32_t>(), ctx->roff32.as<uint32_t>());
+                HIP_TRY(hipGetLastError());
+                HIP_TRY(hipMemcpyAsync(ctx->h_bits, ctx->roff_irregular.p, 8, hipMemcpyDeviceToHost, s));
+                HIP_TRY(hipEventRecord(ctx->ev_bits, s));
+                HIP_TRY(hipEventSynchronize(ctx->ev_bits));
+                const uint32_t irr = ctx->h_bits[0];
+                ctx->roff_mode = !(irr & 1u) ? kOffDense : !(irr & 2u) ? kOffR32 : kOffR64;
+                ctx->read_bits = irr;
+                unit = ctx->roff_mode == kOffR64 ? 4 : 6;
+            }
         }
-        // the pileup element's record offset unit: 64 bytes, or 16 bytes when some
-        // record is not 64-byte aligned; either way a 31-bit count of units
-        const int unit = ctx->roff_mode == kOffR64 ? 4 : 6;
         if (n > 0 && (uint64_t)ctx->pay >= ((uint64_t)(PE_KEEP & PE_OFF) << unit))
             return set_err(MGP_E_INVALID, unit == 6 ? "payload larger than 128 GiB in one context; shard the cells"
                                                     : "payload with 16-byte aligned records larger than 32 GiB in "
@@ -2596,10 +2674,8 @@ int mgp_run(mgp_ctx* ctx) {
         // 3. stable grouping into cell-major order (two passes), duplicate marking in pass B;
         // 8-byte elements when the resident reads allow them (GCompact)
         const uint32_t rbits = ctx->read_bits;
-        const bool track = ((rbits & CHK_PAIRED) && (rbits & CHK_UNPAIRED)) || (rbits & CHK_NOSEQ);
-        const bool compact = !ctx->group_wide && ctx->roff_mode != kOffR64 && unit == 6 && !track &&
-                             !(rbits & (CHK_FULL | CHK_WIDEKEY));
-        STAGE_BEGIN(ST_GROUP_A);
+        const bool compact = spec || (!ctx->group_wide && ctx->roff_mode != kOffR64 && unit == 6 && !track &&
+                                      !(rbits & (CHK_FULL | CHK_WIDEKEY)));
         if (n > 0) {
             int gbits = 0;
             while (gbits < 31 && (1 << gbits) < ngroups) ++gbits;
@@ -2614,11 +2690,14 @@ int mgp_run(mgp_ctx* ctx) {
                 kern<<<ga, kGABlock, a_lds, s>>>(
                     n, ctx->start.as<int32_t>(), ctx->bc.as<int32_t>(), ctx->tlen.as<int32_t>(),
                     ctx->flag.as<uint16_t>(), ctx->mapq.as<uint8_t>(), ctx->roff.as<uint64_t>(),
-                    ctx->roff32.as<uint32_t>(), ctx->bin_start.as<uint32_t>(), ctx->PG.as<uint32_t>(),
-                    ctx->F.as<uint32_t>(), ctx->bin_base.as<uint32_t>(), g, ngroups, gbits, ctx->cfg.min_mapq,
-                    ctx->bucket_off.as<uint32_t>(), ctx->gel2.as<GElem>(), ctx->first_read.as<uint32_t>(), st);
+                    ctx->roff32.as<uint32_t>(), ctx->span.as<uint32_t>(), ctx->bin_start.as<uint32_t>(),
+                    ctx->PG.as<uint32_t>(), ctx->F.as<uint32_t>(), ctx->bin_base.as<uint32_t>(), g, ngroups, gbits,
+                    ctx->cfg.min_mapq, ctx->bucket_off.as<uint32_t>(), ctx->gel2.as<GElem>(),
+                    ctx->first_read.as<uint32_t>(), ctx->roff_irregular.as<uint32_t>(), st);
             };
-            if (compact) {
+            if (spec) {
+                launch_a(k_group_a<kOffSpec, true>);
+            } else if (compact) {
                 if (ctx->roff_mode == kOffDense) launch_a(k_group_a<kOffDense, true>);
                 else launch_a(k_group_a<kOffR32, true>);
             } else if (ctx->roff_mode == kOffDense) {
@@ -2628,6 +2707,9 @@ int mgp_run(mgp_ctx* ctx) {
             } else {
                 launch_a(k_group_a<kOffR64, false>);
             }
+            HIP_TRY(hipGetLastError());
+            // the check's span and order bits into the run's stats (the pileup's halo)
+            k_check_stats<<<1, 64, 0, s>>>(ctx->roff_irregular.as<uint32_t>(), st);
             HIP_TRY(hipGetLastError());
         }
         STAGE_END(ST_GROUP_A);
@@ -2759,6 +2841,12 @@ int mgp_sync(mgp_ctx* ctx) {
     HIP_TRY(hipSetDevice(ctx->dev));
     HIP_TRY(hipStreamSynchronize(ctx->s_comp));
     const uint32_t e = ctx->host_stats.err;
+    if ((e & ERR_RESPEC) && !ctx->no_spec) {  // a read did not fit the compact grouping: run again
+        ctx->no_spec = true;
+        MGP_TRY(mgp_run(ctx));
+        return mgp_sync(ctx);
+    }
+    if (e & ERR_RESPEC) return set_err(MGP_E_STATE, "speculative grouping failed on the fallback path");
     if (e & ERR_UNSORTED) return set_err(MGP_E_UNSORTED, "records are not in coordinate order");
     if (e & ERR_BADBC) return set_err(MGP_E_INVALID, "barcode index >= n_cells");
     if (e & ERR_OVERFLOW) return set_err(MGP_E_INVALID, "inconsistent grouping (unsorted input?)");
@@ -2952,6 +3040,7 @@ int mgp_synth_generate(mgp_ctx* ctx, const mgp_synth_params* p) {
     ctx->n = n;
     ctx->pay = pay;
     ctx->ran = false;
+    ctx->no_spec = false;
     return MGP_OK;
 }
 

@@ -15,6 +15,7 @@ constexpr uint32_t ERR_SPAN = 4u;       // CIGAR reach larger than declared span
 constexpr uint32_t ERR_BADBC = 8u;      // bc >= n_cells
 constexpr uint32_t ERR_OVERFLOW = 16u;  // scatter destination outside its cell segment
 constexpr uint32_t ERR_PACKED = 32u;    // MGP_FLAG_PACKED record outside the packed layout's limits
+constexpr uint32_t ERR_RESPEC = 64u;    // a read does not fit the speculative compact grouping (mgp_sync reruns)
 
 // Counters written by the kernels of one run (zeroed at run start).
 struct DevStats {

@@ -568,3 +568,28 @@ def test_compact_starts_256_apart_are_not_duplicates(engine_lib, oracle_lib, mon
         assert_same(b, exp, f"wide {mode}")
         if mode != "none":
             assert exp.stats["duplicate_reads_with_length"] == 14
+
+
+def test_speculative_compact_falls_back(engine_lib, oracle_lib):
+    """Grouping pass A checks key widths and offsets on the reads it loads while it
+    writes compact elements; a valid read with |tlen| >= 2^16, or one start past
+    mito_len, raises ERR_RESPEC and mgp_sync redoes the run on the standalone check's
+    path. Results equal the oracle either way, and a rerun of the same context too."""
+    from mgatk2_amd.engine import EngineConfig
+    from mgatk2_amd.synth import ReadSoA
+
+    base = _synth(11, 120_000, 60)
+    cfg = EngineConfig(n_cells=60, min_baseq=20, min_mapq=30, dedup_mode="alignment_and_fragment_length")
+    rng = np.random.default_rng(3)
+    tl = base.tlen.copy()
+    pick = rng.choice(base.n, 40, replace=False)
+    tl[pick] = np.where(tl[pick] < 0, -70_000, 70_000) - rng.integers(0, 3, 40)
+    for name, soa in [("wide tlen", ReadSoA(base.start, base.bc, tl, base.flag, base.mapq, base.span,
+                                            base.rec_off, base.payload)),
+                      ("compact", base)]:
+        exp, _ = oracle_lib.oracle_run(cfg, soa)
+        with engine_lib.Engine(cfg) as eng:
+            eng.push(soa)
+            for _ in range(2):
+                eng.run()
+                assert_same(eng.fetch(), exp, name)
