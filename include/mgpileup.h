@@ -314,14 +314,19 @@ int  mgp_reset(mgp_ctx *ctx);
 /* Number of resident reads / payload bytes. */
 int  mgp_resident(mgp_ctx *ctx, int64_t *n_reads, int64_t *payload_bytes);
 
-/* Run the whole hot path over the resident reads (async on the compute stream):
- * the record filters and dedup of readers.py:95-150, process_barcode_worker
+/* Run the whole hot path over the resident reads (async on the compute stream,
+ * with one host wait for the input check's flag bits while the scan runs):
+ * the input check (coordinate order as pysam's fetch yields it, readers.py:87-92;
+ * declared spans; record placement), the record filters and dedup of
+ * readers.py:95-150, process_barcode_worker
  * (processors.py:20-55) = generate_pileup + filter_strand_bias
  * (pileup.py:18-154) for every cell, the per-cell statistics of
  * processors.py:33-51 / writers.py:187-197 and the reference-allele tallies of
  * writers.py:221-222,340-349. */
 int  mgp_run(mgp_ctx *ctx);
-/* Wait for the last run; returns the run's check status (MGP_E_UNSORTED, ...). */
+/* Wait for the last run; returns the run's check status (MGP_E_UNSORTED, ...).
+ * A run whose speculative compact grouping did not fit the resident reads is
+ * run again here on the fallback path before the status is returned. */
 int  mgp_sync(mgp_ctx *ctx);
 /* D2H the results of the last run into caller buffers (implies mgp_sync):
  * the dense form of the per-cell result dicts (processors.py:41-51) and of the

@@ -948,6 +948,7 @@ __global__ void __launch_bounds__(kBlock, Tr::kWaves) k_group_b(const typename T
     __shared__ uint32_t bst[kMaxRbB], bsz[kMaxRbB], spre[kMaxRbB + 1];
     __shared__ int s_be;
     __shared__ uint32_t s_ndup[kGroup], s_nunp[kGroup];  // the group's duplicates / kept unpaired reads in this bin range
+    __shared__ uint16_t wpend[kBlock / kWave][kBPer * kWave];  // per wave: stage indices of deferred walks
     const int gi = blockIdx.x;
     const int B0 = blockIdx.y * rb, B1 = min(g.nbins, B0 + rb);
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -1094,6 +1095,7 @@ __global__ void __launch_bounds__(kBlock, Tr::kWaves) k_group_b(const typename T
         // back is needed only behind kLook + 1 equal starts.
         constexpr int kWo = 2;
         constexpr int kLook = MGP_GB_LOOK;
+        uint32_t npend = 0;  // the wave's deferred walks this step (wave-uniform)
 
 #pragma unroll
         for (int h = 0; h < kBPer; h += kWo) {
@@ -1123,23 +1125,14 @@ __global__ void __launch_bounds__(kBlock, Tr::kWaves) k_group_b(const typename T
             }
 #pragma unroll
             for (int q = 0; q < kWo; ++q) {
-                if (MGP_ABL_B != 1 && __ballot(wk[q]) != 0ull && wk[q]) {
-                    const uint32_t t = threadIdx.x + (uint32_t)(h + q) * kBlock;
-                    const T x = xs[q];
-                    bool dup3 = false, dup2 = d2[q];
-                    for (uint32_t m = t - (uint32_t)kLook; !dup3 && m-- > 0;) {
-                        const T p = stage[m];
-                        if (!Tr::run_eq(p, x)) break;
-                        dup2 |= same_key<Tr>(p, x, dup3);
-                    }
-                    d2[q] = dup2;
-                    d3[q] = dup3;
-                }
-            }
-#pragma unroll
-            for (int q = 0; q < kWo; ++q) {
                 const uint32_t t = threadIdx.x + (uint32_t)(h + q) * kBlock;
-                const bool act = t < cur;
+                // an element behind kLook + 1 equal starts without a full-key match waits
+                // for the wave's deferred walks (one divergent loop per step, not per element)
+                const bool defer = MGP_ABL_B != 1 && wk[q];
+                const unsigned long long dm = __ballot(defer);
+                if (defer) wpend[wid][npend + (uint32_t)__popcll(dm & lt)] = (uint16_t)t;
+                npend += (uint32_t)__popcll(dm);
+                const bool act = t < cur && !defer;
                 const int lc = Tr::lcell(xs[q]);
                 bool keep = false;
                 if (act) {
@@ -1148,6 +1141,37 @@ __global__ void __launch_bounds__(kBlock, Tr::kWaves) k_group_b(const typename T
                 }
                 cell_tally<kTrack, Tr>(act, lc, keep, xs[q], s_ndup, s_nunp, st);
             }
+        }
+        // the deferred walks, one element per lane: every predecessor back to the
+        // run's start (kLook key words loaded together) or a full-key match
+        __builtin_amdgcn_wave_barrier();
+        for (uint32_t p0 = 0; p0 < npend; p0 += kWave) {
+            const bool act = p0 + (uint32_t)lane < npend;
+            const uint32_t t = act ? (uint32_t)wpend[wid][p0 + lane] : 0u;
+            const T x = stage[t];
+            bool dup2 = false, dup3 = false;
+            for (uint32_t m = act ? t : 0u; !dup3 && m > 0; m -= m < (uint32_t)kLook ? m : kLook) {
+                typename Tr::P pk[kLook];
+#pragma unroll
+                for (int k = 0; k < kLook; ++k) pk[k] = Tr::pred(stage, m >= (uint32_t)(k + 1) ? m - (uint32_t)(k + 1) : 0u);
+                bool r = true;
+#pragma unroll
+                for (int k = 0; k < kLook; ++k) {
+                    bool rk, sk, tk;
+                    Tr::match(pk[k], x, rk, sk, tk);
+                    r = r & (m >= (uint32_t)(k + 1)) & rk;
+                    dup2 |= r & sk;
+                    dup3 |= r & sk & tk;
+                }
+                if (!r) break;
+            }
+            const int lc = Tr::lcell(x);
+            bool keep = false;
+            if (act) {
+                const uint32_t pv = group_b_emit<Tr>(x, dup2, dup3, mode, unit, acc, keep);
+                if (MGP_ABL_B < 2 || pv == 7u) pel[cbase[lc] + (t - cstart[lc])] = pv;
+            }
+            cell_tally<kTrack, Tr>(act, lc, keep, x, s_ndup, s_nunp, st);
         }
         __syncthreads();
         if (wid == 0) cbase[lane] += cstart[lane + 1] - cstart[lane];
@@ -2065,7 +2089,7 @@ __global__ void __launch_bounds__(kBlock) k_median(Geom g, int min_reads, const 
                                                    const uint32_t* __restrict__ dmax,
                                                    uint32_t* __restrict__ med_lo, uint32_t* __restrict__ med_hi,
                                                    uint8_t* __restrict__ passed, DevStats* st) {
-    __shared__ uint32_t red[2][kBlock / kWave];
+    __shared__ uint32_t red[2][2][kBlock / kWave];  // [iteration parity][lo, hi][wave]
     const int c = blockIdx.x;
     const uint32_t n = covered[c];
     const uint32_t nr = n_reads[c];
@@ -2103,7 +2127,9 @@ __global__ void __launch_bounds__(kBlock) k_median(Geom g, int min_reads, const 
     const uint32_t t_lo = zeros + (n - 1) / 2 + 1, t_hi = zeros + n / 2 + 1;  // counts to reach
     uint32_t lo0 = 1, lo1 = dmax[c], hi0 = 1, hi1 = dmax[c];  // answers lie in [x0, x1]
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    while (lo0 < lo1 || hi0 < hi1) {
+    // one barrier per step: the partial sums alternate between two LDS sets, and a
+    // set is rewritten two steps later, behind the next step's barrier
+    for (int it = 0; lo0 < lo1 || hi0 < hi1; it ^= 1) {
         const uint32_t ml = lo0 + (lo1 - lo0) / 2, mh = hi0 + (hi1 - hi0) / 2;
         uint32_t cl = 0, ch = 0;
         if (kRegs) {
@@ -2128,17 +2154,16 @@ __global__ void __launch_bounds__(kBlock) k_median(Geom g, int min_reads, const 
         cl = wave_sum(cl);
         ch = wave_sum(ch);
         if (lane == 0) {
-            red[0][wid] = cl;
-            red[1][wid] = ch;
+            red[it][0][wid] = cl;
+            red[it][1][wid] = ch;
         }
         __syncthreads();
         uint32_t sl = 0, shh = 0;
 #pragma unroll
         for (int w = 0; w < kBlock / kWave; ++w) {
-            sl += red[0][w];
-            shh += red[1][w];
+            sl += red[it][0][w];
+            shh += red[it][1][w];
         }
-        __syncthreads();
         if (lo0 < lo1) {
             if (sl >= t_lo) lo1 = ml;
             else lo0 = ml + 1;
