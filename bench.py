@@ -35,6 +35,12 @@ BYTES_PER_READ = 95  # algorithmic input bytes per L=50 read
 BYTES_PER_CELL = 16569 * 10 * 4  # int32 counts (8 planes) + tn5 (2 planes) written once
 
 
+def workload_name(n_reads: int, n_cells: int) -> str:
+    """The BASELINE.json config a run's size matches (C4 is the bench's default)."""
+    return {(200_000_000, 10_000): "C4", (50_000_000, 5_000): "C3", (1_000_000, 500): "C2",
+            (1_000_000_000, 100_000): "C5 on one GPU"}.get((n_reads, n_cells), "custom")
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -186,8 +192,9 @@ def main():
             "dtype": "u32",
             "data": "synthetic (SURVEY.md §8(d) generator, created in HBM by the device generator)",
             "config": {
-                "workload": "C4: 200M chrM reads x 10k cells per GPU, run params (q20, mapq30, "
-                            "dedup=alignment_and_fragment_length, min_reads 1), L=50",
+                "workload": f"{workload_name(n_reads, n_cells)}: {n_reads / 1e6:g}M chrM reads x {n_cells / 1e3:g}k "
+                            f"cells per GPU, run params (q20, mapq30, dedup=alignment_and_fragment_length, "
+                            f"min_reads 1), L={args.read_len}",
                 "reads_per_gpu": n_res,
                 "cells_per_gpu": n_cells,
                 "payload_bytes_per_gpu": pay,
