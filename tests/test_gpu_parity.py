@@ -593,3 +593,38 @@ def test_speculative_compact_falls_back(engine_lib, oracle_lib):
             for _ in range(2):
                 eng.run()
                 assert_same(eng.fetch(), exp, name)
+
+
+@pytest.mark.parametrize("wide", [False, True])
+def test_unsorted_detected_at_every_boundary(engine_lib, monkeypatch, wide):
+    """The coordinate-order check runs on the speculative path inside grouping pass A
+    (a read's predecessor start from the lane below by DPP, from lane 63 of the
+    previous slot, or loaded for the first read of a wave's run) and on the fallback
+    path in k_check_inputs (MGP_GROUP_WIDE=1). One read moved below its predecessor
+    at lane, slot, wave-run, step and start-bin boundaries raises BAMFormatError each
+    time; the sorted set runs clean."""
+    from mgatk2_amd.engine import EngineConfig
+    from mgatk2_amd.exceptions import BAMFormatError
+    from mgatk2_amd.synth import ReadSoA
+
+    if wide:
+        monkeypatch.setenv("MGP_GROUP_WIDE", "1")
+    base = _synth(21, 60_000, 40)
+    cfg = EngineConfig(n_cells=40, min_baseq=20, min_mapq=30, dedup_mode="alignment_and_fragment_length")
+    st = base.start
+    # the first read of some start bins (every part range and wave run starts there)
+    bin_first = np.nonzero(np.diff(st // 8) > 0)[0][[3, 40, 700]] + 1
+    picks = [1, 63, 64, 65, 511, 512, 513, 2048, 4097, 30_001, base.n - 1, *bin_first.tolist()]
+    with engine_lib.Engine(cfg) as eng:
+        eng.push(base)
+        eng.run()
+        eng.sync()
+    for i in picks:
+        s = st.copy()
+        s[i] = s[i - 1] - 1  # below its predecessor only
+        soa = ReadSoA(s, base.bc, base.tlen, base.flag, base.mapq, base.span, base.rec_off, base.payload)
+        with engine_lib.Engine(cfg) as eng:
+            eng.push(soa)
+            eng.run()
+            with pytest.raises(BAMFormatError):
+                eng.sync()
