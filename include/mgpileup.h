@@ -339,6 +339,11 @@ int  mgp_finish(mgp_ctx *ctx, mgp_result *out);
  * measured with HIP events recorded on the compute stream around each stage.
  * names: comma-separated stage names written into `names`. */
 int  mgp_kernel_times(mgp_ctx *ctx, int last_runs, float *ms, int max_n, int *n_out, char *names, int names_len);
+/* Which stages the next runs bracket with HIP events: all (1, the default) or the
+ * pileup's only (0). Every event is a marker between two kernels of the compute
+ * stream, so a run timed for its wall clock records only the pileup's;
+ * mgp_kernel_times averages each stage over the runs that recorded it. */
+int  mgp_set_stage_timing(mgp_ctx *ctx, int all_stages);
 
 /* RCCL: rank 0 creates the unique id (128 bytes), every rank joins. After init,
  * mgp_run all-reduces ref_tally over the communicator (no reference

@@ -132,6 +132,7 @@ struct mgp_ctx {
     int roff_mode = -1;     // pass A's offset source (kOffDense / kOffR32 / kOffR64), from the run's input check
     uint32_t read_bits = 0; // the input check's CHK_* bits of the resident reads
     bool no_spec = false;   // the speculative compact grouping failed on the resident reads (ERR_RESPEC)
+    bool stage_all = true;  // HIP events around every stage (false: the pileup's only, mgp_set_stage_timing)
 
     // run scratch
     DevBuf bin_start, H, P, cell_cnt, cell_base, bin_valid, bin_base, bucket_off, gel2, PG, F;
@@ -2263,6 +2264,29 @@ __global__ void k_add_u64(uint64_t* __restrict__ a, int64_t n, uint64_t add) {
     if (i < n) a[i] += add;
 }
 
+// A run's zeroed state (one launch instead of a memset per buffer): per-cell
+// counters, first reads (all ones), the first-bin bits F, the check words, stats.
+__global__ void k_run_init(int nc, int64_t nF, uint32_t* __restrict__ covered, unsigned long long* __restrict__ dsum,
+                           uint32_t* __restrict__ dmax, uint32_t* __restrict__ n_reads, uint8_t* __restrict__ any_paired,
+                           uint32_t* __restrict__ first_read, uint32_t* __restrict__ F, uint32_t* __restrict__ ck,
+                           DevStats* st) {
+    const int64_t i0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x, step = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = i0; i < nc; i += step) {
+        covered[i] = 0u;
+        dsum[i] = 0ull;
+        dmax[i] = 0u;
+        n_reads[i] = 0u;
+        any_paired[i] = 0u;
+        first_read[i] = 0xFFFFFFFFu;
+    }
+    for (int64_t i = i0; i < nF; i += step) F[i] = 0u;
+    if (i0 == 0) {
+        ck[0] = 0u;
+        ck[1] = 0u;
+        *st = DevStats{};
+    }
+}
+
 // The run's view of the input check: the pileup's halo span and the order check.
 // The standalone input check (the fallback path of mgp_run): every bit and the span
 // over all resident reads, and the u32 offset column roff32 = rec_off >> 6.
@@ -2589,8 +2613,14 @@ static Out16 out16_of(mgp_ctx* ctx) {
     return o;
 }
 
-#define STAGE_BEGIN(st) HIP_TRY(hipEventRecord(ctx->ev[slot][st][0], s)); ctx->stage_ran[slot][st] = true
-#define STAGE_END(st) HIP_TRY(hipEventRecord(ctx->ev[slot][st][1], s))
+// Stage events: each is a marker between two kernels of the stream (about 11 us
+// of idle GPU at a stage boundary on MI355X), so mgp_set_stage_timing can keep the
+// pileup's only.
+#define STAGE_ON(st) (ctx->stage_all || (st) == ST_PILEUP)
+#define STAGE_BEGIN(st) \
+    if (STAGE_ON(st)) { HIP_TRY(hipEventRecord(ctx->ev[slot][st][0], s)); ctx->stage_ran[slot][st] = true; }
+#define STAGE_END(st) \
+    if (STAGE_ON(st)) HIP_TRY(hipEventRecord(ctx->ev[slot][st][1], s))
 
 int mgp_run(mgp_ctx* ctx) {
     if (!ctx) return set_err(MGP_E_INVALID, "null ctx");
@@ -2604,15 +2634,15 @@ int mgp_run(mgp_ctx* ctx) {
     const int slot = (int)(ctx->runs % mgp_ctx::kRing);
     for (int i = 0; i < ST_N; ++i) ctx->stage_ran[slot][i] = false;
     DevStats* st = ctx->stats.as<DevStats>();
-    HIP_TRY(hipMemsetAsync(st, 0, sizeof(DevStats), s));
-
-    if (nc > 0) {
-        HIP_TRY(hipMemsetAsync(ctx->covered.p, 0, (size_t)nc * 4, s));
-        HIP_TRY(hipMemsetAsync(ctx->dsum.p, 0, (size_t)nc * 8, s));
-        HIP_TRY(hipMemsetAsync(ctx->dmax.p, 0, (size_t)nc * 4, s));
-        HIP_TRY(hipMemsetAsync(ctx->n_reads.p, 0, (size_t)nc * 4, s));
-        HIP_TRY(hipMemsetAsync(ctx->any_paired.p, 0, (size_t)nc, s));
-        HIP_TRY(hipMemsetAsync(ctx->first_read.p, 0xFF, (size_t)nc * 4, s));
+    if (nc > 0) {  // the run's per-cell counters, stats, check words and first-bin bits in one launch
+        const int64_t nF = (int64_t)g.nbins * ((nc + 31) / 32);
+        k_run_init<<<std::max(1u, std::min(1024u, blocks_for(std::max<int64_t>(nc, nF)))), kBlock, 0, s>>>(
+            nc, nF, ctx->covered.as<uint32_t>(), ctx->dsum.as<unsigned long long>(), ctx->dmax.as<uint32_t>(),
+            ctx->n_reads.as<uint32_t>(), ctx->any_paired.as<uint8_t>(), ctx->first_read.as<uint32_t>(),
+            ctx->F.as<uint32_t>(), ctx->roff_irregular.as<uint32_t>(), st);
+        HIP_TRY(hipGetLastError());
+    } else {
+        HIP_TRY(hipMemsetAsync(st, 0, sizeof(DevStats), s));
     }
 
     if (nc > 0) {
@@ -2622,10 +2652,8 @@ int mgp_run(mgp_ctx* ctx) {
         // to pinned host memory while the scan runs; the host picks the grouping and pileup
         // variants from them below.
         STAGE_BEGIN(ST_HIST);
-        if (n > 0) HIP_TRY(hipMemsetAsync(ctx->roff_irregular.p, 0, 8, s));
         if (n == 0) HIP_TRY(hipMemsetAsync(ctx->H.p, 0, (size_t)(g.nbins + 1) * nc * 4, s));
         if (n == 0) HIP_TRY(hipMemsetAsync(ctx->bin_start.p, 0, (size_t)(g.nbins + 1) * 4, s));
-        HIP_TRY(hipMemsetAsync(ctx->F.p, 0, (size_t)g.nbins * ((nc + 31) / 32) * 4, s));
         if (n > 0) {
             // cells per slice: whole 64-cell groups, counts + group totals within the LDS budget
             int lds_cells = ctx->lds_hist_max_cells / (kGroup + 1) * kGroup;
@@ -2807,14 +2835,16 @@ int mgp_run(mgp_ctx* ctx) {
             hipStream_t s2 = ctx->s_side;
             HIP_TRY(hipEventRecord(ctx->ev_fork, s));
             HIP_TRY(hipStreamWaitEvent(s2, ctx->ev_fork, 0));
-            HIP_TRY(hipEventRecord(ctx->ev[slot][ST_TALLY][0], s2));
-            ctx->stage_ran[slot][ST_TALLY] = true;
+            if (STAGE_ON(ST_TALLY)) {
+                HIP_TRY(hipEventRecord(ctx->ev[slot][ST_TALLY][0], s2));
+                ctx->stage_ran[slot][ST_TALLY] = true;
+            }
             HIP_TRY(hipMemsetAsync(ctx->tally.p, 0, (size_t)g.L * 32, s2));
             dim3 gt(blocks_for((int64_t)g.L * 4), (unsigned)std::max(1, std::min(g.nchunks, 32)));
             k_tally_reduce<<<gt, kBlock, 0, s2>>>(ctx->tally_part.as<uint32_t>(), g.nchunks, g.L * 4,
                                                   ctx->tally.as<unsigned long long>());
             HIP_TRY(hipGetLastError());
-            HIP_TRY(hipEventRecord(ctx->ev[slot][ST_TALLY][1], s2));
+            if (STAGE_ON(ST_TALLY)) HIP_TRY(hipEventRecord(ctx->ev[slot][ST_TALLY][1], s2));
             HIP_TRY(hipEventRecord(ctx->ev_join, s2));
         }
 
@@ -2944,19 +2974,29 @@ int mgp_kernel_times(mgp_ctx* ctx, int last_runs, float* ms, int max_n, int* n_o
     int k = 0;
     for (int st = 0; st < ST_N && k < max_n; ++st, ++k) {
         double acc = 0.0;
+        int timed = 0;  // runs that recorded this stage (mgp_set_stage_timing)
         for (int r = 0; r < last_runs; ++r) {
             const int slot = (int)((ctx->runs - 1 - r) % mgp_ctx::kRing);
             float t = 0.f;
-            if (ctx->stage_ran[slot][st]) HIP_TRY(hipEventElapsedTime(&t, ctx->ev[slot][st][0], ctx->ev[slot][st][1]));
+            if (ctx->stage_ran[slot][st]) {
+                HIP_TRY(hipEventElapsedTime(&t, ctx->ev[slot][st][0], ctx->ev[slot][st][1]));
+                ++timed;
+            }
             acc += t;
         }
-        if (ms) ms[k] = (float)(acc / last_runs);
+        if (ms) ms[k] = timed ? (float)(acc / timed) : 0.f;
     }
     if (n_out) *n_out = k;
     if (names && names_len > 0) {
         std::strncpy(names, kStageNames, (size_t)names_len - 1);
         names[names_len - 1] = 0;
     }
+    return MGP_OK;
+}
+
+int mgp_set_stage_timing(mgp_ctx* ctx, int all_stages) {
+    if (!ctx) return set_err(MGP_E_INVALID, "null ctx");
+    ctx->stage_all = all_stages != 0;
     return MGP_OK;
 }
 

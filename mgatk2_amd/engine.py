@@ -37,7 +37,7 @@ ABI_SYMBOLS = (
     "mgp_abi_version", "mgp_last_error", "mgp_device_count", "mgp_open", "mgp_close", "mgp_host_alloc",
     "mgp_host_free", "mgp_push_batch", "mgp_reset", "mgp_resident", "mgp_run", "mgp_sync", "mgp_fetch",
     "mgp_finish", "mgp_kernel_times", "mgp_comm_unique_id", "mgp_comm_init", "mgp_synth_generate",
-    "mgp_download_inputs",
+    "mgp_download_inputs", "mgp_set_stage_timing",
 )
 
 
@@ -156,6 +156,7 @@ def load_library(path: Path | None = None) -> C.CDLL:
         "mgp_kernel_times": (
             [vp, C.c_int, C.POINTER(C.c_float), C.c_int, C.POINTER(C.c_int), C.c_char_p, C.c_int], C.c_int
         ),
+        "mgp_set_stage_timing": ([vp, C.c_int], C.c_int),
         "mgp_comm_unique_id": ([C.c_char_p], C.c_int),
         "mgp_comm_init": ([vp, C.c_char_p, C.c_int, C.c_int], C.c_int),
         "mgp_synth_generate": ([vp, C.POINTER(mgp_synth_params)], C.c_int),
@@ -403,6 +404,11 @@ class Engine:
         _ck(self.lib.mgp_kernel_times(self._h, int(last_runs), ms, 32, C.byref(n), names, 512), "mgp_kernel_times")
         keys = names.value.decode().split(",")
         return {k: float(ms[i]) for i, k in enumerate(keys[: n.value])}
+
+    def set_stage_timing(self, all_stages: bool = True):
+        """HIP events around every stage of the next runs (default), or around the
+        pileup only: each event is a marker between two kernels of the stream."""
+        _ck(self.lib.mgp_set_stage_timing(self._h, int(bool(all_stages))), "mgp_set_stage_timing")
 
     # -- multi-GPU ---------------------------------------------------------
     @staticmethod
