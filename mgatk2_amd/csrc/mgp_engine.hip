@@ -143,7 +143,7 @@ struct mgp_ctx {
 
     bool ran = false;
     int last_status = MGP_OK;
-    DevStats host_stats{};
+    DevStats* host_stats = nullptr;  // pinned: the run's stats copy stays asynchronous
 
     ncclComm_t comm = nullptr;
     int nranks = 1;
@@ -2440,6 +2440,8 @@ int mgp_open(const mgp_config* cfg, int hip_device, mgp_ctx** out) {
     HIP_TRY(hipEventCreateWithFlags(&ctx->ev_join, hipEventDisableTiming));
     HIP_TRY(hipEventCreateWithFlags(&ctx->ev_bits, hipEventDisableTiming));
     HIP_TRY(hipHostMalloc((void**)&ctx->h_bits, 8, hipHostMallocDefault));
+    HIP_TRY(hipHostMalloc((void**)&ctx->host_stats, sizeof(DevStats), hipHostMallocDefault));
+    *ctx->host_stats = DevStats{};
     MGP_TRY(ctx->roff_irregular.ensure(8));
     for (int r = 0; r < mgp_ctx::kRing; ++r)
         for (int s = 0; s < ST_N; ++s) {
@@ -2489,6 +2491,7 @@ void mgp_close(mgp_ctx* ctx) {
     (void)hipEventDestroy(ctx->ev_join);
     (void)hipEventDestroy(ctx->ev_bits);
     if (ctx->h_bits) (void)hipHostFree(ctx->h_bits);
+    if (ctx->host_stats) (void)hipHostFree(ctx->host_stats);
     (void)hipStreamDestroy(ctx->s_comp);
     (void)hipStreamDestroy(ctx->s_copy);
     (void)hipStreamDestroy(ctx->s_side);
@@ -2883,7 +2886,7 @@ int mgp_run(mgp_ctx* ctx) {
         if (r != ncclSuccess) return set_err(MGP_E_COMM, std::string("ncclAllReduce: ") + ncclGetErrorString(r));
         STAGE_END(ST_COMM);
     }
-    HIP_TRY(hipMemcpyAsync(&ctx->host_stats, st, sizeof(DevStats), hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipMemcpyAsync(ctx->host_stats, st, sizeof(DevStats), hipMemcpyDeviceToHost, s));
     ctx->ran = true;
     ctx->runs++;
     ctx->last_status = MGP_OK;
@@ -2895,7 +2898,7 @@ int mgp_sync(mgp_ctx* ctx) {
     if (!ctx->ran) return set_err(MGP_E_STATE, "no run to wait for");
     HIP_TRY(hipSetDevice(ctx->dev));
     HIP_TRY(hipStreamSynchronize(ctx->s_comp));
-    const uint32_t e = ctx->host_stats.err;
+    const uint32_t e = ctx->host_stats->err;
     if ((e & ERR_RESPEC) && !ctx->no_spec) {  // a read did not fit the compact grouping: run again
         ctx->no_spec = true;
         MGP_TRY(mgp_run(ctx));
@@ -2944,7 +2947,7 @@ int mgp_fetch(mgp_ctx* ctx, mgp_result* out) {
     MGP_TRY(d2h(out->first_read, ctx->first_read, nc * 4));
     MGP_TRY(d2h(out->ref_tally, ctx->tally, L * 4 * 8));
     if (out->stats) {
-        const DevStats& h = ctx->host_stats;
+        const DevStats& h = *ctx->host_stats;
         mgp_stats* o = out->stats;
         o->total_reads = ctx->n;
         o->filtered_reads = (int64_t)h.filtered;
