@@ -932,7 +932,7 @@ constexpr int kBPer = kStageB / kBlock;  // elements per lane per step
 #endif
 
 #ifndef MGP_GB_LOOK
-#define MGP_GB_LOOK 4  // predecessors compared branch-free before a walk back (A/B: 2-6)
+#define MGP_GB_LOOK 3  // predecessors compared branch-free before a deferred walk (v42 A/B: 2, 4, 6 slower)
 #endif
 template <bool kTrack, class Tr>
 __global__ void __launch_bounds__(kBlock, Tr::kWaves) k_group_b(const typename Tr::T* __restrict__ gel2,
