@@ -255,6 +255,10 @@ __global__ void __launch_bounds__(kHistBlock) k_bin_count(const int32_t* __restr
     if (first && threadIdx.x == 0) {
         bin_lo[b] = (uint32_t)blo;
         if (b == g.nbins - 1) bin_lo[g.nbins] = (uint32_t)n;
+        // sorted starts give monotone bounds, and monotone bounds partition the reads
+        // (each counted once, whatever the order inside); otherwise a read may be in
+        // two bins' ranges and the grouping slots would outgrow their buffers
+        if (s_range[1] < s_range[0]) atomicOr(&st->err, ERR_BOUNDS | ERR_UNSORTED);
     }
     unsigned long long nvalid = 0;
     bool badbc = false;
@@ -491,6 +495,7 @@ __global__ void __launch_bounds__(kGABlock, MGP_GA_WAVES) k_group_a(int64_t n, c
                                                     DevStats* st) {
     static_assert(kOff != kOffSpec || kCompact, "the speculative check writes compact elements");
     constexpr bool kSpec = kOff == kOffSpec;
+    if (__atomic_load_n(&st->err, __ATOMIC_RELAXED) & ERR_BOUNDS) return;  // unsorted input (k_bin_count)
     extern __shared__ uint32_t sm[];
     uint32_t* gcnt = sm;             // [ngroups] next free slot of each bucket (this part)
     uint32_t* fbits = sm + ngroups;  // [ceil(nc/32)] cell's first read is in this bin
@@ -760,7 +765,7 @@ struct DedupAcc {  // per-thread duplicate counters of pass B
 
 
 #ifndef MGP_GB_WAVES
-#define MGP_GB_WAVES 4
+#define MGP_GB_WAVES 3  // wide elements: the LDS stage (32 KB) and the deferred-walk lists allow 3
 #endif
 #ifndef MGP_GB_WAVES_C
 #define MGP_GB_WAVES_C 5
@@ -943,6 +948,7 @@ __global__ void __launch_bounds__(kBlock, Tr::kWaves) k_group_b(const typename T
                                                     unsigned long long* __restrict__ dup_part, DevStats* st) {
     using T = typename Tr::T;
     constexpr bool kCompact = sizeof(T) == 8;
+    if (__atomic_load_n(&st->err, __ATOMIC_RELAXED) & ERR_BOUNDS) return;  // unsorted input (k_bin_count)
     __shared__ T stage[kStageB];
     __shared__ uint32_t wcnt[kBlock / kWave][kGroup];
     __shared__ uint32_t cbase[kGroup], cstart[kGroup + 1];
@@ -1760,6 +1766,7 @@ __global__ void __launch_bounds__(kBlock, MGP_PILEUP_WAVES) k_pileup(
     uint32_t* __restrict__ dmax, uint32_t* __restrict__ tally_part, DevStats* st) {
     extern __shared__ __align__(16) uint32_t tile[];  // [Wp][4] A, C, G, T, then [Wp] Tn5 (fwd | rev << 16)
     uint32_t* t5 = tile + 4 * g.Wp;
+    if (__atomic_load_n(&st->err, __ATOMIC_RELAXED) & ERR_BOUNDS) return;  // unsorted input (k_bin_count)
     __shared__ uint32_t wq_all[kBlock / kWave][kWaveQ];
     __shared__ uint32_t r_cov[4], r_max[4], r_keep[4];
     __shared__ unsigned long long r_sum[4];

@@ -16,6 +16,8 @@ constexpr uint32_t ERR_BADBC = 8u;      // bc >= n_cells
 constexpr uint32_t ERR_OVERFLOW = 16u;  // scatter destination outside its cell segment
 constexpr uint32_t ERR_PACKED = 32u;    // MGP_FLAG_PACKED record outside the packed layout's limits
 constexpr uint32_t ERR_RESPEC = 64u;    // a read does not fit the speculative compact grouping (mgp_sync reruns)
+constexpr uint32_t ERR_BOUNDS = 128u;   // start-bin read ranges not monotone (unsorted input): grouping and
+                                        // pileup kernels exit at entry, so no slot leaves its buffer
 
 // Counters written by the kernels of one run (zeroed at run start).
 struct DevStats {

@@ -628,3 +628,31 @@ def test_unsorted_detected_at_every_boundary(engine_lib, monkeypatch, wide):
             eng.run()
             with pytest.raises(BAMFormatError):
                 eng.sync()
+
+
+@pytest.mark.parametrize("order", ["reversed", "shuffled"])
+def test_scrambled_order_raises_without_faults(engine_lib, order):
+    """Reads far from coordinate order give start-bin bounds that are not monotone:
+    the histogram flags it and the grouping and pileup kernels stop at entry, so the
+    run ends with BAMFormatError and every buffer access stays in bounds. The same
+    context then runs the sorted reads bit-exactly."""
+    from mgatk2_amd.engine import EngineConfig
+    from mgatk2_amd.exceptions import BAMFormatError
+    from mgatk2_amd.synth import ReadSoA
+
+    base = _synth(23, 80_000, 30)
+    cfg = EngineConfig(n_cells=30, min_baseq=20, min_mapq=30, dedup_mode="alignment_and_fragment_length")
+    perm = np.arange(base.n)[::-1] if order == "reversed" else np.random.default_rng(5).permutation(base.n)
+    cols = [np.ascontiguousarray(getattr(base, k)[perm]) for k in ("start", "bc", "tlen", "flag", "mapq", "span",
+                                                                     "rec_off")]
+    bad = ReadSoA(*cols, base.payload)
+    exp = run_engine(engine_lib, cfg, base)
+    with engine_lib.Engine(cfg) as eng:
+        eng.push(bad)
+        eng.run()
+        with pytest.raises(BAMFormatError):
+            eng.sync()
+        eng.reset()
+        eng.push(base)
+        eng.run()
+        assert_same(eng.fetch(), exp, f"{order} then sorted")
