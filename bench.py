@@ -2,17 +2,32 @@
 
 One step = one pass of the hot path (mgp_run: filter + cell-major grouping +
 dedup + CIGAR-walk pileup + strand filter + per-cell stats + reference-allele
-tallies, and the RCCL all-reduce of the tallies when N > 1) over the
-HBM-resident synthetic workload of BASELINE config C4 (200M chrM reads x 10k
-cells, `run` parameters) per GPU. Inputs are generated directly in HBM by the
-device generator (bit-identical to mgatk2_amd/synth.py); the timed region starts
-with them resident.
+tallies, and the RCCL all-reduce of the tallies when N > 1) over BASELINE config
+C4: ONE synthetic set of 200M chrM reads x 10k cells, `run` parameters, split by
+cell over the N GPUs (strong scaling: rank r owns a read-balanced contiguous cell
+range and exactly the reads of those cells, plus an equal share of the reads
+without a whitelisted barcode; the reference's per-cell parallelism,
+processors.py:112-144). Inputs are generated directly in HBM by the device
+generator (bit-identical to mgatk2_amd/synth.py); `value` is timed with them
+resident.
 
-Multi-GPU: one process per GPU (torch.distributed.run), cells sharded (each rank
-owns its own 10k-cell shard of 200M reads: weak scaling). torch.distributed
-(gloo, CPU) is used only for the rendezvous, barriers and the max-over-ranks
-time; the data path has no collective except the RCCL tally all-reduce inside
-mgp_run. Rank 0 prints one JSON line.
+Around the timed steps (never inside them), rank 0 also measures:
+  * sample_check: 3 samples of 8 whole cells of the timed run, bit for bit
+    against the oracle on exactly their reads (cells are independent);
+  * pcie: SURVEY.md §8(d)'s engine metric, from the first SoA batch H2D to the
+    count matrices in host memory: pinned host batches pushed while earlier
+    windows already run (streaming, MGP_CFG_STREAM), then the 16-bit result rows
+    and per-cell statistics copied into pinned host memory (every rank, max over
+    ranks);
+  * cpu_baseline (N = 1 only): the single-threaded C port of the reference's
+    path on a bounded sample of the same generator.
+
+Launch: `python bench.py --gpus N` starts N worker processes itself (one per GPU,
+RANK/LOCAL_RANK/WORLD_SIZE in their environment, before anything touches a GPU);
+under torch.distributed.run the ranks come from the environment. torch.distributed
+(gloo, CPU) is used only for the rendezvous, barriers and max-over-ranks; the
+data path's only collective is the RCCL tally all-reduce inside mgp_run.
+Rank 0 prints one JSON line.
 """
 
 from __future__ import annotations
@@ -20,6 +35,7 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import subprocess
 import sys
 import time
 from pathlib import Path
@@ -33,12 +49,13 @@ METRIC = "chrM reads piled-up/sec (whole node) at 200M reads × 10k cells; bit-e
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 BYTES_PER_READ = 95  # algorithmic input bytes per L=50 read
 BYTES_PER_CELL = 16569 * 10 * 4  # int32 counts (8 planes) + tn5 (2 planes) written once
+ROW16_BYTES_PER_CELL = 16569 * 22  # the pileup's 16-bit rows: 8 + 2 + 1 u16 per position
 
 
 def workload_name(n_reads: int, n_cells: int) -> str:
     """The BASELINE.json config a run's size matches (C4 is the bench's default)."""
     return {(200_000_000, 10_000): "C4", (50_000_000, 5_000): "C3", (1_000_000, 500): "C2",
-            (1_000_000_000, 100_000): "C5 on one GPU"}.get((n_reads, n_cells), "custom")
+            (1_000_000_000, 100_000): "C5"}.get((n_reads, n_cells), "custom")
 
 
 def parse():
@@ -46,26 +63,68 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--reads", type=int, default=200_000_000, help="reads per GPU")
-    ap.add_argument("--cells", type=int, default=10_000, help="cells per GPU")
+    ap.add_argument("--reads", type=int, default=200_000_000, help="reads of the whole set (all GPUs)")
+    ap.add_argument("--cells", type=int, default=10_000, help="cells of the whole set (all GPUs)")
     ap.add_argument("--read-len", type=int, default=50)
     ap.add_argument("--seed", type=int, default=20251015 + 4)
+    ap.add_argument("--weak", action="store_true", help="weak scaling: every rank gets its own full-size set")
     ap.add_argument("--cpu-sample-reads", type=int, default=20_000_000)
     ap.add_argument("--cpu-sample-cells", type=int, default=1000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-check", action="store_true", help="skip the bit-exact sample check")
+    ap.add_argument("--no-pcie", action="store_true", help="skip the PCIe-inclusive (host buffers) leg")
+    ap.add_argument("--pcie-steps", type=int, default=3)
+    ap.add_argument("--batch-reads", type=str, default="16000000",
+                    help="reads per pushed batch in the PCIe leg; a comma list sweeps (first = reported)")
     ap.add_argument("--record-layout", choices=["paired", "packed", "full"], default="paired",
                     help="payload records: packed 64-byte records, two consecutive records of a cell per "
                          "128-byte line (paired, default: the placement of mgp_place_records), packed in BAM "
                          "order, or full 128-byte records")
-    ap.add_argument("--check", action="store_true", help="bit-exact check of a sample against the oracle")
     return ap.parse_args()
+
+
+# ---------------------------------------------------------------------------
+# launcher: one worker process per GPU, started before anything touches a GPU
+# ---------------------------------------------------------------------------
+def launch_workers(n: int, cmd: list[str]) -> int:
+    """Start `cmd` n times, as ranks 0..n-1 of one node (RANK, LOCAL_RANK,
+    WORLD_SIZE, MASTER_ADDR/PORT in the environment); the first nonzero exit code,
+    else 0. The parent never touches a GPU: every HIP call is in the workers."""
+    import socket
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        procs.append(subprocess.Popen(cmd, env=env))
+    codes = [p.wait() for p in procs]
+    return next((c for c in codes if c != 0), 0)
+
+
+def cell_bounds(cdf: np.ndarray, world: int) -> np.ndarray:
+    """Read-balanced contiguous cell ranges (shard.partition_cells over the
+    generator's expected reads per cell)."""
+    from mgatk2_amd.shard import partition_cells
+
+    w = np.diff(np.concatenate([[0.0], cdf.astype(np.float64)]))
+    return partition_cells(w, world)
 
 
 def main():
     args = parse()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_workers(args.gpus, [sys.executable, str(Path(__file__).resolve()), *sys.argv[1:]]))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.gpus != world:
+        print(f"[bench] --gpus {args.gpus} but WORLD_SIZE {world}: running {world} ranks", file=sys.stderr)
+    if args.record_layout == "paired" and args.read_len > 50:
+        raise SystemExit("--record-layout paired places 64-byte packed records: needs --read-len <= 50")
     dist = None
     if world > 1:
         import torch.distributed as tdist
@@ -80,33 +139,35 @@ def main():
         if dist is not None:
             dist.barrier()
 
-    def max_over_ranks(x: float) -> float:
+    def reduce(x: float, op: str) -> float:
         if dist is None:
             return x
         import torch
 
         t = torch.tensor([x], dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX if op == "max" else dist.ReduceOp.SUM)
         return float(t.item())
 
-    def sum_over_ranks(x: float) -> float:
-        if dist is None:
-            return x
-        import torch
-
-        t = torch.tensor([x], dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.SUM)
-        return float(t.item())
-
-    n_reads, n_cells = args.reads, args.cells
-    seed = args.seed + 1_000_003 * rank
+    no_comm = os.environ.get("MGP_BENCH_NO_COMM") == "1"
+    device = 0 if no_comm else local_rank
+    n_glob, nc_glob = args.reads, args.cells
+    seed = args.seed + (1_000_003 * rank if args.weak else 0)
+    cdf, ref = cell_cdf(seed, nc_glob), ref_codes(args.seed)  # one chrM reference for every rank
+    if world > 1 and not args.weak:
+        b = cell_bounds(cdf, world)
+        lo, hi = int(b[rank]), int(b[rank + 1])
+        shard = dict(cells=(lo, hi), shard=(rank, world))
+    else:
+        lo, hi = 0, nc_glob
+        shard = {}
+    n_cells = hi - lo
     cfg = EngineConfig(n_cells=n_cells, min_baseq=20, min_mapq=30, min_distance_from_end=5,
                        dedup_mode="alignment_and_fragment_length", max_strand_bias=1.0, min_reads=1)
-    eng = Engine(cfg, device=local_rank if os.environ.get("MGP_BENCH_NO_COMM") != "1" else 0)
+    eng = Engine(cfg, device=device)
     t0 = time.time()
-    cdf, ref = cell_cdf(seed, n_cells), ref_codes(args.seed)  # one chrM reference for every rank
     packed = args.record_layout in ("packed", "paired")
-    eng.synth(seed, n_reads, cdf, ref, read_len=args.read_len, rec_align=64 if packed else 128, pack=packed)
+    eng.synth(seed, n_glob, cdf, ref, read_len=args.read_len, rec_align=64 if packed else 128, pack=packed, **shard)
+    n_res, pay = eng.resident()
     if args.record_layout == "paired":
         # the producer's placement (mgp_place_records, as the BAM decoder emits it):
         # computed on the host from the generated barcode and flag columns, then the
@@ -114,25 +175,29 @@ def main():
         from mgatk2_amd.bam import PLACE_PAIRED, place_records
 
         soa = eng.download_inputs(columns=("bc", "flag", "start", "tlen"))
-        roff, pay_b = place_records(soa.bc, soa.flag, np.full(n_reads, 64, np.uint32), n_cells, PLACE_PAIRED,
+        roff, pay_b = place_records(soa.bc, soa.flag, np.full(n_res, 64, np.uint32), n_cells, PLACE_PAIRED,
                                     start=soa.start, tlen=soa.tlen)
         del soa
-        eng.synth(seed, n_reads, cdf, ref, read_len=args.read_len, rec_align=64, pack=True, rec_off=roff,
-                  payload_bytes=pay_b)
+        eng.synth(seed, n_glob, cdf, ref, read_len=args.read_len, rec_align=64, pack=True, rec_off=roff,
+                  payload_bytes=pay_b, **shard)
         del roff
     n_res, pay = eng.resident()
     t_gen = time.time() - t0
-    if rank == 0:
-        print(f"[bench] generated {n_res:,} reads ({pay / 1e9:.2f} GB payload) on device in {t_gen:.1f}s",
-              file=sys.stderr, flush=True)
+    print(f"[bench] rank {rank}: cells [{lo}, {hi}), {n_res:,} reads ({pay / 1e9:.2f} GB payload) generated "
+          f"on device {device} in {t_gen:.1f}s", file=sys.stderr, flush=True)
 
     # MGP_BENCH_NO_COMM=1: rehearse the multi-process path with several ranks on one
     # GPU (RCCL refuses two ranks on one device); the tallies are then not reduced
-    if world > 1 and os.environ.get("MGP_BENCH_NO_COMM") != "1":
+    def make_comm(e):
         uid = Engine.comm_unique_id() if rank == 0 else b"\0" * 128
         obj = [uid]
         dist.broadcast_object_list(obj, src=0)
-        eng.comm_init(obj[0], world, rank)
+        e.comm_init(obj[0], world, rank)
+
+    comm_ranks = 1
+    if world > 1 and not no_comm:
+        make_comm(eng)
+        comm_ranks = world
 
     # the timed runs bracket only the pileup with HIP events (its roofline); every
     # other stage boundary would add a marker between two kernels of the stream
@@ -148,8 +213,8 @@ def main():
         eng.run()
     eng.sync()
     barrier()
-    dt = time.perf_counter() - t0
-    dt = max_over_ranks(dt)
+    dt_rank = time.perf_counter() - t0
+    dt = reduce(dt_rank, "max")
 
     kt = eng.kernel_times(last_runs=min(args.steps, 64))
     # the per-stage breakdown from a few more (untimed) runs with every stage bracketed
@@ -160,7 +225,7 @@ def main():
     eng.sync()
     kt_all = eng.kernel_times(last_runs=n_prof)
     res = eng.fetch(dense=False)
-    total_reads = sum_over_ranks(float(n_res))
+    total_reads = reduce(float(n_res), "sum")
     value = total_reads * args.steps / dt
     ms_step = dt / args.steps * 1e3
 
@@ -168,7 +233,7 @@ def main():
     dom = "pileup"
     alg_bytes = n_res * BYTES_PER_READ + n_cells * BYTES_PER_CELL
     achieved = alg_bytes / (kt[dom] * 1e-3) / 1e9
-    step_achieved = alg_bytes / (ms_step * 1e-3) / 1e9
+    step_achieved = alg_bytes / (dt_rank / args.steps) / 1e9
     traffic = None
     pmc = ROOT / "profiles" / "pmc_traffic.json"
     if pmc.exists():
@@ -179,13 +244,20 @@ def main():
                 traffic = d.get(dom)
         except Exception:
             traffic = None
+    kernels = kernel_rooflines(kt_all, n_res, n_cells, res.stats, cfg)
+
+    check = None
+    if rank == 0 and not args.no_check:
+        check = sample_check(eng, cfg, res)
+    eng.close()
+
+    pcie = None
+    if not args.no_pcie:
+        pcie = pcie_leg(args, cfg, seed, cdf, ref, shard, device, comm_ranks, barrier, reduce, make_comm)
 
     cpu = None
-    if rank == 0 and not args.no_cpu_baseline:
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(args, cfg, local_rank)
-    check = None
-    if rank == 0 and args.check:
-        check = sample_check(args, cfg, local_rank)
 
     if rank == 0:
         out = {
@@ -197,19 +269,22 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": ms_step,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "weak" if args.weak else "strong",
             "vs_baseline": None,
             "dtype": "u32",
             "data": "synthetic (SURVEY.md §8(d) generator, created in HBM by the device generator)",
+            "bit_exact": None if check is None else check["bit_exact"],
             "config": {
-                "workload": f"{workload_name(n_reads, n_cells)}: {n_reads / 1e6:g}M chrM reads x {n_cells / 1e3:g}k "
-                            f"cells per GPU, run params (q20, mapq30, dedup=alignment_and_fragment_length, "
-                            f"min_reads 1), L={args.read_len}",
-                "reads_per_gpu": n_res,
-                "cells_per_gpu": n_cells,
-                "payload_bytes_per_gpu": pay,
+                "workload": f"{workload_name(n_glob, nc_glob)}: {n_glob / 1e6:g}M chrM reads x {nc_glob / 1e3:g}k "
+                            f"cells{' per GPU' if args.weak else ' (one set, split by cell over the GPUs)'}, "
+                            f"run params (q20, mapq30, dedup=alignment_and_fragment_length, min_reads 1), "
+                            f"L={args.read_len}",
+                "reads_rank0": n_res,
+                "cells_rank0": n_cells,
+                "payload_bytes_rank0": pay,
                 "record_layout": args.record_layout,
-                "parallelism": f"cell-sharded x{world} (RCCL all-reduce of ref tallies)",
+                "parallelism": f"cell-sharded x{world} (RCCL all-reduce of ref tallies over {comm_ranks} ranks)",
+                "rank0_step_ms": dt_rank / args.steps * 1e3,
             },
             "roofline": {
                 "bound": "hbm",
@@ -222,16 +297,172 @@ def main():
                 "alg_bytes_per_launch": alg_bytes,
                 "step_achieved": step_achieved,
                 "step_frac": step_achieved / HBM_PEAK_GBS,
+                "kernels": kernels,
             },
             "stage_ms": {k: round(v, 4) for k, v in kt_all.items()},
+            "pcie": pcie,
+            "value_pcie": None if pcie is None else pcie["value"],
             "cpu_baseline": cpu,
-            "stats": res.stats,
+            "stats_rank0": res.stats,
             "sample_check": check,
         }
         print(json.dumps(out), flush=True)
-    eng.close()
     if dist is not None:
         dist.destroy_process_group()
+
+
+def kernel_rooflines(kt: dict, n: int, nc: int, stats: dict, cfg) -> dict:
+    """Each kernel's own algorithmic bytes over its HIP-event time."""
+    L = cfg.mito_len
+    nbins = (L + 7) // 8 + 1
+    kept = int(stats.get("filtered_reads", 0))
+    own = {
+        # barcode + flag per read, the H rows
+        "hist": 6 * n + 4 * nbins * nc,
+        # every column of every read (27 B), one 8-byte element per kept-or-duplicate read
+        # (the duplicates are a fraction of the valid reads: the kept reads bound it below)
+        "group_a": 27 * n + 8 * kept,
+        # 8-byte element in, 4-byte pileup element out
+        "group_b": 12 * kept,
+        # 4-byte element + one 64-byte record per kept read (an upper bound: kept reads
+        # below min_mapq are not gathered), the 16-bit result rows written once
+        "pileup": 68 * kept + ROW16_BYTES_PER_CELL * nc,
+        # the 16-bit depth row per cell
+        "median": 2 * L * nc,
+    }
+    out = {}
+    for k, b in own.items():
+        ms = kt.get(k, 0.0)
+        if ms > 0:
+            gbs = b / (ms * 1e-3) / 1e9
+            out[k] = {"alg_bytes": int(b), "ms": round(ms, 4), "GBps": round(gbs, 1),
+                      "frac": round(gbs / HBM_PEAK_GBS, 3)}
+    return out
+
+
+def sample_check(eng, cfg, res) -> dict:
+    """3 samples of 8 whole cells of the timed run (first, middle, last cells of the
+    rank) bit for bit against the oracle on exactly their reads, plus the run
+    statistics' consistency. Cells are independent, so a cell's rows depend only
+    on its own reads."""
+    from mgatk2_amd.engine import EngineConfig
+    from mgatk2_amd.shard import shard_soa
+    from oracle.oracle import oracle_run
+
+    t0 = time.perf_counter()
+    nc = cfg.n_cells
+    ranges = sorted({(0, min(8, nc)), (nc // 2, min(nc, nc // 2 + 8)), (max(0, nc - 8), nc)})
+    got = {r: eng.fetch_cells(*r) for r in ranges}
+    inputs = eng.download_inputs()
+    ok = True
+    bad = []
+    keys = ("counts", "tn5", "depth", "n_reads", "any_paired", "passed", "covered", "depth_sum", "depth_max",
+            "median_lo", "median_hi")
+    for (lo, hi), g in got.items():
+        sub, _ = shard_soa(inputs, lo, hi)
+        exp, _ = oracle_run(EngineConfig(**{**cfg.__dict__, "n_cells": hi - lo}), sub)
+        for k in keys:
+            if not np.array_equal(getattr(g, k), getattr(exp, k)):
+                ok = False
+                bad.append(f"{lo}-{hi}:{k}")
+    del inputs
+    st = res.stats
+    consistent = (st["filtered_reads"] == int(res.n_reads.sum()) and st["cells_passed"] == int(res.passed.sum())
+                  and st["n_barcodes"] == int((res.n_reads > 0).sum()) and st["error_bits"] == 0)
+    return {"bit_exact": bool(ok and consistent), "cells": [list(r) for r in ranges], "mismatches": bad,
+            "stats_consistent": bool(consistent), "seconds": round(time.perf_counter() - t0, 2)}
+
+
+def pcie_leg(args, cfg, seed, cdf, ref, shard, device, comm_ranks, barrier, reduce, make_comm) -> dict:
+    """SURVEY.md §8(d)'s engine metric: host SoA batches in pinned memory -> pushed
+    (H2D on the copy stream; with streaming on, each push runs the windows its reads
+    complete, overlapping the next batches' copies) -> mgp_run -> the 16-bit result
+    rows and per-cell statistics in pinned host memory. The rank's reads are the
+    same as the timed run's, in the dense packed layout a streaming producer emits
+    (records in BAM order: a batch is a contiguous payload range)."""
+    from mgatk2_amd.engine import Engine, EngineConfig, PinnedBuffer, Rows16
+    from mgatk2_amd.synth import ReadSoA
+
+    batch_list = [int(x) for x in str(args.batch_reads).split(",") if x.strip()]
+    scfg = EngineConfig(**{**cfg.__dict__})
+    eng = Engine(scfg, device=device)
+    eng.synth(seed, args.reads, cdf, ref, read_len=args.read_len, rec_align=64, pack=True, **shard)
+    n, pay = eng.resident()
+    col_bytes = n * (4 + 4 + 4 + 2 + 1 + 4 + 8)
+    hbuf = PinnedBuffer(col_bytes + pay + 4096)
+    off = [0]
+
+    def alloc(m, dt):
+        a = hbuf.array(m, dt, off[0])
+        off[0] = (off[0] + m * np.dtype(dt).itemsize + 63) & ~63
+        return a
+
+    host = eng.download_inputs(alloc=alloc)  # the producer's batches: pinned, BAM order
+    assert np.all(host.rec_off == 64 * np.arange(n, dtype=np.uint64))
+    L, nc = cfg.mito_len, cfg.n_cells
+    nw, W = eng.windows()
+    rbuf = PinnedBuffer(nc * L * 22 + nc * nw + 4096)
+    rows = Rows16(rbuf.array((nc, L, 8), np.uint16, 0), rbuf.array((nc, L, 2), np.uint16, nc * L * 16),
+                  rbuf.array((nc, L), np.uint16, nc * L * 20), rbuf.array((nc, nw), np.uint8, nc * L * 22), W)
+    if comm_ranks > 1:
+        make_comm(eng)  # every run all-reduces its tallies, as in the timed steps
+
+    def batches_for(bs):
+        """Batches of bs reads with batch-relative record offsets (dense records: the
+        producer writes them so)."""
+        out = []
+        for a in range(0, n, bs):
+            b = min(n, a + bs)
+            host.rec_off[a:b] = 64 * np.arange(b - a, dtype=np.uint64)
+            out.append(ReadSoA(host.start[a:b], host.bc[a:b], host.tlen[a:b], host.flag[a:b], host.mapq[a:b],
+                               host.span[a:b], host.rec_off[a:b], host.payload[64 * a:64 * b]))
+        return out
+
+    def one(batches, stream):
+        eng.set_streaming(stream)
+        eng.reset()
+        t0 = time.perf_counter()
+        for bt in batches:
+            eng.push(bt)
+        t_push = time.perf_counter() - t0
+        eng.run()
+        eng.fetch_rows16(0, nc, out=rows)
+        r = eng.fetch(dense=False)
+        return time.perf_counter() - t0, t_push, r
+
+    legs = []
+    for bs in batch_list:
+        batches = batches_for(bs)
+        one(batches, True)  # warmup (allocations)
+        for stream in (True, False):
+            ts = []
+            seg0 = eng.stream_info()[0]
+            for _ in range(args.pcie_steps):
+                barrier()
+                dt, t_push, r = one(batches, stream)
+                ts.append((dt, t_push))
+            segs = (eng.stream_info()[0] - seg0) // max(1, args.pcie_steps)
+            dt = min(t for t, _ in ts)
+            dt_max = reduce(dt, "max")
+            legs.append({"batch_reads": bs, "batches": len(batches), "streamed": stream, "segments": int(segs),
+                         "s": dt_max, "push_s": round(min(p for _, p in ts), 4),
+                         "value": reduce(float(n), "sum") / dt_max})
+    stats = r.stats
+    h2d = col_bytes + pay
+    d2h = nc * L * 22 + nc * nw + nc * 34 + L * 4 * 8  # rows, wide flags, per-cell arrays, tallies
+    best = legs[0]
+    eng.close()
+    return {
+        "value": best["value"],
+        "unit": "reads/s",
+        "what": "pinned host SoA batches -> H2D (streamed: windows run as their reads arrive) -> run -> 16-bit "
+                "count rows + per-cell stats in pinned host memory; max over ranks",
+        "h2d_bytes_rank0": h2d,
+        "d2h_bytes_rank0": d2h,
+        "link_GBps_rank0": round((h2d + d2h) / best["s"] / 1e9, 2),
+        "legs": legs,
+        "stats_total_reads_rank0": stats["total_reads"],
+    }
 
 
 def _sample_inputs(args, cfg, device):
@@ -249,34 +480,31 @@ def _sample_inputs(args, cfg, device):
 
 
 def cpu_baseline(args, cfg, device):
+    import platform
+
     from oracle.oracle import oracle_run
 
     scfg, soa = _sample_inputs(args, cfg, device)
     t0 = time.perf_counter()
     oracle_run(scfg, soa, dense=False)
     dt = time.perf_counter() - t0
+    cpu = platform.processor() or ""
+    try:
+        for line in Path("/proc/cpuinfo").read_text().splitlines():
+            if line.startswith("model name"):
+                cpu = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
     return {
         "value": soa.n / dt,
         "unit": "reads/s",
         "cores": 1,
         "kind": "port",
+        "cpu": cpu,
         "sample": f"{soa.n:,} reads x {scfg.n_cells} cells of the same generator (20k reads/cell, run params); "
                   f"oracle/mgp_oracle.c single-threaded, {dt:.1f}s",
     }
-
-
-def sample_check(args, cfg, device):
-    from mgatk2_amd.engine import Engine
-    from oracle.oracle import oracle_run
-
-    scfg, soa = _sample_inputs(args, cfg, device)
-    with Engine(scfg, device=device) as e:
-        e.push(soa)
-        r = e.finish()
-    x, _ = oracle_run(scfg, soa)
-    ok = all(np.array_equal(getattr(r, k), getattr(x, k)) for k in
-             ("counts", "tn5", "depth", "n_reads", "passed", "ref_tally", "median_lo", "median_hi"))
-    return {"reads": soa.n, "cells": scfg.n_cells, "bit_exact": bool(ok)}
 
 
 if __name__ == "__main__":

@@ -46,7 +46,8 @@
 extern "C" {
 #endif
 
-#define MGP_ABI_VERSION 2  /* 2: fixed seq/CIGAR offsets for reads <= 64 bases */
+#define MGP_ABI_VERSION 3  /* 2: fixed seq/CIGAR offsets for reads <= 64 bases;
+                              3: synth cell shards, cell-range and 16-bit fetches, streaming runs */
 
 /* ---- return codes (0 = success) ------------------------------------------ */
 #define MGP_OK               0
@@ -80,6 +81,12 @@ extern "C" {
 #define MGP_CFG_KEEP_TN5       0x1  /* keep Tn5 counts at positions of depth 0 (the unfiltered
                                        generate_pileup() view, pileup.py:100-124); off = the
                                        strand-filtered result the writers consume (pileup.py:151-152) */
+#define MGP_CFG_STREAM         0x2  /* streaming runs: each mgp_push_batch queues, behind its own
+                                       copies, the hot path of the position windows whose reads have
+                                       all arrived (coordinate order), so the copies of later batches
+                                       overlap the compute of earlier ones; mgp_run does the rest.
+                                       Set reserve_reads to the run's read count. Results are those of
+                                       a resident run (reads a segment cannot serve rerun it resident). */
 
 /* Engine configuration: the POD restatement of PipelineConfig
  * (src/core/config.py:77-114) restricted to what the hot path reads. */
@@ -286,7 +293,28 @@ typedef struct mgp_synth_params {
      * producer placement of mgp_place_records (include/mgpileup_host.h) */
     const uint64_t *rec_off;
     int64_t  payload_bytes;
+    /* optional cell shard of the global read set (cell_hi > cell_lo; the context's
+     * n_cells must be cell_hi - cell_lo): only the reads of cells [cell_lo, cell_hi)
+     * are kept, their barcode rebased to cell_lo, in BAM order; of the reads without
+     * a whitelisted barcode those with read index % shard_world == shard_rank are
+     * kept (shard_world = 0: none). rec_off, when given, places the kept reads
+     * (index in the shard). One seed, one global set: the shards of ranks 0..N-1
+     * over a partition of the cells are exactly the global set split by cell
+     * (processors.py:112-144's per-cell parallelism, one GPU per cell range). */
+    int32_t  cell_lo, cell_hi;
+    int32_t  shard_rank, shard_world;
 } mgp_synth_params;
+
+/* The pileup's 16-bit result rows, as the run leaves them in HBM (half the bytes of
+ * the u32 arrays of mgp_result). Exact wherever the cell's window is not `wide`
+ * (a cell window of more than 65535 reads: its 16-bit values saturate at 65535,
+ * the HDF5 form of writers.py:205-218; mgp_fetch_cells gives the exact values). */
+typedef struct mgp_rows16 {
+    uint16_t *counts;   /* [cells][mito_len][8]: A_fwd, A_rev, ... T_rev */
+    uint16_t *tn5;      /* [cells][mito_len][2]                          */
+    uint16_t *depth;    /* [cells][mito_len]                             */
+    uint8_t  *wide;     /* [cells][n_windows] (mgp_windows)              */
+} mgp_rows16;
 
 typedef struct mgp_ctx mgp_ctx;
 
@@ -332,6 +360,18 @@ int  mgp_sync(mgp_ctx *ctx);
  * the dense form of the per-cell result dicts (processors.py:41-51) and of the
  * stats dict (readers.py:193-199). */
 int  mgp_fetch(mgp_ctx *ctx, mgp_result *out);
+/* mgp_fetch for cells [lo, hi) only: every per-cell and per-position array holds
+ * hi - lo cells (cell lo first); ref_tally and stats are the run's. */
+int  mgp_fetch_cells(mgp_ctx *ctx, int32_t lo, int32_t hi, mgp_result *out);
+/* The 16-bit result rows of cells [lo, hi) (implies mgp_sync); NULL members are skipped. */
+int  mgp_fetch_rows16(mgp_ctx *ctx, int32_t lo, int32_t hi, mgp_rows16 *out);
+/* Position windows of the pileup (the `wide` flags' second dimension). */
+int  mgp_windows(mgp_ctx *ctx, int32_t *n_windows, int32_t *window_width);
+/* Streaming on (1) or off (0) for the next pushes (initially MGP_CFG_STREAM). */
+int  mgp_set_streaming(mgp_ctx *ctx, int on);
+/* Streaming: segments queued by pushes so far (all runs), and whether the last run
+ * finished a streamed run (0: it ran resident). */
+int  mgp_stream_info(mgp_ctx *ctx, int64_t *segments, int32_t *last_streamed);
 /* Convenience: mgp_run + mgp_fetch. */
 int  mgp_finish(mgp_ctx *ctx, mgp_result *out);
 

@@ -100,6 +100,11 @@ void mgp_host_buf_free(void *p);
 int mgp_txt_write_cells(const char *prefix, const uint32_t *counts, const uint32_t *depth, int64_t mito_len,
                         const int64_t *cells, int64_t n_write, const char *const *names, int level,
                         int n_threads, int append);
+/* The same from the engine's exact 16-bit rows (mgp_fetch_rows16 when no window is
+ * wide): half the bytes of the u32 form between device and host. */
+int mgp_txt_write_cells16(const char *prefix, const uint16_t *counts, const uint16_t *depth, int64_t mito_len,
+                          const int64_t *cells, int64_t n_write, const char *const *names, int level,
+                          int n_threads, int append);
 
 /* Write an engine batch as a coordinate-sorted BAM (test and benchmark inputs; the
  * inverse of mgp_bam_read_ref). References `ref_names`/`ref_lens`; every record goes

@@ -275,8 +275,10 @@ def txt_write_cells(prefix: str | Path, counts: np.ndarray, depth: np.ndarray, c
                     level: int = 6, n_threads: int = 0, append: bool = True) -> None:
     """Native txt formatter + parallel gzip (libmgphost.so `mgp_txt_write_cells`)."""
     lib = host_library()
-    counts = np.ascontiguousarray(counts, dtype=np.uint32)
-    depth = np.ascontiguousarray(depth, dtype=np.uint32)
+    # the engine's exact 16-bit rows are formatted as they are (no widening copy)
+    dt = np.uint16 if counts.dtype == np.uint16 and depth.dtype == np.uint16 else np.uint32
+    counts = np.ascontiguousarray(counts, dtype=dt)
+    depth = np.ascontiguousarray(depth, dtype=dt)
     cells = np.ascontiguousarray(cells, dtype=np.int64)
     L = depth.shape[-1]
     if counts.shape[-2:] != (L, 8) or counts.reshape(-1, L, 8).shape[0] != depth.reshape(-1, L).shape[0]:
@@ -286,8 +288,9 @@ def txt_write_cells(prefix: str | Path, counts: np.ndarray, depth: np.ndarray, c
     if len(names) != cells.size:
         raise ValueError("one name per written cell")
     arr = (C.c_char_p * max(1, len(names)))(*[n.encode() for n in names])
-    rc = lib.mgp_txt_write_cells(str(prefix).encode(), counts.ctypes.data, depth.ctypes.data, L, cells.ctypes.data,
-                                 cells.size, arr, int(level), int(n_threads or host_threads()), 1 if append else 0)
+    fn = lib.mgp_txt_write_cells16 if dt == np.uint16 else lib.mgp_txt_write_cells
+    rc = fn(str(prefix).encode(), counts.ctypes.data, depth.ctypes.data, L, cells.ctypes.data,
+            cells.size, arr, int(level), int(n_threads or host_threads()), 1 if append else 0)
     if rc != 0:
         raise OSError(_err())
 

@@ -68,15 +68,17 @@ bool gzip_member(const char* src, size_t n, int level, std::vector<uint8_t>& out
     return r == Z_STREAM_END;
 }
 
-// One group of cells -> 5 texts (coverage, A, C, G, T).
-void format_group(const uint32_t* counts, const uint32_t* depth, int64_t L, const int64_t* cells, int64_t c0,
+// One group of cells -> 5 texts (coverage, A, C, G, T). T: u32 rows, or the
+// engine's exact 16-bit rows (mgp_fetch_rows16 without wide windows).
+template <class T>
+void format_group(const T* counts, const T* depth, int64_t L, const int64_t* cells, int64_t c0,
                   int64_t c1, const char* const* names, Text* txt) {
     for (int64_t k = c0; k < c1; ++k) {
         const int64_t c = cells[k];
         const char* bc = names[k];
         const size_t bl = std::strlen(bc);
-        const uint32_t* d = depth + (size_t)c * (size_t)L;
-        const uint32_t* q = counts + (size_t)c * (size_t)L * 8;
+        const T* d = depth + (size_t)c * (size_t)L;
+        const T* q = counts + (size_t)c * (size_t)L * 8;
         for (int64_t p = 0; p < L; ++p) {
             const uint32_t dp = d[p];
             if (!dp) continue;
@@ -90,7 +92,7 @@ void format_group(const uint32_t* counts, const uint32_t* depth, int64_t L, cons
             w = put_u64(w, dp);
             *w++ = '\n';
             txt[0].n += (size_t)(w - s);
-            const uint32_t* e = q + (size_t)p * 8;
+            const T* e = q + (size_t)p * 8;
             for (int b = 0; b < 4; ++b) {
                 const uint32_t fw = e[2 * b], rv = e[2 * b + 1];
                 if (!(fw | rv)) continue;
@@ -112,13 +114,9 @@ void format_group(const uint32_t* counts, const uint32_t* depth, int64_t L, cons
     }
 }
 
-}  // namespace
-
-extern "C" {
-
-int mgp_txt_write_cells(const char* prefix, const uint32_t* counts, const uint32_t* depth, int64_t mito_len,
-                        const int64_t* cells, int64_t n_write, const char* const* names, int level, int n_threads,
-                        int append) {
+template <class T>
+int write_cells(const char* prefix, const T* counts, const T* depth, int64_t mito_len, const int64_t* cells,
+                int64_t n_write, const char* const* names, int level, int n_threads, int append) {
     mgp_host_err().clear();
     if (!prefix || (n_write > 0 && (!counts || !depth || !cells || !names)) || mito_len <= 0 || n_write < 0)
         return fail("bad arguments");
@@ -174,6 +172,22 @@ int mgp_txt_write_cells(const char* prefix, const uint32_t* counts, const uint32
     for (int i = 0; i < 5; ++i)
         if (std::fclose(f[i]) != 0 && rc == 0) rc = fail("close failed");
     return rc;
+}
+
+}  // namespace
+
+extern "C" {
+
+int mgp_txt_write_cells(const char* prefix, const uint32_t* counts, const uint32_t* depth, int64_t mito_len,
+                        const int64_t* cells, int64_t n_write, const char* const* names, int level, int n_threads,
+                        int append) {
+    return write_cells(prefix, counts, depth, mito_len, cells, n_write, names, level, n_threads, append);
+}
+
+int mgp_txt_write_cells16(const char* prefix, const uint16_t* counts, const uint16_t* depth, int64_t mito_len,
+                          const int64_t* cells, int64_t n_write, const char* const* names, int level, int n_threads,
+                          int append) {
+    return write_cells(prefix, counts, depth, mito_len, cells, n_write, names, level, n_threads, append);
 }
 
 }  // extern "C"

@@ -73,6 +73,10 @@ static int set_err(int code, const std::string& msg) {
 struct DevBuf {
     void* p = nullptr;
     size_t cap = 0;
+    DevBuf() = default;
+    DevBuf(const DevBuf&) = delete;
+    DevBuf& operator=(const DevBuf&) = delete;
+    ~DevBuf() { release(); }
     int ensure(size_t bytes, bool preserve = false, size_t used = 0, hipStream_t s = 0) {
         if (bytes <= cap) return MGP_OK;
         size_t ncap = std::max(bytes, cap + cap / 2);
@@ -129,6 +133,7 @@ struct mgp_ctx {
     DevBuf start, bc, tlen, flag, mapq, span, roff, payload;
     DevBuf roff32;          // u32 rec_off >> 6 (grouping pass A reads it when every offset fits, kOffR32)
     DevBuf roff_irregular;  // u32 words of the input check (k_bin_count): CHK_* bits, largest kept span
+    DevBuf order_bad;       // u32: a streaming push found reads out of coordinate order (k_check_order)
     int roff_mode = -1;     // pass A's offset source (kOffDense / kOffR32 / kOffR64), from the run's input check
     uint32_t read_bits = 0; // the input check's CHK_* bits of the resident reads
     bool no_spec = false;   // the speculative compact grouping failed on the resident reads (ERR_RESPEC)
@@ -147,6 +152,16 @@ struct mgp_ctx {
 
     ncclComm_t comm = nullptr;
     int nranks = 1;
+    unsigned long long* h_respec = nullptr;  // pinned: the ranks' all-reduced ERR_RESPEC count
+    bool rerunning = false;                  // mgp_sync is running the fallback rerun
+
+    // streaming runs (MGP_CFG_STREAM): pushes run the complete windows as segments
+    bool stream = false;
+    bool stream_off = false;   // the resident reads cannot stream (payload too large for compact elements)
+    bool seg_open = false;     // segments of the current run are queued (mgp_run finishes it)
+    int w_done = 0;            // windows [0, w_done) of the current run are queued
+    int64_t segments = 0;      // segments queued by pushes (all runs)
+    bool last_streamed = false;
 };
 
 // ---------------------------------------------------------------------------
@@ -174,6 +189,20 @@ __device__ __forceinline__ int64_t bin_threshold(int b, const Geom& g) {
     if (b >= g.nbins) return INT64_MAX;
     if (b == g.nb_reg) return g.L;
     return (int64_t)b * g.G;
+}
+
+// Streaming runs (MGP_CFG_STREAM) process the resident reads in segments of
+// complete position windows [seg_w0, seg_w1) while later batches are still on
+// their way (mgp_push_batch). A segment's start bins are [seg_lo_bin, seg_bhi):
+// the bins of its windows plus the halo bins of window seg_w0, i.e. the bins
+// whose reads can reach seg_w0 given the largest declared span of the reads of
+// the earlier segments (st->max_span when the segment starts: every read before
+// seg_w0 x W was checked by an earlier segment). Other bins count as empty.
+__device__ __forceinline__ int seg_lo_bin(int seg_w0, const Geom& g, const DevStats* st) {
+    if (seg_w0 <= 0) return 0;
+    const uint32_t ms = st->max_span;
+    const int R = (int)((ms + g.G - 1) / g.G) * g.G;
+    return win_lo_bin(seg_w0, R, g);
 }
 
 constexpr int kGroup = 64;  // cells per grouping bucket (pass A) and per pass-B workgroup
@@ -234,7 +263,7 @@ __global__ void __launch_bounds__(kHistBlock) k_bin_count(const int32_t* __restr
                                                           uint32_t* __restrict__ PG, int ngroups,
                                                           uint32_t* __restrict__ bin_lo,
                                                           uint32_t* __restrict__ bin_valid, uint32_t* __restrict__ ck,
-                                                          DevStats* st) {
+                                                          DevStats* st, int seg_w0, int seg_bhi) {
     extern __shared__ uint32_t hist[];  // [slice cells] counts, then cum[slice groups]
     __shared__ int64_t s_range[2];
     __shared__ uint32_t s_nvalid, s_bits;
@@ -251,7 +280,10 @@ __global__ void __launch_bounds__(kHistBlock) k_bin_count(const int32_t* __restr
     for (int c = threadIdx.x; c < ncs; c += blockDim.x) hist[c] = 0;
     if (threadIdx.x == 0) s_nvalid = 0, s_bits = 0;
     __syncthreads();
-    const int64_t blo = s_range[0], bhi = max(s_range[1], blo);
+    // a bin outside the segment counts no read (its bounds are still written: pass A
+    // takes a bin's upper bound from the next bin's lower one)
+    const bool in_seg = b < seg_bhi && b >= seg_lo_bin(seg_w0, g, st);
+    const int64_t blo = s_range[0], bhi = in_seg ? max(s_range[1], blo) : blo;
     if (first && threadIdx.x == 0) {
         bin_lo[b] = (uint32_t)blo;
         if (b == g.nbins - 1) bin_lo[g.nbins] = (uint32_t)n;
@@ -492,7 +524,7 @@ __global__ void __launch_bounds__(kGABlock, MGP_GA_WAVES) k_group_a(int64_t n, c
                                                     Geom g, int ngroups, int gbits, int min_mapq,
                                                     uint32_t* __restrict__ bucket_off, GElem* __restrict__ gel2,
                                                     uint32_t* __restrict__ first_read, uint32_t* __restrict__ ck,
-                                                    DevStats* st) {
+                                                    DevStats* st, int seg_w0, int seg_bhi) {
     static_assert(kOff != kOffSpec || kCompact, "the speculative check writes compact elements");
     constexpr bool kSpec = kOff == kOffSpec;
     if (__atomic_load_n(&st->err, __ATOMIC_RELAXED) & ERR_BOUNDS) return;  // unsorted input (k_bin_count)
@@ -536,6 +568,8 @@ __global__ void __launch_bounds__(kGABlock, MGP_GA_WAVES) k_group_a(int64_t n, c
         }
         if (lane == 0 && part == 0) bucket_off[(size_t)b * (ngroups + 1) + ngroups] = carry;
     }
+    // a bin outside the segment: empty buckets (written above), no reads
+    if (b >= seg_bhi || b < seg_lo_bin(seg_w0, g, st)) return;
     // cells whose first read is in this bin (k_scan_apply)
     const size_t fw = (size_t)(nc + 31) / 32;
     for (int x = threadIdx.x; x < (int)fw; x += blockDim.x) fbits[x] = F[(size_t)b * fw + x];
@@ -837,10 +871,10 @@ struct GCompact {
 // survives the duplicate marking (counted in n_reads, processors.py:22).
 template <class Tr>
 __device__ __forceinline__ uint32_t group_b_emit(const typename Tr::T& e, bool dup2, bool dup3, int mode, int unit,
-                                                 DedupAcc& acc, bool& keep) {
+                                                 DedupAcc& acc, bool& keep, bool cnt = true) {
     keep = mode == MGP_DEDUP_NONE ? true : mode == MGP_DEDUP_START ? !dup2 : !dup3;
-    acc.d2 += dup2;
-    acc.d3 += dup3;
+    acc.d2 += cnt & dup2;
+    acc.d3 += cnt & dup3;
     if (!keep) return PE_DUP;
     if (!Tr::mapq_ok(e)) return PE_KEEP;
     return Tr::pile(e, unit);
@@ -879,7 +913,7 @@ __device__ __forceinline__ void group_b_rank(const typename Tr::T* __restrict__ 
                                              uint32_t* cnt, int lane, unsigned long long lt, typename Tr::T* stage,
                                              const uint32_t* cbase, const uint32_t* cstart, int mode, int unit,
                                              uint32_t* __restrict__ pel, DedupAcc& acc, uint32_t* s_ndup,
-                                             uint32_t* s_nunp, DevStats* st) {
+                                             uint32_t* s_nunp, DevStats* st, bool count_dups) {
     using T = typename Tr::T;
     for (uint32_t k = k0; k < k1; k += kWave) {
         const uint32_t j = k + lane;
@@ -917,7 +951,7 @@ __device__ __forceinline__ void group_b_rank(const typename Tr::T* __restrict__ 
                     }
                 }
                 bool keep;
-                pel[dest] = group_b_emit<Tr>(e, dup2, dup3, mode, unit, acc, keep);
+                pel[dest] = group_b_emit<Tr>(e, dup2, dup3, mode, unit, acc, keep, count_dups);
                 cell_tally<true, Tr>(true, lc, keep, e, s_ndup, s_nunp, st);
             }
         }
@@ -945,7 +979,8 @@ __global__ void __launch_bounds__(kBlock, Tr::kWaves) k_group_b(const typename T
                                                     const uint32_t* __restrict__ O, Geom g, int ngroups, int rb,
                                                     int mode, int unit, uint32_t* __restrict__ pel,
                                                     uint8_t* __restrict__ any_paired,
-                                                    unsigned long long* __restrict__ dup_part, DevStats* st) {
+                                                    unsigned long long* __restrict__ dup_part, DevStats* st,
+                                                    int cnt_lo) {
     using T = typename Tr::T;
     constexpr bool kCompact = sizeof(T) == 8;
     if (__atomic_load_n(&st->err, __ATOMIC_RELAXED) & ERR_BOUNDS) return;  // unsorted input (k_bin_count)
@@ -984,6 +1019,9 @@ __global__ void __launch_bounds__(kBlock, Tr::kWaves) k_group_b(const typename T
             int be = b;
             spre[0] = 0;
             while (be < B1) {
+                // a streaming segment's halo bins (below cnt_lo, counted by an earlier
+                // segment) never share a step with its own bins
+                if (be == cnt_lo && be > b) break;
                 const uint32_t sz = bsz[be - B0];
                 if (tot + sz > (uint32_t)kStageB) break;
                 if (kCompact && be - b >= kCompactBins) break;  // starts compared mod 256
@@ -1031,7 +1069,7 @@ __global__ void __launch_bounds__(kBlock, Tr::kWaves) k_group_b(const typename T
                 wcnt[0][lane] = cbase[lane];
                 __builtin_amdgcn_wave_barrier();
                 group_b_rank<false, Tr>(gel2, bst[b - B0], bst[b - B0] + bsz[b - B0], wcnt[0], lane, lt, nullptr,
-                                    nullptr, nullptr, mode, unit, pel, acc, s_ndup, s_nunp, st);
+                                    nullptr, nullptr, mode, unit, pel, acc, s_ndup, s_nunp, st, b >= cnt_lo);
                 __builtin_amdgcn_wave_barrier();
                 cbase[lane] = wcnt[0][lane];
             }
@@ -1095,6 +1133,7 @@ __global__ void __launch_bounds__(kBlock, Tr::kWaves) k_group_b(const typename T
         const int nbe = nb0 < B1 ? plan(nb0) : nb0;  // (its barrier also completes the stage)
         if (nb0 >= B1) __syncthreads();
         const uint32_t ntot = nbe > nb0 ? load(nb0, nbe) : 0u;
+        const bool cnt = b >= cnt_lo;  // the step's duplicates count (not a halo step)
         // write-out with duplicate marking: equal starts of a cell's run sit just
         // before t, in BAM order; a cell has one run in the stage, so an element of
         // another cell ends the walk. The element and its kLook predecessors are
@@ -1143,7 +1182,7 @@ __global__ void __launch_bounds__(kBlock, Tr::kWaves) k_group_b(const typename T
                 const int lc = Tr::lcell(xs[q]);
                 bool keep = false;
                 if (act) {
-                    const uint32_t pv = group_b_emit<Tr>(xs[q], d2[q], d3[q], mode, unit, acc, keep);
+                    const uint32_t pv = group_b_emit<Tr>(xs[q], d2[q], d3[q], mode, unit, acc, keep, cnt);
                     if (MGP_ABL_B < 2 || pv == 7u) pel[cbase[lc] + (t - cstart[lc])] = pv;
                 }
                 cell_tally<kTrack, Tr>(act, lc, keep, xs[q], s_ndup, s_nunp, st);
@@ -1175,7 +1214,7 @@ __global__ void __launch_bounds__(kBlock, Tr::kWaves) k_group_b(const typename T
             const int lc = Tr::lcell(x);
             bool keep = false;
             if (act) {
-                const uint32_t pv = group_b_emit<Tr>(x, dup2, dup3, mode, unit, acc, keep);
+                const uint32_t pv = group_b_emit<Tr>(x, dup2, dup3, mode, unit, acc, keep, cnt);
                 if (MGP_ABL_B < 2 || pv == 7u) pel[cbase[lc] + (t - cstart[lc])] = pv;
             }
             cell_tally<kTrack, Tr>(act, lc, keep, x, s_ndup, s_nunp, st);
@@ -1763,7 +1802,8 @@ __global__ void __launch_bounds__(kBlock, MGP_PILEUP_WAVES) k_pileup(
     const uint32_t* __restrict__ O, Out16 o16, uint32_t* __restrict__ counts, uint32_t* __restrict__ tn5,
     uint32_t* __restrict__ depth, uint32_t* __restrict__ n_reads, uint8_t* __restrict__ any_paired, int pair_mode,
     uint32_t* __restrict__ covered, unsigned long long* __restrict__ dsum,
-    uint32_t* __restrict__ dmax, uint32_t* __restrict__ tally_part, DevStats* st) {
+    uint32_t* __restrict__ dmax, uint32_t* __restrict__ tally_part, DevStats* st, int w_base,
+    const uint32_t* __restrict__ ck) {
     extern __shared__ __align__(16) uint32_t tile[];  // [Wp][4] A, C, G, T, then [Wp] Tn5 (fwd | rev << 16)
     uint32_t* t5 = tile + 4 * g.Wp;
     if (__atomic_load_n(&st->err, __ATOMIC_RELAXED) & ERR_BOUNDS) return;  // unsorted input (k_bin_count)
@@ -1771,8 +1811,11 @@ __global__ void __launch_bounds__(kBlock, MGP_PILEUP_WAVES) k_pileup(
     __shared__ uint32_t r_cov[4], r_max[4], r_keep[4];
     __shared__ unsigned long long r_sum[4];
 
-    const int k = blockIdx.y;
+    const int k = w_base + (int)blockIdx.y;  // window (a streaming segment's windows start at w_base)
     const int chunk = blockIdx.x;
+    // pair_mode < 0 (streaming): every read paired iff the input check saw only paired
+    // reads (a mix reruns the run resident, ERR_RESPEC)
+    if (pair_mode < 0) pair_mode = (ck[0] & CHK_PAIRED) && !(ck[0] & CHK_UNPAIRED) ? 1 : 0;
     Win w;
     w.w0 = k * g.W;
     w.wlen = min(g.W, g.L - w.w0);
@@ -2195,7 +2238,7 @@ __global__ void __launch_bounds__(kBlock) k_median(Geom g, int min_reads, const 
 __global__ void __launch_bounds__(1024) k_run_stats(const uint32_t* __restrict__ n_reads,
                                                     const uint8_t* __restrict__ passed, int nc,
                                                     const unsigned long long* __restrict__ dup_part, int nparts,
-                                                    DevStats* st) {
+                                                    DevStats* st, int with_dups) {
     __shared__ unsigned long long red[5][1024 / kWave];
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     unsigned long long a = 0, b = 0, c = 0, d = 0, e = 0;
@@ -2228,6 +2271,7 @@ __global__ void __launch_bounds__(1024) k_run_stats(const uint32_t* __restrict__
         if (threadIdx.x == 0) st->filtered = t;
         else if (threadIdx.x == 1) st->n_barcodes = t;
         else if (threadIdx.x == 2) st->cells_passed = t;
+        else if (!with_dups) (void)0;  // a streaming run's segments accumulated them (k_dup_accum)
         else if (threadIdx.x == 3) st->dup_pos = t;
         else st->dup_len = t;
     }
@@ -2247,10 +2291,12 @@ __global__ void k_tally_reduce(const uint32_t* __restrict__ part, int nchunks, i
 // mgp_fetch: the 16-bit result rows widened into the u32 arrays the caller
 // receives (drained windows already hold their exact u32 rows). One thread per
 // (cell, position).
-__global__ void __launch_bounds__(kBlock) k_expand(Geom g, int64_t npos, Out16 o16, uint32_t* __restrict__ counts,
-                                                   uint32_t* __restrict__ tn5, uint32_t* __restrict__ depth) {
-    const int64_t P = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-    if (P >= npos) return;
+__global__ void __launch_bounds__(kBlock) k_expand(Geom g, int64_t p0, int64_t npos, Out16 o16,
+                                                   uint32_t* __restrict__ counts, uint32_t* __restrict__ tn5,
+                                                   uint32_t* __restrict__ depth) {
+    const int64_t x = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (x >= npos) return;
+    const int64_t P = p0 + x;  // (cell, position) index of the cell range's first position p0
     const int64_t c = P / g.L, p = P - c * g.L;
     if (o16.wide[c * g.nwin + p / g.W]) return;
     if (counts) {
@@ -2276,8 +2322,13 @@ __global__ void k_add_u64(uint64_t* __restrict__ a, int64_t n, uint64_t add) {
 __global__ void k_run_init(int nc, int64_t nF, uint32_t* __restrict__ covered, unsigned long long* __restrict__ dsum,
                            uint32_t* __restrict__ dmax, uint32_t* __restrict__ n_reads, uint8_t* __restrict__ any_paired,
                            uint32_t* __restrict__ first_read, uint32_t* __restrict__ F, uint32_t* __restrict__ ck,
-                           DevStats* st) {
+                           DevStats* st, int what) {
+    // what: 1 the run's state (per-cell counters, check words, stats), 2 the first-bin
+    // bits F (every segment of a streaming run; the run state only at its first)
     const int64_t i0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x, step = (int64_t)gridDim.x * blockDim.x;
+    if (what & 2)
+        for (int64_t i = i0; i < nF; i += step) F[i] = 0u;
+    if (!(what & 1)) return;
     for (int64_t i = i0; i < nc; i += step) {
         covered[i] = 0u;
         dsum[i] = 0ull;
@@ -2286,7 +2337,6 @@ __global__ void k_run_init(int nc, int64_t nF, uint32_t* __restrict__ covered, u
         any_paired[i] = 0u;
         first_read[i] = 0xFFFFFFFFu;
     }
-    for (int64_t i = i0; i < nF; i += step) F[i] = 0u;
     if (i0 == 0) {
         ck[0] = 0u;
         ck[1] = 0u;
@@ -2325,11 +2375,61 @@ __global__ void k_check_inputs(const uint64_t* __restrict__ roff, const uint16_t
     }
 }
 
-__global__ void k_check_stats(const uint32_t* __restrict__ ck, DevStats* st) {
+// spec: the grouping took the speculative compact path without the host's look at
+// the flag bits (streaming segments): reads it cannot serve make the run rerun resident.
+// max_span is a running maximum (a streaming run's segments accumulate it).
+__global__ void k_check_stats(const uint32_t* __restrict__ ck, DevStats* st, int spec) {
     if (threadIdx.x == 0) {
-        st->max_span = ck[1];
-        if (ck[0] & CHK_UNSORTED) atomicOr(&st->err, ERR_UNSORTED);
+        const uint32_t b = ck[0];
+        st->max_span = max(st->max_span, ck[1]);
+        if (b & CHK_UNSORTED) atomicOr(&st->err, ERR_UNSORTED);
+        if (spec && ((b & (CHK_FULL | CHK_NOSEQ)) || ((b & CHK_PAIRED) && (b & CHK_UNPAIRED))))
+            atomicOr(&st->err, ERR_RESPEC);
     }
+}
+
+// a streaming segment's duplicate counts into the run's stats (k_run_stats takes
+// them from the partials of a resident run's one pass B)
+__global__ void __launch_bounds__(256) k_dup_accum(const unsigned long long* __restrict__ dup_part, int nparts,
+                                                    DevStats* st) {
+    __shared__ unsigned long long red[2][256 / kWave];
+    unsigned long long d = 0, e = 0;
+    for (int i = threadIdx.x; i < nparts; i += 256) {
+        d += dup_part[2 * (size_t)i];
+        e += dup_part[2 * (size_t)i + 1];
+    }
+    d = wave_sum(d);
+    e = wave_sum(e);
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    if (lane == 0) {
+        red[0][wid] = d;
+        red[1][wid] = e;
+    }
+    __syncthreads();
+    if (threadIdx.x < 2) {
+        unsigned long long t = 0;
+        for (int w = 0; w < 256 / kWave; ++w) t += red[threadIdx.x][w];
+        if (t) atomicAdd(threadIdx.x == 0 ? &st->dup_pos : &st->dup_len, t);
+    }
+}
+
+// Streaming pushes: coordinate order of a pushed batch, and against the batch before
+// (a segment sees only the start bins it runs, so a read out of order outside them
+// would go unnoticed); the flag stays set until the resident set is replaced.
+__global__ void k_check_order(const int32_t* __restrict__ start, int64_t i0, int64_t i1, uint32_t* __restrict__ bad) {
+    const int64_t i = i0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const bool uns = i < i1 && i > 0 && start[i] < start[i - 1];
+    if (__ballot(uns) && (threadIdx.x & 63) == 0) atomicOr(bad, 1u);
+}
+
+__global__ void k_order_err(const uint32_t* __restrict__ bad, DevStats* st) {
+    if (threadIdx.x == 0 && *bad) atomicOr(&st->err, ERR_UNSORTED);
+}
+
+// the run's ERR_RESPEC as a count in the all-reduced buffer (slot after the
+// tallies): every rank then sees whether any rank has to rerun, and all do
+__global__ void k_respec_slot(const DevStats* st, unsigned long long* slot) {
+    if (threadIdx.x == 0) *slot = (st->err & ERR_RESPEC) ? 1ull : 0ull;
 }
 
 // ---------------------------------------------------------------------------
@@ -2390,7 +2490,7 @@ int mgp_open(const mgp_config* cfg, int hip_device, mgp_ctx** out) {
     if (cfg->mito_len <= 0 || cfg->mito_len > (1 << 24)) return set_err(MGP_E_INVALID, "mito_len out of range");
     if (cfg->n_cells < 0) return set_err(MGP_E_INVALID, "n_cells < 0");
     if (cfg->dedup_mode < 0 || cfg->dedup_mode > 2) return set_err(MGP_E_INVALID, "dedup_mode out of range");
-    if (cfg->flags & ~MGP_CFG_KEEP_TN5) return set_err(MGP_E_INVALID, "unknown config.flags bits");
+    if (cfg->flags & ~(MGP_CFG_KEEP_TN5 | MGP_CFG_STREAM)) return set_err(MGP_E_INVALID, "unknown config.flags bits");
     int ndev = 0;
     HIP_TRY(hipGetDeviceCount(&ndev));
     if (hip_device < 0 || hip_device >= ndev)
@@ -2400,6 +2500,7 @@ int mgp_open(const mgp_config* cfg, int hip_device, mgp_ctx** out) {
     mgp_ctx* ctx = new mgp_ctx();
     ctx->cfg = *cfg;
     ctx->dev = hip_device;
+    ctx->stream = (cfg->flags & MGP_CFG_STREAM) != 0;
     int r = configure_geometry(ctx);
     if (r != MGP_OK) {
         delete ctx;
@@ -2448,8 +2549,13 @@ int mgp_open(const mgp_config* cfg, int hip_device, mgp_ctx** out) {
     HIP_TRY(hipEventCreateWithFlags(&ctx->ev_bits, hipEventDisableTiming));
     HIP_TRY(hipHostMalloc((void**)&ctx->h_bits, 8, hipHostMallocDefault));
     HIP_TRY(hipHostMalloc((void**)&ctx->host_stats, sizeof(DevStats), hipHostMallocDefault));
+    HIP_TRY(hipHostMalloc((void**)&ctx->h_respec, 8, hipHostMallocDefault));
+    *ctx->h_respec = 0ull;
     *ctx->host_stats = DevStats{};
     MGP_TRY(ctx->roff_irregular.ensure(8));
+    MGP_TRY(ctx->order_bad.ensure(4));
+    HIP_TRY(hipMemsetAsync(ctx->order_bad.p, 0, 4, ctx->s_copy));
+    HIP_TRY(hipEventRecord(ctx->ev_copy, ctx->s_copy));
     for (int r = 0; r < mgp_ctx::kRing; ++r)
         for (int s = 0; s < ST_N; ++s) {
             HIP_TRY(hipEventCreate(&ctx->ev[r][s][0]));
@@ -2480,7 +2586,7 @@ void mgp_close(mgp_ctx* ctx) {
     if (ctx->comm) ncclCommDestroy(ctx->comm);
     DevBuf* bufs[] = {&ctx->start,     &ctx->bc,        &ctx->tlen,     &ctx->flag,       &ctx->mapq,
                       &ctx->span,      &ctx->roff,      &ctx->payload,  &ctx->bin_start,  &ctx->gel2,
-                      &ctx->roff32,    &ctx->roff_irregular, &ctx->dup_part,
+                      &ctx->roff32,    &ctx->roff_irregular, &ctx->dup_part, &ctx->order_bad,
                       &ctx->H,         &ctx->P,         &ctx->cell_cnt, &ctx->cell_base,  &ctx->pel,
                       &ctx->PG,        &ctx->F,
                       &ctx->tally_part, &ctx->tally,   &ctx->n_reads,    &ctx->any_paired,
@@ -2499,16 +2605,36 @@ void mgp_close(mgp_ctx* ctx) {
     (void)hipEventDestroy(ctx->ev_bits);
     if (ctx->h_bits) (void)hipHostFree(ctx->h_bits);
     if (ctx->host_stats) (void)hipHostFree(ctx->host_stats);
+    if (ctx->h_respec) (void)hipHostFree(ctx->h_respec);
     (void)hipStreamDestroy(ctx->s_comp);
     (void)hipStreamDestroy(ctx->s_copy);
     (void)hipStreamDestroy(ctx->s_side);
     delete ctx;
 }
 
+// Finish what the compute streams have queued (buffers are about to be replaced).
+static int drain_compute(mgp_ctx* ctx) {
+    HIP_TRY(hipSetDevice(ctx->dev));
+    HIP_TRY(hipStreamSynchronize(ctx->s_comp));
+    HIP_TRY(hipStreamSynchronize(ctx->s_side));
+    return MGP_OK;
+}
+
+// A streaming run in progress is abandoned (the resident set is replaced).
+static int drain_stream(mgp_ctx* ctx) {
+    MGP_TRY(drain_compute(ctx));
+    ctx->seg_open = false;
+    ctx->w_done = 0;
+    ctx->stream_off = false;
+    return MGP_OK;
+}
+
 static int ensure_inputs(mgp_ctx* ctx, int64_t n_total, int64_t pay_total, bool preserve) {
     const size_t n = (size_t)n_total;
     const size_t used = preserve ? (size_t)ctx->n : 0;
     hipStream_t s = ctx->s_copy;
+    // growing replaces a buffer that queued kernels (a streaming run's segments) may read
+    if (ctx->start.cap < n * 4 || ctx->payload.cap < (size_t)pay_total + 256) MGP_TRY(drain_compute(ctx));
     MGP_TRY(ctx->start.ensure(n * 4, preserve, used * 4, s));
     MGP_TRY(ctx->bc.ensure(n * 4, preserve, used * 4, s));
     MGP_TRY(ctx->tlen.ensure(n * 4, preserve, used * 4, s));
@@ -2520,6 +2646,8 @@ static int ensure_inputs(mgp_ctx* ctx, int64_t n_total, int64_t pay_total, bool 
     MGP_TRY(ctx->payload.ensure((size_t)pay_total + 256, preserve, preserve ? (size_t)ctx->pay : 0, s));
     return MGP_OK;
 }
+
+static int stream_segments(mgp_ctx* ctx, int64_t last_start);
 
 int mgp_push_batch(mgp_ctx* ctx, const mgp_batch* b) {
     if (!ctx || !b) return set_err(MGP_E_INVALID, "null ctx/batch");
@@ -2548,11 +2676,19 @@ int mgp_push_batch(mgp_ctx* ctx, const mgp_batch* b) {
         k_add_u64<<<blocks_for(nb), kBlock, 0, s>>>(ctx->roff.as<uint64_t>() + n0, nb, (uint64_t)pay0);
         HIP_TRY(hipGetLastError());
     }
+    if (ctx->stream) {
+        k_check_order<<<blocks_for(nb), kBlock, 0, s>>>(ctx->start.as<int32_t>(), n0, n0 + nb,
+                                                        ctx->order_bad.as<uint32_t>());
+        HIP_TRY(hipGetLastError());
+    }
     HIP_TRY(hipEventRecord(ctx->ev_copy, s));
     ctx->n = n0 + nb;
     ctx->pay = pay0 + b->payload_bytes;
     ctx->ran = false;
     ctx->no_spec = false;
+    // streaming: the windows this batch completes go through the hot path now,
+    // behind its copies, while the caller pushes the next batch
+    if (ctx->stream) MGP_TRY(stream_segments(ctx, (int64_t)b->start[nb - 1]));
     return MGP_OK;
 }
 
@@ -2561,10 +2697,15 @@ int mgp_reset(mgp_ctx* ctx) {
     HIP_TRY(hipSetDevice(ctx->dev));
     HIP_TRY(hipStreamSynchronize(ctx->s_copy));
     HIP_TRY(hipStreamSynchronize(ctx->s_comp));
+    HIP_TRY(hipMemsetAsync(ctx->order_bad.p, 0, 4, ctx->s_copy));
+    HIP_TRY(hipEventRecord(ctx->ev_copy, ctx->s_copy));
     ctx->n = 0;
     ctx->pay = 0;
     ctx->ran = false;
     ctx->no_spec = false;
+    ctx->seg_open = false;
+    ctx->w_done = 0;
+    ctx->stream_off = false;
     return MGP_OK;
 }
 
@@ -2577,7 +2718,10 @@ int mgp_resident(mgp_ctx* ctx, int64_t* n_reads, int64_t* payload_bytes) {
 
 static int ensure_run_buffers(mgp_ctx* ctx) {
     const Geom& g = ctx->g;
-    const size_t n = (size_t)std::max<int64_t>(ctx->n, 1);
+    // a streaming run sizes the per-read scratch for the announced read count at once
+    // (growing it between segments would wait for the queued ones)
+    const size_t n = (size_t)std::max<int64_t>(std::max<int64_t>(ctx->n, ctx->stream ? ctx->cfg.reserve_reads : 0), 1);
+    if (ctx->pel.cap < n * 4 || ctx->gel2.cap < n * sizeof(GElem)) MGP_TRY(drain_compute(ctx));
     const size_t nc = (size_t)std::max(g.nc, 1);
     const size_t L = (size_t)g.L;
     MGP_TRY(ctx->bin_start.ensure((size_t)(g.nbins + 1) * 4));
@@ -2593,7 +2737,7 @@ static int ensure_run_buffers(mgp_ctx* ctx) {
     MGP_TRY(ctx->bin_base.ensure((size_t)(g.nbins + 1) * 4));
     MGP_TRY(ctx->bucket_off.ensure((size_t)g.nbins * ((nc + kGroup - 1) / kGroup + 1) * 4));
     MGP_TRY(ctx->tally_part.ensure((size_t)std::max(g.nchunks, 1) * L * 16));
-    MGP_TRY(ctx->tally.ensure(L * 4 * 8));
+    MGP_TRY(ctx->tally.ensure(L * 4 * 8 + 8));  // + the all-reduced ERR_RESPEC slot
     MGP_TRY(ctx->n_reads.ensure(nc * 4));
     MGP_TRY(ctx->any_paired.ensure(nc));
     MGP_TRY(ctx->passed.ensure(nc));
@@ -2625,208 +2769,240 @@ static Out16 out16_of(mgp_ctx* ctx) {
 
 // Stage events: each is a marker between two kernels of the stream (about 11 us
 // of idle GPU at a stage boundary on MI355X), so mgp_set_stage_timing can keep the
-// pileup's only.
-#define STAGE_ON(st) (ctx->stage_all || (st) == ST_PILEUP)
+// pileup's only. A streaming segment (slot < 0) records none.
+#define STAGE_ON(st) (slot >= 0 && (ctx->stage_all || (st) == ST_PILEUP))
 #define STAGE_BEGIN(st) \
     if (STAGE_ON(st)) { HIP_TRY(hipEventRecord(ctx->ev[slot][st][0], s)); ctx->stage_ran[slot][st] = true; }
 #define STAGE_END(st) \
     if (STAGE_ON(st)) HIP_TRY(hipEventRecord(ctx->ev[slot][st][1], s))
 
-int mgp_run(mgp_ctx* ctx) {
-    if (!ctx) return set_err(MGP_E_INVALID, "null ctx");
-    HIP_TRY(hipSetDevice(ctx->dev));
-    MGP_TRY(ensure_run_buffers(ctx));
+// One segment of a run: the resident reads whose start bins lie in the segment
+// through the input check, the histogram, the scan, both grouping passes and the
+// pileup of windows [w0, w1). A resident run is one segment over every window.
+struct Seg {
+    int w0, w1;   // pileup windows
+    int bhi;      // start bins [seg_lo_bin(w0), bhi) (nbins: through the overflow bin)
+    bool first;   // the run's first segment: zero the run's state
+    bool stream;  // a streaming segment: speculative compact grouping, no host wait
+};
+
+static int run_segment(mgp_ctx* ctx, const Seg& sg, int slot, int& dup_parts, int& pair_mode) {
     const Geom g = ctx->g;
     const int64_t n = ctx->n;
     const int nc = g.nc;
     hipStream_t s = ctx->s_comp;
     HIP_TRY(hipStreamWaitEvent(s, ctx->ev_copy, 0));
-    const int slot = (int)(ctx->runs % mgp_ctx::kRing);
-    for (int i = 0; i < ST_N; ++i) ctx->stage_ran[slot][i] = false;
     DevStats* st = ctx->stats.as<DevStats>();
+    dup_parts = 0;
+    pair_mode = 0;
     if (nc > 0) {  // the run's per-cell counters, stats, check words and first-bin bits in one launch
         const int64_t nF = (int64_t)g.nbins * ((nc + 31) / 32);
         k_run_init<<<std::max(1u, std::min(1024u, blocks_for(std::max<int64_t>(nc, nF)))), kBlock, 0, s>>>(
             nc, nF, ctx->covered.as<uint32_t>(), ctx->dsum.as<unsigned long long>(), ctx->dmax.as<uint32_t>(),
             ctx->n_reads.as<uint32_t>(), ctx->any_paired.as<uint8_t>(), ctx->first_read.as<uint32_t>(),
-            ctx->F.as<uint32_t>(), ctx->roff_irregular.as<uint32_t>(), st);
+            ctx->F.as<uint32_t>(), ctx->roff_irregular.as<uint32_t>(), st, sg.first ? 3 : 2);
         HIP_TRY(hipGetLastError());
     } else {
-        HIP_TRY(hipMemsetAsync(st, 0, sizeof(DevStats), s));
+        if (sg.first) HIP_TRY(hipMemsetAsync(st, 0, sizeof(DevStats), s));
+        return MGP_OK;
     }
-
-    if (nc > 0) {
-        const int ngroups = (nc + kGroup - 1) / kGroup;
-        // 1. per (start bin, cell) histogram + per (bin, part, group) counts + bin bounds, and
-        // the flag bits of the input check (pairedness / SEQ mix, record layout). They travel
-        // to pinned host memory while the scan runs; the host picks the grouping and pileup
-        // variants from them below.
-        STAGE_BEGIN(ST_HIST);
-        if (n == 0) HIP_TRY(hipMemsetAsync(ctx->H.p, 0, (size_t)(g.nbins + 1) * nc * 4, s));
-        if (n == 0) HIP_TRY(hipMemsetAsync(ctx->bin_start.p, 0, (size_t)(g.nbins + 1) * 4, s));
-        if (n > 0) {
-            // cells per slice: whole 64-cell groups, counts + group totals within the LDS budget
-            int lds_cells = ctx->lds_hist_max_cells / (kGroup + 1) * kGroup;
-            if (ctx->hist_slice_cells > 0) lds_cells = std::min(lds_cells, ctx->hist_slice_cells);
-            const int slice = nc <= lds_cells ? nc : lds_cells;
-            const int nslices = (nc + slice - 1) / slice;
-            const size_t lds = ((size_t)slice + (slice + kGroup - 1) / kGroup) * 4;
-            k_bin_count<<<dim3((unsigned)g.nbins, (unsigned)nslices), kHistBlock, lds, s>>>(
-                ctx->start.as<int32_t>(), ctx->bc.as<int32_t>(), ctx->flag.as<uint16_t>(), n, g, slice,
-                ctx->H.as<uint32_t>(), ctx->PG.as<uint32_t>(), ngroups, ctx->bin_start.as<uint32_t>(),
-                ctx->bin_valid.as<uint32_t>(), ctx->roff_irregular.as<uint32_t>(), st);
-            HIP_TRY(hipGetLastError());
+    const int ngroups = (nc + kGroup - 1) / kGroup;
+    // 1. per (start bin, cell) histogram + per (bin, part, group) counts + bin bounds, and
+    // the flag bits of the input check (pairedness / SEQ mix, record layout). They travel
+    // to pinned host memory while the scan runs; the host picks the grouping and pileup
+    // variants from them below (a streaming segment takes the speculative variants and
+    // leaves the check to the device).
+    STAGE_BEGIN(ST_HIST);
+    if (n == 0) HIP_TRY(hipMemsetAsync(ctx->H.p, 0, (size_t)(g.nbins + 1) * nc * 4, s));
+    if (n == 0) HIP_TRY(hipMemsetAsync(ctx->bin_start.p, 0, (size_t)(g.nbins + 1) * 4, s));
+    if (n > 0) {
+        // cells per slice: whole 64-cell groups, counts + group totals within the LDS budget
+        int lds_cells = ctx->lds_hist_max_cells / (kGroup + 1) * kGroup;
+        if (ctx->hist_slice_cells > 0) lds_cells = std::min(lds_cells, ctx->hist_slice_cells);
+        const int slice = nc <= lds_cells ? nc : lds_cells;
+        const int nslices = (nc + slice - 1) / slice;
+        const size_t lds = ((size_t)slice + (slice + kGroup - 1) / kGroup) * 4;
+        k_bin_count<<<dim3((unsigned)g.nbins, (unsigned)nslices), kHistBlock, lds, s>>>(
+            ctx->start.as<int32_t>(), ctx->bc.as<int32_t>(), ctx->flag.as<uint16_t>(), n, g, slice,
+            ctx->H.as<uint32_t>(), ctx->PG.as<uint32_t>(), ngroups, ctx->bin_start.as<uint32_t>(),
+            ctx->bin_valid.as<uint32_t>(), ctx->roff_irregular.as<uint32_t>(), st, sg.w0, sg.bhi);
+        HIP_TRY(hipGetLastError());
+        if (!sg.stream) {
             HIP_TRY(hipMemcpyAsync(ctx->h_bits, ctx->roff_irregular.p, 8, hipMemcpyDeviceToHost, s));
             HIP_TRY(hipEventRecord(ctx->ev_bits, s));
         }
-        STAGE_END(ST_HIST);
+    }
+    STAGE_END(ST_HIST);
 
-        // 2. cell-major exclusive scan of the histogram
-        STAGE_BEGIN(ST_SCAN);
-        const int RB = 32;
-        const int nrb = (g.nbins + RB - 1) / RB;
-        dim3 g2((nc + kBlock - 1) / kBlock, nrb);
-        k_scan_colsum<<<g2, kBlock, 0, s>>>(ctx->H.as<uint32_t>(), g.nbins, nc, RB, ctx->P.as<uint32_t>());
-        k_scan_rows<<<blocks_for(nc), kBlock, 0, s>>>(ctx->P.as<uint32_t>(), nrb, nc, ctx->cell_cnt.as<uint32_t>());
-        k_scan_cells<<<1, 1024, 0, s>>>(ctx->cell_cnt.as<uint32_t>(), nc, ctx->cell_base.as<uint32_t>());
-        k_scan_apply<<<g2, kBlock, 0, s>>>(ctx->H.as<uint32_t>(), ctx->P.as<uint32_t>(),
-                                           ctx->cell_base.as<uint32_t>(), ctx->cell_cnt.as<uint32_t>(), g.nbins, nc,
-                                           RB, nrb, ctx->F.as<uint32_t>());
-        HIP_TRY(hipGetLastError());
-        STAGE_END(ST_SCAN);
+    // 2. cell-major exclusive scan of the histogram
+    STAGE_BEGIN(ST_SCAN);
+    const int RB = 32;
+    const int nrb = (g.nbins + RB - 1) / RB;
+    dim3 g2((nc + kBlock - 1) / kBlock, nrb);
+    k_scan_colsum<<<g2, kBlock, 0, s>>>(ctx->H.as<uint32_t>(), g.nbins, nc, RB, ctx->P.as<uint32_t>());
+    k_scan_rows<<<blocks_for(nc), kBlock, 0, s>>>(ctx->P.as<uint32_t>(), nrb, nc, ctx->cell_cnt.as<uint32_t>());
+    k_scan_cells<<<1, 1024, 0, s>>>(ctx->cell_cnt.as<uint32_t>(), nc, ctx->cell_base.as<uint32_t>());
+    k_scan_apply<<<g2, kBlock, 0, s>>>(ctx->H.as<uint32_t>(), ctx->P.as<uint32_t>(),
+                                       ctx->cell_base.as<uint32_t>(), ctx->cell_cnt.as<uint32_t>(), g.nbins, nc,
+                                       RB, nrb, ctx->F.as<uint32_t>());
+    HIP_TRY(hipGetLastError());
+    STAGE_END(ST_SCAN);
 
-        // The input check's flag bits (the GPU runs the scan meanwhile). When they allow
-        // compact grouping elements, pass A checks the rest on the reads it loads (kOffSpec);
-        // otherwise, or once that failed on the resident reads (no_spec, ERR_RESPEC), the
-        // standalone check takes every bit first (k_check_inputs, then a host wait).
-        STAGE_BEGIN(ST_GROUP_A);
-        int unit = 6;  // the pileup element's record offset unit: 64 bytes, or 16 bytes when
-                       // some record is not 64-byte aligned; either way a 31-bit count of units
-        bool spec = false, track = false;
-        ctx->roff_mode = kOffR64;
-        ctx->read_bits = 0;
-        if (n > 0) {
+    // The input check's flag bits (the GPU runs the scan meanwhile). When they allow
+    // compact grouping elements, pass A checks the rest on the reads it loads (kOffSpec);
+    // otherwise, or once that failed on the resident reads (no_spec, ERR_RESPEC), the
+    // standalone check takes every bit first (k_check_inputs, then a host wait).
+    STAGE_BEGIN(ST_GROUP_A);
+    int unit = 6;  // the pileup element's record offset unit: 64 bytes, or 16 bytes when
+                   // some record is not 64-byte aligned; either way a 31-bit count of units
+    bool spec = false, track = false;
+    ctx->roff_mode = kOffR64;
+    ctx->read_bits = 0;
+    if (n > 0 && sg.stream) {
+        spec = true;
+        ctx->roff_mode = kOffSpec;
+    } else if (n > 0) {
+        HIP_TRY(hipEventSynchronize(ctx->ev_bits));
+        const uint32_t fb = ctx->h_bits[0];
+        track = ((fb & CHK_PAIRED) && (fb & CHK_UNPAIRED)) || (fb & CHK_NOSEQ);
+        spec = !ctx->no_spec && !ctx->group_wide && !track && !(fb & CHK_FULL) &&
+               (uint64_t)ctx->pay < ((uint64_t)(PE_KEEP & PE_OFF) << 6);
+        if (spec) {
+            ctx->roff_mode = kOffSpec;
+            ctx->read_bits = fb;
+        } else {
+            k_check_inputs<<<blocks_for(n), kBlock, 0, s>>>(
+                ctx->roff.as<uint64_t>(), ctx->flag.as<uint16_t>(), ctx->start.as<int32_t>(),
+                ctx->tlen.as<int32_t>(), ctx->bc.as<int32_t>(), ctx->span.as<uint32_t>(), ctx->cfg.mito_len,
+                ctx->cfg.n_cells, n, ctx->roff_irregular.as<uint32_t>(), ctx->roff32.as<uint32_t>());
+            HIP_TRY(hipGetLastError());
+            HIP_TRY(hipMemcpyAsync(ctx->h_bits, ctx->roff_irregular.p, 8, hipMemcpyDeviceToHost, s));
+            HIP_TRY(hipEventRecord(ctx->ev_bits, s));
             HIP_TRY(hipEventSynchronize(ctx->ev_bits));
-            const uint32_t fb = ctx->h_bits[0];
-            track = ((fb & CHK_PAIRED) && (fb & CHK_UNPAIRED)) || (fb & CHK_NOSEQ);
-            spec = !ctx->no_spec && !ctx->group_wide && !track && !(fb & CHK_FULL) &&
-                   (uint64_t)ctx->pay < ((uint64_t)(PE_KEEP & PE_OFF) << 6);
-            if (spec) {
-                ctx->roff_mode = kOffSpec;
-                ctx->read_bits = fb;
-            } else {
-                k_check_inputs<<<blocks_for(n), kBlock, 0, s>>>(
-                    ctx->roff.as<uint64_t>(), ctx->flag.as<uint16_t>(), ctx->start.as<int32_t>(),
-                    ctx->tlen.as<int32_t>(), ctx->bc.as<int32_t>(), ctx->span.as<uint32_t>(), ctx->cfg.mito_len,
-                    ctx->cfg.n_cells, n, ctx->roff_irregular.as<uint32_t>(), ctx->roff32.as<uint32_t>());
-                HIP_TRY(hipGetLastError());
-                HIP_TRY(hipMemcpyAsync(ctx->h_bits, ctx->roff_irregular.p, 8, hipMemcpyDeviceToHost, s));
-                HIP_TRY(hipEventRecord(ctx->ev_bits, s));
-                HIP_TRY(hipEventSynchronize(ctx->ev_bits));
-                const uint32_t irr = ctx->h_bits[0];
-                ctx->roff_mode = !(irr & 1u) ? kOffDense : !(irr & 2u) ? kOffR32 : kOffR64;
-                ctx->read_bits = irr;
-                unit = ctx->roff_mode == kOffR64 ? 4 : 6;
-            }
+            const uint32_t irr = ctx->h_bits[0];
+            ctx->roff_mode = !(irr & 1u) ? kOffDense : !(irr & 2u) ? kOffR32 : kOffR64;
+            ctx->read_bits = irr;
+            unit = ctx->roff_mode == kOffR64 ? 4 : 6;
         }
-        if (n > 0 && (uint64_t)ctx->pay >= ((uint64_t)(PE_KEEP & PE_OFF) << unit))
-            return set_err(MGP_E_INVALID, unit == 6 ? "payload larger than 128 GiB in one context; shard the cells"
-                                                    : "payload with 16-byte aligned records larger than 32 GiB in "
-                                                      "one context; place records at 64-byte offsets or shard the cells");
+    }
+    if (n > 0 && (uint64_t)ctx->pay >= ((uint64_t)(PE_KEEP & PE_OFF) << unit))
+        return set_err(MGP_E_INVALID, unit == 6 ? "payload larger than 128 GiB in one context; shard the cells"
+                                                : "payload with 16-byte aligned records larger than 32 GiB in "
+                                                  "one context; place records at 64-byte offsets or shard the cells");
 
-        // 3. stable grouping into cell-major order (two passes), duplicate marking in pass B;
-        // 8-byte elements when the resident reads allow them (GCompact)
-        const uint32_t rbits = ctx->read_bits;
-        const bool compact = spec || (!ctx->group_wide && ctx->roff_mode != kOffR64 && unit == 6 && !track &&
-                                      !(rbits & (CHK_FULL | CHK_WIDEKEY)));
-        if (n > 0) {
-            int gbits = 0;
-            while (gbits < 31 && (1 << gbits) < ngroups) ++gbits;
-            k_scan_cells<<<1, 1024, 0, s>>>(ctx->bin_valid.as<uint32_t>(), g.nbins, ctx->bin_base.as<uint32_t>());
-            const size_t a_lds = (size_t)ngroups * (1 + 2 * (kGABlock / kWave)) * 4 + (size_t)((nc + 31) / 32) * 4;
-            if (a_lds > (size_t)ctx->lds_hist_max_cells * 4)
-                return set_err(MGP_E_INVALID, "too many cells for one context (grouping LDS)");
-            if ((uint64_t)ctx->pay >= (1ull << GM_LCELL_SHIFT))
-                return set_err(MGP_E_INVALID, "payload too large (record offsets must stay below 2^50)");
-            dim3 ga((unsigned)g.nbins, kParts);
-            auto launch_a = [&](auto kern) {
-                kern<<<ga, kGABlock, a_lds, s>>>(
-                    n, ctx->start.as<int32_t>(), ctx->bc.as<int32_t>(), ctx->tlen.as<int32_t>(),
-                    ctx->flag.as<uint16_t>(), ctx->mapq.as<uint8_t>(), ctx->roff.as<uint64_t>(),
-                    ctx->roff32.as<uint32_t>(), ctx->span.as<uint32_t>(), ctx->bin_start.as<uint32_t>(),
-                    ctx->PG.as<uint32_t>(), ctx->F.as<uint32_t>(), ctx->bin_base.as<uint32_t>(), g, ngroups, gbits,
-                    ctx->cfg.min_mapq, ctx->bucket_off.as<uint32_t>(), ctx->gel2.as<GElem>(),
-                    ctx->first_read.as<uint32_t>(), ctx->roff_irregular.as<uint32_t>(), st);
-            };
-            if (spec) {
-                launch_a(k_group_a<kOffSpec, true>);
-            } else if (compact) {
-                if (ctx->roff_mode == kOffDense) launch_a(k_group_a<kOffDense, true>);
-                else launch_a(k_group_a<kOffR32, true>);
-            } else if (ctx->roff_mode == kOffDense) {
-                launch_a(k_group_a<kOffDense, false>);
-            } else if (ctx->roff_mode == kOffR32) {
-                launch_a(k_group_a<kOffR32, false>);
-            } else {
-                launch_a(k_group_a<kOffR64, false>);
-            }
-            HIP_TRY(hipGetLastError());
-            // the check's span and order bits into the run's stats (the pileup's halo)
-            k_check_stats<<<1, 64, 0, s>>>(ctx->roff_irregular.as<uint32_t>(), st);
+    // 3. stable grouping into cell-major order (two passes), duplicate marking in pass B;
+    // 8-byte elements when the resident reads allow them (GCompact)
+    const uint32_t rbits = ctx->read_bits;
+    const bool compact = spec || (!ctx->group_wide && ctx->roff_mode != kOffR64 && unit == 6 && !track &&
+                                  !(rbits & (CHK_FULL | CHK_WIDEKEY)));
+    if (n > 0) {
+        int gbits = 0;
+        while (gbits < 31 && (1 << gbits) < ngroups) ++gbits;
+        k_scan_cells<<<1, 1024, 0, s>>>(ctx->bin_valid.as<uint32_t>(), g.nbins, ctx->bin_base.as<uint32_t>());
+        const size_t a_lds = (size_t)ngroups * (1 + 2 * (kGABlock / kWave)) * 4 + (size_t)((nc + 31) / 32) * 4;
+        if (a_lds > (size_t)ctx->lds_hist_max_cells * 4)
+            return set_err(MGP_E_INVALID, "too many cells for one context (grouping LDS)");
+        if ((uint64_t)ctx->pay >= (1ull << GM_LCELL_SHIFT))
+            return set_err(MGP_E_INVALID, "payload too large (record offsets must stay below 2^50)");
+        dim3 ga((unsigned)g.nbins, kParts);
+        auto launch_a = [&](auto kern) {
+            kern<<<ga, kGABlock, a_lds, s>>>(
+                n, ctx->start.as<int32_t>(), ctx->bc.as<int32_t>(), ctx->tlen.as<int32_t>(),
+                ctx->flag.as<uint16_t>(), ctx->mapq.as<uint8_t>(), ctx->roff.as<uint64_t>(),
+                ctx->roff32.as<uint32_t>(), ctx->span.as<uint32_t>(), ctx->bin_start.as<uint32_t>(),
+                ctx->PG.as<uint32_t>(), ctx->F.as<uint32_t>(), ctx->bin_base.as<uint32_t>(), g, ngroups, gbits,
+                ctx->cfg.min_mapq, ctx->bucket_off.as<uint32_t>(), ctx->gel2.as<GElem>(),
+                ctx->first_read.as<uint32_t>(), ctx->roff_irregular.as<uint32_t>(), st, sg.w0, sg.bhi);
+        };
+        if (spec) {
+            launch_a(k_group_a<kOffSpec, true>);
+        } else if (compact) {
+            if (ctx->roff_mode == kOffDense) launch_a(k_group_a<kOffDense, true>);
+            else launch_a(k_group_a<kOffR32, true>);
+        } else if (ctx->roff_mode == kOffDense) {
+            launch_a(k_group_a<kOffDense, false>);
+        } else if (ctx->roff_mode == kOffR32) {
+            launch_a(k_group_a<kOffR32, false>);
+        } else {
+            launch_a(k_group_a<kOffR64, false>);
+        }
+        HIP_TRY(hipGetLastError());
+        // the check's span and order bits into the run's stats (the pileup's halo); a
+        // streaming segment also checks here the flag bits its variants assume
+        k_check_stats<<<1, 64, 0, s>>>(ctx->roff_irregular.as<uint32_t>(), st, sg.stream ? 1 : 0);
+        HIP_TRY(hipGetLastError());
+    }
+    STAGE_END(ST_GROUP_A);
+    STAGE_BEGIN(ST_GROUP_B);
+    if (MGP_ABL_A == 1) HIP_TRY(hipMemsetAsync(ctx->gel2.p, 0, (size_t)n * sizeof(GElem), s));  // ablation
+    if (MGP_ABL_B >= 2) HIP_TRY(hipMemsetAsync(ctx->pel.p, 0xFF, (size_t)n * 4, s));  // ablation: nothing piles
+    if (n > 0) {
+        // about MGP_GB_WG workgroups (many per slot: 4 fit a CU, so a grid of a few
+        // slot-rounds leaves a tail); bins per workgroup at most kMaxRbB, whose
+        // bucket sizes the workgroup keeps in LDS
+        const int64_t tgt = MGP_GB_WG;
+        const int rb = std::min(kMaxRbB, std::max(1, (int)(((int64_t)ngroups * g.nbins + tgt - 1) / tgt)));
+        dim3 gb((unsigned)ngroups, (unsigned)((g.nbins + rb - 1) / rb));
+        dup_parts = (int)(gb.x * gb.y);
+        MGP_TRY(ctx->dup_part.ensure((size_t)dup_parts * 16));
+        // duplicates of the halo bins of a streaming segment were counted by an earlier one
+        const int cnt_lo = sg.w0 > 0 ? (int)((int64_t)sg.w0 * g.W / g.G) : 0;
+        // per-read pairedness / SEQ tracking only when the reads mix paired and
+        // unpaired ones or some read lacks SEQ/QUAL
+        auto launch_b = [&](auto kern, auto* gel) {
+            kern<<<gb, kBlock, 0, s>>>(gel, ctx->bucket_off.as<uint32_t>(), ctx->H.as<uint32_t>(),
+                                       g, ngroups, rb, ctx->cfg.dedup_mode, unit, ctx->pel.as<uint32_t>(),
+                                       ctx->any_paired.as<uint8_t>(), ctx->dup_part.as<unsigned long long>(), st,
+                                       cnt_lo);
+        };
+        if (compact) launch_b(k_group_b<false, GCompact>, ctx->gel2.as<unsigned long long>());
+        else if (track) launch_b(k_group_b<true, GWide>, ctx->gel2.as<GElem>());
+        else launch_b(k_group_b<false, GWide>, ctx->gel2.as<GElem>());
+        pair_mode = sg.stream ? -1 : track ? 0 : (rbits & CHK_PAIRED) ? 1 : 0;
+        HIP_TRY(hipGetLastError());
+        if (sg.stream) {
+            k_dup_accum<<<1, 256, 0, s>>>(ctx->dup_part.as<unsigned long long>(), dup_parts, st);
             HIP_TRY(hipGetLastError());
         }
-        STAGE_END(ST_GROUP_A);
-        STAGE_BEGIN(ST_GROUP_B);
-        if (MGP_ABL_A == 1) HIP_TRY(hipMemsetAsync(ctx->gel2.p, 0, (size_t)n * sizeof(GElem), s));  // ablation
-        if (MGP_ABL_B >= 2) HIP_TRY(hipMemsetAsync(ctx->pel.p, 0xFF, (size_t)n * 4, s));  // ablation: nothing piles
-        int dup_parts = 0;
-        int pair_mode = 0;  // 1: every read is paired, the pileup flags every cell with a kept read
-        if (n > 0) {
-            // about MGP_GB_WG workgroups (many per slot: 4 fit a CU, so a grid of a few
-            // slot-rounds leaves a tail); bins per workgroup at most kMaxRbB, whose
-            // bucket sizes the workgroup keeps in LDS
-            const int64_t tgt = MGP_GB_WG;
-            const int rb = std::min(kMaxRbB, std::max(1, (int)(((int64_t)ngroups * g.nbins + tgt - 1) / tgt)));
-            dim3 gb((unsigned)ngroups, (unsigned)((g.nbins + rb - 1) / rb));
-            dup_parts = (int)(gb.x * gb.y);
-            MGP_TRY(ctx->dup_part.ensure((size_t)dup_parts * 16));
-            // per-read pairedness / SEQ tracking only when the reads mix paired and
-            // unpaired ones or some read lacks SEQ/QUAL
-            auto launch_b = [&](auto kern, auto* gel) {
-                kern<<<gb, kBlock, 0, s>>>(gel, ctx->bucket_off.as<uint32_t>(), ctx->H.as<uint32_t>(),
-                                           g, ngroups, rb, ctx->cfg.dedup_mode, unit, ctx->pel.as<uint32_t>(),
-                                           ctx->any_paired.as<uint8_t>(), ctx->dup_part.as<unsigned long long>(), st);
-            };
-            if (compact) launch_b(k_group_b<false, GCompact>, ctx->gel2.as<unsigned long long>());
-            else if (track) launch_b(k_group_b<true, GWide>, ctx->gel2.as<GElem>());
-            else launch_b(k_group_b<false, GWide>, ctx->gel2.as<GElem>());
-            pair_mode = track ? 0 : (rbits & CHK_PAIRED) ? 1 : 0;
-            HIP_TRY(hipGetLastError());
-        }
-        STAGE_END(ST_GROUP_B);
+    }
+    STAGE_END(ST_GROUP_B);
 
-        // 5. dedup + pileup + strand filter + stats
-        STAGE_BEGIN(ST_PILEUP);
-        PileCfg pc;
-        pc.min_baseq = ctx->cfg.min_baseq;
-        pc.min_dist = ctx->cfg.min_dist_from_end;
-        pc.min_reads = ctx->cfg.min_reads;
-        pc.dedup_mode = ctx->cfg.dedup_mode;
-        pc.max_bias = ctx->cfg.max_strand_bias;
-        pc.bias_active = ctx->cfg.max_strand_bias < 1.0;
-        pc.keep_tn5 = (ctx->cfg.flags & MGP_CFG_KEEP_TN5) != 0;
-        dim3 gp(g.nchunks, g.nwin);
+    // 5. dedup + pileup + strand filter + stats
+    STAGE_BEGIN(ST_PILEUP);
+    PileCfg pc;
+    pc.min_baseq = ctx->cfg.min_baseq;
+    pc.min_dist = ctx->cfg.min_dist_from_end;
+    pc.min_reads = ctx->cfg.min_reads;
+    pc.dedup_mode = ctx->cfg.dedup_mode;
+    pc.max_bias = ctx->cfg.max_strand_bias;
+    pc.bias_active = ctx->cfg.max_strand_bias < 1.0;
+    pc.keep_tn5 = (ctx->cfg.flags & MGP_CFG_KEEP_TN5) != 0;
+    if (sg.w1 > sg.w0) {
+        dim3 gp(g.nchunks, sg.w1 - sg.w0);
         const size_t psm = (size_t)5 * g.Wp * 4;
-        auto pile_kern = (ctx->read_bits & CHK_FULL) ? k_pileup<false> : k_pileup<true>;
+        auto pile_kern = (!sg.stream && (ctx->read_bits & CHK_FULL)) ? k_pileup<false> : k_pileup<true>;
         pile_kern<<<gp, kBlock, psm, s>>>(g, pc, ctx->payload.as<uint8_t>(), ctx->pel.as<uint32_t>(), unit,
                                          ctx->H.as<uint32_t>(), out16_of(ctx), ctx->counts.as<uint32_t>(),
-                                         ctx->tn5.as<uint32_t>(), ctx->depth.as<uint32_t>(), ctx->n_reads.as<uint32_t>(),
-                                         ctx->any_paired.as<uint8_t>(), pair_mode, ctx->covered.as<uint32_t>(),
-                                         ctx->dsum.as<unsigned long long>(), ctx->dmax.as<uint32_t>(),
-                                         ctx->tally_part.as<uint32_t>(), st);
+                                         ctx->tn5.as<uint32_t>(), ctx->depth.as<uint32_t>(),
+                                         ctx->n_reads.as<uint32_t>(), ctx->any_paired.as<uint8_t>(), pair_mode,
+                                         ctx->covered.as<uint32_t>(), ctx->dsum.as<unsigned long long>(),
+                                         ctx->dmax.as<uint32_t>(), ctx->tally_part.as<uint32_t>(), st, sg.w0,
+                                         ctx->roff_irregular.as<uint32_t>());
         HIP_TRY(hipGetLastError());
-        STAGE_END(ST_PILEUP);
+    }
+    STAGE_END(ST_PILEUP);
+    return MGP_OK;
+}
 
+// The end of a run: min-reads gate, tallies, medians and pass flags, run statistics,
+// the tally all-reduce, and the stats' copy to pinned host memory.
+static int run_finish(mgp_ctx* ctx, int slot, int dup_parts, bool streamed) {
+    const Geom g = ctx->g;
+    const int nc = g.nc;
+    hipStream_t s = ctx->s_comp;
+    DevStats* st = ctx->stats.as<DevStats>();
+    unsigned long long* tally = ctx->tally.as<unsigned long long>();
+    if (nc > 0) {
         // 6. min-reads gate
         if (ctx->cfg.min_reads > 1) {
             STAGE_BEGIN(ST_GATE);
@@ -2849,10 +3025,9 @@ int mgp_run(mgp_ctx* ctx) {
                 HIP_TRY(hipEventRecord(ctx->ev[slot][ST_TALLY][0], s2));
                 ctx->stage_ran[slot][ST_TALLY] = true;
             }
-            HIP_TRY(hipMemsetAsync(ctx->tally.p, 0, (size_t)g.L * 32, s2));
+            HIP_TRY(hipMemsetAsync(tally, 0, (size_t)g.L * 32, s2));
             dim3 gt(blocks_for((int64_t)g.L * 4), (unsigned)std::max(1, std::min(g.nchunks, 32)));
-            k_tally_reduce<<<gt, kBlock, 0, s2>>>(ctx->tally_part.as<uint32_t>(), g.nchunks, g.L * 4,
-                                                  ctx->tally.as<unsigned long long>());
+            k_tally_reduce<<<gt, kBlock, 0, s2>>>(ctx->tally_part.as<uint32_t>(), g.nchunks, g.L * 4, tally);
             HIP_TRY(hipGetLastError());
             if (STAGE_ON(ST_TALLY)) HIP_TRY(hipEventRecord(ctx->ev[slot][ST_TALLY][1], s2));
             HIP_TRY(hipEventRecord(ctx->ev_join, s2));
@@ -2861,39 +3036,87 @@ int mgp_run(mgp_ctx* ctx) {
         // 8. medians + pass flags, run statistics
         STAGE_BEGIN(ST_MEDIAN);
         if (g.L <= kMedRegs * kBlock)
-            k_median<true><<<nc, kBlock, 0, s>>>(
-                                                     g, ctx->cfg.min_reads, ctx->depth16.as<uint16_t>(),
-                                                     ctx->depth.as<uint32_t>(), ctx->wide.as<uint8_t>(),
-                                                     ctx->n_reads.as<uint32_t>(), ctx->covered.as<uint32_t>(),
-                                                     ctx->dmax.as<uint32_t>(),
-                                                     ctx->med_lo.as<uint32_t>(), ctx->med_hi.as<uint32_t>(),
-                                                     ctx->passed.as<uint8_t>(), st);
+            k_median<true><<<nc, kBlock, 0, s>>>(g, ctx->cfg.min_reads, ctx->depth16.as<uint16_t>(),
+                                                 ctx->depth.as<uint32_t>(), ctx->wide.as<uint8_t>(),
+                                                 ctx->n_reads.as<uint32_t>(), ctx->covered.as<uint32_t>(),
+                                                 ctx->dmax.as<uint32_t>(), ctx->med_lo.as<uint32_t>(),
+                                                 ctx->med_hi.as<uint32_t>(), ctx->passed.as<uint8_t>(), st);
         else
-            k_median<false><<<nc, kBlock, 0, s>>>(
-                                                     g, ctx->cfg.min_reads, ctx->depth16.as<uint16_t>(),
-                                                     ctx->depth.as<uint32_t>(), ctx->wide.as<uint8_t>(),
-                                                     ctx->n_reads.as<uint32_t>(), ctx->covered.as<uint32_t>(),
-                                                     ctx->dmax.as<uint32_t>(),
-                                                     ctx->med_lo.as<uint32_t>(), ctx->med_hi.as<uint32_t>(),
-                                                     ctx->passed.as<uint8_t>(), st);
+            k_median<false><<<nc, kBlock, 0, s>>>(g, ctx->cfg.min_reads, ctx->depth16.as<uint16_t>(),
+                                                  ctx->depth.as<uint32_t>(), ctx->wide.as<uint8_t>(),
+                                                  ctx->n_reads.as<uint32_t>(), ctx->covered.as<uint32_t>(),
+                                                  ctx->dmax.as<uint32_t>(), ctx->med_lo.as<uint32_t>(),
+                                                  ctx->med_hi.as<uint32_t>(), ctx->passed.as<uint8_t>(), st);
         HIP_TRY(hipGetLastError());
         k_run_stats<<<1, 1024, 0, s>>>(ctx->n_reads.as<uint32_t>(), ctx->passed.as<uint8_t>(), nc,
-                                       ctx->dup_part.as<unsigned long long>(), dup_parts, st);
+                                       ctx->dup_part.as<unsigned long long>(), streamed ? 0 : dup_parts, st,
+                                       streamed ? 0 : 1);
         HIP_TRY(hipGetLastError());
         STAGE_END(ST_MEDIAN);
         HIP_TRY(hipStreamWaitEvent(s, ctx->ev_join, 0));
     } else {
-        HIP_TRY(hipMemsetAsync(ctx->tally.p, 0, (size_t)g.L * 32, s));
+        HIP_TRY(hipMemsetAsync(tally, 0, (size_t)g.L * 32, s));
     }
 
-    // 9. tallies over ranks
+    // 9. tallies over ranks; the slot after them carries the ranks' ERR_RESPEC so that
+    // every rank reruns when one has to (the reruns' all-reduces then match up)
     if (ctx->comm) {
         STAGE_BEGIN(ST_COMM);
-        ncclResult_t r = ncclAllReduce(ctx->tally.p, ctx->tally.p, (size_t)g.L * 4, ncclUint64, ncclSum, ctx->comm, s);
+        k_respec_slot<<<1, 64, 0, s>>>(st, tally + (size_t)g.L * 4);
+        HIP_TRY(hipGetLastError());
+        ncclResult_t r = ncclAllReduce(tally, tally, (size_t)g.L * 4 + 1, ncclUint64, ncclSum, ctx->comm, s);
         if (r != ncclSuccess) return set_err(MGP_E_COMM, std::string("ncclAllReduce: ") + ncclGetErrorString(r));
+        HIP_TRY(hipMemcpyAsync(ctx->h_respec, tally + (size_t)g.L * 4, 8, hipMemcpyDeviceToHost, s));
         STAGE_END(ST_COMM);
     }
+    k_order_err<<<1, 64, 0, s>>>(ctx->order_bad.as<uint32_t>(), st);
+    HIP_TRY(hipGetLastError());
     HIP_TRY(hipMemcpyAsync(ctx->host_stats, st, sizeof(DevStats), hipMemcpyDeviceToHost, s));
+    return MGP_OK;
+}
+
+// Streaming (MGP_CFG_STREAM): after a push, the windows whose reads have all arrived
+// (every start below the window's end: the input is coordinate-sorted, so the last
+// pushed start says which) go through the hot path as one segment, queued behind the
+// batch's copies while the next batches are still being copied. The last window
+// (it also takes the overflow bin) waits for mgp_run.
+static int stream_segments(mgp_ctx* ctx, int64_t last_start) {
+    const Geom& g = ctx->g;
+    if (ctx->stream_off || g.nc <= 0 || last_start < 0) return MGP_OK;
+    const int64_t wc = std::min<int64_t>(last_start / g.W, g.nwin - 1);  // windows [0, wc) are complete
+    if (wc <= ctx->w_done) return MGP_OK;
+    if ((uint64_t)ctx->pay >= ((uint64_t)(PE_KEEP & PE_OFF) << 6)) {  // not for compact elements: run resident
+        ctx->stream_off = true;
+        return MGP_OK;
+    }
+    MGP_TRY(ensure_run_buffers(ctx));
+    int dup_parts = 0, pair_mode = 0;
+    const Seg sg{ctx->w_done, (int)wc, (int)(wc * g.W / g.G), !ctx->seg_open, true};
+    MGP_TRY(run_segment(ctx, sg, -1, dup_parts, pair_mode));
+    ctx->seg_open = true;
+    ctx->w_done = (int)wc;
+    ctx->segments++;
+    return MGP_OK;
+}
+
+int mgp_run(mgp_ctx* ctx) {
+    if (!ctx) return set_err(MGP_E_INVALID, "null ctx");
+    HIP_TRY(hipSetDevice(ctx->dev));
+    ctx->ran = false;  // (until this run is queued: an error below leaves no results)
+    MGP_TRY(ensure_run_buffers(ctx));
+    const Geom g = ctx->g;
+    const int slot = (int)(ctx->runs % mgp_ctx::kRing);
+    for (int i = 0; i < ST_N; ++i) ctx->stage_ran[slot][i] = false;
+    int dup_parts = 0, pair_mode = 0;
+    // a streaming run whose pushes already ran segments: the rest of the windows;
+    // otherwise (or on the fallback path) one resident segment over everything
+    const bool streamed = ctx->seg_open && !ctx->no_spec && !ctx->stream_off;
+    const Seg sg = streamed ? Seg{ctx->w_done, g.nwin, g.nbins, false, true} : Seg{0, g.nwin, g.nbins, true, false};
+    ctx->seg_open = false;
+    ctx->w_done = 0;
+    MGP_TRY(run_segment(ctx, sg, slot, dup_parts, pair_mode));
+    MGP_TRY(run_finish(ctx, slot, dup_parts, streamed));
+    ctx->last_streamed = streamed;
     ctx->ran = true;
     ctx->runs++;
     ctx->last_status = MGP_OK;
@@ -2906,10 +3129,16 @@ int mgp_sync(mgp_ctx* ctx) {
     HIP_TRY(hipSetDevice(ctx->dev));
     HIP_TRY(hipStreamSynchronize(ctx->s_comp));
     const uint32_t e = ctx->host_stats->err;
-    if ((e & ERR_RESPEC) && !ctx->no_spec) {  // a read did not fit the compact grouping: run again
+    // some read did not fit the speculative grouping (on any rank, with a communicator):
+    // run again on the fallback path, once
+    const bool respec = ctx->comm ? *ctx->h_respec != 0ull : (e & ERR_RESPEC) != 0u;
+    if (respec && !ctx->rerunning) {
         ctx->no_spec = true;
-        MGP_TRY(mgp_run(ctx));
-        return mgp_sync(ctx);
+        ctx->rerunning = true;
+        int r = mgp_run(ctx);
+        if (r == MGP_OK) r = mgp_sync(ctx);
+        ctx->rerunning = false;
+        return r;
     }
     if (e & ERR_RESPEC) return set_err(MGP_E_STATE, "speculative grouping failed on the fallback path");
     if (e & ERR_UNSORTED) return set_err(MGP_E_UNSORTED, "records are not in coordinate order");
@@ -2923,36 +3152,37 @@ int mgp_sync(mgp_ctx* ctx) {
     return MGP_OK;
 }
 
-int mgp_fetch(mgp_ctx* ctx, mgp_result* out) {
+int mgp_fetch_cells(mgp_ctx* ctx, int32_t lo, int32_t hi, mgp_result* out) {
     if (!ctx || !out) return set_err(MGP_E_INVALID, "null ctx/out");
+    if (lo < 0 || hi < lo || hi > ctx->g.nc) return set_err(MGP_E_INVALID, "cell range outside [0, n_cells)");
     MGP_TRY(mgp_sync(ctx));
     const Geom& g = ctx->g;
-    const size_t nc = (size_t)g.nc, L = (size_t)g.L;
-    auto d2h = [&](void* dst, const DevBuf& src, size_t bytes) -> int {
-        if (dst && bytes) HIP_TRY(hipMemcpy(dst, src.p, bytes, hipMemcpyDeviceToHost));
+    const size_t nc = (size_t)(hi - lo), L = (size_t)g.L, c0 = (size_t)lo;
+    auto d2h = [&](void* dst, const DevBuf& src, size_t off, size_t bytes) -> int {
+        if (dst && bytes) HIP_TRY(hipMemcpy(dst, src.as<uint8_t>() + off, bytes, hipMemcpyDeviceToHost));
         return MGP_OK;
     };
     if (nc && (out->counts || out->tn5 || out->depth)) {  // widen the 16-bit rows (drained windows are exact already)
         const int64_t npos = (int64_t)nc * (int64_t)L;
         k_expand<<<blocks_for(npos), kBlock, 0, ctx->s_comp>>>(
-            g, npos, out16_of(ctx), out->counts ? ctx->counts.as<uint32_t>() : nullptr,
+            g, (int64_t)c0 * (int64_t)L, npos, out16_of(ctx), out->counts ? ctx->counts.as<uint32_t>() : nullptr,
             out->tn5 ? ctx->tn5.as<uint32_t>() : nullptr, out->depth ? ctx->depth.as<uint32_t>() : nullptr);
         HIP_TRY(hipGetLastError());
         HIP_TRY(hipStreamSynchronize(ctx->s_comp));
     }
-    MGP_TRY(d2h(out->counts, ctx->counts, nc * L * 32));
-    MGP_TRY(d2h(out->tn5, ctx->tn5, nc * L * 8));
-    MGP_TRY(d2h(out->depth, ctx->depth, nc * L * 4));
-    MGP_TRY(d2h(out->n_reads, ctx->n_reads, nc * 4));
-    MGP_TRY(d2h(out->any_paired, ctx->any_paired, nc));
-    MGP_TRY(d2h(out->passed, ctx->passed, nc));
-    MGP_TRY(d2h(out->covered, ctx->covered, nc * 4));
-    MGP_TRY(d2h(out->depth_sum, ctx->dsum, nc * 8));
-    MGP_TRY(d2h(out->depth_max, ctx->dmax, nc * 4));
-    MGP_TRY(d2h(out->median_lo, ctx->med_lo, nc * 4));
-    MGP_TRY(d2h(out->median_hi, ctx->med_hi, nc * 4));
-    MGP_TRY(d2h(out->first_read, ctx->first_read, nc * 4));
-    MGP_TRY(d2h(out->ref_tally, ctx->tally, L * 4 * 8));
+    MGP_TRY(d2h(out->counts, ctx->counts, c0 * L * 32, nc * L * 32));
+    MGP_TRY(d2h(out->tn5, ctx->tn5, c0 * L * 8, nc * L * 8));
+    MGP_TRY(d2h(out->depth, ctx->depth, c0 * L * 4, nc * L * 4));
+    MGP_TRY(d2h(out->n_reads, ctx->n_reads, c0 * 4, nc * 4));
+    MGP_TRY(d2h(out->any_paired, ctx->any_paired, c0, nc));
+    MGP_TRY(d2h(out->passed, ctx->passed, c0, nc));
+    MGP_TRY(d2h(out->covered, ctx->covered, c0 * 4, nc * 4));
+    MGP_TRY(d2h(out->depth_sum, ctx->dsum, c0 * 8, nc * 8));
+    MGP_TRY(d2h(out->depth_max, ctx->dmax, c0 * 4, nc * 4));
+    MGP_TRY(d2h(out->median_lo, ctx->med_lo, c0 * 4, nc * 4));
+    MGP_TRY(d2h(out->median_hi, ctx->med_hi, c0 * 4, nc * 4));
+    MGP_TRY(d2h(out->first_read, ctx->first_read, c0 * 4, nc * 4));
+    MGP_TRY(d2h(out->ref_tally, ctx->tally, 0, L * 4 * 8));
     if (out->stats) {
         const DevStats& h = *ctx->host_stats;
         mgp_stats* o = out->stats;
@@ -2965,6 +3195,51 @@ int mgp_fetch(mgp_ctx* ctx, mgp_result* out) {
         o->max_span = (int32_t)h.max_span;
         o->error_bits = (int32_t)h.err;
     }
+    return MGP_OK;
+}
+
+int mgp_fetch(mgp_ctx* ctx, mgp_result* out) {
+    if (!ctx) return set_err(MGP_E_INVALID, "null ctx");
+    return mgp_fetch_cells(ctx, 0, ctx->g.nc, out);
+}
+
+int mgp_fetch_rows16(mgp_ctx* ctx, int32_t lo, int32_t hi, mgp_rows16* out) {
+    if (!ctx || !out) return set_err(MGP_E_INVALID, "null ctx/out");
+    if (lo < 0 || hi < lo || hi > ctx->g.nc) return set_err(MGP_E_INVALID, "cell range outside [0, n_cells)");
+    MGP_TRY(mgp_sync(ctx));
+    const Geom& g = ctx->g;
+    const size_t nc = (size_t)(hi - lo), L = (size_t)g.L, c0 = (size_t)lo, nw = (size_t)g.nwin;
+    auto d2h = [&](void* dst, const DevBuf& src, size_t off, size_t bytes) -> int {
+        if (dst && bytes) HIP_TRY(hipMemcpyAsync(dst, src.as<uint8_t>() + off, bytes, hipMemcpyDeviceToHost, ctx->s_comp));
+        return MGP_OK;
+    };
+    // the pileup's 16-bit rows as they are: u16 pairs (fwd, rev) per base, Tn5 (fwd, rev), depth
+    MGP_TRY(d2h(out->counts, ctx->counts16, c0 * L * 16, nc * L * 16));
+    MGP_TRY(d2h(out->tn5, ctx->tn5_16, c0 * L * 4, nc * L * 4));
+    MGP_TRY(d2h(out->depth, ctx->depth16, c0 * L * 2, nc * L * 2));
+    MGP_TRY(d2h(out->wide, ctx->wide, c0 * nw, nc * nw));
+    HIP_TRY(hipStreamSynchronize(ctx->s_comp));
+    return MGP_OK;
+}
+
+int mgp_windows(mgp_ctx* ctx, int32_t* n_windows, int32_t* window_width) {
+    if (!ctx) return set_err(MGP_E_INVALID, "null ctx");
+    if (n_windows) *n_windows = ctx->g.nwin;
+    if (window_width) *window_width = ctx->g.W;
+    return MGP_OK;
+}
+
+int mgp_set_streaming(mgp_ctx* ctx, int on) {
+    if (!ctx) return set_err(MGP_E_INVALID, "null ctx");
+    if (ctx->seg_open) return set_err(MGP_E_STATE, "a streaming run is in progress (mgp_run or mgp_reset first)");
+    ctx->stream = on != 0;
+    return MGP_OK;
+}
+
+int mgp_stream_info(mgp_ctx* ctx, int64_t* segments, int32_t* last_streamed) {
+    if (!ctx) return set_err(MGP_E_INVALID, "null ctx");
+    if (segments) *segments = ctx->segments;
+    if (last_streamed) *last_streamed = ctx->last_streamed ? 1 : 0;
     return MGP_OK;
 }
 
@@ -3059,60 +3334,84 @@ int mgp_download_inputs(mgp_ctx* ctx, int32_t* start, int32_t* bc, int32_t* tlen
 int mgp_synth_fill(void* stream, uint64_t seed, int64_t n, int read_len, int n_cells, int mito_len,
                    const uint32_t* d_cdf, const uint8_t* d_ref, int32_t* start, int32_t* bc, int32_t* tlen,
                    uint16_t* flag, uint8_t* mapq, uint32_t* span, uint64_t* roff, uint8_t* payload,
-                   int64_t* payload_bytes, int rec_align, int pack, int placed);
+                   int64_t* payload_bytes, int rec_align, int pack, int placed, int cell_lo, int cell_hi,
+                   int shard_rank, int shard_world, uint64_t* d_map, int64_t* n_out);
 
 int mgp_synth_generate(mgp_ctx* ctx, const mgp_synth_params* p) {
     if (!ctx || !p || !p->cell_cdf || !p->ref_codes) return set_err(MGP_E_INVALID, "null synth args");
-    if (p->n_cells != ctx->cfg.n_cells) return set_err(MGP_E_INVALID, "synth n_cells != context n_cells");
+    const bool shard = p->cell_hi > p->cell_lo;
+    if (shard) {
+        if (p->cell_lo < 0 || p->cell_hi > p->n_cells || p->shard_world < 0 ||
+            (p->shard_world > 0 && (p->shard_rank < 0 || p->shard_rank >= p->shard_world)))
+            return set_err(MGP_E_INVALID, "synth cell shard out of range");
+        if (p->cell_hi - p->cell_lo != ctx->cfg.n_cells)
+            return set_err(MGP_E_INVALID, "synth shard cells != context n_cells");
+    } else if (p->n_cells != ctx->cfg.n_cells) {
+        return set_err(MGP_E_INVALID, "synth n_cells != context n_cells");
+    }
     if (p->n_reads < 0 || p->n_reads > (int64_t)0xFFFFFFFEll || p->read_len < 12 || p->read_len > 4096)
         return set_err(MGP_E_INVALID, "synth sizes out of range");
     if (ctx->cfg.mito_len < p->read_len) return set_err(MGP_E_INVALID, "mito_len < read_len");
     const int align = p->rec_align ? p->rec_align : 16;
     if (align < 16 || align > 4096 || (align & (align - 1))) return set_err(MGP_E_INVALID, "rec_align must be a power of two in [16, 4096]");
+    MGP_TRY(drain_stream(ctx));
     HIP_TRY(hipSetDevice(ctx->dev));
     HIP_TRY(hipStreamSynchronize(ctx->s_comp));
     HIP_TRY(hipStreamSynchronize(ctx->s_copy));
+    HIP_TRY(hipMemsetAsync(ctx->order_bad.p, 0, 4, ctx->s_copy));
     ctx->n = 0;
     ctx->pay = 0;
     const int64_t n = p->n_reads;
     const int L = ctx->cfg.mito_len;
     const int nc = p->n_cells;
-    // record size is at most 16 + 4*3 + len + (len+1)/2 rounded to 8
+    // bytes the generator writes per record: a packed record (read_len <= MGP_PACK_MAX_LEN),
+    // else the full layout of up to 3 CIGAR operations, at the placement's alignment
     const int64_t max_rec = ((int64_t)mgp_cigar_offset((uint32_t)p->read_len) + 16 + align - 1) & ~(int64_t)(align - 1);
+    const bool packed = p->pack && p->read_len <= MGP_PACK_MAX_LEN;
+    const int64_t rec_bytes = packed ? (int64_t)MGP_PACK_BYTES : max_rec;
     const bool placed = p->rec_off != nullptr;
-    if (placed && (p->payload_bytes < 0 || p->payload_bytes > n * std::max<int64_t>(max_rec, 128) + 128))
-        return set_err(MGP_E_INVALID, "synth payload_bytes out of range");
-    MGP_TRY(ensure_inputs(ctx, std::max<int64_t>(n, 1), placed ? p->payload_bytes : n * max_rec, false));
-    DevBuf cdf, ref;
+    if (placed && p->payload_bytes < 0) return set_err(MGP_E_INVALID, "synth payload_bytes out of range");
+    DevBuf cdf, ref, map;
     MGP_TRY(cdf.ensure((size_t)std::max(nc, 1) * 4));
     MGP_TRY(ref.ensure((size_t)L));
     hipStream_t s = ctx->s_copy;
     if (nc) HIP_TRY(hipMemcpyAsync(cdf.p, p->cell_cdf, (size_t)nc * 4, hipMemcpyHostToDevice, s));
     HIP_TRY(hipMemcpyAsync(ref.p, p->ref_codes, (size_t)L, hipMemcpyHostToDevice, s));
+    // a shard counts its reads first (keep scan only), then allocates for them
+    int64_t n_out = n;
+    int r = MGP_OK;
     int64_t pay = placed ? p->payload_bytes : 0;
-    if (placed && n) {  // every record must fit the payload (the generator writes up to max_rec bytes)
-        for (int64_t i = 0; i < n; ++i)
-            if ((p->rec_off[i] & 15u) || (int64_t)p->rec_off[i] + (p->pack ? MGP_PACK_BYTES : max_rec) > pay) {
-                cdf.release();
-                ref.release();
+    if (shard) {
+        MGP_TRY(map.ensure((size_t)std::max<int64_t>(n, 1) * 8));
+        r = mgp_synth_fill(s, p->seed, n, p->read_len, nc, L, cdf.as<uint32_t>(), ref.as<uint8_t>(), nullptr,
+                           nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, &pay, align, p->pack, -1,
+                           p->cell_lo, p->cell_hi, p->shard_rank, p->shard_world, map.as<uint64_t>(), &n_out);
+        if (r != MGP_OK) return set_err(r, "synth: keep scan failed");
+        pay = placed ? p->payload_bytes : 0;
+    }
+    if (placed && p->payload_bytes > n_out * std::max<int64_t>(max_rec, 128) + 128)
+        return set_err(MGP_E_INVALID, "synth payload_bytes out of range");
+    MGP_TRY(ensure_inputs(ctx, std::max<int64_t>(n_out, 1), placed ? p->payload_bytes : n_out * rec_bytes, false));
+    // placed: rec_off has one entry per kept read
+    if (placed && n_out) {
+        for (int64_t i = 0; i < n_out; ++i)
+            if ((p->rec_off[i] & 15u) || (int64_t)p->rec_off[i] + rec_bytes > pay)
                 return set_err(MGP_E_INVALID, "synth rec_off outside the payload or not 16-byte aligned");
-            }
-        HIP_TRY(hipMemcpyAsync(ctx->roff.p, p->rec_off, (size_t)n * 8, hipMemcpyHostToDevice, s));
+        HIP_TRY(hipMemcpyAsync(ctx->roff.p, p->rec_off, (size_t)n_out * 8, hipMemcpyHostToDevice, s));
     }
-    int r = mgp_synth_fill(s, p->seed, n, p->read_len, nc, L, cdf.as<uint32_t>(), ref.as<uint8_t>(),
-                           ctx->start.as<int32_t>(), ctx->bc.as<int32_t>(), ctx->tlen.as<int32_t>(),
-                           ctx->flag.as<uint16_t>(), ctx->mapq.as<uint8_t>(), ctx->span.as<uint32_t>(),
-                           ctx->roff.as<uint64_t>(), ctx->payload.as<uint8_t>(), &pay, align, p->pack, placed);
-    if (r != MGP_OK) {
-        cdf.release();
-        ref.release();
-        return r;
-    }
+    r = mgp_synth_fill(s, p->seed, n, p->read_len, nc, L, cdf.as<uint32_t>(), ref.as<uint8_t>(),
+                       ctx->start.as<int32_t>(), ctx->bc.as<int32_t>(), ctx->tlen.as<int32_t>(),
+                       ctx->flag.as<uint16_t>(), ctx->mapq.as<uint8_t>(), ctx->span.as<uint32_t>(),
+                       ctx->roff.as<uint64_t>(), ctx->payload.as<uint8_t>(), &pay, align, p->pack, placed,
+                       shard ? p->cell_lo : 0, shard ? p->cell_hi : 0, p->shard_rank, p->shard_world,
+                       map.as<uint64_t>(), &n_out);
+    if (r != MGP_OK) return r == MGP_E_INVALID ? set_err(r, "synth: invalid arguments") : set_err(r, "synth failed");
     HIP_TRY(hipStreamSynchronize(s));
     cdf.release();
     ref.release();
+    map.release();
     HIP_TRY(hipEventRecord(ctx->ev_copy, s));
-    ctx->n = n;
+    ctx->n = n_out;
     ctx->pay = pay;
     ctx->ran = false;
     ctx->no_spec = false;

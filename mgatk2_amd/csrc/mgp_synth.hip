@@ -83,11 +83,41 @@ __device__ __forceinline__ uint64_t rec_size(int ncig, int rl, int align) {
 // are <= 37, at most 3 CIGAR operations with 2 aligned blocks, lengths < 64
 __device__ __forceinline__ bool packs(int rl, int pack) { return pack && rl <= MGP_PACK_MAX_LEN; }
 
-__global__ void k_synth_sizes(uint64_t seed, int64_t n, int rl, int align, int pack, uint64_t* __restrict__ sz) {
+// Cell-range filter (mgp_synth_params.cell_lo/hi, shard_rank/world): a shard of the
+// global read set keeps the reads of its cells (barcode rebased to cell_lo) and, of the
+// reads without a whitelisted barcode, those with index % shard_world == shard_rank.
+struct Filt {
+    int lo, hi, rank, world;  // hi > lo: active
+    const uint64_t* map;      // read index -> index in the shard (exclusive scan of keep)
+};
+
+__device__ __forceinline__ bool keeps(const Filt& f, int64_t i, int b) {
+    if (f.hi <= f.lo) return true;
+    if (b >= 0) return b >= f.lo && b < f.hi;
+    return f.world > 0 && (int)(i % f.world) == f.rank;
+}
+
+__device__ int cell_of(uint64_t h, const uint32_t* cdf, int nc);
+__device__ int read_bc(uint64_t seed, int64_t i, int nc, const uint32_t* cdf);
+
+__global__ void k_synth_sizes(uint64_t seed, int64_t n, int rl, int align, int pack, int nc,
+                              const uint32_t* __restrict__ cdf, Filt f, uint64_t* __restrict__ sz) {
     int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
-    sz[i] = packs(rl, pack) ? (uint64_t)((MGP_PACK_BYTES + align - 1) & ~(align - 1))
+    int64_t j = i;
+    if (f.hi > f.lo) {
+        if (!keeps(f, i, read_bc(seed, i, nc, cdf))) return;
+        j = (int64_t)f.map[i];
+    }
+    sz[j] = packs(rl, pack) ? (uint64_t)((MGP_PACK_BYTES + align - 1) & ~(align - 1))
                             : rec_size(cig_of(seed, i).n, rl, align);
+}
+
+__global__ void k_synth_keep(uint64_t seed, int64_t n, int nc, const uint32_t* __restrict__ cdf, Filt f,
+                             uint64_t* __restrict__ keep) {
+    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    keep[i] = keeps(f, i, read_bc(seed, i, nc, cdf)) ? 1u : 0u;
 }
 
 // ---- generic exclusive scan of u64 (3-phase, 4096 items per block) ----------
@@ -175,7 +205,7 @@ int scan_exclusive_u64(uint64_t* a, int64_t n, hipStream_t s, uint64_t* total) {
     return r;
 }
 
-__device__ __forceinline__ int cell_of(uint64_t h, const uint32_t* cdf, int nc) {
+__device__ int cell_of(uint64_t h, const uint32_t* cdf, int nc) {
     const uint32_t u = (uint32_t)(h & 0xFFFFFFFFull);
     int lo = 0, hi = nc;  // first c with u < cdf[c]
     while (lo < hi) {
@@ -186,14 +216,22 @@ __device__ __forceinline__ int cell_of(uint64_t h, const uint32_t* cdf, int nc) 
     return lo < nc ? lo : nc - 1;
 }
 
+// the barcode column of read i: its origin read's cell, or -1 (no CB / not whitelisted)
+__device__ int read_bc(uint64_t seed, int64_t i, int nc, const uint32_t* cdf) {
+    int64_t A = i;
+    while (read_type(seed, A) != T_ORIG) --A;
+    const int cell = nc > 0 ? cell_of(shash(seed, A, 3), cdf, nc) : -1;
+    return u24(shash(seed, i, 6)) < CAT_NOCB ? -1 : cell;
+}
+
 __device__ __forceinline__ uint32_t code_idx(uint32_t c) { return c == 1 ? 0 : c == 2 ? 1 : c == 4 ? 2 : 3; }
 
 __global__ void k_synth_fill(uint64_t seed, int64_t n, int rl, int nc, int L, const uint32_t* __restrict__ cdf,
                              const uint8_t* __restrict__ ref, int32_t* __restrict__ start, int32_t* __restrict__ bc,
                              int32_t* __restrict__ tlen, uint16_t* __restrict__ flag, uint8_t* __restrict__ mapq,
                              uint32_t* __restrict__ span, const uint64_t* __restrict__ roff,
-                             uint8_t* __restrict__ payload, int pack) {
-    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+                             uint8_t* __restrict__ payload, int pack, Filt flt) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const uint64_t spanpos = (uint64_t)(L - rl + 1);
     int64_t A = i;
@@ -217,12 +255,18 @@ __global__ void k_synth_fill(uint64_t seed, int64_t n, int rl, int nc, int L, co
 
     const bool pk = packs(rl, pack);
     if (pk) f |= MGP_FLAG_PACKED;
-    start[i] = s0;
-    bc[i] = b;
-    tlen[i] = strand ? -tabs : tabs;
-    flag[i] = f;
-    mapq[i] = mq;
-    span[i] = (uint32_t)(cg.cls == C_D ? rl + cg.b : rl);
+    int64_t j = i;  // the read's index in the (shard's) read set
+    if (flt.hi > flt.lo) {
+        if (!keeps(flt, i, b)) return;
+        j = (int64_t)flt.map[i];
+        if (b >= 0) b -= flt.lo;
+    }
+    start[j] = s0;
+    bc[j] = b;
+    tlen[j] = strand ? -tabs : tabs;
+    flag[j] = f;
+    mapq[j] = mq;
+    span[j] = (uint32_t)(cg.cls == C_D ? rl + cg.b : rl);
 
     uint32_t cw[3] = {0, 0, 0};
     if (cg.cls == C_M) {
@@ -239,7 +283,7 @@ __global__ void k_synth_fill(uint64_t seed, int64_t n, int rl, int nc, int L, co
         cw[1] = ((uint32_t)cg.b << 4) | 2;
         cw[2] = ((uint32_t)(rl - cg.a) << 4) | 0;
     }
-    uint8_t* rec = payload + roff[i];
+    uint8_t* rec = payload + roff[j];
     uint8_t* qual = rec + 16;
     uint8_t* seq = rec + mgp_seq_offset((uint32_t)rl);
     if (pk) {  // packed layout (include/mgpileup.h); base bytes are written per base below
@@ -299,27 +343,44 @@ __global__ void k_synth_fill(uint64_t seed, int64_t n, int rl, int nc, int L, co
 
 }  // namespace
 
+// n: reads of the global set; with an active filter (cell_hi > cell_lo) only the
+// shard's reads are written, *n_out of them, barcodes rebased to cell_lo.
 extern "C" int mgp_synth_fill(void* stream, uint64_t seed, int64_t n, int read_len, int n_cells, int mito_len,
                               const uint32_t* d_cdf, const uint8_t* d_ref, int32_t* start, int32_t* bc,
                               int32_t* tlen, uint16_t* flag, uint8_t* mapq, uint32_t* span, uint64_t* roff,
-                              uint8_t* payload, int64_t* payload_bytes, int rec_align, int pack, int placed) {
+                              uint8_t* payload, int64_t* payload_bytes, int rec_align, int pack, int placed,
+                              int cell_lo, int cell_hi, int shard_rank, int shard_world, uint64_t* d_map,
+                              int64_t* n_out) {
     hipStream_t s = (hipStream_t)stream;
     if (read_len < 48) return MGP_E_INVALID;
+    *n_out = n;
     if (n == 0) {
         *payload_bytes = 0;
         return MGP_OK;
     }
     const unsigned nb = (unsigned)((n + kBlock - 1) / kBlock);
+    Filt flt{cell_lo, cell_hi, shard_rank, shard_world, d_map};
+    int64_t nk = n;
+    if (cell_hi > cell_lo) {  // the shard's read indices: exclusive scan of the keep flags
+        k_synth_keep<<<nb, kBlock, 0, s>>>(seed, n, n_cells, d_cdf, flt, d_map);
+        if (hipGetLastError() != hipSuccess) return MGP_E_HIP;
+        uint64_t tot = 0;
+        int r = scan_exclusive_u64(d_map, n, s, &tot);
+        if (r != MGP_OK) return r;
+        nk = (int64_t)tot;
+    }
+    *n_out = nk;
+    if (placed < 0) return MGP_OK;  // the shard's read count only (its placement comes next)
     uint64_t total = (uint64_t)*payload_bytes;
     if (!placed) {  // dense: offsets = exclusive scan of the record sizes; else roff holds the placement
-        k_synth_sizes<<<nb, kBlock, 0, s>>>(seed, n, read_len, rec_align, pack, roff);
+        k_synth_sizes<<<nb, kBlock, 0, s>>>(seed, n, read_len, rec_align, pack, n_cells, d_cdf, flt, roff);
         if (hipGetLastError() != hipSuccess) return MGP_E_HIP;
-        int r = scan_exclusive_u64(roff, n, s, &total);
+        int r = scan_exclusive_u64(roff, nk, s, &total);
         if (r != MGP_OK) return r;
     }
-    if (hipMemsetAsync(payload, 0, (size_t)total, s) != hipSuccess) return MGP_E_HIP;
+    if (total && hipMemsetAsync(payload, 0, (size_t)total, s) != hipSuccess) return MGP_E_HIP;
     k_synth_fill<<<nb, kBlock, 0, s>>>(seed, n, read_len, n_cells, mito_len, d_cdf, d_ref, start, bc, tlen, flag,
-                                       mapq, span, roff, payload, pack);
+                                       mapq, span, roff, payload, pack, flt);
     if (hipGetLastError() != hipSuccess) return MGP_E_HIP;
     if (hipStreamSynchronize(s) != hipSuccess) return MGP_E_HIP;
     *payload_bytes = (int64_t)total;

@@ -37,8 +37,12 @@ ABI_SYMBOLS = (
     "mgp_abi_version", "mgp_last_error", "mgp_device_count", "mgp_open", "mgp_close", "mgp_host_alloc",
     "mgp_host_free", "mgp_push_batch", "mgp_reset", "mgp_resident", "mgp_run", "mgp_sync", "mgp_fetch",
     "mgp_finish", "mgp_kernel_times", "mgp_comm_unique_id", "mgp_comm_init", "mgp_synth_generate",
-    "mgp_download_inputs", "mgp_set_stage_timing",
+    "mgp_download_inputs", "mgp_set_stage_timing", "mgp_fetch_cells", "mgp_fetch_rows16", "mgp_windows",
+    "mgp_stream_info", "mgp_set_streaming",
 )
+ABI_VERSION = 3
+CFG_KEEP_TN5 = 0x1
+CFG_STREAM = 0x2
 
 
 class mgp_config(C.Structure):
@@ -119,6 +123,19 @@ class mgp_synth_params(C.Structure):
         ("pack", C.c_int32),
         ("rec_off", C.c_void_p),
         ("payload_bytes", C.c_int64),
+        ("cell_lo", C.c_int32),
+        ("cell_hi", C.c_int32),
+        ("shard_rank", C.c_int32),
+        ("shard_world", C.c_int32),
+    ]
+
+
+class mgp_rows16(C.Structure):
+    _fields_ = [
+        ("counts", C.c_void_p),
+        ("tn5", C.c_void_p),
+        ("depth", C.c_void_p),
+        ("wide", C.c_void_p),
     ]
 
 
@@ -161,12 +178,17 @@ def load_library(path: Path | None = None) -> C.CDLL:
         "mgp_comm_init": ([vp, C.c_char_p, C.c_int, C.c_int], C.c_int),
         "mgp_synth_generate": ([vp, C.POINTER(mgp_synth_params)], C.c_int),
         "mgp_download_inputs": ([vp] + [vp] * 8, C.c_int),
+        "mgp_fetch_cells": ([vp, i32, i32, C.POINTER(mgp_result)], C.c_int),
+        "mgp_fetch_rows16": ([vp, i32, i32, C.POINTER(mgp_rows16)], C.c_int),
+        "mgp_windows": ([vp, C.POINTER(i32), C.POINTER(i32)], C.c_int),
+        "mgp_stream_info": ([vp, C.POINTER(i64), C.POINTER(i32)], C.c_int),
+        "mgp_set_streaming": ([vp, C.c_int], C.c_int),
     }
     for name, (args, res) in sig.items():
         fn = getattr(lib, name)
         fn.argtypes = args
         fn.restype = res
-    if lib.mgp_abi_version() != 2:
+    if lib.mgp_abi_version() != ABI_VERSION:
         raise ProcessingError("libmgpileup ABI version mismatch")
     if path is None:
         _lib = lib
@@ -210,13 +232,15 @@ class EngineConfig:
     reserve_reads: int = 0
     reserve_payload: int = 0
     keep_tn5: bool = False  # MGP_CFG_KEEP_TN5
+    stream: bool = False  # MGP_CFG_STREAM: pushes run the windows they complete (overlapped H2D)
 
     def to_c(self) -> mgp_config:
         dm = DEDUP_MODES[self.dedup_mode] if isinstance(self.dedup_mode, str) else int(self.dedup_mode)
+        flags = (CFG_KEEP_TN5 if self.keep_tn5 else 0) | (CFG_STREAM if self.stream else 0)
         return mgp_config(
             int(self.min_baseq), int(self.min_mapq), int(self.min_distance_from_end), dm,
             float(self.max_strand_bias), int(self.min_reads), int(self.n_cells), int(self.mito_len),
-            1 if self.keep_tn5 else 0, int(self.reserve_reads), int(self.reserve_payload),
+            flags, int(self.reserve_reads), int(self.reserve_payload),
         )
 
 
@@ -270,6 +294,22 @@ class EngineResult:
         """Cells with >= 1 kept read in first-seen BAM order (dict order of reads_by_barcode)."""
         idx = np.flatnonzero(self.n_reads > 0)
         return idx[np.argsort(self.first_read[idx], kind="stable")]
+
+
+@dataclass
+class Rows16:
+    """The pileup's 16-bit result rows of a cell range (mgp_rows16): exact except in
+    `wide` (cell, window) pairs, where they saturate at 65535."""
+
+    counts: np.ndarray  # [cells, L, 8] u16
+    tn5: np.ndarray  # [cells, L, 2] u16
+    depth: np.ndarray  # [cells, L] u16
+    wide: np.ndarray  # [cells, n_windows] u8
+    window_width: int
+
+    def wide_cells(self) -> np.ndarray:
+        """Cells (range-relative) with a window whose 16-bit rows are not exact."""
+        return np.flatnonzero(self.wide.any(axis=1))
 
 
 def batch_struct(soa: ReadSoA) -> mgp_batch:
@@ -330,27 +370,36 @@ class Engine:
         return int(n.value), int(p.value)
 
     def synth(self, seed: int, n_reads: int, cdf: np.ndarray, ref: np.ndarray, read_len: int = 50,
-              rec_align: int = 64, pack: bool = True, rec_off: np.ndarray | None = None, payload_bytes: int = 0):
+              rec_align: int = 64, pack: bool = True, rec_off: np.ndarray | None = None, payload_bytes: int = 0,
+              cells: tuple[int, int] | None = None, shard: tuple[int, int] = (0, 0)):
         """Device-side synthetic workload (replaces the resident set). rec_off: an
         explicit placement of the records (e.g. host placement of
-        mgp_place_records, `synth.place_records`); None = dense in BAM order."""
+        mgp_place_records, `synth.place_records`); None = dense in BAM order.
+        cells=(lo, hi): only the reads of those cells of the n_reads-read global set
+        (len(cdf) cells; this context's n_cells must be hi - lo), barcodes rebased to
+        lo, plus the reads without a whitelisted barcode whose index % world == rank
+        for shard=(rank, world) (world 0: none)."""
         cdf = np.ascontiguousarray(cdf, np.uint32)
         ref = np.ascontiguousarray(ref, np.uint8)
         ro = None if rec_off is None else np.ascontiguousarray(rec_off, np.uint64)
-        if ro is not None and ro.shape[0] != n_reads:
+        lo, hi = cells if cells is not None else (0, 0)
+        if ro is not None and cells is None and ro.shape[0] != n_reads:
             raise ValueError("rec_off must have n_reads entries")
-        p = mgp_synth_params(int(seed), int(n_reads), int(read_len), int(self.cfg.n_cells), _ptr(cdf), _ptr(ref),
+        p = mgp_synth_params(int(seed), int(n_reads), int(read_len), int(cdf.shape[0]), _ptr(cdf), _ptr(ref),
                              int(rec_align), int(bool(pack)), None if ro is None else _ptr(ro),
-                             int(payload_bytes) if ro is not None else 0)
+                             int(payload_bytes) if ro is not None else 0, int(lo), int(hi), int(shard[0]),
+                             int(shard[1]))
         _ck(self.lib.mgp_synth_generate(self._h, C.byref(p)), "mgp_synth_generate")
 
-    def download_inputs(self, columns: tuple[str, ...] | None = None) -> ReadSoA:
+    def download_inputs(self, columns: tuple[str, ...] | None = None, alloc=None) -> ReadSoA:
         """Resident inputs back on the host; `columns` limits the copy to those SoA
-        fields (the others are empty arrays)."""
+        fields (the others are empty arrays). alloc(n, dtype) -> array: where the
+        columns go (e.g. views of a PinnedBuffer); np.zeros by default."""
         n, pay = self.resident()
 
         def col(name, dt, m):
-            return np.zeros(m if columns is None or name in columns else 0, dt)
+            m = m if columns is None or name in columns else 0
+            return alloc(m, dt) if alloc is not None and m else np.zeros(m, dt)
 
         soa = ReadSoA(
             col("start", np.int32, n), col("bc", np.int32, n), col("tlen", np.int32, n), col("flag", np.uint16, n),
@@ -383,6 +432,58 @@ class Engine:
         _ck(self.lib.mgp_fetch(self._h, C.byref(cres)), "mgp_fetch")
         res.stats = st.as_dict()
         return res
+
+    def fetch_cells(self, lo: int, hi: int, dense: bool = True) -> EngineResult:
+        """mgp_fetch_cells: the results of cells [lo, hi) (cell lo at index 0)."""
+        res = EngineResult.alloc(hi - lo, self.cfg.mito_len, dense)
+        st = mgp_stats()
+        cres = res.to_c(st)
+        _ck(self.lib.mgp_fetch_cells(self._h, int(lo), int(hi), C.byref(cres)), "mgp_fetch_cells")
+        res.stats = st.as_dict()
+        return res
+
+    def fetch_compact(self) -> EngineResult:
+        """The run's results with the per-position arrays as the pileup's exact
+        16-bit rows (u16 counts/tn5/depth: half the bytes of mgp_fetch's u32 arrays,
+        no widening pass on the device). A run with a wide window (a cell window of
+        more than 65535 reads) falls back to the exact u32 arrays."""
+        res = self.fetch(dense=False)
+        r16 = self.fetch_rows16()
+        if r16.wide.any():
+            return self.fetch(dense=True)
+        res.counts, res.tn5, res.depth = r16.counts, r16.tn5, r16.depth
+        return res
+
+    def windows(self) -> tuple[int, int]:
+        nw, w = C.c_int32(), C.c_int32()
+        _ck(self.lib.mgp_windows(self._h, C.byref(nw), C.byref(w)), "mgp_windows")
+        return int(nw.value), int(w.value)
+
+    def fetch_rows16(self, lo: int = 0, hi: int | None = None, out: Rows16 | None = None) -> Rows16:
+        """mgp_fetch_rows16: the 16-bit result rows of cells [lo, hi) (into `out`'s
+        arrays when given, e.g. pinned host memory)."""
+        hi = self.cfg.n_cells if hi is None else hi
+        nw, w = self.windows()
+        L, m = self.cfg.mito_len, hi - lo
+        if out is None:
+            out = Rows16(np.empty((m, L, 8), np.uint16), np.empty((m, L, 2), np.uint16), np.empty((m, L), np.uint16),
+                         np.empty((m, nw), np.uint8), w)
+        for a, shape in ((out.counts, (m, L, 8)), (out.tn5, (m, L, 2)), (out.depth, (m, L)), (out.wide, (m, nw))):
+            if a.shape != shape or not a.flags["C_CONTIGUOUS"]:
+                raise InvalidInputError(f"rows16 array of shape {a.shape}, expected {shape}")
+        r = mgp_rows16(_ptr(out.counts), _ptr(out.tn5), _ptr(out.depth), _ptr(out.wide))
+        _ck(self.lib.mgp_fetch_rows16(self._h, int(lo), int(hi), C.byref(r)), "mgp_fetch_rows16")
+        return out
+
+    def set_streaming(self, on: bool):
+        """Streaming runs on or off for the next pushes (EngineConfig.stream initially)."""
+        _ck(self.lib.mgp_set_streaming(self._h, int(bool(on))), "mgp_set_streaming")
+
+    def stream_info(self) -> tuple[int, bool]:
+        """(segments queued by pushes so far, whether the last run was streamed)."""
+        n, last = C.c_int64(), C.c_int32()
+        _ck(self.lib.mgp_stream_info(self._h, C.byref(n), C.byref(last)), "mgp_stream_info")
+        return int(n.value), bool(last.value)
 
     def finish(self, dense: bool = True) -> EngineResult:
         self.run()
@@ -422,6 +523,44 @@ class Engine:
         if len(uid) != 128:
             raise InvalidInputError("RCCL unique id must be 128 bytes")
         _ck(self.lib.mgp_comm_init(self._h, C.c_char_p(uid), int(nranks), int(rank)), "mgp_comm_init")
+
+
+class _PinnedView:
+    """numpy array-interface holder that keeps its PinnedBuffer alive."""
+
+    def __init__(self, owner, addr: int, shape, dtype):
+        self._owner = owner
+        self.__array_interface__ = {"data": (addr, False), "shape": tuple(shape), "typestr": np.dtype(dtype).str,
+                                    "version": 3}
+
+
+class PinnedBuffer:
+    """Page-locked host memory from mgp_host_alloc (hipHostMalloc): H2D/D2H copies
+    from it run asynchronously at the link's rate. `array(shape, dtype, offset)`
+    gives numpy views, which keep the buffer alive."""
+
+    def __init__(self, nbytes: int):
+        self.lib = load_library()
+        self.nbytes = int(nbytes)
+        p = C.c_void_p()
+        _ck(self.lib.mgp_host_alloc(max(self.nbytes, 1), C.byref(p)), "mgp_host_alloc")
+        self._p = p
+
+    def array(self, shape, dtype, offset: int = 0) -> np.ndarray:
+        dt = np.dtype(dtype)
+        shape = (int(shape),) if np.ndim(shape) == 0 else tuple(int(x) for x in shape)
+        count = int(np.prod(shape))
+        if offset % dt.itemsize or offset + count * dt.itemsize > self.nbytes:
+            raise ValueError("pinned view outside the buffer or misaligned")
+        return np.asarray(_PinnedView(self, self._p.value + offset, shape, dt))
+
+    def __del__(self):
+        try:
+            if getattr(self, "_p", None) is not None and self._p.value:
+                self.lib.mgp_host_free(self._p)
+                self._p = None
+        except Exception:
+            pass
 
 
 def device_count() -> int:

@@ -142,7 +142,7 @@ class MtDNAPipeline:
                 logger.warning("Failed to generate HTML report: %s", e)
         t4 = time.time()
         self.timings = {"bam_ingest": t1 - t0, "engine": t2 - t1, "write": t3 - t2, "report": t4 - t3,
-                        "total": t4 - t0}
+                        "total": t4 - t0, **processor.last_timing}
         logger.info("Pipeline complete")
         logger.info("Elapsed time: %.1fs (ingest %.1fs, engine %.1fs, write %.1fs)", t4 - t0, t1 - t0, t2 - t1,
                     t3 - t2)

@@ -115,3 +115,18 @@ def test_two_rank_gloo(case):
     res = dict(q.get(timeout=5) for _ in procs)
     assert res == {0: "ok", 1: "ok"}, res
     assert all(p.exitcode == 0 for p in procs)
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_bench_launcher(world):
+    """bench.py's own launcher (`python bench.py --gpus N` without torchrun): N
+    worker processes with RANK/WORLD_SIZE set, gloo rendezvous on 127.0.0.1, the
+    bench's cell split, per-rank shards through the oracle, tallies all-reduced."""
+    import sys
+    from pathlib import Path
+
+    sys.path.insert(0, str(Path(__file__).resolve().parent.parent))
+    import bench
+
+    script = str(Path(__file__).resolve().parent / "_bench_rank.py")
+    assert bench.launch_workers(world, [sys.executable, script]) == 0

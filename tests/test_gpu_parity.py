@@ -455,6 +455,108 @@ def test_full_size_invariants_and_cell_sample_c3(engine_lib, oracle_lib):
             np.testing.assert_array_equal(getattr(res, k)[lo:hi], getattr(exp, k), err_msg=f"cells {lo}-{hi} {k}")
 
 
+def _rows16_invariants(r16, res, lo, hi):
+    """Size-independent properties of cells [lo, hi) from their 16-bit rows (exact:
+    no wide window) and per-cell statistics."""
+    assert not r16.wide.any()
+    depth = r16.depth.astype(np.uint64)
+    np.testing.assert_array_equal(r16.counts.sum(axis=2, dtype=np.uint64), depth)
+    assert not np.any(r16.tn5[r16.depth == 0])
+    np.testing.assert_array_equal(res.covered[lo:hi], (r16.depth > 0).sum(axis=1))
+    np.testing.assert_array_equal(res.depth_sum[lo:hi], depth.sum(axis=1))
+    np.testing.assert_array_equal(res.depth_max[lo:hi], r16.depth.max(axis=1))
+    ok = res.passed[lo:hi].astype(bool)
+    assert np.all(res.median_lo[lo:hi][ok] <= res.median_hi[lo:hi][ok])
+    assert np.all(res.median_hi[lo:hi][ok] <= res.depth_max[lo:hi][ok])
+    return r16.counts[ok].reshape(int(ok.sum()), -1, 4, 2).sum(axis=(0, 3), dtype=np.uint64)
+
+
+def test_full_size_invariants_and_cell_sample_c4(engine_lib, oracle_lib):
+    """BASELINE config C4 at full size (200M reads x 10k cells, `run` parameters,
+    the bench's cell-paired placement): the per-cell invariants over every cell
+    (16-bit rows: none is wide), the run statistics and tallies, a rerun, and three
+    samples of 8 whole cells bit-exact against the oracle on exactly their reads."""
+    from mgatk2_amd.bam import PLACE_PAIRED, place_records
+    from mgatk2_amd.engine import Engine, EngineConfig
+    from mgatk2_amd.shard import shard_soa
+    from mgatk2_amd.synth import cell_cdf, ref_codes
+
+    n, nc, seed = 200_000_000, 10_000, 20251015 + 4
+    cfg = EngineConfig(n_cells=nc, min_baseq=20, min_mapq=30, dedup_mode="alignment_and_fragment_length",
+                       min_reads=1)
+    cdf, ref = cell_cdf(seed, nc), ref_codes(seed)
+    with Engine(cfg) as eng:
+        eng.synth(seed, n, cdf, ref)
+        cols = eng.download_inputs(columns=("bc", "flag", "start", "tlen"))
+        roff, pay_b = place_records(cols.bc, cols.flag, np.full(n, 64, np.uint32), nc, PLACE_PAIRED,
+                                    start=cols.start, tlen=cols.tlen)
+        del cols
+        eng.synth(seed, n, cdf, ref, rec_off=roff, payload_bytes=pay_b)
+        del roff
+        eng.run()
+        res = eng.fetch(dense=False)
+        tally = np.zeros_like(res.ref_tally)
+        for lo in range(0, nc, 2500):
+            tally += _rows16_invariants(eng.fetch_rows16(lo, lo + 2500), res, lo, lo + 2500)
+        samples = {(lo, hi): eng.fetch_cells(lo, hi) for lo, hi in ((0, 8), (5000, 5008), (nc - 8, nc))}
+        first = eng.fetch_rows16(0, 2500).counts
+        eng.run()
+        again = eng.fetch(dense=False)
+        np.testing.assert_array_equal(eng.fetch_rows16(0, 2500).counts, first)
+        del first
+        inputs = eng.download_inputs()
+    assert res.stats["total_reads"] == n and res.stats["error_bits"] == 0
+    np.testing.assert_array_equal(res.ref_tally, tally)
+    ok = res.passed.astype(bool)
+    assert res.stats["filtered_reads"] == int(res.n_reads.sum())
+    assert res.stats["n_barcodes"] == int((res.n_reads > 0).sum())
+    assert res.stats["cells_passed"] == int(ok.sum())
+    assert res.stats["duplicate_reads_with_length"] <= res.stats["duplicate_reads_position_only"]
+    for k in ("n_reads", "covered", "depth_sum", "median_lo", "median_hi", "ref_tally"):
+        np.testing.assert_array_equal(getattr(res, k), getattr(again, k), err_msg=f"rerun {k}")
+    for (lo, hi), got in samples.items():
+        sub, _ = shard_soa(inputs, lo, hi)
+        exp, _ = oracle_lib.oracle_run(EngineConfig(**{**cfg.__dict__, "n_cells": hi - lo}), sub)
+        for k in ("counts", "tn5", "depth", "n_reads", "any_paired", "passed", "covered", "depth_sum",
+                  "depth_max", "median_lo", "median_hi"):
+            np.testing.assert_array_equal(getattr(got, k), getattr(exp, k), err_msg=f"cells {lo}-{hi} {k}")
+
+
+def test_full_size_cell_samples_c5(engine_lib, oracle_lib):
+    """BASELINE config C5 on one GPU (1B reads x 100k cells, `run` parameters):
+    sampled cell ranges of the full-size run bit-exact against the oracle on exactly
+    their reads (regenerated as a cell shard of the same global set), the per-cell
+    invariants over 4 ranges of 2000 cells, and the run statistics."""
+    from mgatk2_amd.engine import Engine, EngineConfig
+    from mgatk2_amd.synth import cell_cdf, ref_codes
+
+    n, nc, seed = 1_000_000_000, 100_000, 20251015 + 5
+    cfg = EngineConfig(n_cells=nc, min_baseq=20, min_mapq=30, dedup_mode="alignment_and_fragment_length",
+                       min_reads=1)
+    cdf, ref = cell_cdf(seed, nc), ref_codes(seed)
+    ranges = ((0, 8), (49_996, 50_012), (nc - 8, nc))
+    with Engine(cfg) as eng:
+        eng.synth(seed, n, cdf, ref)
+        eng.run()
+        res = eng.fetch(dense=False)
+        for lo in (0, 31_000, 64_000, nc - 2000):
+            _rows16_invariants(eng.fetch_rows16(lo, lo + 2000), res, lo, lo + 2000)
+        samples = {r: eng.fetch_cells(*r) for r in ranges}
+    assert res.stats["total_reads"] == n and res.stats["error_bits"] == 0
+    assert res.stats["filtered_reads"] == int(res.n_reads.sum())
+    assert res.stats["cells_passed"] == int(res.passed.sum())
+    for (lo, hi), got in samples.items():
+        scfg = EngineConfig(**{**cfg.__dict__, "n_cells": hi - lo})
+        with Engine(scfg) as e2:
+            e2.synth(seed, n, cdf, ref, cells=(lo, hi), shard=(0, 0))
+            sub = e2.download_inputs()
+        assert sub.n > 1000 * (hi - lo)
+        exp, _ = oracle_lib.oracle_run(scfg, sub)
+        for k in ("counts", "tn5", "depth", "n_reads", "any_paired", "passed", "covered", "depth_sum",
+                  "depth_max", "median_lo", "median_hi"):
+            np.testing.assert_array_equal(getattr(got, k), getattr(exp, k), err_msg=f"cells {lo}-{hi} {k}")
+
+
 # ---------------------------------------------------------------------------
 # payload placement (mgp_place_records): cell-paired lines; grouping pass A's
 # offset sources (dense index / u32 column / u64 column, the input check in k_bin_count)

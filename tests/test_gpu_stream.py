@@ -1,0 +1,333 @@
+"""GPU: the ABI v3 paths — cell shards of one synthetic read set (the strong-scaling
+bench), cell-range and 16-bit result fetches, streaming runs (MGP_CFG_STREAM: each
+push runs the windows it completes while later batches are still being copied),
+and the all-reduced speculative-grouping rerun of a communicator run. Every result
+is compared bit for bit with a resident run, the oracle or the reference goldens."""
+
+from __future__ import annotations
+
+import numpy as np
+import pytest
+
+from golden_io import CASES, Golden, check_result
+
+pytestmark = pytest.mark.gpu
+
+CONFIGS = {
+    "tenx": dict(min_baseq=0, min_mapq=0, dedup_mode="alignment_start", min_reads=0),
+    "run": dict(min_baseq=20, min_mapq=30, dedup_mode="alignment_and_fragment_length", min_reads=1),
+    "bias": dict(min_baseq=10, min_mapq=1, dedup_mode="none", min_reads=40, max_strand_bias=0.8),
+}
+KEYS = ("counts", "tn5", "depth", "n_reads", "any_paired", "passed", "covered", "depth_sum", "depth_max",
+        "median_lo", "median_hi", "ref_tally")
+STATS = ("total_reads", "filtered_reads", "n_barcodes", "duplicate_reads_with_length",
+         "duplicate_reads_position_only", "cells_passed")
+
+
+def assert_same(a, b, what="", keys=KEYS, order=True):
+    for k in keys:
+        x, y = getattr(a, k), getattr(b, k)
+        if x is None or y is None:
+            continue
+        np.testing.assert_array_equal(x, y, err_msg=f"{what}: {k}")
+    if order:
+        np.testing.assert_array_equal(a.cell_order(), b.cell_order(), err_msg=f"{what}: order")
+    for k in STATS:
+        assert a.stats[k] == b.stats[k], (what, k, a.stats[k], b.stats[k])
+
+
+def run_resident(engine_lib, cfg, soa):
+    with engine_lib.Engine(cfg) as eng:
+        eng.push(soa)
+        return eng.finish()
+
+
+def run_streamed(engine_lib, cfg, soa, batches):
+    """Pushes in `batches` coordinate-ordered slices on a streaming context."""
+    from dataclasses import replace
+
+    scfg = replace(cfg, stream=True, reserve_reads=soa.n, reserve_payload=int(soa.payload.shape[0]) + 256 * (batches + 1))
+    with engine_lib.Engine(scfg) as eng:
+        seg0, _ = eng.stream_info()
+        cuts = np.linspace(0, soa.n, batches + 1).astype(int)
+        for a, b in zip(cuts[:-1], cuts[1:]):
+            if b > a:
+                eng.push(soa.slice(int(a), int(b)))
+        segs, _ = eng.stream_info()
+        eng.run()
+        res = eng.fetch()
+        _, streamed = eng.stream_info()
+        return res, segs - seg0, streamed
+
+
+def _synth(seed, n, nc):
+    from mgatk2_amd.synth import synth_reads
+
+    return synth_reads(seed, n, nc)
+
+
+# ---------------------------------------------------------------------------
+# cell shards of one global read set (device generator)
+# ---------------------------------------------------------------------------
+def test_synth_cell_shards_partition_the_global_set(engine_lib):
+    from mgatk2_amd.engine import EngineConfig
+    from mgatk2_amd.shard import partition_cells
+    from mgatk2_amd.synth import cell_cdf, ref_codes
+
+    n, nc, seed, world = 300_000, 60, 4242, 3
+    cdf, ref = cell_cdf(seed, nc), ref_codes(seed)
+    with engine_lib.Engine(EngineConfig(n_cells=nc)) as eng:
+        eng.synth(seed, n, cdf, ref)
+        full = eng.download_inputs()
+    w = np.diff(np.concatenate([[0], cdf.astype(np.float64)]))
+    b = partition_cells(w, world)
+    seen = 0
+    for r in range(world):
+        lo, hi = int(b[r]), int(b[r + 1])
+        with engine_lib.Engine(EngineConfig(n_cells=hi - lo)) as eng:
+            eng.synth(seed, n, cdf, ref, cells=(lo, hi), shard=(r, world))
+            sh = eng.download_inputs()
+        i = np.arange(n)
+        idx = np.flatnonzero(((full.bc >= lo) & (full.bc < hi)) | ((full.bc < 0) & (i % world == r)))
+        assert sh.n == idx.size
+        seen += sh.n
+        for k in ("start", "tlen", "flag", "mapq", "span"):
+            np.testing.assert_array_equal(getattr(sh, k), getattr(full, k)[idx], err_msg=k)
+        np.testing.assert_array_equal(sh.bc, np.where(full.bc[idx] >= 0, full.bc[idx] - lo, -1))
+        # packed 64-byte records, dense in both sets: record j of the shard is record idx[j]
+        rec_sh = sh.payload.reshape(-1, 64)[(sh.rec_off // 64).astype(np.int64)]
+        rec_full = full.payload.reshape(-1, 64)[(full.rec_off[idx] // 64).astype(np.int64)]
+        np.testing.assert_array_equal(rec_sh, rec_full)
+    assert seen == n
+
+
+def test_shard_runs_equal_the_global_run(engine_lib):
+    """Each rank's shard run (cells [lo, hi) of the global set) gives exactly the
+    global run's rows of those cells; the tallies sum to the global tallies."""
+    from mgatk2_amd.engine import EngineConfig
+    from mgatk2_amd.shard import partition_cells
+    from mgatk2_amd.synth import cell_cdf, ref_codes
+
+    n, nc, seed, world = 400_000, 90, 777, 4
+    cfg = EngineConfig(n_cells=nc, **CONFIGS["run"])
+    cdf, ref = cell_cdf(seed, nc), ref_codes(seed)
+    with engine_lib.Engine(cfg) as eng:
+        eng.synth(seed, n, cdf, ref)
+        whole = eng.finish()
+    b = partition_cells(np.diff(np.concatenate([[0], cdf.astype(np.float64)])), world)
+    tally = np.zeros_like(whole.ref_tally)
+    total = filt = dups = 0
+    for r in range(world):
+        lo, hi = int(b[r]), int(b[r + 1])
+        scfg = EngineConfig(**{**cfg.__dict__, "n_cells": hi - lo})
+        with engine_lib.Engine(scfg) as eng:
+            eng.synth(seed, n, cdf, ref, cells=(lo, hi), shard=(r, world))
+            part = eng.finish()
+        for k in KEYS[:-1]:
+            np.testing.assert_array_equal(getattr(part, k), getattr(whole, k)[lo:hi], err_msg=f"rank {r} {k}")
+        tally += part.ref_tally
+        total += part.stats["total_reads"]
+        filt += part.stats["filtered_reads"]
+        dups += part.stats["duplicate_reads_with_length"]
+    np.testing.assert_array_equal(tally, whole.ref_tally)
+    assert total == n and filt == whole.stats["filtered_reads"]
+    assert dups == whole.stats["duplicate_reads_with_length"]
+
+
+# ---------------------------------------------------------------------------
+# cell-range and 16-bit fetches
+# ---------------------------------------------------------------------------
+def test_fetch_cells_and_rows16_match_fetch(engine_lib):
+    from mgatk2_amd.engine import EngineConfig
+
+    soa = _synth(31, 200_000, 40)
+    cfg = EngineConfig(n_cells=40, **CONFIGS["tenx"])
+    with engine_lib.Engine(cfg) as eng:
+        eng.push(soa)
+        eng.run()
+        full = eng.fetch()
+        for lo, hi in ((0, 40), (0, 1), (7, 19), (39, 40), (5, 5)):
+            part = eng.fetch_cells(lo, hi)
+            for k in KEYS[:-1] + ("first_read",):
+                np.testing.assert_array_equal(getattr(part, k), getattr(full, k)[lo:hi], err_msg=f"{lo}-{hi} {k}")
+            np.testing.assert_array_equal(part.ref_tally, full.ref_tally)
+            r16 = eng.fetch_rows16(lo, hi)
+            assert not r16.wide.any()
+            np.testing.assert_array_equal(r16.counts.astype(np.uint32), full.counts[lo:hi])
+            np.testing.assert_array_equal(r16.tn5.astype(np.uint32), full.tn5[lo:hi])
+            np.testing.assert_array_equal(r16.depth.astype(np.uint32), full.depth[lo:hi])
+        with pytest.raises(Exception):
+            eng.fetch_cells(3, 41)
+
+
+def test_rows16_wide_windows_saturate_and_fetch_cells_is_exact(engine_lib, oracle_lib):
+    """A cell window with more than 65535 reads is flagged wide: its 16-bit rows
+    saturate at 65535 (the HDF5 form), the cell-range fetch has the exact values."""
+    from mgatk2_amd.engine import EngineConfig
+    from mgatk2_amd.synth import synth_reads
+
+    # one cell, 400k reads all starting in positions [0, 60): ~180k deep, so the first
+    # window holds more than 65535 reads and is drained into the u32 rows
+    deep = synth_reads(91, 400_000, 1)
+    assert np.all(deep.rec_off == 64 * np.arange(deep.n, dtype=np.uint64))  # dense packed records
+    deep.start[:] = np.sort(deep.start % 60).astype(np.int32)
+    deep.payload.reshape(-1, 64)[:, 0:4] = deep.start.view(np.uint8).reshape(-1, 4)
+    cfg = EngineConfig(n_cells=1, min_baseq=0, min_mapq=0, dedup_mode="none", min_reads=0)
+    with engine_lib.Engine(cfg) as eng:
+        eng.push(deep)
+        eng.run()
+        exact = eng.fetch()
+        r16 = eng.fetch_rows16()
+    exp, _ = oracle_lib.oracle_run(cfg, deep)
+    np.testing.assert_array_equal(exact.counts, exp.counts)
+    np.testing.assert_array_equal(exact.depth, exp.depth)
+    assert r16.wide[0, 0] == 1
+    np.testing.assert_array_equal(r16.depth.astype(np.uint32), np.minimum(exp.depth, 65535))
+    np.testing.assert_array_equal(r16.counts.astype(np.uint32), np.minimum(exp.counts, 65535))
+    assert exp.depth.max() > 65535
+
+
+# ---------------------------------------------------------------------------
+# streaming runs
+# ---------------------------------------------------------------------------
+@pytest.mark.parametrize("batches", [1, 3, 17, 64])
+@pytest.mark.parametrize("cfgname", sorted(CONFIGS))
+def test_streaming_matches_resident(engine_lib, cfgname, batches):
+    from mgatk2_amd.engine import EngineConfig
+
+    soa = _synth(5000 + batches, 600_000, 150)
+    cfg = EngineConfig(n_cells=150, **CONFIGS[cfgname])
+    want = run_resident(engine_lib, cfg, soa)
+    got, segs, streamed = run_streamed(engine_lib, cfg, soa, batches)
+    assert_same(got, want, f"stream {cfgname} x{batches}")
+    np.testing.assert_array_equal(got.first_read, want.first_read)
+    assert streamed == (segs > 0)
+    if batches >= 3:
+        assert segs >= 1  # some window completed before the last push
+
+
+@pytest.mark.parametrize("cfgname", ["run", "tenx"])
+def test_streaming_paired_placement_matches_oracle(engine_lib, oracle_lib, cfgname):
+    from mgatk2_amd.engine import EngineConfig
+    from mgatk2_amd.synth import relocate
+
+    soa = relocate(_synth(77, 400_000, 120), paired=True, n_cells=120)
+    cfg = EngineConfig(n_cells=120, **CONFIGS[cfgname])
+    got, segs, streamed = run_streamed(engine_lib, cfg, soa, 9)
+    exp, _ = oracle_lib.oracle_run(cfg, soa)
+    assert segs >= 1 and streamed
+    assert_same(got, exp, f"stream paired {cfgname}")
+
+
+def test_streaming_long_span_halo(engine_lib, oracle_lib):
+    """Reads reaching hundreds of positions past their start (declared spans) in
+    early batches: the later segments' halos must take them."""
+    from mgatk2_amd.engine import EngineConfig
+    from mgatk2_amd.synth import concat_soa, pack_reads
+
+    base = _synth(58, 300_000, 40)
+    reads = []
+    for s0 in (1200, 2600, 5000, 9000, 12000):
+        for k in range(40):
+            reads.append(dict(reference_start=s0 + k % 5, cigartuples=[(0, 10), (2, 700), (0, 30)],
+                              query_sequence="ACGT" * 10, query_qualities=[37] * 40, bc=40 + k % 2, flag=0x1,
+                              mapping_quality=60, template_length=500 + k))
+    extra = pack_reads(reads)
+    soa = concat_soa([base, extra])
+    order = np.argsort(soa.start, kind="stable")
+    from mgatk2_amd.shard import shard_soa
+    from mgatk2_amd.synth import ReadSoA
+
+    sorted_soa = ReadSoA(soa.start[order], soa.bc[order], soa.tlen[order], soa.flag[order], soa.mapq[order],
+                         soa.span[order], soa.rec_off[order], soa.payload)
+    sorted_soa, _ = shard_soa(sorted_soa, 0, 42, paired=False, keep_all=True)
+    cfg = EngineConfig(n_cells=42, **CONFIGS["tenx"])
+    got, segs, streamed = run_streamed(engine_lib, cfg, sorted_soa, 25)
+    exp, _ = oracle_lib.oracle_run(cfg, sorted_soa)
+    assert segs >= 2 and streamed
+    assert got.stats["max_span"] >= 740
+    assert_same(got, exp, "stream long spans")
+
+
+@pytest.mark.parametrize("case", CASES)
+def test_streaming_goldens_fall_back_and_match(engine_lib, case):
+    """The goldens hold full-layout records, quirk reads and mixed pairedness: a
+    streaming run cannot serve them speculatively and reruns resident, with the
+    reference's results."""
+    g = Golden(case)
+    got, segs, streamed = run_streamed(engine_lib, g.config(), g.soa, 7)
+    check_result(got, g)
+
+
+def test_streaming_unsorted_raises(engine_lib):
+    from mgatk2_amd.engine import EngineConfig
+    from mgatk2_amd.exceptions import BAMFormatError
+
+    soa = _synth(12, 200_000, 20)
+    a, b = soa.slice(0, 100_000), soa.slice(100_000, 200_000)
+    from dataclasses import replace
+
+    cfg = replace(EngineConfig(n_cells=20, **CONFIGS["run"]), stream=True, reserve_reads=soa.n,
+                  reserve_payload=int(soa.payload.shape[0]) + 4096)
+    with engine_lib.Engine(cfg) as eng:
+        eng.push(b)
+        eng.push(a)  # starts go back: not coordinate order
+        eng.run()
+        with pytest.raises(BAMFormatError):
+            eng.sync()
+        # the same context then runs sorted input correctly
+        eng.reset()
+        eng.push(a)
+        eng.push(b)
+        eng.run()
+        got = eng.fetch()
+    want = run_resident(engine_lib, EngineConfig(n_cells=20, **CONFIGS["run"]), soa)
+    assert_same(got, want, "after unsorted")
+
+
+def test_streaming_repeated_runs_and_resident_rerun(engine_lib):
+    """A second mgp_run on the same resident set (no pushes) runs resident; a new
+    streamed set after mgp_reset streams again."""
+    from dataclasses import replace
+
+    from mgatk2_amd.engine import EngineConfig
+
+    soa = _synth(99, 300_000, 64)
+    cfg = EngineConfig(n_cells=64, **CONFIGS["run"])
+    want = run_resident(engine_lib, cfg, soa)
+    scfg = replace(cfg, stream=True, reserve_reads=soa.n, reserve_payload=int(soa.payload.shape[0]) + 8192)
+    with engine_lib.Engine(scfg) as eng:
+        for rep in range(2):
+            eng.reset()
+            for a in range(0, soa.n, 50_000):
+                eng.push(soa.slice(a, min(soa.n, a + 50_000)))
+            eng.run()
+            assert_same(eng.fetch(), want, f"streamed {rep}")
+            assert eng.stream_info()[1]
+            eng.run()  # resident rerun of the same set
+            assert_same(eng.fetch(), want, f"resident {rep}")
+            assert not eng.stream_info()[1]
+
+
+# ---------------------------------------------------------------------------
+# communicator: the speculative grouping's rerun is agreed over the ranks
+# ---------------------------------------------------------------------------
+def test_single_rank_comm_respec_rerun(engine_lib, oracle_lib):
+    """A read with |tlen| >= 2^16 does not fit the compact grouping element: the
+    speculative run raises ERR_RESPEC. With a communicator the flag travels in the
+    all-reduced buffer and the rerun follows it (one rank here; RCCL refuses two
+    ranks on one device)."""
+    from mgatk2_amd.engine import Engine, EngineConfig
+    from mgatk2_amd.synth import concat_soa, pack_reads
+
+    base = _synth(4, 100_000, 9)
+    odd = pack_reads([dict(reference_start=16000, cigartuples=[(0, 50)], query_sequence="ACGTA" * 10,
+                           query_qualities=[37] * 50, bc=3, flag=0x1, mapping_quality=60, template_length=70_000)])
+    soa = concat_soa([base, odd])
+    cfg = EngineConfig(n_cells=9, **CONFIGS["run"])
+    exp, _ = oracle_lib.oracle_run(cfg, soa)
+    with Engine(cfg) as eng:
+        eng.comm_init(Engine.comm_unique_id(), 1, 0)
+        eng.push(soa)
+        got = eng.finish()
+    assert_same(got, exp, "comm respec")
