@@ -90,6 +90,7 @@ def host_library() -> C.CDLL:
         lib.mgp_bam_count_tag.restype = C.c_int64
         lib.mgp_txt_write_cells.argtypes = [C.c_char_p, vp, vp, C.c_int64, vp, C.c_int64, C.POINTER(C.c_char_p),
                                             C.c_int, C.c_int, C.c_int]
+        lib.mgp_txt_write_cells16.argtypes = lib.mgp_txt_write_cells.argtypes
         lib.mgp_deflate_tiles.argtypes = [vp, C.c_int64, C.c_int64, C.c_int32, C.c_int64, C.c_int64, C.c_int, C.c_int,
                                           C.POINTER(C.POINTER(C.c_uint8)), vp]
         lib.mgp_deflate_tiles.restype = C.c_int64

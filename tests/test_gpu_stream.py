@@ -321,7 +321,7 @@ def test_single_rank_comm_respec_rerun(engine_lib, oracle_lib):
     from mgatk2_amd.synth import concat_soa, pack_reads
 
     base = _synth(4, 100_000, 9)
-    odd = pack_reads([dict(reference_start=16000, cigartuples=[(0, 50)], query_sequence="ACGTA" * 10,
+    odd = pack_reads([dict(reference_start=int(base.start.max()), cigartuples=[(0, 50)], query_sequence="ACGTA" * 10,
                            query_qualities=[37] * 50, bc=3, flag=0x1, mapping_quality=60, template_length=70_000)])
     soa = concat_soa([base, odd])
     cfg = EngineConfig(n_cells=9, **CONFIGS["run"])
