@@ -76,10 +76,11 @@ def parse():
     ap.add_argument("--pcie-steps", type=int, default=3)
     ap.add_argument("--batch-reads", type=str, default="16000000",
                     help="reads per pushed batch in the PCIe leg; a comma list sweeps (first = reported)")
-    ap.add_argument("--record-layout", choices=["paired", "packed", "full"], default="paired",
-                    help="payload records: packed 64-byte records, two consecutive records of a cell per "
-                         "128-byte line (paired, default: the placement of mgp_place_records), packed in BAM "
-                         "order, or full 128-byte records")
+    ap.add_argument("--record-layout", choices=["quad32", "pack32", "paired", "packed", "full"], default="quad32",
+                    help="payload records: 32-byte records made for the run's min_baseq, four consecutive "
+                         "records of a cell per 128-byte line (quad32, default: the placement of "
+                         "mgp_place_records) or in BAM order (pack32); packed 64-byte records two per line "
+                         "(paired) or in BAM order (packed); or full 128-byte records")
     return ap.parse_args()
 
 
@@ -123,8 +124,8 @@ def main():
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if args.gpus != world:
         print(f"[bench] --gpus {args.gpus} but WORLD_SIZE {world}: running {world} ranks", file=sys.stderr)
-    if args.record_layout == "paired" and args.read_len > 50:
-        raise SystemExit("--record-layout paired places 64-byte packed records: needs --read-len <= 50")
+    if args.record_layout in ("paired", "quad32", "pack32") and args.read_len > 50:
+        raise SystemExit(f"--record-layout {args.record_layout} needs --read-len <= 50 (packed records)")
     dist = None
     if world > 1:
         import torch.distributed as tdist
@@ -165,21 +166,24 @@ def main():
                        dedup_mode="alignment_and_fragment_length", max_strand_bias=1.0, min_reads=1)
     eng = Engine(cfg, device=device)
     t0 = time.time()
-    packed = args.record_layout in ("packed", "paired")
-    eng.synth(seed, n_glob, cdf, ref, read_len=args.read_len, rec_align=64 if packed else 128, pack=packed, **shard)
+    lay = args.record_layout
+    packed = lay in ("packed", "paired", "pack32", "quad32")
+    p32 = cfg.min_baseq if lay in ("pack32", "quad32") else None  # 32-byte records for the run's min_baseq
+    eng.synth(seed, n_glob, cdf, ref, read_len=args.read_len, rec_align=64 if packed else 128, pack=packed,
+              pack32=p32, **shard)
     n_res, pay = eng.resident()
-    if args.record_layout == "paired":
+    if lay in ("paired", "quad32"):
         # the producer's placement (mgp_place_records, as the BAM decoder emits it):
         # computed on the host from the generated barcode and flag columns, then the
         # same reads are generated again at those offsets
         from mgatk2_amd.bam import PLACE_PAIRED, place_records
 
         soa = eng.download_inputs(columns=("bc", "flag", "start", "tlen"))
-        roff, pay_b = place_records(soa.bc, soa.flag, np.full(n_res, 64, np.uint32), n_cells, PLACE_PAIRED,
-                                    start=soa.start, tlen=soa.tlen)
+        roff, pay_b = place_records(soa.bc, soa.flag, np.full(n_res, 32 if p32 is not None else 64, np.uint32),
+                                    n_cells, PLACE_PAIRED, start=soa.start, tlen=soa.tlen)
         del soa
         eng.synth(seed, n_glob, cdf, ref, read_len=args.read_len, rec_align=64, pack=True, rec_off=roff,
-                  payload_bytes=pay_b, **shard)
+                  payload_bytes=pay_b, pack32=p32, **shard)
         del roff
     n_res, pay = eng.resident()
     t_gen = time.time() - t0
@@ -386,7 +390,9 @@ def pcie_leg(args, cfg, seed, cdf, ref, shard, device, comm_ranks, barrier, redu
     batch_list = [int(x) for x in str(args.batch_reads).split(",") if x.strip()]
     scfg = EngineConfig(**{**cfg.__dict__})
     eng = Engine(scfg, device=device)
-    eng.synth(seed, args.reads, cdf, ref, read_len=args.read_len, rec_align=64, pack=True, **shard)
+    p32 = cfg.min_baseq if args.record_layout in ("pack32", "quad32") else None
+    rb = 32 if p32 is not None else 64  # dense records in BAM order
+    eng.synth(seed, args.reads, cdf, ref, read_len=args.read_len, rec_align=64, pack=True, pack32=p32, **shard)
     n, pay = eng.resident()
     col_bytes = n * (4 + 4 + 4 + 2 + 1 + 4 + 8)
     hbuf = PinnedBuffer(col_bytes + pay + 4096)
@@ -398,7 +404,7 @@ def pcie_leg(args, cfg, seed, cdf, ref, shard, device, comm_ranks, barrier, redu
         return a
 
     host = eng.download_inputs(alloc=alloc)  # the producer's batches: pinned, BAM order
-    assert np.all(host.rec_off == 64 * np.arange(n, dtype=np.uint64))
+    assert np.all(host.rec_off == rb * np.arange(n, dtype=np.uint64))
     L, nc = cfg.mito_len, cfg.n_cells
     nw, W = eng.windows()
     rbuf = PinnedBuffer(nc * L * 22 + nc * nw + 4096)
@@ -413,9 +419,9 @@ def pcie_leg(args, cfg, seed, cdf, ref, shard, device, comm_ranks, barrier, redu
         out = []
         for a in range(0, n, bs):
             b = min(n, a + bs)
-            host.rec_off[a:b] = 64 * np.arange(b - a, dtype=np.uint64)
+            host.rec_off[a:b] = rb * np.arange(b - a, dtype=np.uint64)
             out.append(ReadSoA(host.start[a:b], host.bc[a:b], host.tlen[a:b], host.flag[a:b], host.mapq[a:b],
-                               host.span[a:b], host.rec_off[a:b], host.payload[64 * a:64 * b]))
+                               host.span[a:b], host.rec_off[a:b], host.payload[rb * a:rb * b]))
         return out
 
     def one(batches, stream):

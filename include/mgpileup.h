@@ -76,6 +76,7 @@ extern "C" {
 #define MGP_FLAG_SUPPLEMENTARY 0x0800u
 #define MGP_FLAG_NOSEQQUAL     0x1000u
 #define MGP_FLAG_PACKED        0x2000u  /* payload record i uses the packed 64-byte layout (below) */
+#define MGP_FLAG_PACK32        0x4000u  /* payload record i uses the 32-byte layout (below) */
 
 /* mgp_config.flags */
 #define MGP_CFG_KEEP_TN5       0x1  /* keep Tn5 counts at positions of depth 0 (the unfiltered
@@ -145,6 +146,7 @@ typedef struct mgp_config {
  */
 #define MGP_PACK_MAX_LEN 50
 #define MGP_PACK_BYTES   64
+#define MGP_PACK32_BYTES 32
 #if defined(__HIPCC__)
 #define MGP_HD __host__ __device__
 #else
@@ -163,6 +165,7 @@ static inline MGP_HD uint32_t mgp_cigar_offset(uint32_t l_seq) {
  * cigar_off + 4 * n_cigar for a full one (before any alignment padding). */
 static inline MGP_HD uint32_t mgp_record_bytes(const uint8_t *rec, uint16_t flag) {
     uint32_t l_seq, n_cigar;
+    if (flag & MGP_FLAG_PACK32) return MGP_PACK32_BYTES;
     if (flag & MGP_FLAG_PACKED) return MGP_PACK_BYTES;
     l_seq = (uint32_t)rec[4] | ((uint32_t)rec[5] << 8) | ((uint32_t)rec[6] << 16) | ((uint32_t)rec[7] << 24);
     n_cigar = (uint32_t)rec[8] | ((uint32_t)rec[9] << 8);
@@ -232,6 +235,84 @@ static inline MGP_HD int mgp_pack_record(int32_t start, uint32_t l_seq, uint16_t
     return 1;
 }
 
+/* 32-byte record (flag[i] has MGP_FLAG_PACK32): what the pileup reads of a short
+ * read under ONE base-quality threshold, four records per 128-byte line (the
+ * pileup's gathers cost one line request each, whatever the record size):
+ *   uint16 start                    0 <= start < 65536
+ *   uint8  l_seq                    1 .. MGP_PACK_MAX_LEN
+ *   uint8  n_cigar | reverse << 7   n_cigar <= 4
+ *   uint16 cigar[4]                 len << 4 | op (len < 4096), unused entries 0
+ *   3-bit base codes                code k (k < l_seq) at bit 96 + 3k of the record:
+ *                                   counted << 2 | b, b = 0..3 for A, C, G, T; counted =
+ *                                   the base is A/C/G/T and int8(qual) >= min_baseq
+ *                                   (pileup.py:80-86); 0 past l_seq
+ *   int8   min_baseq at byte 31     the threshold the counted bits were made for
+ * A read may be packed so iff it has SEQ and QUAL, 1 <= l_seq <= 50, n_cigar <= 4
+ * with every length < 4096 and at most 2 aligned (M, =, X) operations,
+ * 0 <= start < 65536, and -128 <= min_baseq <= 127. The engine refuses a run whose
+ * min_baseq is not the records' (MGP_E_INVALID). Records sit at 32-byte multiples. */
+static inline MGP_HD int mgp_pack32_record(int32_t start, uint32_t l_seq, uint16_t flag, uint32_t n_cigar,
+                                           const uint32_t *cigar, const uint8_t *seq, const uint8_t *qual,
+                                           int32_t min_baseq, uint8_t *out) {
+    uint32_t k, blocks = 0;
+    if ((flag & MGP_FLAG_NOSEQQUAL) || l_seq == 0u || l_seq > MGP_PACK_MAX_LEN || n_cigar > 4u) return 0;
+    if (start < 0 || start >= 65536 || min_baseq < -128 || min_baseq > 127) return 0;
+    for (k = 0; k < n_cigar; ++k) {
+        const uint32_t op = cigar[k] & 15u;
+        if ((cigar[k] >> 4) >= 4096u) return 0;
+        blocks += (op == 0u || op == 7u || op == 8u);
+    }
+    if (blocks > 2u) return 0;
+    for (k = 0; k < 32u; ++k) out[k] = 0;
+    out[0] = (uint8_t)start;
+    out[1] = (uint8_t)((uint32_t)start >> 8);
+    out[2] = (uint8_t)l_seq;
+    out[3] = (uint8_t)(n_cigar | ((flag & MGP_FLAG_REVERSE) ? 0x80u : 0u));
+    for (k = 0; k < n_cigar; ++k) {
+        out[4 + 2 * k] = (uint8_t)cigar[k];
+        out[5 + 2 * k] = (uint8_t)(cigar[k] >> 8);
+    }
+    for (k = 0; k < l_seq; ++k) {
+        const uint32_t code = (k & 1u) ? (seq[k >> 1] & 15u) : (uint32_t)(seq[k >> 1] >> 4);
+        const int b = code == 1u ? 0 : code == 2u ? 1 : code == 4u ? 2 : code == 8u ? 3 : -1;
+        const uint32_t v = b < 0 ? 0u : (uint32_t)b | (((int32_t)(int8_t)qual[k] >= min_baseq) ? 4u : 0u);
+        const uint32_t bit = 96u + 3u * k;
+        out[bit >> 3] |= (uint8_t)(v << (bit & 7u));
+        if ((bit & 7u) > 5u) out[(bit >> 3) + 1] |= (uint8_t)(v >> (8u - (bit & 7u)));
+    }
+    out[31] = (uint8_t)(int8_t)min_baseq;
+    return 1;
+}
+
+/* Expand a 32-byte record into the full layout in full[0..128): a counted base
+ * becomes its code with quality 127, an uncounted one N with quality 0 (the same
+ * pileup under the record's min_baseq). */
+static inline MGP_HD void mgp_unpack32_record(const uint8_t *p, uint8_t *full) {
+    uint32_t k;
+    const uint32_t lseq = p[2] <= MGP_PACK_MAX_LEN ? p[2] : MGP_PACK_MAX_LEN;
+    const uint32_t nc = (p[3] & 0x7Fu) <= 4u ? (p[3] & 0x7Fu) : 4u;
+    const uint32_t coff = mgp_cigar_offset(lseq), soff = mgp_seq_offset(lseq);
+    for (k = 0; k < 128u; ++k) full[k] = 0;
+    full[0] = p[0];
+    full[1] = p[1];
+    full[4] = (uint8_t)lseq;
+    full[8] = (uint8_t)nc;
+    full[10] = (uint8_t)((p[3] & 0x80u) ? MGP_FLAG_REVERSE : 0u);
+    full[12] = (uint8_t)coff;
+    for (k = 0; k < nc; ++k) {
+        full[coff + 4 * k] = p[4 + 2 * k];
+        full[coff + 4 * k + 1] = p[5 + 2 * k];
+    }
+    for (k = 0; k < lseq; ++k) {
+        const uint32_t bit = 96u + 3u * k;
+        const uint32_t w = (uint32_t)p[bit >> 3] | ((uint32_t)p[(bit >> 3) + 1] << 8);
+        const uint32_t v = (w >> (bit & 7u)) & 7u;
+        const uint8_t code = (v & 4u) ? (uint8_t)(1u << (v & 3u)) : (uint8_t)15;
+        full[16 + k] = (v & 4u) ? (uint8_t)127 : (uint8_t)0;
+        full[soff + (k >> 1)] |= (k & 1u) ? code : (uint8_t)(code << 4);
+    }
+}
+
 typedef struct mgp_batch {
     int64_t         n_reads;
     const int32_t  *start;      /* reference_start                                  */
@@ -287,7 +368,8 @@ typedef struct mgp_synth_params {
     const uint32_t *cell_cdf;   /* host array [n_cells]: cumulative thresholds in [0, 2^32) */
     const uint8_t  *ref_codes;  /* host array [mito_len]: reference bases as BAM 4-bit codes */
     int32_t  rec_align;         /* record placement: offsets are multiples of this (16..4096, pow2) */
-    int32_t  pack;              /* 1: reads that fit get the packed 64-byte layout (MGP_FLAG_PACKED) */
+    int32_t  pack;              /* 1: reads that fit get the packed 64-byte layout (MGP_FLAG_PACKED);
+                                   2: the 32-byte layout (MGP_FLAG_PACK32) for pack_min_baseq */
     /* optional placement (host arrays, NULL = dense in BAM order at rec_align):
      * record i is written at rec_off[i] of a payload_bytes payload, e.g. the
      * producer placement of mgp_place_records (include/mgpileup_host.h) */
@@ -303,6 +385,7 @@ typedef struct mgp_synth_params {
      * (processors.py:112-144's per-cell parallelism, one GPU per cell range). */
     int32_t  cell_lo, cell_hi;
     int32_t  shard_rank, shard_world;
+    int32_t  pack_min_baseq;    /* pack == 2: the min_baseq the 32-byte records are made for */
 } mgp_synth_params;
 
 /* The pileup's 16-bit result rows, as the run leaves them in HBM (half the bytes of

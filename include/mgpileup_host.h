@@ -67,6 +67,10 @@ int  mgp_bam_set_bulk(mgp_bam *bam, int32_t cell);
  * Packing drops the code and quality of non-ACGT bases, so callers that rebuild
  * query_sequence/query_qualities (the SimpleRead API) leave it off (default). */
 int  mgp_bam_set_pack(mgp_bam *bam, int pack);
+/* 32-byte records (MGP_FLAG_PACK32, include/mgpileup.h) for reads that fit, made for
+ * the run's min_baseq (in [-128, 127]); the others get the packed 64-byte or the full
+ * layout. Turns packing on. The engine refuses them under another min_baseq. */
+int  mgp_bam_set_pack32(mgp_bam *bam, int on, int min_baseq);
 
 /* Payload placement of mgp_bam_read_ref (MGP_PLACE_DENSE default, or
  * MGP_PLACE_PAIRED: see mgp_place_records below). */
@@ -129,7 +133,8 @@ int64_t mgp_deflate_tiles(const void *data, int64_t rows, int64_t cols, int32_t 
 /* Payload placement for producers: rec_off[i] for records of rec_bytes[i]
  * bytes, in BAM order. MGP_PLACE_DENSE: consecutive, each rounded up to
  * rec_align. MGP_PLACE_PAIRED: two consecutive packed (64-byte) records of one
- * cell share a 128-byte line (one streaming pass, lines opened in BAM order;
+ * cell share a 128-byte line, four consecutive 32-byte (MGP_FLAG_PACK32) records
+ * of one cell likewise (one streaming pass, lines opened in BAM order;
  * reads the engine's filters drop pair among themselves; full records take
  * 128-byte aligned slots of their own), so one line request of the pileup's
  * gather serves two reads of the cell it piles. With the start and tlen columns

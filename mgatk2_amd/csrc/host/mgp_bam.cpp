@@ -131,6 +131,8 @@ struct mgp_bam {
     char tag[2] = {'C', 'B'};
     int32_t bulk_cell = -1;  // >= 0: every record goes to this cell (bulk calling)
     bool pack = false;       // write the packed record layout where a read fits
+    bool pack32 = false;     // ... the 32-byte layout first, made for pack32_minq (mgp_bam_set_pack32)
+    int pack32_minq = 0;
     int placement = MGP_PLACE_DENSE;  // payload placement (mgp_place_records)
 };
 
@@ -674,7 +676,30 @@ int mgp_bam_set_placement(mgp_bam* b, int mode) {
 int mgp_bam_set_pack(mgp_bam* b, int pack) {
     if (!b) return fail("null argument");
     b->pack = pack != 0;
+    if (!b->pack) b->pack32 = false;
     return 0;
+}
+
+int mgp_bam_set_pack32(mgp_bam* b, int on, int min_baseq) {
+    if (!b) return fail("null argument");
+    if (on && (min_baseq < -128 || min_baseq > 127)) return fail("32-byte records need min_baseq in [-128, 127]");
+    b->pack32 = on != 0;
+    b->pack32_minq = min_baseq;
+    if (b->pack32) b->pack = true;
+    return 0;
+}
+
+// Header-level checks of mgp_pack32_record (include/mgpileup.h) on a raw BAM record.
+static bool bam_packable32(int32_t pos, uint32_t l_seq, uint32_t n_cig, const uint8_t* cig) {
+    if (l_seq == 0 || l_seq > MGP_PACK_MAX_LEN || n_cig > 4 || pos < 0 || pos >= 65536) return false;
+    uint32_t blocks = 0;
+    for (uint32_t k = 0; k < n_cig; ++k) {
+        const uint32_t c = rd32(cig + 4 * k);
+        if ((c >> 4) >= 4096u) return false;
+        const uint32_t op = c & 15u;
+        blocks += op == 0 || op == 7 || op == 8;
+    }
+    return blocks <= 2;
 }
 
 // Header-level and quality checks of mgp_pack_record (include/mgpileup.h) on a
@@ -723,7 +748,7 @@ int mgp_bam_read_ref(mgp_bam* b, int tid, int rec_align, mgp_bam_batch* out) {
     std::vector<uint64_t> rsz;  // payload bytes of each record of the batch (then its offset)
     std::vector<uint32_t> ncg;  // CIGAR operations (CG tag resolved)
     std::vector<const uint8_t*> cgp;
-    std::vector<uint8_t> pkd;   // record is written in the packed layout
+    std::vector<uint8_t> pkd;   // record layout: 0 full, 1 packed 64-byte, 2 32-byte
     // producer placement (mgp_place_records' rule, applied batch by batch as records
     // stream in): open[key] = the line of cell `key` whose second half is free;
     // key n_cells collects the reads the engine's filters drop
@@ -734,12 +759,14 @@ int mgp_bam_read_ref(mgp_bam* b, int tid, int rec_align, mgp_bam_batch* out) {
         if (b->bulk_cell >= 0) n_keys = std::max(n_keys, b->bulk_cell + 1);
     }
     std::vector<uint64_t> open(paired ? (size_t)n_keys + 1 : 0, ~0ull);
+    std::vector<uint64_t> open32(paired ? (size_t)n_keys + 1 : 0, ~0ull);  // 32-byte records: 4 per line
+    std::vector<uint8_t> fill32(paired ? (size_t)n_keys + 1 : 0, 0);
     mgp_host::DupTracker dups(paired ? (size_t)n_keys : 0);  // a cell's repeated keys go with the dropped reads
     uint64_t cursor = 0;  // paired: payload bytes placed so far (128-byte lines)
     // one record: decode (do_fields: the SoA columns, barcode lookup included) and
     // pack (do_rec: the payload record at offset off) at index k
     auto decode = [&](const uint8_t* r, uint32_t bs, size_t k, uint64_t off, uint32_t n_cig, const uint8_t* cig,
-                      bool pk, int64_t& tags, int64_t& first, int64_t gidx, bool do_fields, bool do_rec) {
+                      int pk, int64_t& tags, int64_t& first, int64_t gidx, bool do_fields, bool do_rec) {
         const uint8_t* end = r + bs;
         const int32_t pos = rdi32(r + 4);
         const uint8_t l_name = r[8];
@@ -752,7 +779,8 @@ int mgp_bam_read_ref(mgp_bam* b, int tid, int rec_align, mgp_bam_batch* out) {
         const uint8_t* auxp = qualp + l_seq;
         uint16_t fl = flg & 0x0FFF;
         if (l_seq == 0 || qualp[0] == 0xFF) fl |= MGP_FLAG_NOSEQQUAL;
-        if (pk) fl |= MGP_FLAG_PACKED;
+        if (pk == 1) fl |= MGP_FLAG_PACKED;
+        if (pk == 2) fl |= MGP_FLAG_PACK32;
         if (do_fields) {
             Aux aux{auxp, end};
             int32_t bcv = -1;
@@ -778,7 +806,13 @@ int mgp_bam_read_ref(mgp_bam* b, int tid, int rec_align, mgp_bam_batch* out) {
         }
         if (!do_rec) return;
         uint8_t* rec = G_pay.p + off;
-        if (pk) {
+        if (pk == 2) {
+            uint32_t cw[4] = {0, 0, 0, 0};
+            for (uint32_t q = 0; q < n_cig; ++q) cw[q] = rd32(cig + 4 * q);
+            const uint64_t size = ((uint64_t)MGP_PACK32_BYTES + amask) & ~amask;
+            if (size > MGP_PACK32_BYTES && !paired) std::memset(rec + MGP_PACK32_BYTES, 0, size - MGP_PACK32_BYTES);
+            mgp_pack32_record(pos, l_seq, fl, n_cig, cw, seqp, qualp, b->pack32_minq, rec);  // writes all 32 bytes
+        } else if (pk) {
             uint32_t cw[4] = {0, 0, 0, 0};
             for (uint32_t q = 0; q < n_cig; ++q) cw[q] = rd32(cig + 4 * q);
             const uint64_t size = ((uint64_t)MGP_PACK_BYTES + amask) & ~amask;
@@ -835,8 +869,12 @@ int mgp_bam_read_ref(mgp_bam* b, int tid, int rec_align, mgp_bam_batch* out) {
             ncg[i] = n_cig;
             cgp[i] = cig;
             const uint8_t* qualp = cigp + 4 * (size_t)rd16(r + 12) + ((size_t)l_seq + 1) / 2;
-            pkd[i] = b->pack && bam_packable(rdi32(r + 4), rd16(r + 14), l_seq, n_cig, cig, qualp);
-            const uint64_t rb = pkd[i] ? (uint64_t)MGP_PACK_BYTES : (uint64_t)mgp_cigar_offset(l_seq) + 4ull * n_cig;
+            const bool seqqual = l_seq != 0 && qualp[0] != 0xFF;  // else NOSEQQUAL: never packed
+            pkd[i] = (b->pack32 && seqqual && bam_packable32(rdi32(r + 4), l_seq, n_cig, cig)) ? 2
+                     : (b->pack && bam_packable(rdi32(r + 4), rd16(r + 14), l_seq, n_cig, cig, qualp)) ? 1 : 0;
+            const uint64_t rb = pkd[i] == 2 ? (uint64_t)MGP_PACK32_BYTES
+                                : pkd[i] ? (uint64_t)MGP_PACK_BYTES
+                                         : (uint64_t)mgp_cigar_offset(l_seq) + 4ull * n_cig;
             if (paired) {  // record bytes; the offsets follow the barcodes (pass 1b)
                 rsz[i] = rb;
                 continue;
@@ -862,7 +900,7 @@ int mgp_bam_read_ref(mgp_bam* b, int tid, int rec_align, mgp_bam_batch* out) {
                 const size_t lo = m * (size_t)t / (size_t)tn, hi = m * (size_t)(t + 1) / (size_t)tn;
                 for (size_t i = lo; i < hi; ++i)
                     decode(recs[i], sizes[i], k0 + i, paired ? G_roff.p[k0 + i] : rsz[i], ncg[i], cgp[i],
-                           pkd[i] != 0, tags[(size_t)t], firsts[(size_t)t], (int64_t)(k0 + i), do_fields, do_rec);
+                           (int)pkd[i], tags[(size_t)t], firsts[(size_t)t], (int64_t)(k0 + i), do_fields, do_rec);
             };
             std::vector<std::thread> th;
             for (int t = 1; t < tn; ++t) th.emplace_back(work, t);
@@ -889,6 +927,17 @@ int mgp_bam_read_ref(mgp_bam* b, int tid, int rec_align, mgp_bam_batch* out) {
                 if (key < (size_t)n_keys &&
                     dups.repeat(key, G_start.p[k], (G_flag.p[k] & MGP_FLAG_REVERSE) != 0, G_tlen.p[k]))
                     key = (size_t)n_keys;
+                if (pkd[i] == 2) {  // four 32-byte records of one key per line
+                    if (open32[key] == ~0ull) {
+                        cursor = (cursor + 127) & ~127ull;
+                        open32[key] = cursor;
+                        fill32[key] = 0;
+                        cursor += 128;
+                    }
+                    G_roff.p[k] = open32[key] + (uint64_t)MGP_PACK32_BYTES * fill32[key];
+                    if (++fill32[key] == 4) open32[key] = ~0ull;
+                    continue;
+                }
                 if (open[key] != ~0ull) {
                     G_roff.p[k] = open[key] + MGP_PACK_BYTES;
                     open[key] = ~0ull;
@@ -903,6 +952,10 @@ int mgp_bam_read_ref(mgp_bam* b, int tid, int rec_align, mgp_bam_batch* out) {
             // later batch may still fill them; lines closed here are fully written)
             for (uint64_t o : open)
                 if (o != ~0ull && o >= cur0) std::memset(G_pay.p + o + MGP_PACK_BYTES, 0, MGP_PACK_BYTES);
+            for (size_t key = 0; key < open32.size(); ++key)
+                if (open32[key] != ~0ull && open32[key] >= cur0)
+                    std::memset(G_pay.p + open32[key] + (uint64_t)MGP_PACK32_BYTES * fill32[key], 0,
+                                (uint64_t)MGP_PACK32_BYTES * (4u - fill32[key]));
             run_pass(false, true);
             tot = cursor - G_pay.n;
         }

@@ -160,6 +160,7 @@ struct mgp_ctx {
     bool stream_off = false;   // the resident reads cannot stream (payload too large for compact elements)
     bool seg_open = false;     // segments of the current run are queued (mgp_run finishes it)
     int w_done = 0;            // windows [0, w_done) of the current run are queued
+    int stream_layout = 1;     // kLayP64 / kLayP32: the packed layout the run's segments assume
     int64_t segments = 0;      // segments queued by pushes (all runs)
     bool last_streamed = false;
 };
@@ -241,11 +242,19 @@ constexpr uint32_t kCompactTlen = 1u << 16;       // |tlen| below this fits the 
 // the fallback path, whose standalone check (k_check_inputs) takes every bit first.
 // CHK_PAIRED / CHK_UNPAIRED / CHK_NOSEQ: some read is paired / unpaired / lacks SEQ
 // or QUAL (pass B tracks pairedness and SEQ per read only when the reads mix or lack
-// them). CHK_FULL: some record is in the full layout. CHK_WIDEKEY: some start lies
+// them). CHK_FULL / CHK_P64 / CHK_P32: some record is in the full / packed 64-byte /
+// 32-byte layout (include/mgpileup.h; a flag word with both packed bits is a 32-byte
+// record). CHK_WIDEKEY: some start lies
 // outside [0, mito_len) or some |tlen| >= kCompactTlen (no compact grouping element).
 // CHK_UNSORTED: a start below its predecessor's (pysam's fetch order, readers.py:87-92).
 constexpr uint32_t CHK_PAIRED = 4u, CHK_UNPAIRED = 8u, CHK_NOSEQ = 16u, CHK_FULL = 32u, CHK_WIDEKEY = 64u,
-                   CHK_UNSORTED = 128u;
+                   CHK_UNSORTED = 128u, CHK_P64 = 256u, CHK_P32 = 512u;
+__device__ __forceinline__ uint32_t layout_bit(uint32_t f) {
+    return (f & MGP_FLAG_PACK32) ? CHK_P32 : (f & MGP_FLAG_PACKED) ? CHK_P64 : CHK_FULL;
+}
+// Record layouts (include/mgpileup.h) and the pileup's instantiations: every record of
+// one packed layout (the fast paths), or any mix (kLayAny: the layout per read)
+enum { kLayFull = 0, kLayP64 = 1, kLayP32 = 2, kLayAny = 3 };
 
 // One workgroup (8 waves) per (start bin, cell slice): bin bounds by binary
 // search in the starts, flag/barcode filters (readers.py:95-111) and the LDS
@@ -316,7 +325,7 @@ __global__ void __launch_bounds__(kHistBlock) k_bin_count(const int32_t* __restr
                 const uint32_t f = ff[u];
                 if (i0 + u * kHistBlock < hi)
                     bits |= (f & MGP_FLAG_PAIRED ? CHK_PAIRED : CHK_UNPAIRED) |
-                            (f & MGP_FLAG_NOSEQQUAL ? CHK_NOSEQ : 0u) | (f & MGP_FLAG_PACKED ? 0u : CHK_FULL);
+                            (f & MGP_FLAG_NOSEQQUAL ? CHK_NOSEQ : 0u) | layout_bit(f);
             }
 #pragma unroll
             for (int u = 0; u < kU; ++u) {
@@ -454,7 +463,7 @@ struct __align__(16) GElem {
     uint32_t tlen;
 };
 constexpr unsigned long long GM_REV = 1ull << 56, GM_PAIRED = 2ull << 56, GM_MAPQ_OK = 4ull << 56,
-                             GM_BAD = 8ull << 56, GM_PACKED = 16ull << 56;
+                             GM_BAD = 8ull << 56, GM_PACKED = 16ull << 56, GM_P32 = 32ull << 56;
 
 // Grouping in two passes (a single pass that writes each 16-byte element straight
 // to its cell-major slot is bound by ~200M scattered partial-line stores):
@@ -477,6 +486,9 @@ enum { kOffDense = 0, kOffR32 = 1, kOffR64 = 2, kOffSpec = 3 };
 
 // Pileup element values (see k_group_b)
 constexpr uint32_t PE_DUP = 0xFFFFFFFFu, PE_KEEP = 0xFFFFFFFEu, PE_PACKED = 0x80000000u, PE_OFF = 0x7FFFFFFFu;
+// the wide (any-layout) path's pileup elements: PE_PACKED | PE_P32 for a 32-byte record,
+// PE_PACKED alone for a packed 64-byte one, and a 30-bit offset (below PE_KEEP's)
+constexpr uint32_t PE_P32 = 0x40000000u, PE_OFF30 = 0x3FFFFFFFu;
 
 // Compact grouping element (8 bytes), used when every resident record is packed
 // at a 64-byte multiple below 2^37 (dense or u32 offsets), the reads do not mix
@@ -524,7 +536,7 @@ __global__ void __launch_bounds__(kGABlock, MGP_GA_WAVES) k_group_a(int64_t n, c
                                                     Geom g, int ngroups, int gbits, int min_mapq,
                                                     uint32_t* __restrict__ bucket_off, GElem* __restrict__ gel2,
                                                     uint32_t* __restrict__ first_read, uint32_t* __restrict__ ck,
-                                                    DevStats* st, int seg_w0, int seg_bhi) {
+                                                    DevStats* st, int seg_w0, int seg_bhi, int spec_unit) {
     static_assert(kOff != kOffSpec || kCompact, "the speculative check writes compact elements");
     constexpr bool kSpec = kOff == kOffSpec;
     if (__atomic_load_n(&st->err, __ATOMIC_RELAXED) & ERR_BOUNDS) return;  // unsorted input (k_bin_count)
@@ -674,7 +686,9 @@ __global__ void __launch_bounds__(kGABlock, MGP_GA_WAVES) k_group_a(int64_t n, c
                 const int first = u ? __builtin_amdgcn_readlane(P.s[u > 0 ? u - 1 : 0], kWave - 1) : prev0;
                 const int pv = lane ? below : first;
                 ck_uns |= i < hi && i > 0 && P.s[u] < pv;
-                fit[u] = (P.o[u] & 63ull) == 0ull && P.s[u] >= 0 && P.s[u] < g.L && at < kCompactTlen;
+                // the record's offset in units of its layout's size (64 or 32 bytes)
+                fit[u] = (P.o[u] & ((1ull << spec_unit) - 1ull)) == 0ull && P.s[u] >= 0 && P.s[u] < g.L &&
+                         at < kCompactTlen;
                 if (valid[u]) {
                     ck_span = max(ck_span, spn[u]);
                     ck_bad |= !fit[u];
@@ -712,7 +726,7 @@ __global__ void __launch_bounds__(kGABlock, MGP_GA_WAVES) k_group_a(int64_t n, c
             } else if constexpr (kCompact) {
                 // the record's 64-byte unit (dense: the read index; u32 column: rec_off >> 6);
                 // a read that does not fit (kSpec) piles nothing: the run is redone
-                const uint32_t unit64 = kSpec ? (uint32_t)(P.o[u] >> 6) : (uint32_t)P.o[u];
+                const uint32_t unit64 = kSpec ? (uint32_t)(P.o[u] >> spec_unit) : (uint32_t)P.o[u];
                 const uint32_t lo = fit[u] ? unit64 | (mq ? PE_PACKED : 0u) : 0u;
                 const uint32_t hi = at | ((uint32_t)(P.s[u] & 255) << GC_START_SHIFT) |
                                     (f & MGP_FLAG_REVERSE ? GC_REV : 0u) |
@@ -723,7 +737,8 @@ __global__ void __launch_bounds__(kGABlock, MGP_GA_WAVES) k_group_a(int64_t n, c
                 GElem e;
                 e.w = off | (f & MGP_FLAG_REVERSE ? GM_REV : 0ull) | (f & MGP_FLAG_PAIRED ? GM_PAIRED : 0ull) |
                       (mq ? GM_MAPQ_OK : 0ull) | (f & MGP_FLAG_NOSEQQUAL ? GM_BAD : 0ull) |
-                      (f & MGP_FLAG_PACKED ? GM_PACKED : 0ull) |
+                      (f & (MGP_FLAG_PACKED | MGP_FLAG_PACK32) ? GM_PACKED : 0ull) |
+                      (f & MGP_FLAG_PACK32 ? GM_P32 : 0ull) |
                       ((unsigned long long)(P.c[u] & (kGroup - 1)) << GM_LCELL_SHIFT);
                 e.start = P.s[u];
                 e.tlen = at;
@@ -825,7 +840,7 @@ struct GWide {
     static __device__ __forceinline__ bool tlen_eq(const T& a, const T& b) { return a.tlen == b.tlen; }
     static __device__ __forceinline__ bool mapq_ok(const T& e) { return (e.w & GM_MAPQ_OK) != 0ull; }
     static __device__ __forceinline__ uint32_t pile(const T& e, int unit) {
-        return (uint32_t)((e.w & GM_OFF) >> unit) | (e.w & GM_PACKED ? PE_PACKED : 0u);
+        return (uint32_t)((e.w & GM_OFF) >> unit) | (e.w & GM_PACKED ? PE_PACKED : 0u) | (e.w & GM_P32 ? PE_P32 : 0u);
     }
     // a predecessor's duplicate key, read from the LDS stage, against element x:
     // same run (cell and start), then also strand, then also |tlen|
@@ -1349,7 +1364,7 @@ struct RecLine {
     uint4 h, qv[4], sv[2], cv;
 };
 
-__device__ __forceinline__ void load_line(bool has, bool packed, const uint8_t* __restrict__ rec, const Win& w,
+__device__ __forceinline__ void load_line(bool has, int lay, const uint8_t* __restrict__ rec, const Win& w,
                                           RecLine& R) {
     R.h = make_uint4(0, 0, 0, 0);
     R.cv = make_uint4(0, 0, 0, 0);
@@ -1367,12 +1382,15 @@ __device__ __forceinline__ void load_line(bool has, bool packed, const uint8_t* 
         for (int k = 0; k < 2; ++k) R.sv[k] = make_uint4(0x12481248u, 0x24812481u, 0x48124812u, 0x81248124u);
         R.cv.x = 50u << 4;
     } else if (has) {
+        // a 32-byte record is 2 loads, a packed 64-byte one 4, a full line 8
         const uint4* r4 = reinterpret_cast<const uint4*>(rec);
         R.h = r4[0];
         R.qv[0] = r4[1];
-        R.qv[1] = r4[2];
-        R.qv[2] = r4[3];
-        if (!packed) {
+        if (lay != kLayP32) {
+            R.qv[1] = r4[2];
+            R.qv[2] = r4[3];
+        }
+        if (lay == kLayFull) {
             R.qv[3] = r4[4];
             R.sv[0] = r4[5];
             R.sv[1] = r4[6];
@@ -1381,27 +1399,18 @@ __device__ __forceinline__ void load_line(bool has, bool packed, const uint8_t* 
     }
 }
 
-__device__ __forceinline__ void pile_line(bool has, bool packed, const uint8_t* __restrict__ rec, const RecLine& R,
+__device__ __forceinline__ void pile_line(bool has, int lay, const uint8_t* __restrict__ rec, const RecLine& R,
                                           const Win& w, const PileCfg& pc, uint32_t* tile, uint32_t* t5,
                                           uint32_t max_span, bool& span_err, bool& pk_err);
 
-__device__ __forceinline__ void pile_read(bool has, bool packed, const uint8_t* __restrict__ rec, const Win& w,
+__device__ __forceinline__ void pile_read(bool has, int lay, const uint8_t* __restrict__ rec, const Win& w,
                                           const PileCfg& pc, uint32_t* tile, uint32_t* t5, uint32_t max_span,
                                           bool& span_err, bool& pk_err) {
     if (MGP_ABL == 1) return;
-    if (MGP_ABL == 3) packed = false;  // the synthetic reads are in the full layout
-    if (MGP_ABL == 9) {
-        // experiment: lane pairs read the two halves of ONE 128-B line (the even
-        // lane's record line), emulating a placement where consecutive piled reads
-        // of a cell share a line; counts meaningless
-        const unsigned long long a = (unsigned long long)reinterpret_cast<uintptr_t>(rec);
-        const unsigned long long p = __shfl(a, (int)(threadIdx.x & 62), kWave);
-        rec = reinterpret_cast<const uint8_t*>((p & ~127ull) + 64ull * (threadIdx.x & 1));
-        packed = true;
-    }
+    if (MGP_ABL == 3) lay = kLayFull;  // the synthetic reads are in the full layout
     RecLine R;
-    load_line(has, packed, rec, w, R);
-    pile_line(has, packed, rec, R, w, pc, tile, t5, max_span, span_err, pk_err);
+    load_line(has, lay, rec, w, R);
+    pile_line(has, lay, rec, R, w, pc, tile, t5, max_span, span_err, pk_err);
 }
 
 __device__ __forceinline__ uint32_t byte_at(const uint32_t* wd, int j) { return (wd[j >> 2] >> (8 * (j & 3))) & 0xFFu; }
@@ -1658,19 +1667,96 @@ __device__ __forceinline__ void pile_bases_packed(bool act, int a0, int b0, int 
     else run([&](int qq) { count(qq, r0); });
 }
 
-__device__ __forceinline__ void pile_line(bool has, bool packed, const uint8_t* __restrict__ rec, const RecLine& R,
+// The counted bases of the 32-byte register-path reads of a wave. Code k of a
+// record (bit 96 + 3k: counted << 2 | b) is taken with a static shift (a funnel
+// shift where it straddles two words); a base counts iff its counted bit is set
+// and k lies in the lane's ranges [a_k, b_k) (not tested when every lane of the
+// wave has the same single range, which the loop bounds then are). The count's
+// address is the block's row | plane * 4, or the lane's own scratch word.
+__device__ __forceinline__ void pile_bases_p32(bool act, int a0, int b0, int a1, int b1, int qs1, int dl0, int dl1,
+                                               const RecLine& R, const Win& w, uint32_t* tile, uint32_t inc) {
+    constexpr int kLen = MGP_PACK_MAX_LEN;
+    auto range_mask = [](int lo, int hi) -> unsigned long long {
+        lo = min(max(lo, 0), 64);
+        hi = min(max(hi, 0), 64);
+        const unsigned long long h = hi >= 64 ? ~0ull : ((1ull << hi) - 1ull);
+        const unsigned long long l = lo >= 64 ? ~0ull : ((1ull << lo) - 1ull);
+        return lo < hi ? (h & ~l) : 0ull;
+    };
+    const unsigned long long vm = act ? (range_mask(a0, b0) | range_mask(a1, b1)) : 0ull;
+    int qlo = 1 << 30, qhi = 0;
+    if (vm) {
+        qlo = __builtin_ctzll(vm);
+        qhi = 64 - __builtin_clzll(vm);
+    }
+    const int wq_lo = __builtin_amdgcn_readfirstlane(wave_min(qlo));
+    const int wq_hi = __builtin_amdgcn_readfirstlane(wave_max(qhi));
+    if (wq_lo >= wq_hi) return;
+    const uint32_t cw[6] = {R.h.w, R.qv[0].x, R.qv[0].y, R.qv[0].z, R.qv[0].w, 0u};
+    const uint32_t vlo = (uint32_t)vm, vhi = (uint32_t)(vm >> 32);
+    const uint32_t own = lds_addr(g_own) + 4u * (threadIdx.x & 63);
+    const uint32_t tb = lds_addr(tile);
+    const uint32_t r0 = tb + 16u * (uint32_t)(dl0 - w.w0), r1 = tb + 16u * (uint32_t)(dl1 - w.w0);
+    const bool two = __ballot(act && a1 < b1) != 0ull;
+    // every lane the same single range: the loop bounds are the range (no per-base test)
+    const int ua0 = __builtin_amdgcn_readfirstlane(a0), ub0 = __builtin_amdgcn_readfirstlane(b0);
+    const bool uniform = !two && __ballot(!(act && a0 == ua0 && b0 == ub0)) == 0ull;
+    auto code = [&](int qq) -> uint32_t {
+        const int bit = 3 * qq, j = bit >> 5, sh = bit & 31;
+        return (sh <= 29 ? (cw[j] >> sh) : __builtin_amdgcn_alignbit(cw[j + 1], cw[j], sh)) & 7u;
+    };
+    auto count = [&](int qq, uint32_t row, bool test) {
+        const uint32_t x = code(qq);
+        uint32_t ok = x >> 2;
+        if (test) ok &= ((qq < 32 ? vlo : vhi) >> (qq & 31)) & 1u;
+        lds_add((ok ? (row | ((x & 3u) << 2)) : own) + 16u * (uint32_t)qq, inc);
+    };
+    const unsigned long long smask = range_mask(wq_lo, wq_hi);
+    constexpr int kC0 = 5, kC1 = kLen - 5;
+    auto run = [&](auto&& body) {
+        if (wq_lo <= kC0 && wq_hi >= kC1) {
+            if (wq_lo < kC0) {
+#pragma unroll
+                for (int qq = 0; qq < kC0; ++qq)
+                    if ((smask >> qq) & 1ull) body(qq);
+            }
+#pragma unroll
+            for (int qq = kC0; qq < kC1; ++qq) body(qq);
+            if (wq_hi > kC1) {
+#pragma unroll
+                for (int qq = kC1; qq < kLen; ++qq)
+                    if ((smask >> qq) & 1ull) body(qq);
+            }
+        } else {
+#pragma unroll
+            for (int qq = 0; qq < kLen; ++qq)
+                if ((smask >> qq) & 1ull) body(qq);
+        }
+    };
+    if (uniform) run([&](int qq) { count(qq, r0, false); });
+    else if (two) run([&](int qq) { count(qq, qq >= qs1 ? r1 : r0, true); });
+    else run([&](int qq) { count(qq, r0, true); });
+}
+
+__device__ __forceinline__ void pile_line(bool has, int lay, const uint8_t* __restrict__ rec, const RecLine& R,
                                           const Win& w, const PileCfg& pc, uint32_t* tile, uint32_t* t5,
                                           uint32_t max_span, bool& span_err, bool& pk_err) {
     if (MGP_ABL == 1) return;
     const uint4 h = R.h, cv = R.cv;
-    const int32_t start = (int32_t)h.x;
-    // header fields of either layout (include/mgpileup.h)
-    const uint32_t lseq = packed ? (h.y & 0xFFu) : h.y;
-    const uint32_t ncig = packed ? ((h.y >> 8) & 0x7Fu) : (h.z & 0xFFFFu);
+    const bool packed = lay != kLayFull, p32 = lay == kLayP32;
+    // header fields of the three layouts (include/mgpileup.h)
+    const int32_t start = p32 ? (int32_t)(h.x & 0xFFFFu) : (int32_t)h.x;
+    const uint32_t lseq = p32 ? ((h.x >> 16) & 0xFFu) : packed ? (h.y & 0xFFu) : h.y;
+    const uint32_t ncig = p32 ? ((h.x >> 24) & 0x7Fu) : packed ? ((h.y >> 8) & 0x7Fu) : (h.z & 0xFFFFu);
     const uint32_t coff = h.w;
-    const int strand = packed ? (int)((h.y >> 15) & 1u) : (((h.z >> 16) & MGP_FLAG_REVERSE) ? 1 : 0);
-    const uint32_t cigw[4] = {packed ? (h.y >> 16) : cv.x, packed ? (h.z & 0xFFFFu) : cv.y,
-                              packed ? (h.z >> 16) : cv.z, packed ? (h.w & 0xFFFFu) : cv.w};
+    const int strand = p32 ? (int)(h.x >> 31) : packed ? (int)((h.y >> 15) & 1u)
+                                                     : (((h.z >> 16) & MGP_FLAG_REVERSE) ? 1 : 0);
+    const uint32_t cigw[4] = {p32 ? (h.y & 0xFFFFu) : packed ? (h.y >> 16) : cv.x,
+                              p32 ? (h.y >> 16) : packed ? (h.z & 0xFFFFu) : cv.y,
+                              p32 ? (h.z & 0xFFFFu) : packed ? (h.z >> 16) : cv.z,
+                              p32 ? (h.z >> 16) : packed ? (h.w & 0xFFFFu) : cv.w};
+    // a 32-byte record's counted bits were made for one min_baseq (byte 31)
+    if (has && p32 && (int)(int8_t)(R.qv[0].w >> 24) != pc.min_baseq) pk_err = true;
     tn5_cut(has, start, lseq, strand, w, t5);
 
     bool fast = has && lseq <= (uint32_t)(packed ? MGP_PACK_MAX_LEN : kFastLen) && ncig <= (uint32_t)kFastCig &&
@@ -1733,8 +1819,9 @@ __device__ __forceinline__ void pile_line(bool has, bool packed, const uint8_t* 
     // producers pack every read that fits)
     if (__ballot(fast && !packed) != 0ull)
         pile_bases<false>(fast && !packed, a0, b0, a1, b1, qs1, dl0, dl1, R, w, pc, tile, inc);
-    if (__ballot(fast && packed) != 0ull)
-        pile_bases_packed(fast && packed, a0, b0, a1, b1, qs1, dl0, dl1, R, w, pc, tile, inc);
+    if (__ballot(fast && packed && !p32) != 0ull)
+        pile_bases_packed(fast && packed && !p32, a0, b0, a1, b1, qs1, dl0, dl1, R, w, pc, tile, inc);
+    if (__ballot(fast && p32) != 0ull) pile_bases_p32(fast && p32, a0, b0, a1, b1, qs1, dl0, dl1, R, w, tile, inc);
     const bool slow = has && !fast;
     pk_err = pk_err || (slow && packed);  // a packed record outside the layout's limits
     bool se = false;
@@ -1754,11 +1841,18 @@ static_assert(kWaveQ >= kWave * (kStreamU + 1) && kStreamU <= 7, "pileup ring to
 // record byte offset of a pileup element (MGP_ABL 6, experiments only: every
 // record read from the first 256 MiB of the payload, to time the pileup with a
 // small gather footprint; the counts are then meaningless)
-__device__ __forceinline__ unsigned long long rec_at(uint32_t qe, int unit) {
-    const unsigned long long off = (unsigned long long)(qe & PE_OFF) << unit;
+__device__ __forceinline__ unsigned long long rec_at(uint32_t qe, int unit, uint32_t pe_off) {
+    const unsigned long long off = (unsigned long long)(qe & pe_off) << unit;
     return MGP_ABL == 6 ? off & ((256ull << 20) - 128) : off;
 }
 constexpr uint32_t kSeg = 65535;     // elements per tile segment (16-bit halves cannot carry)
+
+// the record layout of a pileup element (kLayAny: from its PE_PACKED / PE_P32 bits)
+template <int kLayout>
+__device__ __forceinline__ int elem_layout(uint32_t qe) {
+    if (kLayout != kLayAny) return kLayout;
+    return (qe & PE_PACKED) ? ((qe & PE_P32) ? kLayP32 : kLayP64) : kLayFull;
+}
 
 // grid (nchunks, nwin): workgroup = (cell chunk, position window). For each cell
 // of the chunk, the cell's pileup elements with start bin in [window start -
@@ -1796,9 +1890,14 @@ __device__ __forceinline__ uint32_t sat16(uint32_t v) { return v > 0xFFFFu ? 0xF
 #ifndef MGP_PILE_PREFETCH
 #define MGP_PILE_PREFETCH 1
 #endif
-template <bool kPacked>
+// kLayout: kLayP64 / kLayP32 when every resident record has that packed layout (the
+// next batch's records loaded ahead), kLayAny otherwise (the layout from the element's
+// PE_PACKED / PE_P32 bits). pe_off: the element's offset bits (30 for the wide
+// grouping elements, which carry the layout; 31 for the compact ones).
+template <int kLayout>
 __global__ void __launch_bounds__(kBlock, MGP_PILEUP_WAVES) k_pileup(
     Geom g, PileCfg pc, const uint8_t* __restrict__ payload, const uint32_t* __restrict__ pel, int unit,
+    uint32_t pe_off,
     const uint32_t* __restrict__ O, Out16 o16, uint32_t* __restrict__ counts, uint32_t* __restrict__ tn5,
     uint32_t* __restrict__ depth, uint32_t* __restrict__ n_reads, uint8_t* __restrict__ any_paired, int pair_mode,
     uint32_t* __restrict__ covered, unsigned long long* __restrict__ dsum,
@@ -1862,6 +1961,7 @@ __global__ void __launch_bounds__(kBlock, MGP_PILEUP_WAVES) k_pileup(
             const uint32_t seg_hi = min(hi, seg + kSeg);
             // the wave's ring of queued reads: [qh, qh + qn), wave-uniform
             uint32_t qh = 0, qn = 0;
+            constexpr bool kPacked = kLayout == kLayP64 || kLayout == kLayP32;
             RecLine Rp;         // kPacked: the loaded batch waiting to be piled
             bool pend = false;  // (wave-uniform)
             // a stream step: each wave takes kStreamU x 64 consecutive elements (the
@@ -1898,12 +1998,12 @@ __global__ void __launch_bounds__(kBlock, MGP_PILEUP_WAVES) k_pileup(
                     qn -= kWave;
                     if constexpr (kPacked && MGP_PILE_PREFETCH) {
                         RecLine Rn;  // this batch's records load while the pending batch is piled
-                        load_line(true, true, payload + rec_at(qe, unit), w, Rn);
-                        if (pend) pile_line(true, true, nullptr, Rp, w, pc, tile, t5, max_span, span_err, pk_err);
+                        load_line(true, kLayout, payload + rec_at(qe, unit, pe_off), w, Rn);
+                        if (pend) pile_line(true, kLayout, nullptr, Rp, w, pc, tile, t5, max_span, span_err, pk_err);
                         Rp = Rn;
                         pend = true;
                     } else {
-                        pile_read(true, kPacked || (qe & PE_PACKED) != 0u, payload + rec_at(qe, unit), w, pc, tile,
+                        pile_read(true, elem_layout<kLayout>(qe), payload + rec_at(qe, unit, pe_off), w, pc, tile,
                                   t5, max_span, span_err, pk_err);
                     }
                 }
@@ -1913,12 +2013,12 @@ __global__ void __launch_bounds__(kBlock, MGP_PILEUP_WAVES) k_pileup(
                 const uint32_t qe = has ? wq[(qh + lane) & (kWaveQ - 1)] : 0u;
                 if constexpr (kPacked && MGP_PILE_PREFETCH) {
                     RecLine Rn;
-                    load_line(has, true, payload + rec_at(qe, unit), w, Rn);
-                    if (pend) pile_line(true, true, nullptr, Rp, w, pc, tile, t5, max_span, span_err, pk_err);
+                    load_line(has, kLayout, payload + rec_at(qe, unit, pe_off), w, Rn);
+                    if (pend) pile_line(true, kLayout, nullptr, Rp, w, pc, tile, t5, max_span, span_err, pk_err);
                     pend = false;
-                    pile_line(has, true, nullptr, Rn, w, pc, tile, t5, max_span, span_err, pk_err);
+                    pile_line(has, kLayout, nullptr, Rn, w, pc, tile, t5, max_span, span_err, pk_err);
                 } else {
-                    pile_read(has, kPacked || (qe & PE_PACKED) != 0u, payload + rec_at(qe, unit), w, pc, tile, t5,
+                    pile_read(has, elem_layout<kLayout>(qe), payload + rec_at(qe, unit, pe_off), w, pc, tile, t5,
                               max_span, span_err, pk_err);
                 }
             }
@@ -2364,7 +2464,7 @@ __global__ void k_check_inputs(const uint64_t* __restrict__ roff, const uint16_t
     if (in)
         bits = (r != (uint64_t)i * kRecStride ? 1u : 0u) | ((r & 63ull) != 0ull || (r >> 38) != 0ull ? 2u : 0u) |
                (f & MGP_FLAG_PAIRED ? CHK_PAIRED : CHK_UNPAIRED) | (f & MGP_FLAG_NOSEQQUAL ? CHK_NOSEQ : 0u) |
-               (f & MGP_FLAG_PACKED ? 0u : CHK_FULL) |
+               layout_bit(f) |
                (s0 < 0 || s0 >= mito_len || at >= kCompactTlen ? CHK_WIDEKEY : 0u) | (uns ? CHK_UNSORTED : 0u);
     bits = wave_or(bits);
     const uint32_t msp = wave_max(sp);
@@ -2378,12 +2478,14 @@ __global__ void k_check_inputs(const uint64_t* __restrict__ roff, const uint16_t
 // spec: the grouping took the speculative compact path without the host's look at
 // the flag bits (streaming segments): reads it cannot serve make the run rerun resident.
 // max_span is a running maximum (a streaming run's segments accumulate it).
-__global__ void k_check_stats(const uint32_t* __restrict__ ck, DevStats* st, int spec) {
+__global__ void k_check_stats(const uint32_t* __restrict__ ck, DevStats* st, uint32_t spec_layout) {
+    // spec_layout: 0, or the one CHK_P64 / CHK_P32 layout a streaming segment assumed
     if (threadIdx.x == 0) {
         const uint32_t b = ck[0];
         st->max_span = max(st->max_span, ck[1]);
         if (b & CHK_UNSORTED) atomicOr(&st->err, ERR_UNSORTED);
-        if (spec && ((b & (CHK_FULL | CHK_NOSEQ)) || ((b & CHK_PAIRED) && (b & CHK_UNPAIRED))))
+        if (spec_layout && ((b & (CHK_FULL | CHK_P64 | CHK_P32 | CHK_NOSEQ) & ~spec_layout) ||
+                            ((b & CHK_PAIRED) && (b & CHK_UNPAIRED))))
             atomicOr(&st->err, ERR_RESPEC);
     }
 }
@@ -2532,8 +2634,9 @@ int mgp_open(const mgp_config* cfg, int hip_device, mgp_ctx** out) {
                                   hipFuncAttributeMaxDynamicSharedMemorySize, lds_max);
         (void)hipFuncSetAttribute((const void*)k_group_a<kOffSpec, true>,
                                   hipFuncAttributeMaxDynamicSharedMemorySize, lds_max);
-        (void)hipFuncSetAttribute((const void*)k_pileup<false>, hipFuncAttributeMaxDynamicSharedMemorySize, lds_max);
-        (void)hipFuncSetAttribute((const void*)k_pileup<true>, hipFuncAttributeMaxDynamicSharedMemorySize, lds_max);
+        (void)hipFuncSetAttribute((const void*)k_pileup<kLayAny>, hipFuncAttributeMaxDynamicSharedMemorySize, lds_max);
+        (void)hipFuncSetAttribute((const void*)k_pileup<kLayP64>, hipFuncAttributeMaxDynamicSharedMemorySize, lds_max);
+        (void)hipFuncSetAttribute((const void*)k_pileup<kLayP32>, hipFuncAttributeMaxDynamicSharedMemorySize, lds_max);
         (void)hipGetLastError();
         if ((size_t)ctx->g.L * 4 + 2048 > prop.sharedMemPerBlock) {
             delete ctx;
@@ -2647,7 +2750,7 @@ static int ensure_inputs(mgp_ctx* ctx, int64_t n_total, int64_t pay_total, bool 
     return MGP_OK;
 }
 
-static int stream_segments(mgp_ctx* ctx, int64_t last_start);
+static int stream_segments(mgp_ctx* ctx, int64_t last_start, uint16_t last_flag);
 
 int mgp_push_batch(mgp_ctx* ctx, const mgp_batch* b) {
     if (!ctx || !b) return set_err(MGP_E_INVALID, "null ctx/batch");
@@ -2688,7 +2791,7 @@ int mgp_push_batch(mgp_ctx* ctx, const mgp_batch* b) {
     ctx->no_spec = false;
     // streaming: the windows this batch completes go through the hot path now,
     // behind its copies, while the caller pushes the next batch
-    if (ctx->stream) MGP_TRY(stream_segments(ctx, (int64_t)b->start[nb - 1]));
+    if (ctx->stream) MGP_TRY(stream_segments(ctx, (int64_t)b->start[nb - 1], b->flag[nb - 1]));
     return MGP_OK;
 }
 
@@ -2853,23 +2956,32 @@ static int run_segment(mgp_ctx* ctx, const Seg& sg, int slot, int& dup_parts, in
     // otherwise, or once that failed on the resident reads (no_spec, ERR_RESPEC), the
     // standalone check takes every bit first (k_check_inputs, then a host wait).
     STAGE_BEGIN(ST_GROUP_A);
-    int unit = 6;  // the pileup element's record offset unit: 64 bytes, or 16 bytes when
-                   // some record is not 64-byte aligned; either way a 31-bit count of units
+    int unit = 6;  // the pileup element's record offset unit: 64 bytes (32 for 32-byte records on the
+                   // speculative path), or 16 bytes when some record is not 64-byte aligned
     bool spec = false, track = false;
+    int layout = kLayP64;  // the pileup's instantiation (the record layouts present)
     ctx->roff_mode = kOffR64;
     ctx->read_bits = 0;
+    constexpr uint32_t kLayBits = CHK_FULL | CHK_P64 | CHK_P32;
     if (n > 0 && sg.stream) {
+        // the layout the run's first batch showed; k_check_stats makes the run rerun
+        // resident if another one turns up
         spec = true;
         ctx->roff_mode = kOffSpec;
+        layout = ctx->stream_layout;
+        unit = layout == kLayP32 ? 5 : 6;
     } else if (n > 0) {
         HIP_TRY(hipEventSynchronize(ctx->ev_bits));
         const uint32_t fb = ctx->h_bits[0];
+        const uint32_t lb = fb & kLayBits;
+        const int su = lb == CHK_P32 ? 5 : 6;
         track = ((fb & CHK_PAIRED) && (fb & CHK_UNPAIRED)) || (fb & CHK_NOSEQ);
-        spec = !ctx->no_spec && !ctx->group_wide && !track && !(fb & CHK_FULL) &&
-               (uint64_t)ctx->pay < ((uint64_t)(PE_KEEP & PE_OFF) << 6);
+        spec = !ctx->no_spec && !ctx->group_wide && !track && (lb == CHK_P64 || lb == CHK_P32) &&
+               (uint64_t)ctx->pay < ((uint64_t)(PE_KEEP & PE_OFF) << su);
         if (spec) {
             ctx->roff_mode = kOffSpec;
             ctx->read_bits = fb;
+            unit = su;
         } else {
             k_check_inputs<<<blocks_for(n), kBlock, 0, s>>>(
                 ctx->roff.as<uint64_t>(), ctx->flag.as<uint16_t>(), ctx->start.as<int32_t>(),
@@ -2884,17 +2996,22 @@ static int run_segment(mgp_ctx* ctx, const Seg& sg, int slot, int& dup_parts, in
             ctx->read_bits = irr;
             unit = ctx->roff_mode == kOffR64 ? 4 : 6;
         }
+        const uint32_t rl = ctx->read_bits & kLayBits;
+        layout = rl == CHK_P32 ? kLayP32 : (rl == 0u || rl == CHK_P64) ? kLayP64 : kLayAny;
     }
-    if (n > 0 && (uint64_t)ctx->pay >= ((uint64_t)(PE_KEEP & PE_OFF) << unit))
-        return set_err(MGP_E_INVALID, unit == 6 ? "payload larger than 128 GiB in one context; shard the cells"
-                                                : "payload with 16-byte aligned records larger than 32 GiB in "
-                                                  "one context; place records at 64-byte offsets or shard the cells");
 
     // 3. stable grouping into cell-major order (two passes), duplicate marking in pass B;
-    // 8-byte elements when the resident reads allow them (GCompact)
+    // 8-byte elements when the resident reads allow them (GCompact: one packed layout)
     const uint32_t rbits = ctx->read_bits;
     const bool compact = spec || (!ctx->group_wide && ctx->roff_mode != kOffR64 && unit == 6 && !track &&
-                                  !(rbits & (CHK_FULL | CHK_WIDEKEY)));
+                                  layout != kLayAny && !(rbits & CHK_WIDEKEY));
+    // pileup elements: 31 offset bits (compact) or 30 and the layout bits (wide), below PE_KEEP
+    const uint32_t pe_off = compact ? PE_OFF : PE_OFF30;
+    if (n > 0 && (uint64_t)ctx->pay >= ((uint64_t)(PE_KEEP & pe_off) << unit))
+        return set_err(MGP_E_INVALID, "payload of " + std::to_string(ctx->pay) + " bytes above the " +
+                                          std::to_string((uint64_t)(PE_KEEP & pe_off) << unit) +
+                                          "-byte limit of one context for this record placement; shard the "
+                                          "cells or place records at 64-byte offsets");
     if (n > 0) {
         int gbits = 0;
         while (gbits < 31 && (1 << gbits) < ngroups) ++gbits;
@@ -2912,7 +3029,7 @@ static int run_segment(mgp_ctx* ctx, const Seg& sg, int slot, int& dup_parts, in
                 ctx->roff32.as<uint32_t>(), ctx->span.as<uint32_t>(), ctx->bin_start.as<uint32_t>(),
                 ctx->PG.as<uint32_t>(), ctx->F.as<uint32_t>(), ctx->bin_base.as<uint32_t>(), g, ngroups, gbits,
                 ctx->cfg.min_mapq, ctx->bucket_off.as<uint32_t>(), ctx->gel2.as<GElem>(),
-                ctx->first_read.as<uint32_t>(), ctx->roff_irregular.as<uint32_t>(), st, sg.w0, sg.bhi);
+                ctx->first_read.as<uint32_t>(), ctx->roff_irregular.as<uint32_t>(), st, sg.w0, sg.bhi, unit);
         };
         if (spec) {
             launch_a(k_group_a<kOffSpec, true>);
@@ -2929,7 +3046,8 @@ static int run_segment(mgp_ctx* ctx, const Seg& sg, int slot, int& dup_parts, in
         HIP_TRY(hipGetLastError());
         // the check's span and order bits into the run's stats (the pileup's halo); a
         // streaming segment also checks here the flag bits its variants assume
-        k_check_stats<<<1, 64, 0, s>>>(ctx->roff_irregular.as<uint32_t>(), st, sg.stream ? 1 : 0);
+        k_check_stats<<<1, 64, 0, s>>>(ctx->roff_irregular.as<uint32_t>(), st,
+                                       sg.stream ? (layout == kLayP32 ? CHK_P32 : CHK_P64) : 0u);
         HIP_TRY(hipGetLastError());
     }
     STAGE_END(ST_GROUP_A);
@@ -2980,8 +3098,9 @@ static int run_segment(mgp_ctx* ctx, const Seg& sg, int slot, int& dup_parts, in
     if (sg.w1 > sg.w0) {
         dim3 gp(g.nchunks, sg.w1 - sg.w0);
         const size_t psm = (size_t)5 * g.Wp * 4;
-        auto pile_kern = (!sg.stream && (ctx->read_bits & CHK_FULL)) ? k_pileup<false> : k_pileup<true>;
-        pile_kern<<<gp, kBlock, psm, s>>>(g, pc, ctx->payload.as<uint8_t>(), ctx->pel.as<uint32_t>(), unit,
+        auto pile_kern = layout == kLayP32 ? k_pileup<kLayP32> : layout == kLayP64 ? k_pileup<kLayP64>
+                                                                                    : k_pileup<kLayAny>;
+        pile_kern<<<gp, kBlock, psm, s>>>(g, pc, ctx->payload.as<uint8_t>(), ctx->pel.as<uint32_t>(), unit, pe_off,
                                          ctx->H.as<uint32_t>(), out16_of(ctx), ctx->counts.as<uint32_t>(),
                                          ctx->tn5.as<uint32_t>(), ctx->depth.as<uint32_t>(),
                                          ctx->n_reads.as<uint32_t>(), ctx->any_paired.as<uint8_t>(), pair_mode,
@@ -3080,12 +3199,14 @@ static int run_finish(mgp_ctx* ctx, int slot, int dup_parts, bool streamed) {
 // pushed start says which) go through the hot path as one segment, queued behind the
 // batch's copies while the next batches are still being copied. The last window
 // (it also takes the overflow bin) waits for mgp_run.
-static int stream_segments(mgp_ctx* ctx, int64_t last_start) {
+static int stream_segments(mgp_ctx* ctx, int64_t last_start, uint16_t last_flag) {
     const Geom& g = ctx->g;
     if (ctx->stream_off || g.nc <= 0 || last_start < 0) return MGP_OK;
     const int64_t wc = std::min<int64_t>(last_start / g.W, g.nwin - 1);  // windows [0, wc) are complete
     if (wc <= ctx->w_done) return MGP_OK;
-    if ((uint64_t)ctx->pay >= ((uint64_t)(PE_KEEP & PE_OFF) << 6)) {  // not for compact elements: run resident
+    if (!ctx->seg_open) ctx->stream_layout = (last_flag & MGP_FLAG_PACK32) ? kLayP32 : kLayP64;
+    const int unit = ctx->stream_layout == kLayP32 ? 5 : 6;
+    if ((uint64_t)ctx->pay >= ((uint64_t)(PE_KEEP & PE_OFF) << unit)) {  // not for compact elements: run resident
         ctx->stream_off = true;
         return MGP_OK;
     }
@@ -3335,7 +3456,7 @@ int mgp_synth_fill(void* stream, uint64_t seed, int64_t n, int read_len, int n_c
                    const uint32_t* d_cdf, const uint8_t* d_ref, int32_t* start, int32_t* bc, int32_t* tlen,
                    uint16_t* flag, uint8_t* mapq, uint32_t* span, uint64_t* roff, uint8_t* payload,
                    int64_t* payload_bytes, int rec_align, int pack, int placed, int cell_lo, int cell_hi,
-                   int shard_rank, int shard_world, uint64_t* d_map, int64_t* n_out);
+                   int shard_rank, int shard_world, uint64_t* d_map, int64_t* n_out, int p32_minq);
 
 int mgp_synth_generate(mgp_ctx* ctx, const mgp_synth_params* p) {
     if (!ctx || !p || !p->cell_cdf || !p->ref_codes) return set_err(MGP_E_INVALID, "null synth args");
@@ -3367,8 +3488,10 @@ int mgp_synth_generate(mgp_ctx* ctx, const mgp_synth_params* p) {
     // bytes the generator writes per record: a packed record (read_len <= MGP_PACK_MAX_LEN),
     // else the full layout of up to 3 CIGAR operations, at the placement's alignment
     const int64_t max_rec = ((int64_t)mgp_cigar_offset((uint32_t)p->read_len) + 16 + align - 1) & ~(int64_t)(align - 1);
+    if (p->pack < 0 || p->pack > 2 || (p->pack == 2 && (p->pack_min_baseq < -128 || p->pack_min_baseq > 127)))
+        return set_err(MGP_E_INVALID, "synth pack must be 0, 1 or 2 (32-byte records for a min_baseq in [-128, 127])");
     const bool packed = p->pack && p->read_len <= MGP_PACK_MAX_LEN;
-    const int64_t rec_bytes = packed ? (int64_t)MGP_PACK_BYTES : max_rec;
+    const int64_t rec_bytes = packed ? (int64_t)(p->pack == 2 ? MGP_PACK32_BYTES : MGP_PACK_BYTES) : max_rec;
     const bool placed = p->rec_off != nullptr;
     if (placed && p->payload_bytes < 0) return set_err(MGP_E_INVALID, "synth payload_bytes out of range");
     DevBuf cdf, ref, map;
@@ -3385,7 +3508,8 @@ int mgp_synth_generate(mgp_ctx* ctx, const mgp_synth_params* p) {
         MGP_TRY(map.ensure((size_t)std::max<int64_t>(n, 1) * 8));
         r = mgp_synth_fill(s, p->seed, n, p->read_len, nc, L, cdf.as<uint32_t>(), ref.as<uint8_t>(), nullptr,
                            nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, &pay, align, p->pack, -1,
-                           p->cell_lo, p->cell_hi, p->shard_rank, p->shard_world, map.as<uint64_t>(), &n_out);
+                           p->cell_lo, p->cell_hi, p->shard_rank, p->shard_world, map.as<uint64_t>(), &n_out,
+                           p->pack_min_baseq);
         if (r != MGP_OK) return set_err(r, "synth: keep scan failed");
         pay = placed ? p->payload_bytes : 0;
     }
@@ -3404,7 +3528,7 @@ int mgp_synth_generate(mgp_ctx* ctx, const mgp_synth_params* p) {
                        ctx->flag.as<uint16_t>(), ctx->mapq.as<uint8_t>(), ctx->span.as<uint32_t>(),
                        ctx->roff.as<uint64_t>(), ctx->payload.as<uint8_t>(), &pay, align, p->pack, placed,
                        shard ? p->cell_lo : 0, shard ? p->cell_hi : 0, p->shard_rank, p->shard_world,
-                       map.as<uint64_t>(), &n_out);
+                       map.as<uint64_t>(), &n_out, p->pack_min_baseq);
     if (r != MGP_OK) return r == MGP_E_INVALID ? set_err(r, "synth: invalid arguments") : set_err(r, "synth failed");
     HIP_TRY(hipStreamSynchronize(s));
     cdf.release();

@@ -79,9 +79,15 @@ __device__ __forceinline__ uint64_t rec_size(int ncig, int rl, int align) {
     return (uint64_t)((cigar_offset(rl) + 4 * ncig + align - 1) & ~(align - 1));
 }
 
-// every synthetic read fits the packed layout when rl <= MGP_PACK_MAX_LEN: quals
-// are <= 37, at most 3 CIGAR operations with 2 aligned blocks, lengths < 64
+// every synthetic read fits the packed layouts when rl <= MGP_PACK_MAX_LEN: quals
+// are <= 37, at most 3 CIGAR operations with 2 aligned blocks, lengths < 64, starts
+// in [0, 16569) (pack 1: 64-byte records, pack 2: 32-byte ones)
 __device__ __forceinline__ bool packs(int rl, int pack) { return pack && rl <= MGP_PACK_MAX_LEN; }
+__device__ __forceinline__ uint64_t packed_size(int pack, int align) {
+    const int b = pack == 2 ? MGP_PACK32_BYTES : MGP_PACK_BYTES;
+    const int a = pack == 2 && align > MGP_PACK32_BYTES ? MGP_PACK32_BYTES : align;
+    return (uint64_t)((b + a - 1) & ~(a - 1));
+}
 
 // Cell-range filter (mgp_synth_params.cell_lo/hi, shard_rank/world): a shard of the
 // global read set keeps the reads of its cells (barcode rebased to cell_lo) and, of the
@@ -109,8 +115,7 @@ __global__ void k_synth_sizes(uint64_t seed, int64_t n, int rl, int align, int p
         if (!keeps(f, i, read_bc(seed, i, nc, cdf))) return;
         j = (int64_t)f.map[i];
     }
-    sz[j] = packs(rl, pack) ? (uint64_t)((MGP_PACK_BYTES + align - 1) & ~(align - 1))
-                            : rec_size(cig_of(seed, i).n, rl, align);
+    sz[j] = packs(rl, pack) ? packed_size(pack, align) : rec_size(cig_of(seed, i).n, rl, align);
 }
 
 __global__ void k_synth_keep(uint64_t seed, int64_t n, int nc, const uint32_t* __restrict__ cdf, Filt f,
@@ -230,7 +235,7 @@ __global__ void k_synth_fill(uint64_t seed, int64_t n, int rl, int nc, int L, co
                              const uint8_t* __restrict__ ref, int32_t* __restrict__ start, int32_t* __restrict__ bc,
                              int32_t* __restrict__ tlen, uint16_t* __restrict__ flag, uint8_t* __restrict__ mapq,
                              uint32_t* __restrict__ span, const uint64_t* __restrict__ roff,
-                             uint8_t* __restrict__ payload, int pack, Filt flt) {
+                             uint8_t* __restrict__ payload, int pack, int p32_minq, Filt flt) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const uint64_t spanpos = (uint64_t)(L - rl + 1);
@@ -254,7 +259,8 @@ __global__ void k_synth_fill(uint64_t seed, int64_t n, int rl, int nc, int L, co
     const Cig cg = cig_of(seed, i);
 
     const bool pk = packs(rl, pack);
-    if (pk) f |= MGP_FLAG_PACKED;
+    const bool p32 = pk && pack == 2;
+    if (pk) f |= p32 ? MGP_FLAG_PACK32 : MGP_FLAG_PACKED;
     int64_t j = i;  // the read's index in the (shard's) read set
     if (flt.hi > flt.lo) {
         if (!keeps(flt, i, b)) return;
@@ -286,7 +292,13 @@ __global__ void k_synth_fill(uint64_t seed, int64_t n, int rl, int nc, int L, co
     uint8_t* rec = payload + roff[j];
     uint8_t* qual = rec + 16;
     uint8_t* seq = rec + mgp_seq_offset((uint32_t)rl);
-    if (pk) {  // packed layout (include/mgpileup.h); base bytes are written per base below
+    uint32_t w32[8] = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u};  // a 32-byte record, written at the end
+    if (p32) {  // 32-byte layout (include/mgpileup.h): header here, 3-bit codes per base below
+        w32[0] = (uint32_t)s0 | ((uint32_t)rl << 16) | ((uint32_t)(cg.n | (strand ? 0x80 : 0)) << 24);
+        w32[1] = (cw[0] & 0xFFFFu) | ((cw[1] & 0xFFFFu) << 16);
+        w32[2] = (cw[2] & 0xFFFFu);
+        w32[7] = (uint32_t)(uint8_t)(int8_t)p32_minq << 24;
+    } else if (pk) {  // packed layout (include/mgpileup.h); base bytes are written per base below
         *reinterpret_cast<int32_t*>(rec) = s0;
         rec[4] = (uint8_t)rl;
         rec[5] = (uint8_t)(cg.n | (strand ? 0x80 : 0));
@@ -330,6 +342,13 @@ __global__ void k_synth_fill(uint64_t seed, int64_t n, int rl, int nc, int L, co
             else if (m < BASE_SUB) code = kCodes[(code_idx(rc) + 1 + (uint32_t)((hs & 255) % 3)) & 3];
             else code = rc;
         }
+        if (p32) {
+            const uint32_t v = code == 15 ? 0u : code_idx(code) | ((int)(int8_t)qv >= p32_minq ? 4u : 0u);
+            const int bit = 96 + 3 * q;
+            w32[bit >> 5] |= v << (bit & 31);
+            if ((bit & 31) > 29) w32[(bit >> 5) + 1] |= v >> (32 - (bit & 31));
+            continue;
+        }
         if (pk) {
             rec[14 + q] = code == 15 ? (uint8_t)0xFF : (uint8_t)((qv << 2) | code_idx(code));
             continue;
@@ -339,6 +358,11 @@ __global__ void k_synth_fill(uint64_t seed, int64_t n, int rl, int nc, int L, co
         else seq[q >> 1] = (uint8_t)((hi_nib << 4) | code);
     }
     if ((rl & 1) && !pk) seq[rl >> 1] = (uint8_t)(hi_nib << 4);
+    if (p32) {
+        uint4* r4 = reinterpret_cast<uint4*>(rec);
+        r4[0] = make_uint4(w32[0], w32[1], w32[2], w32[3]);
+        r4[1] = make_uint4(w32[4], w32[5], w32[6], w32[7]);
+    }
 }
 
 }  // namespace
@@ -350,7 +374,7 @@ extern "C" int mgp_synth_fill(void* stream, uint64_t seed, int64_t n, int read_l
                               int32_t* tlen, uint16_t* flag, uint8_t* mapq, uint32_t* span, uint64_t* roff,
                               uint8_t* payload, int64_t* payload_bytes, int rec_align, int pack, int placed,
                               int cell_lo, int cell_hi, int shard_rank, int shard_world, uint64_t* d_map,
-                              int64_t* n_out) {
+                              int64_t* n_out, int p32_minq) {
     hipStream_t s = (hipStream_t)stream;
     if (read_len < 48) return MGP_E_INVALID;
     *n_out = n;
@@ -380,7 +404,7 @@ extern "C" int mgp_synth_fill(void* stream, uint64_t seed, int64_t n, int read_l
     }
     if (total && hipMemsetAsync(payload, 0, (size_t)total, s) != hipSuccess) return MGP_E_HIP;
     k_synth_fill<<<nb, kBlock, 0, s>>>(seed, n, read_len, n_cells, mito_len, d_cdf, d_ref, start, bc, tlen, flag,
-                                       mapq, span, roff, payload, pack, flt);
+                                       mapq, span, roff, payload, pack, p32_minq, flt);
     if (hipGetLastError() != hipSuccess) return MGP_E_HIP;
     if (hipStreamSynchronize(s) != hipSuccess) return MGP_E_HIP;
     *payload_bytes = (int64_t)total;

@@ -81,14 +81,18 @@ class BAMReader:
         """Every chrM record as one engine batch (BAM order).
 
         ``bc`` is the whitelist index (-1 = no tag or not whitelisted). In bulk
-        mode every record goes to the ``"bulk"`` cell (readers.py:97-99)."""
+        mode every record goes to the ``"bulk"`` cell (readers.py:97-99). With
+        packing, reads that fit get the 32-byte record made for the run's
+        min_baseq (four to a 128-byte line), the others the 64-byte or full one."""
         bulk = -1
+        q = int(self.config.quality.min_baseq)
+        pack32 = q if pack and -128 <= q <= 127 else None
         if self.is_bulk_mode:
             bulk = max(i for i, b in enumerate(self.barcode_list) if b == "bulk")
         try:
             with self._open() as bam:
                 soa = bam.read_soa(self.config.mito_chr, self.barcode_list, tag=self.config.barcode_tag,
-                                   rec_align=rec_align, bulk_cell=bulk, pack=pack)
+                                   rec_align=rec_align, bulk_cell=bulk, pack=pack, pack32=pack32)
         except BAMReadError:
             raise
         except Exception as e:

@@ -58,8 +58,10 @@ FLAG_SECONDARY = 0x100
 FLAG_SUPPLEMENTARY = 0x800
 FLAG_NOSEQQUAL = 0x1000
 FLAG_PACKED = 0x2000  # the record uses the packed 64-byte layout (include/mgpileup.h)
+FLAG_PACK32 = 0x4000  # the record uses the 32-byte layout (include/mgpileup.h)
 PACK_MAX_LEN = 50
 PACK_BYTES = 64
+PACK32_BYTES = 32
 
 CODES = np.array([1, 2, 4, 8], dtype=np.uint8)  # BAM 4-bit A, C, G, T
 SEQ_NT16 = "=ACMGRSVTWYHKDBN"
@@ -282,6 +284,54 @@ def pack_bytes(start, lseq, reverse, ncig, cig, qual, code) -> np.ndarray:
     return out
 
 
+def pack32_mask(start, flag, lseq, ncig, cig, min_baseq: int) -> np.ndarray:
+    """Which reads fit the 32-byte layout for this min_baseq (mgp_pack32_record)."""
+    start = np.asarray(start, np.int64)
+    lseq = np.asarray(lseq, np.int64)
+    ncig = np.asarray(ncig, np.int64)
+    ok = ((np.asarray(flag) & FLAG_NOSEQQUAL) == 0) & (lseq >= 1) & (lseq <= PACK_MAX_LEN) & (ncig <= 4)
+    ok &= (start >= 0) & (start < 65536) & (-128 <= int(min_baseq) <= 127)
+    cig = np.asarray(cig, np.int64).reshape(start.shape[0], -1)
+    used = np.arange(cig.shape[1])[None, :] < ncig[:, None]
+    op = cig & 15
+    ok &= ~np.any(used & ((cig >> 4) >= 4096), axis=1)
+    ok &= np.sum(used & ((op == 0) | (op == 7) | (op == 8)), axis=1) <= 2
+    return ok
+
+
+def pack32_bytes(start, lseq, reverse, ncig, cig, qual, code, min_baseq: int) -> np.ndarray:
+    """32-byte records [m, 32] (include/mgpileup.h): u16 start, l_seq, n_cigar |
+    reverse << 7, CIGAR as u16, then a 3-bit code per base at bit 96 + 3k
+    (counted << 2 | b; counted = A/C/G/T with int8(qual) >= min_baseq), min_baseq
+    in byte 31."""
+    m = np.asarray(start).shape[0]
+    out = np.zeros((m, PACK32_BYTES), np.uint8)
+    out[:, 0:2] = np.asarray(start, "<u2").reshape(m, 1).view(np.uint8)
+    out[:, 2] = np.asarray(lseq, np.uint8)
+    out[:, 3] = (np.asarray(ncig, np.uint8) | np.where(np.asarray(reverse), 0x80, 0)).astype(np.uint8)
+    c16 = np.zeros((m, 4), "<u2")
+    cig = np.asarray(cig, np.int64).reshape(m, -1)
+    for k in range(min(4, cig.shape[1])):
+        c16[:, k] = np.where(np.asarray(ncig) > k, cig[:, k], 0).astype("<u2")
+    out[:, 4:12] = c16.view(np.uint8).reshape(m, 8)
+    code = np.asarray(code, np.int64)
+    qual = np.asarray(qual, np.int64)
+    n = code.shape[1]
+    b = np.select([code == 1, code == 2, code == 4, code == 8], [0, 1, 2, 3], -1)
+    q8 = np.where(qual >= 128, qual - 256, qual)  # int8(qual): >= 128 wraps (pileup.py Q5)
+    v = np.where(b >= 0, np.maximum(b, 0) | np.where(q8 >= int(min_baseq), 4, 0), 0)
+    v = np.where(np.arange(n)[None, :] < np.asarray(lseq, np.int64).reshape(m, 1), v, 0).astype(np.uint64)
+    bits = np.zeros((m, 4), np.uint64)  # bits 96..351 of the record, as 4 little-endian u64 words
+    for k in range(n):
+        pos = 3 * k
+        bits[:, pos >> 6] |= v[:, k] << np.uint64(pos & 63)
+        if (pos & 63) > 61:
+            bits[:, (pos >> 6) + 1] |= v[:, k] >> np.uint64(64 - (pos & 63))
+    out[:, 12:31] = bits.view(np.uint8).reshape(m, 32)[:, :19]
+    out[:, 31] = np.uint8(int(min_baseq) & 0xFF)
+    return out
+
+
 def rec_size(ncig, lseq, align: int = 16):
     """Bytes a record occupies when records are placed at multiples of `align`."""
     return (cigar_offset(lseq) + 4 * np.asarray(ncig, np.int64) + align - 1) & ~(align - 1)
@@ -393,24 +443,33 @@ def _synth_chunk(seed, i0, i1, n, read_len, n_cells, mito_len, cdf, ref):
     )
 
 
-def _pack_fixed(start, flag, ncig, cig, qual, code, rl, align=REC_ALIGN, pack=True):
+def _pack_fixed(start, flag, ncig, cig, qual, code, rl, align=REC_ALIGN, pack=True, pack32=None):
     """Pack records for reads of one read length (vectorised). Returns (rec_off,
-    payload, flag): reads that fit get the packed layout and MGP_FLAG_PACKED."""
+    payload, flag): reads that fit get the packed layout and MGP_FLAG_PACKED;
+    with pack32 (a min_baseq), reads that fit the 32-byte layout get it first
+    (MGP_FLAG_PACK32, 32-byte records at multiples of min(align, 32))."""
     m = start.shape[0]
-    pk = packable_mask(start, flag, np.full(m, rl), ncig, cig, qual) if pack else np.zeros(m, bool)
-    flag = (flag | np.where(pk, FLAG_PACKED, 0)).astype(np.uint16)
+    p32 = pack32_mask(start, flag, np.full(m, rl), ncig, cig, pack32) if pack32 is not None else np.zeros(m, bool)
+    pk = packable_mask(start, flag, np.full(m, rl), ncig, cig, qual) & ~p32 if pack else np.zeros(m, bool)
+    flag = (flag | np.where(pk, FLAG_PACKED, 0) | np.where(p32, FLAG_PACK32, 0)).astype(np.uint16)
+    a32 = min(align, PACK32_BYTES)
     sizes = np.where(pk, (PACK_BYTES + align - 1) & ~(align - 1), rec_size(ncig, np.full(m, rl), align))
+    sizes = np.where(p32, (PACK32_BYTES + a32 - 1) & ~(a32 - 1), sizes)
     roff = np.zeros(m, np.uint64)
     if m:
         roff[1:] = np.cumsum(sizes[:-1]).astype(np.uint64)
     total = int(sizes.sum())
     pay = np.zeros(total, np.uint8)
     ro = roff.astype(np.int64)
+    if p32.any():
+        pr = pack32_bytes(start[p32], np.full(int(p32.sum()), rl), (flag[p32] & FLAG_REVERSE) != 0, ncig[p32],
+                          cig[p32], qual[p32], code[p32], pack32)
+        pay[ro[p32, None] + np.arange(PACK32_BYTES)[None, :]] = pr
     if pk.any():
         pr = pack_bytes(start[pk], np.full(int(pk.sum()), rl), (flag[pk] & FLAG_REVERSE) != 0, ncig[pk], cig[pk],
                         qual[pk], code[pk])
         pay[ro[pk, None] + np.arange(PACK_BYTES)[None, :]] = pr
-    fu = ~pk
+    fu = ~pk & ~p32
     mf = int(fu.sum())
     if mf == 0:
         return roff, pay, flag
@@ -441,10 +500,11 @@ def _pack_fixed(start, flag, ncig, cig, qual, code, rl, align=REC_ALIGN, pack=Tr
 
 def synth_reads(
     seed: int, n_reads: int, n_cells: int, read_len: int = 50, mito_len: int = MITO_LEN, chunk: int = 262144,
-    rec_align: int = REC_ALIGN, pack: bool = True,
+    rec_align: int = REC_ALIGN, pack: bool = True, pack32: int | None = None,
 ) -> ReadSoA:
     """Host mirror of the device generator (bit-identical). pack: reads that fit
-    get the packed 64-byte record layout (all of them at read_len <= 50)."""
+    get the packed 64-byte record layout (all of them at read_len <= 50); pack32
+    (a min_baseq): the 32-byte layout made for that threshold instead."""
     if read_len < 48:
         raise ValueError("read_len must be >= 48")
     cdf = cell_cdf(seed, n_cells)
@@ -454,7 +514,7 @@ def synth_reads(
         i1 = min(n_reads, i0 + chunk)
         f = _synth_chunk(seed, i0, i1, n_reads, read_len, n_cells, mito_len, cdf, ref)
         roff, pay, flag = _pack_fixed(f["start"], f["flag"], f["ncig"], f["cig"], f["qual"], f["code"], read_len,
-                                      rec_align, pack)
+                                      rec_align, pack, pack32)
         parts.append(ReadSoA(f["start"], f["bc"], f["tlen"], flag, f["mapq"], f["span"], roff, pay))
     soa = _concat_dense(parts)
     soa.extra.update(cdf=cdf, ref=ref, seed=seed, read_len=read_len)
@@ -488,10 +548,12 @@ def cigar_ref_span(cigar) -> int:
     return sum(length for op, length in cigar if op in (0, 2, 3, 7, 8))
 
 
-def pack_reads(reads: list[dict], rec_align: int = REC_ALIGN, pack: bool = True) -> ReadSoA:
+def pack_reads(reads: list[dict], rec_align: int = REC_ALIGN, pack: bool = True,
+               pack32: int | None = None) -> ReadSoA:
     """Pack pysam-like read dicts into the engine input. pack: reads that fit get
     the packed 64-byte layout (include/mgpileup.h), which keeps what the pileup
-    reads but not the code and quality of non-ACGT bases.
+    reads but not the code and quality of non-ACGT bases; pack32 (a min_baseq):
+    reads that fit get the 32-byte layout made for that threshold first.
 
     Keys: ``reference_start``, ``flag`` (BAM flag), ``mapping_quality``,
     ``cigartuples`` (list of (op, len) or None), ``query_sequence`` (str or
@@ -523,10 +585,22 @@ def pack_reads(reads: list[dict], rec_align: int = REC_ALIGN, pack: bool = True)
         mapq[i] = r.get("mapping_quality", 60)
         span[i] = max(cigar_ref_span(cig), lseq)
         roff[i] = off
-        if pack and seq is not None and qual is not None and lseq:
+        if (pack or pack32 is not None) and seq is not None and qual is not None and lseq:
             cw = np.array([[(ln << 4) | op for op, ln in cig] or [0]], np.int64)
             qa = (np.asarray(qual, dtype=np.int64) & 0xFF).reshape(1, -1)
-            if packable_mask([start[i]], [f], [lseq], [len(cig)], cw, qa)[0]:
+            if pack32 is not None and pack32_mask([start[i]], [f], [lseq], [len(cig)], cw, pack32)[0]:
+                codes = np.array([[_NT16_IDX[ch] for ch in seq.upper()]], np.int64)
+                f |= FLAG_PACK32
+                flag[i] = f
+                a32 = min(rec_align, PACK32_BYTES)
+                size = (PACK32_BYTES + a32 - 1) & ~(a32 - 1)
+                rec = np.zeros(size, np.uint8)
+                rec[:PACK32_BYTES] = pack32_bytes([start[i]], [lseq], [(f & FLAG_REVERSE) != 0], [len(cig)], cw, qa,
+                                                  codes, pack32)[0]
+                chunks.append(rec)
+                off += size
+                continue
+            if pack and packable_mask([start[i]], [f], [lseq], [len(cig)], cw, qa)[0]:
                 codes = np.array([[_NT16_IDX[ch] for ch in seq.upper()]], np.int64)
                 f |= FLAG_PACKED
                 flag[i] = f
@@ -566,6 +640,20 @@ def unpack_record(payload: np.ndarray, off: int, flag: int = 0) -> dict:
     """Decode one payload record (flag: the read's flag word, which tells the
     layout). A packed record gives ``N`` with quality 0 for its non-ACGT bases
     and no ``flag`` key beyond the reverse bit."""
+    if int(flag) & FLAG_PACK32:
+        r = payload[off : off + PACK32_BYTES]
+        start = int(r[:2].view("<u2")[0])
+        lseq = int(r[2])
+        ncig = int(r[3]) & 0x7F
+        cig = r[4:12].view("<u2").astype(np.int64).tolist()[:ncig]
+        w = int.from_bytes(bytes(r[12:31]), "little")
+        v = [(w >> (3 * k)) & 7 for k in range(lseq)]
+        seq = "".join("ACGT"[x & 3] if x & 4 else "N" for x in v)
+        return dict(
+            reference_start=start, flag=FLAG_REVERSE if r[3] & 0x80 else 0,
+            cigartuples=[(c & 15, c >> 4) for c in cig], query_sequence=seq,
+            query_qualities=[127 if x & 4 else 0 for x in v], min_baseq=int(r[31].astype(np.int8)),
+        )
     if int(flag) & FLAG_PACKED:
         r = payload[off : off + PACK_BYTES]
         start = int(r[:4].view("<i4")[0])

@@ -335,7 +335,13 @@ int oracle_run(const mgp_config *cfg, const mgp_batch *b, mgp_result *out, int32
         for (int64_t k = 0; k < nr; ++k) {
             const int64_t i = lst[off[c] + k];
             if ((int)b->mapq[i] < cfg->min_mapq) continue; /* pileup.py:33 */
-            if (b->flag[i] & MGP_FLAG_PACKED) {
+            if (b->flag[i] & MGP_FLAG_PACK32) {
+                /* 32-byte record: its counted bits stand for base + quality
+                 * (include/mgpileup.h, made for the run's min_baseq) */
+                uint8_t full[128];
+                mgp_unpack32_record(b->payload + b->rec_off[i], full);
+                pile_read(full, cfg, bc8, tn5);
+            } else if (b->flag[i] & MGP_FLAG_PACKED) {
                 uint8_t full[128];
                 unpack_packed(b->payload + b->rec_off[i], full);
                 pile_read(full, cfg, bc8, tn5);

@@ -1,0 +1,113 @@
+"""32-byte records (MGP_FLAG_PACK32, include/mgpileup.h) on CPU: the packers (C
+header, Python mirror, native BAM decoder) agree, keep every bit the pileup reads
+under the run's min_baseq, and the quad placement puts four of a cell's records
+in a 128-byte line. The GPU side is in tests/test_gpu_pack32.py."""
+
+from __future__ import annotations
+
+import numpy as np
+import pytest
+
+from golden_io import CASES, Golden, check_result
+
+CONFIGS = {
+    "tenx": dict(min_baseq=0, min_mapq=0, dedup_mode="alignment_start", min_reads=0),
+    "run": dict(min_baseq=20, min_mapq=30, dedup_mode="alignment_and_fragment_length", min_reads=1),
+    "bias": dict(min_baseq=10, min_mapq=1, dedup_mode="none", min_reads=40, max_strand_bias=0.8),
+}
+
+
+def _same(a, b, what):
+    for k in ("counts", "tn5", "depth", "n_reads", "any_paired", "passed", "covered", "depth_sum", "median_lo",
+              "median_hi", "ref_tally", "first_read"):
+        np.testing.assert_array_equal(getattr(a, k), getattr(b, k), err_msg=f"{what}: {k}")
+    for k in ("total_reads", "filtered_reads", "duplicate_reads_with_length", "duplicate_reads_position_only"):
+        assert a.stats[k] == b.stats[k], (what, k)
+
+
+@pytest.mark.parametrize("cfgname", sorted(CONFIGS))
+def test_host_generator_pack32_same_pileup(cfgname, oracle_lib):
+    from mgatk2_amd.engine import EngineConfig
+    from mgatk2_amd.synth import FLAG_PACK32, PACK32_BYTES, synth_reads
+
+    cfg = EngineConfig(n_cells=40, **CONFIGS[cfgname])
+    a = synth_reads(321, 60_000, 40)
+    b = synth_reads(321, 60_000, 40, pack32=cfg.min_baseq)
+    assert (b.flag & FLAG_PACK32).all() and b.payload.size == PACK32_BYTES * b.n
+    assert np.all(b.rec_off == PACK32_BYTES * np.arange(b.n, dtype=np.uint64))
+    ra, _ = oracle_lib.oracle_run(cfg, a)
+    rb, _ = oracle_lib.oracle_run(cfg, b)
+    _same(ra, rb, cfgname)
+
+
+def test_pack32_unpack_roundtrip():
+    from mgatk2_amd.synth import FLAG_PACK32, pack_reads, unpack_record
+
+    reads = [
+        dict(reference_start=5, cigartuples=[(4, 2), (0, 7)], query_sequence="ACGTNRY",
+             query_qualities=[0, 1, 62, 30, 4, 200, 6], flag=0x11),
+        dict(reference_start=16560, cigartuples=[(0, 10), (1, 3), (0, 27), (5, 9)], query_sequence="ACGT" * 10,
+             query_qualities=[19, 20, 21, 130] * 10, flag=0x1),
+    ]
+    soa = pack_reads(reads, pack32=20)
+    assert (soa.flag & FLAG_PACK32).all()
+    for i, r in enumerate(reads):
+        d = unpack_record(soa.payload, int(soa.rec_off[i]), int(soa.flag[i]))
+        assert d["reference_start"] == r["reference_start"] and d["cigartuples"] == r["cigartuples"]
+        assert d["min_baseq"] == 20 and bool(d["flag"] & 0x10) == bool(r["flag"] & 0x10)
+        q8 = [q - 256 if q >= 128 else q for q in r["query_qualities"]]
+        want = "".join(c if c in "ACGT" and q >= 20 else "N" for c, q in zip(r["query_sequence"], q8))
+        assert d["query_sequence"] == want
+    # limits: start >= 65536 or < 0, > 4 CIGAR ops, long reads, min_baseq outside int8 keep other layouts
+    bad = [dict(reference_start=70000, cigartuples=[(0, 6)], query_sequence="A" * 6, query_qualities=[30] * 6),
+           dict(reference_start=-3, cigartuples=[(0, 6)], query_sequence="A" * 6, query_qualities=[30] * 6),
+           dict(reference_start=1, cigartuples=[(0, 51)], query_sequence="A" * 51, query_qualities=[30] * 51)]
+    assert not (pack_reads(bad, pack32=20).flag & FLAG_PACK32).any()
+    assert not (pack_reads(reads, pack32=128).flag & FLAG_PACK32).any()
+
+
+def test_quad_placement_four_records_of_a_cell_per_line(oracle_lib):
+    from mgatk2_amd.bam import PLACE_PAIRED, place_records
+    from mgatk2_amd.engine import EngineConfig
+    from mgatk2_amd.synth import FLAG_PACK32, PACK32_BYTES, ReadSoA, relocate, synth_reads
+
+    soa = synth_reads(77, 80_000, 30, pack32=20)
+    roff, total = place_records(soa.bc, soa.flag, np.full(soa.n, PACK32_BYTES, np.uint32), 30, PLACE_PAIRED)
+    assert np.all(roff % PACK32_BYTES == 0) and np.unique(roff).size == soa.n
+    line = roff // 128
+    keep = (soa.bc >= 0) & ((soa.flag & 0x904) == 0)
+    # a line holds the records of one cell (or of dropped reads), at most 4
+    key = np.where(keep, soa.bc, 30)
+    order = np.argsort(line, kind="stable")
+    l_s, k_s = line[order], key[order]
+    same_line = l_s[1:] == l_s[:-1]
+    assert np.all(k_s[1:][same_line] == k_s[:-1][same_line])
+    assert np.bincount(line.astype(np.int64)).max() <= 4
+    assert total < 1.5 * PACK32_BYTES * soa.n  # nearly every line is full
+    # the relocated set (shard gather with the producer placement) piles the same
+    cfg = EngineConfig(n_cells=30, **CONFIGS["run"])
+    quad = relocate(soa, paired=True, n_cells=30)
+    assert (quad.flag & FLAG_PACK32).all()
+    _same(oracle_lib.oracle_run(cfg, quad)[0], oracle_lib.oracle_run(cfg, soa)[0], "quad")
+    assert isinstance(quad, ReadSoA)
+
+
+@pytest.mark.parametrize("case", CASES)
+def test_bam_decoder_pack32_gives_the_reference_results(case, tmp_path, oracle_lib):
+    """The golden reads written as a BAM and decoded natively with 32-byte records
+    for the case's min_baseq (reads that do not fit keep the 64-byte or full
+    layout): the oracle gives the reference's outputs."""
+    from mgatk2_amd.bam import BamFile, soa_to_bam
+    from mgatk2_amd.synth import FLAG_PACK32
+
+    g = Golden(case)
+    cfg = g.config()
+    if not -128 <= cfg.min_baseq <= 127:
+        pytest.skip("min_baseq outside the 32-byte layout's range")
+    soa_to_bam(tmp_path / "x.bam", g.soa, g.whitelist)
+    for paired in (False, True):
+        with BamFile(tmp_path / "x.bam") as bam:
+            soa = bam.read_soa("chrM", g.whitelist, pack=True, paired=paired, pack32=cfg.min_baseq)
+        assert (soa.flag & FLAG_PACK32).any()
+        res, _ = oracle_lib.oracle_run(cfg, soa)
+        check_result(res, g)
