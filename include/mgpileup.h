@@ -236,61 +236,77 @@ static inline MGP_HD int mgp_pack_record(int32_t start, uint32_t l_seq, uint16_t
 }
 
 /* 32-byte record (flag[i] has MGP_FLAG_PACK32): what the pileup reads of a short
- * read under ONE base-quality threshold, four records per 128-byte line (the
- * pileup's gathers cost one line request each, whatever the record size):
+ * read under ONE (min_baseq, min_dist_from_end) pair, four records per 128-byte
+ * line (the pileup's gathers cost one line request each, whatever the record size):
  *   uint16 start                    0 <= start < 65536
  *   uint8  l_seq                    1 .. MGP_PACK_MAX_LEN
- *   uint8  n_cigar | reverse << 7   n_cigar <= 4
+ *   uint8  n_cigar | min_dist << 3 | reverse << 7   n_cigar <= 4, min_dist <= 15
  *   uint16 cigar[4]                 len << 4 | op (len < 4096), unused entries 0
- *   3-bit base codes                code k (k < l_seq) at bit 96 + 3k of the record:
- *                                   counted << 2 | b, b = 0..3 for A, C, G, T; counted =
- *                                   the base is A/C/G/T and int8(qual) >= min_baseq
- *                                   (pileup.py:80-86); 0 past l_seq
- *   int8   min_baseq at byte 31     the threshold the counted bits were made for
+ *   3-bit codes                     code k (k < 50) at bit 96 + 3k of the record:
+ *                                   0..3 = the base A, C, G, T, counted; 4 = not counted
+ *   int8   min_baseq at byte 31     the threshold the codes were made for
+ * Query position k is counted (pileup.py:55-95) iff it lies in the query range of
+ * an aligned (M, =, X) operation as the reference walks the CIGAR (an insertion
+ * does not advance the query position: quirk Q1), min_dist <= k < l_seq - min_dist
+ * (all k when min_dist is 0), int8(qual[k]) >= min_baseq and the base is A, C, G
+ * or T; the reference-range clamp and the pileup window are applied by the engine.
  * A read may be packed so iff it has SEQ and QUAL, 1 <= l_seq <= 50, n_cigar <= 4
- * with every length < 4096 and at most 2 aligned (M, =, X) operations,
- * 0 <= start < 65536, and -128 <= min_baseq <= 127. The engine refuses a run whose
- * min_baseq is not the records' (MGP_E_INVALID). Records sit at 32-byte multiples. */
+ * with every length < 4096 and at most 2 aligned operations, 0 <= start < 65536,
+ * -128 <= min_baseq <= 127 and 0 <= min_dist <= 15 (a negative min_dist_from_end
+ * acts as 0). The engine refuses a run whose thresholds are not the records'
+ * (MGP_E_INVALID). Records sit at 32-byte multiples. */
 static inline MGP_HD int mgp_pack32_record(int32_t start, uint32_t l_seq, uint16_t flag, uint32_t n_cigar,
                                            const uint32_t *cigar, const uint8_t *seq, const uint8_t *qual,
-                                           int32_t min_baseq, uint8_t *out) {
-    uint32_t k, blocks = 0;
+                                           int32_t min_baseq, int32_t min_dist, uint8_t *out) {
+    uint32_t k, blocks = 0, q = 0;
+    uint64_t inblk = 0;  /* query positions inside an aligned operation's range */
+    int32_t md = min_dist > 0 ? min_dist : 0;
     if ((flag & MGP_FLAG_NOSEQQUAL) || l_seq == 0u || l_seq > MGP_PACK_MAX_LEN || n_cigar > 4u) return 0;
-    if (start < 0 || start >= 65536 || min_baseq < -128 || min_baseq > 127) return 0;
+    if (start < 0 || start >= 65536 || min_baseq < -128 || min_baseq > 127 || md > 15) return 0;
     for (k = 0; k < n_cigar; ++k) {
-        const uint32_t op = cigar[k] & 15u;
-        if ((cigar[k] >> 4) >= 4096u) return 0;
-        blocks += (op == 0u || op == 7u || op == 8u);
+        const uint32_t op = cigar[k] & 15u, len = cigar[k] >> 4;
+        if (len >= 4096u) return 0;
+        if (op == 0u || op == 7u || op == 8u) {
+            uint32_t j;
+            ++blocks;
+            for (j = q; j < q + len && j < l_seq; ++j) inblk |= 1ull << j;
+        }
+        if (op == 0u || op == 7u || op == 8u || op == 4u) q += len;
     }
     if (blocks > 2u) return 0;
     for (k = 0; k < 32u; ++k) out[k] = 0;
     out[0] = (uint8_t)start;
     out[1] = (uint8_t)((uint32_t)start >> 8);
     out[2] = (uint8_t)l_seq;
-    out[3] = (uint8_t)(n_cigar | ((flag & MGP_FLAG_REVERSE) ? 0x80u : 0u));
+    out[3] = (uint8_t)(n_cigar | ((uint32_t)md << 3) | ((flag & MGP_FLAG_REVERSE) ? 0x80u : 0u));
     for (k = 0; k < n_cigar; ++k) {
         out[4 + 2 * k] = (uint8_t)cigar[k];
         out[5 + 2 * k] = (uint8_t)(cigar[k] >> 8);
     }
-    for (k = 0; k < l_seq; ++k) {
-        const uint32_t code = (k & 1u) ? (seq[k >> 1] & 15u) : (uint32_t)(seq[k >> 1] >> 4);
-        const int b = code == 1u ? 0 : code == 2u ? 1 : code == 4u ? 2 : code == 8u ? 3 : -1;
-        const uint32_t v = b < 0 ? 0u : (uint32_t)b | (((int32_t)(int8_t)qual[k] >= min_baseq) ? 4u : 0u);
-        const uint32_t bit = 96u + 3u * k;
-        out[bit >> 3] |= (uint8_t)(v << (bit & 7u));
-        if ((bit & 7u) > 5u) out[(bit >> 3) + 1] |= (uint8_t)(v >> (8u - (bit & 7u)));
+    for (k = 0; k < MGP_PACK_MAX_LEN; ++k) {
+        uint32_t v = 4u;
+        if (k < l_seq && ((inblk >> k) & 1u) && (int32_t)k >= md && (int32_t)k < (int32_t)l_seq - md &&
+            (int32_t)(int8_t)qual[k] >= min_baseq) {
+            const uint32_t code = (k & 1u) ? (seq[k >> 1] & 15u) : (uint32_t)(seq[k >> 1] >> 4);
+            v = code == 1u ? 0u : code == 2u ? 1u : code == 4u ? 2u : code == 8u ? 3u : 4u;
+        }
+        {
+            const uint32_t bit = 96u + 3u * k;
+            out[bit >> 3] |= (uint8_t)(v << (bit & 7u));
+            if ((bit & 7u) > 5u) out[(bit >> 3) + 1] |= (uint8_t)(v >> (8u - (bit & 7u)));
+        }
     }
     out[31] = (uint8_t)(int8_t)min_baseq;
     return 1;
 }
 
 /* Expand a 32-byte record into the full layout in full[0..128): a counted base
- * becomes its code with quality 127, an uncounted one N with quality 0 (the same
- * pileup under the record's min_baseq). */
+ * becomes its code with quality 127, any other N with quality 0 (the same pileup
+ * under the record's thresholds). */
 static inline MGP_HD void mgp_unpack32_record(const uint8_t *p, uint8_t *full) {
     uint32_t k;
     const uint32_t lseq = p[2] <= MGP_PACK_MAX_LEN ? p[2] : MGP_PACK_MAX_LEN;
-    const uint32_t nc = (p[3] & 0x7Fu) <= 4u ? (p[3] & 0x7Fu) : 4u;
+    const uint32_t nc = (p[3] & 7u) <= 4u ? (p[3] & 7u) : 4u;
     const uint32_t coff = mgp_cigar_offset(lseq), soff = mgp_seq_offset(lseq);
     for (k = 0; k < 128u; ++k) full[k] = 0;
     full[0] = p[0];
@@ -307,8 +323,8 @@ static inline MGP_HD void mgp_unpack32_record(const uint8_t *p, uint8_t *full) {
         const uint32_t bit = 96u + 3u * k;
         const uint32_t w = (uint32_t)p[bit >> 3] | ((uint32_t)p[(bit >> 3) + 1] << 8);
         const uint32_t v = (w >> (bit & 7u)) & 7u;
-        const uint8_t code = (v & 4u) ? (uint8_t)(1u << (v & 3u)) : (uint8_t)15;
-        full[16 + k] = (v & 4u) ? (uint8_t)127 : (uint8_t)0;
+        const uint8_t code = v < 4u ? (uint8_t)(1u << v) : (uint8_t)15;
+        full[16 + k] = v < 4u ? (uint8_t)127 : (uint8_t)0;
         full[soff + (k >> 1)] |= (k & 1u) ? code : (uint8_t)(code << 4);
     }
 }
@@ -386,6 +402,7 @@ typedef struct mgp_synth_params {
     int32_t  cell_lo, cell_hi;
     int32_t  shard_rank, shard_world;
     int32_t  pack_min_baseq;    /* pack == 2: the min_baseq the 32-byte records are made for */
+    int32_t  pack_min_dist;     /* pack == 2: the min_dist_from_end they are made for (0..15) */
 } mgp_synth_params;
 
 /* The pileup's 16-bit result rows, as the run leaves them in HBM (half the bytes of

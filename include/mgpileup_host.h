@@ -68,9 +68,10 @@ int  mgp_bam_set_bulk(mgp_bam *bam, int32_t cell);
  * query_sequence/query_qualities (the SimpleRead API) leave it off (default). */
 int  mgp_bam_set_pack(mgp_bam *bam, int pack);
 /* 32-byte records (MGP_FLAG_PACK32, include/mgpileup.h) for reads that fit, made for
- * the run's min_baseq (in [-128, 127]); the others get the packed 64-byte or the full
- * layout. Turns packing on. The engine refuses them under another min_baseq. */
-int  mgp_bam_set_pack32(mgp_bam *bam, int on, int min_baseq);
+ * the run's min_baseq (in [-128, 127]) and min_dist_from_end (<= 15); the others get
+ * the packed 64-byte or the full layout. Turns packing on. The engine refuses them
+ * under other thresholds. */
+int  mgp_bam_set_pack32(mgp_bam *bam, int on, int min_baseq, int min_dist);
 
 /* Payload placement of mgp_bam_read_ref (MGP_PLACE_DENSE default, or
  * MGP_PLACE_PAIRED: see mgp_place_records below). */

@@ -79,7 +79,7 @@ def host_library() -> C.CDLL:
         lib.mgp_bam_set_barcodes.argtypes = [vp, C.c_char_p, C.POINTER(C.c_char_p), C.c_int]
         lib.mgp_bam_set_bulk.argtypes = [vp, C.c_int32]
         lib.mgp_bam_set_pack.argtypes = [vp, C.c_int]
-        lib.mgp_bam_set_pack32.argtypes = [vp, C.c_int, C.c_int]
+        lib.mgp_bam_set_pack32.argtypes = [vp, C.c_int, C.c_int, C.c_int]
         lib.mgp_bam_set_placement.argtypes = [vp, C.c_int]
         lib.mgp_bam_read_ref.argtypes = [vp, C.c_int, C.c_int, C.POINTER(mgp_bam_batch)]
         lib.mgp_bam_free_batch.argtypes = [C.POINTER(mgp_bam_batch)]
@@ -200,7 +200,7 @@ class BamFile:
 
     def read_soa(self, contig: str, barcodes: list[str], tag: str = "CB", rec_align: int = 64,
                  bulk_cell: int = -1, pack: bool = True, paired: bool | None = None,
-                 pack32: int | None = None) -> ReadSoA:
+                 pack32: int | None = None, pack32_dist: int = 5) -> ReadSoA:
         """Every record of `contig` (fetch order) as an engine batch; bc = whitelist
         index (last duplicate wins, like the reference's dict) or -1. With
         ``bulk_cell >= 0`` every record goes to that cell (bulk calling). pack:
@@ -210,7 +210,8 @@ class BamFile:
         128-byte line (mgp_place_records), so the pileup's gather fetches half the
         lines; the records are then not in BAM order in the payload. pack32 (the
         run's min_baseq): reads that fit get the 32-byte record made for that
-        threshold (four to a line when paired) before the 64-byte one."""
+        threshold and min_dist_from_end pack32_dist (four to a line when paired)
+        before the 64-byte one."""
         paired = pack if paired is None else paired
         arr = (C.c_char_p * max(1, len(barcodes)))(*[b.encode() for b in barcodes])
         if self.lib.mgp_bam_set_barcodes(self._h, tag.encode(), arr, len(barcodes)) != 0:
@@ -219,7 +220,7 @@ class BamFile:
             raise ProcessingError(_err())
         if self.lib.mgp_bam_set_pack(self._h, int(bool(pack))) != 0:
             raise ProcessingError(_err())
-        if self.lib.mgp_bam_set_pack32(self._h, int(pack32 is not None), int(pack32 or 0)) != 0:
+        if self.lib.mgp_bam_set_pack32(self._h, int(pack32 is not None), int(pack32 or 0), int(pack32_dist)) != 0:
             raise ProcessingError(_err())
         if self.lib.mgp_bam_set_placement(self._h, PLACE_PAIRED if paired else PLACE_DENSE) != 0:
             raise ProcessingError(_err())

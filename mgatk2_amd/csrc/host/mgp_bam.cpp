@@ -133,6 +133,7 @@ struct mgp_bam {
     bool pack = false;       // write the packed record layout where a read fits
     bool pack32 = false;     // ... the 32-byte layout first, made for pack32_minq (mgp_bam_set_pack32)
     int pack32_minq = 0;
+    int pack32_dist = 5;
     int placement = MGP_PLACE_DENSE;  // payload placement (mgp_place_records)
 };
 
@@ -680,11 +681,13 @@ int mgp_bam_set_pack(mgp_bam* b, int pack) {
     return 0;
 }
 
-int mgp_bam_set_pack32(mgp_bam* b, int on, int min_baseq) {
+int mgp_bam_set_pack32(mgp_bam* b, int on, int min_baseq, int min_dist) {
     if (!b) return fail("null argument");
-    if (on && (min_baseq < -128 || min_baseq > 127)) return fail("32-byte records need min_baseq in [-128, 127]");
+    if (on && (min_baseq < -128 || min_baseq > 127 || min_dist > 15))
+        return fail("32-byte records need min_baseq in [-128, 127] and min_dist_from_end <= 15");
     b->pack32 = on != 0;
     b->pack32_minq = min_baseq;
+    b->pack32_dist = min_dist;
     if (b->pack32) b->pack = true;
     return 0;
 }
@@ -811,7 +814,7 @@ int mgp_bam_read_ref(mgp_bam* b, int tid, int rec_align, mgp_bam_batch* out) {
             for (uint32_t q = 0; q < n_cig; ++q) cw[q] = rd32(cig + 4 * q);
             const uint64_t size = ((uint64_t)MGP_PACK32_BYTES + amask) & ~amask;
             if (size > MGP_PACK32_BYTES && !paired) std::memset(rec + MGP_PACK32_BYTES, 0, size - MGP_PACK32_BYTES);
-            mgp_pack32_record(pos, l_seq, fl, n_cig, cw, seqp, qualp, b->pack32_minq, rec);  // writes all 32 bytes
+            mgp_pack32_record(pos, l_seq, fl, n_cig, cw, seqp, qualp, b->pack32_minq, b->pack32_dist, rec);  // all 32 B
         } else if (pk) {
             uint32_t cw[4] = {0, 0, 0, 0};
             for (uint32_t q = 0; q < n_cig; ++q) cw[q] = rd32(cig + 4 * q);

@@ -1277,22 +1277,39 @@ struct Win {
     int w0, wlen, Wp;
 };
 
-// LDS tile: position-major base counts tile[pos * 4 + base] (A, C, G, T), then a
-// Tn5 plane of Wp u32 at tile + 4 Wp; every u32 packs the forward count in its low
-// 16 bits and the reverse count in its high 16 bits (a window is processed in
-// segments of < 65536 reads, so no half can carry). Position-major makes a
-// count's LDS address one shift-add of the base index onto the read's row, with
-// the query offset in the instruction's immediate; a flush reads a position's 4
-// bases with one 16-byte load.
+// LDS tile, plane-major: planes 0..3 count A, C, G, T, plane 4 is a trash plane
+// (never read: where the 32-byte path adds the bases it does not count), plane 5
+// counts Tn5 cuts; every u32 packs the forward count in its low 16 bits and the
+// reverse count in its high 16 bits (a window is processed in segments of < 65536
+// reads, so no half can carry). A plane is kTilePitch words: kTileGuard guard words,
+// the window's positions, guard words (never read either: positions just outside
+// the window). The pointer the pile functions get is position 0 of plane 0. A
+// count's address is the read's row + plane x plane stride + the query offset (in
+// the instruction's immediate). Plane-major puts consecutive positions in
+// consecutive banks: the reads of a wave, a few dozen consecutive starts apart, add
+// to distinct banks (position-major 16-byte rows spread only position mod 8 over
+// the banks: 4-way conflicts on every add, profiles/r03).
+constexpr int kTileGuard = 64;
+constexpr int kPlaneTrash = 4, kPlaneTn5 = 5, kTilePlanes = 6;
+#ifndef MGP_WIN
+#define MGP_WIN 1280  // target window width (positions); W <= kMaxPosPerThread * 256 (A/B: 768-2048)
+#endif
+constexpr int kMaxPosPerThread = MGP_WIN / 256;
+// words per plane: guards + the window (>= W) + MGP_TILE_PAD
+#ifndef MGP_TILE_PAD
+#define MGP_TILE_PAD 0
+#endif
+constexpr int kTilePitch = MGP_WIN + 2 * kTileGuard + MGP_TILE_PAD;
+constexpr uint32_t kPlaneBytes = 4u * kTilePitch;
 __device__ __forceinline__ uint32_t strand_inc(int strand) { return strand ? 0x10000u : 1u; }
 
 __device__ __forceinline__ void tn5_cut(bool has, int32_t start, uint32_t lseq, int strand, const Win& w,
                                         uint32_t* t5) {
     // pileup.py:43-50: reverse reads cut at start + len(seq) - 1. Branch-free: a
-    // lane whose cut is elsewhere adds 0 to slot 0
+    // lane whose cut is elsewhere adds 0 to a guard word of its own
     const int64_t cut = strand ? (int64_t)start + lseq - 1 : (int64_t)start;
     const bool in = has && cut >= w.w0 && cut < (int64_t)w.w0 + w.wlen;
-    atomicAdd(&t5[in ? (int)(cut - w.w0) : 0], in ? strand_inc(strand) : 0u);
+    atomicAdd(&t5[in ? (int)(cut - w.w0) : -1 - (int)(threadIdx.x & 63)], in ? strand_inc(strand) : 0u);
 }
 
 // Generic path (any read): CIGAR walk with byte loads (pileup.py:55-95).
@@ -1321,7 +1338,7 @@ __device__ bool pile_slow(const uint8_t* __restrict__ rec, int32_t start, uint32
                 const uint8_t sb = seq[qq >> 1];
                 const int bi = base_index((qq & 1) ? (sb & 15u) : (sb >> 4));
                 if (bi < 0) continue;
-                atomicAdd(&tile[(int)(ref + k - w.w0) * 4 + bi], inc);
+                atomicAdd(&tile[bi * kTilePitch + (int)(ref + k - w.w0)], inc);
             }
             q += len;
             ref += len;
@@ -1334,11 +1351,6 @@ __device__ bool pile_slow(const uint8_t* __restrict__ rec, int32_t start, uint32
     return max(ref - (int64_t)start, (int64_t)lseq) > (int64_t)max_span;
 }
 
-#ifndef MGP_WIN
-#define MGP_WIN 1280  // target window width (positions); W <= kMaxPosPerThread * 256 (A/B: 768-2048)
-#endif
-constexpr int kMaxPosPerThread = MGP_WIN / 256;
-constexpr int kTilePitch = MGP_WIN;  // positions per tile (>= the window width W)
 constexpr int kFastLen = 64;   // reads up to 64 bases with <= 4 CIGAR ops and <= 2 aligned blocks
 constexpr int kFastCig = 4;
 constexpr uint32_t kValid = 0x0116u;   // codes 1, 2, 4, 8 are counted (pileup.py:83-86)
@@ -1461,13 +1473,13 @@ __device__ __forceinline__ void pile_bases(bool act, int a0, int b0, int a1, int
         }
     }
     const uint32_t sw[8] = {R.sv[0].x, R.sv[0].y, R.sv[0].z, R.sv[0].w, R.sv[1].x, R.sv[1].y, R.sv[1].z, R.sv[1].w};
-    // one count at rowp[4 qq] when ok, branch-free: a lane that does not count
-    // adds 0 at its own slot + 4 qq (tile rows 0..80, inside the tile), so 16 qq bytes
-    // become the atomic's immediate offset and the row select is one pointer select
-    uint32_t* const own = tile + (threadIdx.x & 63);
+    // one count at rowp[qq] when ok, branch-free: a lane that does not count adds at
+    // its own word + qq of the trash plane, so 4 qq bytes become the atomic's
+    // immediate offset and the row select is one pointer select
+    uint32_t* const own = tile + kPlaneTrash * kTilePitch + (threadIdx.x & 63);
     auto count_q = [&](uint32_t ok, uint32_t* rowp, int qq) {
         uint32_t* const p = ok ? rowp : own;
-        atomicAdd(p + 4 * qq, ok ? inc : 0u);
+        atomicAdd(p + qq, inc);
     };
     const int minbq = pc.min_baseq;
     // packed: counted iff qual << 2 | b lies in [4 * max(min_baseq, 0), 252) (0xFF and
@@ -1530,14 +1542,13 @@ __device__ __forceinline__ void pile_bases(bool act, int a0, int b0, int a1, int
         }
     };
     // LDS rows of the read's blocks (u32 index of query offset 0)
-    const int r0 = 4 * (dl0 - w.w0), r1 = 4 * (dl1 - w.w0);
-    uint32_t* const r0p = tile + r0;
-    uint32_t* const r1p = tile + r1;
+    uint32_t* const r0p = tile + (dl0 - w.w0);
+    uint32_t* const r1p = tile + (dl1 - w.w0);
     if (uniform) {
         run(ua0, ub0, [&](int qq) {
             uint32_t plane;
             const uint32_t ok = decode(qq, plane);
-            count_q(ok, r0p + plane, qq);
+            count_q(ok, r0p + plane * kTilePitch, qq);
         });
     } else {
         // the lane's counted query positions as a 64-bit mask: one bit test per base
@@ -1548,7 +1559,7 @@ __device__ __forceinline__ void pile_bases(bool act, int a0, int b0, int a1, int
             run(wq_lo, wq_hi, [&](int qq) {
                 uint32_t plane;
                 const uint32_t ok = decode(qq, plane) & counted(qq);
-                count_q(ok, r0p + plane, qq);
+                count_q(ok, r0p + plane * kTilePitch, qq);
             });
         } else {
             run(wq_lo, wq_hi, [&](int qq) {
@@ -1556,7 +1567,7 @@ __device__ __forceinline__ void pile_bases(bool act, int a0, int b0, int a1, int
                 uint32_t* const rowp = qq >= qs1 ? r1p : r0p;
                 uint32_t plane;
                 const uint32_t ok = decode(qq, plane) & counted(qq);
-                count_q(ok, rowp + plane, qq);
+                count_q(ok, rowp + plane * kTilePitch, qq);
             });
         }
     }
@@ -1570,10 +1581,6 @@ __device__ __forceinline__ uint32_t lds_addr(uint32_t* p) { return (uint32_t)(ui
 __device__ __forceinline__ void lds_add(uint32_t addr, uint32_t v) {
     __hip_atomic_fetch_add((lds_u32*)(uintptr_t)addr, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
-// Where a lane that does not count a base adds: a per-lane word plus the query
-// offset (16 bytes per position), never read. Shared by the waves of a workgroup.
-constexpr int kOwnWords = kWave + 4 * kWave;
-__shared__ uint32_t g_own[kOwnWords];
 
 // The counted bases of the packed register-path reads of a wave. The record's
 // base bytes (qual << 2 | b at +14) outside the lane's counted ranges [a_k, b_k)
@@ -1629,14 +1636,14 @@ __device__ __forceinline__ void pile_bases_packed(bool act, int a0, int b0, int 
     // counted iff qual << 2 | b lies in [4 * max(min_baseq, 0), 252)
     const uint32_t lo4 = 4u * (uint32_t)min(max(pc.min_baseq, 0), 63);
     const uint32_t span4 = 252u - lo4;
-    const uint32_t own = lds_addr(g_own) + 4u * (threadIdx.x & 63);
     const uint32_t tb = lds_addr(tile);
-    // rows: byte address of query offset 0 of each block (16 bytes per position)
-    const uint32_t r0 = tb + 16u * (uint32_t)(dl0 - w.w0), r1 = tb + 16u * (uint32_t)(dl1 - w.w0);
+    const uint32_t own = tb + kPlaneTrash * kPlaneBytes + 4u * (threadIdx.x & 63);  // (trash plane)
+    // rows: byte address of query offset 0 of each block (4 bytes per position)
+    const uint32_t r0 = tb + 4u * (uint32_t)(dl0 - w.w0), r1 = tb + 4u * (uint32_t)(dl1 - w.w0);
     auto count = [&](int qq, uint32_t row) {
         const uint32_t x = (qw[(14 + qq) >> 2] >> (8 * ((14 + qq) & 3))) & 0xFFu;
-        const uint32_t a = row | ((x & 3u) << 2);
-        lds_add((x - lo4 < span4 ? a : own) + 16u * (uint32_t)qq, inc);
+        const uint32_t a = row + (x & 3u) * kPlaneBytes;
+        lds_add((x - lo4 < span4 ? a : own) + 4u * (uint32_t)qq, inc);
     };
     const bool two = __ballot(act && a1 < b1) != 0ull;
     // the wave's range [wq_lo, wq_hi): the core [kC0, kC1) without a test when
@@ -1667,51 +1674,51 @@ __device__ __forceinline__ void pile_bases_packed(bool act, int a0, int b0, int 
     else run([&](int qq) { count(qq, r0); });
 }
 
-// The counted bases of the 32-byte register-path reads of a wave. Code k of a
-// record (bit 96 + 3k: counted << 2 | b) is taken with a static shift (a funnel
-// shift where it straddles two words); a base counts iff its counted bit is set
-// and k lies in the lane's ranges [a_k, b_k) (not tested when every lane of the
-// wave has the same single range, which the loop bounds then are). The count's
-// address is the block's row | plane * 4, or the lane's own scratch word.
+// The counted bases of the 32-byte register-path reads of a wave. A record's codes
+// already say which query positions count (include/mgpileup.h: 0..3 the counted
+// base, 4 not counted), so a base is its 3-bit code (a static bit-field extract, a
+// funnel shift where it straddles two words) and one LDS add at the block's row +
+// code x plane stride + the query offset: code 4 adds to the trash plane. The loop
+// runs over the wave's counted query range [min a_k, max b_k); a lane's positions
+// there outside the window land in the tile's guard words (never read) when every
+// row of the wave stays within kTileGuard positions of the window, else each base
+// is tested. Lanes without a register-path read add all-4 codes (the trash plane).
 __device__ __forceinline__ void pile_bases_p32(bool act, int a0, int b0, int a1, int b1, int qs1, int dl0, int dl1,
                                                const RecLine& R, const Win& w, uint32_t* tile, uint32_t inc) {
     constexpr int kLen = MGP_PACK_MAX_LEN;
-    auto range_mask = [](int lo, int hi) -> unsigned long long {
-        lo = min(max(lo, 0), 64);
-        hi = min(max(hi, 0), 64);
-        const unsigned long long h = hi >= 64 ? ~0ull : ((1ull << hi) - 1ull);
-        const unsigned long long l = lo >= 64 ? ~0ull : ((1ull << lo) - 1ull);
-        return lo < hi ? (h & ~l) : 0ull;
-    };
-    const unsigned long long vm = act ? (range_mask(a0, b0) | range_mask(a1, b1)) : 0ull;
     int qlo = 1 << 30, qhi = 0;
-    if (vm) {
-        qlo = __builtin_ctzll(vm);
-        qhi = 64 - __builtin_clzll(vm);
+    if (act && a0 < b0) {
+        qlo = a0;
+        qhi = b0;
+    }
+    if (act && a1 < b1) {
+        qlo = min(qlo, a1);
+        qhi = max(qhi, b1);
     }
     const int wq_lo = __builtin_amdgcn_readfirstlane(wave_min(qlo));
     const int wq_hi = __builtin_amdgcn_readfirstlane(wave_max(qhi));
     if (wq_lo >= wq_hi) return;
-    const uint32_t cw[6] = {R.h.w, R.qv[0].x, R.qv[0].y, R.qv[0].z, R.qv[0].w, 0u};
-    const uint32_t vlo = (uint32_t)vm, vhi = (uint32_t)(vm >> 32);
-    const uint32_t own = lds_addr(g_own) + 4u * (threadIdx.x & 63);
+    // a lane counting nothing in the window takes code 4 in every 3-bit field (word
+    // by word: fields straddle words) at a row of its own, so such lanes add to
+    // distinct trash words (one shared word would serialize their atomics)
+    const bool live = qlo < qhi;
+    constexpr uint32_t kAll4[5] = {0x24924924u, 0x49249249u, 0x92492492u, 0x24924924u, 0x49249249u};
+    const uint32_t cw[6] = {live ? R.h.w : kAll4[0], live ? R.qv[0].x : kAll4[1], live ? R.qv[0].y : kAll4[2],
+                            live ? R.qv[0].z : kAll4[3], live ? R.qv[0].w : kAll4[4], 0u};
+    // row offsets (window positions of query offset 0): block 1 from qs1 on (a lane
+    // with one block has qs1 past the read)
+    const bool two = __ballot(live && qs1 < kLen) != 0ull;
+    const int e0 = live ? dl0 - w.w0 : (int)(threadIdx.x & 63);
+    const int e1 = live && qs1 < kLen ? dl1 - w.w0 : e0;
+    const int plo = min(e0, e1) + wq_lo, phi = max(e0, e1) + wq_hi - 1;
+    const bool guarded = __ballot(plo < -kTileGuard || phi >= kTilePitch - kTileGuard) == 0ull;
     const uint32_t tb = lds_addr(tile);
-    const uint32_t r0 = tb + 16u * (uint32_t)(dl0 - w.w0), r1 = tb + 16u * (uint32_t)(dl1 - w.w0);
-    const bool two = __ballot(act && a1 < b1) != 0ull;
-    // every lane the same single range: the loop bounds are the range (no per-base test)
-    const int ua0 = __builtin_amdgcn_readfirstlane(a0), ub0 = __builtin_amdgcn_readfirstlane(b0);
-    const bool uniform = !two && __ballot(!(act && a0 == ua0 && b0 == ub0)) == 0ull;
+    const uint32_t r0 = tb + 4u * (uint32_t)e0, r1 = tb + 4u * (uint32_t)e1;
     auto code = [&](int qq) -> uint32_t {
         const int bit = 3 * qq, j = bit >> 5, sh = bit & 31;
-        return (sh <= 29 ? (cw[j] >> sh) : __builtin_amdgcn_alignbit(cw[j + 1], cw[j], sh)) & 7u;
+        return sh <= 29 ? __builtin_amdgcn_ubfe(cw[j], sh, 3) : (__builtin_amdgcn_alignbit(cw[j + 1], cw[j], sh) & 7u);
     };
-    auto count = [&](int qq, uint32_t row, bool test) {
-        const uint32_t x = code(qq);
-        uint32_t ok = x >> 2;
-        if (test) ok &= ((qq < 32 ? vlo : vhi) >> (qq & 31)) & 1u;
-        lds_add((ok ? (row | ((x & 3u) << 2)) : own) + 16u * (uint32_t)qq, inc);
-    };
-    const unsigned long long smask = range_mask(wq_lo, wq_hi);
+    const unsigned long long smask = (wq_hi >= 64 ? ~0ull : ((1ull << wq_hi) - 1ull)) & ~((1ull << wq_lo) - 1ull);
     constexpr int kC0 = 5, kC1 = kLen - 5;
     auto run = [&](auto&& body) {
         if (wq_lo <= kC0 && wq_hi >= kC1) {
@@ -1733,9 +1740,17 @@ __device__ __forceinline__ void pile_bases_p32(bool act, int a0, int b0, int a1,
                 if ((smask >> qq) & 1ull) body(qq);
         }
     };
-    if (uniform) run([&](int qq) { count(qq, r0, false); });
-    else if (two) run([&](int qq) { count(qq, qq >= qs1 ? r1 : r0, true); });
-    else run([&](int qq) { count(qq, r0, true); });
+    if (guarded) {
+        if (two) run([&](int qq) { lds_add((qq >= qs1 ? r1 : r0) + code(qq) * kPlaneBytes + 4u * (uint32_t)qq, inc); });
+        else run([&](int qq) { lds_add(r0 + code(qq) * kPlaneBytes + 4u * (uint32_t)qq, inc); });
+    } else {
+        const uint32_t own = tb + kPlaneTrash * kPlaneBytes + 4u * (threadIdx.x & 63);
+        run([&](int qq) {
+            const int p = (qq >= qs1 ? e1 : e0) + qq;
+            const bool in = (unsigned)p < (unsigned)w.wlen;
+            lds_add(in ? tb + code(qq) * kPlaneBytes + 4u * (uint32_t)p : own, inc);
+        });
+    }
 }
 
 __device__ __forceinline__ void pile_line(bool has, int lay, const uint8_t* __restrict__ rec, const RecLine& R,
@@ -1747,7 +1762,7 @@ __device__ __forceinline__ void pile_line(bool has, int lay, const uint8_t* __re
     // header fields of the three layouts (include/mgpileup.h)
     const int32_t start = p32 ? (int32_t)(h.x & 0xFFFFu) : (int32_t)h.x;
     const uint32_t lseq = p32 ? ((h.x >> 16) & 0xFFu) : packed ? (h.y & 0xFFu) : h.y;
-    const uint32_t ncig = p32 ? ((h.x >> 24) & 0x7Fu) : packed ? ((h.y >> 8) & 0x7Fu) : (h.z & 0xFFFFu);
+    const uint32_t ncig = p32 ? ((h.x >> 24) & 7u) : packed ? ((h.y >> 8) & 0x7Fu) : (h.z & 0xFFFFu);
     const uint32_t coff = h.w;
     const int strand = p32 ? (int)(h.x >> 31) : packed ? (int)((h.y >> 15) & 1u)
                                                      : (((h.z >> 16) & MGP_FLAG_REVERSE) ? 1 : 0);
@@ -1755,8 +1770,10 @@ __device__ __forceinline__ void pile_line(bool has, int lay, const uint8_t* __re
                               p32 ? (h.y >> 16) : packed ? (h.z & 0xFFFFu) : cv.y,
                               p32 ? (h.z & 0xFFFFu) : packed ? (h.z >> 16) : cv.z,
                               p32 ? (h.z >> 16) : packed ? (h.w & 0xFFFFu) : cv.w};
-    // a 32-byte record's counted bits were made for one min_baseq (byte 31)
-    if (has && p32 && (int)(int8_t)(R.qv[0].w >> 24) != pc.min_baseq) pk_err = true;
+    // a 32-byte record's codes were made for one (min_baseq, min_dist) pair (bytes 31, 3)
+    if (has && p32 &&
+        ((int)(int8_t)(R.qv[0].w >> 24) != pc.min_baseq || (int)((h.x >> 27) & 15u) != max(pc.min_dist, 0)))
+        pk_err = true;
     tn5_cut(has, start, lseq, strand, w, t5);
 
     bool fast = has && lseq <= (uint32_t)(packed ? MGP_PACK_MAX_LEN : kFastLen) && ncig <= (uint32_t)kFastCig &&
@@ -1829,6 +1846,9 @@ __device__ __forceinline__ void pile_line(bool has, int lay, const uint8_t* __re
     span_err = span_err || se;
 }
 
+#ifndef MGP_LANE_PERM
+#define MGP_LANE_PERM 1
+#endif
 #ifndef MGP_STREAM_U
 #define MGP_STREAM_U 2
 #endif
@@ -1903,8 +1923,10 @@ __global__ void __launch_bounds__(kBlock, MGP_PILEUP_WAVES) k_pileup(
     uint32_t* __restrict__ covered, unsigned long long* __restrict__ dsum,
     uint32_t* __restrict__ dmax, uint32_t* __restrict__ tally_part, DevStats* st, int w_base,
     const uint32_t* __restrict__ ck) {
-    extern __shared__ __align__(16) uint32_t tile[];  // [Wp][4] A, C, G, T, then [Wp] Tn5 (fwd | rev << 16)
-    uint32_t* t5 = tile + 4 * g.Wp;
+    // the tile: kTilePlanes planes of kTilePitch words (A, C, G, T, trash, Tn5; fwd | rev << 16)
+    extern __shared__ __align__(16) uint32_t tile_planes[];
+    uint32_t* const tile = tile_planes + kTileGuard;  // position 0 of plane 0
+    uint32_t* const t5 = tile + kPlaneTn5 * kTilePitch;
     if (__atomic_load_n(&st->err, __ATOMIC_RELAXED) & ERR_BOUNDS) return;  // unsorted input (k_bin_count)
     __shared__ uint32_t wq_all[kBlock / kWave][kWaveQ];
     __shared__ uint32_t r_cov[4], r_max[4], r_keep[4];
@@ -1922,6 +1944,10 @@ __global__ void __launch_bounds__(kBlock, MGP_PILEUP_WAVES) k_pileup(
     const int L = g.L;
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     uint32_t* wq = wq_all[wid];
+    // the queued read a lane piles: even queue slots in lanes 0..31, odd in 32..63. The
+    // queue is in coordinate order and LDS atomics conflict per 32-lane half, so
+    // reads with the same start (same count address) are split over the halves.
+    const uint32_t qlane = MGP_LANE_PERM ? (uint32_t)(((lane & 31) << 1) | (lane >> 5)) : (uint32_t)lane;
     const uint32_t max_span = st->max_span;
     const int R = (int)((max_span + g.G - 1) / g.G) * g.G;
     const int lo_bin = win_lo_bin(k, R, g);
@@ -1945,7 +1971,7 @@ __global__ void __launch_bounds__(kBlock, MGP_PILEUP_WAVES) k_pileup(
     uint32_t n_hi = c0 < c1 ? O[(size_t)hi_bin * nc + c0] : 0u;
     // the tile starts zeroed; each flush zeroes what it read, so the next cell
     // starts from zero behind the flush's barrier
-    for (int x = threadIdx.x; x < 5 * g.Wp; x += blockDim.x) tile[x] = 0;
+    for (int x = threadIdx.x; x < kTilePlanes * kTilePitch; x += blockDim.x) tile_planes[x] = 0;
     __syncthreads();
     for (int c = c0; c < c1; ++c) {
         const uint32_t lo = n_lo, own = n_own, hi = n_hi;
@@ -1993,7 +2019,7 @@ __global__ void __launch_bounds__(kBlock, MGP_PILEUP_WAVES) k_pileup(
                 }
                 __builtin_amdgcn_wave_barrier();
                 while (qn >= (uint32_t)kWave) {
-                    const uint32_t qe = wq[(qh + lane) & (kWaveQ - 1)];
+                    const uint32_t qe = wq[(qh + qlane) & (kWaveQ - 1)];
                     qh += kWave;
                     qn -= kWave;
                     if constexpr (kPacked && MGP_PILE_PREFETCH) {
@@ -2009,8 +2035,8 @@ __global__ void __launch_bounds__(kBlock, MGP_PILEUP_WAVES) k_pileup(
                 }
             }
             {   // tail: every lane of the wave enters, lanes past qn hold no read
-                const bool has = (uint32_t)lane < qn;
-                const uint32_t qe = has ? wq[(qh + lane) & (kWaveQ - 1)] : 0u;
+                const bool has = qlane < qn;
+                const uint32_t qe = has ? wq[(qh + qlane) & (kWaveQ - 1)] : 0u;
                 if constexpr (kPacked && MGP_PILE_PREFETCH) {
                     RecLine Rn;
                     load_line(has, kLayout, payload + rec_at(qe, unit, pe_off), w, Rn);
@@ -2030,15 +2056,16 @@ __global__ void __launch_bounds__(kBlock, MGP_PILEUP_WAVES) k_pileup(
                     uint4 a = seg == lo ? make_uint4(0, 0, 0, 0) : cp[0];
                     uint4 b = seg == lo ? make_uint4(0, 0, 0, 0) : cp[1];
                     uint2 t = seg == lo ? make_uint2(0, 0) : reinterpret_cast<uint2*>(tn5)[P];
-                    const uint4 xb = reinterpret_cast<const uint4*>(tile)[p];
-                    const uint32_t x0 = xb.x, x1 = xb.y, x2 = xb.z, x3 = xb.w, x4 = t5[p];
+                    const uint32_t x0 = tile[p], x1 = tile[kTilePitch + p], x2 = tile[2 * kTilePitch + p],
+                                   x3 = tile[3 * kTilePitch + p], x4 = t5[p];
                     a.x += x0 & 0xFFFFu; a.y += x0 >> 16; a.z += x1 & 0xFFFFu; a.w += x1 >> 16;
                     b.x += x2 & 0xFFFFu; b.y += x2 >> 16; b.z += x3 & 0xFFFFu; b.w += x3 >> 16;
                     t.x += x4 & 0xFFFFu; t.y += x4 >> 16;
                     cp[0] = a;
                     cp[1] = b;
                     reinterpret_cast<uint2*>(tn5)[P] = t;
-                    reinterpret_cast<uint4*>(tile)[p] = make_uint4(0, 0, 0, 0);
+#pragma unroll
+                    for (int b = 0; b < 4; ++b) tile[b * kTilePitch + p] = 0;
                     t5[p] = 0;
                 }
                 __syncthreads();
@@ -2064,14 +2091,10 @@ __global__ void __launch_bounds__(kBlock, MGP_PILEUP_WAVES) k_pileup(
                     tf = t.x;
                     tr = t.y;
                 } else {
-                    const uint4 xb = reinterpret_cast<const uint4*>(tile)[p];
-                    reinterpret_cast<uint4*>(tile)[p] = make_uint4(0, 0, 0, 0);
-                    pk4[0] = xb.x;
-                    pk4[1] = xb.y;
-                    pk4[2] = xb.z;
-                    pk4[3] = xb.w;
 #pragma unroll
                     for (int x = 0; x < 4; ++x) {
+                        pk4[x] = tile[x * kTilePitch + p];
+                        tile[x * kTilePitch + p] = 0u;
                         v[2 * x] = pk4[x] & 0xFFFFu;
                         v[2 * x + 1] = pk4[x] >> 16;
                     }
@@ -3097,7 +3120,7 @@ static int run_segment(mgp_ctx* ctx, const Seg& sg, int slot, int& dup_parts, in
     pc.keep_tn5 = (ctx->cfg.flags & MGP_CFG_KEEP_TN5) != 0;
     if (sg.w1 > sg.w0) {
         dim3 gp(g.nchunks, sg.w1 - sg.w0);
-        const size_t psm = (size_t)5 * g.Wp * 4;
+        const size_t psm = (size_t)kTilePlanes * kTilePitch * 4;
         auto pile_kern = layout == kLayP32 ? k_pileup<kLayP32> : layout == kLayP64 ? k_pileup<kLayP64>
                                                                                     : k_pileup<kLayAny>;
         pile_kern<<<gp, kBlock, psm, s>>>(g, pc, ctx->payload.as<uint8_t>(), ctx->pel.as<uint32_t>(), unit, pe_off,
@@ -3456,7 +3479,7 @@ int mgp_synth_fill(void* stream, uint64_t seed, int64_t n, int read_len, int n_c
                    const uint32_t* d_cdf, const uint8_t* d_ref, int32_t* start, int32_t* bc, int32_t* tlen,
                    uint16_t* flag, uint8_t* mapq, uint32_t* span, uint64_t* roff, uint8_t* payload,
                    int64_t* payload_bytes, int rec_align, int pack, int placed, int cell_lo, int cell_hi,
-                   int shard_rank, int shard_world, uint64_t* d_map, int64_t* n_out, int p32_minq);
+                   int shard_rank, int shard_world, uint64_t* d_map, int64_t* n_out, int p32_minq, int p32_dist);
 
 int mgp_synth_generate(mgp_ctx* ctx, const mgp_synth_params* p) {
     if (!ctx || !p || !p->cell_cdf || !p->ref_codes) return set_err(MGP_E_INVALID, "null synth args");
@@ -3488,8 +3511,10 @@ int mgp_synth_generate(mgp_ctx* ctx, const mgp_synth_params* p) {
     // bytes the generator writes per record: a packed record (read_len <= MGP_PACK_MAX_LEN),
     // else the full layout of up to 3 CIGAR operations, at the placement's alignment
     const int64_t max_rec = ((int64_t)mgp_cigar_offset((uint32_t)p->read_len) + 16 + align - 1) & ~(int64_t)(align - 1);
-    if (p->pack < 0 || p->pack > 2 || (p->pack == 2 && (p->pack_min_baseq < -128 || p->pack_min_baseq > 127)))
-        return set_err(MGP_E_INVALID, "synth pack must be 0, 1 or 2 (32-byte records for a min_baseq in [-128, 127])");
+    if (p->pack < 0 || p->pack > 2 ||
+        (p->pack == 2 && (p->pack_min_baseq < -128 || p->pack_min_baseq > 127 || p->pack_min_dist > 15)))
+        return set_err(MGP_E_INVALID, "synth pack must be 0, 1 or 2 (32-byte records for a min_baseq in [-128, 127] "
+                                      "and a min_dist_from_end <= 15)");
     const bool packed = p->pack && p->read_len <= MGP_PACK_MAX_LEN;
     const int64_t rec_bytes = packed ? (int64_t)(p->pack == 2 ? MGP_PACK32_BYTES : MGP_PACK_BYTES) : max_rec;
     const bool placed = p->rec_off != nullptr;
@@ -3509,7 +3534,7 @@ int mgp_synth_generate(mgp_ctx* ctx, const mgp_synth_params* p) {
         r = mgp_synth_fill(s, p->seed, n, p->read_len, nc, L, cdf.as<uint32_t>(), ref.as<uint8_t>(), nullptr,
                            nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, &pay, align, p->pack, -1,
                            p->cell_lo, p->cell_hi, p->shard_rank, p->shard_world, map.as<uint64_t>(), &n_out,
-                           p->pack_min_baseq);
+                           p->pack_min_baseq, p->pack_min_dist);
         if (r != MGP_OK) return set_err(r, "synth: keep scan failed");
         pay = placed ? p->payload_bytes : 0;
     }
@@ -3528,7 +3553,7 @@ int mgp_synth_generate(mgp_ctx* ctx, const mgp_synth_params* p) {
                        ctx->flag.as<uint16_t>(), ctx->mapq.as<uint8_t>(), ctx->span.as<uint32_t>(),
                        ctx->roff.as<uint64_t>(), ctx->payload.as<uint8_t>(), &pay, align, p->pack, placed,
                        shard ? p->cell_lo : 0, shard ? p->cell_hi : 0, p->shard_rank, p->shard_world,
-                       map.as<uint64_t>(), &n_out, p->pack_min_baseq);
+                       map.as<uint64_t>(), &n_out, p->pack_min_baseq, p->pack_min_dist);
     if (r != MGP_OK) return r == MGP_E_INVALID ? set_err(r, "synth: invalid arguments") : set_err(r, "synth failed");
     HIP_TRY(hipStreamSynchronize(s));
     cdf.release();

@@ -235,7 +235,7 @@ __global__ void k_synth_fill(uint64_t seed, int64_t n, int rl, int nc, int L, co
                              const uint8_t* __restrict__ ref, int32_t* __restrict__ start, int32_t* __restrict__ bc,
                              int32_t* __restrict__ tlen, uint16_t* __restrict__ flag, uint8_t* __restrict__ mapq,
                              uint32_t* __restrict__ span, const uint64_t* __restrict__ roff,
-                             uint8_t* __restrict__ payload, int pack, int p32_minq, Filt flt) {
+                             uint8_t* __restrict__ payload, int pack, int p32_minq, int p32_dist, Filt flt) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const uint64_t spanpos = (uint64_t)(L - rl + 1);
@@ -294,7 +294,8 @@ __global__ void k_synth_fill(uint64_t seed, int64_t n, int rl, int nc, int L, co
     uint8_t* seq = rec + mgp_seq_offset((uint32_t)rl);
     uint32_t w32[8] = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u};  // a 32-byte record, written at the end
     if (p32) {  // 32-byte layout (include/mgpileup.h): header here, 3-bit codes per base below
-        w32[0] = (uint32_t)s0 | ((uint32_t)rl << 16) | ((uint32_t)(cg.n | (strand ? 0x80 : 0)) << 24);
+        const int md = p32_dist > 0 ? p32_dist : 0;
+        w32[0] = (uint32_t)s0 | ((uint32_t)rl << 16) | ((uint32_t)(cg.n | (md << 3) | (strand ? 0x80 : 0)) << 24);
         w32[1] = (cw[0] & 0xFFFFu) | ((cw[1] & 0xFFFFu) << 16);
         w32[2] = (cw[2] & 0xFFFFu);
         w32[7] = (uint32_t)(uint8_t)(int8_t)p32_minq << 24;
@@ -343,7 +344,13 @@ __global__ void k_synth_fill(uint64_t seed, int64_t n, int rl, int nc, int L, co
             else code = rc;
         }
         if (p32) {
-            const uint32_t v = code == 15 ? 0u : code_idx(code) | ((int)(int8_t)qv >= p32_minq ? 4u : 0u);
+            // counted (include/mgpileup.h): inside an aligned operation's query range (an
+            // insertion does not advance q: the last b positions of aM bI cM are outside),
+            // min_dist <= q < rl - min_dist, int8(qual) >= min_baseq, A/C/G/T
+            const int md = p32_dist > 0 ? p32_dist : 0;
+            const bool inblk = cg.cls == C_S ? q >= cg.a : cg.cls == C_I ? q < rl - cg.b : true;
+            const bool cnt = inblk && q >= md && q < rl - md && (int)(int8_t)qv >= p32_minq && code != 15;
+            const uint32_t v = cnt ? code_idx(code) : 4u;
             const int bit = 96 + 3 * q;
             w32[bit >> 5] |= v << (bit & 31);
             if ((bit & 31) > 29) w32[(bit >> 5) + 1] |= v >> (32 - (bit & 31));
@@ -359,6 +366,11 @@ __global__ void k_synth_fill(uint64_t seed, int64_t n, int rl, int nc, int L, co
     }
     if ((rl & 1) && !pk) seq[rl >> 1] = (uint8_t)(hi_nib << 4);
     if (p32) {
+        for (int q = rl; q < MGP_PACK_MAX_LEN; ++q) {  // never counted
+            const int bit = 96 + 3 * q;
+            w32[bit >> 5] |= 4u << (bit & 31);
+            if ((bit & 31) > 29) w32[(bit >> 5) + 1] |= 4u >> (32 - (bit & 31));
+        }
         uint4* r4 = reinterpret_cast<uint4*>(rec);
         r4[0] = make_uint4(w32[0], w32[1], w32[2], w32[3]);
         r4[1] = make_uint4(w32[4], w32[5], w32[6], w32[7]);
@@ -374,7 +386,7 @@ extern "C" int mgp_synth_fill(void* stream, uint64_t seed, int64_t n, int read_l
                               int32_t* tlen, uint16_t* flag, uint8_t* mapq, uint32_t* span, uint64_t* roff,
                               uint8_t* payload, int64_t* payload_bytes, int rec_align, int pack, int placed,
                               int cell_lo, int cell_hi, int shard_rank, int shard_world, uint64_t* d_map,
-                              int64_t* n_out, int p32_minq) {
+                              int64_t* n_out, int p32_minq, int p32_dist) {
     hipStream_t s = (hipStream_t)stream;
     if (read_len < 48) return MGP_E_INVALID;
     *n_out = n;
@@ -404,7 +416,7 @@ extern "C" int mgp_synth_fill(void* stream, uint64_t seed, int64_t n, int read_l
     }
     if (total && hipMemsetAsync(payload, 0, (size_t)total, s) != hipSuccess) return MGP_E_HIP;
     k_synth_fill<<<nb, kBlock, 0, s>>>(seed, n, read_len, n_cells, mito_len, d_cdf, d_ref, start, bc, tlen, flag,
-                                       mapq, span, roff, payload, pack, p32_minq, flt);
+                                       mapq, span, roff, payload, pack, p32_minq, p32_dist, flt);
     if (hipGetLastError() != hipSuccess) return MGP_E_HIP;
     if (hipStreamSynchronize(s) != hipSuccess) return MGP_E_HIP;
     *payload_bytes = (int64_t)total;

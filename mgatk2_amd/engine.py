@@ -128,6 +128,7 @@ class mgp_synth_params(C.Structure):
         ("shard_rank", C.c_int32),
         ("shard_world", C.c_int32),
         ("pack_min_baseq", C.c_int32),
+        ("pack_min_dist", C.c_int32),
     ]
 
 
@@ -372,7 +373,8 @@ class Engine:
 
     def synth(self, seed: int, n_reads: int, cdf: np.ndarray, ref: np.ndarray, read_len: int = 50,
               rec_align: int = 64, pack: bool = True, rec_off: np.ndarray | None = None, payload_bytes: int = 0,
-              cells: tuple[int, int] | None = None, shard: tuple[int, int] = (0, 0), pack32: int | None = None):
+              cells: tuple[int, int] | None = None, shard: tuple[int, int] = (0, 0), pack32: int | None = None,
+              pack32_dist: int = 5):
         """Device-side synthetic workload (replaces the resident set). rec_off: an
         explicit placement of the records (e.g. host placement of
         mgp_place_records, `synth.place_records`); None = dense in BAM order.
@@ -380,7 +382,8 @@ class Engine:
         (len(cdf) cells; this context's n_cells must be hi - lo), barcodes rebased to
         lo, plus the reads without a whitelisted barcode whose index % world == rank
         for shard=(rank, world) (world 0: none). pack32 (a min_baseq): 32-byte
-        records made for that threshold (MGP_FLAG_PACK32) instead of packed 64-byte ones."""
+        records made for that threshold and min_dist_from_end pack32_dist (MGP_FLAG_PACK32)
+        instead of packed 64-byte ones."""
         cdf = np.ascontiguousarray(cdf, np.uint32)
         ref = np.ascontiguousarray(ref, np.uint8)
         ro = None if rec_off is None else np.ascontiguousarray(rec_off, np.uint64)
@@ -390,7 +393,7 @@ class Engine:
         p = mgp_synth_params(int(seed), int(n_reads), int(read_len), int(cdf.shape[0]), _ptr(cdf), _ptr(ref),
                              int(rec_align), 2 if pack32 is not None else int(bool(pack)),
                              None if ro is None else _ptr(ro), int(payload_bytes) if ro is not None else 0, int(lo),
-                             int(hi), int(shard[0]), int(shard[1]), int(pack32 or 0))
+                             int(hi), int(shard[0]), int(shard[1]), int(pack32 or 0), int(pack32_dist))
         _ck(self.lib.mgp_synth_generate(self._h, C.byref(p)), "mgp_synth_generate")
 
     def download_inputs(self, columns: tuple[str, ...] | None = None, alloc=None) -> ReadSoA:

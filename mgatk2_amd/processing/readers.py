@@ -86,13 +86,15 @@ class BAMReader:
         min_baseq (four to a 128-byte line), the others the 64-byte or full one."""
         bulk = -1
         q = int(self.config.quality.min_baseq)
-        pack32 = q if pack and -128 <= q <= 127 else None
+        md = int(self.config.quality.min_distance_from_end)
+        pack32 = q if pack and -128 <= q <= 127 and md <= 15 else None
         if self.is_bulk_mode:
             bulk = max(i for i, b in enumerate(self.barcode_list) if b == "bulk")
         try:
             with self._open() as bam:
                 soa = bam.read_soa(self.config.mito_chr, self.barcode_list, tag=self.config.barcode_tag,
-                                   rec_align=rec_align, bulk_cell=bulk, pack=pack, pack32=pack32)
+                                   rec_align=rec_align, bulk_cell=bulk, pack=pack, pack32=pack32,
+                                   pack32_dist=int(self.config.quality.min_distance_from_end))
         except BAMReadError:
             raise
         except Exception as e:

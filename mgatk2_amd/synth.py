@@ -284,13 +284,13 @@ def pack_bytes(start, lseq, reverse, ncig, cig, qual, code) -> np.ndarray:
     return out
 
 
-def pack32_mask(start, flag, lseq, ncig, cig, min_baseq: int) -> np.ndarray:
-    """Which reads fit the 32-byte layout for this min_baseq (mgp_pack32_record)."""
+def pack32_mask(start, flag, lseq, ncig, cig, min_baseq: int, min_dist: int = 5) -> np.ndarray:
+    """Which reads fit the 32-byte layout for these thresholds (mgp_pack32_record)."""
     start = np.asarray(start, np.int64)
     lseq = np.asarray(lseq, np.int64)
     ncig = np.asarray(ncig, np.int64)
     ok = ((np.asarray(flag) & FLAG_NOSEQQUAL) == 0) & (lseq >= 1) & (lseq <= PACK_MAX_LEN) & (ncig <= 4)
-    ok &= (start >= 0) & (start < 65536) & (-128 <= int(min_baseq) <= 127)
+    ok &= (start >= 0) & (start < 65536) & (-128 <= int(min_baseq) <= 127) & (int(min_dist) <= 15)
     cig = np.asarray(cig, np.int64).reshape(start.shape[0], -1)
     used = np.arange(cig.shape[1])[None, :] < ncig[:, None]
     op = cig & 15
@@ -299,16 +299,38 @@ def pack32_mask(start, flag, lseq, ncig, cig, min_baseq: int) -> np.ndarray:
     return ok
 
 
-def pack32_bytes(start, lseq, reverse, ncig, cig, qual, code, min_baseq: int) -> np.ndarray:
+def _counted_positions(lseq, ncig, cig, n: int, min_dist: int) -> np.ndarray:
+    """[m, n] bool: query position k lies in an aligned operation's query range as the
+    reference walks the CIGAR (pileup.py:55-95: an insertion does not advance the
+    query position, quirk Q1) and min_dist <= k < l_seq - min_dist."""
+    lseq = np.asarray(lseq, np.int64).reshape(-1)
+    m = lseq.shape[0]
+    cig = np.asarray(cig, np.int64).reshape(m, -1)
+    ncig = np.asarray(ncig, np.int64).reshape(m)
+    k = np.arange(n)[None, :]
+    inblk = np.zeros((m, n), bool)
+    q = np.zeros(m, np.int64)
+    for j in range(cig.shape[1]):
+        live = ncig > j
+        op, ln = cig[:, j] & 15, cig[:, j] >> 4
+        aligned = live & ((op == 0) | (op == 7) | (op == 8))
+        inblk |= aligned[:, None] & (k >= q[:, None]) & (k < (q + ln)[:, None])
+        q = q + np.where(live & (aligned | (op == 4)), ln, 0)
+    md = max(int(min_dist), 0)
+    return inblk & (k < lseq[:, None]) & (k >= md) & (k < (lseq - md)[:, None])
+
+
+def pack32_bytes(start, lseq, reverse, ncig, cig, qual, code, min_baseq: int, min_dist: int = 5) -> np.ndarray:
     """32-byte records [m, 32] (include/mgpileup.h): u16 start, l_seq, n_cigar |
-    reverse << 7, CIGAR as u16, then a 3-bit code per base at bit 96 + 3k
-    (counted << 2 | b; counted = A/C/G/T with int8(qual) >= min_baseq), min_baseq
-    in byte 31."""
+    min_dist << 3 | reverse << 7, CIGAR as u16, then a 3-bit code per position at
+    bit 96 + 3k (0..3 = the counted base A, C, G, T; 4 = not counted), min_baseq in
+    byte 31."""
     m = np.asarray(start).shape[0]
+    md = max(int(min_dist), 0)
     out = np.zeros((m, PACK32_BYTES), np.uint8)
     out[:, 0:2] = np.asarray(start, "<u2").reshape(m, 1).view(np.uint8)
     out[:, 2] = np.asarray(lseq, np.uint8)
-    out[:, 3] = (np.asarray(ncig, np.uint8) | np.where(np.asarray(reverse), 0x80, 0)).astype(np.uint8)
+    out[:, 3] = (np.asarray(ncig, np.uint8) | (md << 3) | np.where(np.asarray(reverse), 0x80, 0)).astype(np.uint8)
     c16 = np.zeros((m, 4), "<u2")
     cig = np.asarray(cig, np.int64).reshape(m, -1)
     for k in range(min(4, cig.shape[1])):
@@ -319,10 +341,11 @@ def pack32_bytes(start, lseq, reverse, ncig, cig, qual, code, min_baseq: int) ->
     n = code.shape[1]
     b = np.select([code == 1, code == 2, code == 4, code == 8], [0, 1, 2, 3], -1)
     q8 = np.where(qual >= 128, qual - 256, qual)  # int8(qual): >= 128 wraps (pileup.py Q5)
-    v = np.where(b >= 0, np.maximum(b, 0) | np.where(q8 >= int(min_baseq), 4, 0), 0)
-    v = np.where(np.arange(n)[None, :] < np.asarray(lseq, np.int64).reshape(m, 1), v, 0).astype(np.uint64)
+    cnt = _counted_positions(lseq, ncig, cig, n, md) & (b >= 0) & (q8 >= int(min_baseq))
+    v = np.full((m, PACK_MAX_LEN), 4, np.uint64)
+    v[:, :n] = np.where(cnt, np.maximum(b, 0), 4).astype(np.uint64)
     bits = np.zeros((m, 4), np.uint64)  # bits 96..351 of the record, as 4 little-endian u64 words
-    for k in range(n):
+    for k in range(PACK_MAX_LEN):
         pos = 3 * k
         bits[:, pos >> 6] |= v[:, k] << np.uint64(pos & 63)
         if (pos & 63) > 61:
@@ -443,13 +466,14 @@ def _synth_chunk(seed, i0, i1, n, read_len, n_cells, mito_len, cdf, ref):
     )
 
 
-def _pack_fixed(start, flag, ncig, cig, qual, code, rl, align=REC_ALIGN, pack=True, pack32=None):
+def _pack_fixed(start, flag, ncig, cig, qual, code, rl, align=REC_ALIGN, pack=True, pack32=None, pack32_dist=5):
     """Pack records for reads of one read length (vectorised). Returns (rec_off,
     payload, flag): reads that fit get the packed layout and MGP_FLAG_PACKED;
     with pack32 (a min_baseq), reads that fit the 32-byte layout get it first
     (MGP_FLAG_PACK32, 32-byte records at multiples of min(align, 32))."""
     m = start.shape[0]
-    p32 = pack32_mask(start, flag, np.full(m, rl), ncig, cig, pack32) if pack32 is not None else np.zeros(m, bool)
+    p32 = (pack32_mask(start, flag, np.full(m, rl), ncig, cig, pack32, pack32_dist) if pack32 is not None
+           else np.zeros(m, bool))
     pk = packable_mask(start, flag, np.full(m, rl), ncig, cig, qual) & ~p32 if pack else np.zeros(m, bool)
     flag = (flag | np.where(pk, FLAG_PACKED, 0) | np.where(p32, FLAG_PACK32, 0)).astype(np.uint16)
     a32 = min(align, PACK32_BYTES)
@@ -463,7 +487,7 @@ def _pack_fixed(start, flag, ncig, cig, qual, code, rl, align=REC_ALIGN, pack=Tr
     ro = roff.astype(np.int64)
     if p32.any():
         pr = pack32_bytes(start[p32], np.full(int(p32.sum()), rl), (flag[p32] & FLAG_REVERSE) != 0, ncig[p32],
-                          cig[p32], qual[p32], code[p32], pack32)
+                          cig[p32], qual[p32], code[p32], pack32, pack32_dist)
         pay[ro[p32, None] + np.arange(PACK32_BYTES)[None, :]] = pr
     if pk.any():
         pr = pack_bytes(start[pk], np.full(int(pk.sum()), rl), (flag[pk] & FLAG_REVERSE) != 0, ncig[pk], cig[pk],
@@ -500,7 +524,7 @@ def _pack_fixed(start, flag, ncig, cig, qual, code, rl, align=REC_ALIGN, pack=Tr
 
 def synth_reads(
     seed: int, n_reads: int, n_cells: int, read_len: int = 50, mito_len: int = MITO_LEN, chunk: int = 262144,
-    rec_align: int = REC_ALIGN, pack: bool = True, pack32: int | None = None,
+    rec_align: int = REC_ALIGN, pack: bool = True, pack32: int | None = None, pack32_dist: int = 5,
 ) -> ReadSoA:
     """Host mirror of the device generator (bit-identical). pack: reads that fit
     get the packed 64-byte record layout (all of them at read_len <= 50); pack32
@@ -514,7 +538,7 @@ def synth_reads(
         i1 = min(n_reads, i0 + chunk)
         f = _synth_chunk(seed, i0, i1, n_reads, read_len, n_cells, mito_len, cdf, ref)
         roff, pay, flag = _pack_fixed(f["start"], f["flag"], f["ncig"], f["cig"], f["qual"], f["code"], read_len,
-                                      rec_align, pack, pack32)
+                                      rec_align, pack, pack32, pack32_dist)
         parts.append(ReadSoA(f["start"], f["bc"], f["tlen"], flag, f["mapq"], f["span"], roff, pay))
     soa = _concat_dense(parts)
     soa.extra.update(cdf=cdf, ref=ref, seed=seed, read_len=read_len)
@@ -549,7 +573,7 @@ def cigar_ref_span(cigar) -> int:
 
 
 def pack_reads(reads: list[dict], rec_align: int = REC_ALIGN, pack: bool = True,
-               pack32: int | None = None) -> ReadSoA:
+               pack32: int | None = None, pack32_dist: int = 5) -> ReadSoA:
     """Pack pysam-like read dicts into the engine input. pack: reads that fit get
     the packed 64-byte layout (include/mgpileup.h), which keeps what the pileup
     reads but not the code and quality of non-ACGT bases; pack32 (a min_baseq):
@@ -588,7 +612,7 @@ def pack_reads(reads: list[dict], rec_align: int = REC_ALIGN, pack: bool = True,
         if (pack or pack32 is not None) and seq is not None and qual is not None and lseq:
             cw = np.array([[(ln << 4) | op for op, ln in cig] or [0]], np.int64)
             qa = (np.asarray(qual, dtype=np.int64) & 0xFF).reshape(1, -1)
-            if pack32 is not None and pack32_mask([start[i]], [f], [lseq], [len(cig)], cw, pack32)[0]:
+            if pack32 is not None and pack32_mask([start[i]], [f], [lseq], [len(cig)], cw, pack32, pack32_dist)[0]:
                 codes = np.array([[_NT16_IDX[ch] for ch in seq.upper()]], np.int64)
                 f |= FLAG_PACK32
                 flag[i] = f
@@ -596,7 +620,7 @@ def pack_reads(reads: list[dict], rec_align: int = REC_ALIGN, pack: bool = True,
                 size = (PACK32_BYTES + a32 - 1) & ~(a32 - 1)
                 rec = np.zeros(size, np.uint8)
                 rec[:PACK32_BYTES] = pack32_bytes([start[i]], [lseq], [(f & FLAG_REVERSE) != 0], [len(cig)], cw, qa,
-                                                  codes, pack32)[0]
+                                                  codes, pack32, pack32_dist)[0]
                 chunks.append(rec)
                 off += size
                 continue
@@ -644,15 +668,16 @@ def unpack_record(payload: np.ndarray, off: int, flag: int = 0) -> dict:
         r = payload[off : off + PACK32_BYTES]
         start = int(r[:2].view("<u2")[0])
         lseq = int(r[2])
-        ncig = int(r[3]) & 0x7F
+        ncig = int(r[3]) & 7
         cig = r[4:12].view("<u2").astype(np.int64).tolist()[:ncig]
         w = int.from_bytes(bytes(r[12:31]), "little")
         v = [(w >> (3 * k)) & 7 for k in range(lseq)]
-        seq = "".join("ACGT"[x & 3] if x & 4 else "N" for x in v)
+        seq = "".join("ACGT"[x] if x < 4 else "N" for x in v)
         return dict(
             reference_start=start, flag=FLAG_REVERSE if r[3] & 0x80 else 0,
             cigartuples=[(c & 15, c >> 4) for c in cig], query_sequence=seq,
-            query_qualities=[127 if x & 4 else 0 for x in v], min_baseq=int(r[31].astype(np.int8)),
+            query_qualities=[127 if x < 4 else 0 for x in v], min_baseq=int(r[31].astype(np.int8)),
+            min_dist=(int(r[3]) >> 3) & 15,
         )
     if int(flag) & FLAG_PACKED:
         r = payload[off : off + PACK_BYTES]

@@ -285,6 +285,24 @@ int oracle_run(const mgp_config *cfg, const mgp_batch *b, mgp_result *out, int32
         return err;
     }
 
+    /* 32-byte records stand for one (min_baseq, min_dist) pair (bytes 31 and 3,
+     * include/mgpileup.h): a run under another pair is refused, as the engine does */
+    for (int64_t i = 0; i < n; ++i)
+        if (b->flag[i] & MGP_FLAG_PACK32) {
+            const uint8_t *r = b->payload + b->rec_off[i];
+            const int32_t md = cfg->min_dist_from_end > 0 ? cfg->min_dist_from_end : 0;
+            if ((int32_t)(int8_t)r[31] != cfg->min_baseq || (int32_t)((r[3] >> 3) & 15u) != md) {
+                err = ORC_E_BADREAD;
+                break;
+            }
+        }
+    if (err) {
+        free(cnt);
+        free(order);
+        free(keep);
+        return err;
+    }
+
     /* per-barcode read lists in BAM order (reads_by_barcode[barcode].append) */
     int64_t *off = (int64_t *)malloc(((size_t)nc + 1) * sizeof(int64_t));
     int64_t *lst = (int64_t *)malloc(((size_t)filtered + 1) * sizeof(int64_t));
@@ -336,8 +354,8 @@ int oracle_run(const mgp_config *cfg, const mgp_batch *b, mgp_result *out, int32
             const int64_t i = lst[off[c] + k];
             if ((int)b->mapq[i] < cfg->min_mapq) continue; /* pileup.py:33 */
             if (b->flag[i] & MGP_FLAG_PACK32) {
-                /* 32-byte record: its counted bits stand for base + quality
-                 * (include/mgpileup.h, made for the run's min_baseq) */
+                /* 32-byte record: its codes stand for base + quality + block +
+                 * end distance (include/mgpileup.h, made for the run's thresholds) */
                 uint8_t full[128];
                 mgp_unpack32_record(b->payload + b->rec_off[i], full);
                 pile_read(full, cfg, bc8, tn5);

@@ -110,14 +110,16 @@ def test_engine_pack32_streaming(engine_lib, oracle_lib):
 
 
 def test_engine_pack32_min_baseq_guard(engine_lib):
-    """Records made for min_baseq 20 refused by a run at another min_baseq."""
+    """Records made for (min_baseq 20, min_dist 5) refused by a run at another pair."""
     from mgatk2_amd.engine import EngineConfig
     from mgatk2_amd.exceptions import InvalidInputError
     from mgatk2_amd.synth import synth_reads
 
-    soa = synth_reads(12, 50_000, 10, pack32=20)
+    soa = synth_reads(12, 50_000, 10, pack32=20, pack32_dist=5)
     with pytest.raises(InvalidInputError):
         run(engine_lib, EngineConfig(n_cells=10, **{**CONFIGS["run"], "min_baseq": 21}), soa)
+    with pytest.raises(InvalidInputError):  # and for min_dist 5
+        run(engine_lib, EngineConfig(n_cells=10, **{**CONFIGS["run"], "min_distance_from_end": 3}), soa)
 
 
 @pytest.mark.parametrize("case", CASES)

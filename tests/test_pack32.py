@@ -41,29 +41,41 @@ def test_host_generator_pack32_same_pileup(cfgname, oracle_lib):
 
 
 def test_pack32_unpack_roundtrip():
+    """A code counts exactly the bases the reference piles: inside an aligned block
+    as the reference walks the CIGAR (an insertion does not advance the query
+    position, pileup.py Q1: M10 I3 M27 piles query 0..36, never 37..39), at least
+    min_dist from either end, int8 quality >= min_baseq, and A/C/G/T."""
     from mgatk2_amd.synth import FLAG_PACK32, pack_reads, unpack_record
 
     reads = [
-        dict(reference_start=5, cigartuples=[(4, 2), (0, 7)], query_sequence="ACGTNRY",
-             query_qualities=[0, 1, 62, 30, 4, 200, 6], flag=0x11),
+        dict(reference_start=5, cigartuples=[(4, 2), (0, 7)], query_sequence="ACGTNRYAC",
+             query_qualities=[0, 1, 62, 30, 4, 200, 6, 40, 41], flag=0x11),
         dict(reference_start=16560, cigartuples=[(0, 10), (1, 3), (0, 27), (5, 9)], query_sequence="ACGT" * 10,
              query_qualities=[19, 20, 21, 130] * 10, flag=0x1),
     ]
-    soa = pack_reads(reads, pack32=20)
-    assert (soa.flag & FLAG_PACK32).all()
-    for i, r in enumerate(reads):
-        d = unpack_record(soa.payload, int(soa.rec_off[i]), int(soa.flag[i]))
-        assert d["reference_start"] == r["reference_start"] and d["cigartuples"] == r["cigartuples"]
-        assert d["min_baseq"] == 20 and bool(d["flag"] & 0x10) == bool(r["flag"] & 0x10)
-        q8 = [q - 256 if q >= 128 else q for q in r["query_qualities"]]
-        want = "".join(c if c in "ACGT" and q >= 20 else "N" for c, q in zip(r["query_sequence"], q8))
-        assert d["query_sequence"] == want
+    blocks = [range(2, 9), range(0, 37)]  # the query positions inside aligned blocks
+    for md in (0, 1, 5):
+        soa = pack_reads(reads, pack32=20, pack32_dist=md)
+        assert (soa.flag & FLAG_PACK32).all()
+        for i, r in enumerate(reads):
+            d = unpack_record(soa.payload, int(soa.rec_off[i]), int(soa.flag[i]))
+            assert d["reference_start"] == r["reference_start"] and d["cigartuples"] == r["cigartuples"]
+            assert d["min_baseq"] == 20 and d["min_dist"] == md
+            assert bool(d["flag"] & 0x10) == bool(r["flag"] & 0x10)
+            n = len(r["query_sequence"])
+            q8 = [q - 256 if q >= 128 else q for q in r["query_qualities"]]
+            want = "".join(c if c in "ACGT" and q >= 20 and k in blocks[i] and md <= k < n - md else "N"
+                           for k, (c, q) in enumerate(zip(r["query_sequence"], q8)))
+            assert d["query_sequence"] == want, (i, md)
+    assert unpack_record(pack_reads(reads, pack32=20, pack32_dist=0).payload, 0, FLAG_PACK32)["query_sequence"] \
+        == "NNGTNNNAC"
     # limits: start >= 65536 or < 0, > 4 CIGAR ops, long reads, min_baseq outside int8 keep other layouts
     bad = [dict(reference_start=70000, cigartuples=[(0, 6)], query_sequence="A" * 6, query_qualities=[30] * 6),
            dict(reference_start=-3, cigartuples=[(0, 6)], query_sequence="A" * 6, query_qualities=[30] * 6),
            dict(reference_start=1, cigartuples=[(0, 51)], query_sequence="A" * 51, query_qualities=[30] * 51)]
     assert not (pack_reads(bad, pack32=20).flag & FLAG_PACK32).any()
     assert not (pack_reads(reads, pack32=128).flag & FLAG_PACK32).any()
+    assert not (pack_reads(reads, pack32=20, pack32_dist=16).flag & FLAG_PACK32).any()
 
 
 def test_quad_placement_four_records_of_a_cell_per_line(oracle_lib):
@@ -111,3 +123,18 @@ def test_bam_decoder_pack32_gives_the_reference_results(case, tmp_path, oracle_l
         assert (soa.flag & FLAG_PACK32).any()
         res, _ = oracle_lib.oracle_run(cfg, soa)
         check_result(res, g)
+
+
+def test_oracle_refuses_pack32_made_for_other_thresholds(oracle_lib):
+    """Records made for (min_baseq 20, min_dist 5) under a run at min_dist 4 or
+    min_baseq 19: the oracle refuses them, as the engine does (ERR_PACKED)."""
+    from oracle.oracle import OracleError
+
+    from mgatk2_amd.engine import EngineConfig
+    from mgatk2_amd.synth import synth_reads
+
+    soa = synth_reads(13, 5_000, 10, pack32=20, pack32_dist=5)
+    oracle_lib.oracle_run(EngineConfig(n_cells=10, min_baseq=20, min_distance_from_end=5), soa)
+    for kw in (dict(min_baseq=20, min_distance_from_end=4), dict(min_baseq=19, min_distance_from_end=5)):
+        with pytest.raises(OracleError):
+            oracle_lib.oracle_run(EngineConfig(n_cells=10, **kw), soa)
