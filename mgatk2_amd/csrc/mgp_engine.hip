@@ -548,7 +548,7 @@ __global__ void __launch_bounds__(kGABlock, MGP_GA_WAVES) k_group_a(int64_t n, c
     uint32_t* wc = fbits + (g.nc + 31) / 32;
     const int b = blockIdx.x, part = blockIdx.y;
     const int nc = g.nc;
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // (scalar)
     const unsigned long long lt = lanemask_lt();
     // exclusive scan over groups (wave 0, 64 at a time) of the bin's bucket sizes
     // (the parts' sums), based at the bin's first slot; this part's slots follow the
@@ -601,20 +601,29 @@ __global__ void __launch_bounds__(kGABlock, MGP_GA_WAVES) k_group_a(int64_t n, c
         OffT o[kAhead];
     };
     // loads issued unconditionally (index clamped into the bin) so every path has
-    // the same number in flight and the waits stay counted
+    // the same number in flight and the waits stay counted. A wave's reads of a step
+    // are i0 + k (k = u * 64 + lane): the column pointers at the clamped run start
+    // are wave-uniform and k a 32-bit lane offset (scalar base + vector offset loads).
     // the record offset: from the index (dense), the u32 column or the u64 column (kOff)
+    auto wave_i0 = [&](int64_t base0) { return base0 + wid * (kAhead * kWave); };
     auto load = [&](Pre& P, int64_t base0) {
+        const int64_t ib = min(wave_i0(base0), hi - 1);           // (uniform; hi > lo here)
+        const uint32_t lim = (uint32_t)(hi - 1 - ib);
+        const int32_t* bcw = bc + ib;
+        const uint16_t* flw = flag + ib;
+        const uint8_t* mqw = mapq + ib;
+        const int32_t* stw = start + ib;
+        const int32_t* tlw = tlen + ib;
 #pragma unroll
         for (int u = 0; u < kAhead; ++u) {
-            const int64_t i = base0 + wid * (kAhead * kWave) + u * kWave + lane;
-            const int64_t j = i < hi ? i : hi - 1;
-            P.c[u] = bc[j];
-            P.fm[u] = (uint32_t)flag[j] | (uint32_t)mapq[j] << 16;
-            P.s[u] = start[j];
-            P.t[u] = tlen[j];
-            if constexpr (kOff == kOffDense) P.o[u] = (OffT)j;
-            else if constexpr (kOff == kOffR32) P.o[u] = roff32[j];
-            else P.o[u] = roff[j];
+            const uint32_t k = min((uint32_t)(u * kWave + lane), lim);
+            P.c[u] = bcw[k];
+            P.fm[u] = (uint32_t)flw[k] | (uint32_t)mqw[k] << 16;
+            P.s[u] = stw[k];
+            P.t[u] = tlw[k];
+            if constexpr (kOff == kOffDense) P.o[u] = (OffT)(ib + k);
+            else if constexpr (kOff == kOffR32) P.o[u] = roff32[ib + k];
+            else P.o[u] = roff[ib + k];
         }
     };
     // A step: each wave ranks its own reads by group (ballot peers, the leader of a
@@ -633,34 +642,45 @@ __global__ void __launch_bounds__(kGABlock, MGP_GA_WAVES) k_group_a(int64_t n, c
         uint32_t spn[kSpec ? kAhead : 1];
         int prev0 = 0;
         if constexpr (kSpec) {
+            const int64_t ib = min(wave_i0(base0), hi - 1);
+            const uint32_t lim = (uint32_t)(hi - 1 - ib);
+            const uint32_t* spw = span + ib;
 #pragma unroll
-            for (int u = 0; u < kAhead; ++u) {
-                const int64_t i = base0 + wid * (kAhead * kWave) + u * kWave + lane;
-                spn[u] = span[i < hi ? i : hi - 1];
-            }
-            const int64_t i0 = base0 + wid * (kAhead * kWave);
-            prev0 = start[i0 > 0 ? (i0 <= hi ? i0 - 1 : hi - 1) : 0];
+            for (int u = 0; u < kAhead; ++u) spn[u] = spw[min((uint32_t)(u * kWave + lane), lim)];
+            const int64_t w0 = wave_i0(base0);
+            prev0 = start[w0 > 0 ? (w0 <= hi ? w0 - 1 : hi - 1) : 0];
         }
         uint32_t* my = wc + ((size_t)set * (kGABlock / kWave) + wid) * ngroups;
         for (int x = lane; x < ngroups; x += kWave) my[x] = 0;
         __builtin_amdgcn_wave_barrier();
         bool valid[kAhead];
         uint32_t rk[kAhead];
+        const int64_t i0 = wave_i0(base0);
+        const int64_t nleft = hi - i0;  // reads of the bin from i0 on (uniform)
 #pragma unroll
         for (int u = 0; u < kAhead; ++u) {
-            const int64_t i = base0 + wid * (kAhead * kWave) + u * kWave + lane;
+            const uint32_t k = (uint32_t)(u * kWave + lane);
             const int c = P.c[u];
-            valid[u] = i < hi && read_valid(c, (uint16_t)P.fm[u], nc);
-            const int gi = c >> 6;
-            unsigned long long pm = __ballot(valid[u]);
-            // wave-uniform loop (gbits is a kernel argument): an early exit on the
-            // per-lane peer mask would make it divergent
-            for (int bit = 0; bit < gbits; ++bit) {
-                const bool x = valid[u] && ((gi >> bit) & 1);
-                const unsigned long long m = __ballot(x);
-                pm &= x ? m : ~m;
-            }
-            if (valid[u] && (fbits[c >> 5] >> (c & 31)) & 1u) atomicMin(&first_read[c], (uint32_t)i);
+            valid[u] = (int64_t)k < nleft && read_valid(c, (uint16_t)P.fm[u], nc);
+            const uint32_t gi = (uint32_t)c >> 6;
+            // peers (same cell group) = AND over the group id's bits of the ballot of
+            // lanes agreeing on that bit (invalid lanes: id 0, outside the initial mask).
+            // The first 8 bits unrolled; group ids above 8 bits take a uniform loop
+            const uint32_t gv = valid[u] ? gi : 0u;
+            const unsigned long long vb = __ballot(valid[u]);
+            uint32_t plo = (uint32_t)vb, phi = (uint32_t)(vb >> 32);
+            auto peer_bit = [&](int bit) {
+                const uint32_t x = (gv >> bit) & 1u;
+                const unsigned long long m = __builtin_amdgcn_uicmp(x, 0u, 33);  // ballot(x != 0): one v_cmp
+                const uint32_t agree = x - 1u;  // 0: bit set (take m), ~0: clear (take ~m)
+                plo &= (uint32_t)m ^ agree;
+                phi &= (uint32_t)(m >> 32) ^ agree;
+            };
+#pragma unroll
+            for (int bit = 0; bit < 8; ++bit) peer_bit(bit);
+            for (int bit = 8; bit < gbits; ++bit) peer_bit(bit);
+            const unsigned long long pm = (unsigned long long)phi << 32 | plo;
+            if (valid[u] && (fbits[c >> 5] >> (c & 31)) & 1u) atomicMin(&first_read[c], (uint32_t)(i0 + k));
             // every peer reads the group's counter in one LDS read, before its leader
             // (lowest peer) stores the bumped value: no cross-lane broadcast needed
             const uint32_t bef = valid[u] ? my[gi] : 0u;
@@ -678,7 +698,7 @@ __global__ void __launch_bounds__(kGABlock, MGP_GA_WAVES) k_group_a(int64_t n, c
         for (int u = 0; u < kAhead; ++u) {
             fit[u] = true;
             if constexpr (kSpec) {
-                const int64_t i = base0 + wid * (kAhead * kWave) + u * kWave + lane;
+                const int64_t i = i0 + u * kWave + lane;
                 const int t = P.t[u];
                 const uint32_t at = t < 0 ? (uint32_t)(-(int64_t)t) : (uint32_t)t;
                 // the previous read's start: DPP wave_shr:1 (lane - 1), lane 0 from the slot before
@@ -711,8 +731,7 @@ __global__ void __launch_bounds__(kGABlock, MGP_GA_WAVES) k_group_a(int64_t n, c
 #pragma unroll
         for (int u = 0; u < kAhead; ++u) {
             if (!valid[u]) continue;
-            const uint32_t dest = MGP_ABL_A == 2 ? (uint32_t)(base0 + wid * (kAhead * kWave) + u * kWave + lane)
-                                                 : my[P.c[u] >> 6] + rk[u];
+            const uint32_t dest = MGP_ABL_A == 2 ? (uint32_t)(i0 + u * kWave + lane) : my[P.c[u] >> 6] + rk[u];
             if (MGP_ABL_A == 1 && dest != 0xFFFFFFFFu) continue;  // ablation: no stores
             const uint16_t f = (uint16_t)P.fm[u];
             const int t = P.t[u];
@@ -1008,7 +1027,7 @@ __global__ void __launch_bounds__(kBlock, Tr::kWaves) k_group_b(const typename T
     __shared__ uint16_t wpend[kBlock / kWave][kBPer * kWave];  // per wave: stage indices of deferred walks
     const int gi = blockIdx.x;
     const int B0 = blockIdx.y * rb, B1 = min(g.nbins, B0 + rb);
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // (scalar)
     const int nc = g.nc;
     const int c = gi * kGroup + lane;
     const unsigned long long lt = lanemask_lt();
@@ -1942,7 +1961,7 @@ __global__ void __launch_bounds__(kBlock, MGP_PILEUP_WAVES) k_pileup(
     w.wlen = min(g.W, g.L - w.w0);
     w.Wp = g.Wp;
     const int L = g.L;
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // (scalar)
     uint32_t* wq = wq_all[wid];
     // the queued read a lane piles: even queue slots in lanes 0..31, odd in 32..63. The
     // queue is in coordinate order and LDS atomics conflict per 32-lane half, so
@@ -3042,6 +3061,7 @@ static int run_segment(mgp_ctx* ctx, const Seg& sg, int slot, int& dup_parts, in
         const size_t a_lds = (size_t)ngroups * (1 + 2 * (kGABlock / kWave)) * 4 + (size_t)((nc + 31) / 32) * 4;
         if (a_lds > (size_t)ctx->lds_hist_max_cells * 4)
             return set_err(MGP_E_INVALID, "too many cells for one context (grouping LDS)");
+        if (gbits > 16) return set_err(MGP_E_INVALID, "too many cells for one context (cell groups)");
         if ((uint64_t)ctx->pay >= (1ull << GM_LCELL_SHIFT))
             return set_err(MGP_E_INVALID, "payload too large (record offsets must stay below 2^50)");
         dim3 ga((unsigned)g.nbins, kParts);
