@@ -50,6 +50,8 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 BYTES_PER_READ = 95  # algorithmic input bytes per L=50 read
 BYTES_PER_CELL = 16569 * 10 * 4  # int32 counts (8 planes) + tn5 (2 planes) written once
 ROW16_BYTES_PER_CELL = 16569 * 22  # the pileup's 16-bit rows: 8 + 2 + 1 u16 per position
+# payload bytes of one record per layout (include/mgpileup.h)
+RECORD_BYTES = {"quad32": 32, "pack32": 32, "paired": 64, "packed": 64, "full": 128}
 
 
 def workload_name(n_reads: int, n_cells: int) -> str:
@@ -233,11 +235,16 @@ def main():
     value = total_reads * args.steps / dt
     ms_step = dt / args.steps * 1e3
 
-    # roofline of the dominant stage (HIP events on the compute stream, averaged over the timed steps)
+    # roofline of the dominant kernel: its own algorithmic bytes per launch (kernel_rooflines)
+    # over its HIP-event time on the compute stream, averaged over the timed steps; the
+    # whole step against SURVEY.md §8(d)'s engine-level count (95 B per read + the u32
+    # result rows per cell) is step_achieved / step_frac
     dom = "pileup"
-    alg_bytes = n_res * BYTES_PER_READ + n_cells * BYTES_PER_CELL
+    kernels = kernel_rooflines(kt_all, n_res, n_cells, res.stats, cfg, args.record_layout)
+    alg_bytes = kernel_bytes(n_res, n_cells, res.stats, cfg, args.record_layout)[dom]
     achieved = alg_bytes / (kt[dom] * 1e-3) / 1e9
-    step_achieved = alg_bytes / (dt_rank / args.steps) / 1e9
+    engine_bytes = n_res * BYTES_PER_READ + n_cells * BYTES_PER_CELL
+    step_achieved = engine_bytes / (dt_rank / args.steps) / 1e9
     traffic = None
     pmc = ROOT / "profiles" / "pmc_traffic.json"
     if pmc.exists():
@@ -248,7 +255,6 @@ def main():
                 traffic = d.get(dom)
         except Exception:
             traffic = None
-    kernels = kernel_rooflines(kt_all, n_res, n_cells, res.stats, cfg)
 
     check = None
     if rank == 0 and not args.no_check:
@@ -299,6 +305,9 @@ def main():
                 "frac": achieved / HBM_PEAK_GBS,
                 "traffic": traffic,
                 "alg_bytes_per_launch": alg_bytes,
+                "alg_bytes_what": f"4-byte pileup element + one {RECORD_BYTES[args.record_layout]}-byte record per "
+                                  f"kept read, 16-bit result rows ({ROW16_BYTES_PER_CELL} B) per cell",
+                "engine_alg_bytes_per_step": engine_bytes,
                 "step_achieved": step_achieved,
                 "step_frac": step_achieved / HBM_PEAK_GBS,
                 "kernels": kernels,
@@ -315,12 +324,13 @@ def main():
         dist.destroy_process_group()
 
 
-def kernel_rooflines(kt: dict, n: int, nc: int, stats: dict, cfg) -> dict:
-    """Each kernel's own algorithmic bytes (DESIGN.md §3) over its HIP-event time."""
+def kernel_bytes(n: int, nc: int, stats: dict, cfg, layout: str) -> dict:
+    """Each kernel's own algorithmic bytes per launch."""
     L = cfg.mito_len
     nbins = (L + 7) // 8 + 1
     kept = int(stats.get("filtered_reads", 0))
-    own = {
+    rec = RECORD_BYTES[layout]
+    return {
         # barcode + flag per read, the H rows
         "hist": 6 * n + 4 * nbins * nc,
         # every column of every read (27 B), one 8-byte element per kept-or-duplicate read
@@ -328,14 +338,18 @@ def kernel_rooflines(kt: dict, n: int, nc: int, stats: dict, cfg) -> dict:
         "group_a": 27 * n + 8 * kept,
         # 8-byte element in, 4-byte pileup element out
         "group_b": 12 * kept,
-        # 4-byte element + one 64-byte record per kept read (an upper bound: kept reads
-        # below min_mapq are not gathered), the 16-bit result rows written once
-        "pileup": 68 * kept + ROW16_BYTES_PER_CELL * nc,
+        # 4-byte element + one record per kept read (an upper bound: kept reads below
+        # min_mapq are not gathered), the 16-bit result rows written once
+        "pileup": (4 + rec) * kept + ROW16_BYTES_PER_CELL * nc,
         # the 16-bit depth row per cell
         "median": 2 * L * nc,
     }
+
+
+def kernel_rooflines(kt: dict, n: int, nc: int, stats: dict, cfg, layout: str) -> dict:
+    """Each kernel's own algorithmic bytes over its HIP-event time."""
     out = {}
-    for k, b in own.items():
+    for k, b in kernel_bytes(n, nc, stats, cfg, layout).items():
         ms = kt.get(k, 0.0)
         if ms > 0:
             gbs = b / (ms * 1e-3) / 1e9

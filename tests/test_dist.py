@@ -130,3 +130,19 @@ def test_bench_launcher(world):
 
     script = str(Path(__file__).resolve().parent / "_bench_rank.py")
     assert bench.launch_workers(world, [sys.executable, script]) == 0
+
+
+def test_bench_kernel_bytes_follow_the_record_layout():
+    """The headline roofline counts the pileup's own bytes: a 4-byte element and one
+    record of the run's layout per kept read, plus the 16-bit rows per cell."""
+    import bench
+    from mgatk2_amd.engine import EngineConfig
+
+    cfg = EngineConfig(n_cells=10)
+    st = {"filtered_reads": 1000}
+    for lay, rec in (("quad32", 32), ("paired", 64), ("full", 128)):
+        b = bench.kernel_bytes(2000, 10, st, cfg, lay)
+        assert b["pileup"] == (4 + rec) * 1000 + bench.ROW16_BYTES_PER_CELL * 10
+        assert b["group_b"] == 12 * 1000
+    kr = bench.kernel_rooflines({"pileup": 1.0}, 2000, 10, st, cfg, "quad32")
+    assert set(kr) == {"pileup"} and kr["pileup"]["alg_bytes"] == 36 * 1000 + bench.ROW16_BYTES_PER_CELL * 10
