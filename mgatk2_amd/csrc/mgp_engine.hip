@@ -513,7 +513,8 @@ constexpr int kCompactBins = 32;             // start bins per pass-B step (comp
 #define MGP_GA_WAVES 1
 #endif
 #ifndef MGP_ABL_A
-#define MGP_ABL_A 0  // pass-A ablations (experiments only): 1 no element stores, 2 no ranking (slot = read index)
+#define MGP_ABL_A 0  // pass-A ablations (experiments only): 1 no element stores, 2 no ranking (slot = read index),
+                     // 3 no span column (the C4 generator's 53 assumed)
 #endif
 #ifndef MGP_GA_DB
 #define MGP_GA_DB 1  // pass A: next step's loads in flight during this step (double buffer)
@@ -646,7 +647,8 @@ __global__ void __launch_bounds__(kGABlock, MGP_GA_WAVES) k_group_a(int64_t n, c
             const uint32_t lim = (uint32_t)(hi - 1 - ib);
             const uint32_t* spw = span + ib;
 #pragma unroll
-            for (int u = 0; u < kAhead; ++u) spn[u] = spw[min((uint32_t)(u * kWave + lane), lim)];
+            for (int u = 0; u < kAhead; ++u)
+                spn[u] = MGP_ABL_A == 3 ? 53u : spw[min((uint32_t)(u * kWave + lane), lim)];
             const int64_t w0 = wave_i0(base0);
             prev0 = start[w0 > 0 ? (w0 <= hi ? w0 - 1 : hi - 1) : 0];
         }
@@ -663,23 +665,8 @@ __global__ void __launch_bounds__(kGABlock, MGP_GA_WAVES) k_group_a(int64_t n, c
             const int c = P.c[u];
             valid[u] = (int64_t)k < nleft && read_valid(c, (uint16_t)P.fm[u], nc);
             const uint32_t gi = (uint32_t)c >> 6;
-            // peers (same cell group) = AND over the group id's bits of the ballot of
-            // lanes agreeing on that bit (invalid lanes: id 0, outside the initial mask).
-            // The first 8 bits unrolled; group ids above 8 bits take a uniform loop
-            const uint32_t gv = valid[u] ? gi : 0u;
-            const unsigned long long vb = __ballot(valid[u]);
-            uint32_t plo = (uint32_t)vb, phi = (uint32_t)(vb >> 32);
-            auto peer_bit = [&](int bit) {
-                const uint32_t x = (gv >> bit) & 1u;
-                const unsigned long long m = __builtin_amdgcn_uicmp(x, 0u, 33);  // ballot(x != 0): one v_cmp
-                const uint32_t agree = x - 1u;  // 0: bit set (take m), ~0: clear (take ~m)
-                plo &= (uint32_t)m ^ agree;
-                phi &= (uint32_t)(m >> 32) ^ agree;
-            };
-#pragma unroll
-            for (int bit = 0; bit < 8; ++bit) peer_bit(bit);
-            for (int bit = 8; bit < gbits; ++bit) peer_bit(bit);
-            const unsigned long long pm = (unsigned long long)phi << 32 | plo;
+            // peers: same cell group (first 8 group-id bits unrolled)
+            const unsigned long long pm = peer_mask<8>(valid[u], gi, gbits);
             if (valid[u] && (fbits[c >> 5] >> (c & 31)) & 1u) atomicMin(&first_read[c], (uint32_t)(i0 + k));
             // every peer reads the group's counter in one LDS read, before its leader
             // (lowest peer) stores the bumped value: no cross-lane broadcast needed
@@ -955,13 +942,7 @@ __device__ __forceinline__ void group_b_rank(const typename Tr::T* __restrict__ 
         T e = Tr::zero();
         if (act) e = gel2[j];
         const int lc = Tr::lcell(e);
-        unsigned long long peers = __ballot(act);
-#pragma unroll
-        for (int bit = 0; bit < 6; ++bit) {
-            const bool x = act && ((lc >> bit) & 1);
-            const unsigned long long m = __ballot(x);
-            peers &= x ? m : ~m;
-        }
+        const unsigned long long peers = peer_mask<6>(act, (uint32_t)lc);
         const uint32_t base = act ? cnt[lc] : 0u;
         __builtin_amdgcn_wave_barrier();
         if (act && (peers & lt) == 0ull) cnt[lc] = base + (uint32_t)__popcll(peers);
@@ -1122,13 +1103,7 @@ __global__ void __launch_bounds__(kBlock, Tr::kWaves) k_group_b(const typename T
             const uint32_t t = (uint32_t)(wid * (kBPer * kWave) + u * kWave + lane);
             const bool act = t < tot;
             const int lc = Tr::lcell(e[u]);
-            unsigned long long peers = __ballot(act);
-#pragma unroll
-            for (int bit = 0; bit < 6; ++bit) {
-                const bool x = act && ((lc >> bit) & 1);
-                const unsigned long long m = __ballot(x);
-                peers &= x ? m : ~m;
-            }
+            const unsigned long long peers = peer_mask<6>(act, (uint32_t)lc);
             const uint32_t base = act ? wcnt[wid][lc] : 0u;
             __builtin_amdgcn_wave_barrier();
             if (act && (peers & lt) == 0ull) wcnt[wid][lc] = base + (uint32_t)__popcll(peers);

@@ -66,6 +66,31 @@ __device__ __forceinline__ unsigned long long lanemask_lt() {
     return lane == 0 ? 0ull : (~0ull >> (64 - lane));
 }
 
+// The lanes of the wave holding the same key as this lane, among the `act` lanes:
+// the AND over the key's bits of the ballot of the lanes that agree on the bit. One
+// v_cmp per bit makes the ballot (the plain __ballot of a compound predicate costs a
+// select and a second compare), and the bit itself gives the agree mask (0: set, take
+// the ballot; ~0: clear, take its complement). Inactive lanes take key 0 and are
+// outside the initial mask. kBits bits unrolled, then bits [kBits, nbits) in a
+// wave-uniform loop.
+template <int kBits>
+__device__ __forceinline__ unsigned long long peer_mask(bool act, uint32_t key, int nbits = kBits) {
+    const uint32_t kv = act ? key : 0u;
+    const unsigned long long vb = __ballot(act);
+    uint32_t plo = (uint32_t)vb, phi = (uint32_t)(vb >> 32);
+    auto bit_step = [&](int bit) {
+        const uint32_t x = (kv >> bit) & 1u;
+        const unsigned long long m = __builtin_amdgcn_uicmp(x, 0u, 33);  // ballot(x != 0)
+        const uint32_t agree = x - 1u;
+        plo &= (uint32_t)m ^ agree;
+        phi &= (uint32_t)(m >> 32) ^ agree;
+    };
+#pragma unroll
+    for (int bit = 0; bit < kBits; ++bit) bit_step(bit);
+    for (int bit = kBits; bit < nbits; ++bit) bit_step(bit);
+    return (unsigned long long)phi << 32 | plo;
+}
+
 // Wave reductions over all 64 lanes (every caller enters with the whole wave
 // active), result in every lane. They are the device library's DPP reductions
 // (row shifts + row broadcasts, then a lane read): ALU work only. A butterfly of

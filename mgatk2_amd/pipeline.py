@@ -93,7 +93,9 @@ class MtDNAPipeline:
         t1 = time.time()
 
         processor = CellProcessor(self.config, self.output_dir, device=self.device, devices=self.devices)
+        ta = time.time()
         res = processor.run_soa(soa, len(self.barcode_list))
+        tb = time.time()
         del soa
         t2 = time.time()
         self.engine_result = res
@@ -142,7 +144,8 @@ class MtDNAPipeline:
                 logger.warning("Failed to generate HTML report: %s", e)
         t4 = time.time()
         self.timings = {"bam_ingest": t1 - t0, "engine": t2 - t1, "write": t3 - t2, "report": t4 - t3,
-                        "total": t4 - t0, **processor.last_timing}
+                        "total": t4 - t0, "engine_setup": ta - t1, "engine_run_soa": tb - ta,
+                        "engine_free_inputs": t2 - tb, **processor.last_timing}
         logger.info("Pipeline complete")
         logger.info("Elapsed time: %.1fs (ingest %.1fs, engine %.1fs, write %.1fs)", t4 - t0, t1 - t0, t2 - t1,
                     t3 - t2)
