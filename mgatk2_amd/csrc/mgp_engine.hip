@@ -585,10 +585,16 @@ __global__ void __launch_bounds__(kGABlock, MGP_GA_WAVES) k_group_a(int64_t n, c
     if (b >= seg_bhi || b < seg_lo_bin(seg_w0, g, st)) return;
     // cells whose first read is in this bin (k_scan_apply)
     const size_t fw = (size_t)(nc + 31) / 32;
-    for (int x = threadIdx.x; x < (int)fw; x += blockDim.x) fbits[x] = F[(size_t)b * fw + x];
+    uint32_t fany = 0u;
+    for (int x = threadIdx.x; x < (int)fw; x += blockDim.x) {
+        const uint32_t f = F[(size_t)b * fw + x];
+        fbits[x] = f;
+        fany |= f;
+    }
     int64_t lo, hi;
     part_range(bin_lo[b], max((int64_t)bin_lo[b + 1], (int64_t)bin_lo[b]), part, lo, hi);
-    __syncthreads();
+    // no cell has its first read in this bin (most bins): no per-read first-read test
+    const bool any_first = __syncthreads_or(fany != 0u) != 0;
     // each wave owns a contiguous run of kAhead*64 reads per step (BAM order = wave
     // order, then round order); waves claim bucket slots in wave order
     constexpr int kAhead = MGP_GA_AHEAD;
@@ -665,9 +671,11 @@ __global__ void __launch_bounds__(kGABlock, MGP_GA_WAVES) k_group_a(int64_t n, c
             const int c = P.c[u];
             valid[u] = (int64_t)k < nleft && read_valid(c, (uint16_t)P.fm[u], nc);
             const uint32_t gi = (uint32_t)c >> 6;
-            // peers: same cell group (first 8 group-id bits unrolled)
+            // peers: same cell group (first 8 group-id bits unrolled; interleaving the
+            // reads' chains measured no faster)
             const unsigned long long pm = peer_mask<8>(valid[u], gi, gbits);
-            if (valid[u] && (fbits[c >> 5] >> (c & 31)) & 1u) atomicMin(&first_read[c], (uint32_t)(i0 + k));
+            if (any_first && valid[u] && (fbits[c >> 5] >> (c & 31)) & 1u)
+                atomicMin(&first_read[c], (uint32_t)(i0 + k));
             // every peer reads the group's counter in one LDS read, before its leader
             // (lowest peer) stores the bumped value: no cross-lane broadcast needed
             const uint32_t bef = valid[u] ? my[gi] : 0u;
@@ -1103,6 +1111,8 @@ __global__ void __launch_bounds__(kBlock, Tr::kWaves) k_group_b(const typename T
             const uint32_t t = (uint32_t)(wid * (kBPer * kWave) + u * kWave + lane);
             const bool act = t < tot;
             const int lc = Tr::lcell(e[u]);
+            // (one element's peers at a time: interleaving the elements' chains spills at
+            // this kernel's 5 waves per SIMD)
             const unsigned long long peers = peer_mask<6>(act, (uint32_t)lc);
             const uint32_t base = act ? wcnt[wid][lc] : 0u;
             __builtin_amdgcn_wave_barrier();

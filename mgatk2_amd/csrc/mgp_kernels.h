@@ -71,24 +71,33 @@ __device__ __forceinline__ unsigned long long lanemask_lt() {
 // v_cmp per bit makes the ballot (the plain __ballot of a compound predicate costs a
 // select and a second compare), and the bit itself gives the agree mask (0: set, take
 // the ballot; ~0: clear, take its complement). Inactive lanes take key 0 and are
-// outside the initial mask. kBits bits unrolled, then bits [kBits, nbits) in a
-// wave-uniform loop.
+// outside the initial mask. Callers ranking several keys per lane run the bit steps
+// of all their keys together (independent dependency chains).
+struct PeerAcc {
+    uint32_t kv, lo, hi;
+};
+__device__ __forceinline__ PeerAcc peer_begin(bool act, uint32_t key) {
+    const unsigned long long vb = __ballot(act);
+    return PeerAcc{act ? key : 0u, (uint32_t)vb, (uint32_t)(vb >> 32)};
+}
+__device__ __forceinline__ void peer_bit(PeerAcc& p, int bit) {
+    const uint32_t x = (p.kv >> bit) & 1u;
+    const unsigned long long m = __builtin_amdgcn_uicmp(x, 0u, 33);  // ballot(x != 0)
+    const uint32_t agree = x - 1u;
+    p.lo &= (uint32_t)m ^ agree;
+    p.hi &= (uint32_t)(m >> 32) ^ agree;
+}
+__device__ __forceinline__ unsigned long long peer_end(const PeerAcc& p) {
+    return (unsigned long long)p.hi << 32 | p.lo;
+}
+// one key: kBits bits unrolled, then bits [kBits, nbits) in a wave-uniform loop
 template <int kBits>
 __device__ __forceinline__ unsigned long long peer_mask(bool act, uint32_t key, int nbits = kBits) {
-    const uint32_t kv = act ? key : 0u;
-    const unsigned long long vb = __ballot(act);
-    uint32_t plo = (uint32_t)vb, phi = (uint32_t)(vb >> 32);
-    auto bit_step = [&](int bit) {
-        const uint32_t x = (kv >> bit) & 1u;
-        const unsigned long long m = __builtin_amdgcn_uicmp(x, 0u, 33);  // ballot(x != 0)
-        const uint32_t agree = x - 1u;
-        plo &= (uint32_t)m ^ agree;
-        phi &= (uint32_t)(m >> 32) ^ agree;
-    };
+    PeerAcc p = peer_begin(act, key);
 #pragma unroll
-    for (int bit = 0; bit < kBits; ++bit) bit_step(bit);
-    for (int bit = kBits; bit < nbits; ++bit) bit_step(bit);
-    return (unsigned long long)phi << 32 | plo;
+    for (int bit = 0; bit < kBits; ++bit) peer_bit(p, bit);
+    for (int bit = kBits; bit < nbits; ++bit) peer_bit(p, bit);
+    return peer_end(p);
 }
 
 // Wave reductions over all 64 lanes (every caller enters with the whole wave
