@@ -137,6 +137,11 @@ struct mgp_ctx {
     int roff_mode = -1;     // pass A's offset source (kOffDense / kOffR32 / kOffR64), from the run's input check
     uint32_t read_bits = 0; // the input check's CHK_* bits of the resident reads
     bool no_spec = false;   // the speculative compact grouping failed on the resident reads (ERR_RESPEC)
+    // the input check's flag bits of the last run over the same resident reads (no push,
+    // reset or generation since): the next run picks its variants from them without the
+    // mid-run host wait, and k_check_stats verifies them on the device (ERR_RESPEC)
+    bool bits_cached = false;
+    uint32_t cached_bits = 0;
     bool stage_all = true;  // HIP events around every stage (false: the pileup's only, mgp_set_stage_timing)
 
     // run scratch
@@ -2406,12 +2411,26 @@ __global__ void __launch_bounds__(1024) k_run_stats(const uint32_t* __restrict__
 
 // grid (ceil(L4 / 256), ny): slice y sums the chunks y, y + ny, ... and adds into
 // the zeroed u64 tallies
+// Sum of the pileup's per-chunk tally partials: grid (L4 / 256, Y), block y sums
+// chunks y, y + Y, ... (four independent loads in flight per thread) and adds its sum
+// to the zeroed tally. Y is small (tens of chunks per thread): the u64 atomics on the
+// same 66k words, Y per word, cost more than the loads (32 per word took 0.13 ms at
+// any size).
 __global__ void k_tally_reduce(const uint32_t* __restrict__ part, int nchunks, int L4,
                                unsigned long long* __restrict__ tally) {
     const int x = blockIdx.x * blockDim.x + threadIdx.x;
     if (x >= L4) return;
-    unsigned long long acc = 0;
-    for (int ch = blockIdx.y; ch < nchunks; ch += gridDim.y) acc += part[(size_t)ch * L4 + x];
+    const int Y = gridDim.y;
+    unsigned long long a0 = 0, a1 = 0, a2 = 0, a3 = 0;
+    int ch = blockIdx.y;
+    for (; ch + 3 * Y < nchunks; ch += 4 * Y) {
+        a0 += part[(size_t)ch * L4 + x];
+        a1 += part[(size_t)(ch + Y) * L4 + x];
+        a2 += part[(size_t)(ch + 2 * Y) * L4 + x];
+        a3 += part[(size_t)(ch + 3 * Y) * L4 + x];
+    }
+    for (; ch < nchunks; ch += Y) a0 += part[(size_t)ch * L4 + x];
+    const unsigned long long acc = a0 + a1 + a2 + a3;
     if (acc) atomicAdd(&tally[x], acc);
 }
 
@@ -2567,6 +2586,9 @@ __global__ void k_respec_slot(const DevStats* st, unsigned long long* slot) {
 #ifndef MGP_PILE_WG
 #define MGP_PILE_WG 16384
 #endif
+#ifndef MGP_PILE_MIN_CPB
+#define MGP_PILE_MIN_CPB 4
+#endif
 static inline unsigned blocks_for(int64_t n, int bs = kBlock) { return (unsigned)((n + bs - 1) / bs); }
 
 static int configure_geometry(mgp_ctx* ctx) {
@@ -2585,10 +2607,14 @@ static int configure_geometry(mgp_ctx* ctx) {
     // offset is a shift folded into the address add (A/B: no bank-conflict cost)
     g.Wp = kTilePitch;
     g.nc = c.n_cells;
-    // cells per pileup workgroup: ~MGP_PILE_WG workgroups over the windows
+    // cells per pileup workgroup: ~MGP_PILE_WG workgroups over the windows, and at least
+    // MGP_PILE_MIN_CPB cells: each (chunk, window) workgroup writes a tally partial row
+    // (16 B per position) that k_tally_reduce reads back, so at few cells per chunk the
+    // partials, not the cells, set the cost (1250 cells at 1 per chunk: 331 MB, the same
+    // as C4's 10k cells at 8; at 4 per chunk the 1250-cell step is 11 % shorter)
     int64_t target = MGP_PILE_WG;
     int64_t cpb = ((int64_t)g.nc * g.nwin + target - 1) / target;
-    g.cpb = (int)std::max<int64_t>(1, std::min<int64_t>(cpb, 64));
+    g.cpb = (int)std::max<int64_t>(MGP_PILE_MIN_CPB, std::min<int64_t>(cpb, 64));
     g.nchunks = g.nc > 0 ? (g.nc + g.cpb - 1) / g.cpb : 0;
     return MGP_OK;
 }
@@ -2816,6 +2842,7 @@ int mgp_push_batch(mgp_ctx* ctx, const mgp_batch* b) {
     ctx->pay = pay0 + b->payload_bytes;
     ctx->ran = false;
     ctx->no_spec = false;
+    ctx->bits_cached = false;
     // streaming: the windows this batch completes go through the hot path now,
     // behind its copies, while the caller pushes the next batch
     if (ctx->stream) MGP_TRY(stream_segments(ctx, (int64_t)b->start[nb - 1], b->flag[nb - 1]));
@@ -2833,6 +2860,7 @@ int mgp_reset(mgp_ctx* ctx) {
     ctx->pay = 0;
     ctx->ran = false;
     ctx->no_spec = false;
+    ctx->bits_cached = false;
     ctx->seg_open = false;
     ctx->w_done = 0;
     ctx->stream_off = false;
@@ -2986,6 +3014,7 @@ static int run_segment(mgp_ctx* ctx, const Seg& sg, int slot, int& dup_parts, in
     int unit = 6;  // the pileup element's record offset unit: 64 bytes (32 for 32-byte records on the
                    // speculative path), or 16 bytes when some record is not 64-byte aligned
     bool spec = false, track = false;
+    uint32_t check_layout = 0;  // the one packed layout the variants assume, verified on the device
     int layout = kLayP64;  // the pileup's instantiation (the record layouts present)
     ctx->roff_mode = kOffR64;
     ctx->read_bits = 0;
@@ -2998,17 +3027,22 @@ static int run_segment(mgp_ctx* ctx, const Seg& sg, int slot, int& dup_parts, in
         layout = ctx->stream_layout;
         unit = layout == kLayP32 ? 5 : 6;
     } else if (n > 0) {
-        HIP_TRY(hipEventSynchronize(ctx->ev_bits));
-        const uint32_t fb = ctx->h_bits[0];
+        const bool cached = ctx->bits_cached && !ctx->no_spec;
+        if (!cached) HIP_TRY(hipEventSynchronize(ctx->ev_bits));
+        const uint32_t fb = cached ? ctx->cached_bits : ctx->h_bits[0];
         const uint32_t lb = fb & kLayBits;
         const int su = lb == CHK_P32 ? 5 : 6;
         track = ((fb & CHK_PAIRED) && (fb & CHK_UNPAIRED)) || (fb & CHK_NOSEQ);
         spec = !ctx->no_spec && !ctx->group_wide && !track && (lb == CHK_P64 || lb == CHK_P32) &&
                (uint64_t)ctx->pay < ((uint64_t)(PE_KEEP & PE_OFF) << su);
+        // only the speculative choice is cached: it needs nothing but these bits
+        ctx->bits_cached = spec;
+        ctx->cached_bits = fb;
         if (spec) {
             ctx->roff_mode = kOffSpec;
             ctx->read_bits = fb;
             unit = su;
+            check_layout = cached ? lb : 0u;
         } else {
             k_check_inputs<<<blocks_for(n), kBlock, 0, s>>>(
                 ctx->roff.as<uint64_t>(), ctx->flag.as<uint16_t>(), ctx->start.as<int32_t>(),
@@ -3075,7 +3109,7 @@ static int run_segment(mgp_ctx* ctx, const Seg& sg, int slot, int& dup_parts, in
         // the check's span and order bits into the run's stats (the pileup's halo); a
         // streaming segment also checks here the flag bits its variants assume
         k_check_stats<<<1, 64, 0, s>>>(ctx->roff_irregular.as<uint32_t>(), st,
-                                       sg.stream ? (layout == kLayP32 ? CHK_P32 : CHK_P64) : 0u);
+                                       sg.stream ? (layout == kLayP32 ? CHK_P32 : CHK_P64) : check_layout);
         HIP_TRY(hipGetLastError());
     }
     STAGE_END(ST_GROUP_A);
@@ -3173,7 +3207,7 @@ static int run_finish(mgp_ctx* ctx, int slot, int dup_parts, bool streamed) {
                 ctx->stage_ran[slot][ST_TALLY] = true;
             }
             HIP_TRY(hipMemsetAsync(tally, 0, (size_t)g.L * 32, s2));
-            dim3 gt(blocks_for((int64_t)g.L * 4), (unsigned)std::max(1, std::min(g.nchunks, 32)));
+            dim3 gt(blocks_for((int64_t)g.L * 4), (unsigned)std::max(1, std::min(g.nchunks / 64, 16)));
             k_tally_reduce<<<gt, kBlock, 0, s2>>>(ctx->tally_part.as<uint32_t>(), g.nchunks, g.L * 4, tally);
             HIP_TRY(hipGetLastError());
             if (STAGE_ON(ST_TALLY)) HIP_TRY(hipEventRecord(ctx->ev[slot][ST_TALLY][1], s2));
@@ -3283,6 +3317,7 @@ int mgp_sync(mgp_ctx* ctx) {
     const bool respec = ctx->comm ? *ctx->h_respec != 0ull : (e & ERR_RESPEC) != 0u;
     if (respec && !ctx->rerunning) {
         ctx->no_spec = true;
+        ctx->bits_cached = false;
         ctx->rerunning = true;
         int r = mgp_run(ctx);
         if (r == MGP_OK) r = mgp_sync(ctx);
@@ -3569,6 +3604,7 @@ int mgp_synth_generate(mgp_ctx* ctx, const mgp_synth_params* p) {
     ctx->pay = pay;
     ctx->ran = false;
     ctx->no_spec = false;
+    ctx->bits_cached = false;
     return MGP_OK;
 }
 

@@ -331,3 +331,32 @@ def test_single_rank_comm_respec_rerun(engine_lib, oracle_lib):
         eng.push(soa)
         got = eng.finish()
     assert_same(got, exp, "comm respec")
+
+
+def test_repeated_resident_runs_reuse_the_check_bits(engine_lib, oracle_lib):
+    """Runs over an unchanged resident set take the previous run's input-check bits
+    (no host wait; verified on the device): identical results; a push in between
+    drops them (the new set has full-layout records: the general path)."""
+    from mgatk2_amd.engine import EngineConfig
+    from mgatk2_amd.synth import concat_soa, synth_reads
+
+    cfg = EngineConfig(n_cells=60, **CONFIGS["run"])
+    a = synth_reads(91, 240_000, 60, pack32=cfg.min_baseq)
+    a = a.slice(0, int(np.searchsorted(a.start, 8000)))  # the first half of chrM
+    with engine_lib.Engine(cfg) as eng:
+        eng.push(a)
+        eng.run()
+        first = eng.fetch()
+        for _ in range(3):
+            eng.run()
+            assert_same(eng.fetch(), first, "cached rerun")
+        b = synth_reads(92, 240_000, 60, pack=False)
+        b = b.slice(int(np.searchsorted(b.start, 8000)), b.n)  # the second half: coordinate order kept
+        assert a.n > 100_000 and b.n > 100_000
+        eng.push(b)
+        eng.run()
+        got = eng.fetch()
+    exp_a, _ = oracle_lib.oracle_run(cfg, a)
+    assert_same(first, exp_a, "first run")
+    exp, _ = oracle_lib.oracle_run(cfg, concat_soa([a, b]))
+    assert_same(got, exp, "after push")
