@@ -227,7 +227,7 @@ __device__ __forceinline__ void part_range(int64_t lo, int64_t hi, int p, int64_
 }
 
 #ifndef MGP_HIST_U
-#define MGP_HIST_U 4  // reads per thread per histogram step
+#define MGP_HIST_U 6  // reads per thread per histogram step (r03 A/B: 4 and 8 slower)
 #endif
 #ifndef MGP_HIST_BLOCK
 #define MGP_HIST_BLOCK 512
@@ -313,7 +313,7 @@ __global__ void __launch_bounds__(kHistBlock) k_bin_count(const int32_t* __restr
     for (int part = 0; part < kParts; ++part) {
         int64_t lo, hi;
         part_range(blo, bhi, part, lo, hi);
-        // 4 reads per thread per step, loads issued together (clamped index, no branches)
+        // MGP_HIST_U reads per thread per step, loads issued together (clamped index, no branches)
         constexpr int kU = MGP_HIST_U;
         for (int64_t i0 = lo + threadIdx.x; i0 < hi; i0 += kU * kHistBlock) {
             int cc[kU];
