@@ -34,6 +34,15 @@ from .processing.readers import MITO_NAMES, BAMReader
 logger = logging.getLogger(__name__)
 
 
+def _release_in_background(box: list) -> None:
+    """Drop the objects in `box` (holding their last references) on a daemon thread:
+    their native free releases the GIL, so the unmapping overlaps the caller's next
+    stage."""
+    import threading
+
+    threading.Thread(target=box.clear, name="mgp-free-inputs", daemon=True).start()
+
+
 class MtDNAPipeline:
     """Single-pass mtDNA genotyping pipeline (pipeline.py:23-74)."""
 
@@ -96,7 +105,11 @@ class MtDNAPipeline:
         ta = time.time()
         res = processor.run_soa(soa, len(self.barcode_list))
         tb = time.time()
+        # the decoded batch (GBs of malloc'd columns and records) is unmapped on a
+        # background thread while the writers run: its free took 0.36 s at C3
+        box = [soa]
         del soa
+        _release_in_background(box)
         t2 = time.time()
         self.engine_result = res
         self.read_stats = {**res.stats, **stats}
