@@ -120,7 +120,7 @@ class IncrementalTextWriter:
         self.cell_stats: list[dict] = []
         self.position_base_counts = np.zeros((config.mito_length, 4), np.int64)
         self.cell_depths: dict[str, float] = {}
-        self.gzip_level = int(os.environ.get("MGP_GZIP_LEVEL", 6)) if gzip_level is None else gzip_level
+        self.gzip_level = int(os.environ.get("MGP_GZIP_LEVEL", 1)) if gzip_level is None else gzip_level
         self.n_threads = n_threads
         self.prefix = self.output_dir / "output"
         for name in [*BASES, "coverage"]:

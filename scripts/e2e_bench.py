@@ -55,7 +55,6 @@ def main():
     print(f"[e2e] generated {args.reads:,} reads in {t1 - t0:.1f}s; BAM {bam.stat().st_size / 1e9:.2f} GB "
           f"written in {t2 - t1:.1f}s", file=sys.stderr, flush=True)
 
-    os.environ.setdefault("MGP_GZIP_LEVEL", "6")
     res = {"config": f"C3: {args.reads:,} reads x {args.cells} cells, run params (q20 mapq30 "
                      "dedup=alignment_and_fragment_length)", "host_threads": args.threads}
     for fmt in args.formats.split(","):

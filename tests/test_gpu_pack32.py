@@ -132,3 +132,20 @@ def test_engine_bam_pack32_matches_reference_goldens(case, engine_lib, tmp_path)
     with BamFile(tmp_path / "x.bam") as bam:
         soa = bam.read_soa("chrM", g.whitelist, pack=True, pack32=cfg.min_baseq)
     check_result(run(engine_lib, cfg, soa), g)
+
+
+@pytest.mark.parametrize("min_dist", [0, 2, 15])
+@pytest.mark.parametrize("min_baseq", [0, 30])
+def test_engine_pack32_end_distance_and_quality(engine_lib, oracle_lib, min_dist, min_baseq):
+    """32-byte records made for other (min_baseq, min_distance_from_end) pairs than the
+    default (the codes carry both): the same counts as the oracle on 64-byte records."""
+    from mgatk2_amd.engine import EngineConfig
+    from mgatk2_amd.synth import relocate, synth_reads
+
+    cfg = EngineConfig(n_cells=90, min_baseq=min_baseq, min_mapq=20, dedup_mode="alignment_start", min_reads=1,
+                       min_distance_from_end=min_dist)
+    ref = synth_reads(600 + min_dist, 300_000, 90)
+    soa = relocate(synth_reads(600 + min_dist, 300_000, 90, pack32=min_baseq, pack32_dist=min_dist), paired=True,
+                   n_cells=90)
+    exp, _ = oracle_lib.oracle_run(cfg, ref)
+    assert_same(run(engine_lib, cfg, soa), exp, f"pack32 q{min_baseq} d{min_dist}")
