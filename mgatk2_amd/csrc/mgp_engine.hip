@@ -146,6 +146,7 @@ struct mgp_ctx {
 
     // run scratch
     DevBuf bin_start, H, P, cell_cnt, cell_base, bin_valid, bin_base, bucket_off, gel2, PG, F;
+    DevBuf chunk_perm;  // the pileup's cell chunks, largest first (k_scan_cells)
     DevBuf pel, tally_part, tally, dup_part;
     DevBuf n_reads, any_paired, passed, covered, dsum, dmax, med_lo, med_hi, first_read;
     DevBuf counts, tn5, depth, stats;  // u32 rows: drained windows, and mgp_fetch's widened copy
@@ -178,7 +179,10 @@ __device__ __forceinline__ bool read_valid(int c, uint16_t f, int nc) {
     return c >= 0 && c < nc && !(f & (MGP_FLAG_UNMAPPED | MGP_FLAG_SECONDARY | MGP_FLAG_SUPPLEMENTARY));
 }
 
-// first index i in [0, n) with start[i] >= t (start[] is coordinate-sorted)
+// first index i in [0, n) with start[i] >= t (start[] is coordinate-sorted). (A
+// workgroup-wide search with blockDim probes per step, ~4 dependent steps at 200M
+// starts, measured slower: its barriers cost more than these dependent loads, which
+// the other resident workgroups hide; r03 v48.)
 __device__ __forceinline__ int64_t lower_bound_start(const int32_t* __restrict__ start, int64_t n, int64_t t) {
     int64_t lo = 0, hi = n;
     while (lo < hi) {
@@ -402,9 +406,14 @@ __global__ void k_scan_rows(uint32_t* __restrict__ P, int nrb, int nc, uint32_t*
     cnt[c] = acc;
 }
 
-// Scan step c: exclusive scan over cells (single workgroup of 1024).
+// Scan step c: exclusive scan over cells (single workgroup of 1024). With `perm`
+// (the cells' scan, not the bins'), it then orders the pileup's cell chunks of cpb
+// cells by size, largest first (a counting sort over 64 size classes): the pileup
+// takes its workgroups' chunks in that order, so the largest chunks are not the
+// grid's tail (lognormal cells: a chunk of 4 cells can hold twice the mean).
 __global__ void __launch_bounds__(1024) k_scan_cells(const uint32_t* __restrict__ cnt, int nc,
-                                                     uint32_t* __restrict__ base) {
+                                                     uint32_t* __restrict__ base, int cpb = 0,
+                                                     int nchunks = 0, uint32_t* __restrict__ perm = nullptr) {
     __shared__ uint32_t wsum[16];
     __shared__ uint32_t carry;
     if (threadIdx.x == 0) carry = 0;
@@ -436,6 +445,38 @@ __global__ void __launch_bounds__(1024) k_scan_cells(const uint32_t* __restrict_
         if (threadIdx.x == 1023) carry = excl + v;
         __syncthreads();
     }
+    if (perm == nullptr) return;
+    // chunk sizes from the cell bases this workgroup just wrote (visible to it behind
+    // the barriers above); the last chunk ends at the total
+    __shared__ uint32_t cls[64], s_max;
+    const uint32_t total = carry;
+    auto size_of = [&](int ch) {
+        const int c0 = ch * cpb, c1 = min(nc, c0 + cpb);
+        return (c1 < nc ? base[c1] : total) - base[c0];
+    };
+    if (threadIdx.x < 64) cls[threadIdx.x] = 0;
+    if (threadIdx.x == 0) s_max = 0;
+    __syncthreads();
+    uint32_t mx = 0;
+    for (int ch = threadIdx.x; ch < nchunks; ch += 1024) mx = max(mx, size_of(ch));
+    mx = wave_max(mx);
+    if (lane == 0 && mx) atomicMax(&s_max, mx);
+    __syncthreads();
+    const uint64_t m1 = (uint64_t)s_max + 1;
+    auto key_of = [&](int ch) { return 63u - (uint32_t)((uint64_t)size_of(ch) * 64u / m1); };
+    for (int ch = threadIdx.x; ch < nchunks; ch += 1024) atomicAdd(&cls[key_of(ch)], 1u);
+    __syncthreads();
+    if (threadIdx.x < 64) {  // exclusive scan of the class counts (one wave)
+        const uint32_t v = cls[threadIdx.x];
+        uint32_t x = v;
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = __shfl_up(x, o, 64);
+            if (lane >= o) x += y;
+        }
+        cls[threadIdx.x] = x - v;
+    }
+    __syncthreads();
+    for (int ch = threadIdx.x; ch < nchunks; ch += 1024) perm[atomicAdd(&cls[key_of(ch)], 1u)] = (uint32_t)ch;
 }
 
 // Scan step d: H[r][c] <- exclusive (cell-major) offset; row nrows <- cell end;
@@ -1931,7 +1972,7 @@ __global__ void __launch_bounds__(kBlock, MGP_PILEUP_WAVES) k_pileup(
     uint32_t* __restrict__ depth, uint32_t* __restrict__ n_reads, uint8_t* __restrict__ any_paired, int pair_mode,
     uint32_t* __restrict__ covered, unsigned long long* __restrict__ dsum,
     uint32_t* __restrict__ dmax, uint32_t* __restrict__ tally_part, DevStats* st, int w_base,
-    const uint32_t* __restrict__ ck) {
+    const uint32_t* __restrict__ ck, const uint32_t* __restrict__ chunk_perm) {
     // the tile: kTilePlanes planes of kTilePitch words (A, C, G, T, trash, Tn5; fwd | rev << 16)
     extern __shared__ __align__(16) uint32_t tile_planes[];
     uint32_t* const tile = tile_planes + kTileGuard;  // position 0 of plane 0
@@ -1941,8 +1982,11 @@ __global__ void __launch_bounds__(kBlock, MGP_PILEUP_WAVES) k_pileup(
     __shared__ uint32_t r_cov[4], r_max[4], r_keep[4];
     __shared__ unsigned long long r_sum[4];
 
-    const int k = w_base + (int)blockIdx.y;  // window (a streaming segment's windows start at w_base)
-    const int chunk = blockIdx.x;
+    // the workgroups take the chunks largest first (chunk_perm, k_scan_cells), all
+    // windows of a chunk in a row; a streaming segment's windows start at w_base
+    const uint32_t nw = gridDim.y, lin = blockIdx.y * gridDim.x + blockIdx.x;
+    const int chunk = (int)chunk_perm[lin / nw];
+    const int k = w_base + (int)(lin % nw);  // window
     // pair_mode < 0 (streaming): every read paired iff the input check saw only paired
     // reads (a mix reruns the run resident, ERR_RESPEC)
     if (pair_mode < 0) pair_mode = (ck[0] & CHK_PAIRED) && !(ck[0] & CHK_UNPAIRED) ? 1 : 0;
@@ -2247,12 +2291,16 @@ __global__ void __launch_bounds__(kBlock) k_gate_fixup(Geom g, int min_reads, co
     }
 }
 // One workgroup per cell: pass flag and the two middle order statistics of the
-// covered depths (np.median, writers.py:190). The depth row sits in registers
-// (65 values per thread at L = 16569); each order statistic is found by a binary
-// search over the value range [1, max depth]: count(depth <= x) per thread, one
-// block reduction per step, both statistics searched in the same steps. No
-// atomics and no histogram, whatever the depths.
-constexpr int kMedRegs = 72;  // register-resident depths per thread (L <= 18432)
+// covered depths (np.median, writers.py:190). Each order statistic is found by a
+// binary search over the value range [1, max depth]: count(depth > x) per thread,
+// one block reduction per step, both statistics searched in the same steps. No
+// atomics and no histogram, whatever the depths. The 16-bit depth row sits in
+// registers as packed pairs (36 words per thread at L <= 18432: 8 waves per SIMD,
+// so twice the cells in flight of a u32 row), counted with packed 16-bit
+// saturating subtracts; a cell with a drained window (exact u32 depths) counts
+// from memory instead.
+constexpr int kMedRegs = 72;  // register-resident depths per thread (L < 18432), two per word
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
 
 // The depth of position p of cell c: the u16 row, or the u32 row in a drained window.
 __device__ __forceinline__ uint32_t depth_at(const Geom& g, int c, int p, const uint16_t* __restrict__ d16,
@@ -2288,50 +2336,57 @@ __global__ void __launch_bounds__(kBlock) k_median(Geom g, int min_reads, const 
     const int L = g.L;
     bool anyw = false;  // a drained window: its depths are in the u32 row
     for (int k = 0; k < g.nwin; ++k) anyw |= wide[(size_t)c * g.nwin + k] != 0;
+    // the register path: no drained window (every depth fits 16 bits) and depths below
+    // 2^15 (the packed counting's sign-bit compare); otherwise count from memory
+    const bool regs = kRegs && !anyw && dmax[c] < 0x8000u;  // (uniform)
     const uint16_t* drow = depth16 + (size_t)c * g.L;
-    uint32_t v[kRegs ? kMedRegs : 1];
-    if (kRegs) {
-        if (anyw) {
+    constexpr int kW = kRegs ? kMedRegs / 2 : 1;
+    // 4-byte loads from the 4-byte aligned address at or below the row's start: word j
+    // holds positions 2j - s and 2j + 1 - s (s = 1 when the row starts mid-word);
+    // halves outside the row are zeroed (a zero is never above a threshold >= 1)
+    u16x2 v[kW];
+    if (regs) {
+        const int s = (int)((reinterpret_cast<uintptr_t>(drow) >> 1) & 1u);  // (uniform)
+        const uint32_t* wrow = reinterpret_cast<const uint32_t*>(drow - s);
+        const uint32_t jmax = (uint32_t)(L - 1 + s) >> 1;  // the row's last word
+        uint32_t w[kW];
 #pragma unroll
-            for (int k = 0; k < kMedRegs; ++k) {
-                const int p = threadIdx.x + k * kBlock;
-                v[k] = p < L ? depth_at(g, c, p, depth16, depth32, wide, true) : 0u;
-            }
-        } else {
+        for (int k = 0; k < kW; ++k) w[k] = wrow[min((uint32_t)(threadIdx.x + k * kBlock), jmax)];  // (clamped)
 #pragma unroll
-            for (int k = 0; k < kMedRegs; ++k) {
-                const int p = threadIdx.x + k * kBlock;
-                v[k] = p < L ? (uint32_t)drow[p] : 0u;
-            }
+        for (int k = 0; k < kW; ++k) {
+            const int p0 = 2 * (int)(threadIdx.x + k * kBlock) - s;
+            const uint32_t keep = (p0 >= 0 && p0 < L ? 0xFFFFu : 0u) | (p0 + 1 < L ? 0xFFFF0000u : 0u);
+            const uint32_t x = w[k] & keep;
+            v[k] = __builtin_bit_cast(u16x2, x);
         }
     }
-    // zero depths sort first: the k-th covered value is the (zeros + k)-th overall
-    const uint32_t zeros = (uint32_t)L - n;
-    const uint32_t t_lo = zeros + (n - 1) / 2 + 1, t_hi = zeros + n / 2 + 1;  // counts to reach
+    // the k-th smallest covered depth: zero depths sort first, so it is the smallest x
+    // with count(depth <= x) >= zeros + k, i.e. count(depth > x) <= L - zeros - k = n - k
+    const uint32_t g_lo = n - ((n - 1) / 2 + 1), g_hi = n - (n / 2 + 1);  // counts above to reach
     uint32_t lo0 = 1, lo1 = dmax[c], hi0 = 1, hi1 = dmax[c];  // answers lie in [x0, x1]
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     // one barrier per step: the partial sums alternate between two LDS sets, and a
     // set is rewritten two steps later, behind the next step's barrier
     for (int it = 0; lo0 < lo1 || hi0 < hi1; it ^= 1) {
         const uint32_t ml = lo0 + (lo1 - lo0) / 2, mh = hi0 + (hi1 - hi0) / 2;
-        uint32_t cl = 0, ch = 0;
-        if (kRegs) {
+        uint32_t cl = 0, ch = 0;  // depths above ml / mh
+        if (regs) {
+            // depths and thresholds are below 2^15 here (regs), so depth > m iff the
+            // 16-bit difference m - depth has its top bit set
+            const u16x2 Ml = {(uint16_t)ml, (uint16_t)ml}, Mh = {(uint16_t)mh, (uint16_t)mh};
+            u16x2 al = {0, 0}, ah = {0, 0};
 #pragma unroll
-            for (int k = 0; k < kMedRegs; ++k) {
-                cl += v[k] <= ml;
-                ch += v[k] <= mh;
+            for (int k = 0; k < kW; ++k) {
+                al += (u16x2)(Ml - v[k]) >> (uint16_t)15;
+                ah += (u16x2)(Mh - v[k]) >> (uint16_t)15;
             }
-            // padding lanes past L hold 0 and were counted as zeros: remove them
-            const uint32_t pad = (uint32_t)(kMedRegs * kBlock - L);
-            if (threadIdx.x == 0) {
-                cl -= pad;
-                ch -= pad;
-            }
+            cl = (uint32_t)al.x + al.y;
+            ch = (uint32_t)ah.x + ah.y;
         } else {
             for (int p = threadIdx.x; p < L; p += kBlock) {
                 const uint32_t d = depth_at(g, c, p, depth16, depth32, wide, anyw);
-                cl += d <= ml;
-                ch += d <= mh;
+                cl += d > ml;
+                ch += d > mh;
             }
         }
         cl = wave_sum(cl);
@@ -2348,11 +2403,11 @@ __global__ void __launch_bounds__(kBlock) k_median(Geom g, int min_reads, const 
             shh += red[it][1][w];
         }
         if (lo0 < lo1) {
-            if (sl >= t_lo) lo1 = ml;
+            if (sl <= g_lo) lo1 = ml;
             else lo0 = ml + 1;
         }
         if (hi0 < hi1) {
-            if (shh >= t_hi) hi1 = mh;
+            if (shh <= g_hi) hi1 = mh;
             else hi0 = mh + 1;
         }
     }
@@ -2744,7 +2799,7 @@ void mgp_close(mgp_ctx* ctx) {
                       &ctx->span,      &ctx->roff,      &ctx->payload,  &ctx->bin_start,  &ctx->gel2,
                       &ctx->roff32,    &ctx->roff_irregular, &ctx->dup_part, &ctx->order_bad,
                       &ctx->H,         &ctx->P,         &ctx->cell_cnt, &ctx->cell_base,  &ctx->pel,
-                      &ctx->PG,        &ctx->F,
+                      &ctx->PG,        &ctx->F,         &ctx->chunk_perm,
                       &ctx->tally_part, &ctx->tally,   &ctx->n_reads,    &ctx->any_paired,
                       &ctx->passed,    &ctx->covered,   &ctx->dsum,     &ctx->dmax,       &ctx->med_lo,
                       &ctx->med_hi,    &ctx->first_read, &ctx->counts,  &ctx->tn5,        &ctx->depth,
@@ -2889,6 +2944,7 @@ static int ensure_run_buffers(mgp_ctx* ctx) {
     MGP_TRY(ctx->P.ensure((size_t)((g.nbins + 31) / 32 + 1) * nc * 4));
     MGP_TRY(ctx->cell_cnt.ensure(nc * 4));
     MGP_TRY(ctx->cell_base.ensure(nc * 4));
+    MGP_TRY(ctx->chunk_perm.ensure((size_t)std::max(g.nchunks, 1) * 4));
     MGP_TRY(ctx->pel.ensure(n * 4));
     MGP_TRY(ctx->gel2.ensure(n * sizeof(GElem)));
     MGP_TRY(ctx->bin_valid.ensure((size_t)(g.nbins + 1) * 4));
@@ -2999,7 +3055,8 @@ static int run_segment(mgp_ctx* ctx, const Seg& sg, int slot, int& dup_parts, in
     dim3 g2((nc + kBlock - 1) / kBlock, nrb);
     k_scan_colsum<<<g2, kBlock, 0, s>>>(ctx->H.as<uint32_t>(), g.nbins, nc, RB, ctx->P.as<uint32_t>());
     k_scan_rows<<<blocks_for(nc), kBlock, 0, s>>>(ctx->P.as<uint32_t>(), nrb, nc, ctx->cell_cnt.as<uint32_t>());
-    k_scan_cells<<<1, 1024, 0, s>>>(ctx->cell_cnt.as<uint32_t>(), nc, ctx->cell_base.as<uint32_t>());
+    k_scan_cells<<<1, 1024, 0, s>>>(ctx->cell_cnt.as<uint32_t>(), nc, ctx->cell_base.as<uint32_t>(), g.cpb,
+                                    g.nchunks, ctx->chunk_perm.as<uint32_t>());
     k_scan_apply<<<g2, kBlock, 0, s>>>(ctx->H.as<uint32_t>(), ctx->P.as<uint32_t>(),
                                        ctx->cell_base.as<uint32_t>(), ctx->cell_cnt.as<uint32_t>(), g.nbins, nc,
                                        RB, nrb, ctx->F.as<uint32_t>());
@@ -3168,7 +3225,7 @@ static int run_segment(mgp_ctx* ctx, const Seg& sg, int slot, int& dup_parts, in
                                          ctx->n_reads.as<uint32_t>(), ctx->any_paired.as<uint8_t>(), pair_mode,
                                          ctx->covered.as<uint32_t>(), ctx->dsum.as<unsigned long long>(),
                                          ctx->dmax.as<uint32_t>(), ctx->tally_part.as<uint32_t>(), st, sg.w0,
-                                         ctx->roff_irregular.as<uint32_t>());
+                                         ctx->roff_irregular.as<uint32_t>(), ctx->chunk_perm.as<uint32_t>());
         HIP_TRY(hipGetLastError());
     }
     STAGE_END(ST_PILEUP);
@@ -3216,7 +3273,7 @@ static int run_finish(mgp_ctx* ctx, int slot, int dup_parts, bool streamed) {
 
         // 8. medians + pass flags, run statistics
         STAGE_BEGIN(ST_MEDIAN);
-        if (g.L <= kMedRegs * kBlock)
+        if (g.L < kMedRegs * kBlock)
             k_median<true><<<nc, kBlock, 0, s>>>(g, ctx->cfg.min_reads, ctx->depth16.as<uint16_t>(),
                                                  ctx->depth.as<uint32_t>(), ctx->wide.as<uint8_t>(),
                                                  ctx->n_reads.as<uint32_t>(), ctx->covered.as<uint32_t>(),

@@ -141,18 +141,27 @@ class ReadSoA:
     rec_off: np.ndarray
     payload: np.ndarray
     extra: dict = field(default_factory=dict)
+    _bam_order: bool | None = field(default=None, repr=False, compare=False)
 
     @property
     def n(self) -> int:
         return int(self.start.shape[0])
+
+    @property
+    def in_bam_order(self) -> bool:
+        """Whether the payload records follow the reads' order (computed once: slicing a
+        large batch into chunks must not rescan rec_off per chunk)."""
+        if self._bam_order is None:
+            ro = self.rec_off.astype(np.int64)
+            self._bam_order = not (self.n > 1 and bool(np.any(np.diff(ro) < 0)))
+        return self._bam_order
 
     def slice(self, lo: int, hi: int) -> ReadSoA:
         """Reads [lo, hi) as a standalone batch (payload re-based). A payload whose
         records are not in BAM order (paired placement) is gathered and re-placed."""
         if hi <= lo:
             return empty_soa()
-        ro = self.rec_off.astype(np.int64)
-        if self.n > 1 and np.any(np.diff(ro) < 0):
+        if not self.in_bam_order:
             from .shard import shard_soa
 
             sub = ReadSoA(self.start[lo:hi], self.bc[lo:hi], self.tlen[lo:hi], self.flag[lo:hi], self.mapq[lo:hi],
