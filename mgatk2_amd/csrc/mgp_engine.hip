@@ -139,7 +139,7 @@ struct mgp_ctx {
     bool no_spec = false;   // the speculative compact grouping failed on the resident reads (ERR_RESPEC)
     // the input check's flag bits of the last run over the same resident reads (no push,
     // reset or generation since): the next run picks its variants from them without the
-    // mid-run host wait, and k_check_stats verifies them on the device (ERR_RESPEC)
+    // mid-run host wait, and check_stats (pass B) verifies them on the device (ERR_RESPEC)
     bool bits_cached = false;
     uint32_t cached_bits = 0;
     bool stage_all = true;  // HIP events around every stage (false: the pileup's only, mgp_set_stage_timing)
@@ -406,22 +406,15 @@ __global__ void k_scan_rows(uint32_t* __restrict__ P, int nrb, int nc, uint32_t*
     cnt[c] = acc;
 }
 
-// Scan step c: exclusive scan over cells (single workgroup of 1024). With `perm`
-// (the cells' scan, not the bins'), it then orders the pileup's cell chunks of cpb
-// cells by size, largest first (a counting sort over 64 size classes): the pileup
-// takes its workgroups' chunks in that order, so the largest chunks are not the
-// grid's tail (lognormal cells: a chunk of 4 cells can hold twice the mean).
-__global__ void __launch_bounds__(1024) k_scan_cells(const uint32_t* __restrict__ cnt, int nc,
-                                                     uint32_t* __restrict__ base, int cpb = 0,
-                                                     int nchunks = 0, uint32_t* __restrict__ perm = nullptr) {
-    __shared__ uint32_t wsum[16];
-    __shared__ uint32_t carry;
-    if (threadIdx.x == 0) carry = 0;
+// Exclusive scan of cnt[0, n) into base by one workgroup of 1024; returns the total.
+__device__ uint32_t block_exclusive_scan(const uint32_t* __restrict__ cnt, int n, uint32_t* __restrict__ base,
+                                         uint32_t* wsum /* [16] LDS */, uint32_t* carry /* LDS */) {
+    if (threadIdx.x == 0) *carry = 0;
     __syncthreads();
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    for (int c0 = 0; c0 < nc; c0 += 1024) {
+    for (int c0 = 0; c0 < n; c0 += 1024) {
         int c = c0 + threadIdx.x;
-        uint32_t v = c < nc ? cnt[c] : 0;
+        uint32_t v = c < n ? cnt[c] : 0;
         uint32_t x = v;  // inclusive wave scan
         for (int o = 1; o < 64; o <<= 1) {
             uint32_t y = __shfl_up(x, o, 64);
@@ -439,17 +432,34 @@ __global__ void __launch_bounds__(1024) k_scan_cells(const uint32_t* __restrict_
             wsum[threadIdx.x] = xs - w;  // exclusive
         }
         __syncthreads();
-        uint32_t excl = carry + wsum[wid] + x - v;
-        if (c < nc) base[c] = excl;
+        uint32_t excl = *carry + wsum[wid] + x - v;
+        if (c < n) base[c] = excl;
         __syncthreads();
-        if (threadIdx.x == 1023) carry = excl + v;
+        if (threadIdx.x == 1023) *carry = excl + v;
         __syncthreads();
     }
-    if (perm == nullptr) return;
+    return *carry;
+}
+
+// Scan step c (single workgroup of 1024): exclusive scan over cells, and over the
+// start bins' valid counts (bin_valid -> bin_base, grouping pass A's bucket bases;
+// nbins = 0: none). Then it orders the pileup's cell chunks of cpb cells by size,
+// largest first (a counting sort over 64 size classes): the pileup takes its
+// workgroups' chunks in that order, so the largest chunks are not the grid's tail
+// (lognormal cells: a chunk of 4 cells can hold twice the mean).
+__global__ void __launch_bounds__(1024) k_scan_cells(const uint32_t* __restrict__ cnt, int nc,
+                                                     uint32_t* __restrict__ base, int cpb, int nchunks,
+                                                     uint32_t* __restrict__ perm,
+                                                     const uint32_t* __restrict__ bin_valid, int nbins,
+                                                     uint32_t* __restrict__ bin_base) {
+    __shared__ uint32_t wsum[16];
+    __shared__ uint32_t carry;
+    const int lane = threadIdx.x & 63;
+    if (nbins > 0) (void)block_exclusive_scan(bin_valid, nbins, bin_base, wsum, &carry);
+    const uint32_t total = block_exclusive_scan(cnt, nc, base, wsum, &carry);
     // chunk sizes from the cell bases this workgroup just wrote (visible to it behind
     // the barriers above); the last chunk ends at the total
     __shared__ uint32_t cls[64], s_max;
-    const uint32_t total = carry;
     auto size_of = [&](int ch) {
         const int c0 = ch * cpb, c1 = min(nc, c0 + cpb);
         return (c1 < nc ? base[c1] : total) - base[c0];
@@ -835,6 +845,22 @@ __global__ void __launch_bounds__(kGABlock, MGP_GA_WAVES) k_group_a(int64_t n, c
     }
 }
 
+// The input check's words into the run's stats (grouping pass B's first workgroup,
+// behind pass A): the pileup's halo span and the order check. spec_layout: 0, or the
+// one CHK_P64 / CHK_P32 layout a streaming segment assumed without the host's look at
+// the flag bits; reads it cannot serve make the run rerun resident. max_span is a
+// running maximum (a streaming run's segments accumulate it).
+__device__ __forceinline__ void check_stats(const uint32_t* __restrict__ ck, DevStats* st, uint32_t spec_layout) {
+    if (threadIdx.x == 0) {
+        const uint32_t b = ck[0];
+        st->max_span = max(st->max_span, ck[1]);
+        if (b & CHK_UNSORTED) atomicOr(&st->err, ERR_UNSORTED);
+        if (spec_layout && ((b & (CHK_FULL | CHK_P64 | CHK_P32 | CHK_NOSEQ) & ~spec_layout) ||
+                            ((b & CHK_PAIRED) && (b & CHK_UNPAIRED))))
+            atomicOr(&st->err, ERR_RESPEC);
+    }
+}
+
 // Pass B: workgroup = (cell group, bin range). A step takes the group's buckets
 // of as many consecutive bins as fit the LDS stage; each wave ranks the elements
 // of its bins (one bin at a time, stable: ballot peers + per-cell counters) and
@@ -1049,9 +1075,11 @@ __global__ void __launch_bounds__(kBlock, Tr::kWaves) k_group_b(const typename T
                                                     int mode, int unit, uint32_t* __restrict__ pel,
                                                     uint8_t* __restrict__ any_paired,
                                                     unsigned long long* __restrict__ dup_part, DevStats* st,
-                                                    int cnt_lo) {
+                                                    int cnt_lo, const uint32_t* __restrict__ ck,
+                                                    uint32_t spec_layout) {
     using T = typename Tr::T;
     constexpr bool kCompact = sizeof(T) == 8;
+    if (blockIdx.x == 0 && blockIdx.y == 0) check_stats(ck, st, spec_layout);
     if (__atomic_load_n(&st->err, __ATOMIC_RELAXED) & ERR_BOUNDS) return;  // unsorted input (k_bin_count)
     __shared__ T stage[kStageB];
     __shared__ uint32_t wcnt[kBlock / kWave][kGroup];
@@ -2425,7 +2453,8 @@ __global__ void __launch_bounds__(kBlock) k_median(Geom g, int min_reads, const 
 __global__ void __launch_bounds__(1024) k_run_stats(const uint32_t* __restrict__ n_reads,
                                                     const uint8_t* __restrict__ passed, int nc,
                                                     const unsigned long long* __restrict__ dup_part, int nparts,
-                                                    DevStats* st, int with_dups) {
+                                                    DevStats* st, int with_dups,
+                                                    const uint32_t* __restrict__ order_bad) {
     __shared__ unsigned long long red[5][1024 / kWave];
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     unsigned long long a = 0, b = 0, c = 0, d = 0, e = 0;
@@ -2452,6 +2481,8 @@ __global__ void __launch_bounds__(1024) k_run_stats(const uint32_t* __restrict__
         red[4][wid] = e;
     }
     __syncthreads();
+    // a streaming push found reads out of coordinate order (k_check_order)
+    if (threadIdx.x == 5 && *order_bad) atomicOr(&st->err, ERR_UNSORTED);
     if (threadIdx.x < 5) {
         unsigned long long t = 0;
         for (int w = 0; w < 1024 / kWave; ++w) t += red[threadIdx.x][w];
@@ -2573,21 +2604,6 @@ __global__ void k_check_inputs(const uint64_t* __restrict__ roff, const uint16_t
     if ((threadIdx.x & 63) == 0) {
         if (msp > __atomic_load_n(ck + 1, __ATOMIC_RELAXED)) atomicMax(ck + 1, msp);
         if (bits && (__atomic_load_n(ck, __ATOMIC_RELAXED) & bits) != bits) atomicOr(ck, bits);
-    }
-}
-
-// spec: the grouping took the speculative compact path without the host's look at
-// the flag bits (streaming segments): reads it cannot serve make the run rerun resident.
-// max_span is a running maximum (a streaming run's segments accumulate it).
-__global__ void k_check_stats(const uint32_t* __restrict__ ck, DevStats* st, uint32_t spec_layout) {
-    // spec_layout: 0, or the one CHK_P64 / CHK_P32 layout a streaming segment assumed
-    if (threadIdx.x == 0) {
-        const uint32_t b = ck[0];
-        st->max_span = max(st->max_span, ck[1]);
-        if (b & CHK_UNSORTED) atomicOr(&st->err, ERR_UNSORTED);
-        if (spec_layout && ((b & (CHK_FULL | CHK_P64 | CHK_P32 | CHK_NOSEQ) & ~spec_layout) ||
-                            ((b & CHK_PAIRED) && (b & CHK_UNPAIRED))))
-            atomicOr(&st->err, ERR_RESPEC);
     }
 }
 
@@ -3041,7 +3057,8 @@ static int run_segment(mgp_ctx* ctx, const Seg& sg, int slot, int& dup_parts, in
             ctx->H.as<uint32_t>(), ctx->PG.as<uint32_t>(), ngroups, ctx->bin_start.as<uint32_t>(),
             ctx->bin_valid.as<uint32_t>(), ctx->roff_irregular.as<uint32_t>(), st, sg.w0, sg.bhi);
         HIP_TRY(hipGetLastError());
-        if (!sg.stream) {
+        // (a rerun on an unchanged resident set takes the cached bits: no copy, no wait)
+        if (!sg.stream && !(ctx->bits_cached && !ctx->no_spec)) {
             HIP_TRY(hipMemcpyAsync(ctx->h_bits, ctx->roff_irregular.p, 8, hipMemcpyDeviceToHost, s));
             HIP_TRY(hipEventRecord(ctx->ev_bits, s));
         }
@@ -3056,7 +3073,8 @@ static int run_segment(mgp_ctx* ctx, const Seg& sg, int slot, int& dup_parts, in
     k_scan_colsum<<<g2, kBlock, 0, s>>>(ctx->H.as<uint32_t>(), g.nbins, nc, RB, ctx->P.as<uint32_t>());
     k_scan_rows<<<blocks_for(nc), kBlock, 0, s>>>(ctx->P.as<uint32_t>(), nrb, nc, ctx->cell_cnt.as<uint32_t>());
     k_scan_cells<<<1, 1024, 0, s>>>(ctx->cell_cnt.as<uint32_t>(), nc, ctx->cell_base.as<uint32_t>(), g.cpb,
-                                    g.nchunks, ctx->chunk_perm.as<uint32_t>());
+                                    g.nchunks, ctx->chunk_perm.as<uint32_t>(), ctx->bin_valid.as<uint32_t>(),
+                                    n > 0 ? g.nbins : 0, ctx->bin_base.as<uint32_t>());
     k_scan_apply<<<g2, kBlock, 0, s>>>(ctx->H.as<uint32_t>(), ctx->P.as<uint32_t>(),
                                        ctx->cell_base.as<uint32_t>(), ctx->cell_cnt.as<uint32_t>(), g.nbins, nc,
                                        RB, nrb, ctx->F.as<uint32_t>());
@@ -3077,7 +3095,7 @@ static int run_segment(mgp_ctx* ctx, const Seg& sg, int slot, int& dup_parts, in
     ctx->read_bits = 0;
     constexpr uint32_t kLayBits = CHK_FULL | CHK_P64 | CHK_P32;
     if (n > 0 && sg.stream) {
-        // the layout the run's first batch showed; k_check_stats makes the run rerun
+        // the layout the run's first batch showed; check_stats (pass B) makes the run rerun
         // resident if another one turns up
         spec = true;
         ctx->roff_mode = kOffSpec;
@@ -3133,7 +3151,6 @@ static int run_segment(mgp_ctx* ctx, const Seg& sg, int slot, int& dup_parts, in
     if (n > 0) {
         int gbits = 0;
         while (gbits < 31 && (1 << gbits) < ngroups) ++gbits;
-        k_scan_cells<<<1, 1024, 0, s>>>(ctx->bin_valid.as<uint32_t>(), g.nbins, ctx->bin_base.as<uint32_t>());
         const size_t a_lds = (size_t)ngroups * (1 + 2 * (kGABlock / kWave)) * 4 + (size_t)((nc + 31) / 32) * 4;
         if (a_lds > (size_t)ctx->lds_hist_max_cells * 4)
             return set_err(MGP_E_INVALID, "too many cells for one context (grouping LDS)");
@@ -3163,11 +3180,6 @@ static int run_segment(mgp_ctx* ctx, const Seg& sg, int slot, int& dup_parts, in
             launch_a(k_group_a<kOffR64, false>);
         }
         HIP_TRY(hipGetLastError());
-        // the check's span and order bits into the run's stats (the pileup's halo); a
-        // streaming segment also checks here the flag bits its variants assume
-        k_check_stats<<<1, 64, 0, s>>>(ctx->roff_irregular.as<uint32_t>(), st,
-                                       sg.stream ? (layout == kLayP32 ? CHK_P32 : CHK_P64) : check_layout);
-        HIP_TRY(hipGetLastError());
     }
     STAGE_END(ST_GROUP_A);
     STAGE_BEGIN(ST_GROUP_B);
@@ -3186,11 +3198,15 @@ static int run_segment(mgp_ctx* ctx, const Seg& sg, int slot, int& dup_parts, in
         const int cnt_lo = sg.w0 > 0 ? (int)((int64_t)sg.w0 * g.W / g.G) : 0;
         // per-read pairedness / SEQ tracking only when the reads mix paired and
         // unpaired ones or some read lacks SEQ/QUAL
+        // pass B's first workgroup also takes the input check's span and order bits into
+        // the run's stats (the pileup's halo); a streaming segment also checks there the
+        // flag bits its variants assume (check_stats)
+        const uint32_t spec_layout = sg.stream ? (layout == kLayP32 ? CHK_P32 : CHK_P64) : check_layout;
         auto launch_b = [&](auto kern, auto* gel) {
             kern<<<gb, kBlock, 0, s>>>(gel, ctx->bucket_off.as<uint32_t>(), ctx->H.as<uint32_t>(),
                                        g, ngroups, rb, ctx->cfg.dedup_mode, unit, ctx->pel.as<uint32_t>(),
                                        ctx->any_paired.as<uint8_t>(), ctx->dup_part.as<unsigned long long>(), st,
-                                       cnt_lo);
+                                       cnt_lo, ctx->roff_irregular.as<uint32_t>(), spec_layout);
         };
         if (compact) launch_b(k_group_b<false, GCompact>, ctx->gel2.as<unsigned long long>());
         else if (track) launch_b(k_group_b<true, GWide>, ctx->gel2.as<GElem>());
@@ -3288,12 +3304,15 @@ static int run_finish(mgp_ctx* ctx, int slot, int dup_parts, bool streamed) {
         HIP_TRY(hipGetLastError());
         k_run_stats<<<1, 1024, 0, s>>>(ctx->n_reads.as<uint32_t>(), ctx->passed.as<uint8_t>(), nc,
                                        ctx->dup_part.as<unsigned long long>(), streamed ? 0 : dup_parts, st,
-                                       streamed ? 0 : 1);
+                                       streamed ? 0 : 1, ctx->order_bad.as<uint32_t>());
         HIP_TRY(hipGetLastError());
         STAGE_END(ST_MEDIAN);
         HIP_TRY(hipStreamWaitEvent(s, ctx->ev_join, 0));
     } else {
         HIP_TRY(hipMemsetAsync(tally, 0, (size_t)g.L * 32, s));
+        // (with cells, k_run_stats takes the streaming order check)
+        k_order_err<<<1, 64, 0, s>>>(ctx->order_bad.as<uint32_t>(), st);
+        HIP_TRY(hipGetLastError());
     }
 
     // 9. tallies over ranks; the slot after them carries the ranks' ERR_RESPEC so that
@@ -3307,8 +3326,6 @@ static int run_finish(mgp_ctx* ctx, int slot, int dup_parts, bool streamed) {
         HIP_TRY(hipMemcpyAsync(ctx->h_respec, tally + (size_t)g.L * 4, 8, hipMemcpyDeviceToHost, s));
         STAGE_END(ST_COMM);
     }
-    k_order_err<<<1, 64, 0, s>>>(ctx->order_bad.as<uint32_t>(), st);
-    HIP_TRY(hipGetLastError());
     HIP_TRY(hipMemcpyAsync(ctx->host_stats, st, sizeof(DevStats), hipMemcpyDeviceToHost, s));
     return MGP_OK;
 }
