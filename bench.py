@@ -408,7 +408,10 @@ def pcie_leg(args, cfg, seed, cdf, ref, shard, device, comm_ranks, barrier, redu
     rb = 32 if p32 is not None else 64  # dense records in BAM order
     eng.synth(seed, args.reads, cdf, ref, read_len=args.read_len, rec_align=64, pack=True, pack32=p32, **shard)
     n, pay = eng.resident()
-    col_bytes = n * (4 + 4 + 4 + 2 + 1 + 4 + 8)
+    # the producer's columns: start, bc, tlen, flag, mapq. No rec_off (dense records in
+    # BAM order) and no span (taken from the records' CIGARs on the device): ABI v3.1
+    cols = ("start", "bc", "tlen", "flag", "mapq", "payload")
+    col_bytes = n * (4 + 4 + 4 + 2 + 1)
     hbuf = PinnedBuffer(col_bytes + pay + 4096)
     off = [0]
 
@@ -417,8 +420,8 @@ def pcie_leg(args, cfg, seed, cdf, ref, shard, device, comm_ranks, barrier, redu
         off[0] = (off[0] + m * np.dtype(dt).itemsize + 63) & ~63
         return a
 
-    host = eng.download_inputs(alloc=alloc)  # the producer's batches: pinned, BAM order
-    assert np.all(host.rec_off == rb * np.arange(n, dtype=np.uint64))
+    host = eng.download_inputs(columns=cols, alloc=alloc)  # the producer's batches: pinned, BAM order
+    assert np.all(eng.download_inputs(columns=("rec_off",)).rec_off == rb * np.arange(n, dtype=np.uint64))
     L, nc = cfg.mito_len, cfg.n_cells
     nw, W = eng.windows()
     rbuf = PinnedBuffer(nc * L * 22 + nc * nw + 4096)
@@ -426,17 +429,18 @@ def pcie_leg(args, cfg, seed, cdf, ref, shard, device, comm_ranks, barrier, redu
                   rbuf.array((nc, L), np.uint16, nc * L * 20), rbuf.array((nc, nw), np.uint8, nc * L * 22), W)
     if comm_ranks > 1:
         make_comm(eng)  # every run all-reduces its tallies, as in the timed steps
+    # the rows leave the device as the windows complete, beside the later batches' H2D
+    try:
+        eng.set_rows16_target(rows)
+        rows_target = True
+    except Exception as e:  # (pinned memory the device cannot map: copy the rows after the run)
+        print(f"[bench] rows target unavailable ({e}); rows fetched after the run", file=sys.stderr)
+        rows_target = False
 
     def batches_for(bs):
-        """Batches of bs reads with batch-relative record offsets (dense records: the
-        producer writes them so)."""
-        out = []
-        for a in range(0, n, bs):
-            b = min(n, a + bs)
-            host.rec_off[a:b] = rb * np.arange(b - a, dtype=np.uint64)
-            out.append(ReadSoA(host.start[a:b], host.bc[a:b], host.tlen[a:b], host.flag[a:b], host.mapq[a:b],
-                               host.span[a:b], host.rec_off[a:b], host.payload[rb * a:rb * b]))
-        return out
+        """Batches of bs reads: their columns and their slice of the dense payload."""
+        return [ReadSoA(host.start[a:b], host.bc[a:b], host.tlen[a:b], host.flag[a:b], host.mapq[a:b], None, None,
+                        host.payload[rb * a:rb * b]) for a, b in ((a, min(n, a + bs)) for a in range(0, n, bs))]
 
     def one(batches, stream):
         eng.set_streaming(stream)
@@ -446,8 +450,9 @@ def pcie_leg(args, cfg, seed, cdf, ref, shard, device, comm_ranks, barrier, redu
             eng.push(bt)
         t_push = time.perf_counter() - t0
         eng.run()
-        eng.fetch_rows16(0, nc, out=rows)
-        r = eng.fetch(dense=False)
+        if not rows_target:
+            eng.fetch_rows16(0, nc, out=rows)
+        r = eng.fetch(dense=False)  # (waits for the rows' copies too)
         return time.perf_counter() - t0, t_push, r
 
     legs = []
@@ -475,11 +480,14 @@ def pcie_leg(args, cfg, seed, cdf, ref, shard, device, comm_ranks, barrier, redu
     return {
         "value": best["value"],
         "unit": "reads/s",
-        "what": "pinned host SoA batches -> H2D (streamed: windows run as their reads arrive) -> run -> 16-bit "
-                "count rows + per-cell stats in pinned host memory; max over ranks",
+        "what": "pinned host SoA batches (start, bc, tlen, flag, mapq + dense 32-byte records; no rec_off or span "
+                "columns: ABI v3.1) -> H2D (streamed: windows run as their reads arrive, and their 16-bit count rows "
+                "go back D2H as each window completes) -> run -> every row + per-cell stats in pinned host memory; "
+                "max over ranks",
         "h2d_bytes_rank0": h2d,
         "d2h_bytes_rank0": d2h,
         "link_GBps_rank0": round((h2d + d2h) / best["s"] / 1e9, 2),
+        "rows_target": rows_target,
         "legs": legs,
         "stats_total_reads_rank0": stats["total_reads"],
     }

@@ -336,8 +336,11 @@ typedef struct mgp_batch {
     const int32_t  *tlen;       /* signed template_length                           */
     const uint16_t *flag;       /* BAM flag | MGP_FLAG_NOSEQQUAL                    */
     const uint8_t  *mapq;       /* mapping_quality                                  */
-    const uint32_t *span;       /* max(reference span of the CIGAR, l_seq)          */
-    const uint64_t *rec_off;    /* byte offset of record i inside `payload`         */
+    const uint32_t *span;       /* max(reference span of the CIGAR, l_seq); NULL: taken
+                                   from the records' CIGARs on the device (ABI v3.1)     */
+    const uint64_t *rec_off;    /* byte offset of record i inside `payload`; NULL: dense
+                                   records in BAM order, record i at i x payload_bytes /
+                                   n_reads (a multiple of 16; ABI v3.1)                  */
     const uint8_t  *payload;
     int64_t         payload_bytes;
 } mgp_batch;
@@ -465,6 +468,16 @@ int  mgp_fetch(mgp_ctx *ctx, mgp_result *out);
 int  mgp_fetch_cells(mgp_ctx *ctx, int32_t lo, int32_t hi, mgp_result *out);
 /* The 16-bit result rows of cells [lo, hi) (implies mgp_sync); NULL members are skipped. */
 int  mgp_fetch_rows16(mgp_ctx *ctx, int32_t lo, int32_t hi, mgp_rows16 *out);
+/* ABI v3.1: the 16-bit rows of every cell go to `rows` (pinned host arrays for all
+ * cells from mgp_host_alloc, written by the device through their mapping) as the
+ * windows complete: each streaming segment writes its windows' rows on a
+ * device-to-host stream behind its pileup, while the copies of
+ * later batches still run the other way; the wide flags follow the run, and mgp_sync
+ * waits for all of it. The caller then needs no mgp_fetch_rows16. Needs min_reads <= 1
+ * (the gate rewrites rows after the pileup: MGP_E_STATE); NULL stops it. Replaces the
+ * reference's per-cell write_cell after each worker (processors.py:112-144): results
+ * leave the device while ingest continues. */
+int  mgp_set_rows16_target(mgp_ctx *ctx, const mgp_rows16 *rows);
 /* Position windows of the pileup (the `wide` flags' second dimension). */
 int  mgp_windows(mgp_ctx *ctx, int32_t *n_windows, int32_t *window_width);
 /* Streaming on (1) or off (0) for the next pushes (initially MGP_CFG_STREAM). */

@@ -116,6 +116,12 @@ struct mgp_ctx {
     int dev = 0;
     hipStream_t s_comp = nullptr, s_copy = nullptr;
     hipStream_t s_side = nullptr;  // the tally reduction, concurrent with the medians
+    // mgp_set_rows16_target: the 16-bit rows of each segment's windows go to these pinned
+    // host arrays on their own stream as soon as the segment's pileup ends
+    hipStream_t s_d2h = nullptr;
+    hipEvent_t ev_rows = nullptr;
+    mgp_rows16 rows_tgt{};
+    bool rows_on = false;
     hipEvent_t ev_copy = nullptr, ev_fork = nullptr, ev_join = nullptr;
     hipEvent_t ev_bits = nullptr;  // the run's input check words have reached h_bits
     uint32_t* h_bits = nullptr;    // pinned host copy of the input check words (roff_irregular)
@@ -2544,6 +2550,58 @@ __global__ void __launch_bounds__(kBlock) k_expand(Geom g, int64_t p0, int64_t n
     if (depth) depth[P] = o16.depth[P];
 }
 
+// mgp_set_rows16_target: positions [p0, p1) of every cell's 16-bit rows into the pinned
+// host target (device-mapped: vector stores over PCIe, consecutive lanes consecutive
+// addresses, so they leave as full-width writes)
+__global__ void __launch_bounds__(kBlock) k_rows_to_host(int L, int nc, int p0, int p1, const uint4* __restrict__ c16,
+                                                         const uint32_t* __restrict__ t16,
+                                                         const uint16_t* __restrict__ d16, uint4* __restrict__ hc,
+                                                         uint32_t* __restrict__ ht, uint16_t* __restrict__ hd) {
+    const int p = p0 + (int)(blockIdx.x * blockDim.x + threadIdx.x);
+    if (p >= p1) return;
+    for (int c = blockIdx.y; c < nc; c += gridDim.y) {
+        const size_t P = (size_t)c * L + p;
+        hc[P] = c16[P];
+        ht[P] = t16[P];
+        hd[P] = d16[P];
+    }
+}
+
+// mgp_push_batch without rec_off: dense records in BAM order, record i at base + i x stride
+__global__ void k_dense_off(uint64_t* __restrict__ roff, int64_t n, uint64_t base, uint64_t stride) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) roff[i] = base + (uint64_t)i * stride;
+}
+
+// mgp_push_batch without span: max(reference span of the CIGAR, l_seq) of each read from
+// its record (include/mgpileup.h, the three layouts), as the BAM decoder computes it
+// (M, D, N, =, X consume the reference)
+__global__ void k_record_span(const uint8_t* __restrict__ payload, const uint64_t* __restrict__ roff,
+                              const uint16_t* __restrict__ flag, int64_t n, uint32_t* __restrict__ span) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint8_t* rec = payload + roff[i];
+    const uint4 h = *reinterpret_cast<const uint4*>(rec);
+    const uint32_t f = flag[i];
+    const bool p32 = (f & MGP_FLAG_PACK32) != 0, packed = (f & (MGP_FLAG_PACKED | MGP_FLAG_PACK32)) != 0;
+    const uint32_t lseq = p32 ? ((h.x >> 16) & 0xFFu) : packed ? (h.y & 0xFFu) : h.y;
+    const uint32_t ncig = p32 ? ((h.x >> 24) & 7u) : packed ? ((h.y >> 8) & 0x7Fu) : (h.z & 0xFFFFu);
+    auto consumes = [](uint32_t op) { return op == 0u || op == 2u || op == 3u || op == 7u || op == 8u; };
+    uint64_t ref = 0;
+    if (packed) {
+        const uint32_t cw[4] = {p32 ? (h.y & 0xFFFFu) : (h.y >> 16), p32 ? (h.y >> 16) : (h.z & 0xFFFFu),
+                                p32 ? (h.z & 0xFFFFu) : (h.z >> 16), p32 ? (h.z >> 16) : (h.w & 0xFFFFu)};
+#pragma unroll
+        for (int o = 0; o < 4; ++o)
+            if ((uint32_t)o < ncig && consumes(cw[o] & 15u)) ref += cw[o] >> 4;
+    } else {
+        const uint32_t* cig = reinterpret_cast<const uint32_t*>(rec + h.w);
+        for (uint32_t o = 0; o < ncig; ++o)
+            if (consumes(cig[o] & 15u)) ref += cig[o] >> 4;
+    }
+    span[i] = (uint32_t)max<uint64_t>(min<uint64_t>(ref, 0xFFFFFFFFull), lseq);
+}
+
 __global__ void k_add_u64(uint64_t* __restrict__ a, int64_t n, uint64_t add) {
     int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i < n) a[i] += add;
@@ -2770,6 +2828,8 @@ int mgp_open(const mgp_config* cfg, int hip_device, mgp_ctx** out) {
     HIP_TRY(hipStreamCreateWithFlags(&ctx->s_comp, hipStreamNonBlocking));
     HIP_TRY(hipStreamCreateWithFlags(&ctx->s_copy, hipStreamNonBlocking));
     HIP_TRY(hipStreamCreateWithFlags(&ctx->s_side, hipStreamNonBlocking));
+    HIP_TRY(hipStreamCreateWithFlags(&ctx->s_d2h, hipStreamNonBlocking));
+    HIP_TRY(hipEventCreateWithFlags(&ctx->ev_rows, hipEventDisableTiming));
     HIP_TRY(hipEventCreateWithFlags(&ctx->ev_copy, hipEventDisableTiming));
     HIP_TRY(hipEventCreateWithFlags(&ctx->ev_fork, hipEventDisableTiming));
     HIP_TRY(hipEventCreateWithFlags(&ctx->ev_join, hipEventDisableTiming));
@@ -2810,6 +2870,7 @@ void mgp_close(mgp_ctx* ctx) {
     (void)hipStreamSynchronize(ctx->s_comp);
     (void)hipStreamSynchronize(ctx->s_copy);
     (void)hipStreamSynchronize(ctx->s_side);
+    (void)hipStreamSynchronize(ctx->s_d2h);
     if (ctx->comm) ncclCommDestroy(ctx->comm);
     DevBuf* bufs[] = {&ctx->start,     &ctx->bc,        &ctx->tlen,     &ctx->flag,       &ctx->mapq,
                       &ctx->span,      &ctx->roff,      &ctx->payload,  &ctx->bin_start,  &ctx->gel2,
@@ -2836,6 +2897,8 @@ void mgp_close(mgp_ctx* ctx) {
     (void)hipStreamDestroy(ctx->s_comp);
     (void)hipStreamDestroy(ctx->s_copy);
     (void)hipStreamDestroy(ctx->s_side);
+    (void)hipStreamDestroy(ctx->s_d2h);
+    (void)hipEventDestroy(ctx->ev_rows);
     delete ctx;
 }
 
@@ -2880,8 +2943,15 @@ int mgp_push_batch(mgp_ctx* ctx, const mgp_batch* b) {
     if (!ctx || !b) return set_err(MGP_E_INVALID, "null ctx/batch");
     if (b->n_reads < 0 || b->payload_bytes < 0) return set_err(MGP_E_INVALID, "negative sizes");
     if (b->n_reads == 0) return MGP_OK;
-    if (!b->start || !b->bc || !b->tlen || !b->flag || !b->mapq || !b->span || !b->rec_off || !b->payload)
+    if (!b->start || !b->bc || !b->tlen || !b->flag || !b->mapq || !b->payload)
         return set_err(MGP_E_INVALID, "null batch array");
+    // rec_off NULL: dense records in BAM order (record i at i x payload_bytes / n_reads);
+    // span NULL: the spans come from the records' CIGARs on the device
+    const bool dense = b->rec_off == nullptr;
+    const int64_t stride = dense ? b->payload_bytes / b->n_reads : 0;
+    if (dense && (stride * b->n_reads != b->payload_bytes || stride < 16 || stride % 16 != 0))
+        return set_err(MGP_E_INVALID, "rec_off NULL needs payload_bytes = n_reads x a record stride that is a "
+                                      "multiple of 16");
     if (ctx->n + b->n_reads > (int64_t)0xFFFFFFFEll)
         return set_err(MGP_E_INVALID, "more than 2^32-2 resident reads per context; shard or batch the run");
     HIP_TRY(hipSetDevice(ctx->dev));
@@ -2894,13 +2964,25 @@ int mgp_push_batch(mgp_ctx* ctx, const mgp_batch* b) {
     HIP_TRY(hipMemcpyAsync(ctx->tlen.as<int32_t>() + n0, b->tlen, nb * 4, hipMemcpyHostToDevice, s));
     HIP_TRY(hipMemcpyAsync(ctx->flag.as<uint16_t>() + n0, b->flag, nb * 2, hipMemcpyHostToDevice, s));
     HIP_TRY(hipMemcpyAsync(ctx->mapq.as<uint8_t>() + n0, b->mapq, nb, hipMemcpyHostToDevice, s));
-    HIP_TRY(hipMemcpyAsync(ctx->span.as<uint32_t>() + n0, b->span, nb * 4, hipMemcpyHostToDevice, s));
-    HIP_TRY(hipMemcpyAsync(ctx->roff.as<uint64_t>() + n0, b->rec_off, nb * 8, hipMemcpyHostToDevice, s));
+    if (b->span)
+        HIP_TRY(hipMemcpyAsync(ctx->span.as<uint32_t>() + n0, b->span, nb * 4, hipMemcpyHostToDevice, s));
+    if (!dense)
+        HIP_TRY(hipMemcpyAsync(ctx->roff.as<uint64_t>() + n0, b->rec_off, nb * 8, hipMemcpyHostToDevice, s));
     if (b->payload_bytes)
         HIP_TRY(hipMemcpyAsync(ctx->payload.as<uint8_t>() + pay0, b->payload, b->payload_bytes,
                                hipMemcpyHostToDevice, s));
-    if (pay0) {
+    if (dense) {
+        k_dense_off<<<blocks_for(nb), kBlock, 0, s>>>(ctx->roff.as<uint64_t>() + n0, nb, (uint64_t)pay0,
+                                                      (uint64_t)stride);
+        HIP_TRY(hipGetLastError());
+    } else if (pay0) {
         k_add_u64<<<blocks_for(nb), kBlock, 0, s>>>(ctx->roff.as<uint64_t>() + n0, nb, (uint64_t)pay0);
+        HIP_TRY(hipGetLastError());
+    }
+    if (!b->span) {
+        k_record_span<<<blocks_for(nb), kBlock, 0, s>>>(ctx->payload.as<uint8_t>(), ctx->roff.as<uint64_t>() + n0,
+                                                        ctx->flag.as<uint16_t>() + n0, nb,
+                                                        ctx->span.as<uint32_t>() + n0);
         HIP_TRY(hipGetLastError());
     }
     if (ctx->stream) {
@@ -2925,6 +3007,7 @@ int mgp_reset(mgp_ctx* ctx) {
     HIP_TRY(hipSetDevice(ctx->dev));
     HIP_TRY(hipStreamSynchronize(ctx->s_copy));
     HIP_TRY(hipStreamSynchronize(ctx->s_comp));
+    HIP_TRY(hipStreamSynchronize(ctx->s_d2h));  // (a rows target's copies read rows the next run rewrites)
     HIP_TRY(hipMemsetAsync(ctx->order_bad.p, 0, 4, ctx->s_copy));
     HIP_TRY(hipEventRecord(ctx->ev_copy, ctx->s_copy));
     ctx->n = 0;
@@ -3243,6 +3326,22 @@ static int run_segment(mgp_ctx* ctx, const Seg& sg, int slot, int& dup_parts, in
                                          ctx->dmax.as<uint32_t>(), ctx->tally_part.as<uint32_t>(), st, sg.w0,
                                          ctx->roff_irregular.as<uint32_t>(), ctx->chunk_perm.as<uint32_t>());
         HIP_TRY(hipGetLastError());
+        // the windows' rows are final now (all cells): to the host target behind them,
+        // while later batches are still being copied in (mgp_set_rows16_target)
+        if (ctx->rows_on) {
+            // written by a kernel into the mapped pinned target (a strided 2D copy of
+            // 10k rows per segment runs as row-by-row DMA transfers: 4x slower overall)
+            const int p0 = sg.w0 * g.W, p1 = std::min(g.L, sg.w1 * g.W);
+            HIP_TRY(hipEventRecord(ctx->ev_rows, s));
+            HIP_TRY(hipStreamWaitEvent(ctx->s_d2h, ctx->ev_rows, 0));
+            const mgp_rows16& t = ctx->rows_tgt;
+            dim3 gr((unsigned)((p1 - p0 + kBlock - 1) / kBlock), (unsigned)std::min(nc, 65535));
+            k_rows_to_host<<<gr, kBlock, 0, ctx->s_d2h>>>(g.L, nc, p0, p1, ctx->counts16.as<uint4>(),
+                                                        ctx->tn5_16.as<uint32_t>(), ctx->depth16.as<uint16_t>(),
+                                                        reinterpret_cast<uint4*>(t.counts),
+                                                        reinterpret_cast<uint32_t*>(t.tn5), t.depth);
+            HIP_TRY(hipGetLastError());
+        }
     }
     STAGE_END(ST_PILEUP);
     return MGP_OK;
@@ -3315,6 +3414,14 @@ static int run_finish(mgp_ctx* ctx, int slot, int dup_parts, bool streamed) {
         HIP_TRY(hipGetLastError());
     }
 
+    // the wide flags of the rows target (the pileups of every segment are behind)
+    if (ctx->rows_on && nc > 0) {
+        HIP_TRY(hipEventRecord(ctx->ev_rows, s));
+        HIP_TRY(hipStreamWaitEvent(ctx->s_d2h, ctx->ev_rows, 0));
+        HIP_TRY(hipMemcpyAsync(ctx->rows_tgt.wide, ctx->wide.p, (size_t)nc * g.nwin, hipMemcpyDeviceToHost,
+                               ctx->s_d2h));
+    }
+
     // 9. tallies over ranks; the slot after them carries the ranks' ERR_RESPEC so that
     // every rank reruns when one has to (the reruns' all-reduces then match up)
     if (ctx->comm) {
@@ -3385,6 +3492,7 @@ int mgp_sync(mgp_ctx* ctx) {
     if (!ctx->ran) return set_err(MGP_E_STATE, "no run to wait for");
     HIP_TRY(hipSetDevice(ctx->dev));
     HIP_TRY(hipStreamSynchronize(ctx->s_comp));
+    if (ctx->rows_on) HIP_TRY(hipStreamSynchronize(ctx->s_d2h));
     const uint32_t e = ctx->host_stats->err;
     // some read did not fit the speculative grouping (on any rank, with a communicator):
     // run again on the fallback path, once
@@ -3484,6 +3592,37 @@ int mgp_windows(mgp_ctx* ctx, int32_t* n_windows, int32_t* window_width) {
     if (!ctx) return set_err(MGP_E_INVALID, "null ctx");
     if (n_windows) *n_windows = ctx->g.nwin;
     if (window_width) *window_width = ctx->g.W;
+    return MGP_OK;
+}
+
+int mgp_set_rows16_target(mgp_ctx* ctx, const mgp_rows16* rows) {
+    if (!ctx) return set_err(MGP_E_INVALID, "null ctx");
+    if (ctx->seg_open) return set_err(MGP_E_STATE, "a streaming run is in progress (mgp_run or mgp_reset first)");
+    HIP_TRY(hipSetDevice(ctx->dev));
+    HIP_TRY(hipStreamSynchronize(ctx->s_d2h));
+    if (!rows) {
+        ctx->rows_on = false;
+        return MGP_OK;
+    }
+    if (!rows->counts || !rows->tn5 || !rows->depth || !rows->wide) return set_err(MGP_E_INVALID, "null rows array");
+    // the min-reads gate rewrites the rows of the cells it drops after the pileup
+    if (ctx->cfg.min_reads > 1) return set_err(MGP_E_STATE, "a rows target needs min_reads <= 1");
+    // the kernel writes the rows through the device's mapping of the pinned arrays
+    mgp_rows16 d{};
+    void* dp = nullptr;
+    if (hipHostGetDevicePointer(&dp, rows->counts, 0) != hipSuccess || !dp)
+        return set_err(MGP_E_INVALID, "rows target not in pinned host memory (mgp_host_alloc)");
+    d.counts = static_cast<uint16_t*>(dp);
+    if (hipHostGetDevicePointer(&dp, rows->tn5, 0) != hipSuccess || !dp)
+        return set_err(MGP_E_INVALID, "rows target not in pinned host memory (mgp_host_alloc)");
+    d.tn5 = static_cast<uint16_t*>(dp);
+    if (hipHostGetDevicePointer(&dp, rows->depth, 0) != hipSuccess || !dp)
+        return set_err(MGP_E_INVALID, "rows target not in pinned host memory (mgp_host_alloc)");
+    d.depth = static_cast<uint16_t*>(dp);
+    d.wide = rows->wide;  // (an async copy: the host pointer)
+    (void)hipGetLastError();
+    ctx->rows_tgt = d;
+    ctx->rows_on = true;
     return MGP_OK;
 }
 

@@ -38,7 +38,7 @@ ABI_SYMBOLS = (
     "mgp_host_free", "mgp_push_batch", "mgp_reset", "mgp_resident", "mgp_run", "mgp_sync", "mgp_fetch",
     "mgp_finish", "mgp_kernel_times", "mgp_comm_unique_id", "mgp_comm_init", "mgp_synth_generate",
     "mgp_download_inputs", "mgp_set_stage_timing", "mgp_fetch_cells", "mgp_fetch_rows16", "mgp_windows",
-    "mgp_stream_info", "mgp_set_streaming",
+    "mgp_stream_info", "mgp_set_streaming", "mgp_set_rows16_target",
 )
 ABI_VERSION = 3
 CFG_KEEP_TN5 = 0x1
@@ -182,6 +182,7 @@ def load_library(path: Path | None = None) -> C.CDLL:
         "mgp_download_inputs": ([vp] + [vp] * 8, C.c_int),
         "mgp_fetch_cells": ([vp, i32, i32, C.POINTER(mgp_result)], C.c_int),
         "mgp_fetch_rows16": ([vp, i32, i32, C.POINTER(mgp_rows16)], C.c_int),
+        "mgp_set_rows16_target": ([vp, C.POINTER(mgp_rows16)], C.c_int),
         "mgp_windows": ([vp, C.POINTER(i32), C.POINTER(i32)], C.c_int),
         "mgp_stream_info": ([vp, C.POINTER(i64), C.POINTER(i32)], C.c_int),
         "mgp_set_streaming": ([vp, C.c_int], C.c_int),
@@ -315,8 +316,13 @@ class Rows16:
 
 
 def batch_struct(soa: ReadSoA) -> mgp_batch:
+    """The C batch of a ReadSoA. ``span`` and ``rec_off`` may be None (ABI v3.1): the
+    spans then come from the records' CIGARs on the device, and the records are dense
+    in BAM order (record i at i x payload bytes / n)."""
     for name in ("start", "bc", "tlen", "flag", "mapq", "span", "rec_off", "payload"):
         a = getattr(soa, name)
+        if a is None and name in ("span", "rec_off"):
+            continue
         if not a.flags["C_CONTIGUOUS"]:
             raise InvalidInputError(f"batch array {name} must be C-contiguous")
     return mgp_batch(
@@ -479,6 +485,23 @@ class Engine:
         r = mgp_rows16(_ptr(out.counts), _ptr(out.tn5), _ptr(out.depth), _ptr(out.wide))
         _ck(self.lib.mgp_fetch_rows16(self._h, int(lo), int(hi), C.byref(r)), "mgp_fetch_rows16")
         return out
+
+    def set_rows16_target(self, rows: Rows16 | None):
+        """mgp_set_rows16_target: every run's 16-bit rows of all cells go to `rows`
+        (pinned arrays, e.g. PinnedBuffer views) as its windows complete; sync() waits
+        for them. None stops it."""
+        if rows is None:
+            _ck(self.lib.mgp_set_rows16_target(self._h, None), "mgp_set_rows16_target")
+            self._rows_tgt = None
+            return
+        nw, _ = self.windows()
+        L, m = self.cfg.mito_len, self.cfg.n_cells
+        for a, shape in ((rows.counts, (m, L, 8)), (rows.tn5, (m, L, 2)), (rows.depth, (m, L)), (rows.wide, (m, nw))):
+            if a.shape != shape or not a.flags["C_CONTIGUOUS"]:
+                raise InvalidInputError(f"rows16 array of shape {a.shape}, expected {shape}")
+        r = mgp_rows16(_ptr(rows.counts), _ptr(rows.tn5), _ptr(rows.depth), _ptr(rows.wide))
+        _ck(self.lib.mgp_set_rows16_target(self._h, C.byref(r)), "mgp_set_rows16_target")
+        self._rows_tgt = rows  # kept alive while the engine copies into it
 
     def set_streaming(self, on: bool):
         """Streaming runs on or off for the next pushes (EngineConfig.stream initially)."""

@@ -360,3 +360,107 @@ def test_repeated_resident_runs_reuse_the_check_bits(engine_lib, oracle_lib):
     assert_same(first, exp_a, "first run")
     exp, _ = oracle_lib.oracle_run(cfg, concat_soa([a, b]))
     assert_same(got, exp, "after push")
+
+
+# ---------------------------------------------------------------------------
+# ABI v3.1: batches without rec_off (dense records in BAM order) and without span
+# (the spans from the records' CIGARs on the device)
+# ---------------------------------------------------------------------------
+def _columnless(soa, a, b, stride):
+    from mgatk2_amd.synth import ReadSoA
+
+    return ReadSoA(soa.start[a:b], soa.bc[a:b], soa.tlen[a:b], soa.flag[a:b], soa.mapq[a:b], None, None,
+                   np.ascontiguousarray(soa.payload[stride * a:stride * b]))
+
+
+@pytest.mark.parametrize("layout", ["p32", "p64", "full"])
+@pytest.mark.parametrize("streamed", [False, True])
+def test_push_without_offsets_and_spans(engine_lib, layout, streamed):
+    """The same reads pushed with and without their rec_off / span columns (three
+    batches, resident and streaming): identical results, and the device's spans
+    equal the producer's (max(reference span of the CIGAR, l_seq), the BAM
+    decoder's definition) for every read, whatever its CIGAR."""
+    from dataclasses import replace
+
+    from mgatk2_amd.engine import EngineConfig
+    from mgatk2_amd.synth import relocate, synth_reads
+
+    cfg = EngineConfig(n_cells=30, **CONFIGS["run"])
+    kw = dict(pack32=cfg.min_baseq) if layout == "p32" else dict(pack=layout == "p64")
+    soa = synth_reads(515, 150_000, 30, **kw)
+    stride = {"p32": 32, "p64": 64, "full": 128}[layout]
+    soa = relocate(soa, rec_align=stride, n_cells=30)  # dense, BAM order
+    assert np.array_equal(soa.rec_off, stride * np.arange(soa.n, dtype=np.uint64)), "dense placement"
+    want = run_resident(engine_lib, cfg, soa)
+    scfg = replace(cfg, stream=True, reserve_reads=soa.n, reserve_payload=int(soa.payload.shape[0]) + 4096) \
+        if streamed else cfg
+    cuts = [0, soa.n // 3, (2 * soa.n) // 3 + 7, soa.n]
+    with engine_lib.Engine(scfg) as eng:
+        for a, b in zip(cuts[:-1], cuts[1:]):
+            eng.push(_columnless(soa, a, b, stride))
+        got = eng.finish()
+        dev = eng.download_inputs(columns=("span",))
+    assert_same(got, want, f"{layout} streamed={streamed}")
+    np.testing.assert_array_equal(dev.span, soa.span)
+
+
+def test_push_without_offsets_rejects_ragged_payloads(engine_lib):
+    from mgatk2_amd.engine import EngineConfig
+    from mgatk2_amd.exceptions import InvalidInputError
+    from mgatk2_amd.synth import relocate, synth_reads
+
+    soa = relocate(synth_reads(516, 1_000, 4, pack32=20), rec_align=32, n_cells=4)
+    bad = _columnless(soa, 0, soa.n, 32)
+    bad.payload = bad.payload[:-16]  # not n x a stride
+    with engine_lib.Engine(EngineConfig(n_cells=4, min_baseq=20)) as eng:
+        with pytest.raises(InvalidInputError):
+            eng.push(bad)
+
+
+# ---------------------------------------------------------------------------
+# ABI v3.1: a rows target (the 16-bit rows leave the device as the windows complete)
+# ---------------------------------------------------------------------------
+@pytest.mark.parametrize("streamed", [False, True])
+def test_rows16_target_equals_fetch_rows16(engine_lib, streamed):
+    """The rows copied to a pinned target segment by segment equal mgp_fetch_rows16
+    of a resident run, for a streamed run of 4 batches and a resident one, also on a
+    rerun of the same context; a min_reads > 1 context refuses a target."""
+    from dataclasses import replace
+
+    from mgatk2_amd.engine import EngineConfig, PinnedBuffer, Rows16
+    from mgatk2_amd.exceptions import ProcessingError
+    from mgatk2_amd.synth import synth_reads
+
+    nc = 40
+    cfg = EngineConfig(n_cells=nc, **CONFIGS["run"])
+    soa = synth_reads(717, 200_000, nc, pack32=cfg.min_baseq)
+    with engine_lib.Engine(cfg) as eng:
+        eng.push(soa)
+        eng.run()
+        want = eng.fetch_rows16()
+        want_res = eng.fetch()
+    L = cfg.mito_len
+    nw = want.wide.shape[1]
+    buf = PinnedBuffer(nc * L * 22 + nc * nw + 64)
+    tgt = Rows16(buf.array((nc, L, 8), np.uint16, 0), buf.array((nc, L, 2), np.uint16, nc * L * 16),
+                 buf.array((nc, L), np.uint16, nc * L * 20), buf.array((nc, nw), np.uint8, nc * L * 22), want.window_width)
+    scfg = replace(cfg, stream=True, reserve_reads=soa.n, reserve_payload=int(soa.payload.shape[0]) + 4096) \
+        if streamed else cfg
+    with engine_lib.Engine(scfg) as eng:
+        eng.set_rows16_target(tgt)
+        for rep in range(2):
+            for a in (tgt.counts, tgt.tn5, tgt.depth, tgt.wide):
+                a.fill(0xAB)
+            eng.reset()
+            cuts = np.linspace(0, soa.n, 5).astype(int)
+            for a, b in zip(cuts[:-1], cuts[1:]):
+                eng.push(soa.slice(int(a), int(b)))
+            eng.run()
+            got = eng.fetch()
+            for k in ("counts", "tn5", "depth", "wide"):
+                np.testing.assert_array_equal(getattr(tgt, k), getattr(want, k), err_msg=f"{k} rep {rep}")
+            assert_same(got, want_res, f"rows target streamed={streamed} rep {rep}")
+        eng.set_rows16_target(None)
+    with engine_lib.Engine(replace(cfg, min_reads=2)) as eng:
+        with pytest.raises(ProcessingError):
+            eng.set_rows16_target(tgt)
