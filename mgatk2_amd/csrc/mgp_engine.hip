@@ -387,9 +387,10 @@ __global__ void __launch_bounds__(kHistBlock) k_bin_count(const int32_t* __restr
     }
 }
 
-// Scan step a: column sums over blocks of RB rows. grid (ceil(nc/256), nrb)
+// Scan step a: column sums over blocks of RB rows, and the cells' totals (zeroed by
+// k_run_init). grid (ceil(nc/256), nrb)
 __global__ void k_scan_colsum(const uint32_t* __restrict__ H, int nrows, int nc, int RB,
-                              uint32_t* __restrict__ P) {
+                              uint32_t* __restrict__ P, uint32_t* __restrict__ cnt) {
     int c = blockIdx.x * blockDim.x + threadIdx.x;
     int rb = blockIdx.y;
     if (c >= nc) return;
@@ -397,21 +398,11 @@ __global__ void k_scan_colsum(const uint32_t* __restrict__ H, int nrows, int nc,
     uint32_t acc = 0;
     for (int r = r0; r < r1; ++r) acc += H[(size_t)r * nc + c];
     P[(size_t)rb * nc + c] = acc;
+    if (acc) atomicAdd(&cnt[c], acc);
 }
 
-// Scan step b: exclusive scan over row blocks per cell; per-cell totals.
-__global__ void k_scan_rows(uint32_t* __restrict__ P, int nrb, int nc, uint32_t* __restrict__ cnt) {
-    int c = blockIdx.x * blockDim.x + threadIdx.x;
-    if (c >= nc) return;
-    uint32_t acc = 0;
-    for (int rb = 0; rb < nrb; ++rb) {
-        uint32_t v = P[(size_t)rb * nc + c];
-        P[(size_t)rb * nc + c] = acc;
-        acc += v;
-    }
-    cnt[c] = acc;
-}
-
+// (Scan step b, before r03 v55: the exclusive scan over row blocks per cell and the
+// cells' totals in a kernel of its own; k_scan_apply now sums its row-block prefix.)
 // Exclusive scan of cnt[0, n) into base by one workgroup of 1024; returns the total.
 __device__ uint32_t block_exclusive_scan(const uint32_t* __restrict__ cnt, int n, uint32_t* __restrict__ base,
                                          uint32_t* wsum /* [16] LDS */, uint32_t* carry /* LDS */) {
@@ -504,7 +495,11 @@ __global__ void k_scan_apply(uint32_t* __restrict__ H, const uint32_t* __restric
     int rb = blockIdx.y;
     if (c >= nc) return;
     const uint32_t b0 = base[c];
-    uint32_t acc = b0 + P[(size_t)rb * nc + c];
+    // the cell's reads in the row blocks before this one (independent loads)
+    uint32_t pre = 0;
+#pragma unroll 8
+    for (int q = 0; q < rb; ++q) pre += P[(size_t)q * nc + c];
+    uint32_t acc = b0 + pre;
     int r0 = rb * RB, r1 = min(nrows, r0 + RB);
     const size_t fw = (size_t)(nc + 31) / 32;
     for (int r = r0; r < r1; ++r) {
@@ -2397,54 +2392,75 @@ __global__ void __launch_bounds__(kBlock) k_median(Geom g, int min_reads, const 
     // the k-th smallest covered depth: zero depths sort first, so it is the smallest x
     // with count(depth <= x) >= zeros + k, i.e. count(depth > x) <= L - zeros - k = n - k
     const uint32_t g_lo = n - ((n - 1) / 2 + 1), g_hi = n - (n / 2 + 1);  // counts above to reach
-    uint32_t lo0 = 1, lo1 = dmax[c], hi0 = 1, hi1 = dmax[c];  // answers lie in [x0, x1]
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    // one barrier per step: the partial sums alternate between two LDS sets, and a
-    // set is rewritten two steps later, behind the next step's barrier
-    for (int it = 0; lo0 < lo1 || hi0 < hi1; it ^= 1) {
-        const uint32_t ml = lo0 + (lo1 - lo0) / 2, mh = hi0 + (hi1 - hi0) / 2;
-        uint32_t cl = 0, ch = 0;  // depths above ml / mh
+    // count(depth > m1), count(depth > m2) and, in the last pass, min{depth > m1}
+    auto count_pass = [&](int it, uint32_t m1, uint32_t m2, bool want_min, uint32_t& s1, uint32_t& s2) {
+        uint32_t c1 = 0, c2 = 0, mn = 0xFFFFFFFFu;
         if (regs) {
             // depths and thresholds are below 2^15 here (regs), so depth > m iff the
             // 16-bit difference m - depth has its top bit set
-            const u16x2 Ml = {(uint16_t)ml, (uint16_t)ml}, Mh = {(uint16_t)mh, (uint16_t)mh};
-            u16x2 al = {0, 0}, ah = {0, 0};
+            const u16x2 M1 = {(uint16_t)m1, (uint16_t)m1}, M2 = {(uint16_t)m2, (uint16_t)m2};
+            u16x2 a1 = {0, 0}, a2 = {0, 0};
+            if (want_min) {
+                u16x2 lo = {0xFFFF, 0xFFFF};
 #pragma unroll
-            for (int k = 0; k < kW; ++k) {
-                al += (u16x2)(Ml - v[k]) >> (uint16_t)15;
-                ah += (u16x2)(Mh - v[k]) >> (uint16_t)15;
+                for (int k = 0; k < kW; ++k) {
+                    const u16x2 gt = (u16x2)(M1 - v[k]) >> (uint16_t)15;  // 1 where depth > m1
+                    a1 += gt;
+                    lo = __builtin_elementwise_min(lo, v[k] | (u16x2)(gt - (uint16_t)1));  // 0xFFFF where not
+                }
+                mn = min((uint32_t)lo.x, (uint32_t)lo.y);
+            } else {
+#pragma unroll
+                for (int k = 0; k < kW; ++k) {
+                    a1 += (u16x2)(M1 - v[k]) >> (uint16_t)15;
+                    a2 += (u16x2)(M2 - v[k]) >> (uint16_t)15;
+                }
             }
-            cl = (uint32_t)al.x + al.y;
-            ch = (uint32_t)ah.x + ah.y;
+            c1 = (uint32_t)a1.x + a1.y;
+            c2 = (uint32_t)a2.x + a2.y;
         } else {
             for (int p = threadIdx.x; p < L; p += kBlock) {
                 const uint32_t d = depth_at(g, c, p, depth16, depth32, wide, anyw);
-                cl += d > ml;
-                ch += d > mh;
+                c1 += d > m1;
+                c2 += d > m2;
+                if (d > m1) mn = min(mn, d);
             }
         }
-        cl = wave_sum(cl);
-        ch = wave_sum(ch);
+        c1 = wave_sum(c1);
+        const uint32_t x = want_min ? wave_min(mn) : wave_sum(c2);
         if (lane == 0) {
-            red[it][0][wid] = cl;
-            red[it][1][wid] = ch;
+            red[it][0][wid] = c1;
+            red[it][1][wid] = x;
         }
         __syncthreads();
-        uint32_t sl = 0, shh = 0;
+        s1 = 0;
+        s2 = want_min ? 0xFFFFFFFFu : 0u;
 #pragma unroll
         for (int w = 0; w < kBlock / kWave; ++w) {
-            sl += red[it][0][w];
-            shh += red[it][1][w];
+            s1 += red[it][0][w];
+            s2 = want_min ? min(s2, red[it][1][w]) : s2 + red[it][1][w];
         }
-        if (lo0 < lo1) {
-            if (sl <= g_lo) lo1 = ml;
-            else lo0 = ml + 1;
-        }
-        if (hi0 < hi1) {
-            if (shh <= g_hi) hi1 = mh;
-            else hi0 = mh + 1;
-        }
+    };
+    // the lower middle value by a three-way search over [1, max depth] (two thresholds per
+    // block reduction); one barrier per step: the partial sums alternate between two LDS
+    // sets, and a set is rewritten two steps later, behind the next step's barrier
+    uint32_t x0 = 1, x1 = dmax[c];  // the answer lies in [x0, x1]
+    int it = 0;
+    for (; x0 < x1; it ^= 1) {
+        const uint32_t span = x1 - x0, m1 = x0 + span / 3, m2 = x0 + (2 * span) / 3;
+        uint32_t s1, s2;
+        count_pass(it, m1, m2, false, s1, s2);
+        if (s1 <= g_lo) x1 = m1;
+        else if (s2 <= g_lo) x0 = m1 + 1, x1 = m2;
+        else x0 = m2 + 1;
     }
+    const uint32_t lo0 = x0;
+    // the upper middle: the lower one when as few depths lie above it as the upper one
+    // allows (n odd, or a run of equal values), else the next larger depth
+    uint32_t above, next;
+    count_pass(it, lo0, lo0, true, above, next);
+    const uint32_t hi0 = above <= g_hi ? lo0 : next;
     if (threadIdx.x == 0) {
         med_lo[c] = lo0;
         med_hi[c] = hi0;
@@ -2501,29 +2517,38 @@ __global__ void __launch_bounds__(1024) k_run_stats(const uint32_t* __restrict__
     }
 }
 
-// grid (ceil(L4 / 256), ny): slice y sums the chunks y, y + ny, ... and adds into
-// the zeroed u64 tallies
-// Sum of the pileup's per-chunk tally partials: grid (L4 / 256, Y), block y sums
-// chunks y, y + Y, ... (four independent loads in flight per thread) and adds its sum
-// to the zeroed tally. Y is small (tens of chunks per thread): the u64 atomics on the
-// same 66k words, Y per word, cost more than the loads (32 per word took 0.13 ms at
-// any size).
+// Sum of the pileup's per-chunk tally partials: grid (L / 256, Y), thread x sums the 4
+// bases of position x over chunks y, y + Y, ... (16-byte loads, four chunks in flight per
+// thread) and adds its sums to the zeroed tally. Y is small (tens of chunks per thread):
+// the u64 atomics on the same 66k words, Y per word, cost more than the loads (32 per
+// word took 0.13 ms at any size).
 __global__ void k_tally_reduce(const uint32_t* __restrict__ part, int nchunks, int L4,
                                unsigned long long* __restrict__ tally) {
-    const int x = blockIdx.x * blockDim.x + threadIdx.x;
-    if (x >= L4) return;
+    const int x = blockIdx.x * blockDim.x + threadIdx.x;  // position: 4 u32 partials
+    const int L = L4 / 4;
+    if (x >= L) return;
+    const uint4* p4 = reinterpret_cast<const uint4*>(part);
     const int Y = gridDim.y;
-    unsigned long long a0 = 0, a1 = 0, a2 = 0, a3 = 0;
+    unsigned long long a[4] = {0, 0, 0, 0};
+    auto add = [&](const uint4 v) {
+        a[0] += v.x;
+        a[1] += v.y;
+        a[2] += v.z;
+        a[3] += v.w;
+    };
     int ch = blockIdx.y;
     for (; ch + 3 * Y < nchunks; ch += 4 * Y) {
-        a0 += part[(size_t)ch * L4 + x];
-        a1 += part[(size_t)(ch + Y) * L4 + x];
-        a2 += part[(size_t)(ch + 2 * Y) * L4 + x];
-        a3 += part[(size_t)(ch + 3 * Y) * L4 + x];
+        const uint4 v0 = p4[(size_t)ch * L + x], v1 = p4[(size_t)(ch + Y) * L + x];
+        const uint4 v2 = p4[(size_t)(ch + 2 * Y) * L + x], v3 = p4[(size_t)(ch + 3 * Y) * L + x];
+        add(v0);
+        add(v1);
+        add(v2);
+        add(v3);
     }
-    for (; ch < nchunks; ch += Y) a0 += part[(size_t)ch * L4 + x];
-    const unsigned long long acc = a0 + a1 + a2 + a3;
-    if (acc) atomicAdd(&tally[x], acc);
+    for (; ch < nchunks; ch += Y) add(p4[(size_t)ch * L + x]);
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+        if (a[k]) atomicAdd(&tally[(size_t)x * 4 + k], a[k]);
 }
 
 // mgp_fetch: the 16-bit result rows widened into the u32 arrays the caller
@@ -2612,12 +2637,15 @@ __global__ void k_add_u64(uint64_t* __restrict__ a, int64_t n, uint64_t add) {
 __global__ void k_run_init(int nc, int64_t nF, uint32_t* __restrict__ covered, unsigned long long* __restrict__ dsum,
                            uint32_t* __restrict__ dmax, uint32_t* __restrict__ n_reads, uint8_t* __restrict__ any_paired,
                            uint32_t* __restrict__ first_read, uint32_t* __restrict__ F, uint32_t* __restrict__ ck,
-                           DevStats* st, int what) {
+                           DevStats* st, int what, uint32_t* __restrict__ cell_cnt) {
     // what: 1 the run's state (per-cell counters, check words, stats), 2 the first-bin
-    // bits F (every segment of a streaming run; the run state only at its first)
+    // bits F and the scan's cell totals (every segment of a streaming run; the run state
+    // only at its first)
     const int64_t i0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x, step = (int64_t)gridDim.x * blockDim.x;
-    if (what & 2)
+    if (what & 2) {
         for (int64_t i = i0; i < nF; i += step) F[i] = 0u;
+        for (int64_t i = i0; i < nc; i += step) cell_cnt[i] = 0u;
+    }
     if (!(what & 1)) return;
     for (int64_t i = i0; i < nc; i += step) {
         covered[i] = 0u;
@@ -2712,11 +2740,15 @@ __global__ void k_respec_slot(const DevStats* st, unsigned long long* slot) {
 // ---------------------------------------------------------------------------
 // host side
 // ---------------------------------------------------------------------------
+// r03 v52 re-sweep with the chunks taken largest first (ab_geo_v52.txt): fewer, larger
+// chunks now cost the pileup little and halve the tally partials the reduction reads
+// beside the medians (C4 6.63 -> 6.60 ms at 8192 workgroups; 1250 cells 1.022 -> 0.992
+// ms at 8 cells per chunk)
 #ifndef MGP_PILE_WG
-#define MGP_PILE_WG 16384
+#define MGP_PILE_WG 8192
 #endif
 #ifndef MGP_PILE_MIN_CPB
-#define MGP_PILE_MIN_CPB 4
+#define MGP_PILE_MIN_CPB 8
 #endif
 static inline unsigned blocks_for(int64_t n, int bs = kBlock) { return (unsigned)((n + bs - 1) / bs); }
 
@@ -3113,7 +3145,8 @@ static int run_segment(mgp_ctx* ctx, const Seg& sg, int slot, int& dup_parts, in
         k_run_init<<<std::max(1u, std::min(1024u, blocks_for(std::max<int64_t>(nc, nF)))), kBlock, 0, s>>>(
             nc, nF, ctx->covered.as<uint32_t>(), ctx->dsum.as<unsigned long long>(), ctx->dmax.as<uint32_t>(),
             ctx->n_reads.as<uint32_t>(), ctx->any_paired.as<uint8_t>(), ctx->first_read.as<uint32_t>(),
-            ctx->F.as<uint32_t>(), ctx->roff_irregular.as<uint32_t>(), st, sg.first ? 3 : 2);
+            ctx->F.as<uint32_t>(), ctx->roff_irregular.as<uint32_t>(), st, sg.first ? 3 : 2,
+            ctx->cell_cnt.as<uint32_t>());
         HIP_TRY(hipGetLastError());
     } else {
         if (sg.first) HIP_TRY(hipMemsetAsync(st, 0, sizeof(DevStats), s));
@@ -3153,8 +3186,8 @@ static int run_segment(mgp_ctx* ctx, const Seg& sg, int slot, int& dup_parts, in
     const int RB = 32;
     const int nrb = (g.nbins + RB - 1) / RB;
     dim3 g2((nc + kBlock - 1) / kBlock, nrb);
-    k_scan_colsum<<<g2, kBlock, 0, s>>>(ctx->H.as<uint32_t>(), g.nbins, nc, RB, ctx->P.as<uint32_t>());
-    k_scan_rows<<<blocks_for(nc), kBlock, 0, s>>>(ctx->P.as<uint32_t>(), nrb, nc, ctx->cell_cnt.as<uint32_t>());
+    k_scan_colsum<<<g2, kBlock, 0, s>>>(ctx->H.as<uint32_t>(), g.nbins, nc, RB, ctx->P.as<uint32_t>(),
+                                        ctx->cell_cnt.as<uint32_t>());
     k_scan_cells<<<1, 1024, 0, s>>>(ctx->cell_cnt.as<uint32_t>(), nc, ctx->cell_base.as<uint32_t>(), g.cpb,
                                     g.nchunks, ctx->chunk_perm.as<uint32_t>(), ctx->bin_valid.as<uint32_t>(),
                                     n > 0 ? g.nbins : 0, ctx->bin_base.as<uint32_t>());
@@ -3379,7 +3412,7 @@ static int run_finish(mgp_ctx* ctx, int slot, int dup_parts, bool streamed) {
                 ctx->stage_ran[slot][ST_TALLY] = true;
             }
             HIP_TRY(hipMemsetAsync(tally, 0, (size_t)g.L * 32, s2));
-            dim3 gt(blocks_for((int64_t)g.L * 4), (unsigned)std::max(1, std::min(g.nchunks / 64, 16)));
+            dim3 gt(blocks_for((int64_t)g.L), (unsigned)std::max(1, std::min(g.nchunks / 16, 16)));
             k_tally_reduce<<<gt, kBlock, 0, s2>>>(ctx->tally_part.as<uint32_t>(), g.nchunks, g.L * 4, tally);
             HIP_TRY(hipGetLastError());
             if (STAGE_ON(ST_TALLY)) HIP_TRY(hipEventRecord(ctx->ev[slot][ST_TALLY][1], s2));

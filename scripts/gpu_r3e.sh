@@ -6,7 +6,8 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 V=${V:-x}
-for args in "" "--reads 25000000 --cells 1250"; do
+IFS=';' read -ra SIZES <<< "${ABSIZES:-;--reads 25000000 --cells 1250}"
+for args in "${SIZES[@]}"; do
     echo "== A/B $args"
     BARGS="--steps 20 --warmup 3 --no-cpu-baseline --no-check --no-pcie $args" \
         bash scripts/ab_bench.sh ${VARIANTS:-} || exit 1
