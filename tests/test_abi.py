@@ -175,3 +175,19 @@ def test_host_synth_is_deterministic_and_sorted():
     # duplicate structure: ~15% full copies of the previous read's key
     same = (a.start[1:] == a.start[:-1]) & (a.bc[1:] == a.bc[:-1]) & (a.tlen[1:] == a.tlen[:-1])
     assert 0.12 < same.mean() < 0.2
+
+
+def test_batch_struct_optional_columns():
+    """ABI v3.1: a batch without rec_off / span passes NULL pointers (the engine then
+    takes dense offsets and the records' spans); every other column is required."""
+    import numpy as np
+
+    from mgatk2_amd.engine import batch_struct
+    from mgatk2_amd.synth import ReadSoA, synth_reads
+
+    soa = synth_reads(3, 500, 4, pack32=20)
+    b = batch_struct(ReadSoA(soa.start, soa.bc, soa.tlen, soa.flag, soa.mapq, None, None, soa.payload))
+    assert b.n_reads == soa.n and b.span is None and b.rec_off is None and b.payload_bytes == soa.payload.shape[0]
+    full = batch_struct(soa)
+    assert full.span == soa.span.ctypes.data and full.rec_off == soa.rec_off.ctypes.data
+    assert np.all(soa.span >= 50)
