@@ -420,11 +420,13 @@ def test_push_without_offsets_rejects_ragged_payloads(engine_lib):
 # ---------------------------------------------------------------------------
 # ABI v3.1: a rows target (the 16-bit rows leave the device as the windows complete)
 # ---------------------------------------------------------------------------
+@pytest.mark.parametrize("layout", ["p32", "full"])
 @pytest.mark.parametrize("streamed", [False, True])
-def test_rows16_target_equals_fetch_rows16(engine_lib, streamed):
+def test_rows16_target_equals_fetch_rows16(engine_lib, streamed, layout):
     """The rows copied to a pinned target segment by segment equal mgp_fetch_rows16
     of a resident run, for a streamed run of 4 batches and a resident one, also on a
-    rerun of the same context; a min_reads > 1 context refuses a target."""
+    rerun of the same context; full-layout records make a streamed run rerun resident
+    (the target then holds the rerun's rows); a min_reads > 1 context refuses a target."""
     from dataclasses import replace
 
     from mgatk2_amd.engine import EngineConfig, PinnedBuffer, Rows16
@@ -433,7 +435,7 @@ def test_rows16_target_equals_fetch_rows16(engine_lib, streamed):
 
     nc = 40
     cfg = EngineConfig(n_cells=nc, **CONFIGS["run"])
-    soa = synth_reads(717, 200_000, nc, pack32=cfg.min_baseq)
+    soa = synth_reads(717, 200_000, nc, **(dict(pack32=cfg.min_baseq) if layout == "p32" else dict(pack=False)))
     with engine_lib.Engine(cfg) as eng:
         eng.push(soa)
         eng.run()
