@@ -75,6 +75,10 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-check", action="store_true", help="skip the bit-exact sample check")
     ap.add_argument("--no-pcie", action="store_true", help="skip the PCIe-inclusive (host buffers) leg")
+    ap.add_argument("--no-device-paired", action="store_true",
+                    help="skip the device leg on quality-carrying 64-byte records (the kernel applies the per-base "
+                         "filter)")
+    ap.add_argument("--no-host-pack", action="store_true", help="skip timing the host's 32-byte record build")
     ap.add_argument("--pcie-steps", type=int, default=3)
     ap.add_argument("--batch-reads", type=str, default="16000000",
                     help="reads per pushed batch in the PCIe leg; a comma list sweeps (first = reported)")
@@ -261,6 +265,17 @@ def main():
         check = sample_check(eng, cfg, res)
     eng.close()
 
+    # the same workload on quality-carrying 64-byte records two per line: the kernel
+    # applies min_baseq / end distance / ACGT per base (pileup.py:67-86), which the
+    # headline's 32-byte records carry resolved (built by the producer, timed below)
+    paired = None
+    if not args.no_device_paired and args.record_layout == "quad32":
+        paired = device_leg(args, cfg, seed, cdf, ref, shard, device, make_comm if comm_ranks > 1 else None,
+                            barrier, reduce, "paired")
+    host_pack = None
+    if rank == 0 and not args.no_host_pack and args.record_layout in ("quad32", "pack32"):
+        host_pack = host_pack_leg(args, cfg, device)
+
     pcie = None
     if not args.no_pcie:
         pcie = pcie_leg(args, cfg, seed, cdf, ref, shard, device, comm_ranks, barrier, reduce, make_comm)
@@ -313,8 +328,16 @@ def main():
                 "kernels": kernels,
             },
             "stage_ms": {k: round(v, 4) for k, v in kt_all.items()},
-            "pcie": pcie,
+            # value is the HBM-resident rate (the task's bench contract: inputs resident
+            # when the timed region starts); SURVEY.md §8(d)'s engine metric, from the first
+            # H2D to the counts in host memory, is value_pcie
+            "value_device": value,
             "value_pcie": None if pcie is None else pcie["value"],
+            "device_ms_paired": None if paired is None else paired["ms_per_step"],
+            "device_paired": paired,
+            "host_pack_ns_per_read": None if host_pack is None else host_pack["ns_per_read_1thread"],
+            "host_pack": host_pack,
+            "pcie": pcie,
             "cpu_baseline": cpu,
             "stats_rank0": res.stats,
             "sample_check": check,
@@ -322,6 +345,80 @@ def main():
         print(json.dumps(out), flush=True)
     if dist is not None:
         dist.destroy_process_group()
+
+
+def device_leg(args, cfg, seed, cdf, ref, shard, device, make_comm, barrier, reduce, layout: str) -> dict:
+    """The timed steps again on another record layout of the same reads (untimed
+    generation): ms per step (max over ranks) and the stage times."""
+    from mgatk2_amd.bam import PLACE_PAIRED, place_records
+    from mgatk2_amd.engine import Engine
+
+    eng = Engine(cfg, device=device)
+    eng.synth(seed, args.reads, cdf, ref, read_len=args.read_len, rec_align=64, pack=True, **shard)
+    n_res, _ = eng.resident()
+    if layout == "paired":
+        soa = eng.download_inputs(columns=("bc", "flag", "start", "tlen"))
+        roff, pay_b = place_records(soa.bc, soa.flag, np.full(n_res, 64, np.uint32), cfg.n_cells, PLACE_PAIRED,
+                                    start=soa.start, tlen=soa.tlen)
+        del soa
+        eng.synth(seed, args.reads, cdf, ref, read_len=args.read_len, rec_align=64, pack=True, rec_off=roff,
+                  payload_bytes=pay_b, **shard)
+        del roff
+    if make_comm is not None:
+        make_comm(eng)
+    eng.set_stage_timing(False)
+    for _ in range(max(1, args.warmup)):
+        eng.run()
+    eng.sync()
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        eng.run()
+    eng.sync()
+    barrier()
+    dt = reduce(time.perf_counter() - t0, "max")
+    pile = eng.kernel_times(last_runs=min(args.steps, 64)).get("pileup")
+    eng.set_stage_timing(True)
+    for _ in range(3):
+        eng.run()
+    eng.sync()
+    kt = eng.kernel_times(last_runs=3)
+    st = eng.fetch(dense=False).stats
+    eng.close()
+    return {"record_layout": layout, "what": "packed 64-byte records (qualities and base codes; the kernel applies "
+            "min_baseq, min_distance_from_end and ACGT per base), two of a cell per 128-byte line",
+            "ms_per_step": dt / args.steps * 1e3, "value": reduce(float(n_res), "sum") * args.steps / dt,
+            "pileup_ms": pile, "stage_ms": {k: round(v, 4) for k, v in kt.items()},
+            "filtered_reads_rank0": st["filtered_reads"], "error_bits": st["error_bits"]}
+
+
+def host_pack_leg(args, cfg, device, n: int = 4_000_000) -> dict:
+    """The producer's cost of the 32-byte records (what the headline's device step
+    does not do): the host builder the BAM decoder calls per record
+    (mgp_pack32_host.h via mgp_repack32) over full records of the same generator,
+    on one thread and on the host threads."""
+    from mgatk2_amd.bam import host_threads, repack32
+    from mgatk2_amd.engine import Engine, EngineConfig
+    from mgatk2_amd.synth import cell_cdf, ref_codes
+
+    seed = args.seed + 91
+    nc = 1000
+    with Engine(EngineConfig(**{**cfg.__dict__, "n_cells": nc}), device=device) as e2:
+        e2.synth(seed, n, cell_cdf(seed, nc), ref_codes(seed), read_len=args.read_len, rec_align=128, pack=False)
+        soa = e2.download_inputs()
+    out32 = np.empty(n * 32, np.uint8)
+    oflag = np.empty(n, np.uint16)
+    repack32(soa, cfg.min_baseq, cfg.min_distance_from_end, 1, out32, oflag)  # (pages faulted in)
+    t0 = time.perf_counter()
+    _, _, k = repack32(soa, cfg.min_baseq, cfg.min_distance_from_end, 1, out32, oflag)
+    t1 = time.perf_counter() - t0
+    nt = host_threads()
+    t0 = time.perf_counter()
+    repack32(soa, cfg.min_baseq, cfg.min_distance_from_end, nt, out32, oflag)
+    tn = time.perf_counter() - t0
+    return {"ns_per_read_1thread": t1 / n * 1e9, "reads_per_s_threads": n / tn, "threads": nt, "packed": k,
+            "sample": f"{n:,} full 128-byte records of the generator (run thresholds q{cfg.min_baseq}, "
+                      f"min_dist {cfg.min_distance_from_end})"}
 
 
 def kernel_bytes(n: int, nc: int, stats: dict, cfg, layout: str) -> dict:

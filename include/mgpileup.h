@@ -46,8 +46,12 @@
 extern "C" {
 #endif
 
-#define MGP_ABI_VERSION 3  /* 2: fixed seq/CIGAR offsets for reads <= 64 bases;
-                              3: synth cell shards, cell-range and 16-bit fetches, streaming runs */
+#define MGP_ABI_VERSION 4  /* 2: fixed seq/CIGAR offsets for reads <= 64 bases;
+                              3: synth cell shards, cell-range and 16-bit fetches, streaming runs;
+                              4: batches without rec_off / span columns and the rows target (the
+                                 round-3 "v3.1" entry points), pushed records checked against
+                                 their batch's payload (MGP_E_INVALID), mgp_copy_wait,
+                                 mgp_synth_params.n_rec_off, rows targets with min_reads > 1 */
 
 /* ---- return codes (0 = success) ------------------------------------------ */
 #define MGP_OK               0
@@ -406,6 +410,8 @@ typedef struct mgp_synth_params {
     int32_t  shard_rank, shard_world;
     int32_t  pack_min_baseq;    /* pack == 2: the min_baseq the 32-byte records are made for */
     int32_t  pack_min_dist;     /* pack == 2: the min_dist_from_end they are made for (0..15) */
+    int64_t  n_rec_off;         /* entries of rec_off: must equal the reads generated (all n_reads,
+                                   or a shard's kept reads), else MGP_E_INVALID */
 } mgp_synth_params;
 
 /* The pileup's 16-bit result rows, as the run leaves them in HBM (half the bytes of
@@ -436,6 +442,9 @@ int  mgp_host_alloc(int64_t bytes, void **out);
 int  mgp_host_free(void *p);
 
 /* Append a batch to the device-resident read set (async H2D on the copy stream).
+ * Every record must lie inside the batch's payload (its offset, header and, for the
+ * full layout, its CIGAR words); a batch that breaks this is checked on the device
+ * and the next run fails with MGP_E_INVALID without reading any record (ABI 4).
  * Replaces the accumulation of reads_by_barcode in
  * BAMReader.collect_reads_by_barcode (src/processing/readers.py:85-165): the
  * batch is every fetch(mito_chr) record in BAM order, unfiltered. */
@@ -473,13 +482,18 @@ int  mgp_fetch_rows16(mgp_ctx *ctx, int32_t lo, int32_t hi, mgp_rows16 *out);
  * windows complete: each streaming segment writes its windows' rows on a
  * device-to-host stream behind its pileup, while the copies of
  * later batches still run the other way; the wide flags follow the run, and mgp_sync
- * waits for all of it. The caller then needs no mgp_fetch_rows16. Needs min_reads <= 1
- * (the gate rewrites rows after the pileup: MGP_E_STATE); NULL stops it. Replaces the
+ * waits for all of it. The caller then needs no mgp_fetch_rows16. With min_reads > 1 the
+ * gate (processors.py:22) also zeroes the target rows of the cells it drops, after the
+ * last segment's rows have landed (ABI 4). NULL stops it. Replaces the
  * reference's per-cell write_cell after each worker (processors.py:112-144): results
  * leave the device while ingest continues. */
 int  mgp_set_rows16_target(mgp_ctx *ctx, const mgp_rows16 *rows);
 /* Position windows of the pileup (the `wide` flags' second dimension). */
 int  mgp_windows(mgp_ctx *ctx, int32_t *n_windows, int32_t *window_width);
+/* Wait until the H2D copies of every batch pushed so far have completed: the caller may
+ * then reuse those host buffers (until then a pushed batch's arrays must stay untouched).
+ * A producer that decodes into a ring of pinned buffers calls it before refilling one. */
+int  mgp_copy_wait(mgp_ctx *ctx);
 /* Streaming on (1) or off (0) for the next pushes (initially MGP_CFG_STREAM). */
 int  mgp_set_streaming(mgp_ctx *ctx, int on);
 /* Streaming: segments queued by pushes so far (all runs), and whether the last run

@@ -167,6 +167,18 @@ int mgp_gather_records(const uint8_t *payload, const uint64_t *rec_off, const ui
                        int64_t payload_bytes, const int64_t *idx, int64_t m, const uint64_t *out_off,
                        int64_t out_bytes, uint8_t *out, int n_threads);
 
+/* 32-byte records (MGP_FLAG_PACK32, include/mgpileup.h) from a batch's full-layout
+ * records, for one run's (min_baseq, min_dist_from_end): out32[i] (32 bytes, dense
+ * in batch order) and out_flag[i] = flag[i] | MGP_FLAG_PACK32 for every full record
+ * with SEQ and QUAL that fits the layout; the others get a zeroed slot and their own
+ * flag word (the caller keeps their records). The same mgp_pack32_record the BAM
+ * decoder calls per decoded record: the per-base filter of pileup.py:67-88 moved to
+ * the producer. Returns the number of records packed, -1 on error (a record outside
+ * the payload). */
+int64_t mgp_repack32(int64_t n, const uint8_t *payload, int64_t payload_bytes, const uint64_t *rec_off,
+                     const uint16_t *flag, int32_t min_baseq, int32_t min_dist, uint8_t *out32,
+                     uint16_t *out_flag, int n_threads);
+
 #ifdef __cplusplus
 }
 #endif

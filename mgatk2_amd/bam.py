@@ -106,6 +106,8 @@ def host_library() -> C.CDLL:
         lib.mgp_bam_write.argtypes = [C.c_char_p, C.POINTER(C.c_char_p), C.POINTER(C.c_int64), C.c_int, C.c_int,
                                       C.POINTER(mgp_bam_batch), C.POINTER(C.c_char_p), C.c_int, C.c_char_p,
                                       C.c_char_p, C.c_int, C.c_int, C.c_int]
+        lib.mgp_repack32.argtypes = [C.c_int64, vp, C.c_int64, vp, vp, C.c_int32, C.c_int32, vp, vp, C.c_int]
+        lib.mgp_repack32.restype = C.c_int64
         lib.mgp_host_buf_free.argtypes = [vp]
         lib.mgp_host_buf_free.restype = None
         _hlib = lib
@@ -147,6 +149,28 @@ def place_records(bc: np.ndarray, flag: np.ndarray, rec_bytes: np.ndarray, n_cel
     if tot < 0:
         raise ValueError(_err())
     return off, int(tot)
+
+
+def repack32(soa: ReadSoA, min_baseq: int, min_dist: int = 5, n_threads: int = 0,
+             out32: np.ndarray | None = None, out_flag: np.ndarray | None = None) -> tuple[np.ndarray, np.ndarray, int]:
+    """libmgphost `mgp_repack32`: the 32-byte records of a batch's full records for one
+    run's thresholds, dense in batch order (record i at 32 x i of the returned payload),
+    with the new flag words and the number of records packed (the others keep their
+    own layout: a zeroed slot and their flag word)."""
+    lib = host_library()
+    n = soa.n
+    out32 = np.empty(n * 32, np.uint8) if out32 is None else out32
+    out_flag = np.empty(n, np.uint16) if out_flag is None else out_flag
+    if out32.shape[0] < n * 32 or out_flag.shape[0] < n:
+        raise ValueError("repack32 output arrays too small")
+    pay = np.ascontiguousarray(soa.payload)
+    roff = np.ascontiguousarray(soa.rec_off, np.uint64)
+    flag = np.ascontiguousarray(soa.flag, np.uint16)
+    k = lib.mgp_repack32(n, pay.ctypes.data, int(pay.shape[0]), roff.ctypes.data, flag.ctypes.data, int(min_baseq),
+                         int(min_dist), out32.ctypes.data, out_flag.ctypes.data, int(n_threads or host_threads()))
+    if k < 0:
+        raise ValueError(_err())
+    return out32, out_flag, int(k)
 
 
 class _BatchOwner:

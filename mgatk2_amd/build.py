@@ -61,8 +61,10 @@ def build_engine(force: bool = False, verbose: bool = False, out: Path | None = 
 def build_host(force: bool = False, verbose: bool = False) -> Path:
     """libmgphost.so: native BAM ingest (include/mgpileup_host.h), plain C++ + zlib."""
     srcs = [CSRC / "host" / "mgp_bam.cpp", CSRC / "host" / "mgp_txt.cpp", CSRC / "host" / "mgp_tiles.cpp",
-            CSRC / "host" / "mgp_bamw.cpp", CSRC / "host" / "mgp_shard.cpp", CSRC / "host" / "mgp_place.cpp"]
-    deps = srcs + [ROOT / "include" / "mgpileup_host.h", ROOT / "include" / "mgpileup.h"]
+            CSRC / "host" / "mgp_bamw.cpp", CSRC / "host" / "mgp_shard.cpp", CSRC / "host" / "mgp_place.cpp",
+            CSRC / "host" / "mgp_repack.cpp"]
+    deps = srcs + [ROOT / "include" / "mgpileup_host.h", ROOT / "include" / "mgpileup.h",
+                   CSRC / "host" / "mgp_pack32_host.h", CSRC / "host" / "mgp_place.h"]
     if force or _stale(HOST_SO, deps):
         LIB_DIR.mkdir(parents=True, exist_ok=True)
         tmp = HOST_SO.with_suffix(".so.tmp")

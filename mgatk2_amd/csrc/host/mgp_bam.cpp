@@ -27,6 +27,7 @@
 
 #include "../../../include/mgpileup.h"
 #include "../../../include/mgpileup_host.h"
+#include "mgp_pack32_host.h"
 #include "mgp_place.h"
 
 // one thread-local error string for every entry point of libmgphost.so
@@ -814,7 +815,8 @@ int mgp_bam_read_ref(mgp_bam* b, int tid, int rec_align, mgp_bam_batch* out) {
             for (uint32_t q = 0; q < n_cig; ++q) cw[q] = rd32(cig + 4 * q);
             const uint64_t size = ((uint64_t)MGP_PACK32_BYTES + amask) & ~amask;
             if (size > MGP_PACK32_BYTES && !paired) std::memset(rec + MGP_PACK32_BYTES, 0, size - MGP_PACK32_BYTES);
-            mgp_pack32_record(pos, l_seq, fl, n_cig, cw, seqp, qualp, b->pack32_minq, b->pack32_dist, rec);  // all 32 B
+            mgp_host::pack32_record_fast(pos, l_seq, fl, n_cig, cw, seqp, qualp, b->pack32_minq, b->pack32_dist,
+                                         rec);  // all 32 B
         } else if (pk) {
             uint32_t cw[4] = {0, 0, 0, 0};
             for (uint32_t q = 0; q < n_cig; ++q) cw[q] = rd32(cig + 4 * q);

@@ -2278,7 +2278,11 @@ __global__ void __launch_bounds__(kBlock) k_gate_fixup(Geom g, int min_reads, co
                                                        uint32_t* __restrict__ tn5, uint32_t* __restrict__ depth,
                                                        uint32_t* __restrict__ covered,
                                                        unsigned long long* __restrict__ dsum,
-                                                       uint32_t* __restrict__ dmax, uint32_t* __restrict__ tally_part) {
+                                                       uint32_t* __restrict__ dmax, uint32_t* __restrict__ tally_part,
+                                                       uint4* __restrict__ hc, uint32_t* __restrict__ ht,
+                                                       uint16_t* __restrict__ hd) {
+    // hc/ht/hd (mgp_set_rows16_target, else null): the pinned host rows, which the
+    // segments' k_rows_to_host already wrote: the dropped cell's rows are zeroed there too
     const int c = blockIdx.x;
     const uint32_t nr = n_reads[c];
     if (nr == 0 || nr >= (uint32_t)min_reads || covered[c] == 0) return;
@@ -2311,6 +2315,11 @@ __global__ void __launch_bounds__(kBlock) k_gate_fixup(Geom g, int min_reads, co
         o16.counts[P] = make_uint4(0, 0, 0, 0);
         o16.tn5[P] = 0u;
         o16.depth[P] = 0;
+        if (hc) {
+            hc[P] = make_uint4(0, 0, 0, 0);
+            ht[P] = 0u;
+            hd[P] = 0;
+        }
     }
     __syncthreads();
     if (threadIdx.x == 0) {
@@ -2598,33 +2607,52 @@ __global__ void k_dense_off(uint64_t* __restrict__ roff, int64_t n, uint64_t bas
     if (i < n) roff[i] = base + (uint64_t)i * stride;
 }
 
-// mgp_push_batch without span: max(reference span of the CIGAR, l_seq) of each read from
-// its record (include/mgpileup.h, the three layouts), as the BAM decoder computes it
-// (M, D, N, =, X consume the reference)
-__global__ void k_record_span(const uint8_t* __restrict__ payload, const uint64_t* __restrict__ roff,
-                              const uint16_t* __restrict__ flag, int64_t n, uint32_t* __restrict__ span) {
+// Every pushed batch: each record (offset, header and, for the full layout, its CIGAR)
+// must lie inside the batch's payload [pay_lo, pay_hi) (a bad offset, CIGAR offset or a
+// dense stride shorter than a full record sets bit 2 of *bad: the run then reports
+// MGP_E_INVALID and no kernel reads a record; k_run_init). span != nullptr (a batch
+// without span, ABI v3.1): max(reference span of the CIGAR, l_seq) of each read from its
+// record (include/mgpileup.h, the three layouts), as the BAM decoder computes it (M, D,
+// N, =, X consume the reference).
+__global__ void k_check_records(const uint8_t* __restrict__ payload, const uint64_t* __restrict__ roff,
+                                const uint16_t* __restrict__ flag, int64_t n, uint64_t pay_lo, uint64_t pay_hi,
+                                uint32_t* __restrict__ span, uint32_t* __restrict__ bad) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    const uint8_t* rec = payload + roff[i];
-    const uint4 h = *reinterpret_cast<const uint4*>(rec);
-    const uint32_t f = flag[i];
-    const bool p32 = (f & MGP_FLAG_PACK32) != 0, packed = (f & (MGP_FLAG_PACKED | MGP_FLAG_PACK32)) != 0;
-    const uint32_t lseq = p32 ? ((h.x >> 16) & 0xFFu) : packed ? (h.y & 0xFFu) : h.y;
-    const uint32_t ncig = p32 ? ((h.x >> 24) & 7u) : packed ? ((h.y >> 8) & 0x7Fu) : (h.z & 0xFFFFu);
-    auto consumes = [](uint32_t op) { return op == 0u || op == 2u || op == 3u || op == 7u || op == 8u; };
-    uint64_t ref = 0;
-    if (packed) {
-        const uint32_t cw[4] = {p32 ? (h.y & 0xFFFFu) : (h.y >> 16), p32 ? (h.y >> 16) : (h.z & 0xFFFFu),
-                                p32 ? (h.z & 0xFFFFu) : (h.z >> 16), p32 ? (h.z >> 16) : (h.w & 0xFFFFu)};
+    bool err = false;
+    if (i < n) {
+        const uint64_t r = roff[i];
+        const uint32_t f = flag[i];
+        const bool p32 = (f & MGP_FLAG_PACK32) != 0, packed = (f & (MGP_FLAG_PACKED | MGP_FLAG_PACK32)) != 0;
+        const uint64_t fixed = p32 ? MGP_PACK32_BYTES : packed ? MGP_PACK_BYTES : 16u;
+        if (r < pay_lo || (r & 15ull) != 0ull || r + fixed > pay_hi) {
+            err = true;
+            if (span) span[i] = 0u;
+        } else {
+            const uint8_t* rec = payload + r;
+            const uint4 h = *reinterpret_cast<const uint4*>(rec);
+            const uint32_t lseq = p32 ? ((h.x >> 16) & 0xFFu) : packed ? (h.y & 0xFFu) : h.y;
+            const uint32_t ncig = p32 ? ((h.x >> 24) & 7u) : packed ? ((h.y >> 8) & 0x7Fu) : (h.z & 0xFFFFu);
+            // a full record's CIGAR at cigar_off (4-byte words, inside the payload)
+            err = !packed && ((h.w & 3u) != 0u || h.w < 16u || r + h.w + 4ull * ncig > pay_hi);
+            if (span) {
+                auto consumes = [](uint32_t op) { return op == 0u || op == 2u || op == 3u || op == 7u || op == 8u; };
+                uint64_t ref = 0;
+                if (packed) {
+                    const uint32_t cw[4] = {p32 ? (h.y & 0xFFFFu) : (h.y >> 16), p32 ? (h.y >> 16) : (h.z & 0xFFFFu),
+                                            p32 ? (h.z & 0xFFFFu) : (h.z >> 16), p32 ? (h.z >> 16) : (h.w & 0xFFFFu)};
 #pragma unroll
-        for (int o = 0; o < 4; ++o)
-            if ((uint32_t)o < ncig && consumes(cw[o] & 15u)) ref += cw[o] >> 4;
-    } else {
-        const uint32_t* cig = reinterpret_cast<const uint32_t*>(rec + h.w);
-        for (uint32_t o = 0; o < ncig; ++o)
-            if (consumes(cig[o] & 15u)) ref += cig[o] >> 4;
+                    for (int o = 0; o < 4; ++o)
+                        if ((uint32_t)o < ncig && consumes(cw[o] & 15u)) ref += cw[o] >> 4;
+                } else if (!err) {
+                    const uint32_t* cig = reinterpret_cast<const uint32_t*>(rec + h.w);
+                    for (uint32_t o = 0; o < ncig; ++o)
+                        if (consumes(cig[o] & 15u)) ref += cig[o] >> 4;
+                }
+                span[i] = (uint32_t)max<uint64_t>(min<uint64_t>(ref, 0xFFFFFFFFull), lseq);
+            }
+        }
     }
-    span[i] = (uint32_t)max<uint64_t>(min<uint64_t>(ref, 0xFFFFFFFFull), lseq);
+    if (__ballot(err) && (threadIdx.x & 63) == 0) atomicOr(bad, 2u);
 }
 
 __global__ void k_add_u64(uint64_t* __restrict__ a, int64_t n, uint64_t add) {
@@ -2637,7 +2665,8 @@ __global__ void k_add_u64(uint64_t* __restrict__ a, int64_t n, uint64_t add) {
 __global__ void k_run_init(int nc, int64_t nF, uint32_t* __restrict__ covered, unsigned long long* __restrict__ dsum,
                            uint32_t* __restrict__ dmax, uint32_t* __restrict__ n_reads, uint8_t* __restrict__ any_paired,
                            uint32_t* __restrict__ first_read, uint32_t* __restrict__ F, uint32_t* __restrict__ ck,
-                           DevStats* st, int what, uint32_t* __restrict__ cell_cnt) {
+                           DevStats* st, int what, uint32_t* __restrict__ cell_cnt,
+                           const uint32_t* __restrict__ order_bad) {
     // what: 1 the run's state (per-cell counters, check words, stats), 2 the first-bin
     // bits F and the scan's cell totals (every segment of a streaming run; the run state
     // only at its first)
@@ -2646,20 +2675,24 @@ __global__ void k_run_init(int nc, int64_t nF, uint32_t* __restrict__ covered, u
         for (int64_t i = i0; i < nF; i += step) F[i] = 0u;
         for (int64_t i = i0; i < nc; i += step) cell_cnt[i] = 0u;
     }
-    if (!(what & 1)) return;
-    for (int64_t i = i0; i < nc; i += step) {
-        covered[i] = 0u;
-        dsum[i] = 0ull;
-        dmax[i] = 0u;
-        n_reads[i] = 0u;
-        any_paired[i] = 0u;
-        first_read[i] = 0xFFFFFFFFu;
+    if (what & 1) {
+        for (int64_t i = i0; i < nc; i += step) {
+            covered[i] = 0u;
+            dsum[i] = 0ull;
+            dmax[i] = 0u;
+            n_reads[i] = 0u;
+            any_paired[i] = 0u;
+            first_read[i] = 0xFFFFFFFFu;
+        }
+        if (i0 == 0) {
+            ck[0] = 0u;
+            ck[1] = 0u;
+            *st = DevStats{};
+        }
     }
-    if (i0 == 0) {
-        ck[0] = 0u;
-        ck[1] = 0u;
-        *st = DevStats{};
-    }
+    // a pushed record outside its batch's payload (k_check_records): no kernel of this
+    // run reads a record (ERR_BOUNDS stops grouping and pileup at entry)
+    if (i0 == 0 && (*order_bad & 2u)) st->err |= ERR_BOUNDS | ERR_BADOFF;
 }
 
 // The run's view of the input check: the pileup's halo span and the order check.
@@ -3011,12 +3044,12 @@ int mgp_push_batch(mgp_ctx* ctx, const mgp_batch* b) {
         k_add_u64<<<blocks_for(nb), kBlock, 0, s>>>(ctx->roff.as<uint64_t>() + n0, nb, (uint64_t)pay0);
         HIP_TRY(hipGetLastError());
     }
-    if (!b->span) {
-        k_record_span<<<blocks_for(nb), kBlock, 0, s>>>(ctx->payload.as<uint8_t>(), ctx->roff.as<uint64_t>() + n0,
-                                                        ctx->flag.as<uint16_t>() + n0, nb,
-                                                        ctx->span.as<uint32_t>() + n0);
-        HIP_TRY(hipGetLastError());
-    }
+    // every record inside the batch's payload (and, without a span column, its span)
+    k_check_records<<<blocks_for(nb), kBlock, 0, s>>>(
+        ctx->payload.as<uint8_t>(), ctx->roff.as<uint64_t>() + n0, ctx->flag.as<uint16_t>() + n0, nb, (uint64_t)pay0,
+        (uint64_t)(pay0 + b->payload_bytes), b->span ? nullptr : ctx->span.as<uint32_t>() + n0,
+        ctx->order_bad.as<uint32_t>());
+    HIP_TRY(hipGetLastError());
     if (ctx->stream) {
         k_check_order<<<blocks_for(nb), kBlock, 0, s>>>(ctx->start.as<int32_t>(), n0, n0 + nb,
                                                         ctx->order_bad.as<uint32_t>());
@@ -3146,7 +3179,7 @@ static int run_segment(mgp_ctx* ctx, const Seg& sg, int slot, int& dup_parts, in
             nc, nF, ctx->covered.as<uint32_t>(), ctx->dsum.as<unsigned long long>(), ctx->dmax.as<uint32_t>(),
             ctx->n_reads.as<uint32_t>(), ctx->any_paired.as<uint8_t>(), ctx->first_read.as<uint32_t>(),
             ctx->F.as<uint32_t>(), ctx->roff_irregular.as<uint32_t>(), st, sg.first ? 3 : 2,
-            ctx->cell_cnt.as<uint32_t>());
+            ctx->cell_cnt.as<uint32_t>(), ctx->order_bad.as<uint32_t>());
         HIP_TRY(hipGetLastError());
     } else {
         if (sg.first) HIP_TRY(hipMemsetAsync(st, 0, sizeof(DevStats), s));
@@ -3392,11 +3425,21 @@ static int run_finish(mgp_ctx* ctx, int slot, int dup_parts, bool streamed) {
         // 6. min-reads gate
         if (ctx->cfg.min_reads > 1) {
             STAGE_BEGIN(ST_GATE);
+            // with a rows target, the rows already sent (the last segment's copies run on
+            // the D2H stream) are final before the gate rewrites the dropped cells there
+            const bool tgt = ctx->rows_on;
+            if (tgt) {
+                HIP_TRY(hipEventRecord(ctx->ev_rows, ctx->s_d2h));
+                HIP_TRY(hipStreamWaitEvent(s, ctx->ev_rows, 0));
+            }
             k_gate_fixup<<<nc, kBlock, 0, s>>>(g, ctx->cfg.min_reads, ctx->n_reads.as<uint32_t>(),
                                                out16_of(ctx), ctx->counts.as<uint32_t>(), ctx->tn5.as<uint32_t>(),
                                                ctx->depth.as<uint32_t>(), ctx->covered.as<uint32_t>(),
                                                ctx->dsum.as<unsigned long long>(), ctx->dmax.as<uint32_t>(),
-                                               ctx->tally_part.as<uint32_t>());
+                                               ctx->tally_part.as<uint32_t>(),
+                                               tgt ? reinterpret_cast<uint4*>(ctx->rows_tgt.counts) : nullptr,
+                                               tgt ? reinterpret_cast<uint32_t*>(ctx->rows_tgt.tn5) : nullptr,
+                                               tgt ? ctx->rows_tgt.depth : nullptr);
             HIP_TRY(hipGetLastError());
             STAGE_END(ST_GATE);
         }
@@ -3539,6 +3582,9 @@ int mgp_sync(mgp_ctx* ctx) {
         ctx->rerunning = false;
         return r;
     }
+    if (e & ERR_BADOFF)
+        return set_err(MGP_E_INVALID, "a pushed record (rec_off, its header or its CIGAR) lies outside its batch's "
+                                      "payload, or a dense stride is shorter than a full record");
     if (e & ERR_RESPEC) return set_err(MGP_E_STATE, "speculative grouping failed on the fallback path");
     if (e & ERR_UNSORTED) return set_err(MGP_E_UNSORTED, "records are not in coordinate order");
     if (e & ERR_BADBC) return set_err(MGP_E_INVALID, "barcode index >= n_cells");
@@ -3547,7 +3593,10 @@ int mgp_sync(mgp_ctx* ctx) {
         return set_err(MGP_E_BADREAD, "a kept read has no SEQ or QUAL (pysam would return None)");
     if (e & ERR_SPAN) return set_err(MGP_E_SPAN, "a read's CIGAR reach exceeds the declared span");
     if (e & ERR_PACKED)
-        return set_err(MGP_E_INVALID, "a record flagged MGP_FLAG_PACKED does not fit the packed layout's limits");
+        return set_err(MGP_E_INVALID, "a packed record (MGP_FLAG_PACKED / MGP_FLAG_PACK32) does not fit its layout's "
+                                      "limits, or a 32-byte record was made for other thresholds than the run's "
+                                      "(its min_baseq in byte 31 and min_distance_from_end in byte 3 must equal "
+                                      "the run's min_baseq and min_dist_from_end)");
     return MGP_OK;
 }
 
@@ -3638,8 +3687,6 @@ int mgp_set_rows16_target(mgp_ctx* ctx, const mgp_rows16* rows) {
         return MGP_OK;
     }
     if (!rows->counts || !rows->tn5 || !rows->depth || !rows->wide) return set_err(MGP_E_INVALID, "null rows array");
-    // the min-reads gate rewrites the rows of the cells it drops after the pileup
-    if (ctx->cfg.min_reads > 1) return set_err(MGP_E_STATE, "a rows target needs min_reads <= 1");
     // the kernel writes the rows through the device's mapping of the pinned arrays
     mgp_rows16 d{};
     void* dp = nullptr;
@@ -3656,6 +3703,13 @@ int mgp_set_rows16_target(mgp_ctx* ctx, const mgp_rows16* rows) {
     (void)hipGetLastError();
     ctx->rows_tgt = d;
     ctx->rows_on = true;
+    return MGP_OK;
+}
+
+int mgp_copy_wait(mgp_ctx* ctx) {
+    if (!ctx) return set_err(MGP_E_INVALID, "null ctx");
+    HIP_TRY(hipSetDevice(ctx->dev));
+    HIP_TRY(hipEventSynchronize(ctx->ev_copy));
     return MGP_OK;
 }
 
@@ -3827,7 +3881,10 @@ int mgp_synth_generate(mgp_ctx* ctx, const mgp_synth_params* p) {
     if (placed && p->payload_bytes > n_out * std::max<int64_t>(max_rec, 128) + 128)
         return set_err(MGP_E_INVALID, "synth payload_bytes out of range");
     MGP_TRY(ensure_inputs(ctx, std::max<int64_t>(n_out, 1), placed ? p->payload_bytes : n_out * rec_bytes, false));
-    // placed: rec_off has one entry per kept read
+    // placed: rec_off has one entry per kept read (n_rec_off of them)
+    if (placed && p->n_rec_off != n_out)
+        return set_err(MGP_E_INVALID, "synth rec_off has " + std::to_string(p->n_rec_off) + " entries for " +
+                                          std::to_string(n_out) + " generated reads");
     if (placed && n_out) {
         for (int64_t i = 0; i < n_out; ++i)
             if ((p->rec_off[i] & 15u) || (int64_t)p->rec_off[i] + rec_bytes > pay)

@@ -18,6 +18,8 @@ constexpr uint32_t ERR_PACKED = 32u;    // MGP_FLAG_PACKED record outside the pa
 constexpr uint32_t ERR_RESPEC = 64u;    // a read does not fit the speculative compact grouping (mgp_sync reruns)
 constexpr uint32_t ERR_BOUNDS = 128u;   // start-bin read ranges not monotone (unsorted input): grouping and
                                         // pileup kernels exit at entry, so no slot leaves its buffer
+constexpr uint32_t ERR_BADOFF = 256u;   // a pushed record (offset, header, CIGAR) lies outside its batch's payload
+                                        // (k_check_records at push; set with ERR_BOUNDS: no kernel reads records)
 
 // Counters written by the kernels of one run (zeroed at run start).
 struct DevStats {

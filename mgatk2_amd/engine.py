@@ -38,9 +38,9 @@ ABI_SYMBOLS = (
     "mgp_host_free", "mgp_push_batch", "mgp_reset", "mgp_resident", "mgp_run", "mgp_sync", "mgp_fetch",
     "mgp_finish", "mgp_kernel_times", "mgp_comm_unique_id", "mgp_comm_init", "mgp_synth_generate",
     "mgp_download_inputs", "mgp_set_stage_timing", "mgp_fetch_cells", "mgp_fetch_rows16", "mgp_windows",
-    "mgp_stream_info", "mgp_set_streaming", "mgp_set_rows16_target",
+    "mgp_stream_info", "mgp_set_streaming", "mgp_set_rows16_target", "mgp_copy_wait",
 )
-ABI_VERSION = 3
+ABI_VERSION = 4
 CFG_KEEP_TN5 = 0x1
 CFG_STREAM = 0x2
 
@@ -129,6 +129,7 @@ class mgp_synth_params(C.Structure):
         ("shard_world", C.c_int32),
         ("pack_min_baseq", C.c_int32),
         ("pack_min_dist", C.c_int32),
+        ("n_rec_off", C.c_int64),
     ]
 
 
@@ -186,6 +187,7 @@ def load_library(path: Path | None = None) -> C.CDLL:
         "mgp_windows": ([vp, C.POINTER(i32), C.POINTER(i32)], C.c_int),
         "mgp_stream_info": ([vp, C.POINTER(i64), C.POINTER(i32)], C.c_int),
         "mgp_set_streaming": ([vp, C.c_int], C.c_int),
+        "mgp_copy_wait": ([vp], C.c_int),
     }
     for name, (args, res) in sig.items():
         fn = getattr(lib, name)
@@ -399,7 +401,8 @@ class Engine:
         p = mgp_synth_params(int(seed), int(n_reads), int(read_len), int(cdf.shape[0]), _ptr(cdf), _ptr(ref),
                              int(rec_align), 2 if pack32 is not None else int(bool(pack)),
                              None if ro is None else _ptr(ro), int(payload_bytes) if ro is not None else 0, int(lo),
-                             int(hi), int(shard[0]), int(shard[1]), int(pack32 or 0), int(pack32_dist))
+                             int(hi), int(shard[0]), int(shard[1]), int(pack32 or 0), int(pack32_dist),
+                             0 if ro is None else int(ro.shape[0]))
         _ck(self.lib.mgp_synth_generate(self._h, C.byref(p)), "mgp_synth_generate")
 
     def download_inputs(self, columns: tuple[str, ...] | None = None, alloc=None) -> ReadSoA:
@@ -502,6 +505,11 @@ class Engine:
         r = mgp_rows16(_ptr(rows.counts), _ptr(rows.tn5), _ptr(rows.depth), _ptr(rows.wide))
         _ck(self.lib.mgp_set_rows16_target(self._h, C.byref(r)), "mgp_set_rows16_target")
         self._rows_tgt = rows  # kept alive while the engine copies into it
+
+    def copy_wait(self):
+        """mgp_copy_wait: every pushed batch's H2D copies are done (their host
+        buffers may be reused). The batches stay referenced until the next sync."""
+        _ck(self.lib.mgp_copy_wait(self._h), "mgp_copy_wait")
 
     def set_streaming(self, on: bool):
         """Streaming runs on or off for the next pushes (EngineConfig.stream initially)."""

@@ -1,0 +1,24 @@
+#!/bin/bash
+# Round 4 GPU pass: the GPU suite (verbose: one line per test), then the default bench
+# line. V names the logs; STEPS picks the parts (suite,bench,fullsize).
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+V=${V:-r4}
+STEPS=${STEPS:-suite,bench}
+if [[ $STEPS == *suite* ]]; then
+    timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread \
+        -p no:cacheprovider > gpurun_out/pytest_gpu_$V.log 2>&1 || { tail -30 gpurun_out/pytest_gpu_$V.log; exit 1; }
+    tail -3 gpurun_out/pytest_gpu_$V.log
+fi
+if [[ $STEPS == *fullsize* ]]; then
+    timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py -x -v -k "full_size" --timeout 300 \
+        --timeout-method thread -p no:cacheprovider > gpurun_out/pytest_fullsize_$V.log 2>&1 \
+        || { tail -30 gpurun_out/pytest_fullsize_$V.log; exit 1; }
+    tail -3 gpurun_out/pytest_fullsize_$V.log
+fi
+if [[ $STEPS == *bench* ]]; then
+    timeout -k 10 500 python -u bench.py > gpurun_out/bench_$V.log 2>&1 || { tail -30 gpurun_out/bench_$V.log; exit 1; }
+    tail -c 1500 gpurun_out/bench_$V.log
+fi

@@ -471,40 +471,81 @@ def _rows16_invariants(r16, res, lo, hi):
     return r16.counts[ok].reshape(int(ok.sum()), -1, 4, 2).sum(axis=(0, 3), dtype=np.uint64)
 
 
-def test_full_size_invariants_and_cell_sample_c4(engine_lib, oracle_lib):
-    """BASELINE config C4 at full size (200M reads x 10k cells, `run` parameters,
-    the bench's cell-paired placement): the per-cell invariants over every cell
-    (16-bit rows: none is wide), the run statistics and tallies, a rerun, and three
-    samples of 8 whole cells bit-exact against the oracle on exactly their reads."""
-    from mgatk2_amd.bam import PLACE_PAIRED, place_records
+def _oracle_cells_from_quality_records(oracle_lib, cfg, seed, n, cdf, ref, lo, hi):
+    """The oracle's results for cells [lo, hi) of the global set, from the
+    quality-carrying full 128-byte records of exactly those reads (regenerated as
+    a cell shard of the same seed): the reference's own per-base filters
+    (pileup.py:67-88: end distance, int8 quality >= min_baseq, ACGT) run on the
+    raw qualities here, so a 32-byte record built wrong by the producer (the
+    device generator's mgp_pack32_record) shows up as a mismatch."""
     from mgatk2_amd.engine import Engine, EngineConfig
-    from mgatk2_amd.shard import shard_soa
+
+    scfg = EngineConfig(**{**cfg.__dict__, "n_cells": hi - lo})
+    with Engine(scfg) as e2:
+        e2.synth(seed, n, cdf, ref, rec_align=128, pack=False, cells=(lo, hi), shard=(0, 0))
+        sub = e2.download_inputs()
+    assert sub.n > 1000 * (hi - lo)
+    assert not np.any(sub.flag & 0x6000)  # every record full (no packed bit): qualities as in the BAM
+    exp, _ = oracle_lib.oracle_run(scfg, sub)
+    return exp
+
+
+def _synth_layout(eng, seed, n, nc, cdf, ref, layout, min_baseq):
+    """The bench's inputs (bench.py): 32-byte records made for min_baseq, four of a
+    cell per 128-byte line (quad32), or packed 64-byte records two per line
+    (paired64), or packed 64-byte records in BAM order (packed64)."""
+    from mgatk2_amd.bam import PLACE_PAIRED, place_records
+
+    p32 = min_baseq if layout == "quad32" else None
+    eng.synth(seed, n, cdf, ref, pack32=p32)
+    if layout == "packed64":
+        return
+    cols = eng.download_inputs(columns=("bc", "flag", "start", "tlen"))
+    roff, pay_b = place_records(cols.bc, cols.flag, np.full(n, 32 if p32 is not None else 64, np.uint32), nc,
+                                PLACE_PAIRED, start=cols.start, tlen=cols.tlen)
+    del cols
+    eng.synth(seed, n, cdf, ref, rec_off=roff, payload_bytes=pay_b, pack32=p32)
+    del roff
+
+
+FULL_KEYS = ("counts", "tn5", "depth", "n_reads", "any_paired", "passed", "covered", "depth_sum", "depth_max",
+             "median_lo", "median_hi")
+
+
+@pytest.mark.parametrize("layout", ["paired64", "quad32"])
+def test_full_size_invariants_and_cell_sample_c4(engine_lib, oracle_lib, layout):
+    """BASELINE config C4 at full size (200M reads x 10k cells, `run` parameters) in
+    the bench's record layouts: the per-cell invariants over every cell (16-bit
+    rows: none is wide), the run statistics and tallies, a rerun, and three samples
+    of 8 whole cells bit-exact against the oracle on exactly their reads, the
+    oracle reading the quality-carrying full records of those reads (for quad32:
+    the producer's per-base filter, moved out of the kernel into the 32-byte
+    records' codes, is checked at full size)."""
+    from mgatk2_amd.engine import Engine, EngineConfig
     from mgatk2_amd.synth import cell_cdf, ref_codes
 
     n, nc, seed = 200_000_000, 10_000, 20251015 + 4
     cfg = EngineConfig(n_cells=nc, min_baseq=20, min_mapq=30, dedup_mode="alignment_and_fragment_length",
                        min_reads=1)
     cdf, ref = cell_cdf(seed, nc), ref_codes(seed)
+    ranges = ((0, 8), (5000, 5008), (nc - 8, nc))
     with Engine(cfg) as eng:
-        eng.synth(seed, n, cdf, ref)
-        cols = eng.download_inputs(columns=("bc", "flag", "start", "tlen"))
-        roff, pay_b = place_records(cols.bc, cols.flag, np.full(n, 64, np.uint32), nc, PLACE_PAIRED,
-                                    start=cols.start, tlen=cols.tlen)
-        del cols
-        eng.synth(seed, n, cdf, ref, rec_off=roff, payload_bytes=pay_b)
-        del roff
+        _synth_layout(eng, seed, n, nc, cdf, ref, layout, cfg.min_baseq)
+        flags = eng.download_inputs(columns=("flag",)).flag
+        want = 0x4000 if layout == "quad32" else 0x2000
+        assert np.count_nonzero(flags & want) == n  # every record in the layout under test
+        del flags
         eng.run()
         res = eng.fetch(dense=False)
         tally = np.zeros_like(res.ref_tally)
         for lo in range(0, nc, 2500):
             tally += _rows16_invariants(eng.fetch_rows16(lo, lo + 2500), res, lo, lo + 2500)
-        samples = {(lo, hi): eng.fetch_cells(lo, hi) for lo, hi in ((0, 8), (5000, 5008), (nc - 8, nc))}
+        samples = {r: eng.fetch_cells(*r) for r in ranges}
         first = eng.fetch_rows16(0, 2500).counts
         eng.run()
         again = eng.fetch(dense=False)
         np.testing.assert_array_equal(eng.fetch_rows16(0, 2500).counts, first)
         del first
-        inputs = eng.download_inputs()
     assert res.stats["total_reads"] == n and res.stats["error_bits"] == 0
     np.testing.assert_array_equal(res.ref_tally, tally)
     ok = res.passed.astype(bool)
@@ -515,18 +556,19 @@ def test_full_size_invariants_and_cell_sample_c4(engine_lib, oracle_lib):
     for k in ("n_reads", "covered", "depth_sum", "median_lo", "median_hi", "ref_tally"):
         np.testing.assert_array_equal(getattr(res, k), getattr(again, k), err_msg=f"rerun {k}")
     for (lo, hi), got in samples.items():
-        sub, _ = shard_soa(inputs, lo, hi)
-        exp, _ = oracle_lib.oracle_run(EngineConfig(**{**cfg.__dict__, "n_cells": hi - lo}), sub)
-        for k in ("counts", "tn5", "depth", "n_reads", "any_paired", "passed", "covered", "depth_sum",
-                  "depth_max", "median_lo", "median_hi"):
-            np.testing.assert_array_equal(getattr(got, k), getattr(exp, k), err_msg=f"cells {lo}-{hi} {k}")
+        exp = _oracle_cells_from_quality_records(oracle_lib, cfg, seed, n, cdf, ref, lo, hi)
+        for k in FULL_KEYS:
+            np.testing.assert_array_equal(getattr(got, k), getattr(exp, k), err_msg=f"{layout} cells {lo}-{hi} {k}")
 
 
-def test_full_size_cell_samples_c5(engine_lib, oracle_lib):
-    """BASELINE config C5 on one GPU (1B reads x 100k cells, `run` parameters):
-    sampled cell ranges of the full-size run bit-exact against the oracle on exactly
-    their reads (regenerated as a cell shard of the same global set), the per-cell
-    invariants over 4 ranges of 2000 cells, and the run statistics."""
+@pytest.mark.parametrize("layout", ["packed64", "quad32"])
+def test_full_size_cell_samples_c5(engine_lib, oracle_lib, layout):
+    """BASELINE config C5 on one GPU (1B reads x 100k cells, `run` parameters) in
+    the 64-byte and the bench's quad32 layout: sampled cell ranges of the
+    full-size run bit-exact against the oracle on the quality-carrying full
+    records of exactly their reads (regenerated as a cell shard of the same
+    global set), the per-cell invariants over 4 ranges of 2000 cells, and the run
+    statistics."""
     from mgatk2_amd.engine import Engine, EngineConfig
     from mgatk2_amd.synth import cell_cdf, ref_codes
 
@@ -536,7 +578,7 @@ def test_full_size_cell_samples_c5(engine_lib, oracle_lib):
     cdf, ref = cell_cdf(seed, nc), ref_codes(seed)
     ranges = ((0, 8), (49_996, 50_012), (nc - 8, nc))
     with Engine(cfg) as eng:
-        eng.synth(seed, n, cdf, ref)
+        _synth_layout(eng, seed, n, nc, cdf, ref, layout, cfg.min_baseq)
         eng.run()
         res = eng.fetch(dense=False)
         for lo in (0, 31_000, 64_000, nc - 2000):
@@ -546,15 +588,9 @@ def test_full_size_cell_samples_c5(engine_lib, oracle_lib):
     assert res.stats["filtered_reads"] == int(res.n_reads.sum())
     assert res.stats["cells_passed"] == int(res.passed.sum())
     for (lo, hi), got in samples.items():
-        scfg = EngineConfig(**{**cfg.__dict__, "n_cells": hi - lo})
-        with Engine(scfg) as e2:
-            e2.synth(seed, n, cdf, ref, cells=(lo, hi), shard=(0, 0))
-            sub = e2.download_inputs()
-        assert sub.n > 1000 * (hi - lo)
-        exp, _ = oracle_lib.oracle_run(scfg, sub)
-        for k in ("counts", "tn5", "depth", "n_reads", "any_paired", "passed", "covered", "depth_sum",
-                  "depth_max", "median_lo", "median_hi"):
-            np.testing.assert_array_equal(getattr(got, k), getattr(exp, k), err_msg=f"cells {lo}-{hi} {k}")
+        exp = _oracle_cells_from_quality_records(oracle_lib, cfg, seed, n, cdf, ref, lo, hi)
+        for k in FULL_KEYS:
+            np.testing.assert_array_equal(getattr(got, k), getattr(exp, k), err_msg=f"{layout} cells {lo}-{hi} {k}")
 
 
 # ---------------------------------------------------------------------------

@@ -420,27 +420,33 @@ def test_push_without_offsets_rejects_ragged_payloads(engine_lib):
 # ---------------------------------------------------------------------------
 # ABI v3.1: a rows target (the 16-bit rows leave the device as the windows complete)
 # ---------------------------------------------------------------------------
+@pytest.mark.parametrize("min_reads", [1, 4500])
 @pytest.mark.parametrize("layout", ["p32", "full"])
 @pytest.mark.parametrize("streamed", [False, True])
-def test_rows16_target_equals_fetch_rows16(engine_lib, streamed, layout):
+def test_rows16_target_equals_fetch_rows16(engine_lib, streamed, layout, min_reads):
     """The rows copied to a pinned target segment by segment equal mgp_fetch_rows16
     of a resident run, for a streamed run of 4 batches and a resident one, also on a
     rerun of the same context; full-layout records make a streamed run rerun resident
-    (the target then holds the rerun's rows); a min_reads > 1 context refuses a target."""
+    (the target then holds the rerun's rows). With min_reads above some cells' read
+    counts the gate (processors.py:22) drops those cells after their rows were sent:
+    their target rows are zeroed too (ABI 4)."""
     from dataclasses import replace
 
     from mgatk2_amd.engine import EngineConfig, PinnedBuffer, Rows16
-    from mgatk2_amd.exceptions import ProcessingError
     from mgatk2_amd.synth import synth_reads
 
     nc = 40
-    cfg = EngineConfig(n_cells=nc, **CONFIGS["run"])
+    cfg = EngineConfig(n_cells=nc, **{**CONFIGS["run"], "min_reads": min_reads})
     soa = synth_reads(717, 200_000, nc, **(dict(pack32=cfg.min_baseq) if layout == "p32" else dict(pack=False)))
     with engine_lib.Engine(cfg) as eng:
         eng.push(soa)
         eng.run()
         want = eng.fetch_rows16()
         want_res = eng.fetch()
+    if min_reads > 1:  # some cells gated, some passing
+        gated = (want_res.n_reads > 0) & (want_res.passed == 0)
+        assert gated.any() and want_res.passed.any()
+        assert not want.depth[gated].any()
     L = cfg.mito_len
     nw = want.wide.shape[1]
     buf = PinnedBuffer(nc * L * 22 + nc * nw + 64)
@@ -463,6 +469,53 @@ def test_rows16_target_equals_fetch_rows16(engine_lib, streamed, layout):
                 np.testing.assert_array_equal(getattr(tgt, k), getattr(want, k), err_msg=f"{k} rep {rep}")
             assert_same(got, want_res, f"rows target streamed={streamed} rep {rep}")
         eng.set_rows16_target(None)
-    with engine_lib.Engine(replace(cfg, min_reads=2)) as eng:
-        with pytest.raises(ProcessingError):
-            eng.set_rows16_target(tgt)
+
+
+@pytest.mark.parametrize("streamed", [False, True])
+@pytest.mark.parametrize("fault", ["offset", "misaligned", "cigar", "stride"])
+def test_records_outside_the_payload_raise(engine_lib, streamed, fault):
+    """A pushed record outside its batch's payload (an offset past the end, a
+    misaligned offset, a full record's CIGAR past the end, a dense stride shorter
+    than a full record) makes the run raise InvalidInputError without any kernel
+    reading the record; the context then runs a good batch normally (ABI 4)."""
+    from dataclasses import replace
+
+    from mgatk2_amd.engine import EngineConfig
+    from mgatk2_amd.exceptions import InvalidInputError
+    from mgatk2_amd.synth import ReadSoA, synth_reads
+
+    nc = 8
+    cfg = EngineConfig(n_cells=nc, **CONFIGS["run"])
+    if streamed:
+        cfg = replace(cfg, stream=True, reserve_reads=50_000, reserve_payload=50_000 * 256)
+    good = synth_reads(99, 20_000, nc, pack=False)  # full 128-byte records
+    with engine_lib.Engine(cfg) as eng:
+        eng.push(good)
+        want = eng.finish()
+    roff = good.rec_off.copy()
+    pay = good.payload.copy()
+    span = good.span
+    if fault == "offset":
+        roff[len(roff) // 2] = np.uint64(pay.shape[0] + 4096)
+    elif fault == "misaligned":
+        roff[7] += np.uint64(8)
+    elif fault == "cigar":
+        i = len(roff) - 1
+        o = int(roff[i])
+        pay[o + 8:o + 10] = np.frombuffer(np.uint16(4000).tobytes(), np.uint8)  # n_cigar far past the end
+    else:  # dense records at a 64-byte stride: a full record is 128 bytes
+        n = 1000
+        d = np.zeros(n * 64, np.uint8)
+        for i in range(n):
+            d[64 * i:64 * i + 64] = good.payload[int(good.rec_off[i]):int(good.rec_off[i]) + 64]
+        bad = ReadSoA(good.start[:n].copy(), good.bc[:n].copy(), good.tlen[:n].copy(), good.flag[:n].copy(),
+                      good.mapq[:n].copy(), None, None, d)
+    if fault != "stride":
+        bad = ReadSoA(good.start, good.bc, good.tlen, good.flag, good.mapq, span, roff, pay)
+    with engine_lib.Engine(cfg) as eng:
+        eng.push(bad)
+        with pytest.raises(InvalidInputError, match="outside its batch"):
+            eng.finish()
+        eng.reset()
+        eng.push(good)
+        assert_same(eng.finish(), want, "after a rejected batch")

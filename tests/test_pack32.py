@@ -138,3 +138,76 @@ def test_oracle_refuses_pack32_made_for_other_thresholds(oracle_lib):
     for kw in (dict(min_baseq=20, min_distance_from_end=4), dict(min_baseq=19, min_distance_from_end=5)):
         with pytest.raises(OracleError):
             oracle_lib.oracle_run(EngineConfig(n_cells=10, **kw), soa)
+
+
+def _random_reads(rng, n):
+    """pysam-like reads over the corners of the 32-byte layout: every CIGAR operation
+    (soft clips, insertions, deletions, skips, =/X, hard clips), 1-50 bases with N and
+    IUPAC codes, qualities 0-255 (>= 128 wraps negative as int8, pileup.py Q5)."""
+    out = []
+    for _ in range(n):
+        lseq = int(rng.integers(1, 51))
+        ops, q = [], 0
+        while q < lseq and len(ops) < 4:
+            op = int(rng.choice([0, 0, 0, 1, 2, 3, 4, 7, 8, 5]))
+            ln = int(rng.integers(1, 20))
+            if op in (0, 1, 4, 7, 8):
+                ln = min(ln, lseq - q)
+                q += ln
+            ops.append((op, ln))
+        if q < lseq and len(ops) < 4:
+            ops.append((0, lseq - q))
+        seq = "".join(rng.choice(list("ACGTACGTACGTNRY"), lseq))
+        qual = [int(x) for x in rng.integers(0, 256 if rng.random() < 0.3 else 64, lseq)]
+        out.append(dict(reference_start=int(rng.integers(0, 16569)), cigartuples=ops, query_sequence=seq,
+                        query_qualities=qual, flag=int(rng.choice([0x1, 0x11, 0x0, 0x10])), bc=0))
+    out.sort(key=lambda r: r["reference_start"])
+    return out
+
+
+@pytest.mark.parametrize("bmi2", [True, False])
+def test_host_pack32_builder_matches_the_definition(bmi2, tmp_path):
+    """The host producers' 32-byte builder (mgp_pack32_host.h, used by the BAM decoder
+    and mgp_repack32: SSE2 quality compares, BMI2 pdep or the portable deposit) gives
+    the bytes of the layout's definition (include/mgpileup.h mgp_pack32_record, via
+    its Python mirror) on random reads at every threshold corner; reads that do not
+    fit (more than 2 aligned blocks, CIGAR lengths >= 4096) keep their own layout."""
+    import subprocess
+    import sys
+    from pathlib import Path
+
+    code = r'''
+import sys, numpy as np
+sys.path.insert(0, sys.argv[1])
+sys.path.insert(0, sys.argv[1] + "/tests")
+from test_pack32 import _random_reads
+from mgatk2_amd.synth import FLAG_PACK32, pack_reads
+from mgatk2_amd.bam import repack32
+rng = np.random.default_rng(2025)
+reads = _random_reads(rng, 4000)
+reads.append(dict(reference_start=10, cigartuples=[(0, 5000)], query_sequence="A" * 20, query_qualities=[30] * 20,
+                  flag=0, bc=0))
+reads.sort(key=lambda r: r["reference_start"])
+full = pack_reads(reads, pack=False)
+n_fit = 0
+for q, d in ((20, 5), (0, 0), (-128, 0), (127, 15), (-5, 7), (63, 1), (-127, 2)):
+    want = pack_reads(reads, pack=False, pack32=q, pack32_dist=d)
+    o, f, k = repack32(full, q, d, n_threads=2)
+    assert np.array_equal(f, want.flag), (q, d)
+    fit = (want.flag & FLAG_PACK32) != 0
+    assert k == int(fit.sum())
+    for i in np.flatnonzero(fit):
+        r = int(want.rec_off[i])
+        assert np.array_equal(o[32 * i:32 * i + 32], want.payload[r:r + 32]), (q, d, i, reads[i])
+    assert not o.reshape(-1, 32)[~fit].any()
+    n_fit += int(fit.sum())
+assert n_fit > 3000 * 7 and not fit.all()
+print("ok", n_fit)
+'''
+    env = dict(__import__("os").environ)
+    if not bmi2:
+        env["MGP_NO_BMI2"] = "1"
+    root = str(Path(__file__).resolve().parent.parent)
+    r = subprocess.run([sys.executable, "-c", code, root], capture_output=True, text=True, env=env, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert r.stdout.startswith("ok")
