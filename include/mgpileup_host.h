@@ -82,6 +82,29 @@ int  mgp_bam_set_placement(mgp_bam *bam, int mode);
 int  mgp_bam_read_ref(mgp_bam *bam, int tid, int rec_align, mgp_bam_batch *out);
 void mgp_bam_free_batch(mgp_bam_batch *b);
 
+/* Records of reference `tid` per the index's metadata pseudo-bin (mapped + placed
+ * unmapped, as `samtools idxstats` counts them): the engine's reserve for a streamed
+ * run. -1 without an index or without the pseudo-bin. */
+int64_t mgp_bam_ref_records(mgp_bam *bam, int tid);
+
+/* Streaming decode of reference `tid` in batches: the one pass of
+ * readers.py:84-93 (`for read in bam.fetch(mito_chr)`), handed out as the engine's
+ * batches while later BGZF blocks are still being read, so the decode overlaps the
+ * device's copies and compute. The settings of `bam` at open (barcodes, bulk, packing,
+ * placement) apply; `bam` must outlive the stream. */
+typedef struct mgp_bam_stream mgp_bam_stream;
+int mgp_bam_stream_open(mgp_bam *bam, int tid, int rec_align, mgp_bam_stream **out);
+/* Decode the next records into the caller's arrays (`into`'s start, bc, tlen, flag,
+ * mapq, span and rec_off hold cap_reads entries, payload cap_payload bytes; e.g.
+ * pinned memory from mgp_host_alloc): as many records as fit both, in BAM order, with
+ * the batch's own payload placement (offsets from 0; paired lines never span
+ * batches: cap_payload needs 64 KiB + 256 bytes per whitelisted cell of slack).
+ * Sets into->n_reads and payload_bytes (256 zeroed bytes follow the payload when
+ * they fit); n_with_tag / first_tag_index count over the stream so far. Returns the
+ * records decoded, 0 at the end of the reference, -1 on error. */
+int64_t mgp_bam_stream_next(mgp_bam_stream *s, int64_t cap_reads, int64_t cap_payload, mgp_bam_batch *into);
+void mgp_bam_stream_close(mgp_bam_stream *s);
+
 /* Tag presence check of BAMReader._validate_bam_file (readers.py:53-59): index of
  * the first of the first `max_records` records of `tid` that carries `tag`, -1
  * if none does, -2 on error. `*n_checked` = records examined. */

@@ -108,6 +108,14 @@ def host_library() -> C.CDLL:
                                       C.c_char_p, C.c_int, C.c_int, C.c_int]
         lib.mgp_repack32.argtypes = [C.c_int64, vp, C.c_int64, vp, vp, C.c_int32, C.c_int32, vp, vp, C.c_int]
         lib.mgp_repack32.restype = C.c_int64
+        lib.mgp_bam_ref_records.argtypes = [vp, C.c_int]
+        lib.mgp_bam_ref_records.restype = C.c_int64
+        lib.mgp_bam_stream_open.argtypes = [vp, C.c_int, C.c_int, C.POINTER(vp)]
+        lib.mgp_bam_stream_open.restype = C.c_int
+        lib.mgp_bam_stream_next.argtypes = [vp, C.c_int64, C.c_int64, C.POINTER(mgp_bam_batch)]
+        lib.mgp_bam_stream_next.restype = C.c_int64
+        lib.mgp_bam_stream_close.argtypes = [vp]
+        lib.mgp_bam_stream_close.restype = None
         lib.mgp_host_buf_free.argtypes = [vp]
         lib.mgp_host_buf_free.restype = None
         _hlib = lib
@@ -236,18 +244,7 @@ class BamFile:
         run's min_baseq): reads that fit get the 32-byte record made for that
         threshold and min_dist_from_end pack32_dist (four to a line when paired)
         before the 64-byte one."""
-        paired = pack if paired is None else paired
-        arr = (C.c_char_p * max(1, len(barcodes)))(*[b.encode() for b in barcodes])
-        if self.lib.mgp_bam_set_barcodes(self._h, tag.encode(), arr, len(barcodes)) != 0:
-            raise ProcessingError(_err())
-        if bulk_cell >= 0 and self.lib.mgp_bam_set_bulk(self._h, int(bulk_cell)) != 0:
-            raise ProcessingError(_err())
-        if self.lib.mgp_bam_set_pack(self._h, int(bool(pack))) != 0:
-            raise ProcessingError(_err())
-        if self.lib.mgp_bam_set_pack32(self._h, int(pack32 is not None), int(pack32 or 0), int(pack32_dist)) != 0:
-            raise ProcessingError(_err())
-        if self.lib.mgp_bam_set_placement(self._h, PLACE_PAIRED if paired else PLACE_DENSE) != 0:
-            raise ProcessingError(_err())
+        self._configure(barcodes, tag, bulk_cell, pack, paired, pack32, pack32_dist)
         b = mgp_bam_batch()
         if self.lib.mgp_bam_read_ref(self._h, self.tid(contig), int(rec_align), C.byref(b)) != 0:
             raise BAMReadError(self.path, f"Read error: {_err()}")
@@ -271,6 +268,37 @@ class BamFile:
         )
         soa.extra.update(n_with_tag=int(b.n_with_tag), first_tag_index=int(b.first_tag_index))
         return soa
+
+    def _configure(self, barcodes: list[str], tag: str, bulk_cell: int, pack: bool, paired: bool | None,
+                   pack32: int | None, pack32_dist: int) -> None:
+        paired = pack if paired is None else paired
+        arr = (C.c_char_p * max(1, len(barcodes)))(*[b.encode() for b in barcodes])
+        if self.lib.mgp_bam_set_barcodes(self._h, tag.encode(), arr, len(barcodes)) != 0:
+            raise ProcessingError(_err())
+        if bulk_cell >= 0 and self.lib.mgp_bam_set_bulk(self._h, int(bulk_cell)) != 0:
+            raise ProcessingError(_err())
+        if self.lib.mgp_bam_set_pack(self._h, int(bool(pack))) != 0:
+            raise ProcessingError(_err())
+        if self.lib.mgp_bam_set_pack32(self._h, int(pack32 is not None), int(pack32 or 0), int(pack32_dist)) != 0:
+            raise ProcessingError(_err())
+        if self.lib.mgp_bam_set_placement(self._h, PLACE_PAIRED if paired else PLACE_DENSE) != 0:
+            raise ProcessingError(_err())
+
+    def ref_records(self, contig: str) -> int:
+        """Records of `contig` per the index's metadata (mapped + placed unmapped), -1 if unknown."""
+        return int(self.lib.mgp_bam_ref_records(self._h, self.tid(contig)))
+
+    def stream(self, contig: str, barcodes: list[str], tag: str = "CB", rec_align: int = 64, bulk_cell: int = -1,
+               pack: bool = True, paired: bool | None = None, pack32: int | None = None,
+               pack32_dist: int = 5) -> BamStream:
+        """Streaming decode of `contig` (mgp_bam_stream_*): batches of the records in
+        fetch order, decoded into the caller's arrays (:meth:`BamStream.next_into`).
+        Same settings as :meth:`read_soa`."""
+        self._configure(barcodes, tag, bulk_cell, pack, paired, pack32, pack32_dist)
+        h = C.c_void_p()
+        if self.lib.mgp_bam_stream_open(self._h, self.tid(contig), int(rec_align), C.byref(h)) != 0:
+            raise BAMReadError(self.path, f"Read error: {_err()}")
+        return BamStream(self, h)
 
     def find_tag(self, contig: str, tag: str, max_records: int) -> tuple[int, int]:
         """(index of the first record carrying `tag` among the first `max_records`
@@ -301,6 +329,75 @@ class BamFile:
             out[key] = cnt
             p = z + 9
         return out
+
+
+class StreamSlot:
+    """One batch's arrays for :meth:`BamStream.next_into` (any host memory; pinned
+    memory, e.g. views of engine.PinnedBuffer, makes the engine's copies async)."""
+
+    COLS = (("start", np.int32), ("bc", np.int32), ("tlen", np.int32), ("flag", np.uint16), ("mapq", np.uint8),
+            ("span", np.uint32), ("rec_off", np.uint64))
+
+    def __init__(self, cap_reads: int, cap_payload: int, alloc=None):
+        alloc = alloc or (lambda m, dt: np.empty(m, dt))
+        self.cap_reads, self.cap_payload = int(cap_reads), int(cap_payload)
+        for name, dt in self.COLS:
+            setattr(self, name, alloc(self.cap_reads, dt))
+        self.payload = alloc(self.cap_payload, np.uint8)
+        self.n = 0
+        self.payload_bytes = 0
+
+    @staticmethod
+    def nbytes(cap_reads: int, cap_payload: int) -> int:
+        return sum(int(cap_reads) * np.dtype(dt).itemsize + 64 for _, dt in StreamSlot.COLS) + int(cap_payload) + 64
+
+    def soa(self) -> ReadSoA:
+        """The decoded batch as views of the slot's arrays."""
+        n, pb = self.n, self.payload_bytes
+        return ReadSoA(self.start[:n], self.bc[:n], self.tlen[:n], self.flag[:n], self.mapq[:n], self.span[:n],
+                       self.rec_off[:n], self.payload[:pb])
+
+
+class BamStream:
+    """mgp_bam_stream: one pass over a contig in batches (readers.py:84-93)."""
+
+    def __init__(self, bam: BamFile, h: C.c_void_p):
+        self.bam = bam  # (outlives the stream)
+        self.lib = bam.lib
+        self._h = h
+        self.n_with_tag = 0
+        self.first_tag_index = -1
+        self.records = 0
+
+    def next_into(self, slot: StreamSlot) -> int:
+        """Decode the next batch into `slot`; returns its records (0 at the end)."""
+        b = mgp_bam_batch(0, *[C.cast(getattr(slot, name).ctypes.data, C.POINTER(t)) for (name, _), t in zip(
+            StreamSlot.COLS, (C.c_int32, C.c_int32, C.c_int32, C.c_uint16, C.c_uint8, C.c_uint32, C.c_uint64))],
+            C.cast(slot.payload.ctypes.data, C.POINTER(C.c_uint8)), 0, 0, -1)
+        n = self.lib.mgp_bam_stream_next(self._h, slot.cap_reads, slot.cap_payload, C.byref(b))
+        if n < 0:
+            raise BAMReadError(self.bam.path, f"Read error: {_err()}")
+        slot.n, slot.payload_bytes = int(b.n_reads), int(b.payload_bytes)
+        self.n_with_tag, self.first_tag_index = int(b.n_with_tag), int(b.first_tag_index)
+        self.records += int(n)
+        return int(n)
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self.lib.mgp_bam_stream_close(self._h)
+            self._h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 def txt_write_cells(prefix: str | Path, counts: np.ndarray, depth: np.ndarray, cells, names: list[str],

@@ -128,6 +128,7 @@ struct mgp_bam {
     uint64_t first_record_voff = 0;  // virtual offset right after the header
     bool has_index = false;
     std::vector<uint64_t> ref_first_voff;  // from the index; UINT64_MAX if the ref has no reads
+    std::vector<int64_t> ref_records;      // mapped + placed unmapped records (index pseudo-bin), -1 unknown
     StrTable wl;
     char tag[2] = {'C', 'B'};
     int32_t bulk_cell = -1;  // >= 0: every record goes to this cell (bulk calling)
@@ -423,6 +424,7 @@ int load_index(mgp_bam* bam) {
     p = 8;
     if (n_ref != (int32_t)bam->ref_names.size()) return fail("BAI reference count does not match the BAM");
     bam->ref_first_voff.assign((size_t)n_ref, UINT64_MAX);
+    bam->ref_records.assign((size_t)n_ref, -1);
     for (int32_t r = 0; r < n_ref; ++r) {
         if (!need(4)) return fail("truncated BAI");
         const int32_t n_bin = rdi32(d.data() + p);
@@ -436,6 +438,8 @@ int load_index(mgp_bam* bam) {
             if (!need((size_t)n_chunk * 16)) return fail("truncated BAI");
             if (bin != 37450)
                 for (int32_t c = 0; c < n_chunk; ++c) first = std::min(first, rd64(d.data() + p + (size_t)c * 16));
+            else if (n_chunk == 2)  // metadata: (extent), (n_mapped, n_unmapped)
+                bam->ref_records[(size_t)r] = (int64_t)(rd64(d.data() + p + 16) + rd64(d.data() + p + 24));
             p += (size_t)n_chunk * 16;
         }
         if (!need(4)) return fail("truncated BAI");
@@ -587,6 +591,339 @@ int for_each_batch(mgp_bam* bam, int tid, F&& f) {
     return 0;
 }
 
+// Header-level checks of mgp_pack32_record (include/mgpileup.h) on a raw BAM record.
+bool bam_packable32(int32_t pos, uint32_t l_seq, uint32_t n_cig, const uint8_t* cig) {
+    if (l_seq == 0 || l_seq > MGP_PACK_MAX_LEN || n_cig > 4 || pos < 0 || pos >= 65536) return false;
+    uint32_t blocks = 0;
+    for (uint32_t k = 0; k < n_cig; ++k) {
+        const uint32_t c = rd32(cig + 4 * k);
+        if ((c >> 4) >= 4096u) return false;
+        const uint32_t op = c & 15u;
+        blocks += op == 0 || op == 7 || op == 8;
+    }
+    return blocks <= 2;
+}
+
+// Header-level and quality checks of mgp_pack_record (include/mgpileup.h) on a
+// raw BAM record; the quality scan tests 8 bytes at a time.
+bool bam_packable(int32_t pos, uint16_t flg, uint32_t l_seq, uint32_t n_cig, const uint8_t* cig,
+                         const uint8_t* qualp) {
+    if (l_seq == 0 || l_seq > MGP_PACK_MAX_LEN || n_cig > 4 || pos < -(1 << 28) || pos >= (1 << 28)) return false;
+    (void)flg;
+    uint32_t blocks = 0;
+    for (uint32_t k = 0; k < n_cig; ++k) {
+        const uint32_t c = rd32(cig + 4 * k);
+        if ((c >> 4) >= 4096u) return false;
+        const uint32_t op = c & 15u;
+        blocks += op == 0 || op == 7 || op == 8;
+    }
+    if (blocks > 2) return false;
+    uint32_t k = 0;
+    for (; k + 8 <= l_seq; k += 8) {  // a byte > 62: its bit 7, or bit 7 of byte + 65
+        uint64_t x;
+        std::memcpy(&x, qualp + k, 8);
+        if ((x | ((x & 0x7F7F7F7F7F7F7F7Full) + 0x4141414141414141ull)) & 0x8080808080808080ull) return false;
+    }
+    for (; k < l_seq; ++k)
+        if (qualp[k] > 62) return false;
+    return true;
+}
+
+// The batch's arrays a decode writes (the library's growable arrays for
+// mgp_bam_read_ref, the caller's fixed arrays for mgp_bam_stream_next).
+struct Cols {
+    int32_t* start;
+    int32_t* bc;
+    int32_t* tlen;
+    uint16_t* flag;
+    uint8_t* mapq;
+    uint32_t* span;
+    uint64_t* roff;
+    uint8_t* pay;
+};
+
+// Record decode + packing + producer placement, one chunk of records at a time:
+// classify() is pass 1 (sequential, header fields only: CIGAR location with the CG
+// tag, record layout, record bytes), decode() places the chunk's records (pass 1b)
+// and decodes the columns and payload records on the thread pool (pass 2). A batch
+// (begin_batch) may take several chunks (inflated buffers); its payload starts at 0.
+struct Decoder {
+    mgp_bam* b;
+    uint64_t amask;
+    bool paired;
+    int32_t n_keys = 0;
+    // paired placement (mgp_place_records' rule, applied chunk by chunk as records
+    // stream in): open[key] = the line of cell `key` whose second half is free; key
+    // n_keys collects the reads the engine's filters drop
+    std::vector<uint64_t> open, open32;
+    std::vector<uint8_t> fill32;
+    mgp_host::DupTracker dups;  // a cell's repeated keys go with the dropped reads
+    uint64_t cursor = 0;        // payload bytes placed in the batch so far
+    int64_t n_tag = 0, first_tag = -1;
+    // the chunk
+    std::vector<const uint8_t*> recs;
+    std::vector<uint32_t> sizes;
+    std::vector<uint64_t> rsz;  // payload bytes of each record (then, unpaired, its offset)
+    std::vector<uint32_t> ncg;  // CIGAR operations (CG tag resolved)
+    std::vector<const uint8_t*> cgp;
+    std::vector<uint8_t> pkd;   // record layout: 0 full, 1 packed 64-byte, 2 32-byte
+    double t_p1 = 0, t_p2 = 0;
+
+    static int32_t keys_of(mgp_bam* b) {
+        int32_t n = 0;
+        for (int32_t v : b->wl.vals) n = std::max(n, v + 1);
+        if (b->bulk_cell >= 0) n = std::max(n, b->bulk_cell + 1);
+        return n;
+    }
+    Decoder(mgp_bam* bam, int rec_align)
+        : b(bam), amask((uint64_t)rec_align - 1), paired(bam->placement == MGP_PLACE_PAIRED),
+          n_keys(paired ? keys_of(bam) : 0), dups(paired ? (size_t)keys_of(bam) : 0) {
+        open.assign(paired ? (size_t)n_keys + 1 : 0, ~0ull);
+        open32.assign(paired ? (size_t)n_keys + 1 : 0, ~0ull);
+        fill32.assign(paired ? (size_t)n_keys + 1 : 0, 0);
+    }
+    void begin_batch() {
+        cursor = 0;
+        std::fill(open.begin(), open.end(), ~0ull);
+        std::fill(open32.begin(), open32.end(), ~0ull);
+        std::fill(fill32.begin(), fill32.end(), (uint8_t)0);
+    }
+    void clear_chunk() {
+        recs.clear();
+        sizes.clear();
+        rsz.clear();
+        ncg.clear();
+        cgp.clear();
+        pkd.clear();
+    }
+    // payload bytes a classified record takes at most in its batch, lines included
+    // (a batch may also leave one partly filled line per key and layout: callers add
+    // 2 x 128 x (n_keys + 1))
+    uint64_t worst(size_t i) const {
+        if (!paired) return (rsz[i] + amask) & ~amask;
+        return pkd[i] ? rsz[i] : ((rsz[i] + 127) & ~127ull) + 127;
+    }
+    uint64_t line_slack() const { return paired ? 2ull * 128ull * ((uint64_t)n_keys + 1) : 0ull; }
+
+    // pass 1 for one record (appended to the chunk); false on a malformed record
+    bool classify(const uint8_t* r, uint32_t size) {
+        const uint8_t l_name = r[8];
+        uint32_t n_cig = rd16(r + 12);
+        const uint32_t l_seq = rd32(r + 16);
+        const uint8_t* cigp = r + 32 + l_name;
+        const uint8_t* auxp = cigp + 4 * (size_t)n_cig + ((size_t)l_seq + 1) / 2 + l_seq;
+        if (auxp > r + size) return fail("corrupt BAM record (fields exceed block_size)"), false;
+        const uint8_t* cig = cigp;
+        // CIGAR with > 65535 operations lives in the CG:B,I tag (placeholder kSmN)
+        if (n_cig == 2 && (rd32(cigp) & 15u) == 4 && (rd32(cigp) >> 4) == l_seq && (rd32(cigp + 4) & 15u) == 3) {
+            Aux aux{auxp, r + size};
+            const uint8_t* t = aux.find("CG");
+            if (t && t[0] == 'B' && (t[1] == 'I' || t[1] == 'i')) {
+                n_cig = rd32(t + 2);
+                cig = t + 6;
+            }
+        }
+        if (n_cig > 0xFFFF)
+            return fail("CIGAR with more than 65535 operations is not supported by the record format"), false;
+        const uint8_t* qualp = cigp + 4 * (size_t)rd16(r + 12) + ((size_t)l_seq + 1) / 2;
+        const bool seqqual = l_seq != 0 && qualp[0] != 0xFF;  // else NOSEQQUAL: never packed
+        const uint8_t pk = (b->pack32 && seqqual && bam_packable32(rdi32(r + 4), l_seq, n_cig, cig)) ? 2
+                           : (b->pack && bam_packable(rdi32(r + 4), rd16(r + 14), l_seq, n_cig, cig, qualp)) ? 1 : 0;
+        recs.push_back(r);
+        sizes.push_back(size);
+        ncg.push_back(n_cig);
+        cgp.push_back(cig);
+        pkd.push_back(pk);
+        rsz.push_back(pk == 2 ? (uint64_t)MGP_PACK32_BYTES
+                      : pk ? (uint64_t)MGP_PACK_BYTES
+                           : (uint64_t)mgp_cigar_offset(l_seq) + 4ull * n_cig);
+        return true;
+    }
+    void unclassify_last() {
+        recs.pop_back();
+        sizes.pop_back();
+        ncg.pop_back();
+        cgp.pop_back();
+        pkd.pop_back();
+        rsz.pop_back();
+    }
+
+    // one record: decode (do_fields: the SoA columns, barcode lookup included) and
+    // pack (do_rec: the payload record at offset off) at index k
+    void decode_one(const Cols& c, const uint8_t* r, uint32_t bs, size_t k, uint64_t off, uint32_t n_cig,
+                    const uint8_t* cig, int pk, int64_t& tags, int64_t& first, int64_t gidx, bool do_fields,
+                    bool do_rec) const {
+        const uint8_t* end = r + bs;
+        const int32_t pos = rdi32(r + 4);
+        const uint8_t l_name = r[8];
+        const uint8_t mq = r[9];
+        const uint16_t flg = rd16(r + 14);
+        const uint32_t l_seq = rd32(r + 16);
+        const int32_t tl = rdi32(r + 28);
+        const uint8_t* seqp = r + 32 + l_name + 4 * (size_t)rd16(r + 12);
+        const uint8_t* qualp = seqp + ((size_t)l_seq + 1) / 2;
+        const uint8_t* auxp = qualp + l_seq;
+        uint16_t fl = flg & 0x0FFF;
+        if (l_seq == 0 || qualp[0] == 0xFF) fl |= MGP_FLAG_NOSEQQUAL;
+        if (pk == 1) fl |= MGP_FLAG_PACKED;
+        if (pk == 2) fl |= MGP_FLAG_PACK32;
+        if (do_fields) {
+            Aux aux{auxp, end};
+            int32_t bcv = -1;
+            const uint8_t* t = aux.find(b->tag);
+            if (t) {
+                ++tags;
+                if (first < 0) first = gidx;
+                if (t[0] == 'Z' || t[0] == 'H') {  // get_tag() -> str; numeric tags never match
+                    const char* sv = (const char*)t + 1;
+                    bcv = b->wl.get(sv, std::strlen(sv));
+                } else if (t[0] == 'A') {
+                    bcv = b->wl.get((const char*)t + 1, 1);
+                }
+            }
+            if (b->bulk_cell >= 0) bcv = b->bulk_cell;
+            c.start[k] = pos;
+            c.bc[k] = bcv;
+            c.tlen[k] = tl;
+            c.flag[k] = fl;
+            c.mapq[k] = mq;
+            c.span[k] = std::max(cigar_ref_span(cig, n_cig), l_seq);
+            c.roff[k] = off;
+        }
+        if (!do_rec) return;
+        uint8_t* rec = c.pay + off;
+        if (pk == 2) {
+            uint32_t cw[4] = {0, 0, 0, 0};
+            for (uint32_t q = 0; q < n_cig; ++q) cw[q] = rd32(cig + 4 * q);
+            const uint64_t size = ((uint64_t)MGP_PACK32_BYTES + amask) & ~amask;
+            if (size > MGP_PACK32_BYTES && !paired) std::memset(rec + MGP_PACK32_BYTES, 0, size - MGP_PACK32_BYTES);
+            mgp_host::pack32_record_fast(pos, l_seq, fl, n_cig, cw, seqp, qualp, b->pack32_minq, b->pack32_dist,
+                                         rec);  // all 32 B
+        } else if (pk) {
+            uint32_t cw[4] = {0, 0, 0, 0};
+            for (uint32_t q = 0; q < n_cig; ++q) cw[q] = rd32(cig + 4 * q);
+            const uint64_t size = ((uint64_t)MGP_PACK_BYTES + amask) & ~amask;
+            if (size > MGP_PACK_BYTES && !paired) std::memset(rec + MGP_PACK_BYTES, 0, size - MGP_PACK_BYTES);
+            mgp_pack_record(pos, l_seq, fl, n_cig, cw, seqp, qualp, rec);  // writes all 64 bytes
+        } else {
+            const uint32_t soff = mgp_seq_offset(l_seq);
+            const uint32_t coff = mgp_cigar_offset(l_seq);
+            const uint64_t size = ((uint64_t)coff + 4ull * n_cig + (paired ? 127u : amask)) & ~(paired ? 127ull : amask);
+            std::memset(rec, 0, size);
+            std::memcpy(rec, &pos, 4);
+            std::memcpy(rec + 4, &l_seq, 4);
+            const uint16_t nc16 = (uint16_t)n_cig;
+            std::memcpy(rec + 8, &nc16, 2);
+            std::memcpy(rec + 10, &fl, 2);
+            std::memcpy(rec + 12, &coff, 4);
+            if (l_seq) {
+                std::memcpy(rec + 16, qualp, l_seq);
+                std::memcpy(rec + soff, seqp, ((size_t)l_seq + 1) / 2);
+            }
+            if (n_cig) std::memcpy(rec + coff, cig, 4 * (size_t)n_cig);
+        }
+    }
+
+    // Decode the chunk's records at index k0 of the batch (global record index gidx0),
+    // payload appended at `cursor`. reserve(kn, pay_end) makes room for kn columns and
+    // pay_end payload bytes (+256), then cols() are the arrays; false = out of memory.
+    template <class Reserve, class GetCols>
+    int decode(size_t k0, int64_t gidx0, int nt, Reserve&& reserve, GetCols&& cols) {
+        const double tp1 = now_s();
+        const size_t m = recs.size();
+        if (!m) return 0;
+        const size_t kn = k0 + m;
+        // unpaired: dense offsets from the cursor (records are rec_align-sized)
+        uint64_t end = cursor;
+        if (!paired) {
+            for (size_t i = 0; i < m; ++i) {
+                const uint64_t off = (end + amask) & ~amask;
+                end = off + ((rsz[i] + amask) & ~amask);
+                rsz[i] = off;
+            }
+        }
+        if (!reserve(kn, paired ? cursor : end)) return fail("out of host memory"), -1;
+        const double tp2 = now_s();
+        t_p1 += tp2 - tp1;
+        const int tn = (int)std::max<size_t>(1, std::min<size_t>((size_t)nt, m / 4096 + 1));
+        std::vector<int64_t> tags((size_t)tn, 0), firsts((size_t)tn, -1);
+        auto run_pass = [&](const Cols& c, bool do_fields, bool do_rec) {
+            auto work = [&](int t) {
+                const size_t lo = m * (size_t)t / (size_t)tn, hi = m * (size_t)(t + 1) / (size_t)tn;
+                for (size_t i = lo; i < hi; ++i)
+                    decode_one(c, recs[i], sizes[i], k0 + i, paired ? c.roff[k0 + i] : rsz[i], ncg[i], cgp[i],
+                               (int)pkd[i], tags[(size_t)t], firsts[(size_t)t], gidx0 + (int64_t)i, do_fields, do_rec);
+            };
+            std::vector<std::thread> th;
+            for (int t = 1; t < tn; ++t) th.emplace_back(work, t);
+            work(0);
+            for (auto& x : th) x.join();
+        };
+        if (!paired) {
+            run_pass(cols(), true, true);
+            cursor = end;
+        } else {
+            {
+                const Cols c = cols();
+                run_pass(c, true, false);
+                // pass 1b: which half-line each record takes (mgp_place_records' rule)
+                const uint16_t drop = MGP_FLAG_UNMAPPED | MGP_FLAG_SECONDARY | MGP_FLAG_SUPPLEMENTARY;
+                for (size_t i = 0; i < m; ++i) {
+                    const size_t k = k0 + i;
+                    if (!pkd[i]) {
+                        cursor = (cursor + 127) & ~127ull;
+                        c.roff[k] = cursor;
+                        cursor += (rsz[i] + 127) & ~127ull;
+                        continue;
+                    }
+                    const int32_t cc = c.bc[k];
+                    size_t key = (cc >= 0 && cc < n_keys && !(c.flag[k] & drop)) ? (size_t)cc : (size_t)n_keys;
+                    if (key < (size_t)n_keys &&
+                        dups.repeat(key, c.start[k], (c.flag[k] & MGP_FLAG_REVERSE) != 0, c.tlen[k]))
+                        key = (size_t)n_keys;
+                    if (pkd[i] == 2) {  // four 32-byte records of one key per line
+                        if (open32[key] == ~0ull) {
+                            cursor = (cursor + 127) & ~127ull;
+                            open32[key] = cursor;
+                            fill32[key] = 0;
+                            cursor += 128;
+                        }
+                        c.roff[k] = open32[key] + (uint64_t)MGP_PACK32_BYTES * fill32[key];
+                        if (++fill32[key] == 4) open32[key] = ~0ull;
+                        continue;
+                    }
+                    if (open[key] != ~0ull) {
+                        c.roff[k] = open[key] + MGP_PACK_BYTES;
+                        open[key] = ~0ull;
+                    } else {
+                        cursor = (cursor + 127) & ~127ull;
+                        c.roff[k] = open[key] = cursor;
+                        cursor += 128;
+                    }
+                }
+            }
+            if (!reserve(kn, cursor)) return fail("out of host memory"), -1;
+            const Cols c = cols();
+            // second halves of lines that stay open: zero (a later chunk may still fill
+            // them; the others are fully written); only lines of this chunk can be open
+            // and unwritten, lines of earlier chunks were zeroed then
+            for (uint64_t o : open)
+                if (o != ~0ull) std::memset(c.pay + o + MGP_PACK_BYTES, 0, MGP_PACK_BYTES);
+            for (size_t key = 0; key < open32.size(); ++key)
+                if (open32[key] != ~0ull)
+                    std::memset(c.pay + open32[key] + (uint64_t)MGP_PACK32_BYTES * fill32[key], 0,
+                                (uint64_t)MGP_PACK32_BYTES * (4u - fill32[key]));
+            run_pass(c, false, true);
+        }
+        for (int t = 0; t < tn; ++t) {
+            n_tag += tags[(size_t)t];
+            if (first_tag < 0 && firsts[(size_t)t] >= 0) first_tag = firsts[(size_t)t];
+        }
+        t_p2 += now_s() - tp2;
+        return 0;
+    }
+};
+
 // Growable malloc'd array (handed to the caller as is: no final copy).
 template <typename T>
 struct Grow {
@@ -693,44 +1030,6 @@ int mgp_bam_set_pack32(mgp_bam* b, int on, int min_baseq, int min_dist) {
     return 0;
 }
 
-// Header-level checks of mgp_pack32_record (include/mgpileup.h) on a raw BAM record.
-static bool bam_packable32(int32_t pos, uint32_t l_seq, uint32_t n_cig, const uint8_t* cig) {
-    if (l_seq == 0 || l_seq > MGP_PACK_MAX_LEN || n_cig > 4 || pos < 0 || pos >= 65536) return false;
-    uint32_t blocks = 0;
-    for (uint32_t k = 0; k < n_cig; ++k) {
-        const uint32_t c = rd32(cig + 4 * k);
-        if ((c >> 4) >= 4096u) return false;
-        const uint32_t op = c & 15u;
-        blocks += op == 0 || op == 7 || op == 8;
-    }
-    return blocks <= 2;
-}
-
-// Header-level and quality checks of mgp_pack_record (include/mgpileup.h) on a
-// raw BAM record; the quality scan tests 8 bytes at a time.
-static bool bam_packable(int32_t pos, uint16_t flg, uint32_t l_seq, uint32_t n_cig, const uint8_t* cig,
-                         const uint8_t* qualp) {
-    if (l_seq == 0 || l_seq > MGP_PACK_MAX_LEN || n_cig > 4 || pos < -(1 << 28) || pos >= (1 << 28)) return false;
-    (void)flg;
-    uint32_t blocks = 0;
-    for (uint32_t k = 0; k < n_cig; ++k) {
-        const uint32_t c = rd32(cig + 4 * k);
-        if ((c >> 4) >= 4096u) return false;
-        const uint32_t op = c & 15u;
-        blocks += op == 0 || op == 7 || op == 8;
-    }
-    if (blocks > 2) return false;
-    uint32_t k = 0;
-    for (; k + 8 <= l_seq; k += 8) {  // a byte > 62: its bit 7, or bit 7 of byte + 65
-        uint64_t x;
-        std::memcpy(&x, qualp + k, 8);
-        if ((x | ((x & 0x7F7F7F7F7F7F7F7Full) + 0x4141414141414141ull)) & 0x8080808080808080ull) return false;
-    }
-    for (; k < l_seq; ++k)
-        if (qualp[k] > 62) return false;
-    return true;
-}
-
 int mgp_bam_read_ref(mgp_bam* b, int tid, int rec_align, mgp_bam_batch* out) {
     g_err.clear();
     if (!b || !out) return fail("null argument");
@@ -743,240 +1042,33 @@ int mgp_bam_read_ref(mgp_bam* b, int tid, int rec_align, mgp_bam_batch* out) {
     Grow<uint8_t> G_mapq, G_pay;
     Grow<uint32_t> G_span;
     Grow<uint64_t> G_roff;
-    int64_t n_tag = 0, first_tag = -1;
-    const uint64_t amask = (uint64_t)rec_align - 1;
     const int nt = std::max(1, b->n_threads);
     const double t_begin = now_s();
-    double t_p1 = 0, t_p2 = 0;
     t_inflate = t_pread = 0;
-    std::vector<uint64_t> rsz;  // payload bytes of each record of the batch (then its offset)
-    std::vector<uint32_t> ncg;  // CIGAR operations (CG tag resolved)
-    std::vector<const uint8_t*> cgp;
-    std::vector<uint8_t> pkd;   // record layout: 0 full, 1 packed 64-byte, 2 32-byte
-    // producer placement (mgp_place_records' rule, applied batch by batch as records
-    // stream in): open[key] = the line of cell `key` whose second half is free;
-    // key n_cells collects the reads the engine's filters drop
-    const bool paired = b->placement == MGP_PLACE_PAIRED;
-    int32_t n_keys = 0;
-    if (paired) {
-        for (int32_t v : b->wl.vals) n_keys = std::max(n_keys, v + 1);
-        if (b->bulk_cell >= 0) n_keys = std::max(n_keys, b->bulk_cell + 1);
-    }
-    std::vector<uint64_t> open(paired ? (size_t)n_keys + 1 : 0, ~0ull);
-    std::vector<uint64_t> open32(paired ? (size_t)n_keys + 1 : 0, ~0ull);  // 32-byte records: 4 per line
-    std::vector<uint8_t> fill32(paired ? (size_t)n_keys + 1 : 0, 0);
-    mgp_host::DupTracker dups(paired ? (size_t)n_keys : 0);  // a cell's repeated keys go with the dropped reads
-    uint64_t cursor = 0;  // paired: payload bytes placed so far (128-byte lines)
-    // one record: decode (do_fields: the SoA columns, barcode lookup included) and
-    // pack (do_rec: the payload record at offset off) at index k
-    auto decode = [&](const uint8_t* r, uint32_t bs, size_t k, uint64_t off, uint32_t n_cig, const uint8_t* cig,
-                      int pk, int64_t& tags, int64_t& first, int64_t gidx, bool do_fields, bool do_rec) {
-        const uint8_t* end = r + bs;
-        const int32_t pos = rdi32(r + 4);
-        const uint8_t l_name = r[8];
-        const uint8_t mq = r[9];
-        const uint16_t flg = rd16(r + 14);
-        const uint32_t l_seq = rd32(r + 16);
-        const int32_t tl = rdi32(r + 28);
-        const uint8_t* seqp = r + 32 + l_name + 4 * (size_t)rd16(r + 12);
-        const uint8_t* qualp = seqp + ((size_t)l_seq + 1) / 2;
-        const uint8_t* auxp = qualp + l_seq;
-        uint16_t fl = flg & 0x0FFF;
-        if (l_seq == 0 || qualp[0] == 0xFF) fl |= MGP_FLAG_NOSEQQUAL;
-        if (pk == 1) fl |= MGP_FLAG_PACKED;
-        if (pk == 2) fl |= MGP_FLAG_PACK32;
-        if (do_fields) {
-            Aux aux{auxp, end};
-            int32_t bcv = -1;
-            const uint8_t* t = aux.find(b->tag);
-            if (t) {
-                ++tags;
-                if (first < 0) first = gidx;
-                if (t[0] == 'Z' || t[0] == 'H') {  // get_tag() -> str; numeric tags never match
-                    const char* sv = (const char*)t + 1;
-                    bcv = b->wl.get(sv, std::strlen(sv));
-                } else if (t[0] == 'A') {
-                    bcv = b->wl.get((const char*)t + 1, 1);
-                }
-            }
-            if (b->bulk_cell >= 0) bcv = b->bulk_cell;
-            G_start.p[k] = pos;
-            G_bc.p[k] = bcv;
-            G_tlen.p[k] = tl;
-            G_flag.p[k] = fl;
-            G_mapq.p[k] = mq;
-            G_span.p[k] = std::max(cigar_ref_span(cig, n_cig), l_seq);
-            G_roff.p[k] = off;
-        }
-        if (!do_rec) return;
-        uint8_t* rec = G_pay.p + off;
-        if (pk == 2) {
-            uint32_t cw[4] = {0, 0, 0, 0};
-            for (uint32_t q = 0; q < n_cig; ++q) cw[q] = rd32(cig + 4 * q);
-            const uint64_t size = ((uint64_t)MGP_PACK32_BYTES + amask) & ~amask;
-            if (size > MGP_PACK32_BYTES && !paired) std::memset(rec + MGP_PACK32_BYTES, 0, size - MGP_PACK32_BYTES);
-            mgp_host::pack32_record_fast(pos, l_seq, fl, n_cig, cw, seqp, qualp, b->pack32_minq, b->pack32_dist,
-                                         rec);  // all 32 B
-        } else if (pk) {
-            uint32_t cw[4] = {0, 0, 0, 0};
-            for (uint32_t q = 0; q < n_cig; ++q) cw[q] = rd32(cig + 4 * q);
-            const uint64_t size = ((uint64_t)MGP_PACK_BYTES + amask) & ~amask;
-            if (size > MGP_PACK_BYTES && !paired) std::memset(rec + MGP_PACK_BYTES, 0, size - MGP_PACK_BYTES);
-            mgp_pack_record(pos, l_seq, fl, n_cig, cw, seqp, qualp, rec);  // writes all 64 bytes
-        } else {
-            const uint32_t soff = mgp_seq_offset(l_seq);
-            const uint32_t coff = mgp_cigar_offset(l_seq);
-            const uint64_t size = ((uint64_t)coff + 4ull * n_cig + (paired ? 127u : amask)) & ~(paired ? 127ull : amask);
-            std::memset(rec, 0, size);
-            std::memcpy(rec, &pos, 4);
-            std::memcpy(rec + 4, &l_seq, 4);
-            const uint16_t nc16 = (uint16_t)n_cig;
-            std::memcpy(rec + 8, &nc16, 2);
-            std::memcpy(rec + 10, &fl, 2);
-            std::memcpy(rec + 12, &coff, 4);
-            if (l_seq) {
-                std::memcpy(rec + 16, qualp, l_seq);
-                std::memcpy(rec + soff, seqp, ((size_t)l_seq + 1) / 2);
-            }
-            if (n_cig) std::memcpy(rec + coff, cig, 4 * (size_t)n_cig);
-        }
+    Decoder dec(b, rec_align);
+    dec.begin_batch();
+    auto reserve = [&](size_t kn, uint64_t pay_end) {
+        return G_start.reserve(kn) && G_bc.reserve(kn) && G_tlen.reserve(kn) && G_flag.reserve(kn) &&
+               G_mapq.reserve(kn) && G_span.reserve(kn) && G_roff.reserve(kn) && G_pay.reserve(pay_end + 256);
     };
+    auto cols = [&]() { return Cols{G_start.p, G_bc.p, G_tlen.p, G_flag.p, G_mapq.p, G_span.p, G_roff.p, G_pay.p}; };
     const int rc = for_each_batch(b, tid, [&](const std::vector<const uint8_t*>& recs,
                                               const std::vector<uint32_t>& sizes) -> int {
         const double tp1 = now_s();
-        const size_t m = recs.size();
-        rsz.resize(m);
-        ncg.resize(m);
-        cgp.resize(m);
-        pkd.assign(m, 0);
-        // pass 1 (sequential, header fields only): sizes, CIGAR location, checks
-        uint64_t tot = 0;
-        for (size_t i = 0; i < m; ++i) {
-            const uint8_t* r = recs[i];
-            const uint8_t l_name = r[8];
-            uint32_t n_cig = rd16(r + 12);
-            const uint32_t l_seq = rd32(r + 16);
-            const uint8_t* cigp = r + 32 + l_name;
-            const uint8_t* auxp = cigp + 4 * (size_t)n_cig + ((size_t)l_seq + 1) / 2 + l_seq;
-            if (auxp > r + sizes[i]) return fail("corrupt BAM record (fields exceed block_size)"), -1;
-            const uint8_t* cig = cigp;
-            // CIGAR with > 65535 operations lives in the CG:B,I tag (placeholder kSmN)
-            if (n_cig == 2 && (rd32(cigp) & 15u) == 4 && (rd32(cigp) >> 4) == l_seq && (rd32(cigp + 4) & 15u) == 3) {
-                Aux aux{auxp, r + sizes[i]};
-                const uint8_t* t = aux.find("CG");
-                if (t && t[0] == 'B' && (t[1] == 'I' || t[1] == 'i')) {
-                    n_cig = rd32(t + 2);
-                    cig = t + 6;
-                }
-            }
-            if (n_cig > 0xFFFF)
-                return fail("CIGAR with more than 65535 operations is not supported by the record format"), -1;
-            ncg[i] = n_cig;
-            cgp[i] = cig;
-            const uint8_t* qualp = cigp + 4 * (size_t)rd16(r + 12) + ((size_t)l_seq + 1) / 2;
-            const bool seqqual = l_seq != 0 && qualp[0] != 0xFF;  // else NOSEQQUAL: never packed
-            pkd[i] = (b->pack32 && seqqual && bam_packable32(rdi32(r + 4), l_seq, n_cig, cig)) ? 2
-                     : (b->pack && bam_packable(rdi32(r + 4), rd16(r + 14), l_seq, n_cig, cig, qualp)) ? 1 : 0;
-            const uint64_t rb = pkd[i] == 2 ? (uint64_t)MGP_PACK32_BYTES
-                                : pkd[i] ? (uint64_t)MGP_PACK_BYTES
-                                         : (uint64_t)mgp_cigar_offset(l_seq) + 4ull * n_cig;
-            if (paired) {  // record bytes; the offsets follow the barcodes (pass 1b)
-                rsz[i] = rb;
-                continue;
-            }
-            const uint64_t off = (G_pay.n + tot + amask) & ~amask;  // records are rec_align-sized
-            rsz[i] = off;
-            tot = off - G_pay.n + ((rb + amask) & ~amask);
-        }
+        dec.clear_chunk();
+        for (size_t i = 0; i < recs.size(); ++i)
+            if (!dec.classify(recs[i], sizes[i])) return -1;
+        dec.t_p1 += now_s() - tp1;
         const size_t k0 = G_start.n;
-        const size_t kn = k0 + m;
-        if (!G_start.reserve(kn) || !G_bc.reserve(kn) || !G_tlen.reserve(kn) || !G_flag.reserve(kn) ||
-            !G_mapq.reserve(kn) || !G_span.reserve(kn) || !G_roff.reserve(kn) ||
-            (!paired && !G_pay.reserve(G_pay.n + tot + 256)))
-            return fail("out of host memory"), -1;
-        const double tp2 = now_s();
-        t_p1 += tp2 - tp1;
-        // pass 2 (parallel): decode + pack; paired: the columns first, then the
-        // placement from the barcodes (pass 1b, sequential), then the records
-        const int tn = (int)std::max<size_t>(1, std::min<size_t>((size_t)nt, m / 4096 + 1));
-        std::vector<int64_t> tags((size_t)tn, 0), firsts((size_t)tn, -1);
-        auto run_pass = [&](bool do_fields, bool do_rec) {
-            auto work = [&](int t) {
-                const size_t lo = m * (size_t)t / (size_t)tn, hi = m * (size_t)(t + 1) / (size_t)tn;
-                for (size_t i = lo; i < hi; ++i)
-                    decode(recs[i], sizes[i], k0 + i, paired ? G_roff.p[k0 + i] : rsz[i], ncg[i], cgp[i],
-                           (int)pkd[i], tags[(size_t)t], firsts[(size_t)t], (int64_t)(k0 + i), do_fields, do_rec);
-            };
-            std::vector<std::thread> th;
-            for (int t = 1; t < tn; ++t) th.emplace_back(work, t);
-            work(0);
-            for (auto& x : th) x.join();
-        };
-        if (!paired) {
-            run_pass(true, true);
-        } else {
-            run_pass(true, false);
-            // pass 1b: which half-line each record takes (mgp_place_records' rule)
-            const uint64_t cur0 = cursor;
-            const uint16_t drop = MGP_FLAG_UNMAPPED | MGP_FLAG_SECONDARY | MGP_FLAG_SUPPLEMENTARY;
-            for (size_t i = 0; i < m; ++i) {
-                const size_t k = k0 + i;
-                if (!pkd[i]) {
-                    cursor = (cursor + 127) & ~127ull;
-                    G_roff.p[k] = cursor;
-                    cursor += (rsz[i] + 127) & ~127ull;
-                    continue;
-                }
-                const int32_t c = G_bc.p[k];
-                size_t key = (c >= 0 && c < n_keys && !(G_flag.p[k] & drop)) ? (size_t)c : (size_t)n_keys;
-                if (key < (size_t)n_keys &&
-                    dups.repeat(key, G_start.p[k], (G_flag.p[k] & MGP_FLAG_REVERSE) != 0, G_tlen.p[k]))
-                    key = (size_t)n_keys;
-                if (pkd[i] == 2) {  // four 32-byte records of one key per line
-                    if (open32[key] == ~0ull) {
-                        cursor = (cursor + 127) & ~127ull;
-                        open32[key] = cursor;
-                        fill32[key] = 0;
-                        cursor += 128;
-                    }
-                    G_roff.p[k] = open32[key] + (uint64_t)MGP_PACK32_BYTES * fill32[key];
-                    if (++fill32[key] == 4) open32[key] = ~0ull;
-                    continue;
-                }
-                if (open[key] != ~0ull) {
-                    G_roff.p[k] = open[key] + MGP_PACK_BYTES;
-                    open[key] = ~0ull;
-                } else {
-                    cursor = (cursor + 127) & ~127ull;
-                    G_roff.p[k] = open[key] = cursor;
-                    cursor += 128;
-                }
-            }
-            if (!G_pay.reserve(cursor + 256)) return fail("out of host memory"), -1;
-            // second halves of lines opened in this batch that stay open: zero (a
-            // later batch may still fill them; lines closed here are fully written)
-            for (uint64_t o : open)
-                if (o != ~0ull && o >= cur0) std::memset(G_pay.p + o + MGP_PACK_BYTES, 0, MGP_PACK_BYTES);
-            for (size_t key = 0; key < open32.size(); ++key)
-                if (open32[key] != ~0ull && open32[key] >= cur0)
-                    std::memset(G_pay.p + open32[key] + (uint64_t)MGP_PACK32_BYTES * fill32[key], 0,
-                                (uint64_t)MGP_PACK32_BYTES * (4u - fill32[key]));
-            run_pass(false, true);
-            tot = cursor - G_pay.n;
-        }
-        for (int t = 0; t < tn; ++t) {
-            n_tag += tags[(size_t)t];
-            if (first_tag < 0 && firsts[(size_t)t] >= 0) first_tag = firsts[(size_t)t];
-        }
-        G_start.n = G_bc.n = G_tlen.n = G_flag.n = G_mapq.n = G_span.n = G_roff.n = kn;
-        G_pay.n += tot;
-        t_p2 += now_s() - tp2;
+        if (dec.decode(k0, (int64_t)k0, nt, reserve, cols) != 0) return -1;
+        G_start.n = G_bc.n = G_tlen.n = G_flag.n = G_mapq.n = G_span.n = G_roff.n = k0 + recs.size();
+        G_pay.n = dec.cursor;
         return 1;
     });
     if (std::getenv("MGP_HOST_PROFILE"))
         std::fprintf(stderr, "[mgp_bam_read_ref] %zu records, %d threads: total %.3f s = pread %.3f + inflate %.3f + "
                      "scan/sizes %.3f + decode %.3f (+ rest)\n", G_start.n, nt, now_s() - t_begin, t_pread, t_inflate,
-                     t_p1, t_p2);
+                     dec.t_p1, dec.t_p2);
     auto release = [&]() {
         std::free(G_start.p); std::free(G_bc.p); std::free(G_tlen.p); std::free(G_flag.p);
         std::free(G_mapq.p); std::free(G_span.p); std::free(G_roff.p); std::free(G_pay.p);
@@ -986,8 +1078,7 @@ int mgp_bam_read_ref(mgp_bam* b, int tid, int rec_align, mgp_bam_batch* out) {
         return -1;
     }
     // at least one element everywhere; >= 256 bytes of payload slack for vector over-reads
-    if (!G_start.reserve(1) || !G_bc.reserve(1) || !G_tlen.reserve(1) || !G_flag.reserve(1) ||
-        !G_mapq.reserve(1) || !G_span.reserve(1) || !G_roff.reserve(1) || !G_pay.reserve(G_pay.n + 256)) {
+    if (!reserve(std::max<size_t>(G_start.n, 1), G_pay.n)) {
         release();
         return fail("out of host memory");
     }
@@ -1002,10 +1093,122 @@ int mgp_bam_read_ref(mgp_bam* b, int tid, int rec_align, mgp_bam_batch* out) {
     out->rec_off = G_roff.p;
     out->payload = G_pay.p;
     out->payload_bytes = (int64_t)G_pay.n;
-    out->n_with_tag = n_tag;
-    out->first_tag_index = first_tag;
+    out->n_with_tag = dec.n_tag;
+    out->first_tag_index = dec.first_tag;
     return 0;
 }
+
+// ---- streaming decode (one pass in batches, readers.py:84-93) -------------------
+struct mgp_bam_stream {
+    mgp_bam* bam = nullptr;
+    int tid = 0;
+    Stream st;
+    bool seen = false, done = false;
+    Decoder dec;
+    int64_t decoded = 0;  // records handed out so far
+    mgp_bam_stream(mgp_bam* b, int rec_align) : bam(b), dec(b, rec_align) {}
+};
+
+int64_t mgp_bam_ref_records(mgp_bam* b, int tid) {
+    if (!b || tid < 0 || tid >= (int)b->ref_names.size() || !b->has_index) return -1;
+    return b->ref_records[(size_t)tid];
+}
+
+int mgp_bam_stream_open(mgp_bam* b, int tid, int rec_align, mgp_bam_stream** out) {
+    g_err.clear();
+    if (!b || !out) return fail("null argument");
+    if (tid < 0 || tid >= (int)b->ref_names.size()) return fail("reference id out of range");
+    if (rec_align < 16 || rec_align > 4096 || (rec_align & (rec_align - 1))) return fail("bad rec_align");
+    std::unique_ptr<mgp_bam_stream> s(new (std::nothrow) mgp_bam_stream(b, rec_align));
+    if (!s) return fail("out of host memory");
+    s->tid = tid;
+    uint64_t voff = b->first_record_voff;
+    if (b->has_index) {
+        voff = b->ref_first_voff[(size_t)tid];
+        if (voff == UINT64_MAX) s->done = true;  // no reads on this reference
+    }
+    if (!s->done && !stream_at(b, voff, s->st)) return -1;
+    *out = s.release();
+    return 0;
+}
+
+int64_t mgp_bam_stream_next(mgp_bam_stream* s, int64_t cap_reads, int64_t cap_payload, mgp_bam_batch* into) {
+    g_err.clear();
+    if (!s || !into || !into->start || !into->bc || !into->tlen || !into->flag || !into->mapq || !into->span ||
+        !into->rec_off || !into->payload)
+        return fail("null argument");
+    Decoder& dec = s->dec;
+    const uint64_t slack = dec.line_slack() + 256;
+    if (cap_reads < 1 || cap_payload < (int64_t)(slack + 65536))
+        return fail("stream batch capacity too small (payload needs >= 64 KiB + 256 B per cell)");
+    const Cols c{into->start, into->bc, into->tlen, into->flag, into->mapq, into->span, into->rec_off, into->payload};
+    auto reserve = [&](size_t kn, uint64_t pay_end) {
+        return kn <= (size_t)cap_reads && pay_end + 256 <= (uint64_t)cap_payload;
+    };
+    auto cols = [&]() { return c; };
+    const int nt = std::max(1, s->bam->n_threads);
+    dec.begin_batch();
+    size_t k = 0;
+    uint64_t bound = 0;
+    bool full = false;
+    Stream& st = s->st;
+    while (!s->done && !full && k < (size_t)cap_reads) {
+        if (!st.fill(4)) {
+            if (!g_err.empty()) return -1;
+            if (st.avail() == 0) {  // clean end of file
+                s->done = true;
+                break;
+            }
+            return fail("truncated BAM record");
+        }
+        const uint32_t bs0 = rd32(st.peek());
+        if (bs0 < 32) return fail("corrupt BAM record (block_size < 32)");
+        if (!st.fill(4 + (size_t)bs0)) return fail(g_err.empty() ? "truncated BAM record body" : g_err);
+        const double tp1 = now_s();
+        dec.clear_chunk();
+        const uint8_t* base = st.buf.data();
+        size_t p = st.pos;
+        const size_t end = st.buf.size();
+        while (end - p >= 4 && k + dec.recs.size() < (size_t)cap_reads) {
+            const uint32_t bs = rd32(base + p);
+            if (bs < 32) return fail("corrupt BAM record (block_size < 32)");
+            if (end - p < 4 + (size_t)bs) break;
+            const int32_t ref = rdi32(base + p + 4);
+            if (ref == s->tid) {
+                s->seen = true;
+                if (!dec.classify(base + p + 4, bs)) return -1;
+                const uint64_t w = dec.worst(dec.recs.size() - 1);
+                if (bound + w + slack > (uint64_t)cap_payload) {
+                    dec.unclassify_last();
+                    full = true;
+                    break;
+                }
+                bound += w;
+            } else if (s->seen || ref > s->tid || ref < 0) {
+                s->done = true;  // coordinate-sorted: tid's records are contiguous
+                break;
+            }
+            p += 4 + (size_t)bs;
+        }
+        dec.t_p1 += now_s() - tp1;
+        if (!dec.recs.empty()) {
+            if (dec.decode(k, s->decoded + (int64_t)k, nt, reserve, cols) != 0) return -1;
+            k += dec.recs.size();
+        }
+        st.pos = p;
+    }
+    if (k == 0 && !s->done && full) return fail("stream batch capacity too small for one record");
+    // >= 256 bytes of zeroed slack after the payload (kernels read up to 128 past a record)
+    std::memset(into->payload + dec.cursor, 0, std::min<uint64_t>(256, (uint64_t)cap_payload - dec.cursor));
+    into->n_reads = (int64_t)k;
+    into->payload_bytes = (int64_t)dec.cursor;
+    into->n_with_tag = dec.n_tag;
+    into->first_tag_index = dec.first_tag;
+    s->decoded += (int64_t)k;
+    return (int64_t)k;
+}
+
+void mgp_bam_stream_close(mgp_bam_stream* s) { delete s; }
 
 void mgp_bam_free_batch(mgp_bam_batch* x) {
     if (!x) return;

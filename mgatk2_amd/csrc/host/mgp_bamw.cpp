@@ -236,7 +236,7 @@ int mgp_bam_write(const char* path, const char* const* ref_names, const int64_t*
             put<int32_t>(x, 0);
             continue;
         }
-        put<int32_t>(x, (int32_t)bins.size());
+        put<int32_t>(x, (int32_t)bins.size() + (pos.empty() ? 0 : 1));
         for (const auto& kv : bins) {
             put<uint32_t>(x, (uint32_t)kv.first);
             put<int32_t>(x, (int32_t)kv.second.size());
@@ -244,6 +244,16 @@ int mgp_bam_write(const char* path, const char* const* ref_names, const int64_t*
                 put<uint64_t>(x, c.first);
                 put<uint64_t>(x, c.second);
             }
+        }
+        if (!pos.empty()) {  // the metadata pseudo-bin (SAM spec §5.2): extent, mapped / unmapped counts
+            uint64_t n_unmapped = 0;
+            for (int64_t i = 0; i < batch->n_reads; ++i) n_unmapped += (batch->flag[i] & 0x4) != 0;
+            put<uint32_t>(x, 37450u);
+            put<int32_t>(x, 2);
+            put<uint64_t>(x, voff(pos.front().ubeg));
+            put<uint64_t>(x, voff(pos.back().uend));
+            put<uint64_t>(x, (uint64_t)batch->n_reads - n_unmapped);
+            put<uint64_t>(x, n_unmapped);
         }
         put<int32_t>(x, (int32_t)lin.size());
         for (uint64_t v : lin) put<uint64_t>(x, v);

@@ -4,10 +4,14 @@ Same entry points as the reference (``MtDNAPipeline(...).run()`` and
 ``run_pipeline(...)``). The flow is the reference's; the work inside is the
 build's:
 
-1. native BAM ingest of every chrM record into one engine batch
-   (:meth:`BAMReader.read_soa`);
-2. one engine run on the GPU: filters, dedup, pileup, strand filter, per-cell
-   statistics and reference tallies (:meth:`CellProcessor.run_soa`);
+1. native BAM ingest of the chrM records in batches on a producer thread
+   (:meth:`BAMReader.open_stream`), each batch pushed to the GPU as soon as it is
+   decoded;
+2. one streamed engine run: every position window goes through filters, dedup,
+   pileup, strand filter and per-cell statistics as soon as its reads have all
+   arrived, and its result rows come back while later batches are still decoded
+   (:meth:`CellProcessor.run_stream`; ``stream=False`` or ``MGP_STREAM=0``: the whole
+   set decoded first, then one run, :meth:`CellProcessor.run_soa`);
 3. the writers format the passing cells, in first-seen order, from the
    engine's arrays;
 4. ``qc/summary.txt`` and, for HDF5 output, the HTML report.
@@ -19,6 +23,7 @@ from __future__ import annotations
 
 import gc
 import logging
+import os
 import time
 from pathlib import Path
 from typing import Any
@@ -60,8 +65,11 @@ class MtDNAPipeline:
         working_directory: str | None = None,
         device: int = 0,
         devices: list[int] | None = None,
+        stream: bool | None = None,
     ):
         self.bam_path = Path(bam_path)
+        # streamed ingest (default; MGP_STREAM=0 decodes the whole chrM set first)
+        self.stream = (os.environ.get("MGP_STREAM", "1") != "0") if stream is None else bool(stream)
         self.barcodes = set(barcodes)
         self.barcode_list = list(barcodes)
         self.output_dir = Path(output_dir)
@@ -98,19 +106,26 @@ class MtDNAPipeline:
         t0 = time.time()
         logger.info("Collecting reads from BAM by barcode...")
         reader = BAMReader(str(self.bam_path), self.config, self.barcode_list)
-        soa, stats = reader.read_soa()
-        t1 = time.time()
-
         processor = CellProcessor(self.config, self.output_dir, device=self.device, devices=self.devices)
-        ta = time.time()
-        res = processor.run_soa(soa, len(self.barcode_list))
-        tb = time.time()
-        # the decoded batch (GBs of malloc'd columns and records) is unmapped on a
-        # background thread while the writers run: its free took 0.36 s at C3
-        box = [soa]
-        del soa
-        _release_in_background(box)
-        t2 = time.time()
+        if self.stream and len(self.devices) == 1:
+            # one pass: batches decoded on a producer thread, each pushed to the device as
+            # it is ready, the windows piled as their reads arrive (readers.py:84-93)
+            res = processor.run_stream(reader, len(self.barcode_list))
+            stats = {"total_reads": int(res.stats["total_reads"])}
+            t1 = ta = t0 + processor.last_timing.get("stream_decode_end", time.time() - t0)
+            tb = t2 = time.time()
+        else:
+            soa, stats = reader.read_soa()
+            t1 = time.time()
+            ta = time.time()
+            res = processor.run_soa(soa, len(self.barcode_list))
+            tb = time.time()
+            # the decoded batch (GBs of malloc'd columns and records) is unmapped on a
+            # background thread while the writers run: its free took 0.36 s at C3
+            box = [soa]
+            del soa
+            _release_in_background(box)
+            t2 = time.time()
         self.engine_result = res
         self.read_stats = {**res.stats, **stats}
         st = self.read_stats
@@ -156,9 +171,12 @@ class MtDNAPipeline:
             except Exception as e:
                 logger.warning("Failed to generate HTML report: %s", e)
         t4 = time.time()
+        # streamed: bam_ingest ends with the last decoded batch and `engine` is only what the
+        # device still did after it (the rest ran under the decode)
         self.timings = {"bam_ingest": t1 - t0, "engine": t2 - t1, "write": t3 - t2, "report": t4 - t3,
                         "total": t4 - t0, "engine_setup": ta - t1, "engine_run_soa": tb - ta,
-                        "engine_free_inputs": t2 - tb, **processor.last_timing}
+                        "engine_free_inputs": t2 - tb, "streamed": bool(self.stream and len(self.devices) == 1),
+                        **processor.last_timing}
         logger.info("Pipeline complete")
         logger.info("Elapsed time: %.1fs (ingest %.1fs, engine %.1fs, write %.1fs)", t4 - t0, t1 - t0, t2 - t1,
                     t3 - t2)

@@ -17,7 +17,10 @@ from __future__ import annotations
 
 import gc
 import logging
+import os
+import threading
 import time
+from queue import Queue
 
 import numpy as np
 
@@ -28,6 +31,11 @@ from .pileup import result_dict, simple_reads_to_dicts
 logger = logging.getLogger(__name__)
 
 MP_CONTEXT = "spawn"  # kept for API compatibility (processors.py:17); no process pool is used
+
+# streamed runs: reads per decoded batch and batches in flight (MGP_STREAM_BATCH /
+# MGP_STREAM_SLOTS override them, read at each run)
+STREAM_BATCH_READS = 4_000_000
+STREAM_SLOTS = 3
 
 
 def _engine_config_for(config, n_cells: int, dedup: bool):
@@ -99,6 +107,122 @@ class CellProcessor:
         # the batches + the run, D2H of the results, teardown
         self.last_timing = {"engine_open": t1 - t0, "engine_h2d_run": t2 - t1, "engine_d2h": t3 - t2,
                             "engine_close": t4 - t3}
+        self.last_result = res
+        return res
+
+    def run_stream(self, reader, n_cells: int, batch_reads: int | None = None, rows_target: bool = True) -> EngineResult:
+        """The production path, streamed (readers.py:84-93's one pass, overlapped with
+        the device): the native decoder fills a ring of pinned batches on a producer
+        thread while this thread pushes each finished batch to a streaming engine
+        context (MGP_CFG_STREAM: its H2D copies, then the hot path of the position
+        windows it completes, run behind the next batches' decode). With a rows
+        target, each window's 16-bit result rows leave the device as soon as it is
+        piled, into pinned host memory the writers read. Results are those of a
+        resident run of the same reads (reads a segment cannot serve rerun it)."""
+        from ..bam import StreamSlot
+        from ..engine import PinnedBuffer, Rows16
+
+        t0 = time.perf_counter()
+        bam, st, expected = reader.open_stream()
+        try:
+            n_hint = expected if expected > 0 else max(1, os.path.getsize(reader.bam_path) // 30)
+            batch_reads = batch_reads or int(os.environ.get("MGP_STREAM_BATCH", STREAM_BATCH_READS))
+            n_slots = max(2, int(os.environ.get("MGP_STREAM_SLOTS", STREAM_SLOTS)))
+            cap_reads = max(1, min(int(batch_reads), n_hint + 1))
+            cap_payload = cap_reads * 48 + 256 * (n_cells + 1) + (1 << 20)
+            ec = self.config.engine_config(n_cells, reserve_reads=n_hint, reserve_payload=n_hint * 40 + (64 << 20))
+            ec.stream = True
+            slot_bytes = StreamSlot.nbytes(cap_reads, cap_payload)
+            slots, bufs = [], []
+            for _ in range(n_slots):
+                pb = PinnedBuffer(slot_bytes)
+                off = [0]
+
+                def alloc(m, dt, pb=pb, off=off):
+                    a = pb.array(m, dt, off[0])
+                    off[0] = (off[0] + m * np.dtype(dt).itemsize + 63) & ~63
+                    return a
+
+                bufs.append(pb)
+                slots.append(StreamSlot(cap_reads, cap_payload, alloc))
+            free: Queue = Queue()
+            full: Queue = Queue()
+            for sl in slots:
+                free.put(sl)
+            times = {}
+
+            def produce():
+                try:
+                    while True:
+                        sl = free.get()
+                        if sl is None:
+                            return
+                        n = st.next_into(sl)
+                        full.put(sl if n else None)
+                        if not n:
+                            times["decode_end"] = time.perf_counter()
+                            return
+                except BaseException as e:  # noqa: BLE001 - handed to the consumer
+                    full.put(e)
+
+            producer = threading.Thread(target=produce, name="mgp-bam-decode", daemon=True)
+            producer.start()
+            eng = Engine(ec, device=self.device)
+            try:
+                rows = None
+                if rows_target and n_cells > 0:
+                    nw, W = eng.windows()
+                    L = self.config.mito_length
+                    rb = PinnedBuffer(n_cells * L * 22 + n_cells * nw + 4096)
+                    rows = Rows16(rb.array((n_cells, L, 8), np.uint16, 0),
+                                  rb.array((n_cells, L, 2), np.uint16, n_cells * L * 16),
+                                  rb.array((n_cells, L), np.uint16, n_cells * L * 20),
+                                  rb.array((n_cells, nw), np.uint8, n_cells * L * 22), W)
+                    eng.set_rows16_target(rows)
+                t1 = time.perf_counter()
+                n_batches = 0
+                while True:
+                    item = full.get()
+                    if item is None:
+                        break
+                    if isinstance(item, BaseException):
+                        raise item
+                    if n_batches == 0:
+                        times["first_batch"] = time.perf_counter()
+                    eng.push(item.soa())
+                    eng.copy_wait()  # its pinned arrays may be refilled now
+                    free.put(item)
+                    n_batches += 1
+                t2 = time.perf_counter()
+                eng.run()
+                eng.sync()
+                t3 = time.perf_counter()
+                res = eng.fetch(dense=False)
+                if rows is not None and not rows.wide.any():
+                    res.counts, res.tn5, res.depth = rows.counts, rows.tn5, rows.depth
+                elif rows is not None:
+                    res = eng.fetch(dense=True)  # a drained window: the exact u32 arrays
+                else:
+                    res = eng.fetch_compact()
+                t4 = time.perf_counter()
+                self.last_stats = eng.kernel_times()
+                _, last_streamed = eng.stream_info()
+            finally:
+                free.put(None)
+                eng.close()
+            producer.join()
+        finally:
+            st.close()
+            bam.close()
+        te = time.perf_counter()
+        # where the streamed engine leg goes: setup (pinned ring + rows target, context),
+        # the pushes (behind the decode), the run's tail after the last batch, results
+        dec_end = times.get("decode_end", t2)
+        self.last_timing = {"stream_setup": t1 - t0, "stream_first_batch": times.get("first_batch", t1) - t0,
+                            "stream_decode_end": dec_end - t0, "stream_push_end": t2 - t0,
+                            "engine_tail": t3 - t2, "engine_fetch": t4 - t3, "engine_close": te - t4,
+                            "stream_batches": n_batches, "stream_batch_reads": cap_reads,
+                            "streamed_run": bool(last_streamed), "rows_target": rows is not None}
         self.last_result = res
         return res
 

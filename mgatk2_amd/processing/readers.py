@@ -84,22 +84,38 @@ class BAMReader:
         mode every record goes to the ``"bulk"`` cell (readers.py:97-99). With
         packing, reads that fit get the 32-byte record made for the run's
         min_baseq (four to a 128-byte line), the others the 64-byte or full one."""
-        bulk = -1
-        q = int(self.config.quality.min_baseq)
-        md = int(self.config.quality.min_distance_from_end)
-        pack32 = q if pack and -128 <= q <= 127 and md <= 15 else None
-        if self.is_bulk_mode:
-            bulk = max(i for i, b in enumerate(self.barcode_list) if b == "bulk")
         try:
             with self._open() as bam:
                 soa = bam.read_soa(self.config.mito_chr, self.barcode_list, tag=self.config.barcode_tag,
-                                   rec_align=rec_align, bulk_cell=bulk, pack=pack, pack32=pack32,
-                                   pack32_dist=int(self.config.quality.min_distance_from_end))
+                                   rec_align=rec_align, **self._pack_settings(pack))
         except BAMReadError:
             raise
         except Exception as e:
             raise BAMReadError(str(self.bam_path), f"Read error: {e}") from e
         return soa, {"total_reads": soa.n}
+
+    def _pack_settings(self, pack: bool) -> dict:
+        q = int(self.config.quality.min_baseq)
+        md = int(self.config.quality.min_distance_from_end)
+        bulk = max(i for i, b in enumerate(self.barcode_list) if b == "bulk") if self.is_bulk_mode else -1
+        return dict(bulk_cell=bulk, pack=pack, pack32=q if pack and -128 <= q <= 127 and md <= 15 else None,
+                    pack32_dist=md)
+
+    def open_stream(self, rec_align: int = 64, pack: bool = True):
+        """The chrM records as a streaming decode (readers.py:84-93's one pass, in
+        batches): returns (BamFile, BamStream, expected records or -1). The caller
+        pulls batches with ``stream.next_into(slot)`` and closes both."""
+        bam = self._open()
+        try:
+            st = bam.stream(self.config.mito_chr, self.barcode_list, tag=self.config.barcode_tag, rec_align=rec_align,
+                            **self._pack_settings(pack))
+        except BAMReadError:
+            bam.close()
+            raise
+        except Exception as e:
+            bam.close()
+            raise BAMReadError(str(self.bam_path), f"Read error: {e}") from e
+        return bam, st, bam.ref_records(self.config.mito_chr)
 
     def collect_reads_by_barcode(self) -> tuple[dict, dict]:
         """readers.py:63-201 on the host: dict[barcode -> list[SimpleRead]] + stats."""

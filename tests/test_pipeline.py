@@ -25,18 +25,52 @@ from mgatk2_amd.exceptions import InvalidInputError, NoBarcodeTagsError, NoChrMR
 TXT_CASES = [c for c in CASES if Golden(c).params["output_format"] == "txt"]
 
 
-@pytest.fixture
-def oracle_engine(monkeypatch, oracle_lib):
-    """Stand the oracle in for the engine (CPU tests of the host logic)."""
+def stream_batches(reader, n_cells, batch_reads=997):
+    """The reader's streaming decode (mgp_bam_stream_*) drained into copies of its
+    batches (small batches: every golden case takes several, so paired lines and
+    placement restart at batch boundaries)."""
+    from mgatk2_amd.bam import StreamSlot
+
+    bam, st, _ = reader.open_stream()
+    parts = []
+    try:
+        slot = StreamSlot(batch_reads, batch_reads * 48 + 256 * (n_cells + 1) + (1 << 20))
+        while st.next_into(slot):
+            v = slot.soa()
+            parts.append(type(v)(*[getattr(v, k).copy() for k in ("start", "bc", "tlen", "flag", "mapq", "span",
+                                                                  "rec_off", "payload")]))
+    finally:
+        st.close()
+        bam.close()
+    return parts
+
+
+def patch_oracle_engine(monkeypatch, oracle_lib):
+    """Stand the oracle in for the engine: the resident path (run_soa) and the
+    streamed one (run_stream: the host's streaming decode, then the oracle on the
+    concatenated batches)."""
     from mgatk2_amd.processing import processors
+    from mgatk2_amd.synth import concat_soa
 
     def run_soa(self, soa_batches, n_cells):
-        soa = soa_batches if not isinstance(soa_batches, list) else soa_batches[0]
+        soa = soa_batches if not isinstance(soa_batches, list) else concat_soa(soa_batches)
         res, _ = oracle_lib.oracle_run(self.config.engine_config(n_cells), soa)
         self.last_result = res
         return res
 
+    def run_stream(self, reader, n_cells, batch_reads=None, rows_target=True):
+        parts = stream_batches(reader, n_cells)
+        self.last_timing = {"stream_batches": len(parts)}
+        return run_soa(self, parts, n_cells)
+
     monkeypatch.setattr(processors.CellProcessor, "run_soa", run_soa)
+    monkeypatch.setattr(processors.CellProcessor, "run_stream", run_stream)
+
+
+@pytest.fixture
+def oracle_engine(monkeypatch, oracle_lib):
+    """Stand the oracle in for the engine (CPU tests of the host logic)."""
+    patch_oracle_engine(monkeypatch, oracle_lib)
 
 
 def _run_case(case, tmp_path, barcode_source="txt"):
@@ -356,7 +390,6 @@ def test_pipeline_autodetect_barcodes_gpu(tmp_path, engine_lib, oracle_lib, monk
     engine runs on them; every output equals the oracle's run of the same pipeline."""
     from mgatk2_amd.file_io.barcode_extraction import extract_barcodes_from_bam
     from mgatk2_amd.pipeline import run_pipeline
-    from mgatk2_amd.processing import processors
 
     g = Golden("synth_run")
     bam = tmp_path / "x.bam"
@@ -366,13 +399,7 @@ def test_pipeline_autodetect_barcodes_gpu(tmp_path, engine_lib, oracle_lib, monk
     ret = run_pipeline(str(bam), None, str(tmp_path / "gpu"), min_barcode_reads=10, output_format="txt")
     assert ret["cells_processed"] > 0
 
-    def run_soa(self, soa_batches, n_cells):
-        soa = soa_batches if not isinstance(soa_batches, list) else soa_batches[0]
-        res, _ = oracle_lib.oracle_run(self.config.engine_config(n_cells), soa)
-        self.last_result = res
-        return res
-
-    monkeypatch.setattr(processors.CellProcessor, "run_soa", run_soa)
+    patch_oracle_engine(monkeypatch, oracle_lib)
     ret2 = run_pipeline(str(bam), None, str(tmp_path / "cpu"), min_barcode_reads=10, output_format="txt")
     assert ret2["cells_processed"] == ret["cells_processed"]
     for name in ("A", "C", "G", "T", "coverage"):
@@ -381,3 +408,81 @@ def test_pipeline_autodetect_barcodes_gpu(tmp_path, engine_lib, oracle_lib, monk
         assert a == b, name
     for rel in ("output/output.depthTable.txt", "output/chrM_refAllele.txt", "qc/cell_stats.csv"):
         assert (tmp_path / "gpu" / rel).read_text() == (tmp_path / "cpu" / rel).read_text(), rel
+
+
+def test_stream_batches_equal_the_whole_decode(tmp_path):
+    """The streaming decode (mgp_bam_stream_*) gives the whole decode's columns in
+    the same order, each record's bytes at its batch's offsets, for every packing /
+    placement setting and batch size; the index's record count is the reads'."""
+    from mgatk2_amd.bam import BamFile
+    from mgatk2_amd.config import PipelineConfig
+    from mgatk2_amd.processing.readers import BAMReader
+    from mgatk2_amd.synth import concat_soa
+
+    g = Golden("synth_run")
+    bam = tmp_path / "x.bam"
+    from mgatk2_amd.bam import write_bam
+
+    write_bam(bam, g.soa, g.whitelist)
+    with BamFile(bam) as bf:
+        assert bf.ref_records("chrM") == g.soa.n
+    for q, pack in ((20, True), (0, True), (20, False)):
+        cfg = PipelineConfig(min_baseq=q)
+        reader = BAMReader(str(bam), cfg, g.whitelist)
+        whole, _ = reader.read_soa(pack=pack)
+        for br in (1, 333, 4096, 10**6):
+            if not pack:
+                break
+            parts = stream_batches(reader, len(g.whitelist), br)
+            assert sum(p.n for p in parts) == whole.n
+            assert all(p.n <= br for p in parts)
+            cat = concat_soa(parts)
+            for k in ("start", "bc", "tlen", "flag", "mapq", "span"):
+                np.testing.assert_array_equal(getattr(cat, k), getattr(whole, k), err_msg=f"q{q} {br} {k}")
+            rb = np.where(whole.flag & 0x4000, 32, np.where(whole.flag & 0x2000, 64, 128))
+            for i in range(0, whole.n, 7):
+                a, b = int(cat.rec_off[i]), int(whole.rec_off[i])
+                m = int(rb[i]) if rb[i] < 128 else 112
+                assert np.array_equal(cat.payload[a:a + m], whole.payload[b:b + m]), (q, br, i)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("batch", ["997", "50000"])
+@pytest.mark.parametrize("case", ["synth_run", "synth_tenx", "synth_bias", "kat_run"])
+def test_pipeline_streamed_equals_resident_gpu(case, batch, tmp_path, engine_lib, monkeypatch):
+    """The production pipeline streamed (batches decoded on a producer thread, each
+    pushed as it is ready, windows piled as their reads arrive, result rows copied
+    back as windows complete) writes byte-identical files to the resident run
+    (whole decode, one run), and both equal the reference's outputs."""
+    monkeypatch.setenv("MGP_STREAM_BATCH", batch)
+    from mgatk2_amd import pipeline
+
+    g = Golden(case)
+    p = g.params
+    bam = tmp_path / "x.bam"
+    soa_to_bam(bam, g.soa, g.whitelist)
+    bfile = tmp_path / "barcodes.tsv"
+    bfile.write_text("".join(b + "\n" for b in g.whitelist))
+    from mgatk2_amd.config import PipelineConfig
+
+    outs = {}
+    for stream in (True, False):
+        cfg = PipelineConfig(min_baseq=p["min_baseq"], min_mapq=p["min_mapq"],
+                             min_reads_per_cell=p["min_reads_per_cell"], max_strand_bias=p["max_strand_bias"],
+                             skip_deduplication=p["skip_deduplication"],
+                             use_fragment_length_dedup=p["use_fragment_length_dedup"])
+        out = tmp_path / f"out_{stream}"
+        pl = pipeline.MtDNAPipeline(str(bam), g.whitelist, out, config=cfg, output_format="txt", stream=stream)
+        ret = pl.run()
+        assert pl.timings["streamed"] == stream
+        if stream:
+            assert pl.timings["stream_batches"] >= (2 if batch == "997" else 1)
+        outs[stream] = (out, ret)
+    for rel in ("output/output.A.txt.gz", "output/output.C.txt.gz", "output/output.G.txt.gz",
+                "output/output.T.txt.gz", "output/output.coverage.txt.gz"):
+        a = gzip.decompress((outs[True][0] / rel).read_bytes())
+        b = gzip.decompress((outs[False][0] / rel).read_bytes())
+        assert a == b, rel
+    for rel in ("output/output.depthTable.txt", "output/chrM_refAllele.txt", "qc/cell_stats.csv"):
+        assert (outs[True][0] / rel).read_text() == (outs[False][0] / rel).read_text(), rel
+    _check_outputs(g, outs[True][0], outs[True][1])
