@@ -64,13 +64,14 @@ def build_host(force: bool = False, verbose: bool = False) -> Path:
             CSRC / "host" / "mgp_bamw.cpp", CSRC / "host" / "mgp_shard.cpp", CSRC / "host" / "mgp_place.cpp",
             CSRC / "host" / "mgp_repack.cpp"]
     deps = srcs + [ROOT / "include" / "mgpileup_host.h", ROOT / "include" / "mgpileup.h",
-                   CSRC / "host" / "mgp_pack32_host.h", CSRC / "host" / "mgp_place.h"]
+                   CSRC / "host" / "mgp_pack32_host.h", CSRC / "host" / "mgp_place.h",
+                   CSRC / "host" / "mgp_zcodec.h"]
     if force or _stale(HOST_SO, deps):
         LIB_DIR.mkdir(parents=True, exist_ok=True)
         tmp = HOST_SO.with_suffix(".so.tmp")
         cxx = shutil.which("g++") or "c++"
         cmd = [cxx, "-O3", "-std=c++17", "-fPIC", "-shared", "-Wall", "-pthread", f"-I{ROOT / 'include'}",
-               *[str(s) for s in srcs], "-o", str(tmp), "-lz"]
+               *[str(s) for s in srcs], "-o", str(tmp), "-lz", "-ldl"]
         if verbose:
             print(" ".join(cmd))
         subprocess.run(cmd, check=True)

@@ -28,6 +28,7 @@
 #include "../../../include/mgpileup.h"
 #include "../../../include/mgpileup_host.h"
 #include "mgp_pack32_host.h"
+#include "mgp_zcodec.h"
 #include "mgp_place.h"
 
 // one thread-local error string for every entry point of libmgphost.so
@@ -171,19 +172,13 @@ uint32_t bgzf_block_size(const uint8_t* p, size_t n) {
     return 0;
 }
 
-bool inflate_block(const uint8_t* blk, uint32_t csize, uint8_t* out, uint32_t isize, z_stream* zs) {
+bool inflate_block(const uint8_t* blk, uint32_t csize, uint8_t* out, uint32_t isize, mgp_host::Inflator& inf) {
     const uint16_t xlen = rd16(blk + 10);
     const uint8_t* cdata = blk + 12 + xlen;
     const uint32_t clen = csize - 12 - xlen - 8;
-    if (inflateReset(zs) != Z_OK) return false;
-    zs->next_in = const_cast<uint8_t*>(cdata);
-    zs->avail_in = clen;
-    zs->next_out = out;
-    zs->avail_out = isize;
-    const int r = inflate(zs, Z_FINISH);
-    if (r != Z_STREAM_END || zs->avail_out != 0) return isize == 0 && r == Z_STREAM_END;
+    if (!inf.raw(cdata, clen, out, isize)) return false;
     const uint32_t crc = rd32(blk + csize - 8);
-    return crc32(0, out, isize) == crc;
+    return mgp_host::crc32_any(0, out, isize) == crc;
 }
 
 // A sequential reader over the inflated BGZF stream, inflating batches of
@@ -307,22 +302,16 @@ struct Stream {
         std::atomic<bool> ok{true};
         const int nt = std::max(1, std::min<int>(bam->n_threads, (int)blocks.size()));
         auto work = [&]() {
-            z_stream zs;
-            std::memset(&zs, 0, sizeof(zs));
-            if (inflateInit2(&zs, -15) != Z_OK) {
-                ok = false;
-                return;
-            }
+            mgp_host::Inflator inf;
             for (;;) {
                 const size_t i = next.fetch_add(1);
                 if (i >= blocks.size()) break;
                 const Block& b = blocks[i];
-                if (!inflate_block(raw_p + b.coff, b.csize, buf.data() + base + b.out_off, b.isize, &zs)) {
+                if (!inflate_block(raw_p + b.coff, b.csize, buf.data() + base + b.out_off, b.isize, inf)) {
                     ok = false;
                     break;
                 }
             }
-            inflateEnd(&zs);
         };
         const double ti0 = now_s();
         std::vector<std::thread> th;

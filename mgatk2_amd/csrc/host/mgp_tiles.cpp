@@ -18,6 +18,7 @@
 #include <thread>
 #include <vector>
 
+#include "mgp_zcodec.h"
 #include "../../../include/mgpileup_host.h"
 
 std::string& mgp_host_err();  // mgp_bam.cpp
@@ -40,6 +41,7 @@ int64_t mgp_deflate_tiles(const void* data, int64_t rows, int64_t cols, int32_t 
     const uint8_t* src = (const uint8_t*)data;
     auto work = [&]() {
         std::vector<uint8_t> tile(chunk_bytes);
+        mgp_host::Deflator dz(level);
         for (;;) {
             const int64_t t = next.fetch_add(1);
             if (t >= n) break;
@@ -49,14 +51,11 @@ int64_t mgp_deflate_tiles(const void* data, int64_t rows, int64_t cols, int32_t 
             for (int64_t r = 0; r < h; ++r)
                 std::memcpy(tile.data() + (size_t)r * ccol * elem_size,
                             src + ((size_t)(r0 + r) * (size_t)cols + (size_t)c0) * elem_size, (size_t)w * elem_size);
-            uLongf dl = compressBound((uLong)chunk_bytes);
-            auto& o = out[(size_t)t];
-            o.resize(dl);
-            if (compress2(o.data(), &dl, tile.data(), (uLong)chunk_bytes, level) != Z_OK) {
+            // the H5Z_DEFLATE form: one zlib stream of the whole (padded) chunk
+            if (!dz.zlib(tile.data(), chunk_bytes, out[(size_t)t])) {
                 ok = false;
                 return;
             }
-            o.resize(dl);
         }
     };
     int nt = n_threads > 0 ? n_threads : (int)std::thread::hardware_concurrency();

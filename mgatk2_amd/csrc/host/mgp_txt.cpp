@@ -20,6 +20,7 @@
 #include <thread>
 #include <vector>
 
+#include "mgp_zcodec.h"
 #include "../../../include/mgpileup_host.h"
 
 std::string& mgp_host_err();  // mgp_bam.cpp
@@ -51,21 +52,10 @@ struct Text {
     }
 };
 
-bool gzip_member(const char* src, size_t n, int level, std::vector<uint8_t>& out) {
+bool gzip_member(const char* src, size_t n, mgp_host::Deflator& dz, std::vector<uint8_t>& out) {
     out.clear();
     if (n == 0) return true;
-    z_stream zs;
-    std::memset(&zs, 0, sizeof(zs));
-    if (deflateInit2(&zs, level, Z_DEFLATED, 15 + 16, 8, Z_DEFAULT_STRATEGY) != Z_OK) return false;
-    out.resize(deflateBound(&zs, (uLong)n) + 64);
-    zs.next_in = (Bytef*)src;
-    zs.avail_in = (uInt)n;  // chunks are kept well below 4 GiB
-    zs.next_out = out.data();
-    zs.avail_out = (uInt)out.size();
-    const int r = deflate(&zs, Z_FINISH);
-    out.resize(zs.total_out);
-    deflateEnd(&zs);
-    return r == Z_STREAM_END;
+    return dz.gzip(reinterpret_cast<const uint8_t*>(src), n, out);
 }
 
 // One group of cells -> 5 texts (coverage, A, C, G, T). T: u32 rows, or the
@@ -145,6 +135,7 @@ int write_cells(const char* prefix, const T* counts, const T* depth, int64_t mit
         std::atomic<int64_t> next{g0};
         auto work = [&]() {
             Text txt[5];
+            mgp_host::Deflator dz(level);
             for (;;) {
                 const int64_t g = next.fetch_add(1);
                 if (g >= g1) break;
@@ -152,7 +143,7 @@ int write_cells(const char* prefix, const T* counts, const T* depth, int64_t mit
                 const int64_t c0 = g * per_group, c1 = std::min(n_write, c0 + per_group);
                 format_group(counts, depth, mito_len, cells, c0, c1, names, txt);
                 for (int i = 0; i < 5; ++i)
-                    if (!gzip_member(txt[i].b.data(), txt[i].n, level, out[(size_t)(g - g0) * 5 + i])) ok = false;
+                    if (!gzip_member(txt[i].b.data(), txt[i].n, dz, out[(size_t)(g - g0) * 5 + i])) ok = false;
             }
         };
         std::vector<std::thread> th;
