@@ -65,7 +65,7 @@ def build_host(force: bool = False, verbose: bool = False) -> Path:
             CSRC / "host" / "mgp_repack.cpp"]
     deps = srcs + [ROOT / "include" / "mgpileup_host.h", ROOT / "include" / "mgpileup.h",
                    CSRC / "host" / "mgp_pack32_host.h", CSRC / "host" / "mgp_place.h",
-                   CSRC / "host" / "mgp_zcodec.h"]
+                   CSRC / "host" / "mgp_zcodec.h", CSRC / "host" / "mgp_pool.h"]
     if force or _stale(HOST_SO, deps):
         LIB_DIR.mkdir(parents=True, exist_ok=True)
         tmp = HOST_SO.with_suffix(".so.tmp")

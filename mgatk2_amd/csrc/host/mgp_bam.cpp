@@ -11,6 +11,9 @@
 #include <algorithm>
 #include <atomic>
 #include <chrono>
+#include <condition_variable>
+#include <deque>
+#include <mutex>
 #include <cerrno>
 #include <cstdint>
 #include <cstdio>
@@ -28,6 +31,7 @@
 #include "../../../include/mgpileup.h"
 #include "../../../include/mgpileup_host.h"
 #include "mgp_pack32_host.h"
+#include "mgp_pool.h"
 #include "mgp_zcodec.h"
 #include "mgp_place.h"
 
@@ -181,159 +185,241 @@ bool inflate_block(const uint8_t* blk, uint32_t csize, uint8_t* out, uint32_t is
     return mgp_host::crc32_any(0, out, isize) == crc;
 }
 
-// A sequential reader over the inflated BGZF stream, inflating batches of
-// blocks in parallel.
-// Byte buffer that grows without zero-filling (std::vector value-initialises:
-// a memset of every inflated batch).
-struct ByteBuf {
-    std::unique_ptr<uint8_t[]> p;
-    size_t n = 0, cap = 0;
-    size_t size() const { return n; }
-    uint8_t* data() { return p.get(); }
-    const uint8_t* data() const { return p.get(); }
-    void clear() { n = 0; }
-    // false (buffer unchanged) when host memory runs out: no exception may cross
-    // the extern "C" entry points
-    bool resize(size_t m) {
-        if (m > cap) {
-            const size_t c = std::max(m, cap + cap / 2);
-            std::unique_ptr<uint8_t[]> q(new (std::nothrow) uint8_t[c]);
-            if (!q) return false;
-            if (n) std::memcpy(q.get(), p.get(), n);
-            p = std::move(q);
-            cap = c;
-        }
-        n = m;
-        return true;
-    }
-    void drop_front(size_t k) {  // drop the first k bytes
-        if (k >= n) {
-            n = 0;
-            return;
-        }
-        std::memmove(p.get(), p.get() + k, n - k);
-        n -= k;
-    }
+// An inflated chunk of the BGZF stream: the bytes of consecutive whole blocks at
+// mem + kHead (the room in front takes the partial record the consumer carries over
+// from the chunk before).
+constexpr size_t kHead = 1u << 20;
+struct Chunk {
+    std::unique_ptr<uint8_t[]> mem;
+    size_t cap = 0;
+    size_t n = 0;       // inflated bytes at mem + kHead
+    bool last = false;  // the end of the file follows
 };
 
-struct Stream {
-    mgp_bam* bam;
-    uint64_t coff;            // next compressed offset to read
-    ByteBuf buf;              // inflated bytes not consumed yet
-    size_t pos = 0;
-    bool eof = false;
-    size_t batch_bytes = 64u << 10;  // grows x4 per refill up to kMaxBatch
-    static constexpr size_t kMaxBatch = 64u << 20;
-
-    bool fill(size_t need) {
-        while (buf.size() - pos < need && !eof) {
-            if (!refill()) return false;
-        }
-        return buf.size() - pos >= need;
+// Reads and inflates the BGZF stream ahead of the consumer on a thread of its own
+// (its blocks inflated on a pool of the bam's threads), so the file reads and the
+// inflate overlap the decode of the chunk before. Chunks start at 64 KiB of
+// compressed bytes (a header or a tag check needs little) and grow x4 up to 16 MiB;
+// at most two wait for the consumer.
+class Prefetch {
+  public:
+    Prefetch(mgp_bam* bam, uint64_t coff) : bam_(bam), coff_(coff), pool_(std::max(1, bam->n_threads)) {
+        th_ = std::thread([this] { run(); });
     }
+    ~Prefetch() {
+        {
+            std::lock_guard<std::mutex> g(mu_);
+            stop_ = true;
+        }
+        cv_.notify_all();
+        th_.join();
+        for (Chunk* c : ready_) delete c;
+        for (Chunk* c : free_) delete c;
+    }
+    // the next chunk in file order; nullptr on error (message in err())
+    Chunk* next() {
+        std::unique_lock<std::mutex> g(mu_);
+        cv_.wait(g, [&] { return !ready_.empty() || failed_; });
+        if (ready_.empty()) return nullptr;
+        Chunk* c = ready_.front();
+        ready_.pop_front();
+        cv_.notify_all();
+        return c;
+    }
+    void recycle(Chunk* c) {
+        {
+            std::lock_guard<std::mutex> g(mu_);
+            free_.push_back(c);
+        }
+        cv_.notify_all();
+    }
+    const std::string& err() const { return err_; }
+    double t_pread = 0, t_inflate = 0;
 
-    bool refill() {
-        if (coff >= (uint64_t)bam->file_size) {
-            eof = true;
+  private:
+    static constexpr size_t kMaxBatch = 16u << 20;
+    static constexpr size_t kAhead = 2;
+    void set_fail(const std::string& m) {
+        std::lock_guard<std::mutex> g(mu_);
+        err_ = m;
+        failed_ = true;
+        cv_.notify_all();
+    }
+    void run() {
+        size_t want_c = 64u << 10;
+        std::vector<uint8_t> raw;
+        std::vector<Block> blocks;
+        bool last = false;
+        while (!last) {
+            Chunk* c = nullptr;
+            {
+                std::unique_lock<std::mutex> g(mu_);
+                cv_.wait(g, [&] { return stop_ || ready_.size() < kAhead; });
+                if (stop_) return;
+                if (!free_.empty()) {
+                    c = free_.back();
+                    free_.pop_back();
+                }
+            }
+            if (!c) c = new (std::nothrow) Chunk();
+            if (!c) return set_fail("out of host memory");
+            c->n = 0;
+            c->last = false;
+            if (coff_ >= (uint64_t)bam_->file_size) {
+                c->last = last = true;
+            } else {
+                size_t want = (size_t)std::min<uint64_t>(want_c, (uint64_t)bam_->file_size - coff_);
+                want_c = std::min(kMaxBatch, want_c * 4);
+                // whole blocks only; a block larger than the read: read it alone
+                for (;;) {
+                    const double tr0 = now_s();
+                    raw.resize(want);
+                    const bool rd_ok = pread_all(bam_->fd, raw.data(), want, coff_);
+                    t_pread += now_s() - tr0;
+                    if (!rd_ok) return delete c, set_fail("read error in " + bam_->path);
+                    blocks.clear();
+                    size_t p = 0, total = 0;
+                    while (p < want) {
+                        const uint32_t bs = bgzf_block_size(raw.data() + p, want - p);
+                        if (bs == 0) {
+                            if (blocks.empty() && want - p >= 18)
+                                return delete c, set_fail("not a BGZF block at offset " + std::to_string(coff_ + p));
+                            break;
+                        }
+                        if (p + bs > want) break;  // partial block: next chunk
+                        Block b;
+                        b.coff = p;
+                        b.csize = bs;
+                        b.isize = rd32(raw.data() + p + bs - 4);
+                        if (b.isize > 65536 || bs < 12u + rd16(raw.data() + p + 10) + 8u)
+                            return delete c, set_fail("corrupt BGZF block at offset " + std::to_string(coff_ + p));
+                        b.out_off = total;
+                        total += b.isize;
+                        blocks.push_back(b);
+                        p += bs;
+                    }
+                    if (!blocks.empty()) {
+                        if (kHead + total > c->cap) {
+                            c->cap = kHead + total + (total >> 3);
+                            c->mem.reset(new (std::nothrow) uint8_t[c->cap]);
+                            if (!c->mem) return delete c, set_fail("out of host memory");
+                        }
+                        std::atomic<size_t> next{0};
+                        std::atomic<bool> ok{true};
+                        const int nt = std::max(1, std::min<int>(pool_.size(), (int)blocks.size()));
+                        uint8_t* out = c->mem.get() + kHead;
+                        const double ti0 = now_s();
+                        pool_.run(nt, [&](int) {
+                            mgp_host::Inflator inf;
+                            for (;;) {
+                                const size_t i = next.fetch_add(1);
+                                if (i >= blocks.size()) break;
+                                const Block& b = blocks[i];
+                                if (!inflate_block(raw.data() + b.coff, b.csize, out + b.out_off, b.isize, inf)) {
+                                    ok = false;
+                                    break;
+                                }
+                            }
+                        });
+                        t_inflate += now_s() - ti0;
+                        if (!ok) return delete c, set_fail("BGZF inflate/CRC error in " + bam_->path);
+                        c->n = total;
+                        coff_ += p;
+                        c->last = last = coff_ >= (uint64_t)bam_->file_size;
+                        break;
+                    }
+                    // no whole block in `want` bytes: the block at coff_ alone
+                    if (want < 18) return delete c, set_fail("truncated BGZF");
+                    const uint32_t bs = bgzf_block_size(raw.data(), want);
+                    if (!bs) return delete c, set_fail("bad BGZF header");
+                    if (coff_ + bs > (uint64_t)bam_->file_size)
+                        return delete c, set_fail("truncated BGZF block at offset " + std::to_string(coff_) + " in " +
+                                                  bam_->path);
+                    want = bs;
+                }
+            }
+            {
+                std::lock_guard<std::mutex> g(mu_);
+                ready_.push_back(c);
+            }
+            cv_.notify_all();
+        }
+    }
+    mgp_bam* bam_;
+    uint64_t coff_;
+    mgp_host::Pool pool_;  // (before th_: alive while run() uses it)
+    std::thread th_;
+    std::mutex mu_;
+    std::condition_variable cv_;
+    std::deque<Chunk*> ready_;
+    std::vector<Chunk*> free_;
+    bool stop_ = false, failed_ = false;
+    std::string err_;
+};
+
+// A sequential reader over the inflated BGZF stream: the consumer's view of the
+// prefetched chunks ([base + pos, base + size) is valid until the next fill).
+struct Stream {
+    mgp_bam* bam = nullptr;
+    std::unique_ptr<Prefetch> pf;
+    Chunk* cur = nullptr;
+    std::vector<uint8_t> big;  // a carried record larger than kHead, with the chunk after it
+    const uint8_t* base = nullptr;
+    size_t size = 0, pos = 0;
+    bool eof = false;
+
+    ~Stream() {
+        if (pf) {  // (the profile counters of mgp_bam_read_ref, on the consumer's thread)
+            t_pread += pf->t_pread;
+            t_inflate += pf->t_inflate;
+        }
+        if (cur && pf) pf->recycle(cur);
+        pf.reset();
+    }
+    bool fill(size_t need) {
+        while (size - pos < need && !eof)
+            if (!advance()) return false;
+        return size - pos >= need;
+    }
+    bool advance() {
+        Chunk* nx = pf->next();
+        if (!nx) return fail(pf->err()), false;
+        if (nx->n == 0) {  // (the end of the file: nothing to append)
+            eof = nx->last;
+            pf->recycle(nx);
             return true;
         }
-        const size_t want = (size_t)std::min<uint64_t>(batch_bytes, (uint64_t)bam->file_size - coff);
-        batch_bytes = std::min(kMaxBatch, batch_bytes * 4);
-        const double tr0 = now_s();
-        std::unique_ptr<uint8_t[]> raw_buf(new (std::nothrow) uint8_t[want]);
-        if (!raw_buf) {
-            fail("out of host memory");
-            return false;
+        const size_t t = size - pos;  // the partial record carried over
+        if (t <= kHead) {
+            uint8_t* dst = nx->mem.get() + kHead - t;
+            if (t) std::memcpy(dst, base + pos, t);
+            base = dst;
+        } else {
+            std::vector<uint8_t> nb(t + nx->n);
+            std::memcpy(nb.data(), base + pos, t);
+            std::memcpy(nb.data() + t, nx->mem.get() + kHead, nx->n);
+            big.swap(nb);
+            base = big.data();
         }
-        uint8_t* const raw_p = raw_buf.get();
-        const bool rd_ok = pread_all(bam->fd, raw_p, want, coff);
-        t_pread += now_s() - tr0;
-        if (!rd_ok) {
-            fail("read error in " + bam->path);
-            return false;
-        }
-        std::vector<Block> blocks;
-        size_t p = 0, total = 0;
-        while (p < want) {
-            const uint32_t bs = bgzf_block_size(raw_p + p, want - p);
-            if (bs == 0) {
-                if (blocks.empty()) {
-                    fail("not a BGZF block at offset " + std::to_string(coff + p));
-                    return false;
-                }
-                break;
-            }
-            if (p + bs > want) break;  // partial block: next batch
-            Block b;
-            b.coff = p;
-            b.csize = bs;
-            b.isize = rd32(raw_p + p + bs - 4);
-            if (b.isize > 65536 || bs < 12u + rd16(raw_p + p + 10) + 8u) {
-                fail("corrupt BGZF block at offset " + std::to_string(coff + p));
-                return false;
-            }
-            b.out_off = total;
-            total += b.isize;
-            blocks.push_back(b);
-            p += bs;
-        }
-        if (blocks.empty()) {
-            // a single block larger than the batch: read it alone
-            uint8_t hdr[18];
-            if (!pread_all(bam->fd, hdr, 18, coff)) return fail("truncated BGZF"), false;
-            const uint32_t bs = bgzf_block_size(hdr, 18);
-            if (!bs) return fail("bad BGZF header"), false;
-            if (coff + bs > (uint64_t)bam->file_size)
-                return fail("truncated BGZF block at offset " + std::to_string(coff) + " in " + bam->path), false;
-            batch_bytes = std::max<size_t>(batch_bytes, bs);
-            return refill();
-        }
-        // compact the consumed prefix, then inflate the batch into the tail
-        if (pos) {
-            buf.drop_front(pos);
-            pos = 0;
-        }
-        const size_t base = buf.size();
-        if (!buf.resize(base + total)) {
-            fail("out of host memory");
-            return false;
-        }
-        std::atomic<size_t> next{0};
-        std::atomic<bool> ok{true};
-        const int nt = std::max(1, std::min<int>(bam->n_threads, (int)blocks.size()));
-        auto work = [&]() {
-            mgp_host::Inflator inf;
-            for (;;) {
-                const size_t i = next.fetch_add(1);
-                if (i >= blocks.size()) break;
-                const Block& b = blocks[i];
-                if (!inflate_block(raw_p + b.coff, b.csize, buf.data() + base + b.out_off, b.isize, inf)) {
-                    ok = false;
-                    break;
-                }
-            }
-        };
-        const double ti0 = now_s();
-        std::vector<std::thread> th;
-        for (int t = 1; t < nt; ++t) th.emplace_back(work);
-        work();
-        for (auto& t : th) t.join();
-        t_inflate += now_s() - ti0;
-        if (!ok) return fail("BGZF inflate/CRC error in " + bam->path), false;
-        coff += p;
+        size = t + nx->n;
+        pos = 0;
+        eof = nx->last;
+        if (cur) pf->recycle(cur);
+        cur = nx;
         return true;
     }
-
-    const uint8_t* peek() const { return buf.data() + pos; }
-    size_t avail() const { return buf.size() - pos; }
+    const uint8_t* peek() const { return base + pos; }
+    size_t avail() const { return size - pos; }
 };
 
 bool stream_at(mgp_bam* bam, uint64_t voff, Stream& st) {
     st.bam = bam;
-    st.coff = voff >> 16;
-    st.buf.clear();
-    st.pos = 0;
+    st.pf.reset();
+    st.cur = nullptr;
+    st.base = nullptr;
+    st.size = st.pos = 0;
     st.eof = false;
+    st.pf.reset(new Prefetch(bam, voff >> 16));
     const size_t uoff = voff & 0xFFFF;
     if (uoff) {
         if (!st.fill(uoff)) return false;
@@ -552,9 +638,9 @@ int for_each_batch(mgp_bam* bam, int tid, F&& f) {
         if (!st.fill(4 + (size_t)bs0)) return fail(g_err.empty() ? "truncated BAM record body" : g_err);
         recs.clear();
         sizes.clear();
-        const uint8_t* base = st.buf.data();
+        const uint8_t* base = st.base;
         size_t p = st.pos;
-        const size_t end = st.buf.size();
+        const size_t end = st.size;
         while (end - p >= 4) {
             const uint32_t bs = rd32(base + p);
             if (bs < 32) return fail("corrupt BAM record (block_size < 32)");
@@ -638,6 +724,7 @@ struct Cols {
 // (begin_batch) may take several chunks (inflated buffers); its payload starts at 0.
 struct Decoder {
     mgp_bam* b;
+    mgp_host::Pool pool;
     uint64_t amask;
     bool paired;
     int32_t n_keys = 0;
@@ -656,7 +743,7 @@ struct Decoder {
     std::vector<uint32_t> ncg;  // CIGAR operations (CG tag resolved)
     std::vector<const uint8_t*> cgp;
     std::vector<uint8_t> pkd;   // record layout: 0 full, 1 packed 64-byte, 2 32-byte
-    double t_p1 = 0, t_p2 = 0;
+    double t_p1 = 0, t_p2 = 0, t_place = 0, t_fields = 0;
 
     static int32_t keys_of(mgp_bam* b) {
         int32_t n = 0;
@@ -665,7 +752,8 @@ struct Decoder {
         return n;
     }
     Decoder(mgp_bam* bam, int rec_align)
-        : b(bam), amask((uint64_t)rec_align - 1), paired(bam->placement == MGP_PLACE_PAIRED),
+        : b(bam), pool(std::max(1, bam->n_threads)), amask((uint64_t)rec_align - 1),
+          paired(bam->placement == MGP_PLACE_PAIRED),
           n_keys(paired ? keys_of(bam) : 0), dups(paired ? (size_t)keys_of(bam) : 0) {
         open.assign(paired ? (size_t)n_keys + 1 : 0, ~0ull);
         open32.assign(paired ? (size_t)n_keys + 1 : 0, ~0ull);
@@ -694,8 +782,43 @@ struct Decoder {
     }
     uint64_t line_slack() const { return paired ? 2ull * 128ull * ((uint64_t)n_keys + 1) : 0ull; }
 
-    // pass 1 for one record (appended to the chunk); false on a malformed record
-    bool classify(const uint8_t* r, uint32_t size) {
+    // pass 1 over the chunk's records (recs/sizes filled by the caller), on the pool;
+    // false on a malformed record
+    bool classify_all() {
+        const size_t m = recs.size();
+        rsz.resize(m);
+        ncg.resize(m);
+        cgp.resize(m);
+        pkd.resize(m);
+        const int tn = (int)std::max<size_t>(1, std::min<size_t>((size_t)pool.size(), m / 8192 + 1));
+        std::atomic<bool> ok{true};
+        std::string msg;
+        std::mutex mu;
+        pool.run(tn, [&](int t) {
+            const size_t lo = m * (size_t)t / (size_t)tn, hi = m * (size_t)(t + 1) / (size_t)tn;
+            for (size_t i = lo; i < hi; ++i)
+                if (!classify_at(i)) {
+                    std::lock_guard<std::mutex> g(mu);
+                    if (ok) msg = g_err;
+                    ok = false;
+                    return;
+                }
+        });
+        if (!ok) g_err = msg;
+        return ok;
+    }
+    void truncate(size_t m) {
+        recs.resize(m);
+        sizes.resize(m);
+        rsz.resize(m);
+        ncg.resize(m);
+        cgp.resize(m);
+        pkd.resize(m);
+    }
+    // pass 1 for record i of the chunk; false on a malformed record
+    bool classify_at(size_t i) {
+        const uint8_t* r = recs[i];
+        const uint32_t size = sizes[i];
         const uint8_t l_name = r[8];
         uint32_t n_cig = rd16(r + 12);
         const uint32_t l_seq = rd32(r + 16);
@@ -718,23 +841,13 @@ struct Decoder {
         const bool seqqual = l_seq != 0 && qualp[0] != 0xFF;  // else NOSEQQUAL: never packed
         const uint8_t pk = (b->pack32 && seqqual && bam_packable32(rdi32(r + 4), l_seq, n_cig, cig)) ? 2
                            : (b->pack && bam_packable(rdi32(r + 4), rd16(r + 14), l_seq, n_cig, cig, qualp)) ? 1 : 0;
-        recs.push_back(r);
-        sizes.push_back(size);
-        ncg.push_back(n_cig);
-        cgp.push_back(cig);
-        pkd.push_back(pk);
-        rsz.push_back(pk == 2 ? (uint64_t)MGP_PACK32_BYTES
-                      : pk ? (uint64_t)MGP_PACK_BYTES
-                           : (uint64_t)mgp_cigar_offset(l_seq) + 4ull * n_cig);
+        ncg[i] = n_cig;
+        cgp[i] = cig;
+        pkd[i] = pk;
+        rsz[i] = pk == 2 ? (uint64_t)MGP_PACK32_BYTES
+                 : pk ? (uint64_t)MGP_PACK_BYTES
+                      : (uint64_t)mgp_cigar_offset(l_seq) + 4ull * n_cig;
         return true;
-    }
-    void unclassify_last() {
-        recs.pop_back();
-        sizes.pop_back();
-        ncg.pop_back();
-        cgp.pop_back();
-        pkd.pop_back();
-        rsz.pop_back();
     }
 
     // one record: decode (do_fields: the SoA columns, barcode lookup included) and
@@ -817,7 +930,8 @@ struct Decoder {
     // payload appended at `cursor`. reserve(kn, pay_end) makes room for kn columns and
     // pay_end payload bytes (+256), then cols() are the arrays; false = out of memory.
     template <class Reserve, class GetCols>
-    int decode(size_t k0, int64_t gidx0, int nt, Reserve&& reserve, GetCols&& cols) {
+    int decode(size_t k0, int64_t gidx0, Reserve&& reserve, GetCols&& cols) {
+        const int nt = pool.size();
         const double tp1 = now_s();
         const size_t m = recs.size();
         if (!m) return 0;
@@ -837,24 +951,24 @@ struct Decoder {
         const int tn = (int)std::max<size_t>(1, std::min<size_t>((size_t)nt, m / 4096 + 1));
         std::vector<int64_t> tags((size_t)tn, 0), firsts((size_t)tn, -1);
         auto run_pass = [&](const Cols& c, bool do_fields, bool do_rec) {
-            auto work = [&](int t) {
+            pool.run(tn, [&](int t) {
                 const size_t lo = m * (size_t)t / (size_t)tn, hi = m * (size_t)(t + 1) / (size_t)tn;
                 for (size_t i = lo; i < hi; ++i)
                     decode_one(c, recs[i], sizes[i], k0 + i, paired ? c.roff[k0 + i] : rsz[i], ncg[i], cgp[i],
                                (int)pkd[i], tags[(size_t)t], firsts[(size_t)t], gidx0 + (int64_t)i, do_fields, do_rec);
-            };
-            std::vector<std::thread> th;
-            for (int t = 1; t < tn; ++t) th.emplace_back(work, t);
-            work(0);
-            for (auto& x : th) x.join();
+            });
         };
         if (!paired) {
             run_pass(cols(), true, true);
             cursor = end;
         } else {
+            double tpl = 0;
             {
                 const Cols c = cols();
+                const double tf = now_s();
                 run_pass(c, true, false);
+                t_fields += now_s() - tf;
+                tpl = now_s();
                 // pass 1b: which half-line each record takes (mgp_place_records' rule)
                 const uint16_t drop = MGP_FLAG_UNMAPPED | MGP_FLAG_SECONDARY | MGP_FLAG_SUPPLEMENTARY;
                 for (size_t i = 0; i < m; ++i) {
@@ -891,6 +1005,7 @@ struct Decoder {
                     }
                 }
             }
+            t_place += now_s() - tpl;
             if (!reserve(kn, cursor)) return fail("out of host memory"), -1;
             const Cols c = cols();
             // second halves of lines that stay open: zero (a later chunk may still fill
@@ -1045,19 +1160,20 @@ int mgp_bam_read_ref(mgp_bam* b, int tid, int rec_align, mgp_bam_batch* out) {
                                               const std::vector<uint32_t>& sizes) -> int {
         const double tp1 = now_s();
         dec.clear_chunk();
-        for (size_t i = 0; i < recs.size(); ++i)
-            if (!dec.classify(recs[i], sizes[i])) return -1;
+        dec.recs = recs;
+        dec.sizes = sizes;
+        if (!dec.classify_all()) return -1;
         dec.t_p1 += now_s() - tp1;
         const size_t k0 = G_start.n;
-        if (dec.decode(k0, (int64_t)k0, nt, reserve, cols) != 0) return -1;
+        if (dec.decode(k0, (int64_t)k0, reserve, cols) != 0) return -1;
         G_start.n = G_bc.n = G_tlen.n = G_flag.n = G_mapq.n = G_span.n = G_roff.n = k0 + recs.size();
         G_pay.n = dec.cursor;
         return 1;
     });
     if (std::getenv("MGP_HOST_PROFILE"))
         std::fprintf(stderr, "[mgp_bam_read_ref] %zu records, %d threads: total %.3f s = pread %.3f + inflate %.3f + "
-                     "scan/sizes %.3f + decode %.3f (+ rest)\n", G_start.n, nt, now_s() - t_begin, t_pread, t_inflate,
-                     dec.t_p1, dec.t_p2);
+                     "scan/sizes %.3f + decode %.3f (fields %.3f, placement %.3f) (+ rest)\n", G_start.n, nt,
+                     now_s() - t_begin, t_pread, t_inflate, dec.t_p1, dec.t_p2, dec.t_fields, dec.t_place);
     auto release = [&]() {
         std::free(G_start.p); std::free(G_bc.p); std::free(G_tlen.p); std::free(G_flag.p);
         std::free(G_mapq.p); std::free(G_span.p); std::free(G_roff.p); std::free(G_pay.p);
@@ -1095,6 +1211,7 @@ struct mgp_bam_stream {
     bool seen = false, done = false;
     Decoder dec;
     int64_t decoded = 0;  // records handed out so far
+    std::vector<size_t> offs;  // the chunk's record offsets in the stream buffer
     mgp_bam_stream(mgp_bam* b, int rec_align) : bam(b), dec(b, rec_align) {}
 };
 
@@ -1135,8 +1252,8 @@ int64_t mgp_bam_stream_next(mgp_bam_stream* s, int64_t cap_reads, int64_t cap_pa
         return kn <= (size_t)cap_reads && pay_end + 256 <= (uint64_t)cap_payload;
     };
     auto cols = [&]() { return c; };
-    const int nt = std::max(1, s->bam->n_threads);
     dec.begin_batch();
+    std::vector<size_t>& offs = s->offs;
     size_t k = 0;
     uint64_t bound = 0;
     bool full = false;
@@ -1155,9 +1272,12 @@ int64_t mgp_bam_stream_next(mgp_bam_stream* s, int64_t cap_reads, int64_t cap_pa
         if (!st.fill(4 + (size_t)bs0)) return fail(g_err.empty() ? "truncated BAM record body" : g_err);
         const double tp1 = now_s();
         dec.clear_chunk();
-        const uint8_t* base = st.buf.data();
+        const uint8_t* base = st.base;
         size_t p = st.pos;
-        const size_t end = st.buf.size();
+        const size_t end = st.size;
+        bool at_end = false;
+        offs.clear();
+        // record boundaries (sequential), then pass 1 on the pool, then the batch's cut
         while (end - p >= 4 && k + dec.recs.size() < (size_t)cap_reads) {
             const uint32_t bs = rd32(base + p);
             if (bs < 32) return fail("corrupt BAM record (block_size < 32)");
@@ -1165,23 +1285,31 @@ int64_t mgp_bam_stream_next(mgp_bam_stream* s, int64_t cap_reads, int64_t cap_pa
             const int32_t ref = rdi32(base + p + 4);
             if (ref == s->tid) {
                 s->seen = true;
-                if (!dec.classify(base + p + 4, bs)) return -1;
-                const uint64_t w = dec.worst(dec.recs.size() - 1);
-                if (bound + w + slack > (uint64_t)cap_payload) {
-                    dec.unclassify_last();
-                    full = true;
-                    break;
-                }
-                bound += w;
+                dec.recs.push_back(base + p + 4);
+                dec.sizes.push_back(bs);
+                offs.push_back(p);
             } else if (s->seen || ref > s->tid || ref < 0) {
-                s->done = true;  // coordinate-sorted: tid's records are contiguous
+                at_end = true;  // coordinate-sorted: tid's records are contiguous
                 break;
             }
             p += 4 + (size_t)bs;
         }
+        if (!dec.classify_all()) return -1;
+        for (size_t i = 0; i < dec.recs.size(); ++i) {
+            const uint64_t w = dec.worst(i);
+            if (bound + w + slack > (uint64_t)cap_payload) {  // the rest goes to the next batch
+                p = offs[i];
+                dec.truncate(i);
+                full = true;
+                at_end = false;
+                break;
+            }
+            bound += w;
+        }
+        if (at_end) s->done = true;
         dec.t_p1 += now_s() - tp1;
         if (!dec.recs.empty()) {
-            if (dec.decode(k, s->decoded + (int64_t)k, nt, reserve, cols) != 0) return -1;
+            if (dec.decode(k, s->decoded + (int64_t)k, reserve, cols) != 0) return -1;
             k += dec.recs.size();
         }
         st.pos = p;
