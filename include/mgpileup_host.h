@@ -154,6 +154,18 @@ int mgp_bam_write(const char *path, const char *const *ref_names, const int64_t 
 int64_t mgp_deflate_tiles(const void *data, int64_t rows, int64_t cols, int32_t elem_size, int64_t crow,
                           int64_t ccol, int level, int n_threads, uint8_t **blob, int64_t *offsets);
 
+/* The HDF5 planes straight from the engine's cell-major rows (IncrementalHDF5Writer,
+ * writers.py:200-218): plane e is plane[p][j] = min(rows[cell_of_col[j]][p][elems[e]],
+ * 65535) (0 where cell_of_col[j] < 0) as a row-major [L][n_cols] u16 array; `rows` is
+ * [n_rows][L][row_elems] of elem_size 2 (the exact 16-bit rows) or 4 (u32). Each plane
+ * is cut into (crow x ccol) chunks and deflated as mgp_deflate_tiles does, all planes of
+ * a chunk from one read of the cells' rows, on n_threads threads. Chunk t of plane e
+ * is blob[offsets[e * n_chunks + t], offsets[e * n_chunks + t + 1]) (`offsets` has
+ * n_planes * n_chunks + 1 entries). Returns n_chunks per plane, -1 on error. */
+int64_t mgp_h5_plane_tiles(const void *rows, int32_t elem_size, int64_t row_elems, int64_t n_rows, int64_t L,
+                           const int64_t *cell_of_col, int64_t n_cols, const int32_t *elems, int32_t n_planes,
+                           int64_t crow, int64_t ccol, int level, int n_threads, uint8_t **blob, int64_t *offsets);
+
 /* Payload placement for producers: rec_off[i] for records of rec_bytes[i]
  * bytes, in BAM order. MGP_PLACE_DENSE: consecutive, each rounded up to
  * rec_align. MGP_PLACE_PAIRED: two consecutive packed (64-byte) records of one

@@ -106,6 +106,10 @@ def host_library() -> C.CDLL:
         lib.mgp_bam_write.argtypes = [C.c_char_p, C.POINTER(C.c_char_p), C.POINTER(C.c_int64), C.c_int, C.c_int,
                                       C.POINTER(mgp_bam_batch), C.POINTER(C.c_char_p), C.c_int, C.c_char_p,
                                       C.c_char_p, C.c_int, C.c_int, C.c_int]
+        lib.mgp_h5_plane_tiles.argtypes = [vp, C.c_int32, C.c_int64, C.c_int64, C.c_int64, vp, C.c_int64, vp,
+                                           C.c_int32, C.c_int64, C.c_int64, C.c_int, C.c_int,
+                                           C.POINTER(C.POINTER(C.c_uint8)), vp]
+        lib.mgp_h5_plane_tiles.restype = C.c_int64
         lib.mgp_repack32.argtypes = [C.c_int64, vp, C.c_int64, vp, vp, C.c_int32, C.c_int32, vp, vp, C.c_int]
         lib.mgp_repack32.restype = C.c_int64
         lib.mgp_bam_ref_records.argtypes = [vp, C.c_int]
@@ -442,6 +446,37 @@ def deflate_tiles(a: np.ndarray, chunks: tuple[int, int], level: int = 4, n_thre
     finally:
         lib.mgp_host_buf_free(C.cast(blob, C.c_void_p))
     return [raw[offs[i]:offs[i + 1]] for i in range(n)]
+
+
+def h5_plane_tiles(rows: np.ndarray, cell_of_col: np.ndarray, elems: list[int], chunks: tuple[int, int],
+                   level: int = 4, n_threads: int = 0) -> list[list[bytes]]:
+    """libmgphost `mgp_h5_plane_tiles`: for each element e of the cell-major rows
+    [cells, L, k] (u16 or u32), the deflated chunks of the [L, n_cols] u16 plane
+    min(rows[cell_of_col[j], p, e], 65535); chunks row-major over the chunk grid."""
+    lib = host_library()
+    if rows.ndim == 2:
+        rows = rows[:, :, None]
+    rows = np.ascontiguousarray(rows)
+    if rows.dtype not in (np.uint16, np.uint32):
+        raise ValueError("rows must be u16 or u32")
+    n_rows, L, k = rows.shape
+    coc = np.ascontiguousarray(cell_of_col, np.int64)
+    el = np.ascontiguousarray(elems, np.int32)
+    if el.size == 0 or el.min() < 0 or el.max() >= k or (coc.size and coc.max() >= n_rows):
+        raise ValueError("plane element or cell index out of range")
+    nr, nc = -(-L // chunks[0]), -(-coc.size // chunks[1])
+    offs = np.zeros(el.size * nr * nc + 1, np.int64)
+    blob = C.POINTER(C.c_uint8)()
+    n = lib.mgp_h5_plane_tiles(rows.ctypes.data, rows.dtype.itemsize, k, n_rows, L, coc.ctypes.data, coc.size,
+                               el.ctypes.data, el.size, int(chunks[0]), int(chunks[1]), int(level),
+                               int(n_threads or host_threads()), C.byref(blob), offs.ctypes.data)
+    if n < 0:
+        raise OSError(_err())
+    try:
+        raw = C.string_at(blob, int(offs[-1])) if offs[-1] else b""
+    finally:
+        lib.mgp_host_buf_free(C.cast(blob, C.c_void_p))
+    return [[raw[offs[e * n + i]:offs[e * n + i + 1]] for i in range(n)] for e in range(el.size)]
 
 
 # ---------------------------------------------------------------------------

@@ -206,10 +206,11 @@ class IncrementalHDF5Writer:
         self.position_base_counts = np.zeros((self.n_positions, 4), np.int64)
         self.cell_depths: dict[str, float] = {}
         L, n = self.n_positions, self.n_barcodes
-        # column buffers; flushed once per dataset (the reference writes per 250-cell batch)
-        self._planes = {f"{b}_{s}": np.zeros((L, n), np.uint16) for b in BASES for s in STRANDS}
-        self._tn5 = {s: np.zeros((L, n), np.uint16) for s in STRANDS}
-        self._coverage = np.zeros((L, n), np.uint16)
+        # the engine's arrays and their columns (write_cells): the planes are built, chunked
+        # and deflated natively at finalize (mgp_h5_plane_tiles); the per-cell API
+        # (write_cell) fills dense column buffers instead
+        self._sources: list[tuple] = []
+        self._planes = self._tn5 = self._coverage = None
         self._meta = {
             "mean_depth": np.zeros(n, np.float32),
             "median_depth": np.zeros(n, np.float32),
@@ -218,8 +219,26 @@ class IncrementalHDF5Writer:
             "total_bases": np.zeros(n, np.float32),
         }
 
+    def _dense(self):
+        """The column buffers of the dense path (flushed once per dataset; the
+        reference writes per 250-cell batch), with every recorded source's columns."""
+        if self._planes is None:
+            L, n = self.n_positions, self.n_barcodes
+            self._planes = {f"{b}_{s}": np.zeros((L, n), np.uint16) for b in BASES for s in STRANDS}
+            self._tn5 = {s: np.zeros((L, n), np.uint16) for s in STRANDS}
+            self._coverage = np.zeros((L, n), np.uint16)
+            for res, sel_a, col_a in self._sources:
+                for bi, b in enumerate(BASES):
+                    for si, s in enumerate(STRANDS):
+                        self._planes[f"{b}_{s}"][:, col_a] = np.minimum(res.counts[sel_a, :, 2 * bi + si], 65535).T
+                for si, s in enumerate(STRANDS):
+                    self._tn5[s][:, col_a] = np.minimum(res.tn5[sel_a, :, si], 65535).T
+                self._coverage[:, col_a] = np.minimum(res.depth[sel_a], 65535).T
+            self._sources = []
+
     def _put(self, col: int, counts: np.ndarray, tn5: np.ndarray, depth: np.ndarray, med_lo: int, med_hi: int,
              depth_sum: int, covered: int, depth_max: int):
+        self._dense()
         sat = np.minimum(counts, 65535).astype(np.uint16)
         for bi, b in enumerate(BASES):
             self._planes[f"{b}_fwd"][:, col] = sat[:, 2 * bi]
@@ -253,12 +272,9 @@ class IncrementalHDF5Writer:
         if sel:
             sel_a = np.asarray(sel, np.int64)
             col_a = np.asarray(cols, np.int64)
-            for bi, b in enumerate(BASES):
-                for si, s in enumerate(STRANDS):
-                    self._planes[f"{b}_{s}"][:, col_a] = np.minimum(res.counts[sel_a, :, 2 * bi + si], 65535).T
-            for si, s in enumerate(STRANDS):
-                self._tn5[s][:, col_a] = np.minimum(res.tn5[sel_a, :, si], 65535).T
-            self._coverage[:, col_a] = np.minimum(res.depth[sel_a], 65535).T
+            self._sources.append((res, sel_a, col_a))
+            if self._planes is not None:
+                self._dense()
             covered = res.covered[sel_a].astype(np.float64)
             dsum = res.depth_sum[sel_a]
             self._meta["mean_depth"][col_a] = (dsum.astype(np.float64) / covered).astype(np.float32)
@@ -300,15 +316,36 @@ class IncrementalHDF5Writer:
         counts_file.attrs["n_positions"] = L
         counts_file.attrs["mito_chr"] = self.config.mito_chr
         counts_file.create_dataset("barcode", data=np.array(self.barcodes, dtype="S"))
-        for b in BASES:
+        names = [f"{b}_{s}" for b in BASES for s in STRANDS]
+        native = (n > 0 and self._planes is None and len(self._sources) == 1
+                  and hasattr(counts_file, "create_dataset_from_chunks"))
+        if native:
+            # the planes straight from the engine's cell-major rows, chunked and deflated in
+            # one native pass (the transposes, not the deflate, were the writer's cost)
+            from ..bam import h5_plane_tiles
+
+            res, sel_a, col_a = self._sources[0]
+            coc = np.full(n, -1, np.int64)
+            coc[col_a] = sel_a
+            tiles = {**dict(zip(names, h5_plane_tiles(res.counts, coc, list(range(8)), chunks, level=4))),
+                     **dict(zip(("tn5_cuts_fwd", "tn5_cuts_rev"), h5_plane_tiles(res.tn5, coc, [0, 1], chunks,
+                                                                                  level=4))),
+                     "coverage": h5_plane_tiles(res.depth, coc, [0], chunks, level=4)[0]}
+            for k in names + ["tn5_cuts_fwd", "tn5_cuts_rev"]:
+                counts_file.create_dataset_from_chunks(k, (L, n), np.uint16, chunks, 4, tiles[k])
+        else:
+            self._dense()
+            for k in names:
+                counts_file.create_dataset(k, data=self._planes[k], chunks=chunks, **comp)
             for s in STRANDS:
-                counts_file.create_dataset(f"{b}_{s}", data=self._planes[f"{b}_{s}"], chunks=chunks, **comp)
-        for s in STRANDS:
-            counts_file.create_dataset(f"tn5_cuts_{s}", data=self._tn5[s], chunks=chunks, **comp)
+                counts_file.create_dataset(f"tn5_cuts_{s}", data=self._tn5[s], chunks=chunks, **comp)
         meta = h5.File(self.output_dir / "metadata.h5", "w", libver="latest")
         meta.attrs["mito_chr"] = self.config.mito_chr
         meta.attrs["mito_length"] = L
-        meta.create_dataset("coverage", data=self._coverage, chunks=chunks, **comp)
+        if native:
+            meta.create_dataset_from_chunks("coverage", (L, n), np.uint16, chunks, 4, tiles["coverage"])
+        else:
+            meta.create_dataset("coverage", data=self._coverage, chunks=chunks, **comp)
         for k, v in self._meta.items():
             meta.create_dataset(k, data=v)
         refs = ref_alleles(self.position_base_counts)

@@ -431,6 +431,36 @@ class Group:
         self._children.append(ds)
         return ds
 
+    def create_dataset_from_chunks(self, name: str, shape, dtype, chunks, level: int, tiles: list[bytes]):
+        """A chunked gzip dataset written from already deflated chunks (the
+        H5Z_DEFLATE form, row-major over the chunk grid: mgp_h5_plane_tiles)."""
+        lib = _h5()
+        t, own = _type_for(np.dtype(dtype))
+        sp = _space(shape)
+        dcpl = _ck(lib.H5Pcreate(_T["H5P_CLS_DATASET_CREATE_ID_g"]), "H5Pcreate")
+        try:
+            _ck(lib.H5Pset_chunk(dcpl, len(chunks), _dims(chunks)), "H5Pset_chunk")
+            _ck(lib.H5Pset_deflate(dcpl, int(level)), "H5Pset_deflate")
+            did = _ck(lib.H5Dcreate2(self._id, name.encode(), t, sp, H5P_DEFAULT, dcpl, H5P_DEFAULT), "H5Dcreate2")
+            try:
+                nc = -(-shape[1] // chunks[1])
+                off = (hsize_t * 2)()
+                for i, blob in enumerate(tiles):
+                    off[0] = (i // nc) * chunks[0]
+                    off[1] = (i % nc) * chunks[1]
+                    _ck(lib.H5Dwrite_chunk(did, H5P_DEFAULT, 0, off, len(blob), blob), "H5Dwrite_chunk")
+            except Exception:
+                lib.H5Dclose(did)
+                raise
+        finally:
+            lib.H5Pclose(dcpl)
+            lib.H5Sclose(sp)
+            if own:
+                lib.H5Tclose(t)
+        ds = Dataset(did, name)
+        self._children.append(ds)
+        return ds
+
     @staticmethod
     def _write_chunks(did: int, arr: np.ndarray, chunks, level: int, n_threads: int):
         from .bam import deflate_tiles

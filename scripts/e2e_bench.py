@@ -30,6 +30,10 @@ def main():
     ap.add_argument("--threads", type=int, default=16)
     ap.add_argument("--out", default="/tmp/mgp_e2e")
     ap.add_argument("--formats", default="txt,hdf5")
+    ap.add_argument("--modes", default="stream,resident",
+                    help="stream: batches decoded and pushed as they come (the default pipeline); resident: the "
+                         "whole chrM set decoded, then one run")
+    ap.add_argument("--bam-level", type=int, default=6, help="BGZF level of the synthetic BAM (samtools' default 6)")
     args = ap.parse_args()
 
     from mgatk2_amd.bam import write_bam
@@ -48,25 +52,45 @@ def main():
     whitelist = barcode_names(args.cells, seed)
     t1 = time.time()
     bam = out / "possorted_bam.bam"
-    write_bam(bam, soa, whitelist, level=1, n_threads=args.threads)
+    write_bam(bam, soa, whitelist, level=args.bam_level, n_threads=args.threads)
     del soa
     t2 = time.time()
     (out / "barcodes.tsv").write_text("".join(b + "\n" for b in whitelist))
     print(f"[e2e] generated {args.reads:,} reads in {t1 - t0:.1f}s; BAM {bam.stat().st_size / 1e9:.2f} GB "
           f"written in {t2 - t1:.1f}s", file=sys.stderr, flush=True)
 
-    res = {"config": f"C3: {args.reads:,} reads x {args.cells} cells, run params (q20 mapq30 "
-                     "dedup=alignment_and_fragment_length)", "host_threads": args.threads}
-    for fmt in args.formats.split(","):
-        cfg = PipelineConfig(min_baseq=20, min_mapq=30, max_strand_bias=1.0, skip_deduplication=False,
-                             use_fragment_length_dedup=True, min_reads_per_cell=1, n_cores=args.threads)
-        t = time.time()
-        p = MtDNAPipeline(str(bam), whitelist, out / f"run_{fmt}", config=cfg, output_format=fmt)
-        ret = p.run()
-        wall = time.time() - t
-        res[fmt] = {"wall_s": round(wall, 2), **{k: round(v, 2) for k, v in p.timings.items()},
-                    "reads_per_s_end_to_end": round(args.reads / wall), "cells_passed": ret.get("cells_passed_qc")}
-        print(f"[e2e] {fmt}: {res[fmt]}", file=sys.stderr, flush=True)
+    name = {(50_000_000, 5_000): "C3", (200_000_000, 10_000): "C4"}.get((args.reads, args.cells), "custom")
+    res = {"config": f"{name}: {args.reads:,} reads x {args.cells} cells, run params (q20 mapq30 "
+                     "dedup=alignment_and_fragment_length)", "host_threads": args.threads,
+           "bam_bytes": bam.stat().st_size, "bam_level": args.bam_level}
+    digests = {}
+    for mode in args.modes.split(","):
+        for fmt in args.formats.split(","):
+            cfg = PipelineConfig(min_baseq=20, min_mapq=30, max_strand_bias=1.0, skip_deduplication=False,
+                                 use_fragment_length_dedup=True, min_reads_per_cell=1, n_cores=args.threads)
+            t = time.time()
+            od = out / f"run_{fmt}_{mode}"
+            p = MtDNAPipeline(str(bam), whitelist, od, config=cfg, output_format=fmt, stream=mode == "stream")
+            ret = p.run()
+            wall = time.time() - t
+            key = f"{fmt}_{mode}"
+            res[key] = {"wall_s": round(wall, 2),
+                        **{k: (round(v, 3) if isinstance(v, float) else v) for k, v in p.timings.items()},
+                        "reads_per_s_end_to_end": round(args.reads / wall), "cells_passed": ret.get("cells_passed_qc")}
+            print(f"[e2e] {key}: {res[key]}", file=sys.stderr, flush=True)
+            if fmt == "txt":  # streamed and resident runs must write the same text
+                import gzip
+                import hashlib
+
+                h = hashlib.sha256()
+                for f in ("A", "C", "G", "T", "coverage"):
+                    h.update(gzip.decompress((od / "output" / f"output.{f}.txt.gz").read_bytes()))
+                digests[mode] = h.hexdigest()
+            import shutil
+
+            shutil.rmtree(od, ignore_errors=True)
+    if len(digests) > 1:
+        res["txt_identical_across_modes"] = len(set(digests.values())) == 1
     print(json.dumps(res), flush=True)
 
 

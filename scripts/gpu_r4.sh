@@ -18,6 +18,17 @@ if [[ $STEPS == *fullsize* ]]; then
         || { tail -30 gpurun_out/pytest_fullsize_$V.log; exit 1; }
     tail -3 gpurun_out/pytest_fullsize_$V.log
 fi
+if [[ $STEPS == *e2e3* ]]; then
+    timeout -k 10 600 python -u scripts/e2e_bench.py --reads 50000000 --cells 5000 --out /tmp/mgp_e2e \
+        > gpurun_out/e2e_c3_$V.json 2> gpurun_out/e2e_c3_$V.log || { tail -30 gpurun_out/e2e_c3_$V.log; exit 1; }
+    cat gpurun_out/e2e_c3_$V.log
+fi
+if [[ $STEPS == *e2e4* ]]; then
+    timeout -k 10 900 python -u scripts/e2e_bench.py --reads 200000000 --cells 10000 --out /tmp/mgp_e2e4 \
+        --modes stream --formats txt,hdf5 > gpurun_out/e2e_c4_$V.json 2> gpurun_out/e2e_c4_$V.log \
+        || { tail -30 gpurun_out/e2e_c4_$V.log; exit 1; }
+    cat gpurun_out/e2e_c4_$V.log
+fi
 if [[ $STEPS == *bench* ]]; then
     timeout -k 10 500 python -u bench.py > gpurun_out/bench_$V.log 2>&1 || { tail -30 gpurun_out/bench_$V.log; exit 1; }
     tail -c 1500 gpurun_out/bench_$V.log
