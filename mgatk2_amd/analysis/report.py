@@ -314,12 +314,21 @@ def _tiles(d, summary):
             ("Mean depth", f"{(md.mean() if md.size else 0.0):.1f}×")]
 
 
+def _from_arrays(a: dict) -> dict:
+    """The writer's in-memory report arrays (IncrementalHDF5Writer.report_arrays) in
+    _load's form: the coverage plane as its per-position column mean."""
+    return {"coverage": np.asarray(a["coverage_mean"], np.float64), "coverage_sum": a["coverage_sum"],
+            "mean_depth": a["mean_depth"], "genome_coverage": a["genome_coverage"], "total_bases": a["total_bases"],
+            "reference": a["reference"], "total": a["total"], "tn5_fwd": a["tn5_fwd"], "tn5_rev": a["tn5_rev"]}
+
+
 def generate_html_report(output_dir: Path, sample_name: str = "mgatk2", title: str | None = None,
                          subtitle: str | None = None, working_directory: str | None = None,
-                         input_dir: str | None = None):
-    """scATAC report (singlecell.csv metadata present)."""
+                         input_dir: str | None = None, arrays: dict | None = None):
+    """scATAC report (singlecell.csv metadata present). ``arrays``: the writer's
+    in-memory sums (the files are then not read back)."""
     output_dir = Path(output_dir)
-    d = _load(output_dir, need_tn5=True, need_meta_group=True)
+    d = _from_arrays(arrays) if arrays is not None else _load(output_dir, need_tn5=True, need_meta_group=True)
     if d is None:
         return None
     summary = _summary(output_dir)
@@ -345,14 +354,15 @@ def generate_html_report(output_dir: Path, sample_name: str = "mgatk2", title: s
 
 def generate_scrna_html_report(output_dir: Path, sample_name: str = "mgatk2", title: str | None = None,
                                subtitle: str | None = None, working_directory: str | None = None,
-                               input_dir: str | None = None):
+                               input_dir: str | None = None, arrays: dict | None = None):
     """scRNA report (no singlecell.csv): read-start track and reads-vs-depth plot."""
     output_dir = Path(output_dir)
-    d = _load(output_dir, need_tn5=False, need_meta_group=False)
+    d = _from_arrays(arrays) if arrays is not None else _load(output_dir, need_tn5=False, need_meta_group=False)
     if d is None:
         return None
     summary = _summary(output_dir)
-    starts = d["coverage"].sum(axis=1, dtype=np.int64) if d["coverage"].ndim == 2 else d["coverage"]
+    starts = d["coverage"].sum(axis=1, dtype=np.int64) if d["coverage"].ndim == 2 else \
+        d.get("coverage_sum", d["coverage"])
     page = _page(
         _title(title, sample_name, working_directory, input_dir), subtitle or "mgatk2 output analysis",
         working_directory, _tiles(d, summary),

@@ -290,6 +290,41 @@ class IncrementalHDF5Writer:
                 cnt = res.counts[int(c)].astype(np.int64)
                 self.position_base_counts += cnt[:, 0::2] + cnt[:, 1::2]
 
+    def _report_arrays(self, refs: list[str]) -> dict:
+        """What the HTML report reads back from the files (report.py _load), from
+        memory: per-position sums over the columns of the coverage and Tn5 planes (of
+        the saturated u16 values, as stored) and the metadata arrays."""
+        L, n = self.n_positions, self.n_barcodes
+        sums = {k: np.zeros(L, np.int64) for k in ("coverage", "tn5_fwd", "tn5_rev")}
+        if self._planes is not None:
+            sums["coverage"] = self._coverage.sum(axis=1, dtype=np.int64)
+            sums["tn5_fwd"] = self._tn5["fwd"].sum(axis=1, dtype=np.int64)
+            sums["tn5_rev"] = self._tn5["rev"].sum(axis=1, dtype=np.int64)
+        else:
+            for res, sel_a, _ in self._sources:
+                for i in range(0, sel_a.size, 512):
+                    part = sel_a[i:i + 512]
+                    d = res.depth[part]
+                    t = res.tn5[part]
+                    if d.dtype != np.uint16:
+                        d, t = np.minimum(d, 65535), np.minimum(t, 65535)
+                    sums["coverage"] += d.sum(axis=0, dtype=np.int64)
+                    sums["tn5_fwd"] += t[:, :, 0].sum(axis=0, dtype=np.int64)
+                    sums["tn5_rev"] += t[:, :, 1].sum(axis=0, dtype=np.int64)
+        total = None
+        if self.barcode_metadata is not None and "total" in self.barcode_metadata:
+            bl = self.barcode_metadata.get("barcode", [])
+            b2i = {bc: i for i, bc in enumerate(bl)}
+            try:
+                total = np.asarray([self.barcode_metadata["total"][b2i[bc]] for bc in self.barcodes if bc in b2i],
+                                   dtype=np.float64)
+            except (TypeError, ValueError, IndexError):
+                total = None
+        return {"coverage_mean": sums["coverage"] / n if n else np.zeros(L), "coverage_sum": sums["coverage"],
+                "tn5_fwd": sums["tn5_fwd"], "tn5_rev": sums["tn5_rev"], "mean_depth": self._meta["mean_depth"],
+                "genome_coverage": self._meta["genome_coverage"], "total_bases": self._meta["total_bases"],
+                "reference": list(refs), "total": total if total is not None else np.zeros(0)}
+
     def write_cell(self, result: dict):
         """Reference per-cell API (writers.py:136-152)."""
         bc = result["barcode"]
@@ -366,6 +401,7 @@ class IncrementalHDF5Writer:
                     logger.warning("Could not store metadata column '%s': %s", col, e)
         counts_file.close()
         meta.close()
+        self.report_arrays = self._report_arrays(refs)
         qc_dir = Path(qc_dir)
         qc_dir.mkdir(exist_ok=True, parents=True)
         if self.cell_stats:

@@ -165,7 +165,8 @@ class MtDNAPipeline:
 
                 gen = generate_html_report if self.barcode_metadata is not None else generate_scrna_html_report
                 gen(self.output_dir, self.sample_name, title=self.report_title, subtitle=self.report_subtitle,
-                    working_directory=self.working_directory, input_dir=str(self.bam_path.parent))
+                    working_directory=self.working_directory, input_dir=str(self.bam_path.parent),
+                    arrays=getattr(writer, "report_arrays", None))
             except ImportError:
                 logger.warning("matplotlib not installed, skipping HTML report generation")
             except Exception as e:

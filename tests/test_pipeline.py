@@ -486,3 +486,33 @@ def test_pipeline_streamed_equals_resident_gpu(case, batch, tmp_path, engine_lib
     for rel in ("output/output.depthTable.txt", "output/chrM_refAllele.txt", "qc/cell_stats.csv"):
         assert (outs[True][0] / rel).read_text() == (outs[False][0] / rel).read_text(), rel
     _check_outputs(g, outs[True][0], outs[True][1])
+
+
+@pytest.mark.parametrize("csv", [False, True])
+def test_report_arrays_equal_the_files(tmp_path, oracle_engine, csv):
+    """The HTML report reads the writer's in-memory sums (no read-back of the planes):
+    they equal what report._load computes from counts.h5 / metadata.h5."""
+    from mgatk2_amd.analysis import report
+    from mgatk2_amd.config import PipelineConfig
+    from mgatk2_amd.file_io import IncrementalHDF5Writer
+    from mgatk2_amd.processing.processors import CellProcessor
+    from mgatk2_amd.synth import synth_reads
+
+    nc = 30
+    soa = synth_reads(5, 60_000, nc)
+    cfg = PipelineConfig(min_baseq=20, min_mapq=30)
+    names = [f"C{i:03d}-1" for i in range(nc)]
+    meta = {"barcode": names[::-1], "total": list(range(100, 100 + nc))} if csv else None
+    proc = CellProcessor(cfg, tmp_path)
+    res = proc.run_soa(soa, nc)
+    w = IncrementalHDF5Writer(tmp_path, cfg, names, barcode_metadata=meta)
+    proc.write_results(res, names, w)
+    w.finalize(tmp_path / "qc")
+    got = report._from_arrays(w.report_arrays)
+    exp = report._load(tmp_path, need_tn5=True, need_meta_group=True)
+    np.testing.assert_allclose(got["coverage"], exp["coverage"].mean(axis=1), rtol=1e-12)
+    np.testing.assert_array_equal(got["coverage_sum"], exp["coverage"].sum(axis=1, dtype=np.int64))
+    for k in ("tn5_fwd", "tn5_rev", "mean_depth", "genome_coverage", "total_bases", "total"):
+        np.testing.assert_array_equal(got[k], exp[k], err_msg=k)
+    assert got["reference"] == exp["reference"]
+    assert report.generate_html_report(tmp_path, "s", arrays=w.report_arrays) is not None
