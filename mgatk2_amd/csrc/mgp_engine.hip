@@ -132,6 +132,7 @@ struct mgp_ctx {
     Geom g{};
     int lds_hist_max_cells = 0;
     int hist_slice_cells = 0;  // > 0: cap on the histogram's cells per slice (MGP_HIST_SLICE_CELLS)
+    bool hist_xcd = true;      // several slices: a bin's slices dealt to one XCD (MGP_HIST_XCD)
     bool group_wide = false;   // MGP_GROUP_WIDE=1: 16-byte grouping elements always (tests, A/B)
 
     // resident inputs (BAM order)
@@ -287,14 +288,25 @@ __global__ void __launch_bounds__(kHistBlock) k_bin_count(const int32_t* __restr
                                                           uint32_t* __restrict__ PG, int ngroups,
                                                           uint32_t* __restrict__ bin_lo,
                                                           uint32_t* __restrict__ bin_valid, uint32_t* __restrict__ ck,
-                                                          DevStats* st, int seg_w0, int seg_bhi) {
+                                                          DevStats* st, int seg_w0, int seg_bhi, int nslices) {
     extern __shared__ uint32_t hist[];  // [slice cells] counts, then cum[slice groups]
     __shared__ int64_t s_range[2];
     __shared__ uint32_t s_nvalid, s_bits;
-    const int b = blockIdx.x;
-    const bool first = blockIdx.y == 0;
+    // grid: (bins, slices), or with several slices a 1-D grid that deals the slices of
+    // one bin to one XCD back to back (workgroups go round-robin over the 8 XCDs: ids
+    // x, x + 8, ... share one), so the slices' re-reads of the bin's barcodes and flags
+    // hit that XCD's L2 instead of HBM (slice-major order re-read every bin ~2000
+    // workgroups later)
+    int b = blockIdx.x, sl = blockIdx.y;
+    if (nslices < 0) {
+        const int ns = -nslices, j = (int)(blockIdx.x >> 3);
+        b = 8 * (j / ns) + (int)(blockIdx.x & 7u);
+        sl = j % ns;
+        if (b >= g.nbins) return;
+    }
+    const bool first = sl == 0;
     const int nc = g.nc;
-    const int c_lo = blockIdx.y * slice_cells, c_hi = min(nc, c_lo + slice_cells);
+    const int c_lo = sl * slice_cells, c_hi = min(nc, c_lo + slice_cells);
     const int ncs = c_hi - c_lo;
     const int g_lo = c_lo / kGroup, ngs = (ncs + kGroup - 1) / kGroup;
     const int lane = threadIdx.x & 63;
@@ -2857,7 +2869,13 @@ int mgp_open(const mgp_config* cfg, int hip_device, mgp_ctx** out) {
     }
     hipDeviceProp_t prop;
     HIP_TRY(hipGetDeviceProperties(&prop, hip_device));
-    ctx->lds_hist_max_cells = (int)std::min<size_t>(prop.sharedMemPerBlock, 96 * 1024) / 4;
+    // the histogram's LDS per workgroup (one workgroup of 8 waves per CU either way): up to
+    // 150 KiB, ~37k cells per slice (C5's 100k cells in 3 slices, not 5 at 96 KiB);
+    // MGP_HIST_LDS_KB / MGP_HIST_XCD=0 for A/B
+    size_t hist_kb = 150;
+    if (const char* e = std::getenv("MGP_HIST_LDS_KB")) hist_kb = (size_t)std::max(16L, std::strtol(e, nullptr, 10));
+    ctx->lds_hist_max_cells = (int)std::min<size_t>(prop.sharedMemPerBlock, hist_kb * 1024) / 4;
+    if (const char* e = std::getenv("MGP_HIST_XCD")) ctx->hist_xcd = std::strtol(e, nullptr, 10) != 0;
     if (const char* e = std::getenv("MGP_HIST_SLICE_CELLS")) {  // tests: force several histogram slices
         const long v = std::strtol(e, nullptr, 10);
         if (v >= kGroup) ctx->hist_slice_cells = (int)(v / kGroup * kGroup);
@@ -3201,10 +3219,13 @@ static int run_segment(mgp_ctx* ctx, const Seg& sg, int slot, int& dup_parts, in
         const int slice = nc <= lds_cells ? nc : lds_cells;
         const int nslices = (nc + slice - 1) / slice;
         const size_t lds = ((size_t)slice + (slice + kGroup - 1) / kGroup) * 4;
-        k_bin_count<<<dim3((unsigned)g.nbins, (unsigned)nslices), kHistBlock, lds, s>>>(
+        const bool xcd = nslices > 1 && ctx->hist_xcd;
+        const dim3 gh = xcd ? dim3((unsigned)(8 * nslices * ((g.nbins + 7) / 8))) : dim3((unsigned)g.nbins, (unsigned)nslices);
+        k_bin_count<<<gh, kHistBlock, lds, s>>>(
             ctx->start.as<int32_t>(), ctx->bc.as<int32_t>(), ctx->flag.as<uint16_t>(), n, g, slice,
             ctx->H.as<uint32_t>(), ctx->PG.as<uint32_t>(), ngroups, ctx->bin_start.as<uint32_t>(),
-            ctx->bin_valid.as<uint32_t>(), ctx->roff_irregular.as<uint32_t>(), st, sg.w0, sg.bhi);
+            ctx->bin_valid.as<uint32_t>(), ctx->roff_irregular.as<uint32_t>(), st, sg.w0, sg.bhi,
+            xcd ? -nslices : nslices);
         HIP_TRY(hipGetLastError());
         // (a rerun on an unchanged resident set takes the cached bits: no copy, no wait)
         if (!sg.stream && !(ctx->bits_cached && !ctx->no_spec)) {

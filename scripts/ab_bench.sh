@@ -4,7 +4,7 @@
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
-BARGS=${BARGS:-"--steps 10 --warmup 2 --no-cpu-baseline --no-check --no-pcie"}
+BARGS=${BARGS:-"--steps 10 --warmup 2 --no-cpu-baseline --no-check --no-pcie --no-device-paired --no-host-pack"}
 for lib in base "$@"; do
     if [ "$lib" = base ]; then unset MGP_LIB; else export MGP_LIB=mgatk2_amd/_lib/$lib; fi
     timeout -k 10 240 python bench.py $BARGS > "gpurun_out/ab_$lib.log" 2>&1 || { echo "$lib failed"; tail -5 "gpurun_out/ab_$lib.log"; exit 1; }

@@ -331,13 +331,16 @@ def test_deep_cell_median_fallback(engine_lib, oracle_lib):
     assert res.depth_max[0] >= 8192
 
 
-@pytest.mark.parametrize("n_cells,slice_cells", [(30_000, None), (5_000, 1024), (3_001, 64)])
-def test_many_cells_sliced_histogram(engine_lib, oracle_lib, monkeypatch, n_cells, slice_cells):
+@pytest.mark.parametrize("n_cells,slice_cells,xcd", [(45_000, None, "1"), (5_000, 1024, "1"), (3_001, 64, "1"),
+                                                    (5_000, 1024, "0")])
+def test_many_cells_sliced_histogram(engine_lib, oracle_lib, monkeypatch, n_cells, slice_cells, xcd):
     """More cells than one LDS histogram holds: the bins are counted in cell
-    slices (30k cells: 2 slices; smaller slices forced with MGP_HIST_SLICE_CELLS:
-    5 and 47, the last one ragged), whose group totals must line up."""
+    slices (45k cells: 2 slices; smaller slices forced with MGP_HIST_SLICE_CELLS:
+    5 and 47, the last one ragged), whose group totals must line up; the slices of
+    a bin dealt to one XCD (default) or in slice-major order (MGP_HIST_XCD=0)."""
     from mgatk2_amd.engine import EngineConfig
 
+    monkeypatch.setenv("MGP_HIST_XCD", xcd)
     if slice_cells:
         monkeypatch.setenv("MGP_HIST_SLICE_CELLS", str(slice_cells))
     soa = _synth(77, 5 * n_cells, n_cells)
