@@ -43,6 +43,32 @@ inline char* put_u64(char* p, uint64_t v) {
     return p;
 }
 
+// decimal text of 0..9999 (the counts and depths of a position are almost always
+// below it): 4 chars + the length, one 8-byte copy per number
+struct Digits {
+    char s[10000][4];
+    uint8_t n[10000];
+    Digits() {
+        for (int v = 0; v < 10000; ++v) {
+            char t[8];
+            const int k = std::snprintf(t, sizeof t, "%d", v);
+            std::memcpy(s[v], t, 4);
+            n[v] = (uint8_t)k;
+        }
+    }
+};
+const Digits& digits() {
+    static const Digits d;
+    return d;
+}
+inline char* put_num(char* p, uint32_t v, const Digits& D) {
+    if (v < 10000u) {
+        std::memcpy(p, D.s[v], 4);
+        return p + D.n[v];
+    }
+    return put_u64(p, v);
+}
+
 struct Text {
     std::vector<char> b;
     size_t n = 0;
@@ -63,23 +89,29 @@ bool gzip_member(const char* src, size_t n, mgp_host::Deflator& dz, std::vector<
 template <class T>
 void format_group(const T* counts, const T* depth, int64_t L, const int64_t* cells, int64_t c0,
                   int64_t c1, const char* const* names, Text* txt) {
+    const Digits& D = digits();
+    std::vector<char> prebuf(256);  // "pos,barcode," of the current position (every line starts with it)
     for (int64_t k = c0; k < c1; ++k) {
         const int64_t c = cells[k];
         const char* bc = names[k];
         const size_t bl = std::strlen(bc);
+        if (prebuf.size() < bl + 32) prebuf.resize(bl + 32);
+        char* const pre = prebuf.data();
         const T* d = depth + (size_t)c * (size_t)L;
         const T* q = counts + (size_t)c * (size_t)L * 8;
         for (int64_t p = 0; p < L; ++p) {
             const uint32_t dp = d[p];
             if (!dp) continue;
-            char* w = txt[0].reserve(bl + 40);
+            char* e0 = put_num(pre, (uint32_t)(p + 1), D);
+            *e0++ = ',';
+            std::memcpy(e0, bc, bl);
+            e0 += bl;
+            *e0++ = ',';
+            const size_t pl = (size_t)(e0 - pre);
+            char* w = txt[0].reserve(pl + 24);
             char* s = w;
-            w = put_u64(w, (uint64_t)p + 1);
-            *w++ = ',';
-            std::memcpy(w, bc, bl);
-            w += bl;
-            *w++ = ',';
-            w = put_u64(w, dp);
+            std::memcpy(w, pre, pl);
+            w = put_num(w + pl, dp, D);
             *w++ = '\n';
             txt[0].n += (size_t)(w - s);
             const T* e = q + (size_t)p * 8;
@@ -87,16 +119,12 @@ void format_group(const T* counts, const T* depth, int64_t L, const int64_t* cel
                 const uint32_t fw = e[2 * b], rv = e[2 * b + 1];
                 if (!(fw | rv)) continue;
                 Text& t = txt[1 + b];
-                char* x = t.reserve(bl + 56);
+                char* x = t.reserve(pl + 48);
                 char* x0 = x;
-                x = put_u64(x, (uint64_t)p + 1);
+                std::memcpy(x, pre, pl);
+                x = put_num(x + pl, fw, D);
                 *x++ = ',';
-                std::memcpy(x, bc, bl);
-                x += bl;
-                *x++ = ',';
-                x = put_u64(x, fw);
-                *x++ = ',';
-                x = put_u64(x, rv);
+                x = put_num(x, rv, D);
                 *x++ = '\n';
                 t.n += (size_t)(x - x0);
             }

@@ -29,6 +29,19 @@ if [[ $STEPS == *e2e4* ]]; then
         || { tail -30 gpurun_out/e2e_c4_$V.log; exit 1; }
     cat gpurun_out/e2e_c4_$V.log
 fi
+if [[ $STEPS == *c5* ]]; then
+    # C5 on one GPU with the PCIe-inclusive leg's batch-size sweep (first = reported)
+    timeout -k 10 900 python -u bench.py --reads 1000000000 --cells 100000 --steps 5 --warmup 1 \
+        --no-cpu-baseline --no-check --no-device-paired --no-host-pack \
+        --batch-reads 16000000,1000000,4000000,64000000 > gpurun_out/bench_c5_$V.log 2>&1 \
+        || { tail -30 gpurun_out/bench_c5_$V.log; exit 1; }
+    tail -c 1500 gpurun_out/bench_c5_$V.log
+fi
+if [[ $STEPS == *ab* ]]; then
+    # A/B of engine variants (AB="libmgpileup_x.so ..."), C4 default bench
+    bash scripts/ab_bench.sh $AB > gpurun_out/ab_$V.txt 2>&1 || { tail -30 gpurun_out/ab_$V.txt; exit 1; }
+    cat gpurun_out/ab_$V.txt
+fi
 if [[ $STEPS == *bench* ]]; then
     timeout -k 10 500 python -u bench.py > gpurun_out/bench_$V.log 2>&1 || { tail -30 gpurun_out/bench_$V.log; exit 1; }
     tail -c 1500 gpurun_out/bench_$V.log
