@@ -107,7 +107,7 @@ class MtDNAPipeline:
         logger.info("Collecting reads from BAM by barcode...")
         reader = BAMReader(str(self.bam_path), self.config, self.barcode_list)
         processor = CellProcessor(self.config, self.output_dir, device=self.device, devices=self.devices)
-        if self.stream and len(self.devices) == 1:
+        if self.stream:
             # one pass: batches decoded on a producer thread, each pushed to the device as
             # it is ready, the windows piled as their reads arrive (readers.py:84-93)
             res = processor.run_stream(reader, len(self.barcode_list))
@@ -176,7 +176,7 @@ class MtDNAPipeline:
         # device still did after it (the rest ran under the decode)
         self.timings = {"bam_ingest": t1 - t0, "engine": t2 - t1, "write": t3 - t2, "report": t4 - t3,
                         "total": t4 - t0, "engine_setup": ta - t1, "engine_run_soa": tb - ta,
-                        "engine_free_inputs": t2 - tb, "streamed": bool(self.stream and len(self.devices) == 1),
+                        "engine_free_inputs": t2 - tb, "streamed": bool(self.stream),
                         **processor.last_timing}
         logger.info("Pipeline complete")
         logger.info("Elapsed time: %.1fs (ingest %.1fs, engine %.1fs, write %.1fs)", t4 - t0, t1 - t0, t2 - t1,

@@ -24,7 +24,7 @@ from queue import Queue
 
 import numpy as np
 
-from ..engine import Engine, EngineResult
+from ..engine import Engine, EngineResult, PinnedBuffer, Rows16
 from ..synth import ReadSoA, pack_reads
 from .pileup import result_dict, simple_reads_to_dicts
 
@@ -110,6 +110,64 @@ class CellProcessor:
         self.last_result = res
         return res
 
+    def _stream_producer(self, reader, n_cells: int, batch_reads: int | None):
+        """The decode side of a streamed run: the native streaming decoder filling a
+        ring of pinned batches on a producer thread. Returns (bam, stream, expected
+        reads, free queue, full queue, thread, times); the consumer takes filled slots
+        from `full` (None at the end, an exception on error) and hands them back
+        through `free` (None stops the producer)."""
+        from ..bam import StreamSlot
+
+        bam, st, expected = reader.open_stream()
+        n_hint = expected if expected > 0 else max(1, os.path.getsize(reader.bam_path) // 30)
+        batch_reads = batch_reads or int(os.environ.get("MGP_STREAM_BATCH", STREAM_BATCH_READS))
+        n_slots = max(2, int(os.environ.get("MGP_STREAM_SLOTS", STREAM_SLOTS)))
+        cap_reads = max(1, min(int(batch_reads), n_hint + 1))
+        cap_payload = cap_reads * 48 + 256 * (n_cells + 1) + (1 << 20)
+        slot_bytes = StreamSlot.nbytes(cap_reads, cap_payload)
+        free: Queue = Queue()
+        full: Queue = Queue()
+        for _ in range(n_slots):
+            pb = PinnedBuffer(slot_bytes)
+            off = [0]
+
+            def alloc(m, dt, pb=pb, off=off):
+                a = pb.array(m, dt, off[0])
+                off[0] = (off[0] + m * np.dtype(dt).itemsize + 63) & ~63
+                return a
+
+            free.put(StreamSlot(cap_reads, cap_payload, alloc))
+        times = {"cap_reads": cap_reads}
+
+        def produce():
+            try:
+                while True:
+                    sl = free.get()
+                    if sl is None:
+                        return
+                    n = st.next_into(sl)
+                    full.put(sl if n else None)
+                    if not n:
+                        times["decode_end"] = time.perf_counter()
+                        return
+            except BaseException as e:  # noqa: BLE001 - handed to the consumer
+                full.put(e)
+
+        producer = threading.Thread(target=produce, name="mgp-bam-decode", daemon=True)
+        producer.start()
+        return bam, st, n_hint, free, full, producer, times
+
+    def _rows_target(self, n_cells: int, eng) -> Rows16 | None:
+        """Pinned 16-bit result rows for all cells (the rows target)."""
+        if n_cells <= 0:
+            return None
+        nw, W = eng.windows()
+        L = self.config.mito_length
+        rb = PinnedBuffer(n_cells * L * 22 + n_cells * nw + 4096)
+        return Rows16(rb.array((n_cells, L, 8), np.uint16, 0), rb.array((n_cells, L, 2), np.uint16, n_cells * L * 16),
+                      rb.array((n_cells, L), np.uint16, n_cells * L * 20),
+                      rb.array((n_cells, nw), np.uint8, n_cells * L * 22), W)
+
     def run_stream(self, reader, n_cells: int, batch_reads: int | None = None, rows_target: bool = True) -> EngineResult:
         """The production path, streamed (readers.py:84-93's one pass, overlapped with
         the device): the native decoder fills a ring of pinned batches on a producer
@@ -118,66 +176,19 @@ class CellProcessor:
         windows it completes, run behind the next batches' decode). With a rows
         target, each window's 16-bit result rows leave the device as soon as it is
         piled, into pinned host memory the writers read. Results are those of a
-        resident run of the same reads (reads a segment cannot serve rerun it)."""
-        from ..bam import StreamSlot
-        from ..engine import PinnedBuffer, Rows16
-
+        resident run of the same reads (reads a segment cannot serve rerun it).
+        Several devices: see :meth:`_run_stream_sharded`."""
+        if len(self.devices) > 1:
+            return self._run_stream_sharded(reader, n_cells, batch_reads, rows_target)
         t0 = time.perf_counter()
-        bam, st, expected = reader.open_stream()
+        bam, st, n_hint, free, full, producer, times = self._stream_producer(reader, n_cells, batch_reads)
         try:
-            n_hint = expected if expected > 0 else max(1, os.path.getsize(reader.bam_path) // 30)
-            batch_reads = batch_reads or int(os.environ.get("MGP_STREAM_BATCH", STREAM_BATCH_READS))
-            n_slots = max(2, int(os.environ.get("MGP_STREAM_SLOTS", STREAM_SLOTS)))
-            cap_reads = max(1, min(int(batch_reads), n_hint + 1))
-            cap_payload = cap_reads * 48 + 256 * (n_cells + 1) + (1 << 20)
             ec = self.config.engine_config(n_cells, reserve_reads=n_hint, reserve_payload=n_hint * 40 + (64 << 20))
             ec.stream = True
-            slot_bytes = StreamSlot.nbytes(cap_reads, cap_payload)
-            slots, bufs = [], []
-            for _ in range(n_slots):
-                pb = PinnedBuffer(slot_bytes)
-                off = [0]
-
-                def alloc(m, dt, pb=pb, off=off):
-                    a = pb.array(m, dt, off[0])
-                    off[0] = (off[0] + m * np.dtype(dt).itemsize + 63) & ~63
-                    return a
-
-                bufs.append(pb)
-                slots.append(StreamSlot(cap_reads, cap_payload, alloc))
-            free: Queue = Queue()
-            full: Queue = Queue()
-            for sl in slots:
-                free.put(sl)
-            times = {}
-
-            def produce():
-                try:
-                    while True:
-                        sl = free.get()
-                        if sl is None:
-                            return
-                        n = st.next_into(sl)
-                        full.put(sl if n else None)
-                        if not n:
-                            times["decode_end"] = time.perf_counter()
-                            return
-                except BaseException as e:  # noqa: BLE001 - handed to the consumer
-                    full.put(e)
-
-            producer = threading.Thread(target=produce, name="mgp-bam-decode", daemon=True)
-            producer.start()
             eng = Engine(ec, device=self.device)
             try:
-                rows = None
-                if rows_target and n_cells > 0:
-                    nw, W = eng.windows()
-                    L = self.config.mito_length
-                    rb = PinnedBuffer(n_cells * L * 22 + n_cells * nw + 4096)
-                    rows = Rows16(rb.array((n_cells, L, 8), np.uint16, 0),
-                                  rb.array((n_cells, L, 2), np.uint16, n_cells * L * 16),
-                                  rb.array((n_cells, L), np.uint16, n_cells * L * 20),
-                                  rb.array((n_cells, nw), np.uint8, n_cells * L * 22), W)
+                rows = self._rows_target(n_cells, eng) if rows_target else None
+                if rows is not None:
                     eng.set_rows16_target(rows)
                 t1 = time.perf_counter()
                 n_batches = 0
@@ -221,8 +232,140 @@ class CellProcessor:
         self.last_timing = {"stream_setup": t1 - t0, "stream_first_batch": times.get("first_batch", t1) - t0,
                             "stream_decode_end": dec_end - t0, "stream_push_end": t2 - t0,
                             "engine_tail": t3 - t2, "engine_fetch": t4 - t3, "engine_close": te - t4,
-                            "stream_batches": n_batches, "stream_batch_reads": cap_reads,
+                            "stream_batches": n_batches, "stream_batch_reads": times["cap_reads"],
                             "streamed_run": bool(last_streamed), "rows_target": rows is not None}
+        self.last_result = res
+        return res
+
+    def _run_stream_sharded(self, reader, n_cells: int, batch_reads: int | None, rows_target: bool) -> EngineResult:
+        """The streamed path over several devices: the cells split
+        into contiguous whitelist ranges of equal size (the reads per cell are not
+        known before the one pass), one streaming context per device, each fed by a
+        thread of its own. This thread routes every decoded batch: the reads of each
+        range, in BAM order, gathered natively into that device's sub-batch (cell ids
+        rebased, records re-placed; reads without a whitelisted barcode go nowhere
+        and count only toward total_reads), while the producer decodes the next.
+        Every device's rows target is its cell range of one pinned result array, so
+        the results need no concatenation; the tallies are summed on the host."""
+        from ..shard import shard_soa
+
+        devs = list(self.devices)
+        D = len(devs)
+        t0 = time.perf_counter()
+        bam, st, n_hint, free, full, producer, times = self._stream_producer(reader, n_cells, batch_reads)
+        bounds = np.linspace(0, n_cells, D + 1).round().astype(np.int64)
+        parts = [(d, int(bounds[d]), int(bounds[d + 1])) for d in range(D) if bounds[d + 1] > bounds[d]]
+        engines, queues, workers, idx_lists, errors = {}, {}, {}, {}, []
+        rows = None
+        try:
+            for d, lo, hi in parts:
+                share = (hi - lo) / max(1, n_cells)
+                ec = self.config.engine_config(hi - lo, reserve_reads=int(n_hint * share * 1.25) + 4096,
+                                               reserve_payload=int(n_hint * share * 1.25) * 40 + (64 << 20))
+                ec.stream = True
+                engines[d] = Engine(ec, device=devs[d])
+            if rows_target and parts:
+                rows = self._rows_target(n_cells, engines[parts[0][0]])
+                for d, lo, hi in parts:
+                    engines[d].set_rows16_target(Rows16(rows.counts[lo:hi], rows.tn5[lo:hi], rows.depth[lo:hi],
+                                                        rows.wide[lo:hi], rows.window_width))
+
+            def work(d):
+                eng = engines[d]
+                try:
+                    while True:
+                        sub = queues[d].get()
+                        if sub is None:
+                            break
+                        eng.push(sub)
+                        eng.copy_wait()
+                    eng.run()
+                    eng.sync()
+                except BaseException as e:  # noqa: BLE001 - re-raised by the router
+                    errors.append(e)
+                    while queues[d].get() is not None:  # drain
+                        pass
+
+            for d, lo, hi in parts:
+                queues[d] = Queue(maxsize=4)
+                idx_lists[d] = []
+                workers[d] = threading.Thread(target=work, args=(d,), name=f"mgp-dev{d}", daemon=True)
+                workers[d].start()
+            t1 = time.perf_counter()
+            n_batches, base = 0, 0
+            try:
+                while True:
+                    item = full.get()
+                    if item is None:
+                        break
+                    if isinstance(item, BaseException):
+                        raise item
+                    if errors:
+                        raise errors[0]
+                    if n_batches == 0:
+                        times["first_batch"] = time.perf_counter()
+                    soa = item.soa()
+                    for d, lo, hi in parts:
+                        sub, idx = shard_soa(soa, lo, hi)
+                        if sub.n:
+                            idx_lists[d].append(idx + base)
+                            queues[d].put(sub)
+                    base += soa.n
+                    free.put(item)  # (the sub-batches are copies)
+                    n_batches += 1
+            finally:
+                for d, _, _ in parts:
+                    queues[d].put(None)
+                for d, _, _ in parts:
+                    workers[d].join()
+            if errors:
+                raise errors[0]
+            t2 = time.perf_counter()
+            L = self.config.mito_length
+            wide = rows is not None and bool(rows.wide.any())
+            res = EngineResult.alloc(n_cells, L, dense=rows is None or wide)
+            st_sum = {k: 0 for k in ("filtered_reads", "n_barcodes", "duplicate_reads_with_length",
+                                     "duplicate_reads_position_only", "cells_passed")}
+            max_span, err = 0, 0
+            for d, lo, hi in parts:
+                r = engines[d].fetch(dense=rows is None or wide)
+                for k in ("n_reads", "any_paired", "passed", "covered", "depth_sum", "depth_max", "median_lo",
+                          "median_hi"):
+                    getattr(res, k)[lo:hi] = getattr(r, k)
+                if rows is None or wide:
+                    for k in ("counts", "tn5", "depth"):
+                        getattr(res, k)[lo:hi] = getattr(r, k)
+                has = r.n_reads > 0
+                if has.any():  # the device's pushed-read index of each cell's first read -> BAM index
+                    idx = np.concatenate(idx_lists[d])
+                    fr = np.full(hi - lo, np.iinfo(np.uint32).max, np.int64)
+                    fr[has] = idx[r.first_read[has].astype(np.int64)]
+                    res.first_read[lo:hi] = fr.astype(np.uint32)
+                else:
+                    res.first_read[lo:hi] = np.iinfo(np.uint32).max
+                res.ref_tally += r.ref_tally
+                for k in st_sum:
+                    st_sum[k] += int(r.stats[k])
+                max_span = max(max_span, int(r.stats["max_span"]))
+                err |= int(r.stats["error_bits"])
+            if rows is not None and not wide:
+                res.counts, res.tn5, res.depth = rows.counts, rows.tn5, rows.depth
+            res.stats = {"total_reads": int(st.records), **st_sum, "max_span": max_span, "error_bits": err}
+            t3 = time.perf_counter()
+            self.last_stats = engines[parts[0][0]].kernel_times() if parts else {}
+        finally:
+            free.put(None)
+            for eng in engines.values():
+                eng.close()
+            producer.join()
+            st.close()
+            bam.close()
+        te = time.perf_counter()
+        self.last_timing = {"stream_setup": t1 - t0, "stream_first_batch": times.get("first_batch", t1) - t0,
+                            "stream_decode_end": times.get("decode_end", t2) - t0, "stream_push_end": t2 - t0,
+                            "engine_tail": 0.0, "engine_fetch": t3 - t2, "engine_close": te - t3,
+                            "stream_batches": n_batches, "stream_batch_reads": times["cap_reads"],
+                            "stream_devices": len(parts), "rows_target": rows is not None}
         self.last_result = res
         return res
 

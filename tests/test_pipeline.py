@@ -360,12 +360,18 @@ def test_insertion_context_matches_loop():
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("stream", ["1", "0"])
 @pytest.mark.parametrize("case", ["synth_run", "synth_bias", "kat_run"])
-def test_pipeline_sharded_gpu(case, tmp_path, engine_lib):
+def test_pipeline_sharded_gpu(case, stream, tmp_path, engine_lib, monkeypatch):
     """Cells sharded over several engine contexts, run concurrently
-    from threads; on a one-GPU box the contexts share device 0. Outputs must equal
-    the reference's, like the single-context run."""
+    from threads; on a one-GPU box the contexts share device 0. Streamed (each
+    decoded batch routed by cell range to the devices' streaming contexts, small
+    batches) and resident. Outputs must equal the reference's, like the
+    single-context run."""
     from mgatk2_amd.pipeline import run_pipeline
+
+    monkeypatch.setenv("MGP_STREAM", stream)
+    monkeypatch.setenv("MGP_STREAM_BATCH", "1500")
 
     g = Golden(case)
     p = g.params
@@ -516,3 +522,91 @@ def test_report_arrays_equal_the_files(tmp_path, oracle_engine, csv):
         np.testing.assert_array_equal(got[k], exp[k], err_msg=k)
     assert got["reference"] == exp["reference"]
     assert report.generate_html_report(tmp_path, "s", arrays=w.report_arrays) is not None
+
+
+class _OracleEngine:
+    """A CPU stand-in for engine.Engine (the oracle behind the same calls) to test
+    the host side of the streamed multi-device path: routing, rows-target views,
+    first-read mapping and the merge."""
+
+    oracle = None
+
+    def __init__(self, cfg, device=0):
+        self.cfg, self.parts, self.rows = cfg, [], None
+
+    def windows(self):
+        return -(-self.cfg.mito_len // 1275), 1275
+
+    def set_rows16_target(self, rows):
+        self.rows = rows
+
+    def push(self, soa):
+        from mgatk2_amd.synth import ReadSoA
+
+        self.parts.append(ReadSoA(*[getattr(soa, k).copy() for k in ("start", "bc", "tlen", "flag", "mapq", "span",
+                                                                     "rec_off", "payload")]))
+
+    def copy_wait(self):
+        pass
+
+    def run(self):
+        from mgatk2_amd.synth import concat_soa
+
+        self.res, _ = self.oracle.oracle_run(self.cfg, concat_soa(self.parts))
+        if self.rows is not None:
+            self.rows.counts[...] = np.minimum(self.res.counts, 65535)
+            self.rows.tn5[...] = np.minimum(self.res.tn5, 65535)
+            self.rows.depth[...] = np.minimum(self.res.depth, 65535)
+            self.rows.wide[...] = 0
+
+    def sync(self):
+        pass
+
+    def fetch(self, dense=True):
+        return self.res
+
+    def kernel_times(self, last_runs=1):
+        return {}
+
+    def close(self):
+        pass
+
+
+@pytest.mark.parametrize("n_dev", [2, 3, 7])
+def test_stream_sharded_routing_host(n_dev, tmp_path, oracle_lib, monkeypatch):
+    """The streamed multi-device path's host side (CellProcessor._run_stream_sharded:
+    batches routed by cell range, per-device rows targets as views of one array, the
+    first reads mapped back to BAM indices, tallies and stats merged), with the oracle
+    standing in for each device's engine: every output equals the reference's."""
+    from mgatk2_amd.engine import PinnedBuffer  # noqa: F401 - (host memory in this stand-in)
+    from mgatk2_amd.processing import processors
+    from mgatk2_amd.pipeline import run_pipeline
+
+    class HostBuf:
+        def __init__(self, nbytes):
+            self.buf = np.zeros(int(nbytes) + 64, np.uint8)
+
+        def array(self, shape, dtype, offset=0):
+            dt = np.dtype(dtype)
+            shape = (int(shape),) if np.ndim(shape) == 0 else tuple(int(x) for x in shape)
+            n = int(np.prod(shape)) * dt.itemsize
+            return self.buf[offset:offset + n].view(dt).reshape(shape)
+
+    _OracleEngine.oracle = oracle_lib
+    monkeypatch.setattr(processors, "Engine", _OracleEngine)
+    monkeypatch.setattr(processors, "PinnedBuffer", HostBuf)
+    monkeypatch.setenv("MGP_STREAM_BATCH", "997")
+    g = Golden("synth_run")
+    p = g.params
+    bam = tmp_path / "x.bam"
+    soa_to_bam(bam, g.soa, g.whitelist)
+    bfile = tmp_path / "barcodes.tsv"
+    bfile.write_text("".join(b + "\n" for b in g.whitelist))
+    out = tmp_path / "out"
+    ret = run_pipeline(
+        str(bam), str(bfile), str(out), min_baseq=p["min_baseq"], min_mapq=p["min_mapq"],
+        min_reads_per_cell=p["min_reads_per_cell"], max_strand_bias=p["max_strand_bias"],
+        skip_deduplication=p["skip_deduplication"], use_fragment_length_dedup=p["use_fragment_length_dedup"],
+        output_format="txt", devices=list(range(n_dev)),
+    )
+    _check_outputs(g, out, ret)
