@@ -50,7 +50,8 @@ extern "C" {
                               3: synth cell shards, cell-range and 16-bit fetches, streaming runs;
                               4: batches without rec_off / span columns and the rows target (the
                                  round-3 "v3.1" entry points), pushed records checked against
-                                 their batch's payload (MGP_E_INVALID), mgp_copy_wait,
+                                 their batch's payload (MGP_E_INVALID), mgp_copy_wait, batches
+                                 without a start column,
                                  mgp_synth_params.n_rec_off, rows targets with min_reads > 1 */
 
 /* ---- return codes (0 = success) ------------------------------------------ */
@@ -335,7 +336,8 @@ static inline MGP_HD void mgp_unpack32_record(const uint8_t *p, uint8_t *full) {
 
 typedef struct mgp_batch {
     int64_t         n_reads;
-    const int32_t  *start;      /* reference_start                                  */
+    const int32_t  *start;      /* reference_start; NULL: taken from each record on the device
+                                   (every layout holds it; ABI 4)                        */
     const int32_t  *bc;         /* whitelist index of the CB tag, -1 if absent or not whitelisted */
     const int32_t  *tlen;       /* signed template_length                           */
     const uint16_t *flag;       /* BAM flag | MGP_FLAG_NOSEQQUAL                    */

@@ -60,54 +60,69 @@ inline uint32_t rd32(const uint8_t* p) { uint32_t v; std::memcpy(&v, p, 4); retu
 inline int32_t rdi32(const uint8_t* p) { int32_t v; std::memcpy(&v, p, 4); return v; }
 inline uint64_t rd64(const uint8_t* p) { uint64_t v; std::memcpy(&v, p, 8); return v; }
 
-uint64_t fnv1a(const char* s, size_t n) {
-    uint64_t h = 1469598103934665603ull;
-    for (size_t i = 0; i < n; ++i) {
-        h ^= (uint8_t)s[i];
-        h *= 1099511628211ull;
+// barcode hash: 8 bytes per step (a per-byte FNV loop was most of a lookup's time)
+inline uint64_t hash_bytes(const char* s, size_t n) {
+    uint64_t h = 0x9E3779B97F4A7C15ull ^ (uint64_t)n;
+    size_t i = 0;
+    for (; i + 8 <= n; i += 8) {
+        uint64_t w;
+        std::memcpy(&w, s + i, 8);
+        h = (h ^ w) * 0xBF58476D1CE4E5B9ull;
+        h ^= h >> 31;
+    }
+    if (i < n) {
+        uint64_t w = 0;
+        std::memcpy(&w, s + i, n - i);
+        h = (h ^ w) * 0x94D049BB133111EBull;
+        h ^= h >> 29;
     }
     return h;
 }
 
-// open-addressing string -> index table (no allocation per lookup)
+// open-addressing string -> index table (no allocation per lookup): the keys' bytes
+// in one pool, each slot's hash, key offset, length and value side by side
 struct StrTable {
-    std::vector<std::string> keys;
-    std::vector<int32_t> vals;
-    std::vector<int64_t> slot;  // index into keys, -1 = empty
-    std::vector<uint64_t> hash;
+    struct Slot {
+        uint64_t hash;
+        uint32_t off, len;
+        int32_t val, used;
+    };
+    std::vector<char> pool;
+    std::vector<Slot> slots;
+    std::vector<int32_t> vals;  // the values (for n_keys)
     uint64_t mask = 0;
     void build(const std::vector<std::string>& k, const std::vector<int32_t>& v) {
         size_t cap = 16;
         while (cap < k.size() * 2 + 1) cap <<= 1;
-        slot.assign(cap, -1);
-        hash.assign(cap, 0);
+        slots.assign(cap, Slot{0, 0, 0, -1, 0});
         mask = cap - 1;
-        keys.clear();
+        pool.clear();
         vals.clear();
         for (size_t i = 0; i < k.size(); ++i) put(k[i], v[i]);
     }
     void put(const std::string& key, int32_t v) {
-        const uint64_t h = fnv1a(key.data(), key.size());
+        const uint64_t h = hash_bytes(key.data(), key.size());
         uint64_t s = h & mask;
-        while (slot[s] >= 0) {
-            if (hash[s] == h && keys[slot[s]] == key) {
-                vals[slot[s]] = v;  // last duplicate wins (dict semantics)
+        while (slots[s].used) {
+            Slot& x = slots[s];
+            if (x.hash == h && x.len == key.size() && std::memcmp(pool.data() + x.off, key.data(), key.size()) == 0) {
+                x.val = v;  // last duplicate wins (dict semantics)
+                vals.push_back(v);
                 return;
             }
             s = (s + 1) & mask;
         }
-        slot[s] = (int64_t)keys.size();
-        hash[s] = h;
-        keys.push_back(key);
+        slots[s] = Slot{h, (uint32_t)pool.size(), (uint32_t)key.size(), v, 1};
+        pool.insert(pool.end(), key.begin(), key.end());
         vals.push_back(v);
     }
     int32_t get(const char* p, size_t n) const {
-        if (slot.empty()) return -1;
-        const uint64_t h = fnv1a(p, n);
+        if (slots.empty()) return -1;
+        const uint64_t h = hash_bytes(p, n);
         uint64_t s = h & mask;
-        while (slot[s] >= 0) {
-            const std::string& k = keys[slot[s]];
-            if (hash[s] == h && k.size() == n && std::memcmp(k.data(), p, n) == 0) return vals[slot[s]];
+        while (slots[s].used) {
+            const Slot& x = slots[s];
+            if (x.hash == h && x.len == n && std::memcmp(pool.data() + x.off, p, n) == 0) return x.val;
             s = (s + 1) & mask;
         }
         return -1;

@@ -2625,10 +2625,12 @@ __global__ void k_dense_off(uint64_t* __restrict__ roff, int64_t n, uint64_t bas
 // MGP_E_INVALID and no kernel reads a record; k_run_init). span != nullptr (a batch
 // without span, ABI v3.1): max(reference span of the CIGAR, l_seq) of each read from its
 // record (include/mgpileup.h, the three layouts), as the BAM decoder computes it (M, D,
-// N, =, X consume the reference).
+// N, =, X consume the reference). start != nullptr (a batch without start, ABI 4): the
+// record's start.
 __global__ void k_check_records(const uint8_t* __restrict__ payload, const uint64_t* __restrict__ roff,
                                 const uint16_t* __restrict__ flag, int64_t n, uint64_t pay_lo, uint64_t pay_hi,
-                                uint32_t* __restrict__ span, uint32_t* __restrict__ bad) {
+                                uint32_t* __restrict__ span, int32_t* __restrict__ start,
+                                uint32_t* __restrict__ bad) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     bool err = false;
     if (i < n) {
@@ -2639,9 +2641,12 @@ __global__ void k_check_records(const uint8_t* __restrict__ payload, const uint6
         if (r < pay_lo || (r & 15ull) != 0ull || r + fixed > pay_hi) {
             err = true;
             if (span) span[i] = 0u;
+            if (start) start[i] = 0;
         } else {
             const uint8_t* rec = payload + r;
             const uint4 h = *reinterpret_cast<const uint4*>(rec);
+            // (a batch without a start column: the record's; every layout holds it)
+            if (start) start[i] = p32 ? (int32_t)(h.x & 0xFFFFu) : (int32_t)h.x;
             const uint32_t lseq = p32 ? ((h.x >> 16) & 0xFFu) : packed ? (h.y & 0xFFu) : h.y;
             const uint32_t ncig = p32 ? ((h.x >> 24) & 7u) : packed ? ((h.y >> 8) & 0x7Fu) : (h.z & 0xFFFFu);
             // a full record's CIGAR at cigar_off (4-byte words, inside the payload)
@@ -3026,8 +3031,7 @@ int mgp_push_batch(mgp_ctx* ctx, const mgp_batch* b) {
     if (!ctx || !b) return set_err(MGP_E_INVALID, "null ctx/batch");
     if (b->n_reads < 0 || b->payload_bytes < 0) return set_err(MGP_E_INVALID, "negative sizes");
     if (b->n_reads == 0) return MGP_OK;
-    if (!b->start || !b->bc || !b->tlen || !b->flag || !b->mapq || !b->payload)
-        return set_err(MGP_E_INVALID, "null batch array");
+    if (!b->bc || !b->tlen || !b->flag || !b->mapq || !b->payload) return set_err(MGP_E_INVALID, "null batch array");
     // rec_off NULL: dense records in BAM order (record i at i x payload_bytes / n_reads);
     // span NULL: the spans come from the records' CIGARs on the device
     const bool dense = b->rec_off == nullptr;
@@ -3042,7 +3046,7 @@ int mgp_push_batch(mgp_ctx* ctx, const mgp_batch* b) {
     const int64_t pay0 = (ctx->pay + 255) & ~int64_t(255);  // keeps the batch's record alignment
     MGP_TRY(ensure_inputs(ctx, n0 + nb, pay0 + b->payload_bytes, true));
     hipStream_t s = ctx->s_copy;
-    HIP_TRY(hipMemcpyAsync(ctx->start.as<int32_t>() + n0, b->start, nb * 4, hipMemcpyHostToDevice, s));
+    if (b->start) HIP_TRY(hipMemcpyAsync(ctx->start.as<int32_t>() + n0, b->start, nb * 4, hipMemcpyHostToDevice, s));
     HIP_TRY(hipMemcpyAsync(ctx->bc.as<int32_t>() + n0, b->bc, nb * 4, hipMemcpyHostToDevice, s));
     HIP_TRY(hipMemcpyAsync(ctx->tlen.as<int32_t>() + n0, b->tlen, nb * 4, hipMemcpyHostToDevice, s));
     HIP_TRY(hipMemcpyAsync(ctx->flag.as<uint16_t>() + n0, b->flag, nb * 2, hipMemcpyHostToDevice, s));
@@ -3062,11 +3066,12 @@ int mgp_push_batch(mgp_ctx* ctx, const mgp_batch* b) {
         k_add_u64<<<blocks_for(nb), kBlock, 0, s>>>(ctx->roff.as<uint64_t>() + n0, nb, (uint64_t)pay0);
         HIP_TRY(hipGetLastError());
     }
-    // every record inside the batch's payload (and, without a span column, its span)
+    // every record inside the batch's payload (and, without a span / start column, its
+    // span / start from the record)
     k_check_records<<<blocks_for(nb), kBlock, 0, s>>>(
         ctx->payload.as<uint8_t>(), ctx->roff.as<uint64_t>() + n0, ctx->flag.as<uint16_t>() + n0, nb, (uint64_t)pay0,
         (uint64_t)(pay0 + b->payload_bytes), b->span ? nullptr : ctx->span.as<uint32_t>() + n0,
-        ctx->order_bad.as<uint32_t>());
+        b->start ? nullptr : ctx->start.as<int32_t>() + n0, ctx->order_bad.as<uint32_t>());
     HIP_TRY(hipGetLastError());
     if (ctx->stream) {
         k_check_order<<<blocks_for(nb), kBlock, 0, s>>>(ctx->start.as<int32_t>(), n0, n0 + nb,
@@ -3081,7 +3086,27 @@ int mgp_push_batch(mgp_ctx* ctx, const mgp_batch* b) {
     ctx->bits_cached = false;
     // streaming: the windows this batch completes go through the hot path now,
     // behind its copies, while the caller pushes the next batch
-    if (ctx->stream) MGP_TRY(stream_segments(ctx, (int64_t)b->start[nb - 1], b->flag[nb - 1]));
+    if (ctx->stream) {
+        // the batch's last start: from its column, or from its last record on the host
+        int64_t last = 0;
+        if (b->start) {
+            last = b->start[nb - 1];
+        } else {
+            const uint64_t ro = dense ? (uint64_t)(nb - 1) * (uint64_t)stride : b->rec_off[nb - 1];
+            const uint16_t f = b->flag[nb - 1];
+            if (ro + 4 <= (uint64_t)b->payload_bytes) {
+                const uint8_t* r = b->payload + ro;
+                if (f & MGP_FLAG_PACK32) {
+                    last = (int64_t)((uint32_t)r[0] | ((uint32_t)r[1] << 8));
+                } else {
+                    int32_t v;
+                    std::memcpy(&v, r, 4);
+                    last = v;
+                }
+            }
+        }
+        MGP_TRY(stream_segments(ctx, last, b->flag[nb - 1]));
+    }
     return MGP_OK;
 }
 

@@ -320,10 +320,11 @@ class Rows16:
 def batch_struct(soa: ReadSoA) -> mgp_batch:
     """The C batch of a ReadSoA. ``span`` and ``rec_off`` may be None (ABI v3.1): the
     spans then come from the records' CIGARs on the device, and the records are dense
-    in BAM order (record i at i x payload bytes / n)."""
+    in BAM order (record i at i x payload bytes / n); ``start`` may be None (ABI 4):
+    taken from each record on the device."""
     for name in ("start", "bc", "tlen", "flag", "mapq", "span", "rec_off", "payload"):
         a = getattr(soa, name)
-        if a is None and name in ("span", "rec_off"):
+        if a is None and name in ("start", "span", "rec_off"):
             continue
         if not a.flags["C_CONTIGUOUS"]:
             raise InvalidInputError(f"batch array {name} must be C-contiguous")

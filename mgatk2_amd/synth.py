@@ -145,7 +145,7 @@ class ReadSoA:
 
     @property
     def n(self) -> int:
-        return int(self.start.shape[0])
+        return int((self.start if self.start is not None else self.bc).shape[0])
 
     @property
     def in_bam_order(self) -> bool:
