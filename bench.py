@@ -505,10 +505,11 @@ def pcie_leg(args, cfg, seed, cdf, ref, shard, device, comm_ranks, barrier, redu
     rb = 32 if p32 is not None else 64  # dense records in BAM order
     eng.synth(seed, args.reads, cdf, ref, read_len=args.read_len, rec_align=64, pack=True, pack32=p32, **shard)
     n, pay = eng.resident()
-    # the producer's columns: start, bc, tlen, flag, mapq. No rec_off (dense records in
-    # BAM order) and no span (taken from the records' CIGARs on the device): ABI v3.1
-    cols = ("start", "bc", "tlen", "flag", "mapq", "payload")
-    col_bytes = n * (4 + 4 + 4 + 2 + 1)
+    # the producer's columns: bc, tlen, flag, mapq. No rec_off (dense records in BAM
+    # order) and no span (taken from the records' CIGARs on the device): ABI v3.1; no
+    # start (taken from the records, which all hold it): ABI 4
+    cols = ("bc", "tlen", "flag", "mapq", "payload")
+    col_bytes = n * (4 + 4 + 2 + 1)
     hbuf = PinnedBuffer(col_bytes + pay + 4096)
     off = [0]
 
@@ -536,7 +537,7 @@ def pcie_leg(args, cfg, seed, cdf, ref, shard, device, comm_ranks, barrier, redu
 
     def batches_for(bs):
         """Batches of bs reads: their columns and their slice of the dense payload."""
-        return [ReadSoA(host.start[a:b], host.bc[a:b], host.tlen[a:b], host.flag[a:b], host.mapq[a:b], None, None,
+        return [ReadSoA(None, host.bc[a:b], host.tlen[a:b], host.flag[a:b], host.mapq[a:b], None, None,
                         host.payload[rb * a:rb * b]) for a, b in ((a, min(n, a + bs)) for a in range(0, n, bs))]
 
     def one(batches, stream):
@@ -577,8 +578,8 @@ def pcie_leg(args, cfg, seed, cdf, ref, shard, device, comm_ranks, barrier, redu
     return {
         "value": best["value"],
         "unit": "reads/s",
-        "what": "pinned host SoA batches (start, bc, tlen, flag, mapq + dense 32-byte records; no rec_off or span "
-                "columns: ABI v3.1) -> H2D (streamed: windows run as their reads arrive, and their 16-bit count rows "
+        "what": "pinned host SoA batches (bc, tlen, flag, mapq + dense 32-byte records; no rec_off or span "
+                "columns: ABI v3.1, no start column: ABI 4, the engine takes them from the records) -> H2D (streamed: windows run as their reads arrive, and their 16-bit count rows "
                 "go back D2H as each window completes) -> run -> every row + per-cell stats in pinned host memory; "
                 "max over ranks",
         "h2d_bytes_rank0": h2d,

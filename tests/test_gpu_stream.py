@@ -366,20 +366,22 @@ def test_repeated_resident_runs_reuse_the_check_bits(engine_lib, oracle_lib):
 # ABI v3.1: batches without rec_off (dense records in BAM order) and without span
 # (the spans from the records' CIGARs on the device)
 # ---------------------------------------------------------------------------
-def _columnless(soa, a, b, stride):
+def _columnless(soa, a, b, stride, no_start=False):
     from mgatk2_amd.synth import ReadSoA
 
-    return ReadSoA(soa.start[a:b], soa.bc[a:b], soa.tlen[a:b], soa.flag[a:b], soa.mapq[a:b], None, None,
-                   np.ascontiguousarray(soa.payload[stride * a:stride * b]))
+    return ReadSoA(None if no_start else soa.start[a:b], soa.bc[a:b], soa.tlen[a:b], soa.flag[a:b], soa.mapq[a:b],
+                   None, None, np.ascontiguousarray(soa.payload[stride * a:stride * b]))
 
 
+@pytest.mark.parametrize("no_start", [False, True])
 @pytest.mark.parametrize("layout", ["p32", "p64", "full"])
 @pytest.mark.parametrize("streamed", [False, True])
-def test_push_without_offsets_and_spans(engine_lib, layout, streamed):
+def test_push_without_offsets_and_spans(engine_lib, layout, streamed, no_start):
     """The same reads pushed with and without their rec_off / span columns (three
-    batches, resident and streaming): identical results, and the device's spans
-    equal the producer's (max(reference span of the CIGAR, l_seq), the BAM
-    decoder's definition) for every read, whatever its CIGAR."""
+    batches, resident and streaming), and without the start column (ABI 4: the starts
+    from the records): identical results, and the device's spans and starts equal the
+    producer's (span: max(reference span of the CIGAR, l_seq), the BAM decoder's
+    definition) for every read, whatever its CIGAR."""
     from dataclasses import replace
 
     from mgatk2_amd.engine import EngineConfig
@@ -397,11 +399,12 @@ def test_push_without_offsets_and_spans(engine_lib, layout, streamed):
     cuts = [0, soa.n // 3, (2 * soa.n) // 3 + 7, soa.n]
     with engine_lib.Engine(scfg) as eng:
         for a, b in zip(cuts[:-1], cuts[1:]):
-            eng.push(_columnless(soa, a, b, stride))
+            eng.push(_columnless(soa, a, b, stride, no_start))
         got = eng.finish()
-        dev = eng.download_inputs(columns=("span",))
-    assert_same(got, want, f"{layout} streamed={streamed}")
+        dev = eng.download_inputs(columns=("span", "start"))
+    assert_same(got, want, f"{layout} streamed={streamed} no_start={no_start}")
     np.testing.assert_array_equal(dev.span, soa.span)
+    np.testing.assert_array_equal(dev.start, soa.start)
 
 
 def test_push_without_offsets_rejects_ragged_payloads(engine_lib):
