@@ -42,6 +42,11 @@ if [[ $STEPS == *ab* ]]; then
     bash scripts/ab_bench.sh $AB > gpurun_out/ab_$V.txt 2>&1 || { tail -30 gpurun_out/ab_$V.txt; exit 1; }
     cat gpurun_out/ab_$V.txt
 fi
+if [[ $STEPS == *prof* ]]; then
+    # rocprofv3 kernel stats + FETCH/WRITE PMC passes of the default bench (gpu_round3.sh)
+    STEPS=rocprof,pmc bash scripts/gpu_round3.sh > gpurun_out/prof_$V.log 2>&1 || { tail -30 gpurun_out/prof_$V.log; exit 1; }
+    grep "rc=" gpurun_out/prof_$V.log
+fi
 if [[ $STEPS == *bench* ]]; then
     timeout -k 10 500 python -u bench.py > gpurun_out/bench_$V.log 2>&1 || { tail -30 gpurun_out/bench_$V.log; exit 1; }
     tail -c 1500 gpurun_out/bench_$V.log

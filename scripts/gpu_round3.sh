@@ -19,7 +19,7 @@ step() {
     tail -n 3 "gpurun_out/$name.log" | cut -c1-3000
     return $rc
 }
-NB="--no-cpu-baseline --no-check --no-pcie"
+NB="--no-cpu-baseline --no-check --no-pcie --no-device-paired --no-host-pack"
 if [[ $STEPS == *fullsize* ]]; then
     step fullsize 700 python -u -m pytest tests/test_gpu_parity.py -x -v -k "c4 or c5" --timeout 300 \
         --timeout-method thread -p no:cacheprovider || exit $?
