@@ -1368,6 +1368,9 @@ struct Win {
     int w0, wlen, Wp;
 };
 
+#ifndef MGP_ROW_OPAQUE
+#define MGP_ROW_OPAQUE 1
+#endif
 // LDS tile, plane-major: planes 0..3 count A, C, G, T, plane 4 is a trash plane
 // (never read: where the 32-byte path adds the bases it does not count), plane 5
 // counts Tn5 cuts; every u32 packs the forward count in its low 16 bits and the
@@ -1804,7 +1807,14 @@ __device__ __forceinline__ void pile_bases_p32(bool act, int a0, int b0, int a1,
     const int plo = min(e0, e1) + wq_lo, phi = max(e0, e1) + wq_hi - 1;
     const bool guarded = __ballot(plo < -kTileGuard || phi >= kTilePitch - kTileGuard) == 0ull;
     const uint32_t tb = lds_addr(tile);
-    const uint32_t r0 = tb + 4u * (uint32_t)e0, r1 = tb + 4u * (uint32_t)e1;
+    uint32_t r0 = tb + 4u * (uint32_t)e0, r1 = tb + 4u * (uint32_t)e1;
+#if MGP_ROW_OPAQUE
+    // the rows as opaque VGPRs: otherwise the compiler splits the uniform tile base
+    // out of them and keeps tile base + 4 x query offset as one SGPR per offset (50 of
+    // them, spilled to VGPR lanes: a v_readlane + s_nop + v_add3 per base) instead of
+    // folding the query offset into the LDS add's immediate (v_mad_u32_u24 + ds_add)
+    asm volatile("" : "+v"(r0), "+v"(r1));
+#endif
     auto code = [&](int qq) -> uint32_t {
         const int bit = 3 * qq, j = bit >> 5, sh = bit & 31;
         return sh <= 29 ? __builtin_amdgcn_ubfe(cw[j], sh, 3) : (__builtin_amdgcn_alignbit(cw[j + 1], cw[j], sh) & 7u);
