@@ -24,10 +24,12 @@ per-position reduction is one numpy call over the position x cell planes.
 from __future__ import annotations
 
 import base64
+import functools
 import html
 import io
 import logging
 import subprocess
+import threading
 from datetime import datetime
 from pathlib import Path
 
@@ -231,12 +233,30 @@ def _summary(output_dir: Path) -> dict[str, str]:
     return out
 
 
+@functools.lru_cache(maxsize=1)
 def _env() -> str:
     try:
         r = subprocess.run(["pip", "list"], capture_output=True, text=True, timeout=30)
         return r.stdout if r.returncode == 0 else "pip not available"
     except Exception:
         return "pip not available"
+
+
+def prewarm() -> threading.Thread:
+    """Start a daemon thread that pays the report's fixed costs early (the pyplot
+    import and the ``pip list`` of the environment section, ~1.5 s together), so a
+    pipeline can overlap them with the BAM decode and the engine."""
+
+    def work():
+        try:
+            _plt()
+        except ImportError:
+            pass
+        _env()
+
+    t = threading.Thread(target=work, name="mgp-report-prewarm", daemon=True)
+    t.start()
+    return t
 
 
 CSS = """
@@ -322,31 +342,54 @@ def _from_arrays(a: dict) -> dict:
             "reference": a["reference"], "total": a["total"], "tn5_fwd": a["tn5_fwd"], "tn5_rev": a["tn5_rev"]}
 
 
-def generate_html_report(output_dir: Path, sample_name: str = "mgatk2", title: str | None = None,
-                         subtitle: str | None = None, working_directory: str | None = None,
-                         input_dir: str | None = None, arrays: dict | None = None):
-    """scATAC report (singlecell.csv metadata present). ``arrays``: the writer's
-    in-memory sums (the files are then not read back)."""
-    output_dir = Path(output_dir)
-    d = _from_arrays(arrays) if arrays is not None else _load(output_dir, need_tn5=True, need_meta_group=True)
-    if d is None:
-        return None
-    summary = _summary(output_dir)
+def _atac_plots(d: dict):
     ctx = insertion_context(d["tn5_fwd"] + d["tn5_rev"], d["reference"])
     total = d["total"]
     depth_frag = _loglog_depth(total, d["mean_depth"][: total.size] if total.size else total,
                                "Total fragments (log10)") if total.size == d["mean_depth"].size else \
         _placeholder("No data available\n(no fragment totals)")
+    sections = [("chrM coverage", coverage_track(d["coverage"]), ""),
+                ("Tn5 transposition frequency", tn5_track(d["tn5_fwd"], d["tn5_rev"]), ""),
+                ("Tn5 insertion sequence context", insertion_context_plot(ctx),
+                 '<p style="color:#666;font-size:.9em">magenta = AT-rich, blue = GC-rich, purple = mixed</p>')]
+    pair = [("Depth per cell", depth_frag),
+            ("chrM coverage", depth_vs_coverage_plot(d["mean_depth"], d["genome_coverage"]))]
+    return sections, pair
+
+
+def _scrna_plots(d: dict):
+    starts = d["coverage"].sum(axis=1, dtype=np.int64) if d["coverage"].ndim == 2 else \
+        d.get("coverage_sum", d["coverage"])
+    sections = [("chrM coverage", coverage_track(d["coverage"]), ""),
+                ("Read start sites", read_start_track(starts), "")]
+    pair = [("Number of reads", _loglog_depth(d["total_bases"] / 150.0, d["mean_depth"], "Number of reads (log10)")),
+            ("chrM coverage", depth_vs_coverage_plot(d["mean_depth"], d["genome_coverage"]))]
+    return sections, pair
+
+
+def render_plots(arrays: dict, scatac: bool):
+    """The report's figures from the writer's in-memory arrays, before the page is
+    put together: a pipeline renders them while the HDF5 files are still being
+    written (the deflate runs in native code without the GIL)."""
+    d = _from_arrays(arrays)
+    return _atac_plots(d) if scatac else _scrna_plots(d)
+
+
+def generate_html_report(output_dir: Path, sample_name: str = "mgatk2", title: str | None = None,
+                         subtitle: str | None = None, working_directory: str | None = None,
+                         input_dir: str | None = None, arrays: dict | None = None, plots=None):
+    """scATAC report (singlecell.csv metadata present). ``arrays``: the writer's
+    in-memory sums (the files are then not read back); ``plots``: the figures
+    already rendered from them (render_plots)."""
+    output_dir = Path(output_dir)
+    d = _from_arrays(arrays) if arrays is not None else _load(output_dir, need_tn5=True, need_meta_group=True)
+    if d is None:
+        return None
+    summary = _summary(output_dir)
+    sections, pair = plots if plots is not None else _atac_plots(d)
     page = _page(
         _title(title, sample_name, working_directory, input_dir), subtitle or "mgatk2 output analysis",
-        working_directory, _tiles(d, summary),
-        [("chrM coverage", coverage_track(d["coverage"]), ""),
-         ("Tn5 transposition frequency", tn5_track(d["tn5_fwd"], d["tn5_rev"]), ""),
-         ("Tn5 insertion sequence context", insertion_context_plot(ctx),
-          '<p style="color:#666;font-size:.9em">magenta = AT-rich, blue = GC-rich, purple = mixed</p>')],
-        [("Depth per cell", depth_frag),
-         ("chrM coverage", depth_vs_coverage_plot(d["mean_depth"], d["genome_coverage"]))],
-        summary, output_dir)
+        working_directory, _tiles(d, summary), sections, pair, summary, output_dir)
     out = output_dir / "mgatk2_report.html"
     out.write_text(page)
     return out
@@ -354,23 +397,17 @@ def generate_html_report(output_dir: Path, sample_name: str = "mgatk2", title: s
 
 def generate_scrna_html_report(output_dir: Path, sample_name: str = "mgatk2", title: str | None = None,
                                subtitle: str | None = None, working_directory: str | None = None,
-                               input_dir: str | None = None, arrays: dict | None = None):
+                               input_dir: str | None = None, arrays: dict | None = None, plots=None):
     """scRNA report (no singlecell.csv): read-start track and reads-vs-depth plot."""
     output_dir = Path(output_dir)
     d = _from_arrays(arrays) if arrays is not None else _load(output_dir, need_tn5=False, need_meta_group=False)
     if d is None:
         return None
     summary = _summary(output_dir)
-    starts = d["coverage"].sum(axis=1, dtype=np.int64) if d["coverage"].ndim == 2 else \
-        d.get("coverage_sum", d["coverage"])
+    sections, pair = plots if plots is not None else _scrna_plots(d)
     page = _page(
         _title(title, sample_name, working_directory, input_dir), subtitle or "mgatk2 output analysis",
-        working_directory, _tiles(d, summary),
-        [("chrM coverage", coverage_track(d["coverage"]), ""),
-         ("Read start sites", read_start_track(starts), "")],
-        [("Number of reads", _loglog_depth(d["total_bases"] / 150.0, d["mean_depth"], "Number of reads (log10)")),
-         ("chrM coverage", depth_vs_coverage_plot(d["mean_depth"], d["genome_coverage"]))],
-        summary, output_dir)
+        working_directory, _tiles(d, summary), sections, pair, summary, output_dir)
     out = output_dir / "mgatk2_report.html"
     out.write_text(page)
     return out

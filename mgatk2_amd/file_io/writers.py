@@ -211,6 +211,7 @@ class IncrementalHDF5Writer:
         # (write_cell) fills dense column buffers instead
         self._sources: list[tuple] = []
         self._planes = self._tn5 = self._coverage = None
+        self.report_arrays = None
         self._meta = {
             "mean_depth": np.zeros(n, np.float32),
             "median_depth": np.zeros(n, np.float32),
@@ -259,6 +260,7 @@ class IncrementalHDF5Writer:
         """Columns of the given cells (whitelist index of their barcode), vectorised
         over cells; values as in _put (writers.py:154-264)."""
         names = barcodes if barcodes is not None else self.barcodes
+        self.report_arrays = None
         sel, cols = [], []
         for c in np.asarray(cells, dtype=np.int64).tolist():
             bc = names[c]
@@ -325,11 +327,19 @@ class IncrementalHDF5Writer:
                 "genome_coverage": self._meta["genome_coverage"], "total_bases": self._meta["total_bases"],
                 "reference": list(refs), "total": total if total is not None else np.zeros(0)}
 
+    def prepare_report_arrays(self) -> dict:
+        """The report's arrays as finalize leaves them, computed now (from memory) so
+        the figures can be rendered while finalize writes the files."""
+        if self.report_arrays is None:
+            self.report_arrays = self._report_arrays(ref_alleles(self.position_base_counts))
+        return self.report_arrays
+
     def write_cell(self, result: dict):
         """Reference per-cell API (writers.py:136-152)."""
         bc = result["barcode"]
         if bc not in self.barcode_to_idx:
             return
+        self.report_arrays = None
         one = _OneCell(result, self.n_positions)
         if "qc" in result:
             self.cell_stats.append(result["qc"])
@@ -401,7 +411,8 @@ class IncrementalHDF5Writer:
                     logger.warning("Could not store metadata column '%s': %s", col, e)
         counts_file.close()
         meta.close()
-        self.report_arrays = self._report_arrays(refs)
+        if self.report_arrays is None:
+            self.report_arrays = self._report_arrays(refs)
         qc_dir = Path(qc_dir)
         qc_dir.mkdir(exist_ok=True, parents=True)
         if self.cell_stats:

@@ -24,6 +24,7 @@ from __future__ import annotations
 import gc
 import logging
 import os
+import threading
 import time
 from pathlib import Path
 from typing import Any
@@ -46,6 +47,27 @@ def _release_in_background(box: list) -> None:
     import threading
 
     threading.Thread(target=box.clear, name="mgp-free-inputs", daemon=True).start()
+
+
+class _Background:
+    """fn(*args) on a thread; result() joins and returns its value or raises its error."""
+
+    def __init__(self, fn, *args):
+        self._out = self._err = None
+        self._t = threading.Thread(target=self._run, args=(fn, args), name="mgp-report-plots", daemon=True)
+        self._t.start()
+
+    def _run(self, fn, args):
+        try:
+            self._out = fn(*args)
+        except BaseException as e:  # handed to result()
+            self._err = e
+
+    def result(self):
+        self._t.join()
+        if self._err is not None:
+            raise self._err
+        return self._out
 
 
 class MtDNAPipeline:
@@ -102,8 +124,21 @@ class MtDNAPipeline:
                 )
         self.output_dir.mkdir(parents=True, exist_ok=True)
 
+    def _render_plots(self, arrays):
+        from .analysis.report import render_plots
+
+        return render_plots(arrays, scatac=self.barcode_metadata is not None)
+
     def run(self) -> dict[str, Any]:
         t0 = time.time()
+        if self.output_format == "hdf5":
+            # the report's pyplot import and package listing, under the decode
+            try:
+                from .analysis.report import prewarm
+
+                prewarm()
+            except ImportError:  # pragma: no cover
+                pass
         logger.info("Collecting reads from BAM by barcode...")
         reader = BAMReader(str(self.bam_path), self.config, self.barcode_list)
         processor = CellProcessor(self.config, self.output_dir, device=self.device, devices=self.devices)
@@ -151,6 +186,11 @@ class MtDNAPipeline:
 
         logger.info("Cleaning up...")
         qc_dir = self.output_dir / "qc"
+        plots = None
+        if self.output_format == "hdf5" and hasattr(writer, "prepare_report_arrays"):
+            # the report's figures are rendered from memory while finalize deflates and
+            # writes the planes (native code, GIL released)
+            plots = _Background(self._render_plots, writer.prepare_report_arrays())
         writer.finalize(qc_dir)
         meta = QCCalculator(self.config).collect_run_metadata(
             str(self.bam_path), str(self.output_dir), n_cells_input, len(cell_results))
@@ -166,7 +206,7 @@ class MtDNAPipeline:
                 gen = generate_html_report if self.barcode_metadata is not None else generate_scrna_html_report
                 gen(self.output_dir, self.sample_name, title=self.report_title, subtitle=self.report_subtitle,
                     working_directory=self.working_directory, input_dir=str(self.bam_path.parent),
-                    arrays=getattr(writer, "report_arrays", None))
+                    arrays=getattr(writer, "report_arrays", None), plots=plots.result() if plots else None)
             except ImportError:
                 logger.warning("matplotlib not installed, skipping HTML report generation")
             except Exception as e:

@@ -513,7 +513,10 @@ def test_report_arrays_equal_the_files(tmp_path, oracle_engine, csv):
     res = proc.run_soa(soa, nc)
     w = IncrementalHDF5Writer(tmp_path, cfg, names, barcode_metadata=meta)
     proc.write_results(res, names, w)
+    early = w.prepare_report_arrays()  # what the pipeline renders from while finalize runs
+    plots = report.render_plots(early, scatac=csv)
     w.finalize(tmp_path / "qc")
+    assert w.report_arrays is early
     got = report._from_arrays(w.report_arrays)
     exp = report._load(tmp_path, need_tn5=True, need_meta_group=True)
     np.testing.assert_allclose(got["coverage"], exp["coverage"].mean(axis=1), rtol=1e-12)
@@ -522,6 +525,9 @@ def test_report_arrays_equal_the_files(tmp_path, oracle_engine, csv):
         np.testing.assert_array_equal(got[k], exp[k], err_msg=k)
     assert got["reference"] == exp["reference"]
     assert report.generate_html_report(tmp_path, "s", arrays=w.report_arrays) is not None
+    gen = report.generate_html_report if csv else report.generate_scrna_html_report
+    page = gen(tmp_path, "s", arrays=w.report_arrays, plots=plots).read_text()
+    assert page.count("data:image/png;base64,") == (5 if csv else 4)
 
 
 class _OracleEngine:
