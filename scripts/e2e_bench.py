@@ -77,6 +77,10 @@ def main():
             res[key] = {"wall_s": round(wall, 2),
                         **{k: (round(v, 3) if isinstance(v, float) else v) for k, v in p.timings.items()},
                         "reads_per_s_end_to_end": round(args.reads / wall), "cells_passed": ret.get("cells_passed_qc")}
+            if fmt == "hdf5":
+                html = od / "mgatk2_report.html"
+                res[key]["report_html_bytes"] = html.stat().st_size if html.exists() else 0
+                res[key]["report_figures"] = html.read_text().count("data:image/png") if html.exists() else 0
             print(f"[e2e] {key}: {res[key]}", file=sys.stderr, flush=True)
             if fmt == "txt":  # streamed and resident runs must write the same text
                 import gzip

@@ -47,6 +47,12 @@ if [[ $STEPS == *prof* ]]; then
     STEPS=rocprof,pmc bash scripts/gpu_round3.sh > gpurun_out/prof_$V.log 2>&1 || { tail -30 gpurun_out/prof_$V.log; exit 1; }
     grep "rc=" gpurun_out/prof_$V.log
 fi
+if [[ $STEPS == *wr* ]]; then
+    # output stage on the box's host cores, C3-shaped arrays (no GPU)
+    MGP_TXT_PROFILE=1 timeout -k 10 400 python -u scripts/writers_bench.py --cells 5000 \
+        > gpurun_out/writers_c3_$V.json 2> gpurun_out/writers_c3_$V.log || { tail -30 gpurun_out/writers_c3_$V.log; exit 1; }
+    cat gpurun_out/writers_c3_$V.log
+fi
 if [[ $STEPS == *bench* ]]; then
     timeout -k 10 500 python -u bench.py > gpurun_out/bench_$V.log 2>&1 || { tail -30 gpurun_out/bench_$V.log; exit 1; }
     tail -c 1500 gpurun_out/bench_$V.log

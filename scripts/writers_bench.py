@@ -36,16 +36,15 @@ def fake_result(n_cells: int, L: int, depth: float, seed: int, dtype=np.uint16):
         lam = scale[c0:c1, None]
         d = rng.poisson(np.broadcast_to(lam, (c1 - c0, L))).astype(np.int64)
         dep[c0:c1] = d
-        fwd = rng.binomial(d, 0.5)
-        alt = rng.binomial(d, 0.01)
+        # ~1% of a position's depth on one other base; strands split at random
+        alt = np.minimum(d, rng.poisson(np.broadcast_to(lam * 0.01, d.shape)))
         altb = (ref[None, :] + 1 + rng.integers(0, 3, d.shape)) % 4
+        split = rng.random(d.shape, np.float32)
         for b in range(4):
-            main = (ref[None, :] == b)
-            n_b = np.where(main, d - alt, 0) + np.where(altb == b, alt, 0)
-            f_b = np.minimum(n_b, rng.binomial(n_b, 0.5))
+            n_b = np.where(ref[None, :] == b, d - alt, 0) + np.where(altb == b, alt, 0)
+            f_b = (n_b * split).astype(np.int64)
             counts[c0:c1, :, 2 * b] = f_b
             counts[c0:c1, :, 2 * b + 1] = n_b - f_b
-        del fwd
         tn5[c0:c1] = rng.poisson(np.broadcast_to(lam / 25.0, (c1 - c0, L))[..., None].repeat(2, -1))
     covered = (dep > 0).sum(1).astype(np.int64)
     dsum = dep.sum(1, dtype=np.int64)
