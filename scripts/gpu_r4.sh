@@ -42,6 +42,12 @@ if [[ $STEPS == *ab* ]]; then
     bash scripts/ab_bench.sh $AB > gpurun_out/ab_$V.txt 2>&1 || { tail -30 gpurun_out/ab_$V.txt; exit 1; }
     cat gpurun_out/ab_$V.txt
 fi
+if [[ $STEPS == *ab5* ]]; then
+    # the same A/B at C5 on one GPU (AB5="libmgpileup_x.so ..."; MGP_* env variants as ENV:NAME=VALUE)
+    BARGS="--reads 1000000000 --cells 100000 --steps 3 --warmup 1 --no-cpu-baseline --no-check --no-pcie --no-device-paired --no-host-pack" \
+        bash scripts/ab_bench.sh $AB5 > gpurun_out/ab5_$V.txt 2>&1 || { tail -30 gpurun_out/ab5_$V.txt; exit 1; }
+    cat gpurun_out/ab5_$V.txt
+fi
 if [[ $STEPS == *prof* ]]; then
     # rocprofv3 kernel stats + FETCH/WRITE PMC passes of the default bench (gpu_round3.sh)
     STEPS=rocprof,pmc bash scripts/gpu_round3.sh > gpurun_out/prof_$V.log 2>&1 || { tail -30 gpurun_out/prof_$V.log; exit 1; }
