@@ -133,6 +133,7 @@ struct mgp_ctx {
     int lds_hist_max_cells = 0;
     int hist_slice_cells = 0;  // > 0: cap on the histogram's cells per slice (MGP_HIST_SLICE_CELLS)
     bool hist_xcd = true;      // several slices: a bin's slices dealt to one XCD (MGP_HIST_XCD)
+    int hist_narrow = -1;      // 8-bit histogram counters: -1 when 32-bit ones need several slices (MGP_HIST_NARROW)
     bool group_wide = false;   // MGP_GROUP_WIDE=1: 16-byte grouping elements always (tests, A/B)
 
     // resident inputs (BAM order)
@@ -281,7 +282,20 @@ enum { kLayFull = 0, kLayP64 = 1, kLayP32 = 2, kLayAny = 3 };
 // the per-(bin, part, group) counts of pass A. Slice 0 writes the bin's bounds and
 // valid count, and ORs the flag bits of the input check into ck[0].
 constexpr int kHistBlock = MGP_HIST_BLOCK;
-__global__ void __launch_bounds__(kHistBlock) k_bin_count(const int32_t* __restrict__ start,
+// kNarrow: 8-bit counters, four cells per LDS word (a slice of up to ~144k cells in
+// 150 KiB: C5's 100k cells in one pass over the bin instead of three). Every add
+// returns the word it found; an add that finds its byte at 255 wraps it (and carries
+// into the next cell's byte), so the workgroup then counts its cells again with 32-bit
+// counters in sub-slices that fit the same LDS (a cell with more than 255 reads
+// starting in one bin: rare, exact either way).
+#ifndef MGP_HIST_NBLOCK
+#define MGP_HIST_NBLOCK 512  // the 8-bit form's threads per workgroup and reads per thread per step
+#endif
+#ifndef MGP_HIST_NU
+#define MGP_HIST_NU 6
+#endif
+template <bool kNarrow, int kHB = kNarrow ? MGP_HIST_NBLOCK : kHistBlock, int kU = kNarrow ? MGP_HIST_NU : MGP_HIST_U>
+__global__ void __launch_bounds__(kHB) k_bin_count(const int32_t* __restrict__ start,
                                                           const int32_t* __restrict__ bc,
                                                           const uint16_t* __restrict__ flag, int64_t n, Geom g,
                                                           int slice_cells, uint32_t* __restrict__ H,
@@ -289,7 +303,7 @@ __global__ void __launch_bounds__(kHistBlock) k_bin_count(const int32_t* __restr
                                                           uint32_t* __restrict__ bin_lo,
                                                           uint32_t* __restrict__ bin_valid, uint32_t* __restrict__ ck,
                                                           DevStats* st, int seg_w0, int seg_bhi, int nslices) {
-    extern __shared__ uint32_t hist[];  // [slice cells] counts, then cum[slice groups]
+    extern __shared__ uint32_t hist[];  // [slice cells] counts (kNarrow: bytes), then cum[slice groups]
     __shared__ int64_t s_range[2];
     __shared__ uint32_t s_nvalid, s_bits;
     // grid: (bins, slices), or with several slices a 1-D grid that deals the slices of
@@ -308,12 +322,9 @@ __global__ void __launch_bounds__(kHistBlock) k_bin_count(const int32_t* __restr
     const int nc = g.nc;
     const int c_lo = sl * slice_cells, c_hi = min(nc, c_lo + slice_cells);
     const int ncs = c_hi - c_lo;
-    const int g_lo = c_lo / kGroup, ngs = (ncs + kGroup - 1) / kGroup;
     const int lane = threadIdx.x & 63;
-    uint32_t* cum = hist + ncs;
     uint32_t* row = H + (size_t)b * nc;
     if (threadIdx.x < 2) s_range[threadIdx.x] = lower_bound_start(start, n, bin_threshold(b + threadIdx.x, g));
-    for (int c = threadIdx.x; c < ncs; c += blockDim.x) hist[c] = 0;
     if (threadIdx.x == 0) s_nvalid = 0, s_bits = 0;
     __syncthreads();
     // a bin outside the segment counts no read (its bounds are still written: pass A
@@ -332,55 +343,87 @@ __global__ void __launch_bounds__(kHistBlock) k_bin_count(const int32_t* __restr
     bool badbc = false;
     uint32_t bits = 0;  // the input check's flag bits (slice 0)
     uint32_t* pg = PG + (size_t)b * kParts * ngroups;
-    for (int part = 0; part < kParts; ++part) {
-        int64_t lo, hi;
-        part_range(blo, bhi, part, lo, hi);
-        // MGP_HIST_U reads per thread per step, loads issued together (clamped index, no branches)
-        constexpr int kU = MGP_HIST_U;
-        for (int64_t i0 = lo + threadIdx.x; i0 < hi; i0 += kU * kHistBlock) {
-            int cc[kU];
-            uint32_t ff[kU];
+    // count the cells [s_lo, s_hi) over the bin's parts; after each part the per-group
+    // totals are snapshotted (pass A's per-(bin, part, group) counts); the rows go out at
+    // the end. primary: the slice's own pass (the run's counts and check bits are taken
+    // once). Returns whether an 8-bit counter wrapped (workgroup-uniform).
+    auto count = [&](const int s_lo, const int s_hi, const bool narrow, const bool primary) -> bool {
+        const int ns = s_hi - s_lo;
+        const int nw = narrow ? (ns + 3) >> 2 : ns;
+        const int gs_lo = s_lo / kGroup, ngss = (ns + kGroup - 1) / kGroup;
+        uint32_t* cum = hist + nw;
+        auto value = [&](int c) -> uint32_t { return narrow ? (hist[c >> 2] >> (8 * (c & 3))) & 0xFFu : hist[c]; };
+        for (int x = threadIdx.x; x < nw; x += blockDim.x) hist[x] = 0;
+        __syncthreads();
+        bool wrap = false;
+        for (int part = 0; part < kParts; ++part) {
+            int64_t lo, hi;
+            part_range(blo, bhi, part, lo, hi);
+            // kU reads per thread per step, loads issued together (clamped index, no branches)
+            for (int64_t i0 = lo + threadIdx.x; i0 < hi; i0 += kU * kHB) {
+                int cc[kU];
+                uint32_t ff[kU];
 #pragma unroll
-            for (int u = 0; u < kU; ++u) {
-                const int64_t i = i0 + u * kHistBlock;
-                const int64_t j = i < hi ? i : hi - 1;
-                cc[u] = bc[j];
-                ff[u] = flag[j];
-            }
+                for (int u = 0; u < kU; ++u) {
+                    const int64_t i = i0 + u * kHB;
+                    const int64_t j = i < hi ? i : hi - 1;
+                    cc[u] = bc[j];
+                    ff[u] = flag[j];
+                }
+                if (primary) {
 #pragma unroll
-            for (int u = 0; u < kU; ++u) {
-                const uint32_t f = ff[u];
-                if (i0 + u * kHistBlock < hi)
-                    bits |= (f & MGP_FLAG_PAIRED ? CHK_PAIRED : CHK_UNPAIRED) |
-                            (f & MGP_FLAG_NOSEQQUAL ? CHK_NOSEQ : 0u) | layout_bit(f);
-            }
+                    for (int u = 0; u < kU; ++u) {
+                        const uint32_t f = ff[u];
+                        if (i0 + u * kHB < hi)
+                            bits |= (f & MGP_FLAG_PAIRED ? CHK_PAIRED : CHK_UNPAIRED) |
+                                    (f & MGP_FLAG_NOSEQQUAL ? CHK_NOSEQ : 0u) | layout_bit(f);
+                    }
+                }
 #pragma unroll
-            for (int u = 0; u < kU; ++u) {
-                const int64_t i = i0 + u * kHistBlock;
-                const int c = cc[u];
-                const bool in = i < hi;
-                badbc |= in && (c >= nc);
-                if (in && read_valid(c, (uint16_t)ff[u], nc)) {
-                    if (c >= c_lo && c < c_hi) atomicAdd(&hist[c - c_lo], 1u);
-                    ++nvalid;
+                for (int u = 0; u < kU; ++u) {
+                    const int64_t i = i0 + u * kHB;
+                    const int c = cc[u];
+                    const bool in = i < hi;
+                    if (primary) badbc |= in && (c >= nc);
+                    if (in && read_valid(c, (uint16_t)ff[u], nc)) {
+                        if (c >= s_lo && c < s_hi) {
+                            const int x = c - s_lo;
+                            if (narrow) {
+                                const uint32_t sh = 8u * (uint32_t)(x & 3);
+                                const uint32_t old = atomicAdd(&hist[x >> 2], 1u << sh);
+                                wrap |= ((old >> sh) & 0xFFu) == 0xFFu;
+                            } else {
+                                atomicAdd(&hist[x], 1u);
+                            }
+                        }
+                        if (primary) ++nvalid;
+                    }
                 }
             }
-        }
-        __syncthreads();
-        // group totals so far; this part's counts are the growth since the last part
-        // (a group is always handled by the same wave, so `cum` needs no barrier)
-        uint32_t* pgp = pg + (size_t)part * ngroups + g_lo;
-        for (int gi = threadIdx.x >> 6; gi < ngs; gi += kHistBlock / kWave) {
-            const int c = gi * kGroup + lane;
-            const uint32_t h = wave_sum(c < ncs ? hist[c] : 0u);
-            if (lane == 0) {
-                pgp[gi] = h - (part ? cum[gi] : 0u);
-                cum[gi] = h;
+            __syncthreads();
+            // group totals so far; this part's counts are the growth since the last part
+            // (a group is always handled by the same wave, so `cum` needs no barrier)
+            uint32_t* pgp = pg + (size_t)part * ngroups + gs_lo;
+            for (int gi = threadIdx.x >> 6; gi < ngss; gi += kHB / kWave) {
+                const int c = gi * kGroup + lane;
+                const uint32_t h = wave_sum(c < ns ? value(c) : 0u);
+                if (lane == 0) {
+                    pgp[gi] = h - (part ? cum[gi] : 0u);
+                    cum[gi] = h;
+                }
             }
+            __syncthreads();  // the snapshot is complete before the next part counts
         }
-        __syncthreads();  // the snapshot is complete before the next part counts
+        for (int c = threadIdx.x; c < ns; c += blockDim.x) row[s_lo + c] = value(c);
+        return narrow && __syncthreads_or(wrap) != 0;
+    };
+    if (count(c_lo, c_hi, kNarrow, true)) {
+        // a wrapped 8-bit counter: 32-bit counts of the same cells, as many as the LDS
+        // holds at a time (whole groups)
+        const int words = (ncs + 3) / 4 + (ncs + kGroup - 1) / kGroup;
+        const int sub = max(kGroup, words / (kGroup + 1) * kGroup);
+        for (int s0 = c_lo; s0 < c_hi; s0 += sub) count(s0, min(c_hi, s0 + sub), false, false);
     }
-    for (int c = threadIdx.x; c < ncs; c += blockDim.x) row[c_lo + c] = hist[c];
     if (!first) return;
     nvalid = wave_sum(nvalid);
     const bool anybad = __ballot(badbc) != 0ull;
@@ -589,12 +632,14 @@ constexpr int kCompactBins = 32;             // start bins per pass-B step (comp
 #define MGP_GA_DB 1  // pass A: next step's loads in flight during this step (double buffer)
 #endif
 #ifndef MGP_GA_BLOCK
-#define MGP_GA_BLOCK 256  // threads per pass-A workgroup
+#define MGP_GA_BLOCK 512  // threads per pass-A workgroup (r04 A/B: 256 2.06, 768 1.85, 1024 1.85 against 1.78 ms at C4)
 #endif
 constexpr int kGABlock = MGP_GA_BLOCK;
-// kCompact: 8-byte elements (GCompact, below; kOff is then dense or u32)
-template <int kOff, bool kCompact>
-__global__ void __launch_bounds__(kGABlock, MGP_GA_WAVES) k_group_a(int64_t n, const int32_t* __restrict__ start,
+// kCompact: 8-byte elements (GCompact, below; kOff is then dense or u32). kBlk: threads
+// per workgroup (kBlk, or 256 when kBlk's per-wave group counters do not fit the
+// LDS: more than ~140k cells)
+template <int kOff, bool kCompact, int kBlk>
+__global__ void __launch_bounds__(kBlk, MGP_GA_WAVES) k_group_a(int64_t n, const int32_t* __restrict__ start,
                                                     const int32_t* __restrict__ bc, const int32_t* __restrict__ tlen,
                                                     const uint16_t* __restrict__ flag, const uint8_t* __restrict__ mapq,
                                                     const uint64_t* __restrict__ roff,
@@ -667,7 +712,7 @@ __global__ void __launch_bounds__(kGABlock, MGP_GA_WAVES) k_group_a(int64_t n, c
     // each wave owns a contiguous run of kAhead*64 reads per step (BAM order = wave
     // order, then round order); waves claim bucket slots in wave order
     constexpr int kAhead = MGP_GA_AHEAD;
-    constexpr int kStep = kAhead * kGABlock;
+    constexpr int kStep = kAhead * kBlk;
     // per read: barcode, start, tlen, flag | mapq << 16 and the record offset
     // (its 64-byte unit or read index for the dense / u32 sources: 32 bits)
     using OffT = typename std::conditional<kOff == kOffR64 || kSpec, uint64_t, uint32_t>::type;
@@ -727,7 +772,7 @@ __global__ void __launch_bounds__(kGABlock, MGP_GA_WAVES) k_group_a(int64_t n, c
             const int64_t w0 = wave_i0(base0);
             prev0 = start[w0 > 0 ? (w0 <= hi ? w0 - 1 : hi - 1) : 0];
         }
-        uint32_t* my = wc + ((size_t)set * (kGABlock / kWave) + wid) * ngroups;
+        uint32_t* my = wc + ((size_t)set * (kBlk / kWave) + wid) * ngroups;
         for (int x = lane; x < ngroups; x += kWave) my[x] = 0;
         __builtin_amdgcn_wave_barrier();
         bool valid[kAhead];
@@ -780,11 +825,11 @@ __global__ void __launch_bounds__(kGABlock, MGP_GA_WAVES) k_group_a(int64_t n, c
             }
         }
         __syncthreads();
-        for (int gi = threadIdx.x; gi < ngroups; gi += kGABlock) {
+        for (int gi = threadIdx.x; gi < ngroups; gi += kBlk) {
             uint32_t run = gcnt[gi];
 #pragma unroll
-            for (int w = 0; w < kGABlock / kWave; ++w) {
-                uint32_t* r = wc + ((size_t)set * (kGABlock / kWave) + w) * ngroups;
+            for (int w = 0; w < kBlk / kWave; ++w) {
+                uint32_t* r = wc + ((size_t)set * (kBlk / kWave) + w) * ngroups;
                 const uint32_t x = r[gi];
                 r[gi] = run;
                 run += x;
@@ -1460,7 +1505,7 @@ constexpr uint32_t kValid = 0x0116u;   // codes 1, 2, 4, 8 are counted (pileup.p
 // and is loaded together with the header; the per-base loop is unrolled so every
 // register index is static. Other reads take the generic byte-load path.
 #ifndef MGP_ABL
-#define MGP_ABL 0  // ablation switch for experiments: 0 = real kernel
+#define MGP_ABL 0  // ablation switch for experiments: 0 = real kernel (11: flush only zeroes the tile, 12: 11 and no piling)
 #endif
 // The first 128-byte line of a record in registers: header, qual (+16), seq (+80)
 // and CIGAR (+112) of a read of <= 64 bases with <= 4 operations
@@ -1512,7 +1557,7 @@ __device__ __forceinline__ void pile_line(bool has, int lay, const uint8_t* __re
 __device__ __forceinline__ void pile_read(bool has, int lay, const uint8_t* __restrict__ rec, const Win& w,
                                           const PileCfg& pc, uint32_t* tile, uint32_t* t5, uint32_t max_span,
                                           bool& span_err, bool& pk_err) {
-    if (MGP_ABL == 1) return;
+    if (MGP_ABL == 1 || MGP_ABL == 12) return;
     if (MGP_ABL == 3) lay = kLayFull;  // the synthetic reads are in the full layout
     RecLine R;
     load_line(has, lay, rec, w, R);
@@ -1857,7 +1902,7 @@ __device__ __forceinline__ void pile_bases_p32(bool act, int a0, int b0, int a1,
 __device__ __forceinline__ void pile_line(bool has, int lay, const uint8_t* __restrict__ rec, const RecLine& R,
                                           const Win& w, const PileCfg& pc, uint32_t* tile, uint32_t* t5,
                                           uint32_t max_span, bool& span_err, bool& pk_err) {
-    if (MGP_ABL == 1) return;
+    if (MGP_ABL == 1 || MGP_ABL == 12) return;
     const uint4 h = R.h, cv = R.cv;
     const bool packed = lay != kLayFull, p32 = lay == kLayP32;
     // header fields of the three layouts (include/mgpileup.h)
@@ -2182,6 +2227,12 @@ __global__ void __launch_bounds__(kBlock, MGP_PILEUP_WAVES) k_pileup(
 #pragma unroll
         for (int m = 0; m < kMaxPosPerThread; ++m) {
             const int p = threadIdx.x + m * kBlock;
+            if ((MGP_ABL == 11 || MGP_ABL == 12) && p < w.wlen) {  // ablation: the flush only zeroes the tile
+#pragma unroll
+                for (int x = 0; x < 4; ++x) tile[x * kTilePitch + p] = 0u;
+                t5[p] = 0u;
+                continue;
+            }
             if (p < w.wlen) {
                 const size_t P = (size_t)c * L + w.w0 + p;
                 uint32_t v[8], tf, tr;
@@ -2886,11 +2937,13 @@ int mgp_open(const mgp_config* cfg, int hip_device, mgp_ctx** out) {
     HIP_TRY(hipGetDeviceProperties(&prop, hip_device));
     // the histogram's LDS per workgroup (one workgroup of 8 waves per CU either way): up to
     // 150 KiB, ~37k cells per slice (C5's 100k cells in 3 slices, not 5 at 96 KiB);
-    // MGP_HIST_LDS_KB / MGP_HIST_XCD=0 for A/B
+    // MGP_HIST_LDS_KB / MGP_HIST_XCD=0 for A/B. The same budget bounds grouping pass A's
+    // per-group counters (its 512-thread form up to ~140k cells, 256 threads beyond)
     size_t hist_kb = 150;
-    if (const char* e = std::getenv("MGP_HIST_LDS_KB")) hist_kb = (size_t)std::max(16L, std::strtol(e, nullptr, 10));
+    if (const char* e = std::getenv("MGP_HIST_LDS_KB")) hist_kb = (size_t)std::max(4L, std::strtol(e, nullptr, 10));
     ctx->lds_hist_max_cells = (int)std::min<size_t>(prop.sharedMemPerBlock, hist_kb * 1024) / 4;
     if (const char* e = std::getenv("MGP_HIST_XCD")) ctx->hist_xcd = std::strtol(e, nullptr, 10) != 0;
+    if (const char* e = std::getenv("MGP_HIST_NARROW")) ctx->hist_narrow = std::strtol(e, nullptr, 10) != 0;
     if (const char* e = std::getenv("MGP_HIST_SLICE_CELLS")) {  // tests: force several histogram slices
         const long v = std::strtol(e, nullptr, 10);
         if (v >= kGroup) ctx->hist_slice_cells = (int)(v / kGroup * kGroup);
@@ -2900,20 +2953,17 @@ int mgp_open(const mgp_config* cfg, int hip_device, mgp_ctx** out) {
     // best effort: the runtime may already allow it without the attribute
     {
         const int lds_max = (int)prop.sharedMemPerBlock;
-        (void)hipFuncSetAttribute((const void*)k_bin_count, hipFuncAttributeMaxDynamicSharedMemorySize,
+        (void)hipFuncSetAttribute((const void*)k_bin_count<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                   lds_max);
-        (void)hipFuncSetAttribute((const void*)k_group_a<kOffDense, false>,
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, lds_max);
-        (void)hipFuncSetAttribute((const void*)k_group_a<kOffR32, false>,
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, lds_max);
-        (void)hipFuncSetAttribute((const void*)k_group_a<kOffR64, false>,
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, lds_max);
-        (void)hipFuncSetAttribute((const void*)k_group_a<kOffDense, true>,
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, lds_max);
-        (void)hipFuncSetAttribute((const void*)k_group_a<kOffR32, true>,
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, lds_max);
-        (void)hipFuncSetAttribute((const void*)k_group_a<kOffSpec, true>,
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, lds_max);
+        (void)hipFuncSetAttribute((const void*)k_bin_count<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  lds_max);
+        for (const void* f : {(const void*)k_group_a<kOffDense, false, kGABlock>, (const void*)k_group_a<kOffR32, false, kGABlock>,
+                              (const void*)k_group_a<kOffR64, false, kGABlock>, (const void*)k_group_a<kOffDense, true, kGABlock>,
+                              (const void*)k_group_a<kOffR32, true, kGABlock>, (const void*)k_group_a<kOffSpec, true, kGABlock>,
+                              (const void*)k_group_a<kOffDense, false, 256>, (const void*)k_group_a<kOffR32, false, 256>,
+                              (const void*)k_group_a<kOffR64, false, 256>, (const void*)k_group_a<kOffDense, true, 256>,
+                              (const void*)k_group_a<kOffR32, true, 256>, (const void*)k_group_a<kOffSpec, true, 256>})
+            (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, lds_max);
         (void)hipFuncSetAttribute((const void*)k_pileup<kLayAny>, hipFuncAttributeMaxDynamicSharedMemorySize, lds_max);
         (void)hipFuncSetAttribute((const void*)k_pileup<kLayP64>, hipFuncAttributeMaxDynamicSharedMemorySize, lds_max);
         (void)hipFuncSetAttribute((const void*)k_pileup<kLayP32>, hipFuncAttributeMaxDynamicSharedMemorySize, lds_max);
@@ -3249,14 +3299,22 @@ static int run_segment(mgp_ctx* ctx, const Seg& sg, int slot, int& dup_parts, in
     if (n == 0) HIP_TRY(hipMemsetAsync(ctx->bin_start.p, 0, (size_t)(g.nbins + 1) * 4, s));
     if (n > 0) {
         // cells per slice: whole 64-cell groups, counts + group totals within the LDS budget
-        int lds_cells = ctx->lds_hist_max_cells / (kGroup + 1) * kGroup;
+        // (32-bit counters: 65 words per group; 8-bit: 17). 8-bit counters when the cells
+        // need more than one 32-bit slice (MGP_HIST_NARROW=0/1 forces the choice)
+        const int wide_cells = ctx->lds_hist_max_cells / (kGroup + 1) * kGroup;
+        const bool narrow = ctx->hist_narrow >= 0 ? ctx->hist_narrow != 0 : nc > wide_cells;
+        int lds_cells = narrow ? ctx->lds_hist_max_cells / (kGroup / 4 + 1) * kGroup : wide_cells;
         if (ctx->hist_slice_cells > 0) lds_cells = std::min(lds_cells, ctx->hist_slice_cells);
         const int slice = nc <= lds_cells ? nc : lds_cells;
         const int nslices = (nc + slice - 1) / slice;
-        const size_t lds = ((size_t)slice + (slice + kGroup - 1) / kGroup) * 4;
+        const size_t lds_words = narrow ? (size_t)(slice + 3) / 4 + (slice + kGroup - 1) / kGroup
+                                        : (size_t)slice + (slice + kGroup - 1) / kGroup;
+        // (the narrow kernel's 32-bit recount takes at least one group: 65 words)
+        const size_t lds = std::max<size_t>(lds_words, narrow ? kGroup + 1 : 0) * 4;
         const bool xcd = nslices > 1 && ctx->hist_xcd;
         const dim3 gh = xcd ? dim3((unsigned)(8 * nslices * ((g.nbins + 7) / 8))) : dim3((unsigned)g.nbins, (unsigned)nslices);
-        k_bin_count<<<gh, kHistBlock, lds, s>>>(
+        auto kern = narrow ? k_bin_count<true> : k_bin_count<false>;
+        kern<<<gh, narrow ? MGP_HIST_NBLOCK : kHistBlock, lds, s>>>(
             ctx->start.as<int32_t>(), ctx->bc.as<int32_t>(), ctx->flag.as<uint16_t>(), n, g, slice,
             ctx->H.as<uint32_t>(), ctx->PG.as<uint32_t>(), ngroups, ctx->bin_start.as<uint32_t>(),
             ctx->bin_valid.as<uint32_t>(), ctx->roff_irregular.as<uint32_t>(), st, sg.w0, sg.bhi,
@@ -3356,15 +3414,20 @@ static int run_segment(mgp_ctx* ctx, const Seg& sg, int slot, int& dup_parts, in
     if (n > 0) {
         int gbits = 0;
         while (gbits < 31 && (1 << gbits) < ngroups) ++gbits;
-        const size_t a_lds = (size_t)ngroups * (1 + 2 * (kGABlock / kWave)) * 4 + (size_t)((nc + 31) / 32) * 4;
+        auto a_lds_for = [&](int blk) {
+            return (size_t)ngroups * (1 + 2 * (blk / kWave)) * 4 + (size_t)((nc + 31) / 32) * 4;
+        };
+        const bool a_wide = a_lds_for(kGABlock) <= (size_t)ctx->lds_hist_max_cells * 4;
+        const size_t a_lds = a_lds_for(a_wide ? kGABlock : 256);
         if (a_lds > (size_t)ctx->lds_hist_max_cells * 4)
             return set_err(MGP_E_INVALID, "too many cells for one context (grouping LDS)");
         if (gbits > 16) return set_err(MGP_E_INVALID, "too many cells for one context (cell groups)");
         if ((uint64_t)ctx->pay >= (1ull << GM_LCELL_SHIFT))
             return set_err(MGP_E_INVALID, "payload too large (record offsets must stay below 2^50)");
         dim3 ga((unsigned)g.nbins, kParts);
-        auto launch_a = [&](auto kern) {
-            kern<<<ga, kGABlock, a_lds, s>>>(
+        auto launch_a = [&](auto kern_wide, auto kern_256) {
+            auto kern = a_wide ? kern_wide : kern_256;
+            kern<<<ga, a_wide ? kGABlock : 256, a_lds, s>>>(
                 n, ctx->start.as<int32_t>(), ctx->bc.as<int32_t>(), ctx->tlen.as<int32_t>(),
                 ctx->flag.as<uint16_t>(), ctx->mapq.as<uint8_t>(), ctx->roff.as<uint64_t>(),
                 ctx->roff32.as<uint32_t>(), ctx->span.as<uint32_t>(), ctx->bin_start.as<uint32_t>(),
@@ -3373,16 +3436,16 @@ static int run_segment(mgp_ctx* ctx, const Seg& sg, int slot, int& dup_parts, in
                 ctx->first_read.as<uint32_t>(), ctx->roff_irregular.as<uint32_t>(), st, sg.w0, sg.bhi, unit);
         };
         if (spec) {
-            launch_a(k_group_a<kOffSpec, true>);
+            launch_a(k_group_a<kOffSpec, true, kGABlock>, k_group_a<kOffSpec, true, 256>);
         } else if (compact) {
-            if (ctx->roff_mode == kOffDense) launch_a(k_group_a<kOffDense, true>);
-            else launch_a(k_group_a<kOffR32, true>);
+            if (ctx->roff_mode == kOffDense) launch_a(k_group_a<kOffDense, true, kGABlock>, k_group_a<kOffDense, true, 256>);
+            else launch_a(k_group_a<kOffR32, true, kGABlock>, k_group_a<kOffR32, true, 256>);
         } else if (ctx->roff_mode == kOffDense) {
-            launch_a(k_group_a<kOffDense, false>);
+            launch_a(k_group_a<kOffDense, false, kGABlock>, k_group_a<kOffDense, false, 256>);
         } else if (ctx->roff_mode == kOffR32) {
-            launch_a(k_group_a<kOffR32, false>);
+            launch_a(k_group_a<kOffR32, false, kGABlock>, k_group_a<kOffR32, false, 256>);
         } else {
-            launch_a(k_group_a<kOffR64, false>);
+            launch_a(k_group_a<kOffR64, false, kGABlock>, k_group_a<kOffR64, false, 256>);
         }
         HIP_TRY(hipGetLastError());
     }

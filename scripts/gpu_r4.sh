@@ -12,6 +12,12 @@ if [[ $STEPS == *suite* ]]; then
         -p no:cacheprovider > gpurun_out/pytest_gpu_$V.log 2>&1 || { tail -30 gpurun_out/pytest_gpu_$V.log; exit 1; }
     tail -3 gpurun_out/pytest_gpu_$V.log
 fi
+if [[ $STEPS == *sel* ]]; then
+    # a selection of the GPU suite (TK: pytest -k expression)
+    timeout -k 10 600 python -u -m pytest tests -m gpu -x -v -k "$TK" --timeout 300 --timeout-method thread \
+        -p no:cacheprovider > gpurun_out/pytest_sel_$V.log 2>&1 || { tail -30 gpurun_out/pytest_sel_$V.log; exit 1; }
+    tail -3 gpurun_out/pytest_sel_$V.log
+fi
 if [[ $STEPS == *fullsize* ]]; then
     timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py -x -v -k "full_size" --timeout 300 \
         --timeout-method thread -p no:cacheprovider > gpurun_out/pytest_fullsize_$V.log 2>&1 \
@@ -47,6 +53,11 @@ if [[ $STEPS == *ab5* ]]; then
     BARGS="--reads 1000000000 --cells 100000 --steps 3 --warmup 1 --no-cpu-baseline --no-check --no-pcie --no-device-paired --no-host-pack" \
         bash scripts/ab_bench.sh $AB5 > gpurun_out/ab5_$V.txt 2>&1 || { tail -30 gpurun_out/ab5_$V.txt; exit 1; }
     cat gpurun_out/ab5_$V.txt
+fi
+if [[ $STEPS == *sqp* ]]; then
+    # k_pileup SQ counters, default and ablation libraries (SQP="libmgpileup_abl1.so ...")
+    V=$V bash scripts/gpu_sq_pile.sh $SQP > gpurun_out/sqp_$V.log 2>&1 || { tail -30 gpurun_out/sqp_$V.log; exit 1; }
+    cat gpurun_out/sq_pile_$V.txt
 fi
 if [[ $STEPS == *prof* ]]; then
     # rocprofv3 kernel stats + FETCH/WRITE PMC passes of the default bench (gpu_round3.sh)

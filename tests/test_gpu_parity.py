@@ -321,8 +321,12 @@ def test_overflow_bin_and_end_clamp(engine_lib, oracle_lib):
     _both(engine_lib, oracle_lib, reads, 2)
 
 
-def test_deep_cell_median_fallback(engine_lib, oracle_lib):
-    """Depth >= 8192 at some positions: the median leaves the LDS histogram path."""
+@pytest.mark.parametrize("narrow", ["0", "1"])
+def test_deep_cell_median_fallback(engine_lib, oracle_lib, monkeypatch, narrow):
+    """Depth >= 8192 at some positions: the median leaves the LDS histogram path.
+    9000 reads of one cell start in one bin: with 8-bit start-bin counters
+    (MGP_HIST_NARROW=1) they wrap, and the bin is counted again in 32 bits."""
+    monkeypatch.setenv("MGP_HIST_NARROW", narrow)
     reads = [_read(1000, [(0, 30)], "ACGT" * 7 + "AC", 0, tlen=100 + k) for k in range(9000)]
     reads += [_read(2000 + 40 * k, [(0, 30)], "G" * 30, 0, tlen=77) for k in range(200)]
     reads += [_read(3000, [(0, 30)], "T" * 30, 1, tlen=100 + k) for k in range(50)]
@@ -331,16 +335,21 @@ def test_deep_cell_median_fallback(engine_lib, oracle_lib):
     assert res.depth_max[0] >= 8192
 
 
-@pytest.mark.parametrize("n_cells,slice_cells,xcd", [(45_000, None, "1"), (5_000, 1024, "1"), (3_001, 64, "1"),
-                                                    (5_000, 1024, "0")])
-def test_many_cells_sliced_histogram(engine_lib, oracle_lib, monkeypatch, n_cells, slice_cells, xcd):
+@pytest.mark.parametrize("n_cells,slice_cells,xcd,narrow", [
+    (45_000, None, "1", "0"), (45_000, None, "1", None), (5_000, 1024, "1", "0"), (3_001, 64, "1", "0"),
+    (5_000, 1024, "0", "0"), (5_000, 1024, "1", "1"), (3_001, 64, "1", "1"), (3_001, None, "1", "1")])
+def test_many_cells_sliced_histogram(engine_lib, oracle_lib, monkeypatch, n_cells, slice_cells, xcd, narrow):
     """More cells than one LDS histogram holds: the bins are counted in cell
-    slices (45k cells: 2 slices; smaller slices forced with MGP_HIST_SLICE_CELLS:
-    5 and 47, the last one ragged), whose group totals must line up; the slices of
-    a bin dealt to one XCD (default) or in slice-major order (MGP_HIST_XCD=0)."""
+    slices (45k cells with 32-bit counters: 2 slices; smaller slices forced with
+    MGP_HIST_SLICE_CELLS: 5 and 47, the last one ragged), whose group totals must
+    line up; the slices of a bin dealt to one XCD (default) or in slice-major
+    order (MGP_HIST_XCD=0). narrow None: the engine's choice (45k cells: one slice
+    of 8-bit counters); "1"/"0": 8-bit / 32-bit counters forced."""
     from mgatk2_amd.engine import EngineConfig
 
     monkeypatch.setenv("MGP_HIST_XCD", xcd)
+    if narrow is not None:
+        monkeypatch.setenv("MGP_HIST_NARROW", narrow)
     if slice_cells:
         monkeypatch.setenv("MGP_HIST_SLICE_CELLS", str(slice_cells))
     soa = _synth(77, 5 * n_cells, n_cells)
@@ -350,7 +359,24 @@ def test_many_cells_sliced_histogram(engine_lib, oracle_lib, monkeypatch, n_cell
     assert_same(res, exp, f"{n_cells} cells / {slice_cells}")
 
 
-def test_deep_bins_parts_and_direct_buckets(engine_lib, oracle_lib):
+@pytest.mark.parametrize("narrow", ["0", "1"])
+def test_small_lds_budget(engine_lib, oracle_lib, monkeypatch, narrow):
+    """A 4 KiB LDS budget (MGP_HIST_LDS_KB) stands in for a context with more cells
+    than grouping pass A's 512-thread form holds (~140k): 5000 cells then take the
+    256-thread form, and the histogram many slices of 32- or 8-bit counters."""
+    from mgatk2_amd.engine import EngineConfig
+
+    monkeypatch.setenv("MGP_HIST_LDS_KB", "4")
+    monkeypatch.setenv("MGP_HIST_NARROW", narrow)
+    soa = _synth(78, 60_000, 5_000)
+    for mode in ("alignment_and_fragment_length", "none"):
+        cfg = EngineConfig(n_cells=5_000, min_baseq=20, min_mapq=30, dedup_mode=mode, min_reads=1)
+        res = run_engine(engine_lib, cfg, soa)
+        exp, _ = oracle_lib.oracle_run(cfg, soa)
+        assert_same(res, exp, f"small LDS budget {mode}")
+
+
+def test_deep_bins_parts_and_direct_buckets(engine_lib, oracle_lib, monkeypatch):
     """All reads start inside 8 start bins: every bin's parts hold tens of thousands
     of reads (per-part group counts of the histogram feed pass A's slots) and every
     (bin, 64-cell group) bucket exceeds pass B's LDS stage (direct path with the
@@ -360,6 +386,8 @@ def test_deep_bins_parts_and_direct_buckets(engine_lib, oracle_lib):
 
     soa = synth_reads(91, 300_000, 200)
     new = (1000 + soa.start.astype(np.int64) * 64 // 16569).astype(np.int32)  # monotone: order kept
+    # ~190 reads per (cell, bin) with 8-bit histogram counters forced: some wrap
+    monkeypatch.setenv("MGP_HIST_NARROW", "1")
     soa.start[:] = new
     hdr = soa.payload.view(np.uint8)
     for k in range(4):  # record header: int32 start at +0 (include/mgpileup.h)
