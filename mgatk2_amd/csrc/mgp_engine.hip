@@ -134,6 +134,7 @@ struct mgp_ctx {
     int hist_slice_cells = 0;  // > 0: cap on the histogram's cells per slice (MGP_HIST_SLICE_CELLS)
     bool hist_xcd = true;      // several slices: a bin's slices dealt to one XCD (MGP_HIST_XCD)
     int hist_narrow = -1;      // 8-bit histogram counters: -1 when 32-bit ones need several slices (MGP_HIST_NARROW)
+    int hist_bounds = -1;      // bin bounds by k_bin_bounds: -1 when a histogram workgroup fills a CU's LDS (MGP_HIST_BOUNDS)
     bool group_wide = false;   // MGP_GROUP_WIDE=1: 16-byte grouping elements always (tests, A/B)
 
     // resident inputs (BAM order)
@@ -289,10 +290,13 @@ constexpr int kHistBlock = MGP_HIST_BLOCK;
 // counters in sub-slices that fit the same LDS (a cell with more than 255 reads
 // starting in one bin: rare, exact either way).
 #ifndef MGP_HIST_NBLOCK
-#define MGP_HIST_NBLOCK 512  // the 8-bit form's threads per workgroup and reads per thread per step
+// the 8-bit form's threads per workgroup and reads per thread per step: its slices fill a
+// CU's LDS (one workgroup per CU), so more waves and more loads in flight per workgroup
+// (r04 A/B at C5: 512 x 6 4.12 ms, 512 x 12 3.56, 1024 x 6 2.64, 1024 x 12 2.49)
+#define MGP_HIST_NBLOCK 1024
 #endif
 #ifndef MGP_HIST_NU
-#define MGP_HIST_NU 6
+#define MGP_HIST_NU 12
 #endif
 template <bool kNarrow, int kHB = kNarrow ? MGP_HIST_NBLOCK : kHistBlock, int kU = kNarrow ? MGP_HIST_NU : MGP_HIST_U>
 __global__ void __launch_bounds__(kHB) k_bin_count(const int32_t* __restrict__ start,
@@ -302,7 +306,8 @@ __global__ void __launch_bounds__(kHB) k_bin_count(const int32_t* __restrict__ s
                                                           uint32_t* __restrict__ PG, int ngroups,
                                                           uint32_t* __restrict__ bin_lo,
                                                           uint32_t* __restrict__ bin_valid, uint32_t* __restrict__ ck,
-                                                          DevStats* st, int seg_w0, int seg_bhi, int nslices) {
+                                                          DevStats* st, int seg_w0, int seg_bhi, int nslices,
+                                                          int pre_bounds) {
     extern __shared__ uint32_t hist[];  // [slice cells] counts (kNarrow: bytes), then cum[slice groups]
     __shared__ int64_t s_range[2];
     __shared__ uint32_t s_nvalid, s_bits;
@@ -324,7 +329,10 @@ __global__ void __launch_bounds__(kHB) k_bin_count(const int32_t* __restrict__ s
     const int ncs = c_hi - c_lo;
     const int lane = threadIdx.x & 63;
     uint32_t* row = H + (size_t)b * nc;
-    if (threadIdx.x < 2) s_range[threadIdx.x] = lower_bound_start(start, n, bin_threshold(b + threadIdx.x, g));
+    // the bin's bounds: searched here, or (pre_bounds) by k_bin_bounds into bin_lo
+    if (threadIdx.x < 2)
+        s_range[threadIdx.x] = pre_bounds ? (int64_t)bin_lo[b + threadIdx.x]
+                                          : lower_bound_start(start, n, bin_threshold(b + threadIdx.x, g));
     if (threadIdx.x == 0) s_nvalid = 0, s_bits = 0;
     __syncthreads();
     // a bin outside the segment counts no read (its bounds are still written: pass A
@@ -332,8 +340,10 @@ __global__ void __launch_bounds__(kHB) k_bin_count(const int32_t* __restrict__ s
     const bool in_seg = b < seg_bhi && b >= seg_lo_bin(seg_w0, g, st);
     const int64_t blo = s_range[0], bhi = in_seg ? max(s_range[1], blo) : blo;
     if (first && threadIdx.x == 0) {
-        bin_lo[b] = (uint32_t)blo;
-        if (b == g.nbins - 1) bin_lo[g.nbins] = (uint32_t)n;
+        if (!pre_bounds) {
+            bin_lo[b] = (uint32_t)blo;
+            if (b == g.nbins - 1) bin_lo[g.nbins] = (uint32_t)n;
+        }
         // sorted starts give monotone bounds, and monotone bounds partition the reads
         // (each counted once, whatever the order inside); otherwise a read may be in
         // two bins' ranges and the grouping slots would outgrow their buffers
@@ -440,6 +450,14 @@ __global__ void __launch_bounds__(kHB) k_bin_count(const int32_t* __restrict__ s
         bin_valid[b] = s_nvalid;
         if (s_bits && (__atomic_load_n(ck, __ATOMIC_RELAXED) & s_bits) != s_bits) atomicOr(ck, s_bits);
     }
+}
+
+// The start bins' bounds, one thread per bin (bin_lo[b] = first read of bin b,
+// bin_lo[nbins] = n), for histograms whose workgroups would each wait on their own
+// ~30 dependent loads with no other workgroup of the CU to hide them (one per CU).
+__global__ void k_bin_bounds(const int32_t* __restrict__ start, int64_t n, Geom g, uint32_t* __restrict__ bin_lo) {
+    const int b = (int)(blockIdx.x * blockDim.x + threadIdx.x);
+    if (b <= g.nbins) bin_lo[b] = (uint32_t)lower_bound_start(start, n, bin_threshold(b, g));
 }
 
 // Scan step a: column sums over blocks of RB rows, and the cells' totals (zeroed by
@@ -2944,6 +2962,7 @@ int mgp_open(const mgp_config* cfg, int hip_device, mgp_ctx** out) {
     ctx->lds_hist_max_cells = (int)std::min<size_t>(prop.sharedMemPerBlock, hist_kb * 1024) / 4;
     if (const char* e = std::getenv("MGP_HIST_XCD")) ctx->hist_xcd = std::strtol(e, nullptr, 10) != 0;
     if (const char* e = std::getenv("MGP_HIST_NARROW")) ctx->hist_narrow = std::strtol(e, nullptr, 10) != 0;
+    if (const char* e = std::getenv("MGP_HIST_BOUNDS")) ctx->hist_bounds = std::strtol(e, nullptr, 10) != 0;
     if (const char* e = std::getenv("MGP_HIST_SLICE_CELLS")) {  // tests: force several histogram slices
         const long v = std::strtol(e, nullptr, 10);
         if (v >= kGroup) ctx->hist_slice_cells = (int)(v / kGroup * kGroup);
@@ -3313,12 +3332,19 @@ static int run_segment(mgp_ctx* ctx, const Seg& sg, int slot, int& dup_parts, in
         const size_t lds = std::max<size_t>(lds_words, narrow ? kGroup + 1 : 0) * 4;
         const bool xcd = nslices > 1 && ctx->hist_xcd;
         const dim3 gh = xcd ? dim3((unsigned)(8 * nslices * ((g.nbins + 7) / 8))) : dim3((unsigned)g.nbins, (unsigned)nslices);
+        // one workgroup per CU (large slices): the bins' bounds searched up front
+        const bool pre = ctx->hist_bounds >= 0 ? ctx->hist_bounds != 0 : lds > 80 * 1024;
+        if (pre) {
+            k_bin_bounds<<<(g.nbins + 1 + 255) / 256, 256, 0, s>>>(ctx->start.as<int32_t>(), n, g,
+                                                                   ctx->bin_start.as<uint32_t>());
+            HIP_TRY(hipGetLastError());
+        }
         auto kern = narrow ? k_bin_count<true> : k_bin_count<false>;
         kern<<<gh, narrow ? MGP_HIST_NBLOCK : kHistBlock, lds, s>>>(
             ctx->start.as<int32_t>(), ctx->bc.as<int32_t>(), ctx->flag.as<uint16_t>(), n, g, slice,
             ctx->H.as<uint32_t>(), ctx->PG.as<uint32_t>(), ngroups, ctx->bin_start.as<uint32_t>(),
             ctx->bin_valid.as<uint32_t>(), ctx->roff_irregular.as<uint32_t>(), st, sg.w0, sg.bhi,
-            xcd ? -nslices : nslices);
+            xcd ? -nslices : nslices, pre ? 1 : 0);
         HIP_TRY(hipGetLastError());
         // (a rerun on an unchanged resident set takes the cached bits: no copy, no wait)
         if (!sg.stream && !(ctx->bits_cached && !ctx->no_spec)) {

@@ -7,35 +7,37 @@ mkdir -p gpurun_out
 export TMPDIR=/tmp
 V=${V:-r4}
 STEPS=${STEPS:-suite,bench}
-if [[ $STEPS == *suite* ]]; then
+has() { [[ ",$STEPS," == *",$1,"* ]]; }  # exact step names, comma-separated
+AB=${AB:-}; AB5=${AB5:-}; SQP=${SQP:-}; TK=${TK:-gpu}
+if has suite; then
     timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread \
         -p no:cacheprovider > gpurun_out/pytest_gpu_$V.log 2>&1 || { tail -30 gpurun_out/pytest_gpu_$V.log; exit 1; }
     tail -3 gpurun_out/pytest_gpu_$V.log
 fi
-if [[ $STEPS == *sel* ]]; then
+if has sel; then
     # a selection of the GPU suite (TK: pytest -k expression)
     timeout -k 10 600 python -u -m pytest tests -m gpu -x -v -k "$TK" --timeout 300 --timeout-method thread \
         -p no:cacheprovider > gpurun_out/pytest_sel_$V.log 2>&1 || { tail -30 gpurun_out/pytest_sel_$V.log; exit 1; }
     tail -3 gpurun_out/pytest_sel_$V.log
 fi
-if [[ $STEPS == *fullsize* ]]; then
+if has fullsize; then
     timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py -x -v -k "full_size" --timeout 300 \
         --timeout-method thread -p no:cacheprovider > gpurun_out/pytest_fullsize_$V.log 2>&1 \
         || { tail -30 gpurun_out/pytest_fullsize_$V.log; exit 1; }
     tail -3 gpurun_out/pytest_fullsize_$V.log
 fi
-if [[ $STEPS == *e2e3* ]]; then
+if has e2e3; then
     timeout -k 10 600 python -u scripts/e2e_bench.py --reads 50000000 --cells 5000 --out /tmp/mgp_e2e \
         > gpurun_out/e2e_c3_$V.json 2> gpurun_out/e2e_c3_$V.log || { tail -30 gpurun_out/e2e_c3_$V.log; exit 1; }
     cat gpurun_out/e2e_c3_$V.log
 fi
-if [[ $STEPS == *e2e4* ]]; then
+if has e2e4; then
     timeout -k 10 900 python -u scripts/e2e_bench.py --reads 200000000 --cells 10000 --out /tmp/mgp_e2e4 \
         --modes stream --formats txt,hdf5 > gpurun_out/e2e_c4_$V.json 2> gpurun_out/e2e_c4_$V.log \
         || { tail -30 gpurun_out/e2e_c4_$V.log; exit 1; }
     cat gpurun_out/e2e_c4_$V.log
 fi
-if [[ $STEPS == *c5* ]]; then
+if has c5; then
     # C5 on one GPU with the PCIe-inclusive leg's batch-size sweep (first = reported)
     timeout -k 10 900 python -u bench.py --reads 1000000000 --cells 100000 --steps 5 --warmup 1 \
         --no-cpu-baseline --no-check --no-device-paired --no-host-pack \
@@ -43,34 +45,34 @@ if [[ $STEPS == *c5* ]]; then
         || { tail -30 gpurun_out/bench_c5_$V.log; exit 1; }
     tail -c 1500 gpurun_out/bench_c5_$V.log
 fi
-if [[ $STEPS == *ab* ]]; then
+if has ab; then
     # A/B of engine variants (AB="libmgpileup_x.so ..."), C4 default bench
     bash scripts/ab_bench.sh $AB > gpurun_out/ab_$V.txt 2>&1 || { tail -30 gpurun_out/ab_$V.txt; exit 1; }
     cat gpurun_out/ab_$V.txt
 fi
-if [[ $STEPS == *ab5* ]]; then
+if has ab5; then
     # the same A/B at C5 on one GPU (AB5="libmgpileup_x.so ..."; MGP_* env variants as ENV:NAME=VALUE)
     BARGS="--reads 1000000000 --cells 100000 --steps 3 --warmup 1 --no-cpu-baseline --no-check --no-pcie --no-device-paired --no-host-pack" \
         bash scripts/ab_bench.sh $AB5 > gpurun_out/ab5_$V.txt 2>&1 || { tail -30 gpurun_out/ab5_$V.txt; exit 1; }
     cat gpurun_out/ab5_$V.txt
 fi
-if [[ $STEPS == *sqp* ]]; then
+if has sqp; then
     # k_pileup SQ counters, default and ablation libraries (SQP="libmgpileup_abl1.so ...")
     V=$V bash scripts/gpu_sq_pile.sh $SQP > gpurun_out/sqp_$V.log 2>&1 || { tail -30 gpurun_out/sqp_$V.log; exit 1; }
     cat gpurun_out/sq_pile_$V.txt
 fi
-if [[ $STEPS == *prof* ]]; then
+if has prof; then
     # rocprofv3 kernel stats + FETCH/WRITE PMC passes of the default bench (gpu_round3.sh)
     STEPS=rocprof,pmc bash scripts/gpu_round3.sh > gpurun_out/prof_$V.log 2>&1 || { tail -30 gpurun_out/prof_$V.log; exit 1; }
     grep "rc=" gpurun_out/prof_$V.log
 fi
-if [[ $STEPS == *wr* ]]; then
+if has wr; then
     # output stage on the box's host cores, C3-shaped arrays (no GPU)
     MGP_TXT_PROFILE=1 timeout -k 10 400 python -u scripts/writers_bench.py --cells 5000 \
         > gpurun_out/writers_c3_$V.json 2> gpurun_out/writers_c3_$V.log || { tail -30 gpurun_out/writers_c3_$V.log; exit 1; }
     cat gpurun_out/writers_c3_$V.log
 fi
-if [[ $STEPS == *bench* ]]; then
+if has bench; then
     timeout -k 10 500 python -u bench.py > gpurun_out/bench_$V.log 2>&1 || { tail -30 gpurun_out/bench_$V.log; exit 1; }
     tail -c 1500 gpurun_out/bench_$V.log
 fi

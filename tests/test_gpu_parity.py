@@ -376,7 +376,8 @@ def test_small_lds_budget(engine_lib, oracle_lib, monkeypatch, narrow):
         assert_same(res, exp, f"small LDS budget {mode}")
 
 
-def test_deep_bins_parts_and_direct_buckets(engine_lib, oracle_lib, monkeypatch):
+@pytest.mark.parametrize("bounds", ["0", "1"])
+def test_deep_bins_parts_and_direct_buckets(engine_lib, oracle_lib, monkeypatch, bounds):
     """All reads start inside 8 start bins: every bin's parts hold tens of thousands
     of reads (per-part group counts of the histogram feed pass A's slots) and every
     (bin, 64-cell group) bucket exceeds pass B's LDS stage (direct path with the
@@ -386,8 +387,10 @@ def test_deep_bins_parts_and_direct_buckets(engine_lib, oracle_lib, monkeypatch)
 
     soa = synth_reads(91, 300_000, 200)
     new = (1000 + soa.start.astype(np.int64) * 64 // 16569).astype(np.int32)  # monotone: order kept
-    # ~190 reads per (cell, bin) with 8-bit histogram counters forced: some wrap
+    # ~190 reads per (cell, bin) with 8-bit histogram counters forced: some wrap; the
+    # bins' bounds searched per workgroup or up front (k_bin_bounds, MGP_HIST_BOUNDS)
     monkeypatch.setenv("MGP_HIST_NARROW", "1")
+    monkeypatch.setenv("MGP_HIST_BOUNDS", bounds)
     soa.start[:] = new
     hdr = soa.payload.view(np.uint8)
     for k in range(4):  # record header: int32 start at +0 (include/mgpileup.h)
