@@ -13,6 +13,7 @@
 #include <chrono>
 #include <condition_variable>
 #include <deque>
+#include <functional>
 #include <mutex>
 #include <cerrno>
 #include <cstdint>
@@ -209,6 +210,11 @@ struct Chunk {
     size_t cap = 0;
     size_t n = 0;       // inflated bytes at mem + kHead
     bool last = false;  // the end of the file follows
+    // the records that start in this chunk (offsets from mem + kHead), their block sizes
+    // and reference ids, when the prefetch thread walked them (walked)
+    bool walked = false;
+    std::vector<uint32_t> rstart, rsize;
+    std::vector<int32_t> rref;
 };
 
 // Reads and inflates the BGZF stream ahead of the consumer on a thread of its own
@@ -218,7 +224,12 @@ struct Chunk {
 // at most two wait for the consumer.
 class Prefetch {
   public:
-    Prefetch(mgp_bam* bam, uint64_t coff) : bam_(bam), coff_(coff), pool_(std::max(1, bam->n_threads)) {
+    // walk_from >= 0: the prefetch thread also walks the record boundaries of every chunk,
+    // the first record starting walk_from bytes into the first chunk (the stream decode's
+    // serial boundary walk, off the consumer's thread)
+    Prefetch(mgp_bam* bam, uint64_t coff, int64_t walk_from = -1)
+        : bam_(bam), coff_(coff), pool_(std::max(1, bam->n_threads)), walking_(walk_from >= 0),
+          wnext_(walk_from) {
         th_ = std::thread([this] { run(); });
     }
     ~Prefetch() {
@@ -249,7 +260,7 @@ class Prefetch {
         cv_.notify_all();
     }
     const std::string& err() const { return err_; }
-    double t_pread = 0, t_inflate = 0;
+    double t_pread = 0, t_inflate = 0, t_walk = 0;
 
   private:
     static constexpr size_t kMaxBatch = 16u << 20;
@@ -259,6 +270,50 @@ class Prefetch {
         err_ = m;
         failed_ = true;
         cv_.notify_all();
+    }
+    // record boundaries of chunk c, continuing the chain from the chunk before: wnext_ =
+    // where the next record starts in this chunk, or (negative, -k) a record whose 4-byte
+    // size field has its first k bytes (wpart_) at the end of the chunk before. A size
+    // below 32 stops the walk (the consumer then walks itself and reports the record).
+    void walk(Chunk* c) {
+        c->walked = false;
+        c->rstart.clear();
+        c->rsize.clear();
+        c->rref.clear();
+        if (!walking_) return;
+        const uint8_t* d = c->mem.get() + kHead;
+        const size_t n = c->n;
+        int64_t q = wnext_;
+        if (q < 0) {
+            const size_t k = (size_t)(-q);
+            if (n < 4 - k) {  // (a chunk of fewer bytes than the field's rest: not walked)
+                walking_ = false;
+                return;
+            }
+            uint8_t f[4];
+            std::memcpy(f, wpart_, k);
+            std::memcpy(f + k, d, 4 - k);
+            q = (int64_t)(4 + rd32(f)) - (int64_t)k;
+        }
+        while ((uint64_t)q + 4 <= n) {
+            const uint32_t bs = rd32(d + q);
+            if (bs < 32) {
+                walking_ = false;
+                return;
+            }
+            c->rstart.push_back((uint32_t)q);
+            c->rsize.push_back(bs);
+            c->rref.push_back((uint64_t)q + 8 <= n ? rdi32(d + q + 4) : INT32_MIN);  // (split: the consumer reads it)
+            q += 4 + (int64_t)bs;
+        }
+        if ((uint64_t)q < n) {
+            const size_t k = n - (size_t)q;
+            std::memcpy(wpart_, d + q, k);
+            wnext_ = -(int64_t)k;
+        } else {
+            wnext_ = q - (int64_t)n;
+        }
+        c->walked = true;
     }
     void run() {
         size_t want_c = 64u << 10;
@@ -280,6 +335,7 @@ class Prefetch {
             if (!c) return set_fail("out of host memory");
             c->n = 0;
             c->last = false;
+            c->walked = false;
             if (coff_ >= (uint64_t)bam_->file_size) {
                 c->last = last = true;
             } else {
@@ -339,6 +395,9 @@ class Prefetch {
                         t_inflate += now_s() - ti0;
                         if (!ok) return delete c, set_fail("BGZF inflate/CRC error in " + bam_->path);
                         c->n = total;
+                        const double tw0 = now_s();
+                        walk(c);
+                        t_walk += now_s() - tw0;
                         coff_ += p;
                         c->last = last = coff_ >= (uint64_t)bam_->file_size;
                         break;
@@ -363,6 +422,9 @@ class Prefetch {
     mgp_bam* bam_;
     uint64_t coff_;
     mgp_host::Pool pool_;  // (before th_: alive while run() uses it)
+    bool walking_;
+    int64_t wnext_;
+    uint8_t wpart_[4] = {0, 0, 0, 0};
     std::thread th_;
     std::mutex mu_;
     std::condition_variable cv_;
@@ -382,14 +444,33 @@ struct Stream {
     const uint8_t* base = nullptr;
     size_t size = 0, pos = 0;
     bool eof = false;
+    // hold: buffers left behind by advance() stay allocated until release_held() (the
+    // pipelined stream decode still reads records of the chunk before)
+    bool hold = false;
+    std::vector<Chunk*> held;
+    std::vector<std::vector<uint8_t>> held_big;
+    // the record boundaries of [base, base + size) from the prefetch thread's walk (walked):
+    // start offsets from base, block sizes, reference ids
+    bool walked = false;
+    std::vector<size_t> wst;
+    std::vector<uint32_t> wsz;
+    std::vector<int32_t> wref;
 
     ~Stream() {
         if (pf) {  // (the profile counters of mgp_bam_read_ref, on the consumer's thread)
             t_pread += pf->t_pread;
             t_inflate += pf->t_inflate;
         }
+        release_held();
         if (cur && pf) pf->recycle(cur);
         pf.reset();
+    }
+    void release_held() {
+        for (Chunk* c : held)
+            if (pf) pf->recycle(c);
+            else delete c;
+        held.clear();
+        held_big.clear();
     }
     bool fill(size_t need) {
         while (size - pos < need && !eof)
@@ -415,11 +496,32 @@ struct Stream {
             std::memcpy(nb.data() + t, nx->mem.get() + kHead, nx->n);
             big.swap(nb);
             base = big.data();
+            if (hold && !nb.empty()) held_big.push_back(std::move(nb));
         }
         size = t + nx->n;
         pos = 0;
         eof = nx->last;
-        if (cur) pf->recycle(cur);
+        // the buffer's boundaries: the carried record at 0, then the chunk's walked records
+        walked = nx->walked && size >= 8;
+        if (walked) {
+            wst.clear();
+            wsz.clear();
+            wref.clear();
+            if (t) {
+                wst.push_back(0);
+                wsz.push_back(rd32(base));
+                wref.push_back(rdi32(base + 4));
+            }
+            for (size_t i = 0; i < nx->rstart.size(); ++i) {
+                wst.push_back(t + nx->rstart[i]);
+                wsz.push_back(nx->rsize[i]);
+                wref.push_back(nx->rref[i]);
+            }
+        }
+        if (cur) {
+            if (hold) held.push_back(cur);
+            else pf->recycle(cur);
+        }
         cur = nx;
         return true;
     }
@@ -427,14 +529,16 @@ struct Stream {
     size_t avail() const { return size - pos; }
 };
 
-bool stream_at(mgp_bam* bam, uint64_t voff, Stream& st) {
+// walk: the prefetch thread also walks the record boundaries from voff on (Stream::walked)
+bool stream_at(mgp_bam* bam, uint64_t voff, Stream& st, bool walk = false) {
     st.bam = bam;
     st.pf.reset();
     st.cur = nullptr;
     st.base = nullptr;
     st.size = st.pos = 0;
     st.eof = false;
-    st.pf.reset(new Prefetch(bam, voff >> 16));
+    st.walked = false;
+    st.pf.reset(new Prefetch(bam, voff >> 16, walk ? (int64_t)(voff & 0xFFFF) : -1));
     const size_t uoff = voff & 0xFFFF;
     if (uoff) {
         if (!st.fill(uoff)) return false;
@@ -737,6 +841,65 @@ struct Cols {
 // tag, record layout, record bytes), decode() places the chunk's records (pass 1b)
 // and decodes the columns and payload records on the thread pool (pass 2). A batch
 // (begin_batch) may take several chunks (inflated buffers); its payload starts at 0.
+// One chunk's records between the stages of the pipelined stream decode (the
+// decoder's per-chunk arrays, moved out while the next chunk is walked).
+struct ChunkRecs {
+    std::vector<const uint8_t*> recs;
+    std::vector<uint32_t> sizes;
+    std::vector<uint64_t> rsz;
+    std::vector<uint32_t> ncg;
+    std::vector<const uint8_t*> cgp;
+    std::vector<uint8_t> pkd;
+    size_t k0 = 0;
+    bool over = false;  // placement ran past the payload capacity (never: the batch cut bounds it)
+};
+
+// A thread that runs one job at a time (the stream decode's serial placement, beside
+// the pool's passes over the next chunk).
+class Worker {
+  public:
+    Worker() : th_([this] { loop(); }) {}
+    ~Worker() {
+        {
+            std::lock_guard<std::mutex> g(mu_);
+            stop_ = true;
+        }
+        cv_.notify_all();
+        th_.join();
+    }
+    void submit(std::function<void()> f) {
+        std::lock_guard<std::mutex> g(mu_);
+        job_ = std::move(f);
+        busy_ = true;
+        cv_.notify_all();
+    }
+    void wait() {
+        std::unique_lock<std::mutex> g(mu_);
+        cv_.wait(g, [&] { return !busy_; });
+    }
+
+  private:
+    void loop() {
+        std::unique_lock<std::mutex> g(mu_);
+        for (;;) {
+            cv_.wait(g, [&] { return stop_ || (busy_ && job_); });
+            if (stop_) return;
+            std::function<void()> f = std::move(job_);
+            job_ = nullptr;
+            g.unlock();
+            f();
+            g.lock();
+            busy_ = false;
+            cv_.notify_all();
+        }
+    }
+    std::mutex mu_;
+    std::condition_variable cv_;
+    std::function<void()> job_;
+    bool busy_ = false, stop_ = false;
+    std::thread th_;
+};
+
 struct Decoder {
     mgp_bam* b;
     mgp_host::Pool pool;
@@ -1041,6 +1204,106 @@ struct Decoder {
         t_p2 += now_s() - tp2;
         return 0;
     }
+
+    // ---- the pipelined stream decode (paired placement): fields of chunk j on the
+    // pool, then chunk j's placement on a thread of its own while the pool walks,
+    // classifies and decodes the fields of chunk j + 1, then chunk j's records.
+    // fields_stage: the current chunk's columns at k0 (no payload yet)
+    void fields_stage(size_t k0, int64_t gidx0, const Cols& c) {
+        const double t0 = now_s();
+        const size_t m = recs.size();
+        const int tn = (int)std::max<size_t>(1, std::min<size_t>((size_t)pool.size(), m / 4096 + 1));
+        std::vector<int64_t> tags((size_t)tn, 0), firsts((size_t)tn, -1);
+        pool.run(tn, [&](int t) {
+            const size_t lo = m * (size_t)t / (size_t)tn, hi = m * (size_t)(t + 1) / (size_t)tn;
+            for (size_t i = lo; i < hi; ++i)
+                decode_one(c, recs[i], sizes[i], k0 + i, 0, ncg[i], cgp[i], (int)pkd[i], tags[(size_t)t],
+                           firsts[(size_t)t], gidx0 + (int64_t)i, true, false);
+        });
+        for (int t = 0; t < tn; ++t) {
+            n_tag += tags[(size_t)t];
+            if (first_tag < 0 && firsts[(size_t)t] >= 0) first_tag = firsts[(size_t)t];
+        }
+        t_fields += now_s() - t0;
+    }
+    // the current chunk's arrays into q (the decoder's are then empty, capacity kept)
+    void move_chunk(ChunkRecs& q, size_t k0) {
+        q.recs.swap(recs);
+        q.sizes.swap(sizes);
+        q.rsz.swap(rsz);
+        q.ncg.swap(ncg);
+        q.cgp.swap(cgp);
+        q.pkd.swap(pkd);
+        q.k0 = k0;
+        q.over = false;
+        clear_chunk();
+    }
+    // placement of chunk q (serial: the line state carries over in BAM order), then the
+    // free slots of the lines left open are zeroed (a later chunk may fill them; every
+    // other slot gets its record)
+    void place_stage(ChunkRecs& q, const Cols& c, uint64_t cap_payload) {
+        const double t0 = now_s();
+        const uint16_t drop = MGP_FLAG_UNMAPPED | MGP_FLAG_SECONDARY | MGP_FLAG_SUPPLEMENTARY;
+        const size_t m = q.recs.size();
+        for (size_t i = 0; i < m; ++i) {
+            const size_t k = q.k0 + i;
+            if (!q.pkd[i]) {
+                cursor = (cursor + 127) & ~127ull;
+                c.roff[k] = cursor;
+                cursor += (q.rsz[i] + 127) & ~127ull;
+                continue;
+            }
+            const int32_t cc = c.bc[k];
+            size_t key = (cc >= 0 && cc < n_keys && !(c.flag[k] & drop)) ? (size_t)cc : (size_t)n_keys;
+            if (key < (size_t)n_keys && dups.repeat(key, c.start[k], (c.flag[k] & MGP_FLAG_REVERSE) != 0, c.tlen[k]))
+                key = (size_t)n_keys;
+            if (q.pkd[i] == 2) {
+                if (open32[key] == ~0ull) {
+                    cursor = (cursor + 127) & ~127ull;
+                    open32[key] = cursor;
+                    fill32[key] = 0;
+                    cursor += 128;
+                }
+                c.roff[k] = open32[key] + (uint64_t)MGP_PACK32_BYTES * fill32[key];
+                if (++fill32[key] == 4) open32[key] = ~0ull;
+                continue;
+            }
+            if (open[key] != ~0ull) {
+                c.roff[k] = open[key] + MGP_PACK_BYTES;
+                open[key] = ~0ull;
+            } else {
+                cursor = (cursor + 127) & ~127ull;
+                c.roff[k] = open[key] = cursor;
+                cursor += 128;
+            }
+        }
+        if (cursor + 256 > cap_payload) {
+            q.over = true;
+        } else {
+            for (uint64_t o : open)
+                if (o != ~0ull) std::memset(c.pay + o + MGP_PACK_BYTES, 0, MGP_PACK_BYTES);
+            for (size_t key = 0; key < open32.size(); ++key)
+                if (open32[key] != ~0ull)
+                    std::memset(c.pay + open32[key] + (uint64_t)MGP_PACK32_BYTES * fill32[key], 0,
+                                (uint64_t)MGP_PACK32_BYTES * (4u - fill32[key]));
+        }
+        t_place += now_s() - t0;
+    }
+    // chunk q's payload records at their placed offsets, on the pool
+    void records_stage(const ChunkRecs& q, const Cols& c) {
+        const double t0 = now_s();
+        const size_t m = q.recs.size();
+        const int tn = (int)std::max<size_t>(1, std::min<size_t>((size_t)pool.size(), m / 4096 + 1));
+        pool.run(tn, [&](int t) {
+            const size_t lo = m * (size_t)t / (size_t)tn, hi = m * (size_t)(t + 1) / (size_t)tn;
+            int64_t tg = 0, fs = -1;  // (tags are counted by fields_stage)
+            for (size_t i = lo; i < hi; ++i)
+                decode_one(c, q.recs[i], q.sizes[i], q.k0 + i, c.roff[q.k0 + i], q.ncg[i], q.cgp[i], (int)q.pkd[i],
+                           tg, fs, 0, false, true);
+        });
+        t_recs += now_s() - t0;
+    }
+    double t_recs = 0;
 };
 
 // Growable malloc'd array (handed to the caller as is: no final copy).
@@ -1227,7 +1490,42 @@ struct mgp_bam_stream {
     Decoder dec;
     int64_t decoded = 0;  // records handed out so far
     std::vector<size_t> offs;  // the chunk's record offsets in the stream buffer
-    mgp_bam_stream(mgp_bam* b, int rec_align) : bam(b), dec(b, rec_align) {}
+    double t_fill = 0, t_walk = 0, t_class = 0, t_open = 0, t_wait = 0;  // MGP_HOST_PROFILE
+    // the pipelined decode (paired placement; MGP_BAM_PIPELINE=0 turns it off): the
+    // chunk whose placement runs on `placer` and whose records are still to be written
+    bool pipe = true;
+    ChunkRecs pend;
+    bool pending = false;
+    Worker placer;
+    mgp_bam_stream(mgp_bam* b, int rec_align) : bam(b), dec(b, rec_align) {
+        t_open = now_s();
+        if (const char* e = std::getenv("MGP_BAM_PIPELINE")) pipe = std::strtol(e, nullptr, 10) != 0;
+        pipe = pipe && dec.paired;
+        st.hold = pipe;
+    }
+    ~mgp_bam_stream() {
+        if (pending) placer.wait();  // (an abandoned batch: its placement may still run)
+        if (std::getenv("MGP_HOST_PROFILE"))
+            std::fprintf(stderr,
+                         "[mgp_bam_stream] %lld records, %d threads%s: open %.3f s; waiting for inflated chunks %.3f, "
+                         "record walk %.3f (prefetch thread %.3f), classify %.3f, fields %.3f, placement %.3f (waited "
+                         "for %.3f), records %.3f\n",
+                         (long long)decoded, dec.pool.size(), pipe ? ", pipelined" : "", now_s() - t_open, t_fill,
+                         t_walk, st.pf ? st.pf->t_walk : 0.0, t_class, dec.t_fields, dec.t_place, t_wait,
+                         pipe ? dec.t_recs : dec.t_p2 - dec.t_fields - dec.t_place);
+    }
+    // the pending chunk's placement finished, its records written, the buffers it read released
+    bool drain(const Cols& c) {
+        if (!pending) return true;
+        const double t0 = now_s();
+        placer.wait();
+        t_wait += now_s() - t0;
+        pending = false;
+        if (pend.over) return fail("stream batch payload overflow"), false;
+        dec.records_stage(pend, c);
+        st.release_held();
+        return true;
+    }
 };
 
 int64_t mgp_bam_ref_records(mgp_bam* b, int tid) {
@@ -1248,7 +1546,8 @@ int mgp_bam_stream_open(mgp_bam* b, int tid, int rec_align, mgp_bam_stream** out
         voff = b->ref_first_voff[(size_t)tid];
         if (voff == UINT64_MAX) s->done = true;  // no reads on this reference
     }
-    if (!s->done && !stream_at(b, voff, s->st)) return -1;
+    const char* ew = std::getenv("MGP_BAM_WALK_AHEAD");
+    if (!s->done && !stream_at(b, voff, s->st, !ew || std::strtol(ew, nullptr, 10) != 0)) return -1;
     *out = s.release();
     return 0;
 }
@@ -1267,6 +1566,16 @@ int64_t mgp_bam_stream_next(mgp_bam_stream* s, int64_t cap_reads, int64_t cap_pa
         return kn <= (size_t)cap_reads && pay_end + 256 <= (uint64_t)cap_payload;
     };
     auto cols = [&]() { return c; };
+    // an error return leaves no placement running on the caller's batch arrays
+    struct Settle {
+        mgp_bam_stream* s;
+        ~Settle() {
+            if (s->pending) {
+                s->placer.wait();
+                s->pending = false;
+            }
+        }
+    } settle{s};
     dec.begin_batch();
     std::vector<size_t>& offs = s->offs;
     size_t k = 0;
@@ -1274,6 +1583,7 @@ int64_t mgp_bam_stream_next(mgp_bam_stream* s, int64_t cap_reads, int64_t cap_pa
     bool full = false;
     Stream& st = s->st;
     while (!s->done && !full && k < (size_t)cap_reads) {
+        const double tf0 = now_s();
         if (!st.fill(4)) {
             if (!g_err.empty()) return -1;
             if (st.avail() == 0) {  // clean end of file
@@ -1286,14 +1596,44 @@ int64_t mgp_bam_stream_next(mgp_bam_stream* s, int64_t cap_reads, int64_t cap_pa
         if (bs0 < 32) return fail("corrupt BAM record (block_size < 32)");
         if (!st.fill(4 + (size_t)bs0)) return fail(g_err.empty() ? "truncated BAM record body" : g_err);
         const double tp1 = now_s();
+        s->t_fill += tp1 - tf0;
         dec.clear_chunk();
         const uint8_t* base = st.base;
         size_t p = st.pos;
         const size_t end = st.size;
         bool at_end = false;
         offs.clear();
-        // record boundaries (sequential), then pass 1 on the pool, then the batch's cut
-        while (end - p >= 4 && k + dec.recs.size() < (size_t)cap_reads) {
+        // record boundaries (the prefetch thread's walk, or sequential here), then pass 1
+        // on the pool, then the batch's cut
+        size_t wi = 0;
+        bool listed = st.walked;
+        if (listed) {
+            wi = (size_t)(std::lower_bound(st.wst.begin(), st.wst.end(), p) - st.wst.begin());
+            listed = wi < st.wst.size() && st.wst[wi] == p;  // (the chain and the position agree)
+        }
+        while (listed && wi < st.wst.size() && k + dec.recs.size() < (size_t)cap_reads) {
+            p = st.wst[wi];
+            if (end - p < 4) break;
+            const uint32_t bs = st.wsz[wi];
+            if (end - p < 4 + (size_t)bs) break;
+            const int32_t ref = st.wref[wi] != INT32_MIN ? st.wref[wi] : rdi32(base + p + 4);
+            if (ref == s->tid) {
+                s->seen = true;
+                dec.recs.push_back(base + p + 4);
+                dec.sizes.push_back(bs);
+                offs.push_back(p);
+            } else if (s->seen || ref > s->tid || ref < 0) {
+                at_end = true;  // coordinate-sorted: tid's records are contiguous
+                break;
+            }
+            p += 4 + (size_t)bs;
+            ++wi;
+        }
+        while (!listed && end - p >= 4 && k + dec.recs.size() < (size_t)cap_reads) {
+            // the walk is a chain of dependent header loads over bytes other threads just
+            // inflated: keep lines ahead of it in flight
+            __builtin_prefetch(base + p + 1024);
+            __builtin_prefetch(base + p + 2048);
             const uint32_t bs = rd32(base + p);
             if (bs < 32) return fail("corrupt BAM record (block_size < 32)");
             if (end - p < 4 + (size_t)bs) break;
@@ -1309,7 +1649,10 @@ int64_t mgp_bam_stream_next(mgp_bam_stream* s, int64_t cap_reads, int64_t cap_pa
             }
             p += 4 + (size_t)bs;
         }
+        const double tw = now_s();
+        s->t_walk += tw - tp1;
         if (!dec.classify_all()) return -1;
+        s->t_class += now_s() - tw;
         for (size_t i = 0; i < dec.recs.size(); ++i) {
             const uint64_t w = dec.worst(i);
             if (bound + w + slack > (uint64_t)cap_payload) {  // the rest goes to the next batch
@@ -1324,11 +1667,21 @@ int64_t mgp_bam_stream_next(mgp_bam_stream* s, int64_t cap_reads, int64_t cap_pa
         if (at_end) s->done = true;
         dec.t_p1 += now_s() - tp1;
         if (!dec.recs.empty()) {
-            if (dec.decode(k, s->decoded + (int64_t)k, reserve, cols) != 0) return -1;
-            k += dec.recs.size();
+            const size_t m = dec.recs.size();
+            if (s->pipe) {
+                dec.fields_stage(k, s->decoded + (int64_t)k, c);
+                if (!s->drain(c)) return -1;  // the chunk before: placed meanwhile, now its records
+                dec.move_chunk(s->pend, k);
+                s->pending = true;
+                s->placer.submit([s, c, cap_payload] { s->dec.place_stage(s->pend, c, (uint64_t)cap_payload); });
+            } else if (dec.decode(k, s->decoded + (int64_t)k, reserve, cols) != 0) {
+                return -1;
+            }
+            k += m;
         }
         st.pos = p;
     }
+    if (!s->drain(c)) return -1;
     if (k == 0 && !s->done && full) return fail("stream batch capacity too small for one record");
     // >= 256 bytes of zeroed slack after the payload (kernels read up to 128 past a record)
     std::memset(into->payload + dec.cursor, 0, std::min<uint64_t>(256, (uint64_t)cap_payload - dec.cursor));

@@ -27,7 +27,7 @@ if has fullsize; then
     tail -3 gpurun_out/pytest_fullsize_$V.log
 fi
 if has e2e3; then
-    timeout -k 10 600 python -u scripts/e2e_bench.py --reads 50000000 --cells 5000 --out /tmp/mgp_e2e \
+    MGP_HOST_PROFILE=1 timeout -k 10 600 python -u scripts/e2e_bench.py --reads 50000000 --cells 5000 --out /tmp/mgp_e2e \
         > gpurun_out/e2e_c3_$V.json 2> gpurun_out/e2e_c3_$V.log || { tail -30 gpurun_out/e2e_c3_$V.log; exit 1; }
     cat gpurun_out/e2e_c3_$V.log
 fi

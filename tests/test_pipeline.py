@@ -452,6 +452,33 @@ def test_stream_batches_equal_the_whole_decode(tmp_path):
                 assert np.array_equal(cat.payload[a:a + m], whole.payload[b:b + m]), (q, br, i)
 
 
+@pytest.mark.parametrize("batch", [70_000, 130_000])
+def test_stream_pipelined_decode_equals_serial(tmp_path, monkeypatch, batch):
+    """The pipelined streaming decode (a chunk's placement on its own thread while the
+    pool decodes the next chunk; MGP_BAM_PIPELINE) writes exactly the serial decode's
+    batches: columns, offsets and payload bytes, over a BAM of many inflated chunks
+    (records carried across chunk ends) and batch cuts inside chunks."""
+    from mgatk2_amd.bam import write_bam
+    from mgatk2_amd.config import PipelineConfig
+    from mgatk2_amd.processing.readers import BAMReader
+    from mgatk2_amd.synth import barcode_names, synth_reads
+
+    nc = 300
+    soa = synth_reads(17, 300_000, nc)
+    names = barcode_names(nc, 17)
+    bam = tmp_path / "p.bam"
+    write_bam(bam, soa, names)
+    out = {}
+    for pipe in ("0", "1"):
+        monkeypatch.setenv("MGP_BAM_PIPELINE", pipe)
+        reader = BAMReader(str(bam), PipelineConfig(min_baseq=20), names)
+        out[pipe] = stream_batches(reader, nc, batch)
+    assert len(out["0"]) == len(out["1"]) > 1
+    for a, b in zip(out["0"], out["1"]):
+        for k in ("start", "bc", "tlen", "flag", "mapq", "span", "rec_off", "payload"):
+            np.testing.assert_array_equal(getattr(a, k), getattr(b, k), err_msg=k)
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("batch", ["997", "50000"])
 @pytest.mark.parametrize("case", ["synth_run", "synth_tenx", "synth_bias", "kat_run"])
