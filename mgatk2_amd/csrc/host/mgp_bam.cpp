@@ -449,12 +449,12 @@ struct Stream {
     bool hold = false;
     std::vector<Chunk*> held;
     std::vector<std::vector<uint8_t>> held_big;
-    // the record boundaries of [base, base + size) from the prefetch thread's walk (walked):
-    // start offsets from base, block sizes, reference ids
+    // the record boundaries of [base, base + size) from the prefetch thread's walk
+    // (walked): the carried record at 0 when wt > 0, then the chunk's records at wt +
+    // wc->rstart[i] (block sizes wc->rsize, reference ids wc->rref)
     bool walked = false;
-    std::vector<size_t> wst;
-    std::vector<uint32_t> wsz;
-    std::vector<int32_t> wref;
+    const Chunk* wc = nullptr;
+    size_t wt = 0;
 
     ~Stream() {
         if (pf) {  // (the profile counters of mgp_bam_read_ref, on the consumer's thread)
@@ -503,21 +503,8 @@ struct Stream {
         eof = nx->last;
         // the buffer's boundaries: the carried record at 0, then the chunk's walked records
         walked = nx->walked && size >= 8;
-        if (walked) {
-            wst.clear();
-            wsz.clear();
-            wref.clear();
-            if (t) {
-                wst.push_back(0);
-                wsz.push_back(rd32(base));
-                wref.push_back(rdi32(base + 4));
-            }
-            for (size_t i = 0; i < nx->rstart.size(); ++i) {
-                wst.push_back(t + nx->rstart[i]);
-                wsz.push_back(nx->rsize[i]);
-                wref.push_back(nx->rref[i]);
-            }
-        }
+        wc = nx;
+        wt = t;
         if (cur) {
             if (hold) held.push_back(cur);
             else pf->recycle(cur);
@@ -1491,6 +1478,8 @@ struct mgp_bam_stream {
     int64_t decoded = 0;  // records handed out so far
     std::vector<size_t> offs;  // the chunk's record offsets in the stream buffer
     double t_fill = 0, t_walk = 0, t_class = 0, t_open = 0, t_wait = 0;  // MGP_HOST_PROFILE
+    double t_list = 0;
+    int64_t n_listed = 0, n_walked = 0;  // chunks whose boundaries came from the prefetch walk / were walked here
     // the pipelined decode (paired placement; MGP_BAM_PIPELINE=0 turns it off): the
     // chunk whose placement runs on `placer` and whose records are still to be written
     bool pipe = true;
@@ -1508,10 +1497,10 @@ struct mgp_bam_stream {
         if (std::getenv("MGP_HOST_PROFILE"))
             std::fprintf(stderr,
                          "[mgp_bam_stream] %lld records, %d threads%s: open %.3f s; waiting for inflated chunks %.3f, "
-                         "record walk %.3f (prefetch thread %.3f), classify %.3f, fields %.3f, placement %.3f (waited "
-                         "for %.3f), records %.3f\n",
+                         "record walk %.3f (listed %.3f; prefetch thread %.3f; %lld + %lld chunks), classify %.3f, fields %.3f, "
+                         "placement %.3f (waited for %.3f), records %.3f\n",
                          (long long)decoded, dec.pool.size(), pipe ? ", pipelined" : "", now_s() - t_open, t_fill,
-                         t_walk, st.pf ? st.pf->t_walk : 0.0, t_class, dec.t_fields, dec.t_place, t_wait,
+                         t_walk, t_list, st.pf ? st.pf->t_walk : 0.0, (long long)n_listed, (long long)n_walked, t_class, dec.t_fields, dec.t_place, t_wait,
                          pipe ? dec.t_recs : dec.t_p2 - dec.t_fields - dec.t_place);
     }
     // the pending chunk's placement finished, its records written, the buffers it read released
@@ -1605,31 +1594,59 @@ int64_t mgp_bam_stream_next(mgp_bam_stream* s, int64_t cap_reads, int64_t cap_pa
         offs.clear();
         // record boundaries (the prefetch thread's walk, or sequential here), then pass 1
         // on the pool, then the batch's cut
-        size_t wi = 0;
+        // the prefetch walk's list: the carried record (at 0) one by one, then, once the
+        // reads are on tid, whole runs of tid's records taken with bulk copies
         bool listed = st.walked;
-        if (listed) {
-            wi = (size_t)(std::lower_bound(st.wst.begin(), st.wst.end(), p) - st.wst.begin());
-            listed = wi < st.wst.size() && st.wst[wi] == p;  // (the chain and the position agree)
-        }
-        while (listed && wi < st.wst.size() && k + dec.recs.size() < (size_t)cap_reads) {
-            p = st.wst[wi];
-            if (end - p < 4) break;
-            const uint32_t bs = st.wsz[wi];
-            if (end - p < 4 + (size_t)bs) break;
-            const int32_t ref = st.wref[wi] != INT32_MIN ? st.wref[wi] : rdi32(base + p + 4);
-            if (ref == s->tid) {
-                s->seen = true;
-                dec.recs.push_back(base + p + 4);
-                dec.sizes.push_back(bs);
-                offs.push_back(p);
-            } else if (s->seen || ref > s->tid || ref < 0) {
-                at_end = true;  // coordinate-sorted: tid's records are contiguous
-                break;
+        const double tl0 = now_s();
+        if (listed && p == 0 && st.wt > 0 && end >= 8) {  // the carried record
+            const uint32_t bs = rd32(base);
+            const int32_t ref = rdi32(base + 4);
+            if (end >= 4 + (size_t)bs) {
+                if (ref == s->tid) {
+                    s->seen = true;
+                    dec.recs.push_back(base + 4);
+                    dec.sizes.push_back(bs);
+                    offs.push_back(0);
+                    p = 4 + (size_t)bs;
+                } else if (s->seen || ref > s->tid || ref < 0) {
+                    at_end = true;
+                }
             }
-            p += 4 + (size_t)bs;
-            ++wi;
+            if (!s->seen) listed = false;  // (still before tid: the walk below finds it)
         }
-        while (!listed && end - p >= 4 && k + dec.recs.size() < (size_t)cap_reads) {
+        size_t wi = 0;
+        const std::vector<uint32_t>* rs = nullptr;
+        if (listed && !at_end) {
+            rs = &st.wc->rstart;
+            const size_t rel = p - st.wt;
+            wi = (size_t)(std::lower_bound(rs->begin(), rs->end(), (uint32_t)rel) - rs->begin());
+            // the chain and the position agree, and the reads are on tid already
+            listed = p >= st.wt && s->seen && (wi == rs->size() ? p == end || end - p < 4 : (*rs)[wi] == rel);
+        }
+        if (listed && !at_end && rs) {
+            const Chunk& ch = *st.wc;
+            const size_t nw = rs->size();
+            size_t i1 = std::min(nw, wi + ((size_t)cap_reads - k - dec.recs.size()));
+            // a record that ends past the buffer (the last one) waits for the next chunk
+            if (i1 > wi && st.wt + ch.rstart[i1 - 1] + 4 + (size_t)ch.rsize[i1 - 1] > end) --i1;
+            size_t j = wi;
+            while (j < i1 && ch.rref[j] == s->tid) ++j;
+            const size_t n0 = dec.recs.size(), cnt = j - wi;
+            dec.recs.resize(n0 + cnt);
+            dec.sizes.resize(n0 + cnt);
+            offs.resize(n0 + cnt);
+            for (size_t x = 0; x < cnt; ++x) {
+                const size_t q = st.wt + ch.rstart[wi + x];
+                dec.recs[n0 + x] = base + q + 4;
+                offs[n0 + x] = q;
+            }
+            std::memcpy(dec.sizes.data() + n0, ch.rsize.data() + wi, cnt * sizeof(uint32_t));
+            if (cnt) p = offs[n0 + cnt - 1] + 4 + (size_t)ch.rsize[j - 1];
+            if (j < i1) at_end = true;  // a record of another reference: tid's records are contiguous
+        }
+        s->t_list += now_s() - tl0;
+        ++(listed ? s->n_listed : s->n_walked);
+        while (!listed && !at_end && end - p >= 4 && k + dec.recs.size() < (size_t)cap_reads) {
             // the walk is a chain of dependent header loads over bytes other threads just
             // inflated: keep lines ahead of it in flight
             __builtin_prefetch(base + p + 1024);

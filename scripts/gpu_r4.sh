@@ -32,7 +32,7 @@ if has e2e3; then
     cat gpurun_out/e2e_c3_$V.log
 fi
 if has e2e4; then
-    timeout -k 10 900 python -u scripts/e2e_bench.py --reads 200000000 --cells 10000 --out /tmp/mgp_e2e4 \
+    MGP_HOST_PROFILE=1 timeout -k 10 900 python -u scripts/e2e_bench.py --reads 200000000 --cells 10000 --out /tmp/mgp_e2e4 \
         --modes stream --formats txt,hdf5 > gpurun_out/e2e_c4_$V.json 2> gpurun_out/e2e_c4_$V.log \
         || { tail -30 gpurun_out/e2e_c4_$V.log; exit 1; }
     cat gpurun_out/e2e_c4_$V.log

@@ -143,6 +143,36 @@ def _rd(pos, flag=0, cb="AAAC-1", seq="ACGTACGTAC", cig=None, tid=1, **kw):
                 tags={} if cb is None else {"CB": cb})
 
 
+def _stream_cols(path, wl, batch, pipe, walk):
+    """The columns of a streaming decode of chrM (MGP_BAM_PIPELINE / MGP_BAM_WALK_AHEAD
+    as given), batches concatenated."""
+    import os
+
+    from mgatk2_amd.bam import StreamSlot
+
+    old = {k: os.environ.get(k) for k in ("MGP_BAM_PIPELINE", "MGP_BAM_WALK_AHEAD")}
+    os.environ["MGP_BAM_PIPELINE"], os.environ["MGP_BAM_WALK_AHEAD"] = pipe, walk
+    try:
+        cols = {k: [] for k in ("start", "bc", "tlen", "flag", "mapq", "span")}
+        with BamFile(path, n_threads=4) as b:
+            st = b.stream("chrM", wl)
+            try:
+                slot = StreamSlot(batch, batch * 300 + 2 * 128 * (len(wl) + 1) + (1 << 20))
+                while st.next_into(slot):
+                    v = slot.soa()
+                    for k in cols:
+                        cols[k].append(getattr(v, k).copy())
+            finally:
+                st.close()
+        return {k: np.concatenate(v) for k, v in cols.items()}
+    finally:
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+
+
 def test_other_contigs_many_blocks_threads(tmp_path):
     """chrM sits between other contigs and spans many BGZF blocks: the index seek,
     the no-index scan and 1 vs 8 inflate threads give the same batch."""
@@ -164,11 +194,22 @@ def test_other_contigs_many_blocks_threads(tmp_path):
         a = b1.read_soa("chrM", wl)
         assert b1.read_soa("chr1", wl).n == 3000
         assert b1.read_soa("chrX", wl).n == 3000
-    (tmp_path / "x.bam.bai").unlink()
+    streamed = {}
+    for idx in ("index", "scan"):
+        if idx == "scan":
+            (tmp_path / "x.bam.bai").unlink()
+        for pipe, walk in (("1", "1"), ("1", "0"), ("0", "1"), ("0", "0")):
+            for batch in (997, 7000):
+                streamed[idx, pipe, walk, batch] = _stream_cols(tmp_path / "x.bam", wl, batch, pipe, walk)
     with BamFile(tmp_path / "x.bam", n_threads=8) as b8:
         assert not b8.has_index
         c = b8.read_soa("chrM", wl)
     _assert_soa_equal(a, c)
+    # the streaming decode (index seek or scan; pipelined placement and the prefetch
+    # thread's boundary walk on or off) gives the same columns in the same order
+    for key, cols in streamed.items():
+        for k, v in cols.items():
+            np.testing.assert_array_equal(v, getattr(a, k), err_msg=f"{key} {k}")
     exp = pack_reads([dict(reference_start=r["pos"], flag=r["flag"], mapping_quality=60,
                            cigartuples=r["cigartuples"], query_sequence=r["query_sequence"],
                            query_qualities=r["query_qualities"], template_length=0,
