@@ -8,7 +8,7 @@ export TMPDIR=/tmp
 V=${V:-r4}
 STEPS=${STEPS:-suite,bench}
 has() { [[ ",$STEPS," == *",$1,"* ]]; }  # exact step names, comma-separated
-AB=${AB:-}; AB5=${AB5:-}; SQP=${SQP:-}; TK=${TK:-gpu}
+AB=${AB:-}; AB5=${AB5:-}; SQP=${SQP:-}; TK=${TK:-gpu}; DECENV=${DECENV:-}
 if has suite; then
     timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread \
         -p no:cacheprovider > gpurun_out/pytest_gpu_$V.log 2>&1 || { tail -30 gpurun_out/pytest_gpu_$V.log; exit 1; }
@@ -30,6 +30,16 @@ if has e2e3; then
     MGP_HOST_PROFILE=1 timeout -k 10 600 python -u scripts/e2e_bench.py --reads 50000000 --cells 5000 --out /tmp/mgp_e2e \
         > gpurun_out/e2e_c3_$V.json 2> gpurun_out/e2e_c3_$V.log || { tail -30 gpurun_out/e2e_c3_$V.log; exit 1; }
     cat gpurun_out/e2e_c3_$V.log
+fi
+if has dec; then
+    # streamed C3 txt pipeline under decoder variants (DECENV: space-separated NAME=VALUE sets, ',' joins)
+    for v in base $DECENV; do
+        envset=(); [ "$v" != base ] && IFS=, read -ra envset <<< "$v"
+        MGP_HOST_PROFILE=1 timeout -k 10 300 env "${envset[@]}" python -u scripts/e2e_bench.py --reads 50000000 \
+            --cells 5000 --out /tmp/mgp_e2e --modes stream --formats txt > gpurun_out/dec_${V}_$v.json \
+            2> gpurun_out/dec_${V}_$v.log || { tail -30 gpurun_out/dec_${V}_$v.log; exit 1; }
+        echo "== $v"; grep -h "mgp_bam_stream\|txt_stream" gpurun_out/dec_${V}_$v.log | cut -c1-300
+    done
 fi
 if has e2e4; then
     MGP_HOST_PROFILE=1 timeout -k 10 900 python -u scripts/e2e_bench.py --reads 200000000 --cells 10000 --out /tmp/mgp_e2e4 \
