@@ -837,7 +837,6 @@ struct ChunkRecs {
     std::vector<uint32_t> ncg;
     std::vector<const uint8_t*> cgp;
     std::vector<uint8_t> pkd;
-    std::vector<uint8_t> rec32;  // the 32-byte records, packed by the fields pass (index order)
     size_t k0 = 0;
     bool over = false;  // placement ran past the payload capacity (never: the batch cut bounds it)
 };
@@ -909,11 +908,6 @@ struct Decoder {
     std::vector<uint32_t> ncg;  // CIGAR operations (CG tag resolved)
     std::vector<const uint8_t*> cgp;
     std::vector<uint8_t> pkd;   // record layout: 0 full, 1 packed 64-byte, 2 32-byte
-    std::vector<uint8_t> rec32;  // (pipelined stream decode) the chunk's 32-byte records, packed early
-    bool early_pack = [] {  // MGP_BAM_EARLY_PACK=0: the records stage packs them
-        const char* e = std::getenv("MGP_BAM_EARLY_PACK");
-        return !e || std::strtol(e, nullptr, 10) != 0;
-    }();
     double t_p1 = 0, t_p2 = 0, t_place = 0, t_fields = 0;
 
     static int32_t keys_of(mgp_bam* b) {
@@ -1023,10 +1017,9 @@ struct Decoder {
 
     // one record: decode (do_fields: the SoA columns, barcode lookup included) and
     // pack (do_rec: the payload record at offset off) at index k
-    // (dst: where the record goes instead of c.pay + off, e.g. a chunk's staging buffer)
     void decode_one(const Cols& c, const uint8_t* r, uint32_t bs, size_t k, uint64_t off, uint32_t n_cig,
                     const uint8_t* cig, int pk, int64_t& tags, int64_t& first, int64_t gidx, bool do_fields,
-                    bool do_rec, uint8_t* dst = nullptr) const {
+                    bool do_rec) const {
         const uint8_t* end = r + bs;
         const int32_t pos = rdi32(r + 4);
         const uint8_t l_name = r[8];
@@ -1065,7 +1058,7 @@ struct Decoder {
             c.roff[k] = off;
         }
         if (!do_rec) return;
-        uint8_t* rec = dst ? dst : c.pay + off;
+        uint8_t* rec = c.pay + off;
         if (pk == 2) {
             uint32_t cw[4] = {0, 0, 0, 0};
             for (uint32_t q = 0; q < n_cig; ++q) cw[q] = rd32(cig + 4 * q);
@@ -1203,20 +1196,16 @@ struct Decoder {
     // pool, then chunk j's placement on a thread of its own while the pool walks,
     // classifies and decodes the fields of chunk j + 1, then chunk j's records.
     // fields_stage: the current chunk's columns at k0 (no payload yet)
-    // The 32-byte records are packed here too, while the record's bytes are in cache,
-    // into a staging buffer that the records stage copies to the placed offsets.
     void fields_stage(size_t k0, int64_t gidx0, const Cols& c) {
         const double t0 = now_s();
         const size_t m = recs.size();
         const int tn = (int)std::max<size_t>(1, std::min<size_t>((size_t)pool.size(), m / 4096 + 1));
         std::vector<int64_t> tags((size_t)tn, 0), firsts((size_t)tn, -1);
-        if (early_pack && rec32.size() < m * (size_t)MGP_PACK32_BYTES) rec32.resize(m * (size_t)MGP_PACK32_BYTES);
         pool.run(tn, [&](int t) {
             const size_t lo = m * (size_t)t / (size_t)tn, hi = m * (size_t)(t + 1) / (size_t)tn;
             for (size_t i = lo; i < hi; ++i)
                 decode_one(c, recs[i], sizes[i], k0 + i, 0, ncg[i], cgp[i], (int)pkd[i], tags[(size_t)t],
-                           firsts[(size_t)t], gidx0 + (int64_t)i, true, early_pack && pkd[i] == 2,
-                           early_pack ? rec32.data() + i * (size_t)MGP_PACK32_BYTES : nullptr);
+                           firsts[(size_t)t], gidx0 + (int64_t)i, true, false);
         });
         for (int t = 0; t < tn; ++t) {
             n_tag += tags[(size_t)t];
@@ -1232,7 +1221,6 @@ struct Decoder {
         q.ncg.swap(ncg);
         q.cgp.swap(cgp);
         q.pkd.swap(pkd);
-        q.rec32.swap(rec32);
         q.k0 = k0;
         q.over = false;
         clear_chunk();
@@ -1296,14 +1284,9 @@ struct Decoder {
         pool.run(tn, [&](int t) {
             const size_t lo = m * (size_t)t / (size_t)tn, hi = m * (size_t)(t + 1) / (size_t)tn;
             int64_t tg = 0, fs = -1;  // (tags are counted by fields_stage)
-            for (size_t i = lo; i < hi; ++i) {
-                const uint64_t off = c.roff[q.k0 + i];
-                if (early_pack && q.pkd[i] == 2)  // packed by fields_stage
-                    std::memcpy(c.pay + off, q.rec32.data() + i * (size_t)MGP_PACK32_BYTES, MGP_PACK32_BYTES);
-                else
-                    decode_one(c, q.recs[i], q.sizes[i], q.k0 + i, off, q.ncg[i], q.cgp[i], (int)q.pkd[i], tg, fs, 0,
-                               false, true);
-            }
+            for (size_t i = lo; i < hi; ++i)
+                decode_one(c, q.recs[i], q.sizes[i], q.k0 + i, c.roff[q.k0 + i], q.ncg[i], q.cgp[i], (int)q.pkd[i],
+                           tg, fs, 0, false, true);
         });
         t_recs += now_s() - t0;
     }
