@@ -1213,6 +1213,48 @@ struct Decoder {
         }
         t_fields += now_s() - t0;
     }
+    // pass 1 and the columns of the current chunk at k0 in one pool pass; hastag[i]: the
+    // record carries the barcode tag (counted by count_tags for the records the batch keeps)
+    std::vector<uint8_t> hastag;
+    bool classify_fields_all(size_t k0, int64_t gidx0, const Cols& c) {
+        const double t0 = now_s();
+        const size_t m = recs.size();
+        rsz.resize(m);
+        ncg.resize(m);
+        cgp.resize(m);
+        pkd.resize(m);
+        hastag.resize(m);
+        const int tn = (int)std::max<size_t>(1, std::min<size_t>((size_t)pool.size(), m / 4096 + 1));
+        std::atomic<bool> ok{true};
+        std::string msg;
+        std::mutex mu;
+        pool.run(tn, [&](int t) {
+            const size_t lo = m * (size_t)t / (size_t)tn, hi = m * (size_t)(t + 1) / (size_t)tn;
+            for (size_t i = lo; i < hi; ++i) {
+                if (!classify_at(i)) {
+                    std::lock_guard<std::mutex> g(mu);
+                    if (ok) msg = g_err;
+                    ok = false;
+                    return;
+                }
+                int64_t tg = 0, fs = -1;
+                decode_one(c, recs[i], sizes[i], k0 + i, 0, ncg[i], cgp[i], (int)pkd[i], tg, fs, gidx0 + (int64_t)i,
+                           true, false);
+                hastag[i] = tg != 0;
+            }
+        });
+        if (!ok) g_err = msg;
+        t_fields += now_s() - t0;
+        return ok;
+    }
+    void count_tags(int64_t gidx0) {
+        const size_t m = recs.size();
+        for (size_t i = 0; i < m; ++i)
+            if (hastag[i]) {
+                ++n_tag;
+                if (first_tag < 0) first_tag = gidx0 + (int64_t)i;
+            }
+    }
     // the current chunk's arrays into q (the decoder's are then empty, capacity kept)
     void move_chunk(ChunkRecs& q, size_t k0) {
         q.recs.swap(recs);
@@ -1482,7 +1524,7 @@ struct mgp_bam_stream {
     int64_t n_listed = 0, n_walked = 0;  // chunks whose boundaries came from the prefetch walk / were walked here
     // the pipelined decode (paired placement; MGP_BAM_PIPELINE=0 turns it off): the
     // chunk whose placement runs on `placer` and whose records are still to be written
-    bool pipe = true;
+    bool pipe = true, fuse = true;
     ChunkRecs pend;
     bool pending = false;
     Worker placer;
@@ -1491,6 +1533,8 @@ struct mgp_bam_stream {
         if (const char* e = std::getenv("MGP_BAM_PIPELINE")) pipe = std::strtol(e, nullptr, 10) != 0;
         pipe = pipe && dec.paired;
         st.hold = pipe;
+        const char* ef = std::getenv("MGP_BAM_FUSE");  // pass 1 and the columns in one pass (pipelined)
+        fuse = pipe && (!ef || std::strtol(ef, nullptr, 10) != 0);
     }
     ~mgp_bam_stream() {
         if (pending) placer.wait();  // (an abandoned batch: its placement may still run)
@@ -1668,7 +1712,9 @@ int64_t mgp_bam_stream_next(mgp_bam_stream* s, int64_t cap_reads, int64_t cap_pa
         }
         const double tw = now_s();
         s->t_walk += tw - tp1;
-        if (!dec.classify_all()) return -1;
+        // pipelined: pass 1 and the columns in one pool pass (one trip through the records'
+        // memory; a record cut off below is decoded again with the next batch)
+        if (s->fuse ? !dec.classify_fields_all(k, s->decoded + (int64_t)k, c) : !dec.classify_all()) return -1;
         s->t_class += now_s() - tw;
         for (size_t i = 0; i < dec.recs.size(); ++i) {
             const uint64_t w = dec.worst(i);
@@ -1686,7 +1732,8 @@ int64_t mgp_bam_stream_next(mgp_bam_stream* s, int64_t cap_reads, int64_t cap_pa
         if (!dec.recs.empty()) {
             const size_t m = dec.recs.size();
             if (s->pipe) {
-                dec.fields_stage(k, s->decoded + (int64_t)k, c);
+                if (s->fuse) dec.count_tags(s->decoded + (int64_t)k);
+                else dec.fields_stage(k, s->decoded + (int64_t)k, c);
                 if (!s->drain(c)) return -1;  // the chunk before: placed meanwhile, now its records
                 dec.move_chunk(s->pend, k);
                 s->pending = true;

@@ -39,6 +39,7 @@ def stream_batches(reader, n_cells, batch_reads=997):
             v = slot.soa()
             parts.append(type(v)(*[getattr(v, k).copy() for k in ("start", "bc", "tlen", "flag", "mapq", "span",
                                                                   "rec_off", "payload")]))
+            parts[-1].extra.update(n_with_tag=st.n_with_tag, first_tag_index=st.first_tag_index)
     finally:
         st.close()
         bam.close()
@@ -477,6 +478,7 @@ def test_stream_pipelined_decode_equals_serial(tmp_path, monkeypatch, batch):
     for a, b in zip(out["0"], out["1"]):
         for k in ("start", "bc", "tlen", "flag", "mapq", "span", "rec_off", "payload"):
             np.testing.assert_array_equal(getattr(a, k), getattr(b, k), err_msg=k)
+        assert a.extra == b.extra  # the barcode-tag counts of the batch
 
 
 @pytest.mark.gpu
