@@ -34,6 +34,8 @@ def main():
                     help="stream: batches decoded and pushed as they come (the default pipeline); resident: the "
                          "whole chrM set decoded, then one run")
     ap.add_argument("--bam-level", type=int, default=6, help="BGZF level of the synthetic BAM (samtools' default 6)")
+    ap.add_argument("--devices", default="0",
+                    help="engine devices, comma-separated (cells split over them; '0,0' runs two shards on one GPU)")
     args = ap.parse_args()
 
     from mgatk2_amd.bam import write_bam
@@ -61,7 +63,7 @@ def main():
 
     name = {(50_000_000, 5_000): "C3", (200_000_000, 10_000): "C4"}.get((args.reads, args.cells), "custom")
     res = {"config": f"{name}: {args.reads:,} reads x {args.cells} cells, run params (q20 mapq30 "
-                     "dedup=alignment_and_fragment_length)", "host_threads": args.threads,
+                     "dedup=alignment_and_fragment_length)", "host_threads": args.threads, "devices": args.devices,
            "bam_bytes": bam.stat().st_size, "bam_level": args.bam_level}
     digests = {}
     for mode in args.modes.split(","):
@@ -70,7 +72,9 @@ def main():
                                  use_fragment_length_dedup=True, min_reads_per_cell=1, n_cores=args.threads)
             t = time.time()
             od = out / f"run_{fmt}_{mode}"
-            p = MtDNAPipeline(str(bam), whitelist, od, config=cfg, output_format=fmt, stream=mode == "stream")
+            devs = [int(x) for x in args.devices.split(",")]
+            p = MtDNAPipeline(str(bam), whitelist, od, config=cfg, output_format=fmt, stream=mode == "stream",
+                              devices=devs if len(devs) > 1 else None)
             ret = p.run()
             wall = time.time() - t
             key = f"{fmt}_{mode}"

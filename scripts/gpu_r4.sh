@@ -41,6 +41,20 @@ if has dec; then
         echo "== $v"; grep -h "mgp_bam_stream\|txt_stream" gpurun_out/dec_${V}_$v.log | cut -c1-300
     done
 fi
+if has e2e4x2; then
+    # C4 through the pipeline with the cells split over two engine contexts on this GPU (the
+    # multi-device streamed path and its host concat of the rows, at scale)
+    MGP_HOST_PROFILE=1 timeout -k 10 900 python -u scripts/e2e_bench.py --reads 200000000 --cells 10000 \
+        --out /tmp/mgp_e2e4 --modes stream --formats hdf5,txt --devices 0,0 > gpurun_out/e2e_c4x2_$V.json \
+        2> gpurun_out/e2e_c4x2_$V.log || { tail -30 gpurun_out/e2e_c4x2_$V.log; exit 1; }
+    grep "\[e2e\]" gpurun_out/e2e_c4x2_$V.log | cut -c1-400
+fi
+if has rehearse; then
+    # bench.py --gpus 2 with both ranks on this GPU (no RCCL): the multi-rank bench path
+    MGP_BENCH_NO_COMM=1 timeout -k 10 400 python -u bench.py --gpus 2 --steps 5 --warmup 2 --no-cpu-baseline \
+        > gpurun_out/rehearse2_$V.log 2>&1 || { tail -30 gpurun_out/rehearse2_$V.log; exit 1; }
+    tail -c 1200 gpurun_out/rehearse2_$V.log
+fi
 if has e2e4; then
     MGP_HOST_PROFILE=1 timeout -k 10 900 python -u scripts/e2e_bench.py --reads 200000000 --cells 10000 --out /tmp/mgp_e2e4 \
         --modes stream --formats txt,hdf5 > gpurun_out/e2e_c4_$V.json 2> gpurun_out/e2e_c4_$V.log \
