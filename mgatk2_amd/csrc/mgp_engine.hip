@@ -134,6 +134,7 @@ struct mgp_ctx {
     int hist_slice_cells = 0;  // > 0: cap on the histogram's cells per slice (MGP_HIST_SLICE_CELLS)
     bool hist_xcd = true;      // several slices: a bin's slices dealt to one XCD (MGP_HIST_XCD)
     int hist_narrow = -1;      // 8-bit histogram counters: -1 when 32-bit ones need several slices (MGP_HIST_NARROW)
+    int64_t ga_wide_min = 16384;  // reads per pass-A workgroup from which it runs 512 threads (MGP_GA_WIDE_MIN)
     int hist_bounds = -1;      // bin bounds by k_bin_bounds: -1 when a histogram workgroup fills a CU's LDS (MGP_HIST_BOUNDS)
     bool group_wide = false;   // MGP_GROUP_WIDE=1: 16-byte grouping elements always (tests, A/B)
 
@@ -653,6 +654,10 @@ constexpr int kCompactBins = 32;             // start bins per pass-B step (comp
 #define MGP_GA_BLOCK 512  // threads per pass-A workgroup (r04 A/B: 256 2.06, 768 1.85, 1024 1.85 against 1.78 ms at C4)
 #endif
 constexpr int kGABlock = MGP_GA_BLOCK;
+#ifndef MGP_GA_NBLOCK
+#define MGP_GA_NBLOCK 256  // pass A's threads per workgroup for small sets / many cells
+#endif
+constexpr int kGANBlock = MGP_GA_NBLOCK;
 // kCompact: 8-byte elements (GCompact, below; kOff is then dense or u32). kBlk: threads
 // per workgroup (kBlk, or 256 when kBlk's per-wave group counters do not fit the
 // LDS: more than ~140k cells)
@@ -2963,6 +2968,7 @@ int mgp_open(const mgp_config* cfg, int hip_device, mgp_ctx** out) {
     if (const char* e = std::getenv("MGP_HIST_XCD")) ctx->hist_xcd = std::strtol(e, nullptr, 10) != 0;
     if (const char* e = std::getenv("MGP_HIST_NARROW")) ctx->hist_narrow = std::strtol(e, nullptr, 10) != 0;
     if (const char* e = std::getenv("MGP_HIST_BOUNDS")) ctx->hist_bounds = std::strtol(e, nullptr, 10) != 0;
+    if (const char* e = std::getenv("MGP_GA_WIDE_MIN")) ctx->ga_wide_min = std::strtoll(e, nullptr, 10);
     if (const char* e = std::getenv("MGP_HIST_SLICE_CELLS")) {  // tests: force several histogram slices
         const long v = std::strtol(e, nullptr, 10);
         if (v >= kGroup) ctx->hist_slice_cells = (int)(v / kGroup * kGroup);
@@ -2979,9 +2985,9 @@ int mgp_open(const mgp_config* cfg, int hip_device, mgp_ctx** out) {
         for (const void* f : {(const void*)k_group_a<kOffDense, false, kGABlock>, (const void*)k_group_a<kOffR32, false, kGABlock>,
                               (const void*)k_group_a<kOffR64, false, kGABlock>, (const void*)k_group_a<kOffDense, true, kGABlock>,
                               (const void*)k_group_a<kOffR32, true, kGABlock>, (const void*)k_group_a<kOffSpec, true, kGABlock>,
-                              (const void*)k_group_a<kOffDense, false, 256>, (const void*)k_group_a<kOffR32, false, 256>,
-                              (const void*)k_group_a<kOffR64, false, 256>, (const void*)k_group_a<kOffDense, true, 256>,
-                              (const void*)k_group_a<kOffR32, true, 256>, (const void*)k_group_a<kOffSpec, true, 256>})
+                              (const void*)k_group_a<kOffDense, false, kGANBlock>, (const void*)k_group_a<kOffR32, false, kGANBlock>,
+                              (const void*)k_group_a<kOffR64, false, kGANBlock>, (const void*)k_group_a<kOffDense, true, kGANBlock>,
+                              (const void*)k_group_a<kOffR32, true, kGANBlock>, (const void*)k_group_a<kOffSpec, true, kGANBlock>})
             (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, lds_max);
         (void)hipFuncSetAttribute((const void*)k_pileup<kLayAny>, hipFuncAttributeMaxDynamicSharedMemorySize, lds_max);
         (void)hipFuncSetAttribute((const void*)k_pileup<kLayP64>, hipFuncAttributeMaxDynamicSharedMemorySize, lds_max);
@@ -3443,8 +3449,12 @@ static int run_segment(mgp_ctx* ctx, const Seg& sg, int slot, int& dup_parts, in
         auto a_lds_for = [&](int blk) {
             return (size_t)ngroups * (1 + 2 * (blk / kWave)) * 4 + (size_t)((nc + 31) / 32) * 4;
         };
-        const bool a_wide = a_lds_for(kGABlock) <= (size_t)ctx->lds_hist_max_cells * 4;
-        const size_t a_lds = a_lds_for(a_wide ? kGABlock : 256);
+        // the 512-thread form pays with several 4096-read steps per (bin, part) workgroup;
+        // small sets (the 4- and 8-GPU shares of C4: under two steps each) run 256 threads
+        // wide (r04 A/B at 1250 / 2500 cells: 0.39 / 0.60 ms at 512 threads, 0.27 / 0.46 at 256)
+        const int64_t per_wg = n / std::max<int64_t>(1, (int64_t)g.nbins * kParts);
+        const bool a_wide = a_lds_for(kGABlock) <= (size_t)ctx->lds_hist_max_cells * 4 && per_wg >= ctx->ga_wide_min;
+        const size_t a_lds = a_lds_for(a_wide ? kGABlock : kGANBlock);
         if (a_lds > (size_t)ctx->lds_hist_max_cells * 4)
             return set_err(MGP_E_INVALID, "too many cells for one context (grouping LDS)");
         if (gbits > 16) return set_err(MGP_E_INVALID, "too many cells for one context (cell groups)");
@@ -3453,7 +3463,7 @@ static int run_segment(mgp_ctx* ctx, const Seg& sg, int slot, int& dup_parts, in
         dim3 ga((unsigned)g.nbins, kParts);
         auto launch_a = [&](auto kern_wide, auto kern_256) {
             auto kern = a_wide ? kern_wide : kern_256;
-            kern<<<ga, a_wide ? kGABlock : 256, a_lds, s>>>(
+            kern<<<ga, a_wide ? kGABlock : kGANBlock, a_lds, s>>>(
                 n, ctx->start.as<int32_t>(), ctx->bc.as<int32_t>(), ctx->tlen.as<int32_t>(),
                 ctx->flag.as<uint16_t>(), ctx->mapq.as<uint8_t>(), ctx->roff.as<uint64_t>(),
                 ctx->roff32.as<uint32_t>(), ctx->span.as<uint32_t>(), ctx->bin_start.as<uint32_t>(),
@@ -3462,16 +3472,16 @@ static int run_segment(mgp_ctx* ctx, const Seg& sg, int slot, int& dup_parts, in
                 ctx->first_read.as<uint32_t>(), ctx->roff_irregular.as<uint32_t>(), st, sg.w0, sg.bhi, unit);
         };
         if (spec) {
-            launch_a(k_group_a<kOffSpec, true, kGABlock>, k_group_a<kOffSpec, true, 256>);
+            launch_a(k_group_a<kOffSpec, true, kGABlock>, k_group_a<kOffSpec, true, kGANBlock>);
         } else if (compact) {
-            if (ctx->roff_mode == kOffDense) launch_a(k_group_a<kOffDense, true, kGABlock>, k_group_a<kOffDense, true, 256>);
-            else launch_a(k_group_a<kOffR32, true, kGABlock>, k_group_a<kOffR32, true, 256>);
+            if (ctx->roff_mode == kOffDense) launch_a(k_group_a<kOffDense, true, kGABlock>, k_group_a<kOffDense, true, kGANBlock>);
+            else launch_a(k_group_a<kOffR32, true, kGABlock>, k_group_a<kOffR32, true, kGANBlock>);
         } else if (ctx->roff_mode == kOffDense) {
-            launch_a(k_group_a<kOffDense, false, kGABlock>, k_group_a<kOffDense, false, 256>);
+            launch_a(k_group_a<kOffDense, false, kGABlock>, k_group_a<kOffDense, false, kGANBlock>);
         } else if (ctx->roff_mode == kOffR32) {
-            launch_a(k_group_a<kOffR32, false, kGABlock>, k_group_a<kOffR32, false, 256>);
+            launch_a(k_group_a<kOffR32, false, kGABlock>, k_group_a<kOffR32, false, kGANBlock>);
         } else {
-            launch_a(k_group_a<kOffR64, false, kGABlock>, k_group_a<kOffR64, false, 256>);
+            launch_a(k_group_a<kOffR64, false, kGABlock>, k_group_a<kOffR64, false, kGANBlock>);
         }
         HIP_TRY(hipGetLastError());
     }

@@ -74,6 +74,15 @@ if has ab; then
     bash scripts/ab_bench.sh $AB > gpurun_out/ab_$V.txt 2>&1 || { tail -30 gpurun_out/ab_$V.txt; exit 1; }
     cat gpurun_out/ab_$V.txt
 fi
+if has abshare; then
+    # the same A/B at the 8- and 4-GPU strong-scaling shares of C4 (1250 and 2500 cells per GPU)
+    for sh in "25000000 1250" "50000000 2500"; do
+        set -- $sh
+        BARGS="--reads $1 --cells $2 --steps 20 --warmup 3 --no-cpu-baseline --no-check --no-pcie --no-device-paired --no-host-pack" \
+            bash scripts/ab_bench.sh $AB > gpurun_out/abshare_${V}_$2.txt 2>&1 || { tail -30 gpurun_out/abshare_${V}_$2.txt; exit 1; }
+        echo "== $2 cells"; cat gpurun_out/abshare_${V}_$2.txt
+    done
+fi
 if has ab5; then
     # the same A/B at C5 on one GPU (AB5="libmgpileup_x.so ..."; MGP_* env variants as ENV:NAME=VALUE)
     BARGS="--reads 1000000000 --cells 100000 --steps 3 --warmup 1 --no-cpu-baseline --no-check --no-pcie --no-device-paired --no-host-pack" \

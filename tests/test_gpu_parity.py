@@ -88,6 +88,22 @@ def test_engine_matches_oracle_synth(engine_lib, oracle_lib, cfgname, n_reads, n
     assert_same(res, exp, f"{cfgname} {n_reads}x{n_cells}")
 
 
+@pytest.mark.parametrize("n_reads,n_cells", [(300_000, 200), (1_000_000, 500)])
+@pytest.mark.parametrize("cfgname", sorted(CONFIGS))
+def test_pass_a_wide_form(engine_lib, oracle_lib, monkeypatch, cfgname, n_reads, n_cells):
+    """Grouping pass A's 512-thread form, which the engine picks only for sets of
+    several 4096-read steps per (bin, part) workgroup (C4, C5), forced on small sets
+    (MGP_GA_WIDE_MIN=0): the same counts as the oracle."""
+    from mgatk2_amd.engine import EngineConfig
+
+    monkeypatch.setenv("MGP_GA_WIDE_MIN", "0")
+    soa = _synth(1000 + n_reads + n_cells, n_reads, n_cells)
+    cfg = EngineConfig(n_cells=n_cells, **CONFIGS[cfgname])
+    res = run_engine(engine_lib, cfg, soa)
+    exp, _ = oracle_lib.oracle_run(cfg, soa)
+    assert_same(res, exp, f"wide pass A {cfgname} {n_reads}x{n_cells}")
+
+
 def test_device_generator_equals_host_mirror(engine_lib):
     from mgatk2_amd.engine import EngineConfig
     from mgatk2_amd.synth import synth_reads
