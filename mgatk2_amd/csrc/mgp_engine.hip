@@ -135,7 +135,7 @@ struct mgp_ctx {
     bool hist_xcd = true;      // several slices: a bin's slices dealt to one XCD (MGP_HIST_XCD)
     int hist_narrow = -1;      // 8-bit histogram counters: -1 when 32-bit ones need several slices (MGP_HIST_NARROW)
     int64_t ga_wide_min = 16384;  // reads per pass-A workgroup from which it runs 512 threads (MGP_GA_WIDE_MIN)
-    int hist_bounds = -1;      // bin bounds by k_bin_bounds: -1 when a histogram workgroup fills a CU's LDS (MGP_HIST_BOUNDS)
+    int hist_bounds = 1;       // bin bounds by k_bin_bounds (MGP_HIST_BOUNDS=0: searched by each histogram workgroup)
     bool group_wide = false;   // MGP_GROUP_WIDE=1: 16-byte grouping elements always (tests, A/B)
 
     // resident inputs (BAM order)
@@ -655,7 +655,7 @@ constexpr int kCompactBins = 32;             // start bins per pass-B step (comp
 #endif
 constexpr int kGABlock = MGP_GA_BLOCK;
 #ifndef MGP_GA_NBLOCK
-#define MGP_GA_NBLOCK 256  // pass A's threads per workgroup for small sets / many cells
+#define MGP_GA_NBLOCK 128  // pass A's threads per workgroup for small sets / many cells (r04 A/B at 1250 cells: 256 0.262, 128 0.219 ms)
 #endif
 constexpr int kGANBlock = MGP_GA_NBLOCK;
 // kCompact: 8-byte elements (GCompact, below; kOff is then dense or u32). kBlk: threads
@@ -3338,8 +3338,10 @@ static int run_segment(mgp_ctx* ctx, const Seg& sg, int slot, int& dup_parts, in
         const size_t lds = std::max<size_t>(lds_words, narrow ? kGroup + 1 : 0) * 4;
         const bool xcd = nslices > 1 && ctx->hist_xcd;
         const dim3 gh = xcd ? dim3((unsigned)(8 * nslices * ((g.nbins + 7) / 8))) : dim3((unsigned)g.nbins, (unsigned)nslices);
-        // one workgroup per CU (large slices): the bins' bounds searched up front
-        const bool pre = ctx->hist_bounds >= 0 ? ctx->hist_bounds != 0 : lds > 80 * 1024;
+        // the bins' bounds searched up front, one thread per bin, instead of by two lanes of
+        // each histogram workgroup (r04 A/B: C5 hist 2.54 -> 2.44 ms, C4 0.298 -> 0.293, the
+        // 1250-cell share 0.070 -> 0.066; MGP_HIST_BOUNDS=0 searches per workgroup)
+        const bool pre = ctx->hist_bounds != 0;
         if (pre) {
             k_bin_bounds<<<(g.nbins + 1 + 255) / 256, 256, 0, s>>>(ctx->start.as<int32_t>(), n, g,
                                                                    ctx->bin_start.as<uint32_t>());
