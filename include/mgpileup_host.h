@@ -201,6 +201,12 @@ int64_t mgp_gather_offsets(const uint8_t *payload, const uint64_t *rec_off, cons
 int mgp_gather_records(const uint8_t *payload, const uint64_t *rec_off, const uint16_t *flag, int64_t n_total,
                        int64_t payload_bytes, const int64_t *idx, int64_t m, const uint64_t *out_off,
                        int64_t out_bytes, uint8_t *out, int n_threads);
+/* The reads of each cell range [bounds[d], bounds[d + 1]) (d < nd; bounds not
+ * decreasing): their indices, range by range and in batch order inside a range,
+ * into idx (room for n), their numbers into counts[nd]; returns the total (-1 on
+ * bad arguments). One pass for all the devices of a multi-device stream. */
+int64_t mgp_split_by_range(const int32_t *bc, int64_t n, const int64_t *bounds, int32_t nd, int64_t *counts,
+                           int64_t *idx);
 
 /* 32-byte records (MGP_FLAG_PACK32, include/mgpileup.h) from a batch's full-layout
  * records, for one run's (min_baseq, min_dist_from_end): out32[i] (32 bytes, dense

@@ -103,6 +103,8 @@ def host_library() -> C.CDLL:
         lib.mgp_gather_records.argtypes = [vp, vp, vp, C.c_int64, C.c_int64, vp, C.c_int64, vp, C.c_int64, vp,
                                            C.c_int]
         lib.mgp_gather_records.restype = C.c_int
+        lib.mgp_split_by_range.argtypes = [vp, C.c_int64, vp, C.c_int32, vp, vp]
+        lib.mgp_split_by_range.restype = C.c_int64
         lib.mgp_bam_write.argtypes = [C.c_char_p, C.POINTER(C.c_char_p), C.POINTER(C.c_int64), C.c_int, C.c_int,
                                       C.POINTER(mgp_bam_batch), C.POINTER(C.c_char_p), C.c_int, C.c_char_p,
                                       C.c_char_p, C.c_int, C.c_int, C.c_int]

@@ -102,4 +102,44 @@ int mgp_gather_records(const uint8_t* payload, const uint64_t* rec_off, const ui
     return 0;
 }
 
+// Reads by cell range: idx[] = the indices of the reads whose cell lies in [bounds[d],
+// bounds[d + 1]), range by range, BAM order inside each; counts[d] = their number. One
+// pass to count and one to place (the router of the multi-device stream used one
+// numpy scan of the batch per device). Returns the indices written.
+int64_t mgp_split_by_range(const int32_t* bc, int64_t n, const int64_t* bounds, int32_t nd, int64_t* counts,
+                           int64_t* idx) {
+    mgp_host_err().clear();
+    if ((!bc && n > 0) || !bounds || nd <= 0 || !counts || (n > 0 && !idx) || n < 0) {
+        mgp_host_err() = "mgp_split_by_range: bad arguments";
+        return -1;
+    }
+    for (int32_t d = 0; d < nd; ++d)
+        if (bounds[d + 1] < bounds[d]) {
+            mgp_host_err() = "mgp_split_by_range: bounds must not decrease";
+            return -1;
+        }
+    const int64_t lo = bounds[0], hi = bounds[nd];
+    // a cell's range by table (cells span at most a few 100k): one lookup per read
+    std::vector<int32_t> dev((size_t)std::max<int64_t>(0, hi - lo));
+    for (int32_t d = 0; d < nd; ++d)
+        for (int64_t c = bounds[d]; c < bounds[d + 1]; ++c) dev[(size_t)(c - lo)] = d;
+    std::vector<int64_t> cnt((size_t)nd, 0);
+    for (int64_t i = 0; i < n; ++i) {
+        const int64_t c = bc[i];
+        if (c >= lo && c < hi) ++cnt[(size_t)dev[(size_t)(c - lo)]];
+    }
+    std::vector<int64_t> at((size_t)nd, 0);
+    int64_t tot = 0;
+    for (int32_t d = 0; d < nd; ++d) {
+        counts[d] = cnt[(size_t)d];
+        at[(size_t)d] = tot;
+        tot += cnt[(size_t)d];
+    }
+    for (int64_t i = 0; i < n; ++i) {
+        const int64_t c = bc[i];
+        if (c >= lo && c < hi) idx[at[(size_t)dev[(size_t)(c - lo)]]++] = i;
+    }
+    return tot;
+}
+
 }  // extern "C"

@@ -1141,7 +1141,11 @@ __device__ __forceinline__ void group_b_rank(const typename Tr::T* __restrict__ 
 // waves' counts give every cell its run in the stage and every wave its place in
 // the run, so the stage fills in (cell, bin, BAM) order. A cell's run is then
 // written to its slots, which continue where the previous step's ended (cbase).
-constexpr int kBPer = kStageB / kBlock;  // elements per lane per step
+#ifndef MGP_GB_BLOCK
+#define MGP_GB_BLOCK 256  // pass-B threads per workgroup
+#endif
+constexpr int kGBBlock = MGP_GB_BLOCK;
+constexpr int kBPer = kStageB / kGBBlock;  // elements per lane per step
 #ifndef MGP_ABL_B
 #define MGP_ABL_B 0  // pass-B ablations (experiments only): 1 no dedup walk, 2 no pel stores, 3 no loads
 #endif
@@ -1150,7 +1154,7 @@ constexpr int kBPer = kStageB / kBlock;  // elements per lane per step
 #define MGP_GB_LOOK 3  // predecessors compared branch-free before a deferred walk (v42 A/B: 2, 4, 6 slower)
 #endif
 template <bool kTrack, class Tr>
-__global__ void __launch_bounds__(kBlock, Tr::kWaves) k_group_b(const typename Tr::T* __restrict__ gel2,
+__global__ void __launch_bounds__(kGBBlock, Tr::kWaves) k_group_b(const typename Tr::T* __restrict__ gel2,
                                                     const uint32_t* __restrict__ bucket_off,
                                                     const uint32_t* __restrict__ O, Geom g, int ngroups, int rb,
                                                     int mode, int unit, uint32_t* __restrict__ pel,
@@ -1163,12 +1167,12 @@ __global__ void __launch_bounds__(kBlock, Tr::kWaves) k_group_b(const typename T
     if (blockIdx.x == 0 && blockIdx.y == 0) check_stats(ck, st, spec_layout);
     if (__atomic_load_n(&st->err, __ATOMIC_RELAXED) & ERR_BOUNDS) return;  // unsorted input (k_bin_count)
     __shared__ T stage[kStageB];
-    __shared__ uint32_t wcnt[kBlock / kWave][kGroup];
+    __shared__ uint32_t wcnt[kGBBlock / kWave][kGroup];
     __shared__ uint32_t cbase[kGroup], cstart[kGroup + 1];
     __shared__ uint32_t bst[kMaxRbB], bsz[kMaxRbB], spre[kMaxRbB + 1];
     __shared__ int s_be;
     __shared__ uint32_t s_ndup[kGroup], s_nunp[kGroup];  // the group's duplicates / kept unpaired reads in this bin range
-    __shared__ uint16_t wpend[kBlock / kWave][kBPer * kWave];  // per wave: stage indices of deferred walks
+    __shared__ uint16_t wpend[kGBBlock / kWave][kBPer * kWave];  // per wave: stage indices of deferred walks
     const int gi = blockIdx.x;
     const int B0 = blockIdx.y * rb, B1 = min(g.nbins, B0 + rb);
     const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // (scalar)
@@ -1178,7 +1182,7 @@ __global__ void __launch_bounds__(kBlock, Tr::kWaves) k_group_b(const typename T
     const size_t bo = (size_t)ngroups + 1;
     const bool dedup = mode != MGP_DEDUP_NONE;
     DedupAcc acc;
-    for (int x = threadIdx.x; x < B1 - B0; x += kBlock) {
+    for (int x = threadIdx.x; x < B1 - B0; x += kGBBlock) {
         const uint32_t o0 = bucket_off[(size_t)(B0 + x) * bo + gi];
         bst[x] = o0;
         bsz[x] = bucket_off[(size_t)(B0 + x) * bo + gi + 1] - o0;
@@ -1279,7 +1283,7 @@ __global__ void __launch_bounds__(kBlock, Tr::kWaves) k_group_b(const typename T
         if (wid == 0) {  // per cell: the waves' places in its run, and the run in the stage
             uint32_t run = 0;
 #pragma unroll
-            for (int w = 0; w < kBlock / kWave; ++w) {
+            for (int w = 0; w < kGBBlock / kWave; ++w) {
                 const uint32_t x = wcnt[w][lane];
                 wcnt[w][lane] = run;
                 run += x;
@@ -1323,7 +1327,7 @@ __global__ void __launch_bounds__(kBlock, Tr::kWaves) k_group_b(const typename T
             bool d2[kWo], d3[kWo], wk[kWo];
 #pragma unroll
             for (int q = 0; q < kWo; ++q) {
-                const uint32_t t = threadIdx.x + (uint32_t)(h + q) * kBlock;
+                const uint32_t t = threadIdx.x + (uint32_t)(h + q) * kGBBlock;
                 const uint32_t tc = t < cur ? t : 0u;
                 const T x = stage[tc];
                 typename Tr::P pk[kLook];
@@ -1345,7 +1349,7 @@ __global__ void __launch_bounds__(kBlock, Tr::kWaves) k_group_b(const typename T
             }
 #pragma unroll
             for (int q = 0; q < kWo; ++q) {
-                const uint32_t t = threadIdx.x + (uint32_t)(h + q) * kBlock;
+                const uint32_t t = threadIdx.x + (uint32_t)(h + q) * kGBBlock;
                 // an element behind kLook + 1 equal starts without a full-key match waits
                 // for the wave's deferred walks (one divergent loop per step, not per element)
                 const bool defer = MGP_ABL_B != 1 && wk[q];
@@ -1407,7 +1411,7 @@ __global__ void __launch_bounds__(kBlock, Tr::kWaves) k_group_b(const typename T
     }
     // per-workgroup duplicate counts (k_run_stats sums them)
     const unsigned long long d2 = wave_sum(acc.d2), d3 = wave_sum(acc.d3);
-    __shared__ unsigned long long s_dup[2][kBlock / kWave];
+    __shared__ unsigned long long s_dup[2][kGBBlock / kWave];
     if (lane == 0) {
         s_dup[0][wid] = d2;
         s_dup[1][wid] = d3;
@@ -1415,7 +1419,7 @@ __global__ void __launch_bounds__(kBlock, Tr::kWaves) k_group_b(const typename T
     __syncthreads();
     if (threadIdx.x < 2) {
         unsigned long long t = 0;
-        for (int w = 0; w < kBlock / kWave; ++w) t += s_dup[threadIdx.x][w];
+        for (int w = 0; w < kGBBlock / kWave; ++w) t += s_dup[threadIdx.x][w];
         dup_part[2 * ((size_t)blockIdx.y * gridDim.x + blockIdx.x) + threadIdx.x] = t;
     }
 }
@@ -3509,7 +3513,7 @@ static int run_segment(mgp_ctx* ctx, const Seg& sg, int slot, int& dup_parts, in
         // flag bits its variants assume (check_stats)
         const uint32_t spec_layout = sg.stream ? (layout == kLayP32 ? CHK_P32 : CHK_P64) : check_layout;
         auto launch_b = [&](auto kern, auto* gel) {
-            kern<<<gb, kBlock, 0, s>>>(gel, ctx->bucket_off.as<uint32_t>(), ctx->H.as<uint32_t>(),
+            kern<<<gb, kGBBlock, 0, s>>>(gel, ctx->bucket_off.as<uint32_t>(), ctx->H.as<uint32_t>(),
                                        g, ngroups, rb, ctx->cfg.dedup_mode, unit, ctx->pel.as<uint32_t>(),
                                        ctx->any_paired.as<uint8_t>(), ctx->dup_part.as<unsigned long long>(), st,
                                        cnt_lo, ctx->roff_irregular.as<uint32_t>(), spec_layout);

@@ -247,7 +247,7 @@ class CellProcessor:
         and count only toward total_reads), while the producer decodes the next.
         Every device's rows target is its cell range of one pinned result array, so
         the results need no concatenation; the tallies are summed on the host."""
-        from ..shard import shard_soa
+        from ..shard import shard_soa, split_by_range
 
         devs = list(self.devices)
         D = len(devs)
@@ -270,27 +270,48 @@ class CellProcessor:
                     engines[d].set_rows16_target(Rows16(rows.counts[lo:hi], rows.tn5[lo:hi], rows.depth[lo:hi],
                                                         rows.wide[lo:hi], rows.window_width))
 
-            def work(d):
+            def work(d, lo, hi):
+                # this device's share of each batch: gathered here (the devices' gathers run
+                # side by side, native and GIL-free), then the batch's slot is released by
+                # the last device done with it
                 eng = engines[d]
                 try:
                     while True:
-                        sub = queues[d].get()
-                        if sub is None:
+                        job = queues[d].get()
+                        if job is None:
                             break
-                        eng.push(sub)
-                        eng.copy_wait()
+                        item, soa, idx, left = job
+                        try:
+                            sub, _ = shard_soa(soa, lo, hi, idx=idx)
+                        finally:
+                            with left[1]:
+                                left[0] -= 1
+                                last = left[0] == 0
+                            if last:
+                                free.put(item)  # (the sub-batches are copies)
+                        if sub.n:
+                            eng.push(sub)
+                            eng.copy_wait()
                     eng.run()
                     eng.sync()
                 except BaseException as e:  # noqa: BLE001 - re-raised by the router
                     errors.append(e)
-                    while queues[d].get() is not None:  # drain
-                        pass
+                    while True:  # drain (releasing the slots it was dealt)
+                        job = queues[d].get()
+                        if job is None:
+                            break
+                        with job[3][1]:
+                            job[3][0] -= 1
+                            last = job[3][0] == 0
+                        if last:
+                            free.put(job[0])
 
             for d, lo, hi in parts:
                 queues[d] = Queue(maxsize=4)
                 idx_lists[d] = []
-                workers[d] = threading.Thread(target=work, args=(d,), name=f"mgp-dev{d}", daemon=True)
+                workers[d] = threading.Thread(target=work, args=(d, lo, hi), name=f"mgp-dev{d}", daemon=True)
                 workers[d].start()
+            pbounds = np.asarray([parts[0][1]] + [hi for _, _, hi in parts], np.int64) if parts else None
             t1 = time.perf_counter()
             n_batches, base = 0, 0
             try:
@@ -305,13 +326,16 @@ class CellProcessor:
                     if n_batches == 0:
                         times["first_batch"] = time.perf_counter()
                     soa = item.soa()
-                    for d, lo, hi in parts:
-                        sub, idx = shard_soa(soa, lo, hi)
-                        if sub.n:
-                            idx_lists[d].append(idx + base)
-                            queues[d].put(sub)
+                    if parts:
+                        split = split_by_range(soa.bc, pbounds)  # (parts are contiguous ranges)
+                        left = [len(parts), threading.Lock()]
+                        for (d, lo, hi), idx in zip(parts, split):
+                            if idx.size:
+                                idx_lists[d].append(idx + base)
+                            queues[d].put((item, soa, idx, left))
+                    else:
+                        free.put(item)
                     base += soa.n
-                    free.put(item)  # (the sub-batches are copies)
                     n_batches += 1
             finally:
                 for d, _, _ in parts:

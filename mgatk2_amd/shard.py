@@ -43,23 +43,43 @@ def reads_per_cell(soa: ReadSoA, n_cells: int) -> np.ndarray:
     return np.bincount(bc, minlength=n_cells)[:n_cells]
 
 
+def split_by_range(bc: np.ndarray, bounds) -> list[np.ndarray]:
+    """The read indices of each cell range [bounds[d], bounds[d + 1]) in batch order
+    (libmgphost `mgp_split_by_range`: one pass over the batch for all ranges)."""
+    from .bam import host_library
+
+    lib = host_library()
+    b = np.ascontiguousarray(bounds, np.int64)
+    nd = b.size - 1
+    bc = np.ascontiguousarray(bc, np.int32)
+    counts = np.zeros(max(nd, 1), np.int64)
+    idx = np.empty(max(bc.size, 1), np.int64)
+    tot = lib.mgp_split_by_range(bc.ctypes.data, bc.size, b.ctypes.data, nd, counts.ctypes.data, idx.ctypes.data)
+    if tot < 0:
+        raise ValueError((lib.mgp_host_last_error() or b"").decode())
+    cuts = np.concatenate([[0], np.cumsum(counts[:nd])])
+    return [idx[cuts[d]:cuts[d + 1]] for d in range(nd)]
+
+
 def shard_soa(soa: ReadSoA, lo: int, hi: int, rec_align: int = 64, paired: bool = True,
-              keep_all: bool = False) -> tuple[ReadSoA, np.ndarray]:
+              keep_all: bool = False, idx: np.ndarray | None = None) -> tuple[ReadSoA, np.ndarray]:
     """Reads of cells [lo, hi) in BAM order, cell ids rebased to lo, payload
     records gathered into a new payload (native, multithreaded: libmgphost.so
     `mgp_gather_offsets` / `mgp_gather_records`), placed by the producer
     placement (two consecutive packed records of a cell per 128-byte line when
     `paired`, else dense at `rec_align`). keep_all: every read (lo must be 0;
     reads outside the range keep their bc). Returns (batch, original read
-    indices)."""
+    indices). idx: the range's read indices when the caller has them already."""
     from .bam import PLACE_DENSE, PLACE_PAIRED, host_library, host_threads
 
     if keep_all:
         if lo != 0:
             raise ValueError("keep_all needs lo == 0")
         idx = np.arange(soa.n, dtype=np.int64)
-    else:
+    elif idx is None:
         idx = np.flatnonzero((soa.bc >= lo) & (soa.bc < hi)).astype(np.int64)
+    else:  # the range's reads, given (split_by_range)
+        idx = np.ascontiguousarray(idx, np.int64)
     lib = host_library()
     roff = np.ascontiguousarray(soa.rec_off, dtype=np.uint64)
     flag = np.ascontiguousarray(soa.flag, dtype=np.uint16)

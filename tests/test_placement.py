@@ -159,3 +159,20 @@ def test_decoder_paired_placement(tmp_path, synth):
     r = relocate(p, n_cells=40)
     np.testing.assert_array_equal(r.rec_off, d.rec_off)
     np.testing.assert_array_equal(r.payload[: d.payload.size], d.payload[: r.payload.size])
+
+
+def test_split_by_range_equals_numpy():
+    """mgp_split_by_range (the multi-device stream's router): each range's read
+    indices in batch order, as one numpy scan per range gives them; empty ranges,
+    reads outside every range and negative (unlisted) barcodes included."""
+    from mgatk2_amd.shard import split_by_range
+
+    rng = np.random.default_rng(3)
+    bc = rng.integers(-3, 1200, 200_001).astype(np.int32)
+    for bounds in ([0, 1000], [0, 250, 250, 600, 1000], [100, 101, 900], [0, 1, 2, 3, 4, 5, 6, 7, 1100]):
+        got = split_by_range(bc, bounds)
+        assert len(got) == len(bounds) - 1
+        for d, idx in enumerate(got):
+            exp = np.flatnonzero((bc >= bounds[d]) & (bc < bounds[d + 1]))
+            np.testing.assert_array_equal(idx, exp)
+    assert [x.size for x in split_by_range(np.zeros(0, np.int32), [0, 5, 9])] == [0, 0]
