@@ -288,6 +288,12 @@ def test_errors(tmp_path):
     (tmp_path / "c.bam").write_bytes(bytes(corrupt))
     with BamFile(tmp_path / "c.bam") as b, pytest.raises(BAMReadError):
         b.read_soa("chrM", g.whitelist)
+    # the streaming decode raises on the same files, in every mode (the pipelined one
+    # leaves no placement running on the caller's arrays)
+    for name in ("t.bam", "c.bam"):
+        for pipe in ("1", "0"):
+            with pytest.raises(BAMReadError):
+                _stream_cols(tmp_path / name, g.whitelist, 997, pipe, pipe)
 
 
 @pytest.mark.parametrize("case", ["synth_run", "kat_run"])
