@@ -486,7 +486,10 @@ int  mgp_fetch_rows16(mgp_ctx *ctx, int32_t lo, int32_t hi, mgp_rows16 *out);
  * later batches still run the other way; the wide flags follow the run, and mgp_sync
  * waits for all of it. The caller then needs no mgp_fetch_rows16. With min_reads > 1 the
  * gate (processors.py:22) also zeroes the target rows of the cells it drops, after the
- * last segment's rows have landed (ABI 4). NULL stops it. Replaces the
+ * last segment's rows have landed (ABI 4). A target may also be set during a
+ * streaming run (not replaced): the rows of the windows piled so far are copied at
+ * once, the later ones as they complete, so the caller can allocate it while the
+ * first batches go in (ABI 4). NULL stops it (not during a streaming run). Replaces the
  * reference's per-cell write_cell after each worker (processors.py:112-144): results
  * leave the device while ingest continues. */
 int  mgp_set_rows16_target(mgp_ctx *ctx, const mgp_rows16 *rows);

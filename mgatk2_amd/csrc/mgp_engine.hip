@@ -3840,7 +3840,10 @@ int mgp_windows(mgp_ctx* ctx, int32_t* n_windows, int32_t* window_width) {
 
 int mgp_set_rows16_target(mgp_ctx* ctx, const mgp_rows16* rows) {
     if (!ctx) return set_err(MGP_E_INVALID, "null ctx");
-    if (ctx->seg_open) return set_err(MGP_E_STATE, "a streaming run is in progress (mgp_run or mgp_reset first)");
+    // (set during a streaming run: the windows piled so far are copied at once, below;
+    // replacing or clearing a target mid-run is not allowed)
+    if (ctx->seg_open && (!rows || ctx->rows_on))
+        return set_err(MGP_E_STATE, "a streaming run is in progress (mgp_run or mgp_reset first)");
     HIP_TRY(hipSetDevice(ctx->dev));
     HIP_TRY(hipStreamSynchronize(ctx->s_d2h));
     if (!rows) {
@@ -3864,6 +3867,18 @@ int mgp_set_rows16_target(mgp_ctx* ctx, const mgp_rows16* rows) {
     (void)hipGetLastError();
     ctx->rows_tgt = d;
     ctx->rows_on = true;
+    if (ctx->seg_open && ctx->w_done > 0) {  // catch up: the rows of the windows piled before
+        const Geom& g = ctx->g;
+        const int p1 = std::min(g.L, ctx->w_done * g.W);
+        HIP_TRY(hipEventRecord(ctx->ev_rows, ctx->s_comp));
+        HIP_TRY(hipStreamWaitEvent(ctx->s_d2h, ctx->ev_rows, 0));
+        dim3 gr((unsigned)((p1 + kBlock - 1) / kBlock), (unsigned)std::min(g.nc, 65535));
+        k_rows_to_host<<<gr, kBlock, 0, ctx->s_d2h>>>(g.L, g.nc, 0, p1, ctx->counts16.as<uint4>(),
+                                                    ctx->tn5_16.as<uint32_t>(), ctx->depth16.as<uint16_t>(),
+                                                    reinterpret_cast<uint4*>(d.counts), reinterpret_cast<uint32_t*>(d.tn5),
+                                                    d.depth);
+        HIP_TRY(hipGetLastError());
+    }
     return MGP_OK;
 }
 

@@ -157,11 +157,11 @@ class CellProcessor:
         producer.start()
         return bam, st, n_hint, free, full, producer, times
 
-    def _rows_target(self, n_cells: int, eng) -> Rows16 | None:
+    def _rows_target(self, n_cells: int, eng=None, windows: tuple[int, int] | None = None) -> Rows16 | None:
         """Pinned 16-bit result rows for all cells (the rows target)."""
         if n_cells <= 0:
             return None
-        nw, W = eng.windows()
+        nw, W = windows if windows is not None else eng.windows()
         L = self.config.mito_length
         rb = PinnedBuffer(n_cells * L * 22 + n_cells * nw + 4096)
         return Rows16(rb.array((n_cells, L, 8), np.uint16, 0), rb.array((n_cells, L, 2), np.uint16, n_cells * L * 16),
@@ -187,9 +187,35 @@ class CellProcessor:
             ec.stream = True
             eng = Engine(ec, device=self.device)
             try:
-                rows = self._rows_target(n_cells, eng) if rows_target else None
-                if rows is not None:
-                    eng.set_rows16_target(rows)
+                # the rows target (GBs of pinned memory: ~0.25 s per GB to pin) is allocated
+                # on a thread while the first batches go in; the engine copies the rows of
+                # the windows piled before it is set when it is set (ABI 4)
+                rows, pending = None, None
+                if rows_target and n_cells > 0:
+                    box: dict = {}
+                    wins = eng.windows()
+
+                    def alloc():
+                        try:
+                            box["rows"] = self._rows_target(n_cells, windows=wins)
+                        except BaseException as e:  # noqa: BLE001 - re-raised below
+                            box["err"] = e
+
+                    pending = threading.Thread(target=alloc, name="mgp-rows-alloc", daemon=True)
+                    pending.start()
+
+                def settle(wait: bool):
+                    nonlocal rows, pending
+                    if pending is None or (not wait and pending.is_alive()):
+                        return
+                    pending.join()
+                    pending = None
+                    if "err" in box:
+                        raise box["err"]
+                    rows = box.get("rows")
+                    if rows is not None:
+                        eng.set_rows16_target(rows)
+
                 t1 = time.perf_counter()
                 n_batches = 0
                 while True:
@@ -200,10 +226,12 @@ class CellProcessor:
                         raise item
                     if n_batches == 0:
                         times["first_batch"] = time.perf_counter()
+                    settle(False)
                     eng.push(item.soa())
                     eng.copy_wait()  # its pinned arrays may be refilled now
                     free.put(item)
                     n_batches += 1
+                settle(True)
                 t2 = time.perf_counter()
                 eng.run()
                 eng.sync()

@@ -423,16 +423,19 @@ def test_push_without_offsets_rejects_ragged_payloads(engine_lib):
 # ---------------------------------------------------------------------------
 # ABI v3.1: a rows target (the 16-bit rows leave the device as the windows complete)
 # ---------------------------------------------------------------------------
+@pytest.mark.parametrize("late", [False, True])
 @pytest.mark.parametrize("min_reads", [1, 4500])
 @pytest.mark.parametrize("layout", ["p32", "full"])
 @pytest.mark.parametrize("streamed", [False, True])
-def test_rows16_target_equals_fetch_rows16(engine_lib, streamed, layout, min_reads):
+def test_rows16_target_equals_fetch_rows16(engine_lib, streamed, layout, min_reads, late):
     """The rows copied to a pinned target segment by segment equal mgp_fetch_rows16
     of a resident run, for a streamed run of 4 batches and a resident one, also on a
     rerun of the same context; full-layout records make a streamed run rerun resident
     (the target then holds the rerun's rows). With min_reads above some cells' read
     counts the gate (processors.py:22) drops those cells after their rows were sent:
-    their target rows are zeroed too (ABI 4)."""
+    their target rows are zeroed too (ABI 4). late: the target is set after two of
+    the four batches (a streaming run has piled windows by then: they are copied
+    when the target is set)."""
     from dataclasses import replace
 
     from mgatk2_amd.engine import EngineConfig, PinnedBuffer, Rows16
@@ -458,13 +461,20 @@ def test_rows16_target_equals_fetch_rows16(engine_lib, streamed, layout, min_rea
     scfg = replace(cfg, stream=True, reserve_reads=soa.n, reserve_payload=int(soa.payload.shape[0]) + 4096) \
         if streamed else cfg
     with engine_lib.Engine(scfg) as eng:
-        eng.set_rows16_target(tgt)
+        if not late:
+            eng.set_rows16_target(tgt)
         for rep in range(2):
             for a in (tgt.counts, tgt.tn5, tgt.depth, tgt.wide):
                 a.fill(0xAB)
             eng.reset()
+            if late:
+                eng.set_rows16_target(None)
             cuts = np.linspace(0, soa.n, 5).astype(int)
-            for a, b in zip(cuts[:-1], cuts[1:]):
+            for i, (a, b) in enumerate(zip(cuts[:-1], cuts[1:])):
+                if late and i == 2:
+                    if streamed and layout == "p32":
+                        assert eng.stream_info()[0] > 0  # windows piled before the target exists
+                    eng.set_rows16_target(tgt)
                 eng.push(soa.slice(int(a), int(b)))
             eng.run()
             got = eng.fetch()
