@@ -292,19 +292,46 @@ class CellProcessor:
                                                reserve_payload=int(n_hint * share * 1.25) * 40 + (64 << 20))
                 ec.stream = True
                 engines[d] = Engine(ec, device=devs[d])
+            # the rows target (all cells, one pinned array) is pinned on a thread while the
+            # first batches go in; each device thread sets its view when it is ready (the
+            # engine copies the windows piled before, ABI 4)
+            rows_box: dict = {}
+            rows_ready = threading.Event()
             if rows_target and parts:
-                rows = self._rows_target(n_cells, engines[parts[0][0]])
-                for d, lo, hi in parts:
-                    engines[d].set_rows16_target(Rows16(rows.counts[lo:hi], rows.tn5[lo:hi], rows.depth[lo:hi],
-                                                        rows.wide[lo:hi], rows.window_width))
+                wins = engines[parts[0][0]].windows()
+
+                def alloc():
+                    try:
+                        rows_box["rows"] = self._rows_target(n_cells, windows=wins)
+                    except BaseException as e:  # noqa: BLE001 - re-raised by the device threads
+                        rows_box["err"] = e
+                    rows_ready.set()
+
+                threading.Thread(target=alloc, name="mgp-rows-alloc", daemon=True).start()
 
             def work(d, lo, hi):
                 # this device's share of each batch: gathered here (the devices' gathers run
                 # side by side, native and GIL-free), then the batch's slot is released by
                 # the last device done with it
                 eng = engines[d]
+                view_set = not (rows_target and parts)
+
+                def set_view(wait: bool):
+                    nonlocal view_set
+                    if view_set or (not wait and not rows_ready.is_set()):
+                        return
+                    rows_ready.wait()
+                    view_set = True
+                    if "err" in rows_box:
+                        raise rows_box["err"]
+                    r = rows_box["rows"]
+                    if r is not None:
+                        eng.set_rows16_target(Rows16(r.counts[lo:hi], r.tn5[lo:hi], r.depth[lo:hi], r.wide[lo:hi],
+                                                     r.window_width))
+
                 try:
                     while True:
+                        set_view(False)
                         job = queues[d].get()
                         if job is None:
                             break
@@ -318,8 +345,10 @@ class CellProcessor:
                             if last:
                                 free.put(item)  # (the sub-batches are copies)
                         if sub.n:
+                            set_view(False)
                             eng.push(sub)
                             eng.copy_wait()
+                    set_view(True)
                     eng.run()
                     eng.sync()
                 except BaseException as e:  # noqa: BLE001 - re-raised by the router
@@ -372,6 +401,7 @@ class CellProcessor:
                     workers[d].join()
             if errors:
                 raise errors[0]
+            rows = rows_box.get("rows")
             t2 = time.perf_counter()
             L = self.config.mito_length
             wide = rows is not None and bool(rows.wide.any())
