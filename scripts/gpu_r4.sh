@@ -9,6 +9,11 @@ V=${V:-r4}
 STEPS=${STEPS:-suite,bench}
 has() { [[ ",$STEPS," == *",$1,"* ]]; }  # exact step names, comma-separated
 AB=${AB:-}; AB5=${AB5:-}; SQP=${SQP:-}; TK=${TK:-gpu}; DECENV=${DECENV:-}
+if has smoke; then
+    timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" \
+        > gpurun_out/smoke_$V.log 2>&1 || { tail -30 gpurun_out/smoke_$V.log; exit 1; }
+    tail -2 gpurun_out/smoke_$V.log
+fi
 if has suite; then
     timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread \
         -p no:cacheprovider > gpurun_out/pytest_gpu_$V.log 2>&1 || { tail -30 gpurun_out/pytest_gpu_$V.log; exit 1; }
