@@ -910,6 +910,29 @@ struct Decoder {
     std::vector<uint8_t> pkd;   // record layout: 0 full, 1 packed 64-byte, 2 32-byte
     double t_p1 = 0, t_p2 = 0, t_place = 0, t_fields = 0;
 
+    // the pool's threads (MGP_BAM_DEC_THREADS overrides the bam's count; A/B of leaving
+    // cores to the placement and walk threads of the pipelined stream decode)
+    static int decoder_threads(mgp_bam* b) {
+        if (const char* e = std::getenv("MGP_BAM_DEC_THREADS")) {
+            const long v = std::strtol(e, nullptr, 10);
+            if (v > 0) return (int)v;
+        }
+        return std::max(1, b->n_threads);
+    }
+    // the next 32-byte slot of `key`: its open line's next quarter, or a new line at the
+    // cursor (always 128-aligned in the paired placement); branch-free (the line opens on
+    // one read in four: a branch on it mispredicted, 18 -> 15 ns per read on one core)
+    uint64_t place32(size_t key) {
+        const uint64_t o0 = open32[key];
+        const uint32_t f0 = fill32[key];
+        const bool opn = o0 == ~0ull;
+        const uint64_t o = opn ? cursor : o0;
+        const uint32_t f = opn ? 0u : f0;
+        cursor += opn ? 128u : 0u;
+        open32[key] = f == 3 ? ~0ull : o;
+        fill32[key] = (uint8_t)((f + 1) & 3u);
+        return o + (uint64_t)MGP_PACK32_BYTES * f;
+    }
     static int32_t keys_of(mgp_bam* b) {
         int32_t n = 0;
         for (int32_t v : b->wl.vals) n = std::max(n, v + 1);
@@ -917,7 +940,7 @@ struct Decoder {
         return n;
     }
     Decoder(mgp_bam* bam, int rec_align)
-        : b(bam), pool(std::max(1, bam->n_threads)), amask((uint64_t)rec_align - 1),
+        : b(bam), pool(decoder_threads(bam)), amask((uint64_t)rec_align - 1),
           paired(bam->placement == MGP_PLACE_PAIRED),
           n_keys(paired ? keys_of(bam) : 0), dups(paired ? (size_t)keys_of(bam) : 0) {
         open.assign(paired ? (size_t)n_keys + 1 : 0, ~0ull);
@@ -1150,14 +1173,7 @@ struct Decoder {
                         dups.repeat(key, c.start[k], (c.flag[k] & MGP_FLAG_REVERSE) != 0, c.tlen[k]))
                         key = (size_t)n_keys;
                     if (pkd[i] == 2) {  // four 32-byte records of one key per line
-                        if (open32[key] == ~0ull) {
-                            cursor = (cursor + 127) & ~127ull;
-                            open32[key] = cursor;
-                            fill32[key] = 0;
-                            cursor += 128;
-                        }
-                        c.roff[k] = open32[key] + (uint64_t)MGP_PACK32_BYTES * fill32[key];
-                        if (++fill32[key] == 4) open32[key] = ~0ull;
+                        c.roff[k] = place32(key);
                         continue;
                     }
                     if (open[key] != ~0ull) {
@@ -1287,14 +1303,7 @@ struct Decoder {
             if (key < (size_t)n_keys && dups.repeat(key, c.start[k], (c.flag[k] & MGP_FLAG_REVERSE) != 0, c.tlen[k]))
                 key = (size_t)n_keys;
             if (q.pkd[i] == 2) {
-                if (open32[key] == ~0ull) {
-                    cursor = (cursor + 127) & ~127ull;
-                    open32[key] = cursor;
-                    fill32[key] = 0;
-                    cursor += 128;
-                }
-                c.roff[k] = open32[key] + (uint64_t)MGP_PACK32_BYTES * fill32[key];
-                if (++fill32[key] == 4) open32[key] = ~0ull;
+                c.roff[k] = place32(key);
                 continue;
             }
             if (open[key] != ~0ull) {
