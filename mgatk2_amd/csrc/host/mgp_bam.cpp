@@ -912,12 +912,15 @@ struct Decoder {
 
     // the pool's threads (MGP_BAM_DEC_THREADS overrides the bam's count; A/B of leaving
     // cores to the placement and walk threads of the pipelined stream decode)
-    static int decoder_threads(mgp_bam* b) {
+    // reserve: threads of the bam's count left to others (the pipelined stream decode's
+    // placement and boundary-walk threads: on the box's 16-core share, 16 pool threads
+    // beside them decoded C3 in 1.78 s, 14 in 1.68, 12 in 1.64)
+    static int decoder_threads(mgp_bam* b, int reserve) {
         if (const char* e = std::getenv("MGP_BAM_DEC_THREADS")) {
             const long v = std::strtol(e, nullptr, 10);
             if (v > 0) return (int)v;
         }
-        return std::max(1, b->n_threads);
+        return std::max(1, b->n_threads - (b->n_threads > 4 ? reserve : 0));
     }
     // the next 32-byte slot of `key`: its open line's next quarter, or a new line at the
     // cursor (always 128-aligned in the paired placement); branch-free (the line opens on
@@ -939,8 +942,8 @@ struct Decoder {
         if (b->bulk_cell >= 0) n = std::max(n, b->bulk_cell + 1);
         return n;
     }
-    Decoder(mgp_bam* bam, int rec_align)
-        : b(bam), pool(decoder_threads(bam)), amask((uint64_t)rec_align - 1),
+    Decoder(mgp_bam* bam, int rec_align, int reserve = 0)
+        : b(bam), pool(decoder_threads(bam, reserve)), amask((uint64_t)rec_align - 1),
           paired(bam->placement == MGP_PLACE_PAIRED),
           n_keys(paired ? keys_of(bam) : 0), dups(paired ? (size_t)keys_of(bam) : 0) {
         open.assign(paired ? (size_t)n_keys + 1 : 0, ~0ull);
@@ -1533,14 +1536,18 @@ struct mgp_bam_stream {
     int64_t n_listed = 0, n_walked = 0;  // chunks whose boundaries came from the prefetch walk / were walked here
     // the pipelined decode (paired placement; MGP_BAM_PIPELINE=0 turns it off): the
     // chunk whose placement runs on `placer` and whose records are still to be written
+    static bool pipe_env() {
+        const char* e = std::getenv("MGP_BAM_PIPELINE");
+        return !e || std::strtol(e, nullptr, 10) != 0;
+    }
     bool pipe = true, fuse = true;
     ChunkRecs pend;
     bool pending = false;
     Worker placer;
-    mgp_bam_stream(mgp_bam* b, int rec_align) : bam(b), dec(b, rec_align) {
+    mgp_bam_stream(mgp_bam* b, int rec_align)
+        : bam(b), dec(b, rec_align, b->placement == MGP_PLACE_PAIRED && pipe_env() ? 2 : 0) {
         t_open = now_s();
-        if (const char* e = std::getenv("MGP_BAM_PIPELINE")) pipe = std::strtol(e, nullptr, 10) != 0;
-        pipe = pipe && dec.paired;
+        pipe = pipe_env() && dec.paired;
         st.hold = pipe;
         const char* ef = std::getenv("MGP_BAM_FUSE");  // pass 1 and the columns in one pass (pipelined)
         fuse = pipe && (!ef || std::strtol(ef, nullptr, 10) != 0);
