@@ -1295,6 +1295,14 @@ struct Decoder {
         const size_t m = q.recs.size();
         for (size_t i = 0; i < m; ++i) {
             const size_t k = q.k0 + i;
+            if ((k & 15) == 0) {  // the columns other cores just wrote: lines well ahead in flight
+                __builtin_prefetch(c.bc + k + 512);
+                __builtin_prefetch(c.start + k + 512);
+                __builtin_prefetch(c.tlen + k + 512);
+                __builtin_prefetch(c.flag + k + 512);
+                __builtin_prefetch(c.roff + k + 512, 1);
+                __builtin_prefetch(c.roff + k + 520, 1);
+            }
             if (!q.pkd[i]) {
                 cursor = (cursor + 127) & ~127ull;
                 c.roff[k] = cursor;
