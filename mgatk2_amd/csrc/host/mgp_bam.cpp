@@ -837,6 +837,7 @@ struct ChunkRecs {
     std::vector<uint32_t> ncg;
     std::vector<const uint8_t*> cgp;
     std::vector<uint8_t> pkd;
+    std::vector<uint64_t> dupbits;  // dup_stage's verdicts: thread t's bits at [t * words, (t + 1) * words)
     size_t k0 = 0;
     bool over = false;  // placement ran past the payload capacity (never: the batch cut bounds it)
 };
@@ -1282,17 +1283,43 @@ struct Decoder {
         q.ncg.swap(ncg);
         q.cgp.swap(cgp);
         q.pkd.swap(pkd);
+        q.dupbits.swap(dupbits);
         q.k0 = k0;
         q.over = false;
         clear_chunk();
     }
+    // The duplicate-key check of the current chunk (DupTracker::repeat in BAM order per
+    // cell) on the pool, cells dealt to the threads by id: a cell's reads stay in order
+    // on one thread, and each thread writes its verdicts to bits of its own. The serial
+    // placement then only reads them (it was the stream decode's critical path at C4).
+    std::vector<uint64_t> dupbits;
+    void dup_stage(size_t k0, const Cols& c) {
+        const double t0 = now_s();
+        const size_t m = recs.size(), words = (m + 63) / 64;
+        const int T = pool.size();
+        dupbits.assign((size_t)T * words, 0ull);
+        const uint16_t drop = MGP_FLAG_UNMAPPED | MGP_FLAG_SECONDARY | MGP_FLAG_SUPPLEMENTARY;
+        pool.run(T, [&](int t) {
+            uint64_t* bits = dupbits.data() + (size_t)t * words;
+            for (size_t i = 0; i < m; ++i) {
+                const size_t k = k0 + i;
+                const int32_t cc = c.bc[k];
+                if (cc < 0 || cc >= n_keys || cc % T != t || !pkd[i] || (c.flag[k] & drop)) continue;
+                if (dups.repeat((size_t)cc, c.start[k], (c.flag[k] & MGP_FLAG_REVERSE) != 0, c.tlen[k]))
+                    bits[i >> 6] |= 1ull << (i & 63);
+            }
+        });
+        t_dups += now_s() - t0;
+    }
+    double t_dups = 0;
     // placement of chunk q (serial: the line state carries over in BAM order), then the
     // free slots of the lines left open are zeroed (a later chunk may fill them; every
     // other slot gets its record)
     void place_stage(ChunkRecs& q, const Cols& c, uint64_t cap_payload) {
         const double t0 = now_s();
         const uint16_t drop = MGP_FLAG_UNMAPPED | MGP_FLAG_SECONDARY | MGP_FLAG_SUPPLEMENTARY;
-        const size_t m = q.recs.size();
+        const size_t m = q.recs.size(), words = (m + 63) / 64;
+        const int T = pool.size();
         for (size_t i = 0; i < m; ++i) {
             const size_t k = q.k0 + i;
             if ((k & 15) == 0) {  // the columns other cores just wrote: lines well ahead in flight
@@ -1311,7 +1338,8 @@ struct Decoder {
             }
             const int32_t cc = c.bc[k];
             size_t key = (cc >= 0 && cc < n_keys && !(c.flag[k] & drop)) ? (size_t)cc : (size_t)n_keys;
-            if (key < (size_t)n_keys && dups.repeat(key, c.start[k], (c.flag[k] & MGP_FLAG_REVERSE) != 0, c.tlen[k]))
+            // (dup_stage's verdict: the bits of the thread that owned the cell)
+            if (key < (size_t)n_keys && (q.dupbits[(size_t)(cc % T) * words + (i >> 6)] >> (i & 63)) & 1ull)
                 key = (size_t)n_keys;
             if (q.pkd[i] == 2) {
                 c.roff[k] = place32(key);
@@ -1566,9 +1594,10 @@ struct mgp_bam_stream {
             std::fprintf(stderr,
                          "[mgp_bam_stream] %lld records, %d threads%s: open %.3f s; waiting for inflated chunks %.3f, "
                          "record walk %.3f (listed %.3f; prefetch thread %.3f; %lld + %lld chunks), classify %.3f, fields %.3f, "
-                         "placement %.3f (waited for %.3f), records %.3f\n",
+                         "duplicate keys %.3f, placement %.3f (waited for %.3f), records %.3f\n",
                          (long long)decoded, dec.pool.size(), pipe ? ", pipelined" : "", now_s() - t_open, t_fill,
-                         t_walk, t_list, st.pf ? st.pf->t_walk : 0.0, (long long)n_listed, (long long)n_walked, t_class, dec.t_fields, dec.t_place, t_wait,
+                         t_walk, t_list, st.pf ? st.pf->t_walk : 0.0, (long long)n_listed, (long long)n_walked, t_class, dec.t_fields,
+                         dec.t_dups, dec.t_place, t_wait,
                          pipe ? dec.t_recs : dec.t_p2 - dec.t_fields - dec.t_place);
     }
     // the pending chunk's placement finished, its records written, the buffers it read released
@@ -1759,6 +1788,7 @@ int64_t mgp_bam_stream_next(mgp_bam_stream* s, int64_t cap_reads, int64_t cap_pa
                 if (s->fuse) dec.count_tags(s->decoded + (int64_t)k);
                 else dec.fields_stage(k, s->decoded + (int64_t)k, c);
                 if (!s->drain(c)) return -1;  // the chunk before: placed meanwhile, now its records
+                dec.dup_stage(k, c);          // (behind the chunk before's placement: cells in order)
                 dec.move_chunk(s->pend, k);
                 s->pending = true;
                 s->placer.submit([s, c, cap_payload] { s->dec.place_stage(s->pend, c, (uint64_t)cap_payload); });

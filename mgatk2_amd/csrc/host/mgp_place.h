@@ -38,7 +38,9 @@ class DupTracker {
 
   private:
     static constexpr uint32_t kKeys = 8;
-    struct Cell {
+    // (a cache line of its own: the stream decoder checks disjoint sets of cells on
+    // several threads at once)
+    struct alignas(64) Cell {
         int32_t start = 0;
         uint32_t n = 0;
         uint64_t key[kKeys];
