@@ -1292,20 +1292,57 @@ struct Decoder {
     // cell) on the pool, cells dealt to the threads by id: a cell's reads stay in order
     // on one thread, and each thread writes its verdicts to bits of its own. The serial
     // placement then only reads them (it was the stream decode's critical path at C4).
+    // (The reads are first dealt to their owners, T ranges counted then listed in
+    // parallel, so each thread walks only its own reads, still in BAM order.)
     std::vector<uint64_t> dupbits;
+    std::vector<uint32_t> dup_idx;
+    std::vector<size_t> dup_at;
     void dup_stage(size_t k0, const Cols& c) {
         const double t0 = now_s();
         const size_t m = recs.size(), words = (m + 63) / 64;
         const int T = pool.size();
         dupbits.assign((size_t)T * words, 0ull);
         const uint16_t drop = MGP_FLAG_UNMAPPED | MGP_FLAG_SECONDARY | MGP_FLAG_SUPPLEMENTARY;
+        auto owner = [&](size_t i) -> int {  // the thread checking read i, -1: no check
+            const size_t k = k0 + i;
+            const int32_t cc = c.bc[k];
+            if (cc < 0 || cc >= n_keys || !pkd[i] || (c.flag[k] & drop)) return -1;
+            return cc % T;
+        };
+        // counts per (range r, owner t), then every (r, t) block's place in the owner-major list
+        dup_at.assign((size_t)T * T + 1, 0);
+        pool.run(T, [&](int r) {
+            const size_t lo = m * (size_t)r / (size_t)T, hi = m * (size_t)(r + 1) / (size_t)T;
+            size_t* cnt = dup_at.data() + (size_t)r * T;
+            for (size_t i = lo; i < hi; ++i) {
+                const int o = owner(i);
+                if (o >= 0) ++cnt[o];
+            }
+        });
+        std::vector<size_t> start((size_t)T * T + 1);
+        size_t tot = 0;
+        for (int t = 0; t < T; ++t)
+            for (int r = 0; r < T; ++r) {
+                start[(size_t)r * T + t] = tot;
+                tot += dup_at[(size_t)r * T + t];
+            }
+        std::vector<size_t> seg((size_t)T + 1);  // owner t's reads: [seg[t], seg[t + 1])
+        for (int t = 0; t < T; ++t) seg[(size_t)t] = start[(size_t)t];
+        seg[(size_t)T] = tot;
+        dup_idx.resize(std::max<size_t>(tot, 1));
+        pool.run(T, [&](int r) {
+            const size_t lo = m * (size_t)r / (size_t)T, hi = m * (size_t)(r + 1) / (size_t)T;
+            size_t* at = start.data() + (size_t)r * T;
+            for (size_t i = lo; i < hi; ++i) {
+                const int o = owner(i);
+                if (o >= 0) dup_idx[at[o]++] = (uint32_t)i;
+            }
+        });
         pool.run(T, [&](int t) {
             uint64_t* bits = dupbits.data() + (size_t)t * words;
-            for (size_t i = 0; i < m; ++i) {
-                const size_t k = k0 + i;
-                const int32_t cc = c.bc[k];
-                if (cc < 0 || cc >= n_keys || cc % T != t || !pkd[i] || (c.flag[k] & drop)) continue;
-                if (dups.repeat((size_t)cc, c.start[k], (c.flag[k] & MGP_FLAG_REVERSE) != 0, c.tlen[k]))
+            for (size_t x = seg[(size_t)t]; x < seg[(size_t)t + 1]; ++x) {
+                const size_t i = dup_idx[x], k = k0 + i;
+                if (dups.repeat((size_t)c.bc[k], c.start[k], (c.flag[k] & MGP_FLAG_REVERSE) != 0, c.tlen[k]))
                     bits[i >> 6] |= 1ull << (i & 63);
             }
         });
