@@ -81,8 +81,8 @@ if has ab; then
 fi
 if has abshare; then
     # the same A/B at the 8- and 4-GPU strong-scaling shares of C4 (1250 and 2500 cells per GPU)
-    for sh in "25000000 1250" "50000000 2500"; do
-        set -- $sh
+    for sh in ${SHARES:-"25000000 1250" "50000000 2500"}; do
+        set -- ${sh//_/ }
         BARGS="--reads $1 --cells $2 --steps 20 --warmup 3 --no-cpu-baseline --no-check --no-pcie --no-device-paired --no-host-pack" \
             bash scripts/ab_bench.sh $AB > gpurun_out/abshare_${V}_$2.txt 2>&1 || { tail -30 gpurun_out/abshare_${V}_$2.txt; exit 1; }
         echo "== $2 cells"; cat gpurun_out/abshare_${V}_$2.txt
