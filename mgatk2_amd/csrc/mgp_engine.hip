@@ -134,7 +134,7 @@ struct mgp_ctx {
     int hist_slice_cells = 0;  // > 0: cap on the histogram's cells per slice (MGP_HIST_SLICE_CELLS)
     bool hist_xcd = true;      // several slices: a bin's slices dealt to one XCD (MGP_HIST_XCD)
     int hist_narrow = -1;      // 8-bit histogram counters: -1 when 32-bit ones need several slices (MGP_HIST_NARROW)
-    int64_t ga_wide_min = 16384;  // reads per pass-A workgroup from which it runs 512 threads (MGP_GA_WIDE_MIN)
+    int64_t ga_wide_min = 8192;   // reads per pass-A workgroup from which it runs 512 threads (MGP_GA_WIDE_MIN)
     int hist_bounds = 1;       // bin bounds by k_bin_bounds (MGP_HIST_BOUNDS=0: searched by each histogram workgroup)
     bool group_wide = false;   // MGP_GROUP_WIDE=1: 16-byte grouping elements always (tests, A/B)
 
@@ -3455,9 +3455,9 @@ static int run_segment(mgp_ctx* ctx, const Seg& sg, int slot, int& dup_parts, in
         auto a_lds_for = [&](int blk) {
             return (size_t)ngroups * (1 + 2 * (blk / kWave)) * 4 + (size_t)((nc + 31) / 32) * 4;
         };
-        // the 512-thread form pays with several 4096-read steps per (bin, part) workgroup;
-        // small sets (the 4- and 8-GPU shares of C4: under two steps each) run 256 threads
-        // wide (r04 A/B at 1250 / 2500 cells: 0.39 / 0.60 ms at 512 threads, 0.27 / 0.46 at 256)
+        // the 512-thread form pays with two or more 4096-read steps per (bin, part) workgroup;
+        // smaller sets (the 4- and 8-GPU shares of C4) run the 128-thread form (r04 A/B at
+        // 1250 / 2500 / 5000 cells: 0.39 / 0.60 / 0.93 ms at 512 threads, 0.22 / 0.47 / 1.07 at 128)
         const int64_t per_wg = n / std::max<int64_t>(1, (int64_t)g.nbins * kParts);
         const bool a_wide = a_lds_for(kGABlock) <= (size_t)ctx->lds_hist_max_cells * 4 && per_wg >= ctx->ga_wide_min;
         const size_t a_lds = a_lds_for(a_wide ? kGABlock : kGANBlock);
