@@ -1,24 +1,29 @@
 """Benchmark: chrM reads piled up per second (whole node), BASELINE.json's metric.
 
-One step = one pass of the hot path (mgp_run: filter + cell-major grouping +
-dedup + CIGAR-walk pileup + strand filter + per-cell stats + reference-allele
-tallies, and the RCCL all-reduce of the tallies when N > 1) over BASELINE config
-C4: ONE synthetic set of 200M chrM reads x 10k cells, `run` parameters, split by
-cell over the N GPUs (strong scaling: rank r owns a read-balanced contiguous cell
-range and exactly the reads of those cells, plus an equal share of the reads
+The step is SURVEY.md §8(d)'s engine metric: one whole pass of the hot path over
+BASELINE config C4 (ONE synthetic set of 200M chrM reads x 10k cells, `run`
+parameters, split by cell over the N GPUs: rank r owns a read-balanced contiguous
+cell range and exactly the reads of those cells, plus an equal share of the reads
 without a whitelisted barcode; the reference's per-cell parallelism,
-processors.py:112-144). Inputs are generated directly in HBM by the device
-generator (bit-identical to mgatk2_amd/synth.py); `value` is timed with them
-resident.
+processors.py:112-144), from the first SoA batch's H2D to the count matrices in host
+memory. The reads sit in pinned host batches as a streaming producer emits them
+(quality-carrying 64-byte records: the kernels apply MAPQ, base quality, end
+distance and ACGT per base, pileup.py:33-88); each push copies its batch on the
+copy stream and queues the whole hot path (filter + cell-major grouping + dedup +
+CIGAR-walk pileup + strand filter) for the windows its reads complete; mgp_run does
+the rest, the per-cell stats, the reference-allele tallies and, for N > 1, their
+RCCL all-reduce; the 16-bit count rows go to pinned host memory as their windows
+complete. `value` = reads of all ranks x K / the slowest rank's time for K steps.
 
-Around the timed steps (never inside them), rank 0 also measures:
-  * sample_check: 3 samples of 8 whole cells of the timed run, bit for bit
+Beside it (never inside the timed steps), the line carries:
+  * device: the same hot path with the inputs already resident in HBM (K x
+    mgp_run, results left in HBM) on the 32-byte records whose per-base filter the
+    producer resolved (value_device, its stage times and per-kernel rooflines),
+    and device_paired on the 64-byte records;
+  * pcie_pack32: the streamed step on 32-byte records, and a batch-size sweep;
+  * sample_check: 3 samples of 8 whole cells of the timed runs, bit for bit
     against the oracle on exactly their reads (cells are independent);
-  * pcie: SURVEY.md §8(d)'s engine metric, from the first SoA batch H2D to the
-    count matrices in host memory: pinned host batches pushed while earlier
-    windows already run (streaming, MGP_CFG_STREAM), then the 16-bit result rows
-    and per-cell statistics copied into pinned host memory (every rank, max over
-    ranks);
+  * host_pack: the producer's cost of the 32-byte records;
   * cpu_baseline (N = 1 only): the single-threaded C port of the reference's
     path on a bounded sample of the same generator.
 
@@ -47,6 +52,7 @@ sys.path.insert(0, str(ROOT))
 
 METRIC = "chrM reads piled-up/sec (whole node) at 200M reads × 10k cells; bit-exact counts"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+PCIE_PEAK_GBS = 63.0  # MI355X_MICROARCH.md: host link PCIe Gen5 x16, 63 GB/s (spec) per direction
 BYTES_PER_READ = 95  # algorithmic input bytes per L=50 read
 BYTES_PER_CELL = 16569 * 10 * 4  # int32 counts (8 planes) + tn5 (2 planes) written once
 ROW16_BYTES_PER_CELL = 16569 * 22  # the pileup's 16-bit rows: 8 + 2 + 1 u16 per position
@@ -73,18 +79,27 @@ def parse():
     ap.add_argument("--cpu-sample-reads", type=int, default=20_000_000)
     ap.add_argument("--cpu-sample-cells", type=int, default=1000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--no-check", action="store_true", help="skip the bit-exact sample check")
-    ap.add_argument("--no-pcie", action="store_true", help="skip the PCIe-inclusive (host buffers) leg")
+    ap.add_argument("--no-check", action="store_true", help="skip the bit-exact sample checks")
+    ap.add_argument("--layout", choices=["packed", "pack32"], default="packed",
+                    help="records of the headline (streamed, PCIe-inclusive) step: quality-carrying 64-byte records "
+                         "the kernel filters per base (packed, default) or 32-byte records the producer made for "
+                         "the run's min_baseq (pack32); dense in BAM order")
+    ap.add_argument("--device-only", action="store_true",
+                    help="no streamed headline: the HBM-resident device leg is the line (kernel A/B runs)")
+    ap.add_argument("--no-device", action="store_true", help="skip the HBM-resident device leg (--record-layout)")
+    ap.add_argument("--no-pcie", action="store_true",
+                    help="skip the extra streamed legs (32-byte records, batch-size sweep)")
     ap.add_argument("--no-device-paired", action="store_true",
-                    help="skip the device leg on quality-carrying 64-byte records (the kernel applies the per-base "
-                         "filter)")
+                    help="skip the resident device leg on quality-carrying 64-byte records")
     ap.add_argument("--no-host-pack", action="store_true", help="skip timing the host's 32-byte record build")
+    ap.add_argument("--no-numa-bind", action="store_true", help="do not move the rank to its GPU's NUMA node")
     ap.add_argument("--pcie-steps", type=int, default=3)
     ap.add_argument("--batch-reads", type=str, default="16000000",
-                    help="reads per pushed batch in the PCIe leg; a comma list sweeps (first = reported)")
+                    help="reads per pushed batch of the streamed legs; a comma list also sweeps the headline layout "
+                         "(untimed extra; the first is the headline's)")
     ap.add_argument("--record-layout", choices=["quad32", "pack32", "paired", "packed", "full"], default="quad32",
-                    help="payload records: 32-byte records made for the run's min_baseq, four consecutive "
-                         "records of a cell per 128-byte line (quad32, default: the placement of "
+                    help="records of the HBM-resident device leg: 32-byte records made for the run's min_baseq, "
+                         "four consecutive records of a cell per 128-byte line (quad32, default: the placement of "
                          "mgp_place_records) or in BAM order (pack32); packed 64-byte records two per line "
                          "(paired) or in BAM order (packed); or full 128-byte records")
     return ap.parse_args()
@@ -121,6 +136,37 @@ def cell_bounds(cdf: np.ndarray, world: int) -> np.ndarray:
     return partition_cells(w, world)
 
 
+def numa_bind(device: int) -> str | None:
+    """Run this rank on the CPUs of its GPU's NUMA node (before any pinned host
+    memory is allocated, so its pages land on that node): the streamed legs move
+    every read across the host link, and on a multi-socket node a batch read from
+    the other socket's memory crosses the socket link first. Best effort: the
+    node's CPUs intersected with the ones allowed; nothing is changed when the
+    PCI topology is unknown."""
+    import ctypes as C
+
+    try:
+        hip = C.CDLL("libamdhip64.so")
+        bus = C.create_string_buffer(64)
+        if hip.hipDeviceGetPCIBusId(bus, 64, int(device)) != 0:
+            return None
+        bdf = bus.value.decode().lower()
+        node = int(Path(f"/sys/bus/pci/devices/{bdf}/numa_node").read_text().strip())
+        if node < 0:
+            return None
+        cpus = set()
+        for part in Path(f"/sys/devices/system/node/node{node}/cpulist").read_text().strip().split(","):
+            a, _, b = part.partition("-")
+            cpus.update(range(int(a), int(b or a) + 1))
+        cpus &= os.sched_getaffinity(0)
+        if not cpus:
+            return None
+        os.sched_setaffinity(0, cpus)
+        return f"node {node} ({len(cpus)} cpus) for GPU {bdf}"
+    except Exception:
+        return None
+
+
 def main():
     args = parse()
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
@@ -130,8 +176,8 @@ def main():
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if args.gpus != world:
         print(f"[bench] --gpus {args.gpus} but WORLD_SIZE {world}: running {world} ranks", file=sys.stderr)
-    if args.record_layout in ("paired", "quad32", "pack32") and args.read_len > 50:
-        raise SystemExit(f"--record-layout {args.record_layout} needs --read-len <= 50 (packed records)")
+    if args.read_len > 50:
+        raise SystemExit("the packed record layouts need --read-len <= 50")
     dist = None
     if world > 1:
         import torch.distributed as tdist
@@ -139,7 +185,7 @@ def main():
         tdist.init_process_group("gloo", rank=rank, world_size=world)
         dist = tdist
 
-    from mgatk2_amd.engine import Engine, EngineConfig
+    from mgatk2_amd.engine import EngineConfig
     from mgatk2_amd.synth import cell_cdf, ref_codes
 
     def barrier():
@@ -157,6 +203,7 @@ def main():
 
     no_comm = os.environ.get("MGP_BENCH_NO_COMM") == "1"
     device = 0 if no_comm else local_rank
+    numa = None if args.no_numa_bind else numa_bind(device)
     n_glob, nc_glob = args.reads, args.cells
     seed = args.seed + (1_000_003 * rank if args.weak else 0)
     cdf, ref = cell_cdf(seed, nc_glob), ref_codes(args.seed)  # one chrM reference for every rank
@@ -170,124 +217,65 @@ def main():
     n_cells = hi - lo
     cfg = EngineConfig(n_cells=n_cells, min_baseq=20, min_mapq=30, min_distance_from_end=5,
                        dedup_mode="alignment_and_fragment_length", max_strand_bias=1.0, min_reads=1)
-    eng = Engine(cfg, device=device)
-    t0 = time.time()
-    lay = args.record_layout
-    packed = lay in ("packed", "paired", "pack32", "quad32")
-    p32 = cfg.min_baseq if lay in ("pack32", "quad32") else None  # 32-byte records for the run's min_baseq
-    eng.synth(seed, n_glob, cdf, ref, read_len=args.read_len, rec_align=64 if packed else 128, pack=packed,
-              pack32=p32, **shard)
-    n_res, pay = eng.resident()
-    if lay in ("paired", "quad32"):
-        # the producer's placement (mgp_place_records, as the BAM decoder emits it):
-        # computed on the host from the generated barcode and flag columns, then the
-        # same reads are generated again at those offsets
-        from mgatk2_amd.bam import PLACE_PAIRED, place_records
-
-        soa = eng.download_inputs(columns=("bc", "flag", "start", "tlen"))
-        roff, pay_b = place_records(soa.bc, soa.flag, np.full(n_res, 32 if p32 is not None else 64, np.uint32),
-                                    n_cells, PLACE_PAIRED, start=soa.start, tlen=soa.tlen)
-        del soa
-        eng.synth(seed, n_glob, cdf, ref, read_len=args.read_len, rec_align=64, pack=True, rec_off=roff,
-                  payload_bytes=pay_b, pack32=p32, **shard)
-        del roff
-    n_res, pay = eng.resident()
-    t_gen = time.time() - t0
-    print(f"[bench] rank {rank}: cells [{lo}, {hi}), {n_res:,} reads ({pay / 1e9:.2f} GB payload) generated "
-          f"on device {device} in {t_gen:.1f}s", file=sys.stderr, flush=True)
 
     # MGP_BENCH_NO_COMM=1: rehearse the multi-process path with several ranks on one
     # GPU (RCCL refuses two ranks on one device); the tallies are then not reduced
     def make_comm(e):
+        from mgatk2_amd.engine import Engine
+
         uid = Engine.comm_unique_id() if rank == 0 else b"\0" * 128
         obj = [uid]
         dist.broadcast_object_list(obj, src=0)
         e.comm_init(obj[0], world, rank)
 
-    comm_ranks = 1
-    if world > 1 and not no_comm:
-        make_comm(eng)
-        comm_ranks = world
+    comm = make_comm if world > 1 and not no_comm else None
+    comm_ranks = world if comm is not None else 1
+    ctx = Ctx(args, cfg, seed, cdf, ref, shard, device, comm, barrier, reduce, rank, world, lo)
 
-    # the timed runs bracket only the pileup with HIP events (its roofline); every
-    # other stage boundary would add a marker between two kernels of the stream
-    eng.set_stage_timing(os.environ.get("MGP_BENCH_ALL_STAGES") == "1")  # (=1: every stage timed, for A/B)
-    for _ in range(args.warmup):
-        eng.run()
-        eng.sync()
-
-    barrier()
-    eng.sync() if args.warmup else None
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        eng.run()
-    eng.sync()
-    barrier()
-    dt_rank = time.perf_counter() - t0
-    dt = reduce(dt_rank, "max")
-
-    kt = eng.kernel_times(last_runs=min(args.steps, 64))
-    # the per-stage breakdown from a few more (untimed) runs with every stage bracketed
-    n_prof = min(3, max(args.steps, 1))
-    eng.set_stage_timing(True)
-    for _ in range(n_prof):
-        eng.run()
-    eng.sync()
-    kt_all = eng.kernel_times(last_runs=n_prof)
-    res = eng.fetch(dense=False)
-    total_reads = reduce(float(n_res), "sum")
-    value = total_reads * args.steps / dt
-    ms_step = dt / args.steps * 1e3
-
-    # roofline of the dominant kernel: its own algorithmic bytes per launch (kernel_rooflines)
-    # over its HIP-event time on the compute stream, averaged over the timed steps; the
-    # whole step against SURVEY.md §8(d)'s engine-level count (95 B per read + the u32
-    # result rows per cell) is step_achieved / step_frac
-    dom = "pileup"
-    kernels = kernel_rooflines(kt_all, n_res, n_cells, res.stats, cfg, args.record_layout)
-    alg_bytes = kernel_bytes(n_res, n_cells, res.stats, cfg, args.record_layout)[dom]
-    achieved = alg_bytes / (kt[dom] * 1e-3) / 1e9
-    engine_bytes = n_res * BYTES_PER_READ + n_cells * BYTES_PER_CELL
-    step_achieved = engine_bytes / (dt_rank / args.steps) / 1e9
-    traffic = None
-    pmc = ROOT / "profiles" / "pmc_traffic.json"
-    if pmc.exists():
-        try:
-            d = json.loads(pmc.read_text())
-            if (d.get("reads") == n_res and d.get("cells") == n_cells
-                    and d.get("record_layout", "full") == args.record_layout):
-                traffic = d.get(dom)
-        except Exception:
-            traffic = None
-
-    check = None
-    if rank == 0 and not args.no_check:
-        check = sample_check(eng, cfg, res, args, seed, cdf, ref, lo, device)
-    eng.close()
-
-    # the same workload on quality-carrying 64-byte records two per line: the kernel
-    # applies min_baseq / end distance / ACGT per base (pileup.py:67-86), which the
-    # headline's 32-byte records carry resolved (built by the producer, timed below)
+    # the headline: SURVEY.md §8(d)'s engine metric, timed over K whole passes of the
+    # hot path from the first SoA batch's H2D to every count row and per-cell
+    # statistic in pinned host memory, on the quality-carrying 64-byte records (the
+    # kernels apply MAPQ, base quality, end distance and ACGT per base)
+    head = None
+    if not args.device_only:
+        head = stream_leg(ctx, args.layout, [int(args.batch_reads.split(",")[0])], timed=True)
+    # the same hot path with the inputs already resident in HBM (the device's own rate),
+    # on the 32-byte records whose per-base filter the producer resolved (value_device)
+    # and on the 64-byte records the kernel filters (device_paired)
+    dev = None
+    if not args.no_device:
+        dev = device_leg(ctx, args.record_layout)
     paired = None
-    if not args.no_device_paired and args.record_layout == "quad32":
-        paired = device_leg(args, cfg, seed, cdf, ref, shard, device, make_comm if comm_ranks > 1 else None,
-                            barrier, reduce, "paired")
+    if not args.device_only and not args.no_device_paired and args.record_layout != "paired":
+        paired = device_leg(ctx, "paired")
     host_pack = None
-    if rank == 0 and not args.no_host_pack and args.record_layout in ("quad32", "pack32"):
+    if rank == 0 and not args.no_host_pack:
         host_pack = host_pack_leg(args, cfg, device)
-
-    pcie = None
+    # the streamed leg on the 32-byte records and the batch-size sweep (untimed extras)
+    pcie_more = None
     if not args.no_pcie:
-        pcie = pcie_leg(args, cfg, seed, cdf, ref, shard, device, comm_ranks, barrier, reduce, make_comm)
-
+        sweep = [int(x) for x in str(args.batch_reads).split(",") if x.strip()]
+        pcie_more = stream_leg(ctx, "pack32", sweep[:1], timed=False)
+        if len(sweep) > 1 and not args.device_only:
+            pcie_more["sweep_" + args.layout] = stream_leg(ctx, args.layout, sweep, timed=False)["legs"]
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(args, cfg, local_rank)
 
     if rank == 0:
+        main_leg = head if head is not None else dev
+        ms_step = main_leg["ms_per_step"]
+        workload = (f"{workload_name(n_glob, nc_glob)}: {n_glob / 1e6:g}M chrM reads x {nc_glob / 1e3:g}k "
+                    f"cells{' per GPU' if args.weak else ' (one set, split by cell over the GPUs)'}, "
+                    f"run params (q20, mapq30, dedup=alignment_and_fragment_length, min_reads 1), "
+                    f"L={args.read_len}")
+        if head is not None:
+            workload += (f"; one step = {head['batches']} pinned host batches of {head['batch_reads'] / 1e6:g}M "
+                         f"reads streamed H2D -> streamed hot path -> count rows + per-cell stats in pinned host "
+                         f"memory")
         out = {
             "metric": METRIC,
-            "value": value,
+            "value": main_leg["value"],
             "unit": "reads/s",
             "n_gpus": world,
             "steps": args.steps,
@@ -297,99 +285,162 @@ def main():
             "scaling": "weak" if args.weak else "strong",
             "vs_baseline": None,
             "dtype": "u32",
-            "data": "synthetic (SURVEY.md §8(d) generator, created in HBM by the device generator)",
-            "bit_exact": None if check is None else check["bit_exact"],
+            "data": "synthetic (SURVEY.md §8(d) generator, created in HBM by the device generator; for the streamed "
+                    "step copied into pinned host batches before the timed region)",
+            "bit_exact": None if main_leg.get("sample_check") is None else main_leg["sample_check"]["bit_exact"],
             "config": {
-                "workload": f"{workload_name(n_glob, nc_glob)}: {n_glob / 1e6:g}M chrM reads x {nc_glob / 1e3:g}k "
-                            f"cells{' per GPU' if args.weak else ' (one set, split by cell over the GPUs)'}, "
-                            f"run params (q20, mapq30, dedup=alignment_and_fragment_length, min_reads 1), "
-                            f"L={args.read_len}",
-                "reads_rank0": n_res,
+                "workload": workload,
+                "timed_region": main_leg["timed_region"],
+                "reads_rank0": main_leg["reads_rank0"],
                 "cells_rank0": n_cells,
-                "payload_bytes_rank0": pay,
-                "record_layout": args.record_layout,
+                "record_layout": main_leg["record_layout"],
                 "parallelism": f"cell-sharded x{world} (RCCL all-reduce of ref tallies over {comm_ranks} ranks)",
-                "rank0_step_ms": dt_rank / args.steps * 1e3,
+                "rank0_step_ms": main_leg["rank0_step_ms"],
+                "numa": numa,
             },
-            "roofline": {
-                "bound": "hbm",
-                "kernel": dom,
-                "achieved": achieved,
-                "peak": HBM_PEAK_GBS,
-                "unit": "GB/s",
-                "frac": achieved / HBM_PEAK_GBS,
-                "traffic": traffic,
-                "alg_bytes_per_launch": alg_bytes,
-                "alg_bytes_what": f"4-byte pileup element + one {RECORD_BYTES[args.record_layout]}-byte record per "
-                                  f"kept read, 16-bit result rows ({ROW16_BYTES_PER_CELL} B) per cell",
-                "engine_alg_bytes_per_step": engine_bytes,
-                "step_achieved": step_achieved,
-                "step_frac": step_achieved / HBM_PEAK_GBS,
-                "kernels": kernels,
-            },
-            "stage_ms": {k: round(v, 4) for k, v in kt_all.items()},
-            # value is the HBM-resident rate (the task's bench contract: inputs resident
-            # when the timed region starts); SURVEY.md §8(d)'s engine metric, from the first
-            # H2D to the counts in host memory, is value_pcie
-            "value_device": value,
-            "value_pcie": None if pcie is None else pcie["value"],
+            "roofline": main_leg["roofline"],
+            "stage_ms": main_leg.get("stage_ms"),
+            "value_pcie": None if head is None else head["value"],
+            "value_device": None if dev is None else dev["value"],
+            "device_ms_quad32": None if dev is None else dev["ms_per_step"],
             "device_ms_paired": None if paired is None else paired["ms_per_step"],
+            "link": None if head is None else head["link"],
+            "stream": None if head is None else {k: head[k] for k in ("batch_reads", "batches", "segments_per_run",
+                                                                     "pileup_launches_per_run", "h2d_bytes_rank0",
+                                                                     "d2h_bytes_rank0", "rows_target")},
+            "device": dev,
             "device_paired": paired,
+            "pcie_pack32": pcie_more,
             "host_pack_ns_per_read": None if host_pack is None else host_pack["ns_per_read_1thread"],
             "host_pack": host_pack,
-            "pcie": pcie,
             "cpu_baseline": cpu,
-            "stats_rank0": res.stats,
-            "sample_check": check,
+            "stats_rank0": main_leg.get("stats"),
+            "sample_check": main_leg.get("sample_check"),
         }
         print(json.dumps(out), flush=True)
     if dist is not None:
         dist.destroy_process_group()
 
 
-def device_leg(args, cfg, seed, cdf, ref, shard, device, make_comm, barrier, reduce, layout: str) -> dict:
-    """The timed steps again on another record layout of the same reads (untimed
-    generation): ms per step (max over ranks) and the stage times."""
+class Ctx:
+    """What every leg of one rank needs."""
+
+    def __init__(self, args, cfg, seed, cdf, ref, shard, device, comm, barrier, reduce, rank, world, cell0):
+        self.args, self.cfg, self.seed, self.cdf, self.ref, self.shard = args, cfg, seed, cdf, ref, shard
+        self.device, self.comm, self.barrier, self.reduce = device, comm, barrier, reduce
+        self.rank, self.world, self.cell0 = rank, world, cell0
+
+
+def pmc_traffic(key: str, n: int, nc: int, layout: str) -> dict | None:
+    """The pileup's PMC traffic for this workload (profiles/pmc_traffic*.json, from
+    scripts/pmc_traffic.py: 2 x FETCH_SIZE + WRITE_SIZE per launch, gfx950 correction)."""
+    f = ROOT / "profiles" / ("pmc_traffic.json" if key == "device" else f"pmc_traffic_{key}.json")
+    if not f.exists():
+        return None
+    try:
+        d = json.loads(f.read_text())
+        if d.get("reads") == n and d.get("cells") == nc and d.get("record_layout") == layout:
+            return d
+    except Exception:
+        pass
+    return None
+
+
+def device_leg(ctx: Ctx, layout: str) -> dict:
+    """The hot path with its inputs resident in HBM: K runs of mgp_run (untimed
+    generation on the device), ms per step (max over ranks), the stage times, the
+    per-kernel rooflines and, on rank 0, the bit-exact sample check."""
     from mgatk2_amd.bam import PLACE_PAIRED, place_records
     from mgatk2_amd.engine import Engine
 
-    eng = Engine(cfg, device=device)
-    eng.synth(seed, args.reads, cdf, ref, read_len=args.read_len, rec_align=64, pack=True, **shard)
-    n_res, _ = eng.resident()
-    if layout == "paired":
+    args, cfg = ctx.args, ctx.cfg
+    eng = Engine(cfg, device=ctx.device)
+    packed = layout in ("packed", "paired", "pack32", "quad32")
+    p32 = cfg.min_baseq if layout in ("pack32", "quad32") else None  # 32-byte records for the run's min_baseq
+    t0 = time.time()
+    eng.synth(ctx.seed, args.reads, ctx.cdf, ctx.ref, read_len=args.read_len, rec_align=64 if packed else 128,
+              pack=packed, pack32=p32, **ctx.shard)
+    n_res, pay = eng.resident()
+    if layout in ("paired", "quad32"):
+        # the producer's placement (mgp_place_records, as the BAM decoder emits it):
+        # computed on the host from the generated barcode and flag columns, then the
+        # same reads are generated again at those offsets
         soa = eng.download_inputs(columns=("bc", "flag", "start", "tlen"))
-        roff, pay_b = place_records(soa.bc, soa.flag, np.full(n_res, 64, np.uint32), cfg.n_cells, PLACE_PAIRED,
-                                    start=soa.start, tlen=soa.tlen)
+        roff, pay_b = place_records(soa.bc, soa.flag, np.full(n_res, 32 if p32 is not None else 64, np.uint32),
+                                    cfg.n_cells, PLACE_PAIRED, start=soa.start, tlen=soa.tlen)
         del soa
-        eng.synth(seed, args.reads, cdf, ref, read_len=args.read_len, rec_align=64, pack=True, rec_off=roff,
-                  payload_bytes=pay_b, **shard)
+        eng.synth(ctx.seed, args.reads, ctx.cdf, ctx.ref, read_len=args.read_len, rec_align=64, pack=True,
+                  rec_off=roff, payload_bytes=pay_b, pack32=p32, **ctx.shard)
         del roff
-    if make_comm is not None:
-        make_comm(eng)
-    eng.set_stage_timing(False)
+    n_res, pay = eng.resident()
+    print(f"[bench] rank {ctx.rank}: device leg {layout}: {n_res:,} reads ({pay / 1e9:.2f} GB payload) generated "
+          f"on device {ctx.device} in {time.time() - t0:.1f}s", file=sys.stderr, flush=True)
+    if ctx.comm is not None:
+        ctx.comm(eng)
+    # the timed runs bracket only the pileup with HIP events (its roofline); every
+    # other stage boundary would add a marker between two kernels of the stream
+    eng.set_stage_timing(os.environ.get("MGP_BENCH_ALL_STAGES") == "1")  # (=1: every stage timed, for A/B)
     for _ in range(max(1, args.warmup)):
         eng.run()
     eng.sync()
-    barrier()
+    ctx.barrier()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         eng.run()
     eng.sync()
-    barrier()
-    dt = reduce(time.perf_counter() - t0, "max")
-    pile = eng.kernel_times(last_runs=min(args.steps, 64)).get("pileup")
+    ctx.barrier()
+    dt_rank = time.perf_counter() - t0
+    dt = ctx.reduce(dt_rank, "max")
+    kt = eng.kernel_times(last_runs=min(args.steps, 64))
+    # the per-stage breakdown from a few more (untimed) runs with every stage bracketed
     eng.set_stage_timing(True)
     for _ in range(3):
         eng.run()
     eng.sync()
-    kt = eng.kernel_times(last_runs=3)
-    st = eng.fetch(dense=False).stats
+    kt_all = eng.kernel_times(last_runs=3)
+    res = eng.fetch(dense=False)
+    nc = cfg.n_cells
+    # roofline of the dominant kernel: its own algorithmic bytes per launch over its
+    # HIP-event time on the compute stream, averaged over the timed steps; the whole
+    # step against SURVEY.md §8(d)'s engine-level count is step_achieved / step_frac
+    dom = "pileup"
+    alg = kernel_bytes(n_res, nc, res.stats, cfg, layout)[dom]
+    achieved = alg / (kt[dom] * 1e-3) / 1e9
+    engine_bytes = n_res * BYTES_PER_READ + nc * BYTES_PER_CELL
+    step_achieved = engine_bytes / (dt_rank / args.steps) / 1e9
+    pmc = pmc_traffic("device", n_res, nc, layout)
+    check = None
+    if ctx.rank == 0 and not args.no_check:
+        check = sample_check(eng, cfg, res, args, ctx.seed, ctx.cdf, ctx.ref, ctx.cell0, ctx.device)
     eng.close()
-    return {"record_layout": layout, "what": "packed 64-byte records (qualities and base codes; the kernel applies "
-            "min_baseq, min_distance_from_end and ACGT per base), two of a cell per 128-byte line",
-            "ms_per_step": dt / args.steps * 1e3, "value": reduce(float(n_res), "sum") * args.steps / dt,
-            "pileup_ms": pile, "stage_ms": {k: round(v, 4) for k, v in kt.items()},
-            "filtered_reads_rank0": st["filtered_reads"], "error_bits": st["error_bits"]}
+    return {
+        "record_layout": layout,
+        "what": {"quad32": "32-byte records made for the run's min_baseq (per-base filter resolved by the producer), "
+                           "four of a cell per 128-byte line",
+                 "paired": "packed 64-byte records (qualities and base codes; the kernel applies min_baseq, "
+                           "min_distance_from_end and ACGT per base), two of a cell per 128-byte line"}.get(layout, layout),
+        "timed_region": "K x mgp_run on inputs resident in HBM (results left in HBM)",
+        "value": ctx.reduce(float(n_res), "sum") * args.steps / dt,
+        "ms_per_step": dt / args.steps * 1e3,
+        "rank0_step_ms": dt_rank / args.steps * 1e3,
+        "reads_rank0": n_res,
+        "payload_bytes_rank0": pay,
+        "stage_ms": {k: round(v, 4) for k, v in kt_all.items()},
+        "roofline": {
+            "bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": achieved / HBM_PEAK_GBS, "traffic": None if pmc is None else pmc.get(dom),
+            "alg_bytes_per_launch": alg, "launches_per_step": 1, "avg_launch_ms": kt[dom],
+            "alg_bytes_what": f"4-byte pileup element + one {RECORD_BYTES[layout]}-byte record per kept read, "
+                              f"16-bit result rows ({ROW16_BYTES_PER_CELL} B) per cell",
+            "engine_alg_bytes_per_step": engine_bytes, "step_achieved": step_achieved,
+            "step_frac": step_achieved / HBM_PEAK_GBS,
+            "kernels": kernel_rooflines(kt_all, n_res, nc, res.stats, cfg, layout),
+        },
+        "stats": res.stats,
+        "filtered_reads_rank0": res.stats["filtered_reads"],
+        "error_bits": res.stats["error_bits"],
+        "sample_check": check,
+    }
 
 
 def host_pack_leg(args, cfg, device, n: int = 4_000_000) -> dict:
@@ -493,22 +544,27 @@ def sample_check(eng, cfg, res, args, seed, cdf, ref, cell0: int, device: int) -
             "sampled cells' reads", "seconds": round(time.perf_counter() - t0, 2)}
 
 
-def pcie_leg(args, cfg, seed, cdf, ref, shard, device, comm_ranks, barrier, reduce, make_comm) -> dict:
-    """SURVEY.md §8(d)'s engine metric: host SoA batches in pinned memory -> pushed
-    (H2D on the copy stream; with streaming on, each push runs the windows its reads
-    complete, overlapping the next batches' copies) -> mgp_run -> the 16-bit result
-    rows and per-cell statistics in pinned host memory. The rank's reads are the
-    same as the timed run's, in the dense packed layout a streaming producer emits
-    (records in BAM order: a batch is a contiguous payload range)."""
-    from mgatk2_amd.engine import Engine, EngineConfig, PinnedBuffer, Rows16
+def stream_leg(ctx: Ctx, layout: str, batch_list: list[int], timed: bool) -> dict:
+    """SURVEY.md §8(d)'s engine metric: the rank's reads in pinned host SoA batches
+    (dense records in BAM order, as a streaming producer emits them: a batch is a
+    contiguous payload range) -> pushed (H2D on the copy stream; with streaming on,
+    each push runs the whole hot path for the windows its reads complete, overlapping
+    the next batches' copies) -> mgp_run -> the 16-bit count rows (written into the
+    pinned target as windows complete) and the per-cell statistics in pinned host
+    memory. timed: the bench's step (W warmup passes, K timed passes bracketed by
+    barrier + device sync, max over ranks), with the pileup's HIP events (every
+    segment's launch) for the roofline and the bit-exact sample check; otherwise the
+    best of --pcie-steps passes per batch size, streamed and not."""
+    from mgatk2_amd.engine import Engine, PinnedBuffer, Rows16
     from mgatk2_amd.synth import ReadSoA
 
-    batch_list = [int(x) for x in str(args.batch_reads).split(",") if x.strip()]
-    scfg = EngineConfig(**{**cfg.__dict__})
-    eng = Engine(scfg, device=device)
-    p32 = cfg.min_baseq if args.record_layout in ("pack32", "quad32") else None
+    args, cfg = ctx.args, ctx.cfg
+    eng = Engine(cfg, device=ctx.device)
+    p32 = cfg.min_baseq if layout == "pack32" else None
     rb = 32 if p32 is not None else 64  # dense records in BAM order
-    eng.synth(seed, args.reads, cdf, ref, read_len=args.read_len, rec_align=64, pack=True, pack32=p32, **shard)
+    t0 = time.time()
+    eng.synth(ctx.seed, args.reads, ctx.cdf, ctx.ref, read_len=args.read_len, rec_align=64, pack=True, pack32=p32,
+              **ctx.shard)
     n, pay = eng.resident()
     # the producer's columns: bc, tlen, flag, mapq. No rec_off (dense records in BAM
     # order) and no span (taken from the records' CIGARs on the device): ABI v3.1; no
@@ -530,8 +586,10 @@ def pcie_leg(args, cfg, seed, cdf, ref, shard, device, comm_ranks, barrier, redu
     rbuf = PinnedBuffer(nc * L * 22 + nc * nw + 4096)
     rows = Rows16(rbuf.array((nc, L, 8), np.uint16, 0), rbuf.array((nc, L, 2), np.uint16, nc * L * 16),
                   rbuf.array((nc, L), np.uint16, nc * L * 20), rbuf.array((nc, nw), np.uint8, nc * L * 22), W)
-    if comm_ranks > 1:
-        make_comm(eng)  # every run all-reduces its tallies, as in the timed steps
+    print(f"[bench] rank {ctx.rank}: stream leg {layout}: {n:,} reads ({(col_bytes + pay) / 1e9:.2f} GB pinned) "
+          f"ready in {time.time() - t0:.1f}s", file=sys.stderr, flush=True)
+    if ctx.comm is not None:
+        ctx.comm(eng)  # every run all-reduces its tallies
     # the rows leave the device as the windows complete, beside the later batches' H2D
     try:
         eng.set_rows16_target(rows)
@@ -539,6 +597,7 @@ def pcie_leg(args, cfg, seed, cdf, ref, shard, device, comm_ranks, barrier, redu
     except Exception as e:  # (pinned memory the device cannot map: copy the rows after the run)
         print(f"[bench] rows target unavailable ({e}); rows fetched after the run", file=sys.stderr)
         rows_target = False
+    eng.set_stage_timing(False)  # HIP events around the pileup launches only
 
     def batches_for(bs):
         """Batches of bs reads: their columns and their slice of the dense payload."""
@@ -548,51 +607,105 @@ def pcie_leg(args, cfg, seed, cdf, ref, shard, device, comm_ranks, barrier, redu
     def one(batches, stream):
         eng.set_streaming(stream)
         eng.reset()
-        t0 = time.perf_counter()
         for bt in batches:
             eng.push(bt)
-        t_push = time.perf_counter() - t0
         eng.run()
         if not rows_target:
             eng.fetch_rows16(0, nc, out=rows)
-        r = eng.fetch(dense=False)  # (waits for the rows' copies too)
-        return time.perf_counter() - t0, t_push, r
+        return eng.fetch(dense=False)  # (waits for the rows' copies too)
 
-    legs = []
-    for bs in batch_list:
-        batches = batches_for(bs)
-        one(batches, True)  # warmup (allocations)
-        for stream in (True, False):
-            ts = []
-            seg0 = eng.stream_info()[0]
-            for _ in range(args.pcie_steps):
-                barrier()
-                dt, t_push, r = one(batches, stream)
-                ts.append((dt, t_push))
-            segs = (eng.stream_info()[0] - seg0) // max(1, args.pcie_steps)
-            dt = min(t for t, _ in ts)
-            dt_max = reduce(dt, "max")
-            legs.append({"batch_reads": bs, "batches": len(batches), "streamed": stream, "segments": int(segs),
-                         "s": dt_max, "push_s": round(min(p for _, p in ts), 4),
-                         "value": reduce(float(n), "sum") / dt_max})
-    stats = r.stats
     h2d = col_bytes + pay
     d2h = nc * L * 22 + nc * nw + nc * 34 + L * 4 * 8  # rows, wide flags, per-cell arrays, tallies
-    best = legs[0]
+    if not timed:
+        legs = []
+        for bs in batch_list:
+            batches = batches_for(bs)
+            one(batches, True)  # warmup (allocations)
+            for stream in (True, False):
+                ts = []
+                seg0 = eng.stream_info()[0]
+                for _ in range(args.pcie_steps):
+                    ctx.barrier()
+                    t1 = time.perf_counter()
+                    r = one(batches, stream)
+                    ts.append(time.perf_counter() - t1)
+                segs = (eng.stream_info()[0] - seg0) // max(1, args.pcie_steps)
+                dt_max = ctx.reduce(min(ts), "max")
+                legs.append({"batch_reads": bs, "batches": len(batches), "streamed": stream, "segments": int(segs),
+                             "s": dt_max, "value": ctx.reduce(float(n), "sum") / dt_max})
+        eng.close()
+        best = max((lg for lg in legs if lg["streamed"]), key=lambda lg: lg["value"])
+        return {"record_layout": layout, "value": best["value"], "best_batch_reads": best["batch_reads"],
+                "h2d_bytes_rank0": h2d, "d2h_bytes_rank0": d2h,
+                "link_GBps_rank0": round((h2d + d2h) / best["s"] / 1e9, 2), "legs": legs,
+                "stats_total_reads_rank0": r.stats["total_reads"]}
+
+    bs = batch_list[0]
+    batches = batches_for(bs)
+    for _ in range(max(1, args.warmup)):
+        one(batches, True)
+    seg0 = eng.stream_info()[0]
+    ctx.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        res = one(batches, True)
+    ctx.barrier()
+    dt_rank = time.perf_counter() - t0
+    dt = ctx.reduce(dt_rank, "max")
+    segs = (eng.stream_info()[0] - seg0) / max(1, args.steps)
+    streamed = eng.stream_info()[1]
+    kt = eng.kernel_times(last_runs=min(args.steps, 64))
+    pile_ms = kt.get("pileup", 0.0)  # per run: every segment's launch + the run's last one
+    launches = segs + 1
+    dom = "pileup"
+    alg = kernel_bytes(n, nc, res.stats, cfg, "packed" if rb == 64 else "pack32")[dom]
+    achieved = alg / (pile_ms * 1e-3) / 1e9 if pile_ms > 0 else None
+    pmc = pmc_traffic("stream", n, nc, layout)
+    step_s = dt_rank / args.steps
+    check = None
+    if ctx.rank == 0 and not args.no_check:
+        check = sample_check(eng, cfg, res, args, ctx.seed, ctx.cdf, ctx.ref, ctx.cell0, ctx.device)
     eng.close()
     return {
-        "value": best["value"],
-        "unit": "reads/s",
-        "what": "pinned host SoA batches (bc, tlen, flag, mapq + dense 32-byte records; no rec_off or span "
-                "columns: ABI v3.1, no start column: ABI 4, the engine takes them from the records) -> H2D (streamed: windows run as their reads arrive, and their 16-bit count rows "
-                "go back D2H as each window completes) -> run -> every row + per-cell stats in pinned host memory; "
-                "max over ranks",
+        "record_layout": layout,
+        "what": {"packed": "packed 64-byte records (qualities and base codes: the kernel applies min_baseq, "
+                           "min_distance_from_end and ACGT per base), dense in BAM order",
+                 "pack32": "32-byte records made for the run's min_baseq (per-base filter resolved by the producer), "
+                           "dense in BAM order"}[layout],
+        "timed_region": "K passes of: reset -> push every pinned host batch (H2D on the copy stream; each push "
+                        "queues the hot path of the windows its reads complete) -> mgp_run -> every 16-bit count row "
+                        "(written into pinned host memory as its windows complete) and the per-cell statistics on "
+                        "the host",
+        "value": ctx.reduce(float(n), "sum") * args.steps / dt,
+        "ms_per_step": dt / args.steps * 1e3,
+        "rank0_step_ms": step_s * 1e3,
+        "reads_rank0": n,
+        "batch_reads": bs,
+        "batches": len(batches),
+        "streamed": bool(streamed),
+        "segments_per_run": segs,
+        "pileup_launches_per_run": launches,
         "h2d_bytes_rank0": h2d,
         "d2h_bytes_rank0": d2h,
-        "link_GBps_rank0": round((h2d + d2h) / best["s"] / 1e9, 2),
         "rows_target": rows_target,
-        "legs": legs,
-        "stats_total_reads_rank0": stats["total_reads"],
+        "link": {"bound": "pcie", "h2d_GBps": round(h2d / step_s / 1e9, 2), "d2h_GBps": round(d2h / step_s / 1e9, 2),
+                 "peak_GBps_per_direction": PCIE_PEAK_GBS, "h2d_frac": round(h2d / step_s / 1e9 / PCIE_PEAK_GBS, 3),
+                 "what": "H2D bytes of the step (columns + records) over the step time, rank 0; PCIe Gen5 x16 spec "
+                         "(MI355X_MICROARCH.md)"},
+        "stage_ms": {"pileup_per_run": round(pile_ms, 4)},
+        "roofline": {
+            "bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": None if achieved is None else achieved / HBM_PEAK_GBS,
+            "traffic": None if pmc is None else pmc.get(dom),
+            "alg_bytes_per_launch": alg / launches, "launches_per_step": launches,
+            "avg_launch_ms": pile_ms / launches,
+            "alg_bytes_what": f"per step (all launches): 4-byte pileup element + one {rb}-byte record per kept read, "
+                              f"16-bit result rows ({ROW16_BYTES_PER_CELL} B) per cell; per launch = / launches",
+            "time_what": "HIP events around every pileup launch of the timed steps (the streaming segments' and the "
+                         "run's own), summed per step",
+        },
+        "stats": res.stats,
+        "sample_check": check,
     }
 
 

@@ -123,11 +123,24 @@ struct mgp_ctx {
     mgp_rows16 rows_tgt{};
     bool rows_on = false;
     hipEvent_t ev_copy = nullptr, ev_fork = nullptr, ev_join = nullptr;
+    // a pushed batch's payload copy split over h2d_split streams (MGP_H2D_SPLIT; the
+    // extra streams and their events are created on the first split copy)
+    int h2d_split = 1;
+    int seg_min_win = 1;  // a streaming push queues a segment once this many windows are complete (MGP_SEG_MIN_WIN)
+    hipStream_t s_cx[3] = {nullptr, nullptr, nullptr};
+    hipEvent_t ev_cx[3] = {nullptr, nullptr, nullptr}, ev_cfork = nullptr;
     hipEvent_t ev_bits = nullptr;  // the run's input check words have reached h_bits
     uint32_t* h_bits = nullptr;    // pinned host copy of the input check words (roff_irregular)
     static constexpr int kRing = 64;   // per-run event slots (timing over many runs without syncs)
     hipEvent_t ev[kRing][ST_N][2];
     bool stage_ran[kRing][ST_N]{};
+    // a streaming run's segment pileups (each mgp_push_batch that completes windows
+    // launches one): HIP event pairs per run slot, created on the first streaming
+    // segment; seg_n = segments recorded for the slot's run (kSegEv + 1: more than
+    // kSegEv, the run's pileup is then untimed)
+    static constexpr int kSegEv = 24;
+    std::vector<hipEvent_t> seg_ev;
+    int seg_n[kRing]{};
     int64_t runs = 0;                  // completed mgp_run calls
     Geom g{};
     int lds_hist_max_cells = 0;
@@ -659,8 +672,9 @@ constexpr int kGABlock = MGP_GA_BLOCK;
 #endif
 constexpr int kGANBlock = MGP_GA_NBLOCK;
 // kCompact: 8-byte elements (GCompact, below; kOff is then dense or u32). kBlk: threads
-// per workgroup (kBlk, or 256 when kBlk's per-wave group counters do not fit the
-// LDS: more than ~140k cells)
+// per workgroup. run_segment launches kGABlock (512) when its per-wave group counters
+// fit the LDS and a (bin, part) workgroup gets at least MGP_GA_WIDE_MIN reads, else
+// kGANBlock (128): small sets (the multi-GPU shares) and more than ~140k cells
 template <int kOff, bool kCompact, int kBlk>
 __global__ void __launch_bounds__(kBlk, MGP_GA_WAVES) k_group_a(int64_t n, const int32_t* __restrict__ start,
                                                     const int32_t* __restrict__ bc, const int32_t* __restrict__ tlen,
@@ -1913,7 +1927,10 @@ __device__ __forceinline__ void pile_bases_p32(bool act, int a0, int b0, int a1,
                 if ((smask >> qq) & 1ull) body(qq);
         }
     };
-    if (guarded) {
+    if (MGP_ABL == 10) {  // ablation (counts meaningless): every lane of a half on its own bank
+        const uint32_t lr = tb + 4u * (threadIdx.x & 63);
+        run([&](int qq) { lds_add(lr + code(qq) * kPlaneBytes + 4u * (uint32_t)qq, inc); });
+    } else if (guarded) {
         if (two) run([&](int qq) { lds_add((qq >= qs1 ? r1 : r0) + code(qq) * kPlaneBytes + 4u * (uint32_t)qq, inc); });
         else run([&](int qq) { lds_add(r0 + code(qq) * kPlaneBytes + 4u * (uint32_t)qq, inc); });
     } else {
@@ -2737,8 +2754,11 @@ __global__ void k_check_records(const uint8_t* __restrict__ payload, const uint6
             if (start) start[i] = p32 ? (int32_t)(h.x & 0xFFFFu) : (int32_t)h.x;
             const uint32_t lseq = p32 ? ((h.x >> 16) & 0xFFu) : packed ? (h.y & 0xFFu) : h.y;
             const uint32_t ncig = p32 ? ((h.x >> 24) & 7u) : packed ? ((h.y >> 8) & 0x7Fu) : (h.z & 0xFFFFu);
-            // a full record's CIGAR at cigar_off (4-byte words, inside the payload)
-            err = !packed && ((h.w & 3u) != 0u || h.w < 16u || r + h.w + 4ull * ncig > pay_hi);
+            // a full record: qual at +16 and seq at mgp_seq_offset(l_seq) (both read by the
+            // pileup for every query position), then the CIGAR at exactly
+            // mgp_cigar_offset(l_seq) (include/mgpileup.h), all inside the payload. The
+            // CIGAR follows qual and seq, so its end bounds the whole record
+            err = !packed && (lseq > (1u << 28) || h.w != mgp_cigar_offset(lseq) || r + h.w + 4ull * ncig > pay_hi);
             if (span) {
                 auto consumes = [](uint32_t op) { return op == 0u || op == 2u || op == 3u || op == 7u || op == 8u; };
                 uint64_t ref = 0;
@@ -3004,6 +3024,8 @@ int mgp_open(const mgp_config* cfg, int hip_device, mgp_ctx** out) {
     }
     HIP_TRY(hipStreamCreateWithFlags(&ctx->s_comp, hipStreamNonBlocking));
     HIP_TRY(hipStreamCreateWithFlags(&ctx->s_copy, hipStreamNonBlocking));
+    if (const char* e = std::getenv("MGP_H2D_SPLIT")) ctx->h2d_split = std::max(1, std::min(4, std::atoi(e)));
+    if (const char* e = std::getenv("MGP_SEG_MIN_WIN")) ctx->seg_min_win = std::max(1, std::atoi(e));
     HIP_TRY(hipStreamCreateWithFlags(&ctx->s_side, hipStreamNonBlocking));
     HIP_TRY(hipStreamCreateWithFlags(&ctx->s_d2h, hipStreamNonBlocking));
     HIP_TRY(hipEventCreateWithFlags(&ctx->ev_rows, hipEventDisableTiming));
@@ -3059,6 +3081,7 @@ void mgp_close(mgp_ctx* ctx) {
                       &ctx->med_hi,    &ctx->first_read, &ctx->counts,  &ctx->tn5,        &ctx->depth,
                       &ctx->stats,     &ctx->counts16,  &ctx->tn5_16,  &ctx->depth16,    &ctx->wide};
     for (DevBuf* b : bufs) b->release();
+    for (auto e : ctx->seg_ev) (void)hipEventDestroy(e);
     for (int r = 0; r < mgp_ctx::kRing; ++r)
         for (int s = 0; s < ST_N; ++s) {
             (void)hipEventDestroy(ctx->ev[r][s][0]);
@@ -3075,6 +3098,11 @@ void mgp_close(mgp_ctx* ctx) {
     (void)hipStreamDestroy(ctx->s_copy);
     (void)hipStreamDestroy(ctx->s_side);
     (void)hipStreamDestroy(ctx->s_d2h);
+    for (int i = 0; i < 3; ++i) {
+        if (ctx->s_cx[i]) (void)hipStreamDestroy(ctx->s_cx[i]);
+        if (ctx->ev_cx[i]) (void)hipEventDestroy(ctx->ev_cx[i]);
+    }
+    if (ctx->ev_cfork) (void)hipEventDestroy(ctx->ev_cfork);
     (void)hipEventDestroy(ctx->ev_rows);
     delete ctx;
 }
@@ -3144,9 +3172,36 @@ int mgp_push_batch(mgp_ctx* ctx, const mgp_batch* b) {
         HIP_TRY(hipMemcpyAsync(ctx->span.as<uint32_t>() + n0, b->span, nb * 4, hipMemcpyHostToDevice, s));
     if (!dense)
         HIP_TRY(hipMemcpyAsync(ctx->roff.as<uint64_t>() + n0, b->rec_off, nb * 8, hipMemcpyHostToDevice, s));
-    if (b->payload_bytes)
-        HIP_TRY(hipMemcpyAsync(ctx->payload.as<uint8_t>() + pay0, b->payload, b->payload_bytes,
-                               hipMemcpyHostToDevice, s));
+    if (b->payload_bytes) {
+        // a large payload in h2d_split parts on as many streams (copy engines), joined
+        // back into the copy stream before the batch's checks
+        const int k = b->payload_bytes >= (int64_t)(64 << 20) ? ctx->h2d_split : 1;
+        uint8_t* dst = ctx->payload.as<uint8_t>() + pay0;
+        if (k <= 1) {
+            HIP_TRY(hipMemcpyAsync(dst, b->payload, b->payload_bytes, hipMemcpyHostToDevice, s));
+        } else {
+            if (!ctx->ev_cfork) {
+                HIP_TRY(hipEventCreateWithFlags(&ctx->ev_cfork, hipEventDisableTiming));
+                for (int i = 0; i < 3; ++i) {
+                    HIP_TRY(hipStreamCreateWithFlags(&ctx->s_cx[i], hipStreamNonBlocking));
+                    HIP_TRY(hipEventCreateWithFlags(&ctx->ev_cx[i], hipEventDisableTiming));
+                }
+            }
+            HIP_TRY(hipEventRecord(ctx->ev_cfork, s));
+            const int64_t part = ((b->payload_bytes + k - 1) / k + 4095) & ~int64_t(4095);
+            for (int i = 0; i < k; ++i) {
+                const int64_t o = i * part, len = std::min(part, b->payload_bytes - o);
+                if (len <= 0) break;
+                hipStream_t si = i == 0 ? s : ctx->s_cx[i - 1];
+                if (i > 0) HIP_TRY(hipStreamWaitEvent(si, ctx->ev_cfork, 0));
+                HIP_TRY(hipMemcpyAsync(dst + o, b->payload + o, len, hipMemcpyHostToDevice, si));
+                if (i > 0) {
+                    HIP_TRY(hipEventRecord(ctx->ev_cx[i - 1], si));
+                    HIP_TRY(hipStreamWaitEvent(s, ctx->ev_cx[i - 1], 0));
+                }
+            }
+        }
+    }
     if (dense) {
         k_dense_off<<<blocks_for(nb), kBlock, 0, s>>>(ctx->roff.as<uint64_t>() + n0, nb, (uint64_t)pay0,
                                                       (uint64_t)stride);
@@ -3540,9 +3595,23 @@ static int run_segment(mgp_ctx* ctx, const Seg& sg, int slot, int& dup_parts, in
     pc.max_bias = ctx->cfg.max_strand_bias;
     pc.bias_active = ctx->cfg.max_strand_bias < 1.0;
     pc.keep_tn5 = (ctx->cfg.flags & MGP_CFG_KEEP_TN5) != 0;
+    // a streaming segment (slot < 0) times its pileup launch into the coming run's
+    // segment events (that run's slot is runs % kRing: mgp_run takes it)
+    hipEvent_t* sev = nullptr;
+    if (slot < 0 && sg.stream && sg.w1 > sg.w0) {
+        const int rs = (int)(ctx->runs % mgp_ctx::kRing);
+        if (sg.first) ctx->seg_n[rs] = 0;
+        if (ctx->seg_ev.empty()) {
+            ctx->seg_ev.assign((size_t)mgp_ctx::kRing * mgp_ctx::kSegEv * 2, nullptr);
+            for (auto& e : ctx->seg_ev) HIP_TRY(hipEventCreate(&e));
+        }
+        if (ctx->seg_n[rs] < mgp_ctx::kSegEv) sev = &ctx->seg_ev[((size_t)rs * mgp_ctx::kSegEv + ctx->seg_n[rs]) * 2];
+        ctx->seg_n[rs] = std::min(ctx->seg_n[rs] + 1, mgp_ctx::kSegEv + 1);
+    }
     if (sg.w1 > sg.w0) {
         dim3 gp(g.nchunks, sg.w1 - sg.w0);
         const size_t psm = (size_t)kTilePlanes * kTilePitch * 4;
+        if (sev) HIP_TRY(hipEventRecord(sev[0], s));
         auto pile_kern = layout == kLayP32 ? k_pileup<kLayP32> : layout == kLayP64 ? k_pileup<kLayP64>
                                                                                     : k_pileup<kLayAny>;
         pile_kern<<<gp, kBlock, psm, s>>>(g, pc, ctx->payload.as<uint8_t>(), ctx->pel.as<uint32_t>(), unit, pe_off,
@@ -3553,6 +3622,7 @@ static int run_segment(mgp_ctx* ctx, const Seg& sg, int slot, int& dup_parts, in
                                          ctx->dmax.as<uint32_t>(), ctx->tally_part.as<uint32_t>(), st, sg.w0,
                                          ctx->roff_irregular.as<uint32_t>(), ctx->chunk_perm.as<uint32_t>());
         HIP_TRY(hipGetLastError());
+        if (sev) HIP_TRY(hipEventRecord(sev[1], s));
         // the windows' rows are final now (all cells): to the host target behind them,
         // while later batches are still being copied in (mgp_set_rows16_target)
         if (ctx->rows_on) {
@@ -3683,7 +3753,7 @@ static int stream_segments(mgp_ctx* ctx, int64_t last_start, uint16_t last_flag)
     const Geom& g = ctx->g;
     if (ctx->stream_off || g.nc <= 0 || last_start < 0) return MGP_OK;
     const int64_t wc = std::min<int64_t>(last_start / g.W, g.nwin - 1);  // windows [0, wc) are complete
-    if (wc <= ctx->w_done) return MGP_OK;
+    if (wc - ctx->w_done < ctx->seg_min_win) return MGP_OK;
     if (!ctx->seg_open) ctx->stream_layout = (last_flag & MGP_FLAG_PACK32) ? kLayP32 : kLayP64;
     const int unit = ctx->stream_layout == kLayP32 ? 5 : 6;
     if ((uint64_t)ctx->pay >= ((uint64_t)(PE_KEEP & PE_OFF) << unit)) {  // not for compact elements: run resident
@@ -3712,6 +3782,7 @@ int mgp_run(mgp_ctx* ctx) {
     // a streaming run whose pushes already ran segments: the rest of the windows;
     // otherwise (or on the fallback path) one resident segment over everything
     const bool streamed = ctx->seg_open && !ctx->no_spec && !ctx->stream_off;
+    if (!streamed) ctx->seg_n[slot] = 0;  // (no segment pileups of this run to time)
     const Seg sg = streamed ? Seg{ctx->w_done, g.nwin, g.nbins, false, true} : Seg{0, g.nwin, g.nbins, true, false};
     ctx->seg_open = false;
     ctx->w_done = 0;
@@ -3923,10 +3994,20 @@ int mgp_kernel_times(mgp_ctx* ctx, int last_runs, float* ms, int max_n, int* n_o
         for (int r = 0; r < last_runs; ++r) {
             const int slot = (int)((ctx->runs - 1 - r) % mgp_ctx::kRing);
             float t = 0.f;
+            const int sn = st == ST_PILEUP ? ctx->seg_n[slot] : 0;
+            if (sn > mgp_ctx::kSegEv) continue;  // (a streamed run with more segments than events)
             if (ctx->stage_ran[slot][st]) {
                 HIP_TRY(hipEventElapsedTime(&t, ctx->ev[slot][st][0], ctx->ev[slot][st][1]));
                 ++timed;
             }
+            // the pileup of a streamed run: its segments' launches, then the run's own
+            for (int k = 0; k < sn; ++k) {
+                float ts = 0.f;
+                const hipEvent_t* e = &ctx->seg_ev[((size_t)slot * mgp_ctx::kSegEv + k) * 2];
+                HIP_TRY(hipEventElapsedTime(&ts, e[0], e[1]));
+                t += ts;
+            }
+            if (sn > 0 && !ctx->stage_ran[slot][st]) ++timed;
             acc += t;
         }
         if (ms) ms[k] = timed ? (float)(acc / timed) : 0.f;

@@ -22,7 +22,10 @@ from __future__ import annotations
 
 import ctypes as C
 import ctypes.util
+import errno
+import logging
 import os
+import time
 
 import numpy as np
 
@@ -64,7 +67,7 @@ def _h5():
         if not cand:
             continue
         try:
-            lib = C.CDLL(cand)
+            lib = C.CDLL(cand, use_errno=True)  # (errno of a failed write: _ck_retry)
             break
         except OSError as e:
             err = e
@@ -76,6 +79,7 @@ def _h5():
         "H5Fcreate": (hid_t, [C.c_char_p, C.c_uint, hid_t, hid_t]),
         "H5Fopen": (hid_t, [C.c_char_p, C.c_uint, hid_t]),
         "H5Fclose": (herr_t, [hid_t]),
+        "H5Fflush": (herr_t, [hid_t, C.c_int]),
         "H5Pcreate": (hid_t, [hid_t]),
         "H5Pclose": (herr_t, [hid_t]),
         "H5Pset_libver_bounds": (herr_t, [hid_t, C.c_int, C.c_int]),
@@ -146,6 +150,43 @@ def _ck(v, what):
     if v < 0:
         raise OSError(f"HDF5 call failed: {what}")
     return v
+
+
+# The reference's retry policy for writes and flushes on network filesystems
+# (writers.py:23-26, _write_batch_with_retry / _flush_with_retry :266-323): a call that
+# fails with EAGAIN is retried up to MAX_RETRIES times in all, sleeping 0.1 s, doubled
+# per attempt up to 5 s; any other failure (or the last EAGAIN) raises at once.
+MAX_RETRIES = 5
+INITIAL_RETRY_DELAY = 0.1
+MAX_RETRY_DELAY = 5.0
+logger = logging.getLogger(__name__)
+write_error_count = 0  # EAGAIN failures seen (the reference's write_error_count)
+
+
+def _ck_retry(call, what, sleep=time.sleep):
+    """Run ``call()`` (a libhdf5 call returning herr_t / hid_t) with the reference's
+    EAGAIN retry and exponential backoff."""
+    global write_error_count
+    delay = INITIAL_RETRY_DELAY
+    for attempt in range(MAX_RETRIES):
+        C.set_errno(0)
+        v = call()
+        if v >= 0:
+            if attempt > 0:
+                logger.info("%s succeeded on attempt %d", what, attempt + 1)
+            return v
+        e = C.get_errno()
+        if e != errno.EAGAIN:
+            raise OSError(e or errno.EIO, f"HDF5 call failed: {what}")
+        write_error_count += 1
+        if attempt == MAX_RETRIES - 1:
+            logger.error("%s failed after %d attempts", what, MAX_RETRIES)
+            raise OSError(errno.EAGAIN, f"HDF5 call failed after {MAX_RETRIES} attempts: {what}")
+        logger.warning("Temporary write error (attempt %d/%d), retrying in %.2fs: %s", attempt + 1, MAX_RETRIES,
+                       delay, what)
+        sleep(delay)
+        delay = min(delay * 2, MAX_RETRY_DELAY)
+    raise AssertionError("unreachable")
 
 
 _NUM = {
@@ -417,7 +458,8 @@ class Group:
                     if dcpl != H5P_DEFAULT and level is not None and arr.ndim == 2:
                         self._write_chunks(did, arr, chunks, int(level), n_threads)
                     else:
-                        _ck(lib.H5Dwrite(did, t, H5S_ALL, H5S_ALL, H5P_DEFAULT, arr.ctypes.data), "H5Dwrite")
+                        _ck_retry(lambda: lib.H5Dwrite(did, t, H5S_ALL, H5S_ALL, H5P_DEFAULT, arr.ctypes.data),
+                                  "H5Dwrite")
             except Exception:
                 lib.H5Dclose(did)
                 raise
@@ -448,7 +490,8 @@ class Group:
                 for i, blob in enumerate(tiles):
                     off[0] = (i // nc) * chunks[0]
                     off[1] = (i % nc) * chunks[1]
-                    _ck(lib.H5Dwrite_chunk(did, H5P_DEFAULT, 0, off, len(blob), blob), "H5Dwrite_chunk")
+                    _ck_retry(lambda: lib.H5Dwrite_chunk(did, H5P_DEFAULT, 0, off, len(blob), blob),
+                              "H5Dwrite_chunk")
             except Exception:
                 lib.H5Dclose(did)
                 raise
@@ -472,7 +515,7 @@ class Group:
         for i, blob in enumerate(tiles):
             off[0] = (i // nc) * chunks[0]
             off[1] = (i % nc) * chunks[1]
-            _ck(lib.H5Dwrite_chunk(did, H5P_DEFAULT, 0, off, len(blob), blob), "H5Dwrite_chunk")
+            _ck_retry(lambda: lib.H5Dwrite_chunk(did, H5P_DEFAULT, 0, off, len(blob), blob), "H5Dwrite_chunk")
 
     def __contains__(self, name: str) -> bool:
         return _h5().H5Lexists(self._id, name.encode(), H5P_DEFAULT) > 0
@@ -525,6 +568,7 @@ class File(Group):
     def __init__(self, path, mode: str = "r", libver=None):
         lib = _h5()
         self.filename = str(path)
+        self._writable = mode in ("w", "w-", "x")
         if mode in ("w", "w-", "x"):
             fapl = _ck(lib.H5Pcreate(_T["H5P_CLS_FILE_ACCESS_ID_g"]), "H5Pcreate")
             if libver == "latest":
@@ -547,6 +591,9 @@ class File(Group):
         lib = _h5()
         self._close_children()
         lib.H5Gclose(self._id)
+        if self._writable:
+            fid = self._fid
+            _ck_retry(lambda: lib.H5Fflush(fid, 0), "H5Fflush")  # (H5F_SCOPE_LOCAL)
         lib.H5Fclose(self._fid)
         self._fid = None
         self._id = None

@@ -4,7 +4,7 @@
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
-BARGS=${BARGS:-"--steps 10 --warmup 2 --no-cpu-baseline --no-check --no-pcie --no-device-paired --no-host-pack"}
+BARGS=${BARGS:-"--device-only --steps 10 --warmup 2 --no-cpu-baseline --no-check --no-pcie --no-device-paired --no-host-pack"}
 for lib in base "$@"; do
     # a variant is a library (libmgpileup_x.so) or an environment setting (ENV:NAME=VALUE)
     unset MGP_LIB

@@ -310,3 +310,64 @@ def test_native_writer_matches_python_writer(case, tmp_path):
         assert a.count_tag("chrM") == b.count_tag("chrM")
     refs, recs = _independent_decode(tmp_path / "n.bam")
     assert refs == ["chr1", "chrM"] and len(recs) == g.soa.n
+
+
+def _parse_bai(data: bytes) -> list[dict]:
+    """An independent reading of a BAI (SAM spec §5.2): per reference, the smallest
+    chunk begin over the real bins and the metadata pseudo-bin 37450's counts."""
+    assert data[:4] == b"BAI\1"
+    (n_ref,) = struct.unpack_from("<i", data, 4)
+    p, out = 8, []
+    for _ in range(n_ref):
+        (n_bin,) = struct.unpack_from("<i", data, p)
+        p += 4
+        first, meta = None, None
+        for _ in range(n_bin):
+            bin_, n_chunk = struct.unpack_from("<Ii", data, p)
+            p += 8
+            chunks = [struct.unpack_from("<QQ", data, p + 16 * c) for c in range(n_chunk)]
+            p += 16 * n_chunk
+            if bin_ == 37450:
+                meta = chunks
+            else:
+                b = min(c[0] for c in chunks)
+                first = b if first is None else min(first, b)
+        (n_intv,) = struct.unpack_from("<i", data, p)
+        p += 4 + 8 * n_intv
+        out.append(dict(n_bin=n_bin, first=first, meta=meta))
+    assert p <= len(data)
+    return out
+
+
+def test_reference_bai_pins_the_index_reader(tmp_path):
+    """The reference's only real index (tests/outs/possorted_bam.bam.bai, kept as the
+    fixture golden/ref_possorted_bam.bam.bai; its BAM is absent upstream): 194
+    references, chrM is reference 22 with 228,149 mapped + 1,619 placed-unmapped
+    records. The native reader (mgp_bam.cpp load_index) must give
+    those counts, nothing for the references without bins, and refuse the index for
+    a header with another reference count."""
+    import shutil
+    from pathlib import Path
+
+    bai = Path(__file__).parent / "golden" / "ref_possorted_bam.bam.bai"
+    data = bai.read_bytes()
+    idx = _parse_bai(data)
+    assert len(idx) == 194
+    assert [i for i, r in enumerate(idx) if r["n_bin"]] == [22]
+    assert idx[22]["meta"][1] == (228_149, 1_619)
+    assert idx[22]["first"] == idx[22]["meta"][0][0]  # the chrM records start where its extent does
+    refs = [(f"chr{i}", 1_000_000) for i in range(194)]
+    refs[22] = ("chrM", 16569)
+    bam = tmp_path / "hdr.bam"
+    BamWriter(bam, refs).close(index=False)
+    shutil.copy(bai, str(bam) + ".bai")
+    with BamFile(bam) as b:
+        assert b.has_index
+        assert len(b.references) == 194 and b.references[22] == "chrM"
+        assert b.ref_records("chrM") == 228_149 + 1_619
+        assert {b.ref_records(f"chr{i}") for i in range(194) if i != 22} == {-1}
+    bad = tmp_path / "hdr193.bam"
+    BamWriter(bad, refs[:193]).close(index=False)
+    shutil.copy(bai, str(bad) + ".bai")
+    with pytest.raises(BAMFormatError, match="reference count"):
+        BamFile(bad)

@@ -485,11 +485,12 @@ def test_rows16_target_equals_fetch_rows16(engine_lib, streamed, layout, min_rea
 
 
 @pytest.mark.parametrize("streamed", [False, True])
-@pytest.mark.parametrize("fault", ["offset", "misaligned", "cigar", "stride"])
+@pytest.mark.parametrize("fault", ["offset", "misaligned", "cigar", "stride", "lseq", "cigar_off"])
 def test_records_outside_the_payload_raise(engine_lib, streamed, fault):
     """A pushed record outside its batch's payload (an offset past the end, a
     misaligned offset, a full record's CIGAR past the end, a dense stride shorter
-    than a full record) makes the run raise InvalidInputError without any kernel
+    than a full record, an l_seq whose qual/seq run past the end, a CIGAR offset
+    other than mgp_cigar_offset(l_seq)) makes the run raise InvalidInputError without any kernel
     reading the record; the context then runs a good batch normally (ABI 4)."""
     from dataclasses import replace
 
@@ -516,6 +517,12 @@ def test_records_outside_the_payload_raise(engine_lib, streamed, fault):
         i = len(roff) - 1
         o = int(roff[i])
         pay[o + 8:o + 10] = np.frombuffer(np.uint16(4000).tobytes(), np.uint8)  # n_cigar far past the end
+    elif fault == "lseq":  # l_seq far past the end (qual and seq would be read past it), CIGAR left in place
+        o = int(roff[len(roff) - 1])
+        pay[o + 4:o + 8] = np.frombuffer(np.uint32(100_000).tobytes(), np.uint8)
+    elif fault == "cigar_off":  # CIGAR offset inside the record but not at mgp_cigar_offset(l_seq)
+        o = int(roff[3])
+        pay[o + 12:o + 16] = np.frombuffer(np.uint32(16).tobytes(), np.uint8)
     else:  # dense records at a 64-byte stride: a full record is 128 bytes
         n = 1000
         d = np.zeros(n * 64, np.uint8)

@@ -169,3 +169,40 @@ def test_hdf5_barcode_metadata_group(tmp_path, oracle_lib):
         assert [b.decode() for b in grp["barcode"][...]] == wl
         np.testing.assert_array_equal(grp["passed_filters"][...], list(reversed(range(len(wl)))))
         assert grp["frac"][...].dtype == np.float64
+
+
+def test_hdf5_write_retries_eagain_with_backoff():
+    """HDF5 writes and flushes retry EAGAIN (network filesystems) the reference's
+    way (writers.py:23-26,266-323): up to 5 attempts, sleeps 0.1, 0.2, 0.4, 0.8 s;
+    another errno, or the fifth EAGAIN, raises at once."""
+    import ctypes as C
+    import errno
+
+    from mgatk2_amd import h5lite
+
+    def failing(fails: int, code: int):
+        n = [0]
+
+        def call():
+            n[0] += 1
+            if n[0] <= fails:
+                C.set_errno(code)
+                return -1
+            return 7
+
+        return call, n
+
+    slept = []
+    call, n = failing(3, errno.EAGAIN)
+    assert h5lite._ck_retry(call, "w", sleep=slept.append) == 7
+    assert n[0] == 4 and slept == [0.1, 0.2, 0.4]
+    slept.clear()
+    call, n = failing(99, errno.EAGAIN)
+    with pytest.raises(OSError) as ei:
+        h5lite._ck_retry(call, "w", sleep=slept.append)
+    assert ei.value.errno == errno.EAGAIN and n[0] == 5 and slept == [0.1, 0.2, 0.4, 0.8]
+    slept.clear()
+    call, n = failing(1, errno.ENOSPC)
+    with pytest.raises(OSError) as ei:
+        h5lite._ck_retry(call, "w", sleep=slept.append)
+    assert ei.value.errno == errno.ENOSPC and n[0] == 1 and slept == []
