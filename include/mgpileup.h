@@ -46,13 +46,14 @@
 extern "C" {
 #endif
 
-#define MGP_ABI_VERSION 4  /* 2: fixed seq/CIGAR offsets for reads <= 64 bases;
+#define MGP_ABI_VERSION 5  /* 2: fixed seq/CIGAR offsets for reads <= 64 bases;
                               3: synth cell shards, cell-range and 16-bit fetches, streaming runs;
                               4: batches without rec_off / span columns and the rows target (the
                                  round-3 "v3.1" entry points), pushed records checked against
                                  their batch's payload (MGP_E_INVALID), mgp_copy_wait, batches
                                  without a start column,
-                                 mgp_synth_params.n_rec_off, rows targets with min_reads > 1 */
+                                 mgp_synth_params.n_rec_off, rows targets with min_reads > 1;
+                              5: mgp_set_cell_range (one device's cells of whole batches) */
 
 /* ---- return codes (0 = success) ------------------------------------------ */
 #define MGP_OK               0
@@ -499,6 +500,17 @@ int  mgp_windows(mgp_ctx *ctx, int32_t *n_windows, int32_t *window_width);
  * then reuse those host buffers (until then a pushed batch's arrays must stay untouched).
  * A producer that decodes into a ring of pinned buffers calls it before refilling one. */
 int  mgp_copy_wait(mgp_ctx *ctx);
+/* The context's cells are whitelist indices [cell_lo, cell_hi) of the pushed batches
+ * (n_cells = cell_hi - cell_lo): every pushed read's barcode index is rebased on the
+ * device behind its copy (bc - cell_lo inside the range, -1 = not this context's
+ * cells outside it), so the devices of a multi-GPU run can all take the same whole
+ * batches and nothing routes reads on the host. Reads outside the range count only
+ * toward total_reads, like reads without a whitelisted barcode; first_read then
+ * indexes the whole pushed stream. Set it before the first push of a run (it stays for
+ * the context's later runs). Without it a barcode index >= n_cells is an error
+ * (MGP_E_INVALID). Replaces the reference's split of the barcodes
+ * over its worker pool (processors.py:112-144) with a split by device. */
+int  mgp_set_cell_range(mgp_ctx *ctx, int32_t cell_lo, int32_t cell_hi);
 /* Streaming on (1) or off (0) for the next pushes (initially MGP_CFG_STREAM). */
 int  mgp_set_streaming(mgp_ctx *ctx, int on);
 /* Streaming: segments queued by pushes so far (all runs), and whether the last run

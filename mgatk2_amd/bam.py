@@ -11,6 +11,7 @@
 from __future__ import annotations
 
 import ctypes as C
+import os
 import struct
 import zlib
 from pathlib import Path
@@ -20,7 +21,8 @@ import numpy as np
 from .exceptions import BAMFormatError, BAMReadError, ProcessingError
 from .synth import SEQ_NT16, ReadSoA
 
-HOST_LIB = Path(__file__).resolve().parent / "_lib" / "libmgphost.so"
+HOST_LIB = Path(os.environ.get("MGP_HOST_LIB") or Path(__file__).resolve().parent / "_lib" / "libmgphost.so")
+# (MGP_HOST_LIB: another build of the library, e.g. scripts/sanitize_host.sh's ASan / TSan builds)
 _NT16 = {ch: i for i, ch in enumerate(SEQ_NT16)}
 CIGAR_OPS = "MIDNSHP=X"
 

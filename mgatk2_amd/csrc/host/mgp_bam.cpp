@@ -233,14 +233,18 @@ class Prefetch {
         th_ = std::thread([this] { run(); });
     }
     ~Prefetch() {
+        join();
+        for (Chunk* c : ready_) delete c;
+        for (Chunk* c : free_) delete c;
+    }
+    // stops the prefetch thread and waits for it (its profile counters are then stable)
+    void join() {
         {
             std::lock_guard<std::mutex> g(mu_);
             stop_ = true;
         }
         cv_.notify_all();
-        th_.join();
-        for (Chunk* c : ready_) delete c;
-        for (Chunk* c : free_) delete c;
+        if (th_.joinable()) th_.join();
     }
     // the next chunk in file order; nullptr on error (message in err())
     Chunk* next() {
@@ -457,12 +461,13 @@ struct Stream {
     size_t wt = 0;
 
     ~Stream() {
-        if (pf) {  // (the profile counters of mgp_bam_read_ref, on the consumer's thread)
+        release_held();
+        if (cur && pf) pf->recycle(cur);
+        if (pf) {  // (the profile counters of mgp_bam_read_ref, read once the prefetch thread has ended)
+            pf->join();
             t_pread += pf->t_pread;
             t_inflate += pf->t_inflate;
         }
-        release_held();
-        if (cur && pf) pf->recycle(cur);
         pf.reset();
     }
     void release_held() {
@@ -1627,6 +1632,7 @@ struct mgp_bam_stream {
     }
     ~mgp_bam_stream() {
         if (pending) placer.wait();  // (an abandoned batch: its placement may still run)
+        if (std::getenv("MGP_HOST_PROFILE") && st.pf) st.pf->join();  // (its counters, once its thread has ended)
         if (std::getenv("MGP_HOST_PROFILE"))
             std::fprintf(stderr,
                          "[mgp_bam_stream] %lld records, %d threads%s: open %.3f s; waiting for inflated chunks %.3f, "

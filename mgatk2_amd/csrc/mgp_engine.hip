@@ -126,7 +126,11 @@ struct mgp_ctx {
     // a pushed batch's payload copy split over h2d_split streams (MGP_H2D_SPLIT; the
     // extra streams and their events are created on the first split copy)
     int h2d_split = 1;
-    int seg_min_win = 1;  // a streaming push queues a segment once this many windows are complete (MGP_SEG_MIN_WIN)
+    int seg_min_win = 1;
+    int rows_wg = 256;
+    int32_t cell_lo = 0;   // mgp_set_cell_range: the context's cells in the pushed batches' barcode indices
+    bool cell_range = false;
+    int pile_wg_stream = 0;  // a streaming run's pileup workgroups per window (set_pile_chunks; 0: the default)    // workgroups of a segment's k_rows_to_host (MGP_ROWS_WG)  // a streaming push queues a segment once this many windows are complete (MGP_SEG_MIN_WIN)
     hipStream_t s_cx[3] = {nullptr, nullptr, nullptr};
     hipEvent_t ev_cx[3] = {nullptr, nullptr, nullptr}, ev_cfork = nullptr;
     hipEvent_t ev_bits = nullptr;  // the run's input check words have reached h_bits
@@ -1753,6 +1757,11 @@ __device__ __forceinline__ void pile_bases(bool act, int a0, int b0, int a1, int
     }
 }
 
+#ifndef MGP_QQ_STRIDE
+#define MGP_QQ_STRIDE 1  // query positions per pass of the per-base core loops (A/B)
+#endif
+constexpr int kQS = MGP_QQ_STRIDE;
+
 // LDS byte addresses: the packed loop computes a count's address as integer
 // arithmetic (row | plane * 4) and adds through an LDS-qualified pointer, so the
 // query offset still folds into the atomic's immediate.
@@ -1837,8 +1846,12 @@ __device__ __forceinline__ void pile_bases_packed(bool act, int a0, int b0, int 
                 for (int qq = 0; qq < kC0; ++qq)
                     if ((smask >> qq) & 1ull) body(qq);
             }
+            // the core in MGP_QQ_STRIDE interleaved passes (consecutive adds of a lane
+            // kQS positions apart, not 1)
 #pragma unroll
-            for (int qq = kC0; qq < kC1; ++qq) body(qq);
+            for (int j = 0; j < kQS; ++j)
+#pragma unroll
+                for (int qq = kC0 + j; qq < kC1; qq += kQS) body(qq);
             if (wq_hi > kC1) {
 #pragma unroll
                 for (int qq = kC1; qq < kLen; ++qq)
@@ -1914,8 +1927,12 @@ __device__ __forceinline__ void pile_bases_p32(bool act, int a0, int b0, int a1,
                 for (int qq = 0; qq < kC0; ++qq)
                     if ((smask >> qq) & 1ull) body(qq);
             }
+            // the core in MGP_QQ_STRIDE interleaved passes (consecutive adds of a lane
+            // kQS positions apart, not 1)
 #pragma unroll
-            for (int qq = kC0; qq < kC1; ++qq) body(qq);
+            for (int j = 0; j < kQS; ++j)
+#pragma unroll
+                for (int qq = kC0 + j; qq < kC1; qq += kQS) body(qq);
             if (wq_hi > kC1) {
 #pragma unroll
                 for (int qq = kC1; qq < kLen; ++qq)
@@ -2718,6 +2735,16 @@ __global__ void __launch_bounds__(kBlock) k_rows_to_host(int L, int nc, int p0, 
     }
 }
 
+// mgp_set_cell_range: a pushed batch's barcode indices rebased to the context's cells
+// [lo, lo + nc); the others -1 (read_valid drops them like reads without a barcode)
+__global__ void k_rebase_bc(int32_t* __restrict__ bc, int64_t n, int32_t lo, int32_t nc) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) {
+        const int32_t v = bc[i];
+        bc[i] = (v >= lo && v - lo < nc) ? v - lo : -1;
+    }
+}
+
 // mgp_push_batch without rec_off: dense records in BAM order, record i at base + i x stride
 __global__ void k_dense_off(uint64_t* __restrict__ roff, int64_t n, uint64_t base, uint64_t stride) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -2908,6 +2935,29 @@ __global__ void k_respec_slot(const DevStats* st, unsigned long long* slot) {
 #ifndef MGP_PILE_MIN_CPB
 #define MGP_PILE_MIN_CPB 8
 #endif
+#ifndef MGP_PILE_WG_STREAM
+#define MGP_PILE_WG_STREAM 2048  // a streaming run's pileup workgroups per window (MGP_PILE_WG_STREAM env too)
+#endif
+// Cells per pileup chunk. A resident run launches every window at once: ~MGP_PILE_WG
+// workgroups over the windows, at least MGP_PILE_MIN_CPB cells: each (chunk, window)
+// workgroup writes a tally partial row (16 B per position) that k_tally_reduce reads
+// back, so at few cells per chunk the partials, not the cells, set the cost (1250
+// cells at 1 per chunk: 331 MB, the same as C4's 10k cells at 8; at 4 per chunk the
+// 1250-cell step is 11 % shorter). A streaming run launches the pileup per segment,
+// about one window each: there the chunks are sized for ~wg_stream workgroups per
+// window (C4: 2000 chunks of 5 cells instead of 625 of 16, which left 40 % of the
+// 1024 workgroup slots of a one-window launch empty), at least 2 cells each.
+static void set_pile_chunks(Geom& g, bool stream, int wg_stream) {
+    int64_t cpb;
+    if (stream) {
+        cpb = std::max<int64_t>(2, ((int64_t)g.nc + wg_stream - 1) / std::max(1, wg_stream));
+    } else {
+        const int64_t target = MGP_PILE_WG;
+        cpb = std::max<int64_t>(MGP_PILE_MIN_CPB, ((int64_t)g.nc * g.nwin + target - 1) / target);
+    }
+    g.cpb = (int)std::min<int64_t>(cpb, 64);
+    g.nchunks = g.nc > 0 ? (g.nc + g.cpb - 1) / g.cpb : 0;
+}
 static inline unsigned blocks_for(int64_t n, int bs = kBlock) { return (unsigned)((n + bs - 1) / bs); }
 
 static int configure_geometry(mgp_ctx* ctx) {
@@ -2926,15 +2976,8 @@ static int configure_geometry(mgp_ctx* ctx) {
     // offset is a shift folded into the address add (A/B: no bank-conflict cost)
     g.Wp = kTilePitch;
     g.nc = c.n_cells;
-    // cells per pileup workgroup: ~MGP_PILE_WG workgroups over the windows, and at least
-    // MGP_PILE_MIN_CPB cells: each (chunk, window) workgroup writes a tally partial row
-    // (16 B per position) that k_tally_reduce reads back, so at few cells per chunk the
-    // partials, not the cells, set the cost (1250 cells at 1 per chunk: 331 MB, the same
-    // as C4's 10k cells at 8; at 4 per chunk the 1250-cell step is 11 % shorter)
-    int64_t target = MGP_PILE_WG;
-    int64_t cpb = ((int64_t)g.nc * g.nwin + target - 1) / target;
-    g.cpb = (int)std::max<int64_t>(MGP_PILE_MIN_CPB, std::min<int64_t>(cpb, 64));
-    g.nchunks = g.nc > 0 ? (g.nc + g.cpb - 1) / g.cpb : 0;
+    // cells per pileup chunk (a resident run's; a streaming run sets its own)
+    set_pile_chunks(g, false, MGP_PILE_WG_STREAM);
     return MGP_OK;
 }
 
@@ -3026,6 +3069,9 @@ int mgp_open(const mgp_config* cfg, int hip_device, mgp_ctx** out) {
     HIP_TRY(hipStreamCreateWithFlags(&ctx->s_copy, hipStreamNonBlocking));
     if (const char* e = std::getenv("MGP_H2D_SPLIT")) ctx->h2d_split = std::max(1, std::min(4, std::atoi(e)));
     if (const char* e = std::getenv("MGP_SEG_MIN_WIN")) ctx->seg_min_win = std::max(1, std::atoi(e));
+    if (const char* e = std::getenv("MGP_ROWS_WG")) ctx->rows_wg = std::max(1, std::atoi(e));
+    ctx->pile_wg_stream = MGP_PILE_WG_STREAM;
+    if (const char* e = std::getenv("MGP_PILE_WG_STREAM")) ctx->pile_wg_stream = std::max(1, std::atoi(e));
     HIP_TRY(hipStreamCreateWithFlags(&ctx->s_side, hipStreamNonBlocking));
     HIP_TRY(hipStreamCreateWithFlags(&ctx->s_d2h, hipStreamNonBlocking));
     HIP_TRY(hipEventCreateWithFlags(&ctx->ev_rows, hipEventDisableTiming));
@@ -3165,6 +3211,10 @@ int mgp_push_batch(mgp_ctx* ctx, const mgp_batch* b) {
     hipStream_t s = ctx->s_copy;
     if (b->start) HIP_TRY(hipMemcpyAsync(ctx->start.as<int32_t>() + n0, b->start, nb * 4, hipMemcpyHostToDevice, s));
     HIP_TRY(hipMemcpyAsync(ctx->bc.as<int32_t>() + n0, b->bc, nb * 4, hipMemcpyHostToDevice, s));
+    if (ctx->cell_range) {
+        k_rebase_bc<<<blocks_for(nb), kBlock, 0, s>>>(ctx->bc.as<int32_t>() + n0, nb, ctx->cell_lo, ctx->g.nc);
+        HIP_TRY(hipGetLastError());
+    }
     HIP_TRY(hipMemcpyAsync(ctx->tlen.as<int32_t>() + n0, b->tlen, nb * 4, hipMemcpyHostToDevice, s));
     HIP_TRY(hipMemcpyAsync(ctx->flag.as<uint16_t>() + n0, b->flag, nb * 2, hipMemcpyHostToDevice, s));
     HIP_TRY(hipMemcpyAsync(ctx->mapq.as<uint8_t>() + n0, b->mapq, nb, hipMemcpyHostToDevice, s));
@@ -3632,7 +3682,12 @@ static int run_segment(mgp_ctx* ctx, const Seg& sg, int slot, int& dup_parts, in
             HIP_TRY(hipEventRecord(ctx->ev_rows, s));
             HIP_TRY(hipStreamWaitEvent(ctx->s_d2h, ctx->ev_rows, 0));
             const mgp_rows16& t = ctx->rows_tgt;
-            dim3 gr((unsigned)((p1 - p0 + kBlock - 1) / kBlock), (unsigned)std::min(nc, 65535));
+            // a few hundred workgroups looping over the cells: the stores wait on the host
+            // link, and a grid of one workgroup per (cell, 256 positions) held every CU
+            // slot of the device while they drained, starving the kernels of the next
+            // segment and the run's medians (MGP_ROWS_WG)
+            const unsigned gx = (unsigned)((p1 - p0 + kBlock - 1) / kBlock);
+            dim3 gr(gx, (unsigned)std::max(1, std::min(std::min(nc, 65535), ctx->rows_wg / (int)gx)));
             k_rows_to_host<<<gr, kBlock, 0, ctx->s_d2h>>>(g.L, nc, p0, p1, ctx->counts16.as<uint4>(),
                                                         ctx->tn5_16.as<uint32_t>(), ctx->depth16.as<uint16_t>(),
                                                         reinterpret_cast<uint4*>(t.counts),
@@ -3760,6 +3815,7 @@ static int stream_segments(mgp_ctx* ctx, int64_t last_start, uint16_t last_flag)
         ctx->stream_off = true;
         return MGP_OK;
     }
+    if (!ctx->seg_open) set_pile_chunks(ctx->g, true, ctx->pile_wg_stream);  // (the whole run's chunks)
     MGP_TRY(ensure_run_buffers(ctx));
     int dup_parts = 0, pair_mode = 0;
     const Seg sg{ctx->w_done, (int)wc, (int)(wc * g.W / g.G), !ctx->seg_open, true};
@@ -3774,6 +3830,9 @@ int mgp_run(mgp_ctx* ctx) {
     if (!ctx) return set_err(MGP_E_INVALID, "null ctx");
     HIP_TRY(hipSetDevice(ctx->dev));
     ctx->ran = false;  // (until this run is queued: an error below leaves no results)
+    // a run not begun by streaming segments is one resident launch of every window
+    const bool streamed_run = ctx->seg_open && !ctx->no_spec && !ctx->stream_off;
+    if (!streamed_run) set_pile_chunks(ctx->g, false, ctx->pile_wg_stream);
     MGP_TRY(ensure_run_buffers(ctx));
     const Geom g = ctx->g;
     const int slot = (int)(ctx->runs % mgp_ctx::kRing);
@@ -3964,6 +4023,16 @@ int mgp_set_streaming(mgp_ctx* ctx, int on) {
     if (!ctx) return set_err(MGP_E_INVALID, "null ctx");
     if (ctx->seg_open) return set_err(MGP_E_STATE, "a streaming run is in progress (mgp_run or mgp_reset first)");
     ctx->stream = on != 0;
+    return MGP_OK;
+}
+
+int mgp_set_cell_range(mgp_ctx* ctx, int32_t cell_lo, int32_t cell_hi) {
+    if (!ctx) return set_err(MGP_E_INVALID, "null ctx");
+    if (cell_lo < 0 || cell_hi < cell_lo || cell_hi - cell_lo != ctx->g.nc)
+        return set_err(MGP_E_INVALID, "cell range [lo, hi) must have n_cells cells, lo >= 0");
+    if (ctx->n > 0) return set_err(MGP_E_STATE, "set the cell range before the first push of a run (mgp_reset)");
+    ctx->cell_lo = cell_lo;
+    ctx->cell_range = true;
     return MGP_OK;
 }
 

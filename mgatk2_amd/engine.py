@@ -38,9 +38,9 @@ ABI_SYMBOLS = (
     "mgp_host_free", "mgp_push_batch", "mgp_reset", "mgp_resident", "mgp_run", "mgp_sync", "mgp_fetch",
     "mgp_finish", "mgp_kernel_times", "mgp_comm_unique_id", "mgp_comm_init", "mgp_synth_generate",
     "mgp_download_inputs", "mgp_set_stage_timing", "mgp_fetch_cells", "mgp_fetch_rows16", "mgp_windows",
-    "mgp_stream_info", "mgp_set_streaming", "mgp_set_rows16_target", "mgp_copy_wait",
+    "mgp_stream_info", "mgp_set_streaming", "mgp_set_rows16_target", "mgp_copy_wait", "mgp_set_cell_range",
 )
-ABI_VERSION = 4
+ABI_VERSION = 5
 CFG_KEEP_TN5 = 0x1
 CFG_STREAM = 0x2
 
@@ -187,6 +187,7 @@ def load_library(path: Path | None = None) -> C.CDLL:
         "mgp_windows": ([vp, C.POINTER(i32), C.POINTER(i32)], C.c_int),
         "mgp_stream_info": ([vp, C.POINTER(i64), C.POINTER(i32)], C.c_int),
         "mgp_set_streaming": ([vp, C.c_int], C.c_int),
+        "mgp_set_cell_range": ([vp, C.c_int32, C.c_int32], C.c_int),
         "mgp_copy_wait": ([vp], C.c_int),
     }
     for name, (args, res) in sig.items():
@@ -511,6 +512,12 @@ class Engine:
         """mgp_copy_wait: every pushed batch's H2D copies are done (their host
         buffers may be reused). The batches stay referenced until the next sync."""
         _ck(self.lib.mgp_copy_wait(self._h), "mgp_copy_wait")
+
+    def set_cell_range(self, lo: int, hi: int):
+        """mgp_set_cell_range: this context's cells are whitelist indices [lo, hi) of the
+        batches pushed from now on (hi - lo = its n_cells); the reads of other cells
+        count only toward total_reads."""
+        _ck(self.lib.mgp_set_cell_range(self._h, int(lo), int(hi)), "mgp_set_cell_range")
 
     def set_streaming(self, on: bool):
         """Streaming runs on or off for the next pushes (EngineConfig.stream initially)."""

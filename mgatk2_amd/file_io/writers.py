@@ -120,7 +120,9 @@ class IncrementalTextWriter:
         self.cell_stats: list[dict] = []
         self.position_base_counts = np.zeros((config.mito_length, 4), np.int64)
         self.cell_depths: dict[str, float] = {}
-        self.gzip_level = int(os.environ.get("MGP_GZIP_LEVEL", 1)) if gzip_level is None else gzip_level
+        # the reference's compresslevel=9 (writers.py:471-486) by default; MGP_GZIP_LEVEL=1
+        # trades ~20 % larger files for a deflate ~15x faster (the decompressed text is the same)
+        self.gzip_level = int(os.environ.get("MGP_GZIP_LEVEL", 9)) if gzip_level is None else gzip_level
         self.n_threads = n_threads
         self.prefix = self.output_dir / "output"
         for name in [*BASES, "coverage"]:

@@ -266,32 +266,46 @@ class CellProcessor:
         return res
 
     def _run_stream_sharded(self, reader, n_cells: int, batch_reads: int | None, rows_target: bool) -> EngineResult:
-        """The streamed path over several devices: the cells split
-        into contiguous whitelist ranges of equal size (the reads per cell are not
-        known before the one pass), one streaming context per device, each fed by a
-        thread of its own. This thread routes every decoded batch: the reads of each
-        range, in BAM order, gathered natively into that device's sub-batch (cell ids
-        rebased, records re-placed; reads without a whitelisted barcode go nowhere
-        and count only toward total_reads), while the producer decodes the next.
-        Every device's rows target is its cell range of one pinned result array, so
-        the results need no concatenation; the tallies are summed on the host."""
-        from ..shard import shard_soa, split_by_range
+        """The streamed path over several devices: one streaming
+        context per device, each owning a contiguous whitelist range of cells, each
+        fed by a thread of its own. Every device takes every decoded batch whole (its
+        own H2D copy over its own link) and keeps its cells' reads on the device
+        (mgp_set_cell_range rebases the barcode indices behind the copy), so no host
+        thread splits, gathers or re-places reads: the decoder's pinned batch goes to
+        all devices as it is, and its slot returns to the decoder when the last
+        device's copy is done. The ranges are read-balanced by the first batch's reads
+        per cell (a cell's reads are spread over all of chrM, so the first batch is a
+        fair sample of the whole set). Every device's rows target is its cell range of
+        one pinned result array, so the results need no concatenation; a cell's first
+        read indexes the whole pushed stream (the BAM's chrM records) on every device;
+        the tallies are summed on the host."""
+        from ..shard import partition_cells
 
         devs = list(self.devices)
         D = len(devs)
         t0 = time.perf_counter()
         bam, st, n_hint, free, full, producer, times = self._stream_producer(reader, n_cells, batch_reads)
-        bounds = np.linspace(0, n_cells, D + 1).round().astype(np.int64)
-        parts = [(d, int(bounds[d]), int(bounds[d + 1])) for d in range(D) if bounds[d + 1] > bounds[d]]
-        engines, queues, workers, idx_lists, errors = {}, {}, {}, {}, []
+        engines, queues, workers, errors = {}, {}, {}, []
+        parts: list[tuple[int, int, int]] = []
         rows = None
         try:
+            first = full.get()
+            if isinstance(first, BaseException):
+                raise first
+            if first is not None:
+                times["first_batch"] = time.perf_counter()
+                bc = first.soa().bc
+                w = np.bincount(bc[(bc >= 0) & (bc < n_cells)], minlength=n_cells).astype(np.float64) + 1e-3
+            else:
+                w = np.ones(n_cells)
+            bounds = partition_cells(w, D)
+            parts = [(d, int(bounds[d]), int(bounds[d + 1])) for d in range(D) if bounds[d + 1] > bounds[d]]
             for d, lo, hi in parts:
-                share = (hi - lo) / max(1, n_cells)
-                ec = self.config.engine_config(hi - lo, reserve_reads=int(n_hint * share * 1.25) + 4096,
-                                               reserve_payload=int(n_hint * share * 1.25) * 40 + (64 << 20))
+                ec = self.config.engine_config(hi - lo, reserve_reads=n_hint + 4096,
+                                               reserve_payload=n_hint * 40 + (64 << 20))
                 ec.stream = True
                 engines[d] = Engine(ec, device=devs[d])
+                engines[d].set_cell_range(lo, hi)
             # the rows target (all cells, one pinned array) is pinned on a thread while the
             # first batches go in; each device thread sets its view when it is ready (the
             # engine copies the windows piled before, ABI 4)
@@ -309,10 +323,16 @@ class CellProcessor:
 
                 threading.Thread(target=alloc, name="mgp-rows-alloc", daemon=True).start()
 
+            def release(left, item):
+                with left[1]:
+                    left[0] -= 1
+                    last = left[0] == 0
+                if last:
+                    free.put(item)
+
             def work(d, lo, hi):
-                # this device's share of each batch: gathered here (the devices' gathers run
-                # side by side, native and GIL-free), then the batch's slot is released by
-                # the last device done with it
+                # every batch as it is: pushed, its copy awaited, its slot released by the
+                # last device done with it
                 eng = engines[d]
                 view_set = not (rows_target and parts)
 
@@ -335,19 +355,12 @@ class CellProcessor:
                         job = queues[d].get()
                         if job is None:
                             break
-                        item, soa, idx, left = job
+                        item, soa, left = job
                         try:
-                            sub, _ = shard_soa(soa, lo, hi, idx=idx)
-                        finally:
-                            with left[1]:
-                                left[0] -= 1
-                                last = left[0] == 0
-                            if last:
-                                free.put(item)  # (the sub-batches are copies)
-                        if sub.n:
-                            set_view(False)
-                            eng.push(sub)
+                            eng.push(soa)
                             eng.copy_wait()
+                        finally:
+                            release(left, item)
                     set_view(True)
                     eng.run()
                     eng.sync()
@@ -357,43 +370,30 @@ class CellProcessor:
                         job = queues[d].get()
                         if job is None:
                             break
-                        with job[3][1]:
-                            job[3][0] -= 1
-                            last = job[3][0] == 0
-                        if last:
-                            free.put(job[0])
+                        release(job[2], job[0])
 
             for d, lo, hi in parts:
                 queues[d] = Queue(maxsize=4)
-                idx_lists[d] = []
                 workers[d] = threading.Thread(target=work, args=(d, lo, hi), name=f"mgp-dev{d}", daemon=True)
                 workers[d].start()
-            pbounds = np.asarray([parts[0][1]] + [hi for _, _, hi in parts], np.int64) if parts else None
             t1 = time.perf_counter()
-            n_batches, base = 0, 0
+            n_batches = 0
             try:
-                while True:
-                    item = full.get()
-                    if item is None:
-                        break
+                item = first
+                while item is not None:
                     if isinstance(item, BaseException):
                         raise item
                     if errors:
                         raise errors[0]
-                    if n_batches == 0:
-                        times["first_batch"] = time.perf_counter()
-                    soa = item.soa()
                     if parts:
-                        split = split_by_range(soa.bc, pbounds)  # (parts are contiguous ranges)
+                        soa = item.soa()
                         left = [len(parts), threading.Lock()]
-                        for (d, lo, hi), idx in zip(parts, split):
-                            if idx.size:
-                                idx_lists[d].append(idx + base)
-                            queues[d].put((item, soa, idx, left))
+                        for d, _, _ in parts:
+                            queues[d].put((item, soa, left))
                     else:
                         free.put(item)
-                    base += soa.n
                     n_batches += 1
+                    item = full.get()
             finally:
                 for d, _, _ in parts:
                     queues[d].put(None)
@@ -412,19 +412,11 @@ class CellProcessor:
             for d, lo, hi in parts:
                 r = engines[d].fetch(dense=rows is None or wide)
                 for k in ("n_reads", "any_paired", "passed", "covered", "depth_sum", "depth_max", "median_lo",
-                          "median_hi"):
+                          "median_hi", "first_read"):
                     getattr(res, k)[lo:hi] = getattr(r, k)
                 if rows is None or wide:
                     for k in ("counts", "tn5", "depth"):
                         getattr(res, k)[lo:hi] = getattr(r, k)
-                has = r.n_reads > 0
-                if has.any():  # the device's pushed-read index of each cell's first read -> BAM index
-                    idx = np.concatenate(idx_lists[d])
-                    fr = np.full(hi - lo, np.iinfo(np.uint32).max, np.int64)
-                    fr[has] = idx[r.first_read[has].astype(np.int64)]
-                    res.first_read[lo:hi] = fr.astype(np.uint32)
-                else:
-                    res.first_read[lo:hi] = np.iinfo(np.uint32).max
                 res.ref_tally += r.ref_tally
                 for k in st_sum:
                     st_sum[k] += int(r.stats[k])
@@ -447,7 +439,8 @@ class CellProcessor:
                             "stream_decode_end": times.get("decode_end", t2) - t0, "stream_push_end": t2 - t0,
                             "engine_tail": 0.0, "engine_fetch": t3 - t2, "engine_close": te - t3,
                             "stream_batches": n_batches, "stream_batch_reads": times["cap_reads"],
-                            "stream_devices": len(parts), "rows_target": rows is not None}
+                            "stream_devices": len(parts), "rows_target": rows is not None,
+                            "cell_bounds": [lo for _, lo, _ in parts] + ([parts[-1][2]] if parts else [])}
         self.last_result = res
         return res
 

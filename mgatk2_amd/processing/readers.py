@@ -16,6 +16,8 @@ and the dedup then run on the GPU (mgatk2_amd/csrc/mgp_engine.hip).
 
 from __future__ import annotations
 
+import os
+
 import logging
 from collections import defaultdict
 from pathlib import Path
@@ -98,8 +100,11 @@ class BAMReader:
         q = int(self.config.quality.min_baseq)
         md = int(self.config.quality.min_distance_from_end)
         bulk = max(i for i, b in enumerate(self.barcode_list) if b == "bulk") if self.is_bulk_mode else -1
-        return dict(bulk_cell=bulk, pack=pack, pack32=q if pack and -128 <= q <= 127 and md <= 15 else None,
-                    pack32_dist=md)
+        # MGP_RECORDS=64: quality-carrying 64-byte records (the kernel applies the per-base
+        # filter); default 32: the 32-byte records made for the run's thresholds
+        p32 = os.environ.get("MGP_RECORDS", "32") != "64"
+        return dict(bulk_cell=bulk, pack=pack,
+                    pack32=q if pack and p32 and -128 <= q <= 127 and md <= 15 else None, pack32_dist=md)
 
     def open_stream(self, rec_align: int = 64, pack: bool = True):
         """The chrM records as a streaming decode (readers.py:84-93's one pass, in

@@ -34,6 +34,10 @@ def main():
                     help="stream: batches decoded and pushed as they come (the default pipeline); resident: the "
                          "whole chrM set decoded, then one run")
     ap.add_argument("--bam-level", type=int, default=6, help="BGZF level of the synthetic BAM (samtools' default 6)")
+    ap.add_argument("--records", default="32",
+                    help="producer record layouts to compare (MGP_RECORDS): 32 (32-byte records made for the run's "
+                         "thresholds, four per line) and/or 64 (quality-carrying 64-byte records, two per line)")
+    ap.add_argument("--gzip-levels", default="9", help="txt gzip levels to time (MGP_GZIP_LEVEL; 9 = the reference's)")
     ap.add_argument("--devices", default="0",
                     help="engine devices, comma-separated (cells split over them; '0,0' runs two shards on one GPU)")
     args = ap.parse_args()
@@ -66,39 +70,47 @@ def main():
                      "dedup=alignment_and_fragment_length)", "host_threads": args.threads, "devices": args.devices,
            "bam_bytes": bam.stat().st_size, "bam_level": args.bam_level}
     digests = {}
-    for mode in args.modes.split(","):
-        for fmt in args.formats.split(","):
-            cfg = PipelineConfig(min_baseq=20, min_mapq=30, max_strand_bias=1.0, skip_deduplication=False,
-                                 use_fragment_length_dedup=True, min_reads_per_cell=1, n_cores=args.threads)
-            t = time.time()
-            od = out / f"run_{fmt}_{mode}"
-            devs = [int(x) for x in args.devices.split(",")]
-            p = MtDNAPipeline(str(bam), whitelist, od, config=cfg, output_format=fmt, stream=mode == "stream",
-                              devices=devs if len(devs) > 1 else None)
-            ret = p.run()
-            wall = time.time() - t
-            key = f"{fmt}_{mode}"
-            res[key] = {"wall_s": round(wall, 2),
-                        **{k: (round(v, 3) if isinstance(v, float) else v) for k, v in p.timings.items()},
-                        "reads_per_s_end_to_end": round(args.reads / wall), "cells_passed": ret.get("cells_passed_qc")}
-            if fmt == "hdf5":
-                html = od / "mgatk2_report.html"
-                res[key]["report_html_bytes"] = html.stat().st_size if html.exists() else 0
-                res[key]["report_figures"] = html.read_text().count("data:image/png") if html.exists() else 0
-            print(f"[e2e] {key}: {res[key]}", file=sys.stderr, flush=True)
-            if fmt == "txt":  # streamed and resident runs must write the same text
-                import gzip
-                import hashlib
+    runs = [(mode, fmt, rec, lvl) for rec in args.records.split(",") for mode in args.modes.split(",")
+            for fmt in args.formats.split(",") for lvl in (args.gzip_levels.split(",") if fmt == "txt" else ["-"])]
+    for mode, fmt, rec, lvl in runs:
+        os.environ["MGP_RECORDS"] = rec
+        if lvl != "-":
+            os.environ["MGP_GZIP_LEVEL"] = lvl
+        cfg = PipelineConfig(min_baseq=20, min_mapq=30, max_strand_bias=1.0, skip_deduplication=False,
+                             use_fragment_length_dedup=True, min_reads_per_cell=1, n_cores=args.threads)
+        t = time.time()
+        od = out / f"run_{fmt}_{mode}"
+        devs = [int(x) for x in args.devices.split(",")]
+        p = MtDNAPipeline(str(bam), whitelist, od, config=cfg, output_format=fmt, stream=mode == "stream",
+                          devices=devs if len(devs) > 1 else None)
+        ret = p.run()
+        wall = time.time() - t
+        key = f"{fmt}_{mode}" + (f"_r{rec}" if "," in args.records else "") + \
+              (f"_z{lvl}" if lvl != "-" and "," in args.gzip_levels else "")
+        res[key] = {"wall_s": round(wall, 2), "records": rec, "gzip_level": None if lvl == "-" else int(lvl),
+                    **{k: (round(v, 3) if isinstance(v, float) else v) for k, v in p.timings.items()},
+                    "reads_per_s_end_to_end": round(args.reads / wall), "cells_passed": ret.get("cells_passed_qc")}
+        if fmt == "txt":
+            res[key]["txt_gz_bytes"] = sum((od / "output" / f"output.{f}.txt.gz").stat().st_size
+                                           for f in ("A", "C", "G", "T", "coverage"))
+        if fmt == "hdf5":
+            html = od / "mgatk2_report.html"
+            res[key]["report_html_bytes"] = html.stat().st_size if html.exists() else 0
+            res[key]["report_figures"] = html.read_text().count("data:image/png") if html.exists() else 0
+        print(f"[e2e] {key}: {res[key]}", file=sys.stderr, flush=True)
+        if fmt == "txt":  # every mode, record layout and level must write the same text
+            import gzip
+            import hashlib
 
-                h = hashlib.sha256()
-                for f in ("A", "C", "G", "T", "coverage"):
-                    h.update(gzip.decompress((od / "output" / f"output.{f}.txt.gz").read_bytes()))
-                digests[mode] = h.hexdigest()
-            import shutil
+            h = hashlib.sha256()
+            for f in ("A", "C", "G", "T", "coverage"):
+                h.update(gzip.decompress((od / "output" / f"output.{f}.txt.gz").read_bytes()))
+            digests[key] = h.hexdigest()
+        import shutil
 
-            shutil.rmtree(od, ignore_errors=True)
+        shutil.rmtree(od, ignore_errors=True)
     if len(digests) > 1:
-        res["txt_identical_across_modes"] = len(set(digests.values())) == 1
+        res["txt_identical_across_runs"] = len(set(digests.values())) == 1
     print(json.dumps(res), flush=True)
 
 

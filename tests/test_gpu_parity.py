@@ -540,21 +540,24 @@ def _oracle_cells_from_quality_records(oracle_lib, cfg, seed, n, cdf, ref, lo, h
     return exp
 
 
-def _synth_layout(eng, seed, n, nc, cdf, ref, layout, min_baseq):
+def _synth_layout(eng, seed, n, nc, cdf, ref, layout, min_baseq, **shard):
     """The bench's inputs (bench.py): 32-byte records made for min_baseq, four of a
     cell per 128-byte line (quad32), or packed 64-byte records two per line
-    (paired64), or packed 64-byte records in BAM order (packed64)."""
+    (paired64), or packed 64-byte records in BAM order (packed64). shard: a cell
+    shard of the global set (cells=(lo, hi), shard=(rank, world)); nc is then the
+    shard's cell count."""
     from mgatk2_amd.bam import PLACE_PAIRED, place_records
 
     p32 = min_baseq if layout == "quad32" else None
-    eng.synth(seed, n, cdf, ref, pack32=p32)
+    eng.synth(seed, n, cdf, ref, pack32=p32, **shard)
     if layout == "packed64":
         return
+    m = eng.resident()[0]
     cols = eng.download_inputs(columns=("bc", "flag", "start", "tlen"))
-    roff, pay_b = place_records(cols.bc, cols.flag, np.full(n, 32 if p32 is not None else 64, np.uint32), nc,
+    roff, pay_b = place_records(cols.bc, cols.flag, np.full(m, 32 if p32 is not None else 64, np.uint32), nc,
                                 PLACE_PAIRED, start=cols.start, tlen=cols.tlen)
     del cols
-    eng.synth(seed, n, cdf, ref, rec_off=roff, payload_bytes=pay_b, pack32=p32)
+    eng.synth(seed, n, cdf, ref, rec_off=roff, payload_bytes=pay_b, pack32=p32, **shard)
     del roff
 
 
@@ -609,6 +612,65 @@ def test_full_size_invariants_and_cell_sample_c4(engine_lib, oracle_lib, layout)
         exp = _oracle_cells_from_quality_records(oracle_lib, cfg, seed, n, cdf, ref, lo, hi)
         for k in FULL_KEYS:
             np.testing.assert_array_equal(getattr(got, k), getattr(exp, k), err_msg=f"{layout} cells {lo}-{hi} {k}")
+
+
+@pytest.mark.timeout(600)
+def test_c4_eight_cell_shards_equal_the_global_run(engine_lib):
+    """BASELINE config C4 in its 8-GPU form, as bench.py splits it: the read-balanced
+    contiguous cell ranges of bench.cell_bounds(cdf, 8), rank r's reads generated as
+    that cell shard of the global set (its cells' reads plus a share of the reads
+    without a whitelisted barcode), quad32 records placed per shard; run here as 8
+    sequential shard contexts on one device. Every shard's 16-bit rows (and wide
+    flags), per-cell statistics and first reads (by their keys) equal the global
+    run's cells bit for bit; the tallies and read counts add up to the global run's
+    (the reference's per-cell independence, processors.py:112-144)."""
+    import bench
+    from mgatk2_amd.engine import Engine, EngineConfig
+    from mgatk2_amd.synth import cell_cdf, ref_codes
+
+    n, nc, seed, world = 200_000_000, 10_000, 20251015 + 4, 8
+    cfg = EngineConfig(n_cells=nc, min_baseq=20, min_mapq=30, dedup_mode="alignment_and_fragment_length",
+                       min_reads=1)
+    cdf, ref = cell_cdf(seed, nc), ref_codes(seed)
+    b = bench.cell_bounds(cdf, world)
+    assert b[0] == 0 and b[-1] == nc and np.all(np.diff(b) > 0)
+    keycols = ("start", "bc", "tlen", "flag", "mapq")
+    with Engine(cfg) as eng:
+        _synth_layout(eng, seed, n, nc, cdf, ref, "quad32", cfg.min_baseq)
+        eng.run()
+        whole = eng.fetch(dense=False)
+        rows = [eng.fetch_rows16(int(b[r]), int(b[r + 1])) for r in range(world)]
+        gk = eng.download_inputs(columns=keycols)
+    tally = np.zeros_like(whole.ref_tally)
+    sums = dict.fromkeys(("total_reads", "filtered_reads", "duplicate_reads_with_length",
+                          "duplicate_reads_position_only", "cells_passed", "n_barcodes"), 0)
+    for r in range(world):
+        lo, hi = int(b[r]), int(b[r + 1])
+        scfg = EngineConfig(**{**cfg.__dict__, "n_cells": hi - lo})
+        with Engine(scfg) as e2:
+            _synth_layout(e2, seed, n, hi - lo, cdf, ref, "quad32", cfg.min_baseq, cells=(lo, hi), shard=(r, world))
+            e2.run()
+            part = e2.fetch(dense=False)
+            prow = e2.fetch_rows16(0, hi - lo)
+            sk = e2.download_inputs(columns=keycols)
+        assert part.stats["error_bits"] == 0
+        for k in ("counts", "tn5", "depth", "wide"):
+            np.testing.assert_array_equal(getattr(prow, k), getattr(rows[r], k), err_msg=f"rank {r} rows {k}")
+        for k in FULL_KEYS[3:]:
+            np.testing.assert_array_equal(getattr(part, k), getattr(whole, k)[lo:hi], err_msg=f"rank {r} {k}")
+        # a cell's first read: the same read of the global set (same keys; bc rebased)
+        has = part.n_reads > 0
+        fs, fg = part.first_read[has].astype(np.int64), whole.first_read[lo:hi][has].astype(np.int64)
+        for k in keycols:
+            a, g = getattr(sk, k)[fs], getattr(gk, k)[fg]
+            np.testing.assert_array_equal(a, g - lo if k == "bc" else g, err_msg=f"rank {r} first read {k}")
+        tally += part.ref_tally
+        for k in sums:
+            sums[k] += part.stats[k]
+        del prow, sk
+    np.testing.assert_array_equal(tally, whole.ref_tally)
+    for k, v in sums.items():
+        assert v == whole.stats[k], k
 
 
 @pytest.mark.parametrize("layout", ["packed64", "quad32"])

@@ -134,6 +134,48 @@ def test_shard_runs_equal_the_global_run(engine_lib):
     assert dups == whole.stats["duplicate_reads_with_length"]
 
 
+@pytest.mark.parametrize("streamed", [False, True])
+def test_cell_range_of_whole_batches_equals_the_global_run(engine_lib, streamed):
+    """mgp_set_cell_range (ABI 5, the streamed multi-device product path): contexts
+    that take the same whole batches, each keeping one contiguous cell range, give
+    exactly the global run's rows, statistics and first reads of their cells; the
+    tallies and read statistics add up (reads of other cells count only toward
+    total_reads, like reads without a whitelisted barcode)."""
+    from dataclasses import replace
+
+    from mgatk2_amd.engine import EngineConfig
+    from mgatk2_amd.shard import partition_cells
+
+    n, nc, world = 400_000, 90, 3
+    soa = _synth(4242, n, nc)
+    cfg = EngineConfig(n_cells=nc, **CONFIGS["run"])
+    whole = run_resident(engine_lib, cfg, soa)
+    b = partition_cells(np.bincount(soa.bc[soa.bc >= 0], minlength=nc).astype(np.float64), world)
+    tally = np.zeros_like(whole.ref_tally)
+    sums = dict.fromkeys(STATS[1:], 0)
+    for r in range(world):
+        lo, hi = int(b[r]), int(b[r + 1])
+        scfg = EngineConfig(**{**cfg.__dict__, "n_cells": hi - lo})
+        if streamed:
+            scfg = replace(scfg, stream=True, reserve_reads=n, reserve_payload=int(soa.payload.shape[0]) + 4096)
+        with engine_lib.Engine(scfg) as eng:
+            eng.set_cell_range(lo, hi)
+            for a, z in zip(range(0, n, 70_001), list(range(70_001, n, 70_001)) + [n]):
+                eng.push(soa.slice(a, z))
+            part = eng.finish()
+            if streamed:
+                assert eng.stream_info()[1]  # (the run was streamed, not rerun resident)
+        for k in KEYS[:-1] + ("first_read",):
+            np.testing.assert_array_equal(getattr(part, k), getattr(whole, k)[lo:hi], err_msg=f"rank {r} {k}")
+        assert part.stats["total_reads"] == n and part.stats["error_bits"] == 0
+        tally += part.ref_tally
+        for k in sums:
+            sums[k] += part.stats[k]
+    np.testing.assert_array_equal(tally, whole.ref_tally)
+    for k, v in sums.items():
+        assert v == whole.stats[k], k
+
+
 # ---------------------------------------------------------------------------
 # cell-range and 16-bit fetches
 # ---------------------------------------------------------------------------

@@ -567,7 +567,11 @@ class _OracleEngine:
     oracle = None
 
     def __init__(self, cfg, device=0):
-        self.cfg, self.parts, self.rows = cfg, [], None
+        self.cfg, self.parts, self.rows, self.lo = cfg, [], None, None
+
+    def set_cell_range(self, lo, hi):  # (mgp_set_cell_range: the barcode indices rebased at push)
+        assert hi - lo == self.cfg.n_cells and not self.parts
+        self.lo = lo
 
     def windows(self):
         return -(-self.cfg.mito_len // 1275), 1275
@@ -578,8 +582,13 @@ class _OracleEngine:
     def push(self, soa):
         from mgatk2_amd.synth import ReadSoA
 
-        self.parts.append(ReadSoA(*[getattr(soa, k).copy() for k in ("start", "bc", "tlen", "flag", "mapq", "span",
-                                                                     "rec_off", "payload")]))
+        part = ReadSoA(*[getattr(soa, k).copy() for k in ("start", "bc", "tlen", "flag", "mapq", "span", "rec_off",
+                                                          "payload")])
+        if self.lo is not None:
+            bc = part.bc
+            keep = (bc >= self.lo) & (bc < self.lo + self.cfg.n_cells)
+            part.bc[:] = np.where(keep, bc - self.lo, -1)
+        self.parts.append(part)
 
     def copy_wait(self):
         pass
@@ -610,8 +619,9 @@ class _OracleEngine:
 @pytest.mark.parametrize("n_dev", [2, 3, 7])
 def test_stream_sharded_routing_host(n_dev, tmp_path, oracle_lib, monkeypatch):
     """The streamed multi-device path's host side (CellProcessor._run_stream_sharded:
-    batches routed by cell range, per-device rows targets as views of one array, the
-    first reads mapped back to BAM indices, tallies and stats merged), with the oracle
+    every batch pushed whole to every device, each keeping its read-balanced cell
+    range (mgp_set_cell_range, restated in the stand-in), per-device rows targets as
+    views of one array, first reads, tallies and stats merged), with the oracle
     standing in for each device's engine: every output equals the reference's."""
     from mgatk2_amd.engine import PinnedBuffer  # noqa: F401 - (host memory in this stand-in)
     from mgatk2_amd.processing import processors
