@@ -94,9 +94,10 @@ def parse():
     ap.add_argument("--no-host-pack", action="store_true", help="skip timing the host's 32-byte record build")
     ap.add_argument("--no-numa-bind", action="store_true", help="do not move the rank to its GPU's NUMA node")
     ap.add_argument("--pcie-steps", type=int, default=3)
-    ap.add_argument("--batch-reads", type=str, default="16000000",
-                    help="reads per pushed batch of the streamed legs; a comma list also sweeps the headline layout "
-                         "(untimed extra; the first is the headline's)")
+    ap.add_argument("--batch-reads", type=str, default="auto",
+                    help="reads per pushed batch of the streamed legs (auto: the rank's reads / 12.5, about one "
+                         "position window per batch: 16M at C4 on one GPU, 2M per rank on 8); a comma list also "
+                         "sweeps the headline layout (untimed extra; the first is the headline's)")
     ap.add_argument("--record-layout", choices=["quad32", "pack32", "paired", "packed", "full"], default="quad32",
                     help="records of the HBM-resident device leg: 32-byte records made for the run's min_baseq, "
                          "four consecutive records of a cell per 128-byte line (quad32, default: the placement of "
@@ -238,7 +239,7 @@ def main():
     # kernels apply MAPQ, base quality, end distance and ACGT per base)
     head = None
     if not args.device_only:
-        head = stream_leg(ctx, args.layout, [int(args.batch_reads.split(",")[0])], timed=True)
+        head = stream_leg(ctx, args.layout, batch_sizes(args.batch_reads)[:1], timed=True)
     # the same hot path with the inputs already resident in HBM (the device's own rate),
     # on the 32-byte records whose per-base filter the producer resolved (value_device)
     # and on the 64-byte records the kernel filters (device_paired)
@@ -254,7 +255,7 @@ def main():
     # the streamed leg on the 32-byte records and the batch-size sweep (untimed extras)
     pcie_more = None
     if not args.no_pcie:
-        sweep = [int(x) for x in str(args.batch_reads).split(",") if x.strip()]
+        sweep = batch_sizes(args.batch_reads)
         pcie_more = stream_leg(ctx, "pack32", sweep[:1], timed=False)
         if len(sweep) > 1 and not args.device_only:
             pcie_more["sweep_" + args.layout] = stream_leg(ctx, args.layout, sweep, timed=False)["legs"]
@@ -320,6 +321,12 @@ def main():
         print(json.dumps(out), flush=True)
     if dist is not None:
         dist.destroy_process_group()
+
+
+def batch_sizes(spec: str) -> list:
+    """--batch-reads: a comma list of read counts or 'auto' (resolved per rank by
+    stream_leg from its read count)."""
+    return [x.strip() if x.strip() == "auto" else int(x) for x in str(spec).split(",") if x.strip()]
 
 
 class Ctx:
@@ -598,6 +605,11 @@ def stream_leg(ctx: Ctx, layout: str, batch_list: list[int], timed: bool) -> dic
         print(f"[bench] rows target unavailable ({e}); rows fetched after the run", file=sys.stderr)
         rows_target = False
     eng.set_stage_timing(False)  # HIP events around the pileup launches only
+
+    # 'auto': about one position window of reads per batch (the windows a push completes
+    # run while the next batch is copied)
+    batch_list = [max(1_000_000, int(round(n / 12.5 / 1e6)) * 1_000_000) if b == "auto" else int(b)
+                  for b in batch_list]
 
     def batches_for(bs):
         """Batches of bs reads: their columns and their slice of the dense payload."""

@@ -1164,6 +1164,9 @@ __device__ __forceinline__ void group_b_rank(const typename Tr::T* __restrict__ 
 #endif
 constexpr int kGBBlock = MGP_GB_BLOCK;
 constexpr int kBPer = kStageB / kGBBlock;  // elements per lane per step
+#ifndef MGP_GB_XCD
+#define MGP_GB_XCD 0  // pass B's workgroups dealt to the XCDs in contiguous (group, range) runs (A/B)
+#endif
 #ifndef MGP_ABL_B
 #define MGP_ABL_B 0  // pass-B ablations (experiments only): 1 no dedup walk, 2 no pel stores, 3 no loads
 #endif
@@ -1182,7 +1185,22 @@ __global__ void __launch_bounds__(kGBBlock, Tr::kWaves) k_group_b(const typename
                                                     uint32_t spec_layout) {
     using T = typename Tr::T;
     constexpr bool kCompact = sizeof(T) == 8;
-    if (blockIdx.x == 0 && blockIdx.y == 0) check_stats(ck, st, spec_layout);
+    // the workgroup's (cell group, bin range): blockIdx as launched, or with MGP_GB_XCD a
+    // 1-D grid whose dispatch index i (XCD i mod 8) is dealt so that each XCD takes a
+    // contiguous run of (group, range) pairs, ranges fastest: the neighbouring ranges
+    // of a group, whose cell runs share their boundary lines in pel, then write them
+    // through one L2 at about the same time
+#if MGP_GB_XCD
+    const int nrg = (g.nbins + rb - 1) / rb;
+    const unsigned per = gridDim.x / 8u, li = (blockIdx.x & 7u) * per + (blockIdx.x >> 3);
+    if (li >= (unsigned)(ngroups * nrg)) return;
+    const int gx = (int)(li / (unsigned)nrg), gy = (int)(li % (unsigned)nrg);
+    const size_t wg_lin = (size_t)gy * ngroups + gx;
+#else
+    const int gx = blockIdx.x, gy = blockIdx.y;
+    const size_t wg_lin = (size_t)blockIdx.y * gridDim.x + blockIdx.x;
+#endif
+    if (gx == 0 && gy == 0) check_stats(ck, st, spec_layout);
     if (__atomic_load_n(&st->err, __ATOMIC_RELAXED) & ERR_BOUNDS) return;  // unsorted input (k_bin_count)
     __shared__ T stage[kStageB];
     __shared__ uint32_t wcnt[kGBBlock / kWave][kGroup];
@@ -1191,8 +1209,8 @@ __global__ void __launch_bounds__(kGBBlock, Tr::kWaves) k_group_b(const typename
     __shared__ int s_be;
     __shared__ uint32_t s_ndup[kGroup], s_nunp[kGroup];  // the group's duplicates / kept unpaired reads in this bin range
     __shared__ uint16_t wpend[kGBBlock / kWave][kBPer * kWave];  // per wave: stage indices of deferred walks
-    const int gi = blockIdx.x;
-    const int B0 = blockIdx.y * rb, B1 = min(g.nbins, B0 + rb);
+    const int gi = gx;
+    const int B0 = gy * rb, B1 = min(g.nbins, B0 + rb);
     const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // (scalar)
     const int nc = g.nc;
     const int c = gi * kGroup + lane;
@@ -1438,7 +1456,7 @@ __global__ void __launch_bounds__(kGBBlock, Tr::kWaves) k_group_b(const typename
     if (threadIdx.x < 2) {
         unsigned long long t = 0;
         for (int w = 0; w < kGBBlock / kWave; ++w) t += s_dup[threadIdx.x][w];
-        dup_part[2 * ((size_t)blockIdx.y * gridDim.x + blockIdx.x) + threadIdx.x] = t;
+        dup_part[2 * wg_lin + threadIdx.x] = t;
     }
 }
 
@@ -3606,8 +3624,13 @@ static int run_segment(mgp_ctx* ctx, const Seg& sg, int slot, int& dup_parts, in
         // bucket sizes the workgroup keeps in LDS
         const int64_t tgt = MGP_GB_WG;
         const int rb = std::min(kMaxRbB, std::max(1, (int)(((int64_t)ngroups * g.nbins + tgt - 1) / tgt)));
+#if MGP_GB_XCD
+        const unsigned nwg_b = (unsigned)ngroups * (unsigned)((g.nbins + rb - 1) / rb);
+        dim3 gb(8u * ((nwg_b + 7u) / 8u));
+#else
         dim3 gb((unsigned)ngroups, (unsigned)((g.nbins + rb - 1) / rb));
-        dup_parts = (int)(gb.x * gb.y);
+#endif
+        dup_parts = ngroups * ((g.nbins + rb - 1) / rb);  // (one partial per (group, range) workgroup)
         MGP_TRY(ctx->dup_part.ensure((size_t)dup_parts * 16));
         // duplicates of the halo bins of a streaming segment were counted by an earlier one
         const int cnt_lo = sg.w0 > 0 ? (int)((int64_t)sg.w0 * g.W / g.G) : 0;

@@ -84,8 +84,9 @@ class BAMReader:
 
         ``bc`` is the whitelist index (-1 = no tag or not whitelisted). In bulk
         mode every record goes to the ``"bulk"`` cell (readers.py:97-99). With
-        packing, reads that fit get the 32-byte record made for the run's
-        min_baseq (four to a 128-byte line), the others the 64-byte or full one."""
+        packing, reads that fit get the packed 64-byte record, two of a cell to a
+        128-byte line (MGP_RECORDS=32: the 32-byte record made for the run's
+        min_baseq, four to a line), the others the full one."""
         try:
             with self._open() as bam:
                 soa = bam.read_soa(self.config.mito_chr, self.barcode_list, tag=self.config.barcode_tag,
@@ -100,9 +101,12 @@ class BAMReader:
         q = int(self.config.quality.min_baseq)
         md = int(self.config.quality.min_distance_from_end)
         bulk = max(i for i, b in enumerate(self.barcode_list) if b == "bulk") if self.is_bulk_mode else -1
-        # MGP_RECORDS=64: quality-carrying 64-byte records (the kernel applies the per-base
-        # filter); default 32: the 32-byte records made for the run's thresholds
-        p32 = os.environ.get("MGP_RECORDS", "32") != "64"
+        # the producer's records: quality-carrying 64-byte records by default (the kernel
+        # applies the per-base filter of pileup.py:67-88); MGP_RECORDS=32: the 32-byte
+        # records made for the run's thresholds (the producer resolves it). C4 end to end,
+        # one box (profiles/r05/e2e_c4_r5f.json): BAM ingest 5.85-6.01 s with 64-byte
+        # records against 6.13-6.71 s with 32-byte ones; the engine is hidden either way
+        p32 = os.environ.get("MGP_RECORDS", "64") == "32"
         return dict(bulk_cell=bulk, pack=pack,
                     pack32=q if pack and p32 and -128 <= q <= 127 and md <= 15 else None, pack32_dist=md)
 

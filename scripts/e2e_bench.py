@@ -38,6 +38,7 @@ def main():
                     help="producer record layouts to compare (MGP_RECORDS): 32 (32-byte records made for the run's "
                          "thresholds, four per line) and/or 64 (quality-carrying 64-byte records, two per line)")
     ap.add_argument("--gzip-levels", default="9", help="txt gzip levels to time (MGP_GZIP_LEVEL; 9 = the reference's)")
+    ap.add_argument("--reuse-bam", action="store_true", help="keep a BAM of the same size already in --out")
     ap.add_argument("--devices", default="0",
                     help="engine devices, comma-separated (cells split over them; '0,0' runs two shards on one GPU)")
     args = ap.parse_args()
@@ -52,15 +53,21 @@ def main():
     out.mkdir(parents=True, exist_ok=True)
     seed = 20251015 + 3
     t0 = time.time()
-    with Engine(EngineConfig(n_cells=args.cells), device=0) as eng:
-        eng.synth(seed, args.reads, cell_cdf(seed, args.cells), ref_codes(seed), read_len=50)
-        soa = eng.download_inputs()
     whitelist = barcode_names(args.cells, seed)
-    t1 = time.time()
     bam = out / "possorted_bam.bam"
-    write_bam(bam, soa, whitelist, level=args.bam_level, n_threads=args.threads)
-    del soa
-    t2 = time.time()
+    tag = out / "possorted_bam.size"
+    want = f"{args.reads} {args.cells} {args.bam_level}"
+    if args.reuse_bam and bam.exists() and tag.exists() and tag.read_text() == want:
+        t1 = t2 = time.time()
+    else:
+        with Engine(EngineConfig(n_cells=args.cells), device=0) as eng:
+            eng.synth(seed, args.reads, cell_cdf(seed, args.cells), ref_codes(seed), read_len=50)
+            soa = eng.download_inputs()
+        t1 = time.time()
+        write_bam(bam, soa, whitelist, level=args.bam_level, n_threads=args.threads)
+        del soa
+        t2 = time.time()
+        tag.write_text(want)
     (out / "barcodes.tsv").write_text("".join(b + "\n" for b in whitelist))
     print(f"[e2e] generated {args.reads:,} reads in {t1 - t0:.1f}s; BAM {bam.stat().st_size / 1e9:.2f} GB "
           f"written in {t2 - t1:.1f}s", file=sys.stderr, flush=True)

@@ -14,6 +14,7 @@ byte after gunzip.
 from __future__ import annotations
 
 import gzip
+import os
 
 import numpy as np
 import pytest
@@ -417,7 +418,7 @@ def test_pipeline_autodetect_barcodes_gpu(tmp_path, engine_lib, oracle_lib, monk
         assert (tmp_path / "gpu" / rel).read_text() == (tmp_path / "cpu" / rel).read_text(), rel
 
 
-def test_stream_batches_equal_the_whole_decode(tmp_path):
+def test_stream_batches_equal_the_whole_decode(tmp_path, monkeypatch):
     """The streaming decode (mgp_bam_stream_*) gives the whole decode's columns in
     the same order, each record's bytes at its batch's offsets, for every packing /
     placement setting and batch size; the index's record count is the reads'."""
@@ -430,10 +431,12 @@ def test_stream_batches_equal_the_whole_decode(tmp_path):
     bam = tmp_path / "x.bam"
     from mgatk2_amd.bam import write_bam
 
+    monkeypatch.setenv("MGP_RECORDS", "64")  # (restored after the test)
     write_bam(bam, g.soa, g.whitelist)
     with BamFile(bam) as bf:
         assert bf.ref_records("chrM") == g.soa.n
-    for q, pack in ((20, True), (0, True), (20, False)):
+    for q, pack, rec in ((20, True, "32"), (20, True, "64"), (0, True, "32"), (20, False, "64")):
+        os.environ["MGP_RECORDS"] = rec  # (read at each decode: the producer's record layout)
         cfg = PipelineConfig(min_baseq=q)
         reader = BAMReader(str(bam), cfg, g.whitelist)
         whole, _ = reader.read_soa(pack=pack)
@@ -482,14 +485,18 @@ def test_stream_pipelined_decode_equals_serial(tmp_path, monkeypatch, batch):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("records", ["64", "32"])
 @pytest.mark.parametrize("batch", ["997", "50000"])
 @pytest.mark.parametrize("case", ["synth_run", "synth_tenx", "synth_bias", "kat_run"])
-def test_pipeline_streamed_equals_resident_gpu(case, batch, tmp_path, engine_lib, monkeypatch):
+def test_pipeline_streamed_equals_resident_gpu(case, batch, records, tmp_path, engine_lib, monkeypatch):
     """The production pipeline streamed (batches decoded on a producer thread, each
     pushed as it is ready, windows piled as their reads arrive, result rows copied
     back as windows complete) writes byte-identical files to the resident run
-    (whole decode, one run), and both equal the reference's outputs."""
+    (whole decode, one run), and both equal the reference's outputs; with the
+    producer's quality-carrying 64-byte records (the default: the kernel filters per
+    base) and with its 32-byte records (MGP_RECORDS=32: the producer filters)."""
     monkeypatch.setenv("MGP_STREAM_BATCH", batch)
+    monkeypatch.setenv("MGP_RECORDS", records)
     from mgatk2_amd import pipeline
 
     g = Golden(case)
