@@ -470,10 +470,15 @@ def host_pack_leg(args, cfg, device, n: int = 4_000_000) -> dict:
     t0 = time.perf_counter()
     _, _, k = repack32(soa, cfg.min_baseq, cfg.min_distance_from_end, 1, out32, oflag)
     t1 = time.perf_counter() - t0
+    # the threaded rate: best of 3 (a run of ~40 ms on the box's 16-CPU share of a
+    # 256-CPU host is shorter than a scheduler quota period: one throttled period, or a
+    # neighbour's burst, once made it read slower than one thread, round 4)
     nt = host_threads()
-    t0 = time.perf_counter()
-    repack32(soa, cfg.min_baseq, cfg.min_distance_from_end, nt, out32, oflag)
-    tn = time.perf_counter() - t0
+    tn = float("inf")
+    for _ in range(3):
+        t0 = time.perf_counter()
+        repack32(soa, cfg.min_baseq, cfg.min_distance_from_end, nt, out32, oflag)
+        tn = min(tn, time.perf_counter() - t0)
     return {"ns_per_read_1thread": t1 / n * 1e9, "reads_per_s_threads": n / tn, "threads": nt, "packed": k,
             "sample": f"{n:,} full 128-byte records of the generator (run thresholds q{cfg.min_baseq}, "
                       f"min_dist {cfg.min_distance_from_end})"}

@@ -1164,6 +1164,9 @@ __device__ __forceinline__ void group_b_rank(const typename Tr::T* __restrict__ 
 #endif
 constexpr int kGBBlock = MGP_GB_BLOCK;
 constexpr int kBPer = kStageB / kGBBlock;  // elements per lane per step
+#ifndef MGP_GB_NT
+#define MGP_GB_NT 1  // pass B's element loads non-temporal: L2 keeps the partial pel lines (r05: write traffic 1.20 -> 1.06 GB, time equal)
+#endif
 #ifndef MGP_GB_XCD
 #define MGP_GB_XCD 0  // pass B's workgroups dealt to the XCDs in contiguous (group, range) runs (A/B)
 #endif
@@ -1271,6 +1274,8 @@ __global__ void __launch_bounds__(kGBBlock, Tr::kWaves) k_group_b(const typename
                 if constexpr (MGP_ABL_B == 3 && !kCompact) {
                     e[u].w = (unsigned long long)((t * 37u) & 63u) << GM_LCELL_SHIFT;
                     e[u].start = (int)(bst[b - B0 + lo] + t);
+                } else if constexpr (MGP_GB_NT && kCompact) {  // (A/B: the stream's lines evict-first in L2)
+                    e[u] = __builtin_nontemporal_load(&gel2[bst[b - B0 + lo] + (t - spre[lo])]);
                 } else {
                     e[u] = gel2[bst[b - B0 + lo] + (t - spre[lo])];
                 }
