@@ -123,16 +123,17 @@ struct mgp_ctx {
     mgp_rows16 rows_tgt{};
     bool rows_on = false;
     hipEvent_t ev_copy = nullptr, ev_fork = nullptr, ev_join = nullptr;
-    // a pushed batch's payload copy split over h2d_split streams (MGP_H2D_SPLIT; the
-    // extra streams and their events are created on the first split copy)
-    int h2d_split = 1;
-    int seg_min_win = 1;
-    int rows_wg = 256;
-    int32_t cell_lo = 0;   // mgp_set_cell_range: the context's cells in the pushed batches' barcode indices
+    int seg_min_win = 1;     // a streaming push queues a segment once this many windows are complete (MGP_SEG_MIN_WIN)
+    int rows_wg = 256;       // workgroups of a segment's k_rows_to_host (MGP_ROWS_WG)
+    int32_t cell_lo = 0;     // mgp_set_cell_range: the context's cells in the pushed batches' barcode indices
     bool cell_range = false;
-    int pile_wg_stream = 0;  // a streaming run's pileup workgroups per window (set_pile_chunks; 0: the default)    // workgroups of a segment's k_rows_to_host (MGP_ROWS_WG)  // a streaming push queues a segment once this many windows are complete (MGP_SEG_MIN_WIN)
-    hipStream_t s_cx[3] = {nullptr, nullptr, nullptr};
-    hipEvent_t ev_cx[3] = {nullptr, nullptr, nullptr}, ev_cfork = nullptr;
+    int pile_wg_stream = 0;  // a streaming run's pileup workgroups per window (set_pile_chunks; 0: the default)
+    // on-device pairing of dense 64-byte batches (mgp_push_batch): two staging buffers
+    // the H2D copies land in, the event after the pairing kernels that last read each
+    bool dev_pair = true;  // (MGP_DEV_PAIR=0: records stay in BAM order, for A/B)
+    int stage_i = 0;
+    DevBuf stage[2], pair_rank, pair_cnt, pair_lines;
+    hipEvent_t ev_stage[2] = {nullptr, nullptr};
     hipEvent_t ev_bits = nullptr;  // the run's input check words have reached h_bits
     uint32_t* h_bits = nullptr;    // pinned host copy of the input check words (roff_irregular)
     static constexpr int kRing = 64;   // per-run event slots (timing over many runs without syncs)
@@ -2768,6 +2769,83 @@ __global__ void k_rebase_bc(int32_t* __restrict__ bc, int64_t n, int32_t lo, int
     }
 }
 
+// ---- on-device pairing of a dense batch of 64-byte records (mgp_push_batch) ----
+// A streaming producer's batch holds its records in BAM order: a 128-byte line then
+// carries two reads of unrelated cells, and the pileup, which gathers each cell's
+// reads, fetches every line twice (the resident step on such records: pileup 5.2 ms
+// at C4 against 3.5 ms with a cell's records two per line, profiles/r05). After the
+// batch lands in a staging buffer, three kernels put the records of one cell two per
+// line, the rule of mgp_place_records applied per workgroup range: each workgroup
+// ranks its range's reads per cell with LDS atomics (reads the engine drops, and
+// reads without a cell of this context, pair among themselves), the ranges' line
+// counts are scanned, and the records are copied to line base + rank / 2, half rank & 1.
+// Atomic ranks follow the waves' progress, so a line's two reads are near each
+// other in the cell's order, not always adjacent; the results never depend on where
+// a record sits (every read is found through its rec_off).
+constexpr int kPairBlock = 1024;
+constexpr int64_t kPairReads = 1 << 18;  // reads of a pairing workgroup's range
+constexpr int kPairMaxKeys = 32768;      // cells + 1 whose counters fit a workgroup's LDS
+
+__device__ __forceinline__ int pair_key(int32_t c, uint16_t f, int nc) {
+    const uint16_t drop = MGP_FLAG_UNMAPPED | MGP_FLAG_SECONDARY | MGP_FLAG_SUPPLEMENTARY;
+    return (c >= 0 && c < nc && !(f & drop)) ? c : nc;
+}
+
+__global__ void __launch_bounds__(kPairBlock) k_pair_rank(const int32_t* __restrict__ bc,
+                                                          const uint16_t* __restrict__ flag, int64_t n, int nc,
+                                                          uint32_t* __restrict__ rank, uint32_t* __restrict__ cntw,
+                                                          uint32_t* __restrict__ lines_w) {
+    extern __shared__ uint32_t pcnt[];  // [nc + 1]
+    __shared__ uint32_t tot;
+    const int64_t lo = (int64_t)blockIdx.x * kPairReads, hi = min(n, lo + kPairReads);
+    for (int k = threadIdx.x; k <= nc; k += blockDim.x) pcnt[k] = 0u;
+    if (threadIdx.x == 0) tot = 0u;
+    __syncthreads();
+    for (int64_t i = lo + threadIdx.x; i < hi; i += blockDim.x) rank[i] = atomicAdd(&pcnt[pair_key(bc[i], flag[i], nc)], 1u);
+    __syncthreads();
+    uint32_t lines = 0;
+    for (int k = threadIdx.x; k <= nc; k += blockDim.x) {
+        const uint32_t x = pcnt[k];
+        cntw[(size_t)blockIdx.x * (nc + 1) + k] = x;
+        lines += (x + 1u) >> 1;
+    }
+    lines = wave_sum(lines);
+    if ((threadIdx.x & 63) == 0) atomicAdd(&tot, lines);
+    __syncthreads();
+    if (threadIdx.x == 0) lines_w[blockIdx.x] = tot;
+}
+
+// the ranges' first lines (exclusive scan of their line counts, in place)
+__global__ void __launch_bounds__(1024) k_pair_scan(uint32_t* __restrict__ lines_w, int nw) {
+    __shared__ uint32_t wsum[16], carry;
+    block_exclusive_scan(lines_w, nw, lines_w, wsum, &carry);
+}
+
+// every record to its line half; rec_off = pay0 + line x 128 + half x 64. Four lanes
+// copy a record (16 bytes each).
+__global__ void __launch_bounds__(kPairBlock) k_pair_place(const uint4* __restrict__ src, const int32_t* __restrict__ bc,
+                                                           const uint16_t* __restrict__ flag, int64_t n, int nc,
+                                                           const uint32_t* __restrict__ rank,
+                                                           const uint32_t* __restrict__ cntw,
+                                                           const uint32_t* __restrict__ wline, uint64_t pay0,
+                                                           uint8_t* __restrict__ payload, uint64_t* __restrict__ roff) {
+    extern __shared__ uint32_t lbase[];  // [nc + 1]: each key's first line in the range
+    __shared__ uint32_t wsum[16], carry;
+    const int64_t lo = (int64_t)blockIdx.x * kPairReads, hi = min(n, lo + kPairReads);
+    for (int k = threadIdx.x; k <= nc; k += blockDim.x) lbase[k] = (cntw[(size_t)blockIdx.x * (nc + 1) + k] + 1u) >> 1;
+    __syncthreads();
+    block_exclusive_scan(lbase, nc + 1, lbase, wsum, &carry);
+    const uint32_t w0 = wline[blockIdx.x];
+    for (int64_t t = lo * 4 + threadIdx.x; t < hi * 4; t += blockDim.x) {
+        const int64_t i = t >> 2;
+        const uint32_t r = rank[i];
+        const uint64_t line = (uint64_t)w0 + lbase[pair_key(bc[i], flag[i], nc)] + (r >> 1);
+        const uint64_t off = pay0 + line * 128u + (uint64_t)(r & 1u) * 64u;
+        reinterpret_cast<uint4*>(payload + off)[t & 3] = src[t];
+        if ((t & 3) == 0) roff[i] = off;
+    }
+}
+
 // mgp_push_batch without rec_off: dense records in BAM order, record i at base + i x stride
 __global__ void k_dense_off(uint64_t* __restrict__ roff, int64_t n, uint64_t base, uint64_t stride) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -3082,6 +3160,8 @@ int mgp_open(const mgp_config* cfg, int hip_device, mgp_ctx** out) {
         (void)hipFuncSetAttribute((const void*)k_pileup<kLayAny>, hipFuncAttributeMaxDynamicSharedMemorySize, lds_max);
         (void)hipFuncSetAttribute((const void*)k_pileup<kLayP64>, hipFuncAttributeMaxDynamicSharedMemorySize, lds_max);
         (void)hipFuncSetAttribute((const void*)k_pileup<kLayP32>, hipFuncAttributeMaxDynamicSharedMemorySize, lds_max);
+        (void)hipFuncSetAttribute((const void*)k_pair_rank, hipFuncAttributeMaxDynamicSharedMemorySize, lds_max);
+        (void)hipFuncSetAttribute((const void*)k_pair_place, hipFuncAttributeMaxDynamicSharedMemorySize, lds_max);
         (void)hipGetLastError();
         if ((size_t)ctx->g.L * 4 + 2048 > prop.sharedMemPerBlock) {
             delete ctx;
@@ -3090,7 +3170,8 @@ int mgp_open(const mgp_config* cfg, int hip_device, mgp_ctx** out) {
     }
     HIP_TRY(hipStreamCreateWithFlags(&ctx->s_comp, hipStreamNonBlocking));
     HIP_TRY(hipStreamCreateWithFlags(&ctx->s_copy, hipStreamNonBlocking));
-    if (const char* e = std::getenv("MGP_H2D_SPLIT")) ctx->h2d_split = std::max(1, std::min(4, std::atoi(e)));
+    if (const char* e = std::getenv("MGP_DEV_PAIR")) ctx->dev_pair = std::atoi(e) != 0;
+    for (int i = 0; i < 2; ++i) HIP_TRY(hipEventCreateWithFlags(&ctx->ev_stage[i], hipEventDisableTiming));
     if (const char* e = std::getenv("MGP_SEG_MIN_WIN")) ctx->seg_min_win = std::max(1, std::atoi(e));
     if (const char* e = std::getenv("MGP_ROWS_WG")) ctx->rows_wg = std::max(1, std::atoi(e));
     ctx->pile_wg_stream = MGP_PILE_WG_STREAM;
@@ -3167,11 +3248,13 @@ void mgp_close(mgp_ctx* ctx) {
     (void)hipStreamDestroy(ctx->s_copy);
     (void)hipStreamDestroy(ctx->s_side);
     (void)hipStreamDestroy(ctx->s_d2h);
-    for (int i = 0; i < 3; ++i) {
-        if (ctx->s_cx[i]) (void)hipStreamDestroy(ctx->s_cx[i]);
-        if (ctx->ev_cx[i]) (void)hipEventDestroy(ctx->ev_cx[i]);
+    for (int i = 0; i < 2; ++i) {
+        if (ctx->ev_stage[i]) (void)hipEventDestroy(ctx->ev_stage[i]);
+        ctx->stage[i].release();
     }
-    if (ctx->ev_cfork) (void)hipEventDestroy(ctx->ev_cfork);
+    ctx->pair_rank.release();
+    ctx->pair_cnt.release();
+    ctx->pair_lines.release();
     (void)hipEventDestroy(ctx->ev_rows);
     delete ctx;
 }
@@ -3230,14 +3313,26 @@ int mgp_push_batch(mgp_ctx* ctx, const mgp_batch* b) {
     HIP_TRY(hipSetDevice(ctx->dev));
     const int64_t n0 = ctx->n, nb = b->n_reads;
     const int64_t pay0 = (ctx->pay + 255) & ~int64_t(255);  // keeps the batch's record alignment
-    MGP_TRY(ensure_inputs(ctx, n0 + nb, pay0 + b->payload_bytes, true));
-    hipStream_t s = ctx->s_copy;
+    const int nc = ctx->g.nc;
+    // a dense batch of 64-byte slots lands in a staging buffer and is paired on the device
+    const bool pair = dense && stride == 64 && ctx->dev_pair && nb >= 65536 && nc + 1 <= kPairMaxKeys;
+    const int npw = pair ? (int)((nb + kPairReads - 1) / kPairReads) : 0;
+    // paired: at most one line per two reads plus one half-empty line per key and range
+    const int64_t pay_b = pair ? 64 * (nb + (int64_t)npw * (nc + 2)) : b->payload_bytes;
+    MGP_TRY(ensure_inputs(ctx, n0 + nb, pay0 + pay_b, true));
+    hipStream_t s = ctx->s_copy, sp = ctx->s_comp;
+    // the copy stream only copies (the link never waits on a kernel); the batch's
+    // kernels follow on the compute stream, ahead of the segments it completes
+    const int j = ctx->stage_i;
+    if (pair) {
+        MGP_TRY(ctx->stage[j].ensure((size_t)b->payload_bytes));
+        MGP_TRY(ctx->pair_rank.ensure((size_t)nb * 4));
+        MGP_TRY(ctx->pair_cnt.ensure((size_t)npw * (nc + 1) * 4));
+        MGP_TRY(ctx->pair_lines.ensure((size_t)npw * 4));
+        HIP_TRY(hipStreamWaitEvent(s, ctx->ev_stage[j], 0));  // the kernels that read this buffer last
+    }
     if (b->start) HIP_TRY(hipMemcpyAsync(ctx->start.as<int32_t>() + n0, b->start, nb * 4, hipMemcpyHostToDevice, s));
     HIP_TRY(hipMemcpyAsync(ctx->bc.as<int32_t>() + n0, b->bc, nb * 4, hipMemcpyHostToDevice, s));
-    if (ctx->cell_range) {
-        k_rebase_bc<<<blocks_for(nb), kBlock, 0, s>>>(ctx->bc.as<int32_t>() + n0, nb, ctx->cell_lo, ctx->g.nc);
-        HIP_TRY(hipGetLastError());
-    }
     HIP_TRY(hipMemcpyAsync(ctx->tlen.as<int32_t>() + n0, b->tlen, nb * 4, hipMemcpyHostToDevice, s));
     HIP_TRY(hipMemcpyAsync(ctx->flag.as<uint16_t>() + n0, b->flag, nb * 2, hipMemcpyHostToDevice, s));
     HIP_TRY(hipMemcpyAsync(ctx->mapq.as<uint8_t>() + n0, b->mapq, nb, hipMemcpyHostToDevice, s));
@@ -3245,59 +3340,52 @@ int mgp_push_batch(mgp_ctx* ctx, const mgp_batch* b) {
         HIP_TRY(hipMemcpyAsync(ctx->span.as<uint32_t>() + n0, b->span, nb * 4, hipMemcpyHostToDevice, s));
     if (!dense)
         HIP_TRY(hipMemcpyAsync(ctx->roff.as<uint64_t>() + n0, b->rec_off, nb * 8, hipMemcpyHostToDevice, s));
-    if (b->payload_bytes) {
-        // a large payload in h2d_split parts on as many streams (copy engines), joined
-        // back into the copy stream before the batch's checks
-        const int k = b->payload_bytes >= (int64_t)(64 << 20) ? ctx->h2d_split : 1;
-        uint8_t* dst = ctx->payload.as<uint8_t>() + pay0;
-        if (k <= 1) {
-            HIP_TRY(hipMemcpyAsync(dst, b->payload, b->payload_bytes, hipMemcpyHostToDevice, s));
-        } else {
-            if (!ctx->ev_cfork) {
-                HIP_TRY(hipEventCreateWithFlags(&ctx->ev_cfork, hipEventDisableTiming));
-                for (int i = 0; i < 3; ++i) {
-                    HIP_TRY(hipStreamCreateWithFlags(&ctx->s_cx[i], hipStreamNonBlocking));
-                    HIP_TRY(hipEventCreateWithFlags(&ctx->ev_cx[i], hipEventDisableTiming));
-                }
-            }
-            HIP_TRY(hipEventRecord(ctx->ev_cfork, s));
-            const int64_t part = ((b->payload_bytes + k - 1) / k + 4095) & ~int64_t(4095);
-            for (int i = 0; i < k; ++i) {
-                const int64_t o = i * part, len = std::min(part, b->payload_bytes - o);
-                if (len <= 0) break;
-                hipStream_t si = i == 0 ? s : ctx->s_cx[i - 1];
-                if (i > 0) HIP_TRY(hipStreamWaitEvent(si, ctx->ev_cfork, 0));
-                HIP_TRY(hipMemcpyAsync(dst + o, b->payload + o, len, hipMemcpyHostToDevice, si));
-                if (i > 0) {
-                    HIP_TRY(hipEventRecord(ctx->ev_cx[i - 1], si));
-                    HIP_TRY(hipStreamWaitEvent(s, ctx->ev_cx[i - 1], 0));
-                }
-            }
-        }
+    if (b->payload_bytes)
+        HIP_TRY(hipMemcpyAsync(pair ? ctx->stage[j].as<uint8_t>() : ctx->payload.as<uint8_t>() + pay0, b->payload,
+                               b->payload_bytes, hipMemcpyHostToDevice, s));
+    HIP_TRY(hipEventRecord(ctx->ev_copy, s));
+    HIP_TRY(hipStreamWaitEvent(sp, ctx->ev_copy, 0));
+    if (ctx->cell_range) {
+        k_rebase_bc<<<blocks_for(nb), kBlock, 0, sp>>>(ctx->bc.as<int32_t>() + n0, nb, ctx->cell_lo, nc);
+        HIP_TRY(hipGetLastError());
     }
-    if (dense) {
-        k_dense_off<<<blocks_for(nb), kBlock, 0, s>>>(ctx->roff.as<uint64_t>() + n0, nb, (uint64_t)pay0,
-                                                      (uint64_t)stride);
+    if (pair) {
+        const size_t lds = (size_t)(nc + 1) * 4;
+        k_pair_rank<<<npw, kPairBlock, lds, sp>>>(ctx->bc.as<int32_t>() + n0, ctx->flag.as<uint16_t>() + n0, nb, nc,
+                                                  ctx->pair_rank.as<uint32_t>(), ctx->pair_cnt.as<uint32_t>(),
+                                                  ctx->pair_lines.as<uint32_t>());
+        HIP_TRY(hipGetLastError());
+        k_pair_scan<<<1, 1024, 0, sp>>>(ctx->pair_lines.as<uint32_t>(), npw);
+        HIP_TRY(hipGetLastError());
+        k_pair_place<<<npw, kPairBlock, lds, sp>>>(
+            ctx->stage[j].as<uint4>(), ctx->bc.as<int32_t>() + n0, ctx->flag.as<uint16_t>() + n0, nb, nc,
+            ctx->pair_rank.as<uint32_t>(), ctx->pair_cnt.as<uint32_t>(), ctx->pair_lines.as<uint32_t>(),
+            (uint64_t)pay0, ctx->payload.as<uint8_t>(), ctx->roff.as<uint64_t>() + n0);
+        HIP_TRY(hipGetLastError());
+        HIP_TRY(hipEventRecord(ctx->ev_stage[j], sp));
+        ctx->stage_i ^= 1;
+    } else if (dense) {
+        k_dense_off<<<blocks_for(nb), kBlock, 0, sp>>>(ctx->roff.as<uint64_t>() + n0, nb, (uint64_t)pay0,
+                                                       (uint64_t)stride);
         HIP_TRY(hipGetLastError());
     } else if (pay0) {
-        k_add_u64<<<blocks_for(nb), kBlock, 0, s>>>(ctx->roff.as<uint64_t>() + n0, nb, (uint64_t)pay0);
+        k_add_u64<<<blocks_for(nb), kBlock, 0, sp>>>(ctx->roff.as<uint64_t>() + n0, nb, (uint64_t)pay0);
         HIP_TRY(hipGetLastError());
     }
     // every record inside the batch's payload (and, without a span / start column, its
     // span / start from the record)
-    k_check_records<<<blocks_for(nb), kBlock, 0, s>>>(
+    k_check_records<<<blocks_for(nb), kBlock, 0, sp>>>(
         ctx->payload.as<uint8_t>(), ctx->roff.as<uint64_t>() + n0, ctx->flag.as<uint16_t>() + n0, nb, (uint64_t)pay0,
-        (uint64_t)(pay0 + b->payload_bytes), b->span ? nullptr : ctx->span.as<uint32_t>() + n0,
+        (uint64_t)(pay0 + pay_b), b->span ? nullptr : ctx->span.as<uint32_t>() + n0,
         b->start ? nullptr : ctx->start.as<int32_t>() + n0, ctx->order_bad.as<uint32_t>());
     HIP_TRY(hipGetLastError());
     if (ctx->stream) {
-        k_check_order<<<blocks_for(nb), kBlock, 0, s>>>(ctx->start.as<int32_t>(), n0, n0 + nb,
-                                                        ctx->order_bad.as<uint32_t>());
+        k_check_order<<<blocks_for(nb), kBlock, 0, sp>>>(ctx->start.as<int32_t>(), n0, n0 + nb,
+                                                         ctx->order_bad.as<uint32_t>());
         HIP_TRY(hipGetLastError());
     }
-    HIP_TRY(hipEventRecord(ctx->ev_copy, s));
     ctx->n = n0 + nb;
-    ctx->pay = pay0 + b->payload_bytes;
+    ctx->pay = pay0 + pay_b;
     ctx->ran = false;
     ctx->no_spec = false;
     ctx->bits_cached = false;

@@ -107,7 +107,10 @@ class BAMReader:
         # one box (profiles/r05/e2e_c4_r5f.json): BAM ingest 5.85-6.01 s with 64-byte
         # records against 6.13-6.71 s with 32-byte ones; the engine is hidden either way
         p32 = os.environ.get("MGP_RECORDS", "64") == "32"
-        return dict(bulk_cell=bulk, pack=pack,
+        # MGP_PLACEMENT=dense: records in BAM order (no cell pairing: one decoder pass writes
+        # columns and records, no placement thread), for A/B
+        paired = os.environ.get("MGP_PLACEMENT", "paired") != "dense"
+        return dict(bulk_cell=bulk, pack=pack, paired=pack and paired,
                     pack32=q if pack and p32 and -128 <= q <= 127 and md <= 15 else None, pack32_dist=md)
 
     def open_stream(self, rec_align: int = 64, pack: bool = True):

@@ -34,7 +34,7 @@ def main():
                     help="stream: batches decoded and pushed as they come (the default pipeline); resident: the "
                          "whole chrM set decoded, then one run")
     ap.add_argument("--bam-level", type=int, default=6, help="BGZF level of the synthetic BAM (samtools' default 6)")
-    ap.add_argument("--records", default="32",
+    ap.add_argument("--records", default="64",
                     help="producer record layouts to compare (MGP_RECORDS): 32 (32-byte records made for the run's "
                          "thresholds, four per line) and/or 64 (quality-carrying 64-byte records, two per line)")
     ap.add_argument("--gzip-levels", default="9", help="txt gzip levels to time (MGP_GZIP_LEVEL; 9 = the reference's)")

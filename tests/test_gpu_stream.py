@@ -449,6 +449,54 @@ def test_push_without_offsets_and_spans(engine_lib, layout, streamed, no_start):
     np.testing.assert_array_equal(dev.start, soa.start)
 
 
+@pytest.mark.parametrize("cfgname", ["run", "tenx"])
+@pytest.mark.parametrize("streamed", [False, True])
+def test_dense_64_byte_batches_paired_on_the_device(engine_lib, monkeypatch, streamed, cfgname):
+    """Dense BAM-order batches of 64-byte records (a streaming producer's, rec_off
+    NULL) are paired on the device (k_pair_rank / k_pair_scan / k_pair_place: a
+    cell's records two per 128-byte line; batches of 100k, 700k and 700k reads, so
+    one and three pairing ranges): the results equal those of the same batches left
+    in BAM order (MGP_DEV_PAIR=0), every record lands in a slot of its own, at a
+    64-byte multiple, with its bytes unchanged, and the two records sharing a line
+    belong to one cell (or are both reads the engine drops)."""
+    from dataclasses import replace
+
+    from mgatk2_amd.engine import EngineConfig
+    from mgatk2_amd.synth import relocate, synth_reads
+
+    nc = 200
+    cfg = EngineConfig(n_cells=nc, **CONFIGS[cfgname])
+    soa = relocate(synth_reads(818, 1_500_000, nc, pack=True), rec_align=64, n_cells=nc)
+    assert np.array_equal(soa.rec_off, 64 * np.arange(soa.n, dtype=np.uint64))
+    if streamed:
+        cfg = replace(cfg, stream=True, reserve_reads=soa.n, reserve_payload=int(soa.payload.shape[0]) * 2)
+    cuts = [0, 100_000, 800_000, soa.n]
+    out = {}
+    for pair in ("1", "0"):
+        monkeypatch.setenv("MGP_DEV_PAIR", pair)
+        with engine_lib.Engine(cfg) as eng:
+            for a, b in zip(cuts[:-1], cuts[1:]):
+                eng.push(_columnless(soa, a, b, 64, no_start=True))
+            res = eng.finish()
+            dev = eng.download_inputs(columns=("rec_off", "payload", "bc", "flag"))
+        out[pair] = (res, dev)
+    assert_same(out["1"][0], out["0"][0], f"paired on the device vs BAM order ({cfgname}, streamed={streamed})")
+    dev = out["1"][1]
+    off = dev.rec_off.astype(np.int64)
+    assert np.all(off % 64 == 0) and np.unique(off).size == soa.n
+    recs = dev.payload.reshape(-1, 64)[off // 64]
+    np.testing.assert_array_equal(recs, soa.payload.reshape(-1, 64))  # every record's bytes, in read order
+    drop = (dev.bc < 0) | ((dev.flag & (0x4 | 0x100 | 0x800)) != 0)
+    key = np.where(drop, -1, dev.bc)
+    line = off // 128
+    order = np.argsort(line, kind="stable")
+    ls, ks = line[order], key[order]
+    shared = ls[1:] == ls[:-1]
+    assert shared.sum() > 0.4 * soa.n  # most records share their line
+    assert np.all(ks[1:][shared] == ks[:-1][shared])
+    assert np.array_equal(out["0"][1].rec_off.astype(np.int64) % 64, np.zeros(soa.n, np.int64))
+
+
 def test_push_without_offsets_rejects_ragged_payloads(engine_lib):
     from mgatk2_amd.engine import EngineConfig
     from mgatk2_amd.exceptions import InvalidInputError
