@@ -1423,6 +1423,30 @@ struct Decoder {
         t_recs += now_s() - t0;
     }
     double t_recs = 0;
+    // BAM-order placement of the current chunk at k0: each record at the cursor in
+    // rec_align-sized slots (a running sum: the sizes come from pass 1)
+    void dense_offsets(size_t k0, const Cols& c) {
+        const size_t m = recs.size();
+        for (size_t i = 0; i < m; ++i) {
+            const uint64_t off = (cursor + amask) & ~amask;
+            c.roff[k0 + i] = off;
+            cursor = off + ((rsz[i] + amask) & ~amask);
+        }
+    }
+    // the current chunk's payload records at their offsets, on the pool
+    void records_inline(size_t k0, const Cols& c) {
+        const double t0 = now_s();
+        const size_t m = recs.size();
+        const int tn = (int)std::max<size_t>(1, std::min<size_t>((size_t)pool.size(), m / 4096 + 1));
+        pool.run(tn, [&](int t) {
+            const size_t lo = m * (size_t)t / (size_t)tn, hi = m * (size_t)(t + 1) / (size_t)tn;
+            int64_t tg = 0, fs = -1;  // (tags are counted by count_tags)
+            for (size_t i = lo; i < hi; ++i)
+                decode_one(c, recs[i], sizes[i], k0 + i, c.roff[k0 + i], ncg[i], cgp[i], (int)pkd[i], tg, fs, 0, false,
+                           true);
+        });
+        t_recs += now_s() - t0;
+    }
 };
 
 // Growable malloc'd array (handed to the caller as is: no final copy).
@@ -1619,6 +1643,11 @@ struct mgp_bam_stream {
         return !e || std::strtol(e, nullptr, 10) != 0;
     }
     bool pipe = true, fuse = true;
+    // BAM-order records (no cell pairing: the engine pairs a dense batch of 64-byte
+    // records on the device, mgp_push_batch): pass 1 and the columns in one pool pass,
+    // the offsets by a running sum, the records in a second pool pass; no placement
+    // thread, no duplicate-key stage (MGP_BAM_DENSE_FUSE=0: the two-pass decode)
+    bool dense_fuse = false;
     ChunkRecs pend;
     bool pending = false;
     Worker placer;
@@ -1629,6 +1658,8 @@ struct mgp_bam_stream {
         st.hold = pipe;
         const char* ef = std::getenv("MGP_BAM_FUSE");  // pass 1 and the columns in one pass (pipelined)
         fuse = pipe && (!ef || std::strtol(ef, nullptr, 10) != 0);
+        const char* ed = std::getenv("MGP_BAM_DENSE_FUSE");
+        dense_fuse = !dec.paired && (!ed || std::strtol(ed, nullptr, 10) != 0);
     }
     ~mgp_bam_stream() {
         if (pending) placer.wait();  // (an abandoned batch: its placement may still run)
@@ -1638,10 +1669,11 @@ struct mgp_bam_stream {
                          "[mgp_bam_stream] %lld records, %d threads%s: open %.3f s; waiting for inflated chunks %.3f, "
                          "record walk %.3f (listed %.3f; prefetch thread %.3f; %lld + %lld chunks), classify %.3f, fields %.3f, "
                          "duplicate keys %.3f, placement %.3f (waited for %.3f), records %.3f\n",
-                         (long long)decoded, dec.pool.size(), pipe ? ", pipelined" : "", now_s() - t_open, t_fill,
+                         (long long)decoded, dec.pool.size(), pipe ? ", pipelined" : dense_fuse ? ", BAM order fused" : "",
+                         now_s() - t_open, t_fill,
                          t_walk, t_list, st.pf ? st.pf->t_walk : 0.0, (long long)n_listed, (long long)n_walked, t_class, dec.t_fields,
                          dec.t_dups, dec.t_place, t_wait,
-                         pipe ? dec.t_recs : dec.t_p2 - dec.t_fields - dec.t_place);
+                         (pipe || dense_fuse) ? dec.t_recs : dec.t_p2 - dec.t_fields - dec.t_place);
     }
     // the pending chunk's placement finished, its records written, the buffers it read released
     bool drain(const Cols& c) {
@@ -1810,7 +1842,9 @@ int64_t mgp_bam_stream_next(mgp_bam_stream* s, int64_t cap_reads, int64_t cap_pa
         s->t_walk += tw - tp1;
         // pipelined: pass 1 and the columns in one pool pass (one trip through the records'
         // memory; a record cut off below is decoded again with the next batch)
-        if (s->fuse ? !dec.classify_fields_all(k, s->decoded + (int64_t)k, c) : !dec.classify_all()) return -1;
+        if ((s->fuse || s->dense_fuse) ? !dec.classify_fields_all(k, s->decoded + (int64_t)k, c)
+                                       : !dec.classify_all())
+            return -1;
         s->t_class += now_s() - tw;
         for (size_t i = 0; i < dec.recs.size(); ++i) {
             const uint64_t w = dec.worst(i);
@@ -1835,6 +1869,10 @@ int64_t mgp_bam_stream_next(mgp_bam_stream* s, int64_t cap_reads, int64_t cap_pa
                 dec.move_chunk(s->pend, k);
                 s->pending = true;
                 s->placer.submit([s, c, cap_payload] { s->dec.place_stage(s->pend, c, (uint64_t)cap_payload); });
+            } else if (s->dense_fuse) {
+                dec.count_tags(s->decoded + (int64_t)k);
+                dec.dense_offsets(k, c);
+                dec.records_inline(k, c);
             } else if (dec.decode(k, s->decoded + (int64_t)k, reserve, cols) != 0) {
                 return -1;
             }

@@ -157,6 +157,17 @@ class CellProcessor:
         producer.start()
         return bam, st, n_hint, free, full, producer, times
 
+    @staticmethod
+    def _push_view(item) -> ReadSoA:
+        """A decoded batch as pushed: records in BAM order, each a 64-byte slot, go
+        without their rec_off / start / span columns (ABI 4: the engine places and
+        pairs them on the device and takes start and span from the records); any
+        other batch with its offsets."""
+        soa = item.soa()
+        if soa.n and item.payload_bytes == 64 * soa.n and not np.any(soa.rec_off[-1:] != 64 * (soa.n - 1)):
+            return ReadSoA(None, soa.bc, soa.tlen, soa.flag, soa.mapq, None, None, soa.payload)
+        return soa
+
     def _rows_target(self, n_cells: int, eng=None, windows: tuple[int, int] | None = None) -> Rows16 | None:
         """Pinned 16-bit result rows for all cells (the rows target)."""
         if n_cells <= 0:
@@ -227,7 +238,7 @@ class CellProcessor:
                     if n_batches == 0:
                         times["first_batch"] = time.perf_counter()
                     settle(False)
-                    eng.push(item.soa())
+                    eng.push(self._push_view(item))
                     eng.copy_wait()  # its pinned arrays may be refilled now
                     free.put(item)
                     n_batches += 1
@@ -386,7 +397,7 @@ class CellProcessor:
                     if errors:
                         raise errors[0]
                     if parts:
-                        soa = item.soa()
+                        soa = self._push_view(item)
                         left = [len(parts), threading.Lock()]
                         for d, _, _ in parts:
                             queues[d].put((item, soa, left))

@@ -107,9 +107,13 @@ class BAMReader:
         # one box (profiles/r05/e2e_c4_r5f.json): BAM ingest 5.85-6.01 s with 64-byte
         # records against 6.13-6.71 s with 32-byte ones; the engine is hidden either way
         p32 = os.environ.get("MGP_RECORDS", "64") == "32"
-        # MGP_PLACEMENT=dense: records in BAM order (no cell pairing: one decoder pass writes
-        # columns and records, no placement thread), for A/B
-        paired = os.environ.get("MGP_PLACEMENT", "paired") != "dense"
+        # where a cell's records are paired two per 128-byte line (the pileup's gathers):
+        # "device" (default with 64-byte records): the decoder leaves the records in BAM
+        # order (pass 1 and the columns in one pool pass, the records in a second, no
+        # placement thread, no duplicate-key stage) and the engine pairs each dense batch
+        # on the device (mgp_push_batch); "paired": the decoder's placement thread
+        # (mgp_place_records' rule; the 32-byte records always take it, four per line)
+        paired = p32 or os.environ.get("MGP_PLACEMENT", "device") == "paired"
         return dict(bulk_cell=bulk, pack=pack, paired=pack and paired,
                     pack32=q if pack and p32 and -128 <= q <= 127 and md <= 15 else None, pack32_dist=md)
 

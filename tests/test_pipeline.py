@@ -432,11 +432,14 @@ def test_stream_batches_equal_the_whole_decode(tmp_path, monkeypatch):
     from mgatk2_amd.bam import write_bam
 
     monkeypatch.setenv("MGP_RECORDS", "64")  # (restored after the test)
+    monkeypatch.setenv("MGP_PLACEMENT", "device")
     write_bam(bam, g.soa, g.whitelist)
     with BamFile(bam) as bf:
         assert bf.ref_records("chrM") == g.soa.n
-    for q, pack, rec in ((20, True, "32"), (20, True, "64"), (0, True, "32"), (20, False, "64")):
-        os.environ["MGP_RECORDS"] = rec  # (read at each decode: the producer's record layout)
+    for q, pack, rec, place in ((20, True, "32", "paired"), (20, True, "64", "paired"), (20, True, "64", "device"),
+                                (0, True, "32", "paired"), (20, False, "64", "device")):
+        os.environ["MGP_RECORDS"] = rec  # (read at each decode: the producer's record layout and placement)
+        os.environ["MGP_PLACEMENT"] = place
         cfg = PipelineConfig(min_baseq=q)
         reader = BAMReader(str(bam), cfg, g.whitelist)
         whole, _ = reader.read_soa(pack=pack)
@@ -589,6 +592,11 @@ class _OracleEngine:
     def push(self, soa):
         from mgatk2_amd.synth import ReadSoA
 
+        if soa.rec_off is None:  # a dense batch of 64-byte records (the engine places and pairs them)
+            n = soa.n
+            rec_off = 64 * np.arange(n, dtype=np.uint64)
+            start = np.ascontiguousarray(soa.payload.reshape(n, 64)[:, :4]).view(np.int32).ravel().copy()
+            soa = ReadSoA(start, soa.bc, soa.tlen, soa.flag, soa.mapq, np.zeros(n, np.uint32), rec_off, soa.payload)
         part = ReadSoA(*[getattr(soa, k).copy() for k in ("start", "bc", "tlen", "flag", "mapq", "span", "rec_off",
                                                           "payload")])
         if self.lo is not None:
