@@ -1272,6 +1272,49 @@ struct Decoder {
         t_fields += now_s() - t0;
         return ok;
     }
+    // BAM-order decode in one pool pass: pass 1, the columns and each record written at
+    // the cursor + 64 x its index in the chunk, the offset it takes when every record of
+    // the chunk is a 64-byte slot (packed, rec_align 64: the speculation); all64 says
+    // whether it held (else the caller places and writes the chunk's records again).
+    // Records past the payload capacity are not written (the batch cut drops them).
+    bool classify_fields_records_all(size_t k0, int64_t gidx0, const Cols& c, uint64_t cap_payload, bool& all64) {
+        const double t0 = now_s();
+        const size_t m = recs.size();
+        rsz.resize(m);
+        ncg.resize(m);
+        cgp.resize(m);
+        pkd.resize(m);
+        hastag.resize(m);
+        const int tn = (int)std::max<size_t>(1, std::min<size_t>((size_t)pool.size(), m / 4096 + 1));
+        std::atomic<bool> ok{true}, spec{amask == 63};
+        std::string msg;
+        std::mutex mu;
+        const uint64_t base = cursor;
+        pool.run(tn, [&](int t) {
+            const size_t lo = m * (size_t)t / (size_t)tn, hi = m * (size_t)(t + 1) / (size_t)tn;
+            bool sp = spec.load(std::memory_order_relaxed);
+            for (size_t i = lo; i < hi; ++i) {
+                if (!classify_at(i)) {
+                    std::lock_guard<std::mutex> g(mu);
+                    if (ok) msg = g_err;
+                    ok = false;
+                    return;
+                }
+                int64_t tg = 0, fs = -1;
+                sp = sp && pkd[i] == 1;
+                const uint64_t off = base + 64ull * i;
+                const bool rec = sp && off + 64 + 256 <= cap_payload;
+                decode_one(c, recs[i], sizes[i], k0 + i, off, ncg[i], cgp[i], (int)pkd[i], tg, fs, gidx0 + (int64_t)i,
+                           true, rec);
+                hastag[i] = tg != 0;
+            }
+            if (!sp) spec.store(false, std::memory_order_relaxed);
+        });
+        if (!ok) g_err = msg;
+        all64 = spec.load();
+        t_fields += now_s() - t0;
+        return ok;
+    }
     void count_tags(int64_t gidx0) {
         const size_t m = recs.size();
         for (size_t i = 0; i < m; ++i)
@@ -1842,8 +1885,10 @@ int64_t mgp_bam_stream_next(mgp_bam_stream* s, int64_t cap_reads, int64_t cap_pa
         s->t_walk += tw - tp1;
         // pipelined: pass 1 and the columns in one pool pass (one trip through the records'
         // memory; a record cut off below is decoded again with the next batch)
-        if ((s->fuse || s->dense_fuse) ? !dec.classify_fields_all(k, s->decoded + (int64_t)k, c)
-                                       : !dec.classify_all())
+        bool all64 = false;
+        if (s->dense_fuse ? !dec.classify_fields_records_all(k, s->decoded + (int64_t)k, c, (uint64_t)cap_payload, all64)
+            : s->fuse    ? !dec.classify_fields_all(k, s->decoded + (int64_t)k, c)
+                         : !dec.classify_all())
             return -1;
         s->t_class += now_s() - tw;
         for (size_t i = 0; i < dec.recs.size(); ++i) {
@@ -1871,8 +1916,13 @@ int64_t mgp_bam_stream_next(mgp_bam_stream* s, int64_t cap_reads, int64_t cap_pa
                 s->placer.submit([s, c, cap_payload] { s->dec.place_stage(s->pend, c, (uint64_t)cap_payload); });
             } else if (s->dense_fuse) {
                 dec.count_tags(s->decoded + (int64_t)k);
-                dec.dense_offsets(k, c);
-                dec.records_inline(k, c);
+                if (all64) {  // every record already at cursor + 64 x i
+                    for (size_t i = 0; i < m; ++i) c.roff[k + i] = dec.cursor + 64ull * i;
+                    dec.cursor += 64ull * m;
+                } else {
+                    dec.dense_offsets(k, c);
+                    dec.records_inline(k, c);
+                }
             } else if (dec.decode(k, s->decoded + (int64_t)k, reserve, cols) != 0) {
                 return -1;
             }

@@ -70,6 +70,14 @@ def process_barcode_worker(args):
     return result_dict(res, 0, barcode, config.mito_length)
 
 
+def _payload_hint(n_reads: int) -> int:
+    """Device payload bytes a streamed run of n_reads needs at once (no regrowth, which
+    waits for the queued segments): 64-byte records plus the on-device pairing's
+    half-empty lines (a few %), or 32-byte records four per line plus their lines."""
+    per = 40 if os.environ.get("MGP_RECORDS", "64") == "32" else 68
+    return int(n_reads) * per + (64 << 20)
+
+
 class CellProcessor:
     def __init__(self, config, output_dir, device: int = 0, devices: list[int] | None = None):
         self.config = config
@@ -194,7 +202,7 @@ class CellProcessor:
         t0 = time.perf_counter()
         bam, st, n_hint, free, full, producer, times = self._stream_producer(reader, n_cells, batch_reads)
         try:
-            ec = self.config.engine_config(n_cells, reserve_reads=n_hint, reserve_payload=n_hint * 40 + (64 << 20))
+            ec = self.config.engine_config(n_cells, reserve_reads=n_hint, reserve_payload=_payload_hint(n_hint))
             ec.stream = True
             eng = Engine(ec, device=self.device)
             try:
@@ -313,7 +321,7 @@ class CellProcessor:
             parts = [(d, int(bounds[d]), int(bounds[d + 1])) for d in range(D) if bounds[d + 1] > bounds[d]]
             for d, lo, hi in parts:
                 ec = self.config.engine_config(hi - lo, reserve_reads=n_hint + 4096,
-                                               reserve_payload=n_hint * 40 + (64 << 20))
+                                               reserve_payload=_payload_hint(n_hint))
                 ec.stream = True
                 engines[d] = Engine(ec, device=devs[d])
                 engines[d].set_cell_range(lo, hi)
