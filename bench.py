@@ -84,6 +84,9 @@ def parse():
                     help="records of the headline (streamed, PCIe-inclusive) step: quality-carrying 64-byte records "
                          "the kernel filters per base (packed, default) or 32-byte records the producer made for "
                          "the run's min_baseq (pack32); dense in BAM order")
+    ap.add_argument("--columns", choices=["16", "32"], default="16",
+                    help="barcode index and |tlen| columns of the streamed batches: 16-bit (mgp_push_batch16, when "
+                         "the cells and every |tlen| fit) or the 32-bit mgp_batch columns")
     ap.add_argument("--device-only", action="store_true",
                     help="no streamed headline: the HBM-resident device leg is the line (kernel A/B runs)")
     ap.add_argument("--no-device", action="store_true", help="skip the HBM-resident device leg (--record-layout)")
@@ -306,7 +309,7 @@ def main():
             "device_ms_quad32": None if dev is None else dev["ms_per_step"],
             "device_ms_paired": None if paired is None else paired["ms_per_step"],
             "link": None if head is None else head["link"],
-            "stream": None if head is None else {k: head[k] for k in ("batch_reads", "batches", "segments_per_run",
+            "stream": None if head is None else {k: head[k] for k in ("batch_reads", "batches", "columns", "segments_per_run",
                                                                      "pileup_launches_per_run", "h2d_bytes_rank0",
                                                                      "d2h_bytes_rank0", "rows_target")},
             "device": dev,
@@ -582,7 +585,15 @@ def stream_leg(ctx: Ctx, layout: str, batch_list: list[int], timed: bool) -> dic
     # order) and no span (taken from the records' CIGARs on the device): ABI v3.1; no
     # start (taken from the records, which all hold it): ABI 4
     cols = ("bc", "tlen", "flag", "mapq", "payload")
-    col_bytes = n * (4 + 4 + 2 + 1)
+    # 16-bit barcode and |tlen| columns (mgp_push_batch16, ABI 5) when every read allows:
+    # 7 bytes of columns per read over the link instead of 11
+    wide = None
+    if args.columns == "16" and cfg.n_cells <= 0xFFFF:
+        wide = eng.download_inputs(columns=("bc", "tlen"))
+        if not np.abs(wide.tlen.astype(np.int64)).max(initial=0) < 0xFFFF:
+            wide = None
+    narrow = wide is not None
+    col_bytes = n * ((2 + 2) if narrow else (4 + 4)) + n * (2 + 1)
     hbuf = PinnedBuffer(col_bytes + pay + 4096)
     off = [0]
 
@@ -591,7 +602,14 @@ def stream_leg(ctx: Ctx, layout: str, batch_list: list[int], timed: bool) -> dic
         off[0] = (off[0] + m * np.dtype(dt).itemsize + 63) & ~63
         return a
 
-    host = eng.download_inputs(columns=cols, alloc=alloc)  # the producer's batches: pinned, BAM order
+    if narrow:  # (bc and tlen through host memory, then their 16-bit forms into the pinned batches)
+        host = eng.download_inputs(columns=("flag", "mapq", "payload"), alloc=alloc)
+        host.bc, host.tlen = alloc(n, np.uint16), alloc(n, np.uint16)
+        np.copyto(host.bc, np.where(wide.bc < 0, 0xFFFF, wide.bc).astype(np.uint16))
+        np.copyto(host.tlen, np.abs(wide.tlen).astype(np.uint16))
+        del wide
+    else:
+        host = eng.download_inputs(columns=cols, alloc=alloc)  # the producer's batches: pinned, BAM order
     assert np.all(eng.download_inputs(columns=("rec_off",)).rec_off == rb * np.arange(n, dtype=np.uint64))
     L, nc = cfg.mito_len, cfg.n_cells
     nw, W = eng.windows()
@@ -653,6 +671,7 @@ def stream_leg(ctx: Ctx, layout: str, batch_list: list[int], timed: bool) -> dic
         eng.close()
         best = max((lg for lg in legs if lg["streamed"]), key=lambda lg: lg["value"])
         return {"record_layout": layout, "value": best["value"], "best_batch_reads": best["batch_reads"],
+                "columns_bytes_per_read": 7 if narrow else 11,
                 "h2d_bytes_rank0": h2d, "d2h_bytes_rank0": d2h,
                 "link_GBps_rank0": round((h2d + d2h) / best["s"] / 1e9, 2), "legs": legs,
                 "stats_total_reads_rank0": r.stats["total_reads"]}
@@ -689,6 +708,8 @@ def stream_leg(ctx: Ctx, layout: str, batch_list: list[int], timed: bool) -> dic
                            "min_distance_from_end and ACGT per base), dense in BAM order",
                  "pack32": "32-byte records made for the run's min_baseq (per-base filter resolved by the producer), "
                            "dense in BAM order"}[layout],
+        "columns": ("u16 bc (0xFFFF: none), u16 |tlen|, u16 flag, u8 mapq: 7 B per read (mgp_push_batch16)" if narrow
+                    else "i32 bc, i32 tlen, u16 flag, u8 mapq: 11 B per read (mgp_push_batch)"),
         "timed_region": "K passes of: reset -> push every pinned host batch (H2D on the copy stream; each push "
                         "queues the hot path of the windows its reads complete) -> mgp_run -> every 16-bit count row "
                         "(written into pinned host memory as its windows complete) and the per-cell statistics on "

@@ -352,6 +352,22 @@ typedef struct mgp_batch {
     int64_t         payload_bytes;
 } mgp_batch;
 
+/* A batch with 16-bit barcode and |tlen| columns (ABI 5): for contexts of at most 65535
+ * cells whose reads all have |template_length| < 65536 (the engine keys duplicates on
+ * abs(tlen) only, readers.py:128-131, so the sign is not needed). The records are dense
+ * in BAM order (record i at i x payload_bytes / n_reads; start and span taken from the
+ * records, as for an mgp_batch without those columns). 7 bytes of columns per read
+ * instead of 11 cross the host link. */
+typedef struct mgp_batch16 {
+    int64_t         n_reads;
+    const uint16_t *bc;         /* whitelist index of the CB tag; 0xFFFF if absent or not whitelisted */
+    const uint16_t *abs_tlen;   /* |template_length|                                 */
+    const uint16_t *flag;       /* BAM flag | MGP_FLAG_NOSEQQUAL                    */
+    const uint8_t  *mapq;       /* mapping_quality                                  */
+    const uint8_t  *payload;    /* dense records in BAM order                       */
+    int64_t         payload_bytes;
+} mgp_batch16;
+
 /* Run-level statistics (readers.py:193-199). */
 typedef struct mgp_stats {
     int64_t total_reads;                   /* every record fed (readers.py:93)               */
@@ -511,6 +527,11 @@ int  mgp_copy_wait(mgp_ctx *ctx);
  * (MGP_E_INVALID). Replaces the reference's split of the barcodes
  * over its worker pool (processors.py:112-144) with a split by device. */
 int  mgp_set_cell_range(mgp_ctx *ctx, int32_t cell_lo, int32_t cell_hi);
+/* Append a batch with 16-bit barcode and |tlen| columns (mgp_batch16; the device widens
+ * them behind the copy). Same semantics and errors as mgp_push_batch for a batch without
+ * rec_off, start and span columns; MGP_E_INVALID when n_cells > 65535. Replaces the
+ * reference's per-read SimpleRead fields (readers.py:153-163) at the host link. */
+int  mgp_push_batch16(mgp_ctx *ctx, const mgp_batch16 *batch);
 /* Streaming on (1) or off (0) for the next pushes (initially MGP_CFG_STREAM). */
 int  mgp_set_streaming(mgp_ctx *ctx, int on);
 /* Streaming: segments queued by pushes so far (all runs), and whether the last run

@@ -133,6 +133,7 @@ struct mgp_ctx {
     bool dev_pair = true;  // (MGP_DEV_PAIR=0: records stay in BAM order, for A/B)
     int stage_i = 0;
     DevBuf stage[2], pair_rank, pair_cnt, pair_lines;
+    DevBuf col16[2];  // a 16-bit batch's barcode and |tlen| columns (mgp_push_batch16), before widening
     hipEvent_t ev_stage[2] = {nullptr, nullptr};
     hipEvent_t ev_bits = nullptr;  // the run's input check words have reached h_bits
     uint32_t* h_bits = nullptr;    // pinned host copy of the input check words (roff_irregular)
@@ -2846,6 +2847,18 @@ __global__ void __launch_bounds__(kPairBlock) k_pair_place(const uint4* __restri
     }
 }
 
+// mgp_push_batch16: the batch's 16-bit barcode (0xFFFF: none) and |tlen| columns widened
+// into the resident 32-bit ones
+__global__ void k_widen16(const uint16_t* __restrict__ c16, int64_t n, int32_t* __restrict__ bc,
+                          int32_t* __restrict__ tlen) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) {
+        const uint32_t b = c16[i];
+        bc[i] = b == 0xFFFFu ? -1 : (int32_t)b;
+        tlen[i] = (int32_t)c16[n + i];
+    }
+}
+
 // mgp_push_batch without rec_off: dense records in BAM order, record i at base + i x stride
 __global__ void k_dense_off(uint64_t* __restrict__ roff, int64_t n, uint64_t base, uint64_t stride) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -3251,6 +3264,7 @@ void mgp_close(mgp_ctx* ctx) {
     for (int i = 0; i < 2; ++i) {
         if (ctx->ev_stage[i]) (void)hipEventDestroy(ctx->ev_stage[i]);
         ctx->stage[i].release();
+        ctx->col16[i].release();
     }
     ctx->pair_rank.release();
     ctx->pair_cnt.release();
@@ -3296,11 +3310,35 @@ static int ensure_inputs(mgp_ctx* ctx, int64_t n_total, int64_t pay_total, bool 
 
 static int stream_segments(mgp_ctx* ctx, int64_t last_start, uint16_t last_flag);
 
+// A batch's copies and kernels (mgp_push_batch, mgp_push_batch16: c16 = the 16-bit
+// barcode and |tlen| columns, then b->bc / b->tlen are unused)
+static int push_impl(mgp_ctx* ctx, const mgp_batch* b, const uint16_t* bc16, const uint16_t* tlen16);
+
 int mgp_push_batch(mgp_ctx* ctx, const mgp_batch* b) {
     if (!ctx || !b) return set_err(MGP_E_INVALID, "null ctx/batch");
     if (b->n_reads < 0 || b->payload_bytes < 0) return set_err(MGP_E_INVALID, "negative sizes");
     if (b->n_reads == 0) return MGP_OK;
     if (!b->bc || !b->tlen || !b->flag || !b->mapq || !b->payload) return set_err(MGP_E_INVALID, "null batch array");
+    return push_impl(ctx, b, nullptr, nullptr);
+}
+
+int mgp_push_batch16(mgp_ctx* ctx, const mgp_batch16* b) {
+    if (!ctx || !b) return set_err(MGP_E_INVALID, "null ctx/batch");
+    if (b->n_reads < 0 || b->payload_bytes < 0) return set_err(MGP_E_INVALID, "negative sizes");
+    if (b->n_reads == 0) return MGP_OK;
+    if (!b->bc || !b->abs_tlen || !b->flag || !b->mapq || !b->payload)
+        return set_err(MGP_E_INVALID, "null batch array");
+    if (ctx->g.nc > 0xFFFF) return set_err(MGP_E_INVALID, "16-bit barcode indices need n_cells <= 65535");
+    mgp_batch w{};
+    w.n_reads = b->n_reads;
+    w.flag = b->flag;
+    w.mapq = b->mapq;
+    w.payload = b->payload;
+    w.payload_bytes = b->payload_bytes;
+    return push_impl(ctx, &w, b->bc, b->abs_tlen);
+}
+
+static int push_impl(mgp_ctx* ctx, const mgp_batch* b, const uint16_t* bc16, const uint16_t* tlen16) {
     // rec_off NULL: dense records in BAM order (record i at i x payload_bytes / n_reads);
     // span NULL: the spans come from the records' CIGARs on the device
     const bool dense = b->rec_off == nullptr;
@@ -3324,16 +3362,23 @@ int mgp_push_batch(mgp_ctx* ctx, const mgp_batch* b) {
     // the copy stream only copies (the link never waits on a kernel); the batch's
     // kernels follow on the compute stream, ahead of the segments it completes
     const int j = ctx->stage_i;
+    const bool staged = pair || bc16;  // (the staging slot j is used: wait for its last readers)
     if (pair) {
         MGP_TRY(ctx->stage[j].ensure((size_t)b->payload_bytes));
         MGP_TRY(ctx->pair_rank.ensure((size_t)nb * 4));
         MGP_TRY(ctx->pair_cnt.ensure((size_t)npw * (nc + 1) * 4));
         MGP_TRY(ctx->pair_lines.ensure((size_t)npw * 4));
-        HIP_TRY(hipStreamWaitEvent(s, ctx->ev_stage[j], 0));  // the kernels that read this buffer last
     }
+    if (bc16) MGP_TRY(ctx->col16[j].ensure((size_t)nb * 4));
+    if (staged) HIP_TRY(hipStreamWaitEvent(s, ctx->ev_stage[j], 0));  // the kernels that read slot j last
     if (b->start) HIP_TRY(hipMemcpyAsync(ctx->start.as<int32_t>() + n0, b->start, nb * 4, hipMemcpyHostToDevice, s));
-    HIP_TRY(hipMemcpyAsync(ctx->bc.as<int32_t>() + n0, b->bc, nb * 4, hipMemcpyHostToDevice, s));
-    HIP_TRY(hipMemcpyAsync(ctx->tlen.as<int32_t>() + n0, b->tlen, nb * 4, hipMemcpyHostToDevice, s));
+    if (bc16) {
+        HIP_TRY(hipMemcpyAsync(ctx->col16[j].as<uint16_t>(), bc16, nb * 2, hipMemcpyHostToDevice, s));
+        HIP_TRY(hipMemcpyAsync(ctx->col16[j].as<uint16_t>() + nb, tlen16, nb * 2, hipMemcpyHostToDevice, s));
+    } else {
+        HIP_TRY(hipMemcpyAsync(ctx->bc.as<int32_t>() + n0, b->bc, nb * 4, hipMemcpyHostToDevice, s));
+        HIP_TRY(hipMemcpyAsync(ctx->tlen.as<int32_t>() + n0, b->tlen, nb * 4, hipMemcpyHostToDevice, s));
+    }
     HIP_TRY(hipMemcpyAsync(ctx->flag.as<uint16_t>() + n0, b->flag, nb * 2, hipMemcpyHostToDevice, s));
     HIP_TRY(hipMemcpyAsync(ctx->mapq.as<uint8_t>() + n0, b->mapq, nb, hipMemcpyHostToDevice, s));
     if (b->span)
@@ -3345,6 +3390,11 @@ int mgp_push_batch(mgp_ctx* ctx, const mgp_batch* b) {
                                b->payload_bytes, hipMemcpyHostToDevice, s));
     HIP_TRY(hipEventRecord(ctx->ev_copy, s));
     HIP_TRY(hipStreamWaitEvent(sp, ctx->ev_copy, 0));
+    if (bc16) {
+        k_widen16<<<blocks_for(nb), kBlock, 0, sp>>>(ctx->col16[j].as<uint16_t>(), nb, ctx->bc.as<int32_t>() + n0,
+                                                     ctx->tlen.as<int32_t>() + n0);
+        HIP_TRY(hipGetLastError());
+    }
     if (ctx->cell_range) {
         k_rebase_bc<<<blocks_for(nb), kBlock, 0, sp>>>(ctx->bc.as<int32_t>() + n0, nb, ctx->cell_lo, nc);
         HIP_TRY(hipGetLastError());
@@ -3362,8 +3412,6 @@ int mgp_push_batch(mgp_ctx* ctx, const mgp_batch* b) {
             ctx->pair_rank.as<uint32_t>(), ctx->pair_cnt.as<uint32_t>(), ctx->pair_lines.as<uint32_t>(),
             (uint64_t)pay0, ctx->payload.as<uint8_t>(), ctx->roff.as<uint64_t>() + n0);
         HIP_TRY(hipGetLastError());
-        HIP_TRY(hipEventRecord(ctx->ev_stage[j], sp));
-        ctx->stage_i ^= 1;
     } else if (dense) {
         k_dense_off<<<blocks_for(nb), kBlock, 0, sp>>>(ctx->roff.as<uint64_t>() + n0, nb, (uint64_t)pay0,
                                                        (uint64_t)stride);
@@ -3371,6 +3419,10 @@ int mgp_push_batch(mgp_ctx* ctx, const mgp_batch* b) {
     } else if (pay0) {
         k_add_u64<<<blocks_for(nb), kBlock, 0, sp>>>(ctx->roff.as<uint64_t>() + n0, nb, (uint64_t)pay0);
         HIP_TRY(hipGetLastError());
+    }
+    if (staged) {  // slot j's readers are queued: the next batch that uses it waits for them
+        HIP_TRY(hipEventRecord(ctx->ev_stage[j], sp));
+        ctx->stage_i ^= 1;
     }
     // every record inside the batch's payload (and, without a span / start column, its
     // span / start from the record)

@@ -39,6 +39,7 @@ ABI_SYMBOLS = (
     "mgp_finish", "mgp_kernel_times", "mgp_comm_unique_id", "mgp_comm_init", "mgp_synth_generate",
     "mgp_download_inputs", "mgp_set_stage_timing", "mgp_fetch_cells", "mgp_fetch_rows16", "mgp_windows",
     "mgp_stream_info", "mgp_set_streaming", "mgp_set_rows16_target", "mgp_copy_wait", "mgp_set_cell_range",
+    "mgp_push_batch16",
 )
 ABI_VERSION = 5
 CFG_KEEP_TN5 = 0x1
@@ -58,6 +59,18 @@ class mgp_config(C.Structure):
         ("flags", C.c_int32),
         ("reserve_reads", C.c_int64),
         ("reserve_payload", C.c_int64),
+    ]
+
+
+class mgp_batch16(C.Structure):
+    _fields_ = [
+        ("n_reads", C.c_int64),
+        ("bc", C.c_void_p),
+        ("abs_tlen", C.c_void_p),
+        ("flag", C.c_void_p),
+        ("mapq", C.c_void_p),
+        ("payload", C.c_void_p),
+        ("payload_bytes", C.c_int64),
     ]
 
 
@@ -167,6 +180,7 @@ def load_library(path: Path | None = None) -> C.CDLL:
         "mgp_host_alloc": ([i64, C.POINTER(vp)], C.c_int),
         "mgp_host_free": ([vp], C.c_int),
         "mgp_push_batch": ([vp, C.POINTER(mgp_batch)], C.c_int),
+        "mgp_push_batch16": ([vp, C.POINTER(mgp_batch16)], C.c_int),
         "mgp_reset": ([vp], C.c_int),
         "mgp_resident": ([vp, C.POINTER(i64), C.POINTER(i64)], C.c_int),
         "mgp_run": ([vp], C.c_int),
@@ -368,8 +382,21 @@ class Engine:
 
     # -- data --------------------------------------------------------------
     def push(self, soa: ReadSoA):
-        b = batch_struct(soa)
-        _ck(self.lib.mgp_push_batch(self._h, C.byref(b)), "mgp_push_batch")
+        """mgp_push_batch; a batch whose bc and tlen are uint16 arrays (16-bit barcode
+        index, 0xFFFF = none, and |tlen|; dense records, no start / span / rec_off) goes
+        through mgp_push_batch16."""
+        if soa.bc is not None and soa.bc.dtype == np.uint16:
+            for name in ("bc", "tlen", "flag", "mapq", "payload"):
+                if not getattr(soa, name).flags["C_CONTIGUOUS"]:
+                    raise InvalidInputError(f"batch array {name} must be C-contiguous")
+            if soa.tlen.dtype != np.uint16 or soa.start is not None or soa.span is not None or soa.rec_off is not None:
+                raise InvalidInputError("a 16-bit batch has uint16 bc and |tlen| and dense records only")
+            b = mgp_batch16(soa.n, _ptr(soa.bc), _ptr(soa.tlen), _ptr(soa.flag), _ptr(soa.mapq), _ptr(soa.payload),
+                            int(soa.payload.shape[0]))
+            _ck(self.lib.mgp_push_batch16(self._h, C.byref(b)), "mgp_push_batch16")
+        else:
+            b = batch_struct(soa)
+            _ck(self.lib.mgp_push_batch(self._h, C.byref(b)), "mgp_push_batch")
         self._keep.append(soa)
 
     def reset(self):

@@ -82,7 +82,8 @@ def test_struct_layouts_match_header(tmp_path):
     from mgatk2_amd import engine
 
     structs = {
-        "mgp_config": engine.mgp_config, "mgp_batch": engine.mgp_batch, "mgp_stats": engine.mgp_stats,
+        "mgp_config": engine.mgp_config, "mgp_batch": engine.mgp_batch, "mgp_batch16": engine.mgp_batch16,
+        "mgp_stats": engine.mgp_stats,
         "mgp_result": engine.mgp_result, "mgp_synth_params": engine.mgp_synth_params,
         "mgp_rows16": engine.mgp_rows16,
     }

@@ -497,6 +497,52 @@ def test_dense_64_byte_batches_paired_on_the_device(engine_lib, monkeypatch, str
     assert np.array_equal(out["0"][1].rec_off.astype(np.int64) % 64, np.zeros(soa.n, np.int64))
 
 
+@pytest.mark.parametrize("streamed", [False, True])
+@pytest.mark.parametrize("layout", ["p64", "p32"])
+def test_push16_equals_push(engine_lib, streamed, layout):
+    """mgp_push_batch16 (ABI 5: 16-bit barcode index, 0xFFFF = none, and |tlen|; dense
+    records): the same results as the 32-bit columns of the same reads, resident and
+    streaming (64-byte batches are also paired on the device), with barcode indices
+    widened to -1 and |tlen| as the columns; n_cells > 65535 is refused."""
+    from dataclasses import replace
+
+    from mgatk2_amd.engine import EngineConfig
+    from mgatk2_amd.exceptions import InvalidInputError
+    from mgatk2_amd.synth import ReadSoA, relocate, synth_reads
+
+    nc = 120
+    cfg = EngineConfig(n_cells=nc, **CONFIGS["run"])
+    stride = 64 if layout == "p64" else 32
+    kw = dict(pack=True) if layout == "p64" else dict(pack32=cfg.min_baseq)
+    soa = relocate(synth_reads(919, 600_000, nc, **kw), rec_align=stride, n_cells=nc)
+    assert int(np.abs(soa.tlen).max()) < 65535
+    if streamed:
+        cfg = replace(cfg, stream=True, reserve_reads=soa.n, reserve_payload=int(soa.payload.shape[0]) * 2)
+    cuts = [0, 150_000, 420_000, soa.n]
+    res = {}
+    for w16 in (False, True):
+        with engine_lib.Engine(cfg) as eng:
+            for a, b in zip(cuts[:-1], cuts[1:]):
+                if w16:
+                    bc = soa.bc[a:b]
+                    eng.push(ReadSoA(None, np.where(bc < 0, 0xFFFF, bc).astype(np.uint16),
+                                     np.abs(soa.tlen[a:b]).astype(np.uint16), soa.flag[a:b].copy(),
+                                     soa.mapq[a:b].copy(), None, None,
+                                     np.ascontiguousarray(soa.payload[stride * a:stride * b])))
+                else:
+                    eng.push(_columnless(soa, a, b, stride, no_start=True))
+            res[w16] = eng.finish()
+            cols = eng.download_inputs(columns=("bc", "tlen"))
+        if w16:
+            np.testing.assert_array_equal(cols.bc, soa.bc)
+            np.testing.assert_array_equal(cols.tlen, np.abs(soa.tlen))
+    assert_same(res[True], res[False], f"push16 {layout} streamed={streamed}")
+    with engine_lib.Engine(EngineConfig(n_cells=70_000)) as eng:
+        with pytest.raises(InvalidInputError, match="65535"):
+            eng.push(ReadSoA(None, np.zeros(4, np.uint16), np.zeros(4, np.uint16), soa.flag[:4].copy(),
+                             soa.mapq[:4].copy(), None, None, np.ascontiguousarray(soa.payload[:4 * stride])))
+
+
 def test_push_without_offsets_rejects_ragged_payloads(engine_lib):
     from mgatk2_amd.engine import EngineConfig
     from mgatk2_amd.exceptions import InvalidInputError
