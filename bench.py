@@ -25,7 +25,10 @@ Beside it (never inside the timed steps), the line carries:
     against the oracle on exactly their reads (cells are independent);
   * host_pack: the producer's cost of the 32-byte records;
   * cpu_baseline (N = 1 only): the single-threaded C port of the reference's
-    path on a bounded sample of the same generator.
+    path on a bounded sample of the same generator;
+  * e2e (N = 1 only): the product end to end on a bounded BAM (20M reads x 1000
+    cells, BGZF level 6): MtDNAPipeline.run to txt (gzip 9) and to HDF5, wall time
+    with BAM ingest and writers separately.
 
 Launch: `python bench.py --gpus N` starts N worker processes itself (one per GPU,
 RANK/LOCAL_RANK/WORLD_SIZE in their environment, before anything touches a GPU);
@@ -97,6 +100,10 @@ def parse():
     ap.add_argument("--no-host-pack", action="store_true", help="skip timing the host's 32-byte record build")
     ap.add_argument("--no-numa-bind", action="store_true", help="do not move the rank to its GPU's NUMA node")
     ap.add_argument("--pcie-steps", type=int, default=3)
+    ap.add_argument("--no-e2e", action="store_true", help="skip the end-to-end leg (BAM -> txt / HDF5 files)")
+    ap.add_argument("--e2e-reads", type=int, default=20_000_000,
+                    help="reads of the end-to-end leg's synthetic BAM (C4's 20k reads per cell at the default)")
+    ap.add_argument("--e2e-cells", type=int, default=1000)
     ap.add_argument("--batch-reads", type=str, default="auto",
                     help="reads per pushed batch of the streamed legs (auto: the rank's reads / 12.5, about one "
                          "position window per batch: 16M at C4 on one GPU, 2M per rank on 8); a comma list also "
@@ -266,6 +273,10 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(args, cfg, local_rank)
 
+    e2e = None
+    if rank == 0 and world == 1 and not args.no_e2e and not args.device_only:
+        e2e = e2e_leg(args)
+
     if rank == 0:
         main_leg = head if head is not None else dev
         ms_step = main_leg["ms_per_step"]
@@ -318,12 +329,43 @@ def main():
             "host_pack_ns_per_read": None if host_pack is None else host_pack["ns_per_read_1thread"],
             "host_pack": host_pack,
             "cpu_baseline": cpu,
+            "e2e": e2e,
             "stats_rank0": main_leg.get("stats"),
             "sample_check": main_leg.get("sample_check"),
         }
         print(json.dumps(out), flush=True)
     if dist is not None:
         dist.destroy_process_group()
+
+
+def e2e_leg(args) -> dict:
+    """The product end to end on a bounded sample ("also report end-to-end
+    wall time including BAM decode and writers separately"): a coordinate-sorted BAM
+    (BGZF level 6) of --e2e-reads reads over --e2e-cells cells (the device generator, C4's
+    reads per cell at the defaults; written before anything is timed), then
+    ``MtDNAPipeline.run`` streamed, once with txt output at the reference's gzip level 9
+    and once with HDF5: wall time, BAM ingest, writers. Full-size C4 runs come from
+    scripts/e2e_bench.py."""
+    import shutil
+    import tempfile
+
+    sys.path.insert(0, str(Path(__file__).resolve().parent / "scripts"))
+    from e2e_bench import run_e2e
+
+    from mgatk2_amd.bam import host_threads
+
+    out = tempfile.mkdtemp(prefix="mgp_bench_e2e_", dir="/tmp")
+    try:
+        t = time.time()
+        res = run_e2e(args.e2e_reads, args.e2e_cells, host_threads(), out, formats=("txt", "hdf5"),
+                      modes=("stream",), gzip_levels=("9",))
+        res["leg_seconds"] = round(time.time() - t, 1)
+    finally:
+        shutil.rmtree(out, ignore_errors=True)
+    res["what"] = ("wall = MtDNAPipeline.run (BAM open -> streamed decode + engine -> files closed); bam_ingest = "
+                   "the streamed decode, engine work under it; write = writers after the last batch; "
+                   "reads_per_s_end_to_end = reads / wall")
+    return res
 
 
 def batch_sizes(spec: str) -> list:

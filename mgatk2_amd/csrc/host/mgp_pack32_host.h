@@ -1,4 +1,4 @@
-// mgp_pack32_host.h — the host producers' 32-byte record builder (libmgphost.so).
+// mgp_pack32_host.h — the host producers' 32- and 64-byte record builders (libmgphost.so).
 //
 // Same bytes as mgp_pack32_record (include/mgpileup.h, the layout's definition, also
 // used by the device generator), built without a branch per query position: the
@@ -149,6 +149,84 @@ inline int pack32_record_fast(int32_t start, uint32_t l_seq, uint16_t flag, uint
     out[30] = (uint8_t)(hi3 >> 16);
     out[31] = (uint8_t)(int8_t)min_baseq;
     return 1;
+}
+
+// ---- 64-byte records (mgp_pack_record's bytes, include/mgpileup.h) ----
+// The definition's per-position loop (nibble, four-way code test, quality shift: ~50
+// branches) was most of the BAM decoder's pool pass. Here 16 positions per step with
+// SSSE3 byte shuffles: the sequence nibbles spread to one byte per position, the BAM
+// code mapped to the base by a 16-entry table (A, C, G, T -> 0..3, any other code ->
+// 0xFF, which ORed into qual << 2 gives the definition's 0xFF), positions >= l_seq
+// set to 0xFF; the record leaves in four 16-byte stores (non-temporal into aligned
+// slots: the decoder never reads the payload back, the device copy does).
+// Precondition: the read is packable (bam_packable / mgp_pack_record's tests passed);
+// seq32 and qual64 are 32 and 64 readable bytes holding the read's sequence and
+// quality first (bytes past them are never used).
+__attribute__((target("ssse3"))) inline void pack64_record_ssse3(int32_t start, uint32_t l_seq, uint16_t flag,
+                                                                   uint32_t n_cigar, const uint32_t* cigar,
+                                                                   const uint8_t* seq32, const uint8_t* qual64,
+                                                                   uint8_t* out) {
+    const __m128i lut = _mm_setr_epi8(-1, 0, 1, -1, 2, -1, -1, -1, 3, -1, -1, -1, -1, -1, -1, -1);
+    const __m128i dup = _mm_setr_epi8(0, 0, 1, 1, 2, 2, 3, 3, 4, 4, 5, 5, 6, 6, 7, 7);
+    const __m128i odd = _mm_set1_epi16((short)0xFF00);
+    const __m128i nib = _mm_set1_epi8(0x0F), fc = _mm_set1_epi8((char)0xFC);
+    const __m128i len = _mm_set1_epi8((char)l_seq);
+    __m128i idx = _mm_setr_epi8(0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15);
+    __m128i v[4];
+    for (int j = 0; j < 4; ++j) {
+        const __m128i x = _mm_shuffle_epi8(_mm_loadl_epi64(reinterpret_cast<const __m128i*>(seq32 + 8 * j)), dup);
+        const __m128i code = _mm_or_si128(_mm_andnot_si128(odd, _mm_and_si128(_mm_srli_epi16(x, 4), nib)),
+                                          _mm_and_si128(odd, _mm_and_si128(x, nib)));
+        const __m128i q = _mm_loadu_si128(reinterpret_cast<const __m128i*>(qual64 + 16 * j));
+        const __m128i b = _mm_or_si128(_mm_and_si128(_mm_slli_epi16(q, 2), fc), _mm_shuffle_epi8(lut, code));
+        v[j] = _mm_or_si128(b, _mm_cmpeq_epi8(_mm_min_epu8(idx, len), len));  // idx >= l_seq -> 0xFF
+        idx = _mm_add_epi8(idx, _mm_set1_epi8(16));
+    }
+    uint64_t c[4] = {0, 0, 0, 0};
+    for (uint32_t k = 0; k < n_cigar && k < 4u; ++k) c[k] = cigar[k] & 0xFFFFu;
+    const uint64_t lo = (uint64_t)(uint32_t)start | (uint64_t)l_seq << 32 |
+                        (uint64_t)(n_cigar | ((flag & MGP_FLAG_REVERSE) ? 0x80u : 0u)) << 40 | c[0] << 48;
+    const uint64_t hi = c[1] | c[2] << 16 | c[3] << 32;
+    const __m128i o0 = _mm_or_si128(_mm_set_epi64x((long long)hi, (long long)lo), _mm_slli_si128(v[0], 14));
+    const __m128i o1 = _mm_alignr_epi8(v[1], v[0], 2), o2 = _mm_alignr_epi8(v[2], v[1], 2);
+    const __m128i o3 = _mm_alignr_epi8(v[3], v[2], 2);
+    __m128i* d = reinterpret_cast<__m128i*>(out);
+    if (((uintptr_t)out & 15u) == 0) {
+        _mm_stream_si128(d, o0);
+        _mm_stream_si128(d + 1, o1);
+        _mm_stream_si128(d + 2, o2);
+        _mm_stream_si128(d + 3, o3);
+    } else {
+        _mm_storeu_si128(d, o0);
+        _mm_storeu_si128(d + 1, o1);
+        _mm_storeu_si128(d + 2, o2);
+        _mm_storeu_si128(d + 3, o3);
+    }
+}
+
+// (MGP_NO_SSSE3=1 forces the definition's loop: tests compare both)
+inline bool cpu_has_ssse3() {
+    static const bool has = __builtin_cpu_supports("ssse3") && !std::getenv("MGP_NO_SSSE3");
+    return has;
+}
+
+// mgp_pack_record for a packable read whose fields lie in a record ending at `end`
+// (the SIMD loads read up to 32 bytes from seq and 64 from qual: shorter tails go
+// through a local copy); callers issue _mm_sfence() before publishing the payload.
+inline void pack64_record_fast(int32_t start, uint32_t l_seq, uint16_t flag, uint32_t n_cigar, const uint32_t* cigar,
+                               const uint8_t* seq, const uint8_t* qual, const uint8_t* end, uint8_t* out) {
+    if (!cpu_has_ssse3()) {
+        mgp_pack_record(start, l_seq, flag, n_cigar, cigar, seq, qual, out);
+        return;
+    }
+    if (seq + 32 <= end && qual + 64 <= end) {
+        pack64_record_ssse3(start, l_seq, flag, n_cigar, cigar, seq, qual, out);
+        return;
+    }
+    alignas(16) uint8_t s[32] = {0}, q[64] = {0};
+    std::memcpy(s, seq, (l_seq + 1u) / 2u);
+    std::memcpy(q, qual, l_seq);
+    pack64_record_ssse3(start, l_seq, flag, n_cigar, cigar, s, q, out);
 }
 
 }  // namespace mgp_host

@@ -23,6 +23,89 @@ ROOT = Path(__file__).resolve().parent.parent
 sys.path.insert(0, str(ROOT))
 
 
+def run_e2e(reads: int, cells: int, threads: int, out: str | Path, formats=("txt", "hdf5"), modes=("stream",),
+            records=("64",), gzip_levels=("9",), bam_level: int = 6, reuse_bam: bool = False, devices: str = "0",
+            log=sys.stderr) -> dict:
+    """Synthetic BAM (device generator + native writer), then ``run_pipeline`` per
+    (record layout, mode, format, gzip level); returns the stage times of each run."""
+    from mgatk2_amd.bam import write_bam
+    from mgatk2_amd.engine import Engine, EngineConfig
+    from mgatk2_amd.pipeline import MtDNAPipeline
+    from mgatk2_amd.config import PipelineConfig
+    from mgatk2_amd.synth import barcode_names, cell_cdf, ref_codes
+
+    out = Path(out)
+    out.mkdir(parents=True, exist_ok=True)
+    seed = 20251015 + 3
+    t0 = time.time()
+    whitelist = barcode_names(cells, seed)
+    bam = out / "possorted_bam.bam"
+    tag = out / "possorted_bam.size"
+    want = f"{reads} {cells} {bam_level}"
+    if reuse_bam and bam.exists() and tag.exists() and tag.read_text() == want:
+        t1 = t2 = time.time()
+    else:
+        with Engine(EngineConfig(n_cells=cells), device=0) as eng:
+            eng.synth(seed, reads, cell_cdf(seed, cells), ref_codes(seed), read_len=50)
+            soa = eng.download_inputs()
+        t1 = time.time()
+        write_bam(bam, soa, whitelist, level=bam_level, n_threads=threads)
+        del soa
+        t2 = time.time()
+        tag.write_text(want)
+    (out / "barcodes.tsv").write_text("".join(b + "\n" for b in whitelist))
+    print(f"[e2e] generated {reads:,} reads in {t1 - t0:.1f}s; BAM {bam.stat().st_size / 1e9:.2f} GB "
+          f"written in {t2 - t1:.1f}s", file=log, flush=True)
+
+    name = {(50_000_000, 5_000): "C3", (200_000_000, 10_000): "C4"}.get((reads, cells), "custom")
+    res = {"config": f"{name}: {reads:,} reads x {cells} cells, run params (q20 mapq30 "
+                     "dedup=alignment_and_fragment_length)", "host_threads": threads, "devices": devices,
+           "bam_bytes": bam.stat().st_size, "bam_level": bam_level}
+    digests = {}
+    runs = [(mode, fmt, rec, lvl) for rec in records for mode in modes
+            for fmt in formats for lvl in (gzip_levels if fmt == "txt" else ["-"])]
+    for mode, fmt, rec, lvl in runs:
+        os.environ["MGP_RECORDS"] = rec
+        if lvl != "-":
+            os.environ["MGP_GZIP_LEVEL"] = lvl
+        cfg = PipelineConfig(min_baseq=20, min_mapq=30, max_strand_bias=1.0, skip_deduplication=False,
+                             use_fragment_length_dedup=True, min_reads_per_cell=1, n_cores=threads)
+        t = time.time()
+        od = out / f"run_{fmt}_{mode}"
+        devs = [int(x) for x in devices.split(",")]
+        p = MtDNAPipeline(str(bam), whitelist, od, config=cfg, output_format=fmt, stream=mode == "stream",
+                          devices=devs if len(devs) > 1 else None)
+        ret = p.run()
+        wall = time.time() - t
+        key = f"{fmt}_{mode}" + (f"_r{rec}" if len(records) > 1 else "") + \
+              (f"_z{lvl}" if lvl != "-" and len(gzip_levels) > 1 else "")
+        res[key] = {"wall_s": round(wall, 2), "records": rec, "gzip_level": None if lvl == "-" else int(lvl),
+                    **{k: (round(v, 3) if isinstance(v, float) else v) for k, v in p.timings.items()},
+                    "reads_per_s_end_to_end": round(reads / wall), "cells_passed": ret.get("cells_passed_qc")}
+        if fmt == "txt":
+            res[key]["txt_gz_bytes"] = sum((od / "output" / f"output.{f}.txt.gz").stat().st_size
+                                           for f in ("A", "C", "G", "T", "coverage"))
+        if fmt == "hdf5":
+            html = od / "mgatk2_report.html"
+            res[key]["report_html_bytes"] = html.stat().st_size if html.exists() else 0
+            res[key]["report_figures"] = html.read_text().count("data:image/png") if html.exists() else 0
+        print(f"[e2e] {key}: {res[key]}", file=log, flush=True)
+        if fmt == "txt":  # every mode, record layout and level must write the same text
+            import gzip
+            import hashlib
+
+            h = hashlib.sha256()
+            for f in ("A", "C", "G", "T", "coverage"):
+                h.update(gzip.decompress((od / "output" / f"output.{f}.txt.gz").read_bytes()))
+            digests[key] = h.hexdigest()
+        import shutil
+
+        shutil.rmtree(od, ignore_errors=True)
+    if len(digests) > 1:
+        res["txt_identical_across_runs"] = len(set(digests.values())) == 1
+    return res
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reads", type=int, default=50_000_000)
@@ -42,82 +125,10 @@ def main():
     ap.add_argument("--devices", default="0",
                     help="engine devices, comma-separated (cells split over them; '0,0' runs two shards on one GPU)")
     args = ap.parse_args()
-
-    from mgatk2_amd.bam import write_bam
-    from mgatk2_amd.engine import Engine, EngineConfig
-    from mgatk2_amd.pipeline import MtDNAPipeline
-    from mgatk2_amd.config import PipelineConfig
-    from mgatk2_amd.synth import barcode_names, cell_cdf, ref_codes
-
-    out = Path(args.out)
-    out.mkdir(parents=True, exist_ok=True)
-    seed = 20251015 + 3
-    t0 = time.time()
-    whitelist = barcode_names(args.cells, seed)
-    bam = out / "possorted_bam.bam"
-    tag = out / "possorted_bam.size"
-    want = f"{args.reads} {args.cells} {args.bam_level}"
-    if args.reuse_bam and bam.exists() and tag.exists() and tag.read_text() == want:
-        t1 = t2 = time.time()
-    else:
-        with Engine(EngineConfig(n_cells=args.cells), device=0) as eng:
-            eng.synth(seed, args.reads, cell_cdf(seed, args.cells), ref_codes(seed), read_len=50)
-            soa = eng.download_inputs()
-        t1 = time.time()
-        write_bam(bam, soa, whitelist, level=args.bam_level, n_threads=args.threads)
-        del soa
-        t2 = time.time()
-        tag.write_text(want)
-    (out / "barcodes.tsv").write_text("".join(b + "\n" for b in whitelist))
-    print(f"[e2e] generated {args.reads:,} reads in {t1 - t0:.1f}s; BAM {bam.stat().st_size / 1e9:.2f} GB "
-          f"written in {t2 - t1:.1f}s", file=sys.stderr, flush=True)
-
-    name = {(50_000_000, 5_000): "C3", (200_000_000, 10_000): "C4"}.get((args.reads, args.cells), "custom")
-    res = {"config": f"{name}: {args.reads:,} reads x {args.cells} cells, run params (q20 mapq30 "
-                     "dedup=alignment_and_fragment_length)", "host_threads": args.threads, "devices": args.devices,
-           "bam_bytes": bam.stat().st_size, "bam_level": args.bam_level}
-    digests = {}
-    runs = [(mode, fmt, rec, lvl) for rec in args.records.split(",") for mode in args.modes.split(",")
-            for fmt in args.formats.split(",") for lvl in (args.gzip_levels.split(",") if fmt == "txt" else ["-"])]
-    for mode, fmt, rec, lvl in runs:
-        os.environ["MGP_RECORDS"] = rec
-        if lvl != "-":
-            os.environ["MGP_GZIP_LEVEL"] = lvl
-        cfg = PipelineConfig(min_baseq=20, min_mapq=30, max_strand_bias=1.0, skip_deduplication=False,
-                             use_fragment_length_dedup=True, min_reads_per_cell=1, n_cores=args.threads)
-        t = time.time()
-        od = out / f"run_{fmt}_{mode}"
-        devs = [int(x) for x in args.devices.split(",")]
-        p = MtDNAPipeline(str(bam), whitelist, od, config=cfg, output_format=fmt, stream=mode == "stream",
-                          devices=devs if len(devs) > 1 else None)
-        ret = p.run()
-        wall = time.time() - t
-        key = f"{fmt}_{mode}" + (f"_r{rec}" if "," in args.records else "") + \
-              (f"_z{lvl}" if lvl != "-" and "," in args.gzip_levels else "")
-        res[key] = {"wall_s": round(wall, 2), "records": rec, "gzip_level": None if lvl == "-" else int(lvl),
-                    **{k: (round(v, 3) if isinstance(v, float) else v) for k, v in p.timings.items()},
-                    "reads_per_s_end_to_end": round(args.reads / wall), "cells_passed": ret.get("cells_passed_qc")}
-        if fmt == "txt":
-            res[key]["txt_gz_bytes"] = sum((od / "output" / f"output.{f}.txt.gz").stat().st_size
-                                           for f in ("A", "C", "G", "T", "coverage"))
-        if fmt == "hdf5":
-            html = od / "mgatk2_report.html"
-            res[key]["report_html_bytes"] = html.stat().st_size if html.exists() else 0
-            res[key]["report_figures"] = html.read_text().count("data:image/png") if html.exists() else 0
-        print(f"[e2e] {key}: {res[key]}", file=sys.stderr, flush=True)
-        if fmt == "txt":  # every mode, record layout and level must write the same text
-            import gzip
-            import hashlib
-
-            h = hashlib.sha256()
-            for f in ("A", "C", "G", "T", "coverage"):
-                h.update(gzip.decompress((od / "output" / f"output.{f}.txt.gz").read_bytes()))
-            digests[key] = h.hexdigest()
-        import shutil
-
-        shutil.rmtree(od, ignore_errors=True)
-    if len(digests) > 1:
-        res["txt_identical_across_runs"] = len(set(digests.values())) == 1
+    res = run_e2e(args.reads, args.cells, args.threads, args.out, formats=tuple(args.formats.split(",")),
+                  modes=tuple(args.modes.split(",")), records=tuple(args.records.split(",")),
+                  gzip_levels=tuple(args.gzip_levels.split(",")), bam_level=args.bam_level,
+                  reuse_bam=args.reuse_bam, devices=args.devices)
     print(json.dumps(res), flush=True)
 
 

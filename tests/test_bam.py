@@ -371,3 +371,65 @@ def test_reference_bai_pins_the_index_reader(tmp_path):
     shutil.copy(bai, str(bad) + ".bai")
     with pytest.raises(BAMFormatError, match="reference count"):
         BamFile(bad)
+
+
+@pytest.mark.parametrize("ssse3", [True, False])
+def test_decoder_64_byte_records_match_the_definition(ssse3, tmp_path):
+    """The decoder's 64-byte records (mgp_pack32_host.h pack64_record_fast: SSSE3
+    shuffles and non-temporal stores, or the definition's loop with MGP_NO_SSSE3=1)
+    are mgp_pack_record's bytes (include/mgpileup.h, via the Python packer) on random
+    reads: every CIGAR operation, 1-50 bases with N and IUPAC codes, qualities up to
+    255 (unpackable ones keep the full layout), reads without a barcode tag (records
+    ending right after the qualities: the short-tail copy), whole and streamed decode."""
+    import os
+    import subprocess
+    import sys
+    from pathlib import Path
+
+    code = r'''
+import sys, numpy as np
+sys.path.insert(0, sys.argv[1])
+sys.path.insert(0, sys.argv[1] + "/tests")
+from test_pack32 import _random_reads
+from mgatk2_amd.bam import BamFile, StreamSlot, soa_to_bam
+from mgatk2_amd.synth import FLAG_PACKED, pack_reads
+rng = np.random.default_rng(77)
+reads = _random_reads(rng, 6000)
+for i, r in enumerate(reads):
+    r["bc"] = -1 if i % 5 == 0 else int(i % 7)
+    r["query_qualities"][0] = min(r["query_qualities"][0], 254)  # (0xFF first: BAM's missing QUAL)
+want = pack_reads(reads)
+soa_to_bam(sys.argv[2], pack_reads(reads, pack=False), [f"BC{i:02d}-1" for i in range(7)])
+wl = [f"BC{i:02d}-1" for i in range(7)]
+with BamFile(sys.argv[2], n_threads=3) as bf:
+    whole = bf.read_soa("chrM", wl, rec_align=64, pack=True, paired=False)
+    slot = StreamSlot(1 << 13, 1 << 20)
+    parts = []
+    with bf.stream("chrM", wl, paired=False) as st:
+        while st.next_into(slot):
+            s = slot.soa()
+            parts.append((s.flag.copy(), s.rec_off.copy(), s.payload.copy()))
+def check(flag, off, pay, lo):
+    pk = (flag & FLAG_PACKED) != 0
+    assert np.array_equal(flag, want.flag[lo:lo + flag.size])
+    for i in np.flatnonzero(pk):
+        a, b = int(off[i]), int(want.rec_off[lo + i])
+        assert np.array_equal(pay[a:a + 64], want.payload[b:b + 64]), (lo + i, reads[lo + i])
+    return int(pk.sum())
+n = check(whole.flag, whole.rec_off, whole.payload, 0)
+lo = m = 0
+for f, o, p in parts:
+    m += check(f, o, p, lo)
+    lo += f.size
+assert lo == len(reads) and n == m and 2000 < n < len(reads)
+print("ok", n)
+'''
+    env = dict(os.environ)
+    env.pop("MGP_NO_SSSE3", None)
+    if not ssse3:
+        env["MGP_NO_SSSE3"] = "1"
+    root = str(Path(__file__).resolve().parent.parent)
+    r = subprocess.run([sys.executable, "-c", code, root, str(tmp_path / "r.bam")], capture_output=True, text=True,
+                       env=env, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert r.stdout.startswith("ok")
