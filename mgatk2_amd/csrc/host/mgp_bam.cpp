@@ -27,6 +27,7 @@
 #include <thread>
 #include <unistd.h>
 #include <unordered_map>
+#include <utility>
 #include <vector>
 
 #include "../../../include/mgpileup.h"
@@ -201,6 +202,53 @@ bool inflate_block(const uint8_t* blk, uint32_t csize, uint8_t* out, uint32_t is
     return mgp_host::crc32_any(0, out, isize) == crc;
 }
 
+// A thread that runs one job at a time (the stream decode's serial placement, beside
+// the pool's passes over the next chunk; the prefetch's boundary walk, beside the
+// next chunk's read and inflate).
+class Worker {
+  public:
+    Worker() : th_([this] { loop(); }) {}
+    ~Worker() {
+        {
+            std::lock_guard<std::mutex> g(mu_);
+            stop_ = true;
+        }
+        cv_.notify_all();
+        th_.join();
+    }
+    void submit(std::function<void()> f) {
+        std::lock_guard<std::mutex> g(mu_);
+        job_ = std::move(f);
+        busy_ = true;
+        cv_.notify_all();
+    }
+    void wait() {
+        std::unique_lock<std::mutex> g(mu_);
+        cv_.wait(g, [&] { return !busy_; });
+    }
+
+  private:
+    void loop() {
+        std::unique_lock<std::mutex> g(mu_);
+        for (;;) {
+            cv_.wait(g, [&] { return stop_ || (busy_ && job_); });
+            if (stop_) return;
+            std::function<void()> f = std::move(job_);
+            job_ = nullptr;
+            g.unlock();
+            f();
+            g.lock();
+            busy_ = false;
+            cv_.notify_all();
+        }
+    }
+    std::mutex mu_;
+    std::condition_variable cv_;
+    std::function<void()> job_;
+    bool busy_ = false, stop_ = false;
+    std::thread th_;
+};
+
 // An inflated chunk of the BGZF stream: the bytes of consecutive whole blocks at
 // mem + kHead (the room in front takes the partial record the consumer carries over
 // from the chunk before).
@@ -320,6 +368,10 @@ class Prefetch {
         c->walked = true;
     }
     void run() {
+        struct Settle {
+            Prefetch* p;
+            ~Settle() { p->settle_walk(); }
+        } settle{this};
         size_t want_c = 64u << 10;
         std::vector<uint8_t> raw;
         std::vector<Block> blocks;
@@ -348,8 +400,17 @@ class Prefetch {
                 // whole blocks only; a block larger than the read: read it alone
                 for (;;) {
                     const double tr0 = now_s();
-                    raw.resize(want);
-                    const bool rd_ok = pread_all(bam_->fd, raw.data(), want, coff_);
+                    bool rd_ok;
+                    if (ahead_want_ && ahead_coff_ == coff_ && ahead_want_ == want) {  // read during the last inflate
+                        reader_.wait();
+                        raw.swap(ahead_);
+                        rd_ok = ahead_ok_;
+                    } else {
+                        if (ahead_want_) reader_.wait();
+                        raw.resize(want);
+                        rd_ok = pread_all(bam_->fd, raw.data(), want, coff_);
+                    }
+                    ahead_want_ = 0;
                     t_pread += now_s() - tr0;
                     if (!rd_ok) return delete c, set_fail("read error in " + bam_->path);
                     blocks.clear();
@@ -374,6 +435,16 @@ class Prefetch {
                         p += bs;
                     }
                     if (!blocks.empty()) {
+                        // (MGP_BAM_READ_AHEAD=1: the next chunk's compressed bytes read on the
+                        // reader while this one inflates)
+                        if (read_ahead_ && coff_ + p < (uint64_t)bam_->file_size) {
+                            ahead_coff_ = coff_ + p;
+                            ahead_want_ = (size_t)std::min<uint64_t>(want_c, (uint64_t)bam_->file_size - ahead_coff_);
+                            reader_.submit([this] {
+                                ahead_.resize(ahead_want_);
+                                ahead_ok_ = pread_all(bam_->fd, ahead_.data(), ahead_want_, ahead_coff_);
+                            });
+                        }
                         if (kHead + total > c->cap) {
                             c->cap = kHead + total + (total >> 3);
                             c->mem.reset(new (std::nothrow) uint8_t[c->cap]);
@@ -399,9 +470,6 @@ class Prefetch {
                         t_inflate += now_s() - ti0;
                         if (!ok) return delete c, set_fail("BGZF inflate/CRC error in " + bam_->path);
                         c->n = total;
-                        const double tw0 = now_s();
-                        walk(c);
-                        t_walk += now_s() - tw0;
                         coff_ += p;
                         c->last = last = coff_ >= (uint64_t)bam_->file_size;
                         break;
@@ -416,16 +484,63 @@ class Prefetch {
                     want = bs;
                 }
             }
-            {
-                std::lock_guard<std::mutex> g(mu_);
-                ready_.push_back(c);
+            // the chunk before leaves its walk first (chunks reach the consumer in file
+            // order); this one's walk then runs on the walker while the loop reads and
+            // inflates the next (the walk is a serial chain: ~30 % of this thread's time)
+            walker_.wait();
+            if (walked_) push_ready(std::exchange(walked_, nullptr));
+            if (walk_async_ && walking_ && c->n > 0 && !last) {
+                walked_ = c;
+                walker_.submit([this, c] {
+                    const double tw0 = now_s();
+                    walk(c);
+                    t_walk += now_s() - tw0;
+                });
+            } else {
+                const double tw0 = now_s();
+                walk(c);
+                t_walk += now_s() - tw0;
+                push_ready(c);
             }
-            cv_.notify_all();
         }
+    }
+    void push_ready(Chunk* c) {
+        {
+            std::lock_guard<std::mutex> g(mu_);
+            ready_.push_back(c);
+        }
+        cv_.notify_all();
+    }
+    // (every return of run(): a chunk still on the walker goes to ready_, which the
+    // destructor frees)
+    void settle_walk() {
+        reader_.wait();
+        walker_.wait();
+        if (walked_) push_ready(std::exchange(walked_, nullptr));
     }
     mgp_bam* bam_;
     uint64_t coff_;
     mgp_host::Pool pool_;  // (before th_: alive while run() uses it)
+    Worker walker_;        // (likewise)
+    Worker reader_;        // (likewise; its read targets ahead_)
+    std::vector<uint8_t> ahead_;
+    uint64_t ahead_coff_ = 0;
+    size_t ahead_want_ = 0;  // 0: no read ahead pending
+    bool ahead_ok_ = false;
+    // (MGP_BAM_READ_AHEAD=1: the next chunk read during this one's inflate. Off: on the
+    // box's 16-core share the kernel's copy competes with the inflate pool, C4 ingest
+    // 3.71-3.95 s against 3.68-3.73 s reading in line, profiles/r05/e2e_walk_r5u_*.log)
+    const bool read_ahead_ = [] {
+        const char* e = std::getenv("MGP_BAM_READ_AHEAD");
+        return e && std::strtol(e, nullptr, 10) != 0;
+    }();
+    Chunk* walked_ = nullptr;  // the chunk on the walker
+    // (MGP_BAM_WALK_ASYNC=0: the walk on this thread, between inflates; C4 ingest 4.80-5.21 s
+    // against 3.65-4.00 s with the walker, profiles/r05/e2e_walk_r5t_*.log)
+    const bool walk_async_ = [] {
+        const char* e = std::getenv("MGP_BAM_WALK_ASYNC");
+        return !e || std::strtol(e, nullptr, 10) != 0;
+    }();
     bool walking_;
     int64_t wnext_;
     uint8_t wpart_[4] = {0, 0, 0, 0};
@@ -847,51 +962,6 @@ struct ChunkRecs {
     bool over = false;  // placement ran past the payload capacity (never: the batch cut bounds it)
 };
 
-// A thread that runs one job at a time (the stream decode's serial placement, beside
-// the pool's passes over the next chunk).
-class Worker {
-  public:
-    Worker() : th_([this] { loop(); }) {}
-    ~Worker() {
-        {
-            std::lock_guard<std::mutex> g(mu_);
-            stop_ = true;
-        }
-        cv_.notify_all();
-        th_.join();
-    }
-    void submit(std::function<void()> f) {
-        std::lock_guard<std::mutex> g(mu_);
-        job_ = std::move(f);
-        busy_ = true;
-        cv_.notify_all();
-    }
-    void wait() {
-        std::unique_lock<std::mutex> g(mu_);
-        cv_.wait(g, [&] { return !busy_; });
-    }
-
-  private:
-    void loop() {
-        std::unique_lock<std::mutex> g(mu_);
-        for (;;) {
-            cv_.wait(g, [&] { return stop_ || (busy_ && job_); });
-            if (stop_) return;
-            std::function<void()> f = std::move(job_);
-            job_ = nullptr;
-            g.unlock();
-            f();
-            g.lock();
-            busy_ = false;
-            cv_.notify_all();
-        }
-    }
-    std::mutex mu_;
-    std::condition_variable cv_;
-    std::function<void()> job_;
-    bool busy_ = false, stop_ = false;
-    std::thread th_;
-};
 
 struct Decoder {
     mgp_bam* b;
@@ -1714,11 +1784,13 @@ struct mgp_bam_stream {
         if (std::getenv("MGP_HOST_PROFILE"))
             std::fprintf(stderr,
                          "[mgp_bam_stream] %lld records, %d threads%s: open %.3f s; waiting for inflated chunks %.3f, "
-                         "record walk %.3f (listed %.3f; prefetch thread %.3f; %lld + %lld chunks), classify %.3f, fields %.3f, "
+                         "record walk %.3f (listed %.3f; prefetch: read %.3f, inflate %.3f, walk %.3f; %lld + %lld chunks), "
+                         "classify %.3f, fields %.3f, "
                          "duplicate keys %.3f, placement %.3f (waited for %.3f), records %.3f\n",
                          (long long)decoded, dec.pool.size(), pipe ? ", pipelined" : dense_fuse ? ", BAM order fused" : "",
                          now_s() - t_open, t_fill,
-                         t_walk, t_list, st.pf ? st.pf->t_walk : 0.0, (long long)n_listed, (long long)n_walked, t_class, dec.t_fields,
+                         t_walk, t_list, st.pf ? st.pf->t_pread : 0.0, st.pf ? st.pf->t_inflate : 0.0,
+                         st.pf ? st.pf->t_walk : 0.0, (long long)n_listed, (long long)n_walked, t_class, dec.t_fields,
                          dec.t_dups, dec.t_place, t_wait,
                          (pipe || dense_fuse) ? dec.t_recs : dec.t_p2 - dec.t_fields - dec.t_place);
     }
