@@ -53,7 +53,9 @@ extern "C" {
                                  their batch's payload (MGP_E_INVALID), mgp_copy_wait, batches
                                  without a start column,
                                  mgp_synth_params.n_rec_off, rows targets with min_reads > 1;
-                              5: mgp_set_cell_range (one device's cells of whole batches) */
+                              5: mgp_set_cell_range (one device's cells of whole batches),
+                                 mgp_push_batch16 (16-bit barcode / |tlen| columns), dense
+                                 64-byte batches paired on the device */
 
 /* ---- return codes (0 = success) ------------------------------------------ */
 #define MGP_OK               0
