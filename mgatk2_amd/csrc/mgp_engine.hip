@@ -1175,6 +1175,18 @@ constexpr int kBPer = kStageB / kGBBlock;  // elements per lane per step
 #ifndef MGP_ABL_B
 #define MGP_ABL_B 0  // pass-B ablations (experiments only): 1 no dedup walk, 2 no pel stores, 3 no loads
 #endif
+#ifndef MGP_GB_CARRY
+// A cell's elements of a step end mid-way through a 64-byte granule of pel; the next
+// step (~16 us later, other lines meanwhile through the XCD's L2) writes the rest, so
+// the granule reached HBM twice (r04-r05: 1.06-1.20 GB written per C4 launch for 0.65 GB
+// of elements). With the carry, a step's incomplete tail granule stays in LDS
+// (carry[cell]) until a later step completes it, and every granule is written once
+// except at the workgroup's first and last (its bin range's ends). Off: it takes the
+// writes from 1.06 to 0.86-0.89 GB but pass B from 1.02 to 1.13 ms, and pass B without
+// any pel store (MGP_ABL_B=2) takes 1.045 ms, so its stores, amplified or not, cost it
+// no time (profiles/r05/ab_carry_r5x.txt).
+#define MGP_GB_CARRY 0
+#endif
 
 #ifndef MGP_GB_LOOK
 #define MGP_GB_LOOK 3  // predecessors compared branch-free before a deferred walk (v42 A/B: 2, 4, 6 slower)
@@ -1214,6 +1226,10 @@ __global__ void __launch_bounds__(kGBBlock, Tr::kWaves) k_group_b(const typename
     __shared__ int s_be;
     __shared__ uint32_t s_ndup[kGroup], s_nunp[kGroup];  // the group's duplicates / kept unpaired reads in this bin range
     __shared__ uint16_t wpend[kGBBlock / kWave][kBPer * kWave];  // per wave: stage indices of deferred walks
+    // MGP_GB_CARRY: per cell, the elements [carry_lo, cbase & 15) of the granule holding
+    // cbase (written by earlier steps, not yet to pel)
+    __shared__ uint32_t carry[MGP_GB_CARRY ? kGroup : 1][16];
+    __shared__ uint32_t carry_lo[kGroup];
     const int gi = gx;
     const int B0 = gy * rb, B1 = min(g.nbins, B0 + rb);
     const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // (scalar)
@@ -1230,10 +1246,29 @@ __global__ void __launch_bounds__(kGBBlock, Tr::kWaves) k_group_b(const typename
     }
     if (wid == 0) {
         cbase[lane] = c < nc ? O[(size_t)B0 * nc + c] : 0u;  // each cell's next slot
+        carry_lo[lane] = cbase[lane] & 15u;                  // (nothing carried)
         s_ndup[lane] = 0u;
         s_nunp[lane] = 0u;
     }
     __syncthreads();
+    // a pileup element to pel, or to its cell's carry when it falls in the step's
+    // incomplete tail granule (stage index t of cell lc's run)
+    auto put = [&](int lc, uint32_t t, uint32_t pv) {
+        const uint32_t p = cbase[lc] + (t - cstart[lc]);
+        const uint32_t e = cbase[lc] + (cstart[lc + 1] - cstart[lc]);
+        if (MGP_GB_CARRY && (p >> 4) == (e >> 4) && (e & 15u)) carry[lc][p & 15u] = pv;
+        else pel[p] = pv;
+    };
+    // every cell's carried elements to pel (full = false: only the cells whose carried
+    // granule this step completes; before the step's tail elements reuse the slots)
+    auto flush = [&](bool full) {
+        for (int x = threadIdx.x; x < kGroup * 16; x += kGBBlock) {
+            const int lc = x >> 4;
+            const uint32_t k = (uint32_t)x & 15u, cb = cbase[lc];
+            const bool done = full || ((cb + (cstart[lc + 1] - cstart[lc])) >> 4) != (cb >> 4);
+            if (done && k >= carry_lo[lc] && k < (cb & 15u)) pel[(cb & ~15u) + k] = carry[lc][k];
+        }
+    };
     // bins [b, s_be) of the step starting at b: as many as fit the stage (one if its
     // bucket alone is larger: direct path); spre = prefix of their bucket sizes
     auto plan = [&](int b) {
@@ -1290,6 +1325,10 @@ __global__ void __launch_bounds__(kGBBlock, Tr::kWaves) k_group_b(const typename
     uint32_t tot = be > b ? load(b, be) : 0u;
     while (b < B1) {
         if (be == b) {  // one bucket larger than the stage: direct stores (wave 0)
+            if (MGP_GB_CARRY) {
+                flush(true);
+                __syncthreads();
+            }
             if (wid == 0) {
                 wcnt[0][lane] = cbase[lane];
                 __builtin_amdgcn_wave_barrier();
@@ -1297,6 +1336,7 @@ __global__ void __launch_bounds__(kGBBlock, Tr::kWaves) k_group_b(const typename
                                     nullptr, nullptr, mode, unit, pel, acc, s_ndup, s_nunp, st, b >= cnt_lo);
                 __builtin_amdgcn_wave_barrier();
                 cbase[lane] = wcnt[0][lane];
+                carry_lo[lane] = cbase[lane] & 15u;
             }
             __syncthreads();
             ++b;
@@ -1351,6 +1391,9 @@ __global__ void __launch_bounds__(kGBBlock, Tr::kWaves) k_group_b(const typename
         // the next step's loads go out now and land while this step is written out
         const uint32_t cur = tot;
         const int nb0 = be;
+        // granules carried from earlier steps that this step completes, before the barrier
+        // below (the step's tail elements then reuse the carry slots)
+        if (MGP_GB_CARRY) flush(false);
         const int nbe = nb0 < B1 ? plan(nb0) : nb0;  // (its barrier also completes the stage)
         if (nb0 >= B1) __syncthreads();
         const uint32_t ntot = nbe > nb0 ? load(nb0, nbe) : 0u;
@@ -1404,7 +1447,7 @@ __global__ void __launch_bounds__(kGBBlock, Tr::kWaves) k_group_b(const typename
                 bool keep = false;
                 if (act) {
                     const uint32_t pv = group_b_emit<Tr>(xs[q], d2[q], d3[q], mode, unit, acc, keep, cnt);
-                    if (MGP_ABL_B < 2 || pv == 7u) pel[cbase[lc] + (t - cstart[lc])] = pv;
+                    if (MGP_ABL_B < 2 || pv == 7u) put(lc, t, pv);
                 }
                 cell_tally<kTrack, Tr>(act, lc, keep, xs[q], s_ndup, s_nunp, st);
             }
@@ -1436,17 +1479,22 @@ __global__ void __launch_bounds__(kGBBlock, Tr::kWaves) k_group_b(const typename
             bool keep = false;
             if (act) {
                 const uint32_t pv = group_b_emit<Tr>(x, dup2, dup3, mode, unit, acc, keep, cnt);
-                if (MGP_ABL_B < 2 || pv == 7u) pel[cbase[lc] + (t - cstart[lc])] = pv;
+                if (MGP_ABL_B < 2 || pv == 7u) put(lc, t, pv);
             }
             cell_tally<kTrack, Tr>(act, lc, keep, x, s_ndup, s_nunp, st);
         }
         __syncthreads();
-        if (wid == 0) cbase[lane] += cstart[lane + 1] - cstart[lane];
+        if (wid == 0) {
+            const uint32_t cb = cbase[lane], e = cb + (cstart[lane + 1] - cstart[lane]);
+            if ((e >> 4) != (cb >> 4)) carry_lo[lane] = 0u;  // the carry now holds e's granule from its start
+            cbase[lane] = e;
+        }
         __syncthreads();
         b = nb0;
         be = nbe;
         tot = ntot;
     }
+    if (MGP_GB_CARRY) flush(true);  // the last granules (the bin range's end)
     // the group's per-cell paired flags over this bin range (kTrack)
     if (kTrack && wid == 0 && c < nc) {
         const uint32_t kept = cbase[lane] - O[(size_t)B0 * nc + c] - s_ndup[lane];
@@ -3142,7 +3190,9 @@ int mgp_open(const mgp_config* cfg, int hip_device, mgp_ctx** out) {
     // the histogram's LDS per workgroup (one workgroup of 8 waves per CU either way): up to
     // 150 KiB, ~37k cells per slice (C5's 100k cells in 3 slices, not 5 at 96 KiB);
     // MGP_HIST_LDS_KB / MGP_HIST_XCD=0 for A/B. The same budget bounds grouping pass A's
-    // per-group counters (its 512-thread form up to ~140k cells, 256 threads beyond)
+    // per-group counters (its 512-thread form when they fit and a workgroup gets at least
+    // MGP_GA_WIDE_MIN reads; kGANBlock = 128 threads otherwise: beyond ~140k cells and for
+    // the small multi-GPU shares)
     size_t hist_kb = 150;
     if (const char* e = std::getenv("MGP_HIST_LDS_KB")) hist_kb = (size_t)std::max(4L, std::strtol(e, nullptr, 10));
     ctx->lds_hist_max_cells = (int)std::min<size_t>(prop.sharedMemPerBlock, hist_kb * 1024) / 4;
