@@ -2833,6 +2833,12 @@ __global__ void k_rebase_bc(int32_t* __restrict__ bc, int64_t n, int32_t lo, int
 // a record sits (every read is found through its rec_off).
 constexpr int kPairBlock = 1024;
 constexpr int64_t kPairReads = 1 << 18;  // reads of a pairing workgroup's range
+#ifndef MGP_PAIR_SPLIT
+// copy workgroups per range: a 16M-read batch has only 61 ranges, and one workgroup per
+// range left three CUs in four idle (k_pair_place 17.2 ms per C4 step, r5aa trace)
+#define MGP_PAIR_SPLIT 16
+#endif
+constexpr int kPairSplit = MGP_PAIR_SPLIT;
 constexpr int kPairMaxKeys = 32768;      // cells + 1 whose counters fit a workgroup's LDS
 
 __device__ __forceinline__ int pair_key(int32_t c, uint16_t f, int nc) {
@@ -2871,7 +2877,8 @@ __global__ void __launch_bounds__(1024) k_pair_scan(uint32_t* __restrict__ lines
 }
 
 // every record to its line half; rec_off = pay0 + line x 128 + half x 64. Four lanes
-// copy a record (16 bytes each).
+// copy a record (16 bytes each); blockIdx.y takes 1 / kPairSplit of range blockIdx.x
+// (each workgroup scans the range's key counts into line bases itself).
 __global__ void __launch_bounds__(kPairBlock) k_pair_place(const uint4* __restrict__ src, const int32_t* __restrict__ bc,
                                                            const uint16_t* __restrict__ flag, int64_t n, int nc,
                                                            const uint32_t* __restrict__ rank,
@@ -2880,7 +2887,9 @@ __global__ void __launch_bounds__(kPairBlock) k_pair_place(const uint4* __restri
                                                            uint8_t* __restrict__ payload, uint64_t* __restrict__ roff) {
     extern __shared__ uint32_t lbase[];  // [nc + 1]: each key's first line in the range
     __shared__ uint32_t wsum[16], carry;
-    const int64_t lo = (int64_t)blockIdx.x * kPairReads, hi = min(n, lo + kPairReads);
+    const int64_t r0 = (int64_t)blockIdx.x * kPairReads, part = kPairReads / kPairSplit;
+    const int64_t lo = r0 + (int64_t)blockIdx.y * part, hi = min(n, lo + part);
+    if (lo >= hi) return;
     for (int k = threadIdx.x; k <= nc; k += blockDim.x) lbase[k] = (cntw[(size_t)blockIdx.x * (nc + 1) + k] + 1u) >> 1;
     __syncthreads();
     block_exclusive_scan(lbase, nc + 1, lbase, wsum, &carry);
@@ -3457,7 +3466,7 @@ static int push_impl(mgp_ctx* ctx, const mgp_batch* b, const uint16_t* bc16, con
         HIP_TRY(hipGetLastError());
         k_pair_scan<<<1, 1024, 0, sp>>>(ctx->pair_lines.as<uint32_t>(), npw);
         HIP_TRY(hipGetLastError());
-        k_pair_place<<<npw, kPairBlock, lds, sp>>>(
+        k_pair_place<<<dim3((unsigned)npw, (unsigned)kPairSplit), kPairBlock, lds, sp>>>(
             ctx->stage[j].as<uint4>(), ctx->bc.as<int32_t>() + n0, ctx->flag.as<uint16_t>() + n0, nb, nc,
             ctx->pair_rank.as<uint32_t>(), ctx->pair_cnt.as<uint32_t>(), ctx->pair_lines.as<uint32_t>(),
             (uint64_t)pay0, ctx->payload.as<uint8_t>(), ctx->roff.as<uint64_t>() + n0);
