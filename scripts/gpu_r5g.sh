@@ -18,8 +18,8 @@ if [[ $STEPS == *bench* ]]; then
     timeout -k 10 400 python -u bench.py > gpurun_out/bench_$V.log 2>&1 || { tail -20 gpurun_out/bench_$V.log; exit 1; }
     tail -c 400 gpurun_out/bench_$V.log
 fi
-HEAD="--steps 5 --warmup 1 --no-cpu-baseline --no-check --no-pcie --no-device --no-device-paired --no-host-pack"
-DEV="--device-only --steps 5 --warmup 1 --no-cpu-baseline --no-check --no-pcie --no-device-paired --no-host-pack"
+HEAD="--steps 5 --warmup 1 --no-cpu-baseline --no-check --no-pcie --no-device --no-device-paired --no-host-pack --no-e2e"
+DEV="--device-only --steps 5 --warmup 1 --no-cpu-baseline --no-check --no-pcie --no-device-paired --no-host-pack --no-e2e"
 if [[ $STEPS == *prof* ]]; then
     for leg in head dev; do
         args=$HEAD; [ $leg = dev ] && args=$DEV
