@@ -128,6 +128,7 @@ struct mgp_ctx {
     int32_t cell_lo = 0;     // mgp_set_cell_range: the context's cells in the pushed batches' barcode indices
     bool cell_range = false;
     int pile_wg_stream = 0;  // a streaming run's pileup workgroups per window (set_pile_chunks; 0: the default)
+    int pile_min_cpb_stream = 1;  // a streaming run's least cells per pileup chunk (MGP_PILE_MIN_CPB_STREAM)
     // on-device pairing of dense 64-byte batches (mgp_push_batch): two staging buffers
     // the H2D copies land in, the event after the pairing kernels that last read each
     bool dev_pair = true;  // (MGP_DEV_PAIR=0: records stay in BAM order, for A/B)
@@ -3117,11 +3118,13 @@ __global__ void k_respec_slot(const DevStats* st, unsigned long long* slot) {
 // 1250-cell step is 11 % shorter). A streaming run launches the pileup per segment,
 // about one window each: there the chunks are sized for ~wg_stream workgroups per
 // window (C4: 2000 chunks of 5 cells instead of 625 of 16, which left 40 % of the
-// 1024 workgroup slots of a one-window launch empty), at least 2 cells each.
-static void set_pile_chunks(Geom& g, bool stream, int wg_stream) {
+// 1024 workgroup slots of a one-window launch empty). Chunks of one cell are allowed
+// there (r05, `abs_r5ad.txt`): the 8-GPU share of C4 (1250 cells) had 625 workgroups per
+// launch at 2 cells each, the pileup 1.19 -> 0.95 ms per step at 1 (the step unchanged).
+static void set_pile_chunks(Geom& g, bool stream, int wg_stream, int min_cpb_stream = 1) {
     int64_t cpb;
     if (stream) {
-        cpb = std::max<int64_t>(2, ((int64_t)g.nc + wg_stream - 1) / std::max(1, wg_stream));
+        cpb = std::max<int64_t>(min_cpb_stream, ((int64_t)g.nc + wg_stream - 1) / std::max(1, wg_stream));
     } else {
         const int64_t target = MGP_PILE_WG;
         cpb = std::max<int64_t>(MGP_PILE_MIN_CPB, ((int64_t)g.nc * g.nwin + target - 1) / target);
@@ -3248,6 +3251,7 @@ int mgp_open(const mgp_config* cfg, int hip_device, mgp_ctx** out) {
     if (const char* e = std::getenv("MGP_ROWS_WG")) ctx->rows_wg = std::max(1, std::atoi(e));
     ctx->pile_wg_stream = MGP_PILE_WG_STREAM;
     if (const char* e = std::getenv("MGP_PILE_WG_STREAM")) ctx->pile_wg_stream = std::max(1, std::atoi(e));
+    if (const char* e = std::getenv("MGP_PILE_MIN_CPB_STREAM")) ctx->pile_min_cpb_stream = std::max(1, std::atoi(e));
     HIP_TRY(hipStreamCreateWithFlags(&ctx->s_side, hipStreamNonBlocking));
     HIP_TRY(hipStreamCreateWithFlags(&ctx->s_d2h, hipStreamNonBlocking));
     HIP_TRY(hipEventCreateWithFlags(&ctx->ev_rows, hipEventDisableTiming));
@@ -4042,7 +4046,7 @@ static int stream_segments(mgp_ctx* ctx, int64_t last_start, uint16_t last_flag)
         ctx->stream_off = true;
         return MGP_OK;
     }
-    if (!ctx->seg_open) set_pile_chunks(ctx->g, true, ctx->pile_wg_stream);  // (the whole run's chunks)
+    if (!ctx->seg_open) set_pile_chunks(ctx->g, true, ctx->pile_wg_stream, ctx->pile_min_cpb_stream);  // (the whole run's chunks)
     MGP_TRY(ensure_run_buffers(ctx));
     int dup_parts = 0, pair_mode = 0;
     const Seg sg{ctx->w_done, (int)wc, (int)(wc * g.W / g.G), !ctx->seg_open, true};
