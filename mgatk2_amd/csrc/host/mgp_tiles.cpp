@@ -14,6 +14,7 @@
 #include <cstdint>
 #include <cstdlib>
 #include <cstring>
+#include <memory>
 #include <string>
 #include <thread>
 #include <vector>
@@ -22,6 +23,53 @@
 #include "../../../include/mgpileup_host.h"
 
 std::string& mgp_host_err();  // mgp_bam.cpp
+
+namespace {
+// The compressed chunks of a parallel deflate: each thread compresses into one scratch
+// buffer and appends the result to an arena of its own; the arenas, scratch buffers, tile
+// buffers and compressors are all allocated before the threads start, so the threads
+// never map or unmap memory (a per-chunk output vector sized to the deflate bound, ~200 KB,
+// is above glibc's mmap threshold, so each chunk mapped and unmapped its own buffer).
+struct Arena {
+    std::vector<uint8_t> buf, scratch;
+    std::vector<uint16_t> tiles;
+    std::unique_ptr<mgp_host::Deflator> dz;
+    void prepare(int level, size_t tile_bytes, size_t expect) {
+        dz.reset(new mgp_host::Deflator(level));
+        scratch.reserve(tile_bytes + tile_bytes / 8 + 4096);  // (above the deflate bound)
+        buf.reserve(expect);
+        tiles.resize((tile_bytes + 1) / 2);
+    }
+};
+struct Piece {
+    int32_t th = 0;
+    uint64_t off = 0, len = 0;
+};
+// the pieces, in order, into one malloc'd blob with offsets[0..m] (offsets[m] = total)
+bool gather_pieces(const std::vector<Piece>& pc, const std::vector<Arena>& ar, uint8_t** blob, int64_t* offsets) {
+    size_t total = 0;
+    for (size_t i = 0; i < pc.size(); ++i) {
+        offsets[i] = (int64_t)total;
+        total += pc[i].len;
+    }
+    offsets[pc.size()] = (int64_t)total;
+    uint8_t* b = (uint8_t*)std::malloc(std::max<size_t>(total, 1));
+    if (!b) return false;
+    for (size_t i = 0; i < pc.size(); ++i)
+        if (pc[i].len) std::memcpy(b + offsets[i], ar[(size_t)pc[i].th].buf.data() + pc[i].off, pc[i].len);
+    *blob = b;
+    return true;
+}
+// one chunk through the thread's scratch into its arena
+bool deflate_piece(mgp_host::Deflator& dz, const uint8_t* src, size_t n, Arena& a, int32_t th, Piece& out) {
+    if (!dz.zlib(src, n, a.scratch)) return false;
+    out.th = th;
+    out.off = a.buf.size();
+    out.len = a.scratch.size();
+    a.buf.insert(a.buf.end(), a.scratch.begin(), a.scratch.end());
+    return true;
+}
+}  // namespace
 
 extern "C" {
 
@@ -35,53 +83,45 @@ int64_t mgp_deflate_tiles(const void* data, int64_t rows, int64_t cols, int32_t 
     }
     const int64_t nr = (rows + crow - 1) / crow, nc = (cols + ccol - 1) / ccol, n = nr * nc;
     const size_t chunk_bytes = (size_t)crow * (size_t)ccol * (size_t)elem_size;
-    std::vector<std::vector<uint8_t>> out((size_t)n);
+    int nt = n_threads > 0 ? n_threads : (int)std::thread::hardware_concurrency();
+    nt = (int)std::max<int64_t>(1, std::min<int64_t>(nt, n));
+    std::vector<Piece> pc((size_t)n);
+    std::vector<Arena> ar((size_t)nt);
     std::atomic<int64_t> next{0};
     std::atomic<bool> ok{true};
     const uint8_t* src = (const uint8_t*)data;
-    auto work = [&]() {
-        std::vector<uint8_t> tile(chunk_bytes);
-        mgp_host::Deflator dz(level);
+    for (auto& a : ar) a.prepare(level, chunk_bytes, chunk_bytes * (size_t)((n + nt - 1) / nt) / 3);
+    auto work = [&](int32_t ti) {
+        Arena& a = ar[(size_t)ti];
+        uint8_t* tile = reinterpret_cast<uint8_t*>(a.tiles.data());
         for (;;) {
             const int64_t t = next.fetch_add(1);
             if (t >= n) break;
             const int64_t r0 = (t / nc) * crow, c0 = (t % nc) * ccol;
             const int64_t h = std::min(crow, rows - r0), w = std::min(ccol, cols - c0);
-            if (h < crow || w < ccol) std::memset(tile.data(), 0, chunk_bytes);
+            if (h < crow || w < ccol) std::memset(tile, 0, chunk_bytes);
             for (int64_t r = 0; r < h; ++r)
-                std::memcpy(tile.data() + (size_t)r * ccol * elem_size,
+                std::memcpy(tile + (size_t)r * ccol * elem_size,
                             src + ((size_t)(r0 + r) * (size_t)cols + (size_t)c0) * elem_size, (size_t)w * elem_size);
             // the H5Z_DEFLATE form: one zlib stream of the whole (padded) chunk
-            if (!dz.zlib(tile.data(), chunk_bytes, out[(size_t)t])) {
+            if (!deflate_piece(*a.dz, tile, chunk_bytes, a, ti, pc[(size_t)t])) {
                 ok = false;
                 return;
             }
         }
     };
-    int nt = n_threads > 0 ? n_threads : (int)std::thread::hardware_concurrency();
-    nt = (int)std::max<int64_t>(1, std::min<int64_t>(nt, n));
     std::vector<std::thread> th;
-    for (int i = 1; i < nt; ++i) th.emplace_back(work);
-    work();
+    for (int i = 1; i < nt; ++i) th.emplace_back(work, (int32_t)i);
+    work(0);
     for (auto& x : th) x.join();
     if (!ok) {
         mgp_host_err() = "deflate failed";
         return -1;
     }
-    size_t total = 0;
-    for (int64_t t = 0; t < n; ++t) {
-        offsets[t] = (int64_t)total;
-        total += out[(size_t)t].size();
-    }
-    offsets[n] = (int64_t)total;
-    uint8_t* b = (uint8_t*)std::malloc(std::max<size_t>(total, 1));
-    if (!b) {
+    if (!gather_pieces(pc, ar, blob, offsets)) {
         mgp_host_err() = "out of host memory";
         return -1;
     }
-    for (int64_t t = 0; t < n; ++t)
-        if (!out[(size_t)t].empty()) std::memcpy(b + offsets[t], out[(size_t)t].data(), out[(size_t)t].size());
-    *blob = b;
     return n;
 }
 
@@ -119,12 +159,17 @@ extern "C" int64_t mgp_h5_plane_tiles(const void* rows, int32_t elem_size, int64
         }
     const int64_t nr = (L + crow - 1) / crow, nc = (n_cols + ccol - 1) / ccol, n = nr * nc;
     const size_t tile_elems = (size_t)crow * (size_t)ccol;
-    std::vector<std::vector<uint8_t>> out((size_t)n * (size_t)n_planes);
+    int nt = n_threads > 0 ? n_threads : (int)std::thread::hardware_concurrency();
+    nt = (int)std::max<int64_t>(1, std::min<int64_t>(nt, n));
+    std::vector<Piece> pc((size_t)n * (size_t)n_planes);
+    std::vector<Arena> ar((size_t)nt);
     std::atomic<int64_t> next{0};
     std::atomic<bool> ok{true};
-    auto work = [&]() {
-        std::vector<uint16_t> tiles(tile_elems * (size_t)n_planes);
-        mgp_host::Deflator dz(level);
+    for (auto& a : ar)
+        a.prepare(level, tile_elems * 2 * (size_t)n_planes, tile_elems * 2 * (size_t)n_planes * (size_t)((n + nt - 1) / nt) / 3);
+    auto work = [&](int32_t ti) {
+        Arena& a = ar[(size_t)ti];
+        std::vector<uint16_t>& tiles = a.tiles;
         for (;;) {
             const int64_t t = next.fetch_add(1);
             if (t >= n || !ok) break;
@@ -153,35 +198,22 @@ extern "C" int64_t mgp_h5_plane_tiles(const void* rows, int32_t elem_size, int64
                 }
             }
             for (int e = 0; e < n_planes; ++e)
-                if (!dz.zlib(reinterpret_cast<const uint8_t*>(tiles.data() + (size_t)e * tile_elems), tile_elems * 2,
-                             out[(size_t)e * (size_t)n + (size_t)t]))
+                if (!deflate_piece(*a.dz, reinterpret_cast<const uint8_t*>(tiles.data() + (size_t)e * tile_elems),
+                                   tile_elems * 2, a, ti, pc[(size_t)e * (size_t)n + (size_t)t]))
                     ok = false;
         }
     };
-    int nt = n_threads > 0 ? n_threads : (int)std::thread::hardware_concurrency();
-    nt = (int)std::max<int64_t>(1, std::min<int64_t>(nt, n));
     std::vector<std::thread> th;
-    for (int i = 1; i < nt; ++i) th.emplace_back(work);
-    work();
+    for (int i = 1; i < nt; ++i) th.emplace_back(work, (int32_t)i);
+    work(0);
     for (auto& x : th) x.join();
     if (!ok) {
         mgp_host_err() = "deflate failed";
         return -1;
     }
-    const size_t m = (size_t)n * (size_t)n_planes;
-    size_t total = 0;
-    for (size_t i = 0; i < m; ++i) {
-        offsets[i] = (int64_t)total;
-        total += out[i].size();
-    }
-    offsets[m] = (int64_t)total;
-    uint8_t* b = (uint8_t*)std::malloc(std::max<size_t>(total, 1));
-    if (!b) {
+    if (!gather_pieces(pc, ar, blob, offsets)) {
         mgp_host_err() = "out of host memory";
         return -1;
     }
-    for (size_t i = 0; i < m; ++i)
-        if (!out[i].empty()) std::memcpy(b + offsets[i], out[i].data(), out[i].size());
-    *blob = b;
     return n;
 }
