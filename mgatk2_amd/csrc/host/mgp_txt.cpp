@@ -14,10 +14,12 @@
 #include <algorithm>
 #include <atomic>
 #include <chrono>
+#include <condition_variable>
 #include <cstdlib>
 #include <cstdint>
 #include <cstdio>
 #include <cstring>
+#include <mutex>
 #include <string>
 #include <thread>
 #include <vector>
@@ -156,50 +158,78 @@ int write_cells(const char* prefix, const T* counts, const T* depth, int64_t mit
     const int64_t n_groups = (n_write + per_group - 1) / per_group;
     const int nt = std::max(1, std::min<int>(n_threads > 0 ? n_threads : (int)std::thread::hardware_concurrency(),
                                              (int)std::max<int64_t>(1, n_groups)));
-    const int64_t round = (int64_t)nt * 4;
-    std::vector<std::vector<uint8_t>> out((size_t)round * 5);
+    // One pool over all groups; this thread writes each group's five members in group
+    // order as they complete, while the pool works on the groups after it (a ring of
+    // `win` groups bounds the buffered output). Until r05 the groups went in rounds of
+    // 4 per thread with the members written between rounds: at C4 and gzip level 1 the
+    // pool sat idle during ~1.8 GB of serial writes.
+    const int64_t win = (int64_t)nt * 4;
+    std::vector<std::vector<uint8_t>> out((size_t)win * 5);
+    std::vector<int64_t> ready((size_t)win, -1);  // group whose members slot g % win holds
+    int64_t written = 0;                           // groups written so far
+    std::mutex mu;
+    std::condition_variable cv;
     std::atomic<bool> ok{true};
-    std::atomic<int64_t> ns_fmt{0}, ns_dfl{0}, n_txt{0};
+    std::atomic<int64_t> next{0}, ns_fmt{0}, ns_dfl{0}, n_txt{0};
     const bool prof = std::getenv("MGP_TXT_PROFILE") != nullptr;
-    int rc = 0;
-    for (int64_t g0 = 0; g0 < n_groups && rc == 0; g0 += round) {
-        const int64_t g1 = std::min(n_groups, g0 + round);
-        std::atomic<int64_t> next{g0};
-        auto work = [&]() {
-            Text txt[5];
-            mgp_host::Deflator dz(level);
-            for (;;) {
-                const int64_t g = next.fetch_add(1);
-                if (g >= g1) break;
-                for (auto& t : txt) t.n = 0;
-                const int64_t c0 = g * per_group, c1 = std::min(n_write, c0 + per_group);
-                const auto a = std::chrono::steady_clock::now();
-                format_group(counts, depth, mito_len, cells, c0, c1, names, txt);
-                const auto b = std::chrono::steady_clock::now();
-                for (int i = 0; i < 5; ++i)
-                    if (!gzip_member(txt[i].b.data(), txt[i].n, dz, out[(size_t)(g - g0) * 5 + i])) ok = false;
-                if (prof) {
-                    const auto e = std::chrono::steady_clock::now();
-                    ns_fmt += std::chrono::duration_cast<std::chrono::nanoseconds>(b - a).count();
-                    ns_dfl += std::chrono::duration_cast<std::chrono::nanoseconds>(e - b).count();
-                    for (auto& x : txt) n_txt += (int64_t)x.n;
-                }
+    auto work = [&]() {
+        Text txt[5];
+        mgp_host::Deflator dz(level);
+        for (;;) {
+            const int64_t g = next.fetch_add(1);
+            if (g >= n_groups || !ok) break;
+            {
+                std::unique_lock<std::mutex> lk(mu);
+                cv.wait(lk, [&] { return g < written + win || !ok; });
+                if (!ok) break;
             }
-        };
-        std::vector<std::thread> th;
-        for (int t = 1; t < nt; ++t) th.emplace_back(work);
-        work();
-        for (auto& t : th) t.join();
-        if (!ok) {
-            rc = fail("deflate failed");
-            break;
+            const size_t slot = (size_t)(g % win);
+            for (auto& t : txt) t.n = 0;
+            const int64_t c0 = g * per_group, c1 = std::min(n_write, c0 + per_group);
+            const auto a = std::chrono::steady_clock::now();
+            format_group(counts, depth, mito_len, cells, c0, c1, names, txt);
+            const auto b = std::chrono::steady_clock::now();
+            bool good = true;
+            for (int i = 0; i < 5; ++i)
+                if (!gzip_member(txt[i].b.data(), txt[i].n, dz, out[slot * 5 + i])) good = false;
+            if (prof) {
+                const auto e = std::chrono::steady_clock::now();
+                ns_fmt += std::chrono::duration_cast<std::chrono::nanoseconds>(b - a).count();
+                ns_dfl += std::chrono::duration_cast<std::chrono::nanoseconds>(e - b).count();
+                for (auto& x : txt) n_txt += (int64_t)x.n;
+            }
+            {
+                std::lock_guard<std::mutex> lk(mu);
+                if (!good) ok = false;
+                ready[slot] = g;
+            }
+            cv.notify_all();
         }
-        for (int64_t g = g0; g < g1 && rc == 0; ++g)
-            for (int i = 0; i < 5; ++i) {
-                const auto& o = out[(size_t)(g - g0) * 5 + i];
-                if (!o.empty() && std::fwrite(o.data(), 1, o.size(), f[i]) != o.size()) rc = fail("write failed");
-            }
+    };
+    std::vector<std::thread> th;
+    for (int t = 0; t < nt; ++t) th.emplace_back(work);
+    int rc = 0;
+    for (int64_t g = 0; g < n_groups; ++g) {
+        const size_t slot = (size_t)(g % win);
+        {
+            std::unique_lock<std::mutex> lk(mu);
+            cv.wait(lk, [&] { return ready[slot] == g || !ok; });
+            if (!ok) break;
+        }
+        for (int i = 0; i < 5 && rc == 0; ++i) {
+            const auto& o = out[slot * 5 + i];
+            if (!o.empty() && std::fwrite(o.data(), 1, o.size(), f[i]) != o.size()) rc = fail("write failed");
+        }
+        {
+            std::lock_guard<std::mutex> lk(mu);
+            if (rc != 0) ok = false;
+            written = g + 1;
+        }
+        cv.notify_all();
+        if (rc != 0) break;
     }
+    for (auto& t : th) t.join();
+    if (rc == 0 && !ok) rc = fail("deflate failed");
     for (int i = 0; i < 5; ++i)
         if (std::fclose(f[i]) != 0 && rc == 0) rc = fail("close failed");
     if (prof)
