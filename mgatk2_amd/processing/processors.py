@@ -187,18 +187,26 @@ class CellProcessor:
                       rb.array((n_cells, L), np.uint16, n_cells * L * 20),
                       rb.array((n_cells, nw), np.uint8, n_cells * L * 22), W)
 
-    def run_stream(self, reader, n_cells: int, batch_reads: int | None = None, rows_target: bool = True) -> EngineResult:
+    def run_stream(self, reader, n_cells: int, batch_reads: int | None = None,
+                   rows_target: bool | None = None) -> EngineResult:
         """The production path, streamed (readers.py:84-93's one pass, overlapped with
         the device): the native decoder fills a ring of pinned batches on a producer
         thread while this thread pushes each finished batch to a streaming engine
         context (MGP_CFG_STREAM: its H2D copies, then the hot path of the position
-        windows it completes, run behind the next batches' decode). With a rows
-        target, each window's 16-bit result rows leave the device as soon as it is
-        piled, into pinned host memory the writers read. Results are those of a
+        windows it completes, run behind the next batches' decode); the 16-bit result
+        rows are fetched after the run. With a rows target (rows_target=True or
+        MGP_ROWS_TARGET=1), each window's rows leave the device as soon as it is piled,
+        into pinned host memory the writers read. Results are those of a
         resident run of the same reads (reads a segment cannot serve rerun it).
         Several devices: see :meth:`_run_stream_sharded`."""
         if len(self.devices) > 1:
-            return self._run_stream_sharded(reader, n_cells, batch_reads, rows_target)
+            return self._run_stream_sharded(reader, n_cells, batch_reads, rows_target is not False)
+        if rows_target is None:
+            # the rows fetched after the run by default: pinning a rows target during the
+            # decode (GBs at ~0.25 s per GB, on a thread) slowed the decode more than the
+            # fetch costs (C4 txt end to end 5.38-5.43 s with the target, 4.72-5.26 s
+            # without, fetch 0.16 s; profiles/r05/e2e_rows_*.log); MGP_ROWS_TARGET=1 keeps it
+            rows_target = os.environ.get("MGP_ROWS_TARGET", "0") == "1"
         t0 = time.perf_counter()
         bam, st, n_hint, free, full, producer, times = self._stream_producer(reader, n_cells, batch_reads)
         try:
