@@ -199,14 +199,14 @@ class CellProcessor:
         into pinned host memory the writers read. Results are those of a
         resident run of the same reads (reads a segment cannot serve rerun it).
         Several devices: see :meth:`_run_stream_sharded`."""
-        if len(self.devices) > 1:
-            return self._run_stream_sharded(reader, n_cells, batch_reads, rows_target is not False)
         if rows_target is None:
             # the rows fetched after the run by default: pinning a rows target during the
             # decode (GBs at ~0.25 s per GB, on a thread) slowed the decode more than the
             # fetch costs (C4 txt end to end 5.38-5.43 s with the target, 4.72-5.26 s
             # without, fetch 0.16 s; profiles/r05/e2e_rows_*.log); MGP_ROWS_TARGET=1 keeps it
             rows_target = os.environ.get("MGP_ROWS_TARGET", "0") == "1"
+        if len(self.devices) > 1:
+            return self._run_stream_sharded(reader, n_cells, batch_reads, rows_target)
         t0 = time.perf_counter()
         bam, st, n_hint, free, full, producer, times = self._stream_producer(reader, n_cells, batch_reads)
         try:
@@ -431,17 +431,27 @@ class CellProcessor:
             rows = rows_box.get("rows")
             t2 = time.perf_counter()
             L = self.config.mito_length
-            wide = rows is not None and bool(rows.wide.any())
-            res = EngineResult.alloc(n_cells, L, dense=rows is None or wide)
+            # without a rows target: every device's exact 16-bit rows fetched into its cell
+            # range of one host array (the u32 arrays only when a window was drained)
+            src = rows
+            if rows is None and parts:
+                nw, W = engines[parts[0][0]].windows()
+                src = Rows16(np.empty((n_cells, L, 8), np.uint16), np.empty((n_cells, L, 2), np.uint16),
+                             np.empty((n_cells, L), np.uint16), np.zeros((n_cells, nw), np.uint8), W)
+                for d, lo, hi in parts:
+                    engines[d].fetch_rows16(lo=0, hi=hi - lo, out=Rows16(src.counts[lo:hi], src.tn5[lo:hi],
+                                                                        src.depth[lo:hi], src.wide[lo:hi], W))
+            wide = src is None or bool(src.wide.any())
+            res = EngineResult.alloc(n_cells, L, dense=wide)
             st_sum = {k: 0 for k in ("filtered_reads", "n_barcodes", "duplicate_reads_with_length",
                                      "duplicate_reads_position_only", "cells_passed")}
             max_span, err = 0, 0
             for d, lo, hi in parts:
-                r = engines[d].fetch(dense=rows is None or wide)
+                r = engines[d].fetch(dense=wide)
                 for k in ("n_reads", "any_paired", "passed", "covered", "depth_sum", "depth_max", "median_lo",
                           "median_hi", "first_read"):
                     getattr(res, k)[lo:hi] = getattr(r, k)
-                if rows is None or wide:
+                if wide:
                     for k in ("counts", "tn5", "depth"):
                         getattr(res, k)[lo:hi] = getattr(r, k)
                 res.ref_tally += r.ref_tally
@@ -449,8 +459,8 @@ class CellProcessor:
                     st_sum[k] += int(r.stats[k])
                 max_span = max(max_span, int(r.stats["max_span"]))
                 err |= int(r.stats["error_bits"])
-            if rows is not None and not wide:
-                res.counts, res.tn5, res.depth = rows.counts, rows.tn5, rows.depth
+            if not wide:
+                res.counts, res.tn5, res.depth = src.counts, src.tn5, src.depth
             res.stats = {"total_reads": int(st.records), **st_sum, "max_span": max_span, "error_bits": err}
             t3 = time.perf_counter()
             self.last_stats = engines[parts[0][0]].kernel_times() if parts else {}

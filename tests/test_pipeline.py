@@ -629,6 +629,14 @@ class _OracleEngine:
     def fetch(self, dense=True):
         return self.res
 
+    def fetch_rows16(self, lo=0, hi=None, out=None):
+        hi = self.cfg.n_cells if hi is None else hi
+        out.counts[...] = np.minimum(self.res.counts[lo:hi], 65535)
+        out.tn5[...] = np.minimum(self.res.tn5[lo:hi], 65535)
+        out.depth[...] = np.minimum(self.res.depth[lo:hi], 65535)
+        out.wide[...] = 0
+        return out
+
     def kernel_times(self, last_runs=1):
         return {}
 
@@ -636,13 +644,16 @@ class _OracleEngine:
         pass
 
 
+@pytest.mark.parametrize("rows", ["0", "1"])
 @pytest.mark.parametrize("n_dev", [2, 3, 7])
-def test_stream_sharded_routing_host(n_dev, tmp_path, oracle_lib, monkeypatch):
+def test_stream_sharded_routing_host(n_dev, rows, tmp_path, oracle_lib, monkeypatch):
     """The streamed multi-device path's host side (CellProcessor._run_stream_sharded:
     every batch pushed whole to every device, each keeping its read-balanced cell
-    range (mgp_set_cell_range, restated in the stand-in), per-device rows targets as
-    views of one array, first reads, tallies and stats merged), with the oracle
+    range (mgp_set_cell_range, restated in the stand-in), the rows fetched per device
+    into its range of one array (or, MGP_ROWS_TARGET=1, per-device rows targets as
+    views of one array), first reads, tallies and stats merged), with the oracle
     standing in for each device's engine: every output equals the reference's."""
+    monkeypatch.setenv("MGP_ROWS_TARGET", rows)
     from mgatk2_amd.engine import PinnedBuffer  # noqa: F401 - (host memory in this stand-in)
     from mgatk2_amd.processing import processors
     from mgatk2_amd.pipeline import run_pipeline
