@@ -2840,6 +2840,9 @@ constexpr int64_t kPairReads = 1 << 18;  // reads of a pairing workgroup's range
 #define MGP_PAIR_SPLIT 16
 #endif
 constexpr int kPairSplit = MGP_PAIR_SPLIT;
+#ifndef MGP_PAIR_NT
+#define MGP_PAIR_NT 0  // the record copy's loads and stores non-temporal (A/B)
+#endif
 constexpr int kPairMaxKeys = 32768;      // cells + 1 whose counters fit a workgroup's LDS
 
 __device__ __forceinline__ int pair_key(int32_t c, uint16_t f, int nc) {
@@ -2900,7 +2903,14 @@ __global__ void __launch_bounds__(kPairBlock) k_pair_place(const uint4* __restri
         const uint32_t r = rank[i];
         const uint64_t line = (uint64_t)w0 + lbase[pair_key(bc[i], flag[i], nc)] + (r >> 1);
         const uint64_t off = pay0 + line * 128u + (uint64_t)(r & 1u) * 64u;
+#if MGP_PAIR_NT
+        // (A/B: the copy's lines streamed past the caches, the pileup's data left in them)
+        typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+        const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(src) + t);
+        __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(payload + off) + (t & 3));
+#else
         reinterpret_cast<uint4*>(payload + off)[t & 3] = src[t];
+#endif
         if ((t & 3) == 0) roff[i] = off;
     }
 }
