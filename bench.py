@@ -47,6 +47,7 @@ import subprocess
 import sys
 import time
 from pathlib import Path
+from types import SimpleNamespace
 
 import numpy as np
 
@@ -563,21 +564,33 @@ def kernel_rooflines(kt: dict, n: int, nc: int, stats: dict, cfg, layout: str) -
     return out
 
 
-def sample_check(eng, cfg, res, args, seed, cdf, ref, cell0: int, device: int) -> dict:
+def sample_check(eng, cfg, res, args, seed, cdf, ref, cell0: int, device: int, delivered=None) -> dict:
     """3 samples of 8 whole cells of the timed run (first, middle, last cells of the
     rank) bit for bit against the oracle on exactly their reads, plus the run
     statistics' consistency. Cells are independent, so a cell's rows depend only
     on its own reads. The oracle reads the quality-carrying full 128-byte records of
     those reads (regenerated as a cell shard of the same seed): with 32-byte records
     the per-base filter (pileup.py:67-88) was resolved by the producer, and this
-    checks that too."""
+    checks that too. delivered (a StreamSet): the rows compared are the ones the
+    timed step left in pinned host memory (the bytes that crossed the link) and the
+    per-cell statistics are the step's own `res`; otherwise (results left in HBM)
+    they are fetched from the device."""
     from mgatk2_amd.engine import Engine, EngineConfig
     from oracle.oracle import oracle_run
 
     t0 = time.perf_counter()
     nc = cfg.n_cells
     ranges = sorted({(0, min(8, nc)), (nc // 2, min(nc, nc // 2 + 8)), (max(0, nc - 8), nc)})
-    got = {r: eng.fetch_cells(*r) for r in ranges}
+    if delivered is not None:
+        per_cell = ("n_reads", "any_paired", "passed", "covered", "depth_sum", "depth_max", "median_lo", "median_hi")
+        got = {}
+        for lo, hi in ranges:
+            d = delivered.cells(lo, hi)
+            for k in per_cell:
+                d[k] = getattr(res, k)[lo:hi]
+            got[(lo, hi)] = SimpleNamespace(**d)
+    else:
+        got = {r: eng.fetch_cells(*r) for r in ranges}
     ok = True
     bad = []
     keys = ("counts", "tn5", "depth", "n_reads", "any_paired", "passed", "covered", "depth_sum", "depth_max",
@@ -598,10 +611,123 @@ def sample_check(eng, cfg, res, args, seed, cdf, ref, cell0: int, device: int) -
                   and st["n_barcodes"] == int((res.n_reads > 0).sum()) and st["error_bits"] == 0)
     return {"bit_exact": bool(ok and consistent), "cells": [list(r) for r in ranges], "mismatches": bad,
             "stats_consistent": bool(consistent), "oracle_input": "full 128-byte records (raw qualities) of the "
-            "sampled cells' reads", "seconds": round(time.perf_counter() - t0, 2)}
+            "sampled cells' reads", "checked": ("the timed step's pinned host rows and per-cell statistics"
+                                                if delivered is not None else "rows fetched from the device"),
+            "wide_cells": None if delivered is None else len(delivered.exact),
+            "seconds": round(time.perf_counter() - t0, 2)}
 
 
-def stream_leg(ctx: Ctx, layout: str, batch_list: list[int], timed: bool) -> dict:
+class StreamSet:
+    """The producer's side of the streamed step (shared with the full-size GPU test
+    of this exact path, tests/test_gpu_stream.py): the engine's resident reads copied
+    into pinned host memory as dense records in BAM order (a batch is a contiguous
+    payload range), with 16-bit barcode and |tlen| columns (mgp_push_batch16, ABI 5)
+    when every read allows, and the pinned 16-bit count rows the engine writes as its
+    windows complete (mgp_set_rows16_target)."""
+
+    def __init__(self, eng, cfg, layout: str, columns16: bool = True):
+        from mgatk2_amd.engine import PinnedBuffer, Rows16
+
+        self.eng, self.cfg, self.layout = eng, cfg, layout
+        self.rb = 32 if layout == "pack32" else 64  # dense records in BAM order
+        n, pay = eng.resident()
+        self.n, self.pay = n, pay
+        # the producer's columns: bc, tlen, flag, mapq. No rec_off (dense records in BAM
+        # order) and no span (taken from the records' CIGARs on the device): ABI v3.1; no
+        # start (taken from the records, which all hold it): ABI 4
+        cols = ("bc", "tlen", "flag", "mapq", "payload")
+        # 16-bit barcode and |tlen| columns when every read allows: 7 bytes of columns
+        # per read over the link instead of 11
+        wide = None
+        if columns16 and cfg.n_cells <= 0xFFFF:
+            wide = eng.download_inputs(columns=("bc", "tlen"))
+            if not np.abs(wide.tlen.astype(np.int64)).max(initial=0) < 0xFFFF:
+                wide = None
+        self.narrow = wide is not None
+        self.col_bytes = n * ((2 + 2) if self.narrow else (4 + 4)) + n * (2 + 1)
+        self.hbuf = PinnedBuffer(self.col_bytes + pay + 4096)
+        off = [0]
+
+        def alloc(m, dt):
+            a = self.hbuf.array(m, dt, off[0])
+            off[0] = (off[0] + m * np.dtype(dt).itemsize + 63) & ~63
+            return a
+
+        if self.narrow:  # (bc and tlen through host memory, then their 16-bit forms into the pinned batches)
+            host = eng.download_inputs(columns=("flag", "mapq", "payload"), alloc=alloc)
+            host.bc, host.tlen = alloc(n, np.uint16), alloc(n, np.uint16)
+            np.copyto(host.bc, np.where(wide.bc < 0, 0xFFFF, wide.bc).astype(np.uint16))
+            np.copyto(host.tlen, np.abs(wide.tlen).astype(np.uint16))
+            del wide
+        else:
+            host = eng.download_inputs(columns=cols, alloc=alloc)  # the producer's batches: pinned, BAM order
+        assert np.all(eng.download_inputs(columns=("rec_off",)).rec_off == self.rb * np.arange(n, dtype=np.uint64))
+        self.host = host
+        L, nc = cfg.mito_len, cfg.n_cells
+        nw, W = eng.windows()
+        self.rbuf = PinnedBuffer(nc * L * 22 + nc * nw + 4096)
+        rbuf = self.rbuf
+        self.rows = Rows16(rbuf.array((nc, L, 8), np.uint16, 0), rbuf.array((nc, L, 2), np.uint16, nc * L * 16),
+                           rbuf.array((nc, L), np.uint16, nc * L * 20), rbuf.array((nc, nw), np.uint8, nc * L * 22), W)
+        # the rows leave the device as the windows complete, beside the later batches' H2D
+        try:
+            eng.set_rows16_target(self.rows)
+            self.rows_target = True
+        except Exception as e:  # (pinned memory the device cannot map: copy the rows after the run)
+            print(f"[bench] rows target unavailable ({e}); rows fetched after the run", file=sys.stderr)
+            self.rows_target = False
+        self.h2d = self.col_bytes + pay
+        self.d2h = nc * L * 22 + nc * nw + nc * 34 + L * 4 * 8  # rows, wide flags, per-cell arrays, tallies
+        self.exact = {}  # cell -> its exact u32 rows (EngineResult of one cell) when a window of it is wide
+
+    def auto_batch(self, b) -> int:
+        """'auto': about one position window of reads per batch (the windows a push
+        completes run while the next batch is copied)."""
+        return max(1_000_000, int(round(self.n / 12.5 / 1e6)) * 1_000_000) if b == "auto" else int(b)
+
+    def batches(self, bs: int) -> list:
+        """Batches of bs reads: their columns and their slice of the dense payload."""
+        from mgatk2_amd.synth import ReadSoA
+
+        h, rb, n = self.host, self.rb, self.n
+        return [ReadSoA(None, h.bc[a:b], h.tlen[a:b], h.flag[a:b], h.mapq[a:b], None, None, h.payload[rb * a:rb * b])
+                for a, b in ((a, min(n, a + bs)) for a in range(0, n, bs))]
+
+    def step(self, batches, stream: bool = True):
+        """One pass: reset -> push every batch -> mgp_run -> the count rows and per-cell
+        statistics in host memory. A cell with a drained window (more than 65535
+        elements: its pinned 16-bit rows saturate) gets its exact u32 rows fetched here,
+        inside the step (self.exact)."""
+        eng = self.eng
+        eng.set_streaming(stream)
+        eng.reset()
+        for bt in batches:
+            eng.push(bt)
+        eng.run()
+        if not self.rows_target:
+            eng.fetch_rows16(0, self.cfg.n_cells, out=self.rows)
+        res = eng.fetch(dense=False)  # (waits for the rows' copies too)
+        self.exact = {}
+        if self.rows.wide.any():
+            for c in self.rows.wide_cells():
+                self.exact[int(c)] = eng.fetch_cells(int(c), int(c) + 1)
+        return res
+
+    def cells(self, lo: int, hi: int) -> dict:
+        """Cells [lo, hi) as the step delivered them to host memory: the pinned 16-bit
+        rows widened to u32 (exact: no wide window), or the exact rows fetched for a
+        cell with a wide window."""
+        r = self.rows
+        out = {"counts": r.counts[lo:hi].astype(np.uint32), "tn5": r.tn5[lo:hi].astype(np.uint32),
+               "depth": r.depth[lo:hi].astype(np.uint32)}
+        for c, e in self.exact.items():
+            if lo <= c < hi:
+                for k in out:
+                    out[k][c - lo] = getattr(e, k)[0]
+        return out
+
+
+def stream_leg(ctx: Ctx, layout: str, batch_list: list, timed: bool) -> dict:
     """SURVEY.md §8(d)'s engine metric: the rank's reads in pinned host SoA batches
     (dense records in BAM order, as a streaming producer emits them: a batch is a
     contiguous payload range) -> pushed (H2D on the copy stream; with streaming on,
@@ -610,101 +736,39 @@ def stream_leg(ctx: Ctx, layout: str, batch_list: list[int], timed: bool) -> dic
     pinned target as windows complete) and the per-cell statistics in pinned host
     memory. timed: the bench's step (W warmup passes, K timed passes bracketed by
     barrier + device sync, max over ranks), with the pileup's HIP events (every
-    segment's launch) for the roofline and the bit-exact sample check; otherwise the
-    best of --pcie-steps passes per batch size, streamed and not."""
-    from mgatk2_amd.engine import Engine, PinnedBuffer, Rows16
-    from mgatk2_amd.synth import ReadSoA
+    segment's launch) for the roofline and the bit-exact sample check of the rows the
+    timed step left in host memory; otherwise the best of --pcie-steps passes per
+    batch size, streamed and not."""
+    from mgatk2_amd.engine import Engine
 
     args, cfg = ctx.args, ctx.cfg
     eng = Engine(cfg, device=ctx.device)
     p32 = cfg.min_baseq if layout == "pack32" else None
-    rb = 32 if p32 is not None else 64  # dense records in BAM order
     t0 = time.time()
     eng.synth(ctx.seed, args.reads, ctx.cdf, ctx.ref, read_len=args.read_len, rec_align=64, pack=True, pack32=p32,
               **ctx.shard)
-    n, pay = eng.resident()
-    # the producer's columns: bc, tlen, flag, mapq. No rec_off (dense records in BAM
-    # order) and no span (taken from the records' CIGARs on the device): ABI v3.1; no
-    # start (taken from the records, which all hold it): ABI 4
-    cols = ("bc", "tlen", "flag", "mapq", "payload")
-    # 16-bit barcode and |tlen| columns (mgp_push_batch16, ABI 5) when every read allows:
-    # 7 bytes of columns per read over the link instead of 11
-    wide = None
-    if args.columns == "16" and cfg.n_cells <= 0xFFFF:
-        wide = eng.download_inputs(columns=("bc", "tlen"))
-        if not np.abs(wide.tlen.astype(np.int64)).max(initial=0) < 0xFFFF:
-            wide = None
-    narrow = wide is not None
-    col_bytes = n * ((2 + 2) if narrow else (4 + 4)) + n * (2 + 1)
-    hbuf = PinnedBuffer(col_bytes + pay + 4096)
-    off = [0]
-
-    def alloc(m, dt):
-        a = hbuf.array(m, dt, off[0])
-        off[0] = (off[0] + m * np.dtype(dt).itemsize + 63) & ~63
-        return a
-
-    if narrow:  # (bc and tlen through host memory, then their 16-bit forms into the pinned batches)
-        host = eng.download_inputs(columns=("flag", "mapq", "payload"), alloc=alloc)
-        host.bc, host.tlen = alloc(n, np.uint16), alloc(n, np.uint16)
-        np.copyto(host.bc, np.where(wide.bc < 0, 0xFFFF, wide.bc).astype(np.uint16))
-        np.copyto(host.tlen, np.abs(wide.tlen).astype(np.uint16))
-        del wide
-    else:
-        host = eng.download_inputs(columns=cols, alloc=alloc)  # the producer's batches: pinned, BAM order
-    assert np.all(eng.download_inputs(columns=("rec_off",)).rec_off == rb * np.arange(n, dtype=np.uint64))
+    ss = StreamSet(eng, cfg, layout, columns16=args.columns == "16")
+    n, rb, narrow, rows_target = ss.n, ss.rb, ss.narrow, ss.rows_target
     L, nc = cfg.mito_len, cfg.n_cells
-    nw, W = eng.windows()
-    rbuf = PinnedBuffer(nc * L * 22 + nc * nw + 4096)
-    rows = Rows16(rbuf.array((nc, L, 8), np.uint16, 0), rbuf.array((nc, L, 2), np.uint16, nc * L * 16),
-                  rbuf.array((nc, L), np.uint16, nc * L * 20), rbuf.array((nc, nw), np.uint8, nc * L * 22), W)
-    print(f"[bench] rank {ctx.rank}: stream leg {layout}: {n:,} reads ({(col_bytes + pay) / 1e9:.2f} GB pinned) "
+    print(f"[bench] rank {ctx.rank}: stream leg {layout}: {n:,} reads ({ss.h2d / 1e9:.2f} GB pinned) "
           f"ready in {time.time() - t0:.1f}s", file=sys.stderr, flush=True)
     if ctx.comm is not None:
         ctx.comm(eng)  # every run all-reduces its tallies
-    # the rows leave the device as the windows complete, beside the later batches' H2D
-    try:
-        eng.set_rows16_target(rows)
-        rows_target = True
-    except Exception as e:  # (pinned memory the device cannot map: copy the rows after the run)
-        print(f"[bench] rows target unavailable ({e}); rows fetched after the run", file=sys.stderr)
-        rows_target = False
     eng.set_stage_timing(False)  # HIP events around the pileup launches only
-
-    # 'auto': about one position window of reads per batch (the windows a push completes
-    # run while the next batch is copied)
-    batch_list = [max(1_000_000, int(round(n / 12.5 / 1e6)) * 1_000_000) if b == "auto" else int(b)
-                  for b in batch_list]
-
-    def batches_for(bs):
-        """Batches of bs reads: their columns and their slice of the dense payload."""
-        return [ReadSoA(None, host.bc[a:b], host.tlen[a:b], host.flag[a:b], host.mapq[a:b], None, None,
-                        host.payload[rb * a:rb * b]) for a, b in ((a, min(n, a + bs)) for a in range(0, n, bs))]
-
-    def one(batches, stream):
-        eng.set_streaming(stream)
-        eng.reset()
-        for bt in batches:
-            eng.push(bt)
-        eng.run()
-        if not rows_target:
-            eng.fetch_rows16(0, nc, out=rows)
-        return eng.fetch(dense=False)  # (waits for the rows' copies too)
-
-    h2d = col_bytes + pay
-    d2h = nc * L * 22 + nc * nw + nc * 34 + L * 4 * 8  # rows, wide flags, per-cell arrays, tallies
+    batch_list = [ss.auto_batch(b) for b in batch_list]
+    h2d, d2h = ss.h2d, ss.d2h
     if not timed:
         legs = []
         for bs in batch_list:
-            batches = batches_for(bs)
-            one(batches, True)  # warmup (allocations)
+            batches = ss.batches(bs)
+            ss.step(batches, True)  # warmup (allocations)
             for stream in (True, False):
                 ts = []
                 seg0 = eng.stream_info()[0]
                 for _ in range(args.pcie_steps):
                     ctx.barrier()
                     t1 = time.perf_counter()
-                    r = one(batches, stream)
+                    r = ss.step(batches, stream)
                     ts.append(time.perf_counter() - t1)
                 segs = (eng.stream_info()[0] - seg0) // max(1, args.pcie_steps)
                 dt_max = ctx.reduce(min(ts), "max")
@@ -719,14 +783,14 @@ def stream_leg(ctx: Ctx, layout: str, batch_list: list[int], timed: bool) -> dic
                 "stats_total_reads_rank0": r.stats["total_reads"]}
 
     bs = batch_list[0]
-    batches = batches_for(bs)
+    batches = ss.batches(bs)
     for _ in range(max(1, args.warmup)):
-        one(batches, True)
+        ss.step(batches, True)
     seg0 = eng.stream_info()[0]
     ctx.barrier()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        res = one(batches, True)
+        res = ss.step(batches, True)
     ctx.barrier()
     dt_rank = time.perf_counter() - t0
     dt = ctx.reduce(dt_rank, "max")
@@ -742,7 +806,8 @@ def stream_leg(ctx: Ctx, layout: str, batch_list: list[int], timed: bool) -> dic
     step_s = dt_rank / args.steps
     check = None
     if ctx.rank == 0 and not args.no_check:
-        check = sample_check(eng, cfg, res, args, ctx.seed, ctx.cdf, ctx.ref, ctx.cell0, ctx.device)
+        check = sample_check(eng, cfg, res, args, ctx.seed, ctx.cdf, ctx.ref, ctx.cell0, ctx.device, delivered=ss)
+    wide_cells = len(ss.exact)
     eng.close()
     return {
         "record_layout": layout,
@@ -754,8 +819,8 @@ def stream_leg(ctx: Ctx, layout: str, batch_list: list[int], timed: bool) -> dic
                     else "i32 bc, i32 tlen, u16 flag, u8 mapq: 11 B per read (mgp_push_batch)"),
         "timed_region": "K passes of: reset -> push every pinned host batch (H2D on the copy stream; each push "
                         "queues the hot path of the windows its reads complete) -> mgp_run -> every 16-bit count row "
-                        "(written into pinned host memory as its windows complete) and the per-cell statistics on "
-                        "the host",
+                        "(written into pinned host memory as its windows complete; the exact u32 rows of any cell "
+                        "with a drained window fetched) and the per-cell statistics on the host",
         "value": ctx.reduce(float(n), "sum") * args.steps / dt,
         "ms_per_step": dt / args.steps * 1e3,
         "rank0_step_ms": step_s * 1e3,
@@ -768,6 +833,7 @@ def stream_leg(ctx: Ctx, layout: str, batch_list: list[int], timed: bool) -> dic
         "h2d_bytes_rank0": h2d,
         "d2h_bytes_rank0": d2h,
         "rows_target": rows_target,
+        "wide_cells": wide_cells,
         "link": {"bound": "pcie", "h2d_GBps": round(h2d / step_s / 1e9, 2), "d2h_GBps": round(d2h / step_s / 1e9, 2),
                  "peak_GBps_per_direction": PCIE_PEAK_GBS, "h2d_frac": round(h2d / step_s / 1e9 / PCIE_PEAK_GBS, 3),
                  "what": "H2D bytes of the step (columns + records) over the step time, rank 0; PCIe Gen5 x16 spec "

@@ -531,7 +531,9 @@ int  mgp_copy_wait(mgp_ctx *ctx);
 int  mgp_set_cell_range(mgp_ctx *ctx, int32_t cell_lo, int32_t cell_hi);
 /* Append a batch with 16-bit barcode and |tlen| columns (mgp_batch16; the device widens
  * them behind the copy). Same semantics and errors as mgp_push_batch for a batch without
- * rec_off, start and span columns; MGP_E_INVALID when n_cells > 65535. Replaces the
+ * rec_off, start and span columns; MGP_E_INVALID when n_cells > 65535, or with a cell
+ * range (mgp_set_cell_range: the columns then hold whole-whitelist indices) when
+ * cell_hi > 65535 (index 0xFFFF is the no-barcode sentinel). Replaces the
  * reference's per-read SimpleRead fields (readers.py:153-163) at the host link. */
 int  mgp_push_batch16(mgp_ctx *ctx, const mgp_batch16 *batch);
 /* Streaming on (1) or off (0) for the next pushes (initially MGP_CFG_STREAM). */

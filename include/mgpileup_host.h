@@ -208,6 +208,51 @@ int mgp_gather_records(const uint8_t *payload, const uint64_t *rec_off, const ui
 int64_t mgp_split_by_range(const int32_t *bc, int64_t n, const int64_t *bounds, int32_t nd, int64_t *counts,
                            int64_t *idx);
 
+/* The 16-bit columns of a decoded batch (mgp_batch16, include/mgpileup.h): bc16 =
+ * bc (0xFFFF for < 0), tlen16 = |tlen|. Returns bit 0 set when the records are dense
+ * at one stride (payload_bytes = n x stride, stride a multiple of 16, and every
+ * rec_off[i] = stride x i when rec_off is given: the batch may go without rec_off),
+ * bit 1 set when every key fits (barcode index and |tlen| below 0xFFFF, n_cells <=
+ * 0xFFFF); both (3): the batch may go as an mgp_batch16 with bc16 / tlen16. -1 on bad
+ * arguments. Replaces nothing in the reference: the
+ * per-read fields of readers.py:153-163, in the form the host link carries. */
+int mgp_batch_columns16(int64_t n, const int32_t *bc, const int32_t *tlen, const uint64_t *rec_off,
+                        int64_t payload_bytes, int32_t n_cells, uint16_t *bc16, uint16_t *tlen16, int n_threads);
+
+/* One device's batch of a routed stream (mgp_route_batch): caller-owned arrays of
+ * cap_reads entries and cap_payload bytes; the router fills n_reads, payload_bytes
+ * (plus 256 zeroed bytes after it) and narrow: 1 = bc16 / tlen16 (local cell index,
+ * |tlen|) with the records dense at one stride (mgp_push_batch16), 0 = bc32 / tlen32 /
+ * rec_off (mgp_push_batch). flag, mapq and payload in both forms. */
+typedef struct mgp_route_part {
+    int64_t   cap_reads, cap_payload;
+    uint16_t *bc16, *tlen16;
+    int32_t  *bc32, *tlen32;
+    uint16_t *flag;
+    uint8_t  *mapq;
+    uint64_t *rec_off;
+    uint8_t  *payload;
+    int64_t   n_reads, payload_bytes;   /* out */
+    int32_t   narrow, pad;              /* out */
+} mgp_route_part;
+
+/* The multi-device stream's router (the reference's split of the
+ * barcodes over its pool, processors.py:112-144, becomes a split over devices): every
+ * read of the batch (records at rec_off[i], or dense at payload_bytes / n x i when
+ * rec_off is NULL) whose barcode index lies in [bounds[d], bounds[d + 1]) and whose flag
+ * passes readers.py:96 (not unmapped / secondary / supplementary) goes to parts[d], in
+ * batch order, its index rebased to bounds[d]; the other reads go nowhere (they count
+ * only toward total_reads). first_seen (may be NULL; bounds[n_parts] - bounds[0]
+ * entries, 0xFFFFFFFF = not yet): lowered to first_index + i for each routed read i, so
+ * over a stream it ends as each cell's first read in BAM order (reads_by_barcode's
+ * insertion order, readers.py:104-163). Returns 0, 1 when a part's arrays are too small
+ * (nothing written: route fewer reads at once), -1 on bad arguments or a record outside
+ * the payload. */
+int mgp_route_batch(int64_t n, const int32_t *bc, const int32_t *tlen, const uint16_t *flag, const uint8_t *mapq,
+                    const uint64_t *rec_off, const uint8_t *payload, int64_t payload_bytes, int32_t n_parts,
+                    const int32_t *bounds, int64_t first_index, uint32_t *first_seen, mgp_route_part *parts,
+                    int n_threads);
+
 /* 32-byte records (MGP_FLAG_PACK32, include/mgpileup.h) from a batch's full-layout
  * records, for one run's (min_baseq, min_dist_from_end): out32[i] (32 bytes, dense
  * in batch order) and out_flag[i] = flag[i] | MGP_FLAG_PACK32 for every full record

@@ -44,18 +44,67 @@ class mgp_bam_batch(C.Structure):
     ]
 
 
+class mgp_route_part(C.Structure):
+    _fields_ = [
+        ("cap_reads", C.c_int64), ("cap_payload", C.c_int64),
+        ("bc16", C.c_void_p), ("tlen16", C.c_void_p), ("bc32", C.c_void_p), ("tlen32", C.c_void_p),
+        ("flag", C.c_void_p), ("mapq", C.c_void_p), ("rec_off", C.c_void_p), ("payload", C.c_void_p),
+        ("n_reads", C.c_int64), ("payload_bytes", C.c_int64), ("narrow", C.c_int32), ("pad", C.c_int32),
+    ]
+
+
 _hlib = None
 
 
-def host_threads() -> int:
-    """Host worker threads: MGP_HOST_THREADS, else OMP_NUM_THREADS, else min(cpus, 16)."""
-    import os
+def cgroup_cpu_quota() -> int | None:
+    """CPUs the process's cgroup may use (cgroup v2 cpu.max, else v1
+    cpu.cfs_quota_us / cpu.cfs_period_us), rounded up; None when unlimited or unknown."""
+    import math
 
-    for var in ("MGP_HOST_THREADS", "OMP_NUM_THREADS"):
-        v = os.environ.get(var)
-        if v and v.isdigit() and int(v) > 0:
-            return int(v)
-    return max(1, min(os.cpu_count() or 1, 16))
+    try:
+        rel = "/"
+        for line in Path("/proc/self/cgroup").read_text().splitlines():
+            parts = line.split(":", 2)
+            if len(parts) == 3 and (parts[0] == "0" or "cpu" in parts[1].split(",")):
+                rel = parts[2] or "/"
+                if parts[0] == "0":
+                    break
+        for base in (Path("/sys/fs/cgroup") / rel.lstrip("/"), Path("/sys/fs/cgroup")):
+            f = base / "cpu.max"
+            if f.exists():
+                fields = f.read_text().split()  # "<quota|max> <period>"
+                if len(fields) >= 2 and fields[0] != "max":
+                    return max(1, math.ceil(int(fields[0]) / int(fields[1])))
+                return None
+        for base in (Path("/sys/fs/cgroup/cpu") / rel.lstrip("/"), Path("/sys/fs/cgroup/cpu"),
+                     Path("/sys/fs/cgroup/cpu,cpuacct")):
+            fq, fp = base / "cpu.cfs_quota_us", base / "cpu.cfs_period_us"
+            if fq.exists() and fp.exists():
+                q, p = int(fq.read_text()), int(fp.read_text())
+                return max(1, math.ceil(q / p)) if q > 0 and p > 0 else None
+    except (OSError, ValueError):
+        return None
+    return None
+
+
+def host_threads() -> int:
+    """Host worker threads: MGP_HOST_THREADS when set; otherwise the CPUs this process
+    may run on (its affinity mask) bounded by its cgroup's CPU quota and by
+    OMP_NUM_THREADS when that is set (the machine's standard per-process knob)."""
+    v = os.environ.get("MGP_HOST_THREADS")
+    if v and v.isdigit() and int(v) > 0:
+        return int(v)
+    try:
+        n = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        n = os.cpu_count() or 1
+    q = cgroup_cpu_quota()
+    if q is not None:
+        n = min(n, q)
+    v = os.environ.get("OMP_NUM_THREADS")
+    if v and v.isdigit() and int(v) > 0:
+        n = min(n, int(v))
+    return max(1, n)
 
 
 def host_library() -> C.CDLL:
@@ -126,6 +175,11 @@ def host_library() -> C.CDLL:
         lib.mgp_bam_stream_close.restype = None
         lib.mgp_host_buf_free.argtypes = [vp]
         lib.mgp_host_buf_free.restype = None
+        lib.mgp_batch_columns16.argtypes = [C.c_int64, vp, vp, vp, C.c_int64, C.c_int32, vp, vp, C.c_int]
+        lib.mgp_batch_columns16.restype = C.c_int
+        lib.mgp_route_batch.argtypes = [C.c_int64, vp, vp, vp, vp, vp, vp, C.c_int64, C.c_int32, vp, C.c_int64, vp,
+                                        C.POINTER(mgp_route_part), C.c_int]
+        lib.mgp_route_batch.restype = C.c_int
         _hlib = lib
     return _hlib
 
@@ -406,6 +460,88 @@ class BamStream:
             self.close()
         except Exception:
             pass
+
+
+def batch_columns16(soa: ReadSoA, n_cells: int, bc16: np.ndarray, tlen16: np.ndarray, n_threads: int = 0,
+                    dense_only: bool = False) -> int:
+    """mgp_batch_columns16: the 16-bit barcode and |tlen| columns of a decoded batch into
+    bc16 / tlen16 (room for soa.n). Returns bit 0 = records dense at one stride (every
+    offset checked), bit 1 = every key fits 16 bits; 3 = the batch may go as an
+    mgp_batch16 (mgp_push_batch16)."""
+    n = soa.n
+    if bc16.shape[0] < n or tlen16.shape[0] < n or bc16.dtype != np.uint16 or tlen16.dtype != np.uint16:
+        raise ValueError("bc16 / tlen16: uint16 arrays of at least n entries")
+    ro = soa.rec_off
+    if ro is not None and ro.shape[0] != n:
+        ro = None if ro.shape[0] == 0 else ro
+    rc = host_library().mgp_batch_columns16(
+        n, soa.bc.ctypes.data, soa.tlen.ctypes.data, None if ro is None else ro.ctypes.data,
+        int(soa.payload.shape[0]), int(n_cells), bc16.ctypes.data, tlen16.ctypes.data, int(n_threads or host_threads()))
+    if rc < 0:
+        raise ValueError(_err())
+    return int(rc)
+
+
+class RoutePart:
+    """One device's batch arrays for :func:`route_batch` (pinned views via alloc(m, dtype)
+    make its H2D copies async)."""
+
+    def __init__(self, cap_reads: int, cap_payload: int, alloc=None):
+        alloc = alloc or (lambda m, dt: np.empty(m, dt))
+        self.cap_reads, self.cap_payload = int(cap_reads), int(cap_payload)
+        m = self.cap_reads
+        self.bc32, self.tlen32 = alloc(m, np.int32), alloc(m, np.int32)
+        self.bc16, self.tlen16 = alloc(m, np.uint16), alloc(m, np.uint16)
+        self.flag, self.mapq = alloc(m, np.uint16), alloc(m, np.uint8)
+        self.rec_off = alloc(m, np.uint64)
+        self.payload = alloc(self.cap_payload, np.uint8)
+        self.n, self.payload_bytes, self.narrow = 0, 0, False
+
+    @staticmethod
+    def nbytes(cap_reads: int, cap_payload: int) -> int:
+        return int(cap_reads) * (4 + 4 + 2 + 2 + 2 + 1 + 8) + int(cap_payload) + 8 * 64
+
+    def c_struct(self) -> mgp_route_part:
+        return mgp_route_part(self.cap_reads, self.cap_payload, self.bc16.ctypes.data, self.tlen16.ctypes.data,
+                              self.bc32.ctypes.data, self.tlen32.ctypes.data, self.flag.ctypes.data,
+                              self.mapq.ctypes.data, self.rec_off.ctypes.data, self.payload.ctypes.data, 0, 0, 0, 0)
+
+    def soa(self) -> ReadSoA:
+        """The routed batch as pushed: an mgp_batch16 (uint16 bc / |tlen|, dense records)
+        or an mgp_batch with rec_off (no start / span: taken from the records)."""
+        n, pb = self.n, self.payload_bytes
+        if self.narrow:
+            return ReadSoA(None, self.bc16[:n], self.tlen16[:n], self.flag[:n], self.mapq[:n], None, None,
+                           self.payload[:pb])
+        return ReadSoA(None, self.bc32[:n], self.tlen32[:n], self.flag[:n], self.mapq[:n], None, self.rec_off[:n],
+                       self.payload[:pb])
+
+
+def route_batch(soa: ReadSoA, bounds: np.ndarray, parts: list, first_index: int = 0,
+                first_seen: np.ndarray | None = None, n_threads: int = 0) -> bool:
+    """mgp_route_batch: every read of `soa` whose cell lies in [bounds[d], bounds[d+1])
+    (and whose flag passes readers.py:96) into parts[d] (its RoutePart), in BAM order,
+    barcode rebased; first_seen[c - bounds[0]] lowered to each cell's first routed read's
+    first_index + i. False (nothing written) when a part's arrays are too small."""
+    b = np.ascontiguousarray(bounds, np.int32)
+    if b.shape[0] != len(parts) + 1:
+        raise ValueError("one part per cell range")
+    if first_seen is not None and (first_seen.dtype != np.uint32 or first_seen.shape[0] < int(b[-1] - b[0])):
+        raise ValueError("first_seen: uint32, one entry per cell of the ranges")
+    cs = (mgp_route_part * len(parts))(*[p.c_struct() for p in parts])
+    ro = soa.rec_off if soa.rec_off is not None and soa.rec_off.shape[0] == soa.n else None
+    rc = host_library().mgp_route_batch(
+        soa.n, soa.bc.ctypes.data, soa.tlen.ctypes.data, soa.flag.ctypes.data, soa.mapq.ctypes.data,
+        None if ro is None else ro.ctypes.data, soa.payload.ctypes.data, int(soa.payload.shape[0]), len(parts),
+        b.ctypes.data, int(first_index), None if first_seen is None else first_seen.ctypes.data, cs,
+        int(n_threads or host_threads()))
+    if rc < 0:
+        raise BAMFormatError(_err()) if "outside the payload" in _err() else ValueError(_err())
+    if rc == 1:
+        return False
+    for p, c in zip(parts, cs):
+        p.n, p.payload_bytes, p.narrow = int(c.n_reads), int(c.payload_bytes), bool(c.narrow)
+    return True
 
 
 def txt_write_cells(prefix: str | Path, counts: np.ndarray, depth: np.ndarray, cells, names: list[str],

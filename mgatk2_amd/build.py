@@ -62,7 +62,7 @@ def build_host(force: bool = False, verbose: bool = False) -> Path:
     """libmgphost.so: native BAM ingest (include/mgpileup_host.h), plain C++ + zlib."""
     srcs = [CSRC / "host" / "mgp_bam.cpp", CSRC / "host" / "mgp_txt.cpp", CSRC / "host" / "mgp_tiles.cpp",
             CSRC / "host" / "mgp_bamw.cpp", CSRC / "host" / "mgp_shard.cpp", CSRC / "host" / "mgp_place.cpp",
-            CSRC / "host" / "mgp_repack.cpp"]
+            CSRC / "host" / "mgp_repack.cpp", CSRC / "host" / "mgp_route.cpp"]
     deps = srcs + [ROOT / "include" / "mgpileup_host.h", ROOT / "include" / "mgpileup.h",
                    CSRC / "host" / "mgp_pack32_host.h", CSRC / "host" / "mgp_place.h",
                    CSRC / "host" / "mgp_zcodec.h", CSRC / "host" / "mgp_pool.h"]

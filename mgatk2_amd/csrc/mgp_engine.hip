@@ -3402,6 +3402,10 @@ int mgp_push_batch16(mgp_ctx* ctx, const mgp_batch16* b) {
     if (!b->bc || !b->abs_tlen || !b->flag || !b->mapq || !b->payload)
         return set_err(MGP_E_INVALID, "null batch array");
     if (ctx->g.nc > 0xFFFF) return set_err(MGP_E_INVALID, "16-bit barcode indices need n_cells <= 65535");
+    // with a cell range the columns hold whole-whitelist indices up to cell_hi - 1, and
+    // 0xFFFF is the no-barcode sentinel
+    if (ctx->cell_range && (int64_t)ctx->cell_lo + ctx->g.nc > 0xFFFF)
+        return set_err(MGP_E_INVALID, "16-bit barcode indices with a cell range need cell_hi <= 65535");
     mgp_batch w{};
     w.n_reads = b->n_reads;
     w.flag = b->flag;

@@ -591,12 +591,14 @@ class File(Group):
         lib = _h5()
         self._close_children()
         lib.H5Gclose(self._id)
-        if self._writable:
-            fid = self._fid
-            _ck_retry(lambda: lib.H5Fflush(fid, 0), "H5Fflush")  # (H5F_SCOPE_LOCAL)
-        lib.H5Fclose(self._fid)
-        self._fid = None
-        self._id = None
+        fid = self._fid
+        try:
+            if self._writable:
+                _ck_retry(lambda: lib.H5Fflush(fid, 0), "H5Fflush")  # (H5F_SCOPE_LOCAL)
+        finally:  # the file id is released (and its lock dropped) even when the flush fails
+            self._fid = None
+            self._id = None
+            lib.H5Fclose(fid)
 
     def __enter__(self):
         return self
