@@ -399,11 +399,13 @@ class StreamSlot:
 
     COLS = (("start", np.int32), ("bc", np.int32), ("tlen", np.int32), ("flag", np.uint16), ("mapq", np.uint8),
             ("span", np.uint32), ("rec_off", np.uint64))
+    # the 16-bit barcode / |tlen| columns of the batch as pushed (mgp_batch_columns16)
+    COLS16 = (("bc16", np.uint16), ("tlen16", np.uint16))
 
     def __init__(self, cap_reads: int, cap_payload: int, alloc=None):
         alloc = alloc or (lambda m, dt: np.empty(m, dt))
         self.cap_reads, self.cap_payload = int(cap_reads), int(cap_payload)
-        for name, dt in self.COLS:
+        for name, dt in self.COLS + self.COLS16:
             setattr(self, name, alloc(self.cap_reads, dt))
         self.payload = alloc(self.cap_payload, np.uint8)
         self.n = 0
@@ -411,7 +413,8 @@ class StreamSlot:
 
     @staticmethod
     def nbytes(cap_reads: int, cap_payload: int) -> int:
-        return sum(int(cap_reads) * np.dtype(dt).itemsize + 64 for _, dt in StreamSlot.COLS) + int(cap_payload) + 64
+        return (sum(int(cap_reads) * np.dtype(dt).itemsize + 64 for _, dt in StreamSlot.COLS + StreamSlot.COLS16)
+                + int(cap_payload) + 64)
 
     def soa(self) -> ReadSoA:
         """The decoded batch as views of the slot's arrays."""

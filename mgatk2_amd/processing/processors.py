@@ -70,12 +70,34 @@ def process_barcode_worker(args):
     return result_dict(res, 0, barcode, config.mito_length)
 
 
-def _payload_hint(n_reads: int) -> int:
+def _pinned_alloc(nbytes: int):
+    """alloc(m, dtype) -> consecutive 64-byte aligned views of one pinned buffer."""
+    pb = PinnedBuffer(nbytes)
+    off = [0]
+
+    def alloc(m, dt):
+        a = pb.array(m, dt, off[0])
+        off[0] = (off[0] + m * np.dtype(dt).itemsize + 63) & ~63
+        return a
+
+    return alloc
+
+
+def _link_bytes(soa: ReadSoA) -> int:
+    """Host-to-device bytes of a pushed batch (its columns and payload)."""
+    return sum(int(a.nbytes) for a in (soa.start, soa.bc, soa.tlen, soa.flag, soa.mapq, soa.span, soa.rec_off,
+                                       soa.payload) if a is not None)
+
+
+def _payload_hint(n_reads: int, n_cells: int = 0, batch_reads: int = STREAM_BATCH_READS) -> int:
     """Device payload bytes a streamed run of n_reads needs at once (no regrowth, which
-    waits for the queued segments): 64-byte records plus the on-device pairing's
-    half-empty lines (a few %), or 32-byte records four per line plus their lines."""
-    per = 40 if os.environ.get("MGP_RECORDS", "64") == "32" else 68
-    return int(n_reads) * per + (64 << 20)
+    waits for the queued segments): 64-byte records plus what the on-device pairing
+    reserves (mgp_push_batch: one half-empty line per cell and key range of 2^18 reads,
+    per batch), or 32-byte records four per line plus their lines."""
+    if os.environ.get("MGP_RECORDS", "64") == "32":
+        return int(n_reads) * 40 + (64 << 20)
+    ranges = -(-int(n_reads) // (1 << 18)) + -(-int(n_reads) // max(1, int(batch_reads))) + 1
+    return int(n_reads) * 64 + ranges * (int(n_cells) + 2) * 64 + (64 << 20)
 
 
 class CellProcessor:
@@ -118,9 +140,10 @@ class CellProcessor:
         self.last_result = res
         return res
 
-    def _stream_producer(self, reader, n_cells: int, batch_reads: int | None):
+    def _stream_producer(self, reader, n_cells: int, batch_reads: int | None, pinned: bool = True):
         """The decode side of a streamed run: the native streaming decoder filling a
-        ring of pinned batches on a producer thread. Returns (bam, stream, expected
+        ring of batches (pinned: the engine copies from them; pinned=False: the router
+        reads them on the host) on a producer thread. Returns (bam, stream, expected
         reads, free queue, full queue, thread, times); the consumer takes filled slots
         from `full` (None at the end, an exception on error) and hands them back
         through `free` (None stops the producer)."""
@@ -136,16 +159,8 @@ class CellProcessor:
         free: Queue = Queue()
         full: Queue = Queue()
         for _ in range(n_slots):
-            pb = PinnedBuffer(slot_bytes)
-            off = [0]
-
-            def alloc(m, dt, pb=pb, off=off):
-                a = pb.array(m, dt, off[0])
-                off[0] = (off[0] + m * np.dtype(dt).itemsize + 63) & ~63
-                return a
-
-            free.put(StreamSlot(cap_reads, cap_payload, alloc))
-        times = {"cap_reads": cap_reads}
+            free.put(StreamSlot(cap_reads, cap_payload, _pinned_alloc(slot_bytes) if pinned else None))
+        times = {"cap_reads": cap_reads, "cap_payload": cap_payload}
 
         def produce():
             try:
@@ -166,13 +181,24 @@ class CellProcessor:
         return bam, st, n_hint, free, full, producer, times
 
     @staticmethod
-    def _push_view(item) -> ReadSoA:
-        """A decoded batch as pushed: records in BAM order, each a 64-byte slot, go
-        without their rec_off / start / span columns (ABI 4: the engine places and
-        pairs them on the device and takes start and span from the records); any
-        other batch with its offsets."""
+    def _push_view(item, n_cells: int) -> ReadSoA:
+        """A decoded batch as pushed. Records dense in BAM order at one stride (every
+        offset checked: a paired placement can give the same payload size with its
+        records permuted) go without their rec_off / start / span columns (ABI 4: the
+        engine places and pairs them on the device and takes start and span from the
+        records), and with 16-bit barcode and |tlen| columns when every key fits
+        (mgp_push_batch16, ABI 5: 7 bytes of columns per read over the link instead of
+        11; MGP_COLUMNS16=0 keeps the 32-bit ones); any other batch with its offsets."""
+        from ..bam import batch_columns16
+
         soa = item.soa()
-        if soa.n and item.payload_bytes == 64 * soa.n and not np.any(soa.rec_off[-1:] != 64 * (soa.n - 1)):
+        n = soa.n
+        if not n:
+            return soa
+        rc = batch_columns16(soa, n_cells, item.bc16, item.tlen16)
+        if rc == 3 and os.environ.get("MGP_COLUMNS16", "1") != "0":
+            return ReadSoA(None, item.bc16[:n], item.tlen16[:n], soa.flag, soa.mapq, None, None, soa.payload)
+        if rc & 1:
             return ReadSoA(None, soa.bc, soa.tlen, soa.flag, soa.mapq, None, None, soa.payload)
         return soa
 
@@ -210,7 +236,8 @@ class CellProcessor:
         t0 = time.perf_counter()
         bam, st, n_hint, free, full, producer, times = self._stream_producer(reader, n_cells, batch_reads)
         try:
-            ec = self.config.engine_config(n_cells, reserve_reads=n_hint, reserve_payload=_payload_hint(n_hint))
+            ec = self.config.engine_config(n_cells, reserve_reads=n_hint,
+                                           reserve_payload=_payload_hint(n_hint, n_cells, times["cap_reads"]))
             ec.stream = True
             eng = Engine(ec, device=self.device)
             try:
@@ -244,7 +271,7 @@ class CellProcessor:
                         eng.set_rows16_target(rows)
 
                 t1 = time.perf_counter()
-                n_batches = 0
+                n_batches, h2d = 0, 0
                 while True:
                     item = full.get()
                     if item is None:
@@ -254,7 +281,9 @@ class CellProcessor:
                     if n_batches == 0:
                         times["first_batch"] = time.perf_counter()
                     settle(False)
-                    eng.push(self._push_view(item))
+                    view = self._push_view(item, n_cells)
+                    eng.push(view)
+                    h2d += _link_bytes(view)
                     eng.copy_wait()  # its pinned arrays may be refilled now
                     free.put(item)
                     n_batches += 1
@@ -288,33 +317,45 @@ class CellProcessor:
                             "stream_decode_end": dec_end - t0, "stream_push_end": t2 - t0,
                             "engine_tail": t3 - t2, "engine_fetch": t4 - t3, "engine_close": te - t4,
                             "stream_batches": n_batches, "stream_batch_reads": times["cap_reads"],
-                            "streamed_run": bool(last_streamed), "rows_target": rows is not None}
+                            "streamed_run": bool(last_streamed), "rows_target": rows is not None,
+                            "h2d_bytes": int(h2d)}
         self.last_result = res
         return res
 
     def _run_stream_sharded(self, reader, n_cells: int, batch_reads: int | None, rows_target: bool) -> EngineResult:
         """The streamed path over several devices: one streaming
-        context per device, each owning a contiguous whitelist range of cells, each
-        fed by a thread of its own. Every device takes every decoded batch whole (its
-        own H2D copy over its own link) and keeps its cells' reads on the device
-        (mgp_set_cell_range rebases the barcode indices behind the copy), so no host
-        thread splits, gathers or re-places reads: the decoder's pinned batch goes to
-        all devices as it is, and its slot returns to the decoder when the last
-        device's copy is done. The ranges are read-balanced by the first batch's reads
-        per cell (a cell's reads are spread over all of chrM, so the first batch is a
-        fair sample of the whole set). Every device's rows target is its cell range of
-        one pinned result array, so the results need no concatenation; a cell's first
-        read indexes the whole pushed stream (the BAM's chrM records) on every device;
-        the tallies are summed on the host."""
+        context per device, each owning a contiguous whitelist range of cells and fed by
+        a thread of its own. The host routes every decoded batch (mgp_route_batch, the
+        reference's split of the barcodes over its pool, processors.py:112-144, as a
+        split over devices): each kept read's columns and record go to its cell's
+        device's pinned batch, in BAM order, the barcode rebased to the device's range;
+        reads without a whitelisted barcode, or that readers.py:96 skips, go nowhere
+        (they count only toward total_reads, which the decoder counts). So each link
+        carries, and each device holds, only its own cells' reads. The ranges are
+        read-balanced by the first batch's reads per cell (a cell's reads are spread
+        over all of chrM, so the first batch is a fair sample of the whole set). The
+        cells' first-seen order (readers.py:104-163) comes from the router: each cell's
+        first routed read's index in the stream. Every device's rows go into its cell
+        range of one result array, so nothing is concatenated; the tallies are summed
+        on the host."""
+        from queue import Empty
+
+        from ..bam import RoutePart, host_threads, route_batch
+        from ..exceptions import ProcessingError
         from ..shard import partition_cells
 
         devs = list(self.devices)
         D = len(devs)
         t0 = time.perf_counter()
-        bam, st, n_hint, free, full, producer, times = self._stream_producer(reader, n_cells, batch_reads)
-        engines, queues, workers, errors = {}, {}, {}, []
+        bam, st, n_hint, free, full, producer, times = self._stream_producer(reader, n_cells, batch_reads,
+                                                                            pinned=False)
+        engines, rings, queues, workers, errors = {}, {}, {}, {}, []
         parts: list[tuple[int, int, int]] = []
         rows = None
+        first_seen = np.full(max(1, n_cells), 0xFFFFFFFF, np.uint32)
+        n_threads = host_threads()
+        n_slots = max(2, int(os.environ.get("MGP_STREAM_SLOTS", STREAM_SLOTS)))
+        link_bytes = {}
         try:
             first = full.get()
             if isinstance(first, BaseException):
@@ -327,12 +368,25 @@ class CellProcessor:
                 w = np.ones(n_cells)
             bounds = partition_cells(w, D)
             parts = [(d, int(bounds[d]), int(bounds[d + 1])) for d in range(D) if bounds[d + 1] > bounds[d]]
+            wsum = float(w.sum()) or 1.0
+            share = {d: float(w[lo:hi].sum()) / wsum for d, lo, hi in parts}
             for d, lo, hi in parts:
-                ec = self.config.engine_config(hi - lo, reserve_reads=n_hint + 4096,
-                                               reserve_payload=_payload_hint(n_hint))
+                m = int(n_hint * share[d] * 1.1) + 65536  # the device's share of the reads, with headroom
+                ec = self.config.engine_config(hi - lo, reserve_reads=m,
+                                               reserve_payload=_payload_hint(m, hi - lo, times["cap_reads"] * share[d]))
                 ec.stream = True
                 engines[d] = Engine(ec, device=devs[d])
-                engines[d].set_cell_range(lo, hi)
+                rings[d], queues[d] = Queue(), Queue()
+                link_bytes[d] = 0
+            route_bounds = np.array([lo for _, lo, _ in parts] + ([parts[-1][2]] if parts else [0]), np.int32)
+            # a device's batch: its share of a decoded batch with headroom (a batch that
+            # does not fit is routed in halves)
+            cap_r, cap_p = times["cap_reads"], times["cap_payload"]
+
+            def part_caps(d):
+                f = min(1.0, share[d] * 1.5 + 0.02)
+                return int(cap_r * f) + 65536, int(cap_p * f) + (1 << 20)
+
             # the rows target (all cells, one pinned array) is pinned on a thread while the
             # first batches go in; each device thread sets its view when it is ready (the
             # engine copies the windows piled before, ABI 4)
@@ -350,16 +404,9 @@ class CellProcessor:
 
                 threading.Thread(target=alloc, name="mgp-rows-alloc", daemon=True).start()
 
-            def release(left, item):
-                with left[1]:
-                    left[0] -= 1
-                    last = left[0] == 0
-                if last:
-                    free.put(item)
-
             def work(d, lo, hi):
-                # every batch as it is: pushed, its copy awaited, its slot released by the
-                # last device done with it
+                # the device's pinned batches (pinned here, beside the other devices'), then
+                # every routed batch pushed, its copy awaited, its arrays back to the ring
                 eng = engines[d]
                 view_set = not (rows_target and parts)
 
@@ -377,34 +424,64 @@ class CellProcessor:
                                                      r.window_width))
 
                 try:
+                    cr, cp = part_caps(d)
+                    for _ in range(n_slots):
+                        rings[d].put(RoutePart(cr, cp, _pinned_alloc(RoutePart.nbytes(cr, cp))))
                     while True:
                         set_view(False)
-                        job = queues[d].get()
-                        if job is None:
+                        pt = queues[d].get()
+                        if pt is None:
                             break
-                        item, soa, left = job
                         try:
-                            eng.push(soa)
+                            sub = pt.soa()
+                            eng.push(sub)
+                            link_bytes[d] += _link_bytes(sub)
                             eng.copy_wait()
                         finally:
-                            release(left, item)
+                            rings[d].put(pt)
                     set_view(True)
                     eng.run()
                     eng.sync()
                 except BaseException as e:  # noqa: BLE001 - re-raised by the router
                     errors.append(e)
-                    while True:  # drain (releasing the slots it was dealt)
-                        job = queues[d].get()
-                        if job is None:
+                    while True:  # drain (handing back the batches it was dealt)
+                        pt = queues[d].get()
+                        if pt is None:
                             break
-                        release(job[2], job[0])
+                        rings[d].put(pt)
+
+            def take(d):
+                while True:
+                    if errors:
+                        raise errors[0]
+                    try:
+                        return rings[d].get(timeout=0.2)
+                    except Empty:
+                        continue
+
+            def route(soa, a, b, base):
+                """Reads [a, b) of a decoded batch to their devices (halves when a device's
+                batch cannot hold its share)."""
+                sub = soa if (a, b) == (0, soa.n) else ReadSoA(None, soa.bc[a:b], soa.tlen[a:b], soa.flag[a:b],
+                                                               soa.mapq[a:b], None, soa.rec_off[a:b], soa.payload)
+                got = [take(d) for d, _, _ in parts]
+                if not route_batch(sub, route_bounds, got, base + a, first_seen, n_threads):
+                    for (d, _, _), pt in zip(parts, got):
+                        rings[d].put(pt)
+                    if b - a <= 1:
+                        raise ProcessingError("a read's record does not fit a device batch")
+                    mid = (a + b) // 2
+                    route(soa, a, mid, base)
+                    route(soa, mid, b, base)
+                    return
+                for (d, _, _), pt in zip(parts, got):
+                    (queues[d] if pt.n else rings[d]).put(pt)
 
             for d, lo, hi in parts:
-                queues[d] = Queue(maxsize=4)
                 workers[d] = threading.Thread(target=work, args=(d, lo, hi), name=f"mgp-dev{d}", daemon=True)
                 workers[d].start()
             t1 = time.perf_counter()
-            n_batches = 0
+            n_batches, base, t_route = 0, 0, 0.0
             try:
                 item = first
                 while item is not None:
@@ -412,13 +489,13 @@ class CellProcessor:
                         raise item
                     if errors:
                         raise errors[0]
-                    if parts:
-                        soa = self._push_view(item)
-                        left = [len(parts), threading.Lock()]
-                        for d, _, _ in parts:
-                            queues[d].put((item, soa, left))
-                    else:
-                        free.put(item)
+                    soa = item.soa()
+                    if parts and soa.n:
+                        tr = time.perf_counter()
+                        route(soa, 0, soa.n, base)
+                        t_route += time.perf_counter() - tr
+                    base += soa.n
+                    free.put(item)
                     n_batches += 1
                     item = full.get()
             finally:
@@ -449,7 +526,7 @@ class CellProcessor:
             for d, lo, hi in parts:
                 r = engines[d].fetch(dense=wide)
                 for k in ("n_reads", "any_paired", "passed", "covered", "depth_sum", "depth_max", "median_lo",
-                          "median_hi", "first_read"):
+                          "median_hi"):
                     getattr(res, k)[lo:hi] = getattr(r, k)
                 if wide:
                     for k in ("counts", "tn5", "depth"):
@@ -459,6 +536,10 @@ class CellProcessor:
                     st_sum[k] += int(r.stats[k])
                 max_span = max(max_span, int(r.stats["max_span"]))
                 err |= int(r.stats["error_bits"])
+            # each cell's first read in the BAM (the router's index over the whole stream)
+            res.first_read[:] = first_seen[:n_cells]
+            if np.any((res.n_reads > 0) != (res.first_read != 0xFFFFFFFF)):
+                raise ProcessingError("routed reads and per-cell read counts disagree")
             if not wide:
                 res.counts, res.tn5, res.depth = src.counts, src.tn5, src.depth
             res.stats = {"total_reads": int(st.records), **st_sum, "max_span": max_span, "error_bits": err}
@@ -476,7 +557,8 @@ class CellProcessor:
                             "stream_decode_end": times.get("decode_end", t2) - t0, "stream_push_end": t2 - t0,
                             "engine_tail": 0.0, "engine_fetch": t3 - t2, "engine_close": te - t3,
                             "stream_batches": n_batches, "stream_batch_reads": times["cap_reads"],
-                            "stream_devices": len(parts), "rows_target": rows is not None,
+                            "stream_devices": len(parts), "rows_target": rows is not None, "route_s": t_route,
+                            "h2d_bytes": int(sum(link_bytes.values())),
                             "cell_bounds": [lo for _, lo, _ in parts] + ([parts[-1][2]] if parts else [])}
         self.last_result = res
         return res

@@ -580,9 +580,11 @@ class _OracleEngine:
     first-read mapping and the merge."""
 
     oracle = None
+    pushed: list = []
 
     def __init__(self, cfg, device=0):
         self.cfg, self.parts, self.rows, self.lo = cfg, [], None, None
+        _OracleEngine.pushed.append((cfg, self.parts))
 
     def set_cell_range(self, lo, hi):  # (mgp_set_cell_range: the barcode indices rebased at push)
         assert hi - lo == self.cfg.n_cells and not self.parts
@@ -597,13 +599,24 @@ class _OracleEngine:
     def push(self, soa):
         from mgatk2_amd.synth import ReadSoA
 
-        if soa.rec_off is None:  # a dense batch of 64-byte records (the engine places and pairs them)
-            n = soa.n
-            rec_off = 64 * np.arange(n, dtype=np.uint64)
-            start = np.ascontiguousarray(soa.payload.reshape(n, 64)[:, :4]).view(np.int32).ravel().copy()
-            soa = ReadSoA(start, soa.bc, soa.tlen, soa.flag, soa.mapq, np.zeros(n, np.uint32), rec_off, soa.payload)
-        part = ReadSoA(*[getattr(soa, k).copy() for k in ("start", "bc", "tlen", "flag", "mapq", "span", "rec_off",
-                                                          "payload")])
+        n = soa.n
+        bc, tlen = soa.bc, soa.tlen
+        if bc.dtype == np.uint16:  # an mgp_batch16: 16-bit barcode index (0xFFFF: none) and |tlen|
+            bc = np.where(bc == 0xFFFF, -1, bc.astype(np.int32)).astype(np.int32)
+            tlen = tlen.astype(np.int32)
+        rec_off = soa.rec_off
+        if rec_off is None:  # dense records (the engine places and pairs them)
+            stride = soa.payload.shape[0] // max(1, n)
+            rec_off = stride * np.arange(n, dtype=np.uint64)
+        start = soa.start
+        if start is None:  # taken from the records (ABI 4): u16 in 32-byte records, i32 in the others
+            at = rec_off.astype(np.int64)
+            b = [soa.payload[at + k].astype(np.int64) for k in range(4)]
+            s32 = (b[0] | b[1] << 8 | b[2] << 16 | b[3] << 24).astype(np.uint32).view(np.int32)
+            start = np.where(soa.flag & 0x4000, b[0] | b[1] << 8, s32).astype(np.int32)
+        span = soa.span if soa.span is not None else np.zeros(n, np.uint32)
+        part = ReadSoA(*[np.array(a, copy=True) for a in (start, bc, tlen, soa.flag, soa.mapq, span, rec_off,
+                                                          soa.payload)])
         if self.lo is not None:
             bc = part.bc
             keep = (bc >= self.lo) & (bc < self.lo + self.cfg.n_cells)
@@ -644,16 +657,22 @@ class _OracleEngine:
         pass
 
 
+@pytest.mark.parametrize("layout", ["64", "64-paired", "32"])
 @pytest.mark.parametrize("rows", ["0", "1"])
 @pytest.mark.parametrize("n_dev", [2, 3, 7])
-def test_stream_sharded_routing_host(n_dev, rows, tmp_path, oracle_lib, monkeypatch):
+def test_stream_sharded_routing_host(n_dev, rows, layout, tmp_path, oracle_lib, monkeypatch):
     """The streamed multi-device path's host side (CellProcessor._run_stream_sharded:
-    every batch pushed whole to every device, each keeping its read-balanced cell
-    range (mgp_set_cell_range, restated in the stand-in), the rows fetched per device
-    into its range of one array (or, MGP_ROWS_TARGET=1, per-device rows targets as
-    views of one array), first reads, tallies and stats merged), with the oracle
-    standing in for each device's engine: every output equals the reference's."""
+    every decoded batch routed by the native router (mgp_route_batch) into each
+    device's batch of its read-balanced cell range, barcodes rebased, 16-bit columns
+    where they fit; the rows fetched per device into its range of one array (or,
+    MGP_ROWS_TARGET=1, per-device rows targets as views of one array), first reads
+    from the router, tallies and stats merged), with the oracle standing in for each
+    device's engine, for the producer's 64-byte records in BAM order, its paired
+    placement and its 32-byte records: every output equals the reference's, and no
+    device is sent a read of another device's cells."""
     monkeypatch.setenv("MGP_ROWS_TARGET", rows)
+    monkeypatch.setenv("MGP_RECORDS", layout[:2])
+    monkeypatch.setenv("MGP_PLACEMENT", "paired" if layout.endswith("paired") else "device")
     from mgatk2_amd.engine import PinnedBuffer  # noqa: F401 - (host memory in this stand-in)
     from mgatk2_amd.processing import processors
     from mgatk2_amd.pipeline import run_pipeline
@@ -669,6 +688,7 @@ def test_stream_sharded_routing_host(n_dev, rows, tmp_path, oracle_lib, monkeypa
             return self.buf[offset:offset + n].view(dt).reshape(shape)
 
     _OracleEngine.oracle = oracle_lib
+    _OracleEngine.pushed = []
     monkeypatch.setattr(processors, "Engine", _OracleEngine)
     monkeypatch.setattr(processors, "PinnedBuffer", HostBuf)
     monkeypatch.setenv("MGP_STREAM_BATCH", "997")
@@ -686,3 +706,7 @@ def test_stream_sharded_routing_host(n_dev, rows, tmp_path, oracle_lib, monkeypa
         output_format="txt", devices=list(range(n_dev)),
     )
     _check_outputs(g, out, ret)
+    assert len(_OracleEngine.pushed) >= 2
+    for cfg, parts in _OracleEngine.pushed:  # every routed read is one of the device's own cells
+        for part in parts:
+            assert np.all((part.bc >= 0) & (part.bc < cfg.n_cells))
