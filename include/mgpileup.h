@@ -46,7 +46,7 @@
 extern "C" {
 #endif
 
-#define MGP_ABI_VERSION 5  /* 2: fixed seq/CIGAR offsets for reads <= 64 bases;
+#define MGP_ABI_VERSION 6  /* 2: fixed seq/CIGAR offsets for reads <= 64 bases;
                               3: synth cell shards, cell-range and 16-bit fetches, streaming runs;
                               4: batches without rec_off / span columns and the rows target (the
                                  round-3 "v3.1" entry points), pushed records checked against
@@ -55,7 +55,9 @@ extern "C" {
                                  mgp_synth_params.n_rec_off, rows targets with min_reads > 1;
                               5: mgp_set_cell_range (one device's cells of whole batches),
                                  mgp_push_batch16 (16-bit barcode / |tlen| columns), dense
-                                 64-byte batches paired on the device */
+                                 64-byte batches paired on the device;
+                              6: mgp_txt_gz_* (the txt count files formatted and deflated on the
+                                 device) */
 
 /* ---- return codes (0 = success) ------------------------------------------ */
 #define MGP_OK               0
@@ -498,6 +500,35 @@ int  mgp_fetch(mgp_ctx *ctx, mgp_result *out);
 int  mgp_fetch_cells(mgp_ctx *ctx, int32_t lo, int32_t hi, mgp_result *out);
 /* The 16-bit result rows of cells [lo, hi) (implies mgp_sync); NULL members are skipped. */
 int  mgp_fetch_rows16(mgp_ctx *ctx, int32_t lo, int32_t hi, mgp_rows16 *out);
+
+/* The txt count files on the device (ABI 6). Replaces IncrementalTextWriter.write_cell
+ * and finalize's gzip at compresslevel 9 (src/file_io/writers.py:430-486): for each
+ * listed cell, in order, its lines
+ *   output.coverage.txt  "pos,barcode,depth"    (depth > 0)
+ *   output.{A,C,G,T}.txt "pos,barcode,fwd,rev"  (depth > 0 and fwd + rev > 0)
+ * (1-based pos, unbounded integers) are formatted from the run's count rows in HBM and
+ * deflated there into one gzip member per (file, cell); a member is 0 bytes when the
+ * cell has no line in that file. Each output file is its members concatenated in cell
+ * order: gzip readers decompress it to exactly the reference's text. */
+typedef struct mgp_txt_gz {
+    int64_t        n_cells;      /* cells to write                                         */
+    const int32_t *cells;        /* host: the context's cell index of each, in output order */
+    const char    *names;        /* host: their barcodes, concatenated (no separators)     */
+    const int64_t *name_off;     /* host: n_cells + 1 offsets into names (each 0..4096 bytes) */
+    int64_t       *member_bytes; /* host out: [5][n_cells] member sizes, files coverage, A, C, G, T */
+    int64_t       *text_bytes;   /* host out (may be NULL): [5][n_cells] decompressed sizes */
+} mgp_txt_gz;
+/* Format and deflate the members of `job` (implies mgp_sync; after mgp_run). *total_bytes
+ * = the sum of member_bytes; the members stay on the device, file-major (all coverage
+ * members in cell order, then A, C, G, T), until mgp_txt_gz_fetch or the next call. */
+int  mgp_txt_gz_run(mgp_ctx *ctx, mgp_txt_gz *job, int64_t *total_bytes);
+/* The last mgp_txt_gz_run's members (total_bytes of them) into dst (cap >= total). */
+int  mgp_txt_gz_fetch(mgp_ctx *ctx, uint8_t *dst, int64_t cap);
+/* The same from caller-supplied u32 rows (counts [n_rows][mito_len][8], depth
+ * [n_rows][mito_len]) on `device`, no engine context: the members into dst (cap bytes;
+ * MGP_E_INVALID with *total_bytes set when it is too small). */
+int  mgp_txt_gz_rows(int device, const uint32_t *counts, const uint32_t *depth, int32_t n_rows, int32_t mito_len,
+                     mgp_txt_gz *job, uint8_t *dst, int64_t cap, int64_t *total_bytes);
 /* ABI v3.1: the 16-bit rows of every cell go to `rows` (pinned host arrays for all
  * cells from mgp_host_alloc, written by the device through their mapping) as the
  * windows complete: each streaming segment writes its windows' rows on a

@@ -24,7 +24,7 @@ HOST_SO = LIB_DIR / "libmgphost.so"
 ORACLE_DIR = ROOT / "oracle"
 ORACLE_SO = ORACLE_DIR / "_build" / "liboracle.so"
 
-HIP_SOURCES = ["mgp_engine.hip", "mgp_synth.hip"]
+HIP_SOURCES = ["mgp_engine.hip", "mgp_synth.hip", "mgp_txtgz.hip"]
 HIP_FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared", "-Wall", "-Wno-unused-function"]
 
 
@@ -45,7 +45,7 @@ def _stale(target: Path, deps: list[Path]) -> bool:
 def build_engine(force: bool = False, verbose: bool = False, out: Path | None = None,
                  defines: tuple[str, ...] = ()) -> Path:
     target = Path(out) if out else ENGINE_SO
-    deps = [CSRC / s for s in HIP_SOURCES] + [CSRC / "mgp_kernels.h", ROOT / "include" / "mgpileup.h"]
+    deps = [CSRC / s for s in HIP_SOURCES] + [CSRC / "mgp_kernels.h", CSRC / "mgp_txtgz.h", ROOT / "include" / "mgpileup.h"]
     if force or _stale(target, deps):
         LIB_DIR.mkdir(parents=True, exist_ok=True)
         tmp = target.with_suffix(".so.tmp")

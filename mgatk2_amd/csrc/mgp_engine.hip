@@ -39,6 +39,7 @@
 
 #include "../../include/mgpileup.h"
 #include "mgp_kernels.h"
+#include "mgp_txtgz.h"
 
 using namespace mgp;
 
@@ -106,6 +107,15 @@ struct DevBuf {
     }
     template <typename T>
     T* as() const { return reinterpret_cast<T*>(p); }
+};
+
+// mgp_txt_gz: the device txt writer's buffers (mgp_txtgz.hip), kept for the next call
+struct TxtState {
+    DevBuf cells, names, name_off, sizes, nlines, offs, text, tok, lines, out, member_bytes, crc_shift, dst_off, packed;
+    DevBuf rows_c, rows_d;  // (mgp_txt_gz_rows: the caller's u32 rows)
+    bool shift_ready = false;
+    int64_t n = 0;
+    uint64_t total = 0;
 };
 
 enum Stage { ST_HIST, ST_SCAN, ST_GROUP_A, ST_GROUP_B, ST_PILEUP, ST_GATE, ST_MEDIAN, ST_TALLY, ST_COMM, ST_N };
@@ -199,6 +209,8 @@ struct mgp_ctx {
     int stream_layout = 1;     // kLayP64 / kLayP32: the packed layout the run's segments assume
     int64_t segments = 0;      // segments queued by pushes (all runs)
     bool last_streamed = false;
+
+    TxtState txt;  // mgp_txt_gz
 };
 
 // ---------------------------------------------------------------------------
@@ -4480,6 +4492,148 @@ int mgp_synth_generate(mgp_ctx* ctx, const mgp_synth_params* p) {
     ctx->no_spec = false;
     ctx->bits_cached = false;
     return MGP_OK;
+}
+
+// ---------------------------------------------------------------------------
+// mgp_txt_gz: the txt count files formatted and deflated on the device
+// (IncrementalTextWriter.write_cell + finalize's gzip -9, writers.py:430-486)
+// ---------------------------------------------------------------------------
+static int txt_run(TxtState& st, hipStream_t s, const txtgz::Rows& rows, int32_t n_rows, const mgp_txt_gz* job) {
+    using namespace txtgz;
+    const int64_t n = job->n_cells;
+    if (n < 0 || (n > 0 && (!job->cells || !job->names || !job->name_off || !job->member_bytes)))
+        return set_err(MGP_E_INVALID, "mgp_txt_gz: bad arguments");
+    st.n = n;
+    st.total = 0;
+    if (n == 0) return MGP_OK;
+    if (n > (int64_t)1 << 26) return set_err(MGP_E_INVALID, "mgp_txt_gz: too many cells for one call");
+    for (int64_t k = 0; k < n; ++k) {
+        if (job->cells[k] < 0 || job->cells[k] >= n_rows) return set_err(MGP_E_INVALID, "mgp_txt_gz: cell out of range");
+        const int64_t bl = job->name_off[k + 1] - job->name_off[k];
+        if (bl < 0 || bl > 4096 || job->name_off[k] < 0)
+            return set_err(MGP_E_INVALID, "mgp_txt_gz: barcode names of 0..4096 bytes");
+    }
+    const int64_t nm = kFiles * n;
+    const size_t nbytes = (size_t)job->name_off[n];
+    MGP_TRY(st.cells.ensure((size_t)n * 4));
+    MGP_TRY(st.names.ensure(nbytes + 1));
+    MGP_TRY(st.name_off.ensure((size_t)(n + 1) * 8));
+    MGP_TRY(st.sizes.ensure((size_t)nm * 8));
+    MGP_TRY(st.nlines.ensure((size_t)nm * 8));
+    MGP_TRY(st.offs.ensure((size_t)3 * (nm + 1) * 8));
+    MGP_TRY(st.member_bytes.ensure((size_t)nm * 4));
+    MGP_TRY(st.dst_off.ensure((size_t)nm * 8));
+    if (!st.shift_ready) {
+        std::vector<uint32_t> M(25 * 32);
+        crc_shift_matrices(M.data());
+        MGP_TRY(st.crc_shift.ensure(M.size() * 4));
+        HIP_TRY(hipMemcpy(st.crc_shift.p, M.data(), M.size() * 4, hipMemcpyHostToDevice));
+        st.shift_ready = true;
+    }
+    HIP_TRY(hipMemcpyAsync(st.cells.p, job->cells, (size_t)n * 4, hipMemcpyHostToDevice, s));
+    if (nbytes) HIP_TRY(hipMemcpyAsync(st.names.p, job->names, nbytes, hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemcpyAsync(st.name_off.p, job->name_off, (size_t)(n + 1) * 8, hipMemcpyHostToDevice, s));
+    Job jb{rows, n, st.cells.as<int32_t>(), st.names.as<char>(), st.name_off.as<int64_t>()};
+    if (txt_sizes(jb, st.sizes.as<uint64_t>(), st.nlines.as<uint64_t>(), s) != 0)
+        return set_err(MGP_E_HIP, "mgp_txt_gz: size kernel launch failed");
+    std::vector<uint64_t> sz((size_t)nm), nl((size_t)nm), offs((size_t)3 * (nm + 1));
+    HIP_TRY(hipMemcpyAsync(sz.data(), st.sizes.p, (size_t)nm * 8, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipMemcpyAsync(nl.data(), st.nlines.p, (size_t)nm * 8, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    uint64_t* to = offs.data();
+    uint64_t* lo = to + nm + 1;
+    uint64_t* oo = lo + nm + 1;
+    to[0] = lo[0] = oo[0] = 0;
+    for (int64_t m = 0; m < nm; ++m) {
+        to[m + 1] = to[m] + sz[(size_t)m];
+        lo[m + 1] = lo[m] + nl[(size_t)m];
+        oo[m + 1] = oo[m] + out_bound(sz[(size_t)m]);
+        if (job->text_bytes) job->text_bytes[m] = (int64_t)sz[(size_t)m];
+    }
+    MGP_TRY(st.text.ensure(to[nm] + 64));
+    MGP_TRY(st.tok.ensure(4 * to[nm] + 64));
+    MGP_TRY(st.lines.ensure(12 * lo[nm] + 64));
+    MGP_TRY(st.out.ensure(oo[nm] + 64));
+    HIP_TRY(hipMemcpyAsync(st.offs.p, offs.data(), offs.size() * 8, hipMemcpyHostToDevice, s));
+    Scratch sc{};
+    sc.text_off = st.offs.as<uint64_t>();
+    sc.line_off = sc.text_off + nm + 1;
+    sc.out_off = sc.line_off + nm + 1;
+    sc.text = st.text.as<uint8_t>();
+    sc.tok = st.tok.as<uint32_t>();
+    sc.lines = st.lines.as<uint32_t>();
+    sc.out = st.out.as<uint32_t>();
+    sc.member_bytes = st.member_bytes.as<uint32_t>();
+    sc.crc_shift = st.crc_shift.as<uint32_t>();
+    if (txt_deflate(jb, sc, s) != 0) return set_err(MGP_E_HIP, "mgp_txt_gz: deflate kernel launch failed");
+    std::vector<uint32_t> mb((size_t)nm);
+    HIP_TRY(hipMemcpyAsync(mb.data(), st.member_bytes.p, (size_t)nm * 4, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    std::vector<uint64_t> dst((size_t)nm);
+    uint64_t tot = 0;
+    for (int64_t m = 0; m < nm; ++m) {
+        dst[(size_t)m] = tot;
+        tot += mb[(size_t)m];
+        job->member_bytes[m] = mb[(size_t)m];
+    }
+    MGP_TRY(st.packed.ensure(tot + 64));
+    HIP_TRY(hipMemcpyAsync(st.dst_off.p, dst.data(), (size_t)nm * 8, hipMemcpyHostToDevice, s));
+    if (txt_pack(sc, nm, st.dst_off.as<uint64_t>(), st.packed.as<uint8_t>(), s) != 0)
+        return set_err(MGP_E_HIP, "mgp_txt_gz: pack kernel launch failed");
+    HIP_TRY(hipStreamSynchronize(s));
+    st.total = tot;
+    return MGP_OK;
+}
+
+int mgp_txt_gz_run(mgp_ctx* ctx, mgp_txt_gz* job, int64_t* total_bytes) {
+    if (!ctx || !job) return set_err(MGP_E_INVALID, "null ctx/job");
+    MGP_TRY(mgp_sync(ctx));
+    HIP_TRY(hipSetDevice(ctx->dev));
+    const Geom& g = ctx->g;
+    if (!ctx->ran) return set_err(MGP_E_STATE, "mgp_txt_gz: no run to write (mgp_run first)");
+    txtgz::Rows rows{reinterpret_cast<const uint4*>(ctx->counts16.p), ctx->depth16.as<uint16_t>(),
+                     ctx->wide.as<uint8_t>(), ctx->counts.as<uint32_t>(), ctx->depth.as<uint32_t>(), g.L, g.W, g.nwin};
+    MGP_TRY(txt_run(ctx->txt, ctx->s_comp, rows, g.nc, job));
+    if (total_bytes) *total_bytes = (int64_t)ctx->txt.total;
+    return MGP_OK;
+}
+
+int mgp_txt_gz_fetch(mgp_ctx* ctx, uint8_t* dst, int64_t cap) {
+    if (!ctx || (!dst && ctx->txt.total)) return set_err(MGP_E_INVALID, "null ctx/dst");
+    if (cap < (int64_t)ctx->txt.total) return set_err(MGP_E_INVALID, "mgp_txt_gz_fetch: destination too small");
+    HIP_TRY(hipSetDevice(ctx->dev));
+    if (ctx->txt.total) HIP_TRY(hipMemcpy(dst, ctx->txt.packed.p, ctx->txt.total, hipMemcpyDeviceToHost));
+    return MGP_OK;
+}
+
+int mgp_txt_gz_rows(int device, const uint32_t* counts, const uint32_t* depth, int32_t n_rows, int32_t mito_len,
+                    mgp_txt_gz* job, uint8_t* dst, int64_t cap, int64_t* total_bytes) {
+    if (!job || n_rows < 0 || mito_len <= 0 || (n_rows > 0 && (!counts || !depth)))
+        return set_err(MGP_E_INVALID, "mgp_txt_gz_rows: bad arguments");
+    HIP_TRY(hipSetDevice(device));
+    hipStream_t s = nullptr;
+    HIP_TRY(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    int rc = MGP_OK;
+    {
+        TxtState st;
+        const size_t npos = (size_t)n_rows * (size_t)mito_len;
+        rc = st.rows_c.ensure(npos * 32 + 64);
+        if (rc == MGP_OK) rc = st.rows_d.ensure(npos * 4 + 64);
+        if (rc == MGP_OK && npos) {
+            if (hipMemcpy(st.rows_c.p, counts, npos * 32, hipMemcpyHostToDevice) != hipSuccess ||
+                hipMemcpy(st.rows_d.p, depth, npos * 4, hipMemcpyHostToDevice) != hipSuccess)
+                rc = set_err(MGP_E_HIP, "mgp_txt_gz_rows: upload failed");
+        }
+        txtgz::Rows rows{nullptr, nullptr, nullptr, st.rows_c.as<uint32_t>(), st.rows_d.as<uint32_t>(), mito_len,
+                         mito_len, 1};
+        if (rc == MGP_OK) rc = txt_run(st, s, rows, n_rows, job);
+        if (rc == MGP_OK && total_bytes) *total_bytes = (int64_t)st.total;
+        if (rc == MGP_OK && (int64_t)st.total > cap) rc = set_err(MGP_E_INVALID, "mgp_txt_gz_rows: destination too small");
+        if (rc == MGP_OK && st.total && hipMemcpy(dst, st.packed.p, st.total, hipMemcpyDeviceToHost) != hipSuccess)
+            rc = set_err(MGP_E_HIP, "mgp_txt_gz_rows: download failed");
+    }
+    (void)hipStreamDestroy(s);
+    return rc;
 }
 
 }  // extern "C"

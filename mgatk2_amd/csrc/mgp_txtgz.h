@@ -1,0 +1,69 @@
+// mgp_txtgz.h — the engine's txt writer on the device (internal interface between
+// mgp_engine.hip and mgp_txtgz.hip; the C-ABI is mgp_txt_gz* in include/mgpileup.h).
+//
+// IncrementalTextWriter (src/file_io/writers.py:430-486) formats, per passing cell,
+//   output.coverage.txt: "pos,barcode,depth\n"   for every position with depth > 0
+//   output.{A,C,G,T}.txt: "pos,barcode,fwd,rev\n" for those with fwd + rev > 0
+// (1-based positions, cells in first-seen order) and then gzips each file at
+// compresslevel=9. Here one workgroup per (cell, file) formats the cell's lines from
+// the count rows resident in HBM and deflates them into one gzip member (a dynamic-
+// Huffman block from an optimal parse over line-aligned match candidates, or a fixed
+// or stored block when smaller), so only the compressed members cross the host link
+// and a file is its members concatenated in cell order (gzip readers, Python's gzip
+// and zcat read multi-member files as one stream).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace mgp {
+namespace txtgz {
+
+constexpr int kFiles = 5;  // coverage, A, C, G, T (member m of cell k is file m % 5 ... see Members)
+
+// The count rows the lines are made from: the engine's 16-bit rows (u16 (fwd, rev)
+// pairs per base as one uint4 per position, u16 depth) with the exact u32 rows of its
+// drained windows (wide flag per (cell, window)), or plain u32 rows (c16 == nullptr).
+struct Rows {
+    const uint4* c16;
+    const uint16_t* d16;
+    const uint8_t* wide;
+    const uint32_t* c32;  // [cells][L][8]
+    const uint32_t* d32;  // [cells][L]
+    int L, W, nwin;
+};
+
+// One batch of cells (the caller's order) and their barcodes (device arrays).
+struct Job {
+    Rows rows;
+    int64_t n;                 // cells of the batch
+    const int32_t* cells;      // row index of each
+    const char* names;         // barcodes, concatenated
+    const int64_t* name_off;   // n + 1
+};
+
+// Device scratch of a batch; every array is sized by the caller from txt_sizes().
+struct Scratch {
+    uint64_t* text_off;   // [5n + 1] member text offsets (member = file * n + cell)
+    uint64_t* line_off;   // [5n + 1]
+    uint64_t* out_off;    // [5n + 1] member output regions (bounds)
+    uint8_t* text;        // text_off[5n] bytes
+    uint32_t* tok;        // text_off[5n] words: the parse's choices, then the tokens
+    uint32_t* lines;      // line_off[5n] x 3 words: start, c1 | c2 << 16, c3 | len << 16
+    uint32_t* out;        // out_off[5n] / 4 words (member outputs)
+    uint32_t* member_bytes;  // [5n] compressed bytes of each member
+    const uint32_t* crc_shift;  // [25][32]: one-zero-byte CRC operator to the powers 2^b (GF(2) matrices)
+};
+
+// member text bytes and lines of every (file, cell) of the batch -> sizes[5n], nlines[5n]
+int txt_sizes(const Job& job, uint64_t* sizes, uint64_t* nlines, hipStream_t s);
+// the members (gzip) into scratch.out at out_off; member_bytes filled
+int txt_deflate(const Job& job, const Scratch& sc, hipStream_t s);
+// members packed back to back in member order (file-major) from out_off into dst at dst_off[5n]
+int txt_pack(const Scratch& sc, int64_t n_members, const uint64_t* dst_off, uint8_t* dst, hipStream_t s);
+// the 25 CRC shift matrices (host)
+void crc_shift_matrices(uint32_t* m /* 25 x 32 */);
+// bound of a member's output region for `text` bytes
+__host__ __device__ inline uint64_t out_bound(uint64_t text) { return ((text + 5 * (text / 65535 + 1) + 64 + 31) & ~uint64_t(31)); }
+
+}  // namespace txtgz
+}  // namespace mgp

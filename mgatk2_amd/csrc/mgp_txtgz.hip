@@ -1,0 +1,820 @@
+// mgp_txtgz.hip — mgatk's txt count files formatted and gzip-deflated on the device
+// (gfx950, wave64). See mgp_txtgz.h for what is written; the layout of one member:
+//
+//   gzip header (10 B) | one deflate block (BFINAL) | CRC-32 | ISIZE
+//
+// One 256-thread workgroup per (file, cell) member. Thread t owns positions
+// [t P, (t + 1) P) of chrM (P = ceil(L / 256)) and with them a contiguous run of the
+// member's lines (a "segment"):
+//   1. format: each thread counts its lines' bytes, a block scan places the segments,
+//      each thread writes its text and a line table (start and field offsets);
+//   2. parse (twice: default prices, then the member's own Huffman lengths): each
+//      thread runs a backward optimal-parse DP over its segment's bytes. The match
+//      candidates are line-aligned: for each of the 16 previous lines, the byte at the
+//      same offset from the start of the current field and the byte at the same offset
+//      from the line's end. Along a line those distances are constant, so a
+//      candidate's match length follows L(i) = T[i] == T[i - d] ? L(i + 1) + 1 : 0
+//      and only a field change costs a forward compare. Tokens never cross a segment
+//      (the cost: one token per ~65 positions). On C4-like text this parse gives
+//      85-94 % of zlib level 9's bytes (tests/test_gpu_txtgz.py measures it);
+//   3. Huffman: length-limited codes from the parse's symbol counts (rank sort over the
+//      workgroup, two-queue merge on one lane), the dynamic header, and the fixed-code
+//      and stored alternatives; the smallest is written;
+//   4. encode: a block scan of the segments' bit counts, each thread writes its bits
+//      (atomic OR only on the words it shares with a neighbour);
+//   5. CRC-32 of the text: per segment (table in LDS), combined up a tree with
+//      GF(2) shift matrices.
+// No shared state between members: the grid is members, nothing is global but the
+// scratch each member owns.
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "mgp_kernels.h"
+#include "mgp_txtgz.h"
+
+namespace mgp {
+namespace txtgz {
+
+constexpr int kT = 256;        // threads per member (one segment each)
+constexpr int kJ = 16;         // previous lines searched for matches
+constexpr int kLMax = 63;      // longest match tried (C4's matches stay below 40)
+constexpr int kRing = 64;      // DP cost ring (> kLMax), u16 costs compared by differences
+constexpr int kMaxDist = 32768;
+constexpr int kLit = 286, kDist = 30;
+
+__constant__ uint16_t c_len_base[29] = {3,  4,  5,  6,  7,  8,  9,  10, 11,  13,  15,  17,  19,  23, 27,
+                                        31, 35, 43, 51, 59, 67, 83, 99, 115, 131, 163, 195, 227, 258};
+__constant__ uint16_t c_dist_base[30] = {1,   2,   3,   4,   5,   7,    9,    13,   17,   25,   33,   49,   65,    97,    129,
+                                         193, 257, 385, 513, 769, 1025, 1537, 2049, 3073, 4097, 6145, 8193, 12289, 16385, 24577};
+
+__constant__ uint8_t c_cl_ord[19] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12, 3, 13, 2, 14, 1, 15};
+
+__device__ __forceinline__ int len_code(int l) {  // 3..258 -> 0..28
+    if (l <= 10) return l - 3;
+    if (l == 258) return 28;
+    const int x = l - 3, n = 31 - __clz(x);
+    return 4 * (n - 1) + ((x >> (n - 2)) & 3);
+}
+__device__ __forceinline__ int len_xb(int c) { return (c < 8 || c == 28) ? 0 : (c >> 2) - 1; }
+__device__ __forceinline__ int dist_code(int d) {  // 1..32768 -> 0..29
+    if (d <= 4) return d - 1;
+    const int x = d - 1, n = 31 - __clz(x);
+    return 2 * n + ((x >> (n - 1)) & 1);
+}
+__device__ __forceinline__ int dist_xb(int c) { return c < 4 ? 0 : (c >> 1) - 1; }
+
+__device__ __forceinline__ uint32_t ndig(uint32_t v) {
+    uint32_t n = 1;
+    while (v >= 10) {
+        v /= 10;
+        ++n;
+    }
+    return n;
+}
+__device__ __forceinline__ uint8_t* put_num(uint8_t* p, uint32_t v, uint32_t nd) {
+    for (uint32_t k = nd; k-- > 0;) {
+        p[k] = (uint8_t)('0' + v % 10);
+        v /= 10;
+    }
+    return p + nd;
+}
+
+// ---- the count rows ----
+__device__ __forceinline__ bool rows16(const Rows& r, int c, int p) {
+    return r.c16 != nullptr && !(r.wide != nullptr && r.wide[(size_t)c * r.nwin + p / r.W]);
+}
+__device__ __forceinline__ uint32_t row_depth(const Rows& r, int c, int p) {
+    const size_t P = (size_t)c * r.L + p;
+    return rows16(r, c, p) ? (uint32_t)r.d16[P] : r.d32[P];
+}
+__device__ __forceinline__ void row_base(const Rows& r, int c, int p, int b, uint32_t& fw, uint32_t& rv) {
+    const size_t P = (size_t)c * r.L + p;
+    if (rows16(r, c, p)) {
+        const uint4 a = r.c16[P];
+        const uint32_t w = b == 0 ? a.x : b == 1 ? a.y : b == 2 ? a.z : a.w;
+        fw = w & 0xFFFFu;
+        rv = w >> 16;
+    } else {
+        fw = r.c32[P * 8 + 2 * b];
+        rv = r.c32[P * 8 + 2 * b + 1];
+    }
+}
+// the line of position p in file f (0 coverage, 1..4 A..T): its length (0: none) and values
+__device__ __forceinline__ uint32_t line_of(const Rows& r, int c, int p, int f, uint32_t bclen, uint32_t& v1,
+                                            uint32_t& v2) {
+    const uint32_t d = row_depth(r, c, p);
+    if (!d) return 0;
+    if (f == 0) {
+        v1 = d;
+        v2 = 0;
+        return ndig((uint32_t)p + 1) + bclen + ndig(d) + 3;
+    }
+    row_base(r, c, p, f - 1, v1, v2);
+    if (!(v1 | v2)) return 0;
+    return ndig((uint32_t)p + 1) + bclen + ndig(v1) + ndig(v2) + 4;
+}
+
+// ---- block-wide helpers (256 threads = 4 waves) ----
+__device__ uint64_t block_excl_scan(uint64_t x, uint64_t* wsum, uint64_t& total) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    uint64_t v = x;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint64_t y = __shfl_up(v, o, 64);
+        if (lane >= o) v += y;
+    }
+    if (lane == 63) wsum[w] = v;
+    __syncthreads();
+    uint64_t base = 0;
+    for (int k = 0; k < w; ++k) base += wsum[k];
+    total = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+    __syncthreads();
+    return base + v - x;
+}
+
+// ---- Huffman code lengths (length-limited), all threads call ----
+struct HuffLds {
+    uint32_t f[kLit];
+    uint16_t order[kLit];
+    uint32_t w[2 * kLit];
+    uint16_t par[2 * kLit];
+    uint8_t dep[2 * kLit];
+    int m, redo;
+};
+// len[s] for s < n from freq[s] (LDS), lengths <= mb; every used symbol gets a code
+__device__ void huff_lengths(const uint32_t* freq, int n, int mb, uint8_t* len, HuffLds& h) {
+    const int t = threadIdx.x;
+    for (int s = t; s < n; s += kT) h.f[s] = freq[s];
+    __syncthreads();
+    for (;;) {
+        if (t == 0) h.m = 0;
+        __syncthreads();
+        // rank sort of the used symbols by (count, symbol)
+        for (int s = t; s < n; s += kT) {
+            const uint32_t fs = h.f[s];
+            if (!fs) continue;
+            int r = 0;
+            for (int q = 0; q < n; ++q) {
+                const uint32_t fq = h.f[q];
+                r += (fq != 0) & ((fq < fs) | ((fq == fs) & (q < s)));
+            }
+            h.order[r] = (uint16_t)s;
+            atomicAdd(&h.m, 1);
+        }
+        __syncthreads();
+        if (t == 0) {
+            const int m = h.m;
+            for (int s = 0; s < n; ++s) len[s] = 0;
+            h.redo = 0;
+            if (m == 1) {
+                len[h.order[0]] = 1;
+            } else if (m > 1) {
+                // two queues: the sorted leaves 0..m-1 and the internal nodes m.. in creation order
+                for (int i = 0; i < m; ++i) h.w[i] = h.f[h.order[i]];
+                int li = 0, ni = m, nn = m;
+                auto take = [&]() -> int {
+                    if (li < m && (ni >= nn || h.w[li] <= h.w[ni])) return li++;
+                    return ni++;
+                };
+                for (int k = 0; k < m - 1; ++k) {
+                    const int a = take(), b = take();
+                    h.w[nn] = h.w[a] + h.w[b];
+                    h.par[a] = (uint16_t)nn;
+                    h.par[b] = (uint16_t)nn;
+                    ++nn;
+                }
+                h.dep[nn - 1] = 0;
+                int mx = 0;
+                for (int x = nn - 2; x >= 0; --x) {
+                    h.dep[x] = (uint8_t)(h.dep[h.par[x]] + 1);
+                    if (x < m && h.dep[x] > mx) mx = h.dep[x];
+                }
+                if (mx > mb) {
+                    for (int s = 0; s < n; ++s) h.f[s] = h.f[s] ? ((h.f[s] >> 1) | 1u) : 0u;
+                    h.redo = 1;
+                } else {
+                    for (int i = 0; i < m; ++i) len[h.order[i]] = h.dep[i];
+                }
+            }
+        }
+        __syncthreads();
+        if (!h.redo) break;
+    }
+}
+
+// canonical codes (bit-reversed for LSB-first output), one thread
+__device__ void canon(const uint8_t* len, int n, uint16_t* code) {
+    uint16_t cnt[16] = {0}, next[16];
+    for (int s = 0; s < n; ++s) cnt[len[s]]++;
+    cnt[0] = 0;
+    uint32_t c = 0;
+    for (int b = 1; b < 16; ++b) {
+        c = (c + cnt[b - 1]) << 1;
+        next[b] = (uint16_t)c;
+    }
+    for (int s = 0; s < n; ++s) {
+        const int l = len[s];
+        code[s] = l ? (uint16_t)(__brev((uint32_t)next[l]++) >> (32 - l)) : 0;
+    }
+}
+
+// ---- the member workgroup's LDS ----
+struct MemberLds {
+    uint64_t wsum[4];
+    uint16_t ring[kT][kRing];
+    uint32_t lit_f[kLit], dist_f[kDist];
+    uint8_t lit_len[kLit], dist_len[kDist];
+    uint16_t lit_code[kLit], dist_code[kDist];
+    uint8_t litcost[256], lencost[kLMax + 1], dcost[kDist];
+    HuffLds h;
+    uint32_t cl_f[19];
+    uint8_t cl_len[19];
+    uint16_t cl_code[19];
+    uint16_t rle[kLit + kDist];  // code-length symbols: sym | extra << 8
+    int n_rle, hlit, hdist, hclen;
+    uint32_t crc_tab[256];
+    uint32_t crc_v[kT];
+    uint32_t crc_n[kT];
+    uint64_t hdr_bits;
+    int mode;  // 0 dynamic, 1 fixed, 2 stored
+};
+
+__device__ __forceinline__ void lds_prices_default(MemberLds& S) {
+    for (int s = threadIdx.x; s < 256; s += kT)
+        S.litcost[s] = (uint8_t)((s >= '0' && s <= '9') || s == ',' ? 4 : s == '\n' ? 5 : 6);
+    for (int l = threadIdx.x; l <= kLMax; l += kT) S.lencost[l] = l < 3 ? 0 : (uint8_t)(7 + len_xb(len_code(l)));
+    for (int c = threadIdx.x; c < kDist; c += kT) S.dcost[c] = (uint8_t)(5 + dist_xb(c));
+}
+__device__ __forceinline__ void lds_prices_from_lengths(MemberLds& S) {
+    for (int s = threadIdx.x; s < 256; s += kT) S.litcost[s] = S.lit_len[s] ? S.lit_len[s] : 16;
+    for (int l = threadIdx.x; l <= kLMax; l += kT) {
+        if (l < 3) {
+            S.lencost[l] = 0;
+            continue;
+        }
+        const int c = len_code(l);
+        S.lencost[l] = (uint8_t)((S.lit_len[257 + c] ? S.lit_len[257 + c] : 16) + len_xb(c));
+    }
+    for (int c = threadIdx.x; c < kDist; c += kT) S.dcost[c] = (uint8_t)((S.dist_len[c] ? S.dist_len[c] : 16) + dist_xb(c));
+}
+
+// forward match length at distance d from i (at most cap)
+__device__ __forceinline__ int fwd_match(const uint8_t* T, int i, int d, int cap) {
+    int L = 0;
+    while (L < cap && T[i + L] == T[i - d + L]) ++L;
+    return L;
+}
+
+// One segment's backward optimal parse: choice[i] = (length << 16) | distance, or 0 for
+// a literal, for i in [t0, t1). Lines [l0, l1) cover exactly [t0, t1).
+__device__ void parse_segment(const uint8_t* T, const uint32_t* lines, uint32_t* choice, int l0, int l1, int t0,
+                              int t1, int nf, uint16_t* ring, const MemberLds& S) {
+    ring[t1 & (kRing - 1)] = 0;
+    for (int k = l1 - 1; k >= l0; --k) {
+        const uint32_t* le = lines + 3 * (size_t)k;
+        const int s = (int)le[0];
+        const int A1 = s + (int)(le[1] & 0xFFFFu), A2 = s + (int)(le[1] >> 16), A3 = s + (int)(le[2] & 0xFFFFu);
+        const int e = s + (int)(le[2] >> 16) - 1;  // the '\n'
+        int dE[kJ], LE[kJ], dF[kJ], LF[kJ];
+#pragma unroll
+        for (int j = 0; j < kJ; ++j) {
+            dE[j] = 0;
+            LE[j] = 0;
+            dF[j] = 0;
+            LF[j] = 0;
+            if (k - j - 1 < 0) continue;
+            const uint32_t* lp = lines + 3 * (size_t)(k - j - 1);
+            const int d = e - ((int)lp[0] + (int)(lp[2] >> 16) - 1);
+            if (d > 0 && d <= kMaxDist) dE[j] = d;
+        }
+        int field = -1;
+        for (int i = e; i >= s; --i) {
+            const int cap = min(kLMax, t1 - i);
+            const int f = (nf > 3 && i >= A3) ? 3 : i >= A2 ? 2 : i >= A1 ? 1 : 0;
+            const uint8_t ti = T[i];
+            if (f != field) {  // entering a field (going backward): its anchor distances, forward compares
+                const int Af = f == 0 ? s : f == 1 ? A1 : f == 2 ? A2 : A3;
+#pragma unroll
+                for (int j = 0; j < kJ; ++j) {
+                    dF[j] = 0;
+                    LF[j] = 0;
+                    if (k - j - 1 < 0) continue;
+                    const uint32_t* lp = lines + 3 * (size_t)(k - j - 1);
+                    const int sp = (int)lp[0];
+                    const int Bf = f == 0 ? sp
+                                 : f == 1 ? sp + (int)(lp[1] & 0xFFFFu)
+                                 : f == 2 ? sp + (int)(lp[1] >> 16)
+                                          : sp + (int)(lp[2] & 0xFFFFu);
+                    const int d = Af - Bf;
+                    if (d > 0 && d <= kMaxDist && d != dE[j]) {
+                        dF[j] = d;
+                        LF[j] = fwd_match(T, i, d, cap);
+                    }
+                }
+                if (field < 0) {
+#pragma unroll
+                    for (int j = 0; j < kJ; ++j)
+                        if (dE[j]) LE[j] = fwd_match(T, i, dE[j], cap);
+                } else {
+#pragma unroll
+                    for (int j = 0; j < kJ; ++j)
+                        if (dE[j]) LE[j] = (i >= dE[j] && T[i - dE[j]] == ti) ? min(LE[j] + 1, cap) : 0;
+                }
+                field = f;
+            } else {
+                // (a field-anchored source stays inside the earlier line's field: i - dF >= 0;
+                // an end-anchored one can run off the member's start when that line is short)
+#pragma unroll
+                for (int j = 0; j < kJ; ++j) {
+                    if (dF[j]) LF[j] = (T[i - dF[j]] == ti) ? min(LF[j] + 1, cap) : 0;
+                    if (dE[j]) LE[j] = (i >= dE[j] && T[i - dE[j]] == ti) ? min(LE[j] + 1, cap) : 0;
+                }
+            }
+            // relaxation: costs relative to cost[i + 1] (u16 ring, differences stay small)
+            const uint16_t c1 = ring[(i + 1) & (kRing - 1)];
+            int best = S.litcost[ti];
+            uint32_t ch = 0;
+            int lo = 3;
+#pragma unroll
+            for (int j = 0; j < kJ; ++j) {
+#pragma unroll
+                for (int q = 0; q < 2; ++q) {
+                    const int L = q ? LE[j] : LF[j];
+                    if (L < lo) continue;
+                    const int d = q ? dE[j] : dF[j];
+                    const int dc = S.dcost[dist_code(d)];
+                    for (int l = lo; l <= L; ++l) {
+                        const int v = (int)S.lencost[l] + dc + (int)(int16_t)(uint16_t)(ring[(i + l) & (kRing - 1)] - c1);
+                        if (v < best) {
+                            best = v;
+                            ch = ((uint32_t)l << 16) | (uint32_t)d;
+                        }
+                    }
+                    lo = L + 1;
+                }
+            }
+            ring[i & (kRing - 1)] = (uint16_t)(c1 + best);
+            choice[i] = ch;
+        }
+    }
+}
+
+// zero-byte CRC operator applied n times (GF(2) matrices M[b] = one-byte operator ^ 2^b)
+__device__ uint32_t crc_shift(uint32_t c, uint64_t n, const uint32_t* M) {
+    for (int b = 0; n && b < 25; ++b, n >>= 1) {
+        if (!(n & 1)) continue;
+        const uint32_t* m = M + 32 * b;
+        uint32_t r = 0;
+        for (int k = 0; k < 32; ++k)
+            if ((c >> k) & 1u) r ^= m[k];
+        c = r;
+    }
+    return c;
+}
+
+// bit writer over the member's u32 words: atomics on the words shared with neighbours
+struct BitW {
+    uint32_t* w;
+    uint64_t word;
+    uint64_t acc;
+    int n;
+    bool first;
+    __device__ BitW(uint32_t* out, uint64_t bit) : w(out), word(bit >> 5), acc(0), n((int)(bit & 31)), first(true) {}
+    __device__ void put(uint32_t v, int nb) {
+        acc |= (uint64_t)v << n;
+        n += nb;
+        while (n >= 32) {
+            if (first) atomicOr(&w[word], (uint32_t)acc);
+            else w[word] = (uint32_t)acc;
+            first = false;
+            ++word;
+            acc >>= 32;
+            n -= 32;
+        }
+    }
+    __device__ void done() {
+        if (n > 0) atomicOr(&w[word], (uint32_t)acc);
+    }
+};
+
+__device__ __forceinline__ void put_token(BitW& bw, uint32_t tk, const uint16_t* lc, const uint8_t* ll, const uint16_t* dcd,
+                                          const uint8_t* dl) {
+    const uint32_t l = tk >> 16;
+    if (!l) {
+        bw.put(lc[tk], ll[tk]);
+        return;
+    }
+    const int d = (int)(tk & 0xFFFFu);
+    const int c = len_code((int)l), xb = len_xb(c);
+    bw.put(lc[257 + c], ll[257 + c]);
+    if (xb) bw.put(l - c_len_base[c], xb);
+    const int e = dist_code(d), yb = dist_xb(e);
+    bw.put(dcd[e], dl[e]);
+    if (yb) bw.put((uint32_t)(d - c_dist_base[e]), yb);
+}
+__device__ __forceinline__ uint32_t token_bits(uint32_t tk, const uint8_t* ll, const uint8_t* dl) {
+    const uint32_t l = tk >> 16;
+    if (!l) return ll[tk];
+    const int c = len_code((int)l), e = dist_code((int)(tk & 0xFFFFu));
+    return ll[257 + c] + len_xb(c) + dl[e] + dist_xb(e);
+}
+__device__ __forceinline__ uint8_t fixed_len(int s) { return s < 144 ? 8 : s < 256 ? 9 : s < 280 ? 7 : 8; }
+
+// ---------------------------------------------------------------------------
+// kernels
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(kT) k_txt_sizes(Job job, uint64_t* __restrict__ sizes, uint64_t* __restrict__ nlines) {
+    __shared__ unsigned long long acc[2 * kFiles];
+    const int k = blockIdx.x, t = threadIdx.x;
+    if (t < 2 * kFiles) acc[t] = 0;
+    __syncthreads();
+    const int c = job.cells[k];
+    const uint32_t bclen = (uint32_t)(job.name_off[k + 1] - job.name_off[k]);
+    uint64_t b[kFiles] = {0, 0, 0, 0, 0};
+    uint32_t n[kFiles] = {0, 0, 0, 0, 0};
+    for (int p = t; p < job.rows.L; p += kT) {
+        for (int f = 0; f < kFiles; ++f) {
+            uint32_t v1, v2;
+            const uint32_t len = line_of(job.rows, c, p, f, bclen, v1, v2);
+            if (!len) {
+                if (f == 0) break;  // depth 0: no line in any file
+                continue;
+            }
+            b[f] += len;
+            ++n[f];
+        }
+    }
+    for (int f = 0; f < kFiles; ++f) {
+        atomicAdd(&acc[f], (unsigned long long)b[f]);
+        atomicAdd(&acc[kFiles + f], (unsigned long long)n[f]);
+    }
+    __syncthreads();
+    if (t < kFiles) {
+        sizes[(size_t)t * job.n + k] = acc[t];
+        nlines[(size_t)t * job.n + k] = acc[kFiles + t];
+    }
+}
+
+__global__ void __launch_bounds__(kT) k_txt_gz(Job job, Scratch sc) {
+    __shared__ MemberLds S;
+    const int t = threadIdx.x;
+    const int64_t m = blockIdx.x;
+    const int f = (int)(m / job.n);
+    const int64_t kc = m - (int64_t)f * job.n;
+    const int c = job.cells[kc];
+    const char* bc = job.names + job.name_off[kc];
+    const uint32_t bclen = (uint32_t)(job.name_off[kc + 1] - job.name_off[kc]);
+    const int L = job.rows.L;
+    const int nf = f ? 4 : 3;
+    uint8_t* const T = sc.text + sc.text_off[m];
+    uint32_t* const lines = sc.lines + 3 * sc.line_off[m];
+    uint32_t* const tok = sc.tok + sc.text_off[m];
+    const uint64_t n_text = sc.text_off[m + 1] - sc.text_off[m];
+    uint32_t* const out = sc.out + sc.out_off[m] / 4;
+    if (n_text == 0) {  // no line: no member
+        if (t == 0) sc.member_bytes[m] = 0;
+        return;
+    }
+    for (int s = t; s < 256; s += kT) {
+        uint32_t r = (uint32_t)s;
+        for (int b = 0; b < 8; ++b) r = (r >> 1) ^ (0xEDB88320u & (0u - (r & 1u)));
+        S.crc_tab[s] = r;
+    }
+    // ---- 1. format ----
+    const int P = (L + kT - 1) / kT;
+    const int p0 = min(L, t * P), p1 = min(L, p0 + P);
+    uint32_t my_b = 0, my_n = 0;
+    for (int p = p0; p < p1; ++p) {
+        uint32_t v1, v2;
+        const uint32_t len = line_of(job.rows, c, p, f, bclen, v1, v2);
+        my_b += len;
+        my_n += len != 0;
+    }
+    uint64_t tot;
+    const uint64_t pre = block_excl_scan(((uint64_t)my_b << 24) | my_n, S.wsum, tot);
+    const int t0 = (int)(pre >> 24), t1 = t0 + (int)my_b;
+    const int l0 = (int)(pre & 0xFFFFFFu), l1 = l0 + (int)my_n;
+    {
+        uint8_t* w = T + t0;
+        int k = l0;
+        for (int p = p0; p < p1; ++p) {
+            uint32_t v1 = 0, v2 = 0;
+            const uint32_t len = line_of(job.rows, c, p, f, bclen, v1, v2);
+            if (!len) continue;
+            uint8_t* const s = w;
+            w = put_num(w, (uint32_t)p + 1, ndig((uint32_t)p + 1));
+            const uint32_t c1 = (uint32_t)(w - s);
+            *w++ = ',';
+            for (uint32_t q = 0; q < bclen; ++q) w[q] = (uint8_t)bc[q];
+            w += bclen;
+            const uint32_t c2 = (uint32_t)(w - s);
+            *w++ = ',';
+            w = put_num(w, v1, ndig(v1));
+            uint32_t c3 = 0;
+            if (f) {
+                c3 = (uint32_t)(w - s);
+                *w++ = ',';
+                w = put_num(w, v2, ndig(v2));
+            }
+            *w++ = '\n';
+            uint32_t* le = lines + 3 * (size_t)k++;
+            le[0] = (uint32_t)(s - T);
+            le[1] = c1 | (c2 << 16);
+            le[2] = c3 | (len << 16);
+        }
+    }
+    __threadfence_block();
+    __syncthreads();
+    // CRC of the segment (raw: init 0, no final xor)
+    {
+        uint32_t r = 0;
+        for (int i = t0; i < t1; ++i) r = S.crc_tab[(r ^ T[i]) & 0xFFu] ^ (r >> 8);
+        S.crc_v[t] = r;
+        S.crc_n[t] = my_b;
+    }
+    // ---- 2. parse, twice ----
+    uint32_t ntok = 0;
+    lds_prices_default(S);
+    for (int pass = 0; pass < 2; ++pass) {
+        for (int s = t; s < kLit; s += kT) S.lit_f[s] = 0;
+        if (t < kDist) S.dist_f[t] = 0;
+        __syncthreads();
+        if (my_b) parse_segment(T, lines, tok, l0, l1, t0, t1, nf, S.ring[t], S);
+        // traceback: the chosen tokens (pass 2 stores them over the choices, compacted)
+        int nt = 0;
+        for (int i = t0; i < t1;) {
+            const uint32_t ch = tok[i];
+            const uint32_t l = ch >> 16;
+            if (!l) {
+                atomicAdd(&S.lit_f[T[i]], 1u);
+                if (pass) tok[t0 + nt] = T[i];
+                ++i;
+            } else {
+                atomicAdd(&S.lit_f[257 + len_code((int)l)], 1u);
+                atomicAdd(&S.dist_f[dist_code((int)(ch & 0xFFFFu))], 1u);
+                if (pass) tok[t0 + nt] = ch;
+                i += (int)l;
+            }
+            ++nt;
+        }
+        if (t == 0) S.lit_f[256] = 1;  // end of block
+        __syncthreads();
+        huff_lengths(S.lit_f, kLit, 15, S.lit_len, S.h);
+        huff_lengths(S.dist_f, kDist, 15, S.dist_len, S.h);
+        if (!pass) {
+            lds_prices_from_lengths(S);
+            __syncthreads();
+        } else {
+            ntok = (uint32_t)nt;
+        }
+    }
+    // ---- 3. codes and the header ----
+    if (t == 0) {
+        // a complete distance code: at least two used lengths (one used or none -> codes 0 and 1)
+        int used = 0;
+        for (int s = 0; s < kDist; ++s) used += S.dist_len[s] != 0;
+        if (used < 2) {
+            int a = -1;
+            for (int s = 0; s < kDist; ++s)
+                if (S.dist_len[s]) a = s;
+            for (int s = 0; s < kDist; ++s) S.dist_len[s] = 0;
+            if (a < 0) a = 0;
+            S.dist_len[a] = 1;
+            S.dist_len[a == 0 ? 1 : 0] = 1;
+        }
+        canon(S.lit_len, kLit, S.lit_code);
+        canon(S.dist_len, kDist, S.dist_code);
+        int hl = 257;
+        for (int s = 257; s < kLit; ++s)
+            if (S.lit_len[s]) hl = s + 1;
+        int hd = 1;
+        for (int s = 0; s < kDist; ++s)
+            if (S.dist_len[s]) hd = s + 1;
+        S.hlit = hl;
+        S.hdist = hd;
+        // run-length code of the lengths (16: repeat previous 3-6, 17: zeros 3-10, 18: zeros 11-138)
+        int nr = 0;
+        for (int s = 0; s < 19; ++s) S.cl_f[s] = 0;
+        const int na = hl + hd;
+        for (int i = 0; i < na;) {
+            const int v = i < hl ? S.lit_len[i] : S.dist_len[i - hl];
+            int r = 1;
+            while (i + r < na && (i + r < hl ? S.lit_len[i + r] : S.dist_len[i + r - hl]) == v) ++r;
+            if (v == 0 && r >= 3) {
+                const int q = min(r, 138);
+                S.rle[nr++] = q >= 11 ? (uint16_t)(18 | (q - 11) << 8) : (uint16_t)(17 | (q - 3) << 8);
+                S.cl_f[q >= 11 ? 18 : 17]++;
+                i += q;
+            } else if (v != 0 && r >= 4) {
+                S.rle[nr++] = (uint16_t)v;
+                S.cl_f[v]++;
+                const int q = min(r - 1, 6);
+                S.rle[nr++] = (uint16_t)(16 | (q - 3) << 8);
+                S.cl_f[16]++;
+                i += 1 + q;
+            } else {
+                S.rle[nr++] = (uint16_t)v;
+                S.cl_f[v]++;
+                ++i;
+            }
+        }
+        S.n_rle = nr;
+    }
+    __syncthreads();
+    huff_lengths(S.cl_f, 19, 7, S.cl_len, S.h);
+    if (t == 0) {
+        // (a code-length code with one symbol: add a second so the code is complete)
+        int used = 0, a = -1;
+        for (int s = 0; s < 19; ++s)
+            if (S.cl_len[s]) {
+                ++used;
+                a = s;
+            }
+        if (used == 1) S.cl_len[a == 0 ? 1 : 0] = 1;
+        canon(S.cl_len, 19, S.cl_code);
+        int hc = 4;
+        for (int i = 0; i < 19; ++i)
+            if (S.cl_len[c_cl_ord[i]]) hc = max(hc, i + 1);
+        S.hclen = hc;
+        uint64_t hb = 3 + 5 + 5 + 4 + 3 * (uint64_t)hc;
+        for (int i = 0; i < S.n_rle; ++i) {
+            const int sym = S.rle[i] & 0xFF;
+            hb += S.cl_len[sym] + (sym == 16 ? 2 : sym == 17 ? 3 : sym == 18 ? 7 : 0);
+        }
+        S.hdr_bits = hb;
+    }
+    __syncthreads();
+    // ---- 4. sizes of the three block kinds, then the encoder ----
+    uint64_t dyn_b = 0, fix_b = 0;
+    for (uint32_t q = 0; q < ntok; ++q) {
+        const uint32_t tk = tok[t0 + q];
+        dyn_b += token_bits(tk, S.lit_len, S.dist_len);
+        const uint32_t l = tk >> 16;
+        if (!l) fix_b += fixed_len((int)tk);
+        else {
+            const int cc = len_code((int)l), e = dist_code((int)(tk & 0xFFFFu));
+            fix_b += fixed_len(257 + cc) + len_xb(cc) + 5 + dist_xb(e);
+        }
+    }
+    if (t == kT - 1) {
+        dyn_b += S.lit_len[256];
+        fix_b += 7;
+    }
+    uint64_t dyn_tot, fix_tot;
+    const uint64_t dyn_pre = block_excl_scan(dyn_b, S.wsum, dyn_tot);
+    const uint64_t fix_pre = block_excl_scan(fix_b, S.wsum, fix_tot);
+    const uint64_t dyn_bytes = (S.hdr_bits + dyn_tot + 7) / 8;
+    const uint64_t fix_bytes = (3 + fix_tot + 7) / 8;
+    const uint64_t n_blk = n_text / 65535 + 1;
+    const uint64_t sto_bytes = n_text + 5 * n_blk;
+    const int mode = (dyn_bytes <= fix_bytes && dyn_bytes <= sto_bytes) ? 0 : (fix_bytes <= sto_bytes ? 1 : 2);
+    const uint64_t blk_bytes = mode == 0 ? dyn_bytes : mode == 1 ? fix_bytes : sto_bytes;
+    const uint64_t region = out_bound(n_text) / 4;
+    for (uint64_t q = t; q < region; q += kT) out[q] = 0;
+    __threadfence_block();
+    __syncthreads();
+    uint8_t* const ob = reinterpret_cast<uint8_t*>(out);
+    if (t == 0) {  // gzip header: magic, deflate, no flags, mtime 0, xfl 2, os 255
+        out[0] = 0x00088B1Fu;
+        out[1] = 0;
+        atomicOr(&out[2], 0xFF02u);
+    }
+    if (mode == 0) {
+        if (t == 0) {
+            BitW bw(out, 80);
+            bw.put(1, 1);  // BFINAL
+            bw.put(2, 2);  // dynamic
+            bw.put((uint32_t)(S.hlit - 257), 5);
+            bw.put((uint32_t)(S.hdist - 1), 5);
+            bw.put((uint32_t)(S.hclen - 4), 4);
+            for (int i = 0; i < S.hclen; ++i) bw.put(S.cl_len[c_cl_ord[i]], 3);
+            for (int i = 0; i < S.n_rle; ++i) {
+                const int sym = S.rle[i] & 0xFF, x = S.rle[i] >> 8;
+                bw.put(S.cl_code[sym], S.cl_len[sym]);
+                if (sym == 16) bw.put((uint32_t)x, 2);
+                else if (sym == 17) bw.put((uint32_t)x, 3);
+                else if (sym == 18) bw.put((uint32_t)x, 7);
+            }
+            bw.done();
+        }
+        BitW bw(out, 80 + S.hdr_bits + dyn_pre);
+        for (uint32_t q = 0; q < ntok; ++q) put_token(bw, tok[t0 + q], S.lit_code, S.lit_len, S.dist_code, S.dist_len);
+        if (t == kT - 1) bw.put(S.lit_code[256], S.lit_len[256]);
+        bw.done();
+    } else if (mode == 1) {
+        // the fixed codes (RFC 1951 3.2.6), canonical from their lengths
+        if (t == 0) {
+            for (int s = 0; s < 288 && s < kLit; ++s) S.lit_len[s] = fixed_len(s);
+            for (int s = 0; s < kDist; ++s) S.dist_len[s] = 5;
+            canon(S.lit_len, kLit, S.lit_code);
+            canon(S.dist_len, kDist, S.dist_code);
+            BitW bw(out, 80);
+            bw.put(1, 1);
+            bw.put(1, 2);  // fixed
+            bw.done();
+        }
+        __syncthreads();
+        BitW bw(out, 80 + 3 + fix_pre);
+        for (uint32_t q = 0; q < ntok; ++q) put_token(bw, tok[t0 + q], S.lit_code, S.lit_len, S.dist_code, S.dist_len);
+        if (t == kT - 1) bw.put(S.lit_code[256], S.lit_len[256]);
+        bw.done();
+    } else {
+        // stored blocks of <= 65535 bytes: BFINAL/BTYPE byte, LEN, NLEN, the bytes
+        for (uint64_t b = t; b < n_blk; b += kT) {
+            const uint64_t o = 10 + b * (65535 + 5);
+            const uint64_t left = n_text - b * 65535;
+            const uint32_t len = (uint32_t)(left < 65535 ? left : 65535);
+            ob[o] = b + 1 == n_blk ? 1 : 0;
+            ob[o + 1] = (uint8_t)len;
+            ob[o + 2] = (uint8_t)(len >> 8);
+            ob[o + 3] = (uint8_t)~len;
+            ob[o + 4] = (uint8_t)(~len >> 8);
+        }
+        for (uint64_t x = t; x < n_text; x += kT) ob[10 + 5 * (x / 65535 + 1) + x] = T[x];
+    }
+    // ---- 5. CRC-32 of the text (segments combined up a tree), trailer ----
+    for (int s = 1; s < kT; s <<= 1) {
+        __syncthreads();
+        uint32_t v = 0, nn = 0;
+        const bool act = (t % (2 * s)) == 0 && t + s < kT;
+        if (act) {
+            v = crc_shift(S.crc_v[t], S.crc_n[t + s], sc.crc_shift) ^ S.crc_v[t + s];
+            nn = S.crc_n[t] + S.crc_n[t + s];
+        }
+        __syncthreads();
+        if (act) {
+            S.crc_v[t] = v;
+            S.crc_n[t] = nn;
+        }
+    }
+    __threadfence_block();
+    __syncthreads();
+    if (t == 0) {
+        const uint32_t crc = S.crc_v[0] ^ crc_shift(0xFFFFFFFFu, n_text, sc.crc_shift) ^ 0xFFFFFFFFu;
+        const uint64_t o = 10 + blk_bytes;
+        const uint32_t isz = (uint32_t)n_text;
+        for (int q = 0; q < 4; ++q) {
+            ob[o + q] = (uint8_t)(crc >> (8 * q));
+            ob[o + 4 + q] = (uint8_t)(isz >> (8 * q));
+        }
+        sc.member_bytes[m] = (uint32_t)(o + 8);
+    }
+}
+
+__global__ void __launch_bounds__(kT) k_txt_pack(const uint32_t* __restrict__ out, const uint64_t* __restrict__ out_off,
+                                                 const uint32_t* __restrict__ member_bytes,
+                                                 const uint64_t* __restrict__ dst_off, uint8_t* __restrict__ dst) {
+    const int64_t m = blockIdx.x;
+    const uint8_t* src = reinterpret_cast<const uint8_t*>(out) + out_off[m];
+    uint8_t* d = dst + dst_off[m];
+    const uint32_t n = member_bytes[m];
+    for (uint32_t q = threadIdx.x; q < n; q += kT) d[q] = src[q];
+}
+
+// ---------------------------------------------------------------------------
+// host side
+// ---------------------------------------------------------------------------
+int txt_sizes(const Job& job, uint64_t* sizes, uint64_t* nlines, hipStream_t s) {
+    if (job.n <= 0) return 0;
+    k_txt_sizes<<<(unsigned)job.n, kT, 0, s>>>(job, sizes, nlines);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+int txt_deflate(const Job& job, const Scratch& sc, hipStream_t s) {
+    if (job.n <= 0) return 0;
+    k_txt_gz<<<(unsigned)(kFiles * job.n), kT, 0, s>>>(job, sc);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+int txt_pack(const Scratch& sc, int64_t n_members, const uint64_t* dst_off, uint8_t* dst, hipStream_t s) {
+    if (n_members <= 0) return 0;
+    k_txt_pack<<<(unsigned)n_members, kT, 0, s>>>(sc.out, sc.out_off, sc.member_bytes, dst_off, dst);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+void crc_shift_matrices(uint32_t* M) {
+    uint32_t tab[256];
+    for (uint32_t s = 0; s < 256; ++s) {
+        uint32_t r = s;
+        for (int b = 0; b < 8; ++b) r = (r >> 1) ^ (0xEDB88320u & (0u - (r & 1u)));
+        tab[s] = r;
+    }
+    for (int k = 0; k < 32; ++k) {  // one zero byte: c -> tab[c & 0xFF] ^ (c >> 8)
+        const uint32_t c = 1u << k;
+        M[k] = tab[c & 0xFFu] ^ (c >> 8);
+    }
+    for (int b = 1; b < 25; ++b) {  // M[b] = M[b-1] o M[b-1]
+        const uint32_t* A = M + 32 * (b - 1);
+        uint32_t* B = M + 32 * b;
+        for (int k = 0; k < 32; ++k) {
+            uint32_t v = A[k], r = 0;
+            for (int q = 0; q < 32; ++q)
+                if ((v >> q) & 1u) r ^= A[q];
+            B[k] = r;
+        }
+    }
+}
+
+}  // namespace txtgz
+}  // namespace mgp

@@ -39,9 +39,9 @@ ABI_SYMBOLS = (
     "mgp_finish", "mgp_kernel_times", "mgp_comm_unique_id", "mgp_comm_init", "mgp_synth_generate",
     "mgp_download_inputs", "mgp_set_stage_timing", "mgp_fetch_cells", "mgp_fetch_rows16", "mgp_windows",
     "mgp_stream_info", "mgp_set_streaming", "mgp_set_rows16_target", "mgp_copy_wait", "mgp_set_cell_range",
-    "mgp_push_batch16",
+    "mgp_push_batch16", "mgp_txt_gz_run", "mgp_txt_gz_fetch", "mgp_txt_gz_rows",
 )
-ABI_VERSION = 5
+ABI_VERSION = 6
 CFG_KEEP_TN5 = 0x1
 CFG_STREAM = 0x2
 
@@ -146,6 +146,17 @@ class mgp_synth_params(C.Structure):
     ]
 
 
+class mgp_txt_gz(C.Structure):
+    _fields_ = [
+        ("n_cells", C.c_int64),
+        ("cells", C.c_void_p),
+        ("names", C.c_void_p),
+        ("name_off", C.c_void_p),
+        ("member_bytes", C.c_void_p),
+        ("text_bytes", C.c_void_p),
+    ]
+
+
 class mgp_rows16(C.Structure):
     _fields_ = [
         ("counts", C.c_void_p),
@@ -203,6 +214,9 @@ def load_library(path: Path | None = None) -> C.CDLL:
         "mgp_set_streaming": ([vp, C.c_int], C.c_int),
         "mgp_set_cell_range": ([vp, C.c_int32, C.c_int32], C.c_int),
         "mgp_copy_wait": ([vp], C.c_int),
+        "mgp_txt_gz_run": ([vp, C.POINTER(mgp_txt_gz), C.POINTER(i64)], C.c_int),
+        "mgp_txt_gz_fetch": ([vp, vp, i64], C.c_int),
+        "mgp_txt_gz_rows": ([C.c_int, vp, vp, i32, i32, C.POINTER(mgp_txt_gz), vp, i64, C.POINTER(i64)], C.c_int),
     }
     for name, (args, res) in sig.items():
         fn = getattr(lib, name)
@@ -347,6 +361,61 @@ def batch_struct(soa: ReadSoA) -> mgp_batch:
         soa.n, _ptr(soa.start), _ptr(soa.bc), _ptr(soa.tlen), _ptr(soa.flag), _ptr(soa.mapq), _ptr(soa.span),
         _ptr(soa.rec_off), _ptr(soa.payload), int(soa.payload.shape[0]),
     )
+
+
+TXT_FILES = ("coverage", "A", "C", "G", "T")  # the member order of mgp_txt_gz (file-major)
+
+
+@dataclass
+class TxtMembers:
+    """The gzip members of mgp_txt_gz: `blob` holds them file-major (all coverage
+    members in cell order, then A, C, G, T); member_bytes / text_bytes are [5, n]."""
+
+    blob: np.ndarray
+    member_bytes: np.ndarray
+    text_bytes: np.ndarray
+
+    def file_part(self, f: int) -> np.ndarray:
+        """The bytes of file f (0 coverage, 1..4 A..T): its members back to back."""
+        per = self.member_bytes.sum(axis=1)
+        a = int(per[:f].sum())
+        return self.blob[a:a + int(per[f])]
+
+
+def _txt_job(cells, names: list[str]):
+    cells = np.ascontiguousarray(cells, dtype=np.int32)
+    enc = [n.encode() for n in names]
+    if len(enc) != cells.shape[0]:
+        raise InvalidInputError("one barcode per written cell")
+    off = np.zeros(len(enc) + 1, np.int64)
+    off[1:] = np.cumsum([len(b) for b in enc])
+    blob = np.frombuffer(b"".join(enc) or b"\0", np.uint8)
+    n = cells.shape[0]
+    mb = np.zeros((5, n), np.int64)
+    tb = np.zeros((5, n), np.int64)
+    job = mgp_txt_gz(n, _ptr(cells), _ptr(blob), _ptr(off), _ptr(mb), _ptr(tb))
+    return job, (cells, blob, off), mb, tb
+
+
+def txt_gz_rows(counts: np.ndarray, depth: np.ndarray, cells, names: list[str], device: int = 0) -> TxtMembers:
+    """mgp_txt_gz_rows: the txt members of `cells` from caller-supplied u32 rows
+    (counts [n, L, 8], depth [n, L]), no engine context."""
+    lib = load_library()
+    counts = np.ascontiguousarray(counts, np.uint32)
+    depth = np.ascontiguousarray(depth, np.uint32)
+    n_rows, L = depth.shape
+    if counts.shape != (n_rows, L, 8):
+        raise InvalidInputError("counts must be [n, L, 8]")
+    job, keep, mb, tb = _txt_job(cells, names)
+    # a bound: every member's text (<= bc + 29 bytes per covered position) plus stored-block overhead
+    nnz = np.count_nonzero(depth, axis=1)[np.asarray(keep[0], np.int64)] if len(names) else np.zeros(0, np.int64)
+    text = nnz.astype(np.int64) * (np.diff(keep[2]) + 29)
+    cap = int((5 * (text + 5 * (text // 65535 + 1) + 96)).sum()) + 64
+    out = np.empty(cap, np.uint8)
+    tot = C.c_int64()
+    _ck(lib.mgp_txt_gz_rows(int(device), _ptr(counts), _ptr(depth), int(n_rows), int(L), C.byref(job), _ptr(out), cap,
+                            C.byref(tot)), "mgp_txt_gz_rows")
+    return TxtMembers(out[:int(tot.value)], mb, tb)
 
 
 class Engine:
@@ -496,6 +565,20 @@ class Engine:
             return self.fetch(dense=True)
         res.counts, res.tn5, res.depth = r16.counts, r16.tn5, r16.depth
         return res
+
+    def txt_gz(self, cells, names: list[str], out: np.ndarray | None = None) -> TxtMembers:
+        """mgp_txt_gz_run + mgp_txt_gz_fetch: the txt count files' gzip members of the run's
+        `cells` (context cell indices, in output order) named `names`, formatted and
+        deflated on the device (writers.py:430-486). `out`: where the members go (e.g. a
+        pinned buffer's view, large enough); a new array otherwise."""
+        job, keep, mb, tb = _txt_job(cells, names)
+        tot = C.c_int64()
+        _ck(self.lib.mgp_txt_gz_run(self._h, C.byref(job), C.byref(tot)), "mgp_txt_gz_run")
+        n = int(tot.value)
+        if out is None or out.shape[0] < n:
+            out = np.empty(max(1, n), np.uint8)
+        _ck(self.lib.mgp_txt_gz_fetch(self._h, _ptr(out), int(out.shape[0])), "mgp_txt_gz_fetch")
+        return TxtMembers(out[:n], mb, tb)
 
     def windows(self) -> tuple[int, int]:
         nw, w = C.c_int32(), C.c_int32()

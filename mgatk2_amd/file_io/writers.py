@@ -138,8 +138,11 @@ class IncrementalTextWriter:
             q = cell_qc(res, c, names[c], L)
             self.cell_stats.append(q)
             self.cell_depths[names[c]] = q["mean_depth"]
-        txt_write_cells(self.prefix, res.counts, res.depth, cells, [names[c] for c in cells.tolist()],
-                        level=self.gzip_level, n_threads=self.n_threads)
+        done = getattr(res, "txt_gz_cells", None)
+        if done is None or not np.array_equal(np.asarray(done, np.int64), cells):
+            txt_write_cells(self.prefix, res.counts, res.depth, cells, [names[c] for c in cells.tolist()],
+                            level=self.gzip_level, n_threads=self.n_threads)
+        # (else the count files were written on the device: CellProcessor.enable_device_txt)
         if tally is not None:
             self.position_base_counts += tally.astype(np.int64)
         else:

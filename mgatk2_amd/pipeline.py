@@ -142,6 +142,12 @@ class MtDNAPipeline:
         logger.info("Collecting reads from BAM by barcode...")
         reader = BAMReader(str(self.bam_path), self.config, self.barcode_list)
         processor = CellProcessor(self.config, self.output_dir, device=self.device, devices=self.devices)
+        txt_writer = None
+        if self.output_format != "hdf5":
+            # the count files are written from the devices' rows at the end of the run
+            # (mgp_txt_gz): the writer's files exist before it
+            txt_writer = IncrementalTextWriter(self.output_dir, self.config, self.barcode_list)
+            processor.enable_device_txt(txt_writer.prefix, self.barcode_list)
         if self.stream:
             # one pass: batches decoded on a producer thread, each pushed to the device as
             # it is ready, the windows piled as their reads arrive (readers.py:84-93)
@@ -178,7 +184,7 @@ class MtDNAPipeline:
             writer = IncrementalHDF5Writer(self.output_dir, self.config, self.barcode_list,
                                            barcode_metadata=self.barcode_metadata)
         else:
-            writer = IncrementalTextWriter(self.output_dir, self.config, self.barcode_list)
+            writer = txt_writer
         cell_results = processor.write_results(res, self.barcode_list, writer)
         if not cell_results:
             logger.error("No cells passed quality filters")

@@ -24,7 +24,7 @@ from queue import Queue
 
 import numpy as np
 
-from ..engine import Engine, EngineResult, PinnedBuffer, Rows16
+from ..engine import TXT_FILES, Engine, EngineResult, PinnedBuffer, Rows16
 from ..synth import ReadSoA, pack_reads
 from .pileup import result_dict, simple_reads_to_dicts
 
@@ -36,6 +36,8 @@ MP_CONTEXT = "spawn"  # kept for API compatibility (processors.py:17); no proces
 # MGP_STREAM_SLOTS override them, read at each run)
 STREAM_BATCH_READS = 4_000_000
 STREAM_SLOTS = 3
+# cells per mgp_txt_gz call (its device scratch is ~7 GB per 1000 C4 cells)
+TXT_CHUNK_CELLS = 2048
 
 
 def _engine_config_for(config, n_cells: int, dedup: bool):
@@ -109,6 +111,76 @@ class CellProcessor:
         self.last_result: EngineResult | None = None
         self.last_stats: dict = {}
         self.last_timing: dict = {}
+        self.txt_out = None
+
+    # txt output on the device ----------------------------------------------
+    def enable_device_txt(self, prefix, names: list[str]):
+        """Write the txt count files (`prefix`.{coverage,A,C,G,T}.txt.gz, appended) from
+        the devices' rows before their contexts close: each passing cell's lines
+        formatted and deflated on its device (mgp_txt_gz, writers.py:430-486), only the
+        gzip members cross the link. The run's result then carries `txt_gz_cells`, the
+        cells written, and IncrementalTextWriter.write_cells writes only the rest
+        (stats, depth table, reference alleles). MGP_TXT_DEVICE=0, or a gzip level other
+        than the reference's 9 (MGP_GZIP_LEVEL), keeps the host formatter."""
+        self.txt_out = (str(prefix), list(names))
+
+    def _txt_device_on(self) -> bool:
+        if self.txt_out is None or os.environ.get("MGP_TXT_DEVICE", "1") == "0":
+            return False
+        return os.environ.get("MGP_GZIP_LEVEL", "9") == "9"
+
+    def _write_txt(self, res: EngineResult, parts: list) -> float:
+        """The passing cells in first-seen order (processors.py:75's write order) through
+        mgp_txt_gz on their devices; parts = [(engine, lo, hi)], each engine holding the
+        cells [lo, hi) as its 0..hi-lo. Members of cells on different devices are
+        interleaved back into the global order. Returns the seconds spent."""
+        t0 = time.perf_counter()
+        prefix, names = self.txt_out
+        written = cells_written(res)
+        his = np.array([hi for _, _, hi in parts], np.int64)
+        files = [open(f"{prefix}.{f}.txt.gz", "ab") for f in TXT_FILES]
+        pool = None
+        try:
+            if len(parts) > 1:
+                from concurrent.futures import ThreadPoolExecutor
+
+                pool = ThreadPoolExecutor(len(parts))
+            for a in range(0, written.size, TXT_CHUNK_CELLS):
+                chunk = written[a:a + TXT_CHUNK_CELLS]
+                dev = np.searchsorted(his, chunk, side="right")  # each cell's part
+                sels = [chunk[dev == d] for d in range(len(parts))]
+
+                def one(d):
+                    eng, lo, _ = parts[d]
+                    sel = sels[d]
+                    return eng.txt_gz(sel - lo, [names[c] for c in sel.tolist()]) if sel.size else None
+
+                mems = list(pool.map(one, range(len(parts)))) if pool else [one(0)]
+                if len(parts) == 1:
+                    for f in range(5):
+                        files[f].write(memoryview(mems[0].file_part(f)))
+                    continue
+                rank = np.zeros(chunk.size, np.int64)  # a cell's index among its part's cells
+                for d in range(len(parts)):
+                    rank[dev == d] = np.arange(int((dev == d).sum()))
+                for f in range(5):
+                    parts_f, offs = [], []
+                    for mem in mems:
+                        if mem is None:
+                            parts_f.append(None)
+                            offs.append(None)
+                            continue
+                        parts_f.append(memoryview(mem.file_part(f)))
+                        offs.append(np.concatenate([[0], np.cumsum(mem.member_bytes[f])]))
+                    files[f].writelines(parts_f[d][offs[d][k]:offs[d][k + 1]]
+                                        for d, k in zip(dev.tolist(), rank.tolist()) if offs[d][k + 1] > offs[d][k])
+        finally:
+            if pool is not None:
+                pool.shutdown()
+            for fh in files:
+                fh.close()
+        res.txt_gz_cells = written
+        return time.perf_counter() - t0
 
     # production path ------------------------------------------------------
     def run_soa(self, soa_batches, n_cells: int) -> EngineResult:
@@ -132,11 +204,12 @@ class CellProcessor:
             res = eng.fetch_compact()  # exact 16-bit rows: half the device-to-host bytes
             t3 = time.perf_counter()
             self.last_stats = eng.kernel_times()
+            t_txt = self._write_txt(res, [(eng, 0, n_cells)]) if self._txt_device_on() else 0.0
         t4 = time.perf_counter()
         # where the engine leg goes (pipeline timings): context + allocation, H2D of
         # the batches + the run, D2H of the results, teardown
         self.last_timing = {"engine_open": t1 - t0, "engine_h2d_run": t2 - t1, "engine_d2h": t3 - t2,
-                            "engine_close": t4 - t3}
+                            "engine_close": t4 - t3 - t_txt, "txt_device": t_txt}
         self.last_result = res
         return res
 
@@ -302,6 +375,7 @@ class CellProcessor:
                 t4 = time.perf_counter()
                 self.last_stats = eng.kernel_times()
                 _, last_streamed = eng.stream_info()
+                t_txt = self._write_txt(res, [(eng, 0, n_cells)]) if self._txt_device_on() else 0.0
             finally:
                 free.put(None)
                 eng.close()
@@ -315,7 +389,8 @@ class CellProcessor:
         dec_end = times.get("decode_end", t2)
         self.last_timing = {"stream_setup": t1 - t0, "stream_first_batch": times.get("first_batch", t1) - t0,
                             "stream_decode_end": dec_end - t0, "stream_push_end": t2 - t0,
-                            "engine_tail": t3 - t2, "engine_fetch": t4 - t3, "engine_close": te - t4,
+                            "engine_tail": t3 - t2, "engine_fetch": t4 - t3, "engine_close": te - t4 - t_txt,
+                            "txt_device": t_txt,
                             "stream_batches": n_batches, "stream_batch_reads": times["cap_reads"],
                             "streamed_run": bool(last_streamed), "rows_target": rows is not None,
                             "h2d_bytes": int(h2d)}
@@ -545,6 +620,8 @@ class CellProcessor:
             res.stats = {"total_reads": int(st.records), **st_sum, "max_span": max_span, "error_bits": err}
             t3 = time.perf_counter()
             self.last_stats = engines[parts[0][0]].kernel_times() if parts else {}
+            t_txt = self._write_txt(res, [(engines[d], lo, hi) for d, lo, hi in parts]) \
+                if parts and self._txt_device_on() else 0.0
         finally:
             free.put(None)
             for eng in engines.values():
@@ -555,7 +632,8 @@ class CellProcessor:
         te = time.perf_counter()
         self.last_timing = {"stream_setup": t1 - t0, "stream_first_batch": times.get("first_batch", t1) - t0,
                             "stream_decode_end": times.get("decode_end", t2) - t0, "stream_push_end": t2 - t0,
-                            "engine_tail": 0.0, "engine_fetch": t3 - t2, "engine_close": te - t3,
+                            "engine_tail": 0.0, "engine_fetch": t3 - t2, "engine_close": te - t3 - t_txt,
+                            "txt_device": t_txt,
                             "stream_batches": n_batches, "stream_batch_reads": times["cap_reads"],
                             "stream_devices": len(parts), "rows_target": rows is not None, "route_s": t_route,
                             "h2d_bytes": int(sum(link_bytes.values())),

@@ -23,9 +23,47 @@ ROOT = Path(__file__).resolve().parent.parent
 sys.path.insert(0, str(ROOT))
 
 
+def _first_members(path: Path, k: int) -> tuple[bytes, int]:
+    """The text of a multi-member gzip file's first k members and their compressed bytes."""
+    import zlib
+
+    buf = path.read_bytes()
+    pos, parts = 0, []
+    for _ in range(k):
+        if pos >= len(buf):
+            break
+        d = zlib.decompressobj(31)
+        parts.append(d.decompress(buf[pos:]))
+        pos = len(buf) - len(d.unused_data)
+    return b"".join(parts), pos
+
+
+def _zlib9_one(args):
+    import gzip
+
+    path, k = args
+    text, nbytes = _first_members(Path(path), k)
+    return Path(path).name, len(text), nbytes, len(gzip.compress(text, compresslevel=9))
+
+
+def zlib9_compare(out_dir: Path, k: int) -> dict:
+    """The written .txt.gz files against the reference's gzip.open(..., compresslevel=9)
+    (writers.py:471-486) on the same text: the first k cells' members of each file (one
+    per cell when the device wrote them) recompressed as one zlib-9 stream; a bounded
+    sample, zlib 9 runs at ~7 MB/s on this text."""
+    from concurrent.futures import ProcessPoolExecutor
+
+    files = [str(out_dir / f"output.{f}.txt.gz") for f in ("coverage", "A", "C", "G", "T")]
+    with ProcessPoolExecutor(5) as ex:
+        rows = list(ex.map(_zlib9_one, [(f, k) for f in files]))
+    return {"sample_cells": k, "files": {n: {"text": t, "written": w, "zlib9": z, "ratio": round(w / z, 4)}
+                                         for n, t, w, z in rows},
+            "max_ratio": round(max(w / z for _, _, w, z in rows), 4)}
+
+
 def run_e2e(reads: int, cells: int, threads: int, out: str | Path, formats=("txt", "hdf5"), modes=("stream",),
             records=("64",), gzip_levels=("9",), bam_level: int = 6, reuse_bam: bool = False, devices: str = "0",
-            log=sys.stderr) -> dict:
+            log=sys.stderr, zlib9_sample: int = 100) -> dict:
     """Synthetic BAM (device generator + native writer), then ``run_pipeline`` per
     (record layout, mode, format, gzip level); returns the stage times of each run."""
     from mgatk2_amd.bam import write_bam
@@ -85,6 +123,8 @@ def run_e2e(reads: int, cells: int, threads: int, out: str | Path, formats=("txt
         if fmt == "txt":
             res[key]["txt_gz_bytes"] = sum((od / "output" / f"output.{f}.txt.gz").stat().st_size
                                            for f in ("A", "C", "G", "T", "coverage"))
+            if zlib9_sample and lvl == "9":
+                res[key]["vs_zlib9"] = zlib9_compare(od / "output", zlib9_sample)
         if fmt == "hdf5":
             html = od / "mgatk2_report.html"
             res[key]["report_html_bytes"] = html.stat().st_size if html.exists() else 0

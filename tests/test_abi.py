@@ -59,7 +59,7 @@ def test_library_exports_header_symbols():
     for s in syms:
         assert hasattr(lib, s), f"libmgpileup.so does not export {s}"
     assert set(syms) == set(engine.ABI_SYMBOLS)
-    assert lib.mgp_abi_version() == engine.ABI_VERSION == 5
+    assert lib.mgp_abi_version() == engine.ABI_VERSION == 6
 
 
 def test_no_device_fails_loudly():

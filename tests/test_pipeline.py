@@ -653,6 +653,28 @@ class _OracleEngine:
     def kernel_times(self, last_runs=1):
         return {}
 
+    def txt_gz(self, cells, names, out=None):
+        """mgp_txt_gz restated on the host (one gzip member per (file, cell) by the host
+        formatter), so the multi-device interleaving of members is tested here."""
+        import tempfile
+
+        from mgatk2_amd.bam import txt_write_cells
+        from mgatk2_amd.engine import TXT_FILES, TxtMembers
+
+        n = len(names)
+        mb, tb = np.zeros((5, n), np.int64), np.zeros((5, n), np.int64)
+        per = [[b""] * n for _ in range(5)]
+        with tempfile.TemporaryDirectory() as d:
+            for k, (c, name) in enumerate(zip(np.asarray(cells).tolist(), names)):
+                txt_write_cells(f"{d}/m", self.res.counts, self.res.depth, [c], [name], level=1, append=False)
+                for f, fn in enumerate(TXT_FILES):
+                    b = open(f"{d}/m.{fn}.txt.gz", "rb").read()
+                    per[f][k] = b
+                    mb[f, k] = len(b)
+                    tb[f, k] = len(gzip.decompress(b)) if b else 0
+        blob = np.frombuffer(b"".join(b"".join(x) for x in per) or b"\0", np.uint8)
+        return TxtMembers(blob[:int(mb.sum())], mb, tb)
+
     def close(self):
         pass
 
