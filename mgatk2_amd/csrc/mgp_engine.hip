@@ -113,6 +113,8 @@ struct DevBuf {
 struct TxtState {
     DevBuf cells, names, name_off, sizes, nlines, offs, text, tok, lines, out, member_bytes, crc_shift, dst_off, packed;
     DevBuf rows_c, rows_d;  // (mgp_txt_gz_rows: the caller's u32 rows)
+    DevBuf prof;            // MGP_TXT_PROF
+    DevBuf seg, crc;
     bool shift_ready = false;
     int64_t n = 0;
     uint64_t total = 0;
@@ -3275,7 +3277,29 @@ int mgp_open(const mgp_config* cfg, int hip_device, mgp_ctx** out) {
     if (const char* e = std::getenv("MGP_PILE_WG_STREAM")) ctx->pile_wg_stream = std::max(1, std::atoi(e));
     if (const char* e = std::getenv("MGP_PILE_MIN_CPB_STREAM")) ctx->pile_min_cpb_stream = std::max(1, std::atoi(e));
     HIP_TRY(hipStreamCreateWithFlags(&ctx->s_side, hipStreamNonBlocking));
-    HIP_TRY(hipStreamCreateWithFlags(&ctx->s_d2h, hipStreamNonBlocking));
+    // the rows target's kernel stores into pinned host memory: each store waits on the
+    // host link, and a CU with a queue of them serves other kernels' loads late (the
+    // streamed run's last medians and tally ran 20-30x slower beside it, round 5).
+    // MGP_D2H_CUS=N keeps that stream's kernels on N CUs spread over the XCDs (0: any)
+    {
+        int d2h_cus = 0;
+        if (const char* e = std::getenv("MGP_D2H_CUS")) d2h_cus = std::max(0, std::atoi(e));
+        hipDeviceProp_t prop{};
+        if (d2h_cus > 0 && hipGetDeviceProperties(&prop, hip_device) == hipSuccess &&
+            d2h_cus < prop.multiProcessorCount) {
+            const int ncu = prop.multiProcessorCount;
+            std::vector<uint32_t> mask((size_t)(ncu + 31) / 32, 0u);
+            // every (ncu / N)-th CU: the CU ids interleave the XCDs, so the set covers each
+            const int step = std::max(1, ncu / d2h_cus);
+            for (int k = 0; k < d2h_cus; ++k) {
+                const int cu = (k * step) % ncu;
+                mask[(size_t)cu / 32] |= 1u << (cu % 32);
+            }
+            HIP_TRY(hipExtStreamCreateWithCUMask(&ctx->s_d2h, (uint32_t)mask.size(), mask.data()));
+        } else {
+            HIP_TRY(hipStreamCreateWithFlags(&ctx->s_d2h, hipStreamNonBlocking));
+        }
+    }
     HIP_TRY(hipEventCreateWithFlags(&ctx->ev_rows, hipEventDisableTiming));
     HIP_TRY(hipEventCreateWithFlags(&ctx->ev_copy, hipEventDisableTiming));
     HIP_TRY(hipEventCreateWithFlags(&ctx->ev_fork, hipEventDisableTiming));
@@ -4565,7 +4589,42 @@ static int txt_run(TxtState& st, hipStream_t s, const txtgz::Rows& rows, int32_t
     sc.out = st.out.as<uint32_t>();
     sc.member_bytes = st.member_bytes.as<uint32_t>();
     sc.crc_shift = st.crc_shift.as<uint32_t>();
+    MGP_TRY(st.seg.ensure((size_t)nm * 257 * 4));
+    MGP_TRY(st.crc.ensure((size_t)nm * 4));
+    sc.seg = st.seg.as<uint32_t>();
+    sc.crc = st.crc.as<uint32_t>();
+    sc.prof = nullptr;
+    const bool prof = std::getenv("MGP_TXT_PROF") != nullptr;
+    if (prof) {
+        MGP_TRY(st.prof.ensure((size_t)nm * 64));
+        HIP_TRY(hipMemsetAsync(st.prof.p, 0, (size_t)nm * 64, s));
+        sc.prof = st.prof.as<uint64_t>();
+    }
     if (txt_deflate(jb, sc, s) != 0) return set_err(MGP_E_HIP, "mgp_txt_gz: deflate kernel launch failed");
+    if (prof) {  // per-phase means over the members that have text (us), to stderr
+        std::vector<uint64_t> pr((size_t)nm * 8);
+        HIP_TRY(hipMemcpyAsync(pr.data(), st.prof.p, pr.size() * 8, hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipStreamSynchronize(s));
+        // stamps: 0 format start, 1 format end, 2 match end, 3 parse end, 4 code end; each
+        // kernel's span over all members (first start to last end) and the mean per member
+        double mean[3] = {0, 0, 0};
+        uint64_t lo[3] = {UINT64_MAX, UINT64_MAX, UINT64_MAX}, hi[3] = {0, 0, 0};
+        int64_t cnt = 0;
+        for (int64_t m = 0; m < nm; ++m) {
+            const uint64_t* q = pr.data() + m * 8;
+            if (!q[4]) continue;
+            ++cnt;
+            mean[0] += (double)(q[1] - q[0]) * 0.01;
+            lo[0] = std::min(lo[0], q[0]);
+            hi[0] = std::max(hi[0], q[1]);
+            hi[1] = std::max(hi[1], q[2]);
+            hi[2] = std::max(hi[2], q[4]);
+            mean[2] += (double)(q[4] - q[3]) * 0.01;
+        }
+        std::fprintf(stderr, "[mgp_txt_gz] %lld members: format %.1f ms (%.1f us per member), match %.1f ms, code %.1f ms "
+                     "(tail %.1f us per member)\n", (long long)cnt, (hi[0] - lo[0]) * 1e-5, mean[0] / cnt,
+                     (hi[1] - hi[0]) * 1e-5, (hi[2] - hi[1]) * 1e-5, mean[2] / cnt);
+    }
     std::vector<uint32_t> mb((size_t)nm);
     HIP_TRY(hipMemcpyAsync(mb.data(), st.member_bytes.p, (size_t)nm * 4, hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));

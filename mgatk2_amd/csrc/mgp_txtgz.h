@@ -52,6 +52,9 @@ struct Scratch {
     uint32_t* out;        // out_off[5n] / 4 words (member outputs)
     uint32_t* member_bytes;  // [5n] compressed bytes of each member
     const uint32_t* crc_shift;  // [25][32]: one-zero-byte CRC operator to the powers 2^b (GF(2) matrices)
+    uint32_t* seg;              // [5n][257] each thread's segment start in its member's text (and the end)
+    uint32_t* crc;              // [5n] CRC-32 of each member's text
+    uint64_t* prof;             // MGP_TXT_PROF: [5n][8] kernel stamps (100 MHz wall clock), else null
 };
 
 // member text bytes and lines of every (file, cell) of the batch -> sizes[5n], nlines[5n]

@@ -38,10 +38,11 @@ namespace txtgz {
 
 constexpr int kT = 256;        // threads per member (one segment each)
 constexpr int kJ = 16;         // previous lines searched for matches
-constexpr int kLMax = 63;      // longest match tried (C4's matches stay below 40)
-constexpr int kRing = 64;      // DP cost ring (> kLMax), u16 costs compared by differences
+constexpr int kLMax = 31;      // longest match tried (longer ones gain nothing on C4-like text)
+constexpr int kRing = 32;      // DP cost ring (> kLMax), u16 costs compared by differences
 constexpr int kMaxDist = 32768;
 constexpr int kLit = 286, kDist = 30;
+constexpr int kWinBytes = 24 * 1024;  // LDS text window of the match finder
 
 __constant__ uint16_t c_len_base[29] = {3,  4,  5,  6,  7,  8,  9,  10, 11,  13,  15,  17,  19,  23, 27,
                                         31, 35, 43, 51, 59, 67, 83, 99, 115, 131, 163, 195, 227, 258};
@@ -219,10 +220,10 @@ __device__ void canon(const uint8_t* len, int n, uint16_t* code) {
     }
 }
 
-// ---- the member workgroup's LDS ----
-struct MemberLds {
+// ---- the LDS of the coding kernel (k_txt_code) ----
+struct CodeLds {
     uint64_t wsum[4];
-    uint16_t ring[kT][kRing];
+    uint16_t ring[kT][kRing];  // the DP's cost rings
     uint32_t lit_f[kLit], dist_f[kDist];
     uint8_t lit_len[kLit], dist_len[kDist];
     uint16_t lit_code[kLit], dist_code[kDist];
@@ -233,20 +234,16 @@ struct MemberLds {
     uint16_t cl_code[19];
     uint16_t rle[kLit + kDist];  // code-length symbols: sym | extra << 8
     int n_rle, hlit, hdist, hclen;
-    uint32_t crc_tab[256];
-    uint32_t crc_v[kT];
-    uint32_t crc_n[kT];
     uint64_t hdr_bits;
-    int mode;  // 0 dynamic, 1 fixed, 2 stored
 };
 
-__device__ __forceinline__ void lds_prices_default(MemberLds& S) {
+__device__ __forceinline__ void lds_prices_default(CodeLds& S) {
     for (int s = threadIdx.x; s < 256; s += kT)
         S.litcost[s] = (uint8_t)((s >= '0' && s <= '9') || s == ',' ? 4 : s == '\n' ? 5 : 6);
     for (int l = threadIdx.x; l <= kLMax; l += kT) S.lencost[l] = l < 3 ? 0 : (uint8_t)(7 + len_xb(len_code(l)));
     for (int c = threadIdx.x; c < kDist; c += kT) S.dcost[c] = (uint8_t)(5 + dist_xb(c));
 }
-__device__ __forceinline__ void lds_prices_from_lengths(MemberLds& S) {
+__device__ __forceinline__ void lds_prices_from_lengths(CodeLds& S) {
     for (int s = threadIdx.x; s < 256; s += kT) S.litcost[s] = S.lit_len[s] ? S.lit_len[s] : 16;
     for (int l = threadIdx.x; l <= kLMax; l += kT) {
         if (l < 3) {
@@ -259,104 +256,137 @@ __device__ __forceinline__ void lds_prices_from_lengths(MemberLds& S) {
     for (int c = threadIdx.x; c < kDist; c += kT) S.dcost[c] = (uint8_t)((S.dist_len[c] ? S.dist_len[c] : 16) + dist_xb(c));
 }
 
-// forward match length at distance d from i (at most cap)
-__device__ __forceinline__ int fwd_match(const uint8_t* T, int i, int d, int cap) {
+// forward match length at distance d from i (at most cap), text staged in LDS
+__device__ __forceinline__ int fwd_match(const uint8_t* W, int i, int d, int cap) {
     int L = 0;
-    while (L < cap && T[i + L] == T[i - d + L]) ++L;
+    while (L < cap && W[i + L] == W[i - d + L]) ++L;
     return L;
 }
 
-// One segment's backward optimal parse: choice[i] = (length << 16) | distance, or 0 for
-// a literal, for i in [t0, t1). Lines [l0, l1) cover exactly [t0, t1).
-__device__ void parse_segment(const uint8_t* T, const uint32_t* lines, uint32_t* choice, int l0, int l1, int t0,
-                              int t1, int nf, uint16_t* ring, const MemberLds& S) {
-    ring[t1 & (kRing - 1)] = 0;
-    for (int k = l1 - 1; k >= l0; --k) {
+// The match finder over one window of lines [k0, k1), the text staged in LDS (W[x] =
+// T[x + base], lines k0 - kJ .. k1 and 64 bytes beyond): each thread takes whole lines
+// and walks them backward. Candidates per previous line m = k - 1 - j (j < kJ): the same
+// offset from the start of the current field (distance constant along the field) and
+// from the line's end (constant along the line); along a run of one distance the
+// length follows L(i) = T[i] == T[i - d] ? L(i + 1) + 1 : 0, so only the first byte
+// visited (the line end, a field's last byte) costs a forward compare. Every position
+// keeps its longest candidate (the nearest on ties): cand[i] = d | L << 16, 0 if L < 3.
+__device__ void match_window(const uint8_t* W, int64_t base, int64_t wend, const uint32_t* lines, int k0, int k1,
+                             int kb, int nf, uint32_t* cand) {
+    for (int k = k0 + (int)threadIdx.x; k < k1; k += kT) {
         const uint32_t* le = lines + 3 * (size_t)k;
-        const int s = (int)le[0];
+        const int s = (int)((int64_t)le[0] - base);
         const int A1 = s + (int)(le[1] & 0xFFFFu), A2 = s + (int)(le[1] >> 16), A3 = s + (int)(le[2] & 0xFFFFu);
         const int e = s + (int)(le[2] >> 16) - 1;  // the '\n'
-        int dE[kJ], LE[kJ], dF[kJ], LF[kJ];
+        // per previous line j: distances dd = dE | dF << 16 and lengths ll = LE | LF << 8
+        // (packed: 32 registers for the 32 candidates)
+        uint32_t dd[kJ], ll[kJ];
 #pragma unroll
         for (int j = 0; j < kJ; ++j) {
-            dE[j] = 0;
-            LE[j] = 0;
-            dF[j] = 0;
-            LF[j] = 0;
-            if (k - j - 1 < 0) continue;
+            dd[j] = 0;
+            ll[j] = 0;
+            if (k - j - 1 < kb) continue;  // (lines before the window: no candidate)
             const uint32_t* lp = lines + 3 * (size_t)(k - j - 1);
-            const int d = e - ((int)lp[0] + (int)(lp[2] >> 16) - 1);
-            if (d > 0 && d <= kMaxDist) dE[j] = d;
+            const int d = e - ((int)((int64_t)lp[0] - base) + (int)(lp[2] >> 16) - 1);
+            if (d > 0 && d <= kMaxDist) dd[j] = (uint32_t)d;
         }
+        const int cap_e = (int)min((int64_t)kLMax, wend - base - e);
         int field = -1;
         for (int i = e; i >= s; --i) {
-            const int cap = min(kLMax, t1 - i);
             const int f = (nf > 3 && i >= A3) ? 3 : i >= A2 ? 2 : i >= A1 ? 1 : 0;
-            const uint8_t ti = T[i];
-            if (f != field) {  // entering a field (going backward): its anchor distances, forward compares
+            const uint8_t ti = W[i];
+            const int cap = min(kLMax, cap_e + (e - i));
+            if (f != field) {
                 const int Af = f == 0 ? s : f == 1 ? A1 : f == 2 ? A2 : A3;
 #pragma unroll
                 for (int j = 0; j < kJ; ++j) {
-                    dF[j] = 0;
-                    LF[j] = 0;
-                    if (k - j - 1 < 0) continue;
-                    const uint32_t* lp = lines + 3 * (size_t)(k - j - 1);
-                    const int sp = (int)lp[0];
-                    const int Bf = f == 0 ? sp
-                                 : f == 1 ? sp + (int)(lp[1] & 0xFFFFu)
-                                 : f == 2 ? sp + (int)(lp[1] >> 16)
-                                          : sp + (int)(lp[2] & 0xFFFFu);
-                    const int d = Af - Bf;
-                    if (d > 0 && d <= kMaxDist && d != dE[j]) {
-                        dF[j] = d;
-                        LF[j] = fwd_match(T, i, d, cap);
+                    const int dE = (int)(dd[j] & 0xFFFFu);
+                    int LE = (int)(ll[j] & 0xFFu);
+                    if (dE) {
+                        if (field < 0) LE = i - dE >= 0 ? fwd_match(W, i, dE, cap) : 0;
+                        else LE = (i - dE >= 0 && W[i - dE] == ti) ? min(LE + 1, cap) : 0;
                     }
-                }
-                if (field < 0) {
-#pragma unroll
-                    for (int j = 0; j < kJ; ++j)
-                        if (dE[j]) LE[j] = fwd_match(T, i, dE[j], cap);
-                } else {
-#pragma unroll
-                    for (int j = 0; j < kJ; ++j)
-                        if (dE[j]) LE[j] = (i >= dE[j] && T[i - dE[j]] == ti) ? min(LE[j] + 1, cap) : 0;
+                    int dF = 0, LF = 0;
+                    if (k - j - 1 >= kb) {
+                        const uint32_t* lp = lines + 3 * (size_t)(k - j - 1);
+                        const int sp = (int)((int64_t)lp[0] - base);
+                        const int Bf = f == 0 ? sp
+                                     : f == 1 ? sp + (int)(lp[1] & 0xFFFFu)
+                                     : f == 2 ? sp + (int)(lp[1] >> 16)
+                                              : sp + (int)(lp[2] & 0xFFFFu);
+                        const int d = Af - Bf;
+                        if (d > 0 && d <= kMaxDist && d != dE) {
+                            dF = d;
+                            LF = fwd_match(W, i, d, cap);
+                        }
+                    }
+                    dd[j] = (uint32_t)dE | (uint32_t)dF << 16;
+                    ll[j] = (uint32_t)LE | (uint32_t)LF << 8;
                 }
                 field = f;
             } else {
-                // (a field-anchored source stays inside the earlier line's field: i - dF >= 0;
-                // an end-anchored one can run off the member's start when that line is short)
+                // (a field-anchored source stays inside the earlier line's field; an
+                // end-anchored one can run off the window's start when that line is short)
 #pragma unroll
                 for (int j = 0; j < kJ; ++j) {
-                    if (dF[j]) LF[j] = (T[i - dF[j]] == ti) ? min(LF[j] + 1, cap) : 0;
-                    if (dE[j]) LE[j] = (i >= dE[j] && T[i - dE[j]] == ti) ? min(LE[j] + 1, cap) : 0;
+                    const int dE = (int)(dd[j] & 0xFFFFu), dF = (int)(dd[j] >> 16);
+                    int LE = (int)(ll[j] & 0xFFu), LF = (int)(ll[j] >> 8);
+                    if (dF) LF = (W[i - dF] == ti) ? min(LF + 1, cap) : 0;
+                    if (dE) LE = (i - dE >= 0 && W[i - dE] == ti) ? min(LE + 1, cap) : 0;
+                    ll[j] = (uint32_t)LE | (uint32_t)LF << 8;
                 }
             }
-            // relaxation: costs relative to cost[i + 1] (u16 ring, differences stay small)
-            const uint16_t c1 = ring[(i + 1) & (kRing - 1)];
-            int best = S.litcost[ti];
-            uint32_t ch = 0;
-            int lo = 3;
+            int bl = 0, bd = 0;
 #pragma unroll
-            for (int j = 0; j < kJ; ++j) {
-#pragma unroll
-                for (int q = 0; q < 2; ++q) {
-                    const int L = q ? LE[j] : LF[j];
-                    if (L < lo) continue;
-                    const int d = q ? dE[j] : dF[j];
-                    const int dc = S.dcost[dist_code(d)];
-                    for (int l = lo; l <= L; ++l) {
-                        const int v = (int)S.lencost[l] + dc + (int)(int16_t)(uint16_t)(ring[(i + l) & (kRing - 1)] - c1);
-                        if (v < best) {
-                            best = v;
-                            ch = ((uint32_t)l << 16) | (uint32_t)d;
-                        }
-                    }
-                    lo = L + 1;
+            for (int j = 0; j < kJ; ++j) {  // nearest first: a later candidate must be longer
+                const int dE = (int)(dd[j] & 0xFFFFu), dF = (int)(dd[j] >> 16);
+                const int LE = (int)(ll[j] & 0xFFu), LF = (int)(ll[j] >> 8);
+                if (LF > bl || (LF == bl && dF && dF < bd)) {
+                    bl = LF;
+                    bd = dF;
+                }
+                if (LE > bl || (LE == bl && dE && dE < bd)) {
+                    bl = LE;
+                    bd = dE;
                 }
             }
-            ring[i & (kRing - 1)] = (uint16_t)(c1 + best);
-            choice[i] = ch;
+            cand[i + base] = bl >= 3 ? ((uint32_t)bd | (uint32_t)bl << 16) : 0u;
         }
+    }
+}
+
+// One segment's backward optimal parse over its candidates (tok[i] = d | L << 16 from
+// match_window): the chosen length (0: a literal, else 3..L at distance d) goes into
+// bits 22-27 of tok[i]. Costs are u16 in a per-lane ring, compared by differences.
+__device__ void dp_segment(const uint8_t* T, uint32_t* tok, int t0, int t1, uint16_t* ring, const CodeLds& S) {
+    ring[t1 & (kRing - 1)] = 0;
+    if (t1 <= t0) return;
+    uint32_t w_next = tok[t1 - 1];
+    uint8_t b_next = T[t1 - 1];
+    for (int i = t1 - 1; i >= t0; --i) {
+        const uint32_t w = w_next;
+        const uint8_t ti = b_next;
+        if (i > t0) {  // the next position's loads, ahead of this one's work
+            w_next = tok[i - 1];
+            b_next = T[i - 1];
+        }
+        const uint16_t c1 = ring[(i + 1) & (kRing - 1)];
+        int best = S.litcost[ti];
+        uint32_t bl = 0;
+        const int L = min((int)((w >> 16) & 63u), t1 - i);
+        if (L >= 3) {
+            const int d = (int)(w & 0xFFFFu);
+            const int dc = S.dcost[dist_code(d)];
+            for (int l = 3; l <= L; ++l) {
+                const int v = (int)S.lencost[l] + dc + (int)(int16_t)(uint16_t)(ring[(i + l) & (kRing - 1)] - c1);
+                if (v < best) {
+                    best = v;
+                    bl = (uint32_t)l;
+                }
+            }
+        }
+        ring[i & (kRing - 1)] = (uint16_t)(c1 + best);
+        tok[i] = (w & 0x3FFFFFu) | (bl << 22);
     }
 }
 
@@ -456,8 +486,25 @@ __global__ void __launch_bounds__(kT) k_txt_sizes(Job job, uint64_t* __restrict_
     }
 }
 
-__global__ void __launch_bounds__(kT) k_txt_gz(Job job, Scratch sc) {
-    __shared__ MemberLds S;
+// MGP_TXT_PROF: thread 0 stamps the 100 MHz wall clock when a kernel's member is done
+#define PROF_STAMP(k)                                                            \
+    do {                                                                         \
+        if (sc.prof) {                                                           \
+            __syncthreads();                                                     \
+            if (threadIdx.x == 0) sc.prof[m * 8 + (k)] = wall_clock64();         \
+        }                                                                        \
+    } while (0)
+
+struct FormatLds {
+    uint64_t wsum[4];
+    uint32_t crc_tab[256];
+    uint32_t crc_v[kT];
+    uint32_t crc_n[kT];
+};
+
+// Kernel 1 (per member): the text, the line table, the segments' starts and the CRC-32.
+__global__ void __launch_bounds__(kT) k_txt_format(Job job, Scratch sc) {
+    __shared__ FormatLds S;
     const int t = threadIdx.x;
     const int64_t m = blockIdx.x;
     const int f = (int)(m / job.n);
@@ -466,16 +513,11 @@ __global__ void __launch_bounds__(kT) k_txt_gz(Job job, Scratch sc) {
     const char* bc = job.names + job.name_off[kc];
     const uint32_t bclen = (uint32_t)(job.name_off[kc + 1] - job.name_off[kc]);
     const int L = job.rows.L;
-    const int nf = f ? 4 : 3;
     uint8_t* const T = sc.text + sc.text_off[m];
     uint32_t* const lines = sc.lines + 3 * sc.line_off[m];
-    uint32_t* const tok = sc.tok + sc.text_off[m];
     const uint64_t n_text = sc.text_off[m + 1] - sc.text_off[m];
-    uint32_t* const out = sc.out + sc.out_off[m] / 4;
-    if (n_text == 0) {  // no line: no member
-        if (t == 0) sc.member_bytes[m] = 0;
-        return;
-    }
+    if (n_text == 0) return;
+    PROF_STAMP(0);
     for (int s = t; s < 256; s += kT) {
         uint32_t r = (uint32_t)s;
         for (int b = 0; b < 8; ++b) r = (r >> 1) ^ (0xEDB88320u & (0u - (r & 1u)));
@@ -533,42 +575,124 @@ __global__ void __launch_bounds__(kT) k_txt_gz(Job job, Scratch sc) {
         S.crc_v[t] = r;
         S.crc_n[t] = my_b;
     }
-    // ---- 2. parse, twice ----
-    uint32_t ntok = 0;
-    lds_prices_default(S);
-    for (int pass = 0; pass < 2; ++pass) {
-        for (int s = t; s < kLit; s += kT) S.lit_f[s] = 0;
-        if (t < kDist) S.dist_f[t] = 0;
+    // the CRC-32 of the text: segments combined up a tree
+    for (int s = 1; s < kT; s <<= 1) {
         __syncthreads();
-        if (my_b) parse_segment(T, lines, tok, l0, l1, t0, t1, nf, S.ring[t], S);
-        // traceback: the chosen tokens (pass 2 stores them over the choices, compacted)
-        int nt = 0;
-        for (int i = t0; i < t1;) {
-            const uint32_t ch = tok[i];
-            const uint32_t l = ch >> 16;
-            if (!l) {
-                atomicAdd(&S.lit_f[T[i]], 1u);
-                if (pass) tok[t0 + nt] = T[i];
-                ++i;
-            } else {
-                atomicAdd(&S.lit_f[257 + len_code((int)l)], 1u);
-                atomicAdd(&S.dist_f[dist_code((int)(ch & 0xFFFFu))], 1u);
-                if (pass) tok[t0 + nt] = ch;
-                i += (int)l;
-            }
-            ++nt;
+        uint32_t v = 0, nn = 0;
+        const bool act = (t % (2 * s)) == 0 && t + s < kT;
+        if (act) {
+            v = crc_shift(S.crc_v[t], S.crc_n[t + s], sc.crc_shift) ^ S.crc_v[t + s];
+            nn = S.crc_n[t] + S.crc_n[t + s];
         }
-        if (t == 0) S.lit_f[256] = 1;  // end of block
         __syncthreads();
-        huff_lengths(S.lit_f, kLit, 15, S.lit_len, S.h);
-        huff_lengths(S.dist_f, kDist, 15, S.dist_len, S.h);
-        if (!pass) {
-            lds_prices_from_lengths(S);
-            __syncthreads();
-        } else {
-            ntok = (uint32_t)nt;
+        if (act) {
+            S.crc_v[t] = v;
+            S.crc_n[t] = nn;
         }
     }
+    if (t == 0) sc.crc[m] = S.crc_v[0] ^ crc_shift(0xFFFFFFFFu, n_text, sc.crc_shift) ^ 0xFFFFFFFFu;
+    sc.seg[m * (kT + 1) + t] = (uint32_t)t0;
+    if (t == kT - 1) sc.seg[m * (kT + 1) + kT] = (uint32_t)t1;
+    PROF_STAMP(1);
+}
+
+struct MatchLds {
+    uint8_t win[kWinBytes];
+    int win_k1, win_kb;
+};
+
+// Kernel 2 (per member): the match candidates of every position (windows of lines
+// staged in LDS, match_window).
+__global__ void __launch_bounds__(kT, 4) k_txt_match(Job job, Scratch sc) {
+    __shared__ MatchLds S;
+    const int t = threadIdx.x;
+    const int64_t m = blockIdx.x;
+    const int f = (int)(m / job.n);
+    const int nf = f ? 4 : 3;
+    const uint8_t* const T = sc.text + sc.text_off[m];
+    const uint32_t* const lines = sc.lines + 3 * sc.line_off[m];
+    uint32_t* const tok = sc.tok + sc.text_off[m];
+    const uint64_t n_text = sc.text_off[m + 1] - sc.text_off[m];
+    if (n_text == 0) return;
+    const int n_lines = (int)(sc.line_off[m + 1] - sc.line_off[m]);
+    // ---- 2. match candidates, windows of lines staged in LDS ----
+    auto line_start = [&](int k) -> int64_t { return k >= n_lines ? (int64_t)n_text : (int64_t)lines[3 * (size_t)k]; };
+    for (int k0 = 0; k0 < n_lines;) {
+        if (t == 0) {
+            // look back up to kJ lines (at most half the window), then as many lines as fit
+            // with 64 bytes of look-ahead (a line is at most 4096 + 29 bytes)
+            const int64_t s0 = line_start(k0);
+            int kb = max(0, k0 - kJ);
+            while (kb < k0 && s0 - line_start(kb) > kWinBytes / 2) ++kb;
+            const int64_t base = line_start(kb);
+            int lo = k0 + 1, hi = n_lines;  // largest k1 in [k0 + 1, n_lines] whose text fits
+            while (lo < hi) {
+                const int mid = (lo + hi + 1) / 2;
+                if (line_start(mid) + 64 - base <= kWinBytes) lo = mid;
+                else hi = mid - 1;
+            }
+            S.win_kb = kb;
+            S.win_k1 = lo;
+        }
+        __syncthreads();
+        const int kb = S.win_kb, k1 = S.win_k1;
+        const int64_t base = line_start(kb);
+        const int64_t wend = min((int64_t)n_text, line_start(k1) + 64);
+        for (int64_t x = base + t; x < wend; x += kT) S.win[x - base] = T[x];
+        __syncthreads();
+        match_window(S.win, base, wend, lines, k0, k1, kb, nf, tok);
+        __syncthreads();
+        k0 = k1;
+    }
+    PROF_STAMP(2);
+}
+
+
+// Kernel 3 (per member): the optimal parse of each segment, the Huffman codes, the
+// encoded block (dynamic, fixed or stored: the smallest) and the gzip frame.
+__global__ void __launch_bounds__(kT) k_txt_code(Job job, Scratch sc) {
+    __shared__ CodeLds S;
+    const int t = threadIdx.x;
+    const int64_t m = blockIdx.x;
+    const uint8_t* const T = sc.text + sc.text_off[m];
+    uint32_t* const tok = sc.tok + sc.text_off[m];
+    const uint64_t n_text = sc.text_off[m + 1] - sc.text_off[m];
+    uint32_t* const out = sc.out + sc.out_off[m] / 4;
+    if (n_text == 0) {  // no line: no member
+        if (t == 0) sc.member_bytes[m] = 0;
+        return;
+    }
+    const int t0 = (int)sc.seg[m * (kT + 1) + t], t1 = (int)sc.seg[m * (kT + 1) + t + 1];
+    // ---- 3. optimal parse (one pass at default prices: a second pass at the member's own
+    // code lengths gained 0.4-1 % on C4-like text for twice the parse time) ----
+    lds_prices_default(S);
+    for (int s = t; s < kLit; s += kT) S.lit_f[s] = 0;
+    if (t < kDist) S.dist_f[t] = 0;
+    __syncthreads();
+    dp_segment(T, tok, t0, t1, S.ring[t], S);
+    // traceback: the chosen tokens, stored over the candidates (compacted), and their counts
+    uint32_t ntok = 0;
+    for (int i = t0; i < t1;) {
+        const uint32_t w = tok[i];
+        const uint32_t l = (w >> 22) & 63u;
+        if (!l) {
+            atomicAdd(&S.lit_f[T[i]], 1u);
+            tok[t0 + ntok] = T[i];
+            ++i;
+        } else {
+            const uint32_t d = w & 0xFFFFu;
+            atomicAdd(&S.lit_f[257 + len_code((int)l)], 1u);
+            atomicAdd(&S.dist_f[dist_code((int)d)], 1u);
+            tok[t0 + ntok] = (l << 16) | d;
+            i += (int)l;
+        }
+        ++ntok;
+    }
+    if (t == 0) S.lit_f[256] = 1;  // end of block
+    __syncthreads();
+    huff_lengths(S.lit_f, kLit, 15, S.lit_len, S.h);
+    huff_lengths(S.dist_f, kDist, 15, S.dist_len, S.h);
+    PROF_STAMP(3);
     // ---- 3. codes and the header ----
     if (t == 0) {
         // a complete distance code: at least two used lengths (one used or none -> codes 0 and 1)
@@ -733,25 +857,10 @@ __global__ void __launch_bounds__(kT) k_txt_gz(Job job, Scratch sc) {
         }
         for (uint64_t x = t; x < n_text; x += kT) ob[10 + 5 * (x / 65535 + 1) + x] = T[x];
     }
-    // ---- 5. CRC-32 of the text (segments combined up a tree), trailer ----
-    for (int s = 1; s < kT; s <<= 1) {
-        __syncthreads();
-        uint32_t v = 0, nn = 0;
-        const bool act = (t % (2 * s)) == 0 && t + s < kT;
-        if (act) {
-            v = crc_shift(S.crc_v[t], S.crc_n[t + s], sc.crc_shift) ^ S.crc_v[t + s];
-            nn = S.crc_n[t] + S.crc_n[t + s];
-        }
-        __syncthreads();
-        if (act) {
-            S.crc_v[t] = v;
-            S.crc_n[t] = nn;
-        }
-    }
     __threadfence_block();
     __syncthreads();
     if (t == 0) {
-        const uint32_t crc = S.crc_v[0] ^ crc_shift(0xFFFFFFFFu, n_text, sc.crc_shift) ^ 0xFFFFFFFFu;
+        const uint32_t crc = sc.crc[m];
         const uint64_t o = 10 + blk_bytes;
         const uint32_t isz = (uint32_t)n_text;
         for (int q = 0; q < 4; ++q) {
@@ -759,7 +868,7 @@ __global__ void __launch_bounds__(kT) k_txt_gz(Job job, Scratch sc) {
             ob[o + 4 + q] = (uint8_t)(isz >> (8 * q));
         }
         sc.member_bytes[m] = (uint32_t)(o + 8);
-    }
+    }    PROF_STAMP(4);
 }
 
 __global__ void __launch_bounds__(kT) k_txt_pack(const uint32_t* __restrict__ out, const uint64_t* __restrict__ out_off,
@@ -783,7 +892,10 @@ int txt_sizes(const Job& job, uint64_t* sizes, uint64_t* nlines, hipStream_t s) 
 
 int txt_deflate(const Job& job, const Scratch& sc, hipStream_t s) {
     if (job.n <= 0) return 0;
-    k_txt_gz<<<(unsigned)(kFiles * job.n), kT, 0, s>>>(job, sc);
+    const unsigned nm = (unsigned)(kFiles * job.n);
+    k_txt_format<<<nm, kT, 0, s>>>(job, sc);
+    k_txt_match<<<nm, kT, 0, s>>>(job, sc);
+    k_txt_code<<<nm, kT, 0, s>>>(job, sc);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
