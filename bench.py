@@ -333,6 +333,7 @@ def main():
             "e2e": e2e,
             "stats_rank0": main_leg.get("stats"),
             "sample_check": main_leg.get("sample_check"),
+            "stream_kernels": None if head is None else stream_kernels(head["reads_rank0"], n_cells),
         }
         print(json.dumps(out), flush=True)
     if dist is not None:
@@ -395,6 +396,21 @@ def pmc_traffic(key: str, n: int, nc: int, layout: str) -> dict | None:
         if d.get("reads") == n and d.get("cells") == nc and d.get("record_layout") == layout:
             return d
     except Exception:
+        pass
+    return None
+
+
+def stream_kernels(n: int, nc: int) -> dict | None:
+    """The streamed step's per-kernel GPU time (profiles/stream_kernels.json, from
+    scripts/stream_kernels.py over a rocprofv3 --stats run of this step: every kernel's
+    calls and ms per step, pairing / check / grouping / pileup / rows), when it is of
+    this workload."""
+    f = ROOT / "profiles" / "stream_kernels.json"
+    try:
+        d = json.loads(f.read_text())
+        if d.get("reads") == n and d.get("cells") == nc:
+            return d
+    except (OSError, ValueError):
         pass
     return None
 

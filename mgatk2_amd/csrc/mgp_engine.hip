@@ -134,6 +134,8 @@ struct mgp_ctx {
     hipEvent_t ev_rows = nullptr;
     mgp_rows16 rows_tgt{};
     bool rows_on = false;
+    bool rows_pending = false;  // the run's last segment's rows: copied by run_finish
+    int rows_p0 = 0, rows_p1 = 0;
     hipEvent_t ev_copy = nullptr, ev_fork = nullptr, ev_join = nullptr;
     int seg_min_win = 1;     // a streaming push queues a segment once this many windows are complete (MGP_SEG_MIN_WIN)
     int rows_wg = 256;       // workgroups of a segment's k_rows_to_host (MGP_ROWS_WG)
@@ -143,7 +145,10 @@ struct mgp_ctx {
     int pile_min_cpb_stream = 1;  // a streaming run's least cells per pileup chunk (MGP_PILE_MIN_CPB_STREAM)
     // on-device pairing of dense 64-byte batches (mgp_push_batch): two staging buffers
     // the H2D copies land in, the event after the pairing kernels that last read each
-    bool dev_pair = true;  // (MGP_DEV_PAIR=0: records stay in BAM order, for A/B)
+    // Off by default since round 6: the pairing copy (k_pair_rank + k_pair_place, ~10 ms of
+    // GPU time per C4 step) saved ~1.3 ms of pileup, and the streamed step is link-bound
+    // with or without it (profiles/r06/tail_r6i.txt); MGP_DEV_PAIR=1 turns it on
+    bool dev_pair = false;
     int stage_i = 0;
     DevBuf stage[2], pair_rank, pair_cnt, pair_lines;
     DevBuf col16[2];  // a 16-bit batch's barcode and |tlen| columns (mgp_push_batch16), before widening
@@ -3675,7 +3680,32 @@ struct Seg {
     int bhi;      // start bins [seg_lo_bin(w0), bhi) (nbins: through the overflow bin)
     bool first;   // the run's first segment: zero the run's state
     bool stream;  // a streaming segment: speculative compact grouping, no host wait
+    bool last;    // the run's last segment: its rows leave after the medians (run_finish)
 };
+
+// The rows of windows' positions [p0, p1) of every cell to the host target, on the D2H
+// stream behind the compute stream's work so far (mgp_set_rows16_target): written by a
+// kernel into the mapped pinned target (a strided 2D copy of 10k rows per segment runs as
+// row-by-row DMA transfers: 4x slower overall)
+static int rows_copy(mgp_ctx* ctx, int p0, int p1) {
+    const Geom& g = ctx->g;
+    const int nc = g.nc;
+    HIP_TRY(hipEventRecord(ctx->ev_rows, ctx->s_comp));
+    HIP_TRY(hipStreamWaitEvent(ctx->s_d2h, ctx->ev_rows, 0));
+    const mgp_rows16& t = ctx->rows_tgt;
+    // a few hundred workgroups looping over the cells: the stores wait on the host
+    // link, and a grid of one workgroup per (cell, 256 positions) held every CU
+    // slot of the device while they drained, starving the kernels of the next
+    // segment and the run's medians (MGP_ROWS_WG)
+    const unsigned gx = (unsigned)((p1 - p0 + kBlock - 1) / kBlock);
+    dim3 gr(gx, (unsigned)std::max(1, std::min(std::min(nc, 65535), ctx->rows_wg / (int)gx)));
+    k_rows_to_host<<<gr, kBlock, 0, ctx->s_d2h>>>(g.L, nc, p0, p1, ctx->counts16.as<uint4>(),
+                                                ctx->tn5_16.as<uint32_t>(), ctx->depth16.as<uint16_t>(),
+                                                reinterpret_cast<uint4*>(t.counts), reinterpret_cast<uint32_t*>(t.tn5),
+                                                t.depth);
+    HIP_TRY(hipGetLastError());
+    return MGP_OK;
+}
 
 static int run_segment(mgp_ctx* ctx, const Seg& sg, int slot, int& dup_parts, int& pair_mode) {
     const Geom g = ctx->g;
@@ -3955,25 +3985,19 @@ static int run_segment(mgp_ctx* ctx, const Seg& sg, int slot, int& dup_parts, in
         HIP_TRY(hipGetLastError());
         if (sev) HIP_TRY(hipEventRecord(sev[1], s));
         // the windows' rows are final now (all cells): to the host target behind them,
-        // while later batches are still being copied in (mgp_set_rows16_target)
+        // while later batches are still being copied in (mgp_set_rows16_target). The
+        // run's last segment leaves its rows to run_finish: host-bound stores queued in
+        // the memory system slowed every kernel beside them, and the medians and tallies
+        // of the run's tail ran 20-30x slower under them (round 5)
         if (ctx->rows_on) {
-            // written by a kernel into the mapped pinned target (a strided 2D copy of
-            // 10k rows per segment runs as row-by-row DMA transfers: 4x slower overall)
             const int p0 = sg.w0 * g.W, p1 = std::min(g.L, sg.w1 * g.W);
-            HIP_TRY(hipEventRecord(ctx->ev_rows, s));
-            HIP_TRY(hipStreamWaitEvent(ctx->s_d2h, ctx->ev_rows, 0));
-            const mgp_rows16& t = ctx->rows_tgt;
-            // a few hundred workgroups looping over the cells: the stores wait on the host
-            // link, and a grid of one workgroup per (cell, 256 positions) held every CU
-            // slot of the device while they drained, starving the kernels of the next
-            // segment and the run's medians (MGP_ROWS_WG)
-            const unsigned gx = (unsigned)((p1 - p0 + kBlock - 1) / kBlock);
-            dim3 gr(gx, (unsigned)std::max(1, std::min(std::min(nc, 65535), ctx->rows_wg / (int)gx)));
-            k_rows_to_host<<<gr, kBlock, 0, ctx->s_d2h>>>(g.L, nc, p0, p1, ctx->counts16.as<uint4>(),
-                                                        ctx->tn5_16.as<uint32_t>(), ctx->depth16.as<uint16_t>(),
-                                                        reinterpret_cast<uint4*>(t.counts),
-                                                        reinterpret_cast<uint32_t*>(t.tn5), t.depth);
-            HIP_TRY(hipGetLastError());
+            if (sg.last) {
+                ctx->rows_p0 = p0;
+                ctx->rows_p1 = p1;
+                ctx->rows_pending = true;
+            } else {
+                MGP_TRY(rows_copy(ctx, p0, p1));
+            }
         }
     }
     STAGE_END(ST_PILEUP);
@@ -4050,7 +4074,11 @@ static int run_finish(mgp_ctx* ctx, int slot, int dup_parts, bool streamed) {
         HIP_TRY(hipGetLastError());
         STAGE_END(ST_MEDIAN);
         HIP_TRY(hipStreamWaitEvent(s, ctx->ev_join, 0));
+        // the last segment's rows, now that the medians and tallies are done
+        if (ctx->rows_pending && ctx->rows_on) MGP_TRY(rows_copy(ctx, ctx->rows_p0, ctx->rows_p1));
+        ctx->rows_pending = false;
     } else {
+        ctx->rows_pending = false;
         HIP_TRY(hipMemsetAsync(tally, 0, (size_t)g.L * 32, s));
         // (with cells, k_run_stats takes the streaming order check)
         k_order_err<<<1, 64, 0, s>>>(ctx->order_bad.as<uint32_t>(), st);
@@ -4123,7 +4151,8 @@ int mgp_run(mgp_ctx* ctx) {
     // otherwise (or on the fallback path) one resident segment over everything
     const bool streamed = ctx->seg_open && !ctx->no_spec && !ctx->stream_off;
     if (!streamed) ctx->seg_n[slot] = 0;  // (no segment pileups of this run to time)
-    const Seg sg = streamed ? Seg{ctx->w_done, g.nwin, g.nbins, false, true} : Seg{0, g.nwin, g.nbins, true, false};
+    const Seg sg = streamed ? Seg{ctx->w_done, g.nwin, g.nbins, false, true, true}
+                            : Seg{0, g.nwin, g.nbins, true, false, true};
     ctx->seg_open = false;
     ctx->w_done = 0;
     MGP_TRY(run_segment(ctx, sg, slot, dup_parts, pair_mode));

@@ -15,7 +15,7 @@ for v in "$@"; do
     i=$((i + 1))
     d=gpurun_out/${name}_$i
     rm -rf "$d"
-    env $v timeout -k 10 240 rocprofv3 --kernel-trace --stats -d "$d" -o run -- python3 bench.py $HEAD ${BENCH_ARGS:-} \
+    env $v timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d "$d" -o run -- python3 bench.py $HEAD ${BENCH_ARGS:-} \
         > "$d.log" 2>&1 || { echo "variant $v failed"; tail -5 "$d.log"; exit 1; }
     python3 - "$d" "$v" >> gpurun_out/$name.txt <<'PY'
 import csv, glob, json, sys
