@@ -910,6 +910,11 @@ def cpu_baseline(args, cfg, device):
         "cpu": cpu,
         "sample": f"{soa.n:,} reads x {scfg.n_cells} cells of the same generator (20k reads/cell, run params); "
                   f"oracle/mgp_oracle.c single-threaded, {dt:.1f}s",
+        "comparison": "the reference's per-read path restated in C on one core (oracle/mgp_oracle.c): at C4's "
+                      "density (> 2500 reads per cell) the reference itself runs its cells sequentially on one "
+                      "core (processors.py:96-103), and its Python does ~14k reads/s there (SURVEY.md §6 probe), "
+                      "so this port is ~130x the reference's own rate; value / this = the GPU's margin over the "
+                      "port, not over the reference",
     }
 
 

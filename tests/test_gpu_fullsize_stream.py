@@ -7,7 +7,7 @@ C5 configuration streamed and split by cell.
   pairing, streamed segments, and the 16-bit count rows written into pinned host
   memory as windows complete (mgp_set_rows16_target). Checked from the host rows the
   step delivered: the per-cell invariants over every cell, the run statistics and
-  tallies, a second step byte-identical, and 3 x 8 whole cells bit-exact against the
+  tallies, a second step byte-identical, and 8 x 8 whole cells bit-exact against the
   oracle on the quality-carrying full records of exactly their reads.
 * C5 (1B reads x 100k cells) streamed the same way at its best batch size (80M reads,
   profiles/r05/bench_c5_r5j.log), with the same checks.
@@ -97,8 +97,9 @@ def _streamed_full_size(engine_lib, oracle_lib, n, nc, seed, batch, ranges, chun
 def test_c4_streamed_headline_path_full_size(engine_lib, oracle_lib):
     """C4 exactly as the bench's timed step streams it (see the module docstring)."""
     nc = 10_000
-    _streamed_full_size(engine_lib, oracle_lib, 200_000_000, nc, 20251015 + 4, "auto",
-                        ((0, 8), (5000, 5008), (nc - 8, nc)), 2500)
+    # 8 ranges of 8 whole cells (64 cells, spread over the cell range) against the oracle
+    ranges = tuple((lo, lo + 8) for lo in (0, 1250, 2500, 3750, 5000, 6250, 7500, nc - 8))
+    _streamed_full_size(engine_lib, oracle_lib, 200_000_000, nc, 20251015 + 4, "auto", ranges, 2500)
 
 
 @pytest.mark.timeout(1200)
