@@ -88,6 +88,9 @@ def parse():
                     help="records of the headline (streamed, PCIe-inclusive) step: quality-carrying 64-byte records "
                          "the kernel filters per base (packed, default) or 32-byte records the producer made for "
                          "the run's min_baseq (pack32); dense in BAM order")
+    ap.add_argument("--rows", choices=["8", "16"], default="8",
+                    help="streamed step's rows target: 8 = the 8-bit target beside the 16-bit one (ABI 7), "
+                         "16 = the 16-bit target alone")
     ap.add_argument("--columns", choices=["16", "32"], default="16",
                     help="barcode index and |tlen| columns of the streamed batches: 16-bit (mgp_push_batch16, when "
                          "the cells and every |tlen| fit) or the 32-bit mgp_batch columns")
@@ -323,7 +326,8 @@ def main():
             "link": None if head is None else head["link"],
             "stream": None if head is None else {k: head[k] for k in ("batch_reads", "batches", "columns", "segments_per_run",
                                                                      "pileup_launches_per_run", "h2d_bytes_rank0",
-                                                                     "d2h_bytes_rank0", "rows_target")},
+                                                                     "d2h_bytes_rank0", "rows_target", "rows",
+                                                                     "rows8_windows_frac")},
             "device": dev,
             "device_paired": paired,
             "pcie_pack32": pcie_more,
@@ -630,6 +634,9 @@ def sample_check(eng, cfg, res, args, seed, cdf, ref, cell0: int, device: int, d
             "sampled cells' reads", "checked": ("the timed step's pinned host rows and per-cell statistics"
                                                 if delivered is not None else "rows fetched from the device"),
             "wide_cells": None if delivered is None else len(delivered.exact),
+            "windows_from_rows8": (None if delivered is None or delivered.rows8 is None else
+                                   sum(int(delivered.rows8.narrow[lo:hi].sum()) for lo, hi in ranges)),
+            "windows_checked": None if delivered is None else sum((hi - lo) * delivered.nw for lo, hi in ranges),
             "seconds": round(time.perf_counter() - t0, 2)}
 
 
@@ -639,10 +646,12 @@ class StreamSet:
     into pinned host memory as dense records in BAM order (a batch is a contiguous
     payload range), with 16-bit barcode and |tlen| columns (mgp_push_batch16, ABI 5)
     when every read allows, and the pinned 16-bit count rows the engine writes as its
-    windows complete (mgp_set_rows16_target)."""
+    windows complete (mgp_set_rows16_target), with the 8-bit target beside them
+    (mgp_set_rows_target, ABI 7: a (cell, window) whose values all fit a byte leaves as
+    half the bytes) unless rows8 is off."""
 
-    def __init__(self, eng, cfg, layout: str, columns16: bool = True):
-        from mgatk2_amd.engine import PinnedBuffer, Rows16
+    def __init__(self, eng, cfg, layout: str, columns16: bool = True, rows8: bool = True):
+        from mgatk2_amd.engine import PinnedBuffer, Rows8, Rows16
 
         self.eng, self.cfg, self.layout = eng, cfg, layout
         self.rb = 32 if layout == "pack32" else 64  # dense records in BAM order
@@ -681,19 +690,28 @@ class StreamSet:
         self.host = host
         L, nc = cfg.mito_len, cfg.n_cells
         nw, W = eng.windows()
-        self.rbuf = PinnedBuffer(nc * L * 22 + nc * nw + 4096)
+        self.nw = nw
+        o8 = (nc * L * 22 + nc * nw + 4095) & ~4095  # the 8-bit target after the 16-bit one
+        self.rbuf = PinnedBuffer(o8 + (nc * L * 11 + nc * nw if rows8 else 0) + 4096)
         rbuf = self.rbuf
         self.rows = Rows16(rbuf.array((nc, L, 8), np.uint16, 0), rbuf.array((nc, L, 2), np.uint16, nc * L * 16),
                            rbuf.array((nc, L), np.uint16, nc * L * 20), rbuf.array((nc, nw), np.uint8, nc * L * 22), W)
+        self.rows8 = Rows8(rbuf.array((nc, L, 8), np.uint8, o8), rbuf.array((nc, L, 2), np.uint8, o8 + nc * L * 8),
+                           rbuf.array((nc, L), np.uint8, o8 + nc * L * 10),
+                           rbuf.array((nc, nw), np.uint8, o8 + nc * L * 11)) if rows8 else None
         # the rows leave the device as the windows complete, beside the later batches' H2D
+        # (MGP_BENCH_ABL_NO_ROWS=1, an A/B only: the rows stay on the device, no D2H)
+        self.abl_no_rows = os.environ.get("MGP_BENCH_ABL_NO_ROWS") == "1"
         try:
-            eng.set_rows16_target(self.rows)
+            if not self.abl_no_rows:
+                eng.set_rows_target(self.rows, self.rows8)
             self.rows_target = True
         except Exception as e:  # (pinned memory the device cannot map: copy the rows after the run)
             print(f"[bench] rows target unavailable ({e}); rows fetched after the run", file=sys.stderr)
             self.rows_target = False
         self.h2d = self.col_bytes + pay
         self.d2h = nc * L * 22 + nc * nw + nc * 34 + L * 4 * 8  # rows, wide flags, per-cell arrays, tallies
+        # (with the 8-bit target: d2h_bytes() after a step, from the narrow flags)
         self.exact = {}  # cell -> its exact u32 rows (EngineResult of one cell) when a window of it is wide
 
     def auto_batch(self, b) -> int:
@@ -722,6 +740,8 @@ class StreamSet:
         eng.run()
         if not self.rows_target:
             eng.fetch_rows16(0, self.cfg.n_cells, out=self.rows)
+            if self.rows8 is not None:
+                self.rows8.narrow.fill(0)
         res = eng.fetch(dense=False)  # (waits for the rows' copies too)
         self.exact = {}
         if self.rows.wide.any():
@@ -733,14 +753,34 @@ class StreamSet:
         """Cells [lo, hi) as the step delivered them to host memory: the pinned 16-bit
         rows widened to u32 (exact: no wide window), or the exact rows fetched for a
         cell with a wide window."""
-        r = self.rows
-        out = {"counts": r.counts[lo:hi].astype(np.uint32), "tn5": r.tn5[lo:hi].astype(np.uint32),
-               "depth": r.depth[lo:hi].astype(np.uint32)}
+        from mgatk2_amd.engine import merge_rows
+
+        out = merge_rows(self.rows, self.rows8, lo, hi)
         for c, e in self.exact.items():
             if lo <= c < hi:
                 for k in out:
                     out[k][c - lo] = getattr(e, k)[0]
         return out
+
+    def rows16(self, lo: int, hi: int):
+        """Cells [lo, hi) as one 16-bit Rows16 (copies: the 8-bit target's windows
+        widened into the 16-bit rows), the form mgp_fetch_rows16 gives."""
+        from mgatk2_amd.engine import Rows16, merge_rows
+
+        m = merge_rows(self.rows, self.rows8, lo, hi)
+        return Rows16(m["counts"].astype(np.uint16), m["tn5"].astype(np.uint16), m["depth"].astype(np.uint16),
+                      self.rows.wide[lo:hi].copy(), self.rows.window_width)
+
+    def d2h_bytes(self) -> int:
+        """Bytes of the last step's results to host memory: 22 per position of a 16-bit
+        window, 11 of an 8-bit one, the flags, per-cell arrays and tallies."""
+        nc, L = self.cfg.n_cells, self.cfg.mito_len
+        if self.rows8 is None:
+            return self.d2h
+        W = self.rows.window_width
+        wl = np.minimum(W, L - W * np.arange(self.nw))  # positions per window
+        narrow_pos = int((self.rows8.narrow.astype(np.int64) * wl).sum())
+        return self.d2h - 11 * narrow_pos + nc * self.nw
 
 
 def stream_leg(ctx: Ctx, layout: str, batch_list: list, timed: bool) -> dict:
@@ -763,7 +803,7 @@ def stream_leg(ctx: Ctx, layout: str, batch_list: list, timed: bool) -> dict:
     t0 = time.time()
     eng.synth(ctx.seed, args.reads, ctx.cdf, ctx.ref, read_len=args.read_len, rec_align=64, pack=True, pack32=p32,
               **ctx.shard)
-    ss = StreamSet(eng, cfg, layout, columns16=args.columns == "16")
+    ss = StreamSet(eng, cfg, layout, columns16=args.columns == "16", rows8=args.rows == "8")
     n, rb, narrow, rows_target = ss.n, ss.rb, ss.narrow, ss.rows_target
     L, nc = cfg.mito_len, cfg.n_cells
     print(f"[bench] rank {ctx.rank}: stream leg {layout}: {n:,} reads ({ss.h2d / 1e9:.2f} GB pinned) "
@@ -790,6 +830,7 @@ def stream_leg(ctx: Ctx, layout: str, batch_list: list, timed: bool) -> dict:
                 dt_max = ctx.reduce(min(ts), "max")
                 legs.append({"batch_reads": bs, "batches": len(batches), "streamed": stream, "segments": int(segs),
                              "s": dt_max, "value": ctx.reduce(float(n), "sum") / dt_max})
+        d2h = ss.d2h_bytes()
         eng.close()
         best = max((lg for lg in legs if lg["streamed"]), key=lambda lg: lg["value"])
         return {"record_layout": layout, "value": best["value"], "best_batch_reads": best["batch_reads"],
@@ -824,6 +865,8 @@ def stream_leg(ctx: Ctx, layout: str, batch_list: list, timed: bool) -> dict:
     if ctx.rank == 0 and not args.no_check:
         check = sample_check(eng, cfg, res, args, ctx.seed, ctx.cdf, ctx.ref, ctx.cell0, ctx.device, delivered=ss)
     wide_cells = len(ss.exact)
+    d2h = ss.d2h_bytes()
+    narrow_frac = None if ss.rows8 is None else float(ss.rows8.narrow.mean())
     eng.close()
     return {
         "record_layout": layout,
@@ -849,6 +892,9 @@ def stream_leg(ctx: Ctx, layout: str, batch_list: list, timed: bool) -> dict:
         "h2d_bytes_rank0": h2d,
         "d2h_bytes_rank0": d2h,
         "rows_target": rows_target,
+        "rows": ("16-bit rows, and 8-bit rows for the (cell, window) pairs whose values all fit a byte "
+                 "(mgp_set_rows_target)" if ss.rows8 is not None else "16-bit rows (mgp_set_rows16_target)"),
+        "rows8_windows_frac": narrow_frac,
         "wide_cells": wide_cells,
         "link": {"bound": "pcie", "h2d_GBps": round(h2d / step_s / 1e9, 2), "d2h_GBps": round(d2h / step_s / 1e9, 2),
                  "peak_GBps_per_direction": PCIE_PEAK_GBS, "h2d_frac": round(h2d / step_s / 1e9 / PCIE_PEAK_GBS, 3),

@@ -46,7 +46,7 @@
 extern "C" {
 #endif
 
-#define MGP_ABI_VERSION 6  /* 2: fixed seq/CIGAR offsets for reads <= 64 bases;
+#define MGP_ABI_VERSION 7  /* 2: fixed seq/CIGAR offsets for reads <= 64 bases;
                               3: synth cell shards, cell-range and 16-bit fetches, streaming runs;
                               4: batches without rec_off / span columns and the rows target (the
                                  round-3 "v3.1" entry points), pushed records checked against
@@ -57,7 +57,8 @@ extern "C" {
                                  mgp_push_batch16 (16-bit barcode / |tlen| columns), dense
                                  64-byte batches paired on the device;
                               6: mgp_txt_gz_* (the txt count files formatted and deflated on the
-                                 device) */
+                                 device);
+                              7: mgp_set_rows_target (an 8-bit rows target beside the 16-bit one) */
 
 /* ---- return codes (0 = success) ------------------------------------------ */
 #define MGP_OK               0
@@ -543,6 +544,22 @@ int  mgp_txt_gz_rows(int device, const uint32_t *counts, const uint32_t *depth, 
  * reference's per-cell write_cell after each worker (processors.py:112-144): results
  * leave the device while ingest continues. */
 int  mgp_set_rows16_target(mgp_ctx *ctx, const mgp_rows16 *rows);
+/* The 8-bit form of the same rows (ABI 7): a (cell, window) whose every count, tn5 cut
+ * and depth is at most 255 (the pileup's flush knows it when it writes the window) has
+ * its rows written here, one byte per value, and `narrow` set; the others go to the
+ * 16-bit target as before (narrow 0). Exact values: the 16-bit target where narrow is 0
+ * and wide is 0, these bytes where narrow is 1, mgp_fetch_cells where wide is 1. Half
+ * the bytes leave the device for a cell of depth below 256 (the rows cross the host
+ * link while later batches still come the other way). */
+typedef struct mgp_rows8 {
+    uint8_t *counts;    /* [cells][mito_len][8] (pinned, mgp_host_alloc) */
+    uint8_t *tn5;       /* [cells][mito_len][2]                          */
+    uint8_t *depth;     /* [cells][mito_len]                             */
+    uint8_t *narrow;    /* [cells][n_windows]: 1 = this window's rows are here */
+} mgp_rows8;
+/* mgp_set_rows16_target(ctx, rows16) with the 8-bit target rows8 beside it (NULL: the
+ * 16-bit target alone); rows16 NULL stops both. */
+int  mgp_set_rows_target(mgp_ctx *ctx, const mgp_rows16 *rows16, const mgp_rows8 *rows8);
 /* Position windows of the pileup (the `wide` flags' second dimension). */
 int  mgp_windows(mgp_ctx *ctx, int32_t *n_windows, int32_t *window_width);
 /* Wait until the H2D copies of every batch pushed so far have completed: the caller may

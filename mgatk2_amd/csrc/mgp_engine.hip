@@ -134,6 +134,8 @@ struct mgp_ctx {
     hipEvent_t ev_rows = nullptr;
     mgp_rows16 rows_tgt{};
     bool rows_on = false;
+    mgp_rows8 rows8_tgt{};  // mgp_set_rows_target: the 8-bit target of the windows that fit (ABI 7)
+    bool rows8_on = false;
     bool rows_pending = false;  // the run's last segment's rows: copied by run_finish
     int rows_p0 = 0, rows_p1 = 0;
     hipEvent_t ev_copy = nullptr, ev_fork = nullptr, ev_join = nullptr;
@@ -197,7 +199,7 @@ struct mgp_ctx {
     DevBuf pel, tally_part, tally, dup_part;
     DevBuf n_reads, any_paired, passed, covered, dsum, dmax, med_lo, med_hi, first_read;
     DevBuf counts, tn5, depth, stats;  // u32 rows: drained windows, and mgp_fetch's widened copy
-    DevBuf counts16, tn5_16, depth16, wide;  // the run's 16-bit result rows (Out16)
+    DevBuf counts16, tn5_16, depth16, wide, fit8;  // the run's 16-bit result rows (Out16)
 
     bool ran = false;
     int last_status = MGP_OK;
@@ -2198,6 +2200,7 @@ struct Out16 {
     uint32_t* tn5;     // [cells][L]: fwd | rev << 16
     uint16_t* depth;   // [cells][L]
     uint8_t* wide;     // [cells][nwin]: 1 = exact values in the u32 arrays
+    uint8_t* fit8;     // [cells][nwin]: 1 = every value of the window's rows is <= 255 (the 8-bit target)
 };
 
 __device__ __forceinline__ uint32_t sat16(uint32_t v) { return v > 0xFFFFu ? 0xFFFFu : v; }
@@ -2229,7 +2232,7 @@ __global__ void __launch_bounds__(kBlock, MGP_PILEUP_WAVES) k_pileup(
     uint32_t* const t5 = tile + kPlaneTn5 * kTilePitch;
     if (__atomic_load_n(&st->err, __ATOMIC_RELAXED) & ERR_BOUNDS) return;  // unsorted input (k_bin_count)
     __shared__ uint32_t wq_all[kBlock / kWave][kWaveQ];
-    __shared__ uint32_t r_cov[4], r_max[4], r_keep[4];
+    __shared__ uint32_t r_cov[4], r_max[4], r_keep[4], r_big[4];
     __shared__ unsigned long long r_sum[4];
 
     // the workgroups take the chunks largest first (chunk_perm, k_scan_cells), all
@@ -2376,7 +2379,7 @@ __global__ void __launch_bounds__(kBlock, MGP_PILEUP_WAVES) k_pileup(
         }
         nkeep = wave_sum(nkeep);
         __syncthreads();
-        uint32_t cov = 0, mx = 0;
+        uint32_t cov = 0, mx = 0, big = 0;  // big: a value of the rows above 255
         unsigned long long sum = 0;
 #pragma unroll
         for (int m = 0; m < kMaxPosPerThread; ++m) {
@@ -2451,8 +2454,10 @@ __global__ void __launch_bounds__(kBlock, MGP_PILEUP_WAVES) k_pileup(
                 cov += d > 0;
                 sum += d;
                 mx = d > mx ? d : mx;
+                big |= (d | tf | tr) > 0xFFu;  // (every count is at most d)
             }
         }
+        const bool anybig = __ballot(big != 0u) != 0ull;
         cov = wave_sum(cov);
         sum = wave_sum(sum);
         mx = wave_max(mx);
@@ -2461,10 +2466,12 @@ __global__ void __launch_bounds__(kBlock, MGP_PILEUP_WAVES) k_pileup(
             r_sum[wid] = sum;
             r_max[wid] = mx;
             r_keep[wid] = nkeep;
+            r_big[wid] = anybig;
         }
         __syncthreads();
         if (threadIdx.x == 0) {
             o16.wide[(size_t)c * g.nwin + k] = drained ? 1u : 0u;
+            o16.fit8[(size_t)c * g.nwin + k] = (drained || r_big[0] || r_big[1] || r_big[2] || r_big[3]) ? 0u : 1u;
             uint32_t C = 0, M = 0, K = 0;
             unsigned long long S = 0;
             for (int q = 0; q < 4; ++q) {
@@ -2507,7 +2514,8 @@ __global__ void __launch_bounds__(kBlock) k_gate_fixup(Geom g, int min_reads, co
                                                        unsigned long long* __restrict__ dsum,
                                                        uint32_t* __restrict__ dmax, uint32_t* __restrict__ tally_part,
                                                        uint4* __restrict__ hc, uint32_t* __restrict__ ht,
-                                                       uint16_t* __restrict__ hd) {
+                                                       uint16_t* __restrict__ hd, uint2* __restrict__ hc8,
+                                                       uint16_t* __restrict__ ht8, uint8_t* __restrict__ hd8) {
     // hc/ht/hd (mgp_set_rows16_target, else null): the pinned host rows, which the
     // segments' k_rows_to_host already wrote: the dropped cell's rows are zeroed there too
     const int c = blockIdx.x;
@@ -2546,6 +2554,11 @@ __global__ void __launch_bounds__(kBlock) k_gate_fixup(Geom g, int min_reads, co
             hc[P] = make_uint4(0, 0, 0, 0);
             ht[P] = 0u;
             hd[P] = 0;
+        }
+        if (hc8) {  // (the 8-bit target, ABI 7: whichever of the two holds the window)
+            hc8[P] = make_uint2(0, 0);
+            ht8[P] = 0;
+            hd8[P] = 0;
         }
     }
     __syncthreads();
@@ -2825,6 +2838,41 @@ __global__ void __launch_bounds__(kBlock) k_rows_to_host(int L, int nc, int p0, 
         hc[P] = c16[P];
         ht[P] = t16[P];
         hd[P] = d16[P];
+    }
+}
+
+// the low bytes of the four u16 halves of x, y (x's first)
+__device__ __forceinline__ uint32_t low_bytes(uint32_t x, uint32_t y) {
+    return (x & 0xFFu) | ((x >> 8) & 0xFF00u) | ((y & 0xFFu) << 16) | ((y << 8) & 0xFF000000u);
+}
+
+// The same with the 8-bit target beside (mgp_set_rows_target, ABI 7): a position of a
+// (cell, window) whose values all fit a byte (fit8, set by the pileup's flush) leaves as
+// 11 bytes instead of 22
+__global__ void __launch_bounds__(kBlock) k_rows_to_host8(int L, int nc, int p0, int p1, int W, int nwin,
+                                                          const uint4* __restrict__ c16, const uint32_t* __restrict__ t16,
+                                                          const uint16_t* __restrict__ d16,
+                                                          const uint8_t* __restrict__ fit8, uint4* __restrict__ hc,
+                                                          uint32_t* __restrict__ ht, uint16_t* __restrict__ hd,
+                                                          uint2* __restrict__ hc8, uint16_t* __restrict__ ht8,
+                                                          uint8_t* __restrict__ hd8) {
+    const int p = p0 + (int)(blockIdx.x * blockDim.x + threadIdx.x);
+    if (p >= p1) return;
+    const int k = p / W;
+    for (int c = blockIdx.y; c < nc; c += gridDim.y) {
+        const size_t P = (size_t)c * L + p;
+        const uint4 a = c16[P];
+        const uint32_t t = t16[P];
+        const uint16_t d = d16[P];
+        if (fit8[(size_t)c * nwin + k]) {  // (u16 pairs -> bytes: the low byte of each half)
+            hc8[P] = make_uint2(low_bytes(a.x, a.y), low_bytes(a.z, a.w));
+            ht8[P] = (uint16_t)((t & 0xFFu) | ((t >> 8) & 0xFF00u));
+            hd8[P] = (uint8_t)d;
+        } else {
+            hc[P] = a;
+            ht[P] = t;
+            hd[P] = d;
+        }
     }
 }
 
@@ -3356,7 +3404,8 @@ void mgp_close(mgp_ctx* ctx) {
                       &ctx->tally_part, &ctx->tally,   &ctx->n_reads,    &ctx->any_paired,
                       &ctx->passed,    &ctx->covered,   &ctx->dsum,     &ctx->dmax,       &ctx->med_lo,
                       &ctx->med_hi,    &ctx->first_read, &ctx->counts,  &ctx->tn5,        &ctx->depth,
-                      &ctx->stats,     &ctx->counts16,  &ctx->tn5_16,  &ctx->depth16,    &ctx->wide};
+                      &ctx->stats,     &ctx->counts16,  &ctx->tn5_16,  &ctx->depth16,    &ctx->wide,
+                      &ctx->fit8};
     for (DevBuf* b : bufs) b->release();
     for (auto e : ctx->seg_ev) (void)hipEventDestroy(e);
     for (int r = 0; r < mgp_ctx::kRing; ++r)
@@ -3650,6 +3699,7 @@ static int ensure_run_buffers(mgp_ctx* ctx) {
     MGP_TRY(ctx->tn5_16.ensure(nc * L * 4));
     MGP_TRY(ctx->depth16.ensure(nc * L * 2));
     MGP_TRY(ctx->wide.ensure(nc * (size_t)std::max(g.nwin, 1)));
+    MGP_TRY(ctx->fit8.ensure(nc * (size_t)std::max(g.nwin, 1)));
     MGP_TRY(ctx->stats.ensure(sizeof(DevStats)));
     return MGP_OK;
 }
@@ -3660,6 +3710,7 @@ static Out16 out16_of(mgp_ctx* ctx) {
     o.tn5 = ctx->tn5_16.as<uint32_t>();
     o.depth = ctx->depth16.as<uint16_t>();
     o.wide = ctx->wide.as<uint8_t>();
+    o.fit8 = ctx->fit8.as<uint8_t>();
     return o;
 }
 
@@ -3683,6 +3734,28 @@ struct Seg {
     bool last;    // the run's last segment: its rows leave after the medians (run_finish)
 };
 
+// k_rows_to_host (or k_rows_to_host8 with an 8-bit target) over positions [p0, p1) on the
+// D2H stream
+static int rows_launch(mgp_ctx* ctx, dim3 gr, int p0, int p1) {
+    const Geom& g = ctx->g;
+    const mgp_rows16& t = ctx->rows_tgt;
+    if (ctx->rows8_on) {
+        const mgp_rows8& t8 = ctx->rows8_tgt;
+        k_rows_to_host8<<<gr, kBlock, 0, ctx->s_d2h>>>(
+            g.L, g.nc, p0, p1, g.W, g.nwin, ctx->counts16.as<uint4>(), ctx->tn5_16.as<uint32_t>(),
+            ctx->depth16.as<uint16_t>(), ctx->fit8.as<uint8_t>(), reinterpret_cast<uint4*>(t.counts),
+            reinterpret_cast<uint32_t*>(t.tn5), t.depth, reinterpret_cast<uint2*>(t8.counts),
+            reinterpret_cast<uint16_t*>(t8.tn5), t8.depth);
+    } else {
+        k_rows_to_host<<<gr, kBlock, 0, ctx->s_d2h>>>(g.L, g.nc, p0, p1, ctx->counts16.as<uint4>(),
+                                                    ctx->tn5_16.as<uint32_t>(), ctx->depth16.as<uint16_t>(),
+                                                    reinterpret_cast<uint4*>(t.counts),
+                                                    reinterpret_cast<uint32_t*>(t.tn5), t.depth);
+    }
+    HIP_TRY(hipGetLastError());
+    return MGP_OK;
+}
+
 // The rows of windows' positions [p0, p1) of every cell to the host target, on the D2H
 // stream behind the compute stream's work so far (mgp_set_rows16_target): written by a
 // kernel into the mapped pinned target (a strided 2D copy of 10k rows per segment runs as
@@ -3692,19 +3765,13 @@ static int rows_copy(mgp_ctx* ctx, int p0, int p1) {
     const int nc = g.nc;
     HIP_TRY(hipEventRecord(ctx->ev_rows, ctx->s_comp));
     HIP_TRY(hipStreamWaitEvent(ctx->s_d2h, ctx->ev_rows, 0));
-    const mgp_rows16& t = ctx->rows_tgt;
     // a few hundred workgroups looping over the cells: the stores wait on the host
     // link, and a grid of one workgroup per (cell, 256 positions) held every CU
     // slot of the device while they drained, starving the kernels of the next
     // segment and the run's medians (MGP_ROWS_WG)
     const unsigned gx = (unsigned)((p1 - p0 + kBlock - 1) / kBlock);
     dim3 gr(gx, (unsigned)std::max(1, std::min(std::min(nc, 65535), ctx->rows_wg / (int)gx)));
-    k_rows_to_host<<<gr, kBlock, 0, ctx->s_d2h>>>(g.L, nc, p0, p1, ctx->counts16.as<uint4>(),
-                                                ctx->tn5_16.as<uint32_t>(), ctx->depth16.as<uint16_t>(),
-                                                reinterpret_cast<uint4*>(t.counts), reinterpret_cast<uint32_t*>(t.tn5),
-                                                t.depth);
-    HIP_TRY(hipGetLastError());
-    return MGP_OK;
+    return rows_launch(ctx, gr, p0, p1);
 }
 
 static int run_segment(mgp_ctx* ctx, const Seg& sg, int slot, int& dup_parts, int& pair_mode) {
@@ -4018,7 +4085,7 @@ static int run_finish(mgp_ctx* ctx, int slot, int dup_parts, bool streamed) {
             STAGE_BEGIN(ST_GATE);
             // with a rows target, the rows already sent (the last segment's copies run on
             // the D2H stream) are final before the gate rewrites the dropped cells there
-            const bool tgt = ctx->rows_on;
+            const bool tgt = ctx->rows_on, tgt8 = tgt && ctx->rows8_on;
             if (tgt) {
                 HIP_TRY(hipEventRecord(ctx->ev_rows, ctx->s_d2h));
                 HIP_TRY(hipStreamWaitEvent(s, ctx->ev_rows, 0));
@@ -4030,7 +4097,10 @@ static int run_finish(mgp_ctx* ctx, int slot, int dup_parts, bool streamed) {
                                                ctx->tally_part.as<uint32_t>(),
                                                tgt ? reinterpret_cast<uint4*>(ctx->rows_tgt.counts) : nullptr,
                                                tgt ? reinterpret_cast<uint32_t*>(ctx->rows_tgt.tn5) : nullptr,
-                                               tgt ? ctx->rows_tgt.depth : nullptr);
+                                               tgt ? ctx->rows_tgt.depth : nullptr,
+                                               tgt8 ? reinterpret_cast<uint2*>(ctx->rows8_tgt.counts) : nullptr,
+                                               tgt8 ? reinterpret_cast<uint16_t*>(ctx->rows8_tgt.tn5) : nullptr,
+                                               tgt8 ? ctx->rows8_tgt.depth : nullptr);
             HIP_TRY(hipGetLastError());
             STAGE_END(ST_GATE);
         }
@@ -4091,6 +4161,9 @@ static int run_finish(mgp_ctx* ctx, int slot, int dup_parts, bool streamed) {
         HIP_TRY(hipStreamWaitEvent(ctx->s_d2h, ctx->ev_rows, 0));
         HIP_TRY(hipMemcpyAsync(ctx->rows_tgt.wide, ctx->wide.p, (size_t)nc * g.nwin, hipMemcpyDeviceToHost,
                                ctx->s_d2h));
+        if (ctx->rows8_on)
+            HIP_TRY(hipMemcpyAsync(ctx->rows8_tgt.narrow, ctx->fit8.p, (size_t)nc * g.nwin, hipMemcpyDeviceToHost,
+                                   ctx->s_d2h));
     }
 
     // 9. tallies over ranks; the slot after them carries the ranks' ERR_RESPEC so that
@@ -4278,7 +4351,18 @@ int mgp_windows(mgp_ctx* ctx, int32_t* n_windows, int32_t* window_width) {
     return MGP_OK;
 }
 
-int mgp_set_rows16_target(mgp_ctx* ctx, const mgp_rows16* rows) {
+// the device's mapping of a pinned host array (the rows targets)
+static int mapped(void* host, void** dev) {
+    void* dp = nullptr;
+    if (!host || hipHostGetDevicePointer(&dp, host, 0) != hipSuccess || !dp) {
+        (void)hipGetLastError();
+        return set_err(MGP_E_INVALID, "rows target not in pinned host memory (mgp_host_alloc)");
+    }
+    *dev = dp;
+    return MGP_OK;
+}
+
+int mgp_set_rows_target(mgp_ctx* ctx, const mgp_rows16* rows, const mgp_rows8* rows8) {
     if (!ctx) return set_err(MGP_E_INVALID, "null ctx");
     // (set during a streaming run: the windows piled so far are copied at once, below;
     // replacing or clearing a target mid-run is not allowed)
@@ -4288,39 +4372,47 @@ int mgp_set_rows16_target(mgp_ctx* ctx, const mgp_rows16* rows) {
     HIP_TRY(hipStreamSynchronize(ctx->s_d2h));
     if (!rows) {
         ctx->rows_on = false;
+        ctx->rows8_on = false;
         return MGP_OK;
     }
     if (!rows->counts || !rows->tn5 || !rows->depth || !rows->wide) return set_err(MGP_E_INVALID, "null rows array");
+    if (rows8 && (!rows8->counts || !rows8->tn5 || !rows8->depth || !rows8->narrow))
+        return set_err(MGP_E_INVALID, "null rows8 array");
     // the kernel writes the rows through the device's mapping of the pinned arrays
     mgp_rows16 d{};
     void* dp = nullptr;
-    if (hipHostGetDevicePointer(&dp, rows->counts, 0) != hipSuccess || !dp)
-        return set_err(MGP_E_INVALID, "rows target not in pinned host memory (mgp_host_alloc)");
+    MGP_TRY(mapped(rows->counts, &dp));
     d.counts = static_cast<uint16_t*>(dp);
-    if (hipHostGetDevicePointer(&dp, rows->tn5, 0) != hipSuccess || !dp)
-        return set_err(MGP_E_INVALID, "rows target not in pinned host memory (mgp_host_alloc)");
+    MGP_TRY(mapped(rows->tn5, &dp));
     d.tn5 = static_cast<uint16_t*>(dp);
-    if (hipHostGetDevicePointer(&dp, rows->depth, 0) != hipSuccess || !dp)
-        return set_err(MGP_E_INVALID, "rows target not in pinned host memory (mgp_host_alloc)");
+    MGP_TRY(mapped(rows->depth, &dp));
     d.depth = static_cast<uint16_t*>(dp);
     d.wide = rows->wide;  // (an async copy: the host pointer)
-    (void)hipGetLastError();
+    mgp_rows8 d8{};
+    if (rows8) {
+        MGP_TRY(mapped(rows8->counts, &dp));
+        d8.counts = static_cast<uint8_t*>(dp);
+        MGP_TRY(mapped(rows8->tn5, &dp));
+        d8.tn5 = static_cast<uint8_t*>(dp);
+        MGP_TRY(mapped(rows8->depth, &dp));
+        d8.depth = static_cast<uint8_t*>(dp);
+        d8.narrow = rows8->narrow;  // (an async copy: the host pointer)
+    }
     ctx->rows_tgt = d;
+    ctx->rows8_tgt = d8;
     ctx->rows_on = true;
+    ctx->rows8_on = rows8 != nullptr;
     if (ctx->seg_open && ctx->w_done > 0) {  // catch up: the rows of the windows piled before
         const Geom& g = ctx->g;
         const int p1 = std::min(g.L, ctx->w_done * g.W);
         HIP_TRY(hipEventRecord(ctx->ev_rows, ctx->s_comp));
         HIP_TRY(hipStreamWaitEvent(ctx->s_d2h, ctx->ev_rows, 0));
-        dim3 gr((unsigned)((p1 + kBlock - 1) / kBlock), (unsigned)std::min(g.nc, 65535));
-        k_rows_to_host<<<gr, kBlock, 0, ctx->s_d2h>>>(g.L, g.nc, 0, p1, ctx->counts16.as<uint4>(),
-                                                    ctx->tn5_16.as<uint32_t>(), ctx->depth16.as<uint16_t>(),
-                                                    reinterpret_cast<uint4*>(d.counts), reinterpret_cast<uint32_t*>(d.tn5),
-                                                    d.depth);
-        HIP_TRY(hipGetLastError());
+        MGP_TRY(rows_launch(ctx, dim3((unsigned)((p1 + kBlock - 1) / kBlock), (unsigned)std::min(g.nc, 65535)), 0, p1));
     }
     return MGP_OK;
 }
+
+int mgp_set_rows16_target(mgp_ctx* ctx, const mgp_rows16* rows) { return mgp_set_rows_target(ctx, rows, nullptr); }
 
 int mgp_copy_wait(mgp_ctx* ctx) {
     if (!ctx) return set_err(MGP_E_INVALID, "null ctx");

@@ -39,7 +39,6 @@ namespace txtgz {
 constexpr int kT = 256;        // threads per member (one segment each)
 constexpr int kJ = 16;         // previous lines searched for matches
 constexpr int kLMax = 31;      // longest match tried (longer ones gain nothing on C4-like text)
-constexpr int kRing = 32;      // DP cost ring (> kLMax), u16 costs compared by differences
 constexpr int kMaxDist = 32768;
 constexpr int kLit = 286, kDist = 30;
 constexpr int kWinBytes = 24 * 1024;  // LDS text window of the match finder
@@ -556,7 +555,7 @@ __global__ void __launch_bounds__(kT) k_txt_format(Job job, Scratch sc) {
     uint64_t tot;
     const uint64_t pre = block_excl_scan(((uint64_t)my_b << 24) | my_n, S.wsum, tot);
     const int t0 = (int)(pre >> 24), t1 = t0 + (int)my_b;
-    const int l0 = (int)(pre & 0xFFFFFFu), l1 = l0 + (int)my_n;
+    const int l0 = (int)(pre & 0xFFFFFFu);
     {
         uint8_t* w = T + t0;
         int k = l0;

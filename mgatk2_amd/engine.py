@@ -39,9 +39,9 @@ ABI_SYMBOLS = (
     "mgp_finish", "mgp_kernel_times", "mgp_comm_unique_id", "mgp_comm_init", "mgp_synth_generate",
     "mgp_download_inputs", "mgp_set_stage_timing", "mgp_fetch_cells", "mgp_fetch_rows16", "mgp_windows",
     "mgp_stream_info", "mgp_set_streaming", "mgp_set_rows16_target", "mgp_copy_wait", "mgp_set_cell_range",
-    "mgp_push_batch16", "mgp_txt_gz_run", "mgp_txt_gz_fetch", "mgp_txt_gz_rows",
+    "mgp_push_batch16", "mgp_txt_gz_run", "mgp_txt_gz_fetch", "mgp_txt_gz_rows", "mgp_set_rows_target",
 )
-ABI_VERSION = 6
+ABI_VERSION = 7
 CFG_KEEP_TN5 = 0x1
 CFG_STREAM = 0x2
 
@@ -166,6 +166,15 @@ class mgp_rows16(C.Structure):
     ]
 
 
+class mgp_rows8(C.Structure):
+    _fields_ = [
+        ("counts", C.c_void_p),
+        ("tn5", C.c_void_p),
+        ("depth", C.c_void_p),
+        ("narrow", C.c_void_p),
+    ]
+
+
 _lib = None
 
 
@@ -209,6 +218,7 @@ def load_library(path: Path | None = None) -> C.CDLL:
         "mgp_fetch_cells": ([vp, i32, i32, C.POINTER(mgp_result)], C.c_int),
         "mgp_fetch_rows16": ([vp, i32, i32, C.POINTER(mgp_rows16)], C.c_int),
         "mgp_set_rows16_target": ([vp, C.POINTER(mgp_rows16)], C.c_int),
+        "mgp_set_rows_target": ([vp, C.POINTER(mgp_rows16), C.POINTER(mgp_rows8)], C.c_int),
         "mgp_windows": ([vp, C.POINTER(i32), C.POINTER(i32)], C.c_int),
         "mgp_stream_info": ([vp, C.POINTER(i64), C.POINTER(i32)], C.c_int),
         "mgp_set_streaming": ([vp, C.c_int], C.c_int),
@@ -344,6 +354,39 @@ class Rows16:
     def wide_cells(self) -> np.ndarray:
         """Cells (range-relative) with a window whose 16-bit rows are not exact."""
         return np.flatnonzero(self.wide.any(axis=1))
+
+
+@dataclass
+class Rows8:
+    """The 8-bit rows target beside a Rows16 one (mgp_rows8, ABI 7): the rows of the
+    (cell, window) pairs whose values all fit a byte (`narrow`); the others are in the
+    16-bit target."""
+
+    counts: np.ndarray  # [cells, L, 8] u8
+    tn5: np.ndarray  # [cells, L, 2] u8
+    depth: np.ndarray  # [cells, L] u8
+    narrow: np.ndarray  # [cells, n_windows] u8
+
+
+def merge_rows(r16: Rows16, r8: Rows8 | None, lo: int, hi: int) -> dict:
+    """Cells [lo, hi) of a rows target as u32 arrays (counts, tn5, depth): each window
+    from the 8-bit target where it is narrow, else from the 16-bit one (exact unless
+    r16.wide)."""
+    out = {"counts": r16.counts[lo:hi].astype(np.uint32), "tn5": r16.tn5[lo:hi].astype(np.uint32),
+           "depth": r16.depth[lo:hi].astype(np.uint32)}
+    if r8 is None:
+        return out
+    W = r16.window_width
+    L = out["depth"].shape[1]
+    nar = r8.narrow[lo:hi].astype(bool)
+    for k in range(nar.shape[1]):
+        m = np.flatnonzero(nar[:, k])
+        if m.size == 0:
+            continue
+        a, b = k * W, min(L, (k + 1) * W)
+        for key in ("counts", "tn5", "depth"):
+            out[key][m, a:b] = getattr(r8, key)[lo + m, a:b]
+    return out
 
 
 def batch_struct(soa: ReadSoA) -> mgp_batch:
@@ -617,6 +660,25 @@ class Engine:
         r = mgp_rows16(_ptr(rows.counts), _ptr(rows.tn5), _ptr(rows.depth), _ptr(rows.wide))
         _ck(self.lib.mgp_set_rows16_target(self._h, C.byref(r)), "mgp_set_rows16_target")
         self._rows_tgt = rows  # kept alive while the engine copies into it
+
+    def set_rows_target(self, rows: Rows16 | None, rows8: Rows8 | None = None):
+        """mgp_set_rows_target (ABI 7): set_rows16_target with the 8-bit target beside
+        it (the windows whose values all fit a byte leave as half the bytes; merge_rows
+        reads them back)."""
+        if rows is None or rows8 is None:
+            self.set_rows16_target(rows)
+            return
+        nw, _ = self.windows()
+        L, m = self.cfg.mito_len, self.cfg.n_cells
+        for a, shape in ((rows.counts, (m, L, 8)), (rows.tn5, (m, L, 2)), (rows.depth, (m, L)), (rows.wide, (m, nw)),
+                         (rows8.counts, (m, L, 8)), (rows8.tn5, (m, L, 2)), (rows8.depth, (m, L)),
+                         (rows8.narrow, (m, nw))):
+            if a.shape != shape or not a.flags["C_CONTIGUOUS"]:
+                raise InvalidInputError(f"rows array of shape {a.shape}, expected {shape}")
+        r = mgp_rows16(_ptr(rows.counts), _ptr(rows.tn5), _ptr(rows.depth), _ptr(rows.wide))
+        r8 = mgp_rows8(_ptr(rows8.counts), _ptr(rows8.tn5), _ptr(rows8.depth), _ptr(rows8.narrow))
+        _ck(self.lib.mgp_set_rows_target(self._h, C.byref(r), C.byref(r8)), "mgp_set_rows_target")
+        self._rows_tgt = (rows, rows8)
 
     def copy_wait(self):
         """mgp_copy_wait: every pushed batch's H2D copies are done (their host

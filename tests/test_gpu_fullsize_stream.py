@@ -4,8 +4,9 @@ C5 configuration streamed and split by cell.
 * C4 (200M reads x 10k cells, `run` parameters) through bench.StreamSet, the code the
   bench's timed step runs: dense 64-byte quality-carrying records in pinned host
   batches of 16M reads, 16-bit barcode / |tlen| columns (mgp_push_batch16), on-device
-  pairing, streamed segments, and the 16-bit count rows written into pinned host
-  memory as windows complete (mgp_set_rows16_target). Checked from the host rows the
+  pairing, streamed segments, and the count rows written into pinned host memory as
+  windows complete (mgp_set_rows_target: 8-bit rows for the (cell, window) pairs whose
+  values all fit a byte, 16-bit rows for the others). Checked from the host rows the
   step delivered: the per-cell invariants over every cell, the run statistics and
   tallies, a second step byte-identical, and 8 x 8 whole cells bit-exact against the
   oracle on the quality-carrying full records of exactly their reads.
@@ -30,12 +31,6 @@ pytestmark = pytest.mark.gpu
 
 RUN = dict(min_baseq=20, min_mapq=30, dedup_mode="alignment_and_fragment_length", min_reads=1)
 PER_CELL = ("n_reads", "any_paired", "passed", "covered", "depth_sum", "depth_max", "median_lo", "median_hi")
-
-
-def _rows_view(rows, lo, hi):
-    from mgatk2_amd.engine import Rows16
-
-    return Rows16(rows.counts[lo:hi], rows.tn5[lo:hi], rows.depth[lo:hi], rows.wide[lo:hi], rows.window_width)
 
 
 def _delivered(ss, res, lo, hi) -> dict:
@@ -66,12 +61,13 @@ def _streamed_full_size(engine_lib, oracle_lib, n, nc, seed, batch, ranges, chun
         segs, streamed = eng.stream_info()
         assert streamed and segs - seg0 >= 4, (segs - seg0, streamed)
         assert not ss.rows.wide.any() and not ss.exact
+        assert ss.rows8 is not None and ss.rows8.narrow.any()  # (the bench's default: 8-bit rows beside)
         st = res.stats
         assert st["total_reads"] == n and st["error_bits"] == 0
         tally = np.zeros_like(res.ref_tally)
         for lo in range(0, nc, chunk):
             hi = min(nc, lo + chunk)
-            tally += _rows16_invariants(_rows_view(ss.rows, lo, hi), res, lo, hi)
+            tally += _rows16_invariants(ss.rows16(lo, hi), res, lo, hi)
         np.testing.assert_array_equal(res.ref_tally, tally)
         ok = res.passed.astype(bool)
         assert st["filtered_reads"] == int(res.n_reads.sum())
@@ -80,12 +76,14 @@ def _streamed_full_size(engine_lib, oracle_lib, n, nc, seed, batch, ranges, chun
         assert st["duplicate_reads_with_length"] <= st["duplicate_reads_position_only"]
         got = {r: _delivered(ss, res, *r) for r in ranges}
         # a second step over the same pinned batches: the same bytes in host memory
-        first = ss.rows.counts[:chunk].copy()
+        first = ss.rows16(0, chunk)
         again = ss.step(batches, True)
-        np.testing.assert_array_equal(ss.rows.counts[:chunk], first)
+        second = ss.rows16(0, chunk)
+        for k in ("counts", "tn5", "depth", "wide"):
+            np.testing.assert_array_equal(getattr(second, k), getattr(first, k), err_msg=f"second step {k}")
         for k in ("n_reads", "covered", "depth_sum", "median_lo", "median_hi", "ref_tally"):
             np.testing.assert_array_equal(getattr(res, k), getattr(again, k), err_msg=f"second step {k}")
-        del first
+        del first, second
     for (lo, hi), g in got.items():
         exp = _oracle_cells_from_quality_records(oracle_lib, cfg, seed, n, cdf, ref, lo, hi)
         for k in FULL_KEYS:
@@ -146,8 +144,10 @@ def test_c5_eight_streamed_cell_shards_equal_the_global_run(engine_lib):
             part = ss.step(ss.batches(ss.auto_batch("auto")), True)
             assert e2.stream_info()[1], f"rank {r}: not streamed"
             assert part.stats["error_bits"] == 0
+            got = ss.rows16(0, hi - lo)
             for k in ("counts", "tn5", "depth", "wide"):
-                np.testing.assert_array_equal(getattr(ss.rows, k), getattr(rows[r], k), err_msg=f"rank {r} rows {k}")
+                np.testing.assert_array_equal(getattr(got, k), getattr(rows[r], k), err_msg=f"rank {r} rows {k}")
+            del got
             for k in PER_CELL:
                 np.testing.assert_array_equal(getattr(part, k), getattr(whole, k)[lo:hi], err_msg=f"rank {r} {k}")
             tally += part.ref_tally

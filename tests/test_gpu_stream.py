@@ -620,6 +620,110 @@ def test_rows16_target_equals_fetch_rows16(engine_lib, streamed, layout, min_rea
         eng.set_rows16_target(None)
 
 
+def _rows_targets(nc, L, nw, W):
+    """A pinned 16-bit rows target and the 8-bit one beside it (ABI 7)."""
+    from mgatk2_amd.engine import PinnedBuffer, Rows8, Rows16
+
+    o8 = nc * L * 22 + nc * nw + 64
+    buf = PinnedBuffer(o8 + nc * L * 11 + nc * nw + 64)
+    t16 = Rows16(buf.array((nc, L, 8), np.uint16, 0), buf.array((nc, L, 2), np.uint16, nc * L * 16),
+                 buf.array((nc, L), np.uint16, nc * L * 20), buf.array((nc, nw), np.uint8, nc * L * 22), W)
+    t8 = Rows8(buf.array((nc, L, 8), np.uint8, o8), buf.array((nc, L, 2), np.uint8, o8 + nc * L * 8),
+               buf.array((nc, L), np.uint8, o8 + nc * L * 10), buf.array((nc, nw), np.uint8, o8 + nc * L * 11))
+    return buf, t16, t8
+
+
+@pytest.mark.parametrize("late", [False, True])
+@pytest.mark.parametrize("gate", [False, True])
+@pytest.mark.parametrize("streamed", [False, True])
+def test_rows8_target_equals_the_exact_rows(engine_lib, streamed, gate, late):
+    """ABI 7 (mgp_set_rows_target): with the 8-bit target beside the 16-bit one, each
+    (cell, window) lands in exactly one of them: `narrow` iff every count, tn5 cut and
+    depth of the window is at most 255. 8 cells of 40-320 depth (both kinds of window),
+    streamed in 4 batches or resident, twice on one context; gate: min_reads between
+    the cells' read counts, so the gate (processors.py:22) zeroes some cells after their
+    rows were sent; late: the target set after two batches. The merged rows equal the
+    exact u32 rows of a resident run."""
+    from dataclasses import replace
+
+    from mgatk2_amd.engine import EngineConfig, merge_rows
+    from mgatk2_amd.synth import synth_reads
+
+    nc = 8
+    soa = synth_reads(717, 800_000, nc, pack=True)
+    cfg = EngineConfig(n_cells=nc, **CONFIGS["run"])
+    with engine_lib.Engine(cfg) as eng:
+        eng.push(soa)
+        eng.run()
+        ungated = eng.fetch()  # (the narrow flags are the pileup's, before the gate zeroes a cell)
+        nw, W = eng.windows()
+    nr = ungated.n_reads
+    if gate:
+        cfg = replace(cfg, min_reads=int(np.sort(nr)[nc // 2]))
+    with engine_lib.Engine(cfg) as eng:
+        eng.push(soa)
+        eng.run()
+        want = eng.fetch()
+    if gate:
+        assert (want.passed == 0).any() and want.passed.any()
+    L = cfg.mito_len
+    big = np.maximum(ungated.depth, ungated.tn5.max(axis=2))
+    fits = np.array([[big[c, k * W:(k + 1) * W].max() <= 255 for k in range(nw)] for c in range(nc)])
+    assert fits.any() and not fits.all()
+    buf, t16, t8 = _rows_targets(nc, L, nw, W)
+    scfg = replace(cfg, stream=True, reserve_reads=soa.n, reserve_payload=int(soa.payload.shape[0]) + 4096) \
+        if streamed else cfg
+    with engine_lib.Engine(scfg) as eng:
+        if not late:
+            eng.set_rows_target(t16, t8)
+        for rep in range(2):
+            for a in (t16.counts, t16.tn5, t16.depth, t16.wide, t8.counts, t8.tn5, t8.depth, t8.narrow):
+                a.fill(0xAB)
+            eng.reset()
+            if late:
+                eng.set_rows_target(None)
+            cuts = np.linspace(0, soa.n, 5).astype(int)
+            for i, (a, b) in enumerate(zip(cuts[:-1], cuts[1:])):
+                if late and i == 2:
+                    eng.set_rows_target(t16, t8)
+                eng.push(soa.slice(int(a), int(b)))
+            eng.run()
+            got = eng.fetch()
+            np.testing.assert_array_equal(t8.narrow.astype(bool), fits, err_msg=f"narrow flags rep {rep}")
+            assert not t16.wide.any()
+            m = merge_rows(t16, t8, 0, nc)
+            for k in ("counts", "tn5", "depth"):
+                np.testing.assert_array_equal(m[k], getattr(want, k), err_msg=f"{k} rep {rep}")
+            assert_same(got, want, f"rows8 target streamed={streamed} rep {rep}")
+        eng.set_rows_target(None)
+
+
+def test_rows8_target_with_a_wide_window(engine_lib):
+    """A drained window (more than 65535 reads: wide) is never narrow; its 16-bit rows
+    saturate as with the 16-bit target alone, the cell's other windows go 8-bit."""
+    from mgatk2_amd.engine import EngineConfig, merge_rows
+    from mgatk2_amd.synth import synth_reads
+
+    deep = synth_reads(91, 400_000, 1)  # (as test_rows16_wide_windows_saturate_and_fetch_cells_is_exact)
+    deep.start[:] = np.sort(deep.start % 60).astype(np.int32)
+    deep.payload.reshape(-1, 64)[:, 0:4] = deep.start.view(np.uint8).reshape(-1, 4)
+    cfg = EngineConfig(n_cells=1, min_baseq=0, min_mapq=0, dedup_mode="none", min_reads=0)
+    with engine_lib.Engine(cfg) as eng:
+        nw, W = eng.windows()
+        buf, t16, t8 = _rows_targets(1, cfg.mito_len, nw, W)
+        eng.set_rows_target(t16, t8)
+        eng.push(deep)
+        eng.run()
+        exact = eng.fetch()
+        eng.set_rows_target(None)
+    assert t16.wide[0, 0] == 1 and t8.narrow[0, 0] == 0 and t8.narrow[0, 1:].all()
+    m = merge_rows(t16, t8, 0, 1)
+    np.testing.assert_array_equal(m["depth"], np.minimum(exact.depth, 65535))
+    np.testing.assert_array_equal(m["counts"], np.minimum(exact.counts, 65535))
+    np.testing.assert_array_equal(m["tn5"], np.minimum(exact.tn5, 65535))
+    assert exact.depth.max() > 65535
+
+
 @pytest.mark.parametrize("streamed", [False, True])
 @pytest.mark.parametrize("fault", ["offset", "misaligned", "cigar", "stride", "lseq", "cigar_off"])
 def test_records_outside_the_payload_raise(engine_lib, streamed, fault):
