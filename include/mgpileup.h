@@ -58,7 +58,8 @@ extern "C" {
                                  64-byte batches paired on the device;
                               6: mgp_txt_gz_* (the txt count files formatted and deflated on the
                                  device);
-                              7: mgp_set_rows_target (an 8-bit rows target beside the 16-bit one) */
+                              7: mgp_set_rows_target (an 8-bit rows target beside the 16-bit one),
+                                 mgp_h5_tiles_* (the HDF5 chunks deflated on the device) */
 
 /* ---- return codes (0 = success) ------------------------------------------ */
 #define MGP_OK               0
@@ -560,6 +561,25 @@ typedef struct mgp_rows8 {
 /* mgp_set_rows16_target(ctx, rows16) with the 8-bit target rows8 beside it (NULL: the
  * 16-bit target alone); rows16 NULL stops both. */
 int  mgp_set_rows_target(mgp_ctx *ctx, const mgp_rows16 *rows16, const mgp_rows8 *rows8);
+/* The HDF5 count datasets' chunks deflated on the device (ABI 7). Replaces the gzip-4
+ * filter pipeline of IncrementalHDF5Writer's 11 datasets (src/file_io/writers.py:60-131:
+ * A_fwd, A_rev, C_fwd, C_rev, G_fwd, G_rev, T_fwd, T_rev, tn5_cuts_fwd, tn5_cuts_rev in
+ * counts.h5 and coverage in metadata.h5, u16 [mito_len][n_cols], chunks of
+ * chunk_rows x chunk_cols): plane values min(v, 65535) of the last run's cells, column j
+ * holding cell cell_of_col[j] (-1: zeros), edge chunks padded with 0, each chunk one
+ * zlib stream (the H5Z_DEFLATE form; runs and dynamic Huffman codes, about zlib level
+ * 4's size). One call covers the column chunks [col_chunk_lo, col_chunk_hi); its streams
+ * stay on the device, plane-major, then row chunk, then column chunk, until
+ * mgp_h5_tiles_fetch or the next call. The caller writes them with H5Dwrite_chunk. */
+typedef struct mgp_h5_tiles {
+    int64_t        n_cols;          /* columns of the datasets                           */
+    const int32_t *cell_of_col;     /* host: the context's cell of each column, -1: none */
+    int32_t        chunk_rows, chunk_cols;
+    int32_t        col_chunk_lo, col_chunk_hi;
+    int64_t       *chunk_bytes;     /* host out: [11][row chunks][hi - lo] stream sizes  */
+} mgp_h5_tiles;
+int  mgp_h5_tiles_run(mgp_ctx *ctx, mgp_h5_tiles *job, int64_t *total_bytes);
+int  mgp_h5_tiles_fetch(mgp_ctx *ctx, uint8_t *dst, int64_t cap);
 /* Position windows of the pileup (the `wide` flags' second dimension). */
 int  mgp_windows(mgp_ctx *ctx, int32_t *n_windows, int32_t *window_width);
 /* Wait until the H2D copies of every batch pushed so far have completed: the caller may

@@ -120,6 +120,12 @@ struct TxtState {
     uint64_t total = 0;
 };
 
+// mgp_h5_tiles: the HDF5 chunk deflate's buffers (mgp_txtgz.hip), kept for the next call
+struct H5State {
+    DevBuf coc, raw, tok, out, out_off, chunk_bytes, dst_off, packed;
+    uint64_t total = 0;
+};
+
 enum Stage { ST_HIST, ST_SCAN, ST_GROUP_A, ST_GROUP_B, ST_PILEUP, ST_GATE, ST_MEDIAN, ST_TALLY, ST_COMM, ST_N };
 static const char* kStageNames = "hist,scan,group_a,group_b,pileup,gate,median,tally,comm";
 
@@ -220,6 +226,7 @@ struct mgp_ctx {
     bool last_streamed = false;
 
     TxtState txt;  // mgp_txt_gz
+    H5State h5;    // mgp_h5_tiles
 };
 
 // ---------------------------------------------------------------------------
@@ -4783,6 +4790,83 @@ int mgp_txt_gz_fetch(mgp_ctx* ctx, uint8_t* dst, int64_t cap) {
     if (cap < (int64_t)ctx->txt.total) return set_err(MGP_E_INVALID, "mgp_txt_gz_fetch: destination too small");
     HIP_TRY(hipSetDevice(ctx->dev));
     if (ctx->txt.total) HIP_TRY(hipMemcpy(dst, ctx->txt.packed.p, ctx->txt.total, hipMemcpyDeviceToHost));
+    return MGP_OK;
+}
+
+// ---------------------------------------------------------------------------
+// mgp_h5_tiles: the HDF5 count datasets' chunks deflated on the device
+// (IncrementalHDF5Writer, writers.py:60-131: 11 u16 planes, gzip-4 chunks of 1000 x 100)
+// ---------------------------------------------------------------------------
+int mgp_h5_tiles_run(mgp_ctx* ctx, mgp_h5_tiles* job, int64_t* total_bytes) {
+    using namespace txtgz;
+    if (!ctx || !job) return set_err(MGP_E_INVALID, "null ctx/job");
+    MGP_TRY(mgp_sync(ctx));
+    HIP_TRY(hipSetDevice(ctx->dev));
+    if (!ctx->ran) return set_err(MGP_E_STATE, "mgp_h5_tiles: no run to write (mgp_run first)");
+    const Geom& g = ctx->g;
+    H5State& st = ctx->h5;
+    st.total = 0;
+    const int64_t nco = job->n_cols;
+    const int crow = job->chunk_rows, ccol = job->chunk_cols;
+    if (nco < 0 || crow <= 0 || ccol <= 0 || (int64_t)crow * ccol > (1 << 22) || !job->chunk_bytes ||
+        (nco > 0 && !job->cell_of_col))
+        return set_err(MGP_E_INVALID, "mgp_h5_tiles: bad arguments");
+    const int64_t ncc_all = (nco + ccol - 1) / ccol;
+    const int lo = job->col_chunk_lo, hi = job->col_chunk_hi;
+    if (lo < 0 || hi < lo || hi > ncc_all) return set_err(MGP_E_INVALID, "mgp_h5_tiles: column chunks out of range");
+    const int nrc = (g.L + crow - 1) / crow, ncc = hi - lo;
+    const int64_t nch = (int64_t)kPlanes * nrc * ncc;
+    if (nch == 0) {
+        if (total_bytes) *total_bytes = 0;
+        return MGP_OK;
+    }
+    if (nch > (int64_t)1 << 20) return set_err(MGP_E_INVALID, "mgp_h5_tiles: too many chunks for one call");
+    for (int64_t j = 0; j < nco; ++j)
+        if (job->cell_of_col[j] < -1 || job->cell_of_col[j] >= g.nc)
+            return set_err(MGP_E_INVALID, "mgp_h5_tiles: cell of a column out of range");
+    hipStream_t s = ctx->s_comp;
+    const uint64_t chunk_raw = (uint64_t)crow * ccol * 2, stride = out_bound(chunk_raw);
+    MGP_TRY(st.coc.ensure((size_t)std::max<int64_t>(nco, 1) * 4));
+    MGP_TRY(st.raw.ensure((size_t)(nch * chunk_raw) + 64));
+    MGP_TRY(st.tok.ensure((size_t)(nch * chunk_raw) * 4 + 64));
+    MGP_TRY(st.out.ensure((size_t)(nch * stride) + 64));
+    MGP_TRY(st.out_off.ensure((size_t)nch * 8));
+    MGP_TRY(st.chunk_bytes.ensure((size_t)nch * 4));
+    MGP_TRY(st.dst_off.ensure((size_t)nch * 8));
+    std::vector<uint64_t> oo((size_t)nch);
+    for (int64_t k = 0; k < nch; ++k) oo[(size_t)k] = (uint64_t)k * stride;
+    if (nco) HIP_TRY(hipMemcpyAsync(st.coc.p, job->cell_of_col, (size_t)nco * 4, hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemcpyAsync(st.out_off.p, oo.data(), (size_t)nch * 8, hipMemcpyHostToDevice, s));
+    H5Job jb{ctx->counts16.as<uint4>(), ctx->tn5_16.as<uint32_t>(), ctx->depth16.as<uint16_t>(), g.L,
+             st.coc.as<int32_t>(), nco, crow, ccol, nrc, lo, ncc};
+    H5Scratch sc{st.raw.as<uint8_t>(), st.tok.as<uint32_t>(), st.out.as<uint32_t>(), st.out_off.as<uint64_t>(),
+                 st.chunk_bytes.as<uint32_t>(), chunk_raw, stride};
+    if (h5_deflate(jb, sc, s) != 0) return set_err(MGP_E_HIP, "mgp_h5_tiles: deflate kernel launch failed");
+    std::vector<uint32_t> cb((size_t)nch);
+    HIP_TRY(hipMemcpyAsync(cb.data(), st.chunk_bytes.p, (size_t)nch * 4, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    std::vector<uint64_t> dst((size_t)nch);
+    uint64_t tot = 0;
+    for (int64_t k = 0; k < nch; ++k) {
+        dst[(size_t)k] = tot;
+        tot += cb[(size_t)k];
+        job->chunk_bytes[k] = cb[(size_t)k];
+    }
+    MGP_TRY(st.packed.ensure(tot + 64));
+    HIP_TRY(hipMemcpyAsync(st.dst_off.p, dst.data(), (size_t)nch * 8, hipMemcpyHostToDevice, s));
+    if (h5_pack(sc, nch, st.dst_off.as<uint64_t>(), st.packed.as<uint8_t>(), s) != 0)
+        return set_err(MGP_E_HIP, "mgp_h5_tiles: pack kernel launch failed");
+    HIP_TRY(hipStreamSynchronize(s));
+    st.total = tot;
+    if (total_bytes) *total_bytes = (int64_t)tot;
+    return MGP_OK;
+}
+
+int mgp_h5_tiles_fetch(mgp_ctx* ctx, uint8_t* dst, int64_t cap) {
+    if (!ctx || (!dst && ctx->h5.total)) return set_err(MGP_E_INVALID, "null ctx/dst");
+    if (cap < (int64_t)ctx->h5.total) return set_err(MGP_E_INVALID, "mgp_h5_tiles_fetch: destination too small");
+    HIP_TRY(hipSetDevice(ctx->dev));
+    if (ctx->h5.total) HIP_TRY(hipMemcpy(dst, ctx->h5.packed.p, ctx->h5.total, hipMemcpyDeviceToHost));
     return MGP_OK;
 }
 

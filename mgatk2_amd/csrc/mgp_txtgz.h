@@ -65,6 +65,38 @@ int txt_deflate(const Job& job, const Scratch& sc, hipStream_t s);
 int txt_pack(const Scratch& sc, int64_t n_members, const uint64_t* dst_off, uint8_t* dst, hipStream_t s);
 // the 25 CRC shift matrices (host)
 void crc_shift_matrices(uint32_t* m /* 25 x 32 */);
+// ---- HDF5 chunks (IncrementalHDF5Writer's count datasets, writers.py:60-131) ----
+// The 11 u16 planes [L][n_cols] (A_fwd, A_rev, ..., T_rev, tn5_cuts_fwd, tn5_cuts_rev,
+// coverage; min(v, 65535) of the run's values, which its 16-bit rows hold; a column is a
+// cell of the rows or zeros) cut into (crow x ccol) chunks, edge chunks padded with 0,
+// each deflated on the device into one zlib stream, the H5Z_DEFLATE filter's form.
+constexpr int kPlanes = 11;
+struct H5Job {
+    const uint4* c16;           // [cells][L]: 8 x u16 (A_fwd, A_rev, ..., T_rev)
+    const uint32_t* t16;        // [cells][L]: tn5 fwd | rev << 16
+    const uint16_t* d16;        // [cells][L]
+    int L;
+    const int32_t* cell_of_col;  // [n_cols]: a cell of the rows, -1: a zero column
+    int64_t n_cols;
+    int crow, ccol;             // chunk shape
+    int nrc;                    // row chunks, ceil(L / crow)
+    int cc0, ncc;               // this batch: column chunks [cc0, cc0 + ncc)
+};
+// Batch chunk k = (plane * nrc + rc) * ncc + (cc - cc0): its raw bytes at raw + k chunk_raw,
+// its output region at out + k out_stride (out_off[k]).
+struct H5Scratch {
+    uint8_t* raw;
+    uint32_t* tok;           // chunk_raw words per chunk
+    uint32_t* out;
+    const uint64_t* out_off;
+    uint32_t* chunk_bytes;   // [chunks] zlib stream bytes
+    uint64_t chunk_raw, out_stride;
+};
+// the planes' raw chunks of the batch, then their zlib streams (chunk_bytes filled)
+int h5_deflate(const H5Job& job, const H5Scratch& sc, hipStream_t s);
+// the streams packed back to back (chunk order) into dst at dst_off[chunks]
+int h5_pack(const H5Scratch& sc, int64_t n_chunks, const uint64_t* dst_off, uint8_t* dst, hipStream_t s);
+
 // bound of a member's output region for `text` bytes
 __host__ __device__ inline uint64_t out_bound(uint64_t text) { return ((text + 5 * (text / 65535 + 1) + 64 + 31) & ~uint64_t(31)); }
 

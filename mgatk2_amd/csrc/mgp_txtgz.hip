@@ -667,51 +667,19 @@ __global__ void __launch_bounds__(kT, 4) k_txt_match(Job job, Scratch sc) {
 }
 
 
-// Kernel 3 (per member): the optimal parse of each segment, the Huffman codes, the
-// encoded block (dynamic, fixed or stored: the smallest) and the gzip frame.
-__global__ void __launch_bounds__(kT) k_txt_code(Job job, Scratch sc) {
-    __shared__ CodeLds S;
+// The tokens of every thread (tok[t0 .. t0 + ntok): literal bytes or l << 16 | d; their
+// symbol counts in S.lit_f / S.dist_f) as one final deflate block after the frame's
+// header bytes (hdr, hdr_len <= 10) in out, whose region (out_bound(n_text) bytes, room
+// for the frame included) is zeroed here: dynamic Huffman codes (length-limited), or
+// the fixed codes, or stored blocks of the n_text raw bytes T, whichever is smallest.
+// Returns the block's bytes (every thread). All threads call.
+__device__ uint64_t deflate_block(CodeLds& S, const uint8_t* T, const uint32_t* tok, int t0, uint32_t ntok,
+                                  uint64_t n_text, uint32_t* out, const uint8_t* hdr, int hdr_len) {
     const int t = threadIdx.x;
-    const int64_t m = blockIdx.x;
-    const uint8_t* const T = sc.text + sc.text_off[m];
-    uint32_t* const tok = sc.tok + sc.text_off[m];
-    const uint64_t n_text = sc.text_off[m + 1] - sc.text_off[m];
-    uint32_t* const out = sc.out + sc.out_off[m] / 4;
-    if (n_text == 0) {  // no line: no member
-        if (t == 0) sc.member_bytes[m] = 0;
-        return;
-    }
-    const int t0 = (int)sc.seg[m * (kT + 1) + t], t1 = (int)sc.seg[m * (kT + 1) + t + 1];
-    // ---- 3. optimal parse (one pass at default prices: a second pass at the member's own
-    // code lengths gained 0.4-1 % on C4-like text for twice the parse time) ----
-    lds_prices_default(S);
-    for (int s = t; s < kLit; s += kT) S.lit_f[s] = 0;
-    if (t < kDist) S.dist_f[t] = 0;
-    __syncthreads();
-    dp_segment(T, tok, t0, t1, S);
-    // traceback: the chosen tokens, stored over the candidates (compacted), and their counts
-    uint32_t ntok = 0;
-    for (int i = t0; i < t1;) {
-        const uint32_t w = tok[i];
-        const uint32_t l = (w >> 22) & 63u;
-        if (!l) {
-            atomicAdd(&S.lit_f[T[i]], 1u);
-            tok[t0 + ntok] = T[i];
-            ++i;
-        } else {
-            const uint32_t d = w & 0xFFFFu;
-            atomicAdd(&S.lit_f[257 + len_code((int)l)], 1u);
-            atomicAdd(&S.dist_f[dist_code((int)d)], 1u);
-            tok[t0 + ntok] = (l << 16) | d;
-            i += (int)l;
-        }
-        ++ntok;
-    }
     if (t == 0) S.lit_f[256] = 1;  // end of block
     __syncthreads();
     huff_lengths(S.lit_f, kLit, 15, S.lit_len, S.h);
     huff_lengths(S.dist_f, kDist, 15, S.dist_len, S.h);
-    PROF_STAMP(3);
     // ---- 3. codes and the header ----
     if (t == 0) {
         // a complete distance code: at least two used lengths (one used or none -> codes 0 and 1)
@@ -813,19 +781,16 @@ __global__ void __launch_bounds__(kT) k_txt_code(Job job, Scratch sc) {
     const uint64_t sto_bytes = n_text + 5 * n_blk;
     const int mode = (dyn_bytes <= fix_bytes && dyn_bytes <= sto_bytes) ? 0 : (fix_bytes <= sto_bytes ? 1 : 2);
     const uint64_t blk_bytes = mode == 0 ? dyn_bytes : mode == 1 ? fix_bytes : sto_bytes;
-    const uint64_t region = out_bound(n_text) / 4;
+    const uint64_t region = out_bound(n_text) / 4;  // (the bound has room for the frame)
     for (uint64_t q = t; q < region; q += kT) out[q] = 0;
     __threadfence_block();
     __syncthreads();
     uint8_t* const ob = reinterpret_cast<uint8_t*>(out);
-    if (t == 0) {  // gzip header: magic, deflate, no flags, mtime 0, xfl 2, os 255
-        out[0] = 0x00088B1Fu;
-        out[1] = 0;
-        atomicOr(&out[2], 0xFF02u);
-    }
+    if (t == 0)  // the frame's header bytes (the block's first bits share their last word)
+        for (int k = 0; k < hdr_len; ++k) atomicOr(&out[k / 4], (uint32_t)hdr[k] << (8 * (k % 4)));
     if (mode == 0) {
         if (t == 0) {
-            BitW bw(out, 80);
+            BitW bw(out, 8 * (uint64_t)hdr_len);
             bw.put(1, 1);  // BFINAL
             bw.put(2, 2);  // dynamic
             bw.put((uint32_t)(S.hlit - 257), 5);
@@ -841,7 +806,7 @@ __global__ void __launch_bounds__(kT) k_txt_code(Job job, Scratch sc) {
             }
             bw.done();
         }
-        BitW bw(out, 80 + S.hdr_bits + dyn_pre);
+        BitW bw(out, 8 * (uint64_t)hdr_len + S.hdr_bits + dyn_pre);
         for (uint32_t q = 0; q < ntok; ++q) put_token(bw, tok[t0 + q], S.lit_code, S.lit_len, S.dist_code, S.dist_len);
         if (t == kT - 1) bw.put(S.lit_code[256], S.lit_len[256]);
         bw.done();
@@ -852,20 +817,20 @@ __global__ void __launch_bounds__(kT) k_txt_code(Job job, Scratch sc) {
             for (int s = 0; s < kDist; ++s) S.dist_len[s] = 5;
             canon(S.lit_len, kLit, S.lit_code);
             canon(S.dist_len, kDist, S.dist_code);
-            BitW bw(out, 80);
+            BitW bw(out, 8 * (uint64_t)hdr_len);
             bw.put(1, 1);
             bw.put(1, 2);  // fixed
             bw.done();
         }
         __syncthreads();
-        BitW bw(out, 80 + 3 + fix_pre);
+        BitW bw(out, 8 * (uint64_t)hdr_len + 3 + fix_pre);
         for (uint32_t q = 0; q < ntok; ++q) put_token(bw, tok[t0 + q], S.lit_code, S.lit_len, S.dist_code, S.dist_len);
         if (t == kT - 1) bw.put(S.lit_code[256], S.lit_len[256]);
         bw.done();
     } else {
         // stored blocks of <= 65535 bytes: BFINAL/BTYPE byte, LEN, NLEN, the bytes
         for (uint64_t b = t; b < n_blk; b += kT) {
-            const uint64_t o = 10 + b * (65535 + 5);
+            const uint64_t o = hdr_len + b * (65535 + 5);
             const uint64_t left = n_text - b * 65535;
             const uint32_t len = (uint32_t)(left < 65535 ? left : 65535);
             ob[o] = b + 1 == n_blk ? 1 : 0;
@@ -874,8 +839,57 @@ __global__ void __launch_bounds__(kT) k_txt_code(Job job, Scratch sc) {
             ob[o + 3] = (uint8_t)~len;
             ob[o + 4] = (uint8_t)(~len >> 8);
         }
-        for (uint64_t x = t; x < n_text; x += kT) ob[10 + 5 * (x / 65535 + 1) + x] = T[x];
+        for (uint64_t x = t; x < n_text; x += kT) ob[hdr_len + 5 * (x / 65535 + 1) + x] = T[x];
     }
+    __threadfence_block();
+    __syncthreads();
+    return blk_bytes;
+}
+
+// Kernel 3 (per member): the optimal parse of each segment, the Huffman codes, the
+// encoded block (dynamic, fixed or stored: the smallest) and the gzip frame.
+__global__ void __launch_bounds__(kT) k_txt_code(Job job, Scratch sc) {
+    __shared__ CodeLds S;
+    const int t = threadIdx.x;
+    const int64_t m = blockIdx.x;
+    const uint8_t* const T = sc.text + sc.text_off[m];
+    uint32_t* const tok = sc.tok + sc.text_off[m];
+    const uint64_t n_text = sc.text_off[m + 1] - sc.text_off[m];
+    uint32_t* const out = sc.out + sc.out_off[m] / 4;
+    if (n_text == 0) {  // no line: no member
+        if (t == 0) sc.member_bytes[m] = 0;
+        return;
+    }
+    const int t0 = (int)sc.seg[m * (kT + 1) + t], t1 = (int)sc.seg[m * (kT + 1) + t + 1];
+    // ---- 3. optimal parse (one pass at default prices: a second pass at the member's own
+    // code lengths gained 0.4-1 % on C4-like text for twice the parse time) ----
+    lds_prices_default(S);
+    for (int s = t; s < kLit; s += kT) S.lit_f[s] = 0;
+    if (t < kDist) S.dist_f[t] = 0;
+    __syncthreads();
+    dp_segment(T, tok, t0, t1, S);
+    // traceback: the chosen tokens, stored over the candidates (compacted), and their counts
+    uint32_t ntok = 0;
+    for (int i = t0; i < t1;) {
+        const uint32_t w = tok[i];
+        const uint32_t l = (w >> 22) & 63u;
+        if (!l) {
+            atomicAdd(&S.lit_f[T[i]], 1u);
+            tok[t0 + ntok] = T[i];
+            ++i;
+        } else {
+            const uint32_t d = w & 0xFFFFu;
+            atomicAdd(&S.lit_f[257 + len_code((int)l)], 1u);
+            atomicAdd(&S.dist_f[dist_code((int)d)], 1u);
+            tok[t0 + ntok] = (l << 16) | d;
+            i += (int)l;
+        }
+        ++ntok;
+    }
+    PROF_STAMP(3);
+    const uint8_t gz_hdr[10] = {0x1F, 0x8B, 0x08, 0, 0, 0, 0, 0, 0x02, 0xFF};  // magic, deflate, mtime 0, xfl 2, os 255
+    const uint64_t blk_bytes = deflate_block(S, T, tok, t0, ntok, n_text, out, gz_hdr, 10);
+    uint8_t* const ob = reinterpret_cast<uint8_t*>(out);
     __threadfence_block();
     __syncthreads();
     if (t == 0) {
@@ -887,7 +901,8 @@ __global__ void __launch_bounds__(kT) k_txt_code(Job job, Scratch sc) {
             ob[o + 4 + q] = (uint8_t)(isz >> (8 * q));
         }
         sc.member_bytes[m] = (uint32_t)(o + 8);
-    }    PROF_STAMP(4);
+    }
+    PROF_STAMP(4);
 }
 
 __global__ void __launch_bounds__(kT) k_txt_pack(const uint32_t* __restrict__ out, const uint64_t* __restrict__ out_off,
@@ -898,6 +913,115 @@ __global__ void __launch_bounds__(kT) k_txt_pack(const uint32_t* __restrict__ ou
     uint8_t* d = dst + dst_off[m];
     const uint32_t n = member_bytes[m];
     for (uint32_t q = threadIdx.x; q < n; q += kT) d[q] = src[q];
+}
+
+// ---------------------------------------------------------------------------
+// HDF5 chunks: the 11 planes' (crow x ccol) u16 chunks as zlib streams
+// ---------------------------------------------------------------------------
+// One workgroup per (row chunk, column chunk) of the batch: each position of each column
+// read once (a cell's 8 counts as one uint4), the 11 planes' raw chunks written row-major
+// (consecutive threads, consecutive columns of a chunk row).
+__global__ void __launch_bounds__(kT) k_h5_gather(H5Job job, H5Scratch sc) {
+    const int r = blockIdx.x;
+    const int rc = r / job.ncc, ccl = r - rc * job.ncc;
+    const int cc = job.cc0 + ccl;
+    const int n = job.crow * job.ccol;
+    uint16_t* const base = reinterpret_cast<uint16_t*>(sc.raw);
+    const size_t pstride = (size_t)job.nrc * job.ncc * (sc.chunk_raw / 2);  // one plane's chunks (u16)
+    const size_t k0 = ((size_t)rc * job.ncc + ccl) * (sc.chunk_raw / 2);
+    for (int x = threadIdx.x; x < n; x += kT) {
+        const int row = x / job.ccol, c = x - row * job.ccol;
+        const int p = rc * job.crow + row;
+        const int64_t col = (int64_t)cc * job.ccol + c;
+        const int cell = (p < job.L && col < job.n_cols) ? job.cell_of_col[col] : -1;
+        uint4 a = make_uint4(0, 0, 0, 0);
+        uint32_t tt = 0, d = 0;
+        if (cell >= 0) {
+            const size_t P = (size_t)cell * job.L + p;
+            a = job.c16[P];
+            tt = job.t16[P];
+            d = job.d16[P];
+        }
+        const uint32_t w[4] = {a.x, a.y, a.z, a.w};
+        uint16_t* const o = base + k0 + x;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            o[(2 * q) * pstride] = (uint16_t)(w[q] & 0xFFFFu);
+            o[(2 * q + 1) * pstride] = (uint16_t)(w[q] >> 16);
+        }
+        o[8 * pstride] = (uint16_t)(tt & 0xFFFFu);
+        o[9 * pstride] = (uint16_t)(tt >> 16);
+        o[10 * pstride] = (uint16_t)d;
+    }
+}
+
+// One workgroup per chunk: a greedy parse into runs (distance 1, lengths 3-258: on C4
+// count planes it gives 0.20 of the raw bytes where zlib level 4, the reference's
+// compression_opts, gives 0.204, and further distances, same cell one position back or
+// the next column, made the streams larger), the block (deflate_block) and the zlib frame
+// (header 78 5E, Adler-32). Thread t parses [s_t, s_t+1) where s_t is its nominal start
+// moved past the run that continues across it (so the run stays one token of thread t-1).
+__global__ void __launch_bounds__(kT) k_h5_code(H5Job job, H5Scratch sc) {
+    __shared__ CodeLds S;
+    __shared__ uint64_t red[4];
+    const int t = threadIdx.x;
+    const int64_t k = blockIdx.x;
+    const uint8_t* const T = sc.raw + k * sc.chunk_raw;
+    uint32_t* const tok = sc.tok + k * sc.chunk_raw;
+    uint32_t* const out = sc.out + k * (sc.out_stride / 4);
+    const int n = (int)sc.chunk_raw;
+    const int P = (n + kT - 1) / kT;
+    auto start = [&](int u) -> int {  // thread u's start
+        const int s0 = min(n, u * P);
+        if (u == 0 || s0 >= n) return s0;
+        const uint8_t v = T[s0 - 1];
+        int r = 0;
+        while (r < P && s0 + r < n && T[s0 + r] == v) ++r;
+        return s0 + r;
+    };
+    const int t0 = start(t), t1 = t == kT - 1 ? n : start(t + 1);
+    for (int q = t; q < kLit; q += kT) S.lit_f[q] = 0;
+    if (t < kDist) S.dist_f[t] = 0;
+    __syncthreads();
+    uint32_t ntok = 0;
+    uint64_t A = 0, W = 0;  // Adler-32 partial sums: sum of bytes, sum of (t1 - i) x byte
+    for (int i = t0; i < t1;) {
+        const uint8_t v = T[i];
+        int l = 0;
+        if (i > 0) {
+            const uint8_t pv = T[i - 1];
+            const int cap = min(258, t1 - i);
+            while (l < cap && T[i + l] == pv) ++l;
+        }
+        if (l >= 3) {
+            atomicAdd(&S.lit_f[257 + len_code(l)], 1u);
+            atomicAdd(&S.dist_f[0], 1u);
+            tok[t0 + ntok] = ((uint32_t)l << 16) | 1u;
+            A += (uint64_t)v * l;  // (l copies of the previous byte, which equals v)
+            W += (uint64_t)v * ((uint64_t)(t1 - i) * l - (uint64_t)l * (l - 1) / 2);
+            i += l;
+        } else {
+            atomicAdd(&S.lit_f[v], 1u);
+            tok[t0 + ntok] = v;
+            A += v;
+            W += (uint64_t)v * (uint64_t)(t1 - i);
+            ++i;
+        }
+        ++ntok;
+    }
+    // Adler-32 of the chunk: s1 = 1 + sum b, s2 = n + sum_i (n - i) b_i
+    uint64_t a_tot, w_tot;
+    (void)block_excl_scan(A, red, a_tot);
+    (void)block_excl_scan(W + (uint64_t)(n - t1) * A, red, w_tot);
+    const uint32_t s1 = (uint32_t)((1 + a_tot) % 65521u), s2 = (uint32_t)(((uint64_t)n + w_tot) % 65521u);
+    const uint8_t zhdr[2] = {0x78, 0x5E};
+    const uint64_t blk = deflate_block(S, T, tok, t0, ntok, (uint64_t)n, out, zhdr, 2);
+    if (t == 0) {
+        uint8_t* const ob = reinterpret_cast<uint8_t*>(out);
+        const uint32_t ad = (s2 << 16) | s1;
+        for (int q = 0; q < 4; ++q) ob[2 + blk + q] = (uint8_t)(ad >> (24 - 8 * q));  // big-endian
+        sc.chunk_bytes[k] = (uint32_t)(2 + blk + 4);
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -921,6 +1045,20 @@ int txt_deflate(const Job& job, const Scratch& sc, hipStream_t s) {
 int txt_pack(const Scratch& sc, int64_t n_members, const uint64_t* dst_off, uint8_t* dst, hipStream_t s) {
     if (n_members <= 0) return 0;
     k_txt_pack<<<(unsigned)n_members, kT, 0, s>>>(sc.out, sc.out_off, sc.member_bytes, dst_off, dst);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+int h5_deflate(const H5Job& job, const H5Scratch& sc, hipStream_t s) {
+    const unsigned regions = (unsigned)(job.nrc * job.ncc);
+    if (!regions) return 0;
+    k_h5_gather<<<regions, kT, 0, s>>>(job, sc);
+    k_h5_code<<<regions * kPlanes, kT, 0, s>>>(job, sc);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+int h5_pack(const H5Scratch& sc, int64_t n_chunks, const uint64_t* dst_off, uint8_t* dst, hipStream_t s) {
+    if (n_chunks <= 0) return 0;
+    k_txt_pack<<<(unsigned)n_chunks, kT, 0, s>>>(sc.out, sc.out_off, sc.chunk_bytes, dst_off, dst);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

@@ -40,6 +40,7 @@ ABI_SYMBOLS = (
     "mgp_download_inputs", "mgp_set_stage_timing", "mgp_fetch_cells", "mgp_fetch_rows16", "mgp_windows",
     "mgp_stream_info", "mgp_set_streaming", "mgp_set_rows16_target", "mgp_copy_wait", "mgp_set_cell_range",
     "mgp_push_batch16", "mgp_txt_gz_run", "mgp_txt_gz_fetch", "mgp_txt_gz_rows", "mgp_set_rows_target",
+    "mgp_h5_tiles_run", "mgp_h5_tiles_fetch",
 )
 ABI_VERSION = 7
 CFG_KEEP_TN5 = 0x1
@@ -157,6 +158,22 @@ class mgp_txt_gz(C.Structure):
     ]
 
 
+class mgp_h5_tiles(C.Structure):
+    _fields_ = [
+        ("n_cols", C.c_int64),
+        ("cell_of_col", C.c_void_p),
+        ("chunk_rows", C.c_int32),
+        ("chunk_cols", C.c_int32),
+        ("col_chunk_lo", C.c_int32),
+        ("col_chunk_hi", C.c_int32),
+        ("chunk_bytes", C.c_void_p),
+    ]
+
+
+H5_PLANES = ("A_fwd", "A_rev", "C_fwd", "C_rev", "G_fwd", "G_rev", "T_fwd", "T_rev", "tn5_cuts_fwd", "tn5_cuts_rev",
+             "coverage")  # the planes of mgp_h5_tiles, in its order
+
+
 class mgp_rows16(C.Structure):
     _fields_ = [
         ("counts", C.c_void_p),
@@ -225,6 +242,8 @@ def load_library(path: Path | None = None) -> C.CDLL:
         "mgp_set_cell_range": ([vp, C.c_int32, C.c_int32], C.c_int),
         "mgp_copy_wait": ([vp], C.c_int),
         "mgp_txt_gz_run": ([vp, C.POINTER(mgp_txt_gz), C.POINTER(i64)], C.c_int),
+        "mgp_h5_tiles_run": ([vp, C.POINTER(mgp_h5_tiles), C.POINTER(i64)], C.c_int),
+        "mgp_h5_tiles_fetch": ([vp, vp, i64], C.c_int),
         "mgp_txt_gz_fetch": ([vp, vp, i64], C.c_int),
         "mgp_txt_gz_rows": ([C.c_int, vp, vp, i32, i32, C.POINTER(mgp_txt_gz), vp, i64, C.POINTER(i64)], C.c_int),
     }
@@ -622,6 +641,35 @@ class Engine:
             out = np.empty(max(1, n), np.uint8)
         _ck(self.lib.mgp_txt_gz_fetch(self._h, _ptr(out), int(out.shape[0])), "mgp_txt_gz_fetch")
         return TxtMembers(out[:n], mb, tb)
+
+    def h5_tiles(self, cell_of_col, chunks: tuple[int, int] = (1000, 100), cols_per_call: int = 3200) -> dict:
+        """mgp_h5_tiles_run / _fetch over every column chunk (cols_per_call columns at a
+        time): the zlib streams of the HDF5 count datasets' chunks of the run
+        (writers.py:60-131), {plane: [chunk bytes, row-major over the chunk grid]} for
+        the planes of H5_PLANES; column j holds the run's cell cell_of_col[j] (-1: zeros)."""
+        coc = np.ascontiguousarray(cell_of_col, np.int32)
+        crow, ccol = int(chunks[0]), int(chunks[1])
+        nrc = -(-self.cfg.mito_len // crow)
+        ncc = -(-coc.size // ccol)
+        step = max(1, int(cols_per_call) // ccol)
+        grid = {p: [[None] * ncc for _ in range(nrc)] for p in H5_PLANES}
+        for lo in range(0, ncc, step):
+            hi = min(ncc, lo + step)
+            cb = np.zeros(len(H5_PLANES) * nrc * (hi - lo), np.int64)
+            job = mgp_h5_tiles(coc.size, _ptr(coc), crow, ccol, lo, hi, _ptr(cb))
+            tot = C.c_int64()
+            _ck(self.lib.mgp_h5_tiles_run(self._h, C.byref(job), C.byref(tot)), "mgp_h5_tiles_run")
+            buf = np.empty(max(1, int(tot.value)), np.uint8)
+            _ck(self.lib.mgp_h5_tiles_fetch(self._h, _ptr(buf), int(buf.shape[0])), "mgp_h5_tiles_fetch")
+            raw = buf.tobytes()
+            offs = np.concatenate([[0], np.cumsum(cb)])
+            k = 0
+            for p in H5_PLANES:
+                for rc in range(nrc):
+                    for cc in range(lo, hi):
+                        grid[p][rc][cc] = raw[offs[k]:offs[k + 1]]
+                        k += 1
+        return {p: [b for row in grid[p] for b in row] for p in H5_PLANES}
 
     def windows(self) -> tuple[int, int]:
         nw, w = C.c_int32(), C.c_int32()

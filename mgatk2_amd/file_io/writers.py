@@ -194,6 +194,28 @@ def _h5py():
     return h5lite.module()
 
 
+def hdf5_columns(writer_barcodes: list[str], names: list[str], cells) -> tuple[np.ndarray, np.ndarray]:
+    """The cells of `cells` that IncrementalHDF5Writer.write_cells stores and their
+    columns: a cell whose barcode (names[c]) is in the writer's list goes to that
+    barcode's column (the last duplicate's, writers.py:146-152)."""
+    to_idx = {bc: i for i, bc in enumerate(writer_barcodes)}
+    sel, cols = [], []
+    for c in np.asarray(cells, dtype=np.int64).tolist():
+        j = to_idx.get(names[c])
+        if j is not None:
+            sel.append(c)
+            cols.append(j)
+    return np.asarray(sel, np.int64), np.asarray(cols, np.int64)
+
+
+def hdf5_cell_of_col(n_cols: int, sel: np.ndarray, cols: np.ndarray) -> np.ndarray:
+    """Column -> cell of the written cells (-1: an empty column; a later cell of the
+    same column wins)."""
+    coc = np.full(n_cols, -1, np.int64)
+    coc[cols] = sel
+    return coc
+
+
 class IncrementalHDF5Writer:
     """counts.h5 / metadata.h5 (writers.py:20-406)."""
 
@@ -266,19 +288,13 @@ class IncrementalHDF5Writer:
         over cells; values as in _put (writers.py:154-264)."""
         names = barcodes if barcodes is not None else self.barcodes
         self.report_arrays = None
-        sel, cols = [], []
-        for c in np.asarray(cells, dtype=np.int64).tolist():
+        sel_a, col_a = hdf5_columns(self.barcodes, names, cells)
+        for c in sel_a.tolist():
             bc = names[c]
-            if bc not in self.barcode_to_idx:
-                continue
-            sel.append(c)
-            cols.append(self.barcode_to_idx[bc])
             q = cell_qc(res, c, bc, self.n_positions)
             self.cell_stats.append(q)
             self.cell_depths[bc] = q["mean_depth"]
-        if sel:
-            sel_a = np.asarray(sel, np.int64)
-            col_a = np.asarray(cols, np.int64)
+        if sel_a.size:
             self._sources.append((res, sel_a, col_a))
             if self._planes is not None:
                 self._dense()
@@ -375,12 +391,15 @@ class IncrementalHDF5Writer:
             from ..bam import h5_plane_tiles
 
             res, sel_a, col_a = self._sources[0]
-            coc = np.full(n, -1, np.int64)
-            coc[col_a] = sel_a
-            tiles = {**dict(zip(names, h5_plane_tiles(res.counts, coc, list(range(8)), chunks, level=4))),
-                     **dict(zip(("tn5_cuts_fwd", "tn5_cuts_rev"), h5_plane_tiles(res.tn5, coc, [0, 1], chunks,
-                                                                                  level=4))),
-                     "coverage": h5_plane_tiles(res.depth, coc, [0], chunks, level=4)[0]}
+            coc = hdf5_cell_of_col(n, sel_a, col_a)
+            dev = getattr(res, "h5_tiles", None)  # (deflated on the device: CellProcessor.enable_device_h5)
+            if dev is not None and dev[1] == chunks and np.array_equal(dev[0], coc):
+                tiles = dev[2]
+            else:
+                tiles = {**dict(zip(names, h5_plane_tiles(res.counts, coc, list(range(8)), chunks, level=4))),
+                         **dict(zip(("tn5_cuts_fwd", "tn5_cuts_rev"), h5_plane_tiles(res.tn5, coc, [0, 1], chunks,
+                                                                                      level=4))),
+                         "coverage": h5_plane_tiles(res.depth, coc, [0], chunks, level=4)[0]}
             for k in names + ["tn5_cuts_fwd", "tn5_cuts_rev"]:
                 counts_file.create_dataset_from_chunks(k, (L, n), np.uint16, chunks, 4, tiles[k])
         else:

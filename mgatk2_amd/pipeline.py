@@ -148,6 +148,9 @@ class MtDNAPipeline:
             # (mgp_txt_gz): the writer's files exist before it
             txt_writer = IncrementalTextWriter(self.output_dir, self.config, self.barcode_list)
             processor.enable_device_txt(txt_writer.prefix, self.barcode_list)
+        else:
+            # the HDF5 chunks are deflated on the device at the end of the run (mgp_h5_tiles)
+            processor.enable_device_h5(self.barcode_list)
         if self.stream:
             # one pass: batches decoded on a producer thread, each pushed to the device as
             # it is ready, the windows piled as their reads arrive (readers.py:84-93)

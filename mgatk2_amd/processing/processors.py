@@ -112,6 +112,7 @@ class CellProcessor:
         self.last_stats: dict = {}
         self.last_timing: dict = {}
         self.txt_out = None
+        self.h5_out = None
 
     # txt output on the device ----------------------------------------------
     def enable_device_txt(self, prefix, names: list[str]):
@@ -123,6 +124,31 @@ class CellProcessor:
         (stats, depth table, reference alleles). MGP_TXT_DEVICE=0, or a gzip level other
         than the reference's 9 (MGP_GZIP_LEVEL), keeps the host formatter."""
         self.txt_out = (str(prefix), list(names))
+
+    def enable_device_h5(self, names: list[str]):
+        """Deflate the HDF5 count datasets' chunks (writers.py:60-131) on the device before
+        its context closes (mgp_h5_tiles): the run's result then carries `h5_tiles`, which
+        IncrementalHDF5Writer.finalize writes instead of deflating the planes on the host.
+        `names`: the writer's barcodes (its columns). One device only; MGP_H5_DEVICE=0 keeps
+        the host deflate."""
+        self.h5_out = list(names)
+
+    def _h5_device_on(self) -> bool:
+        return self.h5_out is not None and os.environ.get("MGP_H5_DEVICE", "1") != "0"
+
+    def _write_h5(self, res: EngineResult, eng) -> float:
+        """The written cells' columns (hdf5_columns over the passing cells in first-seen
+        order), their chunks deflated on `eng`. Returns the seconds spent."""
+        from ..file_io.writers import hdf5_cell_of_col, hdf5_columns
+
+        t0 = time.perf_counter()
+        names = self.h5_out
+        sel, cols = hdf5_columns(names, names, cells_written(res))
+        if len(names) and sel.size:
+            coc = hdf5_cell_of_col(len(names), sel, cols)
+            chunks = (min(1000, self.config.mito_length), min(100, len(names)))
+            res.h5_tiles = (coc, chunks, eng.h5_tiles(coc, chunks))
+        return time.perf_counter() - t0
 
     def _txt_device_on(self) -> bool:
         if self.txt_out is None or os.environ.get("MGP_TXT_DEVICE", "1") == "0":
@@ -205,11 +231,12 @@ class CellProcessor:
             t3 = time.perf_counter()
             self.last_stats = eng.kernel_times()
             t_txt = self._write_txt(res, [(eng, 0, n_cells)]) if self._txt_device_on() else 0.0
+            t_h5 = self._write_h5(res, eng) if self._h5_device_on() else 0.0
         t4 = time.perf_counter()
         # where the engine leg goes (pipeline timings): context + allocation, H2D of
         # the batches + the run, D2H of the results, teardown
         self.last_timing = {"engine_open": t1 - t0, "engine_h2d_run": t2 - t1, "engine_d2h": t3 - t2,
-                            "engine_close": t4 - t3 - t_txt, "txt_device": t_txt}
+                            "engine_close": t4 - t3 - t_txt - t_h5, "txt_device": t_txt, "h5_device": t_h5}
         self.last_result = res
         return res
 
@@ -376,6 +403,7 @@ class CellProcessor:
                 self.last_stats = eng.kernel_times()
                 _, last_streamed = eng.stream_info()
                 t_txt = self._write_txt(res, [(eng, 0, n_cells)]) if self._txt_device_on() else 0.0
+                t_h5 = self._write_h5(res, eng) if self._h5_device_on() else 0.0
             finally:
                 free.put(None)
                 eng.close()
@@ -389,8 +417,8 @@ class CellProcessor:
         dec_end = times.get("decode_end", t2)
         self.last_timing = {"stream_setup": t1 - t0, "stream_first_batch": times.get("first_batch", t1) - t0,
                             "stream_decode_end": dec_end - t0, "stream_push_end": t2 - t0,
-                            "engine_tail": t3 - t2, "engine_fetch": t4 - t3, "engine_close": te - t4 - t_txt,
-                            "txt_device": t_txt,
+                            "engine_tail": t3 - t2, "engine_fetch": t4 - t3,
+                            "engine_close": te - t4 - t_txt - t_h5, "txt_device": t_txt, "h5_device": t_h5,
                             "stream_batches": n_batches, "stream_batch_reads": times["cap_reads"],
                             "streamed_run": bool(last_streamed), "rows_target": rows is not None,
                             "h2d_bytes": int(h2d)}

@@ -85,7 +85,7 @@ def test_struct_layouts_match_header(tmp_path):
         "mgp_config": engine.mgp_config, "mgp_batch": engine.mgp_batch, "mgp_batch16": engine.mgp_batch16,
         "mgp_stats": engine.mgp_stats,
         "mgp_result": engine.mgp_result, "mgp_synth_params": engine.mgp_synth_params,
-        "mgp_rows16": engine.mgp_rows16, "mgp_rows8": engine.mgp_rows8,
+        "mgp_rows16": engine.mgp_rows16, "mgp_rows8": engine.mgp_rows8, "mgp_h5_tiles": engine.mgp_h5_tiles,
     }
     lines = ['#include <stdio.h>', '#include <stddef.h>', f'#include "{ROOT}/include/mgpileup.h"', "int main(){"]
     for name, cls in structs.items():

@@ -675,6 +675,17 @@ class _OracleEngine:
         blob = np.frombuffer(b"".join(b"".join(x) for x in per) or b"\0", np.uint8)
         return TxtMembers(blob[:int(mb.sum())], mb, tb)
 
+    def h5_tiles(self, cell_of_col, chunks=(1000, 100)):
+        """mgp_h5_tiles restated with the host deflate (mgp_h5_plane_tiles)."""
+        from mgatk2_amd.bam import h5_plane_tiles
+        from mgatk2_amd.engine import H5_PLANES
+
+        coc = np.asarray(cell_of_col, np.int64)
+        t = (h5_plane_tiles(self.res.counts, coc, list(range(8)), chunks, level=4)
+             + h5_plane_tiles(self.res.tn5, coc, [0, 1], chunks, level=4)
+             + h5_plane_tiles(self.res.depth, coc, [0], chunks, level=4))
+        return dict(zip(H5_PLANES, t))
+
     def close(self):
         pass
 
