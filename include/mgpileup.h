@@ -577,6 +577,9 @@ typedef struct mgp_h5_tiles {
     int32_t        chunk_rows, chunk_cols;
     int32_t        col_chunk_lo, col_chunk_hi;
     int64_t       *chunk_bytes;     /* host out: [11][row chunks][hi - lo] stream sizes  */
+    int64_t       *col_sums;        /* host out (may be NULL): [3][mito_len] per-position sums over
+                                       this call's columns of coverage, tn5 fwd, tn5 rev (the
+                                       QC report's, writers.py / report.py)               */
 } mgp_h5_tiles;
 int  mgp_h5_tiles_run(mgp_ctx *ctx, mgp_h5_tiles *job, int64_t *total_bytes);
 int  mgp_h5_tiles_fetch(mgp_ctx *ctx, uint8_t *dst, int64_t cap);

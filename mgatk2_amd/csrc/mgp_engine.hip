@@ -122,7 +122,7 @@ struct TxtState {
 
 // mgp_h5_tiles: the HDF5 chunk deflate's buffers (mgp_txtgz.hip), kept for the next call
 struct H5State {
-    DevBuf coc, raw, tok, out, out_off, chunk_bytes, dst_off, packed;
+    DevBuf coc, raw, tok, out, out_off, chunk_bytes, dst_off, packed, sums, prof;
     uint64_t total = 0;
 };
 
@@ -4826,24 +4826,50 @@ int mgp_h5_tiles_run(mgp_ctx* ctx, mgp_h5_tiles* job, int64_t* total_bytes) {
             return set_err(MGP_E_INVALID, "mgp_h5_tiles: cell of a column out of range");
     hipStream_t s = ctx->s_comp;
     const uint64_t chunk_raw = (uint64_t)crow * ccol * 2, stride = out_bound(chunk_raw);
+    const uint64_t raw_stride = (chunk_raw + 15) & ~uint64_t(15);
     MGP_TRY(st.coc.ensure((size_t)std::max<int64_t>(nco, 1) * 4));
-    MGP_TRY(st.raw.ensure((size_t)(nch * chunk_raw) + 64));
+    MGP_TRY(st.raw.ensure((size_t)(nch * raw_stride) + 64));
     MGP_TRY(st.tok.ensure((size_t)(nch * chunk_raw) * 4 + 64));
     MGP_TRY(st.out.ensure((size_t)(nch * stride) + 64));
     MGP_TRY(st.out_off.ensure((size_t)nch * 8));
     MGP_TRY(st.chunk_bytes.ensure((size_t)nch * 4));
     MGP_TRY(st.dst_off.ensure((size_t)nch * 8));
+    MGP_TRY(st.sums.ensure((size_t)3 * g.L * 8));
+    HIP_TRY(hipMemsetAsync(st.sums.p, 0, (size_t)3 * g.L * 8, s));
     std::vector<uint64_t> oo((size_t)nch);
     for (int64_t k = 0; k < nch; ++k) oo[(size_t)k] = (uint64_t)k * stride;
     if (nco) HIP_TRY(hipMemcpyAsync(st.coc.p, job->cell_of_col, (size_t)nco * 4, hipMemcpyHostToDevice, s));
     HIP_TRY(hipMemcpyAsync(st.out_off.p, oo.data(), (size_t)nch * 8, hipMemcpyHostToDevice, s));
     H5Job jb{ctx->counts16.as<uint4>(), ctx->tn5_16.as<uint32_t>(), ctx->depth16.as<uint16_t>(), g.L,
-             st.coc.as<int32_t>(), nco, crow, ccol, nrc, lo, ncc};
+             st.coc.as<int32_t>(), nco, crow, ccol, nrc, lo, ncc, st.sums.as<unsigned long long>()};
     H5Scratch sc{st.raw.as<uint8_t>(), st.tok.as<uint32_t>(), st.out.as<uint32_t>(), st.out_off.as<uint64_t>(),
-                 st.chunk_bytes.as<uint32_t>(), chunk_raw, stride};
+                 st.chunk_bytes.as<uint32_t>(), chunk_raw, stride, raw_stride, nullptr};
+    const bool prof = std::getenv("MGP_H5_PROF") != nullptr;
+    if (prof) {
+        MGP_TRY(st.prof.ensure((size_t)nch * 32));
+        HIP_TRY(hipMemsetAsync(st.prof.p, 0, (size_t)nch * 32, s));
+        sc.prof = st.prof.as<uint64_t>();
+    }
     if (h5_deflate(jb, sc, s) != 0) return set_err(MGP_E_HIP, "mgp_h5_tiles: deflate kernel launch failed");
+    if (prof) {  // per-phase means over the chunks (us) and the code kernel's span, to stderr
+        std::vector<uint64_t> pr((size_t)nch * 4);
+        HIP_TRY(hipMemcpyAsync(pr.data(), st.prof.p, pr.size() * 8, hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipStreamSynchronize(s));
+        double m[3] = {0, 0, 0};
+        uint64_t a = UINT64_MAX, b = 0;
+        for (int64_t k = 0; k < nch; ++k) {
+            const uint64_t* q = pr.data() + k * 4;
+            for (int i = 0; i < 3; ++i) m[i] += (double)(q[i + 1] - q[i]) * 0.01;
+            a = std::min(a, q[0]);
+            b = std::max(b, q[3]);
+        }
+        std::fprintf(stderr, "[mgp_h5_tiles] %lld chunks: parse %.1f us, adler %.1f us, block %.1f us per chunk; "
+                     "span %.2f ms\n", (long long)nch, m[0] / nch, m[1] / nch, m[2] / nch, (b - a) * 1e-5);
+    }
     std::vector<uint32_t> cb((size_t)nch);
     HIP_TRY(hipMemcpyAsync(cb.data(), st.chunk_bytes.p, (size_t)nch * 4, hipMemcpyDeviceToHost, s));
+    if (job->col_sums)
+        HIP_TRY(hipMemcpyAsync(job->col_sums, st.sums.p, (size_t)3 * g.L * 8, hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));
     std::vector<uint64_t> dst((size_t)nch);
     uint64_t tot = 0;

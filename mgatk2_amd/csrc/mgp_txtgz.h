@@ -81,8 +81,10 @@ struct H5Job {
     int crow, ccol;             // chunk shape
     int nrc;                    // row chunks, ceil(L / crow)
     int cc0, ncc;               // this batch: column chunks [cc0, cc0 + ncc)
+    unsigned long long* sums;   // [3][L]: per-position sums over the batch's columns of the
+                                // coverage, tn5 fwd and tn5 rev planes (zeroed by the caller)
 };
-// Batch chunk k = (plane * nrc + rc) * ncc + (cc - cc0): its raw bytes at raw + k chunk_raw,
+// Batch chunk k = (plane * nrc + rc) * ncc + (cc - cc0): its raw bytes at raw + k raw_stride,
 // its output region at out + k out_stride (out_off[k]).
 struct H5Scratch {
     uint8_t* raw;
@@ -91,6 +93,8 @@ struct H5Scratch {
     const uint64_t* out_off;
     uint32_t* chunk_bytes;   // [chunks] zlib stream bytes
     uint64_t chunk_raw, out_stride;
+    uint64_t raw_stride;     // chunk_raw rounded up to 16 bytes (the parse loads 16 at a time)
+    uint64_t* prof;          // MGP_H5_PROF: [chunks][4] phase stamps (100 MHz wall clock), else null
 };
 // the planes' raw chunks of the batch, then their zlib streams (chunk_bytes filled)
 int h5_deflate(const H5Job& job, const H5Scratch& sc, hipStream_t s);

@@ -921,14 +921,21 @@ __global__ void __launch_bounds__(kT) k_txt_pack(const uint32_t* __restrict__ ou
 // One workgroup per (row chunk, column chunk) of the batch: each position of each column
 // read once (a cell's 8 counts as one uint4), the 11 planes' raw chunks written row-major
 // (consecutive threads, consecutive columns of a chunk row).
+constexpr int kSumRows = 4096;  // chunk rows whose column sums a workgroup gathers in LDS
+
 __global__ void __launch_bounds__(kT) k_h5_gather(H5Job job, H5Scratch sc) {
+    __shared__ uint32_t srow[3][kSumRows];  // (<= 100 columns x 65535 per row and plane)
+    const bool lsum = job.crow <= kSumRows && (int64_t)job.ccol * 65535 < ((int64_t)1 << 32);
+    if (lsum)
+        for (int q = threadIdx.x; q < 3 * job.crow; q += kT) srow[q / job.crow][q % job.crow] = 0;
+    __syncthreads();
     const int r = blockIdx.x;
     const int rc = r / job.ncc, ccl = r - rc * job.ncc;
     const int cc = job.cc0 + ccl;
     const int n = job.crow * job.ccol;
     uint16_t* const base = reinterpret_cast<uint16_t*>(sc.raw);
-    const size_t pstride = (size_t)job.nrc * job.ncc * (sc.chunk_raw / 2);  // one plane's chunks (u16)
-    const size_t k0 = ((size_t)rc * job.ncc + ccl) * (sc.chunk_raw / 2);
+    const size_t pstride = (size_t)job.nrc * job.ncc * (sc.raw_stride / 2);  // one plane's chunks (u16)
+    const size_t k0 = ((size_t)rc * job.ncc + ccl) * (sc.raw_stride / 2);
     for (int x = threadIdx.x; x < n; x += kT) {
         const int row = x / job.ccol, c = x - row * job.ccol;
         const int p = rc * job.crow + row;
@@ -952,6 +959,21 @@ __global__ void __launch_bounds__(kT) k_h5_gather(H5Job job, H5Scratch sc) {
         o[8 * pstride] = (uint16_t)(tt & 0xFFFFu);
         o[9 * pstride] = (uint16_t)(tt >> 16);
         o[10 * pstride] = (uint16_t)d;
+        // the report's per-position sums over the columns (writers.py:_report_arrays)
+        const uint32_t v3[3] = {d, tt & 0xFFFFu, tt >> 16};
+#pragma unroll
+        for (int q = 0; q < 3; ++q) {
+            if (!v3[q]) continue;
+            if (lsum) atomicAdd(&srow[q][row], v3[q]);
+            else atomicAdd(&job.sums[(size_t)q * job.L + p], (unsigned long long)v3[q]);
+        }
+    }
+    if (!lsum) return;
+    __syncthreads();
+    for (int q = threadIdx.x; q < 3 * job.crow; q += kT) {
+        const int pl = q / job.crow, row = q - pl * job.crow, p = rc * job.crow + row;
+        const uint32_t v = srow[pl][row];
+        if (v && p < job.L) atomicAdd(&job.sums[(size_t)pl * job.L + p], (unsigned long long)v);
     }
 }
 
@@ -966,55 +988,93 @@ __global__ void __launch_bounds__(kT) k_h5_code(H5Job job, H5Scratch sc) {
     __shared__ uint64_t red[4];
     const int t = threadIdx.x;
     const int64_t k = blockIdx.x;
-    const uint8_t* const T = sc.raw + k * sc.chunk_raw;
+    const uint8_t* const T = sc.raw + k * sc.raw_stride;
     uint32_t* const tok = sc.tok + k * sc.chunk_raw;
     uint32_t* const out = sc.out + k * (sc.out_stride / 4);
     const int n = (int)sc.chunk_raw;
-    const int P = (n + kT - 1) / kT;
-    auto start = [&](int u) -> int {  // thread u's start
-        const int s0 = min(n, u * P);
-        if (u == 0 || s0 >= n) return s0;
-        const uint8_t v = T[s0 - 1];
-        int r = 0;
-        while (r < P && s0 + r < n && T[s0 + r] == v) ++r;
-        return s0 + r;
-    };
-    const int t0 = start(t), t1 = t == kT - 1 ? n : start(t + 1);
+    const int P = (((n + kT - 1) / kT) + 15) & ~15;  // 16-byte aligned nominal segments
+    __shared__ int rr[kT];
+#define H5_STAMP(q)                                                                   \
+    do {                                                                              \
+        if (sc.prof) {                                                                \
+            __syncthreads();                                                          \
+            if (t == 0) sc.prof[k * 4 + (q)] = wall_clock64();                        \
+        }                                                                             \
+    } while (0)
+    H5_STAMP(0);
+    // the run continuing across a nominal start belongs to the previous thread's last token
+    const int s = min(n, t * P), snext = min(n, s + P);
+    int r = 0;
+    if (t > 0 && s < n) {
+        const uint32_t v = T[s - 1];
+        bool go = true;
+        for (int i = s; go && i < snext; i += 4) {
+            const uint32_t w = *reinterpret_cast<const uint32_t*>(T + i);
+#pragma unroll
+            for (int b = 0; b < 4; ++b) {
+                go = go && i + b < snext && ((w >> (8 * b)) & 0xFFu) == v;
+                r += go;
+            }
+        }
+    }
+    rr[t] = r;
     for (int q = t; q < kLit; q += kT) S.lit_f[q] = 0;
     if (t < kDist) S.dist_f[t] = 0;
     __syncthreads();
+    const int t0 = s + r, t1 = snext + (t + 1 < kT ? rr[t + 1] : 0);
+    // one forward pass over the bytes (16 per load, no load waits on a token): a run of
+    // bytes equal to the previous one is pending until it breaks or reaches 258 bytes,
+    // then it is a match (>= 3 bytes, distance 1) or literals
     uint32_t ntok = 0;
     uint64_t A = 0, W = 0;  // Adler-32 partial sums: sum of bytes, sum of (t1 - i) x byte
-    for (int i = t0; i < t1;) {
-        const uint8_t v = T[i];
-        int l = 0;
-        if (i > 0) {
-            const uint8_t pv = T[i - 1];
-            const int cap = min(258, t1 - i);
-            while (l < cap && T[i + l] == pv) ++l;
-        }
-        if (l >= 3) {
-            atomicAdd(&S.lit_f[257 + len_code(l)], 1u);
+    int pend = 0;
+    int pv = t0 > 0 ? (int)T[t0 - 1] : -1;
+    auto flush = [&]() {
+        if (pend >= 3) {
+            atomicAdd(&S.lit_f[257 + len_code(pend)], 1u);
             atomicAdd(&S.dist_f[0], 1u);
-            tok[t0 + ntok] = ((uint32_t)l << 16) | 1u;
-            A += (uint64_t)v * l;  // (l copies of the previous byte, which equals v)
-            W += (uint64_t)v * ((uint64_t)(t1 - i) * l - (uint64_t)l * (l - 1) / 2);
-            i += l;
+            tok[t0 + ntok++] = ((uint32_t)pend << 16) | 1u;
         } else {
-            atomicAdd(&S.lit_f[v], 1u);
-            tok[t0 + ntok] = v;
-            A += v;
-            W += (uint64_t)v * (uint64_t)(t1 - i);
-            ++i;
+            for (int q = 0; q < pend; ++q) {
+                atomicAdd(&S.lit_f[pv], 1u);
+                tok[t0 + ntok++] = (uint32_t)pv;
+            }
         }
-        ++ntok;
+    };
+    for (int base = t0 & ~15; base < t1; base += 16) {
+        const uint4 w4 = *reinterpret_cast<const uint4*>(T + base);
+        const uint32_t ws[4] = {w4.x, w4.y, w4.z, w4.w};
+#pragma unroll
+        for (int b = 0; b < 16; ++b) {
+            const int i = base + b;
+            if (i < t0 || i >= t1) continue;
+            const int c = (int)((ws[b >> 2] >> (8 * (b & 3))) & 0xFFu);
+            A += (uint64_t)c;
+            W += (uint64_t)c * (uint64_t)(t1 - i);
+            if (c == pv && pend < 258) {
+                ++pend;
+                continue;
+            }
+            flush();
+            if (c == pv) {  // (a run past 258 bytes goes on)
+                pend = 1;
+            } else {
+                pend = 0;
+                atomicAdd(&S.lit_f[c], 1u);
+                tok[t0 + ntok++] = (uint32_t)c;
+                pv = c;
+            }
+        }
     }
+    flush();
+    H5_STAMP(1);
     // Adler-32 of the chunk: s1 = 1 + sum b, s2 = n + sum_i (n - i) b_i
     uint64_t a_tot, w_tot;
     (void)block_excl_scan(A, red, a_tot);
     (void)block_excl_scan(W + (uint64_t)(n - t1) * A, red, w_tot);
     const uint32_t s1 = (uint32_t)((1 + a_tot) % 65521u), s2 = (uint32_t)(((uint64_t)n + w_tot) % 65521u);
     const uint8_t zhdr[2] = {0x78, 0x5E};
+    H5_STAMP(2);
     const uint64_t blk = deflate_block(S, T, tok, t0, ntok, (uint64_t)n, out, zhdr, 2);
     if (t == 0) {
         uint8_t* const ob = reinterpret_cast<uint8_t*>(out);
@@ -1022,6 +1082,8 @@ __global__ void __launch_bounds__(kT) k_h5_code(H5Job job, H5Scratch sc) {
         for (int q = 0; q < 4; ++q) ob[2 + blk + q] = (uint8_t)(ad >> (24 - 8 * q));  // big-endian
         sc.chunk_bytes[k] = (uint32_t)(2 + blk + 4);
     }
+    H5_STAMP(3);
+#undef H5_STAMP
 }
 
 // ---------------------------------------------------------------------------

@@ -167,6 +167,7 @@ class mgp_h5_tiles(C.Structure):
         ("col_chunk_lo", C.c_int32),
         ("col_chunk_hi", C.c_int32),
         ("chunk_bytes", C.c_void_p),
+        ("col_sums", C.c_void_p),
     ]
 
 
@@ -642,33 +643,42 @@ class Engine:
         _ck(self.lib.mgp_txt_gz_fetch(self._h, _ptr(out), int(out.shape[0])), "mgp_txt_gz_fetch")
         return TxtMembers(out[:n], mb, tb)
 
-    def h5_tiles(self, cell_of_col, chunks: tuple[int, int] = (1000, 100), cols_per_call: int = 3200) -> dict:
+    def h5_tiles(self, cell_of_col, chunks: tuple[int, int] = (1000, 100), cols_per_call: int = 3200,
+                 sums: dict | None = None) -> dict:
         """mgp_h5_tiles_run / _fetch over every column chunk (cols_per_call columns at a
         time): the zlib streams of the HDF5 count datasets' chunks of the run
-        (writers.py:60-131), {plane: [chunk bytes, row-major over the chunk grid]} for
-        the planes of H5_PLANES; column j holds the run's cell cell_of_col[j] (-1: zeros)."""
+        (writers.py:60-131), {plane: [chunk (u8 array), row-major over the chunk grid]} for
+        the planes of H5_PLANES; column j holds the run's cell cell_of_col[j] (-1: zeros).
+        sums (a dict): filled with the per-position sums over the columns of the stored
+        coverage / tn5 planes ("coverage", "tn5_fwd", "tn5_rev", int64 [L])."""
         coc = np.ascontiguousarray(cell_of_col, np.int32)
         crow, ccol = int(chunks[0]), int(chunks[1])
         nrc = -(-self.cfg.mito_len // crow)
         ncc = -(-coc.size // ccol)
         step = max(1, int(cols_per_call) // ccol)
         grid = {p: [[None] * ncc for _ in range(nrc)] for p in H5_PLANES}
+        L = self.cfg.mito_len
+        acc = np.zeros((3, L), np.int64)
+        part = np.zeros((3, L), np.int64)
         for lo in range(0, ncc, step):
             hi = min(ncc, lo + step)
             cb = np.zeros(len(H5_PLANES) * nrc * (hi - lo), np.int64)
-            job = mgp_h5_tiles(coc.size, _ptr(coc), crow, ccol, lo, hi, _ptr(cb))
+            job = mgp_h5_tiles(coc.size, _ptr(coc), crow, ccol, lo, hi, _ptr(cb), _ptr(part))
             tot = C.c_int64()
             _ck(self.lib.mgp_h5_tiles_run(self._h, C.byref(job), C.byref(tot)), "mgp_h5_tiles_run")
             buf = np.empty(max(1, int(tot.value)), np.uint8)
             _ck(self.lib.mgp_h5_tiles_fetch(self._h, _ptr(buf), int(buf.shape[0])), "mgp_h5_tiles_fetch")
-            raw = buf.tobytes()
-            offs = np.concatenate([[0], np.cumsum(cb)])
+            offs = np.concatenate([[0], np.cumsum(cb)]).tolist()
             k = 0
             for p in H5_PLANES:
                 for rc in range(nrc):
+                    row = grid[p][rc]
                     for cc in range(lo, hi):
-                        grid[p][rc][cc] = raw[offs[k]:offs[k + 1]]
+                        row[cc] = buf[offs[k]:offs[k + 1]]  # (views of the call's buffer)
                         k += 1
+            acc += part
+        if sums is not None:
+            sums.update(coverage=acc[0], tn5_fwd=acc[1], tn5_rev=acc[2])
         return {p: [b for row in grid[p] for b in row] for p in H5_PLANES}
 
     def windows(self) -> tuple[int, int]:

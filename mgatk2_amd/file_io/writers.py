@@ -313,13 +313,29 @@ class IncrementalHDF5Writer:
                 cnt = res.counts[int(c)].astype(np.int64)
                 self.position_base_counts += cnt[:, 0::2] + cnt[:, 1::2]
 
+    def _device_tiles(self, coc: np.ndarray, chunks):
+        """The device's chunks of the one recorded source (CellProcessor.enable_device_h5:
+        (cell_of_col, chunks, tiles, column sums)) when they are of these columns and chunks."""
+        if len(self._sources) != 1:
+            return None
+        dev = getattr(self._sources[0][0], "h5_tiles", None)
+        if dev is None or tuple(dev[1]) != tuple(chunks) or not np.array_equal(dev[0], coc):
+            return None
+        return dev
+
     def _report_arrays(self, refs: list[str]) -> dict:
         """What the HTML report reads back from the files (report.py _load), from
         memory: per-position sums over the columns of the coverage and Tn5 planes (of
         the saturated u16 values, as stored) and the metadata arrays."""
         L, n = self.n_positions, self.n_barcodes
         sums = {k: np.zeros(L, np.int64) for k in ("coverage", "tn5_fwd", "tn5_rev")}
-        if self._planes is not None:
+        dev = None
+        if self._planes is None and len(self._sources) == 1 and n:
+            res, sel_a, col_a = self._sources[0]
+            dev = self._device_tiles(hdf5_cell_of_col(n, sel_a, col_a), (min(1000, L), min(100, n)))
+        if dev is not None and len(dev) > 3:  # the device's sums over the stored planes' columns
+            sums = {k: np.asarray(dev[3][k], np.int64) for k in ("coverage", "tn5_fwd", "tn5_rev")}
+        elif self._planes is not None:
             sums["coverage"] = self._coverage.sum(axis=1, dtype=np.int64)
             sums["tn5_fwd"] = self._tn5["fwd"].sum(axis=1, dtype=np.int64)
             sums["tn5_rev"] = self._tn5["rev"].sum(axis=1, dtype=np.int64)
@@ -392,8 +408,8 @@ class IncrementalHDF5Writer:
 
             res, sel_a, col_a = self._sources[0]
             coc = hdf5_cell_of_col(n, sel_a, col_a)
-            dev = getattr(res, "h5_tiles", None)  # (deflated on the device: CellProcessor.enable_device_h5)
-            if dev is not None and dev[1] == chunks and np.array_equal(dev[0], coc):
+            dev = self._device_tiles(coc, chunks)  # (deflated on the device: CellProcessor.enable_device_h5)
+            if dev is not None:
                 tiles = dev[2]
             else:
                 tiles = {**dict(zip(names, h5_plane_tiles(res.counts, coc, list(range(8)), chunks, level=4))),

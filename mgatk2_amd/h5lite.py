@@ -475,7 +475,8 @@ class Group:
 
     def create_dataset_from_chunks(self, name: str, shape, dtype, chunks, level: int, tiles: list[bytes]):
         """A chunked gzip dataset written from already deflated chunks (the
-        H5Z_DEFLATE form, row-major over the chunk grid: mgp_h5_plane_tiles)."""
+        H5Z_DEFLATE form, row-major over the chunk grid: mgp_h5_plane_tiles, or
+        mgp_h5_tiles on the device as u8 arrays)."""
         lib = _h5()
         t, own = _type_for(np.dtype(dtype))
         sp = _space(shape)
@@ -490,7 +491,9 @@ class Group:
                 for i, blob in enumerate(tiles):
                     off[0] = (i // nc) * chunks[0]
                     off[1] = (i % nc) * chunks[1]
-                    _ck_retry(lambda: lib.H5Dwrite_chunk(did, H5P_DEFAULT, 0, off, len(blob), blob),
+                    # (bytes, or a u8 array view: Engine.h5_tiles)
+                    ptr = blob.ctypes.data if isinstance(blob, np.ndarray) else blob
+                    _ck_retry(lambda: lib.H5Dwrite_chunk(did, H5P_DEFAULT, 0, off, len(blob), ptr),
                               "H5Dwrite_chunk")
             except Exception:
                 lib.H5Dclose(did)

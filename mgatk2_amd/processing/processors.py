@@ -147,7 +147,8 @@ class CellProcessor:
         if len(names) and sel.size:
             coc = hdf5_cell_of_col(len(names), sel, cols)
             chunks = (min(1000, self.config.mito_length), min(100, len(names)))
-            res.h5_tiles = (coc, chunks, eng.h5_tiles(coc, chunks))
+            sums = {}
+            res.h5_tiles = (coc, chunks, eng.h5_tiles(coc, chunks, sums=sums), sums)
         return time.perf_counter() - t0
 
     def _txt_device_on(self) -> bool:

@@ -79,8 +79,13 @@ def test_device_h5_chunks_equal_the_planes(engine_lib, chunks, cols_per_call):
         eng.push(soa)
         eng.run()
         res = eng.fetch()
-        tiles = eng.h5_tiles(coc, chunks, cols_per_call=cols_per_call)
+        sums = {}
+        tiles = eng.h5_tiles(coc, chunks, cols_per_call=cols_per_call, sums=sums)
     _check(tiles, res, coc, chunks)
+    # the report's per-position sums over the stored columns (duplicates count twice)
+    ok = coc >= 0
+    for k, a in (("coverage", res.depth), ("tn5_fwd", res.tn5[:, :, 0]), ("tn5_rev", res.tn5[:, :, 1])):
+        np.testing.assert_array_equal(sums[k], np.minimum(a[coc[ok]], 65535).astype(np.int64).sum(axis=0), err_msg=k)
 
 
 def test_device_h5_chunks_saturate_a_wide_window(engine_lib):
@@ -96,8 +101,10 @@ def test_device_h5_chunks_saturate_a_wide_window(engine_lib):
         eng.push(deep)
         eng.run()
         res = eng.fetch()
-        tiles = eng.h5_tiles(np.array([0, -1, 0]), (1000, 3))
+        sums = {}
+        tiles = eng.h5_tiles(np.array([0, -1, 0]), (1000, 3), sums=sums)
     assert res.depth.max() > 65535
+    np.testing.assert_array_equal(sums["coverage"], 2 * np.minimum(res.depth[0], 65535).astype(np.int64))
     _check(tiles, res, np.array([0, -1, 0]), (1000, 3))
 
 

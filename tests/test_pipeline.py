@@ -675,12 +675,17 @@ class _OracleEngine:
         blob = np.frombuffer(b"".join(b"".join(x) for x in per) or b"\0", np.uint8)
         return TxtMembers(blob[:int(mb.sum())], mb, tb)
 
-    def h5_tiles(self, cell_of_col, chunks=(1000, 100)):
+    def h5_tiles(self, cell_of_col, chunks=(1000, 100), sums=None):
         """mgp_h5_tiles restated with the host deflate (mgp_h5_plane_tiles)."""
         from mgatk2_amd.bam import h5_plane_tiles
         from mgatk2_amd.engine import H5_PLANES
 
         coc = np.asarray(cell_of_col, np.int64)
+        if sums is not None:
+            ok = coc[coc >= 0]
+            sat = lambda a: np.minimum(a[ok], 65535).astype(np.int64).sum(axis=0)  # noqa: E731
+            sums.update(coverage=sat(self.res.depth), tn5_fwd=sat(self.res.tn5[:, :, 0]),
+                        tn5_rev=sat(self.res.tn5[:, :, 1]))
         t = (h5_plane_tiles(self.res.counts, coc, list(range(8)), chunks, level=4)
              + h5_plane_tiles(self.res.tn5, coc, [0, 1], chunks, level=4)
              + h5_plane_tiles(self.res.depth, coc, [0], chunks, level=4))
