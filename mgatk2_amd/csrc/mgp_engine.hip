@@ -4846,25 +4846,28 @@ int mgp_h5_tiles_run(mgp_ctx* ctx, mgp_h5_tiles* job, int64_t* total_bytes) {
                  st.chunk_bytes.as<uint32_t>(), chunk_raw, stride, raw_stride, nullptr};
     const bool prof = std::getenv("MGP_H5_PROF") != nullptr;
     if (prof) {
-        MGP_TRY(st.prof.ensure((size_t)nch * 32));
-        HIP_TRY(hipMemsetAsync(st.prof.p, 0, (size_t)nch * 32, s));
+        MGP_TRY(st.prof.ensure((size_t)nch * 64));
+        HIP_TRY(hipMemsetAsync(st.prof.p, 0, (size_t)nch * 64, s));
         sc.prof = st.prof.as<uint64_t>();
     }
     if (h5_deflate(jb, sc, s) != 0) return set_err(MGP_E_HIP, "mgp_h5_tiles: deflate kernel launch failed");
     if (prof) {  // per-phase means over the chunks (us) and the code kernel's span, to stderr
-        std::vector<uint64_t> pr((size_t)nch * 4);
+        // stamps: 0 start, 1 parse, 2 adler, 3 end; 4 lit/dist lengths, 5 header, 6 sizes (deflate_block)
+        std::vector<uint64_t> pr((size_t)nch * 8);
         HIP_TRY(hipMemcpyAsync(pr.data(), st.prof.p, pr.size() * 8, hipMemcpyDeviceToHost, s));
         HIP_TRY(hipStreamSynchronize(s));
-        double m[3] = {0, 0, 0};
+        const int ord[7] = {0, 1, 2, 4, 5, 6, 3};  // phases in time order
+        double m[6] = {0, 0, 0, 0, 0, 0};
         uint64_t a = UINT64_MAX, b = 0;
         for (int64_t k = 0; k < nch; ++k) {
-            const uint64_t* q = pr.data() + k * 4;
-            for (int i = 0; i < 3; ++i) m[i] += (double)(q[i + 1] - q[i]) * 0.01;
+            const uint64_t* q = pr.data() + k * 8;
+            for (int i = 0; i < 6; ++i) m[i] += (double)(q[ord[i + 1]] - q[ord[i]]) * 0.01;
             a = std::min(a, q[0]);
             b = std::max(b, q[3]);
         }
-        std::fprintf(stderr, "[mgp_h5_tiles] %lld chunks: parse %.1f us, adler %.1f us, block %.1f us per chunk; "
-                     "span %.2f ms\n", (long long)nch, m[0] / nch, m[1] / nch, m[2] / nch, (b - a) * 1e-5);
+        std::fprintf(stderr, "[mgp_h5_tiles] %lld chunks: parse %.1f us, adler %.1f, huffman %.1f, header %.1f, "
+                     "sizes %.1f, encode %.1f us per chunk; span %.2f ms\n", (long long)nch, m[0] / nch, m[1] / nch,
+                     m[2] / nch, m[3] / nch, m[4] / nch, m[5] / nch, (b - a) * 1e-5);
     }
     std::vector<uint32_t> cb((size_t)nch);
     HIP_TRY(hipMemcpyAsync(cb.data(), st.chunk_bytes.p, (size_t)nch * 4, hipMemcpyDeviceToHost, s));

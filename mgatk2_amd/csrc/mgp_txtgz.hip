@@ -674,8 +674,15 @@ __global__ void __launch_bounds__(kT, 4) k_txt_match(Job job, Scratch sc) {
 // the fixed codes, or stored blocks of the n_text raw bytes T, whichever is smallest.
 // Returns the block's bytes (every thread). All threads call.
 __device__ uint64_t deflate_block(CodeLds& S, const uint8_t* T, const uint32_t* tok, int t0, uint32_t ntok,
-                                  uint64_t n_text, uint32_t* out, const uint8_t* hdr, int hdr_len) {
+                                  uint64_t n_text, uint32_t* out, const uint8_t* hdr, int hdr_len,
+                                  uint64_t* stamps = nullptr) {
     const int t = threadIdx.x;
+    auto stamp = [&](int q) {  // (profiling: the wall clock after each phase)
+        if (stamps) {
+            __syncthreads();
+            if (t == 0) stamps[q] = wall_clock64();
+        }
+    };
     if (t == 0) S.lit_f[256] = 1;  // end of block
     __syncthreads();
     huff_lengths(S.lit_f, kLit, 15, S.lit_len, S.h);
@@ -733,6 +740,7 @@ __device__ uint64_t deflate_block(CodeLds& S, const uint8_t* T, const uint32_t* 
         S.n_rle = nr;
     }
     __syncthreads();
+    stamp(0);
     huff_lengths(S.cl_f, 19, 7, S.cl_len, S.h);
     if (t == 0) {
         // (a code-length code with one symbol: add a second so the code is complete)
@@ -756,6 +764,7 @@ __device__ uint64_t deflate_block(CodeLds& S, const uint8_t* T, const uint32_t* 
         S.hdr_bits = hb;
     }
     __syncthreads();
+    stamp(1);
     // ---- 4. sizes of the three block kinds, then the encoder ----
     uint64_t dyn_b = 0, fix_b = 0;
     for (uint32_t q = 0; q < ntok; ++q) {
@@ -781,6 +790,7 @@ __device__ uint64_t deflate_block(CodeLds& S, const uint8_t* T, const uint32_t* 
     const uint64_t sto_bytes = n_text + 5 * n_blk;
     const int mode = (dyn_bytes <= fix_bytes && dyn_bytes <= sto_bytes) ? 0 : (fix_bytes <= sto_bytes ? 1 : 2);
     const uint64_t blk_bytes = mode == 0 ? dyn_bytes : mode == 1 ? fix_bytes : sto_bytes;
+    stamp(2);
     const uint64_t region = out_bound(n_text) / 4;  // (the bound has room for the frame)
     for (uint64_t q = t; q < region; q += kT) out[q] = 0;
     __threadfence_block();
@@ -998,7 +1008,7 @@ __global__ void __launch_bounds__(kT) k_h5_code(H5Job job, H5Scratch sc) {
     do {                                                                              \
         if (sc.prof) {                                                                \
             __syncthreads();                                                          \
-            if (t == 0) sc.prof[k * 4 + (q)] = wall_clock64();                        \
+            if (t == 0) sc.prof[k * 8 + (q)] = wall_clock64();                        \
         }                                                                             \
     } while (0)
     H5_STAMP(0);
@@ -1075,7 +1085,7 @@ __global__ void __launch_bounds__(kT) k_h5_code(H5Job job, H5Scratch sc) {
     const uint32_t s1 = (uint32_t)((1 + a_tot) % 65521u), s2 = (uint32_t)(((uint64_t)n + w_tot) % 65521u);
     const uint8_t zhdr[2] = {0x78, 0x5E};
     H5_STAMP(2);
-    const uint64_t blk = deflate_block(S, T, tok, t0, ntok, (uint64_t)n, out, zhdr, 2);
+    const uint64_t blk = deflate_block(S, T, tok, t0, ntok, (uint64_t)n, out, zhdr, 2, sc.prof ? sc.prof + k * 8 + 4 : nullptr);
     if (t == 0) {
         uint8_t* const ob = reinterpret_cast<uint8_t*>(out);
         const uint32_t ad = (s2 << 16) | s1;
