@@ -4829,7 +4829,7 @@ int mgp_h5_tiles_run(mgp_ctx* ctx, mgp_h5_tiles* job, int64_t* total_bytes) {
     const uint64_t raw_stride = (chunk_raw + 15) & ~uint64_t(15);
     MGP_TRY(st.coc.ensure((size_t)std::max<int64_t>(nco, 1) * 4));
     MGP_TRY(st.raw.ensure((size_t)(nch * raw_stride) + 64));
-    MGP_TRY(st.tok.ensure((size_t)(nch * chunk_raw) * 4 + 64));
+    MGP_TRY(st.tok.ensure((size_t)(nch * h5_tok_words(chunk_raw)) * 4 + 64));
     MGP_TRY(st.out.ensure((size_t)(nch * stride) + 64));
     MGP_TRY(st.out_off.ensure((size_t)nch * 8));
     MGP_TRY(st.chunk_bytes.ensure((size_t)nch * 4));
@@ -4843,7 +4843,7 @@ int mgp_h5_tiles_run(mgp_ctx* ctx, mgp_h5_tiles* job, int64_t* total_bytes) {
     H5Job jb{ctx->counts16.as<uint4>(), ctx->tn5_16.as<uint32_t>(), ctx->depth16.as<uint16_t>(), g.L,
              st.coc.as<int32_t>(), nco, crow, ccol, nrc, lo, ncc, st.sums.as<unsigned long long>()};
     H5Scratch sc{st.raw.as<uint8_t>(), st.tok.as<uint32_t>(), st.out.as<uint32_t>(), st.out_off.as<uint64_t>(),
-                 st.chunk_bytes.as<uint32_t>(), chunk_raw, stride, raw_stride, nullptr};
+                 st.chunk_bytes.as<uint32_t>(), chunk_raw, stride, raw_stride, h5_tok_words(chunk_raw), nullptr};
     const bool prof = std::getenv("MGP_H5_PROF") != nullptr;
     if (prof) {
         MGP_TRY(st.prof.ensure((size_t)nch * 64));

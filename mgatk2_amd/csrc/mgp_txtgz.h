@@ -88,14 +88,19 @@ struct H5Job {
 // its output region at out + k out_stride (out_off[k]).
 struct H5Scratch {
     uint8_t* raw;
-    uint32_t* tok;           // chunk_raw words per chunk
+    uint32_t* tok;           // tok_stride words per chunk (h5_tok_words)
     uint32_t* out;
     const uint64_t* out_off;
     uint32_t* chunk_bytes;   // [chunks] zlib stream bytes
     uint64_t chunk_raw, out_stride;
     uint64_t raw_stride;     // chunk_raw rounded up to 16 bytes (the parse loads 16 at a time)
+    uint64_t tok_stride;     // h5_tok_words(chunk_raw)
     uint64_t* prof;          // MGP_H5_PROF: [chunks][4] phase stamps (100 MHz wall clock), else null
 };
+// a chunk's parse segment (bytes per thread, 16-aligned) and its token words (u16 tokens,
+// at most two segments' worth per thread)
+__host__ __device__ inline int h5_seg_bytes(uint64_t chunk_raw) { return (int)((((chunk_raw + 255) / 256) + 15) & ~uint64_t(15)); }
+__host__ __device__ inline uint64_t h5_tok_words(uint64_t chunk_raw) { return (uint64_t)h5_seg_bytes(chunk_raw) * 256; }
 // the planes' raw chunks of the batch, then their zlib streams (chunk_bytes filled)
 int h5_deflate(const H5Job& job, const H5Scratch& sc, hipStream_t s);
 // the streams packed back to back (chunk order) into dst at dst_off[chunks]

@@ -37,6 +37,7 @@ namespace mgp {
 namespace txtgz {
 
 constexpr int kT = 256;        // threads per member (one segment each)
+static_assert(kT == 256, "h5_seg_bytes / h5_tok_words (mgp_txtgz.h) assume 256 threads per chunk");
 constexpr int kJ = 16;         // previous lines searched for matches
 constexpr int kLMax = 31;      // longest match tried (longer ones gain nothing on C4-like text)
 constexpr int kMaxDist = 32768;
@@ -140,67 +141,85 @@ struct HuffLds {
     uint32_t w[2 * kLit];
     uint16_t par[2 * kLit];
     uint8_t dep[2 * kLit];
-    int m, redo;
+    int m;
 };
-// len[s] for s < n from freq[s] (LDS), lengths <= mb; every used symbol gets a code
+// len[s] for s < n from freq[s] (LDS), lengths <= mb; every used symbol gets a code and
+// the code is complete (Kraft sum 1, as inflate requires). One Huffman tree; leaves deeper
+// than mb are clipped to mb, then the per-length counts are repaired (the deepest shorter
+// leaf moved one level down until the Kraft sum fits, then leaves moved up until it is
+// exactly 1) and the lengths dealt out by frequency, the longest to the rarest (zlib's
+// gen_bitlen does the same repair; halving the counts and rebuilding, as before, took
+// ~7 rebuilds on count planes: 0.5 ms per chunk).
 __device__ void huff_lengths(const uint32_t* freq, int n, int mb, uint8_t* len, HuffLds& h) {
     const int t = threadIdx.x;
     for (int s = t; s < n; s += kT) h.f[s] = freq[s];
+    if (t == 0) h.m = 0;
     __syncthreads();
-    for (;;) {
-        if (t == 0) h.m = 0;
-        __syncthreads();
-        // rank sort of the used symbols by (count, symbol)
-        for (int s = t; s < n; s += kT) {
-            const uint32_t fs = h.f[s];
-            if (!fs) continue;
-            int r = 0;
-            for (int q = 0; q < n; ++q) {
-                const uint32_t fq = h.f[q];
-                r += (fq != 0) & ((fq < fs) | ((fq == fs) & (q < s)));
-            }
-            h.order[r] = (uint16_t)s;
-            atomicAdd(&h.m, 1);
+    // rank sort of the used symbols by (count, symbol)
+    for (int s = t; s < n; s += kT) {
+        const uint32_t fs = h.f[s];
+        if (!fs) continue;
+        int r = 0;
+        for (int q = 0; q < n; ++q) {
+            const uint32_t fq = h.f[q];
+            r += (fq != 0) & ((fq < fs) | ((fq == fs) & (q < s)));
         }
-        __syncthreads();
-        if (t == 0) {
-            const int m = h.m;
-            for (int s = 0; s < n; ++s) len[s] = 0;
-            h.redo = 0;
-            if (m == 1) {
-                len[h.order[0]] = 1;
-            } else if (m > 1) {
-                // two queues: the sorted leaves 0..m-1 and the internal nodes m.. in creation order
-                for (int i = 0; i < m; ++i) h.w[i] = h.f[h.order[i]];
-                int li = 0, ni = m, nn = m;
-                auto take = [&]() -> int {
-                    if (li < m && (ni >= nn || h.w[li] <= h.w[ni])) return li++;
-                    return ni++;
-                };
-                for (int k = 0; k < m - 1; ++k) {
-                    const int a = take(), b = take();
-                    h.w[nn] = h.w[a] + h.w[b];
-                    h.par[a] = (uint16_t)nn;
-                    h.par[b] = (uint16_t)nn;
-                    ++nn;
-                }
-                h.dep[nn - 1] = 0;
-                int mx = 0;
-                for (int x = nn - 2; x >= 0; --x) {
-                    h.dep[x] = (uint8_t)(h.dep[h.par[x]] + 1);
-                    if (x < m && h.dep[x] > mx) mx = h.dep[x];
-                }
-                if (mx > mb) {
-                    for (int s = 0; s < n; ++s) h.f[s] = h.f[s] ? ((h.f[s] >> 1) | 1u) : 0u;
-                    h.redo = 1;
-                } else {
-                    for (int i = 0; i < m; ++i) len[h.order[i]] = h.dep[i];
-                }
-            }
-        }
-        __syncthreads();
-        if (!h.redo) break;
+        h.order[r] = (uint16_t)s;
+        atomicAdd(&h.m, 1);
     }
+    __syncthreads();
+    if (t == 0) {
+        const int m = h.m;
+        for (int s = 0; s < n; ++s) len[s] = 0;
+        if (m == 1) {
+            len[h.order[0]] = 1;
+        } else if (m > 1) {
+            // two queues: the sorted leaves 0..m-1 and the internal nodes m.. in creation order
+            for (int i = 0; i < m; ++i) h.w[i] = h.f[h.order[i]];
+            int li = 0, ni = m, nn = m;
+            auto take = [&]() -> int {
+                if (li < m && (ni >= nn || h.w[li] <= h.w[ni])) return li++;
+                return ni++;
+            };
+            for (int k = 0; k < m - 1; ++k) {
+                const int a = take(), b = take();
+                h.w[nn] = h.w[a] + h.w[b];
+                h.par[a] = (uint16_t)nn;
+                h.par[b] = (uint16_t)nn;
+                ++nn;
+            }
+            h.dep[nn - 1] = 0;
+            uint32_t cnt[16] = {0};  // leaves per length (clipped to mb)
+            for (int x = nn - 2; x >= 0; --x) {
+                const int d = h.dep[h.par[x]] + 1;
+                h.dep[x] = (uint8_t)(d < 255 ? d : 255);
+                if (x < m) cnt[d < mb ? d : mb]++;
+            }
+            // Kraft sum in units of 2^-mb
+            int64_t K = 0;
+            for (int l = 1; l <= mb; ++l) K += (int64_t)cnt[l] << (mb - l);
+            const int64_t full = (int64_t)1 << mb;
+            while (K > full) {  // the deepest leaf above mb one level down
+                int b = mb - 1;
+                while (cnt[b] == 0) --b;
+                cnt[b]--;
+                cnt[b + 1]++;
+                K -= (int64_t)1 << (mb - b - 1);
+            }
+            while (K < full) {  // a leaf whose move up fits, the deepest first
+                int b = mb;
+                while (cnt[b] == 0 || ((int64_t)1 << (mb - b)) > full - K) --b;
+                cnt[b]--;
+                cnt[b - 1]++;
+                K += (int64_t)1 << (mb - b);
+            }
+            // the rarest symbols (order ascending) get the longest codes
+            int i = 0;
+            for (int l = mb; l >= 1; --l)
+                for (uint32_t c = 0; c < cnt[l]; ++c) len[h.order[i++]] = (uint8_t)l;
+        }
+    }
+    __syncthreads();
 }
 
 // canonical codes (bit-reversed for LSB-first output), one thread
@@ -667,13 +686,15 @@ __global__ void __launch_bounds__(kT, 4) k_txt_match(Job job, Scratch sc) {
 }
 
 
-// The tokens of every thread (tok[t0 .. t0 + ntok): literal bytes or l << 16 | d; their
+// The tokens of every thread (ntok each: literal bytes or l << 16 | d; their
 // symbol counts in S.lit_f / S.dist_f) as one final deflate block after the frame's
 // header bytes (hdr, hdr_len <= 10) in out, whose region (out_bound(n_text) bytes, room
 // for the frame included) is zeroed here: dynamic Huffman codes (length-limited), or
 // the fixed codes, or stored blocks of the n_text raw bytes T, whichever is smallest.
-// Returns the block's bytes (every thread). All threads call.
-__device__ uint64_t deflate_block(CodeLds& S, const uint8_t* T, const uint32_t* tok, int t0, uint32_t ntok,
+// Returns the block's bytes (every thread). All threads call. tok(q): the calling thread's
+// q-th token (a functor over the caller's token layout).
+template <class Tok>
+__device__ uint64_t deflate_block(CodeLds& S, const uint8_t* T, const Tok& tok, uint32_t ntok,
                                   uint64_t n_text, uint32_t* out, const uint8_t* hdr, int hdr_len,
                                   uint64_t* stamps = nullptr) {
     const int t = threadIdx.x;
@@ -768,7 +789,7 @@ __device__ uint64_t deflate_block(CodeLds& S, const uint8_t* T, const uint32_t* 
     // ---- 4. sizes of the three block kinds, then the encoder ----
     uint64_t dyn_b = 0, fix_b = 0;
     for (uint32_t q = 0; q < ntok; ++q) {
-        const uint32_t tk = tok[t0 + q];
+        const uint32_t tk = tok(q);
         dyn_b += token_bits(tk, S.lit_len, S.dist_len);
         const uint32_t l = tk >> 16;
         if (!l) fix_b += fixed_len((int)tk);
@@ -817,7 +838,7 @@ __device__ uint64_t deflate_block(CodeLds& S, const uint8_t* T, const uint32_t* 
             bw.done();
         }
         BitW bw(out, 8 * (uint64_t)hdr_len + S.hdr_bits + dyn_pre);
-        for (uint32_t q = 0; q < ntok; ++q) put_token(bw, tok[t0 + q], S.lit_code, S.lit_len, S.dist_code, S.dist_len);
+        for (uint32_t q = 0; q < ntok; ++q) put_token(bw, tok(q), S.lit_code, S.lit_len, S.dist_code, S.dist_len);
         if (t == kT - 1) bw.put(S.lit_code[256], S.lit_len[256]);
         bw.done();
     } else if (mode == 1) {
@@ -834,7 +855,7 @@ __device__ uint64_t deflate_block(CodeLds& S, const uint8_t* T, const uint32_t* 
         }
         __syncthreads();
         BitW bw(out, 8 * (uint64_t)hdr_len + 3 + fix_pre);
-        for (uint32_t q = 0; q < ntok; ++q) put_token(bw, tok[t0 + q], S.lit_code, S.lit_len, S.dist_code, S.dist_len);
+        for (uint32_t q = 0; q < ntok; ++q) put_token(bw, tok(q), S.lit_code, S.lit_len, S.dist_code, S.dist_len);
         if (t == kT - 1) bw.put(S.lit_code[256], S.lit_len[256]);
         bw.done();
     } else {
@@ -898,7 +919,7 @@ __global__ void __launch_bounds__(kT) k_txt_code(Job job, Scratch sc) {
     }
     PROF_STAMP(3);
     const uint8_t gz_hdr[10] = {0x1F, 0x8B, 0x08, 0, 0, 0, 0, 0, 0x02, 0xFF};  // magic, deflate, mtime 0, xfl 2, os 255
-    const uint64_t blk_bytes = deflate_block(S, T, tok, t0, ntok, n_text, out, gz_hdr, 10);
+    const uint64_t blk_bytes = deflate_block(S, T, [&](uint32_t q) { return tok[t0 + q]; }, ntok, n_text, out, gz_hdr, 10);
     uint8_t* const ob = reinterpret_cast<uint8_t*>(out);
     __threadfence_block();
     __syncthreads();
@@ -999,10 +1020,10 @@ __global__ void __launch_bounds__(kT) k_h5_code(H5Job job, H5Scratch sc) {
     const int t = threadIdx.x;
     const int64_t k = blockIdx.x;
     const uint8_t* const T = sc.raw + k * sc.raw_stride;
-    uint32_t* const tok = sc.tok + k * sc.chunk_raw;
+    uint32_t* const tok = sc.tok + k * sc.tok_stride;
     uint32_t* const out = sc.out + k * (sc.out_stride / 4);
     const int n = (int)sc.chunk_raw;
-    const int P = (((n + kT - 1) / kT) + 15) & ~15;  // 16-byte aligned nominal segments
+    const int P = h5_seg_bytes(sc.chunk_raw);  // 16-byte aligned nominal segments (kT of them)
     __shared__ int rr[kT];
 #define H5_STAMP(q)                                                                   \
     do {                                                                              \
@@ -1039,15 +1060,21 @@ __global__ void __launch_bounds__(kT) k_h5_code(H5Job job, H5Scratch sc) {
     uint64_t A = 0, W = 0;  // Adler-32 partial sums: sum of bytes, sum of (t1 - i) x byte
     int pend = 0;
     int pv = t0 > 0 ? (int)T[t0 - 1] : -1;
+    // the tokens as u16 (a literal byte, or 256 + length - 3 of a distance-1 match), the
+    // thread's q-th at tok16[q kT + t]: each wave's loads and stores of its q-th tokens are
+    // one contiguous range (the thread-contiguous layout cost 0.6 ms per chunk in each
+    // pass over the tokens: 64 lines per wave access)
+    uint16_t* const tok16 = reinterpret_cast<uint16_t*>(tok);
+    auto put = [&](uint32_t v) { tok16[(size_t)ntok++ * kT + t] = (uint16_t)v; };
     auto flush = [&]() {
         if (pend >= 3) {
             atomicAdd(&S.lit_f[257 + len_code(pend)], 1u);
             atomicAdd(&S.dist_f[0], 1u);
-            tok[t0 + ntok++] = ((uint32_t)pend << 16) | 1u;
+            put(256u + (uint32_t)(pend - 3));
         } else {
             for (int q = 0; q < pend; ++q) {
                 atomicAdd(&S.lit_f[pv], 1u);
-                tok[t0 + ntok++] = (uint32_t)pv;
+                put((uint32_t)pv);
             }
         }
     };
@@ -1071,7 +1098,7 @@ __global__ void __launch_bounds__(kT) k_h5_code(H5Job job, H5Scratch sc) {
             } else {
                 pend = 0;
                 atomicAdd(&S.lit_f[c], 1u);
-                tok[t0 + ntok++] = (uint32_t)c;
+                put((uint32_t)c);
                 pv = c;
             }
         }
@@ -1085,7 +1112,11 @@ __global__ void __launch_bounds__(kT) k_h5_code(H5Job job, H5Scratch sc) {
     const uint32_t s1 = (uint32_t)((1 + a_tot) % 65521u), s2 = (uint32_t)(((uint64_t)n + w_tot) % 65521u);
     const uint8_t zhdr[2] = {0x78, 0x5E};
     H5_STAMP(2);
-    const uint64_t blk = deflate_block(S, T, tok, t0, ntok, (uint64_t)n, out, zhdr, 2, sc.prof ? sc.prof + k * 8 + 4 : nullptr);
+    auto tok_of = [&](uint32_t q) -> uint32_t {
+        const uint32_t v = tok16[(size_t)q * kT + t];
+        return v < 256u ? v : ((v - 253u) << 16) | 1u;  // (length v - 256 + 3, distance 1)
+    };
+    const uint64_t blk = deflate_block(S, T, tok_of, ntok, (uint64_t)n, out, zhdr, 2, sc.prof ? sc.prof + k * 8 + 4 : nullptr);
     if (t == 0) {
         uint8_t* const ob = reinterpret_cast<uint8_t*>(out);
         const uint32_t ad = (s2 << 16) | s1;
