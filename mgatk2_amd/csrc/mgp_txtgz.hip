@@ -273,8 +273,12 @@ __device__ __forceinline__ void lds_prices_from_lengths(CodeLds& S) {
     for (int c = threadIdx.x; c < kDist; c += kT) S.dcost[c] = (uint8_t)((S.dist_len[c] ? S.dist_len[c] : 16) + dist_xb(c));
 }
 
-// forward match length at distance d from i (at most cap), text staged in LDS
+#ifndef MGP_TXT_FWD_CAP
+#define MGP_TXT_FWD_CAP 8  // (8 and 12 gave the same members on C4 text, 31: 0.04 % smaller, match 12 % slower)
+#endif
+// forward match length at distance d from i (at most cap and MGP_TXT_FWD_CAP), text staged in LDS
 __device__ __forceinline__ int fwd_match(const uint8_t* W, int i, int d, int cap) {
+    cap = min(cap, MGP_TXT_FWD_CAP);
     int L = 0;
     while (L < cap && W[i + L] == W[i - d + L]) ++L;
     return L;
@@ -288,10 +292,12 @@ __device__ __forceinline__ int fwd_match(const uint8_t* W, int i, int d, int cap
 // length follows L(i) = T[i] == T[i - d] ? L(i + 1) + 1 : 0, so only the first byte
 // visited (the line end, a field's last byte) costs a forward compare. Every position
 // keeps its longest candidate (the nearest on ties): cand[i] = d | L << 16, 0 if L < 3.
-__device__ void match_window(const uint8_t* W, int64_t base, int64_t wend, const uint32_t* lines, int k0, int k1,
+__device__ void match_window(const uint8_t* W, int64_t base, int64_t wend, const uint32_t* ln, int k0, int k1,
                              int kb, int nf, uint32_t* cand) {
+    // ln: the window's line table in LDS, lines kb .. k1 - 1
+    auto line = [&](int k) -> const uint32_t* { return ln + 3 * (size_t)(k - kb); };
     for (int k = k0 + (int)threadIdx.x; k < k1; k += kT) {
-        const uint32_t* le = lines + 3 * (size_t)k;
+        const uint32_t* le = line(k);
         const int s = (int)((int64_t)le[0] - base);
         const int A1 = s + (int)(le[1] & 0xFFFFu), A2 = s + (int)(le[1] >> 16), A3 = s + (int)(le[2] & 0xFFFFu);
         const int e = s + (int)(le[2] >> 16) - 1;  // the '\n'
@@ -303,7 +309,7 @@ __device__ void match_window(const uint8_t* W, int64_t base, int64_t wend, const
             dd[j] = 0;
             ll[j] = 0;
             if (k - j - 1 < kb) continue;  // (lines before the window: no candidate)
-            const uint32_t* lp = lines + 3 * (size_t)(k - j - 1);
+            const uint32_t* lp = line(k - j - 1);
             const int d = e - ((int)((int64_t)lp[0] - base) + (int)(lp[2] >> 16) - 1);
             if (d > 0 && d <= kMaxDist) dd[j] = (uint32_t)d;
         }
@@ -325,7 +331,7 @@ __device__ void match_window(const uint8_t* W, int64_t base, int64_t wend, const
                     }
                     int dF = 0, LF = 0;
                     if (k - j - 1 >= kb) {
-                        const uint32_t* lp = lines + 3 * (size_t)(k - j - 1);
+                        const uint32_t* lp = line(k - j - 1);
                         const int sp = (int)((int64_t)lp[0] - base);
                         const int Bf = f == 0 ? sp
                                      : f == 1 ? sp + (int)(lp[1] & 0xFFFFu)
@@ -634,8 +640,11 @@ __global__ void __launch_bounds__(kT) k_txt_format(Job job, Scratch sc) {
     PROF_STAMP(1);
 }
 
+constexpr int kWinLines = 1024;  // line table entries of a window (LDS)
+
 struct MatchLds {
     uint8_t win[kWinBytes];
+    uint32_t ln[3 * kWinLines];  // the window's lines (start, field offsets, length)
     int win_k1, win_kb;
 };
 
@@ -663,7 +672,7 @@ __global__ void __launch_bounds__(kT, 4) k_txt_match(Job job, Scratch sc) {
             int kb = max(0, k0 - kJ);
             while (kb < k0 && s0 - line_start(kb) > kWinBytes / 2) ++kb;
             const int64_t base = line_start(kb);
-            int lo = k0 + 1, hi = n_lines;  // largest k1 in [k0 + 1, n_lines] whose text fits
+            int lo = k0 + 1, hi = min(n_lines, kb + kWinLines);  // largest k1 whose text and lines fit
             while (lo < hi) {
                 const int mid = (lo + hi + 1) / 2;
                 if (line_start(mid) + 64 - base <= kWinBytes) lo = mid;
@@ -677,8 +686,9 @@ __global__ void __launch_bounds__(kT, 4) k_txt_match(Job job, Scratch sc) {
         const int64_t base = line_start(kb);
         const int64_t wend = min((int64_t)n_text, line_start(k1) + 64);
         for (int64_t x = base + t; x < wend; x += kT) S.win[x - base] = T[x];
+        for (int q = t; q < 3 * (k1 - kb); q += kT) S.ln[q] = lines[3 * (size_t)kb + q];
         __syncthreads();
-        match_window(S.win, base, wend, lines, k0, k1, kb, nf, tok);
+        match_window(S.win, base, wend, S.ln, k0, k1, kb, nf, tok);
         __syncthreads();
         k0 = k1;
     }
