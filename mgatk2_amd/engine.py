@@ -644,24 +644,25 @@ class Engine:
         return TxtMembers(out[:n], mb, tb)
 
     def h5_tiles(self, cell_of_col, chunks: tuple[int, int] = (1000, 100), cols_per_call: int = 3200,
-                 sums: dict | None = None) -> dict:
+                 sums: dict | None = None, col_chunks: tuple[int, int] | None = None) -> dict:
         """mgp_h5_tiles_run / _fetch over every column chunk (cols_per_call columns at a
         time): the zlib streams of the HDF5 count datasets' chunks of the run
         (writers.py:60-131), {plane: [chunk (u8 array), row-major over the chunk grid]} for
         the planes of H5_PLANES; column j holds the run's cell cell_of_col[j] (-1: zeros).
         sums (a dict): filled with the per-position sums over the columns of the stored
-        coverage / tn5 planes ("coverage", "tn5_fwd", "tn5_rev", int64 [L])."""
+        coverage / tn5 planes ("coverage", "tn5_fwd", "tn5_rev", int64 [L]). col_chunks
+        (c0, c1): only those column chunks (the lists then row-major over that sub-grid)."""
         coc = np.ascontiguousarray(cell_of_col, np.int32)
         crow, ccol = int(chunks[0]), int(chunks[1])
         nrc = -(-self.cfg.mito_len // crow)
-        ncc = -(-coc.size // ccol)
+        c0, c1 = (0, -(-coc.size // ccol)) if col_chunks is None else (int(col_chunks[0]), int(col_chunks[1]))
         step = max(1, int(cols_per_call) // ccol)
-        grid = {p: [[None] * ncc for _ in range(nrc)] for p in H5_PLANES}
+        grid = {p: [[None] * (c1 - c0) for _ in range(nrc)] for p in H5_PLANES}
         L = self.cfg.mito_len
         acc = np.zeros((3, L), np.int64)
         part = np.zeros((3, L), np.int64)
-        for lo in range(0, ncc, step):
-            hi = min(ncc, lo + step)
+        for lo in range(c0, c1, step):
+            hi = min(c1, lo + step)
             cb = np.zeros(len(H5_PLANES) * nrc * (hi - lo), np.int64)
             job = mgp_h5_tiles(coc.size, _ptr(coc), crow, ccol, lo, hi, _ptr(cb), _ptr(part))
             tot = C.c_int64()
@@ -674,7 +675,7 @@ class Engine:
                 for rc in range(nrc):
                     row = grid[p][rc]
                     for cc in range(lo, hi):
-                        row[cc] = buf[offs[k]:offs[k + 1]]  # (views of the call's buffer)
+                        row[cc - c0] = buf[offs[k]:offs[k + 1]]  # (views of the call's buffer)
                         k += 1
             acc += part
         if sums is not None:

@@ -126,29 +126,91 @@ class CellProcessor:
         self.txt_out = (str(prefix), list(names))
 
     def enable_device_h5(self, names: list[str]):
-        """Deflate the HDF5 count datasets' chunks (writers.py:60-131) on the device before
-        its context closes (mgp_h5_tiles): the run's result then carries `h5_tiles`, which
+        """Deflate the HDF5 count datasets' chunks (writers.py:60-131) on the devices before
+        their contexts close (mgp_h5_tiles): the run's result then carries `h5_tiles`, which
         IncrementalHDF5Writer.finalize writes instead of deflating the planes on the host.
-        `names`: the writer's barcodes (its columns). One device only; MGP_H5_DEVICE=0 keeps
-        the host deflate."""
+        `names`: the writer's barcodes (its columns). MGP_H5_DEVICE=0 keeps the host deflate."""
         self.h5_out = list(names)
 
     def _h5_device_on(self) -> bool:
         return self.h5_out is not None and os.environ.get("MGP_H5_DEVICE", "1") != "0"
 
-    def _write_h5(self, res: EngineResult, eng) -> float:
+    def _write_h5(self, res: EngineResult, parts: list) -> float:
         """The written cells' columns (hdf5_columns over the passing cells in first-seen
-        order), their chunks deflated on `eng`. Returns the seconds spent."""
+        order), their chunks deflated on the devices: parts = [(engine, lo, hi)], each
+        engine holding the cells [lo, hi) as its 0..hi-lo. A column chunk whose cells lie
+        on one device is made there; one that spans two devices' cells (at most one per
+        boundary) is deflated on the host from the fetched rows. Returns the seconds spent."""
+        from concurrent.futures import ThreadPoolExecutor
+
+        from ..bam import h5_plane_tiles
+        from ..engine import H5_PLANES
         from ..file_io.writers import hdf5_cell_of_col, hdf5_columns
 
         t0 = time.perf_counter()
         names = self.h5_out
         sel, cols = hdf5_columns(names, names, cells_written(res))
-        if len(names) and sel.size:
-            coc = hdf5_cell_of_col(len(names), sel, cols)
-            chunks = (min(1000, self.config.mito_length), min(100, len(names)))
-            sums = {}
-            res.h5_tiles = (coc, chunks, eng.h5_tiles(coc, chunks, sums=sums), sums)
+        if not (len(names) and sel.size):
+            return time.perf_counter() - t0
+        n, L = len(names), self.config.mito_length
+        coc = hdf5_cell_of_col(n, sel, cols)
+        chunks = (min(1000, L), min(100, n))
+        crow, ccol = chunks
+        nrc, ncc = -(-L // crow), -(-n // ccol)
+        los = np.array([lo for _, lo, _ in parts], np.int64)
+        his = np.array([hi for _, _, hi in parts], np.int64)
+        owner = np.zeros(ncc, np.int64)  # the part making each column chunk, -1: the host
+        for cc in range(ncc):
+            v = coc[cc * ccol:(cc + 1) * ccol]
+            v = v[v >= 0]
+            if v.size:
+                d = np.searchsorted(his, v, side="right")
+                owner[cc] = d[0] if np.all(d == d[0]) else -1
+        tiles = {p: [None] * (nrc * ncc) for p in H5_PLANES}
+        total = np.zeros((3, L), np.int64)
+
+        def runs(d):  # (c0, c1) runs of consecutive column chunks of part d
+            idx = np.flatnonzero(owner == d)
+            if not idx.size:
+                return []
+            cut = np.flatnonzero(np.diff(idx) > 1) + 1
+            return [(int(g[0]), int(g[-1]) + 1) for g in np.split(idx, cut)]
+
+        def one(d):
+            eng, lo, hi = parts[d]
+            local = np.where((coc >= lo) & (coc < hi), coc - lo, -1)
+            out = []
+            for c0, c1 in runs(d):
+                sums = {}
+                out.append((c0, c1, eng.h5_tiles(local, chunks, sums=sums, col_chunks=(c0, c1)), sums))
+            return out
+
+        if len(parts) > 1:
+            with ThreadPoolExecutor(len(parts)) as pool:
+                made = list(pool.map(one, range(len(parts))))
+        else:
+            made = [one(0)]
+        for got in made:
+            for c0, c1, tl, sums in got:
+                w = c1 - c0
+                for p in H5_PLANES:
+                    src = tl[p]
+                    for rc in range(nrc):
+                        tiles[p][rc * ncc + c0:rc * ncc + c1] = src[rc * w:(rc + 1) * w]
+                total += np.stack([sums["coverage"], sums["tn5_fwd"], sums["tn5_rev"]])
+        for cc in np.flatnonzero(owner < 0).tolist():  # chunks across a device boundary
+            sub = coc[cc * ccol:(cc + 1) * ccol]
+            made_h = (h5_plane_tiles(res.counts, sub, list(range(8)), chunks, level=4)
+                      + h5_plane_tiles(res.tn5, sub, [0, 1], chunks, level=4)
+                      + h5_plane_tiles(res.depth, sub, [0], chunks, level=4))
+            for p, lst in zip(H5_PLANES, made_h):
+                for rc in range(nrc):
+                    tiles[p][rc * ncc + cc] = lst[rc]
+            ok = sub[sub >= 0]
+            total[0] += np.minimum(res.depth[ok], 65535).astype(np.int64).sum(axis=0)
+            total[1] += np.minimum(res.tn5[ok, :, 0], 65535).astype(np.int64).sum(axis=0)
+            total[2] += np.minimum(res.tn5[ok, :, 1], 65535).astype(np.int64).sum(axis=0)
+        res.h5_tiles = (coc, chunks, tiles, {"coverage": total[0], "tn5_fwd": total[1], "tn5_rev": total[2]})
         return time.perf_counter() - t0
 
     def _txt_device_on(self) -> bool:
@@ -159,51 +221,46 @@ class CellProcessor:
     def _write_txt(self, res: EngineResult, parts: list) -> float:
         """The passing cells in first-seen order (processors.py:75's write order) through
         mgp_txt_gz on their devices; parts = [(engine, lo, hi)], each engine holding the
-        cells [lo, hi) as its 0..hi-lo. Members of cells on different devices are
-        interleaved back into the global order. Returns the seconds spent."""
+        cells [lo, hi) as its 0..hi-lo. With several devices each writes its own cells (in
+        the global order, TXT_CHUNK_CELLS per call, the devices concurrently) and the
+        members are interleaved back into the global order. Returns the seconds spent."""
         t0 = time.perf_counter()
         prefix, names = self.txt_out
         written = cells_written(res)
-        his = np.array([hi for _, _, hi in parts], np.int64)
         files = [open(f"{prefix}.{f}.txt.gz", "ab") for f in TXT_FILES]
-        pool = None
         try:
-            if len(parts) > 1:
+            if len(parts) == 1:
+                eng, lo, _ = parts[0]
+                for a in range(0, written.size, TXT_CHUNK_CELLS):
+                    chunk = written[a:a + TXT_CHUNK_CELLS]
+                    mem = eng.txt_gz(chunk - lo, [names[c] for c in chunk.tolist()])
+                    for f in range(5):
+                        files[f].write(memoryview(mem.file_part(f)))
+            else:
                 from concurrent.futures import ThreadPoolExecutor
 
-                pool = ThreadPoolExecutor(len(parts))
-            for a in range(0, written.size, TXT_CHUNK_CELLS):
-                chunk = written[a:a + TXT_CHUNK_CELLS]
-                dev = np.searchsorted(his, chunk, side="right")  # each cell's part
-                sels = [chunk[dev == d] for d in range(len(parts))]
+                his = np.array([hi for _, _, hi in parts], np.int64)
+                dev = np.searchsorted(his, written, side="right")  # each cell's part
 
                 def one(d):
                     eng, lo, _ = parts[d]
-                    sel = sels[d]
-                    return eng.txt_gz(sel - lo, [names[c] for c in sel.tolist()]) if sel.size else None
+                    sel = written[dev == d]
+                    return [eng.txt_gz(ch - lo, [names[c] for c in ch.tolist()])
+                            for ch in (sel[a:a + TXT_CHUNK_CELLS] for a in range(0, sel.size, TXT_CHUNK_CELLS))]
 
-                mems = list(pool.map(one, range(len(parts)))) if pool else [one(0)]
-                if len(parts) == 1:
-                    for f in range(5):
-                        files[f].write(memoryview(mems[0].file_part(f)))
-                    continue
-                rank = np.zeros(chunk.size, np.int64)  # a cell's index among its part's cells
+                with ThreadPoolExecutor(len(parts)) as pool:
+                    mems = list(pool.map(one, range(len(parts))))
+                rank = np.zeros(written.size, np.int64)  # a cell's index among its part's cells
                 for d in range(len(parts)):
                     rank[dev == d] = np.arange(int((dev == d).sum()))
+                call, k_in = np.divmod(rank, TXT_CHUNK_CELLS)
+                order = list(zip(dev.tolist(), call.tolist(), k_in.tolist()))
                 for f in range(5):
-                    parts_f, offs = [], []
-                    for mem in mems:
-                        if mem is None:
-                            parts_f.append(None)
-                            offs.append(None)
-                            continue
-                        parts_f.append(memoryview(mem.file_part(f)))
-                        offs.append(np.concatenate([[0], np.cumsum(mem.member_bytes[f])]))
-                    files[f].writelines(parts_f[d][offs[d][k]:offs[d][k + 1]]
-                                        for d, k in zip(dev.tolist(), rank.tolist()) if offs[d][k + 1] > offs[d][k])
+                    views = [[memoryview(m.file_part(f)) for m in ms] for ms in mems]
+                    offs = [[np.concatenate([[0], np.cumsum(m.member_bytes[f])]).tolist() for m in ms] for ms in mems]
+                    files[f].writelines(views[d][j][offs[d][j][k]:offs[d][j][k + 1]]
+                                        for d, j, k in order if offs[d][j][k + 1] > offs[d][j][k])
         finally:
-            if pool is not None:
-                pool.shutdown()
             for fh in files:
                 fh.close()
         res.txt_gz_cells = written
@@ -232,7 +289,7 @@ class CellProcessor:
             t3 = time.perf_counter()
             self.last_stats = eng.kernel_times()
             t_txt = self._write_txt(res, [(eng, 0, n_cells)]) if self._txt_device_on() else 0.0
-            t_h5 = self._write_h5(res, eng) if self._h5_device_on() else 0.0
+            t_h5 = self._write_h5(res, [(eng, 0, n_cells)]) if self._h5_device_on() else 0.0
         t4 = time.perf_counter()
         # where the engine leg goes (pipeline timings): context + allocation, H2D of
         # the batches + the run, D2H of the results, teardown
@@ -404,7 +461,7 @@ class CellProcessor:
                 self.last_stats = eng.kernel_times()
                 _, last_streamed = eng.stream_info()
                 t_txt = self._write_txt(res, [(eng, 0, n_cells)]) if self._txt_device_on() else 0.0
-                t_h5 = self._write_h5(res, eng) if self._h5_device_on() else 0.0
+                t_h5 = self._write_h5(res, [(eng, 0, n_cells)]) if self._h5_device_on() else 0.0
             finally:
                 free.put(None)
                 eng.close()
@@ -651,6 +708,8 @@ class CellProcessor:
             self.last_stats = engines[parts[0][0]].kernel_times() if parts else {}
             t_txt = self._write_txt(res, [(engines[d], lo, hi) for d, lo, hi in parts]) \
                 if parts and self._txt_device_on() else 0.0
+            t_h5 = self._write_h5(res, [(engines[d], lo, hi) for d, lo, hi in parts]) \
+                if parts and self._h5_device_on() else 0.0
         finally:
             free.put(None)
             for eng in engines.values():
@@ -661,8 +720,8 @@ class CellProcessor:
         te = time.perf_counter()
         self.last_timing = {"stream_setup": t1 - t0, "stream_first_batch": times.get("first_batch", t1) - t0,
                             "stream_decode_end": times.get("decode_end", t2) - t0, "stream_push_end": t2 - t0,
-                            "engine_tail": 0.0, "engine_fetch": t3 - t2, "engine_close": te - t3 - t_txt,
-                            "txt_device": t_txt,
+                            "engine_tail": 0.0, "engine_fetch": t3 - t2, "engine_close": te - t3 - t_txt - t_h5,
+                            "txt_device": t_txt, "h5_device": t_h5,
                             "stream_batches": n_batches, "stream_batch_reads": times["cap_reads"],
                             "stream_devices": len(parts), "rows_target": rows is not None, "route_s": t_route,
                             "h2d_bytes": int(sum(link_bytes.values())),

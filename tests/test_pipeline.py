@@ -392,6 +392,32 @@ def test_pipeline_sharded_gpu(case, stream, tmp_path, engine_lib, monkeypatch):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("stream", ["1", "0"])
+def test_pipeline_sharded_hdf5_gpu(stream, tmp_path, engine_lib, monkeypatch):
+    """HDF5 output from cells sharded over 3 engine contexts (one GPU): the chunks made
+    on the contexts holding their cells (mgp_h5_tiles), the ones across a boundary on the
+    host; the files equal the reference's."""
+    from mgatk2_amd.pipeline import run_pipeline
+
+    monkeypatch.setenv("MGP_STREAM", stream)
+    monkeypatch.setenv("MGP_STREAM_BATCH", "1500")
+    g = Golden(H5_CASES[0])
+    p = g.params
+    bam = tmp_path / "x.bam"
+    soa_to_bam(bam, g.soa, g.whitelist)
+    bfile = tmp_path / "barcodes.tsv"
+    bfile.write_text("".join(b + "\n" for b in g.whitelist))
+    out = tmp_path / "out"
+    run_pipeline(
+        str(bam), str(bfile), str(out), min_baseq=p["min_baseq"], min_mapq=p["min_mapq"],
+        min_reads_per_cell=p["min_reads_per_cell"], max_strand_bias=p["max_strand_bias"],
+        skip_deduplication=p["skip_deduplication"], use_fragment_length_dedup=p["use_fragment_length_dedup"],
+        output_format="hdf5", devices=[0, 0, 0],
+    )
+    _check_h5(g, out)
+
+
+@pytest.mark.gpu
 def test_pipeline_autodetect_barcodes_gpu(tmp_path, engine_lib, oracle_lib, monkeypatch):
     """barcode_file=None through the HIP engine (pipeline.py:212-223 ->
     barcode_extraction.py:12-46): the native CB count picks the barcodes, the
@@ -675,12 +701,15 @@ class _OracleEngine:
         blob = np.frombuffer(b"".join(b"".join(x) for x in per) or b"\0", np.uint8)
         return TxtMembers(blob[:int(mb.sum())], mb, tb)
 
-    def h5_tiles(self, cell_of_col, chunks=(1000, 100), sums=None):
-        """mgp_h5_tiles restated with the host deflate (mgp_h5_plane_tiles)."""
+    def h5_tiles(self, cell_of_col, chunks=(1000, 100), sums=None, col_chunks=None):
+        """mgp_h5_tiles restated with the host deflate (mgp_h5_plane_tiles); col_chunks:
+        only those column chunks (their columns' sums)."""
         from mgatk2_amd.bam import h5_plane_tiles
         from mgatk2_amd.engine import H5_PLANES
 
         coc = np.asarray(cell_of_col, np.int64)
+        if col_chunks is not None:
+            coc = coc[col_chunks[0] * chunks[1]:col_chunks[1] * chunks[1]]
         if sums is not None:
             ok = coc[coc >= 0]
             sat = lambda a: np.minimum(a[ok], 65535).astype(np.int64).sum(axis=0)  # noqa: E731
@@ -693,6 +722,93 @@ class _OracleEngine:
 
     def close(self):
         pass
+
+
+def _stand_in_devices(monkeypatch, oracle_lib):
+    from mgatk2_amd.processing import processors
+
+    class HostBuf:
+        def __init__(self, nbytes):
+            self.buf = np.zeros(int(nbytes) + 64, np.uint8)
+
+        def array(self, shape, dtype, offset=0):
+            dt = np.dtype(dtype)
+            shape = (int(shape),) if np.ndim(shape) == 0 else tuple(int(x) for x in shape)
+            n = int(np.prod(shape)) * dt.itemsize
+            return self.buf[offset:offset + n].view(dt).reshape(shape)
+
+    _OracleEngine.oracle = oracle_lib
+    _OracleEngine.pushed = []
+    monkeypatch.setattr(processors, "Engine", _OracleEngine)
+    monkeypatch.setattr(processors, "PinnedBuffer", HostBuf)
+
+
+@pytest.mark.parametrize("n_dev", [2, 3])
+def test_stream_sharded_hdf5_host(n_dev, tmp_path, oracle_lib, monkeypatch):
+    """The streamed multi-device path with HDF5 output: each column chunk of the datasets
+    deflated by the (stand-in) device holding its cells, the chunks across a device
+    boundary on the host (CellProcessor._write_h5); the files equal the reference's."""
+    _stand_in_devices(monkeypatch, oracle_lib)
+    monkeypatch.setenv("MGP_STREAM_BATCH", "997")
+    from mgatk2_amd.pipeline import run_pipeline
+
+    case = H5_CASES[0]
+    g = Golden(case)
+    p = g.params
+    bam = tmp_path / "x.bam"
+    soa_to_bam(bam, g.soa, g.whitelist)
+    bfile = tmp_path / "barcodes.tsv"
+    bfile.write_text("".join(b + "\n" for b in g.whitelist))
+    out = tmp_path / "out"
+    run_pipeline(
+        str(bam), str(bfile), str(out), min_baseq=p["min_baseq"], min_mapq=p["min_mapq"],
+        min_reads_per_cell=p["min_reads_per_cell"], max_strand_bias=p["max_strand_bias"],
+        skip_deduplication=p["skip_deduplication"], use_fragment_length_dedup=p["use_fragment_length_dedup"],
+        output_format="hdf5", devices=list(range(n_dev)),
+    )
+    _check_h5(g, out)
+
+
+def test_write_h5_partition(tmp_path, oracle_lib):
+    """CellProcessor._write_h5 over 3 stand-in devices holding cell ranges that do not
+    fall on 100-column chunk edges, columns shuffled and repeated: every chunk equals
+    the host deflate's of the same plane, and the report's column sums are the planes'."""
+    import zlib
+
+    from mgatk2_amd.bam import h5_plane_tiles
+    from mgatk2_amd.config import PipelineConfig
+    from mgatk2_amd.engine import H5_PLANES
+    from mgatk2_amd.processing.processors import CellProcessor
+    from mgatk2_amd.synth import synth_reads
+
+    nc, L = 260, 16569
+    soa = synth_reads(5, 60_000, nc)
+    cfg = PipelineConfig()
+    res, _ = oracle_lib.oracle_run(cfg.engine_config(nc), soa)
+    bounds = [0, 77, 201, nc]
+    parts = []
+    for lo, hi in zip(bounds[:-1], bounds[1:]):
+        e = _OracleEngine.__new__(_OracleEngine)
+        e.res = type("R", (), {"counts": res.counts[lo:hi], "tn5": res.tn5[lo:hi], "depth": res.depth[lo:hi]})()
+        parts.append((e, lo, hi))
+    names = [f"B{i:04d}-1" for i in range(nc)]
+    rng = np.random.default_rng(1)
+    writer_names = names[:] + [names[int(i)] for i in rng.integers(0, nc, 20)]  # (later duplicates win)
+    proc = CellProcessor(cfg, tmp_path)
+    proc.enable_device_h5(writer_names)
+    proc.config.mito_length = L
+    res.passed[:] = 1
+    proc._write_h5(res, parts)
+    coc, chunks, tiles, sums = res.h5_tiles
+    want = (h5_plane_tiles(res.counts, coc, list(range(8)), chunks) + h5_plane_tiles(res.tn5, coc, [0, 1], chunks)
+            + h5_plane_tiles(res.depth, coc, [0], chunks))
+    for p, w in zip(H5_PLANES, want):
+        assert len(tiles[p]) == len(w)
+        for i, (a, b) in enumerate(zip(tiles[p], w)):
+            assert zlib.decompress(bytes(a)) == zlib.decompress(b), (p, i)
+    ok = coc[coc >= 0]
+    np.testing.assert_array_equal(sums["coverage"], np.minimum(res.depth[ok], 65535).astype(np.int64).sum(axis=0))
+    np.testing.assert_array_equal(sums["tn5_rev"], np.minimum(res.tn5[ok, :, 1], 65535).astype(np.int64).sum(axis=0))
 
 
 @pytest.mark.parametrize("layout", ["64", "64-paired", "32"])
