@@ -230,12 +230,25 @@ class CellProcessor:
         files = [open(f"{prefix}.{f}.txt.gz", "ab") for f in TXT_FILES]
         try:
             if len(parts) == 1:
+                from concurrent.futures import ThreadPoolExecutor
+
                 eng, lo, _ = parts[0]
-                for a in range(0, written.size, TXT_CHUNK_CELLS):
-                    chunk = written[a:a + TXT_CHUNK_CELLS]
-                    mem = eng.txt_gz(chunk - lo, [names[c] for c in chunk.tolist()])
+
+                def put(mem):
                     for f in range(5):
                         files[f].write(memoryview(mem.file_part(f)))
+
+                # a chunk's members go to the files while the device makes the next chunk's
+                with ThreadPoolExecutor(1) as wr:
+                    pending = None
+                    for a in range(0, written.size, TXT_CHUNK_CELLS):
+                        chunk = written[a:a + TXT_CHUNK_CELLS]
+                        mem = eng.txt_gz(chunk - lo, [names[c] for c in chunk.tolist()])
+                        if pending is not None:
+                            pending.result()
+                        pending = wr.submit(put, mem)
+                    if pending is not None:
+                        pending.result()
             else:
                 from concurrent.futures import ThreadPoolExecutor
 
