@@ -4676,7 +4676,7 @@ static int txt_run(TxtState& st, hipStream_t s, const txtgz::Rows& rows, int32_t
     MGP_TRY(st.member_bytes.ensure((size_t)nm * 4));
     MGP_TRY(st.dst_off.ensure((size_t)nm * 8));
     if (!st.shift_ready) {
-        std::vector<uint32_t> M(25 * 32);
+        std::vector<uint32_t> M(txtgz::kShiftPow * 32);
         crc_shift_matrices(M.data());
         MGP_TRY(st.crc_shift.ensure(M.size() * 4));
         HIP_TRY(hipMemcpy(st.crc_shift.p, M.data(), M.size() * 4, hipMemcpyHostToDevice));
@@ -4749,8 +4749,19 @@ static int txt_run(TxtState& st, hipStream_t s, const txtgz::Rows& rows, int32_t
             hi[2] = std::max(hi[2], q[4]);
             mean[2] += (double)(q[4] - q[3]) * 0.01;
         }
-        std::fprintf(stderr, "[mgp_txt_gz] %lld members: format %.1f ms (%.1f us per member), match %.1f ms, code %.1f ms "
-                     "(tail %.1f us per member)\n", (long long)cnt, (hi[0] - lo[0]) * 1e-5, mean[0] / cnt,
+        // format phases per member: 0 start, 5 sizes + scan, 6 text written, 7 own CRC, 1 end
+        double fp[4] = {0, 0, 0, 0};
+        for (int64_t m = 0; m < nm; ++m) {
+            const uint64_t* q = pr.data() + m * 8;
+            if (!q[4]) continue;
+            fp[0] += (double)(q[5] - q[0]) * 0.01;
+            fp[1] += (double)(q[6] - q[5]) * 0.01;
+            fp[2] += (double)(q[7] - q[6]) * 0.01;
+            fp[3] += (double)(q[1] - q[7]) * 0.01;
+        }
+        std::fprintf(stderr, "[mgp_txt_gz] %lld members: format %.1f ms (%.1f us per member: sizes %.1f, text %.1f, "
+                     "crc %.1f, combine %.1f), match %.1f ms, code %.1f ms (tail %.1f us per member)\n", (long long)cnt,
+                     (hi[0] - lo[0]) * 1e-5, mean[0] / cnt, fp[0] / cnt, fp[1] / cnt, fp[2] / cnt, fp[3] / cnt,
                      (hi[1] - hi[0]) * 1e-5, (hi[2] - hi[1]) * 1e-5, mean[2] / cnt);
     }
     std::vector<uint32_t> mb((size_t)nm);

@@ -51,7 +51,7 @@ struct Scratch {
     uint32_t* lines;      // line_off[5n] x 3 words: start, c1 | c2 << 16, c3 | len << 16
     uint32_t* out;        // out_off[5n] / 4 words (member outputs)
     uint32_t* member_bytes;  // [5n] compressed bytes of each member
-    const uint32_t* crc_shift;  // [25][32]: one-zero-byte CRC operator to the powers 2^b (GF(2) matrices)
+    const uint32_t* crc_shift;  // [kShiftPow][32]: one-zero-byte CRC operator to the powers 2^b (GF(2) matrices)
     uint32_t* seg;              // [5n][257] each thread's segment start in its member's text (and the end)
     uint32_t* crc;              // [5n] CRC-32 of each member's text
     uint64_t* prof;             // MGP_TXT_PROF: [5n][8] kernel stamps (100 MHz wall clock), else null
@@ -63,8 +63,10 @@ int txt_sizes(const Job& job, uint64_t* sizes, uint64_t* nlines, hipStream_t s);
 int txt_deflate(const Job& job, const Scratch& sc, hipStream_t s);
 // members packed back to back in member order (file-major) from out_off into dst at dst_off[5n]
 int txt_pack(const Scratch& sc, int64_t n_members, const uint64_t* dst_off, uint8_t* dst, hipStream_t s);
-// the 25 CRC shift matrices (host)
-void crc_shift_matrices(uint32_t* m /* 25 x 32 */);
+// the CRC shift matrices (host): texts up to 2^kShiftPow bytes (a member of 16569 lines
+// of 4096-byte barcodes is ~68 MB)
+constexpr int kShiftPow = 28;
+void crc_shift_matrices(uint32_t* m /* kShiftPow x 32 */);
 // ---- HDF5 chunks (IncrementalHDF5Writer's count datasets, writers.py:60-131) ----
 // The 11 u16 planes [L][n_cols] (A_fwd, A_rev, ..., T_rev, tn5_cuts_fwd, tn5_cuts_rev,
 // coverage; min(v, 65535) of the run's values, which its 16-bit rows hold; a column is a

@@ -436,7 +436,7 @@ __device__ void dp_segment(const uint8_t* T, uint32_t* tok, int t0, int t1, cons
 
 // zero-byte CRC operator applied n times (GF(2) matrices M[b] = one-byte operator ^ 2^b)
 __device__ uint32_t crc_shift(uint32_t c, uint64_t n, const uint32_t* M) {
-    for (int b = 0; n && b < 25; ++b, n >>= 1) {
+    for (int b = 0; n && b < kShiftPow; ++b, n >>= 1) {
         if (!(n & 1)) continue;
         const uint32_t* m = M + 32 * b;
         uint32_t r = 0;
@@ -541,9 +541,9 @@ __global__ void __launch_bounds__(kT) k_txt_sizes(Job job, uint64_t* __restrict_
 
 struct FormatLds {
     uint64_t wsum[4];
-    uint32_t crc_tab[256];
-    uint32_t crc_v[kT];
-    uint32_t crc_n[kT];
+    uint32_t crc_tab[4][256];  // slicing-by-4 tables (crc_tab[0]: the byte table)
+    uint32_t shift[kShiftPow * 32];  // the zero-byte operator's powers (Scratch::crc_shift)
+    uint32_t crc_x[kT / 64];   // the waves' XORs
 };
 
 // Kernel 1 (per member): the text, the line table, the segments' starts and the CRC-32.
@@ -565,7 +565,16 @@ __global__ void __launch_bounds__(kT) k_txt_format(Job job, Scratch sc) {
     for (int s = t; s < 256; s += kT) {
         uint32_t r = (uint32_t)s;
         for (int b = 0; b < 8; ++b) r = (r >> 1) ^ (0xEDB88320u & (0u - (r & 1u)));
-        S.crc_tab[s] = r;
+        S.crc_tab[0][s] = r;
+    }
+    for (int q = t; q < kShiftPow * 32; q += kT) S.shift[q] = sc.crc_shift[q];
+    __syncthreads();
+    for (int s = t; s < 256; s += kT) {
+        uint32_t r = S.crc_tab[0][s];
+        for (int k = 1; k < 4; ++k) {
+            r = (r >> 8) ^ S.crc_tab[0][r & 0xFFu];
+            S.crc_tab[k][s] = r;
+        }
     }
     // ---- 1. format ----
     const int P = (L + kT - 1) / kT;
@@ -579,6 +588,7 @@ __global__ void __launch_bounds__(kT) k_txt_format(Job job, Scratch sc) {
     }
     uint64_t tot;
     const uint64_t pre = block_excl_scan(((uint64_t)my_b << 24) | my_n, S.wsum, tot);
+    PROF_STAMP(5);
     const int t0 = (int)(pre >> 24), t1 = t0 + (int)my_b;
     const int l0 = (int)(pre & 0xFFFFFFu);
     {
@@ -611,30 +621,33 @@ __global__ void __launch_bounds__(kT) k_txt_format(Job job, Scratch sc) {
         }
     }
     __threadfence_block();
+    PROF_STAMP(6);
     __syncthreads();
-    // CRC of the segment (raw: init 0, no final xor)
+    // CRC of the segment (raw: init 0, no final xor), four bytes per step (slicing-by-4)
+    uint32_t r = 0;
     {
-        uint32_t r = 0;
-        for (int i = t0; i < t1; ++i) r = S.crc_tab[(r ^ T[i]) & 0xFFu] ^ (r >> 8);
-        S.crc_v[t] = r;
-        S.crc_n[t] = my_b;
-    }
-    // the CRC-32 of the text: segments combined up a tree
-    for (int s = 1; s < kT; s <<= 1) {
-        __syncthreads();
-        uint32_t v = 0, nn = 0;
-        const bool act = (t % (2 * s)) == 0 && t + s < kT;
-        if (act) {
-            v = crc_shift(S.crc_v[t], S.crc_n[t + s], sc.crc_shift) ^ S.crc_v[t + s];
-            nn = S.crc_n[t] + S.crc_n[t + s];
+        int i = t0;
+        for (; i < t1 && (reinterpret_cast<uintptr_t>(T + i) & 3u); ++i) r = S.crc_tab[0][(r ^ T[i]) & 0xFFu] ^ (r >> 8);
+        for (; i + 4 <= t1; i += 4) {
+            r ^= *reinterpret_cast<const uint32_t*>(T + i);
+            r = S.crc_tab[3][r & 0xFFu] ^ S.crc_tab[2][(r >> 8) & 0xFFu] ^ S.crc_tab[1][(r >> 16) & 0xFFu] ^
+                S.crc_tab[0][r >> 24];
         }
-        __syncthreads();
-        if (act) {
-            S.crc_v[t] = v;
-            S.crc_n[t] = nn;
-        }
+        for (; i < t1; ++i) r = S.crc_tab[0][(r ^ T[i]) & 0xFFu] ^ (r >> 8);
     }
-    if (t == 0) sc.crc[m] = S.crc_v[0] ^ crc_shift(0xFFFFFFFFu, n_text, sc.crc_shift) ^ 0xFFFFFFFFu;
+    PROF_STAMP(7);
+    // the text's CRC-32: raw CRCs are linear, so CRC(S_0 .. S_255) = XOR over t of segment t's
+    // CRC shifted past the bytes after it (one shift per thread, no tree of barriers)
+    uint32_t x = crc_shift(r, n_text - (uint64_t)t1, S.shift);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) x ^= __shfl_xor(x, o, 64);
+    if ((t & 63) == 0) S.crc_x[t >> 6] = x;
+    __syncthreads();
+    if (t == 0) {
+        uint32_t raw = 0;
+        for (int w = 0; w < kT / 64; ++w) raw ^= S.crc_x[w];
+        sc.crc[m] = raw ^ crc_shift(0xFFFFFFFFu, n_text, S.shift) ^ 0xFFFFFFFFu;
+    }
     sc.seg[m * (kT + 1) + t] = (uint32_t)t0;
     if (t == kT - 1) sc.seg[m * (kT + 1) + kT] = (uint32_t)t1;
     PROF_STAMP(1);
@@ -1186,7 +1199,7 @@ void crc_shift_matrices(uint32_t* M) {
         const uint32_t c = 1u << k;
         M[k] = tab[c & 0xFFu] ^ (c >> 8);
     }
-    for (int b = 1; b < 25; ++b) {  // M[b] = M[b-1] o M[b-1]
+    for (int b = 1; b < kShiftPow; ++b) {  // M[b] = M[b-1] o M[b-1]
         const uint32_t* A = M + 32 * (b - 1);
         uint32_t* B = M + 32 * b;
         for (int k = 0; k < 32; ++k) {

@@ -156,3 +156,21 @@ def test_device_txt_smaller_than_zlib9_on_c4_density(engine_lib, oracle_lib, tmp
         z9 = len(gzip.compress(text[f], compresslevel=9))
         print(f"{f}: text {len(text[f])} device {dev} zlib9 {z9} ratio {dev / z9:.3f}")
         assert dev <= z9, (f, dev, z9)
+
+
+def test_device_txt_member_past_32_mb(engine_lib, tmp_path):
+    """A member whose text passes 2^25 bytes (every position covered, a 4096-byte
+    barcode: ~68 MB of coverage lines): its CRC-32 (per-segment CRCs shifted past the
+    bytes after them) and the member still gunzip to the host formatter's text."""
+    from mgatk2_amd.engine import txt_gz_rows
+
+    L = 16569
+    counts = np.zeros((1, L, 8), np.uint32)
+    counts[0, :, 0] = 7
+    counts[0, ::3, 3] = 2
+    depth = counts.sum(axis=2).astype(np.uint32)
+    names = ["ACGT" * 1024]
+    mem = txt_gz_rows(counts, depth, [0], names)
+    assert mem.text_bytes[0, 0] > 1 << 25
+    check_members(mem, 1)
+    assert device_text(mem) == host_text(counts, depth, [0], names, tmp_path)
