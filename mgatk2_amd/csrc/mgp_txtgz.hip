@@ -82,38 +82,50 @@ __device__ __forceinline__ uint8_t* put_num(uint8_t* p, uint32_t v, uint32_t nd)
 }
 
 // ---- the count rows ----
-__device__ __forceinline__ bool rows16(const Rows& r, int c, int p) {
-    return r.c16 != nullptr && !(r.wide != nullptr && r.wide[(size_t)c * r.nwin + p / r.W]);
-}
-__device__ __forceinline__ uint32_t row_depth(const Rows& r, int c, int p) {
-    const size_t P = (size_t)c * r.L + p;
-    return rows16(r, c, p) ? (uint32_t)r.d16[P] : r.d32[P];
-}
-__device__ __forceinline__ void row_base(const Rows& r, int c, int p, int b, uint32_t& fw, uint32_t& rv) {
-    const size_t P = (size_t)c * r.L + p;
-    if (rows16(r, c, p)) {
-        const uint4 a = r.c16[P];
-        const uint32_t w = b == 0 ? a.x : b == 1 ? a.y : b == 2 ? a.z : a.w;
-        fw = w & 0xFFFFu;
-        rv = w >> 16;
-    } else {
-        fw = r.c32[P * 8 + 2 * b];
-        rv = r.c32[P * 8 + 2 * b + 1];
-    }
-}
-// the line of position p in file f (0 coverage, 1..4 A..T): its length (0: none) and values
+// the line of position p in file f (0 coverage, 1..4 A..T): its length (0: none) and values.
+// u16: the position's window has exact 16-bit rows (rows16, decided by the caller from the
+// cell's wide flags staged in LDS); the depth and the counts are loaded together
 __device__ __forceinline__ uint32_t line_of(const Rows& r, int c, int p, int f, uint32_t bclen, uint32_t& v1,
-                                            uint32_t& v2) {
-    const uint32_t d = row_depth(r, c, p);
+                                            uint32_t& v2, bool u16) {
+    const size_t P = (size_t)c * r.L + p;
+    uint32_t d, a = 0, b = 0;
+    if (u16) {
+        d = r.d16[P];
+        if (f) {
+            const uint4 q = r.c16[P];
+            const uint32_t w = f == 1 ? q.x : f == 2 ? q.y : f == 3 ? q.z : q.w;
+            a = w & 0xFFFFu;
+            b = w >> 16;
+        }
+    } else {
+        d = r.d32[P];
+        if (f) {
+            a = r.c32[P * 8 + 2 * (f - 1)];
+            b = r.c32[P * 8 + 2 * (f - 1) + 1];
+        }
+    }
     if (!d) return 0;
     if (f == 0) {
         v1 = d;
         v2 = 0;
         return ndig((uint32_t)p + 1) + bclen + ndig(d) + 3;
     }
-    row_base(r, c, p, f - 1, v1, v2);
+    v1 = a;
+    v2 = b;
     if (!(v1 | v2)) return 0;
     return ndig((uint32_t)p + 1) + bclen + ndig(v1) + ndig(v2) + 4;
+}
+constexpr int kMaxWin = 256;  // wide flags of a cell staged in LDS (the first kMaxWin windows)
+__device__ __forceinline__ bool wide_at(const Rows& r, int c, int win) {
+    return r.c16 == nullptr || (r.wide && r.wide[(size_t)c * r.nwin + win]);
+}
+// the cell's wide flags into LDS (all threads; 1: the u32 rows)
+__device__ __forceinline__ void stage_wide(const Rows& r, int c, uint8_t* wf) {
+    for (int q = threadIdx.x; q < min(r.nwin, kMaxWin); q += blockDim.x) wf[q] = wide_at(r, c, q) ? 1 : 0;
+}
+// window win of cell c has exact 16-bit rows
+__device__ __forceinline__ bool u16_at(const Rows& r, int c, int win, const uint8_t* wf) {
+    return win < kMaxWin ? !wf[win] : !wide_at(r, c, win);
 }
 
 // ---- block-wide helpers (256 threads = 4 waves) ----
@@ -500,17 +512,20 @@ __device__ __forceinline__ uint8_t fixed_len(int s) { return s < 144 ? 8 : s < 2
 // ---------------------------------------------------------------------------
 __global__ void __launch_bounds__(kT) k_txt_sizes(Job job, uint64_t* __restrict__ sizes, uint64_t* __restrict__ nlines) {
     __shared__ unsigned long long acc[2 * kFiles];
+    __shared__ uint8_t wf[kMaxWin];
     const int k = blockIdx.x, t = threadIdx.x;
     if (t < 2 * kFiles) acc[t] = 0;
-    __syncthreads();
     const int c = job.cells[k];
+    stage_wide(job.rows, c, wf);
+    __syncthreads();
     const uint32_t bclen = (uint32_t)(job.name_off[k + 1] - job.name_off[k]);
     uint64_t b[kFiles] = {0, 0, 0, 0, 0};
     uint32_t n[kFiles] = {0, 0, 0, 0, 0};
     for (int p = t; p < job.rows.L; p += kT) {
+        const bool u16 = u16_at(job.rows, c, p / job.rows.W, wf);
         for (int f = 0; f < kFiles; ++f) {
             uint32_t v1, v2;
-            const uint32_t len = line_of(job.rows, c, p, f, bclen, v1, v2);
+            const uint32_t len = line_of(job.rows, c, p, f, bclen, v1, v2, u16);
             if (!len) {
                 if (f == 0) break;  // depth 0: no line in any file
                 continue;
@@ -541,6 +556,7 @@ __global__ void __launch_bounds__(kT) k_txt_sizes(Job job, uint64_t* __restrict_
 
 struct FormatLds {
     uint64_t wsum[4];
+    uint8_t wf[kMaxWin];
     uint32_t crc_tab[4][256];  // slicing-by-4 tables (crc_tab[0]: the byte table)
     uint32_t shift[kShiftPow * 32];  // the zero-byte operator's powers (Scratch::crc_shift)
     uint32_t crc_x[kT / 64];   // the waves' XORs
@@ -568,6 +584,7 @@ __global__ void __launch_bounds__(kT) k_txt_format(Job job, Scratch sc) {
         S.crc_tab[0][s] = r;
     }
     for (int q = t; q < kShiftPow * 32; q += kT) S.shift[q] = sc.crc_shift[q];
+    stage_wide(job.rows, c, S.wf);
     __syncthreads();
     for (int s = t; s < 256; s += kT) {
         uint32_t r = S.crc_tab[0][s];
@@ -580,11 +597,19 @@ __global__ void __launch_bounds__(kT) k_txt_format(Job job, Scratch sc) {
     const int P = (L + kT - 1) / kT;
     const int p0 = min(L, t * P), p1 = min(L, p0 + P);
     uint32_t my_b = 0, my_n = 0;
-    for (int p = p0; p < p1; ++p) {
-        uint32_t v1, v2;
-        const uint32_t len = line_of(job.rows, c, p, f, bclen, v1, v2);
-        my_b += len;
-        my_n += len != 0;
+    const int W = job.rows.W;
+    {
+        int win = p0 / W, wnext = (win + 1) * W;
+        for (int p = p0; p < p1; ++p) {
+            if (p >= wnext) {
+                ++win;
+                wnext += W;
+            }
+            uint32_t v1, v2;
+            const uint32_t len = line_of(job.rows, c, p, f, bclen, v1, v2, u16_at(job.rows, c, win, S.wf));
+            my_b += len;
+            my_n += len != 0;
+        }
     }
     uint64_t tot;
     const uint64_t pre = block_excl_scan(((uint64_t)my_b << 24) | my_n, S.wsum, tot);
@@ -594,9 +619,14 @@ __global__ void __launch_bounds__(kT) k_txt_format(Job job, Scratch sc) {
     {
         uint8_t* w = T + t0;
         int k = l0;
+        int win = p0 / W, wnext = (win + 1) * W;
         for (int p = p0; p < p1; ++p) {
+            if (p >= wnext) {
+                ++win;
+                wnext += W;
+            }
             uint32_t v1 = 0, v2 = 0;
-            const uint32_t len = line_of(job.rows, c, p, f, bclen, v1, v2);
+            const uint32_t len = line_of(job.rows, c, p, f, bclen, v1, v2, u16_at(job.rows, c, win, S.wf));
             if (!len) continue;
             uint8_t* const s = w;
             w = put_num(w, (uint32_t)p + 1, ndig((uint32_t)p + 1));

@@ -174,3 +174,25 @@ def test_device_txt_member_past_32_mb(engine_lib, tmp_path):
     assert mem.text_bytes[0, 0] > 1 << 25
     check_members(mem, 1)
     assert device_text(mem) == host_text(counts, depth, [0], names, tmp_path)
+
+
+def test_device_txt_with_a_wide_window(engine_lib, tmp_path):
+    """A cell with drained windows (more than 65535 reads: its exact u32 rows there, the
+    16-bit rows elsewhere) through the engine's writer: the same text as the host
+    formatter's from the exact result."""
+    from mgatk2_amd.engine import Engine, EngineConfig
+    from mgatk2_amd.synth import synth_reads
+
+    deep = synth_reads(91, 400_000, 1)
+    deep.start[:] = np.sort(deep.start % 3000).astype(np.int32)
+    deep.payload.reshape(-1, 64)[:, 0:4] = deep.start.view(np.uint8).reshape(-1, 4)
+    cfg = EngineConfig(n_cells=1, min_baseq=0, min_mapq=0, dedup_mode="none", min_reads=0)
+    with Engine(cfg) as eng:
+        eng.push(deep)
+        eng.run()
+        exact = eng.fetch()
+        r16 = eng.fetch_rows16()
+        mem = eng.txt_gz([0], ["ACGTACGTACGTACGT-1"])
+    assert r16.wide[0].any() and not r16.wide[0].all()  # (u32 rows in the drained windows, 16-bit elsewhere)
+    check_members(mem, 1)
+    assert device_text(mem) == host_text(exact.counts, exact.depth, [0], ["ACGTACGTACGTACGT-1"], tmp_path)
