@@ -4697,18 +4697,19 @@ static int txt_run(TxtState& st, hipStream_t s, const txtgz::Rows& rows, int32_t
     uint64_t* oo = lo + nm + 1;
     to[0] = lo[0] = oo[0] = 0;
     for (int64_t m = 0; m < nm; ++m) {
-        to[m + 1] = to[m] + sz[(size_t)m];
+        to[m + 1] = to[m] + ((sz[(size_t)m] + 15) & ~uint64_t(15));  // (aligned: the parse loads 16 bytes)
         lo[m + 1] = lo[m] + nl[(size_t)m];
         oo[m + 1] = oo[m] + out_bound(sz[(size_t)m]);
         if (job->text_bytes) job->text_bytes[m] = (int64_t)sz[(size_t)m];
     }
-    MGP_TRY(st.text.ensure(to[nm] + 64));
-    MGP_TRY(st.tok.ensure(4 * to[nm] + 64));
+    MGP_TRY(st.text.ensure(to[nm] + 256));  // (slack: a parse block reads up to 31 positions past a text)
+    MGP_TRY(st.tok.ensure(4 * to[nm] + 1024));
     MGP_TRY(st.lines.ensure(12 * lo[nm] + 64));
     MGP_TRY(st.out.ensure(oo[nm] + 64));
     HIP_TRY(hipMemcpyAsync(st.offs.p, offs.data(), offs.size() * 8, hipMemcpyHostToDevice, s));
     Scratch sc{};
     sc.text_off = st.offs.as<uint64_t>();
+    sc.text_n = st.sizes.as<uint64_t>();
     sc.line_off = sc.text_off + nm + 1;
     sc.out_off = sc.line_off + nm + 1;
     sc.text = st.text.as<uint8_t>();

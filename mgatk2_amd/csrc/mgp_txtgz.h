@@ -43,7 +43,8 @@ struct Job {
 
 // Device scratch of a batch; every array is sized by the caller from txt_sizes().
 struct Scratch {
-    uint64_t* text_off;   // [5n + 1] member text offsets (member = file * n + cell)
+    uint64_t* text_off;   // [5n + 1] member text offsets (member = file * n + cell), 16-byte aligned
+    const uint64_t* text_n;  // [5n] member text bytes (txt_sizes)
     uint64_t* line_off;   // [5n + 1]
     uint64_t* out_off;    // [5n + 1] member output regions (bounds)
     uint8_t* text;        // text_off[5n] bytes

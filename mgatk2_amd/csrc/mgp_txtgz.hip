@@ -412,14 +412,27 @@ __device__ void dp_segment(const uint8_t* T, uint32_t* tok, int t0, int t1, cons
 #pragma unroll
     for (int k = 0; k < 32; ++k) ring[k] = 0;  // cost[t1] = 0; the others are never read
     for (int b0 = (t1 - 1) & ~31; b0 + 31 >= t0; b0 -= 32) {
+        // the block's 32 candidates and bytes in 10 aligned 16-byte loads, all in flight
+        // together (member texts start 16-byte aligned; positions outside [t0, t1) are read
+        // but never used, and the buffers have slack past the last member)
         uint32_t w[32];
         uint32_t tb[32];
+        const uint4* const w4 = reinterpret_cast<const uint4*>(tok + b0);
+        const uint4* const t4 = reinterpret_cast<const uint4*>(T + b0);
 #pragma unroll
-        for (int u = 0; u < 32; ++u) {  // the block's loads, all in flight together
-            const int p = b0 + u;
-            const bool act = p >= t0 && p < t1;
-            w[u] = act ? tok[p] : 0u;
-            tb[u] = act ? T[p] : 0u;
+        for (int q = 0; q < 8; ++q) {
+            const uint4 v = w4[q];
+            w[4 * q] = v.x;
+            w[4 * q + 1] = v.y;
+            w[4 * q + 2] = v.z;
+            w[4 * q + 3] = v.w;
+        }
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+            const uint4 v = t4[q];
+            const uint32_t ws[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+            for (int u = 0; u < 16; ++u) tb[16 * q + u] = (ws[u >> 2] >> (8 * (u & 3))) & 0xFFu;
         }
 #pragma unroll
         for (int u = 31; u >= 0; --u) {
@@ -644,7 +657,7 @@ __global__ void __launch_bounds__(kT) k_txt_format(Job job, Scratch sc) {
     const int L = job.rows.L;
     uint8_t* const T = sc.text + sc.text_off[m];
     uint32_t* const lines = sc.lines + 3 * sc.line_off[m];
-    const uint64_t n_text = sc.text_off[m + 1] - sc.text_off[m];
+    const uint64_t n_text = sc.text_n[m];
     if (n_text == 0) return;
     PROF_STAMP(0);
     for (int s = t; s < 256; s += kT) {
@@ -777,7 +790,7 @@ __global__ void __launch_bounds__(kT, 4) k_txt_match(Job job, Scratch sc) {
     const uint8_t* const T = sc.text + sc.text_off[m];
     const uint32_t* const lines = sc.lines + 3 * sc.line_off[m];
     uint32_t* const tok = sc.tok + sc.text_off[m];
-    const uint64_t n_text = sc.text_off[m + 1] - sc.text_off[m];
+    const uint64_t n_text = sc.text_n[m];
     if (n_text == 0) return;
     const int n_lines = (int)(sc.line_off[m + 1] - sc.line_off[m]);
     // ---- 2. match candidates, windows of lines staged in LDS ----
@@ -1013,7 +1026,7 @@ __global__ void __launch_bounds__(kT) k_txt_code(Job job, Scratch sc) {
     const int64_t m = blockIdx.x;
     const uint8_t* const T = sc.text + sc.text_off[m];
     uint32_t* const tok = sc.tok + sc.text_off[m];
-    const uint64_t n_text = sc.text_off[m + 1] - sc.text_off[m];
+    const uint64_t n_text = sc.text_n[m];
     uint32_t* const out = sc.out + sc.out_off[m] / 4;
     if (n_text == 0) {  // no line: no member
         if (t == 0) sc.member_bytes[m] = 0;
